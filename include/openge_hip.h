@@ -1,0 +1,143 @@
+/* openge_hip.h -- C ABI of libopenge_hip.so, the MI355X (gfx950) drop-in for OpenGE's
+ * post-alignment hot path: coordinate sort, duplicate marking, local-realignment scoring.
+ *
+ * Conventions: every entry point returns 0 on success and a negative oge_status on failure
+ * (message via oge_last_error); no C++ exceptions cross the ABI; plain pointers and sizes
+ * only.  Record buffers hold BAM records exactly as in a decompressed BAM stream
+ * (block_size u32 + 32-byte core + variable data, util/bam_deserializer.h:143-193) and are
+ * addressed by a u64 byte offset per record.
+ *
+ * Entry points named *_dev take device (HBM) pointers and run on the context's HIP stream;
+ * the others take host buffers and copy in/out.  One context per host thread and GPU.
+ *
+ * Reference interfaces replaced (paths under openge/src/):
+ *   oge_sort_coord*      <- ReadSorter (algorithms/read_sorter.h:32-105, .cpp:48-232) with
+ *                           Sort::ByPosition (util/bamtools/Sort.h:116-136) and the
+ *                           MultiReader run merge (util/read_stream_reader.h:132-153)
+ *   oge_gather_records*  <- BamSerializer::write's record encode incl. bin recompute
+ *                           (util/bam_serializer.h:105-147) applied to the sorted stream
+ *   oge_markdup*         <- MarkDuplicates::runInternal/buildSortedReadEndLists/
+ *                           generateDuplicateIndexes (algorithms/mark_duplicates.cpp:185-475)
+ *   oge_realign_scan*    <- LocalRealignment::findBestOffset + mismatchQualitySumIgnoreCigar
+ *                           (algorithms/local_realignment.cpp:641-679,1126-1164)
+ */
+#ifndef OPENGE_HIP_H
+#define OPENGE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum oge_status {
+    OGE_OK = 0,
+    OGE_ERR_ARG = -1,      /* bad argument / malformed record */
+    OGE_ERR_HIP = -2,      /* HIP runtime error (no device, launch failure, OOM) */
+    OGE_ERR_LIMIT = -3,    /* input outside supported limits */
+    OGE_ERR_IO = -4        /* file / codec error */
+} oge_status;
+
+typedef struct oge_ctx oge_ctx;
+
+/* ---- context ---------------------------------------------------------------------- */
+int oge_ctx_create(int device, oge_ctx **out);
+/* stream: a hipStream_t (0 = the context's own non-blocking stream) */
+int oge_ctx_set_stream(oge_ctx *ctx, void *stream);
+void *oge_ctx_stream(oge_ctx *ctx);
+int oge_ctx_sync(oge_ctx *ctx);
+void oge_ctx_destroy(oge_ctx *ctx);
+const char *oge_last_error(const oge_ctx *ctx);   /* ctx may be NULL (thread-local last error) */
+/* last pipeline's kernel timings in ms, measured with HIP events on the context stream */
+int oge_ctx_timing(oge_ctx *ctx, const char *stage, double *ms_out);
+/* version string of the library, gfx target it was built for */
+const char *oge_version(void);
+
+/* ---- coordinate sort (ReadSorter + Sort::ByPosition) ------------------------------ */
+/* perm_out[k] = input index of the record at sorted position k.  Order: refID ascending with
+ * refID == -1 last; pos; forward before reverse; read name bytes; flag; input index (the
+ * reference's final tie-break is the record's heap address).  Records with
+ * refID == -1 keep input order (reference order there is implementation-defined, Q11).
+ * n_ref: number of reference sequences (refIDs must lie in [-1, n_ref)). */
+int oge_sort_coord(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const uint64_t *rec_off,
+                   uint64_t n, int32_t n_ref, uint32_t *perm_out);
+int oge_sort_coord_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
+                       int32_t n_ref, uint32_t *d_perm);
+
+/* ---- permutation gather with BAM re-encode (bin recompute) ------------------------- */
+/* out record k = record perm[k] with its bin field recomputed as the reference writer does.
+ * d_out_off (n+1 entries) receives the output offsets; d_out must hold the same byte total. */
+int oge_gather_records_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
+                           uint64_t n, uint8_t *d_out, uint64_t *d_out_off);
+
+/* ---- duplicate marking (MarkDuplicates) ------------------------------------------- */
+typedef struct oge_markdup_opts {
+    int32_t n_ref;
+    /* Read-group -> library table: rg_ids is n_rg NUL-terminated IDs back to back; rg_lib[i] is
+     * the library id (>= 1) of rg i.  Records whose RG is absent / unknown / has no LB use
+     * unknown_lib (getLibraryName, algorithms/mark_duplicates.cpp:301-318). */
+    const char *rg_ids;
+    uint64_t rg_ids_bytes;
+    const int16_t *rg_lib;
+    int32_t n_rg;
+    int16_t unknown_lib;
+    int16_t pad0;
+    /* Reproduce the reference's non-verbose index bug: the record index only
+     * advances under -v, so every ReadEnds carries index 0.  Default 0 = -v semantics. */
+    int32_t compat_nonverbose_index;
+    /* 1 = drop duplicates from the output (-r/-R); affects oge_markdup's n_kept only */
+    int32_t remove_duplicates;
+} oge_markdup_opts;
+
+/* dup_out[i] (per input record, input order = record index): 1 if record i is flagged
+ * 0x400, 0 if a primary record that gets 0x400 cleared, 2 if non-primary (flag untouched).
+ * flags_out (optional, may be NULL): the record's new FLAG field. */
+int oge_markdup(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const uint64_t *rec_off, uint64_t n,
+                const oge_markdup_opts *opts, uint8_t *dup_out, uint64_t *n_dup_out);
+/* Device form: also rewrites FLAG 0x400 in place in d_recs when apply != 0. */
+int oge_markdup_dev(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
+                    const oge_markdup_opts *opts, uint8_t *d_dup, int apply, uint64_t *n_dup_out);
+
+/* ---- fused sort + markdup (mergesort -M --nosplit) on device-resident records -------- */
+/* d_out/d_out_off receive the sorted records with bin recomputed and 0x400 applied.
+ * d_perm (n) receives the permutation. */
+int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
+                         const oge_markdup_opts *opts, uint32_t *d_perm, uint8_t *d_out, uint64_t *d_out_off,
+                         uint64_t *n_dup_out);
+
+/* ---- synthetic data (bench / tests) ------------------------------------------------ */
+/* params: a pointer to oge_synth_params (openge_amd/csrc/synth.h) */
+int oge_synth_finalize(void *params);
+uint64_t oge_synth_params_size(void);
+/* Host generation of slots [0, 2*n_pairs): sizes first (offs gets n+1 prefix offsets), then bytes. */
+int oge_synth_offsets_host(const void *params, uint64_t *offs, int threads);
+int oge_synth_records_host(const void *params, const uint64_t *offs, uint8_t *out, int threads);
+int oge_synth_header_text(const void *params, char *buf, uint64_t cap, uint64_t *len_out);
+/* Device generation straight into HBM. */
+int oge_synth_offsets_dev(oge_ctx *ctx, const void *params, uint64_t *d_offs);
+int oge_synth_records_dev(oge_ctx *ctx, const void *params, const uint64_t *d_offs, uint8_t *d_out);
+
+/* ---- BAM file helpers (host) -------------------------------------------------------- */
+typedef struct oge_bam oge_bam;
+int oge_bam_read(const char *path, int threads, oge_bam **out);
+void oge_bam_free(oge_bam *b);
+uint64_t oge_bam_count(const oge_bam *b);
+const uint8_t *oge_bam_records(const oge_bam *b, uint64_t *bytes_out);
+const uint64_t *oge_bam_offsets(const oge_bam *b);
+int32_t oge_bam_n_ref(const oge_bam *b);
+/* regenerated header text (BamHeader::toString, util/bam_header.cpp:184-214) */
+int oge_bam_header_text(const oge_bam *b, char *buf, uint64_t cap, uint64_t *len_out);
+/* Build the RG -> library table MarkDuplicates derives from the header. Caller frees with free(). */
+int oge_bam_markdup_opts(const oge_bam *b, oge_markdup_opts *opts, char **rg_ids_buf, int16_t **rg_lib_buf);
+/* Write a BGZF BAM: header from `header_text`, records in the given order (order may be NULL
+ * for identity), optional FLAG overrides (flags may be NULL). sort_order: -1 keep, else
+ * BamHeader::sort_order_t. */
+int oge_bam_write(const char *path, const char *header_text, uint64_t header_len, int sort_order,
+                  const uint8_t *recs, const uint64_t *offs, uint64_t n, const uint32_t *order,
+                  const uint16_t *flags, int level, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OPENGE_HIP_H */

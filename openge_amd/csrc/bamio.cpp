@@ -1,0 +1,348 @@
+// bamio.cpp -- host BGZF/BAM codec (see bamio.h for the reference interfaces replaced).
+#include "bamio.h"
+
+#include <zlib.h>
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <sstream>
+#include <thread>
+
+namespace oge {
+
+static inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static inline uint16_t rd16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+
+template <class F>
+static void parallel_for(size_t n, int threads, F f) {
+    if (threads <= 1 || n < 2) { for (size_t i = 0; i < n; ++i) f(i); return; }
+    std::atomic<size_t> next(0);
+    std::vector<std::thread> ts;
+    int t = (int)std::min<size_t>((size_t)threads, n);
+    for (int k = 0; k < t; ++k)
+        ts.emplace_back([&]() {
+            for (;;) {
+                size_t i = next.fetch_add(1);
+                if (i >= n) break;
+                f(i);
+            }
+        });
+    for (auto &th : ts) th.join();
+}
+
+// ---------------- BGZF inflate ----------------
+bool bgzf_inflate_all(const uint8_t *src, size_t n, std::vector<uint8_t> &out, int threads, std::string &err) {
+    struct Blk { size_t coff, clen, cdata, dlen, uoff; };
+    std::vector<Blk> blocks;
+    size_t p = 0, total = 0;
+    while (p < n) {
+        if (n - p < 18 || src[p] != 31 || src[p + 1] != 139 || src[p + 2] != 8 || !(src[p + 3] & 4)) {
+            err = "not a BGZF stream or truncated block header";
+            return false;
+        }
+        uint16_t xlen = rd16(src + p + 10);
+        size_t x = p + 12, xend = x + xlen, bsize = 0;
+        if (xend > n) { err = "truncated BGZF extra field"; return false; }
+        while (x + 4 <= xend) {
+            uint16_t slen = rd16(src + x + 2);
+            if (src[x] == 'B' && src[x + 1] == 'C' && slen == 2) bsize = (size_t)rd16(src + x + 4) + 1;
+            x += 4 + slen;
+        }
+        if (!bsize) { err = "BGZF block without BC field"; return false; }
+        if (p + bsize > n) { err = "truncated BGZF block (file cut short?)"; return false; }
+        size_t cdata = xend;
+        uint32_t isize = rd32(src + p + bsize - 4);
+        blocks.push_back({p, bsize, cdata, isize, total});
+        total += isize;
+        p += bsize;
+    }
+    out.resize(total);
+    std::atomic<bool> ok(true);
+    parallel_for(blocks.size(), threads, [&](size_t i) {
+        const Blk &b = blocks[i];
+        if (b.dlen == 0) return;
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        if (inflateInit2(&zs, -15) != Z_OK) { ok = false; return; }
+        zs.next_in = (Bytef *)(src + b.cdata);
+        zs.avail_in = (uInt)(b.coff + b.clen - 8 - b.cdata);
+        zs.next_out = (Bytef *)(out.data() + b.uoff);
+        zs.avail_out = (uInt)b.dlen;
+        int rc = inflate(&zs, Z_FINISH);
+        if (rc != Z_STREAM_END || zs.total_out != b.dlen) ok = false;
+        else {
+            uint32_t crc = (uint32_t)crc32(0L, out.data() + b.uoff, (uInt)b.dlen);
+            if (crc != rd32(src + b.coff + b.clen - 8)) ok = false;
+        }
+        inflateEnd(&zs);
+    });
+    if (!ok) { err = "BGZF block failed to inflate (corrupt data)"; return false; }
+    return true;
+}
+
+// ---------------- BGZF deflate ----------------
+static const size_t kBlockPayload = 65280;
+
+BgzfWriter::BgzfWriter(FILE *f, int level, int threads) : f_(f), level_(level), threads_(threads), closed_(false) {}
+BgzfWriter::~BgzfWriter() { if (!closed_) close(); }
+
+static void bgzf_block(const uint8_t *src, size_t n, int level, std::vector<uint8_t> &dst) {
+    size_t bound = compressBound((uLong)n) + 64;
+    dst.resize(18 + bound + 8);
+    z_stream zs;
+    memset(&zs, 0, sizeof(zs));
+    deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+    zs.next_in = (Bytef *)src;
+    zs.avail_in = (uInt)n;
+    zs.next_out = dst.data() + 18;
+    zs.avail_out = (uInt)bound;
+    deflate(&zs, Z_FINISH);
+    size_t clen = zs.total_out;
+    deflateEnd(&zs);
+    size_t bsize = 18 + clen + 8;
+    static const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
+    memcpy(dst.data(), hdr, 16);
+    dst[16] = (uint8_t)((bsize - 1) & 0xff);
+    dst[17] = (uint8_t)((bsize - 1) >> 8);
+    uint32_t crc = (uint32_t)crc32(0L, src, (uInt)n);
+    memcpy(dst.data() + 18 + clen, &crc, 4);
+    uint32_t isz = (uint32_t)n;
+    memcpy(dst.data() + 18 + clen + 4, &isz, 4);
+    dst.resize(bsize);
+}
+
+void BgzfWriter::write(const void *data, size_t n) {
+    const uint8_t *p = (const uint8_t *)data;
+    pending_.insert(pending_.end(), p, p + n);
+    if (pending_.size() >= kBlockPayload * (size_t)std::max(1, threads_) * 4) flush_blocks(false);
+}
+
+void BgzfWriter::flush_blocks(bool final) {
+    size_t nblk = pending_.size() / kBlockPayload;
+    if (final && pending_.size() % kBlockPayload) nblk++;
+    if (!nblk) return;
+    std::vector<std::vector<uint8_t>> outs(nblk);
+    parallel_for(nblk, threads_, [&](size_t i) {
+        size_t off = i * kBlockPayload;
+        size_t len = std::min(kBlockPayload, pending_.size() - off);
+        bgzf_block(pending_.data() + off, len, level_, outs[i]);
+    });
+    for (auto &o : outs) fwrite(o.data(), 1, o.size(), f_);
+    size_t consumed = std::min(pending_.size(), nblk * kBlockPayload);
+    pending_.erase(pending_.begin(), pending_.begin() + consumed);
+}
+
+void BgzfWriter::close() {
+    if (closed_) return;
+    flush_blocks(true);
+    std::vector<uint8_t> eof;
+    bgzf_block(nullptr, 0, level_, eof);
+    fwrite(eof.data(), 1, eof.size(), f_);
+    fflush(f_);
+    closed_ = true;
+}
+
+// ---------------- header model (util/bam_header.cpp:27-278) ----------------
+static std::vector<std::string> split_tabs(const std::string &line) {
+    std::vector<std::string> ret;
+    size_t i = 0;
+    for (;;) {
+        size_t j = line.find('\t', i);
+        if (j == std::string::npos) { ret.push_back(line.substr(i)); break; }
+        ret.push_back(line.substr(i, j - i));
+        i = j + 1;
+    }
+    return ret;
+}
+
+bool BamHeaderModel::parse(const std::string &text, std::string &err) {
+    // getline loop that stops when the stream is no longer good: a final line without a
+    // trailing newline is dropped (util/bam_header.cpp:113-116).
+    std::string t(text);
+    t.push_back('\0');  // the reference parses a text_len+1 buffer with a trailing NUL
+    std::stringstream in(t);
+    for (;;) {
+        std::string line;
+        std::getline(in, line);
+        if (!in.good()) break;
+        if (line.empty() || line[0] != '@') { err = "Sam header format problem: line doesn't begin with a '@'"; return false; }
+        if (line.size() < 4 || line[3] != '\t') { err = "Sam header format problem: line doesn't have a tab after the tag"; return false; }
+        std::string tag = line.substr(1, 2), data = line.substr(4);
+        std::vector<std::string> segs = split_tabs(data);
+        auto field = [&](const std::string &s, std::string &k, std::string &v) -> bool {
+            if (s.size() < 3) { err = "malformed header field '" + s + "'"; return false; }
+            k = s.substr(0, 2); v = s.substr(3); return true;
+        };
+        if (tag == "CO") {
+            co.push_back(data);
+        } else if (tag == "RG") {
+            RgRecord r;
+            for (auto &s : segs) {
+                std::string k, v;
+                if (!field(s, k, v)) return false;
+                if (k == "ID") r.id = v; else if (k == "CN") r.cn = v; else if (k == "DS") r.ds = v;
+                else if (k == "DT") r.dt = v; else if (k == "FO") r.fo = v; else if (k == "KS") r.ks = v;
+                else if (k == "LB") r.lb = v; else if (k == "PG") r.pg = v; else if (k == "PI") r.pi = v;
+                else if (k == "PL") r.pl = v; else if (k == "PU") r.pu = v; else if (k == "SM") r.sm = v;
+            }
+            if (r.id.empty()) { err = "Mandatory field missing in header read group line."; return false; }
+            rg.push_back(r);
+        } else if (tag == "SQ") {
+            SqRecord r;
+            for (auto &s : segs) {
+                std::string k, v;
+                if (!field(s, k, v)) return false;
+                if (k == "SN") r.name = v; else if (k == "LN") r.length = (long long)(size_t)(long)atoi(v.c_str());
+                else if (k == "AS") r.as = v; else if (k == "M5") r.m5 = v; else if (k == "SP") r.sp = v;
+                else if (k == "UR") r.ur = v;
+            }
+            if (r.name.empty() || r.length == -1) { err = "Mandatory field missing in header sequence line."; return false; }
+            sq.push_back(r);
+        } else if (tag == "PG") {
+            PgRecord r;
+            for (auto &s : segs) {
+                std::string k, v;
+                if (!field(s, k, v)) return false;
+                if (k == "ID") r.id = v; else if (k == "PN") r.pn = v; else if (k == "CL") r.cl = v;
+                else if (k == "PP") r.pp = v; else if (k == "VN") r.vn = v;
+            }
+            if (r.id.empty()) { err = "Mandatory field missing in header program record line."; return false; }
+            pg.push_back(r);
+        } else if (tag == "HD") {
+            std::string so;
+            for (auto &s : segs) {
+                std::string k, v;
+                if (!field(s, k, v)) return false;
+                if (k == "VN") format_version = v; else if (k == "SO") so = v;
+            }
+            if (so.empty() || format_version.empty()) { err = "Mandatory field missing in header HD line."; return false; }
+            if (so == "unsorted") sort_order = UNSORTED;
+            else if (so == "coordinate") sort_order = COORDINATE;
+            else if (so == "queryname") sort_order = QUERYNAME;
+            else if (so == "unknown") sort_order = UNKNOWN;
+            else { err = "Unknown sort order '" + so + "'."; return false; }
+        } else {
+            err = "Sam header format problem: tag '" + tag + "' wasn't CO RG SQ PG or HD.";
+            return false;
+        }
+    }
+    if (format_version.empty()) { format_version = "1.4"; sort_order = UNKNOWN; }
+    return true;
+}
+
+std::string BamHeaderModel::to_string() const {
+    std::ostringstream s;
+    static const char *so_names[] = {"unknown", "unsorted", "queryname", "coordinate"};
+    s << "@HD\tVN:" << format_version << "\tSO:" << so_names[sort_order] << "\n";
+    for (auto &r : sq) {
+        s << "@SQ\tSN:" << r.name << "\tLN:" << (size_t)r.length;
+        if (!r.as.empty()) s << "\tAS:" << r.as;
+        if (!r.m5.empty()) s << "\tM5:" << r.m5;
+        if (!r.sp.empty()) s << "\tSP:" << r.sp;
+        if (!r.ur.empty()) s << "\tUR:" << r.ur;
+        s << "\n";
+    }
+    for (auto &r : rg) {
+        s << "@RG\tID:" << r.id;
+        if (!r.cn.empty()) s << "\tCN:" << r.cn;
+        if (!r.ds.empty()) s << "\tDS:" << r.ds;
+        if (!r.dt.empty()) s << "\tDT:" << r.dt;
+        if (!r.fo.empty()) s << "\tFO:" << r.fo;
+        if (!r.ks.empty()) s << "\tKS:" << r.ks;
+        if (!r.ks.empty()) s << "\tKS:" << r.ks;  // printed twice by the reference (bam_header.cpp:243-246)
+        if (!r.lb.empty()) s << "\tLB:" << r.lb;
+        if (!r.pg.empty()) s << "\tPG:" << r.pg;
+        if (!r.pi.empty()) s << "\tPI:" << r.pi;
+        if (!r.pl.empty()) s << "\tPL:" << r.pl;
+        if (!r.pu.empty()) s << "\tPU:" << r.pu;
+        if (!r.sm.empty()) s << "\tSM:" << r.sm;
+        s << "\n";
+    }
+    for (auto &r : pg) {
+        s << "@PG\tID:" << r.id;
+        if (!r.pn.empty()) s << "\tPN:" << r.pn;
+        if (!r.cl.empty()) s << "\tCL:" << r.cl;
+        if (!r.pp.empty()) s << "\tPP:" << r.pp;
+        if (!r.vn.empty()) s << "\tVN:" << r.vn;
+        s << "\n";
+    }
+    for (auto &c : co) s << "@CO\t" << c << "\n";
+    return s.str();
+}
+
+// ---------------- BAM ----------------
+bool bam_parse(std::vector<uint8_t> &&raw, BamFile &out, std::string &err) {
+    out.data = std::move(raw);
+    const uint8_t *d = out.data.data();
+    size_t n = out.data.size();
+    if (n < 12 || memcmp(d, "BAM\1", 4) != 0) { err = "Error reading BAM stream header magic bytes."; return false; }
+    uint32_t l_text = rd32(d + 4);
+    if (8 + (size_t)l_text + 4 > n) { err = "Error reading BAM stream header text."; return false; }
+    out.header_text.assign((const char *)d + 8, l_text);
+    size_t p = 8 + l_text;
+    if (!out.header.parse(out.header_text, err)) return false;
+    uint32_t n_ref = rd32(d + p);
+    p += 4;
+    for (uint32_t i = 0; i < n_ref; ++i) {
+        if (p + 4 > n) { err = "Error reading BAM stream reference sequence name length."; return false; }
+        uint32_t ln = rd32(d + p);
+        p += 4;
+        if (p + ln + 4 > n || ln == 0) { err = "Error reading BAM stream reference sequence."; return false; }
+        std::string name((const char *)d + p, ln - 1);
+        p += ln;
+        int32_t len = (int32_t)rd32(d + p);
+        p += 4;
+        out.ref_names.push_back(name);
+        out.ref_lens.push_back(len);
+        // util/bam_deserializer.h:126-133 -- binary list must match the text @SQ lines
+        if (i >= out.header.sq.size() || out.header.sq[i].name != name || (int32_t)out.header.sq[i].length != len) {
+            err = "BAM header text doesn't match sequence information.";
+            return false;
+        }
+    }
+    out.rec_base = p;
+    out.offsets.clear();
+    size_t q = p;
+    while (q < n) {
+        if (q + 4 > n) { err = "Expected more bytes reading BAM core. Is this file truncated or corrupted?"; return false; }
+        uint32_t bs = rd32(d + q);
+        // util/bam_deserializer.h:160-163
+        if (bs < 32 || bs > 10000) { err = "Invalid BAM block size(" + std::to_string(bs) + ")."; return false; }
+        if (q + 4 + bs > n) { err = "Expected more bytes reading BAM core. Is this file truncated or corrupted?"; return false; }
+        out.offsets.push_back(q - p);
+        q += 4 + bs;
+    }
+    return true;
+}
+
+bool bam_read_file(const std::string &path, BamFile &out, int threads, std::string &err) {
+    FILE *f = (path == "-" || path == "stdin") ? stdin : fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot open " + path; return false; }
+    std::vector<uint8_t> comp;
+    uint8_t buf[1 << 16];
+    size_t r;
+    while ((r = fread(buf, 1, sizeof(buf), f)) > 0) comp.insert(comp.end(), buf, buf + r);
+    if (f != stdin) fclose(f);
+    std::vector<uint8_t> raw;
+    if (!bgzf_inflate_all(comp.data(), comp.size(), raw, threads, err)) return false;
+    return bam_parse(std::move(raw), out, err);
+}
+
+std::vector<uint8_t> bam_encode_header(const BamHeaderModel &h) {
+    std::vector<uint8_t> o;
+    auto put32 = [&](uint32_t v) { uint8_t b[4]; memcpy(b, &v, 4); o.insert(o.end(), b, b + 4); };
+    std::string text = h.to_string();
+    o.insert(o.end(), {'B', 'A', 'M', 1});
+    put32((uint32_t)text.size());
+    o.insert(o.end(), text.begin(), text.end());
+    put32((uint32_t)h.sq.size());
+    for (auto &s : h.sq) {
+        put32((uint32_t)s.name.size() + 1);
+        o.insert(o.end(), s.name.begin(), s.name.end());
+        o.push_back(0);
+        put32((uint32_t)(int32_t)s.length);
+    }
+    return o;
+}
+
+} // namespace oge

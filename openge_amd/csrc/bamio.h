@@ -1,0 +1,77 @@
+// bamio.h -- host-side BAM/BGZF codec and header model for the openge_amd drop-in.
+//
+// Replaces the reference's L2 codec layer for the hot path:
+//   BgzfInputStream  (util/bgzf_input_stream.cpp:65-142,208-240)  -> bgzf_inflate_all()
+//   BgzfOutputStream (util/bgzf_output_stream.cpp:59-250)         -> BgzfWriter
+//   BamDeserializer::open/read (util/bam_deserializer.h:38-193)   -> bam_parse()
+//   BamSerializer::open/write  (util/bam_serializer.h:46-147)     -> bam_write_header()/records
+//   BamHeader parse/toString   (util/bam_header.cpp:108-278)      -> BamHeaderModel
+// Records stay in their BAM byte layout inside one contiguous arena with a u64 offset per
+// record, which is exactly what the device kernels consume.
+#pragma once
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+namespace oge {
+
+// ---------------- BGZF ----------------
+// Inflate an entire BGZF byte string (any number of blocks) into `out`, in parallel.
+// Returns false and fills `err` on a malformed or truncated stream.
+bool bgzf_inflate_all(const uint8_t *src, size_t n, std::vector<uint8_t> &out, int threads, std::string &err);
+
+class BgzfWriter {
+public:
+    // level: zlib level 0..9; block payload is 65280 bytes (htslib framing; the reference uses
+    // 65536/65472, SURVEY Q17 -- compressed bytes are not part of parity).
+    BgzfWriter(FILE *f, int level, int threads);
+    ~BgzfWriter();
+    void write(const void *data, size_t n);
+    void close();  // flush + EOF marker
+private:
+    void flush_blocks(bool final);
+    FILE *f_;
+    int level_, threads_;
+    std::vector<uint8_t> pending_;
+    bool closed_;
+};
+
+// ---------------- header model ----------------
+struct SqRecord { std::string name, as, m5, sp, ur; long long length = -1; };
+struct RgRecord { std::string id, cn, ds, dt, fo, ks, lb, pg, pi, pl, pu, sm; };
+struct PgRecord { std::string id, pn, cl, pp, vn; };
+
+struct BamHeaderModel {
+    std::string format_version;
+    enum SortOrder { UNKNOWN = 0, UNSORTED = 1, QUERYNAME = 2, COORDINATE = 3 } sort_order = UNKNOWN;
+    std::vector<SqRecord> sq;
+    std::vector<RgRecord> rg;
+    std::vector<PgRecord> pg;
+    std::vector<std::string> co;
+    bool parse(const std::string &text, std::string &err);
+    std::string to_string() const;
+    // Library id per read group in the order MarkDuplicates would discover them does not
+    // matter; ids here: 1 + index of the distinct LB name, "Unknown Library" last.
+};
+
+// ---------------- BAM ----------------
+struct BamFile {
+    BamHeaderModel header;
+    std::string header_text;              // as stored in the file
+    std::vector<std::string> ref_names;   // binary reference list
+    std::vector<int32_t> ref_lens;
+    std::vector<uint8_t> data;            // decompressed stream (records start at rec_base)
+    size_t rec_base = 0;
+    std::vector<uint64_t> offsets;        // record offsets relative to data.data() + rec_base
+    const uint8_t *recs() const { return data.data() + rec_base; }
+    uint64_t rec_bytes() const { return data.size() - rec_base; }
+};
+
+bool bam_read_file(const std::string &path, BamFile &out, int threads, std::string &err);
+bool bam_parse(std::vector<uint8_t> &&raw, BamFile &out, std::string &err);
+// Serialize header block (magic, text, reference list taken from the header @SQ lines, as
+// BamSerializer::open does at util/bam_serializer.h:54-76).
+std::vector<uint8_t> bam_encode_header(const BamHeaderModel &h);
+
+} // namespace oge

@@ -1,0 +1,281 @@
+// capi_dev.hip -- C-ABI entry points that run on the GPU, the context implementation, and the
+// device-side synthetic generator.
+#include "oge_ctx.h"
+#include "bam_layout.h"
+#include "synth.h"
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+// implemented in sort.hip / markdup.hip
+int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+                      uint64_t **kout, uint32_t **vout);
+int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
+                          const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off);
+int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
+                    uint8_t *d_dup, int apply, uint64_t *n_dup_out);
+
+static thread_local std::string g_last_error;
+
+int oge_fail(oge_ctx *ctx, int code, const char *msg) {
+    g_last_error = msg ? msg : "";
+    if (ctx) ctx->err = g_last_error;
+    return code;
+}
+
+// ---------------------------------------------------------------- context
+void *oge_ctx::ws(const char *name, size_t bytes) {
+    Buf &b = bufs[name];
+    if (bytes == 0) bytes = 1;
+    if (b.cap >= bytes) return b.p;
+    if (b.p) {
+        hipStreamSynchronize(stream);
+        hipFree(b.p);
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    size_t cap = bytes + 64;  // slack so 4-byte over-reads at the end stay inside the allocation
+    hipError_t e = hipMalloc(&b.p, cap);
+    if (e != hipSuccess) {
+        b.p = nullptr;
+        std::string m = std::string("hipMalloc(") + name + ", " + std::to_string(cap) + " B): " + hipGetErrorString(e);
+        oge_fail(this, OGE_ERR_HIP, m.c_str());
+        return nullptr;
+    }
+    b.cap = cap;
+    return b.p;
+}
+
+OgeStageTimer *oge_ctx::begin_stage(const char *name) {
+    if (!timing) return nullptr;
+    if (event_pool_used == event_pool.size()) {
+        OgeStageTimer t;
+        hipEventCreate(&t.start);
+        hipEventCreate(&t.stop);
+        event_pool.push_back(t);
+    }
+    OgeStageTimer *t = &event_pool[event_pool_used++];
+    hipEventRecord(t->start, stream);
+    stage_events[name].push_back(*t);
+    return t;
+}
+
+void oge_ctx::end_stage(OgeStageTimer *t) {
+    if (t) hipEventRecord(t->stop, stream);
+}
+
+void oge_ctx::reset_timing() {
+    stage_events.clear();
+    event_pool_used = 0;
+}
+
+extern "C" {
+
+const char *oge_version(void) { return "openge_amd 0.1 (gfx950)"; }
+
+const char *oge_last_error(const oge_ctx *ctx) { return ctx ? ctx->err.c_str() : g_last_error.c_str(); }
+
+int oge_ctx_create(int device, oge_ctx **out) {
+    if (!out) return oge_fail(nullptr, OGE_ERR_ARG, "oge_ctx_create: out is NULL");
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0)
+        return oge_fail(nullptr, OGE_ERR_HIP, "oge_ctx_create: no HIP device (the GPU path has no CPU fallback)");
+    if (device < 0 || device >= ndev) return oge_fail(nullptr, OGE_ERR_ARG, "oge_ctx_create: bad device index");
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return oge_fail(nullptr, OGE_ERR_HIP, hipGetErrorString(e));
+    oge_ctx *c = new oge_ctx();
+    c->device = device;
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return oge_fail(nullptr, OGE_ERR_HIP, hipGetErrorString(e));
+    }
+    c->own_stream = true;
+    *out = c;
+    return OGE_OK;
+}
+
+int oge_ctx_set_stream(oge_ctx *ctx, void *stream) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    hipSetDevice(ctx->device);
+    if (stream) {
+        if (ctx->own_stream) hipStreamDestroy(ctx->stream);
+        ctx->stream = (hipStream_t)stream;
+        ctx->own_stream = false;
+    }
+    return OGE_OK;
+}
+
+void *oge_ctx_stream(oge_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int oge_ctx_sync(oge_ctx *ctx) {
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return OGE_OK;
+}
+
+void oge_ctx_destroy(oge_ctx *ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    for (auto &kv : ctx->bufs)
+        if (kv.second.p) hipFree(kv.second.p);
+    for (auto &t : ctx->event_pool) {
+        hipEventDestroy(t.start);
+        hipEventDestroy(t.stop);
+    }
+    if (ctx->own_stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int oge_ctx_timing(oge_ctx *ctx, const char *stage, double *ms_out) {
+    if (!ctx || !stage || !ms_out) return oge_fail(ctx, OGE_ERR_ARG, "oge_ctx_timing: null argument");
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    double tot = 0;
+    auto it = ctx->stage_events.find(stage);
+    if (it == ctx->stage_events.end()) { *ms_out = -1; return OGE_OK; }
+    for (auto &t : it->second) {
+        float ms = 0;
+        OGE_HIP_TRY(ctx, hipEventElapsedTime(&ms, t.start, t.stop));
+        tot += ms;
+    }
+    *ms_out = tot;
+    return OGE_OK;
+}
+
+// ---------------------------------------------------------------- sort
+int oge_sort_coord_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref, uint32_t *d_perm) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    hipSetDevice(ctx->device);
+    ctx->reset_timing();
+    uint64_t *k;
+    uint32_t *v;
+    int rc = oge_sort_keys_dev(ctx, d_recs, d_off, n, n_ref, &k, &v);
+    if (rc) return rc;
+    if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_perm, v, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    return OGE_OK;
+}
+
+int oge_gather_records_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm, uint64_t n,
+                           uint8_t *d_out, uint64_t *d_out_off) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    hipSetDevice(ctx->device);
+    return oge_gather_with_sizes(ctx, d_recs, d_off, d_perm, nullptr, n, d_out, d_out_off);
+}
+
+static int upload(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const uint64_t *rec_off, uint64_t n, uint8_t **d_recs,
+                  uint64_t **d_off) {
+    *d_recs = (uint8_t *)ctx->ws("host_recs", rec_bytes + 16);
+    *d_off = (uint64_t *)ctx->ws("host_off", (n + 1) * 8);
+    if (!*d_recs || !*d_off) return OGE_ERR_HIP;
+    if (rec_bytes) OGE_HIP_TRY(ctx, hipMemcpyAsync(*d_recs, recs, rec_bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(*d_off, rec_off, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    return OGE_OK;
+}
+
+int oge_sort_coord(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const uint64_t *rec_off, uint64_t n, int32_t n_ref,
+                   uint32_t *perm_out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    hipSetDevice(ctx->device);
+    uint8_t *dr;
+    uint64_t *dof;
+    int rc = upload(ctx, recs, rec_bytes, rec_off, n, &dr, &dof);
+    if (rc) return rc;
+    uint32_t *dp = (uint32_t *)ctx->ws("host_perm", (n + 1) * 4);
+    if (!dp) return OGE_ERR_HIP;
+    rc = oge_sort_coord_dev(ctx, dr, dof, n, n_ref, dp);
+    if (rc) return rc;
+    if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(perm_out, dp, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return OGE_OK;
+}
+
+// ---------------------------------------------------------------- markdup
+int oge_markdup_dev(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
+                    uint8_t *d_dup, int apply, uint64_t *n_dup_out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    hipSetDevice(ctx->device);
+    ctx->reset_timing();
+    uint64_t nd = 0;
+    int rc = oge_markdup_run(ctx, d_recs, d_off, n, opts, d_dup, apply, &nd);
+    if (n_dup_out) *n_dup_out = nd;
+    return rc;
+}
+
+int oge_markdup(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const uint64_t *rec_off, uint64_t n,
+                const oge_markdup_opts *opts, uint8_t *dup_out, uint64_t *n_dup_out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    hipSetDevice(ctx->device);
+    uint8_t *dr;
+    uint64_t *dof;
+    int rc = upload(ctx, recs, rec_bytes, rec_off, n, &dr, &dof);
+    if (rc) return rc;
+    uint8_t *dd = (uint8_t *)ctx->ws("host_dup", n + 1);
+    if (!dd) return OGE_ERR_HIP;
+    rc = oge_markdup_dev(ctx, dr, dof, n, opts, dd, 0, n_dup_out);
+    if (rc) return rc;
+    if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(dup_out, dd, n, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return OGE_OK;
+}
+
+int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
+                         uint32_t *d_perm, uint8_t *d_out, uint64_t *d_out_off, uint64_t *n_dup_out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    hipSetDevice(ctx->device);
+    ctx->reset_timing();
+    uint64_t *k;
+    uint32_t *v;
+    int rc = oge_sort_keys_dev(ctx, d_recs, d_off, n, opts ? opts->n_ref : 0, &k, &v);
+    if (rc) return rc;
+    if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_perm, v, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    rc = oge_gather_with_sizes(ctx, d_recs, d_off, v, k, n, d_out, d_out_off);
+    if (rc) return rc;
+    uint8_t *dd = (uint8_t *)ctx->ws("sm_dup", n + 1);
+    if (!dd) return OGE_ERR_HIP;
+    uint64_t nd = 0;
+    rc = oge_markdup_run(ctx, d_out, d_out_off, n, opts, dd, 1, &nd);
+    if (n_dup_out) *n_dup_out = nd;
+    return rc;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- device synth
+namespace {
+__global__ __launch_bounds__(256) void k_synth_sizes(oge_synth_params P, uint64_t *offs) {
+    uint64_t n = 2 * P.n_pairs;
+    uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s < n) offs[s] = oge_synth_slot_bytes(&P, s);
+    else if (s == n) offs[s] = 0;
+}
+__global__ __launch_bounds__(256) void k_synth_write(oge_synth_params P, const uint64_t *offs, uint8_t *out) {
+    uint64_t n = 2 * P.n_pairs;
+    uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s < n) oge_synth_write_slot(&P, s, out + offs[s]);
+}
+}  // namespace
+
+extern "C" {
+int oge_synth_offsets_dev(oge_ctx *ctx, const void *params, uint64_t *d_offs) {
+    if (!ctx || !params) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    hipSetDevice(ctx->device);
+    const oge_synth_params *P = (const oge_synth_params *)params;
+    uint64_t n = 2 * P->n_pairs;
+    hipLaunchKernelGGL(k_synth_sizes, dim3(oge_ceil_div(n + 1, 256)), dim3(256), 0, ctx->stream, *P, d_offs);
+    OGE_LAUNCH_CHECK(ctx);
+    return oge_exclusive_scan_u64(ctx, d_offs, d_offs, n + 1);
+}
+int oge_synth_records_dev(oge_ctx *ctx, const void *params, const uint64_t *d_offs, uint8_t *d_out) {
+    if (!ctx || !params) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    hipSetDevice(ctx->device);
+    const oge_synth_params *P = (const oge_synth_params *)params;
+    uint64_t n = 2 * P->n_pairs;
+    if (n) {
+        hipLaunchKernelGGL(k_synth_write, dim3(oge_ceil_div(n, 256)), dim3(256), 0, ctx->stream, *P, d_offs, d_out);
+        OGE_LAUNCH_CHECK(ctx);
+    }
+    return OGE_OK;
+}
+}  // extern "C"

@@ -1,0 +1,62 @@
+// oge_ctx.h -- internal device context: stream, grow-only workspace, HIP-event stage timing.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/openge_hip.h"
+#include "capi_common.h"
+
+struct OgeStageTimer {
+    hipEvent_t start, stop;
+};
+
+struct oge_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    struct Buf { void *p = nullptr; size_t cap = 0; };
+    std::map<std::string, Buf> bufs;
+    // stage -> list of (start, stop) event pairs recorded during the last pipeline call
+    std::map<std::string, std::vector<OgeStageTimer>> stage_events;
+    std::vector<OgeStageTimer> event_pool;
+    size_t event_pool_used = 0;
+    bool timing = true;
+
+    // Grow-only named scratch buffer; contents are undefined between calls.
+    void *ws(const char *name, size_t bytes);
+    OgeStageTimer *begin_stage(const char *name);
+    void end_stage(OgeStageTimer *t);
+    void reset_timing();
+};
+
+#define OGE_HIP_TRY(ctx, expr)                                                                     \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess) {                                                                    \
+            std::string _m = std::string(#expr) + ": " + hipGetErrorString(_e);                   \
+            return oge_fail((ctx), OGE_ERR_HIP, _m.c_str());                                       \
+        }                                                                                          \
+    } while (0)
+
+// Launch-error check after a kernel launch.
+#define OGE_LAUNCH_CHECK(ctx) OGE_HIP_TRY(ctx, hipGetLastError())
+
+static inline uint32_t oge_ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+// ---- device primitives (prims.hip) ----
+// In-place-or-not exclusive scans. `out` may alias `in`.
+int oge_exclusive_scan_u32(oge_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n);
+int oge_exclusive_scan_u64(oge_ctx *ctx, const uint64_t *in, uint64_t *out, uint64_t n);
+// Stable LSD radix sort of (key, value) pairs on key bits selected by `bit_mask` (only bits set
+// in the mask are sorted; set bits are grouped into digit passes of <= 8 contiguous bits).
+// Buffers: keys/vals hold the input; ktmp/vtmp scratch of the same size.  On return *kout/*vout
+// point at whichever pair of buffers holds the result.
+int oge_radix_sort_pairs(oge_ctx *ctx, uint64_t *keys, uint32_t *vals, uint64_t *ktmp, uint32_t *vtmp,
+                         uint64_t n, uint64_t bit_mask, uint64_t **kout, uint32_t **vout);
+// OR / AND reduction of a u64 array (for choosing the varying key bits).
+int oge_reduce_or_and_u64(oge_ctx *ctx, const uint64_t *in, uint64_t n, uint64_t mask, uint64_t *or_out, uint64_t *and_out);

@@ -1,0 +1,317 @@
+"""ctypes binding of libopenge_hip.so (the C ABI declared in include/openge_hip.h).
+
+Python is test/bench plumbing here: the product is the C ABI and the C++ `openge` CLI.  Device
+buffers can be torch tensors (``tensor.data_ptr()``) so torch owns HBM allocation and RCCL, and
+the library only runs kernels on the context's stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libopenge_hip.so"
+
+MAX_REF = 64
+
+
+class SynthParams(C.Structure):
+    """Mirror of oge_synth_params (openge_amd/csrc/synth.h)."""
+
+    _fields_ = [
+        ("seed", C.c_uint64), ("n_pairs", C.c_uint64), ("n_ref", C.c_uint32), ("read_len", C.c_uint32),
+        ("ins_min", C.c_uint32), ("ins_max", C.c_uint32), ("dup_ppm", C.c_uint32), ("inter_ppm", C.c_uint32),
+        ("munmap_ppm", C.c_uint32), ("clip_ppm", C.c_uint32), ("n_rg", C.c_uint32), ("qual_min", C.c_uint32),
+        ("qual_max", C.c_uint32), ("shuffle", C.c_uint32),
+        ("ref_len", C.c_uint64 * MAX_REF), ("ref_cum", C.c_uint64 * (MAX_REF + 1)),
+    ]
+
+
+class MarkdupOpts(C.Structure):
+    """Mirror of oge_markdup_opts (include/openge_hip.h)."""
+
+    _fields_ = [
+        ("n_ref", C.c_int32), ("rg_ids", C.c_void_p), ("rg_ids_bytes", C.c_uint64), ("rg_lib", C.c_void_p),
+        ("n_rg", C.c_int32), ("unknown_lib", C.c_int16), ("pad0", C.c_int16),
+        ("compat_nonverbose_index", C.c_int32), ("remove_duplicates", C.c_int32),
+    ]
+
+
+# GRCh38 primary-assembly lengths chr1..22, X, Y (Mbp, rounded) -- relative contig sizes of C2.
+GRCH38_MB = [248.96, 242.19, 198.30, 190.21, 181.54, 170.81, 159.35, 145.14, 138.39, 133.80, 135.09, 133.28,
+             114.36, 107.04, 101.99, 90.34, 83.26, 80.37, 58.62, 64.44, 46.71, 50.82, 156.04, 57.23]
+
+
+def synth_params(n_pairs: int, *, preset: str = "c1", seed: int = 1234, **over) -> SynthParams:
+    """Synthetic read-set parameters.
+
+    preset "c1": SURVEY §8d C1 -- one 5 Mbp contig, 150 bp pairs, 10% duplicate pairs, 1 RG.
+    preset "c2": SURVEY §8d C2 -- 24 contigs with GRCh38 relative lengths scaled to 1.5 Gbp, 8% dup
+                 pairs, 1% inter-contig, 0.5% mate-unmapped, 2 read groups / libraries.
+    preset "mix": small multi-contig set exercising clipping, inter-contig and unmapped mates.
+    """
+    p = SynthParams()
+    p.seed, p.n_pairs, p.read_len = seed, n_pairs, 150
+    p.ins_min, p.ins_max, p.qual_min, p.qual_max, p.shuffle = 250, 450, 2, 40, 1
+    if preset == "c1":
+        p.n_ref, p.n_rg = 1, 1
+        p.ref_len[0] = 5_000_000
+        p.dup_ppm, p.inter_ppm, p.munmap_ppm, p.clip_ppm = 100_000, 0, 0, 0
+    elif preset == "c2":
+        p.n_ref, p.n_rg = 24, 2
+        tot = sum(GRCH38_MB)
+        for i, mb in enumerate(GRCH38_MB):
+            p.ref_len[i] = int(1.5e9 * mb / tot)
+        p.dup_ppm, p.inter_ppm, p.munmap_ppm, p.clip_ppm = 80_000, 10_000, 5_000, 50_000
+    elif preset == "mix":
+        p.n_ref, p.n_rg = 5, 3
+        for i in range(5):
+            p.ref_len[i] = 20_000 + 7_000 * i
+        p.dup_ppm, p.inter_ppm, p.munmap_ppm, p.clip_ppm = 150_000, 40_000, 20_000, 200_000
+    else:
+        raise ValueError(preset)
+    for k, v in over.items():
+        if k == "ref_len":
+            for i, x in enumerate(v):
+                p.ref_len[i] = x
+        else:
+            setattr(p, k, v)
+    return p
+
+
+class OgeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libopenge_hip.so (fails loudly if it has not been built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise OgeError(f"{LIB_PATH} is missing: run `python -m openge_amd.build` (no CPU fallback exists)")
+    L = C.CDLL(str(LIB_PATH))
+    vp, u64, i32, u32 = C.c_void_p, C.c_uint64, C.c_int32, C.c_uint32
+    sig = {
+        "oge_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "oge_ctx_set_stream": (C.c_int, [vp, vp]),
+        "oge_ctx_stream": (vp, [vp]),
+        "oge_ctx_sync": (C.c_int, [vp]),
+        "oge_ctx_destroy": (None, [vp]),
+        "oge_last_error": (C.c_char_p, [vp]),
+        "oge_ctx_timing": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_double)]),
+        "oge_version": (C.c_char_p, []),
+        "oge_sort_coord": (C.c_int, [vp, vp, u64, vp, u64, i32, vp]),
+        "oge_sort_coord_dev": (C.c_int, [vp, vp, vp, u64, i32, vp]),
+        "oge_gather_records_dev": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
+        "oge_markdup": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, C.POINTER(u64)]),
+        "oge_markdup_dev": (C.c_int, [vp, vp, vp, u64, vp, vp, C.c_int, C.POINTER(u64)]),
+        "oge_sort_markdup_dev": (C.c_int, [vp, vp, vp, u64, vp, vp, vp, vp, C.POINTER(u64)]),
+        "oge_synth_finalize": (C.c_int, [vp]),
+        "oge_synth_params_size": (u64, []),
+        "oge_synth_offsets_host": (C.c_int, [vp, vp, C.c_int]),
+        "oge_synth_records_host": (C.c_int, [vp, vp, vp, C.c_int]),
+        "oge_synth_header_text": (C.c_int, [vp, vp, u64, C.POINTER(u64)]),
+        "oge_synth_offsets_dev": (C.c_int, [vp, vp, vp]),
+        "oge_synth_records_dev": (C.c_int, [vp, vp, vp, vp]),
+        "oge_bam_read": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(vp)]),
+        "oge_bam_free": (None, [vp]),
+        "oge_bam_count": (u64, [vp]),
+        "oge_bam_records": (vp, [vp, C.POINTER(u64)]),
+        "oge_bam_offsets": (vp, [vp]),
+        "oge_bam_n_ref": (i32, [vp]),
+        "oge_bam_header_text": (C.c_int, [vp, vp, u64, C.POINTER(u64)]),
+        "oge_bam_markdup_opts": (C.c_int, [vp, vp, C.POINTER(vp), C.POINTER(vp)]),
+        "oge_bam_write": (C.c_int, [C.c_char_p, C.c_char_p, u64, C.c_int, vp, vp, u64, vp, vp, C.c_int, C.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name, None)
+        if f is None:
+            continue
+        f.restype, f.argtypes = res, args
+    _lib = L
+    return L
+
+
+def exported_symbols() -> list[str]:
+    """Symbols include/openge_hip.h declares (parsed from the header)."""
+    import re
+
+    text = (PKG.parent / "include" / "openge_hip.h").read_text()
+    return sorted(set(re.findall(r"\b(oge_[a-z0-9_]+)\s*\(", text)))
+
+
+def check(rc: int, ctx=None) -> None:
+    if rc != 0:
+        msg = lib().oge_last_error(ctx)
+        raise OgeError(f"openge_hip error {rc}: {msg.decode() if msg else ''}")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+# ------------------------------------------------------------------------- synthetic data (host)
+def synth_host(p: SynthParams, threads: int = 0) -> tuple[np.ndarray, np.ndarray, str]:
+    """Generate the records on the host: (recs u8, offs u64[n+1], header text)."""
+    L = lib()
+    check(L.oge_synth_finalize(C.byref(p)))
+    n = 2 * p.n_pairs
+    offs = np.empty(n + 1, dtype=np.uint64)
+    check(L.oge_synth_offsets_host(C.byref(p), _ptr(offs), threads))
+    recs = np.empty(int(offs[-1]) + 16, dtype=np.uint8)
+    check(L.oge_synth_records_host(C.byref(p), _ptr(offs), _ptr(recs), threads))
+    ln = C.c_uint64()
+    check(L.oge_synth_header_text(C.byref(p), None, 0, C.byref(ln)))
+    buf = C.create_string_buffer(ln.value + 1)
+    check(L.oge_synth_header_text(C.byref(p), buf, ln.value + 1, None))
+    return recs, offs, buf.value.decode()
+
+
+# ------------------------------------------------------------------------- BAM files
+class Bam:
+    """A BAM file decoded into one record arena (records in file order)."""
+
+    def __init__(self, path: str | os.PathLike, threads: int = 8):
+        L = lib()
+        h = C.c_void_p()
+        check(L.oge_bam_read(str(path).encode(), threads, C.byref(h)))
+        self._h = h
+        n = L.oge_bam_count(h)
+        nb = C.c_uint64()
+        rp = L.oge_bam_records(h, C.byref(nb))
+        self.n = int(n)
+        self.recs = np.ctypeslib.as_array((C.c_uint8 * nb.value).from_address(rp)) if nb.value else np.zeros(0, np.uint8)
+        op = L.oge_bam_offsets(h)
+        self.offs = np.ctypeslib.as_array((C.c_uint64 * self.n).from_address(op)) if self.n else np.zeros(0, np.uint64)
+        self.n_ref = int(L.oge_bam_n_ref(h))
+        ln = C.c_uint64()
+        check(L.oge_bam_header_text(h, None, 0, C.byref(ln)))
+        buf = C.create_string_buffer(ln.value + 1)
+        check(L.oge_bam_header_text(h, buf, ln.value + 1, None))
+        self.header_text = buf.value.decode()
+
+    def markdup_opts(self) -> tuple[MarkdupOpts, tuple]:
+        o = MarkdupOpts()
+        ids, libs = C.c_void_p(), C.c_void_p()
+        check(lib().oge_bam_markdup_opts(self._h, C.byref(o), C.byref(ids), C.byref(libs)))
+        return o, (ids, libs)
+
+    def __del__(self):
+        try:
+            lib().oge_bam_free(self._h)
+        except Exception:
+            pass
+
+
+def markdup_opts_from_header(header_text: str, n_ref: int, compat_nonverbose: bool = False) -> tuple[MarkdupOpts, tuple]:
+    """RG -> library table as MarkDuplicates::getLibraryName resolves it (mark_duplicates.cpp:301-318)."""
+    ids, libs, names = [], [], {}
+    for line in header_text.splitlines():
+        if not line.startswith("@RG\t"):
+            continue
+        f = dict(x.split(":", 1) for x in line.split("\t")[1:] if len(x) >= 3)
+        lb = f.get("LB", "") or "Unknown Library"
+        names.setdefault(lb, len(names) + 1)
+        ids.append(f.get("ID", ""))
+        libs.append(names[lb])
+    unknown = names.get("Unknown Library", len(names) + 1)
+    idbuf = b"".join(i.encode() + b"\0" for i in ids)
+    ida = np.frombuffer(idbuf + b"\0", dtype=np.uint8).copy()
+    liba = np.array(libs + [0], dtype=np.int16)
+    o = MarkdupOpts()
+    o.n_ref, o.rg_ids, o.rg_ids_bytes = n_ref, _ptr(ida), len(idbuf)
+    o.rg_lib, o.n_rg, o.unknown_lib = _ptr(liba), len(ids), unknown
+    o.compat_nonverbose_index = 1 if compat_nonverbose else 0
+    return o, (ida, liba)
+
+
+def write_bam(path, header_text: str, recs: np.ndarray, offs: np.ndarray, n: int, order=None, flags=None,
+              sort_order: int = -1, level: int = 6, threads: int = 8) -> None:
+    L = lib()
+    hb = header_text.encode()
+    check(L.oge_bam_write(str(path).encode(), hb, len(hb), sort_order, _ptr(recs), _ptr(offs), n,
+                          _ptr(order) if order is not None else None, _ptr(flags) if flags is not None else None,
+                          level, threads))
+
+
+# ------------------------------------------------------------------------- device context
+class Context:
+    """A HIP device context (one per process/GPU)."""
+
+    def __init__(self, device: int = 0, stream: int | None = None):
+        L = lib()
+        h = C.c_void_p()
+        check(L.oge_ctx_create(device, C.byref(h)))
+        self.h = h
+        if stream:
+            check(L.oge_ctx_set_stream(h, C.c_void_p(stream)), h)
+
+    def close(self):
+        if self.h:
+            lib().oge_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return lib().oge_ctx_stream(self.h) or 0
+
+    def sync(self):
+        check(lib().oge_ctx_sync(self.h), self.h)
+
+    def timing(self, stage: str) -> float:
+        ms = C.c_double()
+        check(lib().oge_ctx_timing(self.h, stage.encode(), C.byref(ms)), self.h)
+        return ms.value
+
+    # host-buffer entry points
+    def sort_coord(self, recs: np.ndarray, offs: np.ndarray, n: int, n_ref: int) -> np.ndarray:
+        perm = np.empty(max(n, 1), dtype=np.uint32)
+        check(lib().oge_sort_coord(self.h, _ptr(recs), recs.nbytes, _ptr(offs), n, n_ref, _ptr(perm)), self.h)
+        return perm[:n]
+
+    def markdup(self, recs: np.ndarray, offs: np.ndarray, n: int, opts: MarkdupOpts) -> tuple[np.ndarray, int]:
+        dup = np.empty(max(n, 1), dtype=np.uint8)
+        nd = C.c_uint64()
+        check(lib().oge_markdup(self.h, _ptr(recs), recs.nbytes, _ptr(offs), n, C.byref(opts), _ptr(dup),
+                                C.byref(nd)), self.h)
+        return dup[:n], nd.value
+
+    # device entry points (pointers are ints, e.g. torch tensor .data_ptr())
+    def sort_coord_dev(self, d_recs: int, d_off: int, n: int, n_ref: int, d_perm: int) -> None:
+        check(lib().oge_sort_coord_dev(self.h, d_recs, d_off, n, n_ref, d_perm), self.h)
+
+    def gather_records_dev(self, d_recs, d_off, d_perm, n, d_out, d_out_off) -> None:
+        check(lib().oge_gather_records_dev(self.h, d_recs, d_off, d_perm, n, d_out, d_out_off), self.h)
+
+    def markdup_dev(self, d_recs, d_off, n, opts: MarkdupOpts, d_dup, apply: bool = True) -> int:
+        nd = C.c_uint64()
+        check(lib().oge_markdup_dev(self.h, d_recs, d_off, n, C.byref(opts), d_dup, 1 if apply else 0, C.byref(nd)),
+              self.h)
+        return nd.value
+
+    def sort_markdup_dev(self, d_recs, d_off, n, opts: MarkdupOpts, d_perm, d_out, d_out_off) -> int:
+        nd = C.c_uint64()
+        check(lib().oge_sort_markdup_dev(self.h, d_recs, d_off, n, C.byref(opts), d_perm, d_out, d_out_off,
+                                         C.byref(nd)), self.h)
+        return nd.value
+
+    def synth_dev(self, p: SynthParams, d_offs: int, d_out: int | None) -> None:
+        L = lib()
+        check(L.oge_synth_finalize(C.byref(p)))
+        if d_offs:
+            check(L.oge_synth_offsets_dev(self.h, C.byref(p), d_offs), self.h)
+        if d_out:
+            check(L.oge_synth_records_dev(self.h, C.byref(p), d_offs, d_out), self.h)

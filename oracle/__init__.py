@@ -1,0 +1,84 @@
+"""TEST INFRASTRUCTURE ONLY -- CPU oracle for the openge_amd parity tests.
+
+`oge_oracle.c` restates the reference's coordinate sort order (util/bamtools/Sort.h:116-133) and
+MarkDuplicates (algorithms/mark_duplicates.cpp:185-540) in plain C.  Only tests/, the smoke check
+in __graft_entry__ and bench.py's cpu_baseline leg may use this package, and only as the checker
+or the timed CPU baseline -- never as the thing measured or shipped.
+
+The restatement is pinned against the reference itself: oracle/_ref/ref_driver is built from the
+reference's own sources (oracle/Makefile.ref) and its outputs are the committed goldens under
+tests/golden/ (see tests/golden/make_goldens.py and tests/test_oracle.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+SO = HERE / "liboge_oracle.so"
+SRC = HERE / "oge_oracle.c"
+REF_DRIVER = HERE / "_ref" / "ref_driver"
+
+
+def build() -> Path:
+    if not SO.exists() or SO.stat().st_mtime < SRC.stat().st_mtime:
+        subprocess.run(["gcc", "-O2", "-std=c99", "-fPIC", "-shared", "-o", str(SO), str(SRC)], check=True)
+    return SO
+
+
+def build_ref() -> Path | None:
+    """Build oracle/_ref/ref_driver from /root/reference (only where the reference is present)."""
+    if not Path("/root/reference/openge/src").exists():
+        return None
+    subprocess.run(["make", "-s", "-f", str(HERE / "Makefile.ref"), "-j8"], check=True, cwd=str(HERE.parent))
+    return REF_DRIVER
+
+
+_lib = None
+
+
+def _L():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(str(SO))
+        L.oracle_sort_perm.restype = C.c_int
+        L.oracle_sort_perm.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.oracle_markdup.restype = C.c_int64
+        L.oracle_markdup.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
+                                     C.c_int32, C.c_int16, C.c_int, C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def sort_perm(recs: np.ndarray, offs: np.ndarray, n: int) -> np.ndarray:
+    """perm[k] = input index at sorted position k (Sort::ByPosition, input-index tie-break)."""
+    perm = np.empty(max(n, 1), dtype=np.uint32)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    if _L().oracle_sort_perm(recs.ctypes.data, offs.ctypes.data, n, perm.ctypes.data) != 0:
+        raise MemoryError("oracle_sort_perm")
+    return perm[:n]
+
+
+def markdup(recs: np.ndarray, offs: np.ndarray, n: int, header_text: str, compat_nonverbose: bool = False):
+    """dup[i] in {0,1,2} (2 = non-primary, untouched) and the number of records flagged."""
+    ids, libs, names = [], [], {}
+    for line in header_text.splitlines():
+        if line.startswith("@RG\t"):
+            f = dict(x.split(":", 1) for x in line.split("\t")[1:] if len(x) >= 3)
+            lb = f.get("LB", "") or "Unknown Library"
+            names.setdefault(lb, len(names) + 1)
+            ids.append(f.get("ID", ""))
+            libs.append(names[lb])
+    unknown = names.get("Unknown Library", len(names) + 1)
+    idbuf = b"".join(i.encode() + b"\0" for i in ids) + b"\0"
+    ida = np.frombuffer(idbuf, dtype=np.uint8).copy()
+    liba = np.array(libs + [0], dtype=np.int16)
+    dup = np.empty(max(n, 1), dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    nd = _L().oracle_markdup(recs.ctypes.data, offs.ctypes.data, n, ida.ctypes.data, len(idbuf) - 1,
+                             liba.ctypes.data, len(ids), unknown, 1 if compat_nonverbose else 0, dup.ctypes.data)
+    return dup[:n], int(nd)

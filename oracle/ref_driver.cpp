@@ -1,0 +1,131 @@
+// ref_driver.cpp -- TEST INFRASTRUCTURE ONLY (oracle/_ref harness).
+//
+// Own code (not copied from the reference).  It links against the reference's
+// own algorithm modules, compiled from /root/reference by oracle/Makefile.ref,
+// and wires the same module chains the reference commands build:
+//   sort       : FileReader -> ReadSorter -> sink     (cmd/command_mergesort.cpp:77-117, no -M)
+//   dedup      : FileReader -> MarkDuplicates -> sink (cmd/command_dedup.cpp:48-69, --nosplit)
+//   sortdedup  : FileReader -> ReadSorter -> MarkDuplicates -> sink (command_mergesort.cpp:68-117, -M --nosplit)
+//   realign    : FileReader -> LocalRealignment -> sink (cmd/command_localrealign.cpp:37-75)
+// The sink writes BGZF BAM through the reference's BamSerializer<BgzfOutputStream>,
+// i.e. exactly the serializer FileWriter uses (alg/file_writer.cpp:144-166), with
+// no @PG line (the `--nopg` behaviour).  Global settings mirror
+// cmd/commands.cpp:67-84.
+//
+// It is never shipped and never runs on the GPU box.
+
+#include "algorithms/algorithm_module.h"
+#include "algorithms/file_reader.h"
+#include "algorithms/read_sorter.h"
+#include "algorithms/mark_duplicates.h"
+#include "algorithms/local_realignment.h"
+#include "util/bam_serializer.h"
+#include "util/bgzf_output_stream.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <iostream>
+
+class CaptureSink : public AlgorithmModule {
+public:
+    std::string filename;
+    int level;
+    CaptureSink() : level(6) {}
+protected:
+    virtual int runInternal() {
+        BamHeader header = getHeader();
+        BamSerializer<BgzfOutputStream> writer;
+        writer.getOutputStream().setCompressionLevel(level);
+        if (!writer.open(filename, header)) {
+            std::cerr << "ref_driver: cannot open " << filename << std::endl;
+            exit(2);
+        }
+        while (true) {
+            OGERead *r = getInputAlignment();
+            if (!r) break;
+            writer.write(*r);
+            putOutputAlignment(r);
+        }
+        writer.close();
+        return 0;
+    }
+};
+
+static void usage() {
+    fprintf(stderr,
+            "usage: ref_driver sort|dedup|sortdedup|realign [-v] [-t N] [-n N] [-T tmpdir] [-c level]\n"
+            "                  [-R ref.fa -L intervals] in.bam out.bam\n");
+    exit(2);
+}
+
+int main(int argc, char **argv) {
+    if (argc < 4) usage();
+    std::string mode = argv[1];
+    bool verbose = false;
+    int threads = 8, per_tmp = 500000, level = 6;
+    std::string tmpdir = "/tmp", ref, intervals;
+    std::vector<std::string> pos;
+    for (int i = 2; i < argc; i++) {
+        std::string a = argv[i];
+        if (a == "-v") verbose = true;
+        else if (a == "-t" && i + 1 < argc) threads = atoi(argv[++i]);
+        else if (a == "-n" && i + 1 < argc) per_tmp = atoi(argv[++i]);
+        else if (a == "-T" && i + 1 < argc) tmpdir = argv[++i];
+        else if (a == "-c" && i + 1 < argc) level = atoi(argv[++i]);
+        else if (a == "-R" && i + 1 < argc) ref = argv[++i];
+        else if (a == "-L" && i + 1 < argc) intervals = argv[++i];
+        else pos.push_back(a);
+    }
+    if (pos.size() != 2) usage();
+    tmpdir += "/";
+
+    OGEParallelismSettings::setNumberThreads(threads);
+    AlgorithmModule::setNothreads(false);
+    AlgorithmModule::setVerbose(verbose);
+    OGEParallelismSettings::enableMultithreading();
+
+    FileReader reader;
+    reader.setLoadStringData(false);
+    reader.addFile(pos[0]);
+    CaptureSink sink;
+    sink.filename = pos[1];
+    sink.level = level;
+
+    if (mode == "sort" || mode == "sortdedup") {
+        ReadSorter sorter(tmpdir);
+        MarkDuplicates md(tmpdir);
+        sorter.setSortBy(BamHeader::SORT_COORDINATE);
+        sorter.setCompressTempFiles(false);
+        sorter.setAlignmentsPerTempfile(per_tmp);
+        reader.addSink(&sorter);
+        if (mode == "sortdedup") {
+            sorter.addSink(&md);
+            md.addSink(&sink);
+        } else {
+            sorter.addSink(&sink);
+        }
+        sink.runChain();
+    } else if (mode == "dedup") {
+        MarkDuplicates md(tmpdir);
+        reader.addSink(&md);
+        md.addSink(&sink);
+        sink.runChain();
+    } else if (mode == "realign") {
+        if (ref.empty() || intervals.empty()) usage();
+        LocalRealignment lr;
+        reader.addSink(&lr);
+        lr.addSink(&sink);
+        lr.verbose = verbose;
+        lr.setReferenceFilename(ref);
+        lr.setIntervalsFilename(intervals);
+        reader.runChain();
+    } else {
+        usage();
+    }
+    OGERead::clearCachedAllocations();
+    ThreadPool::closeSharedPool();
+    return 0;
+}
