@@ -96,6 +96,13 @@ def lib() -> C.CDLL:
         return _lib
     if not LIB_PATH.exists():
         raise OgeError(f"{LIB_PATH} is missing: run `python -m openge_amd.build` (no CPU fallback exists)")
+    # torch wheels bundle their own libamdhip64.so.7.  Load torch first so the dynamic loader
+    # resolves our NEEDED libamdhip64.so.7 to that same, already-loaded runtime: two HIP runtimes
+    # in one process make the second one see no GPUs.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     L = C.CDLL(str(LIB_PATH))
     vp, u64, i32, u32 = C.c_void_p, C.c_uint64, C.c_int32, C.c_uint32
     sig = {
