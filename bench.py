@@ -1,0 +1,182 @@
+#!/usr/bin/env python
+"""bench.py -- OpenGE post-alignment hot path on MI355X.
+
+Metric (BASELINE.json): Mreads/s of sort+dedup (`openge mergesort -M --nosplit` semantics: coordinate
+sort, Picard MarkDuplicates with -v semantics, output records re-encoded with bin recompute and
+FLAG 0x400 applied).  Workload at N=1: configs[1]+[2] -- a 300M-read (150M pairs) 30x WGS-shaped
+synthetic read set (SURVEY.md §8d C2 generator, seed 1234), generated straight into HBM; one step =
+the whole device pipeline over the resident records (oge_sort_markdup_dev).
+
+Multi-GPU (torchrun, one rank per GPU): every rank processes its own 300M-read shard (a different
+seed), i.e. N independent per-sample pipelines -- weak scaling, no data-path collective (DESIGN.md
+"Multi-GPU").  value = reads of all ranks / max-over-ranks wall time.
+
+Also reported on the same JSON line:
+  roofline     -- dominant kernel (the permutation gather, algorithmic bytes 2*B per launch, B = record
+                  bytes) timed live with HIP events on the stream it runs on; traffic from the committed
+                  rocprofv3 PMC summary when present (profiles/)
+  pipeline     -- the same for the whole step (algorithmic bytes of SURVEY §8d: sort 2B + dedup B-seq+2N)
+  cpu_baseline -- the oracle port (oracle/oge_oracle.c, single thread, in memory) timed on this box's host
+                  on a bounded C2-shaped sample
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "Mreads/sec sort+dedup (and realign intervals/sec), 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
+STAGES = ["sort_keypack", "sort_radix", "sort_ties", "gather_offsets", "gather_records", "md_readends", "md_matejoin",
+          "md_pairs", "md_frags", "md_apply"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pairs", type=int, default=150_000_000, help="read pairs per GPU (default 150M = 300M reads)")
+    ap.add_argument("--cpu-sample-reads", type=int, default=8_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(sample_reads: int) -> dict:
+    """The oracle port (TEST INFRASTRUCTURE, timed as the CPU baseline only) on a C2-shaped sample."""
+    import oracle
+    from openge_amd import lib as L
+
+    p = L.synth_params(sample_reads // 2, preset="c2", seed=1234)
+    recs, offs, hdr = L.synth_host(p)
+    n = 2 * (sample_reads // 2)
+    t0 = time.perf_counter()
+    perm = oracle.sort_perm(recs, offs, n)
+    oracle.markdup(recs, offs[:-1][perm], n, hdr)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mreads/s", "cores": 1, "kind": "port",
+            "sample": f"{n} reads of the C2 generator (seed 1234), in-memory oracle sort + markdup, 1 thread",
+            "seconds": round(dt, 2)}
+
+
+def pmc_traffic() -> dict | None:
+    f = ROOT / "profiles" / "pmc_gather_records.json"
+    if f.exists():
+        try:
+            return json.loads(f.read_text())
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from openge_amd import lib as L
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")  # RCCL on ROCm
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+    ctx = L.Context(local, stream=stream.cuda_stream)
+
+    # ---- inputs resident in HBM before the timed region ----
+    p = L.synth_params(args.pairs, preset="c2", seed=1234 + rank)
+    n = 2 * args.pairs
+    d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ctx.synth_dev(p, d_offs.data_ptr(), None)
+    ctx.sync()
+    B = int(d_offs[-1].item())
+    d_recs = torch.empty(B + 64, dtype=torch.uint8, device=dev)
+    ctx.synth_dev(p, d_offs.data_ptr(), d_recs.data_ptr())
+    d_out = torch.empty(B + 64, dtype=torch.uint8, device=dev)
+    d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_perm = torch.empty(n, dtype=torch.int32, device=dev)
+    hdr_len = 1 << 16
+    import ctypes as C
+    buf = C.create_string_buffer(hdr_len)
+    L.check(L.lib().oge_synth_header_text(C.byref(p), buf, hdr_len, None))
+    opts, keep = L.markdup_opts_from_header(buf.value.decode(), p.n_ref)
+    ctx.sync()
+
+    def step():
+        return ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(), d_out.data_ptr(),
+                                    d_out_off.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    stage_tot = {s: 0.0 for s in STAGES}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ndup = 0
+    for _ in range(args.steps):
+        ndup = step()
+        for s in STAGES:  # HIP events recorded around each stage on the context stream
+            ms = ctx.timing(s)
+            stage_tot[s] += max(ms, 0.0)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    if rank == 0:
+        K = args.steps
+        ms_step = dt / K * 1e3
+        reads_total = n * world
+        value = reads_total * K / dt / 1e6
+        stages_ms = {s: round(v / K, 3) for s, v in stage_tot.items()}
+        t_gather = stages_ms["gather_records"] / 1e3
+        gather_bytes = 2 * B  # sort = 2*B (each record read once, written once)
+        achieved = gather_bytes / t_gather / 1e9 if t_gather > 0 else 0.0
+        seq_bytes = n * ((p.read_len + 1) // 2)
+        pipe_bytes = 2 * B + (B - seq_bytes) + 2 * n
+        pipe_gbs = pipe_bytes / (ms_step / 1e3) / 1e9
+        pmc = pmc_traffic()
+        roof = {"kernel": "k_gather_records (permutation gather + BAM re-encode)", "bound": "hbm",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                "algorithmic_bytes": gather_bytes, "avg_ms": stages_ms["gather_records"]}
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Mreads/s", "n_gpus": world, "steps": K,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234+rank; records resident in HBM",
+            "config": {"workload": "C2+C3 sort+dedup (mergesort -M --nosplit semantics), 300M reads/GPU",
+                       "reads_per_gpu": n, "record_bytes_per_gpu": B, "duplicates_flagged": ndup,
+                       "parallelism": f"{world} independent per-GPU pipelines" if world > 1 else "1 GPU"},
+            "roofline": roof,
+            "pipeline": {"algorithmic_bytes": pipe_bytes, "achieved": round(pipe_gbs, 1), "unit": "GB/s",
+                         "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)},
+            "stages_ms": stages_ms,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(args.cpu_sample_reads)
+            cb["gpu_speedup"] = round(value / cb["value"], 1)
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -67,6 +67,7 @@ typedef struct oge_pair_place {
     uint8_t kind;      // 0 = FR pair, 1 = inter-contig, 2 = second mate unmapped
     uint8_t pad;
     int32_t ins;
+    uint64_t src;      // pair whose placement (and read group) this pair copies
 } oge_pair_place;
 
 OGE_HD int oge_synth_is_dup(const oge_synth_params *P, uint64_t p) {
@@ -138,7 +139,9 @@ OGE_HD oge_pair_place oge_synth_place(const oge_synth_params *P, uint64_t p) {
             if (!oge_synth_is_dup(P, q)) { src = q; break; }
         }
     }
-    return oge_synth_base_place(P, src);
+    oge_pair_place pl = oge_synth_base_place(P, src);
+    pl.src = src;
+    return pl;
 }
 
 // Per-read soft clip: returns clip length (0 = none), *at_start = clip before the M block.
@@ -203,7 +206,12 @@ OGE_HD void oge_synth_write_slot(const oge_synth_params *P, uint64_t slot, uint8
     if (mapped && pl.rev[m]) flag |= OGE_F_REVERSE;
     if (mate_mapped && pl.rev[o]) flag |= OGE_F_MREVERSE;
 
-    int32_t pos = pl.pos[m];
+    // A soft clip before the aligned block moves the alignment start right, so the unclipped
+    // 5' end (what MarkDuplicates keys on) stays at the fragment end, as an aligner reports it.
+    int32_t pos = pl.pos[m] + ((mapped && clip && at_start) ? (int32_t)clip : 0);
+    int mate_at_start = 0;
+    uint32_t mate_clip = mate_mapped ? oge_synth_clip(P, p, o, &mate_at_start) : 0;
+    int32_t mpos = pl.pos[o] + ((mate_mapped && mate_clip && mate_at_start) ? (int32_t)mate_clip : 0);
     int32_t tlen = 0;
     if (pl.kind == 0) tlen = (pl.pos[m] <= pl.pos[o] && !pl.rev[m]) ? pl.ins : -pl.ins;
     uint32_t mlen = L - clip;
@@ -219,7 +227,7 @@ OGE_HD void oge_synth_write_slot(const oge_synth_params *P, uint64_t slot, uint8
     oge_wr_u16(out + OGE_OFF_FLAG, (uint16_t)flag);
     oge_wr_u32(out + OGE_OFF_LSEQ, L);
     oge_wr_u32(out + OGE_OFF_MREFID, (uint32_t)pl.ref[o]);
-    oge_wr_u32(out + OGE_OFF_MPOS, (uint32_t)pl.pos[o]);
+    oge_wr_u32(out + OGE_OFF_MPOS, (uint32_t)mpos);
     oge_wr_u32(out + OGE_OFF_TLEN, (uint32_t)tlen);
 
     uint8_t *q = out + OGE_OFF_NAME;
@@ -256,6 +264,6 @@ OGE_HD void oge_synth_write_slot(const oge_synth_params *P, uint64_t slot, uint8
     }
     q += L;
 
-    uint32_t rg = 1 + (uint32_t)(oge_rng(P->seed, p, 5) % P->n_rg);
+    uint32_t rg = 1 + (uint32_t)(oge_rng(P->seed, pl.src, 5) % P->n_rg);
     q[0] = 'R'; q[1] = 'G'; q[2] = 'Z'; q[3] = 'r'; q[4] = 'g'; q[5] = (uint8_t)('0' + rg); q[6] = 0;
 }

@@ -151,6 +151,7 @@ def exported_symbols() -> list[str]:
     import re
 
     text = (PKG.parent / "include" / "openge_hip.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(oge_[a-z0-9_]+)\s*\(", text)))
 
 
@@ -173,6 +174,7 @@ def synth_host(p: SynthParams, threads: int = 0) -> tuple[np.ndarray, np.ndarray
     offs = np.empty(n + 1, dtype=np.uint64)
     check(L.oge_synth_offsets_host(C.byref(p), _ptr(offs), threads))
     recs = np.empty(int(offs[-1]) + 16, dtype=np.uint8)
+    recs[-16:] = 0
     check(L.oge_synth_records_host(C.byref(p), _ptr(offs), _ptr(recs), threads))
     ln = C.c_uint64()
     check(L.oge_synth_header_text(C.byref(p), None, 0, C.byref(ln)))
