@@ -33,8 +33,8 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mreads/sec sort+dedup (and realign intervals/sec), 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
-STAGES = ["sort_keypack", "sort_radix", "sort_ties", "gather_offsets", "gather_records", "md_readends", "md_matejoin",
-          "md_pairs", "md_frags", "md_apply"]
+STAGES = ["input_pass", "sort_radix", "sort_ties", "meta_gather", "md_matejoin", "md_pairs", "md_frags", "md_apply",
+          "gather_offsets", "gather_records"]
 
 
 def parse():

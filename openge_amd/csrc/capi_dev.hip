@@ -3,16 +3,25 @@
 #include "oge_ctx.h"
 #include "bam_layout.h"
 #include "synth.h"
+#include "records.h"
 
 #include <cstdio>
 #include <cstring>
 #include <string>
 
 // implemented in sort.hip / markdup.hip
+int oge_sort_buffers(oge_ctx *ctx, uint64_t n, uint64_t **keys, uint32_t **vals);
+unsigned int *oge_sort_counts(oge_ctx *ctx);
 int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
-                      uint64_t **kout, uint32_t **vout);
+                      bool keys_ready, uint64_t **kout, uint32_t **vout);
 int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
-                          const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off);
+                          const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
+                          const RecMeta *smeta, const uint8_t *d_dup);
+int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, const char *name, RecMeta **meta,
+                        OgeRgTable *rg);
+int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
+                       const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out);
+int oge_meta_gather(oge_ctx *ctx, const RecMeta *in, const uint32_t *perm, uint64_t n, RecMeta *out);
 int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
                     uint8_t *d_dup, int apply, uint64_t *n_dup_out);
 
@@ -151,7 +160,7 @@ int oge_sort_coord_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_of
     ctx->reset_timing();
     uint64_t *k;
     uint32_t *v;
-    int rc = oge_sort_keys_dev(ctx, d_recs, d_off, n, n_ref, &k, &v);
+    int rc = oge_sort_keys_dev(ctx, d_recs, d_off, n, n_ref, false, &k, &v);
     if (rc) return rc;
     if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_perm, v, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
     return OGE_OK;
@@ -161,7 +170,8 @@ int oge_gather_records_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *
                            uint8_t *d_out, uint64_t *d_out_off) {
     if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
     hipSetDevice(ctx->device);
-    return oge_gather_with_sizes(ctx, d_recs, d_off, d_perm, nullptr, n, d_out, d_out_off);
+    ctx->reset_timing();
+    return oge_gather_with_sizes(ctx, d_recs, d_off, d_perm, nullptr, n, d_out, d_out_off, nullptr, nullptr);
 }
 
 static int upload(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const uint64_t *rec_off, uint64_t n, uint8_t **d_recs,
@@ -222,22 +232,58 @@ int oge_markdup(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const uin
 
 int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
                          uint32_t *d_perm, uint8_t *d_out, uint64_t *d_out_off, uint64_t *n_dup_out) {
+    // mergesort -M --nosplit on device:
+    //   1 input pass   : sort keys + 32-byte ReadEnds summaries, records read once in input order
+    //   2 sort         : radix sort of the coordinate keys, name/flag tie runs
+    //   3 meta gather  : summaries into sorted order (record index = sorted position, as in the
+    //                    reference where MarkDuplicates consumes the sorter's output stream)
+    //   4 markdup      : mate join, pair/fragment groups -> dup[] in sorted order
+    //   5 record gather: sorted records written once with bin recomputed and 0x400 applied
     if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if (!opts) return oge_fail(ctx, OGE_ERR_ARG, "sort_markdup: opts is NULL");
     hipSetDevice(ctx->device);
     ctx->reset_timing();
+    RecMeta *meta_in;
+    OgeRgTable rg;
+    int rc = oge_markdup_prepare(ctx, opts, n, "md_meta_in", &meta_in, &rg);
+    if (rc) return rc;
+    uint64_t *keys;
+    uint32_t *vals;
+    if (oge_sort_buffers(ctx, n, &keys, &vals)) return OGE_ERR_HIP;
+    unsigned int *counts = oge_sort_counts(ctx);
+    if (!counts) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 16, ctx->stream));
+    OgeStageTimer *t = ctx->begin_stage("input_pass");
+    OgePassArgs a = {};
+    a.recs = d_recs;
+    a.off = d_off;
+    a.n = n;
+    a.meta = meta_in;
+    a.rg = rg;
+    a.keys = keys;
+    a.vals = vals;
+    a.n_ref = opts->n_ref;
+    a.bad = counts + 2;
+    rc = oge_input_pass(ctx, a);
+    if (rc) return rc;
+    ctx->end_stage(t);
     uint64_t *k;
     uint32_t *v;
-    int rc = oge_sort_keys_dev(ctx, d_recs, d_off, n, opts ? opts->n_ref : 0, &k, &v);
+    rc = oge_sort_keys_dev(ctx, d_recs, d_off, n, opts->n_ref, true, &k, &v);
     if (rc) return rc;
     if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_perm, v, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
-    rc = oge_gather_with_sizes(ctx, d_recs, d_off, v, k, n, d_out, d_out_off);
-    if (rc) return rc;
+    RecMeta *meta = (RecMeta *)ctx->ws("md_meta", (n + 1) * sizeof(RecMeta));
     uint8_t *dd = (uint8_t *)ctx->ws("sm_dup", n + 1);
-    if (!dd) return OGE_ERR_HIP;
+    if (!meta || !dd) return OGE_ERR_HIP;
+    t = ctx->begin_stage("meta_gather");
+    rc = oge_meta_gather(ctx, meta_in, v, n, meta);
+    if (rc) return rc;
+    ctx->end_stage(t);
     uint64_t nd = 0;
-    rc = oge_markdup_run(ctx, d_out, d_out_off, n, opts, dd, 1, &nd);
+    rc = oge_markdup_finish(ctx, (uint8_t *)d_recs, d_off, n, opts, meta, dd, 0, &nd);
+    if (rc) return rc;
     if (n_dup_out) *n_dup_out = nd;
-    return rc;
+    return oge_gather_with_sizes(ctx, d_recs, d_off, v, k, n, d_out, d_out_off, meta, dd);
 }
 
 }  // extern "C"

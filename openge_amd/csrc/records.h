@@ -1,0 +1,57 @@
+// records.h -- per-record metadata shared by records.hip (producer) and markdup.hip (consumer).
+#pragma once
+#include <stdint.h>
+
+// RecMeta.m (u64):
+//   [0,16)  score (int16, getScore)        [16,32) library id
+//   bit 32 fragment ReadEnds exists (mapped, refID != -1, primary)   bit 33 reverse strand
+//   bit 34 pair candidate (paired && mate mapped)                    bit 35 primary (0x100 clear)
+//   bit 36 isPaired() (read2Sequence = mate refID != -1)             [40,48) original FLAG >> 8
+//   [48,64) bin the writer must store (recomputed, util/bam_serializer.h:112-116)
+constexpr uint64_t OGE_M_FRAG = 1ull << 32, OGE_M_REV = 1ull << 33, OGE_M_CAND = 1ull << 34,
+                   OGE_M_PRIMARY = 1ull << 35, OGE_M_PAIRED = 1ull << 36;
+
+// 32-byte record summary (array-of-structs: one 32-byte access moves a record's metadata).
+struct alignas(16) RecMeta {
+    uint64_t m;
+    uint64_t src;    // byte offset of the record in the input arena
+    int32_t seq;     // read1Sequence (refID)
+    int32_t coord;   // unclipped 5' coordinate (0-based)
+    int32_t r2seq;   // mate refID if paired && mate mapped, else -1
+    uint32_t hash;   // FNV-1a of RG ":" name (pair key), candidates only
+};
+
+// Read-group table on the device: ids back to back, off[g]..off[g+1]-1 is "ID\0" of group g.
+struct OgeRgTable {
+    const uint8_t *ids;
+    const uint32_t *off;
+    const int16_t *lib;
+    int32_t n_rg;
+    int16_t unknown_lib;
+};
+
+// Sort-key packing of the KEYS output (see sort.hip for the layout).
+constexpr uint64_t OGE_SORT_KEY_MASK = (1ull << 50) - 1;
+
+struct OgePassArgs {
+    const uint8_t *recs;     // input arena
+    const uint64_t *off;     // n record offsets into recs
+    uint64_t n;
+    // input pass outputs (either may be NULL)
+    RecMeta *meta;           // summary of input record i
+    OgeRgTable rg;
+    uint64_t *keys;          // coordinate sort key of input record i (+ byte size payload)
+    uint32_t *vals;          // = i
+    int32_t n_ref;
+    unsigned int *bad;       // bit 0: refID/pos out of range, bit 1: block_size out of [32, 10000]
+    // gather pass: output record k = input record perm[k] (or meta[k].src when smeta is given)
+    const uint32_t *perm;
+    const RecMeta *smeta;    // summaries in OUTPUT order (bin, flags, src offset), optional
+    const uint8_t *dup;      // output order: 1 sets 0x400, 0 clears it (primary records only)
+    uint8_t *out;
+    const uint64_t *out_off; // n+1 output offsets
+};
+
+struct oge_ctx;
+int oge_input_pass(oge_ctx *ctx, const OgePassArgs &a);
+int oge_gather_pass(oge_ctx *ctx, const OgePassArgs &a);

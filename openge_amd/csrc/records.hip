@@ -1,0 +1,361 @@
+// records.hip -- the two streaming passes over BAM records of the sort+dedup pipeline.
+//
+// k_input_pass (input order, records read once): a 256-thread block stages a tile of 256
+//   consecutive records (~73 KB for 150 bp reads) into LDS with aligned 16-byte loads, then each
+//   thread parses one record from LDS and emits
+//     KEYS: the coordinate sort key (sort.hip) and its index
+//     META: a 32-byte summary -- the fragment ReadEnds fields of buildReadEnds
+//           (algorithms/mark_duplicates.cpp:147-164: getUnclippedStart/End :88-129, getScore :135-144,
+//           getLibraryId :282-318), the RG ":" name pair-key hash (:210-213), the bin the writer must
+//           store (util/bam_serializer.h:112-116), the flag byte and the record's source offset.
+//   Records outside the staged window (non-contiguous offsets, >76 KB tiles) are parsed straight
+//   from global memory by the same code.
+//
+// k_gather16 (output order, records read once and written once): a wave owns 64 consecutive
+//   output records, whose output bytes are one contiguous range.  Lanes write that range as
+//   aligned 16-byte chunks; a chunk is one unaligned 16-byte load of the source record (two, merged,
+//   where a record boundary falls inside the chunk -- gfx950 serves unaligned dwordx4 at stream
+//   rate, tools/probes/unaligned.hip), with bin and FLAG 0x400 patched in registers.  Only the two
+//   chunks at the ends of a batch, shared with neighbouring waves, fall back to byte stores.
+#include "oge_ctx.h"
+#include "bam_layout.h"
+#include "dev_util.h"
+#include "records.h"
+
+namespace {
+
+constexpr int kT = 256;
+constexpr uint32_t kTileRecs = 256;
+constexpr uint32_t kLdsCap = 76 * 1024;
+
+// --- byte readers over the LDS tile or global memory (x = absolute byte index) ---
+struct LdsRd {
+    const uint8_t *b;  // LDS tile base (16-byte aligned)
+    __device__ __forceinline__ uint32_t u8(uint64_t x) const { return b[x]; }
+    __device__ __forceinline__ uint32_t a32(uint64_t x) const { return *(const uint32_t *)(b + x); }
+    __device__ __forceinline__ uint32_t u32(uint64_t x) const {
+        const uint32_t sh = (uint32_t)(x & 3) * 8;
+        const uint32_t lo = a32(x & ~3ull);
+        return sh ? (lo >> sh) | (a32((x & ~3ull) + 4) << (32 - sh)) : lo;
+    }
+};
+struct GlbRd {
+    const uint8_t *b;  // arena base
+    __device__ __forceinline__ uint32_t u8(uint64_t x) const { return b[x]; }
+    __device__ __forceinline__ uint32_t a32(uint64_t x) const { return *(const uint32_t *)(b + x); }
+    __device__ __forceinline__ uint32_t u32(uint64_t x) const { return oge_ldu32(b + x); }
+};
+
+__device__ __forceinline__ uint32_t h_step(uint32_t h, uint32_t c) { return (h ^ c) * 16777619u; }
+
+// Record at absolute index r of reader `rd`; i = record index, src = its offset in the arena.
+template <bool META, bool KEYS, class Rd>
+__device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i, uint64_t src, const OgePassArgs &a) {
+    const uint32_t bs = rd.u32(r);
+    const int32_t ref = (int32_t)rd.u32(r + OGE_OFF_REFID);
+    const int32_t pos = (int32_t)rd.u32(r + OGE_OFF_POS);
+    const uint32_t w12 = rd.u32(r + OGE_OFF_LNAME);
+    const uint32_t w16 = rd.u32(r + OGE_OFF_NCIGAR);
+    const uint32_t lname = w12 & 0xFF, nc = w16 & 0xFFFF, flag = w16 >> 16;
+    const uint32_t lseq = rd.u32(r + OGE_OFF_LSEQ);
+    if (KEYS) {
+        uint64_t k;
+        if (ref == -1) {
+            k = (uint64_t)(uint32_t)a.n_ref << 33;
+        } else {
+            if (ref < -1 || ref >= a.n_ref || pos < -1) atomicOr(a.bad, 1u);
+            k = ((uint64_t)(uint32_t)ref << 33) | ((uint64_t)(uint32_t)(pos + 1) << 1) | ((flag >> 4) & 1u);
+        }
+        if (bs < 32 || bs > 10000) atomicOr(a.bad, 2u);
+        a.keys[i] = k | ((uint64_t)(bs + 4) << 50);
+        a.vals[i] = (uint32_t)i;
+    }
+    if (!META) return;
+    const uint64_t c = r + OGE_OFF_NAME + lname;
+    int32_t rl = 0, lead = 0, trail = 0;
+    bool in_lead = true;
+    for (uint32_t k = 0; k < nc; ++k) {
+        const uint32_t op = rd.u32(c + 4 * k), t = op & 0xF, len = op >> 4;
+        if (t == OGE_CIG_M || t == OGE_CIG_D || t == OGE_CIG_N || t == OGE_CIG_EQ || t == OGE_CIG_X) rl += (int32_t)len;
+        const bool clip = (t == OGE_CIG_S || t == OGE_CIG_H);
+        if (in_lead && clip) lead += (int32_t)len; else in_lead = false;
+        trail = clip ? trail + (int32_t)len : 0;
+    }
+    RecMeta M;
+    M.src = src;
+    M.seq = -1;
+    M.coord = 0;
+    M.r2seq = -1;
+    M.hash = 0;
+    uint64_t m = ((uint64_t)oge_reg2bin(pos, pos + rl) << 48) | ((uint64_t)(flag >> 8) << 40);
+    if (!(flag & OGE_F_SECONDARY)) m |= OGE_M_PRIMARY;
+    if (!((flag & OGE_F_UNMAP) || ref == -1 || (flag & OGE_F_SECONDARY))) {
+        m |= OGE_M_FRAG;
+        const bool rev = (flag & OGE_F_REVERSE) != 0;
+        if (rev) m |= OGE_M_REV;
+        M.coord = rev ? pos + rl - 1 + trail : pos - lead;  // getUnclippedEnd / getUnclippedStart
+        M.seq = ref;
+        // getScore: int16 accumulator over raw quality bytes >= 15
+        const uint64_t q0 = c + 4 * nc + (lseq + 1) / 2, q1 = q0 + lseq;
+        uint32_t sc = 0;
+        uint64_t x = q0;
+        for (; x < q1 && (x & 3); ++x) { const uint32_t b = rd.u8(x); sc += b >= 15 ? b : 0; }
+        for (; x + 4 <= q1; x += 4) {
+            const uint32_t w = rd.a32(x);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) { const uint32_t b = (w >> (8 * s)) & 0xff; sc += b >= 15 ? b : 0; }
+        }
+        for (; x < q1; ++x) { const uint32_t b = rd.u8(x); sc += b >= 15 ? b : 0; }
+        m |= (uint64_t)(uint16_t)sc;
+        // RG tag (GetTag<string> / FindTag semantics, util/bamtools/BamAlignment.cpp:270-294,699-780)
+        const uint64_t tend = r + 4 + bs;
+        uint64_t p = q1, rgv = 0;
+        uint32_t rgl = 0;
+        bool has = false;
+        while (p + 3 <= tend) {
+            const uint32_t w = rd.u32(p);
+            const uint32_t t0 = w & 0xff, t1 = (w >> 8) & 0xff, type = (w >> 16) & 0xff;
+            p += 3;
+            if (t0 == 'R' && t1 == 'G') {
+                uint64_t s = p;
+                while (s < tend && rd.u8(s)) ++s;
+                rgv = p;
+                rgl = (uint32_t)(s - p);
+                has = true;
+                break;
+            }
+            if (type == 0) break;
+            bool ok = true;
+            switch (type) {
+            case 'A': case 'c': case 'C': p += 1; break;
+            case 's': case 'S': p += 2; break;
+            case 'f': case 'i': case 'I': p += 4; break;
+            case 'Z': case 'H':
+                while (p < tend && rd.u8(p)) ++p;
+                ++p;
+                break;
+            case 'B': {
+                if (p + 5 > tend) { ok = false; break; }
+                const uint32_t at = rd.u8(p);
+                const int32_t cnt = (int32_t)rd.u32(p + 1);
+                p += 5;
+                const int sz = (at == 'c' || at == 'C') ? 1 : (at == 's' || at == 'S') ? 2 : (at == 'f' || at == 'i' || at == 'I') ? 4 : 0;
+                if (!sz) { ok = false; break; }
+                p += (int64_t)cnt * sz;
+                break;
+            }
+            default: ok = false;
+            }
+            if (!ok || p >= tend || rd.u8(p) == 0) break;
+        }
+        int16_t lib = a.rg.unknown_lib;
+        if (has && rgl) {
+            for (int32_t g = 0; g < a.rg.n_rg; ++g) {
+                const uint32_t o = a.rg.off[g], Lg = a.rg.off[g + 1] - o - 1;
+                if (Lg != rgl) continue;
+                bool eq = true;
+                for (uint32_t y = 0; y < Lg && eq; ++y) eq = a.rg.ids[o + y] == rd.u8(rgv + y);
+                if (eq) { lib = a.rg.lib[g]; break; }
+            }
+        }
+        m |= (uint64_t)(uint16_t)lib << 16;
+        const bool paired_mm = (flag & OGE_F_PAIRED) && !(flag & OGE_F_MUNMAP);
+        M.r2seq = paired_mm ? (int32_t)rd.u32(r + OGE_OFF_MREFID) : -1;
+        if (M.r2seq != -1) m |= OGE_M_PAIRED;
+        if (paired_mm) {
+            m |= OGE_M_CAND;
+            uint32_t h = 2166136261u;
+            for (uint32_t y = 0; y < rgl; ++y) h = h_step(h, rd.u8(rgv + y));
+            h = h_step(h, ':');
+            const uint32_t nl = lname ? lname - 1u : 0u;
+            for (uint32_t y = 0; y < nl; ++y) h = h_step(h, rd.u8(r + OGE_OFF_NAME + y));
+            M.hash = h;
+        }
+    }
+    M.m = m;
+    a.meta[i] = M;
+}
+
+template <bool META, bool KEYS>
+__global__ __launch_bounds__(kT) void k_input_pass(OgePassArgs a) {
+    __shared__ uint4 tile[kLdsCap / 16];
+    __shared__ uint64_t tb[2];
+    const uint8_t *lds = (const uint8_t *)tile;
+    for (uint64_t r0 = (uint64_t)blockIdx.x * kTileRecs; r0 < a.n; r0 += (uint64_t)gridDim.x * kTileRecs) {
+        const uint64_t r1 = (a.n - r0) < kTileRecs ? a.n : r0 + kTileRecs;
+        if (threadIdx.x == 0) {
+            const uint64_t b0 = a.off[r0] & ~15ull;
+            const uint64_t last = a.off[r1 - 1];
+            const uint64_t e = last + 4 + oge_ldu32(a.recs + last);
+            tb[0] = b0;
+            tb[1] = (e > b0 && e - b0 <= kLdsCap) ? e : b0;  // empty window: parse from global
+        }
+        __syncthreads();
+        const uint64_t b0 = tb[0], b1 = tb[1];
+        const uint64_t nch = (b1 - b0 + 15) >> 4;
+        const uint4 *g = (const uint4 *)(a.recs + b0);
+        for (uint64_t ch = threadIdx.x; ch < nch; ch += kT) tile[ch] = g[ch];
+        __syncthreads();
+        const uint64_t i = r0 + threadIdx.x;
+        if (i < r1) {
+            const uint64_t o = a.off[i];
+            const uint32_t bs = (o >= b0 && o + 4 <= b1) ? LdsRd{lds}.u32(o - b0) : 0u;
+            if (bs && o + 4 + bs <= b1) parse_input<META, KEYS>(LdsRd{lds}, o - b0, i, o, a);
+            else parse_input<META, KEYS>(GlbRd{a.recs}, o, i, o, a);
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- gather
+__device__ __forceinline__ uint4 ldu128(const uint8_t *p) { return *(const uint4 *)p; }
+
+__device__ __forceinline__ uint32_t merge32(uint32_t a, uint32_t b, int keep) {  // keep = low bytes taken from a
+    if (keep <= 0) return b;
+    if (keep >= 4) return a;
+    const uint32_t m = (1u << (8 * keep)) - 1u;
+    return (a & m) | (b & ~m);
+}
+
+__device__ __forceinline__ void set_byte(uint4 &v, int pos, uint32_t byte) {
+    const uint32_t sh = 8 * (pos & 3), mk = ~(0xffu << sh), bv = byte << sh;
+    switch (pos >> 2) {
+    case 0: v.x = (v.x & mk) | bv; break;
+    case 1: v.y = (v.y & mk) | bv; break;
+    case 2: v.z = (v.z & mk) | bv; break;
+    default: v.w = (v.w & mk) | bv; break;
+    }
+}
+
+// bytes 14,15 (bin) and 19 (FLAG high byte) of a record starting at `rs` (relative), chunk at `rel`
+__device__ __forceinline__ void patch_chunk(uint4 &v, int64_t rel, int64_t rs, uint32_t bf) {
+    const int64_t p14 = rs + 14 - rel, p19 = rs + 19 - rel;
+    if (p14 >= 0 && p14 < 16) set_byte(v, (int)p14, bf & 0xff);
+    if (p14 + 1 >= 0 && p14 + 1 < 16) set_byte(v, (int)(p14 + 1), (bf >> 8) & 0xff);
+    if (p19 >= 0 && p19 < 16) set_byte(v, (int)p19, (bf >> 16) & 0xff);
+}
+
+__device__ __forceinline__ uint32_t patch_byte(uint64_t ro, uint32_t byte, uint32_t bf) {
+    if (ro == 14) return bf & 0xff;
+    if (ro == 15) return (bf >> 8) & 0xff;
+    if (ro == 19) return (bf >> 16) & 0xff;
+    return byte;
+}
+
+template <bool SMETA>
+__global__ __launch_bounds__(kT) void k_gather16(OgePassArgs a) {
+    __shared__ uint32_t sd[kT / 64][65];   // per wave: output start of record j relative to the batch
+    __shared__ uint64_t ss[kT / 64][64];   // source offset of record j
+    __shared__ uint32_t sbf[kT / 64][64];  // bin | FLAG-high-byte << 16 to write
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t wave = ((uint64_t)blockIdx.x * kT + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * kT) >> 6;
+    for (uint64_t R = wave * 64; R < a.n; R += nwaves * 64) {
+        const uint32_t cnt = (uint32_t)((a.n - R) < 64 ? (a.n - R) : 64);
+        const uint64_t D0 = a.out_off[R];
+        if (lane < cnt) {
+            const uint64_t rec = R + lane;
+            const uint64_t d = a.out_off[rec];
+            if (lane == cnt - 1) sd[w][cnt] = (uint32_t)(a.out_off[rec + 1] - D0);
+            uint64_t s;
+            uint32_t bin, fhi;
+            bool primary;
+            if (SMETA) {
+                const RecMeta M = a.smeta[rec];
+                s = M.src;
+                bin = (uint32_t)(M.m >> 48);
+                fhi = (uint32_t)(M.m >> 40) & 0xff;
+                primary = (M.m & OGE_M_PRIMARY) != 0;
+            } else {
+                s = a.off[a.perm ? a.perm[rec] : rec];
+                const uint8_t *r = a.recs + s;
+                const int32_t pos = (int32_t)oge_ldu32(r + OGE_OFF_POS);
+                const uint32_t w16 = oge_ldu32(r + OGE_OFF_NCIGAR);
+                const uint32_t nc = w16 & 0xFFFF, flag = w16 >> 16;
+                const uint8_t *cg = r + OGE_OFF_NAME + r[OGE_OFF_LNAME];
+                int32_t rl = 0;
+                for (uint32_t k = 0; k < nc; ++k) {
+                    const uint32_t op = oge_ldu32(cg + 4 * k), t = op & 0xF;
+                    if (t == OGE_CIG_M || t == OGE_CIG_D || t == OGE_CIG_N || t == OGE_CIG_EQ || t == OGE_CIG_X) rl += (int32_t)(op >> 4);
+                }
+                bin = oge_reg2bin(pos, pos + rl);
+                fhi = flag >> 8;
+                primary = !(flag & OGE_F_SECONDARY);
+            }
+            if (a.dup && primary) fhi = a.dup[rec] == 1 ? (fhi | 0x04u) : (fhi & ~0x04u);
+            sd[w][lane] = (uint32_t)(d - D0);
+            ss[w][lane] = s;
+            sbf[w][lane] = (bin & 0xffff) | (fhi << 16);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint64_t Dend = D0 + sd[w][cnt];
+        for (uint64_t A = (D0 & ~15ull) + 16ull * lane; A < Dend; A += 1024) {
+            const int64_t rel = (int64_t)A - (int64_t)D0;  // chunk start relative to the batch
+            const int64_t x0 = rel < 0 ? 0 : rel;
+            int lo = 0, hi = (int)cnt - 1;                 // record holding byte x0
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if ((int64_t)sd[w][mid] <= x0) lo = mid; else hi = mid - 1;
+            }
+            const int k = lo;
+            const int64_t rs = sd[w][k];
+            const bool full = rel >= 0 && A + 16 <= Dend;
+            const bool two = (k + 1 < (int)cnt) && (int64_t)sd[w][k + 1] < rel + 16;
+            if (full && !(two && ss[w][k + 1] < 16)) {
+                uint4 v = ldu128(a.recs + ss[w][k] + (rel - rs));
+                patch_chunk(v, rel, rs, sbf[w][k]);
+                if (two) {
+                    const int64_t rs2 = sd[w][k + 1];
+                    const int keep = (int)(rs2 - rel);
+                    uint4 v2 = ldu128(a.recs + ss[w][k + 1] - keep);
+                    patch_chunk(v2, rel, rs2, sbf[w][k + 1]);
+                    v.x = merge32(v.x, v2.x, keep);
+                    v.y = merge32(v.y, v2.y, keep - 4);
+                    v.z = merge32(v.z, v2.z, keep - 8);
+                    v.w = merge32(v.w, v2.w, keep - 12);
+                }
+                *(uint4 *)(a.out + A) = v;
+            } else {
+                // batch edge (bytes shared with neighbouring waves) or a record at the arena start
+                const uint64_t xe = (A + 16 < Dend ? A + 16 : Dend) - D0;
+                int kk = k;
+                for (uint64_t x = (uint64_t)x0; x < xe; ++x) {
+                    while (kk + 1 < (int)cnt && sd[w][kk + 1] <= x) ++kk;
+                    const uint64_t ro = x - sd[w][kk];
+                    a.out[D0 + x] = (uint8_t)patch_byte(ro, a.recs[ss[w][kk] + ro], sbf[w][kk]);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+}  // namespace
+
+int oge_input_pass(oge_ctx *ctx, const OgePassArgs &a) {
+    if (!a.n) return OGE_OK;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, kTileRecs), 256u * 8u);
+    if (a.meta && a.keys)
+        hipLaunchKernelGGL((k_input_pass<true, true>), dim3(blocks), dim3(kT), 0, ctx->stream, a);
+    else if (a.meta)
+        hipLaunchKernelGGL((k_input_pass<true, false>), dim3(blocks), dim3(kT), 0, ctx->stream, a);
+    else if (a.keys)
+        hipLaunchKernelGGL((k_input_pass<false, true>), dim3(blocks), dim3(kT), 0, ctx->stream, a);
+    else
+        return OGE_OK;
+    OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}
+
+int oge_gather_pass(oge_ctx *ctx, const OgePassArgs &a) {
+    if (!a.n) return OGE_OK;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, 64 * (kT / 64)), 256u * 16u);
+    if (a.smeta)
+        hipLaunchKernelGGL(k_gather16<true>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
+    else
+        hipLaunchKernelGGL(k_gather16<false>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
+    OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}

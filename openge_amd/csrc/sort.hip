@@ -13,13 +13,17 @@
 // run keeps input order.
 #include "oge_ctx.h"
 #include "bam_layout.h"
+#include "dev_util.h"
+#include "records.h"
 
 #include <algorithm>
 #include <vector>
 
+unsigned int *oge_sort_counts(oge_ctx *ctx);
+
 namespace {
 
-constexpr uint64_t kSortKeyMask = (1ull << 50) - 1;
+constexpr uint64_t kSortKeyMask = OGE_SORT_KEY_MASK;
 constexpr int kT = 256;
 
 __global__ __launch_bounds__(kT) void k_keypack(const uint8_t *__restrict__ recs, const uint64_t *__restrict__ off,
@@ -63,38 +67,34 @@ __device__ __forceinline__ bool tie_less(const uint8_t *__restrict__ recs, const
     return a < b;
 }
 
-__global__ __launch_bounds__(kT) void k_find_ties(const uint64_t *__restrict__ keys, uint64_t n, int32_t n_ref,
-                                                   uint2 *__restrict__ small, uint2 *__restrict__ large,
-                                                   unsigned int *__restrict__ counts) {
-    uint64_t p = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (p + 1 >= n) return;
-    uint64_t k = keys[p] & kSortKeyMask;
-    if (p > 0 && (keys[p - 1] & kSortKeyMask) == k) return;
-    if ((keys[p + 1] & kSortKeyMask) != k) return;
-    if ((k >> 33) == (uint64_t)(uint32_t)n_ref) return;  // refID == -1 tail keeps input order
-    uint64_t e = p + 2;
-    while (e < n && (keys[e] & kSortKeyMask) == k) ++e;
-    uint32_t len = (uint32_t)(e - p);
-    if (len <= 32) {
-        unsigned int s = atomicAdd(&counts[0], 1u);
-        small[s] = make_uint2((uint32_t)p, len);
-    } else {
-        unsigned int s = atomicAdd(&counts[1], 1u);
-        large[s] = make_uint2((uint32_t)p, len);
+// One thread per sorted position: a run head with 2..32 equal keys insertion-sorts its run in place
+// by (name, flag, index); longer runs go to `large` (rare; one wave-aggregated append).  No
+// counter is touched for the common case, so nothing serialises on an atomic.
+__global__ __launch_bounds__(kT) void k_ties(const uint8_t *__restrict__ recs, const uint64_t *__restrict__ off,
+                                              uint64_t *__restrict__ keys, uint32_t *__restrict__ vals, uint64_t n,
+                                              int32_t n_ref, uint2 *__restrict__ large, unsigned int *__restrict__ nlarge) {
+    const uint64_t p = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    uint32_t len = 0;
+    if (p + 1 < n) {
+        const uint64_t k = keys[p] & kSortKeyMask;
+        const bool head = (p == 0 || (keys[p - 1] & kSortKeyMask) != k) && (keys[p + 1] & kSortKeyMask) == k &&
+                          (k >> 33) != (uint64_t)(uint32_t)n_ref;  // refID == -1 tail keeps input order
+        if (head) {
+            uint64_t e = p + 2;
+            while (e < n && e - p <= 32 && (keys[e] & kSortKeyMask) == k) ++e;
+            if (e - p > 32) { while (e < n && (keys[e] & kSortKeyMask) == k) ++e; }
+            len = (uint32_t)(e - p);
+        }
     }
-}
-
-__global__ __launch_bounds__(kT) void k_tie_small(const uint8_t *__restrict__ recs, const uint64_t *__restrict__ off,
-                                                   uint64_t *__restrict__ keys, uint32_t *__restrict__ vals,
-                                                   const uint2 *__restrict__ segs, uint32_t nseg) {
-    uint32_t s = blockIdx.x * kT + threadIdx.x;
-    if (s >= nseg) return;
-    uint2 sg = segs[s];
-    uint64_t *k = keys + sg.x;
-    uint32_t *v = vals + sg.x;
-    for (uint32_t i = 1; i < sg.y; ++i) {
-        uint32_t vi = v[i];
-        uint64_t ki = k[i];
+    const bool is_large = len > 32;
+    const uint32_t l = oge_wave_append(is_large, nlarge);
+    if (is_large) large[l] = make_uint2((uint32_t)p, len);
+    if (len < 2 || len > 32) return;
+    uint64_t *k = keys + p;
+    uint32_t *v = vals + p;
+    for (uint32_t i = 1; i < len; ++i) {
+        const uint32_t vi = v[i];
+        const uint64_t ki = k[i];
         int j = (int)i - 1;
         while (j >= 0 && tie_less(recs, off, vi, v[j])) {
             v[j + 1] = v[j];
@@ -160,84 +160,38 @@ __global__ __launch_bounds__(kT) void k_sizes_from_perm(const uint8_t *__restric
     else if (p == n) sizes[p] = 0;
 }
 
-// One wave per record: dword-granular copy with funnel shifts for any src/dst alignment, byte
-// stores only on the two edge dwords shared with neighbouring records.  The bin field (record
-// bytes 14-15) is replaced by the recomputed bin as BamSerializer::write does.
-__global__ __launch_bounds__(kT) void k_gather_records(const uint8_t *__restrict__ recs, const uint64_t *__restrict__ off,
-                                                        const uint32_t *__restrict__ perm, uint64_t n,
-                                                        uint8_t *__restrict__ out, const uint64_t *__restrict__ out_off) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t wave = ((uint64_t)blockIdx.x * kT + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * kT) >> 6;
-    for (uint64_t rec = wave; rec < n; rec += nwaves) {
-        const uint8_t *src = recs + off[perm[rec]];
-        const uint64_t d0 = out_off[rec];
-        const uint64_t len = out_off[rec + 1] - d0;
-        uint32_t bin = 0;
-        if (lane == 0) bin = oge_rec_bin(src);
-        bin = __shfl(bin, 0, 64);
-        const uint64_t a0 = d0 & ~3ull;
-        const uint64_t dend = d0 + len;
-        const uint64_t nwords = (((dend + 3) & ~3ull) - a0) >> 2;
-        const uintptr_t sbase = (uintptr_t)src;
-        for (uint64_t w = lane; w < nwords; w += 64) {
-            const uint64_t A = a0 + 4 * w;
-            if (A >= d0 && A + 4 <= dend) {
-                const uint64_t ro = A - d0;  // record byte offset of this dword
-                const uintptr_t s = sbase + ro;
-                const uint32_t sh = (uint32_t)(s & 3);
-                const uint32_t *sp = (const uint32_t *)(s & ~(uintptr_t)3);
-                uint32_t lo = sp[0];
-                uint32_t v = lo;
-                if (sh) {
-                    uint32_t hi = sp[1];
-                    v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));
-                }
-                if (ro <= 15 && ro + 4 > 14) {
-#pragma unroll
-                    for (uint32_t b = 0; b < 4; ++b) {
-                        uint64_t x = ro + b;
-                        if (x == 14 || x == 15) {
-                            uint32_t byte = (x == 14) ? (bin & 0xff) : ((bin >> 8) & 0xff);
-                            v = (v & ~(0xffu << (8 * b))) | (byte << (8 * b));
-                        }
-                    }
-                }
-                *(uint32_t *)(out + A) = v;
-            } else {
-                for (uint64_t x = (A > d0 ? A : d0); x < A + 4 && x < dend; ++x) {
-                    uint64_t ro = x - d0;
-                    uint8_t byte = src[ro];
-                    if (ro == 14) byte = (uint8_t)(bin & 0xff);
-                    if (ro == 15) byte = (uint8_t)(bin >> 8);
-                    out[x] = byte;
-                }
-            }
-        }
-    }
-}
-
 }  // namespace
 
+// Buffers the coordinate sort reads its (key, value) input from.
+int oge_sort_buffers(oge_ctx *ctx, uint64_t n, uint64_t **keys, uint32_t **vals) {
+    *keys = (uint64_t *)ctx->ws("sort_keys", (n + 1) * 8);
+    *vals = (uint32_t *)ctx->ws("sort_vals", (n + 1) * 4);
+    return (*keys && *vals) ? OGE_OK : OGE_ERR_HIP;
+}
+
 // Sort keys/vals for records; on return *kout/*vout hold the sorted (key, input index) pairs.
+// keys_ready: the KEYS pass (records.hip) already filled oge_sort_buffers and the `bad` word.
 int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
-                      uint64_t **kout, uint32_t **vout) {
+                      bool keys_ready, uint64_t **kout, uint32_t **vout) {
     if (n_ref < 0 || n_ref >= (1 << 17)) return oge_fail(ctx, OGE_ERR_LIMIT, "sort: n_ref outside [0, 131072)");
     if (n > 0xFFFFFFFEull) return oge_fail(ctx, OGE_ERR_LIMIT, "sort: more than 2^32-2 records");
-    uint64_t *keys = (uint64_t *)ctx->ws("sort_keys", (n + 1) * 8);
-    uint32_t *vals = (uint32_t *)ctx->ws("sort_vals", (n + 1) * 4);
+    uint64_t *keys;
+    uint32_t *vals;
+    if (oge_sort_buffers(ctx, n, &keys, &vals)) return OGE_ERR_HIP;
     uint64_t *ktmp = (uint64_t *)ctx->ws("sort_ktmp", (n + 1) * 8);
     uint32_t *vtmp = (uint32_t *)ctx->ws("sort_vtmp", (n + 1) * 4);
-    unsigned int *counts = (unsigned int *)ctx->ws("sort_counts", 16);
-    if (!keys || !vals || !ktmp || !vtmp || !counts) return OGE_ERR_HIP;
-    OgeStageTimer *t = ctx->begin_stage("sort_keypack");
-    OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 16, ctx->stream));
-    if (n) {
-        hipLaunchKernelGGL(k_keypack, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off, n, n_ref, keys,
-                           vals, counts + 2);
-        OGE_LAUNCH_CHECK(ctx);
+    unsigned int *counts = oge_sort_counts(ctx);
+    if (!ktmp || !vtmp || !counts) return OGE_ERR_HIP;
+    if (!keys_ready) {
+        OgeStageTimer *t = ctx->begin_stage("sort_keypack");
+        OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 16, ctx->stream));
+        if (n) {
+            hipLaunchKernelGGL(k_keypack, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off, n, n_ref, keys,
+                               vals, counts + 2);
+            OGE_LAUNCH_CHECK(ctx);
+        }
+        ctx->end_stage(t);
     }
-    ctx->end_stage(t);
     uint64_t o = 0, a = 0;
     int rc = oge_reduce_or_and_u64(ctx, keys, n, kSortKeyMask, &o, &a);
     if (rc) return rc;
@@ -245,46 +199,41 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     OGE_HIP_TRY(ctx, hipMemcpy(&bad, counts + 2, 4, hipMemcpyDeviceToHost));
     if (bad & 1) return oge_fail(ctx, OGE_ERR_ARG, "sort: record with refID outside [-1, n_ref) or pos < -1");
     if (bad & 2) return oge_fail(ctx, OGE_ERR_ARG, "sort: record block_size outside [32, 10000] (util/bam_deserializer.h:160)");
-    t = ctx->begin_stage("sort_radix");
+    OgeStageTimer *t = ctx->begin_stage("sort_radix");
     rc = oge_radix_sort_pairs(ctx, keys, vals, ktmp, vtmp, n, (o ^ a) & kSortKeyMask, kout, vout);
     if (rc) return rc;
     ctx->end_stage(t);
 
     // equal-coordinate runs -> (name, flag, index) order
     t = ctx->begin_stage("sort_ties");
-    uint2 *small = (uint2 *)ctx->ws("sort_small", (n / 2 + 1) * sizeof(uint2));
     uint2 *large = (uint2 *)ctx->ws("sort_large", (n / 33 + 1) * sizeof(uint2));
-    if (!small || !large) return OGE_ERR_HIP;
+    if (!large) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 8, ctx->stream));
     if (n > 1) {
-        hipLaunchKernelGGL(k_find_ties, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)*kout, n,
-                           n_ref, small, large, counts);
+        hipLaunchKernelGGL(k_ties, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout, n, n_ref,
+                           large, counts + 1);
         OGE_LAUNCH_CHECK(ctx);
     }
-    unsigned int cnt[2];
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(cnt, counts, 8, hipMemcpyDeviceToHost, ctx->stream));
+    unsigned int nlarge = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&nlarge, counts + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (cnt[0]) {
-        hipLaunchKernelGGL(k_tie_small, dim3(oge_ceil_div(cnt[0], kT)), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout,
-                           *vout, (const uint2 *)small, cnt[0]);
-        OGE_LAUNCH_CHECK(ctx);
-    }
-    if (cnt[1]) {
-        std::vector<uint2> h(cnt[1]);
-        OGE_HIP_TRY(ctx, hipMemcpy(h.data(), large, cnt[1] * sizeof(uint2), hipMemcpyDeviceToHost));
-        std::vector<uint64_t> so(cnt[1]);
+    if (nlarge) {
+        std::vector<uint2> h(nlarge);
+        OGE_HIP_TRY(ctx, hipMemcpy(h.data(), large, nlarge * sizeof(uint2), hipMemcpyDeviceToHost));
+        std::vector<uint64_t> so(nlarge);
         uint64_t tot = 0;
-        for (unsigned i = 0; i < cnt[1]; ++i) {
+        for (unsigned i = 0; i < nlarge; ++i) {
             uint64_t P = 1;
             while (P < h[i].y) P <<= 1;
             so[i] = tot;
             tot += P;
         }
-        uint64_t *dso = (uint64_t *)ctx->ws("sort_large_off", cnt[1] * 8);
+        uint64_t *dso = (uint64_t *)ctx->ws("sort_large_off", nlarge * 8);
         uint64_t *sk = (uint64_t *)ctx->ws("sort_large_k", tot * 8);
         uint32_t *sv = (uint32_t *)ctx->ws("sort_large_v", tot * 4);
         if (!dso || !sk || !sv) return OGE_ERR_HIP;
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(dso, so.data(), cnt[1] * 8, hipMemcpyHostToDevice, ctx->stream));
-        hipLaunchKernelGGL(k_tie_large, dim3(cnt[1]), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout,
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(dso, so.data(), nlarge * 8, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_tie_large, dim3(nlarge), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout,
                            (const uint2 *)large, (const uint64_t *)dso, sk, sv);
         OGE_LAUNCH_CHECK(ctx);
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -293,8 +242,13 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     return OGE_OK;
 }
 
+unsigned int *oge_sort_counts(oge_ctx *ctx) { return (unsigned int *)ctx->ws("sort_counts", 16); }
+
+// Output offsets (from the size payload of the sorted keys, or from the records) and the gather.
+// smeta (output-order summaries) and dup are optional (see OgePassArgs).
 int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
-                          const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off) {
+                          const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
+                          const RecMeta *smeta, const uint8_t *d_dup) {
     OgeStageTimer *t = ctx->begin_stage("gather_offsets");
     if (sorted_keys)
         hipLaunchKernelGGL(k_sizes_from_keys, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, sorted_keys, n,
@@ -308,10 +262,17 @@ int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d
     ctx->end_stage(t);
     if (!n) return OGE_OK;
     t = ctx->begin_stage("gather_records");
-    uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(n, kT / 64), 256u * 32u);
-    hipLaunchKernelGGL(k_gather_records, dim3(blocks), dim3(kT), 0, ctx->stream, d_recs, d_off, d_perm, n, d_out,
-                       (const uint64_t *)d_out_off);
-    OGE_LAUNCH_CHECK(ctx);
+    OgePassArgs a = {};
+    a.recs = d_recs;
+    a.off = d_off;
+    a.perm = d_perm;
+    a.n = n;
+    a.out = d_out;
+    a.out_off = d_out_off;
+    a.smeta = smeta;
+    a.dup = d_dup;
+    rc = oge_gather_pass(ctx, a);
+    if (rc) return rc;
     ctx->end_stage(t);
     return OGE_OK;
 }
