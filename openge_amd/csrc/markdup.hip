@@ -35,15 +35,12 @@ __global__ __launch_bounds__(kT) void k_cand_flags(const RecMeta *__restrict__ m
     if (i < n) f[i] = (meta[i].m & OGE_M_CAND) ? 1u : 0u;
     else if (i == n) f[i] = 0;
 }
+// candidate key = pair-key hash << 32 | record index; only the hash half is radix-sorted, and
+// the stable LSD sort keeps record order inside a hash run (the ReadEndsMap's first/second-seen)
 __global__ __launch_bounds__(kT) void k_cand_scatter(const RecMeta *__restrict__ meta, uint64_t n,
-                                                      const uint32_t *__restrict__ pos, uint64_t *__restrict__ ckey,
-                                                      uint32_t *__restrict__ cval) {
+                                                      const uint32_t *__restrict__ pos, uint64_t *__restrict__ ckey) {
     uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i < n && (meta[i].m & OGE_M_CAND)) {
-        const uint32_t p = pos[i];
-        ckey[p] = meta[i].hash;
-        cval[p] = (uint32_t)i;
-    }
+    if (i < n && (meta[i].m & OGE_M_CAND)) ckey[pos[i]] = ((uint64_t)meta[i].hash << 32) | (uint32_t)i;
 }
 
 __device__ bool pair_key_of(const uint8_t *r, const uint8_t **rg, uint32_t *rgl, uint32_t *nl) {
@@ -59,9 +56,29 @@ __device__ bool pair_key_of(const uint8_t *r, const uint8_t **rg, uint32_t *rgl,
 __device__ __forceinline__ uint8_t key_byte(const uint8_t *rgv, uint32_t rgl, const uint8_t *name, uint32_t k) {
     return k < rgl ? rgv[k] : (k == rgl ? (uint8_t)':' : name[k - rgl - 1]);
 }
-// exact RG ":" name comparison of the records summarised by meta[a] and meta[b]
-__device__ bool same_pair_key(const uint8_t *recs, const RecMeta *meta, uint32_t a, uint32_t b) {
-    const uint8_t *ra = recs + meta[a].src, *rb = recs + meta[b].src;
+// Exact RG ":" name comparison (the ReadEndsMap key, mark_duplicates.cpp:210-213) of the records
+// summarised by A and B.  Same listed read group -> the keys are equal iff the names are, which is
+// one 16-byte-chunked compare at record byte 36; anything else compares the whole key strings.
+__device__ bool same_pair_key(const uint8_t *recs, const RecMeta &A, const RecMeta &B) {
+    const uint8_t *ra = recs + A.src, *rb = recs + B.src;
+    if (A.rgi == B.rgi && A.rgi != OGE_RGI_UNLISTED) {
+        const uint32_t la = ra[OGE_OFF_LNAME];
+        if (la != rb[OGE_OFF_LNAME]) return false;
+        for (uint32_t k = 0; k < la; k += 16) {  // compares the NUL too: equal lengths
+            const uint4 x = *(const uint4 *)(ra + OGE_OFF_NAME + k), y = *(const uint4 *)(rb + OGE_OFF_NAME + k);
+            const uint32_t rem = la - k;
+            uint32_t d0 = x.x ^ y.x, d1 = x.y ^ y.y, d2 = x.z ^ y.z, d3 = x.w ^ y.w;
+            if (rem < 16) {  // ignore bytes past the name
+                const uint32_t keep[4] = {rem >= 4 ? 0xffffffffu : (rem ? (1u << (8 * rem)) - 1u : 0u),
+                                          rem >= 8 ? 0xffffffffu : (rem > 4 ? (1u << (8 * (rem - 4))) - 1u : 0u),
+                                          rem >= 12 ? 0xffffffffu : (rem > 8 ? (1u << (8 * (rem - 8))) - 1u : 0u),
+                                          rem > 12 ? (1u << (8 * (rem - 12))) - 1u : 0u};
+                d0 &= keep[0]; d1 &= keep[1]; d2 &= keep[2]; d3 &= keep[3];
+            }
+            if (d0 | d1 | d2 | d3) return false;
+        }
+        return true;
+    }
     const uint8_t *ga = nullptr, *gb = nullptr;
     uint32_t la = 0, lb = 0, na = 0, nb = 0;
     pair_key_of(ra, &ga, &la, &na);
@@ -77,32 +94,36 @@ __device__ bool same_pair_key(const uint8_t *recs, const RecMeta *meta, uint32_t
 // Common case (a run of exactly two): flag[p] = 1 and the pair is stored at p (compacted later by a
 // scan, no atomics).  Longer runs (hash collisions, supplementary records) append to `extra`.
 __global__ __launch_bounds__(kT) void k_pair_runs(const uint8_t *__restrict__ recs, const RecMeta *__restrict__ meta,
-                                                   const uint64_t *__restrict__ ckey,
-                                                   const uint32_t *__restrict__ cval, uint64_t nc, uint8_t *__restrict__ used,
+                                                   const uint64_t *__restrict__ ckey, uint64_t nc, uint8_t *__restrict__ used,
                                                    uint32_t *__restrict__ flag, uint2 *__restrict__ sparse,
                                                    uint2 *__restrict__ extra, unsigned int *__restrict__ nextra) {
     const uint64_t p = (uint64_t)blockIdx.x * kT + threadIdx.x;
     if (p > nc) return;
     if (p == nc) { flag[p] = 0; return; }
     uint32_t f = 0;
-    const uint32_t h = (uint32_t)ckey[p];
-    if (p == 0 || (uint32_t)ckey[p - 1] != h) {
+    const uint64_t kp = ckey[p];
+    const uint32_t h = (uint32_t)(kp >> 32);
+    if (p == 0 || (uint32_t)(ckey[p - 1] >> 32) != h) {
         uint64_t e = p + 1;
-        while (e < nc && (uint32_t)ckey[e] == h) ++e;
+        while (e < nc && (uint32_t)(ckey[e] >> 32) == h) ++e;
         if (e - p == 2) {
-            if (same_pair_key(recs, meta, cval[p], cval[p + 1])) {
+            const uint32_t a = (uint32_t)kp, b = (uint32_t)ckey[p + 1];
+            if (same_pair_key(recs, meta[a], meta[b])) {
                 f = 1;
-                sparse[p] = make_uint2(cval[p], cval[p + 1]);
+                sparse[p] = make_uint2(a, b);
             }
         } else if (e - p > 2) {
             for (uint64_t x = p; x < e; ++x) {
                 if (used[x]) continue;
+                const uint32_t a = (uint32_t)ckey[x];
+                const RecMeta A = meta[a];
                 for (uint64_t y = x + 1; y < e; ++y) {
                     if (used[y]) continue;
-                    if (same_pair_key(recs, meta, cval[x], cval[y])) {
+                    const uint32_t b = (uint32_t)ckey[y];
+                    if (same_pair_key(recs, A, meta[b])) {
                         used[x] = used[y] = 1;
                         const unsigned int t = atomicAdd(nextra, 1u);
-                        extra[t] = make_uint2(cval[x], cval[y]);
+                        extra[t] = make_uint2(a, b);
                         break;
                     }
                 }
@@ -354,24 +375,21 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     const uint64_t nc1 = (uint64_t)nc + 1;
     uint64_t *ck = (uint64_t *)ctx->ws("md_ck", nc1 * 8);
-    uint32_t *cv = (uint32_t *)ctx->ws("md_cv", nc1 * 4);
     uint64_t *ck2 = (uint64_t *)ctx->ws("md_ck2", nc1 * 8);
-    uint32_t *cv2 = (uint32_t *)ctx->ws("md_cv2", nc1 * 4);
     uint8_t *used = (uint8_t *)ctx->ws("md_used", nc1);
     uint32_t *pflag = (uint32_t *)ctx->ws("md_pflag", nc1 * 4);
     uint2 *sparse = (uint2 *)ctx->ws("md_sparse", nc1 * sizeof(uint2));
     uint2 *pairs = (uint2 *)ctx->ws("md_pairs", (nc1 / 2 + 1) * sizeof(uint2));
     uint2 *extra = (uint2 *)ctx->ws("md_extra", (nc1 / 2 + 1) * sizeof(uint2));
-    if (!ck || !cv || !ck2 || !cv2 || !used || !pflag || !sparse || !pairs || !extra) return OGE_ERR_HIP;
-    hipLaunchKernelGGL(k_cand_scatter, dim3(nb), dim3(kT), 0, ctx->stream, meta, n, (const uint32_t *)cpos, ck, cv);
+    if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !extra) return OGE_ERR_HIP;
+    hipLaunchKernelGGL(k_cand_scatter, dim3(nb), dim3(kT), 0, ctx->stream, meta, n, (const uint32_t *)cpos, ck);
     OGE_LAUNCH_CHECK(ctx);
     uint64_t *sk;
-    uint32_t *sv;
-    rc = oge_radix_sort_pairs(ctx, ck, cv, ck2, cv2, nc, 0xFFFFFFFFull, &sk, &sv);
+    rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, 0xFFFFFFFF00000000ull, &sk, nullptr);
     if (rc) return rc;
     OGE_HIP_TRY(ctx, hipMemsetAsync(used, 0, nc1, ctx->stream));
     hipLaunchKernelGGL(k_pair_runs, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint8_t *)d_recs, meta,
-                       (const uint64_t *)sk, (const uint32_t *)sv, (uint64_t)nc, used, pflag, sparse, extra, cnt);
+                       (const uint64_t *)sk, (uint64_t)nc, used, pflag, sparse, extra, cnt);
     OGE_LAUNCH_CHECK(ctx);
     rc = oge_exclusive_scan_u32(ctx, pflag, pflag, nc1);
     if (rc) return rc;

@@ -55,7 +55,7 @@ int oge_exclusive_scan_u64(oge_ctx *ctx, const uint64_t *in, uint64_t *out, uint
 // Stable LSD radix sort of (key, value) pairs on key bits selected by `bit_mask` (only bits set
 // in the mask are sorted; set bits are grouped into digit passes of <= 8 contiguous bits).
 // Buffers: keys/vals hold the input; ktmp/vtmp scratch of the same size.  On return *kout/*vout
-// point at whichever pair of buffers holds the result.
+// point at whichever pair of buffers holds the result.  vals == NULL sorts keys only.
 int oge_radix_sort_pairs(oge_ctx *ctx, uint64_t *keys, uint32_t *vals, uint64_t *ktmp, uint32_t *vtmp,
                          uint64_t n, uint64_t bit_mask, uint64_t **kout, uint32_t **vout);
 // OR / AND reduction of a u64 array (for choosing the varying key bits).

@@ -165,41 +165,50 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
     }
 }
 
+// Stable scatter of one 4096-key tile.  Ranks come from 64-lane ballot peer masks per wave; the
+// tile is then re-ordered by digit in LDS so that the global writes of each digit bucket are
+// contiguous runs written by consecutive lanes (instead of 16 scattered 8-byte writes per bucket).
+template <bool HAS_V>
 __global__ __launch_bounds__(kThreads) void k_radix_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                              uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint64_t n,
                                                              Digit dg, uint32_t nbins, const uint32_t *__restrict__ offs,
                                                              uint32_t nblocks) {
+    __shared__ uint64_t sk[kTile];
+    __shared__ uint32_t sv[HAS_V ? kTile : 1];
     __shared__ uint32_t wcnt[kWaves][256];
+    __shared__ uint32_t dstart[256];
+    __shared__ uint32_t gbase[256];
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint32_t nbits = dg.w0 + dg.w1;
     for (uint32_t i = tid; i < kWaves * 256; i += kThreads) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)w * (kItems * 64);
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kTile;
+    const uint64_t base = tile0 + (uint64_t)w * (kItems * 64);
     const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
     uint64_t key[kItems];
     uint32_t val[kItems];
     uint32_t rank[kItems];
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
-        uint64_t idx = base + (uint64_t)j * 64 + lane;
-        bool valid = idx < n;
+        const uint64_t idx = base + (uint64_t)j * 64 + lane;
+        const bool valid = idx < n;
         key[j] = valid ? kin[idx] : 0ull;
-        val[j] = valid ? vin[idx] : 0u;
+        if (HAS_V) val[j] = valid ? vin[idx] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
-        uint64_t idx = base + (uint64_t)j * 64 + lane;
-        bool valid = idx < n;
-        uint32_t d = digit_of(key[j], dg);
+        const uint64_t idx = base + (uint64_t)j * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t d = digit_of(key[j], dg);
         uint64_t peers = __ballot(valid);
         for (uint32_t b = 0; b < nbits; ++b) {
-            uint64_t m = __ballot((d >> b) & 1u);
+            const uint64_t m = __ballot((d >> b) & 1u);
             peers &= ((d >> b) & 1u) ? m : ~m;
         }
-        uint32_t below = (uint32_t)__popcll(peers & lt_mask);
-        uint32_t cnt = (uint32_t)__popcll(peers);
-        uint32_t leader = (uint32_t)(__ffsll((long long)peers) - 1);
-        uint32_t prev = valid ? wcnt[w][d] : 0u;
+        const uint32_t below = (uint32_t)__popcll(peers & lt_mask);
+        const uint32_t cnt = (uint32_t)__popcll(peers);
+        const uint32_t leader = (uint32_t)(__ffsll((long long)peers) - 1);
+        const uint32_t prev = valid ? wcnt[w][d] : 0u;
         // all peers of the wave read wcnt[w][d] in the same ds_read before the leader's write
         __builtin_amdgcn_wave_barrier();
         if (valid && lane == leader) wcnt[w][d] = prev + cnt;
@@ -207,25 +216,43 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(const uint64_t *__re
         rank[j] = prev + below;
     }
     __syncthreads();
-    for (uint32_t d = tid; d < nbins; d += kThreads) {
-        uint32_t run = offs[(uint64_t)d * nblocks + blockIdx.x];
+    // per digit: tile total -> exclusive scan over digits (block-local bucket starts)
+    uint32_t tot = 0;
+    if (tid < nbins) {
+#pragma unroll
+        for (int i = 0; i < kWaves; ++i) tot += wcnt[i][tid];
+    }
+    uint32_t dummy;
+    const uint32_t ds = block_excl_scan(tot, &dummy);
+    if (tid < nbins) {
+        dstart[tid] = ds;
+        gbase[tid] = offs[(uint64_t)tid * nblocks + blockIdx.x];
+        uint32_t run = ds;
 #pragma unroll
         for (int i = 0; i < kWaves; ++i) {
-            uint32_t c = wcnt[i][d];
-            wcnt[i][d] = run;
+            const uint32_t c = wcnt[i][tid];
+            wcnt[i][tid] = run;
             run += c;
         }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
-        uint64_t idx = base + (uint64_t)j * 64 + lane;
+        const uint64_t idx = base + (uint64_t)j * 64 + lane;
         if (idx < n) {
-            uint32_t d = digit_of(key[j], dg);
-            uint32_t pos = wcnt[w][d] + rank[j];
-            kout[pos] = key[j];
-            vout[pos] = val[j];
+            const uint32_t lpos = wcnt[w][digit_of(key[j], dg)] + rank[j];
+            sk[lpos] = key[j];
+            if (HAS_V) sv[lpos] = val[j];
         }
+    }
+    __syncthreads();
+    const uint32_t cnt_tile = (uint32_t)((n - tile0) < (uint64_t)kTile ? (n - tile0) : (uint64_t)kTile);
+    for (uint32_t i = tid; i < cnt_tile; i += kThreads) {
+        const uint64_t k = sk[i];
+        const uint32_t d = digit_of(k, dg);
+        const uint32_t g = gbase[d] + (i - dstart[d]);
+        kout[g] = k;
+        if (HAS_V) vout[g] = sv[i];
     }
 }
 
@@ -294,29 +321,35 @@ int oge_reduce_or_and_u64(oge_ctx *ctx, const uint64_t *in, uint64_t n, uint64_t
 int oge_radix_sort_pairs(oge_ctx *ctx, uint64_t *keys, uint32_t *vals, uint64_t *ktmp, uint32_t *vtmp, uint64_t n,
                          uint64_t bit_mask, uint64_t **kout, uint32_t **vout) {
     *kout = keys;
-    *vout = vals;
+    if (vout) *vout = vals;
     if (n < 2 || bit_mask == 0) return OGE_OK;
     if (n > 0xFFFFFFFFull) return oge_fail(ctx, OGE_ERR_LIMIT, "radix sort: more than 2^32-1 elements");
+    const bool has_v = vals != nullptr;
     std::vector<Digit> digits = plan_digits(bit_mask);
-    uint32_t nblocks = oge_ceil_div(n, kTile);
+    const uint32_t nblocks = oge_ceil_div(n, kTile);
     uint32_t *hist = (uint32_t *)ctx->ws("radix_hist", (size_t)256 * nblocks * sizeof(uint32_t));
     if (!hist) return OGE_ERR_HIP;
     uint64_t *ka = keys, *kb = ktmp;
     uint32_t *va = vals, *vb = vtmp;
     for (const Digit &d : digits) {
-        uint32_t nbins = 1u << (d.w0 + d.w1);
+        const uint32_t nbins = 1u << (d.w0 + d.w1);
         hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(kThreads), 0, ctx->stream, (const uint64_t *)ka, n, d, nbins,
                            hist, nblocks);
         OGE_LAUNCH_CHECK(ctx);
         int rc = oge_exclusive_scan_u32(ctx, hist, hist, (uint64_t)nbins * nblocks);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_radix_scatter, dim3(nblocks), dim3(kThreads), 0, ctx->stream, (const uint64_t *)ka,
-                           (const uint32_t *)va, kb, vb, n, d, nbins, (const uint32_t *)hist, nblocks);
+        if (has_v)
+            hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nblocks), dim3(kThreads), 0, ctx->stream, (const uint64_t *)ka,
+                               (const uint32_t *)va, kb, vb, n, d, nbins, (const uint32_t *)hist, nblocks);
+        else
+            hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nblocks), dim3(kThreads), 0, ctx->stream, (const uint64_t *)ka,
+                               (const uint32_t *)nullptr, kb, (uint32_t *)nullptr, n, d, nbins, (const uint32_t *)hist,
+                               nblocks);
         OGE_LAUNCH_CHECK(ctx);
         std::swap(ka, kb);
         std::swap(va, vb);
     }
     *kout = ka;
-    *vout = va;
+    if (vout) *vout = va;
     return OGE_OK;
 }

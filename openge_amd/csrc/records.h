@@ -17,9 +17,11 @@ struct alignas(16) RecMeta {
     uint64_t src;    // byte offset of the record in the input arena
     int32_t seq;     // read1Sequence (refID)
     int32_t coord;   // unclipped 5' coordinate (0-based)
-    int32_t r2seq;   // mate refID if paired && mate mapped, else -1
+    int32_t rgi;     // read group of the record: index in the header table, -2 = no/empty RG tag,
+                     // -1 = RG value not in the table (pair keys then compare the RG bytes)
     uint32_t hash;   // FNV-1a of RG ":" name (pair key), candidates only
 };
+constexpr int32_t OGE_RGI_NONE = -2, OGE_RGI_UNLISTED = -1;
 
 // Read-group table on the device: ids back to back, off[g]..off[g+1]-1 is "ID\0" of group g.
 struct OgeRgTable {

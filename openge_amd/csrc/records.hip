@@ -85,7 +85,7 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
     M.src = src;
     M.seq = -1;
     M.coord = 0;
-    M.r2seq = -1;
+    M.rgi = OGE_RGI_NONE;
     M.hash = 0;
     uint64_t m = ((uint64_t)oge_reg2bin(pos, pos + rl) << 48) | ((uint64_t)(flag >> 8) << 40);
     if (!(flag & OGE_F_SECONDARY)) m |= OGE_M_PRIMARY;
@@ -149,19 +149,21 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
             if (!ok || p >= tend || rd.u8(p) == 0) break;
         }
         int16_t lib = a.rg.unknown_lib;
+        M.rgi = OGE_RGI_NONE;
         if (has && rgl) {
+            M.rgi = OGE_RGI_UNLISTED;
             for (int32_t g = 0; g < a.rg.n_rg; ++g) {
                 const uint32_t o = a.rg.off[g], Lg = a.rg.off[g + 1] - o - 1;
                 if (Lg != rgl) continue;
                 bool eq = true;
                 for (uint32_t y = 0; y < Lg && eq; ++y) eq = a.rg.ids[o + y] == rd.u8(rgv + y);
-                if (eq) { lib = a.rg.lib[g]; break; }
+                if (eq) { lib = a.rg.lib[g]; M.rgi = g; break; }
             }
         }
         m |= (uint64_t)(uint16_t)lib << 16;
         const bool paired_mm = (flag & OGE_F_PAIRED) && !(flag & OGE_F_MUNMAP);
-        M.r2seq = paired_mm ? (int32_t)rd.u32(r + OGE_OFF_MREFID) : -1;
-        if (M.r2seq != -1) m |= OGE_M_PAIRED;
+        // isPaired(): read2Sequence = mate refID (buildReadEnds :156-158), -1 otherwise
+        if (paired_mm && (int32_t)rd.u32(r + OGE_OFF_MREFID) != -1) m |= OGE_M_PAIRED;
         if (paired_mm) {
             m |= OGE_M_CAND;
             uint32_t h = 2166136261u;
