@@ -38,9 +38,10 @@ __global__ __launch_bounds__(kT) void k_cand_flags(const RecMeta *__restrict__ m
 // candidate key = pair-key hash << 32 | record index; only the hash half is radix-sorted, and
 // the stable LSD sort keeps record order inside a hash run (the ReadEndsMap's first/second-seen)
 __global__ __launch_bounds__(kT) void k_cand_scatter(const RecMeta *__restrict__ meta, uint64_t n,
-                                                      const uint32_t *__restrict__ pos, uint64_t *__restrict__ ckey) {
+                                                      const uint32_t *__restrict__ pos, uint32_t hmask,
+                                                      uint64_t *__restrict__ ckey) {
     uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i < n && (meta[i].m & OGE_M_CAND)) ckey[pos[i]] = ((uint64_t)meta[i].hash << 32) | (uint32_t)i;
+    if (i < n && (meta[i].m & OGE_M_CAND)) ckey[pos[i]] = ((uint64_t)(meta[i].hash & hmask) << 32) | (uint32_t)i;
 }
 
 __device__ bool pair_key_of(const uint8_t *r, const uint8_t **rg, uint32_t *rgl, uint32_t *nl) {
@@ -60,23 +61,21 @@ __device__ __forceinline__ uint8_t key_byte(const uint8_t *rgv, uint32_t rgl, co
 // summarised by A and B.  Same listed read group -> the keys are equal iff the names are, which is
 // one 16-byte-chunked compare at record byte 36; anything else compares the whole key strings.
 __device__ bool same_pair_key(const uint8_t *recs, const RecMeta &A, const RecMeta &B) {
+    if (A.rgi == B.rgi && A.rgi != OGE_RGI_UNLISTED && (A.m & B.m & OGE_M_NAMEFIT)) {
+        // same listed read group: keys equal iff names equal; both names sit NUL-terminated and
+        // zero-padded in the metadata slots
+        const uint4 *x = (const uint4 *)A.name, *y = (const uint4 *)B.name;
+#pragma unroll
+        for (uint32_t q = 0; q < OGE_NAME_SLOT / 16; ++q)
+            if (x[q].x != y[q].x || x[q].y != y[q].y || x[q].z != y[q].z || x[q].w != y[q].w) return false;
+        return true;
+    }
     const uint8_t *ra = recs + A.src, *rb = recs + B.src;
     if (A.rgi == B.rgi && A.rgi != OGE_RGI_UNLISTED) {
         const uint32_t la = ra[OGE_OFF_LNAME];
         if (la != rb[OGE_OFF_LNAME]) return false;
-        for (uint32_t k = 0; k < la; k += 16) {  // compares the NUL too: equal lengths
-            const uint4 x = *(const uint4 *)(ra + OGE_OFF_NAME + k), y = *(const uint4 *)(rb + OGE_OFF_NAME + k);
-            const uint32_t rem = la - k;
-            uint32_t d0 = x.x ^ y.x, d1 = x.y ^ y.y, d2 = x.z ^ y.z, d3 = x.w ^ y.w;
-            if (rem < 16) {  // ignore bytes past the name
-                const uint32_t keep[4] = {rem >= 4 ? 0xffffffffu : (rem ? (1u << (8 * rem)) - 1u : 0u),
-                                          rem >= 8 ? 0xffffffffu : (rem > 4 ? (1u << (8 * (rem - 4))) - 1u : 0u),
-                                          rem >= 12 ? 0xffffffffu : (rem > 8 ? (1u << (8 * (rem - 8))) - 1u : 0u),
-                                          rem > 12 ? (1u << (8 * (rem - 12))) - 1u : 0u};
-                d0 &= keep[0]; d1 &= keep[1]; d2 &= keep[2]; d3 &= keep[3];
-            }
-            if (d0 | d1 | d2 | d3) return false;
-        }
+        for (uint32_t k = 0; k < la; ++k)
+            if (ra[OGE_OFF_NAME + k] != rb[OGE_OFF_NAME + k]) return false;
         return true;
     }
     const uint8_t *ga = nullptr, *gb = nullptr;
@@ -95,8 +94,8 @@ __device__ bool same_pair_key(const uint8_t *recs, const RecMeta &A, const RecMe
 // scan, no atomics).  Longer runs (hash collisions, supplementary records) append to `extra`.
 __global__ __launch_bounds__(kT) void k_pair_runs(const uint8_t *__restrict__ recs, const RecMeta *__restrict__ meta,
                                                    const uint64_t *__restrict__ ckey, uint64_t nc, uint8_t *__restrict__ used,
-                                                   uint32_t *__restrict__ flag, uint2 *__restrict__ sparse,
-                                                   uint2 *__restrict__ extra, unsigned int *__restrict__ nextra) {
+                                                   uint32_t *__restrict__ flag, uint64_t *__restrict__ sparse,
+                                                   uint64_t *__restrict__ extra, unsigned int *__restrict__ nextra) {
     const uint64_t p = (uint64_t)blockIdx.x * kT + threadIdx.x;
     if (p > nc) return;
     if (p == nc) { flag[p] = 0; return; }
@@ -107,11 +106,10 @@ __global__ __launch_bounds__(kT) void k_pair_runs(const uint8_t *__restrict__ re
         uint64_t e = p + 1;
         while (e < nc && (uint32_t)(ckey[e] >> 32) == h) ++e;
         if (e - p == 2) {
-            const uint32_t a = (uint32_t)kp, b = (uint32_t)ckey[p + 1];
-            if (same_pair_key(recs, meta[a], meta[b])) {
-                f = 1;
-                sparse[p] = make_uint2(a, b);
-            }
+            // provisional pair (first-seen a < b): confirmed by k_pair_build, which visits pairs in
+            // sorted-position order so both summaries are read from nearby rows
+            f = 1;
+            sparse[p] = (kp << 32) | (uint32_t)ckey[p + 1];
         } else if (e - p > 2) {
             for (uint64_t x = p; x < e; ++x) {
                 if (used[x]) continue;
@@ -123,7 +121,7 @@ __global__ __launch_bounds__(kT) void k_pair_runs(const uint8_t *__restrict__ re
                     if (same_pair_key(recs, A, meta[b])) {
                         used[x] = used[y] = 1;
                         const unsigned int t = atomicAdd(nextra, 1u);
-                        extra[t] = make_uint2(a, b);
+                        extra[t] = ((uint64_t)a << 32) | b;
                         break;
                     }
                 }
@@ -134,8 +132,8 @@ __global__ __launch_bounds__(kT) void k_pair_runs(const uint8_t *__restrict__ re
 }
 
 // after the exclusive scan, position p holds a pair iff pos[p+1] != pos[p]
-__global__ __launch_bounds__(kT) void k_pair_compact_scan(const uint32_t *__restrict__ pos, const uint2 *__restrict__ sparse,
-                                                           uint64_t nc, uint2 *__restrict__ pairs) {
+__global__ __launch_bounds__(kT) void k_pair_compact_scan(const uint32_t *__restrict__ pos, const uint64_t *__restrict__ sparse,
+                                                           uint64_t nc, uint64_t *__restrict__ pairs) {
     const uint64_t p = (uint64_t)blockIdx.x * kT + threadIdx.x;
     if (p < nc && pos[p + 1] != pos[p]) pairs[pos[p]] = sparse[p];
 }
@@ -148,16 +146,19 @@ __device__ __forceinline__ int orient_byte(bool r1neg, bool r2neg) {
     return r1neg ? (r2neg ? RE_RR : RE_RF) : (r2neg ? RE_FR : RE_FF);
 }
 
+// Pairs (a << 32 | b, sorted by a) -> pair ReadEnds group keys.  The pair key is confirmed here
+// (same_pair_key); a hash-collision "pair" gets bit 63 of lo and is ignored by k_pair_groups.
 // hi = score(16) << 48 | lib << (sb+32) | r1Seq << 32 | biased r1Coord
-// lo = (orient-3) << (sb+32) | r2Seq << 32 | biased r2Coord
-__global__ __launch_bounds__(kT) void k_pair_build(const uint2 *__restrict__ pairs, uint32_t np,
+// lo = invalid << 63 | (orient-3) << (sb+32) | r2Seq << 32 | biased r2Coord
+__global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ pairs, uint32_t np, const uint8_t *__restrict__ recs,
                                                     const RecMeta *__restrict__ meta, KeyLayout L, uint64_t *__restrict__ hi,
                                                     uint64_t *__restrict__ lo, uint2 *__restrict__ idx, uint32_t *__restrict__ val) {
     uint32_t p = blockIdx.x * kT + threadIdx.x;
     if (p >= np) return;
-    uint32_t a = pairs[p].x, b = pairs[p].y;  // a seen first (smaller record index)
+    uint32_t a = (uint32_t)(pairs[p] >> 32), b = (uint32_t)pairs[p];  // a seen first (smaller record index)
     if (a > b) { uint32_t t = a; a = b; b = t; }
     const RecMeta A = meta[a], B = meta[b];
+    const uint64_t bad = same_pair_key(recs, A, B) ? 0ull : (1ull << 63);
     const uint64_t ma = A.m, mb = B.m;
     const int32_t sa = A.seq, ca = A.coord, sb_ = B.seq, cb = B.coord;
     const bool reva = (ma & OGE_M_REV) != 0, revb = (mb & OGE_M_REV) != 0;
@@ -175,7 +176,8 @@ __global__ __launch_bounds__(kT) void k_pair_build(const uint2 *__restrict__ pai
     const uint64_t lib = (ma >> 16) & 0xFFFF;
     hi[p] = ((uint64_t)score << 48) | (lib << (L.sb + 32)) | ((uint64_t)(uint32_t)r1s << 32) |
             (uint64_t)((uint32_t)r1c ^ 0x80000000u);
-    lo[p] = ((uint64_t)(o - RE_FF) << (L.sb + 32)) | ((uint64_t)(uint32_t)r2s << 32) | (uint64_t)((uint32_t)r2c ^ 0x80000000u);
+    lo[p] = bad | ((uint64_t)(o - RE_FF) << (L.sb + 32)) | ((uint64_t)(uint32_t)r2s << 32) |
+            (uint64_t)((uint32_t)r2c ^ 0x80000000u);
     idx[p] = make_uint2(i1, i2);
     val[p] = p;
 }
@@ -194,6 +196,7 @@ __global__ __launch_bounds__(kT) void k_pair_groups(const uint64_t *__restrict__
     if (q >= np) return;
     const uint64_t kmask = (1ull << 48) - 1;
     const uint64_t h = shi[q] & kmask, l = lo[sval[q]];
+    if (l >> 63) return;  // unconfirmed pair key (hash collision): not a pair
     if (q > 0 && (shi[q - 1] & kmask) == h && lo[sval[q - 1]] == l) return;
     uint32_t e = q + 1;
     while (e < np && (shi[e] & kmask) == h && lo[sval[e]] == l) ++e;
@@ -305,6 +308,12 @@ uint32_t bits_for(uint64_t v) {  // bits to hold values 0..v
     return b ? b : 1;
 }
 
+// high-32-bit mask covering record indices 0..n-1 (only the bits that can vary)
+uint64_t bits_mask_hi32(uint64_t n) {
+    const uint32_t b = bits_for(n ? n - 1 : 0);
+    return (b >= 32 ? 0xFFFFFFFFull : ((1ull << b) - 1)) << 32;
+}
+
 }  // namespace
 
 // Allocate the per-record ReadEnds summaries (`name` selects the buffer) and upload the RG table.
@@ -378,11 +387,14 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     uint64_t *ck2 = (uint64_t *)ctx->ws("md_ck2", nc1 * 8);
     uint8_t *used = (uint8_t *)ctx->ws("md_used", nc1);
     uint32_t *pflag = (uint32_t *)ctx->ws("md_pflag", nc1 * 4);
-    uint2 *sparse = (uint2 *)ctx->ws("md_sparse", nc1 * sizeof(uint2));
-    uint2 *pairs = (uint2 *)ctx->ws("md_pairs", (nc1 / 2 + 1) * sizeof(uint2));
-    uint2 *extra = (uint2 *)ctx->ws("md_extra", (nc1 / 2 + 1) * sizeof(uint2));
-    if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !extra) return OGE_ERR_HIP;
-    hipLaunchKernelGGL(k_cand_scatter, dim3(nb), dim3(kT), 0, ctx->stream, meta, n, (const uint32_t *)cpos, ck);
+    uint64_t *sparse = (uint64_t *)ctx->ws("md_sparse", nc1 * 8);
+    uint64_t *pairs = (uint64_t *)ctx->ws("md_pairs", (nc1 / 2 + 1) * 8);
+    uint64_t *pairs2 = (uint64_t *)ctx->ws("md_pairs2", (nc1 / 2 + 1) * 8);
+    uint64_t *extra = (uint64_t *)ctx->ws("md_extra", (nc1 / 2 + 1) * 8);
+    if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !extra) return OGE_ERR_HIP;
+    const uint32_t hmask = (opts->debug_hash_bits > 0 && opts->debug_hash_bits < 32) ? (1u << opts->debug_hash_bits) - 1u
+                                                                                     : 0xFFFFFFFFu;
+    hipLaunchKernelGGL(k_cand_scatter, dim3(nb), dim3(kT), 0, ctx->stream, meta, n, (const uint32_t *)cpos, hmask, ck);
     OGE_LAUNCH_CHECK(ctx);
     uint64_t *sk;
     rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, 0xFFFFFFFF00000000ull, &sk, nullptr);
@@ -399,11 +411,15 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     // flags were overwritten by the scan: compact by comparing neighbouring prefix sums
     hipLaunchKernelGGL(k_pair_compact_scan, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)pflag,
-                       (const uint2 *)sparse, (uint64_t)nc, pairs);
+                       (const uint64_t *)sparse, (uint64_t)nc, pairs);
     OGE_LAUNCH_CHECK(ctx);
     if (hc[1])
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(pairs + hc[0], extra, (size_t)hc[1] * sizeof(uint2), hipMemcpyDeviceToDevice, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(pairs + hc[0], extra, (size_t)hc[1] * 8, hipMemcpyDeviceToDevice, ctx->stream));
     const uint32_t np = hc[0] + hc[1];
+    // order the pairs by first-mate position: k_pair_build then reads both summaries from nearby rows
+    uint64_t *spairs = pairs;
+    rc = oge_radix_sort_pairs(ctx, pairs, nullptr, pairs2, nullptr, np, bits_mask_hi32(n), &spairs, nullptr);
+    if (rc) return rc;
     ctx->end_stage(t);
 
     // ---- pair groups ----
@@ -418,7 +434,8 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
         uint32_t *pv2 = (uint32_t *)ctx->ws("md_pv2", (uint64_t)np * 4);
         if (!hi || !lo || !lo2 || !hi2 || !pidx || !pv || !pv2) return OGE_ERR_HIP;
         const uint32_t pb = oge_ceil_div(np, kT);
-        hipLaunchKernelGGL(k_pair_build, dim3(pb), dim3(kT), 0, ctx->stream, (const uint2 *)pairs, np, meta, L, hi, lo, pidx, pv);
+        hipLaunchKernelGGL(k_pair_build, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)spairs, np,
+                           (const uint8_t *)d_recs, meta, L, hi, lo, pidx, pv);
         OGE_LAUNCH_CHECK(ctx);
         // LSD over (hi, lo): sort by lo first (copy lo so the unsorted lo stays addressable by pair index)
         OGE_HIP_TRY(ctx, hipMemcpyAsync(lo2, lo, (uint64_t)np * 8, hipMemcpyDeviceToDevice, ctx->stream));

@@ -6,12 +6,16 @@
 //   [0,16)  score (int16, getScore)        [16,32) library id
 //   bit 32 fragment ReadEnds exists (mapped, refID != -1, primary)   bit 33 reverse strand
 //   bit 34 pair candidate (paired && mate mapped)                    bit 35 primary (0x100 clear)
-//   bit 36 isPaired() (read2Sequence = mate refID != -1)             [40,48) original FLAG >> 8
+//   bit 36 isPaired() (read2Sequence = mate refID != -1)             bit 37 whole name in `name`
+//   [40,48) original FLAG >> 8
 //   [48,64) bin the writer must store (recomputed, util/bam_serializer.h:112-116)
 constexpr uint64_t OGE_M_FRAG = 1ull << 32, OGE_M_REV = 1ull << 33, OGE_M_CAND = 1ull << 34,
-                   OGE_M_PRIMARY = 1ull << 35, OGE_M_PAIRED = 1ull << 36;
+                   OGE_M_PRIMARY = 1ull << 35, OGE_M_PAIRED = 1ull << 36, OGE_M_NAMEFIT = 1ull << 37;
+constexpr uint32_t OGE_NAME_SLOT = 32;
 
-// 32-byte record summary (array-of-structs: one 32-byte access moves a record's metadata).
+// 64-byte record summary (array-of-structs: one 64-byte access moves a record's metadata).  The
+// read name rides along (NUL-terminated, zero-padded) so mates can be confirmed without touching
+// the record arena; names longer than the slot fall back to the record bytes.
 struct alignas(16) RecMeta {
     uint64_t m;
     uint64_t src;    // byte offset of the record in the input arena
@@ -20,6 +24,7 @@ struct alignas(16) RecMeta {
     int32_t rgi;     // read group of the record: index in the header table, -2 = no/empty RG tag,
                      // -1 = RG value not in the table (pair keys then compare the RG bytes)
     uint32_t hash;   // FNV-1a of RG ":" name (pair key), candidates only
+    uint8_t name[OGE_NAME_SLOT];
 };
 constexpr int32_t OGE_RGI_NONE = -2, OGE_RGI_UNLISTED = -1;
 

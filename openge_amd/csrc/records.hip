@@ -172,6 +172,21 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
             const uint32_t nl = lname ? lname - 1u : 0u;
             for (uint32_t y = 0; y < nl; ++y) h = h_step(h, rd.u8(r + OGE_OFF_NAME + y));
             M.hash = h;
+            // name slot: l_read_name bytes (with the NUL) when they fit, zero-padded
+            if (lname <= OGE_NAME_SLOT) {
+                m |= OGE_M_NAMEFIT;
+                uint32_t *ns = (uint32_t *)M.name;
+#pragma unroll
+                for (uint32_t q = 0; q < OGE_NAME_SLOT / 4; ++q) {
+                    uint32_t v = 0;
+                    if (4 * q < lname) {
+                        v = rd.u32(r + OGE_OFF_NAME + 4 * q);
+                        const uint32_t rem = lname - 4 * q;
+                        if (rem < 4) v &= (1u << (8 * rem)) - 1u;
+                    }
+                    ns[q] = v;
+                }
+            }
         }
     }
     M.m = m;

@@ -102,3 +102,19 @@ def test_fused_sort_markdup(ctx, preset, npairs, seed):
         o = int(soffs[k])
         exp[o + 18:o + 20] = np.frombuffer(int(fl[k]).to_bytes(2, "little"), dtype=np.uint8)
     assert np.array_equal(out[:tot], exp[:tot])
+
+
+@pytest.mark.parametrize("bits", [1, 6, 12])
+def test_markdup_forced_hash_collisions(ctx, bits):
+    """Truncating the pair-key hash forces long hash runs and colliding 2-runs of non-mates:
+    the exact key confirmation must keep the result identical to the oracle."""
+    p = L.synth_params(1500, preset="mix", seed=11)
+    recs, offs, hdr = L.synth_host(p)
+    n = 3000
+    perm = oracle.sort_perm(recs, offs, n)
+    so = np.append(offs[:-1][perm], 0).astype(np.uint64)
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    opts.debug_hash_bits = bits
+    dup, nd = ctx.markdup(recs, so, n, opts)
+    odup, ond = oracle.markdup(recs, so, n, hdr)
+    assert nd == ond and np.array_equal(dup, odup)
