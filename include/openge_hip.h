@@ -88,7 +88,7 @@ typedef struct oge_markdup_opts {
     int32_t compat_nonverbose_index;
     /* 1 = drop duplicates from the output (-r/-R); affects oge_markdup's n_kept only */
     int32_t remove_duplicates;
-    /* Test knob: keep only this many bits (1..31) of the 32-bit pair-key hash, to force the
+    /* Test knob: keep only this many bits (1..47) of the 48-bit pair-key hash, to force the
      * collision paths of the mate join.  0 = full hash.  Results must not change. */
     int32_t debug_hash_bits;
 } oge_markdup_opts;

@@ -35,13 +35,21 @@ __global__ __launch_bounds__(kT) void k_cand_flags(const RecMeta *__restrict__ m
     if (i < n) f[i] = (meta[i].m & OGE_M_CAND) ? 1u : 0u;
     else if (i == n) f[i] = 0;
 }
-// candidate key = pair-key hash << 32 | record index; only the hash half is radix-sorted, and
-// the stable LSD sort keeps record order inside a hash run (the ReadEndsMap's first/second-seen)
+// candidate key = top hb bits of the 48-bit pair-key hash << ib | record index (ib = bits for an
+// index, hb = min(48, 64 - ib)): the hash takes every key bit the index leaves free, so collision
+// runs (which fall to the exact slow path of k_pair_runs) stay rare at full-GPU sizes.  Only the hash
+// bits are radix-sorted; the stable LSD sort keeps record order inside a hash run (the
+// ReadEndsMap's first/second-seen).
+struct CandKey {
+    uint32_t ib, hb;
+    __host__ __device__ uint64_t idx_mask() const { return (1ull << ib) - 1; }
+    __host__ __device__ uint64_t hash_of(uint64_t k) const { return k >> ib; }
+};
 __global__ __launch_bounds__(kT) void k_cand_scatter(const RecMeta *__restrict__ meta, uint64_t n,
-                                                      const uint32_t *__restrict__ pos, uint32_t hmask,
+                                                      const uint32_t *__restrict__ pos, CandKey ck,
                                                       uint64_t *__restrict__ ckey) {
     uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i < n && (meta[i].m & OGE_M_CAND)) ckey[pos[i]] = ((uint64_t)(meta[i].hash & hmask) << 32) | (uint32_t)i;
+    if (i < n && (meta[i].m & OGE_M_CAND)) ckey[pos[i]] = ((oge_meta_hash48(meta[i]) >> (48 - ck.hb)) << ck.ib) | i;
 }
 
 __device__ bool pair_key_of(const uint8_t *r, const uint8_t **rg, uint32_t *rgl, uint32_t *nl) {
@@ -93,7 +101,7 @@ __device__ bool same_pair_key(const uint8_t *recs, const RecMeta &A, const RecMe
 // Common case (a run of exactly two): flag[p] = 1 and the pair is stored at p (compacted later by a
 // scan, no atomics).  Longer runs (hash collisions, supplementary records) append to `extra`.
 __global__ __launch_bounds__(kT) void k_pair_runs(const uint8_t *__restrict__ recs, const RecMeta *__restrict__ meta,
-                                                   const uint64_t *__restrict__ ckey, uint64_t nc, uint8_t *__restrict__ used,
+                                                   const uint64_t *__restrict__ ckey, uint64_t nc, CandKey ck, uint8_t *__restrict__ used,
                                                    uint32_t *__restrict__ flag, uint64_t *__restrict__ sparse,
                                                    uint64_t *__restrict__ extra, unsigned int *__restrict__ nextra) {
     const uint64_t p = (uint64_t)blockIdx.x * kT + threadIdx.x;
@@ -101,23 +109,23 @@ __global__ __launch_bounds__(kT) void k_pair_runs(const uint8_t *__restrict__ re
     if (p == nc) { flag[p] = 0; return; }
     uint32_t f = 0;
     const uint64_t kp = ckey[p];
-    const uint32_t h = (uint32_t)(kp >> 32);
-    if (p == 0 || (uint32_t)(ckey[p - 1] >> 32) != h) {
+    const uint64_t h = ck.hash_of(kp);
+    if (p == 0 || ck.hash_of(ckey[p - 1]) != h) {
         uint64_t e = p + 1;
-        while (e < nc && (uint32_t)(ckey[e] >> 32) == h) ++e;
+        while (e < nc && ck.hash_of(ckey[e]) == h) ++e;
         if (e - p == 2) {
             // provisional pair (first-seen a < b): confirmed by k_pair_build, which visits pairs in
             // sorted-position order so both summaries are read from nearby rows
             f = 1;
-            sparse[p] = (kp << 32) | (uint32_t)ckey[p + 1];
+            sparse[p] = ((kp & ck.idx_mask()) << 32) | (ckey[p + 1] & ck.idx_mask());
         } else if (e - p > 2) {
             for (uint64_t x = p; x < e; ++x) {
                 if (used[x]) continue;
-                const uint32_t a = (uint32_t)ckey[x];
+                const uint32_t a = (uint32_t)(ckey[x] & ck.idx_mask());
                 const RecMeta A = meta[a];
                 for (uint64_t y = x + 1; y < e; ++y) {
                     if (used[y]) continue;
-                    const uint32_t b = (uint32_t)ckey[y];
+                    const uint32_t b = (uint32_t)(ckey[y] & ck.idx_mask());
                     if (same_pair_key(recs, A, meta[b])) {
                         used[x] = used[y] = 1;
                         const unsigned int t = atomicAdd(nextra, 1u);
@@ -323,6 +331,7 @@ int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, 
     if (n > 0xFFFFFFFEull) return oge_fail(ctx, OGE_ERR_LIMIT, "markdup: more than 2^32-2 records");
     if (opts->n_rg < 0 || (opts->n_rg && (!opts->rg_ids || !opts->rg_lib)))
         return oge_fail(ctx, OGE_ERR_ARG, "markdup: bad read-group table");
+    if (opts->n_rg > OGE_MAX_RG) return oge_fail(ctx, OGE_ERR_LIMIT, "markdup: more than 32767 read groups");
     *meta = (RecMeta *)ctx->ws(name, (n + 1) * sizeof(RecMeta));
     std::vector<uint32_t> offs(opts->n_rg + 1, 0);
     const char *p = opts->rg_ids;
@@ -392,16 +401,18 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     uint64_t *pairs2 = (uint64_t *)ctx->ws("md_pairs2", (nc1 / 2 + 1) * 8);
     uint64_t *extra = (uint64_t *)ctx->ws("md_extra", (nc1 / 2 + 1) * 8);
     if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !extra) return OGE_ERR_HIP;
-    const uint32_t hmask = (opts->debug_hash_bits > 0 && opts->debug_hash_bits < 32) ? (1u << opts->debug_hash_bits) - 1u
-                                                                                     : 0xFFFFFFFFu;
-    hipLaunchKernelGGL(k_cand_scatter, dim3(nb), dim3(kT), 0, ctx->stream, meta, n, (const uint32_t *)cpos, hmask, ck);
+    CandKey ckl;
+    ckl.ib = bits_for(n - 1);
+    ckl.hb = std::min<uint32_t>(48, 64 - ckl.ib);
+    if (opts->debug_hash_bits > 0 && (uint32_t)opts->debug_hash_bits < ckl.hb) ckl.hb = (uint32_t)opts->debug_hash_bits;
+    hipLaunchKernelGGL(k_cand_scatter, dim3(nb), dim3(kT), 0, ctx->stream, meta, n, (const uint32_t *)cpos, ckl, ck);
     OGE_LAUNCH_CHECK(ctx);
     uint64_t *sk;
-    rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, 0xFFFFFFFF00000000ull, &sk, nullptr);
+    rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, ((1ull << ckl.hb) - 1) << ckl.ib, &sk, nullptr);
     if (rc) return rc;
     OGE_HIP_TRY(ctx, hipMemsetAsync(used, 0, nc1, ctx->stream));
     hipLaunchKernelGGL(k_pair_runs, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint8_t *)d_recs, meta,
-                       (const uint64_t *)sk, (uint64_t)nc, used, pflag, sparse, extra, cnt);
+                       (const uint64_t *)sk, (uint64_t)nc, ckl, used, pflag, sparse, extra, cnt);
     OGE_LAUNCH_CHECK(ctx);
     rc = oge_exclusive_scan_u32(ctx, pflag, pflag, nc1);
     if (rc) return rc;

@@ -21,12 +21,15 @@ struct alignas(16) RecMeta {
     uint64_t src;    // byte offset of the record in the input arena
     int32_t seq;     // read1Sequence (refID)
     int32_t coord;   // unclipped 5' coordinate (0-based)
-    int32_t rgi;     // read group of the record: index in the header table, -2 = no/empty RG tag,
+    int16_t rgi;     // read group of the record: index in the header table, -2 = no/empty RG tag,
                      // -1 = RG value not in the table (pair keys then compare the RG bytes)
-    uint32_t hash;   // FNV-1a of RG ":" name (pair key), candidates only
+    uint16_t hash_hi;
+    uint32_t hash;   // hash_hi:hash = 48-bit hash of RG ":" name (pair key), candidates only
     uint8_t name[OGE_NAME_SLOT];
 };
 constexpr int32_t OGE_RGI_NONE = -2, OGE_RGI_UNLISTED = -1;
+constexpr int32_t OGE_MAX_RG = 32767;  // read groups addressable by RecMeta.rgi
+__host__ __device__ inline uint64_t oge_meta_hash48(const RecMeta &M) { return ((uint64_t)M.hash_hi << 32) | M.hash; }
 
 // Read-group table on the device: ids back to back, off[g]..off[g+1]-1 is "ID\0" of group g.
 struct OgeRgTable {

@@ -46,7 +46,12 @@ struct GlbRd {
     __device__ __forceinline__ uint32_t u32(uint64_t x) const { return oge_ldu32(b + x); }
 };
 
-__device__ __forceinline__ uint32_t h_step(uint32_t h, uint32_t c) { return (h ^ c) * 16777619u; }
+// FNV-1a (64-bit) over the pair key, finished with the MurmurHash3 fmix64 avalanche so every bit
+// of the 48 kept is usable as a radix digit (the mate join sorts by as many bits as fit)
+__device__ __forceinline__ uint64_t h_step(uint64_t h, uint32_t c) { return (h ^ c) * 0x100000001b3ull; }
+__device__ __forceinline__ uint64_t h_fmix(uint64_t h) {
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; return h ^ (h >> 33);
+}
 
 // Record at absolute index r of reader `rd`; i = record index, src = its offset in the arena.
 template <bool META, bool KEYS, class Rd>
@@ -86,6 +91,7 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
     M.seq = -1;
     M.coord = 0;
     M.rgi = OGE_RGI_NONE;
+    M.hash_hi = 0;
     M.hash = 0;
     uint64_t m = ((uint64_t)oge_reg2bin(pos, pos + rl) << 48) | ((uint64_t)(flag >> 8) << 40);
     if (!(flag & OGE_F_SECONDARY)) m |= OGE_M_PRIMARY;
@@ -157,7 +163,7 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
                 if (Lg != rgl) continue;
                 bool eq = true;
                 for (uint32_t y = 0; y < Lg && eq; ++y) eq = a.rg.ids[o + y] == rd.u8(rgv + y);
-                if (eq) { lib = a.rg.lib[g]; M.rgi = g; break; }
+                if (eq) { lib = a.rg.lib[g]; M.rgi = (int16_t)g; break; }
             }
         }
         m |= (uint64_t)(uint16_t)lib << 16;
@@ -166,12 +172,14 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
         if (paired_mm && (int32_t)rd.u32(r + OGE_OFF_MREFID) != -1) m |= OGE_M_PAIRED;
         if (paired_mm) {
             m |= OGE_M_CAND;
-            uint32_t h = 2166136261u;
+            uint64_t h = 0xcbf29ce484222325ull;
             for (uint32_t y = 0; y < rgl; ++y) h = h_step(h, rd.u8(rgv + y));
             h = h_step(h, ':');
             const uint32_t nl = lname ? lname - 1u : 0u;
             for (uint32_t y = 0; y < nl; ++y) h = h_step(h, rd.u8(r + OGE_OFF_NAME + y));
-            M.hash = h;
+            h = h_fmix(h);
+            M.hash = (uint32_t)h;
+            M.hash_hi = (uint16_t)(h >> 32);
             // name slot: l_read_name bytes (with the NUL) when they fit, zero-padded
             if (lname <= OGE_NAME_SLOT) {
                 m |= OGE_M_NAMEFIT;
