@@ -65,13 +65,21 @@ def cpu_baseline(sample_reads: int) -> dict:
             "seconds": round(dt, 2)}
 
 
-def pmc_traffic() -> dict | None:
-    f = ROOT / "profiles" / "pmc_gather_records.json"
-    if f.exists():
-        try:
-            return json.loads(f.read_text())
-        except Exception:
-            return None
+def pmc_traffic(kernel: str, rec_bytes: int) -> dict | None:
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*_pmc.json,
+    written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes).
+    When the profiled workload had a different record-byte total, the count is scaled by bytes."""
+    files = sorted((ROOT / "profiles").glob("r*_pmc.json"))
+    if not files:
+        return None
+    try:
+        d = json.loads(files[-1].read_text())
+    except Exception:
+        return None
+    for name, v in d.get("kernels", {}).items():
+        if kernel in name:
+            b = d["workload"].get("record_bytes_per_gpu") or rec_bytes
+            return {"bytes": v["hbm_bytes"] * rec_bytes / b, "source": files[-1].name}
     return None
 
 
@@ -149,11 +157,12 @@ def main():
         seq_bytes = n * ((p.read_len + 1) // 2)
         pipe_bytes = 2 * B + (B - seq_bytes) + 2 * n
         pipe_gbs = pipe_bytes / (ms_step / 1e3) / 1e9
-        pmc = pmc_traffic()
+        pmc = pmc_traffic("k_gather16", B)
         roof = {"kernel": "k_gather_records (permutation gather + BAM re-encode)", "bound": "hbm",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                "traffic": round(pmc["bytes"]) if pmc else None,
+                "traffic_source": pmc["source"] if pmc else None,
                 "algorithmic_bytes": gather_bytes, "avg_ms": stages_ms["gather_records"]}
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mreads/s", "n_gpus": world, "steps": K,

@@ -1,0 +1,49 @@
+"""Summarise a gpurun round directory into profiles/: kernel stats + PMC HBM bytes per kernel.
+
+usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<tag>
+
+HBM bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes).  The factor 2 on FETCH_SIZE is
+the gfx950 correction of /opt/skills/guides/MI355X_MICROARCH.md ("HBM" section): FETCH_SIZE counts
+64 B per 128 B memory-side read request of a wide (16 B/lane) streaming read.  WRITE_SIZE is exact
+for 16 B/lane streaming stores.  FETCH_SIZE and WRITE_SIZE come from separate --pmc passes.
+"""
+import csv
+import json
+import shutil
+import sys
+from pathlib import Path
+
+
+def per_kernel(path):
+    agg = {}
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"]
+        agg.setdefault(k, []).append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    src, dst = Path(sys.argv[1]), Path(sys.argv[2])
+    dst.parent.mkdir(parents=True, exist_ok=True)
+    stats = src / "prof" / "run_kernel_stats.csv"
+    if stats.exists():
+        shutil.copy(stats, str(dst) + "_kernel_stats.csv")
+    for j in ["bench.json", "prof_bench.json"]:
+        if (src / j).exists():
+            shutil.copy(src / j, str(dst) + "_" + j)
+    fetch = src / "pmc_FETCH_SIZE" / "run_counter_collection.csv"
+    write = src / "pmc_WRITE_SIZE" / "run_counter_collection.csv"
+    if not (fetch.exists() and write.exists()):
+        return
+    f, w = per_kernel(fetch), per_kernel(write)
+    bench = json.loads((src / "pmc_FETCH_SIZE.json").read_text())
+    out = {"workload": bench["config"], "note": "bytes per launch; hbm = 2*FETCH_SIZE + WRITE_SIZE", "kernels": {}}
+    for k in sorted(set(f) | set(w), key=lambda k: -(2 * f.get(k, 0) + w.get(k, 0))):
+        out["kernels"][k] = {"fetch_size_bytes": f.get(k), "write_size_bytes": w.get(k),
+                             "hbm_bytes": 2 * f.get(k, 0) + w.get(k, 0)}
+    Path(str(dst) + "_pmc.json").write_text(json.dumps(out, indent=1))
+    print(f"wrote {dst}_pmc.json")
+
+
+if __name__ == "__main__":
+    main()
