@@ -109,6 +109,55 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
                          const oge_markdup_opts *opts, uint32_t *d_perm, uint8_t *d_out, uint64_t *d_out_off,
                          uint64_t *n_dup_out);
 
+/* ---- local realignment (LocalRealignment) ----------------------------------------- */
+/* Offset scan, the realigner's hot loop: for every pair (consensus c, altRead r) the best
+ * offset of r on c and its mismatch-quality score, exactly as findBestOffset returns them
+ * (algorithms/local_realignment.cpp:1126-1164 over mismatchQualitySumIgnoreCigar :641-679).
+ * cons / bases are ASCII bases; quals are raw phred bytes (BAM layout) aligned with bases;
+ * pairs holds n_pairs x {cons index, read index, orig offset, maxPossibleStart}. */
+typedef struct oge_realign_scan_batch {
+    const uint8_t *cons;
+    uint64_t cons_bytes;
+    const uint64_t *cons_off;   /* n_cons + 1 */
+    uint32_t n_cons;
+    uint32_t n_reads;
+    const uint8_t *bases;
+    const uint8_t *quals;
+    uint64_t read_bytes;
+    const uint64_t *read_off;   /* n_reads + 1 */
+    const int32_t *pairs;
+    uint64_t n_pairs;
+} oge_realign_scan_batch;
+int oge_realign_scan(oge_ctx *ctx, const oge_realign_scan_batch *batch, int32_t *best_index, int32_t *best_score);
+
+/* LocalRealignment's tunables (constructor constants, algorithms/local_realignment.cpp:1434-1460) */
+typedef struct oge_realign_opts {
+    double lod_threshold;            /* 5.0 */
+    double mismatch_threshold;       /* 0.15 (entropy) */
+    int32_t max_records_in_memory;   /* 150000 */
+    int32_t max_isize_for_movement;  /* 3000 */
+    int32_t max_pos_move_allowed;    /* 200 */
+    int32_t max_reads;               /* 20000 */
+    int32_t no_original_alignment_tags;
+    int32_t threads;                 /* host threads, 0 = all cores */
+} oge_realign_opts;
+void oge_realign_opts_init(oge_realign_opts *opts);
+
+/* Whole LocalRealignment module (map_func binning, consensus generation, offset scan on the GPU,
+ * LOD / entropy decision, CIGAR + tag updates, ConstrainedMateFixingManager emission) over
+ * coordinate-sorted records; replaces LocalRealignment::runInternal
+ * (algorithms/local_realignment.cpp:1462-1490) with the writer chain of
+ * cmd/command_localrealign.cpp:37-75.  header_text supplies the sequence dictionary. */
+typedef struct oge_realign_result oge_realign_result;
+int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len, const uint8_t *recs,
+                     const uint64_t *rec_off, uint64_t n, const char *fasta_path, const char *intervals_path,
+                     const oge_realign_opts *opts, oge_realign_result **out);
+uint64_t oge_realign_result_count(const oge_realign_result *r);
+const uint8_t *oge_realign_result_records(const oge_realign_result *r, uint64_t *bytes_out);
+const uint64_t *oge_realign_result_offsets(const oge_realign_result *r);   /* count + 1 entries */
+const char *oge_realign_result_stats(const oge_realign_result *r);          /* JSON */
+void oge_realign_result_free(oge_realign_result *r);
+
 /* ---- synthetic data (bench / tests) ------------------------------------------------ */
 /* params: a pointer to oge_synth_params (openge_amd/csrc/synth.h) */
 int oge_synth_finalize(void *params);
@@ -117,6 +166,18 @@ uint64_t oge_synth_params_size(void);
 int oge_synth_offsets_host(const void *params, uint64_t *offs, int threads);
 int oge_synth_records_host(const void *params, const uint64_t *offs, uint8_t *out, int threads);
 int oge_synth_header_text(const void *params, char *buf, uint64_t cap, uint64_t *len_out);
+/* Local-realignment data set (SURVEY §8d C5 shape; openge_amd/csrc/realign_synth.cpp): writes a
+ * reference FASTA (+ .fai), a target-interval list and a coordinate-sorted BAM. */
+typedef struct oge_realign_synth_params {
+    uint64_t seed;
+    uint32_t n_ref, n_intervals, spacing, read_len, frags_per_interval;
+    uint32_t qual_min, qual_max, ins_min, ins_max;
+    uint32_t err_ppm, noindel_ppm, gapped_ppm, alt_indel_ppm, dup_ppm, mapq0_ppm, clip_ppm;
+    uint32_t lower_ppm, n_ppm, md_ppm, uq_ppm;
+} oge_realign_synth_params;
+void oge_realign_synth_defaults(oge_realign_synth_params *p);   /* C5: 50k intervals, 24 contigs */
+int oge_synth_realign(const oge_realign_synth_params *p, const char *fasta_path, const char *intervals_path,
+                      const char *bam_path, int level, int threads);
 /* Device generation straight into HBM. */
 int oge_synth_offsets_dev(oge_ctx *ctx, const void *params, uint64_t *d_offs);
 int oge_synth_records_dev(oge_ctx *ctx, const void *params, const uint64_t *d_offs, uint8_t *d_out);

@@ -23,7 +23,7 @@ CXX = os.environ.get("CXX", "g++")
 ARCH = "gfx950"
 
 HIP_SRCS = ["prims.hip", "sort.hip", "records.hip", "markdup.hip", "capi_dev.hip", "realign.hip"]
-HOST_SRCS = ["bamio.cpp", "host_capi.cpp"]
+HOST_SRCS = ["bamio.cpp", "host_capi.cpp", "realign.cpp", "realign_synth.cpp"]
 CLI_SRCS = ["openge_cli.cpp", "modules.cpp"]
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", f"-I{ROOT / 'include'}"]

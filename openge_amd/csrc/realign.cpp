@@ -1,0 +1,1279 @@
+// realign.cpp -- LocalRealignment host phases A, B, D, E (see realign.h).  Offset scoring (phase C)
+// goes through the ScanFn the caller binds (the HIP kernel in realign.hip).
+//
+// Every function below restates one reference routine; the citation names it (paths under
+// openge/src/).  Quirks the parity target depends on are reproduced and marked "Q<n>" after
+// SURVEY.md Appendix A.
+#include "realign.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <thread>
+#include <unordered_map>
+
+#include "bam_layout.h"
+
+namespace oge {
+
+// =====================================================================================  records
+static const char kSeqChars[] = "=ACMGRSVTWYHKDBN";
+static const char kCigChars[] = "MIDNSHP=X";
+
+std::string RRead::bases() const {
+    std::string s(l_seq, 'N');
+    for (uint32_t i = 0; i < l_seq; ++i) {
+        uint8_t b = (uint8_t)seq4[i >> 1];
+        s[i] = kSeqChars[(i & 1) ? (b & 0xF) : (b >> 4)];
+    }
+    return s;
+}
+
+std::string RRead::quals_ascii() const {
+    std::string q(qual);
+    for (auto &c : q) c = (char)(c + 33);  // BamAlignmentSupportData::getQual (BamAlignment.cpp:846-851)
+    return q;
+}
+
+static inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+
+bool rread_decode(const uint8_t *rec, RRead &r, std::string &err) {
+    uint32_t bs = rd32(rec);
+    if (bs < 32 || bs > 10000) {  // BamDeserializer::read rejects these (util/bam_deserializer.h:160-163)
+        err = "record block_size out of [32, 10000]";
+        return false;
+    }
+    r.ref = (int32_t)rd32(rec + OGE_OFF_REFID);
+    r.pos = (int32_t)rd32(rec + OGE_OFF_POS);
+    uint32_t lname = rec[OGE_OFF_LNAME];
+    r.mapq = rec[OGE_OFF_MAPQ];
+    uint32_t nc = oge_rd_u16(rec + OGE_OFF_NCIGAR);
+    r.flag = oge_rd_u16(rec + OGE_OFF_FLAG);
+    r.l_seq = rd32(rec + OGE_OFF_LSEQ);
+    r.mref = (int32_t)rd32(rec + OGE_OFF_MREFID);
+    r.mpos = (int32_t)rd32(rec + OGE_OFF_MPOS);
+    r.tlen = (int32_t)rd32(rec + OGE_OFF_TLEN);
+    uint64_t need = 32ull + lname + 4ull * nc + (r.l_seq + 1) / 2 + r.l_seq;
+    if (need > bs) {
+        err = "record fields overrun block_size";
+        return false;
+    }
+    const uint8_t *p = rec + OGE_OFF_NAME;
+    r.name.assign((const char *)p, lname ? lname - 1 : 0);
+    p += lname;
+    r.cigar.resize(nc);
+    for (uint32_t i = 0; i < nc; ++i) {
+        uint32_t op = rd32(p + 4 * i);
+        r.cigar[i].t = kCigChars[(op & 0xF) < 9 ? (op & 0xF) : 0];
+        r.cigar[i].n = op >> 4;
+    }
+    p += 4 * nc;
+    r.seq4.assign((const char *)p, (r.l_seq + 1) / 2);
+    p += (r.l_seq + 1) / 2;
+    r.qual.assign((const char *)p, r.l_seq);
+    p += r.l_seq;
+    r.tags.assign((const char *)p, (size_t)(rec + 4 + bs - p));
+    return true;
+}
+
+static uint32_t cig_code(char t) {
+    const char *q = strchr(kCigChars, t);
+    return q ? (uint32_t)(q - kCigChars) : 0;
+}
+
+// BamSerializer::write (util/bam_serializer.h:105-147): block size from the char data, bin
+// recomputed from pos and GetEndPosition (M, D, N, =, X).
+void rread_encode(const RRead &r, std::vector<uint8_t> &out) {
+    const uint32_t lname = (uint32_t)r.name.size() + 1;
+    const uint32_t nc = (uint32_t)r.cigar.size();
+    const uint32_t bs = 32 + lname + 4 * nc + (uint32_t)r.seq4.size() + (uint32_t)r.qual.size() + (uint32_t)r.tags.size();
+    int32_t end = r.pos;
+    for (auto &c : r.cigar)
+        if (c.t == 'M' || c.t == 'D' || c.t == 'N' || c.t == '=' || c.t == 'X') end += (int32_t)c.n;
+    const uint32_t bin = oge_reg2bin(r.pos, end);
+    size_t o = out.size();
+    out.resize(o + 4 + bs);
+    uint8_t *p = out.data() + o;
+    uint32_t core[9];
+    core[0] = bs;
+    core[1] = (uint32_t)r.ref;
+    core[2] = (uint32_t)r.pos;
+    core[3] = (bin << 16) | ((uint32_t)r.mapq << 8) | lname;
+    core[4] = ((uint32_t)r.flag << 16) | nc;
+    core[5] = r.l_seq;
+    core[6] = (uint32_t)r.mref;
+    core[7] = (uint32_t)r.mpos;
+    core[8] = (uint32_t)r.tlen;
+    memcpy(p, core, 36);
+    p += 36;
+    memcpy(p, r.name.data(), r.name.size());
+    p[r.name.size()] = 0;
+    p += lname;
+    for (uint32_t i = 0; i < nc; ++i) {
+        uint32_t op = (r.cigar[i].n << 4) | cig_code(r.cigar[i].t);
+        memcpy(p + 4 * i, &op, 4);
+    }
+    p += 4 * nc;
+    memcpy(p, r.seq4.data(), r.seq4.size());
+    p += r.seq4.size();
+    memcpy(p, r.qual.data(), r.qual.size());
+    p += r.qual.size();
+    memcpy(p, r.tags.data(), r.tags.size());
+}
+
+std::string cigar_to_string(const Cigar &c) {
+    std::string s;
+    for (auto &e : c) s += std::to_string(e.n) + e.t;
+    return s;
+}
+
+// =====================================================================================  tags
+// Walk of BamAlignment::FindTag / SkipToNextTag (util/bamtools/BamAlignment.cpp).
+static size_t tag_value_len(const std::string &t, size_t at /* index of the type byte */) {
+    char ty = t[at];
+    size_t v = at + 1;
+    switch (ty) {
+        case 'A': case 'c': case 'C': return 1;
+        case 's': case 'S': return 2;
+        case 'i': case 'I': case 'f': return 4;
+        case 'Z': case 'H': {
+            size_t e = t.find('\0', v);
+            return (e == std::string::npos ? t.size() : e + 1) - v;
+        }
+        case 'B': {
+            if (v + 5 > t.size()) return t.size() - v;
+            char sub = t[v];
+            uint32_t cnt;
+            memcpy(&cnt, t.data() + v + 1, 4);
+            size_t el = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+            return 5 + el * cnt;
+        }
+        default: return t.size() - v;  // unknown type: the rest (reference fails the parse)
+    }
+}
+
+bool tag_find(const std::string &t, const char *tag, size_t *at, size_t *len) {
+    size_t p = 0;
+    while (p + 3 <= t.size()) {
+        size_t vl = tag_value_len(t, p + 2);
+        if (t[p] == tag[0] && t[p + 1] == tag[1]) {
+            if (at) *at = p;
+            if (len) *len = 3 + vl;
+            return true;
+        }
+        p += 3 + vl;
+    }
+    return false;
+}
+
+bool tag_add_int(std::string &t, const char *tag, char type, int64_t v, int bytes) {
+    if (tag_find(t, tag, nullptr, nullptr)) return false;  // AddTag never overwrites (BamAlignment.h:305-310)
+    t.push_back(tag[0]);
+    t.push_back(tag[1]);
+    t.push_back(type);
+    uint64_t u = (uint64_t)v;
+    for (int i = 0; i < bytes; ++i) t.push_back((char)(u >> (8 * i)));
+    return true;
+}
+
+bool tag_add_string(std::string &t, const char *tag, const std::string &v) {
+    if (tag_find(t, tag, nullptr, nullptr)) return false;
+    t.push_back(tag[0]);
+    t.push_back(tag[1]);
+    t.push_back('Z');
+    t += v;
+    t.push_back('\0');
+    return true;
+}
+
+void tag_remove(std::string &t, const char *tag) {
+    size_t at, len;
+    if (tag_find(t, tag, &at, &len)) t.erase(at, len);
+}
+
+static bool tag_get_string(const std::string &t, const char *tag, std::string &v) {
+    size_t at, len;
+    if (!tag_find(t, tag, &at, &len) || t[at + 2] != 'Z') return false;
+    v.assign(t.data() + at + 3, len > 4 ? len - 4 : 0);
+    return true;
+}
+
+// EditTag(tag, "i", int): RemoveTag + AddTag, so the tag moves to the end (BamAlignment.h:463-469)
+static void tag_edit_i32(std::string &t, const char *tag, int32_t v) {
+    tag_remove(t, tag);
+    tag_add_int(t, tag, 'i', v, 4);
+}
+
+// =====================================================================================  FASTA
+// FastaReader (util/fasta_reader.cpp): sequences by name; readSequence(name, start, length) returns
+// the raw bytes (case preserved).
+struct Fasta {
+    std::unordered_map<std::string, std::string> seq;
+    bool load(const std::string &path, std::string &err) {
+        FILE *f = fopen(path.c_str(), "rb");
+        if (!f) {
+            err = "cannot open reference FASTA " + path;
+            return false;
+        }
+        std::string data;
+        char buf[1 << 16];
+        size_t k;
+        while ((k = fread(buf, 1, sizeof buf, f)) > 0) data.append(buf, k);
+        fclose(f);
+        size_t p = 0;
+        std::string *cur = nullptr;
+        while (p < data.size()) {
+            size_t e = data.find('\n', p);
+            if (e == std::string::npos) e = data.size();
+            if (data[p] == '>') {
+                size_t ne = p + 1;
+                while (ne < e && data[ne] != ' ' && data[ne] != '\t' && data[ne] != '\r') ++ne;
+                cur = &seq[data.substr(p + 1, ne - p - 1)];
+                cur->clear();
+            } else if (cur) {
+                size_t ee = e;
+                if (ee > p && data[ee - 1] == '\r') --ee;
+                cur->append(data, p, ee - p);
+            }
+            p = e + 1;
+        }
+        if (seq.empty()) {
+            err = "no sequences in reference FASTA " + path;
+            return false;
+        }
+        return true;
+    }
+    const std::string *get(const std::string &name) const {
+        auto it = seq.find(name);
+        return it == seq.end() ? nullptr : &it->second;
+    }
+};
+
+// =====================================================================================  GenomeLoc
+struct GLoc {
+    int contig = -1, start = 0, stop = 0;
+    bool is_before(const GLoc &o) const {  // GenomeLoc::isBefore (GenomeLoc.cpp:290-293)
+        return contig < o.contig || (contig == o.contig && stop < o.start);
+    }
+    bool overlaps(const GLoc &o) const {  // overlapsP = !disjointP (GenomeLoc.h:119-131)
+        return !(contig != o.contig || start > o.stop || o.start > stop);
+    }
+};
+
+// GenomeLocParser::createGenomeLoc(const OGERead&) (GenomeLocParser.cpp:377-400): length = l_seq
+// + D - I - S - H (N ignored, H subtracted although not in SEQ); stop = max(end - 1, pos).
+static GLoc read_loc(const RRead &r) {
+    int length = (int)r.l_seq;
+    for (auto &c : r.cigar) {
+        if (c.t == 'D') length += (int)c.n;
+        if (c.t == 'I') length -= (int)c.n;
+        if (c.t == 'S' || c.t == 'H') length -= (int)c.n;
+    }
+    int end = r.mapped() ? std::max(r.pos + length, r.pos) : r.pos;
+    GLoc g;
+    g.contig = r.ref;
+    g.start = r.pos;
+    g.stop = std::max(end - 1, r.pos);
+    return g;
+}
+
+// =====================================================================================  cigar utils
+static Cigar unclip_cigar(const Cigar &c) {  // LocalRealignment::unclipCigar (:1393-1403)
+    Cigar e;
+    for (auto &x : c)
+        if (!(x.t == 'S' || x.t == 'H' || x.t == 'P')) e.push_back(x);
+    return e;
+}
+static bool is_clip(const CigOp &x) { return x.t == 'S' || x.t == 'H' || x.t == 'P'; }
+
+// LocalRealignment::reclipCigar (:1409-1432), including its skip of one element after the
+// leading clips.
+static Cigar reclip_cigar(const Cigar &cigar, const RRead &read) {
+    Cigar e;
+    const Cigar &cd = read.cigar;
+    size_t i = 0, n = cd.size();
+    while (i < n && is_clip(cd[i])) e.push_back(cd[i++]);
+    e.insert(e.end(), cigar.begin(), cigar.end());
+    i++;
+    while (i < n && !is_clip(cd[i])) i++;
+    while (i < n && is_clip(cd[i])) e.push_back(cd[i++]);
+    return e;
+}
+
+// AlignmentUtils::createIndelString (AlignmentUtils.cpp:724-783).  `ok` = false stands for both the
+// empty-string and the NULL returns (Q26; the reference throws on the latter).
+static std::string create_indel_string(const Cigar &cigar, int idx, const std::string &ref, const std::string &rs,
+                                       int refIndex, int readIndex, bool &ok) {
+    ok = false;
+    const CigOp indel = cigar[idx];
+    int64_t indelLength = indel.n;
+    int64_t totalRefBases = 0;
+    for (int i = 0; i < idx; ++i) {
+        const CigOp &ce = cigar[i];
+        switch (ce.t) {
+            case 'M': readIndex += ce.n; refIndex += ce.n; totalRefBases += ce.n; break;
+            case 'S': readIndex += ce.n; break;
+            case 'N': refIndex += ce.n; totalRefBases += ce.n; break;
+            default: break;
+        }
+    }
+    const int64_t rsz = (int64_t)ref.size();
+    if (totalRefBases + indelLength > rsz) indelLength -= (totalRefBases + indelLength - rsz);
+    const int64_t altsz = rsz + (indel.t == 'D' ? -indelLength : indelLength);
+    if (altsz < 0 || refIndex < 0 || refIndex > altsz || refIndex > rsz) return std::string();
+    std::string alt((size_t)altsz, ' ');
+    memcpy(&alt[0], ref.data(), (size_t)refIndex);
+    int64_t cur = refIndex, ri = refIndex;
+    if (indel.t == 'D') {
+        ri += indelLength;
+    } else {
+        for (int64_t k = 0; k < indelLength; ++k)
+            alt[(size_t)(cur + k)] = (readIndex + k) < (int64_t)rs.size() ? rs[(size_t)(readIndex + k)] : '\0';
+        cur += indelLength;
+    }
+    // size_t arithmetic of the reference: refSeq.size() - refIndex > alt.size() - currentPos
+    if ((uint64_t)(rsz - ri) > (uint64_t)(altsz - cur)) return std::string();
+    if (ri < rsz) memcpy(&alt[(size_t)cur], ref.data() + ri, (size_t)(rsz - ri));
+    ok = true;
+    return alt;
+}
+
+static Cigar move_cigar_left(const Cigar &c, int idx) {  // AlignmentUtils::moveCigarLeft (:700-722)
+    Cigar e;
+    for (int i = 0; i < idx - 1; ++i) e.push_back(c[i]);
+    CigOp ce = c[idx - 1];
+    e.push_back({ce.t, ce.n - 1});
+    e.push_back(c[idx]);
+    if (idx + 1 < (int)c.size()) e.push_back({c[idx + 1].t, c[idx + 1].n + 1});
+    else e.push_back({'M', 1});
+    for (int i = idx + 2; i < (int)c.size(); ++i) e.push_back(c[i]);
+    return e;
+}
+
+static Cigar clean_up_cigar(const Cigar &c) {  // AlignmentUtils::cleanUpCigar (:687-698)
+    Cigar e;
+    for (auto &x : c)
+        if (x.n != 0 && (!e.empty() || x.t != 'D')) e.push_back(x);
+    return e;
+}
+
+// AlignmentUtils::leftAlignIndel (:632-677)
+static Cigar left_align_indel(Cigar cigar, const std::string &ref, const std::string &rs, int refIndex, int readIndex) {
+    int idx = -1;
+    for (int i = 0; i < (int)cigar.size(); ++i) {
+        if (cigar[i].t == 'D' || cigar[i].t == 'I') {
+            if (idx != -1) return cigar;
+            idx = i;
+        }
+    }
+    if (idx < 1) return cigar;
+    const int indelLength = (int)cigar[idx].n;
+    bool ok;
+    std::string alt = create_indel_string(cigar, idx, ref, rs, refIndex, readIndex, ok);
+    if (!ok || alt.empty()) return cigar;
+    Cigar nc = cigar;
+    for (int i = 0; i < indelLength; ++i) {
+        nc = move_cigar_left(nc, idx);
+        std::string na = create_indel_string(nc, idx, ref, rs, refIndex, readIndex, ok);
+        bool reachedEnd = false;
+        for (auto &x : nc)
+            if (x.n == 0) reachedEnd = true;
+        if (ok && alt == na) {
+            cigar = nc;
+            i = -1;
+            if (reachedEnd) cigar = clean_up_cigar(cigar);
+        }
+        if (reachedEnd) break;
+    }
+    return cigar;
+}
+
+// =====================================================================================  AlignedRead
+static inline bool is_regular(char b) {  // BaseUtils::isRegularBase (util/gatk/BaseUtils.h:49-57)
+    return b == 'A' || b == 'C' || b == 'G' || b == 'T' || b == 'a' || b == 'c' || b == 'g' || b == 't' || b == '*';
+}
+
+struct AlignedRead {
+    RRead *read;
+    std::string bases, quals;  // getUnclippedBases (:137-164): M and I of the ORIGINAL cigar
+    Cigar newCigar;
+    int newStart = -1;
+    int misRef = 0;
+    long aligner = 0;
+
+    explicit AlignedRead(RRead *r) : read(r) {
+        const std::string ab = r->bases(), aq = r->quals_ascii();
+        size_t from = 0;
+        for (auto &ce : r->cigar) {
+            if (ce.t == 'S') from += ce.n;
+            else if (ce.t == 'M' || ce.t == 'I') {
+                if (from < ab.size()) {
+                    bases.append(ab, from, ce.n);
+                    quals.append(aq, from, ce.n);
+                }
+                from += ce.n;
+            }
+        }
+    }
+    int read_length() const { return bases.empty() ? (int)read->l_seq : (int)bases.size(); }
+    const Cigar &cigar() const { return newCigar.empty() ? read->cigar : newCigar; }
+    size_t cigar_length() const {  // getCigarLength (local_realignment.h:251-269)
+        size_t len = 0;
+        for (auto &c : cigar())
+            if (!(c.t == 'H' || c.t == 'S' || c.t == 'D')) len += c.n;
+        return len;
+    }
+    int alignment_start() const { return newStart != -1 ? newStart : read->pos; }
+    // setCigar (:176-201)
+    void set_cigar(const Cigar &in, bool fixClipped = true) {
+        bool reclip = fixClipped && (int64_t)bases.size() < (int64_t)read->l_seq;
+        Cigar c = reclip ? reclip_cigar(in, *read) : in;
+        if (read->cigar == c) {
+            newCigar.clear();
+            return;
+        }
+        newCigar = c;
+    }
+};
+
+// mismatchQualitySumIgnoreCigar (:641-679) with quit = INT_MAX (the raw mismatch score)
+static int mismatch_sum_ignore_cigar(const AlignedRead &a, const std::string &ref, int refIndex) {
+    const std::string &rs = a.bases, &q = a.quals;
+    const int64_t L = (int64_t)rs.size(), R = (int64_t)ref.size();
+    int sum = 0;
+    for (int64_t i = 0; i < L; ++i) {
+        int64_t k = refIndex + i;
+        if (k >= R) {
+            sum += 99;  // MAX_QUAL
+            continue;
+        }
+        if (k < 0) continue;  // not reachable for reads inside their bin (Q26: defined behaviour)
+        char rc = ref[(size_t)k], bc = rs[(size_t)i];
+        if (!is_regular(bc) || !is_regular(rc)) continue;
+        if (bc != rc) sum += (int)(signed char)q[(size_t)i] - 33;
+    }
+    return sum;
+}
+
+// AlignmentUtils::getMismatchCount (AlignmentUtils.cpp:58-108), mismatchQualities only
+static long mismatching_qualities(const RRead &r, const std::string &ref, int refIndex) {
+    long mq = 0;
+    int readIdx = 0;
+    const int endOnRead = (int)r.l_seq - 1;
+    const std::string rs = r.bases(), qa = r.quals_ascii();
+    for (auto &ce : r.cigar) {
+        if (readIdx > endOnRead) break;
+        switch (ce.t) {
+            case 'M':
+                for (uint32_t j = 0; j < ce.n; ++j, ++refIndex, ++readIdx) {
+                    if (refIndex < 0 || refIndex >= (int)ref.size()) continue;
+                    if (readIdx > endOnRead) break;
+                    if (rs[readIdx] != ref[refIndex]) mq += (int)(signed char)qa[readIdx] - 33;
+                }
+                break;
+            case 'I': case 'S': readIdx += ce.n; break;
+            case 'D': case 'N': refIndex += ce.n; break;
+            default: break;  // H, P (and '='/'X', which the reference asserts on)
+        }
+    }
+    return mq;
+}
+
+struct Consensus {
+    std::string str;
+    Cigar cigar;
+    int pos = 0;
+    long sum = 0;
+    std::vector<std::pair<int, int>> readIndexes;
+};
+
+// createAlternateConsensus from a read (:1022-1088)
+static bool create_consensus(int indexOnRef, const Cigar &c, const std::string &ref, const std::string &readStr, Consensus &out) {
+    if (indexOnRef < 0) return false;
+    if (c.size() == 1 && c[0].t == 'M') return false;
+    std::string sb;
+    sb.reserve(ref.size() + 64);
+    sb.append(ref, 0, std::min<size_t>((size_t)indexOnRef, ref.size()));
+    Cigar el;
+    int indelCount = 0, altIdx = 0;
+    int64_t refIdx = indexOnRef;
+    bool ok = true;
+    for (auto &ce : c) {
+        const int64_t n = ce.n;
+        switch (ce.t) {
+            case 'D':
+                refIdx += n;
+                indelCount++;
+                el.push_back(ce);
+                break;
+            case 'M':
+                altIdx += (int)n;
+                // fall through
+            case 'N':
+                if ((int64_t)ref.size() < refIdx + n) ok = false;
+                else sb.append(ref, (size_t)refIdx, (size_t)n);
+                refIdx += n;
+                el.push_back({'M', (uint32_t)n});
+                break;
+            case 'I':
+                for (int64_t j = 0; j < n; ++j) {
+                    char b = (altIdx + j) < (int64_t)readStr.size() ? readStr[(size_t)(altIdx + j)] : '\0';
+                    if (!is_regular(b)) {
+                        ok = false;
+                        break;
+                    }
+                    sb.push_back(b);
+                }
+                altIdx += (int)n;
+                indelCount++;
+                el.push_back(ce);
+                break;
+            default: break;
+        }
+    }
+    if (!ok || indelCount != 1 || (int64_t)ref.size() < refIdx) return false;
+    sb.append(ref, (size_t)refIdx, std::string::npos);
+    out.str = sb;
+    out.cigar = el;
+    out.pos = indexOnRef;
+    return true;
+}
+
+// updateRead (:1166-1272)
+static bool update_read(const Cigar &alt, int altPosOnRef, int myPosOnAlt, AlignedRead &a, int leftmost) {
+    Cigar rc;
+    if (alt.size() == 1) {
+        a.newStart = leftmost + myPosOnAlt;
+        rc.push_back({'M', (uint32_t)a.read_length()});
+        a.set_cigar(rc);
+        return true;
+    }
+    CigOp e1 = alt[0], e2 = alt[1], indel{'M', 0};
+    int lead = 0;
+    if (e1.t == 'I') {
+        indel = e1;
+        if (e2.t != 'M') return false;
+    } else {
+        if (e1.t != 'M') return false;
+        if (e2.t == 'I' || e2.t == 'D') indel = e2;
+        else return false;
+        lead = (int)e1.n;
+    }
+    const int endOfFirst = altPosOnRef + lead;
+    bool saw = false;
+    const int rl = a.read_length();
+    if (myPosOnAlt < endOfFirst) {
+        a.newStart = leftmost + myPosOnAlt;
+        saw = true;
+        if (myPosOnAlt + rl <= endOfFirst) {
+            a.newCigar.clear();
+            return true;
+        }
+        rc.push_back({'M', (uint32_t)(endOfFirst - myPosOnAlt)});
+    }
+    if (indel.t == 'I') {
+        if (myPosOnAlt + rl < endOfFirst + (int)indel.n) {
+            int partial = myPosOnAlt + rl - endOfFirst;
+            if (!saw) partial = rl;
+            rc.push_back({'I', (uint32_t)partial});
+            a.set_cigar(rc);
+            return true;
+        }
+        if (!saw && myPosOnAlt < endOfFirst + (int)indel.n) {
+            a.newStart = leftmost + endOfFirst;
+            rc.push_back({'I', (uint32_t)((int)indel.n - (myPosOnAlt - endOfFirst))});
+            saw = true;
+        } else if (saw) {
+            rc.push_back(indel);
+        }
+    } else if (indel.t == 'D') {
+        if (saw) rc.push_back(indel);
+    }
+    if (!saw) {
+        a.newCigar.clear();
+        return true;
+    }
+    int remaining = (int)a.bases.size();
+    for (auto &ce : rc)
+        if (ce.t != 'D') remaining -= (int)ce.n;
+    if (remaining > 0) rc.push_back({'M', (uint32_t)remaining});
+    a.set_cigar(rc);
+    return true;
+}
+
+// alternateReducesEntropy (:1274-1391)
+static bool reduces_entropy(const std::vector<std::unique_ptr<AlignedRead>> &reads, const std::string &ref, int leftmost,
+                            double mismatchThreshold) {
+    const size_t n = ref.size();
+    std::vector<int> om(n, 0), cm(n, 0), to(n, 0), tc(n, 0);
+    for (auto &ap : reads) {
+        const AlignedRead &a = *ap;
+        int blocks = 0;
+        for (auto &c : a.read->cigar)
+            if (c.t == 'M' || c.t == '=' || c.t == 'X') blocks++;
+        if (blocks > 1) continue;
+        int refIdx = a.read->pos - leftmost;
+        const std::string &rs = a.bases, &q = a.quals;
+        for (size_t j = 0; j < rs.size(); ++j, ++refIdx) {
+            if (refIdx < 0 || refIdx >= (int)n) break;
+            int w = (int)(signed char)q[j] - 33;
+            to[refIdx] += w;
+            if (rs[j] != ref[refIdx]) om[refIdx] += w;
+        }
+        refIdx = a.alignment_start() - leftmost;
+        int altIdx = 0;
+        for (auto &ce : a.cigar()) {
+            switch (ce.t) {
+                case 'M':
+                    for (uint32_t k = 0; k < ce.n; ++k, ++refIdx, ++altIdx) {
+                        if (refIdx < 0 || refIdx >= (int)n) break;
+                        char qc = altIdx < (int)q.size() ? q[altIdx] : '\0';
+                        char bc = altIdx < (int)rs.size() ? rs[altIdx] : '\0';
+                        int w = (int)(signed char)qc - 33;
+                        tc[refIdx] += w;
+                        if (bc != ref[refIdx]) cm[refIdx] += w;
+                    }
+                    break;
+                case 'I': altIdx += (int)ce.n; break;
+                case 'D': refIdx += (int)ce.n; break;
+                default: break;
+            }
+        }
+    }
+    int oc = 0, cc = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (cm[i] == om[i]) continue;
+        if (om[i] > to[i] * mismatchThreshold) {
+            oc++;
+            if (tc[i] > 0 && ((double)cm[i] / (double)tc[i]) > ((double)om[i] / (double)to[i]) * (1.0 - 0.75)) cc++;
+        } else if (cm[i] > tc[i] * mismatchThreshold) {
+            cc++;
+        }
+    }
+    return oc == 0 || cc < oc;
+}
+
+static inline bool bases_equal(char l, char r) {  // SequenceUtil::basesEqual (SequenceUtil.cpp:91-99)
+    if (l == r) return true;
+    if (l > 90) l -= 32;
+    if (r > 90) r -= 32;
+    return l == r;
+}
+
+// SequenceUtil::calculateSamNmTag / sumQualitiesOfMismatches (SequenceUtil.cpp:134-228) over the
+// read's alignment blocks (getAlignmentBlocks :55-88).  UQ sums ASCII qualities (Q23).
+static void nm_uq(const RRead &r, const std::string &ref, int leftmost, int *nm, int *uq) {
+    const std::string rs = r.bases(), qa = r.quals_ascii();
+    int readBase = 0, refBase = r.pos - leftmost, mis = 0, qs = 0;
+    auto refc = [&](int k) -> char { return (k >= 0 && k < (int)ref.size()) ? ref[k] : '\0'; };
+    auto readc = [&](int k) -> char { return (k >= 0 && k < (int)rs.size()) ? rs[k] : '\0'; };
+    for (auto &e : r.cigar) {
+        switch (e.t) {
+            case 'S': case 'I': readBase += (int)e.n; break;
+            case 'N': case 'D': refBase += (int)e.n; break;
+            case 'M': case '=': case 'X':
+                for (uint32_t i = 0; i < e.n; ++i) {
+                    const int k = readBase + (int)i;
+                    if (!bases_equal(readc(k), refc(refBase + (int)i))) {
+                        mis++;
+                        qs += (int)(signed char)(k < (int)qa.size() ? qa[k] : 0);
+                    }
+                }
+                readBase += (int)e.n;
+                refBase += (int)e.n;
+                break;
+            default: break;
+        }
+    }
+    int ind = 0;
+    for (auto &e : r.cigar)
+        if (e.t == 'I' || e.t == 'D') ind += (int)e.n;
+    *nm = mis + ind;
+    *uq = qs;
+}
+
+// =====================================================================================  phase data
+struct IntervalData {
+    int interval = -1;                   // index into the interval list, -1 = invalid (None)
+    std::vector<RRead *> toClean, notToClean;
+    GLoc binLoc;                          // ReadBin::loc before padding
+    bool hasLoc = false;
+    // phase B/D results
+    std::string reference;
+    int leftmost = 0;
+    long totalRaw = 0;
+    std::vector<std::unique_ptr<AlignedRead>> alt;
+    std::vector<Consensus> cons;
+    uint64_t pairBase = 0;
+    std::vector<std::pair<RRead *, RRead>> pending;  // read -> updated copy (applied in phase E)
+    bool cleanable = false;
+};
+
+enum EvType { EV_READ, EV_CLEAN, EV_LIST };
+struct Event {
+    EvType t;
+    RRead *read;
+    IntervalData *id;
+};
+
+struct ByPos {  // Sort::ByPosition (util/bamtools/Sort.h:116-133); idx stands in for the address (Q10)
+    bool operator()(const RRead *a, const RRead *b) const {
+        if (a->ref == -1) return false;
+        if (b->ref == -1) return true;
+        if (a->ref != b->ref) return a->ref < b->ref;
+        if (a->pos != b->pos) return a->pos < b->pos;
+        if (a->rev() != b->rev()) return !a->rev();
+        if (a->name != b->name) return a->name < b->name;
+        if (a->flag != b->flag) return a->flag < b->flag;
+        return a->idx < b->idx;
+    }
+};
+
+// =====================================================================================  phase E
+// ConstrainedMateFixingManager (util/gatk/ConstrainedMateFixingManager.cpp), run in stream order.
+class MateFixer {
+public:
+    MateFixer(const RealignParams &P, std::vector<RRead *> &out) : P_(P), out_(out) {}
+
+    // canMoveReads (:245-251)
+    bool can_move(const GLoc &earliest) const {
+        return !hasLast_ || last_.contig != earliest.contig ||
+               std::abs(last_.start - earliest.start) > P_.max_isize_for_movement;
+    }
+
+    void add(RRead *nr, bool modified, bool canFlush) {  // addReadInternal (:312-419)
+        const bool tooMany = waiting_.size() >= (size_t)P_.max_records_in_memory;
+        if ((canFlush && tooMany) || (!waiting_.empty() && (*waiting_.begin())->ref != nr->ref)) {
+            while (waiting_.size() > 1) write(pop());
+            RRead *last = pop();
+            if (last->ref == -1) {
+                hasLast_ = false;
+            } else {
+                hasLast_ = true;
+                last_ = read_loc(*last);
+            }
+            write(last);
+            if (!tooMany) mates_.clear();
+            else purge_unmodified();
+        }
+        if (nr->paired()) {
+            auto it = mates_.find(nr->name);
+            if (it != mates_.end()) {
+                RRead *mate = it->second.first;
+                bool doNotFix = !nr->mapped() && (!mate->mapped() || !waiting_.count(mate));
+                if (!doNotFix) {
+                    bool requeue = !mate->mapped() && nr->mapped();
+                    if (requeue && waiting_.erase(mate) == 0) requeue = false;
+                    set_mate_info(*mate, *nr);
+                    if (requeue) waiting_.insert(mate);
+                }
+                mates_.erase(it);
+            } else if (movable(*nr)) {
+                mates_[nr->name] = std::make_pair(nr, modified);
+            }
+        }
+        waiting_.insert(nr);
+        if (++counter_ % 1000 == 0) {  // EMIT_FREQUENCY (ConstrainedMateFixingManager.h:66)
+            while (!waiting_.empty()) {
+                RRead *r = *waiting_.begin();
+                if (cannot_move_before(r->pos, *nr) && (!movable(*r) || cannot_move_before(r->mpos, *nr))) {
+                    mates_.erase(r->name);
+                    write(pop());
+                } else {
+                    break;
+                }
+            }
+        }
+    }
+
+    void close() {
+        while (!waiting_.empty()) write(pop());
+    }
+
+private:
+    bool cannot_move_before(int pos, const RRead &added) const {  // noReadCanMoveBefore (:253-255)
+        return pos + 2 * P_.max_pos_move_allowed < added.pos;
+    }
+    bool too_big(const RRead &r) const {  // iSizeTooBigToMove (:433-436): query length used as isize (Q22)
+        return (r.paired() && r.mapped() && r.ref != r.mref) || std::abs((int)r.l_seq) > P_.max_isize_for_movement;
+    }
+    bool movable(const RRead &r) const {  // pairedReadIsMovable (:449-454)
+        return r.paired() && (r.mapped() || r.mate_mapped()) && !too_big(r);
+    }
+    RRead *pop() {
+        auto it = waiting_.begin();
+        RRead *r = *it;
+        waiting_.erase(it);
+        return r;
+    }
+    void write(RRead *r) { out_.push_back(r); }
+    void purge_unmodified() {
+        for (auto it = mates_.begin(); it != mates_.end();) {
+            if (!it->second.second) it = mates_.erase(it);
+            else ++it;
+        }
+    }
+    static int end_position(const RRead &r) {  // getEndPosition (:100-120)
+        int len = 0;
+        for (auto &c : r.cigar)
+            if (c.t == 'M' || c.t == 'D' || c.t == 'N' || c.t == '=' || c.t == 'X') len += (int)c.n;
+        return r.pos + len - 1;
+    }
+    static int insert_size(const RRead &a, const RRead &b) {  // computeInsertSize (:125-141)
+        if (!a.mapped() || !b.mapped()) return 0;
+        if ((a.ref == 0 ? 1 : 0) == b.ref) return 0;  // `!firstEnd.getRefID() == secondEnd.getRefID()` (Q22)
+        const int p1 = a.rev() ? end_position(a) : a.pos;
+        const int p2 = b.rev() ? end_position(b) : b.pos;
+        return p2 - p1 + ((p2 >= p1) ? 1 : -1);
+    }
+    static void set_flag(RRead &r, uint16_t bit, bool on) { r.flag = on ? (r.flag | bit) : (r.flag & ~bit); }
+    static void set_mate_info(RRead &r1, RRead &r2) {  // setMateInfo (:143-201)
+        if (r1.mapped() && r2.mapped()) {
+            r1.mref = r2.mref;  // Q22: the mate's mate reference, not its reference
+            r1.mpos = r2.pos;
+            set_flag(r1, 0x20, r2.rev());
+            set_flag(r1, 0x8, false);
+            tag_add_int(r1.tags, "MQ", 'S', r2.mapq, 2);
+            r2.mref = r1.ref;
+            r2.mpos = r1.pos;
+            set_flag(r2, 0x20, r1.rev());
+            set_flag(r2, 0x8, false);
+            tag_add_int(r2.tags, "MQ", 'S', r1.mapq, 2);
+        } else if (!r1.mapped() && !r2.mapped()) {
+            r1.ref = -1; r1.pos = -1; r1.mref = -1; r1.mpos = -1;
+            set_flag(r1, 0x20, r2.rev());
+            set_flag(r1, 0x8, true);
+            tag_remove(r2.tags, "MQ");
+            r2.ref = -1; r2.pos = -1; r2.mref = -1; r2.mpos = -1;
+            set_flag(r2, 0x20, r1.rev());
+            set_flag(r2, 0x8, false);
+            tag_remove(r2.tags, "MQ");
+        } else {
+            RRead &m = r1.mapped() ? r1 : r2;
+            RRead &u = r1.mapped() ? r2 : r1;
+            u.ref = m.ref;
+            u.pos = m.pos;
+            m.mref = u.ref;
+            m.mpos = u.pos;
+            set_flag(m, 0x20, u.rev());
+            set_flag(m, 0x8, true);
+            u.mref = m.ref;
+            u.mpos = m.pos;
+            set_flag(u, 0x20, m.rev());
+            set_flag(u, 0x8, false);
+        }
+        int is = insert_size(r1, r2);
+        if (is > 0) is--;
+        if (is < 0) is++;
+        r1.tlen = is;
+        r2.tlen = -is;
+    }
+
+    const RealignParams &P_;
+    std::vector<RRead *> &out_;
+    std::multiset<RRead *, ByPos> waiting_;
+    std::map<std::string, std::pair<RRead *, bool>> mates_;
+    GLoc last_;
+    bool hasLast_ = false;
+    uint64_t counter_ = 0;
+};
+
+// =====================================================================================  driver
+template <class F>
+static void par_for(size_t n, int threads, F f) {
+    if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+    threads = (int)std::min<size_t>((size_t)threads, std::max<size_t>(1, n));
+    if (threads <= 1) {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<size_t> next(0);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t)
+        ts.emplace_back([&]() {
+            for (;;) {
+                size_t i = next.fetch_add(1);
+                if (i >= n) break;
+                f(i);
+            }
+        });
+    for (auto &t : ts) t.join();
+}
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// GenomeLocParser::parseGenomeLoc (GenomeLocParser.cpp:274-328): "contig:start[-stop]", 1-based.
+static bool parse_intervals(const std::string &path, const std::vector<std::string> &names, std::vector<GLoc> &out,
+                            std::string &err) {
+    std::ifstream f(path);
+    if (!f) {
+        err = "cannot open intervals file " + path;
+        return false;
+    }
+    std::unordered_map<std::string, int> idx;
+    for (size_t i = 0; i < names.size(); ++i) idx[names[i]] = (int)i;
+    std::string line;
+    while (std::getline(f, line)) {
+        if (line.empty()) break;  // the reference stops at the first empty line (:326-331)
+        size_t colon = line.find(':');
+        if (colon == std::string::npos) {
+            err = "Could not find colon in interval file: " + line;
+            return false;
+        }
+        size_t hy = line.find('-');
+        std::string contig = line.substr(0, std::min(colon, hy));
+        GLoc g;
+        g.start = (int)strtol(line.c_str() + colon + 1, nullptr, 10) - 1;
+        g.stop = g.start;
+        if (hy != std::string::npos) g.stop = (int)strtol(line.c_str() + hy + 1, nullptr, 10) - 1;
+        auto it = idx.find(contig);
+        if (it == idx.end()) {
+            err = "Contig '" + contig + "' does not match any contig in the sequence dictionary";
+            return false;
+        }
+        g.contig = it->second;
+        out.push_back(g);
+    }
+    if (out.empty()) {
+        err = "Error parsing intervals file. Aborting.";
+        return false;
+    }
+    return true;
+}
+
+// doNotTryToClean (:555-575)
+static bool do_not_clean(const RRead &r, const RealignParams &P) {
+    std::string rg;
+    bool is454 = tag_get_string(r.tags, "RG", rg) && rg.find("454") != std::string::npos;
+    bool tooBig = (r.paired() && r.mapped() && r.ref != r.mref) || std::abs((int)r.l_seq) > P.max_isize_for_movement;
+    return !r.mapped() || (r.flag & 0x100) || (r.flag & 0x200) || r.mapq == 0 || r.pos == -1 || tooBig || is454;
+}
+
+int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, const uint64_t *offs, uint64_t n,
+                const std::string &fasta_path, const std::string &intervals_path, const RealignParams &P, const ScanFn &scan,
+                std::vector<uint8_t> &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err) {
+    double t0 = now_s();
+    Fasta fa;
+    if (!fa.load(fasta_path, err)) return -4;
+    std::vector<GLoc> ivs;
+    if (!parse_intervals(intervals_path, ref_names, ivs, err)) return -1;
+    st.intervals = ivs.size();
+
+    std::vector<RRead> reads(n);
+    std::atomic<bool> bad(false);
+    std::mutex emu;
+    std::string derr;
+    par_for(n, P.threads, [&](size_t i) {
+        std::string e;
+        if (!rread_decode(recs + offs[i], reads[i], e)) {
+            std::lock_guard<std::mutex> g(emu);
+            bad = true;
+            derr = e;
+        }
+        reads[i].idx = (uint32_t)i;
+    });
+    if (bad) {
+        err = derr;
+        return -1;
+    }
+    uint64_t in_bytes = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        in_bytes += 4 + rd32(recs + offs[i]);
+        if (reads[i].ref < -1 || reads[i].ref >= (int)ref_names.size()) {
+            err = "record refID outside the sequence dictionary";
+            return -1;
+        }
+    }
+
+    // ---------------------------------------------------------------- A: map_func (:455-553)
+    std::vector<std::unique_ptr<IntervalData>> ids;
+    std::vector<Event> ev;
+    auto new_id = [&](int interval) {
+        ids.emplace_back(new IntervalData());
+        ids.back()->interval = interval;
+        return ids.back().get();
+    };
+    size_t it = 0;
+    IntervalData *loading = new_id(ivs.empty() ? -1 : 0);
+    bool saw = false;
+    auto bin_add = [&](IntervalData *d, RRead *r) {  // ReadBin::add (:263-275)
+        GLoc l = read_loc(*r);
+        if (!d->hasLoc) {
+            d->binLoc = l;
+            d->hasLoc = true;
+        } else if (l.stop > d->binLoc.stop) {
+            d->binLoc.stop = l.stop;
+        }
+        d->toClean.push_back(r);
+    };
+    std::function<void(RRead *)> map_func = [&](RRead *r) {
+        if (loading->interval < 0) {
+            ev.push_back({EV_READ, r, loading});
+            loading = new_id(-1);
+            return;
+        }
+        if (r->ref == -1) {
+            ev.push_back({EV_CLEAN, nullptr, loading});
+            it = ivs.size();
+            loading = new_id(-1);
+            saw = false;
+            map_func(r);
+            return;
+        }
+        GLoc rl = read_loc(*r);
+        if (rl.stop == 0) rl.stop = rl.start;
+        const GLoc &cur = ivs[loading->interval];
+        if (rl.is_before(cur)) {
+            if (!saw) ev.push_back({EV_READ, r, loading});
+            else loading->notToClean.push_back(r);
+        } else if (rl.overlaps(cur)) {
+            saw = true;
+            if (do_not_clean(*r, P)) loading->notToClean.push_back(r);
+            else bin_add(loading, r);
+            if ((int)(loading->toClean.size() + loading->notToClean.size()) >= P.max_reads) {
+                ev.push_back({EV_LIST, nullptr, loading});
+                ++it;
+                loading = new_id(it < ivs.size() ? (int)it : -1);
+                saw = false;
+            }
+        } else {
+            ev.push_back({EV_CLEAN, nullptr, loading});
+            do {
+                ++it;
+            } while (it < ivs.size() && ivs[it].is_before(rl));
+            loading = new_id(it < ivs.size() ? (int)it : -1);
+            saw = false;
+            map_func(r);
+        }
+    };
+    for (uint64_t i = 0; i < n; ++i) map_func(&reads[i]);
+    // onTraversalDone (:577-607)
+    if (!loading->toClean.empty()) ev.push_back({EV_CLEAN, nullptr, loading});
+    else if (!loading->notToClean.empty()) ev.push_back({EV_LIST, nullptr, loading});
+    double t1 = now_s();
+    st.t_bin = t1 - t0;
+
+    // ---------------------------------------------------------------- B: prepare (:681-700, :918-999)
+    std::vector<IntervalData *> work;
+    for (auto &e : ev)
+        if (e.t == EV_CLEAN && !e.id->toClean.empty()) work.push_back(e.id);
+    std::atomic<bool> ferr(false);
+    std::string fmsg;
+    par_for(work.size(), P.threads, [&](size_t w) {
+        IntervalData &d = *work[w];
+        const std::string &contig = ref_names[d.binLoc.contig];
+        const std::string *seq = fa.get(contig);
+        // ReadBin::getReference (:277-293): pad 30, clamp, upper-case
+        int padLeft = std::max(d.binLoc.start - 30, 0);
+        int padRight = seq ? std::min(d.binLoc.stop + 30, (int)seq->size() - 1) : -1;
+        if (!seq || padRight < padLeft) {
+            std::lock_guard<std::mutex> g(emu);
+            ferr = true;
+            fmsg = seq ? "Requested FASTA read beyond end of sequence " + contig : "Sequence " + contig + " not found in FASTA";
+            return;
+        }
+        d.reference = seq->substr((size_t)padLeft, (size_t)(padRight - padLeft + 1));
+        for (auto &c : d.reference) c = (char)toupper((unsigned char)c);
+        d.leftmost = padLeft;
+        const std::string &ref = d.reference;
+        for (RRead *r : d.toClean) {
+            if (r->cigar.empty()) continue;  // refReads
+            std::unique_ptr<AlignedRead> a(new AlignedRead(r));
+            int blocks = 0;
+            for (auto &c : r->cigar)
+                if (c.t == 'M' || c.t == '=' || c.t == 'X') blocks++;
+            if (blocks == 2) {
+                Cigar nc = left_align_indel(unclip_cigar(r->cigar), ref, r->bases(), r->pos - d.leftmost, 0);
+                a->set_cigar(nc, false);
+            }
+            const int startOnRef = r->pos - d.leftmost;
+            const int raw = mismatch_sum_ignore_cigar(*a, ref, startOnRef);
+            if (raw > 0) {
+                if (!r->dup()) d.totalRaw += raw;
+                a->misRef = raw;
+                a->aligner = mismatching_qualities(*r, ref, startOnRef);
+                if (blocks == 2) {
+                    Consensus c;
+                    if (create_consensus(startOnRef, a->cigar(), ref, a->bases, c)) {
+                        bool exists = false;
+                        for (auto &o : d.cons)
+                            if (o.str == c.str) exists = true;
+                        if (!exists) d.cons.push_back(std::move(c));
+                    }
+                }
+                d.alt.push_back(std::move(a));
+            }
+        }
+    });
+    if (ferr) {
+        err = fmsg;
+        return -4;
+    }
+    double t2 = now_s();
+    st.t_prepare = t2 - t1;
+
+    // ---------------------------------------------------------------- C: offset scan (GPU)
+    ScanBatch B;
+    B.cons_off.push_back(0);
+    B.read_off.push_back(0);
+    for (IntervalData *d : work) {
+        if (d->cons.empty()) continue;
+        const uint32_t c0 = (uint32_t)(B.cons_off.size() - 1), r0 = (uint32_t)(B.read_off.size() - 1);
+        d->pairBase = B.pairs.size();
+        for (auto &c : d->cons) {
+            B.cons.insert(B.cons.end(), c.str.begin(), c.str.end());
+            B.cons_off.push_back(B.cons.size());
+        }
+        for (auto &a : d->alt) {
+            B.bases.insert(B.bases.end(), a->bases.begin(), a->bases.end());
+            for (char q : a->quals) B.quals.push_back((uint8_t)(q - 33));
+            B.read_off.push_back(B.bases.size());
+        }
+        for (uint32_t ci = 0; ci < d->cons.size(); ++ci) {
+            const int consLen = (int)d->cons[ci].str.size();
+            for (uint32_t j = 0; j < d->alt.size(); ++j) {
+                const AlignedRead &a = *d->alt[j];
+                ScanPair sp;
+                sp.cons = c0 + ci;
+                sp.read = r0 + j;
+                sp.orig = a.read->pos - d->leftmost;
+                sp.max_start = consLen - (int)a.cigar_length();
+                B.pairs.push_back(sp);
+                const int offsets = std::max(sp.orig, sp.max_start) + 1;
+                st.scan_ops += (uint64_t)std::max(offsets, 0) * a.bases.size();
+            }
+        }
+    }
+    st.scan_pairs = B.pairs.size();
+    std::vector<int32_t> bidx, bscore;
+    if (!B.pairs.empty()) {
+        int rc = scan(B, bidx, bscore);
+        if (rc) {
+            err = "offset scan failed";
+            return rc;
+        }
+    }
+    double t3 = now_s();
+    st.t_scan = t3 - t2;
+
+    // ---------------------------------------------------------------- D: decide (:713-892)
+    par_for(work.size(), P.threads, [&](size_t w) {
+        IntervalData &d = *work[w];
+        if (d.cons.empty()) return;
+        Consensus *best = nullptr;
+        uint64_t pi = d.pairBase;
+        for (auto &c : d.cons) {  // deterministic consensus order (Q19: the reference shuffles)
+            c.sum = 0;
+            for (size_t j = 0; j < d.alt.size(); ++j, ++pi) {
+                AlignedRead &a = *d.alt[j];
+                int my = bscore[pi];
+                if (my > a.aligner || my >= a.misRef) my = a.misRef;
+                else c.readIndexes.push_back(std::make_pair((int)j, (int)bidx[pi]));
+                if (!a.read->dup()) c.sum += my;
+            }
+            if (!best || best->sum > c.sum) best = &c;  // first strictly smaller sum (:764)
+        }
+        const double improvement = best ? (double)(d.totalRaw - best->sum) / 10.0 : -1;
+        if (!(improvement >= P.lod_threshold)) return;
+        best->cigar = left_align_indel(best->cigar, d.reference, best->str, best->pos, best->pos);
+        for (auto &ip : best->readIndexes)
+            if (!update_read(best->cigar, best->pos, ip.second, *d.alt[ip.first], d.leftmost)) return;
+        if (!reduces_entropy(d.alt, d.reference, d.leftmost, P.mismatch_threshold)) return;
+        std::string reference = d.reference;
+        int leftmost = d.leftmost;
+        const std::string &contig = ref_names[ivs[d.interval].contig];
+        const std::string *fseq = fa.get(contig);
+        for (auto &ip : best->readIndexes) {
+            AlignedRead &a = *d.alt[ip.first];
+            // constizeUpdate (:218-241)
+            if (a.newCigar.empty()) continue;
+            RRead u = *a.read;
+            int ns = a.newStart == -1 ? u.pos : a.newStart;
+            if (a.newStart != -1 && std::abs(a.newStart - u.pos) > P.max_pos_move_allowed) continue;
+            if (!P.no_original_alignment_tags) {
+                tag_add_string(u.tags, "OC", cigar_to_string(u.cigar));
+                if (ns != u.pos) tag_add_int(u.tags, "OP", 'i', u.pos + 1, 4);
+            }
+            u.cigar = a.newCigar;
+            u.pos = ns;
+            if (u.mapq != 255) u.mapq = (uint16_t)std::min((int)u.mapq + 10, 254);
+            // reference refetch for the tag fix-ups (:864-872); the refetched bases keep their case
+            int64_t needL = (int64_t)leftmost - u.pos;
+            int64_t needR = (int64_t)u.pos + (int64_t)u.l_seq - leftmost - (int64_t)reference.size() + 1;
+            int needed = (int)std::max(needL, needR);
+            if (needed > 0 && fseq) {
+                int padLeft = std::max(leftmost - needed, 1);
+                int64_t padRight =
+                    std::min<int64_t>((int64_t)leftmost + (int64_t)reference.size() + needed, (int64_t)fseq->size());
+                reference = fseq->substr((size_t)padLeft, (size_t)std::max<int64_t>(0, padRight - padLeft));
+                leftmost = padLeft;
+            }
+            int nm, uq;
+            nm_uq(u, reference, leftmost, &nm, &uq);
+            if (tag_find(u.tags, "NM", nullptr, nullptr)) tag_edit_i32(u.tags, "NM", nm);
+            if (tag_find(u.tags, "UQ", nullptr, nullptr)) tag_edit_i32(u.tags, "UQ", uq);
+            tag_remove(u.tags, "MD");
+            d.pending.push_back(std::make_pair(a.read, std::move(u)));
+        }
+        d.cleanable = true;
+    });
+    double t4 = now_s();
+    st.t_decide = t4 - t3;
+
+    // ---------------------------------------------------------------- E: emit + mate fixing
+    std::vector<RRead *> order;
+    order.reserve(n);
+    MateFixer mf(P, order);
+    std::set<RRead *> cleaned;
+    for (auto &e : ev) {
+        if (e.t == EV_READ) {
+            mf.add(e.read, false, true);
+            continue;
+        }
+        IntervalData &d = *e.id;
+        cleaned.clear();
+        if (e.t == EV_CLEAN && !d.toClean.empty()) {
+            // CleanAndEmitReadList::runJob (:435-453): clean only if the writer allows moves here
+            if (mf.can_move(read_loc(*d.toClean[0])) && d.cleanable) {
+                st.intervals_cleaned++;
+                for (auto &pu : d.pending) {
+                    *pu.first = std::move(pu.second);
+                    cleaned.insert(pu.first);
+                }
+                st.reads_realigned += d.pending.size();
+            }
+        }
+        // emitReadLists (:370-376)
+        std::vector<RRead *> lst = d.notToClean;
+        lst.insert(lst.end(), d.toClean.begin(), d.toClean.end());
+        std::stable_sort(lst.begin(), lst.end(), ByPos());
+        for (RRead *r : lst) mf.add(r, cleaned.count(r) > 0, false);
+    }
+    mf.close();
+    if (order.size() != n) {
+        err = "internal: emitted " + std::to_string(order.size()) + " of " + std::to_string(n) + " records";
+        return -1;
+    }
+    out.reserve(out.size() + in_bytes + n * 16);
+    for (RRead *r : order) {
+        out_off.push_back(out.size());
+        rread_encode(*r, out);
+    }
+    out_off.push_back(out.size());
+    st.t_emit = now_s() - t4;
+    return 0;
+}
+
+}  // namespace oge

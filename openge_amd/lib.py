@@ -40,6 +40,56 @@ class MarkdupOpts(C.Structure):
     ]
 
 
+class RealignSynthParams(C.Structure):
+    """Mirror of oge_realign_synth_params (include/openge_hip.h)."""
+
+    _fields_ = [("seed", C.c_uint64)] + [(k, C.c_uint32) for k in (
+        "n_ref", "n_intervals", "spacing", "read_len", "frags_per_interval", "qual_min", "qual_max", "ins_min", "ins_max",
+        "err_ppm", "noindel_ppm", "gapped_ppm", "alt_indel_ppm", "dup_ppm", "mapq0_ppm", "clip_ppm", "lower_ppm", "n_ppm",
+        "md_ppm", "uq_ppm")]
+
+
+class RealignOpts(C.Structure):
+    """Mirror of oge_realign_opts (include/openge_hip.h)."""
+
+    _fields_ = [("lod_threshold", C.c_double), ("mismatch_threshold", C.c_double)] + [(k, C.c_int32) for k in (
+        "max_records_in_memory", "max_isize_for_movement", "max_pos_move_allowed", "max_reads",
+        "no_original_alignment_tags", "threads")]
+
+
+class RealignScanBatch(C.Structure):
+    """Mirror of oge_realign_scan_batch (include/openge_hip.h)."""
+
+    _fields_ = [("cons", C.c_void_p), ("cons_bytes", C.c_uint64), ("cons_off", C.c_void_p), ("n_cons", C.c_uint32),
+                ("n_reads", C.c_uint32), ("bases", C.c_void_p), ("quals", C.c_void_p), ("read_bytes", C.c_uint64),
+                ("read_off", C.c_void_p), ("pairs", C.c_void_p), ("n_pairs", C.c_uint64)]
+
+
+def realign_synth_params(**over) -> RealignSynthParams:
+    """C5-shaped realignment data set parameters (defaults: 50k intervals on 24 contigs)."""
+    p = RealignSynthParams()
+    lib().oge_realign_synth_defaults(C.byref(p))
+    for k, v in over.items():
+        setattr(p, k, v)
+    return p
+
+
+def synth_realign(p: RealignSynthParams, directory, level: int = 6, threads: int = 8) -> tuple[str, str, str]:
+    """Write ref.fa (+ .fai), targets.intervals and reads.bam into `directory`; returns their paths."""
+    d = Path(directory)
+    fa, iv, bam = str(d / "ref.fa"), str(d / "targets.intervals"), str(d / "reads.bam")
+    check(lib().oge_synth_realign(C.byref(p), fa.encode(), iv.encode(), bam.encode(), level, threads))
+    return fa, iv, bam
+
+
+def realign_opts(**over) -> RealignOpts:
+    o = RealignOpts()
+    lib().oge_realign_opts_init(C.byref(o))
+    for k, v in over.items():
+        setattr(o, k, v)
+    return o
+
+
 # GRCh38 primary-assembly lengths chr1..22, X, Y (Mbp, rounded) -- relative contig sizes of C2.
 GRCH38_MB = [248.96, 242.19, 198.30, 190.21, 181.54, 170.81, 159.35, 145.14, 138.39, 133.80, 135.09, 133.28,
              114.36, 107.04, 101.99, 90.34, 83.26, 80.37, 58.62, 64.44, 46.71, 50.82, 156.04, 57.23]
@@ -136,6 +186,16 @@ def lib() -> C.CDLL:
         "oge_bam_header_text": (C.c_int, [vp, vp, u64, C.POINTER(u64)]),
         "oge_bam_markdup_opts": (C.c_int, [vp, vp, C.POINTER(vp), C.POINTER(vp)]),
         "oge_bam_write": (C.c_int, [C.c_char_p, C.c_char_p, u64, C.c_int, vp, vp, u64, vp, vp, C.c_int, C.c_int]),
+        "oge_realign_scan": (C.c_int, [vp, vp, vp, vp]),
+        "oge_realign_opts_init": (None, [vp]),
+        "oge_localrealign": (C.c_int, [vp, C.c_char_p, u64, vp, vp, u64, C.c_char_p, C.c_char_p, vp, C.POINTER(vp)]),
+        "oge_realign_result_count": (u64, [vp]),
+        "oge_realign_result_records": (vp, [vp, C.POINTER(u64)]),
+        "oge_realign_result_offsets": (vp, [vp]),
+        "oge_realign_result_stats": (C.c_char_p, [vp]),
+        "oge_realign_result_free": (None, [vp]),
+        "oge_realign_synth_defaults": (None, [vp]),
+        "oge_synth_realign": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)
@@ -316,6 +376,38 @@ class Context:
         check(lib().oge_sort_markdup_dev(self.h, d_recs, d_off, n, C.byref(opts), d_perm, d_out, d_out_off,
                                          C.byref(nd)), self.h)
         return nd.value
+
+    def realign_scan(self, cons: np.ndarray, cons_off: np.ndarray, bases: np.ndarray, quals: np.ndarray,
+                     read_off: np.ndarray, pairs: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """findBestOffset for every (consensus, read) pair -> (best_index, best_score)."""
+        pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 4)
+        n = len(pairs)
+        b = RealignScanBatch(_ptr(cons), cons.nbytes, _ptr(cons_off), len(cons_off) - 1, len(read_off) - 1, _ptr(bases),
+                             _ptr(quals), bases.nbytes, _ptr(read_off), _ptr(pairs), n)
+        bi, bs = np.empty(max(n, 1), np.int32), np.empty(max(n, 1), np.int32)
+        check(lib().oge_realign_scan(self.h, C.byref(b), _ptr(bi), _ptr(bs)), self.h)
+        return bi[:n], bs[:n]
+
+    def localrealign(self, header_text: str, recs: np.ndarray, offs: np.ndarray, n: int, fasta: str, intervals: str,
+                     opts: RealignOpts | None = None) -> tuple[np.ndarray, np.ndarray, dict]:
+        """LocalRealignment over coordinate-sorted records -> (out recs, out offsets[n+1], stats)."""
+        import json
+        L = lib()
+        hb = header_text.encode()
+        res = C.c_void_p()
+        check(L.oge_localrealign(self.h, hb, len(hb), _ptr(recs), _ptr(offs), n, fasta.encode(), intervals.encode(),
+                                 C.byref(opts) if opts is not None else None, C.byref(res)), self.h)
+        try:
+            cnt = int(L.oge_realign_result_count(res))
+            nb = C.c_uint64()
+            rp = L.oge_realign_result_records(res, C.byref(nb))
+            out = np.ctypeslib.as_array((C.c_uint8 * nb.value).from_address(rp)).copy() if nb.value else np.zeros(0, np.uint8)
+            op = L.oge_realign_result_offsets(res)
+            oo = np.ctypeslib.as_array((C.c_uint64 * (cnt + 1)).from_address(op)).copy()
+            stats = json.loads(L.oge_realign_result_stats(res).decode())
+        finally:
+            L.oge_realign_result_free(res)
+        return out, oo, stats
 
     def synth_dev(self, p: SynthParams, d_offs: int, d_out: int | None) -> None:
         L = lib()

@@ -1,7 +1,8 @@
 """TEST INFRASTRUCTURE ONLY -- CPU oracle for the openge_amd parity tests.
 
-`oge_oracle.c` restates the reference's coordinate sort order (util/bamtools/Sort.h:116-133) and
-MarkDuplicates (algorithms/mark_duplicates.cpp:185-540) in plain C.  Only tests/, the smoke check
+`oge_oracle.c` restates the reference's coordinate sort order (util/bamtools/Sort.h:116-133),
+MarkDuplicates (algorithms/mark_duplicates.cpp:185-540) and the local-realignment offset scan
+(findBestOffset, algorithms/local_realignment.cpp:641-679,1126-1164) in plain C.  Only tests/, the smoke check
 in __graft_entry__ and bench.py's cpu_baseline leg may use this package, and only as the checker
 or the timed CPU baseline -- never as the thing measured or shipped.
 
@@ -47,6 +48,8 @@ def _L():
         L = C.CDLL(str(SO))
         L.oracle_sort_perm.restype = C.c_int
         L.oracle_sort_perm.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.oracle_realign_scan.restype = C.c_int
+        L.oracle_realign_scan.argtypes = [C.c_void_p] * 6 + [C.c_uint64, C.c_void_p, C.c_void_p]
         L.oracle_markdup.restype = C.c_int64
         L.oracle_markdup.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
                                      C.c_int32, C.c_int16, C.c_int, C.c_void_p]
@@ -82,3 +85,14 @@ def markdup(recs: np.ndarray, offs: np.ndarray, n: int, header_text: str, compat
     nd = _L().oracle_markdup(recs.ctypes.data, offs.ctypes.data, n, ida.ctypes.data, len(idbuf) - 1,
                              liba.ctypes.data, len(ids), unknown, 1 if compat_nonverbose else 0, dup.ctypes.data)
     return dup[:n], int(nd)
+
+
+def realign_scan(cons, cons_off, bases, quals, read_off, pairs):
+    """findBestOffset for every (consensus, read) pair, literal restatement -> (best_index, best_score)."""
+    pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 4)
+    n = len(pairs)
+    bi, bs = np.empty(max(n, 1), np.int32), np.empty(max(n, 1), np.int32)
+    arrs = [np.ascontiguousarray(a) for a in (cons, np.asarray(cons_off, np.uint64), bases, quals,
+                                              np.asarray(read_off, np.uint64))]
+    _L().oracle_realign_scan(*[a.ctypes.data for a in arrs], pairs.ctypes.data, n, bi.ctypes.data, bs.ctypes.data)
+    return bi[:n], bs[:n]

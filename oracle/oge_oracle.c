@@ -461,3 +461,78 @@ int64_t oracle_markdup(const uint8_t *recs, const uint64_t *offs, uint64_t n,
     free(tmp.s); free(pairs.v); free(frags.v); free(is_dup);
     return flagged;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Local realignment offset scan: LocalRealignment::findBestOffset
+ * (algorithms/local_realignment.cpp:1126-1164) over mismatchQualitySumIgnoreCigar (:641-679),
+ * restated literally -- including its early exits (quitAboveThisValue, the return at score 0)
+ * and its two loops -- so the HIP kernel's closed form (min over (score, visit rank)) is checked
+ * against the reference's control flow, not against itself.  Qualities are ASCII chars
+ * (phred + 33, kept as char: values above 94 wrap negative as in the reference); isRegularBase is
+ * util/gatk/BaseUtils.h:49-57.  Offsets past the consensus end (Q26: the reference reads out of
+ * range there) count 99 per base, the defined behaviour the product also uses.
+ * ------------------------------------------------------------------------------------------ */
+static int is_regular_base(char b) {
+    return b == 'A' || b == 'C' || b == 'G' || b == 'T' || b == 'a' || b == 'c' || b == 'g' || b == 't' || b == '*';
+}
+
+static int mismatch_quality_sum(const char *read, const char *quals, int64_t rlen, const char *ref, int64_t reflen,
+                                int64_t refIndex, int quit) {
+    int sum = 0;
+    int64_t common = refIndex >= reflen ? 0 : (rlen < reflen - refIndex - 1 ? rlen : reflen - refIndex - 1);
+    int64_t readIndex = 0;
+    for (; readIndex < common && sum <= quit; refIndex++, readIndex++) {
+        char refChr = ref[refIndex], readChr = read[readIndex];
+        if (!is_regular_base(readChr) || !is_regular_base(refChr)) continue;
+        if (readChr != refChr) sum += (int)quals[readIndex] - 33;
+    }
+    for (; readIndex < rlen && sum <= quit; refIndex++, readIndex++) {
+        if (refIndex >= reflen) {
+            sum += 99; /* MAX_QUAL */
+        } else {
+            char refChr = ref[refIndex], readChr = read[readIndex];
+            if (!is_regular_base(readChr) || !is_regular_base(refChr)) continue;
+            if (readChr != refChr) sum += (int)quals[readIndex] - 33;
+        }
+    }
+    return sum;
+}
+
+/* quals_phred: raw BAM quality bytes (converted to the reference's ASCII chars here) */
+int oracle_find_best_offset(const char *cons, int64_t cons_len, const char *read, const uint8_t *quals_phred, int64_t rlen,
+                            int orig, int max_start, int *best_score) {
+    char *q = (char *)malloc((size_t)(rlen > 0 ? rlen : 1));
+    for (int64_t i = 0; i < rlen; ++i) q[i] = (char)(quals_phred[i] + 33);
+    int bestScore = mismatch_quality_sum(read, q, rlen, cons, cons_len, orig, 0x7FFFFFFF);
+    int bestIndex = orig;
+    if (bestScore == 0) goto done;
+    for (int i = 0; i < orig; i++) {
+        int score = mismatch_quality_sum(read, q, rlen, cons, cons_len, i, bestScore);
+        if (score < bestScore) { bestScore = score; bestIndex = i; }
+        if (bestScore == 0) goto done;
+    }
+    for (int i = orig + 1; i <= max_start; i++) {
+        int score = mismatch_quality_sum(read, q, rlen, cons, cons_len, i, bestScore);
+        if (score < bestScore) { bestScore = score; bestIndex = i; }
+        if (bestScore == 0) goto done;
+    }
+done:
+    free(q);
+    *best_score = bestScore;
+    return bestIndex;
+}
+
+/* Batch form with the layout of oge_realign_scan (include/openge_hip.h). */
+int oracle_realign_scan(const uint8_t *cons, const uint64_t *cons_off, const uint8_t *bases, const uint8_t *quals,
+                        const uint64_t *read_off, const int32_t *pairs, uint64_t n_pairs, int32_t *best_index,
+                        int32_t *best_score) {
+    for (uint64_t p = 0; p < n_pairs; ++p) {
+        const int32_t *P = pairs + 4 * p;
+        const uint64_t c0 = cons_off[P[0]], c1 = cons_off[P[0] + 1], r0 = read_off[P[1]], r1 = read_off[P[1] + 1];
+        int s;
+        best_index[p] = oracle_find_best_offset((const char *)cons + c0, (int64_t)(c1 - c0), (const char *)bases + r0,
+                                                quals + r0, (int64_t)(r1 - r0), P[2], P[3], &s);
+        best_score[p] = s;
+    }
+    return 0;
+}

@@ -1,0 +1,54 @@
+// realign_cpu.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// Links the product's host realignment phases (openge_amd/csrc/realign.cpp) with the oracle's
+// restated offset scan (oracle/oge_oracle.c: oracle_realign_scan) in place of the HIP kernel, so the
+// CPU test suite can pin the host logic (binning, consensus generation, LOD/entropy decisions,
+// CIGAR/tag surgery, mate fixing) against the reference's own outputs without a GPU.  Never shipped;
+// the product library binds the GPU scan only.
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../openge_amd/csrc/bamio.h"
+#include "../../openge_amd/csrc/realign.h"
+
+extern "C" int oracle_realign_scan(const uint8_t *cons, const uint64_t *cons_off, const uint8_t *bases,
+                                   const uint8_t *quals, const uint64_t *read_off, const int32_t *pairs, uint64_t n_pairs,
+                                   int32_t *best_index, int32_t *best_score);
+
+struct Out {
+    std::vector<uint8_t> recs;
+    std::vector<uint64_t> offs;
+    std::string msg;
+};
+
+extern "C" {
+
+void *realign_cpu(const char *header, uint64_t hlen, const uint8_t *recs, const uint64_t *offs, uint64_t n,
+                  const char *fasta, const char *intervals, int threads) {
+    Out *o = new Out();
+    oge::BamHeaderModel h;
+    if (!h.parse(std::string(header, hlen), o->msg)) return o;
+    std::vector<std::string> names;
+    for (auto &sq : h.sq) names.push_back(sq.name);
+    oge::RealignParams P;
+    P.threads = threads;
+    oge::ScanFn scan = [](const oge::ScanBatch &B, std::vector<int32_t> &bi, std::vector<int32_t> &bs) {
+        bi.resize(B.pairs.size());
+        bs.resize(B.pairs.size());
+        return oracle_realign_scan(B.cons.data(), B.cons_off.data(), B.bases.data(), B.quals.data(), B.read_off.data(),
+                                   (const int32_t *)B.pairs.data(), B.pairs.size(), bi.data(), bs.data());
+    };
+    oge::RealignStats st;
+    std::string err;
+    int rc = oge::realign_run(names, recs, offs, n, fasta, intervals, P, scan, o->recs, o->offs, st, err);
+    if (rc) o->msg = err.empty() ? "realign failed" : err;
+    return o;
+}
+const char *realign_cpu_error(void *h) { return ((Out *)h)->msg.c_str(); }
+uint64_t realign_cpu_count(void *h) { Out *o = (Out *)h; return o->offs.empty() ? 0 : o->offs.size() - 1; }
+const uint8_t *realign_cpu_records(void *h, uint64_t *bytes) { Out *o = (Out *)h; *bytes = o->recs.size(); return o->recs.data(); }
+const uint64_t *realign_cpu_offsets(void *h) { return ((Out *)h)->offs.data(); }
+void realign_cpu_free(void *h) { delete (Out *)h; }
+}
