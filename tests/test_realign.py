@@ -44,7 +44,7 @@ def random_batch(rng, n_cons=6, reads_per=5, cons_len=(20, 90), read_len=(5, 40)
                  qual_max=60):
     cons, co, bases, quals, ro, pairs = [], [0], [], [], [0], []
     for c in range(n_cons):
-        s = bytes(rng.choice(list(b"ACGT" if rng.random() < .5 else alphabet), rng.integers(*cons_len)))
+        s = rng.choice(list(b"ACGT" if rng.random() < .5 else alphabet), rng.integers(*cons_len)).astype(np.uint8).tobytes()
         cons.append(s)
         co.append(co[-1] + len(s))
         for _ in range(reads_per):
@@ -56,7 +56,7 @@ def random_batch(rng, n_cons=6, reads_per=5, cons_len=(20, 90), read_len=(5, 40)
                     r[int(rng.integers(0, ln))] = int(rng.choice(list(b"ACGT")))
                 r = bytes(r)
             else:
-                r = bytes(rng.choice(list(alphabet), ln))
+                r = rng.choice(list(alphabet), ln).astype(np.uint8).tobytes()
             q = bytes(rng.integers(0, qual_max + 1, ln).astype(np.uint8))
             bases.append(r)
             quals.append(q)
@@ -65,6 +65,7 @@ def random_batch(rng, n_cons=6, reads_per=5, cons_len=(20, 90), read_len=(5, 40)
             ms = len(s) - ln - int(rng.integers(-3, 4))
             pairs.append([c, len(ro) - 2, orig, ms])
     u8 = lambda bs: np.frombuffer(b"".join(bs) + b"\0", np.uint8)[:-1].copy()
+    assert co[-1] == sum(map(len, cons)) and ro[-1] == sum(map(len, bases))
     return (u8(cons), np.array(co, np.uint64), u8(bases), u8(quals), np.array(ro, np.uint64),
             np.array(pairs, np.int32))
 
