@@ -54,6 +54,12 @@ int oge_ctx_timing(oge_ctx *ctx, const char *stage, double *ms_out);
 /* version string of the library, gfx target it was built for */
 const char *oge_version(void);
 
+/* ---- device buffers (for host code that stages records in HBM without HIP headers) ---- */
+int oge_dev_alloc(oge_ctx *ctx, uint64_t bytes, void **out);
+int oge_dev_free(oge_ctx *ctx, void *p);
+/* kind: 1 = host->device, 2 = device->host, 3 = device->device; synchronous on the ctx stream */
+int oge_memcpy(oge_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
+
 /* ---- coordinate sort (ReadSorter + Sort::ByPosition) ------------------------------ */
 /* perm_out[k] = input index of the record at sorted position k.  Order: refID ascending with
  * refID == -1 last; pos; forward before reverse; read name bytes; flag; input index (the

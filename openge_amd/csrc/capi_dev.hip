@@ -153,6 +153,32 @@ int oge_ctx_timing(oge_ctx *ctx, const char *stage, double *ms_out) {
     return OGE_OK;
 }
 
+// ---------------------------------------------------------------- device buffers
+int oge_dev_alloc(oge_ctx *ctx, uint64_t bytes, void **out) {
+    if (!ctx || !out) return oge_fail(ctx, OGE_ERR_ARG, "oge_dev_alloc: null argument");
+    hipSetDevice(ctx->device);
+    *out = nullptr;
+    OGE_HIP_TRY(ctx, hipMalloc(out, bytes ? bytes : 1));
+    return OGE_OK;
+}
+
+int oge_dev_free(oge_ctx *ctx, void *p) {
+    if (!ctx) return oge_fail(ctx, OGE_ERR_ARG, "oge_dev_free: null ctx");
+    hipSetDevice(ctx->device);
+    if (p) OGE_HIP_TRY(ctx, hipFree(p));
+    return OGE_OK;
+}
+
+int oge_memcpy(oge_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind) {
+    if (!ctx || (bytes && (!dst || !src))) return oge_fail(ctx, OGE_ERR_ARG, "oge_memcpy: null argument");
+    hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    if (kind < 1 || kind > 3) return oge_fail(ctx, OGE_ERR_ARG, "oge_memcpy: bad kind");
+    hipSetDevice(ctx->device);
+    if (bytes) OGE_HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, k, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return OGE_OK;
+}
+
 // ---------------------------------------------------------------- sort
 int oge_sort_coord_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref, uint32_t *d_perm) {
     if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");

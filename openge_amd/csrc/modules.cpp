@@ -1,0 +1,270 @@
+// modules.cpp -- AlgorithmModule chain over the C ABI (see modules.h).
+#include "modules.h"
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+
+#include "bam_layout.h"
+
+namespace oge {
+
+bool AlgorithmModule::verbose_ = false;
+
+int ChainContext::fail(const std::string &where) {
+    fprintf(stderr, "openge: %s: %s\n", where.c_str(), oge_last_error(ctx));
+    return -1;
+}
+
+int ChainContext::to_device(ReadBatch &b) {
+    if (b.dev_valid) return 0;
+    const uint64_t bytes = b.offs[b.n];
+    void *r = nullptr, *o = nullptr;
+    if (oge_dev_alloc(ctx, bytes + 64, &r) || oge_dev_alloc(ctx, (b.n + 1) * 8, &o)) return fail("device allocation");
+    if (oge_memcpy(ctx, r, b.recs.data(), bytes, 1) || oge_memcpy(ctx, o, b.offs.data(), (b.n + 1) * 8, 1))
+        return fail("host->device copy");
+    b.d_recs = (uint8_t *)r;
+    b.d_offs = (uint64_t *)o;
+    b.d_bytes = bytes;
+    b.dev_valid = true;
+    return 0;
+}
+
+int ChainContext::to_host(ReadBatch &b) {
+    if (b.host_valid) return 0;
+    b.recs.assign(b.d_bytes + 16, 0);
+    b.offs.resize(b.n + 1);
+    if (oge_memcpy(ctx, b.recs.data(), b.d_recs, b.d_bytes, 2) || oge_memcpy(ctx, b.offs.data(), b.d_offs, (b.n + 1) * 8, 2))
+        return fail("device->host copy");
+    b.host_valid = true;
+    return 0;
+}
+
+void ChainContext::free_device(ReadBatch &b) {
+    if (b.d_recs) oge_dev_free(ctx, b.d_recs);
+    if (b.d_offs) oge_dev_free(ctx, b.d_offs);
+    b.d_recs = nullptr;
+    b.d_offs = nullptr;
+    b.dev_valid = false;
+}
+
+int AlgorithmModule::runChain(ChainContext &cc) {
+    AlgorithmModule *head = this;
+    while (head->source_) head = head->source_;
+    ReadBatch b;
+    bool marked = false;  // ReadSorter fused MarkDuplicates into its device pipeline
+    for (AlgorithmModule *m = head; m; m = m->sink_) {
+        if (marked && dynamic_cast<MarkDuplicates *>(m)) {
+            b.drop_duplicates = static_cast<MarkDuplicates *>(m)->removeDuplicates;
+            marked = false;
+            continue;
+        }
+        if (verbose_) fprintf(stderr, "[openge] running %s on %llu records\n", m->name(), (unsigned long long)b.n);
+        int rc = m->runInternal(cc, b);
+        if (rc) {
+            cc.free_device(b);
+            return rc;
+        }
+        if (dynamic_cast<ReadSorter *>(m) && dynamic_cast<MarkDuplicates *>(m->sink_)) marked = true;
+    }
+    cc.free_device(b);
+    return 0;
+}
+
+// ----------------------------------------------------------------------------------- FileReader
+int FileReader::runInternal(ChainContext &cc, ReadBatch &b) {
+    (void)cc;
+    if (files_.empty()) files_.push_back("stdin");
+    for (size_t i = 0; i < files_.size(); ++i) {
+        const std::string path = files_[i] == "stdin" ? "/dev/stdin" : files_[i];
+        BamFile f;
+        std::string err;
+        if (!bam_read_file(path, f, cc.threads > 0 ? cc.threads : 8, err)) {
+            fprintf(stderr, "openge: error reading %s: %s\n", files_[i].c_str(), err.c_str());
+            return -1;
+        }
+        if (i == 0) {
+            b.header = f.header;
+            b.ref_names = f.ref_names;
+            b.recs.assign(f.recs(), f.recs() + f.rec_bytes());
+            b.offs = f.offsets;
+        } else {
+            if (f.ref_names != b.ref_names) {
+                fprintf(stderr, "openge: %s has a different sequence dictionary than %s\n", files_[i].c_str(), files_[0].c_str());
+                return -1;
+            }
+            const uint64_t base = b.recs.size();
+            b.recs.insert(b.recs.end(), f.recs(), f.recs() + f.rec_bytes());
+            for (uint64_t o : f.offsets) b.offs.push_back(base + o);
+        }
+    }
+    b.n = b.offs.size();
+    b.offs.push_back(b.recs.size());
+    b.recs.resize(b.recs.size() + 16, 0);
+    b.host_valid = true;
+    return 0;
+}
+
+// ----------------------------------------------------------------------------------- dedup opts
+// RG -> library table as MarkDuplicates::getLibraryName resolves it (mark_duplicates.cpp:301-318).
+struct MdOpts {
+    oge_markdup_opts o;
+    std::string ids;
+    std::vector<int16_t> libs;
+};
+static void markdup_opts(const ReadBatch &b, bool compat, MdOpts &m) {
+    std::map<std::string, int16_t> lib_ids;
+    int16_t next = 1;
+    for (auto &rg : b.header.rg) {
+        std::string lib = rg.lb.empty() ? std::string("Unknown Library") : rg.lb;
+        auto it = lib_ids.find(lib);
+        if (it == lib_ids.end()) it = lib_ids.emplace(lib, next++).first;
+        m.libs.push_back(it->second);
+        m.ids += rg.id;
+        m.ids.push_back('\0');
+    }
+    auto unk = lib_ids.find("Unknown Library");
+    m.libs.push_back(0);
+    memset(&m.o, 0, sizeof m.o);
+    m.o.n_ref = (int32_t)b.ref_names.size();
+    m.o.rg_ids = m.ids.c_str();
+    m.o.rg_ids_bytes = m.ids.size();
+    m.o.rg_lib = m.libs.data();
+    m.o.n_rg = (int32_t)b.header.rg.size();
+    m.o.unknown_lib = unk != lib_ids.end() ? unk->second : next;
+    m.o.compat_nonverbose_index = compat ? 1 : 0;
+}
+
+// ----------------------------------------------------------------------------------- ReadSorter
+int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
+    if (order_ != BamHeaderModel::COORDINATE) {
+        fprintf(stderr, "openge: sort by name (-b) is not provided by the GPU path\n");
+        return -1;
+    }
+    if (cc.to_device(b)) return -1;
+    void *perm = nullptr, *out = nullptr, *out_off = nullptr;
+    if (oge_dev_alloc(cc.ctx, b.n * 4 + 4, &perm) || oge_dev_alloc(cc.ctx, b.d_bytes + 64, &out) ||
+        oge_dev_alloc(cc.ctx, (b.n + 1) * 8, &out_off))
+        return cc.fail("device allocation");
+    int rc;
+    MarkDuplicates *md = dynamic_cast<MarkDuplicates *>(sink_);
+    if (md) {  // mergesort -M: one fused device pipeline (sort, dedup, gather with 0x400 applied)
+        MdOpts m;
+        markdup_opts(b, md->compatNonverbose, m);
+        uint64_t nd = 0;
+        rc = oge_sort_markdup_dev(cc.ctx, b.d_recs, b.d_offs, b.n, &m.o, (uint32_t *)perm, (uint8_t *)out,
+                                  (uint64_t *)out_off, &nd);
+        md->duplicates = nd;
+    } else {
+        rc = oge_sort_coord_dev(cc.ctx, b.d_recs, b.d_offs, b.n, (int32_t)b.ref_names.size(), (uint32_t *)perm);
+        if (!rc) rc = oge_gather_records_dev(cc.ctx, b.d_recs, b.d_offs, (uint32_t *)perm, b.n, (uint8_t *)out, (uint64_t *)out_off);
+    }
+    if (!rc) rc = oge_ctx_sync(cc.ctx);
+    oge_dev_free(cc.ctx, perm);
+    if (rc) {
+        oge_dev_free(cc.ctx, out);
+        oge_dev_free(cc.ctx, out_off);
+        return cc.fail("ReadSorter");
+    }
+    cc.free_device(b);
+    b.d_recs = (uint8_t *)out;
+    b.d_offs = (uint64_t *)out_off;
+    b.dev_valid = true;
+    b.host_valid = false;
+    b.header.sort_order = BamHeaderModel::COORDINATE;  // read_sorter.cpp:257-258
+    return 0;
+}
+
+// ----------------------------------------------------------------------------------- MarkDuplicates
+int MarkDuplicates::runInternal(ChainContext &cc, ReadBatch &b) {
+    if (cc.to_device(b)) return -1;
+    void *dup = nullptr;
+    if (oge_dev_alloc(cc.ctx, b.n + 1, &dup)) return cc.fail("device allocation");
+    MdOpts m;
+    markdup_opts(b, compatNonverbose, m);
+    uint64_t nd = 0;
+    int rc = oge_markdup_dev(cc.ctx, b.d_recs, b.d_offs, b.n, &m.o, (uint8_t *)dup, 1, &nd);
+    if (!rc) rc = oge_ctx_sync(cc.ctx);
+    oge_dev_free(cc.ctx, dup);
+    if (rc) return cc.fail("MarkDuplicates");
+    duplicates = nd;
+    b.host_valid = false;
+    b.drop_duplicates = removeDuplicates;
+    return 0;
+}
+
+// ----------------------------------------------------------------------------------- LocalRealignment
+int LocalRealignment::runInternal(ChainContext &cc, ReadBatch &b) {
+    if (cc.to_host(b)) return -1;
+    cc.free_device(b);
+    oge_realign_opts o;
+    oge_realign_opts_init(&o);
+    o.threads = cc.threads;
+    const std::string ht = b.header.to_string();
+    oge_realign_result *r = nullptr;
+    if (oge_localrealign(cc.ctx, ht.data(), ht.size(), b.recs.data(), b.offs.data(), b.n, reference_.c_str(),
+                         intervals_.c_str(), &o, &r))
+        return cc.fail("LocalRealignment");
+    uint64_t bytes = 0;
+    const uint8_t *rp = oge_realign_result_records(r, &bytes);
+    const uint64_t *op = oge_realign_result_offsets(r);
+    const uint64_t n = oge_realign_result_count(r);
+    b.recs.assign(rp, rp + bytes);
+    b.recs.resize(bytes + 16, 0);
+    b.offs.assign(op, op + n + 1);
+    b.n = n;
+    if (verbose) fprintf(stderr, "[openge] LocalRealignment: %s\n", oge_realign_result_stats(r));
+    oge_realign_result_free(r);
+    return 0;
+}
+
+// ----------------------------------------------------------------------------------- FileWriter
+int FileWriter::setFormat(const std::string &f) {
+    if (f == "bam" || f == "BAM") return 0;
+    fprintf(stderr, "openge: output format %s is not provided (BAM only)\n", f.c_str());
+    return -1;
+}
+
+int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
+    if (cc.to_host(b)) return -1;
+    BamHeaderModel h = b.header;
+    if (!program_line_.empty()) {  // file_writer.cpp:76-89
+        PgRecord pg;
+        pg.id = "openge";
+        auto has = [&](const std::string &id) {
+            for (auto &p : h.pg)
+                if (p.id == id) return true;
+            return false;
+        };
+        for (int i = 2; has(pg.id); i++) pg.id = "openge-" + std::to_string(i);
+        pg.vn = "0.3-dev";  // OPENGE_VERSION_STRING (oge/CMakeLists.txt:11-12)
+        pg.cl = program_line_;
+        h.pg.push_back(pg);
+    }
+    FILE *f = filename_ == "stdout" || filename_ == "-" ? stdout : fopen(filename_.c_str(), "wb");
+    if (!f) {
+        fprintf(stderr, "Error opening BAM file to write.\n");
+        return -1;
+    }
+    {
+        BgzfWriter w(f, level_, cc.threads > 0 ? cc.threads : 8);
+        std::vector<uint8_t> hb = bam_encode_header(h);
+        w.write(hb.data(), hb.size());
+        std::vector<uint8_t> tmp;
+        for (uint64_t k = 0; k < b.n; ++k) {
+            const uint8_t *r = b.recs.data() + b.offs[k];
+            const uint32_t bs = oge_rd_u32(r);
+            if (b.drop_duplicates && (oge_rd_u16(r + OGE_OFF_FLAG) & OGE_F_DUP)) continue;
+            tmp.assign(r, r + 4 + bs);
+            oge_wr_u16(tmp.data() + OGE_OFF_BIN, oge_rec_bin(tmp.data()));  // bam_serializer.h:112-116
+            w.write(tmp.data(), tmp.size());
+        }
+        w.close();
+    }
+    if (f != stdout) fclose(f);
+    else fflush(stdout);
+    return 0;
+}
+
+}  // namespace oge

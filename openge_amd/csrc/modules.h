@@ -1,0 +1,141 @@
+// modules.h -- the AlgorithmModule operator API of OpenGE (algorithms/algorithm_module.h:33-107),
+// re-designed for MI355X: a chain of modules hands ONE batch of records (the whole input) from
+// module to module instead of streaming OGERead* through polled per-module queues.  Records stay in
+// HBM between device modules (ReadSorter -> MarkDuplicates is fused into one device pipeline), and
+// only the file endpoints touch host memory.  Module names, setters and defaults follow the
+// reference; each class cites the module it replaces.
+//
+// Built on the C ABI only (include/openge_hip.h): this layer is what an OpenGE maintainer would
+// link against, and it contains no HIP code of its own.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/openge_hip.h"
+#include "bamio.h"
+
+namespace oge {
+
+// Records of one chain, resident in host memory, HBM, or both.
+struct ReadBatch {
+    BamHeaderModel header;
+    std::vector<std::string> ref_names;
+    uint64_t n = 0;
+    // host form
+    std::vector<uint8_t> recs;        // + 16 bytes of slack
+    std::vector<uint64_t> offs;       // n + 1
+    bool host_valid = false;
+    // device form
+    uint8_t *d_recs = nullptr;
+    uint64_t *d_offs = nullptr;
+    uint64_t d_bytes = 0;
+    bool dev_valid = false;
+    // dedup output applied by the writer (-r / -R: records carrying 0x400 are not written)
+    bool drop_duplicates = false;
+
+    uint64_t bytes() const { return host_valid ? offs[n] : d_bytes; }
+};
+
+struct ChainContext {
+    oge_ctx *ctx = nullptr;
+    int device = 0;
+    int threads = 0;
+    bool verbose = false;
+    int fail(const std::string &where);  // prints oge_last_error, returns -1
+    int to_device(ReadBatch &b);
+    int to_host(ReadBatch &b);
+    void free_device(ReadBatch &b);
+};
+
+class AlgorithmModule {
+public:
+    virtual ~AlgorithmModule() {}
+    void addSink(AlgorithmModule *sink) { sink_ = sink; sink->source_ = this; }
+    // AlgorithmModule::runChain (algorithm_module.cpp:92-116): run every module of the chain that
+    // ends at this one, from its first source.  Returns 0 or the first failing module's status
+    // (the reference always returns 0).
+    int runChain(ChainContext &cc);
+    static void setVerbose(bool v) { verbose_ = v; }
+    static bool isVerbose() { return verbose_; }
+    const char *name() const { return name_; }
+
+protected:
+    explicit AlgorithmModule(const char *name) : name_(name) {}
+    // consume `b` (the previous module's output) in place; sources ignore it and fill it
+    virtual int runInternal(ChainContext &cc, ReadBatch &b) = 0;
+    AlgorithmModule *source_ = nullptr, *sink_ = nullptr;
+    static bool verbose_;
+    const char *name_;
+    friend class ReadSorter;
+};
+
+// FileReader (algorithms/file_reader.cpp:29-63): BAM input(s).  Several inputs are concatenated
+// in the order given (the reference's MultiReader interleaves them by position; for mergesort the
+// sort makes both equivalent).
+class FileReader : public AlgorithmModule {
+public:
+    FileReader() : AlgorithmModule("FileReader") {}
+    void addFile(const std::string &f) { files_.push_back(f); }
+    void addFiles(const std::vector<std::string> &f) { files_.insert(files_.end(), f.begin(), f.end()); }
+    void setLoadStringData(bool) {}  // the record arena always keeps the full record bytes
+protected:
+    int runInternal(ChainContext &cc, ReadBatch &b) override;
+    std::vector<std::string> files_;
+};
+
+// ReadSorter (algorithms/read_sorter.h:32-105): coordinate sort on the GPU (oge_sort_coord_dev +
+// permutation gather).  The temp-file knobs are accepted for interface parity; one device sort
+// replaces the reference's spilled runs and k-way merge.
+class ReadSorter : public AlgorithmModule {
+public:
+    explicit ReadSorter(const std::string &tmpdir = "/tmp/") : AlgorithmModule("ReadSorter") { (void)tmpdir; }
+    void setSortBy(BamHeaderModel::SortOrder o) { order_ = o; }
+    void setCompressTempFiles(bool) {}
+    void setAlignmentsPerTempfile(int) {}
+protected:
+    int runInternal(ChainContext &cc, ReadBatch &b) override;
+    BamHeaderModel::SortOrder order_ = BamHeaderModel::COORDINATE;
+};
+
+// MarkDuplicates (algorithms/mark_duplicates.h:27-68): -v --nosplit semantics on the GPU.
+class MarkDuplicates : public AlgorithmModule {
+public:
+    explicit MarkDuplicates(const std::string &tmpdir = "/tmp/") : AlgorithmModule("MarkDuplicates") { (void)tmpdir; }
+    bool removeDuplicates = false;
+    bool compatNonverbose = false;  // reproduce the index bug of runs without -v
+    uint64_t duplicates = 0;
+protected:
+    int runInternal(ChainContext &cc, ReadBatch &b) override;
+    friend class ReadSorter;
+};
+
+// LocalRealignment (algorithms/local_realignment.h:67-527): oge_localrealign (host phases + the
+// GPU offset scan).
+class LocalRealignment : public AlgorithmModule {
+public:
+    LocalRealignment() : AlgorithmModule("LocalRealignment") {}
+    bool verbose = false;
+    void setReferenceFilename(const std::string &f) { reference_ = f; }
+    void setIntervalsFilename(const std::string &f) { intervals_ = f; }
+protected:
+    int runInternal(ChainContext &cc, ReadBatch &b) override;
+    std::string reference_, intervals_;
+};
+
+// FileWriter (algorithms/file_writer.cpp:69-196): BAM output, @PG record unless --nopg, BGZF at the
+// given level, bin recomputed on every record.
+class FileWriter : public AlgorithmModule {
+public:
+    FileWriter() : AlgorithmModule("FileWriter") {}
+    void setFilename(const std::string &f) { filename_ = f; }
+    void setCompressionLevel(int l) { level_ = l; }
+    void addProgramLine(const std::string &cl) { program_line_ = cl; }
+    int setFormat(const std::string &f);  // only "bam" is supported (SAM/FASTQ out of scope)
+protected:
+    int runInternal(ChainContext &cc, ReadBatch &b) override;
+    std::string filename_ = "stdout", program_line_;
+    int level_ = 6;
+};
+
+}  // namespace oge

@@ -1,0 +1,114 @@
+"""GPU: the `openge` command-line drop-in (openge_amd/openge) end to end, BAM in -> BAM out, against
+the REFERENCE's own outputs (tests/golden; made by oracle/_ref from the reference's modules).  These
+read like the reference's CTest smoke tests (openge/test/CMakeLists.txt:32,44-45) with the outputs
+pinned byte for byte (decompressed records + header text; compressed bytes are not part of parity)."""
+import hashlib
+import subprocess
+
+import numpy as np
+import pytest
+
+import bamutil
+import realign_util as R
+from goldens import CASE_NAMES, GOLDEN, load_case
+from openge_amd import lib as L
+from test_realign import RL_CASES, check_output, load_rl_case
+
+pytestmark = pytest.mark.gpu
+OPENGE = str(L.PKG / "openge")
+
+
+def run(*args):
+    r = subprocess.run([OPENGE, *map(str, args)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r
+
+
+def case_input(case, tmp_path):
+    if case.meta["spec"]["kind"] == "file":
+        return GOLDEN / "inputs" / case.meta["spec"]["file"]
+    path = tmp_path / "in.bam"
+    bamutil.write_bam_py(path, case.header, _refs(case.header), [bamutil.rec_bytes(case.recs, o) for o in case.offs[:-1]])
+    return path
+
+
+def _refs(header):
+    out = []
+    for line in header.splitlines():
+        if line.startswith("@SQ"):
+            f = dict(x.split(":", 1) for x in line.split("\t")[1:])
+            out.append((f["SN"], int(f["LN"])))
+    return out
+
+
+def digests(path):
+    h, _, recs, offs = bamutil.read_bam(path)
+    hm, tail = hashlib.sha256(), []
+    for o in offs:
+        rb = bamutil.rec_bytes(recs, o)
+        (tail.append(rb) if int.from_bytes(rb[4:8], "little", signed=True) == -1 else hm.update(rb))
+    return h, hm.hexdigest(), hashlib.sha256(b"".join(sorted(tail))).hexdigest()
+
+
+@pytest.fixture(scope="module", params=CASE_NAMES)
+def case(request, built):
+    return load_case(request.param)
+
+
+def test_cli_mergesort_M_matches_reference(case, tmp_path):
+    src = case_input(case, tmp_path)
+    run("mergesort", "-M", "--nopg", src, "-o", tmp_path / "o.bam")
+    h, m, t = digests(tmp_path / "o.bam")
+    g = case.meta["sortdedup_v"]
+    assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
+
+
+def test_cli_sort_alias_then_dedup_matches_reference(case, tmp_path):
+    src = case_input(case, tmp_path)
+    run("sort", "--nopg", src, "-o", tmp_path / "s.bam")
+    h, m, t = digests(tmp_path / "s.bam")
+    assert h == case.meta["sorted_header"] and m == case.meta["sort"]["mapped_sha256"]
+    run("dedup", "--nopg", tmp_path / "s.bam", "-o", tmp_path / "d.bam")
+    h, m, t = digests(tmp_path / "d.bam")
+    g = case.meta["dedup_sorted_v"]
+    assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
+
+
+def test_cli_dedup_remove_drops_flagged_records(case, tmp_path):
+    src = case_input(case, tmp_path)
+    run("mergesort", "-R", "--nopg", src, "-o", tmp_path / "r.bam")
+    _, _, recs, offs = bamutil.read_bam(tmp_path / "r.bam")
+    assert len(offs) == case.n - case.meta["sortdedup_v"]["n_dup"]
+    assert not (bamutil.flags_of(recs, offs) & 0x400).any()
+
+
+def test_cli_program_record(tmp_path):
+    src = tmp_path / "mix.bam"
+    p = L.synth_params(200, preset="mix", seed=3)
+    recs, offs, hdr = L.synth_host(p)
+    L.write_bam(src, hdr, recs, offs, 400)
+    run("mergesort", src, "-o", tmp_path / "p.bam", "-c", "1")
+    h = bamutil.read_bam(tmp_path / "p.bam")[0]
+    pg = [l for l in h.splitlines() if l.startswith("@PG")]
+    # FileWriter::runInternal (algorithms/file_writer.cpp:76-89) + BamProgramRecord::toString
+    assert pg == [f"@PG\tID:openge\tCL:openge mergesort {src} -o {tmp_path / 'p.bam'} -c 1 \tVN:0.3-dev"]
+    run("mergesort", tmp_path / "p.bam", "-o", tmp_path / "p2.bam")
+    ids = [l.split("\t")[1] for l in bamutil.read_bam(tmp_path / "p2.bam")[0].splitlines() if l.startswith("@PG")]
+    assert ids == ["ID:openge", "ID:openge-2"]
+
+
+@pytest.mark.parametrize("name", ["rl_small", "rl_edge"])
+def test_cli_localrealign_matches_reference(name, tmp_path):
+    meta, arrays, h, recs, offs, fa, iv = load_rl_case(name, tmp_path)
+    run("localrealign", "--nopg", "-R", fa, "-L", iv, tmp_path / "reads.bam", "-o", tmp_path / "rl.bam")
+    oh, _, orecs, ooffs = bamutil.read_bam(tmp_path / "rl.bam")
+    assert oh == meta["output_header"]
+    check_output(meta, arrays, orecs, np.append(ooffs, np.uint64(len(orecs))))
+
+
+def test_cli_errors_are_loud(tmp_path):
+    r = subprocess.run([OPENGE, "localrealign", str(GOLDEN / "inputs" / "simple.bam")], capture_output=True, text=True)
+    assert r.returncode != 0 and "FASTA reference" in r.stderr
+    r = subprocess.run([OPENGE, "mergesort", str(GOLDEN / "inputs" / "208.truncated.bam"), "-o", str(tmp_path / "t.bam")],
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "truncated" in r.stderr
