@@ -1,0 +1,30 @@
+"""End-to-end `openge mergesort -M` BAM -> BAM timing on a C2-shaped synthetic BAM (N reads).
+
+usage: python tools/e2e_cli.py N_READS OUTDIR [threads]
+Writes OUTDIR/c2_<N>.bam (BGZF level 6, product writer), runs the CLI, prints one JSON line."""
+import json
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from openge_amd import lib as L  # noqa: E402
+
+n = int(sys.argv[1])
+out = Path(sys.argv[2])
+th = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+out.mkdir(parents=True, exist_ok=True)
+src = out / f"c2_{n}.bam"
+if not src.exists():
+    p = L.synth_params(n // 2, preset="c2", seed=1234)
+    recs, offs, hdr = L.synth_host(p, threads=th)
+    L.write_bam(src, hdr, recs, offs, n, level=6, threads=th)
+    del recs, offs
+t0 = time.perf_counter()
+r = subprocess.run([str(ROOT / "openge_amd/openge"), "mergesort", "-M", "--nopg", "-v", "-t", str(th), str(src), "-o",
+                    str(out / "sorted_dedup.bam")], capture_output=True, text=True)
+dt = time.perf_counter() - t0
+print(json.dumps({"reads": n, "seconds": round(dt, 3), "mreads_per_s": round(n / dt / 1e6, 3), "threads": th,
+                  "rc": r.returncode, "stderr_tail": r.stderr[-600:], "in_bytes": src.stat().st_size}))
