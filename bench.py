@@ -7,9 +7,11 @@ FLAG 0x400 applied).  Workload at N=1: configs[1]+[2] -- a 300M-read (150M pairs
 synthetic read set (SURVEY.md §8d C2 generator, seed 1234), generated straight into HBM; one step =
 the whole device pipeline over the resident records (oge_sort_markdup_dev).
 
-Multi-GPU (torchrun, one rank per GPU): every rank processes its own 300M-read shard (a different
-seed), i.e. N independent per-sample pipelines -- weak scaling, no data-path collective (DESIGN.md
-"Multi-GPU").  value = reads of all ranks / max-over-ranks wall time.
+Multi-GPU (torchrun, one rank per GPU): the same 300M-read sample split across N ranks (strong
+scaling); openge_amd/shard.py routes records to the rank owning their contig with an RCCL all-to-all
+over xGMI (ghost copies of cross-rank mates keep MarkDuplicates exact), each rank sorts + dedups its
+range, and the ranks' outputs concatenate into the single-GPU result.  value = reads / max-over-ranks
+wall time.
 
 Also reported on the same JSON line:
   roofline     -- dominant kernel (the permutation gather, algorithmic bytes 2*B per launch, B = record
@@ -130,24 +132,29 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")  # RCCL on ROCm
+        # RCCL on ROCm: all-to-all over xGMI.  OGE_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs.
+        dist.init_process_group(os.environ.get("OGE_DIST_BACKEND", "nccl"))
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    stream = torch.cuda.current_stream(dev)
+    # one stream for torch ops and our kernels (the default stream is the legacy null stream, which
+    # the context's non-blocking stream would not order against)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     ctx = L.Context(local, stream=stream.cuda_stream)
 
-    # ---- inputs resident in HBM before the timed region ----
-    p = L.synth_params(args.pairs, preset="c2", seed=1234 + rank)
-    n = 2 * args.pairs
+    # ---- inputs resident in HBM before the timed region.  One 300M-read sample (C2); with N ranks
+    # each holds 1/N of it (an arbitrary slice of the unsorted input: strong scaling).
+    p = L.synth_params(args.pairs, preset="c2", seed=1234)
+    n_all = 2 * args.pairs
+    s0, s1 = n_all * rank // world, n_all * (rank + 1) // world
+    n = s1 - s0
     d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    ctx.synth_dev(p, d_offs.data_ptr(), None)
+    ctx.synth_range_dev(p, s0, n, d_offs.data_ptr(), None)
     ctx.sync()
     B = int(d_offs[-1].item())
     d_recs = torch.empty(B + 64, dtype=torch.uint8, device=dev)
-    ctx.synth_dev(p, d_offs.data_ptr(), d_recs.data_ptr())
-    d_out = torch.empty(B + 64, dtype=torch.uint8, device=dev)
-    d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    d_perm = torch.empty(n, dtype=torch.int32, device=dev)
+    ctx.synth_range_dev(p, s0, n, d_offs.data_ptr(), d_recs.data_ptr())
     hdr_len = 1 << 16
     import ctypes as C
     buf = C.create_string_buffer(hdr_len)
@@ -155,12 +162,31 @@ def main():
     opts, keep = L.markdup_opts_from_header(buf.value.decode(), p.n_ref)
     ctx.sync()
 
-    def step():
-        return ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(), d_out.data_ptr(),
-                                    d_out_off.data_ptr())
+    shard_t = {}
+    if world == 1:
+        d_out = torch.empty(B + 64, dtype=torch.uint8, device=dev)
+        d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        d_perm = torch.empty(n, dtype=torch.int32, device=dev)
+
+        def step():
+            return ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(),
+                                        d_out.data_ptr(), d_out_off.data_ptr())
+    else:
+        from openge_amd import shard
+        backend = shard.HipBackend(ctx)
+        owners = shard.contig_owners([int(p.ref_len[i]) for i in range(p.n_ref)], world)
+
+        def step():
+            T = {}
+            out, off, k = shard.sort_markdup_sharded(backend, d_recs, d_offs, n, p.n_ref, owners, opts, timings=T)
+            for key, v in T.items():
+                shard_t[key] = shard_t.get(key, 0.0) + v
+            del out, off
+            return k
 
     for _ in range(args.warmup):
         step()
+    shard_t.clear()
     stage_tot = {s: 0.0 for s in STAGES}
     if world > 1:
         dist.barrier()
@@ -169,9 +195,9 @@ def main():
     ndup = 0
     for _ in range(args.steps):
         ndup = step()
-        for s in STAGES:  # HIP events recorded around each stage on the context stream
-            ms = ctx.timing(s)
-            stage_tot[s] += max(ms, 0.0)
+        if world == 1:
+            for s in STAGES:  # HIP events recorded around each stage on the context stream
+                stage_tot[s] += max(ctx.timing(s), 0.0)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -184,41 +210,46 @@ def main():
     if rank == 0:
         K = args.steps
         ms_step = dt / K * 1e3
-        reads_total = n * world
-        value = reads_total * K / dt / 1e6
-        stages_ms = {s: round(v / K, 3) for s, v in stage_tot.items()}
-        t_gather = stages_ms["gather_records"] / 1e3
-        gather_bytes = 2 * B  # sort = 2*B (each record read once, written once)
-        achieved = gather_bytes / t_gather / 1e9 if t_gather > 0 else 0.0
-        seq_bytes = n * ((p.read_len + 1) // 2)
-        pipe_bytes = 2 * B + (B - seq_bytes) + 2 * n
-        pipe_gbs = pipe_bytes / (ms_step / 1e3) / 1e9
-        pmc = pmc_traffic("k_gather16", B)
-        roof = {"kernel": "k_gather_records (permutation gather + BAM re-encode)", "bound": "hbm",
-                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": round(pmc["bytes"]) if pmc else None,
-                "traffic_source": pmc["source"] if pmc else None,
-                "algorithmic_bytes": gather_bytes, "avg_ms": stages_ms["gather_records"]}
+        value = n_all * K / dt / 1e6
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mreads/s", "n_gpus": world, "steps": K,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234+rank; records resident in HBM",
-            "config": {"workload": "C2+C3 sort+dedup (mergesort -M --nosplit semantics), 300M reads/GPU",
-                       "reads_per_gpu": n, "record_bytes_per_gpu": B, "duplicates_flagged": ndup,
-                       "parallelism": f"{world} independent per-GPU pipelines" if world > 1 else "1 GPU"},
-            "roofline": roof,
-            "pipeline": {"algorithmic_bytes": pipe_bytes, "achieved": round(pipe_gbs, 1), "unit": "GB/s",
-                         "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)},
-            "stages_ms": stages_ms,
+            "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234; records resident in HBM",
+            "config": {"workload": f"C2+C3 sort+dedup (mergesort -M --nosplit semantics), {n_all // 1000000}M reads "
+                                   "in total" + (f", {world} contig-sharded ranks" if world > 1 else ""),
+                       "reads_total": n_all, "reads_rank0": n, "record_bytes_rank0": B,
+                       "parallelism": (f"{world} ranks: contig ownership + RCCL all-to-all + ghost mates"
+                                       if world > 1 else "1 GPU")},
         }
-        if world == 1 and not args.no_realign:
-            out["realign"] = realign_leg(ctx, args.realign_intervals)
-        if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(args.cpu_sample_reads)
-            cb["gpu_speedup"] = round(value / cb["value"], 1)
-            out["cpu_baseline"] = cb
+        if world == 1:
+            out["config"]["duplicates_flagged"] = ndup
+            stages_ms = {s: round(v / K, 3) for s, v in stage_tot.items()}
+            t_gather = stages_ms["gather_records"] / 1e3
+            gather_bytes = 2 * B  # sort = 2*B (each record read once, written once)
+            achieved = gather_bytes / t_gather / 1e9 if t_gather > 0 else 0.0
+            seq_bytes = n * ((p.read_len + 1) // 2)
+            pipe_bytes = 2 * B + (B - seq_bytes) + 2 * n
+            pipe_gbs = pipe_bytes / (ms_step / 1e3) / 1e9
+            pmc = pmc_traffic("k_gather16", B)
+            out["roofline"] = {"kernel": "k_gather_records (permutation gather + BAM re-encode)", "bound": "hbm",
+                               "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(achieved / HBM_PEAK_GBS, 4),
+                               "traffic": round(pmc["bytes"]) if pmc else None,
+                               "traffic_source": pmc["source"] if pmc else None,
+                               "algorithmic_bytes": gather_bytes, "avg_ms": stages_ms["gather_records"]}
+            out["pipeline"] = {"algorithmic_bytes": pipe_bytes, "achieved": round(pipe_gbs, 1), "unit": "GB/s",
+                               "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)}
+            out["stages_ms"] = stages_ms
+            if not args.no_realign:
+                out["realign"] = realign_leg(ctx, args.realign_intervals)
+            if not args.no_cpu_baseline:
+                cb = cpu_baseline(args.cpu_sample_reads)
+                cb["gpu_speedup"] = round(value / cb["value"], 1)
+                out["cpu_baseline"] = cb
+        else:
+            out["shard_rank0_s_per_step"] = {k: (round(v / K, 4) if isinstance(v, float) else v // K)
+                                             for k, v in shard_t.items()}
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:

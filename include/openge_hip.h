@@ -115,6 +115,22 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
                          const oge_markdup_opts *opts, uint32_t *d_perm, uint8_t *d_out, uint64_t *d_out_off,
                          uint64_t *n_dup_out);
 
+/* ---- multi-GPU contig sharding (replaces SplitByChromosome/SortedMerge) -------------- */
+/* Per record: d_dest = owner rank of its refID (d_owner has n_ref + 1 entries, the last one for
+ * refID -1; it must be non-decreasing so rank outputs concatenate in sorted order); d_ghost = the
+ * mate's owner when the record is a mate-join candidate whose mate is owned by another rank, else
+ * -1; d_back = d_dest when my_rank holds the record as a ghost whose mate is the pair's read1
+ * (mate refID < refID), else -1.  Any output may be NULL.  Replaces
+ * algorithms/split_by_chromosome.cpp:30-58 + algorithms/sorted_merge.cpp:66-101. */
+int oge_shard_route_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
+                        const int32_t *d_owner, int32_t n_ref, int32_t my_rank, int32_t *d_dest,
+                        int32_t *d_ghost, int32_t *d_back);
+/* Device synthetic generation of the slot range [slot0, slot0 + nslots) of a data set (one rank's
+ * shard of a multi-GPU input). */
+int oge_synth_offsets_range_dev(oge_ctx *ctx, const void *params, uint64_t slot0, uint64_t nslots, uint64_t *d_offs);
+int oge_synth_records_range_dev(oge_ctx *ctx, const void *params, uint64_t slot0, uint64_t nslots,
+                                const uint64_t *d_offs, uint8_t *d_out);
+
 /* ---- local realignment (LocalRealignment) ----------------------------------------- */
 /* Offset scan, the realigner's hot loop: for every pair (consensus c, altRead r) the best
  * offset of r on c and its mismatch-quality score, exactly as findBestOffset returns them

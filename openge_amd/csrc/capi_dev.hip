@@ -316,38 +316,46 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
 
 // ---------------------------------------------------------------- device synth
 namespace {
-__global__ __launch_bounds__(256) void k_synth_sizes(oge_synth_params P, uint64_t *offs) {
-    uint64_t n = 2 * P.n_pairs;
+__global__ __launch_bounds__(256) void k_synth_sizes(oge_synth_params P, uint64_t s0, uint64_t n, uint64_t *offs) {
     uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s < n) offs[s] = oge_synth_slot_bytes(&P, s);
+    if (s < n) offs[s] = oge_synth_slot_bytes(&P, s0 + s);
     else if (s == n) offs[s] = 0;
 }
-__global__ __launch_bounds__(256) void k_synth_write(oge_synth_params P, const uint64_t *offs, uint8_t *out) {
-    uint64_t n = 2 * P.n_pairs;
+__global__ __launch_bounds__(256) void k_synth_write(oge_synth_params P, uint64_t s0, uint64_t n, const uint64_t *offs,
+                                                     uint8_t *out) {
     uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s < n) oge_synth_write_slot(&P, s, out + offs[s]);
+    if (s < n) oge_synth_write_slot(&P, s0 + s, out + offs[s]);
 }
 }  // namespace
 
 extern "C" {
-int oge_synth_offsets_dev(oge_ctx *ctx, const void *params, uint64_t *d_offs) {
+int oge_synth_offsets_range_dev(oge_ctx *ctx, const void *params, uint64_t slot0, uint64_t n, uint64_t *d_offs) {
     if (!ctx || !params) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
-    hipSetDevice(ctx->device);
     const oge_synth_params *P = (const oge_synth_params *)params;
-    uint64_t n = 2 * P->n_pairs;
-    hipLaunchKernelGGL(k_synth_sizes, dim3(oge_ceil_div(n + 1, 256)), dim3(256), 0, ctx->stream, *P, d_offs);
+    if (slot0 + n > 2 * P->n_pairs) return oge_fail(ctx, OGE_ERR_ARG, "synth: slot range outside the data set");
+    hipSetDevice(ctx->device);
+    hipLaunchKernelGGL(k_synth_sizes, dim3(oge_ceil_div(n + 1, 256)), dim3(256), 0, ctx->stream, *P, slot0, n, d_offs);
     OGE_LAUNCH_CHECK(ctx);
     return oge_exclusive_scan_u64(ctx, d_offs, d_offs, n + 1);
 }
-int oge_synth_records_dev(oge_ctx *ctx, const void *params, const uint64_t *d_offs, uint8_t *d_out) {
+int oge_synth_records_range_dev(oge_ctx *ctx, const void *params, uint64_t slot0, uint64_t n, const uint64_t *d_offs,
+                                uint8_t *d_out) {
     if (!ctx || !params) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
-    hipSetDevice(ctx->device);
     const oge_synth_params *P = (const oge_synth_params *)params;
-    uint64_t n = 2 * P->n_pairs;
+    if (slot0 + n > 2 * P->n_pairs) return oge_fail(ctx, OGE_ERR_ARG, "synth: slot range outside the data set");
+    hipSetDevice(ctx->device);
     if (n) {
-        hipLaunchKernelGGL(k_synth_write, dim3(oge_ceil_div(n, 256)), dim3(256), 0, ctx->stream, *P, d_offs, d_out);
+        hipLaunchKernelGGL(k_synth_write, dim3(oge_ceil_div(n, 256)), dim3(256), 0, ctx->stream, *P, slot0, n, d_offs, d_out);
         OGE_LAUNCH_CHECK(ctx);
     }
     return OGE_OK;
+}
+int oge_synth_offsets_dev(oge_ctx *ctx, const void *params, uint64_t *d_offs) {
+    if (!params) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    return oge_synth_offsets_range_dev(ctx, params, 0, 2 * ((const oge_synth_params *)params)->n_pairs, d_offs);
+}
+int oge_synth_records_dev(oge_ctx *ctx, const void *params, const uint64_t *d_offs, uint8_t *d_out) {
+    if (!params) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    return oge_synth_records_range_dev(ctx, params, 0, 2 * ((const oge_synth_params *)params)->n_pairs, d_offs, d_out);
 }
 }  // extern "C"

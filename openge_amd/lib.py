@@ -187,6 +187,12 @@ def lib() -> C.CDLL:
         "oge_bam_markdup_opts": (C.c_int, [vp, vp, C.POINTER(vp), C.POINTER(vp)]),
         "oge_bam_write": (C.c_int, [C.c_char_p, C.c_char_p, u64, C.c_int, vp, vp, u64, vp, vp, C.c_int, C.c_int]),
         "oge_realign_scan": (C.c_int, [vp, vp, vp, vp]),
+        "oge_shard_route_dev": (C.c_int, [vp, vp, vp, u64, vp, i32, i32, vp, vp, vp]),
+        "oge_synth_offsets_range_dev": (C.c_int, [vp, vp, u64, u64, vp]),
+        "oge_synth_records_range_dev": (C.c_int, [vp, vp, u64, u64, vp, vp]),
+        "oge_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
+        "oge_dev_free": (C.c_int, [vp, vp]),
+        "oge_memcpy": (C.c_int, [vp, vp, vp, u64, C.c_int]),
         "oge_realign_opts_init": (None, [vp]),
         "oge_localrealign": (C.c_int, [vp, C.c_char_p, u64, vp, vp, u64, C.c_char_p, C.c_char_p, vp, C.POINTER(vp)]),
         "oge_realign_result_count": (u64, [vp]),
@@ -408,6 +414,15 @@ class Context:
         finally:
             L.oge_realign_result_free(res)
         return out, oo, stats
+
+    def synth_range_dev(self, p: SynthParams, slot0: int, nslots: int, d_offs: int, d_out: int | None) -> None:
+        """Slots [slot0, slot0 + nslots) of the data set (one rank's input shard)."""
+        L = lib()
+        check(L.oge_synth_finalize(C.byref(p)))
+        if d_offs and not d_out:
+            check(L.oge_synth_offsets_range_dev(self.h, C.byref(p), slot0, nslots, d_offs), self.h)
+        if d_out:
+            check(L.oge_synth_records_range_dev(self.h, C.byref(p), slot0, nslots, d_offs, d_out), self.h)
 
     def synth_dev(self, p: SynthParams, d_offs: int, d_out: int | None) -> None:
         L = lib()
