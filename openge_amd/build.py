@@ -69,7 +69,7 @@ def build(verbose: bool = False) -> Path:
         list(ex.map(lambda j: _compile(*j), jobs))
     objs = [j[1] for j in jobs]
     if _stale(LIB, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs), "-lz", "-lpthread"])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs), "-lz", "-lpthread", "-ldl"])
         if verbose:
             print(f"built {LIB}")
     cli_srcs = [CSRC / s for s in CLI_SRCS if (CSRC / s).exists()]
@@ -81,7 +81,7 @@ def build(verbose: bool = False) -> Path:
             cli_objs.append(o)
         if _stale(CLI, cli_objs + [LIB]):
             _run([HIPCC, "-o", str(CLI), *map(str, cli_objs), f"-L{PKG}", "-lopenge_hip",
-                  f"-Wl,-rpath,$ORIGIN", "-lz", "-lpthread"])
+                  f"-Wl,-rpath,$ORIGIN", "-lz", "-lpthread", "-ldl"])
     return LIB
 
 

@@ -1,8 +1,10 @@
 // bamio.cpp -- host BGZF/BAM codec (see bamio.h for the reference interfaces replaced).
 #include "bamio.h"
 
+#include <dlfcn.h>
 #include <zlib.h>
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <cstring>
 #include <sstream>
@@ -29,6 +31,62 @@ static void parallel_for(size_t n, int threads, F f) {
         });
     for (auto &th : ts) th.join();
 }
+
+// ---------------- DEFLATE engine ----------------
+// libdeflate (the image's libdeflate.so.0, loaded at run time) when present: 2-3x zlib's speed for
+// both directions.  Compressed bytes are not part of parity, records are.
+// OGE_BGZF_CODEC=zlib forces zlib.
+struct LibDeflate {
+    bool ok = false;
+    void *(*alloc_c)(int) = nullptr;
+    size_t (*compress)(void *, const void *, size_t, void *, size_t) = nullptr;
+    void (*free_c)(void *) = nullptr;
+    void *(*alloc_d)() = nullptr;
+    int (*decompress)(void *, const void *, size_t, void *, size_t, size_t *) = nullptr;
+    void (*free_d)(void *) = nullptr;
+    uint32_t (*crc32)(uint32_t, const void *, size_t) = nullptr;
+};
+
+static const LibDeflate &libdeflate() {
+    static LibDeflate L = [] {
+        LibDeflate l;
+        const char *env = getenv("OGE_BGZF_CODEC");
+        if (env && std::string(env) == "zlib") return l;
+        void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return l;
+        l.alloc_c = (void *(*)(int))dlsym(h, "libdeflate_alloc_compressor");
+        l.compress = (size_t(*)(void *, const void *, size_t, void *, size_t))dlsym(h, "libdeflate_deflate_compress");
+        l.free_c = (void (*)(void *))dlsym(h, "libdeflate_free_compressor");
+        l.alloc_d = (void *(*)())dlsym(h, "libdeflate_alloc_decompressor");
+        l.decompress = (int (*)(void *, const void *, size_t, void *, size_t, size_t *))dlsym(h, "libdeflate_deflate_decompress");
+        l.free_d = (void (*)(void *))dlsym(h, "libdeflate_free_decompressor");
+        l.crc32 = (uint32_t(*)(uint32_t, const void *, size_t))dlsym(h, "libdeflate_crc32");
+        l.ok = l.alloc_c && l.compress && l.free_c && l.alloc_d && l.decompress && l.free_d && l.crc32;
+        return l;
+    }();
+    return L;
+}
+
+static uint32_t block_crc(const uint8_t *p, size_t n) {
+    const LibDeflate &L = libdeflate();
+    return L.ok ? L.crc32(0, p, n) : (uint32_t)crc32(0L, p, (uInt)n);
+}
+
+// thread-local libdeflate handles (allocation is not free; one per worker thread and level)
+struct DeflateTls {
+    void *comp[10] = {nullptr};
+    void *decomp = nullptr;
+    ~DeflateTls() {
+        const LibDeflate &L = libdeflate();
+        if (!L.ok) return;
+        for (void *c : comp)
+            if (c) L.free_c(c);
+        if (decomp) L.free_d(decomp);
+    }
+};
+static thread_local DeflateTls tls_deflate;
+
+const char *bgzf_codec_name() { return libdeflate().ok ? "libdeflate" : "zlib"; }
 
 // ---------------- BGZF inflate ----------------
 bool bgzf_inflate_all(const uint8_t *src, size_t n, std::vector<uint8_t> &out, int threads, std::string &err) {
@@ -61,6 +119,16 @@ bool bgzf_inflate_all(const uint8_t *src, size_t n, std::vector<uint8_t> &out, i
     parallel_for(blocks.size(), threads, [&](size_t i) {
         const Blk &b = blocks[i];
         if (b.dlen == 0) return;
+        const LibDeflate &LD = libdeflate();
+        if (LD.ok) {
+            if (!tls_deflate.decomp) tls_deflate.decomp = LD.alloc_d();
+            size_t got = 0;
+            int rc = LD.decompress(tls_deflate.decomp, src + b.cdata, b.coff + b.clen - 8 - b.cdata, out.data() + b.uoff,
+                                   b.dlen, &got);
+            if (rc != 0 || got != b.dlen || block_crc(out.data() + b.uoff, b.dlen) != rd32(src + b.coff + b.clen - 8))
+                ok = false;
+            return;
+        }
         z_stream zs;
         memset(&zs, 0, sizeof(zs));
         if (inflateInit2(&zs, -15) != Z_OK) { ok = false; return; }
@@ -89,22 +157,31 @@ BgzfWriter::~BgzfWriter() { if (!closed_) close(); }
 static void bgzf_block(const uint8_t *src, size_t n, int level, std::vector<uint8_t> &dst) {
     size_t bound = compressBound((uLong)n) + 64;
     dst.resize(18 + bound + 8);
-    z_stream zs;
-    memset(&zs, 0, sizeof(zs));
-    deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
-    zs.next_in = (Bytef *)src;
-    zs.avail_in = (uInt)n;
-    zs.next_out = dst.data() + 18;
-    zs.avail_out = (uInt)bound;
-    deflate(&zs, Z_FINISH);
-    size_t clen = zs.total_out;
-    deflateEnd(&zs);
+    size_t clen = 0;
+    const LibDeflate &LD = libdeflate();
+    level = std::max(0, std::min(9, level));
+    if (LD.ok) {
+        if (!tls_deflate.comp[level]) tls_deflate.comp[level] = LD.alloc_c(level);
+        clen = LD.compress(tls_deflate.comp[level], src, n, dst.data() + 18, bound);
+    }
+    if (!clen) {
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+        zs.next_in = (Bytef *)src;
+        zs.avail_in = (uInt)n;
+        zs.next_out = dst.data() + 18;
+        zs.avail_out = (uInt)bound;
+        deflate(&zs, Z_FINISH);
+        clen = zs.total_out;
+        deflateEnd(&zs);
+    }
     size_t bsize = 18 + clen + 8;
     static const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0};
     memcpy(dst.data(), hdr, 16);
     dst[16] = (uint8_t)((bsize - 1) & 0xff);
     dst[17] = (uint8_t)((bsize - 1) >> 8);
-    uint32_t crc = (uint32_t)crc32(0L, src, (uInt)n);
+    uint32_t crc = n ? block_crc(src, n) : 0;
     memcpy(dst.data() + 18 + clen, &crc, 4);
     uint32_t isz = (uint32_t)n;
     memcpy(dst.data() + 18 + clen + 4, &isz, 4);
@@ -114,7 +191,7 @@ static void bgzf_block(const uint8_t *src, size_t n, int level, std::vector<uint
 void BgzfWriter::write(const void *data, size_t n) {
     const uint8_t *p = (const uint8_t *)data;
     pending_.insert(pending_.end(), p, p + n);
-    if (pending_.size() >= kBlockPayload * (size_t)std::max(1, threads_) * 4) flush_blocks(false);
+    if (pending_.size() >= kBlockPayload * (size_t)std::max(1, threads_) * 64) flush_blocks(false);
 }
 
 void BgzfWriter::flush_blocks(bool final) {
@@ -319,9 +396,20 @@ bool bam_read_file(const std::string &path, BamFile &out, int threads, std::stri
     FILE *f = (path == "-" || path == "stdin") ? stdin : fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
     std::vector<uint8_t> comp;
-    uint8_t buf[1 << 16];
-    size_t r;
-    while ((r = fread(buf, 1, sizeof(buf), f)) > 0) comp.insert(comp.end(), buf, buf + r);
+    if (f != stdin && fseeko(f, 0, SEEK_END) == 0) {  // regular file: one read into a sized buffer
+        off_t sz = ftello(f);
+        fseeko(f, 0, SEEK_SET);
+        comp.resize(sz > 0 ? (size_t)sz : 0);
+        if (sz > 0 && fread(comp.data(), 1, comp.size(), f) != comp.size()) {
+            fclose(f);
+            err = "short read on " + path;
+            return false;
+        }
+    } else {
+        uint8_t buf[1 << 16];
+        size_t r;
+        while ((r = fread(buf, 1, sizeof(buf), f)) > 0) comp.insert(comp.end(), buf, buf + r);
+    }
     if (f != stdin) fclose(f);
     std::vector<uint8_t> raw;
     if (!bgzf_inflate_all(comp.data(), comp.size(), raw, threads, err)) return false;

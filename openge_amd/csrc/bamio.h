@@ -20,6 +20,7 @@ namespace oge {
 // Inflate an entire BGZF byte string (any number of blocks) into `out`, in parallel.
 // Returns false and fills `err` on a malformed or truncated stream.
 bool bgzf_inflate_all(const uint8_t *src, size_t n, std::vector<uint8_t> &out, int threads, std::string &err);
+const char *bgzf_codec_name();  // "libdeflate" or "zlib"
 
 class BgzfWriter {
 public:
