@@ -18,6 +18,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <set>
 #include <thread>
 #include <unordered_map>
@@ -69,7 +70,7 @@ bool rread_decode(const uint8_t *rec, RRead &r, std::string &err) {
         return false;
     }
     const uint8_t *p = rec + OGE_OFF_NAME;
-    r.name.assign((const char *)p, lname ? lname - 1 : 0);
+    r.name = std::string_view((const char *)p, lname ? lname - 1 : 0);
     p += lname;
     r.cigar.resize(nc);
     for (uint32_t i = 0; i < nc; ++i) {
@@ -78,11 +79,14 @@ bool rread_decode(const uint8_t *rec, RRead &r, std::string &err) {
         r.cigar[i].n = op >> 4;
     }
     p += 4 * nc;
-    r.seq4.assign((const char *)p, (r.l_seq + 1) / 2);
+    r.seq4 = std::string_view((const char *)p, (r.l_seq + 1) / 2);
     p += (r.l_seq + 1) / 2;
-    r.qual.assign((const char *)p, r.l_seq);
+    r.qual = std::string_view((const char *)p, r.l_seq);
     p += r.l_seq;
-    r.tags.assign((const char *)p, (size_t)(rec + 4 + bs - p));
+    r.tags_in = std::string_view((const char *)p, (size_t)(rec + 4 + bs - p));
+    r.tags_own.clear();
+    r.tags_owned = false;
+    r.mq_add = -1;
     return true;
 }
 
@@ -92,18 +96,22 @@ static uint32_t cig_code(char t) {
 }
 
 // BamSerializer::write (util/bam_serializer.h:105-147): block size from the char data, bin
-// recomputed from pos and GetEndPosition (M, D, N, =, X).
-void rread_encode(const RRead &r, std::vector<uint8_t> &out) {
+// recomputed from pos and GetEndPosition (M, D, N, =, X).  A pending mate-fixer MQ lands last, where
+// AddTag would have put it.
+size_t rread_encoded_size(const RRead &r) {
+    return 36 + r.name.size() + 1 + 4 * r.cigar.size() + r.seq4.size() + r.qual.size() + r.tags().size() +
+           (r.mq_add >= 0 ? 5 : 0);
+}
+
+void rread_encode_to(const RRead &r, uint8_t *p) {
     const uint32_t lname = (uint32_t)r.name.size() + 1;
     const uint32_t nc = (uint32_t)r.cigar.size();
-    const uint32_t bs = 32 + lname + 4 * nc + (uint32_t)r.seq4.size() + (uint32_t)r.qual.size() + (uint32_t)r.tags.size();
+    const std::string_view tags = r.tags();
+    const uint32_t bs = (uint32_t)rread_encoded_size(r) - 4;
     int32_t end = r.pos;
     for (auto &c : r.cigar)
         if (c.t == 'M' || c.t == 'D' || c.t == 'N' || c.t == '=' || c.t == 'X') end += (int32_t)c.n;
     const uint32_t bin = oge_reg2bin(r.pos, end);
-    size_t o = out.size();
-    out.resize(o + 4 + bs);
-    uint8_t *p = out.data() + o;
     uint32_t core[9];
     core[0] = bs;
     core[1] = (uint32_t)r.ref;
@@ -128,7 +136,21 @@ void rread_encode(const RRead &r, std::vector<uint8_t> &out) {
     p += r.seq4.size();
     memcpy(p, r.qual.data(), r.qual.size());
     p += r.qual.size();
-    memcpy(p, r.tags.data(), r.tags.size());
+    memcpy(p, tags.data(), tags.size());
+    p += tags.size();
+    if (r.mq_add >= 0) {
+        p[0] = 'M';
+        p[1] = 'Q';
+        p[2] = 'S';
+        p[3] = (uint8_t)(r.mq_add & 0xFF);
+        p[4] = (uint8_t)((r.mq_add >> 8) & 0xFF);
+    }
+}
+
+void rread_encode(const RRead &r, std::vector<uint8_t> &out) {
+    size_t o = out.size();
+    out.resize(o + rread_encoded_size(r));
+    rread_encode_to(r, out.data() + o);
 }
 
 std::string cigar_to_string(const Cigar &c) {
@@ -139,7 +161,7 @@ std::string cigar_to_string(const Cigar &c) {
 
 // =====================================================================================  tags
 // Walk of BamAlignment::FindTag / SkipToNextTag (util/bamtools/BamAlignment.cpp).
-static size_t tag_value_len(const std::string &t, size_t at /* index of the type byte */) {
+static size_t tag_value_len(std::string_view t, size_t at /* index of the type byte */) {
     char ty = t[at];
     size_t v = at + 1;
     switch (ty) {
@@ -148,7 +170,7 @@ static size_t tag_value_len(const std::string &t, size_t at /* index of the type
         case 'i': case 'I': case 'f': return 4;
         case 'Z': case 'H': {
             size_t e = t.find('\0', v);
-            return (e == std::string::npos ? t.size() : e + 1) - v;
+            return (e == std::string_view::npos ? t.size() : e + 1) - v;
         }
         case 'B': {
             if (v + 5 > t.size()) return t.size() - v;
@@ -162,7 +184,7 @@ static size_t tag_value_len(const std::string &t, size_t at /* index of the type
     }
 }
 
-bool tag_find(const std::string &t, const char *tag, size_t *at, size_t *len) {
+bool tag_find(std::string_view t, const char *tag, size_t *at, size_t *len) {
     size_t p = 0;
     while (p + 3 <= t.size()) {
         size_t vl = tag_value_len(t, p + 2);
@@ -201,7 +223,7 @@ void tag_remove(std::string &t, const char *tag) {
     if (tag_find(t, tag, &at, &len)) t.erase(at, len);
 }
 
-static bool tag_get_string(const std::string &t, const char *tag, std::string &v) {
+static bool tag_get_string(std::string_view t, const char *tag, std::string &v) {
     size_t at, len;
     if (!tag_find(t, tag, &at, &len) || t[at + 2] != 'Z') return false;
     v.assign(t.data() + at + 3, len > 4 ? len - 4 : 0);
@@ -740,6 +762,75 @@ struct ByPos {  // Sort::ByPosition (util/bamtools/Sort.h:116-133); idx stands i
 };
 
 // =====================================================================================  phase E
+// The writer's waitingReads multiset (ConstrainedMateFixingManager.h:94) as a binary heap.  Entries
+// the comparator calls equivalent (only unmapped refID -1 reads; everything else is ordered down to
+// idx) leave in insertion order, as they would from the multiset's upper-bound inserts.  The
+// (refID, pos, strand) part of the comparison is cached in `key`; none of those fields changes
+// while a read waits (setMateInfo moves an unmapped read only after the requeue erase).
+class WaitQueue {
+public:
+    bool empty() const { return h_.empty(); }
+    size_t size() const { return h_.size(); }
+    RRead *top() const { return h_.front().r; }
+    void insert(RRead *r) {
+        h_.push_back({key(*r), seq_++, r});
+        std::push_heap(h_.begin(), h_.end(), After());
+    }
+    RRead *pop() {
+        std::pop_heap(h_.begin(), h_.end(), After());
+        RRead *r = h_.back().r;
+        h_.pop_back();
+        return r;
+    }
+    // multiset::count / erase by key: every entry equivalent to r under ByPosition
+    size_t count(const RRead *r) const {
+        const uint64_t k = key(*r);
+        size_t c = 0;
+        for (auto &e : h_) c += equivalent(e, k, r);
+        return c;
+    }
+    size_t erase(const RRead *r) {
+        const uint64_t k = key(*r);
+        size_t before = h_.size();
+        h_.erase(std::remove_if(h_.begin(), h_.end(), [&](const Entry &e) { return equivalent(e, k, r); }), h_.end());
+        if (h_.size() != before) std::make_heap(h_.begin(), h_.end(), After());
+        return before - h_.size();
+    }
+
+private:
+    struct Entry {
+        uint64_t key, seq;
+        RRead *r;
+    };
+    // Sort::ByPosition (util/bamtools/Sort.h:116-133): refID -1 sorts last and ties with itself
+    static uint64_t key(const RRead &r) {
+        if (r.ref == -1) return ~0ull;
+        return ((uint64_t)(uint32_t)r.ref << 33) | ((uint64_t)(uint32_t)(r.pos + 1) << 1) | (r.rev() ? 1u : 0u);
+    }
+    static int tail_cmp(const RRead &a, const RRead &b) {  // name, flag, idx (Q10)
+        int c = a.name.compare(b.name);
+        if (c) return c;
+        if (a.flag != b.flag) return a.flag < b.flag ? -1 : 1;
+        if (a.idx != b.idx) return a.idx < b.idx ? -1 : 1;
+        return 0;
+    }
+    static bool equivalent(const Entry &e, uint64_t k, const RRead *r) {
+        return e.key == k && (k == ~0ull || tail_cmp(*e.r, *r) == 0);
+    }
+    struct After {  // heap order: true when a leaves after b
+        bool operator()(const Entry &a, const Entry &b) const {
+            if (a.key != b.key) return a.key > b.key;
+            if (a.key != ~0ull) {
+                int c = tail_cmp(*a.r, *b.r);
+                if (c) return c > 0;
+            }
+            return a.seq > b.seq;
+        }
+    };
+    std::vector<Entry> h_;
+    uint64_t seq_ = 0;
+};
+
 // ConstrainedMateFixingManager (util/gatk/ConstrainedMateFixingManager.cpp), run in stream order.
 class MateFixer {
 public:
@@ -753,7 +844,7 @@ public:
 
     void add(RRead *nr, bool modified, bool canFlush) {  // addReadInternal (:312-419)
         const bool tooMany = waiting_.size() >= (size_t)P_.max_records_in_memory;
-        if ((canFlush && tooMany) || (!waiting_.empty() && (*waiting_.begin())->ref != nr->ref)) {
+        if ((canFlush && tooMany) || (!waiting_.empty() && waiting_.top()->ref != nr->ref)) {
             while (waiting_.size() > 1) write(pop());
             RRead *last = pop();
             if (last->ref == -1) {
@@ -785,7 +876,7 @@ public:
         waiting_.insert(nr);
         if (++counter_ % 1000 == 0) {  // EMIT_FREQUENCY (ConstrainedMateFixingManager.h:66)
             while (!waiting_.empty()) {
-                RRead *r = *waiting_.begin();
+                RRead *r = waiting_.top();
                 if (cannot_move_before(r->pos, *nr) && (!movable(*r) || cannot_move_before(r->mpos, *nr))) {
                     mates_.erase(r->name);
                     write(pop());
@@ -810,12 +901,7 @@ private:
     bool movable(const RRead &r) const {  // pairedReadIsMovable (:449-454)
         return r.paired() && (r.mapped() || r.mate_mapped()) && !too_big(r);
     }
-    RRead *pop() {
-        auto it = waiting_.begin();
-        RRead *r = *it;
-        waiting_.erase(it);
-        return r;
-    }
+    RRead *pop() { return waiting_.pop(); }
     void write(RRead *r) { out_.push_back(r); }
     void purge_unmodified() {
         for (auto it = mates_.begin(); it != mates_.end();) {
@@ -837,27 +923,36 @@ private:
         return p2 - p1 + ((p2 >= p1) ? 1 : -1);
     }
     static void set_flag(RRead &r, uint16_t bit, bool on) { r.flag = on ? (r.flag | bit) : (r.flag & ~bit); }
+    // AddTag("MQ", "S", ...) deferred to encode (nothing edits tags after the mate fixer), so the
+    // common case copies no tag bytes; RemoveTag("MQ") drops a pending one first.
+    static void add_mq(RRead &r, uint16_t mq) {
+        if (r.mq_add < 0 && !tag_find(r.tags(), "MQ", nullptr, nullptr)) r.mq_add = mq;
+    }
+    static void remove_mq(RRead &r) {
+        if (r.mq_add >= 0) r.mq_add = -1;
+        else if (tag_find(r.tags(), "MQ", nullptr, nullptr)) tag_remove(r.tags_mut(), "MQ");
+    }
     static void set_mate_info(RRead &r1, RRead &r2) {  // setMateInfo (:143-201)
         if (r1.mapped() && r2.mapped()) {
             r1.mref = r2.mref;  // Q22: the mate's mate reference, not its reference
             r1.mpos = r2.pos;
             set_flag(r1, 0x20, r2.rev());
             set_flag(r1, 0x8, false);
-            tag_add_int(r1.tags, "MQ", 'S', r2.mapq, 2);
+            add_mq(r1, r2.mapq);
             r2.mref = r1.ref;
             r2.mpos = r1.pos;
             set_flag(r2, 0x20, r1.rev());
             set_flag(r2, 0x8, false);
-            tag_add_int(r2.tags, "MQ", 'S', r1.mapq, 2);
+            add_mq(r2, r1.mapq);
         } else if (!r1.mapped() && !r2.mapped()) {
             r1.ref = -1; r1.pos = -1; r1.mref = -1; r1.mpos = -1;
             set_flag(r1, 0x20, r2.rev());
             set_flag(r1, 0x8, true);
-            tag_remove(r2.tags, "MQ");
+            remove_mq(r2);
             r2.ref = -1; r2.pos = -1; r2.mref = -1; r2.mpos = -1;
             set_flag(r2, 0x20, r1.rev());
             set_flag(r2, 0x8, false);
-            tag_remove(r2.tags, "MQ");
+            remove_mq(r2);
         } else {
             RRead &m = r1.mapped() ? r1 : r2;
             RRead &u = r1.mapped() ? r2 : r1;
@@ -881,8 +976,8 @@ private:
 
     const RealignParams &P_;
     std::vector<RRead *> &out_;
-    std::multiset<RRead *, ByPos> waiting_;
-    std::map<std::string, std::pair<RRead *, bool>> mates_;
+    WaitQueue waiting_;
+    std::unordered_map<std::string_view, std::pair<RRead *, bool>> mates_;
     GLoc last_;
     bool hasLast_ = false;
     uint64_t counter_ = 0;
@@ -956,14 +1051,14 @@ static bool parse_intervals(const std::string &path, const std::vector<std::stri
 // doNotTryToClean (:555-575)
 static bool do_not_clean(const RRead &r, const RealignParams &P) {
     std::string rg;
-    bool is454 = tag_get_string(r.tags, "RG", rg) && rg.find("454") != std::string::npos;
+    bool is454 = tag_get_string(r.tags(), "RG", rg) && rg.find("454") != std::string::npos;
     bool tooBig = (r.paired() && r.mapped() && r.ref != r.mref) || std::abs((int)r.l_seq) > P.max_isize_for_movement;
     return !r.mapped() || (r.flag & 0x100) || (r.flag & 0x200) || r.mapq == 0 || r.pos == -1 || tooBig || is454;
 }
 
 int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, const uint64_t *offs, uint64_t n,
                 const std::string &fasta_path, const std::string &intervals_path, const RealignParams &P, const ScanFn &scan,
-                std::vector<uint8_t> &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err) {
+                ByteBuf &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err) {
     double t0 = now_s();
     Fasta fa;
     if (!fa.load(fasta_path, err)) return -4;
@@ -971,32 +1066,58 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     if (!parse_intervals(intervals_path, ref_names, ivs, err)) return -1;
     st.intervals = ivs.size();
 
-    std::vector<RRead> reads(n);
+    const double tf = now_s();
+    // decoded records, constructed (first-touched) and destroyed by the worker threads
+    const uint64_t dchunk = 4096;
+    struct ReadArray {
+        RRead *p;
+        uint64_t n;
+        int threads;
+        ~ReadArray() {
+            par_for((n + dchunk - 1) / dchunk, threads, [&](size_t c) {
+                for (uint64_t i = c * dchunk, e = std::min<uint64_t>(n, i + dchunk); i < e; ++i) p[i].~RRead();
+            });
+            std::free(p);
+        }
+        RRead &operator[](uint64_t i) { return p[i]; }
+    };
+    RRead *rmem = (RRead *)std::malloc(std::max<uint64_t>(n, 1) * sizeof(RRead));
+    if (!rmem) {
+        err = "out of host memory for the decoded records";
+        return -1;
+    }
+    ReadArray reads{rmem, 0, P.threads};
+    par_for((n + dchunk - 1) / dchunk, P.threads, [&](size_t c) {
+        for (uint64_t i = c * dchunk, end = std::min<uint64_t>(n, i + dchunk); i < end; ++i) new (&rmem[i]) RRead();
+    });
+    reads.n = n;
     std::atomic<bool> bad(false);
     std::mutex emu;
     std::string derr;
-    par_for(n, P.threads, [&](size_t i) {
+    par_for((n + dchunk - 1) / dchunk, P.threads, [&](size_t c) {
         std::string e;
-        if (!rread_decode(recs + offs[i], reads[i], e)) {
-            std::lock_guard<std::mutex> g(emu);
-            bad = true;
-            derr = e;
+        for (uint64_t i = c * dchunk, end = std::min<uint64_t>(n, i + dchunk); i < end; ++i) {
+            if (!rread_decode(recs + offs[i], reads[i], e)) {
+                std::lock_guard<std::mutex> g(emu);
+                bad = true;
+                derr = e;
+            }
+            reads[i].idx = (uint32_t)i;
         }
-        reads[i].idx = (uint32_t)i;
     });
     if (bad) {
         err = derr;
         return -1;
     }
-    uint64_t in_bytes = 0;
     for (uint64_t i = 0; i < n; ++i) {
-        in_bytes += 4 + rd32(recs + offs[i]);
         if (reads[i].ref < -1 || reads[i].ref >= (int)ref_names.size()) {
             err = "record refID outside the sequence dictionary";
             return -1;
         }
     }
 
+    const double td = now_s();
+    if (getenv("OGE_RL_DEBUG")) fprintf(stderr, "fasta+intervals %.3f decode %.3f\n", tf - t0, td - tf);
     // ---------------------------------------------------------------- A: map_func (:455-553)
     std::vector<std::unique_ptr<IntervalData>> ids;
     std::vector<Event> ev;
@@ -1203,8 +1324,8 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
             int ns = a.newStart == -1 ? u.pos : a.newStart;
             if (a.newStart != -1 && std::abs(a.newStart - u.pos) > P.max_pos_move_allowed) continue;
             if (!P.no_original_alignment_tags) {
-                tag_add_string(u.tags, "OC", cigar_to_string(u.cigar));
-                if (ns != u.pos) tag_add_int(u.tags, "OP", 'i', u.pos + 1, 4);
+                tag_add_string(u.tags_mut(), "OC", cigar_to_string(u.cigar));
+                if (ns != u.pos) tag_add_int(u.tags_mut(), "OP", 'i', u.pos + 1, 4);
             }
             u.cigar = a.newCigar;
             u.pos = ns;
@@ -1222,9 +1343,9 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
             }
             int nm, uq;
             nm_uq(u, reference, leftmost, &nm, &uq);
-            if (tag_find(u.tags, "NM", nullptr, nullptr)) tag_edit_i32(u.tags, "NM", nm);
-            if (tag_find(u.tags, "UQ", nullptr, nullptr)) tag_edit_i32(u.tags, "UQ", uq);
-            tag_remove(u.tags, "MD");
+            if (tag_find(u.tags(), "NM", nullptr, nullptr)) tag_edit_i32(u.tags_mut(), "NM", nm);
+            if (tag_find(u.tags(), "UQ", nullptr, nullptr)) tag_edit_i32(u.tags_mut(), "UQ", uq);
+            if (tag_find(u.tags(), "MD", nullptr, nullptr)) tag_remove(u.tags_mut(), "MD");
             d.pending.push_back(std::make_pair(a.read, std::move(u)));
         }
         d.cleanable = true;
@@ -1262,16 +1383,23 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         for (RRead *r : lst) mf.add(r, cleaned.count(r) > 0, false);
     }
     mf.close();
+    if (getenv("OGE_RL_DEBUG")) fprintf(stderr, "mate fixing %.3f\n", now_s() - t4);
     if (order.size() != n) {
         err = "internal: emitted " + std::to_string(order.size()) + " of " + std::to_string(n) + " records";
         return -1;
     }
-    out.reserve(out.size() + in_bytes + n * 16);
-    for (RRead *r : order) {
-        out_off.push_back(out.size());
-        rread_encode(*r, out);
+    out_off.assign(n + 1, 0);
+    for (uint64_t i = 0; i < n; ++i) out_off[i + 1] = rread_encoded_size(*order[i]);
+    for (uint64_t i = 0; i < n; ++i) out_off[i + 1] += out_off[i];
+    if (!out.alloc(out_off[n])) {
+        err = "out of host memory for the output records";
+        return -1;
     }
-    out_off.push_back(out.size());
+    const uint64_t chunk = 4096;
+    par_for((n + chunk - 1) / chunk, P.threads, [&](size_t c) {
+        for (uint64_t i = c * chunk, e = std::min<uint64_t>(n, i + chunk); i < e; ++i)
+            rread_encode_to(*order[i], out.data() + out_off[i]);
+    });
     st.t_emit = now_s() - t4;
     return 0;
 }

@@ -14,7 +14,10 @@
 #pragma once
 #include <cstdint>
 #include <functional>
+#include <cstdlib>
+#include <cstring>
 #include <string>
+#include <string_view>
 #include <vector>
 
 namespace oge {
@@ -24,19 +27,116 @@ struct CigOp {
     uint32_t n;
     bool operator==(const CigOp &o) const { return t == o.t && n == o.n; }
 };
-typedef std::vector<CigOp> Cigar;
+
+// CIGAR with inline room for 4 operations (nearly every short-read alignment), so decoding millions
+// of records does not allocate.
+class Cigar {
+public:
+    Cigar() = default;
+    Cigar(const Cigar &o) { assign(o.begin(), o.end()); }
+    Cigar(Cigar &&o) noexcept { take(o); }
+    ~Cigar() { delete[] heap_; }
+    Cigar &operator=(const Cigar &o) {
+        if (this != &o) assign(o.begin(), o.end());
+        return *this;
+    }
+    Cigar &operator=(Cigar &&o) noexcept {
+        if (this != &o) {
+            delete[] heap_;
+            heap_ = nullptr;
+            take(o);
+        }
+        return *this;
+    }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    CigOp *begin() { return data(); }
+    CigOp *end() { return data() + n_; }
+    const CigOp *begin() const { return data(); }
+    const CigOp *end() const { return data() + n_; }
+    CigOp &operator[](size_t i) { return data()[i]; }
+    const CigOp &operator[](size_t i) const { return data()[i]; }
+    CigOp &back() { return data()[n_ - 1]; }
+    void clear() { n_ = 0; }
+    void reserve(size_t c) {
+        if (c <= cap_) return;
+        CigOp *h = new CigOp[c];
+        std::memcpy((void *)h, (const void *)data(), n_ * sizeof(CigOp));
+        delete[] heap_;
+        heap_ = h;
+        cap_ = (uint32_t)c;
+    }
+    void resize(size_t c) {
+        reserve(c);
+        n_ = (uint32_t)c;
+    }
+    void push_back(const CigOp &x) {
+        if (n_ == cap_) reserve(2 * cap_);
+        data()[n_++] = x;
+    }
+    void insert(CigOp *at, const CigOp *first, const CigOp *last) {  // append form only
+        (void)at;
+        for (; first != last; ++first) push_back(*first);
+    }
+    bool operator==(const Cigar &o) const {
+        if (n_ != o.n_) return false;
+        for (uint32_t i = 0; i < n_; ++i)
+            if (!(data()[i] == o.data()[i])) return false;
+        return true;
+    }
+    bool operator!=(const Cigar &o) const { return !(*this == o); }
+
+private:
+    CigOp *data() { return heap_ ? heap_ : inl_; }
+    const CigOp *data() const { return heap_ ? heap_ : inl_; }
+    void assign(const CigOp *f, const CigOp *l) {
+        n_ = 0;
+        reserve((size_t)(l - f));
+        for (; f != l; ++f) data()[n_++] = *f;
+    }
+    void take(Cigar &o) {
+        n_ = o.n_;
+        cap_ = o.cap_;
+        if (o.heap_) {
+            heap_ = o.heap_;
+            o.heap_ = nullptr;
+        } else {
+            std::memcpy((void *)inl_, (const void *)o.inl_, n_ * sizeof(CigOp));
+        }
+        o.n_ = 0;
+        o.cap_ = kInline;
+    }
+    static constexpr uint32_t kInline = 4;
+    CigOp inl_[kInline];
+    CigOp *heap_ = nullptr;
+    uint32_t n_ = 0, cap_ = kInline;
+};
 
 // One BAM record, decoded into mutable fields (the OGERead/BamAlignment state the reference edits).
+// Fields the realigner never changes (name, bases, qualities) are views into the input record, which
+// outlives the run; tags are viewed until the first edit copies them.
 struct RRead {
     int32_t ref = -1, pos = -1, mref = -1, mpos = -1, tlen = 0;
     uint16_t mapq = 0, flag = 0;
-    std::string name;          // without the NUL
+    std::string_view name;     // without the NUL
     Cigar cigar;
     uint32_t l_seq = 0;
-    std::string seq4;          // packed 4-bit bases (BAM layout)
-    std::string qual;          // raw phred bytes (BAM layout)
-    std::string tags;          // raw tag bytes
+    std::string_view seq4;     // packed 4-bit bases (BAM layout)
+    std::string_view qual;     // raw phred bytes (BAM layout)
+    std::string_view tags_in;  // raw tag bytes of the input record
+    std::string tags_own;      // edited tag bytes (valid when tags_owned)
+    bool tags_owned = false;
+    int32_t mq_add = -1;       // MQ:S value appended at encode (the mate fixer's AddTag("MQ")), -1 = none
     uint32_t idx = 0;          // input order (stands in for the reference's heap-address tie-break)
+
+    std::string_view tags() const { return tags_owned ? std::string_view(tags_own) : tags_in; }
+    std::string &tags_mut() {
+        if (!tags_owned) {
+            tags_own.assign(tags_in.data(), tags_in.size());
+            tags_owned = true;
+        }
+        return tags_own;
+    }
 
     bool mapped() const { return !(flag & 0x4); }
     bool paired() const { return flag & 0x1; }
@@ -49,9 +149,11 @@ struct RRead {
 
 bool rread_decode(const uint8_t *rec, RRead &r, std::string &err);
 void rread_encode(const RRead &r, std::vector<uint8_t> &out);  // appends; bin recomputed (W1)
+size_t rread_encoded_size(const RRead &r);
+void rread_encode_to(const RRead &r, uint8_t *p);  // writes rread_encoded_size(r) bytes
 
 // ---- tags (BamAlignment::AddTag / EditTag / RemoveTag semantics) ----
-bool tag_find(const std::string &tags, const char *tag, size_t *at, size_t *len);
+bool tag_find(std::string_view tags, const char *tag, size_t *at, size_t *len);
 bool tag_add_int(std::string &tags, const char *tag, char type, int64_t v, int bytes);  // no-op if present
 bool tag_add_string(std::string &tags, const char *tag, const std::string &v);
 void tag_remove(std::string &tags, const char *tag);
@@ -88,15 +190,37 @@ struct RealignParams {
 
 struct RealignStats {
     uint64_t intervals = 0, intervals_cleaned = 0, reads_realigned = 0, scan_pairs = 0, scan_ops = 0;
-    double t_bin = 0, t_prepare = 0, t_scan = 0, t_decide = 0, t_emit = 0;
+    double t_bin = 0, t_prepare = 0, t_scan = 0, t_decide = 0, t_emit = 0, t_run = 0;
+};
+
+// Output record bytes: malloc'ed without zero-fill so the parallel encoder's first touch is the only
+// pass over fresh pages.
+struct ByteBuf {
+    ByteBuf() = default;
+    ByteBuf(const ByteBuf &) = delete;
+    ByteBuf &operator=(const ByteBuf &) = delete;
+    ~ByteBuf() { std::free(p_); }
+    bool alloc(size_t n) {
+        std::free(p_);
+        p_ = (uint8_t *)std::malloc(n ? n : 1);
+        n_ = p_ ? n : 0;
+        return p_ != nullptr;
+    }
+    uint8_t *data() { return p_; }
+    const uint8_t *data() const { return p_; }
+    size_t size() const { return n_; }
+
+private:
+    uint8_t *p_ = nullptr;
+    size_t n_ = 0;
 };
 
 // Runs LocalRealignment over coordinate-sorted records.  `ref_names` = the BAM header's @SQ names
 // (sequence dictionary), `fasta` = path of the reference FASTA, `intervals` = path of the target
 // interval list ("chr:start-stop", 1-based).  Output records (encoded, in emission order) are
-// appended to `out`, their offsets to `out_off`.
+// written to `out`, their offsets (n + 1) to `out_off`.
 int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, const uint64_t *offs, uint64_t n,
                 const std::string &fasta, const std::string &intervals, const RealignParams &P, const ScanFn &scan,
-                std::vector<uint8_t> &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err);
+                ByteBuf &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err);
 
 }  // namespace oge

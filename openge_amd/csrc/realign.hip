@@ -251,7 +251,7 @@ static int realign_scan_host(oge_ctx *ctx, const uint8_t *cons, uint64_t cons_by
 }
 
 struct oge_realign_result {
-    std::vector<uint8_t> recs;
+    oge::ByteBuf recs;
     std::vector<uint64_t> offs;
     std::string stats;
 };
@@ -320,16 +320,18 @@ int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len,
     };
     std::unique_ptr<oge_realign_result> r(new oge_realign_result());
     oge::RealignStats st;
+    const auto tr0 = std::chrono::steady_clock::now();
     int rc = oge::realign_run(names, recs, rec_off, n, fasta_path, intervals_path, P, scan, r->recs, r->offs, st, err);
+    st.t_run = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
     if (rc) return scan_rc ? scan_rc : oge_fail(ctx, rc, ("oge_localrealign: " + err).c_str());
     char buf[1024];
     snprintf(buf, sizeof buf,
              "{\"intervals\": %llu, \"intervals_cleaned\": %llu, \"reads_realigned\": %llu, \"scan_pairs\": %llu, "
              "\"scan_ops\": %llu, \"scan_kernel_ms\": %.4f, \"t_bin\": %.4f, \"t_prepare\": %.4f, \"t_scan\": %.4f, "
-             "\"t_decide\": %.4f, \"t_emit\": %.4f}",
+             "\"t_decide\": %.4f, \"t_emit\": %.4f, \"t_run\": %.4f}",
              (unsigned long long)st.intervals, (unsigned long long)st.intervals_cleaned, (unsigned long long)st.reads_realigned,
              (unsigned long long)st.scan_pairs, (unsigned long long)st.scan_ops, scan_kernel_ms, st.t_bin, st.t_prepare,
-             st.t_scan, st.t_decide, st.t_emit);
+             st.t_scan, st.t_decide, st.t_emit, st.t_run);
     r->stats = buf;
     *out = r.release();
     return OGE_OK;

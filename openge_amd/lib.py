@@ -317,6 +317,19 @@ def write_bam(path, header_text: str, recs: np.ndarray, offs: np.ndarray, n: int
 
 
 # ------------------------------------------------------------------------- device context
+class _RealignResult:
+    """Owns an oge_realign_result; the record/offset arrays returned by Context.localrealign are
+    zero-copy views that keep it alive."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        if self.h:
+            lib().oge_realign_result_free(self.h)
+            self.h = None
+
+
 class Context:
     """A HIP device context (one per process/GPU)."""
 
@@ -396,23 +409,28 @@ class Context:
 
     def localrealign(self, header_text: str, recs: np.ndarray, offs: np.ndarray, n: int, fasta: str, intervals: str,
                      opts: RealignOpts | None = None) -> tuple[np.ndarray, np.ndarray, dict]:
-        """LocalRealignment over coordinate-sorted records -> (out recs, out offsets[n+1], stats)."""
+        """LocalRealignment over coordinate-sorted records -> (out recs, out offsets[n+1], stats).
+        The arrays are read-only-by-convention views of the library's result buffer (no copy)."""
         import json
         L = lib()
         hb = header_text.encode()
         res = C.c_void_p()
         check(L.oge_localrealign(self.h, hb, len(hb), _ptr(recs), _ptr(offs), n, fasta.encode(), intervals.encode(),
                                  C.byref(opts) if opts is not None else None, C.byref(res)), self.h)
-        try:
-            cnt = int(L.oge_realign_result_count(res))
-            nb = C.c_uint64()
-            rp = L.oge_realign_result_records(res, C.byref(nb))
-            out = np.ctypeslib.as_array((C.c_uint8 * nb.value).from_address(rp)).copy() if nb.value else np.zeros(0, np.uint8)
-            op = L.oge_realign_result_offsets(res)
-            oo = np.ctypeslib.as_array((C.c_uint64 * (cnt + 1)).from_address(op)).copy()
-            stats = json.loads(L.oge_realign_result_stats(res).decode())
-        finally:
-            L.oge_realign_result_free(res)
+        holder = _RealignResult(res)  # frees the result when the last view goes away
+        cnt = int(L.oge_realign_result_count(res))
+        nb = C.c_uint64()
+        rp = L.oge_realign_result_records(res, C.byref(nb))
+        stats = json.loads(L.oge_realign_result_stats(res).decode())
+        if nb.value:
+            ra = (C.c_uint8 * nb.value).from_address(rp)
+            ra._holder = holder
+            out = np.ctypeslib.as_array(ra)
+        else:
+            out = np.zeros(0, np.uint8)
+        oa = (C.c_uint64 * (cnt + 1)).from_address(L.oge_realign_result_offsets(res))
+        oa._holder = holder
+        oo = np.ctypeslib.as_array(oa)
         return out, oo, stats
 
     def synth_range_dev(self, p: SynthParams, slot0: int, nslots: int, d_offs: int, d_out: int | None) -> None:

@@ -5,6 +5,8 @@
 // CPU test suite can pin the host logic (binning, consensus generation, LOD/entropy decisions,
 // CIGAR/tag surgery, mate fixing) against the reference's own outputs without a GPU.  Never shipped;
 // the product library binds the GPU scan only.
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -18,9 +20,10 @@ extern "C" int oracle_realign_scan(const uint8_t *cons, const uint64_t *cons_off
                                    int32_t *best_index, int32_t *best_score);
 
 struct Out {
-    std::vector<uint8_t> recs;
+    oge::ByteBuf recs;
     std::vector<uint64_t> offs;
     std::string msg;
+    std::string stats;
 };
 
 extern "C" {
@@ -42,11 +45,18 @@ void *realign_cpu(const char *header, uint64_t hlen, const uint8_t *recs, const 
     };
     oge::RealignStats st;
     std::string err;
+    const auto tr0 = std::chrono::steady_clock::now();
     int rc = oge::realign_run(names, recs, offs, n, fasta, intervals, P, scan, o->recs, o->offs, st, err);
+    st.t_run = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
     if (rc) o->msg = err.empty() ? "realign failed" : err;
+    char b[512];
+    snprintf(b, sizeof b, "{\"t_bin\": %.3f, \"t_prepare\": %.3f, \"t_scan\": %.3f, \"t_decide\": %.3f, \"t_emit\": %.3f, \"t_run\": %.3f, \"scan_pairs\": %llu}",
+             st.t_bin, st.t_prepare, st.t_scan, st.t_decide, st.t_emit, st.t_run, (unsigned long long)st.scan_pairs);
+    o->stats = b;
     return o;
 }
 const char *realign_cpu_error(void *h) { return ((Out *)h)->msg.c_str(); }
+const char *realign_cpu_stats(void *h) { return ((Out *)h)->stats.c_str(); }
 uint64_t realign_cpu_count(void *h) { Out *o = (Out *)h; return o->offs.empty() ? 0 : o->offs.size() - 1; }
 const uint8_t *realign_cpu_records(void *h, uint64_t *bytes) { Out *o = (Out *)h; *bytes = o->recs.size(); return o->recs.data(); }
 const uint64_t *realign_cpu_offsets(void *h) { return ((Out *)h)->offs.data(); }
