@@ -10,6 +10,8 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <condition_variable>
+#include <functional>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -27,16 +29,113 @@
 
 namespace oge {
 
+// =====================================================================================  threads
+// Persistent workers for one realign_run.  run_static maps index i to worker i % size() in every
+// phase, so what a worker allocates for interval i (prepare, decide) it also frees (teardown): the
+// frees stay in that thread's malloc arena instead of contending for other threads' arena locks.
+class Pool {
+public:
+    explicit Pool(int threads) {
+        if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+        n_ = threads;
+        for (int t = 1; t < n_; ++t) ts_.emplace_back([this, t]() { loop(t); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : ts_) t.join();
+    }
+    int size() const { return n_; }
+    template <class F>
+    void run_static(size_t n, F f) {
+        if (n_ == 1 || n <= 1) {
+            for (size_t i = 0; i < n; ++i) f(i);
+            return;
+        }
+        exec([&](int t) {
+            for (size_t i = (size_t)t; i < n; i += (size_t)n_) f(i);
+        });
+    }
+    template <class F>
+    void run(size_t n, F f) {  // dynamic: indices handed out one at a time
+        if (n_ == 1 || n <= 1) {
+            for (size_t i = 0; i < n; ++i) f(i);
+            return;
+        }
+        std::atomic<size_t> next(0);
+        exec([&](int) {
+            for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+        });
+    }
+    template <class F>
+    void run_chunks(size_t n, size_t chunk, F f) {  // f(begin, end) over [0, n) in chunks
+        run((n + chunk - 1) / chunk, [&](size_t c) { f(c * chunk, std::min(n, (c + 1) * chunk)); });
+    }
+
+private:
+    void exec(const std::function<void(int)> &job) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &job;
+            busy_ = n_ - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        job(0);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [&] { return busy_ == 0; });
+        job_ = nullptr;
+    }
+    void loop(int id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)> *job;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                job = job_;
+            }
+            (*job)(id);
+            std::lock_guard<std::mutex> g(m_);
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    int n_ = 1;
+    std::vector<std::thread> ts_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    int busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 // =====================================================================================  records
 static const char kSeqChars[] = "=ACMGRSVTWYHKDBN";
 static const char kCigChars[] = "MIDNSHP=X";
 
+// packed byte -> its two base characters
+static const struct SeqPairs {
+    char p[256][2];
+    SeqPairs() {
+        for (int b = 0; b < 256; ++b) {
+            p[b][0] = kSeqChars[b >> 4];
+            p[b][1] = kSeqChars[b & 0xF];
+        }
+    }
+} kSeqPairs;
+
 std::string RRead::bases() const {
     std::string s(l_seq, 'N');
-    for (uint32_t i = 0; i < l_seq; ++i) {
-        uint8_t b = (uint8_t)seq4[i >> 1];
-        s[i] = kSeqChars[(i & 1) ? (b & 0xF) : (b >> 4)];
-    }
+    char *o = &s[0];
+    const uint32_t full = l_seq >> 1;
+    for (uint32_t k = 0; k < full; ++k) memcpy(o + 2 * k, kSeqPairs.p[(uint8_t)seq4[k]], 2);
+    if (l_seq & 1) o[l_seq - 1] = kSeqPairs.p[(uint8_t)seq4[full]][0];
     return s;
 }
 
@@ -84,9 +183,13 @@ bool rread_decode(const uint8_t *rec, RRead &r, std::string &err) {
     r.qual = std::string_view((const char *)p, r.l_seq);
     p += r.l_seq;
     r.tags_in = std::string_view((const char *)p, (size_t)(rec + 4 + bs - p));
+    uint32_t h = 2166136261u;
+    for (char ch : r.name) h = (h ^ (uint8_t)ch) * 16777619u;
+    r.name_hash = h;
     r.tags_own.clear();
     r.tags_owned = false;
     r.mq_add = -1;
+    r.cleaned = false;
     return true;
 }
 
@@ -241,34 +344,52 @@ static void tag_edit_i32(std::string &t, const char *tag, int32_t v) {
 // the raw bytes (case preserved).
 struct Fasta {
     std::unordered_map<std::string, std::string> seq;
-    bool load(const std::string &path, std::string &err) {
+    // Whole file in one read; contigs (">" lines) located serially, their bodies de-lined in
+    // parallel.  Line handling as FastaReader: name up to the first blank, CR before LF dropped.
+    bool load(const std::string &path, std::string &err, Pool &pool) {
         FILE *f = fopen(path.c_str(), "rb");
         if (!f) {
             err = "cannot open reference FASTA " + path;
             return false;
         }
         std::string data;
+        if (fseek(f, 0, SEEK_END) == 0) {
+            long sz = ftell(f);
+            if (sz > 0) {
+                data.resize((size_t)sz);
+                fseek(f, 0, SEEK_SET);
+                data.resize(fread(&data[0], 1, (size_t)sz, f));
+            }
+        }
         char buf[1 << 16];
         size_t k;
-        while ((k = fread(buf, 1, sizeof buf, f)) > 0) data.append(buf, k);
+        while ((k = fread(buf, 1, sizeof buf, f)) > 0) data.append(buf, k);  // non-seekable input
         fclose(f);
-        size_t p = 0;
-        std::string *cur = nullptr;
-        while (p < data.size()) {
-            size_t e = data.find('\n', p);
-            if (e == std::string::npos) e = data.size();
-            if (data[p] == '>') {
-                size_t ne = p + 1;
-                while (ne < e && data[ne] != ' ' && data[ne] != '\t' && data[ne] != '\r') ++ne;
-                cur = &seq[data.substr(p + 1, ne - p - 1)];
-                cur->clear();
-            } else if (cur) {
-                size_t ee = e;
-                if (ee > p && data[ee - 1] == '\r') --ee;
-                cur->append(data, p, ee - p);
+        std::vector<size_t> hs;
+        const char *b = data.data(), *e = b + data.size();
+        for (const char *q = b; q < e && (q = (const char *)memchr(q, '>', (size_t)(e - q))); ++q)
+            if (q == b || q[-1] == '\n') hs.push_back((size_t)(q - b));
+        std::vector<std::string> names(hs.size()), bodies(hs.size());
+        pool.run(hs.size(), [&](size_t c) {
+            const size_t h = hs[c], stop = c + 1 < hs.size() ? hs[c + 1] : data.size();
+            size_t le = data.find('\n', h);
+            if (le == std::string::npos || le > stop) le = stop;
+            size_t ne = h + 1;
+            while (ne < le && data[ne] != ' ' && data[ne] != '\t' && data[ne] != '\r') ++ne;
+            names[c].assign(data, h + 1, ne - h - 1);
+            std::string &out = bodies[c];
+            out.reserve(stop > le ? stop - le : 0);
+            size_t p = le + 1;
+            while (p < stop) {
+                size_t q = data.find('\n', p);
+                if (q == std::string::npos || q > stop) q = stop;
+                size_t qe = q;
+                if (qe > p && data[qe - 1] == '\r') --qe;
+                out.append(data, p, qe - p);
+                p = q + 1;
             }
-            p = e + 1;
-        }
+        });
+        for (size_t c = 0; c < hs.size(); ++c) seq[names[c]] = std::move(bodies[c]);
         if (seq.empty()) {
             err = "no sequences in reference FASTA " + path;
             return false;
@@ -513,6 +634,7 @@ static long mismatching_qualities(const RRead &r, const std::string &ref, int re
 
 struct Consensus {
     std::string str;
+    size_t hash = 0;  // of str (duplicate check)
     Cigar cigar;
     int pos = 0;
     long sum = 0;
@@ -831,10 +953,76 @@ private:
     uint64_t seq_ = 0;
 };
 
+// The writer's forMateMatching map (read name -> read, modified) as an open-addressing table keyed
+// on the precomputed name hash; removal shifts the probe run back (no tombstones).
+class MateTable {
+public:
+    struct Slot {
+        RRead *r;
+        bool modified;
+    };
+    MateTable() { t_.assign(1024, Slot{nullptr, false}); }
+    Slot *find(const RRead *k) {
+        for (size_t i = k->name_hash & mask(); t_[i].r; i = (i + 1) & mask())
+            if (t_[i].r->name_hash == k->name_hash && t_[i].r->name == k->name) return &t_[i];
+        return nullptr;
+    }
+    void insert(RRead *r, bool modified) {  // caller checked find() == nullptr
+        if (2 * (n_ + 1) > t_.size()) grow();
+        size_t i = r->name_hash & mask();
+        while (t_[i].r) i = (i + 1) & mask();
+        t_[i] = Slot{r, modified};
+        n_++;
+    }
+    void erase(Slot *s) {
+        size_t i = (size_t)(s - t_.data());
+        t_[i].r = nullptr;
+        n_--;
+        for (size_t j = (i + 1) & mask(); t_[j].r; j = (j + 1) & mask()) {
+            const size_t home = t_[j].r->name_hash & mask();
+            // move j back into the hole at i when its home is not in the cyclic range (i, j]
+            if ((j > i && (home <= i || home > j)) || (j < i && (home <= i && home > j))) {
+                t_[i] = t_[j];
+                t_[j].r = nullptr;
+                i = j;
+            }
+        }
+    }
+    void erase_name(const RRead *k) {
+        if (Slot *s = find(k)) erase(s);
+    }
+    void clear() {
+        if (n_) std::fill(t_.begin(), t_.end(), Slot{nullptr, false});
+        n_ = 0;
+    }
+    void purge_unmodified() {
+        std::vector<Slot> keep;
+        for (auto &s : t_)
+            if (s.r && s.modified) keep.push_back(s);
+        clear();
+        for (auto &s : keep) insert(s.r, s.modified);
+    }
+
+private:
+    size_t mask() const { return t_.size() - 1; }
+    void grow() {
+        std::vector<Slot> old;
+        old.swap(t_);
+        t_.assign(old.size() * 2, Slot{nullptr, false});
+        n_ = 0;
+        for (auto &s : old)
+            if (s.r) insert(s.r, s.modified);
+    }
+    std::vector<Slot> t_;
+    size_t n_ = 0;
+};
+
 // ConstrainedMateFixingManager (util/gatk/ConstrainedMateFixingManager.cpp), run in stream order.
 class MateFixer {
 public:
-    MateFixer(const RealignParams &P, std::vector<RRead *> &out) : P_(P), out_(out) {}
+    // `counter` = reads added before this one's first (EMIT_FREQUENCY counts the whole stream)
+    MateFixer(const RealignParams &P, std::vector<RRead *> &out, uint64_t counter = 0) : P_(P), out_(out), counter_(counter) {}
+    size_t waiting() const { return waiting_.size(); }
 
     // canMoveReads (:245-251)
     bool can_move(const GLoc &earliest) const {
@@ -858,9 +1046,9 @@ public:
             else purge_unmodified();
         }
         if (nr->paired()) {
-            auto it = mates_.find(nr->name);
-            if (it != mates_.end()) {
-                RRead *mate = it->second.first;
+            MateTable::Slot *it = mates_.find(nr);
+            if (it) {
+                RRead *mate = it->r;
                 bool doNotFix = !nr->mapped() && (!mate->mapped() || !waiting_.count(mate));
                 if (!doNotFix) {
                     bool requeue = !mate->mapped() && nr->mapped();
@@ -870,7 +1058,7 @@ public:
                 }
                 mates_.erase(it);
             } else if (movable(*nr)) {
-                mates_[nr->name] = std::make_pair(nr, modified);
+                mates_.insert(nr, modified);
             }
         }
         waiting_.insert(nr);
@@ -878,7 +1066,7 @@ public:
             while (!waiting_.empty()) {
                 RRead *r = waiting_.top();
                 if (cannot_move_before(r->pos, *nr) && (!movable(*r) || cannot_move_before(r->mpos, *nr))) {
-                    mates_.erase(r->name);
+                    mates_.erase_name(r);
                     write(pop());
                 } else {
                     break;
@@ -903,12 +1091,7 @@ private:
     }
     RRead *pop() { return waiting_.pop(); }
     void write(RRead *r) { out_.push_back(r); }
-    void purge_unmodified() {
-        for (auto it = mates_.begin(); it != mates_.end();) {
-            if (!it->second.second) it = mates_.erase(it);
-            else ++it;
-        }
-    }
+    void purge_unmodified() { mates_.purge_unmodified(); }
     static int end_position(const RRead &r) {  // getEndPosition (:100-120)
         int len = 0;
         for (auto &c : r.cigar)
@@ -976,35 +1159,14 @@ private:
 
     const RealignParams &P_;
     std::vector<RRead *> &out_;
+    uint64_t counter_ = 0;
     WaitQueue waiting_;
-    std::unordered_map<std::string_view, std::pair<RRead *, bool>> mates_;
+    MateTable mates_;
     GLoc last_;
     bool hasLast_ = false;
-    uint64_t counter_ = 0;
 };
 
 // =====================================================================================  driver
-template <class F>
-static void par_for(size_t n, int threads, F f) {
-    if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
-    threads = (int)std::min<size_t>((size_t)threads, std::max<size_t>(1, n));
-    if (threads <= 1) {
-        for (size_t i = 0; i < n; ++i) f(i);
-        return;
-    }
-    std::atomic<size_t> next(0);
-    std::vector<std::thread> ts;
-    for (int t = 0; t < threads; ++t)
-        ts.emplace_back([&]() {
-            for (;;) {
-                size_t i = next.fetch_add(1);
-                if (i >= n) break;
-                f(i);
-            }
-        });
-    for (auto &t : ts) t.join();
-}
-
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1060,8 +1222,9 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
                 const std::string &fasta_path, const std::string &intervals_path, const RealignParams &P, const ScanFn &scan,
                 ByteBuf &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err) {
     double t0 = now_s();
+    Pool pool(P.threads);
     Fasta fa;
-    if (!fa.load(fasta_path, err)) return -4;
+    if (!fa.load(fasta_path, err, pool)) return -4;
     std::vector<GLoc> ivs;
     if (!parse_intervals(intervals_path, ref_names, ivs, err)) return -1;
     st.intervals = ivs.size();
@@ -1072,12 +1235,15 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     struct ReadArray {
         RRead *p;
         uint64_t n;
-        int threads;
-        ~ReadArray() {
-            par_for((n + dchunk - 1) / dchunk, threads, [&](size_t c) {
-                for (uint64_t i = c * dchunk, e = std::min<uint64_t>(n, i + dchunk); i < e; ++i) p[i].~RRead();
+        Pool &pool;
+        ~ReadArray() { release(); }
+        void release() {
+            pool.run_chunks(n, dchunk, [&](size_t b, size_t e) {
+                for (size_t i = b; i < e; ++i) p[i].~RRead();
             });
             std::free(p);
+            p = nullptr;
+            n = 0;
         }
         RRead &operator[](uint64_t i) { return p[i]; }
     };
@@ -1086,23 +1252,29 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         err = "out of host memory for the decoded records";
         return -1;
     }
-    ReadArray reads{rmem, 0, P.threads};
-    par_for((n + dchunk - 1) / dchunk, P.threads, [&](size_t c) {
-        for (uint64_t i = c * dchunk, end = std::min<uint64_t>(n, i + dchunk); i < end; ++i) new (&rmem[i]) RRead();
+    ReadArray reads{rmem, 0, pool};
+    pool.run_chunks(n, dchunk, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) new (&rmem[i]) RRead();
     });
     reads.n = n;
     std::atomic<bool> bad(false);
     std::mutex emu;
     std::string derr;
-    par_for((n + dchunk - 1) / dchunk, P.threads, [&](size_t c) {
+    // decode, plus what binning asks of every read (its GenomeLoc stop, doNotTryToClean)
+    std::vector<int32_t> lstop(n);
+    std::vector<uint8_t> dnc(n);
+    pool.run_chunks(n, dchunk, [&](size_t b, size_t end) {
         std::string e;
-        for (uint64_t i = c * dchunk, end = std::min<uint64_t>(n, i + dchunk); i < end; ++i) {
+        for (size_t i = b; i < end; ++i) {
             if (!rread_decode(recs + offs[i], reads[i], e)) {
                 std::lock_guard<std::mutex> g(emu);
                 bad = true;
                 derr = e;
+                continue;
             }
             reads[i].idx = (uint32_t)i;
+            lstop[i] = read_loc(reads[i]).stop;
+            dnc[i] = do_not_clean(reads[i], P);
         }
     });
     if (bad) {
@@ -1117,7 +1289,8 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     }
 
     const double td = now_s();
-    if (getenv("OGE_RL_DEBUG")) fprintf(stderr, "fasta+intervals %.3f decode %.3f\n", tf - t0, td - tf);
+    st.t_fasta = tf - t0;
+    st.t_decode = td - tf;
     // ---------------------------------------------------------------- A: map_func (:455-553)
     std::vector<std::unique_ptr<IntervalData>> ids;
     std::vector<Event> ev;
@@ -1129,8 +1302,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     size_t it = 0;
     IntervalData *loading = new_id(ivs.empty() ? -1 : 0);
     bool saw = false;
-    auto bin_add = [&](IntervalData *d, RRead *r) {  // ReadBin::add (:263-275)
-        GLoc l = read_loc(*r);
+    auto bin_add = [&](IntervalData *d, RRead *r, const GLoc &l) {  // ReadBin::add (:263-275)
         if (!d->hasLoc) {
             d->binLoc = l;
             d->hasLoc = true;
@@ -1139,47 +1311,55 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         }
         d->toClean.push_back(r);
     };
-    std::function<void(RRead *)> map_func = [&](RRead *r) {
-        if (loading->interval < 0) {
-            ev.push_back({EV_READ, r, loading});
-            loading = new_id(-1);
-            return;
-        }
-        if (r->ref == -1) {
-            ev.push_back({EV_CLEAN, nullptr, loading});
-            it = ivs.size();
-            loading = new_id(-1);
-            saw = false;
-            map_func(r);
-            return;
-        }
-        GLoc rl = read_loc(*r);
-        if (rl.stop == 0) rl.stop = rl.start;
-        const GLoc &cur = ivs[loading->interval];
-        if (rl.is_before(cur)) {
-            if (!saw) ev.push_back({EV_READ, r, loading});
-            else loading->notToClean.push_back(r);
-        } else if (rl.overlaps(cur)) {
-            saw = true;
-            if (do_not_clean(*r, P)) loading->notToClean.push_back(r);
-            else bin_add(loading, r);
-            if ((int)(loading->toClean.size() + loading->notToClean.size()) >= P.max_reads) {
-                ev.push_back({EV_LIST, nullptr, loading});
-                ++it;
+    // map_func; `continue` re-dispatches the read after the loading bin changed (the reference's
+    // recursive calls).  Once the intervals are exhausted every read passes straight through (a bin
+    // of its own in the reference, which emits it unchanged).
+    for (uint64_t i = 0; i < n; ++i) {
+        RRead *r = &reads[i];
+        for (;;) {
+            if (loading->interval < 0) {
+                ev.push_back({EV_READ, r, loading});
+                break;
+            }
+            if (r->ref == -1) {
+                ev.push_back({EV_CLEAN, nullptr, loading});
+                it = ivs.size();
+                loading = new_id(-1);
+                saw = false;
+                continue;
+            }
+            GLoc loc;
+            loc.contig = r->ref;
+            loc.start = r->pos;
+            loc.stop = lstop[i];
+            GLoc rl = loc;
+            if (rl.stop == 0) rl.stop = rl.start;
+            const GLoc &cur = ivs[loading->interval];
+            if (rl.is_before(cur)) {
+                if (!saw) ev.push_back({EV_READ, r, loading});
+                else loading->notToClean.push_back(r);
+            } else if (rl.overlaps(cur)) {
+                saw = true;
+                if (dnc[i]) loading->notToClean.push_back(r);
+                else bin_add(loading, r, loc);
+                if ((int)(loading->toClean.size() + loading->notToClean.size()) >= P.max_reads) {
+                    ev.push_back({EV_LIST, nullptr, loading});
+                    ++it;
+                    loading = new_id(it < ivs.size() ? (int)it : -1);
+                    saw = false;
+                }
+            } else {
+                ev.push_back({EV_CLEAN, nullptr, loading});
+                do {
+                    ++it;
+                } while (it < ivs.size() && ivs[it].is_before(rl));
                 loading = new_id(it < ivs.size() ? (int)it : -1);
                 saw = false;
+                continue;
             }
-        } else {
-            ev.push_back({EV_CLEAN, nullptr, loading});
-            do {
-                ++it;
-            } while (it < ivs.size() && ivs[it].is_before(rl));
-            loading = new_id(it < ivs.size() ? (int)it : -1);
-            saw = false;
-            map_func(r);
+            break;
         }
-    };
-    for (uint64_t i = 0; i < n; ++i) map_func(&reads[i]);
+    }
     // onTraversalDone (:577-607)
     if (!loading->toClean.empty()) ev.push_back({EV_CLEAN, nullptr, loading});
     else if (!loading->notToClean.empty()) ev.push_back({EV_LIST, nullptr, loading});
@@ -1192,7 +1372,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         if (e.t == EV_CLEAN && !e.id->toClean.empty()) work.push_back(e.id);
     std::atomic<bool> ferr(false);
     std::string fmsg;
-    par_for(work.size(), P.threads, [&](size_t w) {
+    pool.run_static(work.size(), [&](size_t w) {
         IntervalData &d = *work[w];
         const std::string &contig = ref_names[d.binLoc.contig];
         const std::string *seq = fa.get(contig);
@@ -1228,9 +1408,10 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
                 if (blocks == 2) {
                     Consensus c;
                     if (create_consensus(startOnRef, a->cigar(), ref, a->bases, c)) {
+                        c.hash = std::hash<std::string>()(c.str);
                         bool exists = false;
                         for (auto &o : d.cons)
-                            if (o.str == c.str) exists = true;
+                            if (o.hash == c.hash && o.str == c.str) exists = true;
                         if (!exists) d.cons.push_back(std::move(c));
                     }
                 }
@@ -1246,37 +1427,68 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     st.t_prepare = t2 - t1;
 
     // ---------------------------------------------------------------- C: offset scan (GPU)
+    // batch layout: per-interval extents, prefix sums, then a parallel fill
     ScanBatch B;
-    B.cons_off.push_back(0);
-    B.read_off.push_back(0);
-    for (IntervalData *d : work) {
-        if (d->cons.empty()) continue;
-        const uint32_t c0 = (uint32_t)(B.cons_off.size() - 1), r0 = (uint32_t)(B.read_off.size() - 1);
-        d->pairBase = B.pairs.size();
-        for (auto &c : d->cons) {
-            B.cons.insert(B.cons.end(), c.str.begin(), c.str.end());
-            B.cons_off.push_back(B.cons.size());
+    const size_t nw = work.size();
+    std::vector<uint64_t> xc(nw + 1, 0), xcb(nw + 1, 0), xr(nw + 1, 0), xrb(nw + 1, 0), xp(nw + 1, 0);
+    for (size_t w = 0; w < nw; ++w) {
+        const IntervalData &d = *work[w];
+        uint64_t cb = 0, rb = 0;
+        const bool on = !d.cons.empty();
+        if (on) {
+            for (auto &c : d.cons) cb += c.str.size();
+            for (auto &a : d.alt) rb += a->bases.size();
         }
-        for (auto &a : d->alt) {
-            B.bases.insert(B.bases.end(), a->bases.begin(), a->bases.end());
-            for (char q : a->quals) B.quals.push_back((uint8_t)(q - 33));
-            B.read_off.push_back(B.bases.size());
+        xc[w + 1] = xc[w] + (on ? d.cons.size() : 0);
+        xcb[w + 1] = xcb[w] + cb;
+        xr[w + 1] = xr[w] + (on ? d.alt.size() : 0);
+        xrb[w + 1] = xrb[w] + rb;
+        xp[w + 1] = xp[w] + (on ? (uint64_t)d.cons.size() * d.alt.size() : 0);
+    }
+    B.cons.resize(xcb[nw]);
+    B.cons_off.resize(xc[nw] + 1);
+    B.bases.resize(xrb[nw]);
+    B.quals.resize(xrb[nw]);
+    B.read_off.resize(xr[nw] + 1);
+    B.pairs.resize(xp[nw]);
+    B.cons_off[0] = 0;
+    B.read_off[0] = 0;
+    std::vector<uint64_t> wops(nw, 0);
+    pool.run_static(nw, [&](size_t w) {
+        IntervalData &d = *work[w];
+        if (d.cons.empty()) return;
+        d.pairBase = xp[w];
+        uint64_t cb = xcb[w], ci0 = xc[w];
+        for (size_t c = 0; c < d.cons.size(); ++c) {
+            memcpy(B.cons.data() + cb, d.cons[c].str.data(), d.cons[c].str.size());
+            cb += d.cons[c].str.size();
+            B.cons_off[ci0 + c + 1] = cb;
         }
-        for (uint32_t ci = 0; ci < d->cons.size(); ++ci) {
-            const int consLen = (int)d->cons[ci].str.size();
-            for (uint32_t j = 0; j < d->alt.size(); ++j) {
-                const AlignedRead &a = *d->alt[j];
-                ScanPair sp;
-                sp.cons = c0 + ci;
-                sp.read = r0 + j;
-                sp.orig = a.read->pos - d->leftmost;
+        uint64_t rb = xrb[w], ri0 = xr[w];
+        for (size_t j = 0; j < d.alt.size(); ++j) {
+            const AlignedRead &a = *d.alt[j];
+            memcpy(B.bases.data() + rb, a.bases.data(), a.bases.size());
+            for (size_t k = 0; k < a.quals.size(); ++k) B.quals[rb + k] = (uint8_t)(a.quals[k] - 33);
+            rb += a.bases.size();
+            B.read_off[ri0 + j + 1] = rb;
+        }
+        uint64_t pi = xp[w], ops = 0;
+        for (uint32_t c = 0; c < d.cons.size(); ++c) {
+            const int consLen = (int)d.cons[c].str.size();
+            for (uint32_t j = 0; j < d.alt.size(); ++j) {
+                const AlignedRead &a = *d.alt[j];
+                ScanPair &sp = B.pairs[pi++];
+                sp.cons = (uint32_t)(ci0 + c);
+                sp.read = (uint32_t)(ri0 + j);
+                sp.orig = a.read->pos - d.leftmost;
                 sp.max_start = consLen - (int)a.cigar_length();
-                B.pairs.push_back(sp);
                 const int offsets = std::max(sp.orig, sp.max_start) + 1;
-                st.scan_ops += (uint64_t)std::max(offsets, 0) * a.bases.size();
+                ops += (uint64_t)std::max(offsets, 0) * a.bases.size();
             }
         }
-    }
+        wops[w] = ops;
+    });
+    for (uint64_t o : wops) st.scan_ops += o;
     st.scan_pairs = B.pairs.size();
     std::vector<int32_t> bidx, bscore;
     if (!B.pairs.empty()) {
@@ -1290,7 +1502,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     st.t_scan = t3 - t2;
 
     // ---------------------------------------------------------------- D: decide (:713-892)
-    par_for(work.size(), P.threads, [&](size_t w) {
+    pool.run_static(work.size(), [&](size_t w) {
         IntervalData &d = *work[w];
         if (d.cons.empty()) return;
         Consensus *best = nullptr;
@@ -1354,36 +1566,107 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     st.t_decide = t4 - t3;
 
     // ---------------------------------------------------------------- E: emit + mate fixing
-    std::vector<RRead *> order;
-    order.reserve(n);
-    MateFixer mf(P, order);
-    std::set<RRead *> cleaned;
-    for (auto &e : ev) {
-        if (e.t == EV_READ) {
-            mf.add(e.read, false, true);
-            continue;
-        }
-        IntervalData &d = *e.id;
-        cleaned.clear();
-        if (e.t == EV_CLEAN && !d.toClean.empty()) {
-            // CleanAndEmitReadList::runJob (:435-453): clean only if the writer allows moves here
-            if (mf.can_move(read_loc(*d.toClean[0])) && d.cleanable) {
-                st.intervals_cleaned++;
-                for (auto &pu : d.pending) {
-                    *pu.first = std::move(pu.second);
-                    cleaned.insert(pu.first);
-                }
-                st.reads_realigned += d.pending.size();
+    // The writer (ConstrainedMateFixingManager) flushes everything waiting and forgets its mate map
+    // whenever a read of another contig arrives; the stream is never empty at that point (the last
+    // read added is still waiting).  So per-contig segments of the event stream run independently,
+    // each on its own writer whose EMIT_FREQUENCY counter starts where the stream's would be -- with
+    // one exception: a flush that also finds >= maxRecordsInMemory reads waiting keeps the modified
+    // mate entries.  A segment ending that way sends the whole phase to the sequential path.
+    auto emit_events = [&](size_t e0, size_t e1, uint64_t add0, std::vector<RRead *> &ord, uint64_t &cl, uint64_t &rr) {
+        MateFixer mf(P, ord, add0);
+        for (size_t k = e0; k < e1; ++k) {
+            const Event &e = ev[k];
+            if (e.t == EV_READ) {
+                mf.add(e.read, false, true);
+                continue;
             }
+            IntervalData &d = *e.id;
+            if (e.t == EV_CLEAN && !d.toClean.empty()) {
+                // CleanAndEmitReadList::runJob (:435-453): clean only if the writer allows moves here
+                if (mf.can_move(read_loc(*d.toClean[0])) && d.cleanable) {
+                    cl++;
+                    for (auto &pu : d.pending) {
+                        *pu.first = pu.second;  // a copy: the sequential fallback may apply it again
+                        pu.first->cleaned = true;
+                    }
+                    rr += d.pending.size();
+                }
+            }
+            // emitReadLists (:370-376)
+            std::vector<RRead *> lst = d.notToClean;
+            lst.insert(lst.end(), d.toClean.begin(), d.toClean.end());
+            std::stable_sort(lst.begin(), lst.end(), ByPos());
+            for (RRead *r : lst) mf.add(r, r->cleaned, false);
         }
-        // emitReadLists (:370-376)
-        std::vector<RRead *> lst = d.notToClean;
-        lst.insert(lst.end(), d.toClean.begin(), d.toClean.end());
-        std::stable_sort(lst.begin(), lst.end(), ByPos());
-        for (RRead *r : lst) mf.add(r, cleaned.count(r) > 0, false);
+        const size_t left = mf.waiting();
+        mf.close();
+        return left;
+    };
+    struct Seg {
+        size_t e0, e1;
+        uint64_t add0;
+        std::vector<RRead *> ord;
+        uint64_t cl = 0, rr = 0;
+        size_t left = 0;
+    };
+    std::vector<Seg> segs;
+    bool mixed = false;
+    {
+        uint64_t adds = 0;
+        int32_t cur = INT32_MIN;
+        for (size_t k = 0; k < ev.size(); ++k) {
+            const Event &e = ev[k];
+            int32_t ref = INT32_MIN;
+            uint64_t cnt = 0;
+            if (e.t == EV_READ) {
+                ref = e.read->ref;
+                cnt = 1;
+            } else {
+                const IntervalData &d = *e.id;
+                for (const auto *v : {&d.notToClean, &d.toClean})
+                    for (RRead *r : *v) {
+                        if (ref == INT32_MIN) ref = r->ref;
+                        else if (r->ref != ref) mixed = true;
+                        cnt++;
+                    }
+            }
+            if (cnt && ref != cur) {
+                if (!segs.empty()) segs.back().e1 = k;
+                segs.push_back(Seg{segs.empty() ? 0 : k, ev.size(), adds, {}, 0, 0, 0});
+                cur = ref;
+            }
+            adds += cnt;
+        }
     }
-    mf.close();
-    if (getenv("OGE_RL_DEBUG")) fprintf(stderr, "mate fixing %.3f\n", now_s() - t4);
+    bool sequential = mixed || segs.size() <= 1 || P.mate_sequential;
+    if (!sequential) {
+        pool.run(segs.size(), [&](size_t k) {
+            Seg &g = segs[k];
+            g.left = emit_events(g.e0, g.e1, g.add0, g.ord, g.cl, g.rr);
+        });
+        for (size_t k = 0; k + 1 < segs.size(); ++k)
+            if (segs[k].left >= (size_t)P.max_records_in_memory) sequential = true;
+        if (sequential) {  // undo: fresh records, then the one-writer path
+            pool.run_chunks(n, dchunk, [&](size_t b, size_t end) {
+                std::string e;
+                for (size_t i = b; i < end; ++i) rread_decode(recs + offs[i], reads[i], e);
+            });
+        }
+    }
+    std::vector<RRead *> order;
+    if (sequential) {
+        order.reserve(n);
+        emit_events(0, ev.size(), 0, order, st.intervals_cleaned, st.reads_realigned);
+    } else {
+        order.reserve(n);
+        for (auto &g : segs) {
+            order.insert(order.end(), g.ord.begin(), g.ord.end());
+            st.intervals_cleaned += g.cl;
+            st.reads_realigned += g.rr;
+        }
+    }
+    st.mate_segments = sequential ? 1 : segs.size();
+    st.t_mate = now_s() - t4;
     if (order.size() != n) {
         err = "internal: emitted " + std::to_string(order.size()) + " of " + std::to_string(n) + " records";
         return -1;
@@ -1396,11 +1679,20 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         return -1;
     }
     const uint64_t chunk = 4096;
-    par_for((n + chunk - 1) / chunk, P.threads, [&](size_t c) {
-        for (uint64_t i = c * chunk, e = std::min<uint64_t>(n, i + chunk); i < e; ++i)
-            rread_encode_to(*order[i], out.data() + out_off[i]);
+    pool.run_chunks(n, chunk, [&](size_t b, size_t e) {
+        for (size_t i = b; i < e; ++i) rread_encode_to(*order[i], out.data() + out_off[i]);
     });
     st.t_emit = now_s() - t4;
+    const double t5 = now_s();
+    // teardown on the workers that allocated (run_static, same mapping as prepare/decide)
+    pool.run_static(work.size(), [&](size_t w) {
+        IntervalData &d = *work[w];
+        for (auto &pu : d.pending) std::string().swap(pu.first->tags_own);
+        *work[w] = IntervalData();
+    });
+    ids.clear();
+    reads.release();
+    st.t_release = now_s() - t5;
     return 0;
 }
 

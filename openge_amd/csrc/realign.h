@@ -127,6 +127,8 @@ struct RRead {
     std::string tags_own;      // edited tag bytes (valid when tags_owned)
     bool tags_owned = false;
     int32_t mq_add = -1;       // MQ:S value appended at encode (the mate fixer's AddTag("MQ")), -1 = none
+    uint32_t name_hash = 0;    // FNV-1a of name (mate-table probe)
+    bool cleaned = false;      // realigned in the interval being emitted
     uint32_t idx = 0;          // input order (stands in for the reference's heap-address tie-break)
 
     std::string_view tags() const { return tags_owned ? std::string_view(tags_own) : tags_in; }
@@ -186,11 +188,14 @@ struct RealignParams {
     int max_reads = 20000;               // (:1444)
     bool no_original_alignment_tags = false;
     int threads = 0;
+    bool mate_sequential = false;        // one writer over the whole stream (tests compare the two)
 };
 
 struct RealignStats {
     uint64_t intervals = 0, intervals_cleaned = 0, reads_realigned = 0, scan_pairs = 0, scan_ops = 0;
+    uint64_t mate_segments = 0;  // writer segments run in parallel (1 = sequential)
     double t_bin = 0, t_prepare = 0, t_scan = 0, t_decide = 0, t_emit = 0, t_run = 0;
+    double t_fasta = 0, t_decode = 0, t_mate = 0, t_release = 0;  // parts of t_bin / t_emit; teardown
 };
 
 // Output record bytes: malloc'ed without zero-fill so the parallel encoder's first touch is the only

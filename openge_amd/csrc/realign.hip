@@ -328,10 +328,11 @@ int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len,
     snprintf(buf, sizeof buf,
              "{\"intervals\": %llu, \"intervals_cleaned\": %llu, \"reads_realigned\": %llu, \"scan_pairs\": %llu, "
              "\"scan_ops\": %llu, \"scan_kernel_ms\": %.4f, \"t_bin\": %.4f, \"t_prepare\": %.4f, \"t_scan\": %.4f, "
-             "\"t_decide\": %.4f, \"t_emit\": %.4f, \"t_run\": %.4f}",
+             "\"t_decide\": %.4f, \"t_emit\": %.4f, \"t_run\": %.4f, \"t_fasta\": %.4f, \"t_decode\": %.4f, "
+             "\"t_mate\": %.4f, \"t_release\": %.4f}",
              (unsigned long long)st.intervals, (unsigned long long)st.intervals_cleaned, (unsigned long long)st.reads_realigned,
              (unsigned long long)st.scan_pairs, (unsigned long long)st.scan_ops, scan_kernel_ms, st.t_bin, st.t_prepare,
-             st.t_scan, st.t_decide, st.t_emit, st.t_run);
+             st.t_scan, st.t_decide, st.t_emit, st.t_run, st.t_fasta, st.t_decode, st.t_mate, st.t_release);
     r->stats = buf;
     *out = r.release();
     return OGE_OK;

@@ -29,7 +29,7 @@ struct Out {
 extern "C" {
 
 void *realign_cpu(const char *header, uint64_t hlen, const uint8_t *recs, const uint64_t *offs, uint64_t n,
-                  const char *fasta, const char *intervals, int threads) {
+                  const char *fasta, const char *intervals, int threads, int max_records, int mate_sequential) {
     Out *o = new Out();
     oge::BamHeaderModel h;
     if (!h.parse(std::string(header, hlen), o->msg)) return o;
@@ -37,6 +37,8 @@ void *realign_cpu(const char *header, uint64_t hlen, const uint8_t *recs, const 
     for (auto &sq : h.sq) names.push_back(sq.name);
     oge::RealignParams P;
     P.threads = threads;
+    if (max_records > 0) P.max_records_in_memory = max_records;
+    P.mate_sequential = mate_sequential != 0;
     oge::ScanFn scan = [](const oge::ScanBatch &B, std::vector<int32_t> &bi, std::vector<int32_t> &bs) {
         bi.resize(B.pairs.size());
         bs.resize(B.pairs.size());
@@ -50,8 +52,9 @@ void *realign_cpu(const char *header, uint64_t hlen, const uint8_t *recs, const 
     st.t_run = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
     if (rc) o->msg = err.empty() ? "realign failed" : err;
     char b[512];
-    snprintf(b, sizeof b, "{\"t_bin\": %.3f, \"t_prepare\": %.3f, \"t_scan\": %.3f, \"t_decide\": %.3f, \"t_emit\": %.3f, \"t_run\": %.3f, \"scan_pairs\": %llu}",
-             st.t_bin, st.t_prepare, st.t_scan, st.t_decide, st.t_emit, st.t_run, (unsigned long long)st.scan_pairs);
+    snprintf(b, sizeof b, "{\"t_bin\": %.3f, \"t_prepare\": %.3f, \"t_scan\": %.3f, \"t_decide\": %.3f, \"t_emit\": %.3f, \"t_run\": %.3f, \"t_fasta\": %.3f, \"t_decode\": %.3f, \"t_mate\": %.3f, \"t_release\": %.3f, \"scan_pairs\": %llu, \"mate_segments\": %llu}",
+             st.t_bin, st.t_prepare, st.t_scan, st.t_decide, st.t_emit, st.t_run, st.t_fasta, st.t_decode, st.t_mate, st.t_release, (unsigned long long)st.scan_pairs,
+             (unsigned long long)st.mate_segments);
     o->stats = b;
     return o;
 }

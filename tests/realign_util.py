@@ -19,7 +19,9 @@ def harness():
         L = C.CDLL(str(build_native()))
         L.realign_cpu.restype = C.c_void_p
         L.realign_cpu.argtypes = [C.c_char_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_char_p, C.c_char_p,
-                                  C.c_int]
+                                  C.c_int, C.c_int, C.c_int]
+        L.realign_cpu_stats.restype = C.c_char_p
+        L.realign_cpu_stats.argtypes = [C.c_void_p]
         L.realign_cpu_error.restype = C.c_char_p
         L.realign_cpu_error.argtypes = [C.c_void_p]
         L.realign_cpu_count.restype = C.c_uint64
@@ -33,16 +35,22 @@ def harness():
     return _h
 
 
-def realign_cpu(header: str, recs: np.ndarray, offs: np.ndarray, n: int, fasta: str, intervals: str, threads: int = 4):
-    """-> (out recs, out offsets[n+1]) from the product host phases with the oracle scan."""
+def realign_cpu(header: str, recs: np.ndarray, offs: np.ndarray, n: int, fasta: str, intervals: str, threads: int = 4,
+                max_records: int = 0, mate_sequential: bool = False, stats: dict | None = None):
+    """-> (out recs, out offsets[n+1]) from the product host phases with the oracle scan.
+    max_records > 0 overrides MAX_RECORDS_IN_MEMORY; mate_sequential forces the one-writer path."""
     L = harness()
     hb = header.encode()
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
-    h = L.realign_cpu(hb, len(hb), recs.ctypes.data, offs.ctypes.data, n, fasta.encode(), intervals.encode(), threads)
+    h = L.realign_cpu(hb, len(hb), recs.ctypes.data, offs.ctypes.data, n, fasta.encode(), intervals.encode(), threads,
+                      max_records, int(mate_sequential))
     try:
         err = L.realign_cpu_error(h).decode()
         if err:
             raise RuntimeError(err)
+        if stats is not None:
+            import json
+            stats.update(json.loads(L.realign_cpu_stats(h).decode()))
         cnt = int(L.realign_cpu_count(h))
         nb = C.c_uint64()
         rp = L.realign_cpu_records(h, C.byref(nb))

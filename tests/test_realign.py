@@ -121,6 +121,24 @@ def test_host_realign_phases_match_reference(built, tmp_path, name):
     check_output(meta, arrays, out, oo)
 
 
+@pytest.mark.parametrize("max_records", [0, 7, 60, 400])
+def test_parallel_mate_fixing_equals_one_writer(built, tmp_path, max_records):
+    """Per-contig writer segments (run in parallel) against one writer over the whole stream, with
+    MAX_RECORDS_IN_MEMORY small enough to force flushes inside segments and at contig boundaries
+    (the latter sends the product to its sequential fallback)."""
+    meta, arrays, h, recs, offs, fa, iv = load_rl_case("rl_c5_2k", tmp_path)
+    n = len(offs) - 1
+    st_par, st_seq = {}, {}
+    a = R.realign_cpu(h, recs, offs, n, fa, iv, threads=4, max_records=max_records, stats=st_par)
+    b = R.realign_cpu(h, recs, offs, n, fa, iv, threads=4, max_records=max_records, mate_sequential=True, stats=st_seq)
+    assert st_seq["mate_segments"] == 1
+    if max_records == 0:
+        assert st_par["mate_segments"] > 1
+        check_output(meta, arrays, *a)
+    assert a[1].tolist() == b[1].tolist()
+    assert a[0].tobytes() == b[0].tobytes()
+
+
 def test_realign_synth_is_deterministic(built, tmp_path):
     p = L.realign_synth_params(n_intervals=40, n_ref=2, seed=5)
     (tmp_path / "a").mkdir()
