@@ -26,6 +26,8 @@ struct oge_ctx {
     std::vector<OgeStageTimer> event_pool;
     size_t event_pool_used = 0;
     bool timing = true;
+    bool last_scan_generic = false;  // realign scan fell back to the byte-wise kernel
+    double scan_t[3] = {0, 0, 0};    // realign scan host timings: validate, upload, device + download
 
     // Grow-only named scratch buffer; contents are undefined between calls.
     void *ws(const char *name, size_t bytes);

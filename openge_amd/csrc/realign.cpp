@@ -20,6 +20,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <sys/mman.h>
 #include <new>
 #include <set>
 #include <thread>
@@ -114,6 +115,15 @@ private:
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
+
+// Hand the pages of a large block about to be freed back to the kernel from all workers: one
+// munmap of ~1 GB frees its pages serially.
+static void release_pages(Pool &pool, void *p, size_t bytes) {
+    const size_t pg = 4096, chunk = 64ull << 20;
+    const uintptr_t b = ((uintptr_t)p + pg - 1) & ~(uintptr_t)(pg - 1), e = ((uintptr_t)p + bytes) & ~(uintptr_t)(pg - 1);
+    if (e <= b + chunk) return;
+    pool.run_chunks(e - b, chunk, [&](size_t lo, size_t hi) { madvise((void *)(b + lo), hi - lo, MADV_DONTNEED); });
+}
 
 // =====================================================================================  records
 static const char kSeqChars[] = "=ACMGRSVTWYHKDBN";
@@ -1241,6 +1251,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
             pool.run_chunks(n, dchunk, [&](size_t b, size_t e) {
                 for (size_t i = b; i < e; ++i) p[i].~RRead();
             });
+            if (p) release_pages(pool, p, n * sizeof(RRead));
             std::free(p);
             p = nullptr;
             n = 0;
@@ -1490,6 +1501,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     });
     for (uint64_t o : wops) st.scan_ops += o;
     st.scan_pairs = B.pairs.size();
+    st.t_scan_build = now_s() - t2;
     std::vector<int32_t> bidx, bscore;
     if (!B.pairs.empty()) {
         int rc = scan(B, bidx, bscore);

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <string>
 #include <string_view>
+#include <utility>
 #include <vector>
 
 namespace oge {
@@ -168,13 +169,36 @@ struct ScanPair {
     int32_t orig;       // original alignment start - leftmostIndex
     int32_t max_start;  // consensus length - read cigar length (findBestOffset :1149-1150)
 };
+// std::vector whose resize() leaves trivial elements uninitialised (the batch is filled in parallel;
+// a zero-fill would be a serial pass over every page first)
+template <class T>
+struct UninitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        typedef UninitAlloc<U> other;
+    };
+    UninitAlloc() = default;
+    template <class U>
+    UninitAlloc(const UninitAlloc<U> &) {}
+    template <class U>
+    void construct(U *p) noexcept {
+        ::new ((void *)p) U;
+    }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) {
+        ::new ((void *)p) U(std::forward<A>(a)...);
+    }
+};
+template <class T>
+using uvector = std::vector<T, UninitAlloc<T>>;
+
 struct ScanBatch {
-    std::vector<uint8_t> cons;           // consensus bytes, back to back
-    std::vector<uint64_t> cons_off;      // n_cons + 1
-    std::vector<uint8_t> bases;          // altRead bases (M/I only), back to back
-    std::vector<uint8_t> quals;          // raw phred bytes aligned with bases
-    std::vector<uint64_t> read_off;      // n_reads + 1
-    std::vector<ScanPair> pairs;
+    uvector<uint8_t> cons;           // consensus bytes, back to back
+    uvector<uint64_t> cons_off;      // n_cons + 1
+    uvector<uint8_t> bases;          // altRead bases (M/I only), back to back
+    uvector<uint8_t> quals;          // raw phred bytes aligned with bases
+    uvector<uint64_t> read_off;      // n_reads + 1
+    uvector<ScanPair> pairs;
 };
 // Fills best_index / best_score (one per pair).  Returns 0 on success.
 typedef std::function<int(const ScanBatch &, std::vector<int32_t> &best_index, std::vector<int32_t> &best_score)> ScanFn;
@@ -196,6 +220,7 @@ struct RealignStats {
     uint64_t mate_segments = 0;  // writer segments run in parallel (1 = sequential)
     double t_bin = 0, t_prepare = 0, t_scan = 0, t_decide = 0, t_emit = 0, t_run = 0;
     double t_fasta = 0, t_decode = 0, t_mate = 0, t_release = 0;  // parts of t_bin / t_emit; teardown
+    double t_scan_build = 0;                                       // part of t_scan: batch assembly
 };
 
 // Output record bytes: malloc'ed without zero-fill so the parallel encoder's first touch is the only

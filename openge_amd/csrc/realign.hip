@@ -11,11 +11,16 @@
 // while every weight is >= 0 its answer is the minimum of (score, visit rank) -- early exits never
 // change it.  A quality >= 95 makes its weight negative; such reads take the literal scan (lit_best).
 //
-// Kernel: one 256-thread workgroup per consensus (all altReads of an interval share it).  The
-// consensus is staged in LDS as 1-byte base codes; each read in turn is staged as packed
-// (code | weight << 16) words that every lane reads at the same address (LDS broadcast).  Lanes own
-// offsets; a wave/workgroup min-reduction over the packed (score, rank) key gives the answer.
-// Integer VALU + LDS bound; no MFMA (no dense contraction).
+// Kernels.  k_planes turns every consensus and altRead into bit planes, 64 positions per word
+// (wave ballots): base-code bits b0,b1 and a "regular base" mask v; for reads also the 7 bit planes
+// of the weight.  k_scan_bp then gives each (consensus, read) pair one wave; lane l owns offsets
+// k = 64a + l, so its consensus window is a fixed l-bit funnel shift of consecutive plane words, and
+// the plane words every lane needs are the same (scalar loads).  Per 64 read positions and offset:
+//     m = win(v) & rv & ((win(b0) ^ r0) | (win(b1) ^ r1));   S += sum_b popcount(m & W_b) << b
+// (~50 VALU ops instead of ~450 byte-wise).  A wave min-reduction over the packed (score, rank) key
+// gives the answer.  Integer VALU bound; no MFMA (no dense contraction), no LDS.
+// k_realign_scan (byte-wise, one workgroup per consensus, LDS-staged) remains for batches holding
+// lower-case bases or '*' (codes 4..8, which the 2-bit planes do not carry).
 #include "oge_ctx.h"
 #include "bamio.h"
 #include "realign.h"
@@ -182,6 +187,150 @@ __global__ __launch_bounds__(kT) void k_realign_scan(const uint8_t *__restrict__
     }
 }
 
+// ---------------------------------------------------------------- bit-parallel path
+struct CPlane {  // 64 consensus positions
+    uint64_t b0, b1, v, pad;
+};
+struct RPlane {  // 64 read positions
+    uint64_t b0, b1, v, w[7];
+};
+
+__device__ __forceinline__ uint64_t ballot64(bool x) { return __ballot(x); }
+
+// one wave per consensus (g < n_cons) or altRead (g - n_cons); *generic set when a code 4..8 occurs
+__global__ __launch_bounds__(kT) void k_planes(const uint8_t *__restrict__ cons, const uint64_t *__restrict__ cons_off,
+                                               uint32_t n_cons, const uint64_t *__restrict__ cons_woff,
+                                               const uint8_t *__restrict__ bases, const uint8_t *__restrict__ quals,
+                                               const uint64_t *__restrict__ read_off, uint32_t n_reads,
+                                               const uint64_t *__restrict__ read_woff, CPlane *__restrict__ cp,
+                                               RPlane *__restrict__ rp, uint32_t *__restrict__ rflags,
+                                               uint32_t *__restrict__ generic) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * (kT / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    bool gen = false;
+    if (g < n_cons) {
+        const uint8_t *c = cons + cons_off[g];
+        const uint64_t C = cons_off[g + 1] - cons_off[g];
+        const uint64_t w0 = cons_woff[g], nw = cons_woff[g + 1] - w0;
+        for (uint64_t w = 0; w < nw; ++w) {
+            const uint64_t i = 64 * w + lane;
+            const uint32_t code = i < C ? base_code(c[i]) : 0x80u;
+            gen |= code >= 4 && code <= 8;
+            const bool ok = code < 4;
+            const uint64_t b0 = ballot64(ok && (code & 1)), b1 = ballot64(ok && (code & 2)), v = ballot64(ok);
+            if (lane < 3) (&cp[w0 + w].b0)[lane] = lane == 0 ? b0 : (lane == 1 ? b1 : v);
+            if (lane == 3) cp[w0 + w].pad = 0;
+        }
+    } else if (g < (uint64_t)n_cons + n_reads) {
+        const uint64_t r = g - n_cons;
+        const uint8_t *b = bases + read_off[r], *q = quals + read_off[r];
+        const uint64_t L = read_off[r + 1] - read_off[r];
+        const uint64_t w0 = read_woff[r], nw = read_woff[r + 1] - w0;
+        bool neg = false;
+        int32_t orw = 0;
+        for (uint64_t w = 0; w < nw; ++w) {
+            const uint64_t i = 64 * w + lane;
+            uint32_t code = 0x80u;
+            int32_t wt = 0;
+            if (i < L) {
+                code = base_code(b[i]);
+                wt = (int32_t)(signed char)(uint8_t)(q[i] + 33) - 33;
+            }
+            gen |= code >= 4 && code <= 8;
+            neg |= wt < 0;
+            if (wt > 0) orw |= wt;
+            const bool ok = code < 4;
+            uint64_t pl = 0;
+            const uint64_t b0 = ballot64(ok && (code & 1)), b1 = ballot64(ok && (code & 2)), v = ballot64(ok);
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                const uint64_t wk = ballot64(wt > 0 && ((wt >> k) & 1));
+                if (lane == 3 + k) pl = wk;
+            }
+            if (lane == 0) pl = b0;
+            if (lane == 1) pl = b1;
+            if (lane == 2) pl = v;
+            if (lane < 10) (&rp[w0 + w].b0)[lane] = pl;
+        }
+        const bool anyneg = ballot64(neg) != 0;
+        int32_t o = orw;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) o |= __shfl_xor(o, d, 64);
+        if (lane == 0) rflags[r] = (anyneg ? 1u : 0u) | ((uint32_t)(o ? 32 - __clz(o) : 0) << 8);
+    }
+    if (ballot64(gen) && lane == 0) atomicOr(generic, 1u);
+}
+
+// bits [sh, sh + 64) of hi:lo
+__device__ __forceinline__ uint64_t win64(uint64_t lo, uint64_t hi, uint32_t sh) {
+    return (lo >> sh) | ((hi << (63 - sh)) << 1);
+}
+
+__global__ __launch_bounds__(kT) void k_scan_bp(const int4 *__restrict__ pairs, uint64_t n_pairs,
+                                                const uint64_t *__restrict__ cons_off, const uint64_t *__restrict__ cons_woff,
+                                                const CPlane *__restrict__ cp, const uint64_t *__restrict__ read_off,
+                                                const uint64_t *__restrict__ read_woff, const RPlane *__restrict__ rp,
+                                                const uint32_t *__restrict__ rflags, const uint8_t *__restrict__ cons,
+                                                const uint8_t *__restrict__ bases, const uint8_t *__restrict__ quals,
+                                                int32_t *__restrict__ best_idx, int32_t *__restrict__ best_score) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t p = (uint64_t)blockIdx.x * (kT / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (p >= n_pairs) return;
+    const int4 P = pairs[p];  // (cons, read, orig, max_start)
+    const int C = (int)(cons_off[P.x + 1] - cons_off[P.x]);
+    const int L = (int)(read_off[P.y + 1] - read_off[P.y]);
+    const uint32_t fl = rflags[P.y];
+    const int orig = P.z;
+    if (fl & 1u) {  // a negative weight: literal scan (one lane, rare)
+        if (lane == 0) {
+            const uint8_t *cg = cons + cons_off[P.x], *bg = bases + read_off[P.y], *qg = quals + read_off[P.y];
+            int bi, bs;
+            lit_best([&](int k) { return base_code(cg[k]); }, [&](int i) { return read_word(bg, qg, i); }, L, C, orig, P.w,
+                     &bi, &bs);
+            best_idx[p] = bi;
+            best_score[p] = bs;
+        }
+        return;
+    }
+    const int nb = (int)(fl >> 8);
+    const CPlane *c = cp + cons_woff[P.x];
+    const uint64_t Wc = cons_woff[P.x + 1] - cons_woff[P.x];
+    const RPlane *r = rp + read_woff[P.y];
+    const uint64_t RW = read_woff[P.y + 1] - read_woff[P.y];
+    const int nOff = (orig > P.w ? orig : P.w) + 1;
+    uint64_t best = ~0ull;
+    for (int a = 0; 64 * a < nOff; ++a) {
+        const int k = 64 * a + (int)lane;
+        uint32_t s = 0;
+        CPlane cur = (uint64_t)a < Wc ? c[a] : CPlane{0, 0, 0, 0};
+        for (uint64_t j = 0; j < RW; ++j) {
+            const CPlane nxt = (uint64_t)a + j + 1 < Wc ? c[a + j + 1] : CPlane{0, 0, 0, 0};
+            const RPlane R = r[j];
+            const uint64_t m = win64(cur.v, nxt.v, lane) & R.v &
+                               ((win64(cur.b0, nxt.b0, lane) ^ R.b0) | (win64(cur.b1, nxt.b1, lane) ^ R.b1));
+            uint32_t t = 0;
+#pragma unroll
+            for (int b = 6; b >= 0; --b)  // constant plane indices keep R in scalar registers
+                if (b < nb) t = 2 * t + (uint32_t)__popcll(m & R.w[b]);
+            s += t;
+            cur = nxt;
+        }
+        int lim = C - k;
+        lim = lim < L ? lim : L;
+        lim = lim > 0 ? lim : 0;
+        const int sc = (int)s + 99 * (L - lim);
+        const uint32_t rank = k == orig ? 0u : (k < orig ? (uint32_t)k + 1u : (uint32_t)k);
+        const uint64_t key = ((uint64_t)(uint32_t)(sc + 0x40000000) << 32) | rank;
+        if (k < nOff && key < best) best = key;
+    }
+    best = wave_min_u64(best);
+    if (lane == 0) {
+        const uint32_t rank = (uint32_t)best;
+        best_idx[p] = rank == 0 ? orig : (rank <= (uint32_t)orig ? (int)rank - 1 : (int)rank);
+        best_score[p] = (int)(uint32_t)(best >> 32) - 0x40000000;
+    }
+}
+
 }  // namespace
 
 // Device scan over a host batch: upload, one launch per job class, download.  Jobs are maximal runs
@@ -190,39 +339,42 @@ static int realign_scan_host(oge_ctx *ctx, const uint8_t *cons, uint64_t cons_by
                              const uint8_t *bases, const uint8_t *quals, uint64_t read_bytes, const uint64_t *read_off,
                              uint32_t n_reads, const int32_t *pairs, uint64_t n_pairs, int32_t *best_index, int32_t *best_score) {
     if (!n_pairs) return OGE_OK;
+    auto clk = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double h0 = clk();
     if (n_pairs > 0x7FFFFFFFull) return oge_fail(ctx, OGE_ERR_LIMIT, "realign_scan: too many pairs");
     // validate on the host: the kernel trusts every index it is given
     if (cons_off[0] != 0 || cons_off[n_cons] != cons_bytes || read_off[0] != 0 || read_off[n_reads] != read_bytes)
         return oge_fail(ctx, OGE_ERR_ARG, "realign_scan: offset tables do not match the byte counts");
-    std::vector<ScanJob> small, big;
-    for (uint64_t i = 0; i < n_pairs;) {
-        const int32_t *p = pairs + 4 * i;
-        const uint32_t c = (uint32_t)p[0];
-        uint64_t j = i;
-        bool isbig = false;
-        for (; j < n_pairs && (uint32_t)pairs[4 * j] == c; ++j) {
-            const int32_t *q = pairs + 4 * j;
-            if ((uint32_t)q[0] >= n_cons || (uint32_t)q[1] >= n_reads || q[2] < 0 || q[2] > (1 << 28) || q[3] > (1 << 28))
-                return oge_fail(ctx, OGE_ERR_ARG, "realign_scan: pair out of range");
-            if (cons_off[c + 1] < cons_off[c] || read_off[q[1] + 1] < read_off[q[1]])
-                return oge_fail(ctx, OGE_ERR_ARG, "realign_scan: offsets not increasing");
-            if (read_off[q[1] + 1] - read_off[q[1]] > kReadCap) isbig = true;
-        }
-        if (c >= n_cons) return oge_fail(ctx, OGE_ERR_ARG, "realign_scan: pair out of range");
-        if (cons_off[c + 1] - cons_off[c] > kConsCap) isbig = true;
-        (isbig ? big : small).push_back({c, (uint32_t)i, (uint32_t)(j - i), 0});
-        i = j;
+    for (uint64_t i = 0; i < n_pairs; ++i) {
+        const int32_t *q = pairs + 4 * i;
+        if ((uint32_t)q[0] >= n_cons || (uint32_t)q[1] >= n_reads || q[2] < 0 || q[2] > (1 << 28) || q[3] > (1 << 28))
+            return oge_fail(ctx, OGE_ERR_ARG, "realign_scan: pair out of range");
     }
+    for (uint32_t c = 0; c < n_cons; ++c)
+        if (cons_off[c + 1] < cons_off[c]) return oge_fail(ctx, OGE_ERR_ARG, "realign_scan: offsets not increasing");
+    for (uint32_t r = 0; r < n_reads; ++r)
+        if (read_off[r + 1] < read_off[r]) return oge_fail(ctx, OGE_ERR_ARG, "realign_scan: offsets not increasing");
+    // plane word offsets: a consensus gets one zero word past its end (the last window's high half)
+    std::vector<uint64_t> cwo(n_cons + 1, 0), rwo(n_reads + 1, 0);
+    for (uint32_t c = 0; c < n_cons; ++c) cwo[c + 1] = cwo[c] + (cons_off[c + 1] - cons_off[c] + 63) / 64 + 1;
+    for (uint32_t r = 0; r < n_reads; ++r) rwo[r + 1] = rwo[r] + (read_off[r + 1] - read_off[r] + 63) / 64;
+    const double h1 = clk();
     uint8_t *dc = (uint8_t *)ctx->ws("rs_cons", cons_bytes + 16);
     uint64_t *dco = (uint64_t *)ctx->ws("rs_cons_off", (n_cons + 1) * 8);
     uint8_t *db = (uint8_t *)ctx->ws("rs_bases", read_bytes + 16);
     uint8_t *dq = (uint8_t *)ctx->ws("rs_quals", read_bytes + 16);
     uint64_t *dro = (uint64_t *)ctx->ws("rs_read_off", (n_reads + 1) * 8);
     int4 *dp = (int4 *)ctx->ws("rs_pairs", n_pairs * 16);
-    ScanJob *dj = (ScanJob *)ctx->ws("rs_jobs", (small.size() + big.size() + 1) * sizeof(ScanJob));
     int32_t *di = (int32_t *)ctx->ws("rs_idx", n_pairs * 4);
     int32_t *ds = (int32_t *)ctx->ws("rs_score", n_pairs * 4);
-    if (!dc || !dco || !db || !dq || !dro || !dp || !dj || !di || !ds) return OGE_ERR_HIP;
+    uint64_t *dcwo = (uint64_t *)ctx->ws("rs_cwo", (n_cons + 1) * 8);
+    uint64_t *drwo = (uint64_t *)ctx->ws("rs_rwo", (n_reads + 1) * 8);
+    CPlane *dcp = (CPlane *)ctx->ws("rs_cplanes", (cwo[n_cons] + 1) * sizeof(CPlane));
+    RPlane *drp = (RPlane *)ctx->ws("rs_rplanes", (rwo[n_reads] + 1) * sizeof(RPlane));
+    uint32_t *drf = (uint32_t *)ctx->ws("rs_rflags", ((uint64_t)n_reads + 1) * 4);
+    uint32_t *dgen = (uint32_t *)ctx->ws("rs_generic", 4);
+    if (!dc || !dco || !db || !dq || !dro || !dp || !di || !ds || !dcwo || !drwo || !dcp || !drp || !drf || !dgen)
+        return OGE_ERR_HIP;
     hipStream_t s = ctx->stream;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dc, cons, cons_bytes, hipMemcpyHostToDevice, s));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dco, cons_off, (n_cons + 1) * 8, hipMemcpyHostToDevice, s));
@@ -230,23 +382,62 @@ static int realign_scan_host(oge_ctx *ctx, const uint8_t *cons, uint64_t cons_by
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dq, quals, read_bytes, hipMemcpyHostToDevice, s));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dro, read_off, (n_reads + 1) * 8, hipMemcpyHostToDevice, s));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dp, pairs, n_pairs * 16, hipMemcpyHostToDevice, s));
-    std::vector<ScanJob> all(small);
-    all.insert(all.end(), big.begin(), big.end());
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(dj, all.data(), all.size() * sizeof(ScanJob), hipMemcpyHostToDevice, s));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(dcwo, cwo.data(), (n_cons + 1) * 8, hipMemcpyHostToDevice, s));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(drwo, rwo.data(), (n_reads + 1) * 8, hipMemcpyHostToDevice, s));
+    OGE_HIP_TRY(ctx, hipMemsetAsync(dgen, 0, 4, s));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(s));
+    const double h2 = clk();
+    uint32_t generic = 0;
     OgeStageTimer *t = ctx->begin_stage("realign_scan");
-    if (!small.empty()) {
-        hipLaunchKernelGGL(k_realign_scan<false>, dim3((uint32_t)small.size()), dim3(kT), 0, s, dc, dco, db, dq, dro, dp, dj, di, ds);
+    const uint64_t items = (uint64_t)n_cons + n_reads;
+    hipLaunchKernelGGL(k_planes, dim3((uint32_t)((items + 3) / 4)), dim3(kT), 0, s, dc, dco, n_cons, dcwo, db, dq, dro, n_reads,
+                       drwo, dcp, drp, drf, dgen);
+    OGE_LAUNCH_CHECK(ctx);
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&generic, dgen, 4, hipMemcpyDeviceToHost, s));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(s));
+    if (!generic) {
+        hipLaunchKernelGGL(k_scan_bp, dim3((uint32_t)((n_pairs + 3) / 4)), dim3(kT), 0, s, dp, n_pairs, dco, dcwo, dcp, dro, drwo,
+                           drp, drf, dc, db, dq, di, ds);
         OGE_LAUNCH_CHECK(ctx);
-    }
-    if (!big.empty()) {
-        hipLaunchKernelGGL(k_realign_scan<true>, dim3((uint32_t)big.size()), dim3(kT), 0, s, dc, dco, db, dq, dro, dp,
-                           dj + small.size(), di, ds);
-        OGE_LAUNCH_CHECK(ctx);
+    } else {
+        // lower-case bases or '*' present: byte-wise kernel, one workgroup per run of same-consensus pairs
+        std::vector<ScanJob> small, big;
+        for (uint64_t i = 0; i < n_pairs;) {
+            const uint32_t c = (uint32_t)pairs[4 * i];
+            uint64_t j = i;
+            bool isbig = cons_off[c + 1] - cons_off[c] > kConsCap;
+            for (; j < n_pairs && (uint32_t)pairs[4 * j] == c; ++j) {
+                const uint32_t rd = (uint32_t)pairs[4 * j + 1];
+                if (read_off[rd + 1] - read_off[rd] > kReadCap) isbig = true;
+            }
+            (isbig ? big : small).push_back({c, (uint32_t)i, (uint32_t)(j - i), 0});
+            i = j;
+        }
+        ScanJob *dj = (ScanJob *)ctx->ws("rs_jobs", (small.size() + big.size() + 1) * sizeof(ScanJob));
+        if (!dj) return OGE_ERR_HIP;
+        std::vector<ScanJob> all(small);
+        all.insert(all.end(), big.begin(), big.end());
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(dj, all.data(), all.size() * sizeof(ScanJob), hipMemcpyHostToDevice, s));
+        if (!small.empty()) {
+            hipLaunchKernelGGL(k_realign_scan<false>, dim3((uint32_t)small.size()), dim3(kT), 0, s, dc, dco, db, dq, dro, dp, dj, di,
+                               ds);
+            OGE_LAUNCH_CHECK(ctx);
+        }
+        if (!big.empty()) {
+            hipLaunchKernelGGL(k_realign_scan<true>, dim3((uint32_t)big.size()), dim3(kT), 0, s, dc, dco, db, dq, dro, dp,
+                               dj + small.size(), di, ds);
+            OGE_LAUNCH_CHECK(ctx);
+        }
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(s));  // `all` must outlive the upload
     }
     ctx->end_stage(t);
+    ctx->last_scan_generic = generic != 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(best_index, di, n_pairs * 4, hipMemcpyDeviceToHost, s));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(best_score, ds, n_pairs * 4, hipMemcpyDeviceToHost, s));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(s));
+    ctx->scan_t[0] = h1 - h0;
+    ctx->scan_t[1] = h2 - h1;
+    ctx->scan_t[2] = clk() - h2;
     return OGE_OK;
 }
 
@@ -324,15 +515,17 @@ int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len,
     int rc = oge::realign_run(names, recs, rec_off, n, fasta_path, intervals_path, P, scan, r->recs, r->offs, st, err);
     st.t_run = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
     if (rc) return scan_rc ? scan_rc : oge_fail(ctx, rc, ("oge_localrealign: " + err).c_str());
-    char buf[1024];
+    char buf[2048];
     snprintf(buf, sizeof buf,
              "{\"intervals\": %llu, \"intervals_cleaned\": %llu, \"reads_realigned\": %llu, \"scan_pairs\": %llu, "
              "\"scan_ops\": %llu, \"scan_kernel_ms\": %.4f, \"t_bin\": %.4f, \"t_prepare\": %.4f, \"t_scan\": %.4f, "
              "\"t_decide\": %.4f, \"t_emit\": %.4f, \"t_run\": %.4f, \"t_fasta\": %.4f, \"t_decode\": %.4f, "
-             "\"t_mate\": %.4f, \"t_release\": %.4f}",
+             "\"t_mate\": %.4f, \"t_release\": %.4f, \"t_scan_build\": %.4f, \"t_scan_validate\": %.4f, \"t_scan_upload\": %.4f, "
+             "\"t_scan_device\": %.4f, \"mate_segments\": %llu, \"scan_kernel\": \"%s\"}",
              (unsigned long long)st.intervals, (unsigned long long)st.intervals_cleaned, (unsigned long long)st.reads_realigned,
              (unsigned long long)st.scan_pairs, (unsigned long long)st.scan_ops, scan_kernel_ms, st.t_bin, st.t_prepare,
-             st.t_scan, st.t_decide, st.t_emit, st.t_run, st.t_fasta, st.t_decode, st.t_mate, st.t_release);
+             st.t_scan, st.t_decide, st.t_emit, st.t_run, st.t_fasta, st.t_decode, st.t_mate, st.t_release, st.t_scan_build, ctx->scan_t[0], ctx->scan_t[1], ctx->scan_t[2],
+             (unsigned long long)st.mate_segments, ctx->last_scan_generic ? "k_realign_scan (byte-wise)" : "k_planes + k_scan_bp");
     r->stats = buf;
     *out = r.release();
     return OGE_OK;

@@ -1,7 +1,8 @@
 """GPU: local realignment through the C ABI.
 
-* oge_realign_scan (the HIP offset-scan kernel) against the oracle's literal findBestOffset
-  restatement on random batches, including the LDS-overflow path (consensus > 40 KB, read > 4 KB),
+* oge_realign_scan (the HIP offset-scan kernels: bit-plane k_scan_bp, byte-wise k_realign_scan for
+  batches with lower-case/'*' bases) against the oracle's literal findBestOffset restatement on
+  random batches, including long consensuses/reads (the byte-wise kernel's LDS-overflow path),
   offsets past the consensus end and negative quality weights (literal early-exit path);
 * oge_localrealign (host phases + GPU scan) against the REFERENCE's own outputs (tests/golden/rl_*).
 """
@@ -18,6 +19,20 @@ pytestmark = pytest.mark.gpu
 def test_gpu_scan_matches_oracle(ctx, seed):
     rng = np.random.default_rng(100 + seed)
     b = random_batch(rng, n_cons=12, reads_per=8, qual_max=(120 if seed % 3 == 0 else 60))
+    gi, gs = ctx.realign_scan(*b)
+    oi, os_ = oracle.realign_scan(*b)
+    assert np.array_equal(gs, os_)
+    assert np.array_equal(gi, oi)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_scan_bitplane_path(ctx, seed):
+    """Upper-case batches run k_planes + k_scan_bp (2-bit planes); lower case / '*' anywhere in a
+    batch sends it to the byte-wise kernel (covered above).  Multi-word reads, offsets past the
+    consensus end, zero and negative weights."""
+    rng = np.random.default_rng(500 + seed)
+    b = random_batch(rng, n_cons=16, reads_per=10, cons_len=(30, 700), read_len=(5, 300), alphabet=b"ACGTN",
+                     qual_max=(120 if seed % 2 else 93))
     gi, gs = ctx.realign_scan(*b)
     oi, os_ = oracle.realign_scan(*b)
     assert np.array_equal(gs, os_)
