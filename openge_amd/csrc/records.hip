@@ -13,10 +13,15 @@
 //
 // k_gather16 (output order, records read once and written once): a wave owns 64 consecutive
 //   output records, whose output bytes are one contiguous range.  Lanes write that range as
-//   aligned 16-byte chunks; a chunk is one unaligned 16-byte load of the source record (two, merged,
-//   where a record boundary falls inside the chunk -- gfx950 serves unaligned dwordx4 at stream
-//   rate, tools/probes/unaligned.hip), with bin and FLAG 0x400 patched in registers.  Only the two
-//   chunks at the ends of a batch, shared with neighbouring waves, fall back to byte stores.
+//   aligned 16-byte chunks; a chunk is one unaligned 16-byte load of the source record (gfx950 serves
+//   unaligned dwordx4 at stream rate, tools/probes/unaligned.hip).  Where a record boundary falls
+//   inside the chunk it is the tail 16 bytes of one record and the head 16 bytes of the next,
+//   funnel-shifted together -- every load stays inside its record, so no cache line outside the
+//   records is fetched.  Bin and FLAG 0x400 are patched in registers.  Only the two chunks at the
+//   ends of a batch, shared with neighbouring waves, fall back to byte stores.
+#include <algorithm>
+#include <cstdlib>
+
 #include "oge_ctx.h"
 #include "bam_layout.h"
 #include "dev_util.h"
@@ -235,11 +240,17 @@ __global__ __launch_bounds__(kT) void k_input_pass(OgePassArgs a) {
 // ---------------------------------------------------------------- gather
 __device__ __forceinline__ uint4 ldu128(const uint8_t *p) { return *(const uint4 *)p; }
 
-__device__ __forceinline__ uint32_t merge32(uint32_t a, uint32_t b, int keep) {  // keep = low bytes taken from a
-    if (keep <= 0) return b;
-    if (keep >= 4) return a;
-    const uint32_t m = (1u << (8 * keep)) - 1u;
-    return (a & m) | (b & ~m);
+// bytes [o, o + 16) of the 32-byte string t ++ h (1 <= o <= 15)
+__device__ __forceinline__ uint4 funnel16(uint4 t, uint4 h, int o) {
+    const uint64_t W0 = ((uint64_t)t.y << 32) | t.x, W1 = ((uint64_t)t.w << 32) | t.z;
+    const uint64_t W2 = ((uint64_t)h.y << 32) | h.x, W3 = ((uint64_t)h.w << 32) | h.z;
+    const uint32_t sh = 8u * (uint32_t)o;  // 8..120
+    const bool hi = sh >= 64;
+    const uint32_t r = sh & 63;
+    const uint64_t a0 = hi ? W1 : W0, a1 = hi ? W2 : W1, a2 = hi ? W3 : W2;
+    const uint64_t q0 = r ? (a0 >> r) | (a1 << (64 - r)) : a0;
+    const uint64_t q1 = r ? (a1 >> r) | (a2 << (64 - r)) : a1;
+    return make_uint4((uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32));
 }
 
 __device__ __forceinline__ void set_byte(uint4 &v, int pos, uint32_t byte) {
@@ -265,6 +276,32 @@ __device__ __forceinline__ uint32_t patch_byte(uint64_t ro, uint32_t byte, uint3
     if (ro == 15) return (bf >> 8) & 0xff;
     if (ro == 19) return (bf >> 16) & 0xff;
     return byte;
+}
+
+// Where output chunk A (16-byte aligned, relative position rel = A - D0 in the wave's batch) reads
+// from: record k of the batch at byte src of its source, or -- when a record boundary falls inside
+// the chunk (two) -- the last 16 bytes of record k (src = its length - 16) and the first 16 of k+1.
+struct GChunk {
+    int k;
+    bool full, two;
+    int64_t rel, rs;
+    uint64_t src;
+};
+__device__ __forceinline__ GChunk gchunk_plan(const uint32_t *sdw, uint32_t cnt, uint64_t A, uint64_t D0, uint64_t Dend) {
+    GChunk g;
+    g.rel = (int64_t)A - (int64_t)D0;
+    const int64_t x0 = g.rel < 0 ? 0 : g.rel;
+    int lo = 0, hi = (int)cnt - 1;  // record holding byte x0
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((int64_t)sdw[mid] <= x0) lo = mid; else hi = mid - 1;
+    }
+    g.k = lo;
+    g.rs = sdw[lo];
+    g.full = g.rel >= 0 && A + 16 <= Dend;
+    g.two = (lo + 1 < (int)cnt) && (int64_t)sdw[lo + 1] < g.rel + 16;
+    g.src = g.two ? (uint64_t)((int64_t)sdw[lo + 1] - g.rs) - 16 : (uint64_t)(g.rel - g.rs);
+    return g;
 }
 
 template <bool SMETA>
@@ -317,36 +354,25 @@ __global__ __launch_bounds__(kT) void k_gather16(OgePassArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint64_t Dend = D0 + sd[w][cnt];
         for (uint64_t A = (D0 & ~15ull) + 16ull * lane; A < Dend; A += 1024) {
-            const int64_t rel = (int64_t)A - (int64_t)D0;  // chunk start relative to the batch
-            const int64_t x0 = rel < 0 ? 0 : rel;
-            int lo = 0, hi = (int)cnt - 1;                 // record holding byte x0
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if ((int64_t)sd[w][mid] <= x0) lo = mid; else hi = mid - 1;
-            }
-            const int k = lo;
-            const int64_t rs = sd[w][k];
-            const bool full = rel >= 0 && A + 16 <= Dend;
-            const bool two = (k + 1 < (int)cnt) && (int64_t)sd[w][k + 1] < rel + 16;
-            if (full && !(two && ss[w][k + 1] < 16)) {
-                uint4 v = ldu128(a.recs + ss[w][k] + (rel - rs));
-                patch_chunk(v, rel, rs, sbf[w][k]);
-                if (two) {
-                    const int64_t rs2 = sd[w][k + 1];
-                    const int keep = (int)(rs2 - rel);
-                    uint4 v2 = ldu128(a.recs + ss[w][k + 1] - keep);
-                    patch_chunk(v2, rel, rs2, sbf[w][k + 1]);
-                    v.x = merge32(v.x, v2.x, keep);
-                    v.y = merge32(v.y, v2.y, keep - 4);
-                    v.z = merge32(v.z, v2.z, keep - 8);
-                    v.w = merge32(v.w, v2.w, keep - 12);
+            const GChunk g = gchunk_plan(sd[w], cnt, A, D0, Dend);
+            if (g.full) {
+                uint4 v = ldu128(a.recs + ss[w][g.k] + g.src);
+                if (g.two) {
+                    // the last `keep` bytes of record k and the head of record k+1, each loaded from
+                    // inside its own record (no bytes of source neighbours, which would pull in cache
+                    // lines no record here needs), funnelled together
+                    const int64_t rs2 = sd[w][g.k + 1];
+                    const uint4 h = ldu128(a.recs + ss[w][g.k + 1]);
+                    v = funnel16(v, h, 16 - (int)(rs2 - g.rel));
+                    patch_chunk(v, g.rel, rs2, sbf[w][g.k + 1]);
                 }
+                patch_chunk(v, g.rel, g.rs, sbf[w][g.k]);
                 *(uint4 *)(a.out + A) = v;
             } else {
-                // batch edge (bytes shared with neighbouring waves) or a record at the arena start
+                // batch edge: bytes shared with neighbouring waves
                 const uint64_t xe = (A + 16 < Dend ? A + 16 : Dend) - D0;
-                int kk = k;
-                for (uint64_t x = (uint64_t)x0; x < xe; ++x) {
+                int kk = g.k;
+                for (uint64_t x = (uint64_t)(g.rel < 0 ? 0 : g.rel); x < xe; ++x) {
                     while (kk + 1 < (int)cnt && sd[w][kk + 1] <= x) ++kk;
                     const uint64_t ro = x - sd[w][kk];
                     a.out[D0 + x] = (uint8_t)patch_byte(ro, a.recs[ss[w][kk] + ro], sbf[w][kk]);
@@ -361,7 +387,11 @@ __global__ __launch_bounds__(kT) void k_gather16(OgePassArgs a) {
 
 int oge_input_pass(oge_ctx *ctx, const OgePassArgs &a) {
     if (!a.n) return OGE_OK;
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, kTileRecs), 256u * 8u);
+    static const uint64_t cap = [] {
+        const char *e = getenv("OGE_INPUT_BLOCKS");
+        return (e && *e) ? std::max<uint64_t>(256, strtoull(e, nullptr, 10)) : 256ull * 8u;
+    }();
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, kTileRecs), cap);
     if (a.meta && a.keys)
         hipLaunchKernelGGL((k_input_pass<true, true>), dim3(blocks), dim3(kT), 0, ctx->stream, a);
     else if (a.meta)
@@ -376,7 +406,11 @@ int oge_input_pass(oge_ctx *ctx, const OgePassArgs &a) {
 
 int oge_gather_pass(oge_ctx *ctx, const OgePassArgs &a) {
     if (!a.n) return OGE_OK;
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, 64 * (kT / 64)), 256u * 16u);
+    static const uint64_t cap = [] {
+        const char *e = getenv("OGE_GATHER_BLOCKS");
+        return (e && *e) ? std::max<uint64_t>(256, strtoull(e, nullptr, 10)) : 131072ull;
+    }();
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, 64 * (kT / 64)), cap);
     if (a.smeta)
         hipLaunchKernelGGL(k_gather16<true>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
     else
