@@ -77,6 +77,12 @@ int oge_sort_coord_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_of
 int oge_gather_records_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
                            uint64_t n, uint8_t *d_out, uint64_t *d_out_off);
 
+/* Device primitive used by every sort above, exposed for tests: stable LSD radix sort of
+ * (u64 key, u32 value) pairs on the key bits in bit_mask (d_vals/d_vtmp may be NULL).  The sorted
+ * pairs end in (d_keys, d_vals) when *in_tmp_out == 0, in (d_ktmp, d_vtmp) when 1. */
+int oge_radix_sort_pairs_dev(oge_ctx *ctx, uint64_t *d_keys, uint32_t *d_vals, uint64_t *d_ktmp, uint32_t *d_vtmp,
+                             uint64_t n, uint64_t bit_mask, int *in_tmp_out);
+
 /* ---- duplicate marking (MarkDuplicates) ------------------------------------------- */
 typedef struct oge_markdup_opts {
     int32_t n_ref;

@@ -359,3 +359,16 @@ int oge_synth_records_dev(oge_ctx *ctx, const void *params, const uint64_t *d_of
     return oge_synth_records_range_dev(ctx, params, 0, 2 * ((const oge_synth_params *)params)->n_pairs, d_offs, d_out);
 }
 }  // extern "C"
+
+extern "C" int oge_radix_sort_pairs_dev(oge_ctx *ctx, uint64_t *d_keys, uint32_t *d_vals, uint64_t *d_ktmp, uint32_t *d_vtmp,
+                                        uint64_t n, uint64_t bit_mask, int *in_tmp_out) {
+    if (!ctx || (n && (!d_keys || !d_ktmp)) || ((d_vals == nullptr) != (d_vtmp == nullptr)) || !in_tmp_out)
+        return oge_fail(ctx, OGE_ERR_ARG, "oge_radix_sort_pairs_dev: bad arguments");
+    hipSetDevice(ctx->device);
+    uint64_t *ko = d_keys;
+    uint32_t *vo = d_vals;
+    int rc = oge_radix_sort_pairs(ctx, d_keys, d_vals, d_ktmp, d_vtmp, n, bit_mask, &ko, d_vals ? &vo : nullptr);
+    if (rc) return rc;
+    *in_tmp_out = ko != d_keys;
+    return OGE_OK;
+}

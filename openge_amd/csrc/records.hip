@@ -1,7 +1,8 @@
 // records.hip -- the two streaming passes over BAM records of the sort+dedup pipeline.
 //
 // k_input_pass (input order, records read once): a 256-thread block stages a tile of 256
-//   consecutive records (~73 KB for 150 bp reads) into LDS with aligned 16-byte loads, then each
+//   consecutive records (~73 KB for 150 bp reads) into LDS with 16-byte LDS-DMA loads
+//   (global_load_lds_dwordx4: the whole tile in flight at once), then each
 //   thread parses one record from LDS and emits
 //     KEYS: the coordinate sort key (sort.hip) and its index
 //     META: a 32-byte summary -- the fragment ReadEnds fields of buildReadEnds
@@ -214,9 +215,16 @@ __global__ __launch_bounds__(kT) void k_input_pass(OgePassArgs a) {
     for (uint64_t r0 = (uint64_t)blockIdx.x * kTileRecs; r0 < a.n; r0 += (uint64_t)gridDim.x * kTileRecs) {
         const uint64_t r1 = (a.n - r0) < kTileRecs ? a.n : r0 + kTileRecs;
         if (threadIdx.x == 0) {
+            // window = [first record, next tile's first record); only a cache: every record is
+            // checked against it below and parsed from global memory when it is not inside
             const uint64_t b0 = a.off[r0] & ~15ull;
-            const uint64_t last = a.off[r1 - 1];
-            const uint64_t e = last + 4 + oge_ldu32(a.recs + last);
+            uint64_t e;
+            if (r1 < a.n) {
+                e = a.off[r1];
+            } else {
+                const uint64_t last = a.off[r1 - 1];
+                e = last + 4 + oge_ldu32(a.recs + last);
+            }
             tb[0] = b0;
             tb[1] = (e > b0 && e - b0 <= kLdsCap) ? e : b0;  // empty window: parse from global
         }
@@ -224,7 +232,13 @@ __global__ __launch_bounds__(kT) void k_input_pass(OgePassArgs a) {
         const uint64_t b0 = tb[0], b1 = tb[1];
         const uint64_t nch = (b1 - b0 + 15) >> 4;
         const uint4 *g = (const uint4 *)(a.recs + b0);
-        for (uint64_t ch = threadIdx.x; ch < nch; ch += kT) tile[ch] = g[ch];
+        // LDS-DMA: every chunk load of the tile in flight at once, no VGPR round trip
+        const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        for (uint64_t c0 = (uint64_t)wv * 64; c0 < nch; c0 += kT)
+            if (c0 + ln < nch)
+                __builtin_amdgcn_global_load_lds((const void *)(g + c0 + ln),
+                                                 (__attribute__((address_space(3))) void *)(tile + c0), 16, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const uint64_t i = r0 + threadIdx.x;
         if (i < r1) {

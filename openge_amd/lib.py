@@ -167,6 +167,7 @@ def lib() -> C.CDLL:
         "oge_sort_coord": (C.c_int, [vp, vp, u64, vp, u64, i32, vp]),
         "oge_sort_coord_dev": (C.c_int, [vp, vp, vp, u64, i32, vp]),
         "oge_gather_records_dev": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
+        "oge_radix_sort_pairs_dev": (C.c_int, [vp, vp, vp, vp, vp, u64, u64, C.POINTER(C.c_int)]),
         "oge_markdup": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, C.POINTER(u64)]),
         "oge_markdup_dev": (C.c_int, [vp, vp, vp, u64, vp, vp, C.c_int, C.POINTER(u64)]),
         "oge_sort_markdup_dev": (C.c_int, [vp, vp, vp, u64, vp, vp, vp, vp, C.POINTER(u64)]),
@@ -383,6 +384,13 @@ class Context:
 
     def gather_records_dev(self, d_recs, d_off, d_perm, n, d_out, d_out_off) -> None:
         check(lib().oge_gather_records_dev(self.h, d_recs, d_off, d_perm, n, d_out, d_out_off), self.h)
+
+    def radix_sort_pairs_dev(self, d_keys, d_vals, d_ktmp, d_vtmp, n, bit_mask) -> bool:
+        """Stable radix sort of device (u64 key, u32 value) pairs on the bits of bit_mask; returns True
+        when the result sits in the tmp buffers."""
+        t = C.c_int()
+        check(lib().oge_radix_sort_pairs_dev(self.h, d_keys, d_vals, d_ktmp, d_vtmp, n, bit_mask, C.byref(t)), self.h)
+        return bool(t.value)
 
     def markdup_dev(self, d_recs, d_off, n, opts: MarkdupOpts, d_dup, apply: bool = True) -> int:
         nd = C.c_uint64()
