@@ -103,6 +103,12 @@ typedef struct oge_markdup_opts {
     /* Test knob: keep only this many bits (1..47) of the 48-bit pair-key hash, to force the
      * collision paths of the mate join.  0 = full hash.  Results must not change. */
     int32_t debug_hash_bits;
+    /* Split-by-chromosome emulation (cmd/command_dedup.cpp:71-106,
+     * algorithms/split_by_chromosome.cpp:45-48): K > 1 gives the result of K MarkDuplicates chains
+     * fed refID % K (refID < 0 -> chain 0) -- mates in different chains never pair.  The
+     * reference's default when --nosplit is absent, with K = min(12, threads / 2).  0 or 1 =
+     * --nosplit.  Not combinable with compat_nonverbose_index. */
+    int32_t split_chains;
 } oge_markdup_opts;
 
 /* dup_out[i] (per input record, input order = record index): 1 if record i is flagged

@@ -42,6 +42,7 @@ __global__ __launch_bounds__(kT) void k_cand_flags(const RecMeta *__restrict__ m
 // ReadEndsMap's first/second-seen).
 struct CandKey {
     uint32_t ib, hb;
+    int32_t split_k;
     __host__ __device__ uint64_t idx_mask() const { return (1ull << ib) - 1; }
     __host__ __device__ uint64_t hash_of(uint64_t k) const { return k >> ib; }
 };
@@ -68,7 +69,10 @@ __device__ __forceinline__ uint8_t key_byte(const uint8_t *rgv, uint32_t rgl, co
 // Exact RG ":" name comparison (the ReadEndsMap key, mark_duplicates.cpp:210-213) of the records
 // summarised by A and B.  Same listed read group -> the keys are equal iff the names are, which is
 // one 16-byte-chunked compare at record byte 36; anything else compares the whole key strings.
-__device__ bool same_pair_key(const uint8_t *recs, const RecMeta &A, const RecMeta &B) {
+// With split_k > 1 the key also carries the chain (refID % K): SplitByChromosome gives every chain
+// its own MarkDuplicates, so mates routed to different chains never meet.
+__device__ bool same_pair_key(const uint8_t *recs, const RecMeta &A, const RecMeta &B, int32_t split_k) {
+    if (split_k > 1 && A.seq % split_k != B.seq % split_k) return false;
     if (A.rgi == B.rgi && A.rgi != OGE_RGI_UNLISTED && (A.m & B.m & OGE_M_NAMEFIT)) {
         // same listed read group: keys equal iff names equal; both names sit NUL-terminated and
         // zero-padded in the metadata slots
@@ -126,7 +130,7 @@ __global__ __launch_bounds__(kT) void k_pair_runs(const uint8_t *__restrict__ re
                 for (uint64_t y = x + 1; y < e; ++y) {
                     if (used[y]) continue;
                     const uint32_t b = (uint32_t)(ckey[y] & ck.idx_mask());
-                    if (same_pair_key(recs, A, meta[b])) {
+                    if (same_pair_key(recs, A, meta[b], ck.split_k)) {
                         used[x] = used[y] = 1;
                         const unsigned int t = atomicAdd(nextra, 1u);
                         extra[t] = ((uint64_t)a << 32) | b;
@@ -148,6 +152,7 @@ __global__ __launch_bounds__(kT) void k_pair_compact_scan(const uint32_t *__rest
 
 struct KeyLayout {
     uint32_t sb, lb;  // bits for refID and library id
+    int32_t split_k;
 };
 
 __device__ __forceinline__ int orient_byte(bool r1neg, bool r2neg) {
@@ -166,7 +171,7 @@ __global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ 
     uint32_t a = (uint32_t)(pairs[p] >> 32), b = (uint32_t)pairs[p];  // a seen first (smaller record index)
     if (a > b) { uint32_t t = a; a = b; b = t; }
     const RecMeta A = meta[a], B = meta[b];
-    const uint64_t bad = same_pair_key(recs, A, B) ? 0ull : (1ull << 63);
+    const uint64_t bad = same_pair_key(recs, A, B, L.split_k) ? 0ull : (1ull << 63);
     const uint64_t ma = A.m, mb = B.m;
     const int32_t sa = A.seq, ca = A.coord, sb_ = B.seq, cb = B.coord;
     const bool reva = (ma & OGE_M_REV) != 0, revb = (mb & OGE_M_REV) != 0;
@@ -328,6 +333,10 @@ uint64_t bits_mask_hi32(uint64_t n) {
 int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, const char *name, RecMeta **meta,
                         OgeRgTable *rg) {
     if (!opts) return oge_fail(ctx, OGE_ERR_ARG, "markdup: opts is NULL");
+    if (opts->split_chains < 0 || opts->split_chains > 4096)
+        return oge_fail(ctx, OGE_ERR_ARG, "markdup: split_chains out of [0, 4096]");
+    if (opts->split_chains > 1 && opts->compat_nonverbose_index)
+        return oge_fail(ctx, OGE_ERR_ARG, "markdup: split_chains > 1 with compat_nonverbose_index is not supported");
     if (n > 0xFFFFFFFEull) return oge_fail(ctx, OGE_ERR_LIMIT, "markdup: more than 2^32-2 records");
     if (opts->n_rg < 0 || (opts->n_rg && (!opts->rg_ids || !opts->rg_lib)))
         return oge_fail(ctx, OGE_ERR_ARG, "markdup: bad read-group table");
@@ -352,6 +361,7 @@ int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, 
     rg->lib = lib;
     rg->n_rg = opts->n_rg;
     rg->unknown_lib = opts->unknown_lib;
+    rg->split_k = opts->split_chains;
     // the host copies above read pageable memory; make sure they are done before returning
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return OGE_OK;
@@ -368,7 +378,7 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     if (opts->unknown_lib < 0) return oge_fail(ctx, OGE_ERR_ARG, "markdup: negative library id");
     for (int32_t g = 0; g < opts->n_rg; ++g)
         if (opts->rg_lib[g] < 0) return oge_fail(ctx, OGE_ERR_ARG, "markdup: negative library id");
-    const KeyLayout L{bits_for((uint64_t)std::max(opts->n_ref, 1)), bits_for((uint64_t)maxlib)};
+    const KeyLayout L{bits_for((uint64_t)std::max(opts->n_ref, 1)), bits_for((uint64_t)maxlib), opts->split_chains};
     if (L.sb + L.lb + 34 > 47 || L.sb + L.lb > 16)
         return oge_fail(ctx, OGE_ERR_LIMIT, "markdup: too many references x libraries for the packed group key");
     unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
@@ -404,6 +414,7 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     CandKey ckl;
     ckl.ib = bits_for(n - 1);
     ckl.hb = std::min<uint32_t>(48, 64 - ckl.ib);
+    ckl.split_k = opts->split_chains;
     if (opts->debug_hash_bits > 0 && (uint32_t)opts->debug_hash_bits < ckl.hb) ckl.hb = (uint32_t)opts->debug_hash_bits;
     hipLaunchKernelGGL(k_cand_scatter, dim3(nb), dim3(kT), 0, ctx->stream, meta, n, (const uint32_t *)cpos, ckl, ck);
     OGE_LAUNCH_CHECK(ctx);

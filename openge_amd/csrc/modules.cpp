@@ -113,7 +113,7 @@ struct MdOpts {
     std::string ids;
     std::vector<int16_t> libs;
 };
-static void markdup_opts(const ReadBatch &b, bool compat, MdOpts &m) {
+static void markdup_opts(const ReadBatch &b, bool compat, int split, MdOpts &m) {
     std::map<std::string, int16_t> lib_ids;
     int16_t next = 1;
     for (auto &rg : b.header.rg) {
@@ -134,6 +134,7 @@ static void markdup_opts(const ReadBatch &b, bool compat, MdOpts &m) {
     m.o.n_rg = (int32_t)b.header.rg.size();
     m.o.unknown_lib = unk != lib_ids.end() ? unk->second : next;
     m.o.compat_nonverbose_index = compat ? 1 : 0;
+    m.o.split_chains = split;
 }
 
 // ----------------------------------------------------------------------------------- ReadSorter
@@ -151,7 +152,7 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
     MarkDuplicates *md = dynamic_cast<MarkDuplicates *>(sink_);
     if (md) {  // mergesort -M: one fused device pipeline (sort, dedup, gather with 0x400 applied)
         MdOpts m;
-        markdup_opts(b, md->compatNonverbose, m);
+        markdup_opts(b, md->compatNonverbose, md->splitChains, m);
         uint64_t nd = 0;
         rc = oge_sort_markdup_dev(cc.ctx, b.d_recs, b.d_offs, b.n, &m.o, (uint32_t *)perm, (uint8_t *)out,
                                   (uint64_t *)out_off, &nd);
@@ -182,7 +183,7 @@ int MarkDuplicates::runInternal(ChainContext &cc, ReadBatch &b) {
     void *dup = nullptr;
     if (oge_dev_alloc(cc.ctx, b.n + 1, &dup)) return cc.fail("device allocation");
     MdOpts m;
-    markdup_opts(b, compatNonverbose, m);
+    markdup_opts(b, compatNonverbose, splitChains, m);
     uint64_t nd = 0;
     int rc = oge_markdup_dev(cc.ctx, b.d_recs, b.d_offs, b.n, &m.o, (uint8_t *)dup, 1, &nd);
     if (!rc) rc = oge_ctx_sync(cc.ctx);

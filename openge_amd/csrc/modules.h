@@ -104,6 +104,7 @@ public:
     explicit MarkDuplicates(const std::string &tmpdir = "/tmp/") : AlgorithmModule("MarkDuplicates") { (void)tmpdir; }
     bool removeDuplicates = false;
     bool compatNonverbose = false;  // reproduce the index bug of runs without -v
+    int splitChains = 0;            // > 1 = the result of the split-by-chromosome chains
     uint64_t duplicates = 0;
 protected:
     int runInternal(ChainContext &cc, ReadBatch &b) override;

@@ -4,9 +4,11 @@
 // same module chain the reference builds (commands/command_mergesort.cpp:68-117,
 // command_dedup.cpp:48-69, command_localrealign.cpp:37-75) out of the modules in modules.h.
 //
-// Deliberate differences: dedup always has `-v --nosplit` semantics (Q1, Q3;
-// --compat-nonverbose-dedup reproduces the non-verbose index bug); sort-by-name (-b), region/MAPQ
-// filters (-r/-q) and SAM/FASTQ output are not provided and fail loudly.
+// Deliberate differences: dedup defaults to `-v --nosplit` semantics (Q1, Q3).
+// --compat-nonverbose-dedup reproduces the non-verbose index bug; --split-chains K reproduces K
+// split-by-chromosome chains, and --compat-split the reference's own rule for them (without
+// --nosplit/--nothreads: K = min(12, threads / 2), command_dedup.cpp:46-48).  Sort-by-name (-b),
+// region/MAPQ filters (-r/-q) and SAM/FASTQ output are not provided and fail loudly.
 #include <sys/resource.h>
 #include <sys/time.h>
 
@@ -33,7 +35,8 @@ struct Opt {
 const Opt kGlobal[] = {{"v", "verbose", false}, {"t", "threads", true}, {"d", "nothreads", false},
                        {"T", "tmpdir", true},   {"", "nosplit", false},  {"i", "in", true},
                        {"F", "format", true},   {"c", "compression", true}, {"", "nopg", false},
-                       {"", "device", true},    {"", "compat-nonverbose-dedup", false}};
+                       {"", "device", true},    {"", "compat-nonverbose-dedup", false},
+                       {"", "split-chains", true}, {"", "compat-split", false}};
 const Opt kMergesort[] = {{"o", "out", true}, {"r", "region", true},  {"q", "mapq", true},
                           {"b", "byname", false}, {"n", "n", true}, {"C", "compresstempfiles", false},
                           {"M", "markduplicates", false}, {"R", "removeduplicates", false}};
@@ -142,6 +145,12 @@ int main(int argc, const char **argv) {
     AlgorithmModule::setVerbose(cc.verbose);
     const int level = atoi(p.get("compression", "6").c_str());
     const bool compat = p.count("compat-nonverbose-dedup");
+    int split = atoi(p.get("split-chains", "0").c_str());
+    if (p.count("compat-split") && !p.count("nosplit") && !p.count("nothreads")) split = std::min(12, cc.threads / 2);
+    if (split > 1 && compat) {
+        fprintf(stderr, "openge: split chains with --compat-nonverbose-dedup are not supported\n");
+        return -1;
+    }
     timeval t0;
     gettimeofday(&t0, nullptr);
     if (oge_ctx_create(cc.device, &cc.ctx)) {
@@ -173,6 +182,7 @@ int main(int argc, const char **argv) {
         if (dedup) {
             md.removeDuplicates = p.count("removeduplicates");
             md.compatNonverbose = compat;
+            md.splitChains = split;
             sorter.addSink(&md);
             md.addSink(&writer);
         } else {
@@ -184,6 +194,7 @@ int main(int argc, const char **argv) {
         MarkDuplicates md;
         md.removeDuplicates = p.count("remove");
         md.compatNonverbose = compat;
+        md.splitChains = split;
         reader.addSink(&md);
         md.addSink(&writer);
         ret = writer.runChain(cc);

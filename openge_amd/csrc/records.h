@@ -38,6 +38,7 @@ struct OgeRgTable {
     const int16_t *lib;
     int32_t n_rg;
     int16_t unknown_lib;
+    int32_t split_k;  // > 1: split-by-chromosome emulation, the pair key carries the chain refID % K
 };
 
 // Sort-key packing of the KEYS output (see sort.hip for the layout).

@@ -179,6 +179,7 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
         if (paired_mm) {
             m |= OGE_M_CAND;
             uint64_t h = 0xcbf29ce484222325ull;
+            if (a.rg.split_k > 1) h = h_step(h, 0x100u + (uint32_t)(ref % a.rg.split_k));  // the chain
             for (uint32_t y = 0; y < rgl; ++y) h = h_step(h, rd.u8(rgv + y));
             h = h_step(h, ':');
             const uint32_t nl = lname ? lname - 1u : 0u;

@@ -37,6 +37,7 @@ class MarkdupOpts(C.Structure):
         ("n_ref", C.c_int32), ("rg_ids", C.c_void_p), ("rg_ids_bytes", C.c_uint64), ("rg_lib", C.c_void_p),
         ("n_rg", C.c_int32), ("unknown_lib", C.c_int16), ("pad0", C.c_int16),
         ("compat_nonverbose_index", C.c_int32), ("remove_duplicates", C.c_int32), ("debug_hash_bits", C.c_int32),
+        ("split_chains", C.c_int32),
     ]
 
 
@@ -286,7 +287,8 @@ class Bam:
             pass
 
 
-def markdup_opts_from_header(header_text: str, n_ref: int, compat_nonverbose: bool = False) -> tuple[MarkdupOpts, tuple]:
+def markdup_opts_from_header(header_text: str, n_ref: int, compat_nonverbose: bool = False,
+                             split_chains: int = 0) -> tuple[MarkdupOpts, tuple]:
     """RG -> library table as MarkDuplicates::getLibraryName resolves it (mark_duplicates.cpp:301-318)."""
     ids, libs, names = [], [], {}
     for line in header_text.splitlines():
@@ -305,6 +307,7 @@ def markdup_opts_from_header(header_text: str, n_ref: int, compat_nonverbose: bo
     o.n_ref, o.rg_ids, o.rg_ids_bytes = n_ref, _ptr(ida), len(idbuf)
     o.rg_lib, o.n_rg, o.unknown_lib = _ptr(liba), len(ids), unknown
     o.compat_nonverbose_index = 1 if compat_nonverbose else 0
+    o.split_chains = split_chains
     return o, (ida, liba)
 
 

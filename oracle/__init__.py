@@ -50,6 +50,9 @@ def _L():
         L.oracle_sort_perm.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
         L.oracle_realign_scan.restype = C.c_int
         L.oracle_realign_scan.argtypes = [C.c_void_p] * 6 + [C.c_uint64, C.c_void_p, C.c_void_p]
+        L.oracle_markdup_split.restype = C.c_int64
+        L.oracle_markdup_split.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
+                                           C.c_int32, C.c_int16, C.c_int, C.c_int, C.c_void_p]
         L.oracle_markdup.restype = C.c_int64
         L.oracle_markdup.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
                                      C.c_int32, C.c_int16, C.c_int, C.c_void_p]
@@ -66,8 +69,10 @@ def sort_perm(recs: np.ndarray, offs: np.ndarray, n: int) -> np.ndarray:
     return perm[:n]
 
 
-def markdup(recs: np.ndarray, offs: np.ndarray, n: int, header_text: str, compat_nonverbose: bool = False):
-    """dup[i] in {0,1,2} (2 = non-primary, untouched) and the number of records flagged."""
+def markdup(recs: np.ndarray, offs: np.ndarray, n: int, header_text: str, compat_nonverbose: bool = False,
+            split_chains: int = 0):
+    """dup[i] in {0,1,2} (2 = non-primary, untouched) and the number of records flagged.
+    split_chains > 1 restates the default split-by-chromosome chains."""
     ids, libs, names = [], [], {}
     for line in header_text.splitlines():
         if line.startswith("@RG\t"):
@@ -82,8 +87,9 @@ def markdup(recs: np.ndarray, offs: np.ndarray, n: int, header_text: str, compat
     liba = np.array(libs + [0], dtype=np.int16)
     dup = np.empty(max(n, 1), dtype=np.uint8)
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
-    nd = _L().oracle_markdup(recs.ctypes.data, offs.ctypes.data, n, ida.ctypes.data, len(idbuf) - 1,
-                             liba.ctypes.data, len(ids), unknown, 1 if compat_nonverbose else 0, dup.ctypes.data)
+    nd = _L().oracle_markdup_split(recs.ctypes.data, offs.ctypes.data, n, ida.ctypes.data, len(idbuf) - 1,
+                                   liba.ctypes.data, len(ids), unknown, 1 if compat_nonverbose else 0, split_chains,
+                                   dup.ctypes.data)
     return dup[:n], int(nd)
 
 

@@ -462,6 +462,35 @@ int64_t oracle_markdup(const uint8_t *recs, const uint64_t *offs, uint64_t n,
     return flagged;
 }
 
+/* Split-by-chromosome: cmd/command_dedup.cpp:71-106 feeds record i to chain
+ * refID % K (refID < 0 -> chain 0, algorithms/split_by_chromosome.cpp:45-48); every chain is its
+ * own MarkDuplicates over its records in stream order, and SortedMerge puts the records back in
+ * stream order (chains never hold equal-position records of one another).  Restated literally:
+ * one oracle_markdup per chain. */
+int64_t oracle_markdup_split(const uint8_t *recs, const uint64_t *offs, uint64_t n,
+                             const char *rg_ids, uint64_t rg_ids_bytes, const int16_t *rg_lib, int32_t n_rg,
+                             int16_t unknown_lib, int compat_nonverbose_index, int chains, uint8_t *dup_out) {
+    if (chains <= 1)
+        return oracle_markdup(recs, offs, n, rg_ids, rg_ids_bytes, rg_lib, n_rg, unknown_lib, compat_nonverbose_index,
+                              dup_out);
+    uint64_t *sub = (uint64_t *)malloc((n ? n : 1) * sizeof(uint64_t));
+    uint64_t *idx = (uint64_t *)malloc((n ? n : 1) * sizeof(uint64_t));
+    uint8_t *d = (uint8_t *)malloc(n ? n : 1);
+    int64_t total = 0;
+    for (int c = 0; c < chains; ++c) {
+        uint64_t m = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            int32_t refid = rdi32(recs + offs[i] + OFF_REFID);
+            int chain = refid < 0 ? 0 : refid % chains;
+            if (chain == c) { sub[m] = offs[i]; idx[m] = i; ++m; }
+        }
+        total += oracle_markdup(recs, sub, m, rg_ids, rg_ids_bytes, rg_lib, n_rg, unknown_lib, compat_nonverbose_index, d);
+        for (uint64_t j = 0; j < m; ++j) dup_out[idx[j]] = d[j];
+    }
+    free(sub); free(idx); free(d);
+    return total;
+}
+
 /* ------------------------------------------------------------------------------------------
  * Local realignment offset scan: LocalRealignment::findBestOffset
  * (algorithms/local_realignment.cpp:1126-1164) over mismatchQualitySumIgnoreCigar (:641-679),

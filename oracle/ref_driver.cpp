@@ -7,6 +7,9 @@
 //   dedup      : FileReader -> MarkDuplicates -> sink (cmd/command_dedup.cpp:48-69, --nosplit)
 //   sortdedup  : FileReader -> ReadSorter -> MarkDuplicates -> sink (command_mergesort.cpp:68-117, -M --nosplit)
 //   realign    : FileReader -> LocalRealignment -> sink (cmd/command_localrealign.cpp:37-75)
+// With -K k (k > 1) dedup / sortdedup run the reference's default split-by-chromosome chain
+// instead (cmd/command_dedup.cpp:71-106, command_mergesort.cpp:118-170):
+//   ... -> SplitByChromosome -> k x MarkDuplicates -> SortedMerge -> sink
 // The sink writes BGZF BAM through the reference's BamSerializer<BgzfOutputStream>,
 // i.e. exactly the serializer FileWriter uses (alg/file_writer.cpp:144-166), with
 // no @PG line (the `--nopg` behaviour).  Global settings mirror
@@ -19,6 +22,8 @@
 #include "algorithms/read_sorter.h"
 #include "algorithms/mark_duplicates.h"
 #include "algorithms/local_realignment.h"
+#include "algorithms/split_by_chromosome.h"
+#include "algorithms/sorted_merge.h"
 #include "util/bam_serializer.h"
 #include "util/bgzf_output_stream.h"
 
@@ -56,7 +61,7 @@ protected:
 
 static void usage() {
     fprintf(stderr,
-            "usage: ref_driver sort|dedup|sortdedup|realign [-v] [-t N] [-n N] [-T tmpdir] [-c level]\n"
+            "usage: ref_driver sort|dedup|sortdedup|realign [-v] [-t N] [-n N] [-T tmpdir] [-c level] [-K chains]\n"
             "                  [-R ref.fa -L intervals] in.bam out.bam\n");
     exit(2);
 }
@@ -65,7 +70,7 @@ int main(int argc, char **argv) {
     if (argc < 4) usage();
     std::string mode = argv[1];
     bool verbose = false;
-    int threads = 8, per_tmp = 500000, level = 6;
+    int threads = 8, per_tmp = 500000, level = 6, chains = 0;
     std::string tmpdir = "/tmp", ref, intervals;
     std::vector<std::string> pos;
     for (int i = 2; i < argc; i++) {
@@ -75,6 +80,7 @@ int main(int argc, char **argv) {
         else if (a == "-n" && i + 1 < argc) per_tmp = atoi(argv[++i]);
         else if (a == "-T" && i + 1 < argc) tmpdir = argv[++i];
         else if (a == "-c" && i + 1 < argc) level = atoi(argv[++i]);
+        else if (a == "-K" && i + 1 < argc) chains = atoi(argv[++i]);
         else if (a == "-R" && i + 1 < argc) ref = argv[++i];
         else if (a == "-L" && i + 1 < argc) intervals = argv[++i];
         else pos.push_back(a);
@@ -94,7 +100,29 @@ int main(int argc, char **argv) {
     sink.filename = pos[1];
     sink.level = level;
 
-    if (mode == "sort" || mode == "sortdedup") {
+    if ((mode == "dedup" || mode == "sortdedup") && chains > 1) {
+        ReadSorter sorter(tmpdir);
+        SplitByChromosome split;
+        SortedMerge merge;
+        std::vector<MarkDuplicates *> md;
+        if (mode == "sortdedup") {
+            sorter.setSortBy(BamHeader::SORT_COORDINATE);
+            sorter.setCompressTempFiles(false);
+            sorter.setAlignmentsPerTempfile(per_tmp);
+            reader.addSink(&sorter);
+            sorter.addSink(&split);
+        } else {
+            reader.addSink(&split);
+        }
+        merge.addSink(&sink);
+        for (int c = 0; c < chains; ++c) {
+            md.push_back(new MarkDuplicates(tmpdir));
+            merge.addSource(md.back());
+            split.addSink(md.back());
+        }
+        sink.runChain();
+        for (size_t c = 0; c < md.size(); ++c) delete md[c];
+    } else if (mode == "sort" || mode == "sortdedup") {
         ReadSorter sorter(tmpdir);
         MarkDuplicates md(tmpdir);
         sorter.setSortBy(BamHeader::SORT_COORDINATE);

@@ -6,6 +6,8 @@ oracle/_ref/ref_driver is the reference's own ReadSorter / MarkDuplicates module
   dedup -v        on the reference's sorted output and on the unsorted input
   dedup           (non-verbose) on the unsorted input
   sortdedup -v    (mergesort -M --nosplit)
+  dedup -v -K k   (split-by-chromosome chains, the reference's default without --nosplit; k = 3, 12)
+                  on the sorted output, and sortdedup -v -K 3
 and the outputs are reduced to small fixtures: the sort permutation (input index per output
 record), indices of records carrying 0x400, SHA-256 digests of the output record streams and the
 regenerated header text.  Inputs are either fixtures the reference's own tests hold
@@ -46,6 +48,7 @@ CASES = {
     "c1_100k": {"kind": "synth", "preset": "c1", "n_pairs": 50000, "seed": 1234},
 }
 FULL_ARRAYS_MAX = 20000
+SPLIT_K = (3, 12)
 
 
 def materialize(name: str, spec: dict, tmp: Path) -> Path:
@@ -103,13 +106,19 @@ def main():
             run(driver, "dedup", src, di_path, "-v")
             run(driver, "dedup", src, dn_path)
             run(driver, "sortdedup", src, sd_path, "-v")
+            split_paths = {}
+            for k in SPLIT_K:  # the reference's default split-by-chromosome chains
+                split_paths[f"dedup_sorted_v_k{k}"] = tmp / f"{name}.sorted.dedup_k{k}.bam"
+                run(driver, "dedup", s_path, split_paths[f"dedup_sorted_v_k{k}"], "-v", "-K", str(k))
+            split_paths["sortdedup_v_k3"] = tmp / f"{name}.sd_k3.bam"
+            run(driver, "sortdedup", src, split_paths["sortdedup_v_k3"], "-v", "-K", "3")
             hs, _, srecs, soffs = bamutil.read_bam(s_path)
             perm = bamutil.perm_of(srecs, soffs, irecs, ioffs)
             meta = {"case": name, "spec": spec, "n": n, "sorted_header": hs, "sort": stream_digests(srecs, soffs),
                     "perm_sha256": hashlib.sha256(perm.tobytes()).hexdigest()}
             arrays = {}
             for key, path in [("dedup_sorted_v", dv_path), ("dedup_input_v", di_path), ("dedup_input_nv", dn_path),
-                              ("sortdedup_v", sd_path)]:
+                              ("sortdedup_v", sd_path)] + sorted(split_paths.items()):
                 h, _, r, o = bamutil.read_bam(path)
                 fl = bamutil.flags_of(r, o)
                 idx = np.nonzero(fl & 0x400)[0].astype(np.uint32)

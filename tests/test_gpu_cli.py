@@ -74,6 +74,24 @@ def test_cli_sort_alias_then_dedup_matches_reference(case, tmp_path):
     assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
 
 
+def test_cli_split_chains_match_reference(case, tmp_path):
+    """the reference's split-by-chromosome chains, explicitly (--split-chains K) and by
+    the reference's own rule (--compat-split: K = min(12, -t / 2))."""
+    src = case_input(case, tmp_path)
+    run("mergesort", "-M", "--nopg", "--split-chains", 3, src, "-o", tmp_path / "m3.bam")
+    h, m, t = digests(tmp_path / "m3.bam")
+    g = case.meta["sortdedup_v_k3"]
+    assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
+    run("sort", "--nopg", src, "-o", tmp_path / "s.bam")
+    run("dedup", "--nopg", "--compat-split", "-t", 24, tmp_path / "s.bam", "-o", tmp_path / "d12.bam")
+    h, m, t = digests(tmp_path / "d12.bam")
+    g = case.meta["dedup_sorted_v_k12"]
+    assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
+    run("dedup", "--nopg", "--compat-split", "--nosplit", "-t", 24, tmp_path / "s.bam", "-o", tmp_path / "dn.bam")
+    h, m, t = digests(tmp_path / "dn.bam")
+    assert m == case.meta["dedup_sorted_v"]["mapped_sha256"]
+
+
 def test_cli_dedup_remove_drops_flagged_records(case, tmp_path):
     src = case_input(case, tmp_path)
     run("mergesort", "-R", "--nopg", src, "-o", tmp_path / "r.bam")

@@ -34,6 +34,14 @@ def test_oracle_dedup_input_nonverbose_quirk(case):
     assert nd <= 1
 
 
+@pytest.mark.parametrize("k", [3, 12])
+def test_oracle_dedup_split_chains(case, k):
+    """the reference's default split-by-chromosome chains (dedup without --nosplit)."""
+    perm = oracle.sort_perm(case.recs, case.offs, case.n)
+    dup, nd = oracle.markdup(case.recs, case.offs[:-1][perm], case.n, case.header, split_chains=k)
+    check_dups(case, f"dedup_sorted_v_k{k}", dup, case.offs[:-1][perm])
+
+
 def test_yhet208_survey_count():
     """The survey's independent run of the reference: 6,642 duplicates on sorted 208.yhet.bam with -v."""
     case = load_case("yhet208")
