@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <atomic>
+#include <unistd.h>
 #include <cstring>
 #include <sstream>
 #include <thread>
@@ -89,7 +90,7 @@ static thread_local DeflateTls tls_deflate;
 const char *bgzf_codec_name() { return libdeflate().ok ? "libdeflate" : "zlib"; }
 
 // ---------------- BGZF inflate ----------------
-bool bgzf_inflate_all(const uint8_t *src, size_t n, std::vector<uint8_t> &out, int threads, std::string &err) {
+bool bgzf_inflate_all(const uint8_t *src, size_t n, bytevec &out, int threads, std::string &err, size_t slack) {
     struct Blk { size_t coff, clen, cdata, dlen, uoff; };
     std::vector<Blk> blocks;
     size_t p = 0, total = 0;
@@ -114,7 +115,10 @@ bool bgzf_inflate_all(const uint8_t *src, size_t n, std::vector<uint8_t> &out, i
         total += isize;
         p += bsize;
     }
-    out.resize(total);
+    out.reserve(total + slack);
+    out.resize(total + slack);
+    memset(out.data() + total, 0, slack);
+    out.resize(total);  // capacity keeps the zeroed slack
     std::atomic<bool> ok(true);
     parallel_for(blocks.size(), threads, [&](size_t i) {
         const Blk &b = blocks[i];
@@ -152,7 +156,23 @@ bool bgzf_inflate_all(const uint8_t *src, size_t n, std::vector<uint8_t> &out, i
 static const size_t kBlockPayload = 65280;
 
 BgzfWriter::BgzfWriter(FILE *f, int level, int threads) : f_(f), level_(level), threads_(threads), closed_(false) {}
-BgzfWriter::~BgzfWriter() { if (!closed_) close(); }
+BgzfWriter::~BgzfWriter() {
+    if (!closed_) close();
+    drain();
+}
+
+void BgzfWriter::drain() {
+    if (writer_.joinable()) writer_.join();
+    writing_.clear();
+}
+
+void BgzfWriter::emit(std::vector<std::vector<uint8_t>> &&blocks) {
+    drain();  // the previous batch goes out first
+    writing_ = std::move(blocks);
+    writer_ = std::thread([this]() {
+        for (auto &o : writing_) fwrite(o.data(), 1, o.size(), f_);
+    });
+}
 
 static void bgzf_block(const uint8_t *src, size_t n, int level, std::vector<uint8_t> &dst) {
     size_t bound = compressBound((uLong)n) + 64;
@@ -204,14 +224,37 @@ void BgzfWriter::flush_blocks(bool final) {
         size_t len = std::min(kBlockPayload, pending_.size() - off);
         bgzf_block(pending_.data() + off, len, level_, outs[i]);
     });
-    for (auto &o : outs) fwrite(o.data(), 1, o.size(), f_);
+    emit(std::move(outs));
     size_t consumed = std::min(pending_.size(), nblk * kBlockPayload);
     pending_.erase(pending_.begin(), pending_.begin() + consumed);
+}
+
+void BgzfWriter::write_span(const uint8_t *data, size_t n) {
+    // complete the partial block held in pending_, then compress the span's whole blocks in place
+    if (!pending_.empty()) {
+        const size_t fill = std::min(n, (kBlockPayload - pending_.size() % kBlockPayload) % kBlockPayload);
+        pending_.insert(pending_.end(), data, data + fill);
+        data += fill;
+        n -= fill;
+        if (pending_.size() % kBlockPayload == 0) flush_blocks(false);
+    }
+    const size_t whole = n / kBlockPayload;
+    const size_t window = (size_t)std::max(1, threads_) * 64;  // blocks per parallel step (bounded memory)
+    for (size_t b0 = 0; b0 < whole; b0 += window) {
+        const size_t nb = std::min(window, whole - b0);
+        std::vector<std::vector<uint8_t>> outs(nb);
+        parallel_for(nb, threads_, [&](size_t i) {
+            bgzf_block(data + (b0 + i) * kBlockPayload, kBlockPayload, level_, outs[i]);
+        });
+        emit(std::move(outs));  // written while the next window compresses
+    }
+    pending_.insert(pending_.end(), data + whole * kBlockPayload, data + n);
 }
 
 void BgzfWriter::close() {
     if (closed_) return;
     flush_blocks(true);
+    drain();
     std::vector<uint8_t> eof;
     bgzf_block(nullptr, 0, level_, eof);
     fwrite(eof.data(), 1, eof.size(), f_);
@@ -348,7 +391,7 @@ std::string BamHeaderModel::to_string() const {
 }
 
 // ---------------- BAM ----------------
-bool bam_parse(std::vector<uint8_t> &&raw, BamFile &out, std::string &err) {
+bool bam_parse(bytevec &&raw, BamFile &out, std::string &err) {
     out.data = std::move(raw);
     const uint8_t *d = out.data.data();
     size_t n = out.data.size();
@@ -395,12 +438,25 @@ bool bam_parse(std::vector<uint8_t> &&raw, BamFile &out, std::string &err) {
 bool bam_read_file(const std::string &path, BamFile &out, int threads, std::string &err) {
     FILE *f = (path == "-" || path == "stdin") ? stdin : fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
-    std::vector<uint8_t> comp;
-    if (f != stdin && fseeko(f, 0, SEEK_END) == 0) {  // regular file: one read into a sized buffer
+    bytevec comp;
+    if (f != stdin && fseeko(f, 0, SEEK_END) == 0) {  // regular file: parallel preads into a sized buffer
         off_t sz = ftello(f);
-        fseeko(f, 0, SEEK_SET);
         comp.resize(sz > 0 ? (size_t)sz : 0);
-        if (sz > 0 && fread(comp.data(), 1, comp.size(), f) != comp.size()) {
+        const int fd = fileno(f);
+        const size_t chunk = 64ull << 20, nch = (comp.size() + chunk - 1) / chunk;
+        std::atomic<bool> short_read(false);
+        parallel_for(nch, threads, [&](size_t c) {
+            size_t o = c * chunk, e = std::min(comp.size(), o + chunk);
+            while (o < e) {
+                ssize_t r = pread(fd, comp.data() + o, e - o, (off_t)o);
+                if (r <= 0) {
+                    short_read = true;
+                    return;
+                }
+                o += (size_t)r;
+            }
+        });
+        if (short_read) {
             fclose(f);
             err = "short read on " + path;
             return false;
@@ -411,7 +467,7 @@ bool bam_read_file(const std::string &path, BamFile &out, int threads, std::stri
         while ((r = fread(buf, 1, sizeof(buf), f)) > 0) comp.insert(comp.end(), buf, buf + r);
     }
     if (f != stdin) fclose(f);
-    std::vector<uint8_t> raw;
+    bytevec raw;
     if (!bgzf_inflate_all(comp.data(), comp.size(), raw, threads, err)) return false;
     return bam_parse(std::move(raw), out, err);
 }

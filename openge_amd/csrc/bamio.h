@@ -12,14 +12,18 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include "uvector.h"
 
 namespace oge {
 
 // ---------------- BGZF ----------------
 // Inflate an entire BGZF byte string (any number of blocks) into `out`, in parallel.
 // Returns false and fills `err` on a malformed or truncated stream.
-bool bgzf_inflate_all(const uint8_t *src, size_t n, std::vector<uint8_t> &out, int threads, std::string &err);
+// out is sized to the stream (plus `slack` zeroed bytes past it) without a serial zero-fill first
+bool bgzf_inflate_all(const uint8_t *src, size_t n, bytevec &out, int threads, std::string &err, size_t slack = 64);
 const char *bgzf_codec_name();  // "libdeflate" or "zlib"
 
 class BgzfWriter {
@@ -29,10 +33,17 @@ public:
     BgzfWriter(FILE *f, int level, int threads);
     ~BgzfWriter();
     void write(const void *data, size_t n);
+    // Append n bytes: whole blocks are compressed straight from the caller's bytes, all in parallel,
+    // with no staging copy (only a partial tail block is copied).
+    void write_span(const uint8_t *data, size_t n);
     void close();  // flush + EOF marker
 private:
     void flush_blocks(bool final);
+    void emit(std::vector<std::vector<uint8_t>> &&blocks);  // ordered, written by a background thread
+    void drain();                                          // wait for the background write
     FILE *f_;
+    std::thread writer_;
+    std::vector<std::vector<uint8_t>> writing_;
     int level_, threads_;
     std::vector<uint8_t> pending_;
     bool closed_;
@@ -62,7 +73,7 @@ struct BamFile {
     std::string header_text;              // as stored in the file
     std::vector<std::string> ref_names;   // binary reference list
     std::vector<int32_t> ref_lens;
-    std::vector<uint8_t> data;            // decompressed stream (records start at rec_base)
+    bytevec data;                         // decompressed stream (records start at rec_base)
     size_t rec_base = 0;
     std::vector<uint64_t> offsets;        // record offsets relative to data.data() + rec_base
     const uint8_t *recs() const { return data.data() + rec_base; }
@@ -70,7 +81,7 @@ struct BamFile {
 };
 
 bool bam_read_file(const std::string &path, BamFile &out, int threads, std::string &err);
-bool bam_parse(std::vector<uint8_t> &&raw, BamFile &out, std::string &err);
+bool bam_parse(bytevec &&raw, BamFile &out, std::string &err);
 // Serialize header block (magic, text, reference list taken from the header @SQ lines, as
 // BamSerializer::open does at util/bam_serializer.h:54-76).
 std::vector<uint8_t> bam_encode_header(const BamHeaderModel &h);

@@ -1,10 +1,13 @@
 // modules.cpp -- AlgorithmModule chain over the C ABI (see modules.h).
 #include "modules.h"
 
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
+#include <atomic>
+#include <thread>
 
 #include "bam_layout.h"
 
@@ -33,7 +36,9 @@ int ChainContext::to_device(ReadBatch &b) {
 
 int ChainContext::to_host(ReadBatch &b) {
     if (b.host_valid) return 0;
-    b.recs.assign(b.d_bytes + 16, 0);
+    b.recs.clear();
+    b.recs.resize(b.d_bytes + 16);  // uninitialised: the copy below writes every byte but the slack
+    memset(b.recs.data() + b.d_bytes, 0, 16);
     b.offs.resize(b.n + 1);
     if (oge_memcpy(ctx, b.recs.data(), b.d_recs, b.d_bytes, 2) || oge_memcpy(ctx, b.offs.data(), b.d_offs, (b.n + 1) * 8, 2))
         return fail("device->host copy");
@@ -61,7 +66,11 @@ int AlgorithmModule::runChain(ChainContext &cc) {
             continue;
         }
         if (verbose_) fprintf(stderr, "[openge] running %s on %llu records\n", m->name(), (unsigned long long)b.n);
+        const auto t0 = std::chrono::steady_clock::now();
         int rc = m->runInternal(cc, b);
+        if (verbose_)
+            fprintf(stderr, "[openge] %s: %.3f s\n", m->name(),
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
         if (rc) {
             cc.free_device(b);
             return rc;
@@ -84,11 +93,13 @@ int FileReader::runInternal(ChainContext &cc, ReadBatch &b) {
             fprintf(stderr, "openge: error reading %s: %s\n", files_[i].c_str(), err.c_str());
             return -1;
         }
-        if (i == 0) {
+        if (i == 0) {  // take the decompressed stream as it is: records start at rec_base
             b.header = f.header;
             b.ref_names = f.ref_names;
-            b.recs.assign(f.recs(), f.recs() + f.rec_bytes());
-            b.offs = f.offsets;
+            const uint64_t base = f.rec_base;
+            b.offs.resize(f.offsets.size());
+            for (size_t k = 0; k < f.offsets.size(); ++k) b.offs[k] = base + f.offsets[k];
+            b.recs = std::move(f.data);
         } else {
             if (f.ref_names != b.ref_names) {
                 fprintf(stderr, "openge: %s has a different sequence dictionary than %s\n", files_[i].c_str(), files_[0].c_str());
@@ -143,7 +154,9 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
         fprintf(stderr, "openge: sort by name (-b) is not provided by the GPU path\n");
         return -1;
     }
+    const auto t0 = std::chrono::steady_clock::now();
     if (cc.to_device(b)) return -1;
+    const auto t1 = std::chrono::steady_clock::now();
     void *perm = nullptr, *out = nullptr, *out_off = nullptr;
     if (oge_dev_alloc(cc.ctx, b.n * 4 + 4, &perm) || oge_dev_alloc(cc.ctx, b.d_bytes + 64, &out) ||
         oge_dev_alloc(cc.ctx, (b.n + 1) * 8, &out_off))
@@ -162,6 +175,10 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
         if (!rc) rc = oge_gather_records_dev(cc.ctx, b.d_recs, b.d_offs, (uint32_t *)perm, b.n, (uint8_t *)out, (uint64_t *)out_off);
     }
     if (!rc) rc = oge_ctx_sync(cc.ctx);
+    if (verbose_)
+        fprintf(stderr, "[openge] ReadSorter: host->device %.3f s, device pipeline %.3f s\n",
+                std::chrono::duration<double>(t1 - t0).count(),
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
     oge_dev_free(cc.ctx, perm);
     if (rc) {
         oge_dev_free(cc.ctx, out);
@@ -227,8 +244,33 @@ int FileWriter::setFormat(const std::string &f) {
     return -1;
 }
 
+// the bin every record must carry (bam_serializer.h:112-116), recomputed in place by the workers
+static void fix_bins(ReadBatch &b, int threads) {
+    const uint64_t n = b.n, chunk = 1 << 16;
+    const uint64_t nc = (n + chunk - 1) / chunk;
+    std::atomic<uint64_t> next(0);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < std::max(1, threads); ++t)
+        ts.emplace_back([&]() {
+            for (uint64_t c; (c = next.fetch_add(1)) < nc;)
+                for (uint64_t k = c * chunk, e = std::min(n, k + chunk); k < e; ++k) {
+                    uint8_t *r = b.recs.data() + b.offs[k];
+                    oge_wr_u16(r + OGE_OFF_BIN, oge_rec_bin(r));
+                }
+        });
+    for (auto &t : ts) t.join();
+}
+
 int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
+        return std::chrono::duration<double>(z - a).count();
+    };
+    const auto t0 = clk();
     if (cc.to_host(b)) return -1;
+    const auto t1 = clk();
+    fix_bins(b, cc.threads);
+    const auto t2 = clk();
     BamHeaderModel h = b.header;
     if (!program_line_.empty()) {  // file_writer.cpp:76-89
         PgRecord pg;
@@ -252,18 +294,31 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
         BgzfWriter w(f, level_, cc.threads > 0 ? cc.threads : 8);
         std::vector<uint8_t> hb = bam_encode_header(h);
         w.write(hb.data(), hb.size());
-        std::vector<uint8_t> tmp;
-        for (uint64_t k = 0; k < b.n; ++k) {
+        // maximal runs of records that sit back to back in memory go out as spans (no copy)
+        uint64_t k = 0;
+        while (k < b.n) {
             const uint8_t *r = b.recs.data() + b.offs[k];
-            const uint32_t bs = oge_rd_u32(r);
-            if (b.drop_duplicates && (oge_rd_u16(r + OGE_OFF_FLAG) & OGE_F_DUP)) continue;
-            tmp.assign(r, r + 4 + bs);
-            oge_wr_u16(tmp.data() + OGE_OFF_BIN, oge_rec_bin(tmp.data()));  // bam_serializer.h:112-116
-            w.write(tmp.data(), tmp.size());
+            if (b.drop_duplicates && (oge_rd_u16(r + OGE_OFF_FLAG) & OGE_F_DUP)) {
+                ++k;
+                continue;
+            }
+            const uint64_t s = b.offs[k];
+            uint64_t e = s + 4 + oge_rd_u32(r);
+            ++k;
+            while (k < b.n && b.offs[k] == e) {
+                const uint8_t *q = b.recs.data() + e;
+                if (b.drop_duplicates && (oge_rd_u16(q + OGE_OFF_FLAG) & OGE_F_DUP)) break;
+                e += 4 + oge_rd_u32(q);
+                ++k;
+            }
+            w.write_span(b.recs.data() + s, e - s);
         }
         w.close();
     }
     if (f != stdout) fclose(f);
+    if (verbose_)
+        fprintf(stderr, "[openge] FileWriter: device->host %.3f s, bins %.3f s, BGZF %.3f s (%s)\n", sec(t0, t1), sec(t1, t2),
+                sec(t2, clk()), bgzf_codec_name());
     else fflush(stdout);
     return 0;
 }

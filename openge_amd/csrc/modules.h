@@ -23,7 +23,7 @@ struct ReadBatch {
     std::vector<std::string> ref_names;
     uint64_t n = 0;
     // host form
-    std::vector<uint8_t> recs;        // + 16 bytes of slack
+    bytevec recs;                     // + 16 bytes of slack
     std::vector<uint64_t> offs;       // n + 1
     bool host_valid = false;
     // device form

@@ -21,6 +21,8 @@
 #include <utility>
 #include <vector>
 
+#include "uvector.h"
+
 namespace oge {
 
 struct CigOp {
@@ -169,29 +171,6 @@ struct ScanPair {
     int32_t orig;       // original alignment start - leftmostIndex
     int32_t max_start;  // consensus length - read cigar length (findBestOffset :1149-1150)
 };
-// std::vector whose resize() leaves trivial elements uninitialised (the batch is filled in parallel;
-// a zero-fill would be a serial pass over every page first)
-template <class T>
-struct UninitAlloc : std::allocator<T> {
-    template <class U>
-    struct rebind {
-        typedef UninitAlloc<U> other;
-    };
-    UninitAlloc() = default;
-    template <class U>
-    UninitAlloc(const UninitAlloc<U> &) {}
-    template <class U>
-    void construct(U *p) noexcept {
-        ::new ((void *)p) U;
-    }
-    template <class U, class... A>
-    void construct(U *p, A &&...a) {
-        ::new ((void *)p) U(std::forward<A>(a)...);
-    }
-};
-template <class T>
-using uvector = std::vector<T, UninitAlloc<T>>;
-
 struct ScanBatch {
     uvector<uint8_t> cons;           // consensus bytes, back to back
     uvector<uint64_t> cons_off;      // n_cons + 1
