@@ -131,7 +131,7 @@ def pmc_traffic(kernel: str, rec_bytes: int) -> dict | None:
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*_pmc.json,
     written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes).
     When the profiled workload had a different record-byte total, the count is scaled by bytes."""
-    files = sorted((ROOT / "profiles").glob("r*_pmc.json"))
+    files = sorted(f for f in (ROOT / "profiles").glob("r*_pmc.json") if "realign" not in f.name)
     if not files:
         return None
     try:
@@ -140,7 +140,8 @@ def pmc_traffic(kernel: str, rec_bytes: int) -> dict | None:
         return None
     for name, v in d.get("kernels", {}).items():
         if kernel in name:
-            b = d["workload"].get("record_bytes_per_gpu") or rec_bytes
+            w = d.get("workload", {})
+            b = w.get("record_bytes_rank0") or w.get("record_bytes_per_gpu") or rec_bytes
             return {"bytes": v["hbm_bytes"] * rec_bytes / b, "source": files[-1].name}
     return None
 
