@@ -56,12 +56,15 @@ def parse():
 VALU_INT32_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12  # CUs x SIMDs x lanes/clk x 2.4 GHz (MI355X_MICROARCH.md)
 
 
-def realign_leg(ctx, n_intervals: int) -> dict:
+def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1) -> dict | None:
     """configs[4]: openge localrealign on the C5 synthetic set (50k indel intervals, 24 contigs).
     Host phases (binning, consensus generation, decisions, mate fixing) + the HIP offset scan; the
-    records are decoded in host memory before the timed region (the module's input queue)."""
+    records are decoded in host memory before the timed region (the module's input queue).  With
+    world > 1 every rank realigns its contig range (openge_amd/realign_shard.py, no exchange); the
+    time is the max over ranks between barriers.  Returns the result on rank 0 (None elsewhere)."""
     import tempfile
     from openge_amd import lib as L
+    from openge_amd import realign_shard as RS
 
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         p = L.realign_synth_params(n_intervals=n_intervals)
@@ -70,10 +73,30 @@ def realign_leg(ctx, n_intervals: int) -> dict:
         import numpy as np
         offs = np.append(b.offs, np.uint64(b.recs.size))
         opts = L.realign_opts(threads=16)
-        ctx.localrealign(b.header_text, b.recs, offs, b.n, fa, iv, opts)  # warm-up (first-touch, kernel load)
+        ref_lens = [int(dict(x.split(":", 1) for x in ln.split("\t")[1:])["LN"])
+                    for ln in b.header_text.splitlines() if ln.startswith("@SQ")]
+        lo, hi = RS.contig_slices(b.recs, offs, b.n, ref_lens, world)[rank]
+        run = lambda: RS.localrealign_slice(ctx, b.header_text, b.recs, offs, lo, hi, fa, iv, opts,
+                                            last=(rank == world - 1))
+        run()  # warm-up (first-touch, kernel load)
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            dist.barrier()
         t0 = time.perf_counter()
-        out, oo, st = ctx.localrealign(b.header_text, b.recs, offs, b.n, fa, iv, opts)
+        out, oo, st = run()
         dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+            if rank != 0:
+                return None
+            return {"metric": "realign intervals/sec", "value": round(n_intervals / dt, 1), "unit": "intervals/s",
+                    "workload": f"C5: {n_intervals} indel intervals, 24 contigs, {b.n} reads (seed 1234)",
+                    "seconds": round(dt, 3), "n_gpus": world, "scaling": "strong",
+                    "parallelism": f"{world} ranks, contig-range shards, no exchange", "host_threads_per_rank": 16,
+                    "rank0_reads": hi - lo, "rank0_stats": st}
     # VALU lane-ops per launch from the committed PMC pass (SQ_INSTS_VALU x 64; the instruction count
     # is fixed by the workload), divided by the live HIP-event time of the scan stage
     valu = realign_pmc_valu()
@@ -237,6 +260,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    realign_multi = None
+    if world > 1 and not args.no_realign:  # every rank realigns its contig range
+        realign_multi = realign_leg(ctx, args.realign_intervals, rank, world)
+
     if rank == 0:
         K = args.steps
         ms_step = dt / K * 1e3
@@ -280,6 +307,8 @@ def main():
         else:
             out["shard_rank0_s_per_step"] = {k: (round(v / K, 4) if isinstance(v, float) else v // K)
                                              for k, v in shard_t.items()}
+            if realign_multi is not None:
+                out["realign"] = realign_multi
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:

@@ -1668,9 +1668,10 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     std::vector<RRead *> order;
     if (sequential) {
         order.reserve(n);
-        emit_events(0, ev.size(), 0, order, st.intervals_cleaned, st.reads_realigned);
+        st.tail_waiting = emit_events(0, ev.size(), 0, order, st.intervals_cleaned, st.reads_realigned);
     } else {
         order.reserve(n);
+        st.tail_waiting = segs.back().left;
         for (auto &g : segs) {
             order.insert(order.end(), g.ord.begin(), g.ord.end());
             st.intervals_cleaned += g.cl;

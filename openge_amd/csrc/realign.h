@@ -197,6 +197,8 @@ struct RealignParams {
 struct RealignStats {
     uint64_t intervals = 0, intervals_cleaned = 0, reads_realigned = 0, scan_pairs = 0, scan_ops = 0;
     uint64_t mate_segments = 0;  // writer segments run in parallel (1 = sequential)
+    uint64_t tail_waiting = 0;   // reads the writer still held when the stream ended (a run cut at a
+                                 // contig boundary is exact unless this reaches maxRecordsInMemory)
     double t_bin = 0, t_prepare = 0, t_scan = 0, t_decide = 0, t_emit = 0, t_run = 0;
     double t_fasta = 0, t_decode = 0, t_mate = 0, t_release = 0;  // parts of t_bin / t_emit; teardown
     double t_scan_build = 0;                                       // part of t_scan: batch assembly

@@ -521,11 +521,11 @@ int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len,
              "\"scan_ops\": %llu, \"scan_kernel_ms\": %.4f, \"t_bin\": %.4f, \"t_prepare\": %.4f, \"t_scan\": %.4f, "
              "\"t_decide\": %.4f, \"t_emit\": %.4f, \"t_run\": %.4f, \"t_fasta\": %.4f, \"t_decode\": %.4f, "
              "\"t_mate\": %.4f, \"t_release\": %.4f, \"t_scan_build\": %.4f, \"t_scan_validate\": %.4f, \"t_scan_upload\": %.4f, "
-             "\"t_scan_device\": %.4f, \"mate_segments\": %llu, \"scan_kernel\": \"%s\"}",
+             "\"t_scan_device\": %.4f, \"mate_segments\": %llu, \"tail_waiting\": %llu, \"scan_kernel\": \"%s\"}",
              (unsigned long long)st.intervals, (unsigned long long)st.intervals_cleaned, (unsigned long long)st.reads_realigned,
              (unsigned long long)st.scan_pairs, (unsigned long long)st.scan_ops, scan_kernel_ms, st.t_bin, st.t_prepare,
              st.t_scan, st.t_decide, st.t_emit, st.t_run, st.t_fasta, st.t_decode, st.t_mate, st.t_release, st.t_scan_build, ctx->scan_t[0], ctx->scan_t[1], ctx->scan_t[2],
-             (unsigned long long)st.mate_segments, ctx->last_scan_generic ? "k_realign_scan (byte-wise)" : "k_planes + k_scan_bp");
+             (unsigned long long)st.mate_segments, (unsigned long long)st.tail_waiting, ctx->last_scan_generic ? "k_realign_scan (byte-wise)" : "k_planes + k_scan_bp");
     r->stats = buf;
     *out = r.release();
     return OGE_OK;

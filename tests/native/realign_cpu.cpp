@@ -52,9 +52,9 @@ void *realign_cpu(const char *header, uint64_t hlen, const uint8_t *recs, const 
     st.t_run = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
     if (rc) o->msg = err.empty() ? "realign failed" : err;
     char b[512];
-    snprintf(b, sizeof b, "{\"t_bin\": %.3f, \"t_prepare\": %.3f, \"t_scan\": %.3f, \"t_decide\": %.3f, \"t_emit\": %.3f, \"t_run\": %.3f, \"t_fasta\": %.3f, \"t_decode\": %.3f, \"t_mate\": %.3f, \"t_release\": %.3f, \"scan_pairs\": %llu, \"mate_segments\": %llu}",
+    snprintf(b, sizeof b, "{\"t_bin\": %.3f, \"t_prepare\": %.3f, \"t_scan\": %.3f, \"t_decide\": %.3f, \"t_emit\": %.3f, \"t_run\": %.3f, \"t_fasta\": %.3f, \"t_decode\": %.3f, \"t_mate\": %.3f, \"t_release\": %.3f, \"scan_pairs\": %llu, \"mate_segments\": %llu, \"tail_waiting\": %llu}",
              st.t_bin, st.t_prepare, st.t_scan, st.t_decide, st.t_emit, st.t_run, st.t_fasta, st.t_decode, st.t_mate, st.t_release, (unsigned long long)st.scan_pairs,
-             (unsigned long long)st.mate_segments);
+             (unsigned long long)st.mate_segments, (unsigned long long)st.tail_waiting);
     o->stats = b;
     return o;
 }

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import oracle
-from test_realign import RL_CASES, check_output, load_rl_case, random_batch
+from test_realign import RL_CASES, _offsets_of, _ref_lens, check_output, load_rl_case, random_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -74,3 +74,21 @@ def test_gpu_localrealign_matches_reference(ctx, tmp_path, name):
     out, oo, stats = ctx.localrealign(h, recs, offs, len(offs) - 1, fa, iv)
     check_output(meta, arrays, out, oo)
     assert stats["scan_pairs"] > 0 and stats["intervals_cleaned"] > 0
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_gpu_contig_sharded_realign_equals_reference(ctx, tmp_path, world):
+    """Multi-GPU realign (openge_amd/realign_shard.py): each rank's contig range through the C ABI,
+    concatenated, equals the reference's single-process output."""
+    import realign_util as R
+    from openge_amd import realign_shard as RS
+    meta, arrays, h, recs, offs, fa, iv = load_rl_case("rl_c5_2k", tmp_path)
+    n = len(offs) - 1
+    sl = RS.contig_slices(recs, offs, n, _ref_lens(h), world)
+    parts = []
+    for r, (lo, hi) in enumerate(sl):
+        out, oo, st = RS.localrealign_slice(ctx, h, recs, offs, lo, hi, fa, iv, None, last=(r == world - 1))
+        parts.append(bytes(out[:int(oo[-1])]))
+    whole = b"".join(parts)
+    d = R.digest(np.frombuffer(whole + b"\0" * 16, np.uint8), _offsets_of(whole))
+    assert d["stream_sha256"] == meta["stream_sha256"]

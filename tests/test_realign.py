@@ -139,6 +139,40 @@ def test_parallel_mate_fixing_equals_one_writer(built, tmp_path, max_records):
     assert a[0].tobytes() == b[0].tobytes()
 
 
+def _ref_lens(header):
+    return [int(dict(x.split(":", 1) for x in ln.split("\t")[1:])["LN"]) for ln in header.splitlines()
+            if ln.startswith("@SQ")]
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_contig_sharded_realign_equals_whole(built, tmp_path, world):
+    """realignment of contig-range shards (openge_amd/realign_shard.py), concatenated in
+    rank order, is the single-process output (here: the reference's own output)."""
+    from openge_amd import realign_shard as RS
+    meta, arrays, h, recs, offs, fa, iv = load_rl_case("rl_c5_2k", tmp_path)
+    n = len(offs) - 1
+    sl = RS.contig_slices(recs, offs, n, _ref_lens(h), world)
+    assert sl[0][0] == 0 and sl[-1][1] == n and all(a[1] == b[0] for a, b in zip(sl, sl[1:]))
+    parts, stats = [], []
+    for lo, hi in sl:
+        st = {}
+        out, oo = R.realign_cpu(h, recs, offs[lo:hi + 1], hi - lo, fa, iv, stats=st)
+        parts.append(bytes(out[:oo[-1]]))
+        stats.append(st)
+    assert all(st["tail_waiting"] < 150000 for st in stats[:-1])
+    whole = b"".join(parts)
+    d = R.digest(np.frombuffer(whole + b"\0" * 16, np.uint8), _offsets_of(whole))
+    assert d["stream_sha256"] == meta["stream_sha256"]
+
+
+def _offsets_of(stream: bytes) -> np.ndarray:
+    o, out = 0, []
+    while o < len(stream):
+        out.append(o)
+        o += 4 + int.from_bytes(stream[o:o + 4], "little")
+    return np.array(out, np.uint64)
+
+
 def test_realign_synth_is_deterministic(built, tmp_path):
     p = L.realign_synth_params(n_intervals=40, n_ref=2, seed=5)
     (tmp_path / "a").mkdir()
