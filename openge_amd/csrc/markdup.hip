@@ -101,46 +101,74 @@ __device__ bool same_pair_key(const uint8_t *recs, const RecMeta &A, const RecMe
     return true;
 }
 
-// One thread per hash run: pair consecutive occurrences of each exact key (in record order).
-// Common case (a run of exactly two): flag[p] = 1 and the pair is stored at p (compacted later by a
-// scan, no atomics).  Longer runs (hash collisions, supplementary records) append to `extra`.
-__global__ __launch_bounds__(kT) void k_pair_runs(const uint8_t *__restrict__ recs, const RecMeta *__restrict__ meta,
-                                                   const uint64_t *__restrict__ ckey, uint64_t nc, CandKey ck, uint8_t *__restrict__ used,
+// One thread per sorted candidate position p (a run = equal hash bits, in record order).  Common
+// case, a run of exactly two: a provisional pair (first-seen a < b, confirmed by k_pair_build) at
+// flag[p] / sparse[p], compacted later by a scan with no atomics.  Longer runs (hash collisions,
+// supplementary records) are queued (one wave-aggregated atomic) for k_pair_runs_slow, so no wave
+// waits on exact key compares.
+__global__ __launch_bounds__(kT) void k_pair_runs(const uint64_t *__restrict__ ckey, uint64_t nc, CandKey ck,
                                                    uint32_t *__restrict__ flag, uint64_t *__restrict__ sparse,
-                                                   uint64_t *__restrict__ extra, unsigned int *__restrict__ nextra) {
+                                                   uint32_t *__restrict__ slow, unsigned int *__restrict__ nslow) {
     const uint64_t p = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (p > nc) return;
-    if (p == nc) { flag[p] = 0; return; }
-    uint32_t f = 0;
-    const uint64_t kp = ckey[p];
-    const uint64_t h = ck.hash_of(kp);
-    if (p == 0 || ck.hash_of(ckey[p - 1]) != h) {
-        uint64_t e = p + 1;
-        while (e < nc && ck.hash_of(ckey[e]) == h) ++e;
-        if (e - p == 2) {
-            // provisional pair (first-seen a < b): confirmed by k_pair_build, which visits pairs in
-            // sorted-position order so both summaries are read from nearby rows
-            f = 1;
-            sparse[p] = ((kp & ck.idx_mask()) << 32) | (ckey[p + 1] & ck.idx_mask());
-        } else if (e - p > 2) {
-            for (uint64_t x = p; x < e; ++x) {
-                if (used[x]) continue;
-                const uint32_t a = (uint32_t)(ckey[x] & ck.idx_mask());
-                const RecMeta A = meta[a];
-                for (uint64_t y = x + 1; y < e; ++y) {
-                    if (used[y]) continue;
-                    const uint32_t b = (uint32_t)(ckey[y] & ck.idx_mask());
-                    if (same_pair_key(recs, A, meta[b], ck.split_k)) {
-                        used[x] = used[y] = 1;
-                        const unsigned int t = atomicAdd(nextra, 1u);
-                        extra[t] = ((uint64_t)a << 32) | b;
-                        break;
-                    }
-                }
+    bool queue = false;
+    if (p < nc) {
+        uint32_t f = 0;
+        const uint64_t kp = ckey[p];
+        const uint64_t h = ck.hash_of(kp);
+        if (p == 0 || ck.hash_of(ckey[p - 1]) != h) {
+            uint64_t e = p + 1;
+            while (e < nc && e - p <= 2 && ck.hash_of(ckey[e]) == h) ++e;
+            if (e - p == 2) {
+                f = 1;
+                sparse[p] = ((kp & ck.idx_mask()) << 32) | (ckey[p + 1] & ck.idx_mask());
+            } else if (e - p > 2) {
+                queue = true;
+            }
+        }
+        flag[p] = f;
+    } else if (p == nc) {
+        flag[p] = 0;
+    }
+    const uint64_t m = __ballot(queue);
+    if (m) {
+        const uint32_t lane = threadIdx.x & 63;
+        const uint32_t leader = (uint32_t)(__ffsll((long long)m) - 1);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(nslow, (unsigned int)__popcll(m));
+        base = __shfl(base, (int)leader, 64);
+        if (queue) slow[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint32_t)p;
+    }
+}
+
+// One thread per long run: the exact consecutive-occurrence pairing (ReadEndsMap first-seen /
+// second-seen, mark_duplicates.cpp:214-245) with full key compares; a pair is stored at the
+// sorted position of its first member, like the fast path.
+__global__ __launch_bounds__(kT) void k_pair_runs_slow(const uint8_t *__restrict__ recs, const RecMeta *__restrict__ meta,
+                                                        const uint64_t *__restrict__ ckey, uint64_t nc, CandKey ck,
+                                                        const uint32_t *__restrict__ slow, uint32_t nslow,
+                                                        uint8_t *__restrict__ used, uint32_t *__restrict__ flag,
+                                                        uint64_t *__restrict__ sparse) {
+    const uint32_t t = blockIdx.x * kT + threadIdx.x;
+    if (t >= nslow) return;
+    const uint64_t p = slow[t];
+    const uint64_t h = ck.hash_of(ckey[p]);
+    uint64_t e = p + 1;
+    while (e < nc && ck.hash_of(ckey[e]) == h) ++e;
+    for (uint64_t x = p; x < e; ++x) {
+        if (used[x]) continue;
+        const uint32_t a = (uint32_t)(ckey[x] & ck.idx_mask());
+        const RecMeta A = meta[a];
+        for (uint64_t y = x + 1; y < e; ++y) {
+            if (used[y]) continue;
+            const uint32_t b = (uint32_t)(ckey[y] & ck.idx_mask());
+            if (same_pair_key(recs, A, meta[b], ck.split_k)) {
+                used[x] = used[y] = 1;
+                flag[x] = 1;
+                sparse[x] = ((uint64_t)a << 32) | b;
+                break;
             }
         }
     }
-    flag[p] = f;
 }
 
 // after the exclusive scan, position p holds a pair iff pos[p+1] != pos[p]
@@ -409,8 +437,8 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     uint64_t *sparse = (uint64_t *)ctx->ws("md_sparse", nc1 * 8);
     uint64_t *pairs = (uint64_t *)ctx->ws("md_pairs", (nc1 / 2 + 1) * 8);
     uint64_t *pairs2 = (uint64_t *)ctx->ws("md_pairs2", (nc1 / 2 + 1) * 8);
-    uint64_t *extra = (uint64_t *)ctx->ws("md_extra", (nc1 / 2 + 1) * 8);
-    if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !extra) return OGE_ERR_HIP;
+    uint32_t *slow = (uint32_t *)ctx->ws("md_slow", nc1 * 4);
+    if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !slow) return OGE_ERR_HIP;
     CandKey ckl;
     ckl.ib = bits_for(n - 1);
     ckl.hb = std::min<uint32_t>(48, 64 - ckl.ib);
@@ -421,23 +449,27 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     uint64_t *sk;
     rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, ((1ull << ckl.hb) - 1) << ckl.ib, &sk, nullptr);
     if (rc) return rc;
-    OGE_HIP_TRY(ctx, hipMemsetAsync(used, 0, nc1, ctx->stream));
-    hipLaunchKernelGGL(k_pair_runs, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint8_t *)d_recs, meta,
-                       (const uint64_t *)sk, (uint64_t)nc, ckl, used, pflag, sparse, extra, cnt);
+    hipLaunchKernelGGL(k_pair_runs, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)sk, (uint64_t)nc, ckl,
+                       pflag, sparse, slow, cnt + 2);
     OGE_LAUNCH_CHECK(ctx);
+    uint32_t nslow = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&nslow, cnt + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (nslow) {
+        OGE_HIP_TRY(ctx, hipMemsetAsync(used, 0, nc1, ctx->stream));
+        hipLaunchKernelGGL(k_pair_runs_slow, dim3(oge_ceil_div(nslow, kT)), dim3(kT), 0, ctx->stream, (const uint8_t *)d_recs,
+                           meta, (const uint64_t *)sk, (uint64_t)nc, ckl, (const uint32_t *)slow, nslow, used, pflag, sparse);
+        OGE_LAUNCH_CHECK(ctx);
+    }
     rc = oge_exclusive_scan_u32(ctx, pflag, pflag, nc1);
     if (rc) return rc;
-    uint32_t hc[2] = {0, 0};
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&hc[0], pflag + nc, 4, hipMemcpyDeviceToHost, ctx->stream));
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&hc[1], cnt, 4, hipMemcpyDeviceToHost, ctx->stream));
+    uint32_t np = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&np, pflag + nc, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     // flags were overwritten by the scan: compact by comparing neighbouring prefix sums
     hipLaunchKernelGGL(k_pair_compact_scan, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)pflag,
                        (const uint64_t *)sparse, (uint64_t)nc, pairs);
     OGE_LAUNCH_CHECK(ctx);
-    if (hc[1])
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(pairs + hc[0], extra, (size_t)hc[1] * 8, hipMemcpyDeviceToDevice, ctx->stream));
-    const uint32_t np = hc[0] + hc[1];
     // order the pairs by first-mate position: k_pair_build then reads both summaries from nearby rows
     uint64_t *spairs = pairs;
     rc = oge_radix_sort_pairs(ctx, pairs, nullptr, pairs2, nullptr, np, bits_mask_hi32(n), &spairs, nullptr);
