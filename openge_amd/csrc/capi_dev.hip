@@ -13,7 +13,8 @@
 int oge_sort_buffers(oge_ctx *ctx, uint64_t n, uint64_t **keys, uint32_t **vals);
 unsigned int *oge_sort_counts(oge_ctx *ctx);
 int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
-                      bool keys_ready, uint64_t **kout, uint32_t **vout);
+                      bool keys_ready, uint64_t **kout, uint32_t **vout, const RecMeta *meta_in = nullptr,
+                      RecMeta *meta_out = nullptr);
 int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
                           const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
                           const RecMeta *smeta, const uint8_t *d_dup);
@@ -295,16 +296,12 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
     ctx->end_stage(t);
     uint64_t *k;
     uint32_t *v;
-    rc = oge_sort_keys_dev(ctx, d_recs, d_off, n, opts->n_ref, true, &k, &v);
-    if (rc) return rc;
-    if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_perm, v, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
     RecMeta *meta = (RecMeta *)ctx->ws("md_meta", (n + 1) * sizeof(RecMeta));
     uint8_t *dd = (uint8_t *)ctx->ws("sm_dup", n + 1);
     if (!meta || !dd) return OGE_ERR_HIP;
-    t = ctx->begin_stage("meta_gather");
-    rc = oge_meta_gather(ctx, meta_in, v, n, meta);
+    rc = oge_sort_keys_dev(ctx, d_recs, d_off, n, opts->n_ref, true, &k, &v, meta_in, meta);
     if (rc) return rc;
-    ctx->end_stage(t);
+    if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_perm, v, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
     uint64_t nd = 0;
     rc = oge_markdup_finish(ctx, (uint8_t *)d_recs, d_off, n, opts, meta, dd, 0, &nd);
     if (rc) return rc;

@@ -67,12 +67,110 @@ __device__ __forceinline__ bool tie_less(const uint8_t *__restrict__ recs, const
     return a < b;
 }
 
+// (name, flag, index) order of two records from their sorted summaries: the 32-byte name slots
+// (NUL-terminated, zero-padded: byte order of the slots = std::string order of the names) when
+// both names fit; the record bytes otherwise, and for the flag when the names are equal.
+__device__ __forceinline__ bool tie_less_meta(const uint8_t *__restrict__ recs, const RecMeta &A, const RecMeta &B,
+                                              uint32_t ia, uint32_t ib) {
+    if (A.m & B.m & OGE_M_NAMEFIT) {
+        const uint32_t *x = (const uint32_t *)A.name, *y = (const uint32_t *)B.name;
+#pragma unroll
+        for (int q = 0; q < OGE_NAME_SLOT / 4; ++q) {
+            if (x[q] != y[q]) return __builtin_bswap32(x[q]) < __builtin_bswap32(y[q]);
+        }
+        const uint16_t fa = oge_rd_u16(recs + A.src + OGE_OFF_FLAG), fb = oge_rd_u16(recs + B.src + OGE_OFF_FLAG);
+        if (fa != fb) return fa < fb;
+        return ia < ib;
+    }
+    const uint8_t *ra = recs + A.src, *rb = recs + B.src;
+    uint32_t la = ra[OGE_OFF_LNAME], lb = rb[OGE_OFF_LNAME];
+    uint32_t m = la < lb ? la : lb;
+    for (uint32_t i = 0; i < m; ++i) {
+        const uint8_t u = ra[OGE_OFF_NAME + i], v = rb[OGE_OFF_NAME + i];
+        if (u != v) return u < v;
+    }
+    if (la != lb) return la < lb;
+    const uint16_t fa = oge_rd_u16(ra + OGE_OFF_FLAG), fb = oge_rd_u16(rb + OGE_OFF_FLAG);
+    if (fa != fb) return fa < fb;
+    return ia < ib;
+}
+
+// Tie runs on the output-order summaries.  A block owns a 4096-position tile: it finds the run
+// heads of its tile (16 positions per thread, coalesced), collects the small runs (2..32 equal keys)
+// in LDS and then sorts them with every lane busy -- one run per lane, rows of a run contiguous.
+// Runs longer than 32 are appended to `large` (rare) for k_tie_large.  Keys, input indices and
+// rows move together.
+constexpr uint32_t kTieTile = 4096;
+__global__ __launch_bounds__(kT) void k_ties_meta(const uint8_t *__restrict__ recs, uint64_t *__restrict__ keys,
+                                                   uint32_t *__restrict__ vals, RecMeta *__restrict__ smeta, uint64_t n,
+                                                   int32_t n_ref, uint2 *__restrict__ large, unsigned int *__restrict__ nlarge) {
+    __shared__ uint32_t hp[kTieTile / 2];
+    __shared__ uint8_t hl[kTieTile / 2];
+    __shared__ unsigned int nh;
+    if (threadIdx.x == 0) nh = 0;
+    __syncthreads();
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kTieTile;
+    for (uint32_t j = 0; j < kTieTile / kT; ++j) {
+        const uint64_t p = tile0 + j * kT + threadIdx.x;
+        uint32_t len = 0;
+        if (p + 1 < n) {
+            const uint64_t k0 = keys[p] & kSortKeyMask;
+            if ((p == 0 || (keys[p - 1] & kSortKeyMask) != k0) && (keys[p + 1] & kSortKeyMask) == k0 &&
+                (k0 >> 33) != (uint64_t)(uint32_t)n_ref) {
+                uint64_t e = p + 2;
+                while (e < n && e - p <= 32 && (keys[e] & kSortKeyMask) == k0) ++e;
+                if (e - p > 32) { while (e < n && (keys[e] & kSortKeyMask) == k0) ++e; }
+                len = (uint32_t)(e - p);
+            }
+        }
+        const bool is_large = len > 32;
+        const uint32_t l = oge_wave_append(is_large, nlarge);
+        if (is_large) large[l] = make_uint2((uint32_t)p, len);
+        if (len >= 2 && len <= 32) {
+            const unsigned int h = atomicAdd(&nh, 1u);
+            hp[h] = (uint32_t)(p - tile0);
+            hl[h] = (uint8_t)len;
+        }
+    }
+    __syncthreads();
+    for (uint32_t h = threadIdx.x; h < nh; h += kT) {
+        const uint64_t p = tile0 + hp[h];
+        const uint32_t len = hl[h];
+        uint64_t *k = keys + p;
+        uint32_t *v = vals + p;
+        RecMeta *M = smeta + p;
+        for (uint32_t i = 1; i < len; ++i) {
+            const RecMeta mi = M[i];
+            const uint32_t vi = v[i];
+            const uint64_t ki = k[i];
+            int jj = (int)i - 1;
+            while (jj >= 0 && tie_less_meta(recs, mi, M[jj], vi, v[jj])) {
+                M[jj + 1] = M[jj];
+                v[jj + 1] = v[jj];
+                k[jj + 1] = k[jj];
+                --jj;
+            }
+            M[jj + 1] = mi;
+            v[jj + 1] = vi;
+            k[jj + 1] = ki;
+        }
+    }
+}
+
+// after k_tie_large re-ordered a long run's input indices: its rows again
+__global__ __launch_bounds__(kT) void k_meta_refill(const RecMeta *__restrict__ meta_in, const uint32_t *__restrict__ vals,
+                                                     const uint2 *__restrict__ large, RecMeta *__restrict__ smeta) {
+    const uint2 L = large[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < L.y; i += kT) smeta[L.x + i] = meta_in[vals[L.x + i]];
+}
+
 // One thread per sorted position: a run head with 2..32 equal keys insertion-sorts its run in place
 // by (name, flag, index); longer runs go to `large` (rare; one wave-aggregated append).  No
 // counter is touched for the common case, so nothing serialises on an atomic.
 __global__ __launch_bounds__(kT) void k_ties(const uint8_t *__restrict__ recs, const uint64_t *__restrict__ off,
                                               uint64_t *__restrict__ keys, uint32_t *__restrict__ vals, uint64_t n,
-                                              int32_t n_ref, uint2 *__restrict__ large, unsigned int *__restrict__ nlarge) {
+                                              int32_t n_ref, uint2 *__restrict__ large, unsigned int *__restrict__ nlarge,
+                                              bool sort_small) {
     const uint64_t p = (uint64_t)blockIdx.x * kT + threadIdx.x;
     uint32_t len = 0;
     if (p + 1 < n) {
@@ -89,7 +187,7 @@ __global__ __launch_bounds__(kT) void k_ties(const uint8_t *__restrict__ recs, c
     const bool is_large = len > 32;
     const uint32_t l = oge_wave_append(is_large, nlarge);
     if (is_large) large[l] = make_uint2((uint32_t)p, len);
-    if (len < 2 || len > 32) return;
+    if (len < 2 || len > 32 || !sort_small) return;
     uint64_t *k = keys + p;
     uint32_t *v = vals + p;
     for (uint32_t i = 1; i < len; ++i) {
@@ -171,8 +269,12 @@ int oge_sort_buffers(oge_ctx *ctx, uint64_t n, uint64_t **keys, uint32_t **vals)
 
 // Sort keys/vals for records; on return *kout/*vout hold the sorted (key, input index) pairs.
 // keys_ready: the KEYS pass (records.hip) already filled oge_sort_buffers and the `bad` word.
+int oge_meta_gather(oge_ctx *ctx, const RecMeta *in, const uint32_t *perm, uint64_t n, RecMeta *out);
+
+// With meta_in/meta_out, meta_out receives the summaries in output order, and the small tie runs
+// are ordered on them (k_ties_meta) instead of on the record bytes.
 int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
-                      bool keys_ready, uint64_t **kout, uint32_t **vout) {
+                      bool keys_ready, uint64_t **kout, uint32_t **vout, const RecMeta *meta_in, RecMeta *meta_out) {
     if (n_ref < 0 || n_ref >= (1 << 17)) return oge_fail(ctx, OGE_ERR_LIMIT, "sort: n_ref outside [0, 131072)");
     if (n > 0xFFFFFFFEull) return oge_fail(ctx, OGE_ERR_LIMIT, "sort: more than 2^32-2 records");
     uint64_t *keys;
@@ -204,14 +306,26 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     if (rc) return rc;
     ctx->end_stage(t);
 
-    // equal-coordinate runs -> (name, flag, index) order
-    t = ctx->begin_stage("sort_ties");
+    // equal-coordinate runs -> (name, flag, index) order.  With summaries: gather them first and
+    // order the small runs on them (k_ties_meta); long runs on the record bytes (k_tie_large), whose
+    // rows are then re-gathered.
     uint2 *large = (uint2 *)ctx->ws("sort_large", (n / 33 + 1) * sizeof(uint2));
     if (!large) return OGE_ERR_HIP;
     OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 8, ctx->stream));
+    if (meta_out) {
+        t = ctx->begin_stage("meta_gather");
+        rc = oge_meta_gather(ctx, meta_in, *vout, n, meta_out);
+        if (rc) return rc;
+        ctx->end_stage(t);
+    }
+    t = ctx->begin_stage("sort_ties");
     if (n > 1) {
-        hipLaunchKernelGGL(k_ties, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout, n, n_ref,
-                           large, counts + 1);
+        if (meta_out)
+            hipLaunchKernelGGL(k_ties_meta, dim3(oge_ceil_div(n, kTieTile)), dim3(kT), 0, ctx->stream, d_recs, *kout, *vout,
+                               meta_out, n, n_ref, large, counts + 1);
+        else
+            hipLaunchKernelGGL(k_ties, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout, n,
+                               n_ref, large, counts + 1, true);
         OGE_LAUNCH_CHECK(ctx);
     }
     unsigned int nlarge = 0;
@@ -236,6 +350,11 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
         hipLaunchKernelGGL(k_tie_large, dim3(nlarge), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout,
                            (const uint2 *)large, (const uint64_t *)dso, sk, sv);
         OGE_LAUNCH_CHECK(ctx);
+        if (meta_out) {
+            hipLaunchKernelGGL(k_meta_refill, dim3(nlarge), dim3(kT), 0, ctx->stream, meta_in, (const uint32_t *)*vout,
+                               (const uint2 *)large, meta_out);
+            OGE_LAUNCH_CHECK(ctx);
+        }
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
     ctx->end_stage(t);
