@@ -6,7 +6,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <atomic>
+#include <chrono>
 #include <unistd.h>
+#include <sys/mman.h>
 #include <cstring>
 #include <sstream>
 #include <thread>
@@ -89,6 +91,15 @@ static thread_local DeflateTls tls_deflate;
 
 const char *bgzf_codec_name() { return libdeflate().ok ? "libdeflate" : "zlib"; }
 
+// Large fresh buffers: ask for transparent huge pages before the first touch (a 5.7 GB stream is
+// 1.4M 4-KiB page faults otherwise, which serialise in the kernel).
+void want_huge_pages(void *p, size_t n) {
+    if (n < (64ull << 20)) return;
+    const uintptr_t a = ((uintptr_t)p + (2ull << 20) - 1) & ~(uintptr_t)((2ull << 20) - 1);
+    const uintptr_t e = ((uintptr_t)p + n) & ~(uintptr_t)((2ull << 20) - 1);
+    if (e > a) madvise((void *)a, e - a, MADV_HUGEPAGE);
+}
+
 // ---------------- BGZF inflate ----------------
 bool bgzf_inflate_all(const uint8_t *src, size_t n, bytevec &out, int threads, std::string &err, size_t slack) {
     struct Blk { size_t coff, clen, cdata, dlen, uoff; };
@@ -116,6 +127,7 @@ bool bgzf_inflate_all(const uint8_t *src, size_t n, bytevec &out, int threads, s
         p += bsize;
     }
     out.reserve(total + slack);
+    want_huge_pages(out.data(), total + slack);
     out.resize(total + slack);
     memset(out.data() + total, 0, slack);
     out.resize(total);  // capacity keeps the zeroed slack
@@ -391,7 +403,69 @@ std::string BamHeaderModel::to_string() const {
 }
 
 // ---------------- BAM ----------------
-bool bam_parse(bytevec &&raw, BamFile &out, std::string &err) {
+// Record offsets of the stream d[p, n) on all threads.  Each chunk but the first finds its first
+// record by trying positions until 16 consecutive records look well-formed (block_size in
+// [32, 10000], refIDs in range, NUL-terminated name, fixed fields inside the block), then walks to
+// the first record at or past the next chunk's start.  The walks must meet exactly at every
+// boundary and the last must end at n -- then the chain is the one a sequential walk from p takes
+// (it is anchored at p); otherwise the caller falls back to the sequential walk, which also
+// produces the reference's error messages for malformed input.
+static bool plausible_record(const uint8_t *d, size_t s, size_t n, int32_t n_ref) {
+    if (s + 36 > n) return false;
+    const uint32_t bs = rd32(d + s);
+    if (bs < 32 || bs > 10000 || s + 4 + bs > n) return false;
+    const int32_t ref = (int32_t)rd32(d + s + 4), mref = (int32_t)rd32(d + s + 24);
+    if (ref < -1 || ref >= n_ref || mref < -1 || mref >= n_ref) return false;
+    const uint32_t lname = d[s + 12], nc = rd16(d + s + 16), lseq = rd32(d + s + 20);
+    if (lname == 0 || d[s + 36 + lname - 1] != 0) return false;
+    return 32ull + lname + 4ull * nc + (lseq + 1ull) / 2 + lseq <= bs;
+}
+
+static bool parse_offsets_parallel(const uint8_t *d, size_t p, size_t n, int32_t n_ref, int threads,
+                                   std::vector<uint64_t> &offsets) {
+    const int T = threads;
+    std::vector<size_t> cut(T + 1);
+    for (int i = 0; i <= T; ++i) cut[i] = p + (n - p) * (size_t)i / (size_t)T;
+    std::vector<size_t> start(T, 0), stop(T, 0);
+    std::vector<std::vector<uint64_t>> part(T);
+    std::atomic<bool> ok(true);
+    parallel_for((size_t)T, T, [&](size_t i) {
+        size_t s = cut[i];
+        if (i > 0) {
+            const size_t lim = std::min(n, cut[i] + 20016);
+            for (; s < lim; ++s) {
+                size_t q = s;
+                int k = 0;
+                for (; k < 16 && q < n && plausible_record(d, q, n, n_ref); ++k) q += 4 + rd32(d + q);
+                if (k == 16 || (q == n && k > 0)) break;
+            }
+            if (s >= lim) { ok = false; return; }
+        }
+        start[i] = s;
+        std::vector<uint64_t> &o = part[i];
+        o.reserve((cut[i + 1] - cut[i]) / 200 + 16);
+        size_t q = s;
+        while (q < cut[i + 1]) {
+            if (q + 4 > n) { ok = false; return; }
+            const uint32_t bs = rd32(d + q);
+            if (bs < 32 || bs > 10000 || q + 4 + bs > n) { ok = false; return; }
+            o.push_back(q - p);
+            q += 4 + bs;
+        }
+        stop[i] = q;
+    });
+    if (!ok) return false;
+    for (int i = 0; i + 1 < T; ++i)
+        if (stop[i] != start[i + 1]) return false;
+    if (stop[T - 1] != n) return false;
+    std::vector<size_t> at(T + 1, 0);
+    for (int i = 0; i < T; ++i) at[i + 1] = at[i] + part[i].size();
+    offsets.resize(at[T]);
+    parallel_for((size_t)T, T, [&](size_t i) { std::copy(part[i].begin(), part[i].end(), offsets.begin() + at[i]); });
+    return true;
+}
+
+bool bam_parse(bytevec &&raw, BamFile &out, std::string &err, int threads) {
     out.data = std::move(raw);
     const uint8_t *d = out.data.data();
     size_t n = out.data.size();
@@ -422,6 +496,9 @@ bool bam_parse(bytevec &&raw, BamFile &out, std::string &err) {
     }
     out.rec_base = p;
     out.offsets.clear();
+    if (threads > 1 && n - p >= (64ull << 20) && parse_offsets_parallel(d, p, n, (int32_t)n_ref, threads, out.offsets))
+        return true;
+    out.offsets.clear();
     size_t q = p;
     while (q < n) {
         if (q + 4 > n) { err = "Expected more bytes reading BAM core. Is this file truncated or corrupted?"; return false; }
@@ -436,11 +513,16 @@ bool bam_parse(bytevec &&raw, BamFile &out, std::string &err) {
 }
 
 bool bam_read_file(const std::string &path, BamFile &out, int threads, std::string &err) {
+    static const bool dbg = getenv("OGE_IO_DEBUG") != nullptr;
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = clk();
     FILE *f = (path == "-" || path == "stdin") ? stdin : fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
     bytevec comp;
     if (f != stdin && fseeko(f, 0, SEEK_END) == 0) {  // regular file: parallel preads into a sized buffer
         off_t sz = ftello(f);
+        comp.reserve(sz > 0 ? (size_t)sz : 0);
+        want_huge_pages(comp.data(), comp.capacity());
         comp.resize(sz > 0 ? (size_t)sz : 0);
         const int fd = fileno(f);
         const size_t chunk = 64ull << 20, nch = (comp.size() + chunk - 1) / chunk;
@@ -467,9 +549,16 @@ bool bam_read_file(const std::string &path, BamFile &out, int threads, std::stri
         while ((r = fread(buf, 1, sizeof(buf), f)) > 0) comp.insert(comp.end(), buf, buf + r);
     }
     if (f != stdin) fclose(f);
+    const auto t1 = clk();
     bytevec raw;
     if (!bgzf_inflate_all(comp.data(), comp.size(), raw, threads, err)) return false;
-    return bam_parse(std::move(raw), out, err);
+    const auto t2 = clk();
+    const bool ok = bam_parse(std::move(raw), out, err, threads);
+    if (dbg)
+        fprintf(stderr, "[openge] read %s: file %.3f s, inflate %.3f s, parse %.3f s\n", path.c_str(),
+                std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count(),
+                std::chrono::duration<double>(clk() - t2).count());
+    return ok;
 }
 
 std::vector<uint8_t> bam_encode_header(const BamHeaderModel &h) {

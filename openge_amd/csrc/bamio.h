@@ -81,7 +81,9 @@ struct BamFile {
 };
 
 bool bam_read_file(const std::string &path, BamFile &out, int threads, std::string &err);
-bool bam_parse(bytevec &&raw, BamFile &out, std::string &err);
+// madvise(MADV_HUGEPAGE) over a large buffer before its first touch
+void want_huge_pages(void *p, size_t n);
+bool bam_parse(bytevec &&raw, BamFile &out, std::string &err, int threads = 1);
 // Serialize header block (magic, text, reference list taken from the header @SQ lines, as
 // BamSerializer::open does at util/bam_serializer.h:54-76).
 std::vector<uint8_t> bam_encode_header(const BamHeaderModel &h);

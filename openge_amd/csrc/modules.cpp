@@ -37,6 +37,8 @@ int ChainContext::to_device(ReadBatch &b) {
 int ChainContext::to_host(ReadBatch &b) {
     if (b.host_valid) return 0;
     b.recs.clear();
+    b.recs.reserve(b.d_bytes + 16);
+    want_huge_pages(b.recs.data(), b.d_bytes + 16);
     b.recs.resize(b.d_bytes + 16);  // uninitialised: the copy below writes every byte but the slack
     memset(b.recs.data() + b.d_bytes, 0, 16);
     b.offs.resize(b.n + 1);

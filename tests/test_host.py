@@ -81,6 +81,21 @@ def test_writer_reproduces_reference_output_stream(built, tmp_path, name):
     assert ms == g["mapped_sha256"] and ts == g["tail_multiset_sha256"]
 
 
+def test_parallel_record_parse_equals_sequential(built, tmp_path):
+    """bam_parse splits a >= 64 MB stream across threads (verified chain joins); the record offsets
+    must equal the one-thread walk, also when a chunk boundary falls inside a record."""
+    p = L.synth_params(160_000, preset="mix", seed=11)
+    recs, offs, hdr = L.synth_host(p)
+    path = tmp_path / "big.bam"
+    L.write_bam(path, hdr, recs, offs, 320_000, level=1)
+    one = L.Bam(path, threads=1)
+    for t in (3, 8, 16):
+        many = L.Bam(path, threads=t)
+        assert many.n == one.n == 320_000
+        assert np.array_equal(many.offs, one.offs)
+        assert many.recs.tobytes() == one.recs.tobytes()
+
+
 def test_synth_host_is_deterministic_and_thread_independent(built):
     p = L.synth_params(3000, preset="c2", seed=42)
     a, ao, _ = L.synth_host(p, threads=1)
