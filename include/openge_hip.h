@@ -235,6 +235,26 @@ int oge_bam_write(const char *path, const char *header_text, uint64_t header_len
                   const uint8_t *recs, const uint64_t *offs, uint64_t n, const uint32_t *order,
                   const uint16_t *flags, int level, int threads);
 
+/* ---- BGZF compression on the device (replaces BgzfOutputStream's deflate workers,
+ * util/bgzf_output_stream.cpp:59-250; crc32 at :139) ---------------------------------- */
+/* Worst-case size of the BGZF stream for n payload bytes (one 64 KiB slot per 65,280-byte block). */
+uint64_t oge_bgzf_bound(uint64_t n);
+/* Compress n bytes at d_src into consecutive BGZF blocks (65,280-byte payloads; dynamic-Huffman
+ * deflate, or stored blocks for level 0 / incompressible payloads) written back to back at d_dst.
+ * No EOF marker is appended.  dst_cap must be >= oge_bgzf_bound(n); *out_bytes = stream size.
+ * Deterministic: the same input gives the same bytes. */
+int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t n, int level, uint8_t *d_dst,
+                         uint64_t dst_cap, uint64_t *out_bytes);
+/* Host-buffer form (uploads, compresses, downloads); dst_cap >= the compressed size. */
+int oge_bgzf_deflate(oge_ctx *ctx, const uint8_t *src, uint64_t n, int level, uint8_t *dst, uint64_t dst_cap,
+                     uint64_t *out_bytes);
+/* Recompute every record's bin field in place (BamSerializer::write, util/bam_serializer.h:112-116). */
+int oge_fix_bins_dev(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n);
+/* Copy the records whose FLAG has none of flag_mask set, in order, to d_out / d_out_off (n_out
+ * records): the writer side of -r/-R (MarkDuplicates::runInternal, mark_duplicates.cpp:456-458). */
+int oge_drop_flagged_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, uint16_t flag_mask,
+                         uint8_t *d_out, uint64_t *d_out_off, uint64_t *n_out);
+
 #ifdef __cplusplus
 }
 #endif

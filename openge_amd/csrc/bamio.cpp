@@ -91,6 +91,11 @@ static thread_local DeflateTls tls_deflate;
 
 const char *bgzf_codec_name() { return libdeflate().ok ? "libdeflate" : "zlib"; }
 
+bool bgzf_host_codec_forced() {
+    const char *env = getenv("OGE_BGZF_CODEC");
+    return env && (std::string(env) == "zlib" || std::string(env) == "libdeflate");
+}
+
 // Large fresh buffers: ask for transparent huge pages before the first touch (a 5.7 GB stream is
 // 1.4M 4-KiB page faults otherwise, which serialise in the kernel).
 void want_huge_pages(void *p, size_t n) {
@@ -261,6 +266,12 @@ void BgzfWriter::write_span(const uint8_t *data, size_t n) {
         emit(std::move(outs));  // written while the next window compresses
     }
     pending_.insert(pending_.end(), data + whole * kBlockPayload, data + n);
+}
+
+void BgzfWriter::write_compressed(const uint8_t *z, size_t n) {
+    flush_blocks(true);
+    drain();
+    if (n) fwrite(z, 1, n, f_);
 }
 
 void BgzfWriter::close() {

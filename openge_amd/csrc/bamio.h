@@ -25,6 +25,8 @@ namespace oge {
 // out is sized to the stream (plus `slack` zeroed bytes past it) without a serial zero-fill first
 bool bgzf_inflate_all(const uint8_t *src, size_t n, bytevec &out, int threads, std::string &err, size_t slack = 64);
 const char *bgzf_codec_name();  // "libdeflate" or "zlib"
+// OGE_BGZF_CODEC=zlib|libdeflate: compress on the host even when the records sit on the device.
+bool bgzf_host_codec_forced();
 
 class BgzfWriter {
 public:
@@ -36,6 +38,9 @@ public:
     // Append n bytes: whole blocks are compressed straight from the caller's bytes, all in parallel,
     // with no staging copy (only a partial tail block is copied).
     void write_span(const uint8_t *data, size_t n);
+    // Append already-compressed BGZF blocks (e.g. from oge_bgzf_deflate_dev): the pending partial
+    // block is flushed as a block of its own first, so block boundaries stay intact.
+    void write_compressed(const uint8_t *z, size_t n);
     void close();  // flush + EOF marker
 private:
     void flush_blocks(bool final);

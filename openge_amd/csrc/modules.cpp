@@ -263,15 +263,85 @@ static void fix_bins(ReadBatch &b, int threads) {
     for (auto &t : ts) t.join();
 }
 
+// Device-resident records: drop duplicates (-r/-R), recompute bins and BGZF-compress on the GPU;
+// only the compressed stream crosses PCIe.  The records of a batch are back to back in its arena
+// (the reader's stream, a gather's output), so the stream is the byte range [off[0], off[n]).
+int FileWriter::compress_on_device(ChainContext &cc, ReadBatch &b, bytevec &z, double *t_dev, double *t_d2h) {
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = clk();
+    uint8_t *recs = b.d_recs;
+    uint64_t *offs = b.d_offs;
+    uint64_t n = b.n;
+    void *kept = nullptr, *kept_off = nullptr, *dz = nullptr;
+    auto release = [&]() {
+        if (kept) oge_dev_free(cc.ctx, kept);
+        if (kept_off) oge_dev_free(cc.ctx, kept_off);
+        if (dz) oge_dev_free(cc.ctx, dz);
+    };
+    if (b.drop_duplicates && n) {
+        if (oge_dev_alloc(cc.ctx, b.d_bytes + 64, &kept) || oge_dev_alloc(cc.ctx, (n + 1) * 8, &kept_off)) {
+            release();
+            return cc.fail("device allocation");
+        }
+        uint64_t m = 0;
+        if (oge_drop_flagged_dev(cc.ctx, recs, offs, n, OGE_F_DUP, (uint8_t *)kept, (uint64_t *)kept_off, &m)) {
+            release();
+            return cc.fail("FileWriter: drop duplicates");
+        }
+        recs = (uint8_t *)kept;
+        offs = (uint64_t *)kept_off;
+        n = m;
+    }
+    uint64_t ends[2] = {0, 0};
+    if (n && (oge_fix_bins_dev(cc.ctx, recs, offs, n) || oge_memcpy(cc.ctx, &ends[0], offs, 8, 2) ||
+              oge_memcpy(cc.ctx, &ends[1], offs + n, 8, 2))) {
+        release();
+        return cc.fail("FileWriter: bins");
+    }
+    const uint64_t len = ends[1] - ends[0];
+    uint64_t zb = 0;
+    if (len) {
+        const uint64_t cap = oge_bgzf_bound(len);
+        if (oge_dev_alloc(cc.ctx, cap, &dz)) {
+            release();
+            return cc.fail("device allocation");
+        }
+        if (oge_bgzf_deflate_dev(cc.ctx, recs + ends[0], len, std::max(0, std::min(9, level_)), (uint8_t *)dz, cap, &zb) || oge_ctx_sync(cc.ctx)) {
+            release();
+            return cc.fail("FileWriter: BGZF on the device");
+        }
+    }
+    const auto t1 = clk();
+    z.clear();
+    z.reserve(zb + 16);
+    want_huge_pages(z.data(), zb + 16);
+    z.resize(zb);
+    if (zb && oge_memcpy(cc.ctx, z.data(), dz, zb, 2)) {
+        release();
+        return cc.fail("device->host copy");
+    }
+    release();
+    *t_dev = std::chrono::duration<double>(t1 - t0).count();
+    *t_d2h = std::chrono::duration<double>(clk() - t1).count();
+    return 0;
+}
+
 int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
     auto clk = [] { return std::chrono::steady_clock::now(); };
     auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
         return std::chrono::duration<double>(z - a).count();
     };
     const auto t0 = clk();
-    if (cc.to_host(b)) return -1;
+    const bool on_device = b.dev_valid && !b.host_valid && !bgzf_host_codec_forced();
+    bytevec z;
+    double t_dev = 0, t_d2h = 0;
+    if (on_device) {
+        if (compress_on_device(cc, b, z, &t_dev, &t_d2h)) return -1;
+    } else if (cc.to_host(b)) {
+        return -1;
+    }
     const auto t1 = clk();
-    fix_bins(b, cc.threads);
+    if (!on_device) fix_bins(b, cc.threads);
     const auto t2 = clk();
     BamHeaderModel h = b.header;
     if (!program_line_.empty()) {  // file_writer.cpp:76-89
@@ -296,9 +366,13 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
         BgzfWriter w(f, level_, cc.threads > 0 ? cc.threads : 8);
         std::vector<uint8_t> hb = bam_encode_header(h);
         w.write(hb.data(), hb.size());
+        if (on_device) {
+            w.write_compressed(z.data(), z.size());
+            w.close();
+        }
         // maximal runs of records that sit back to back in memory go out as spans (no copy)
         uint64_t k = 0;
-        while (k < b.n) {
+        while (!on_device && k < b.n) {
             const uint8_t *r = b.recs.data() + b.offs[k];
             if (b.drop_duplicates && (oge_rd_u16(r + OGE_OFF_FLAG) & OGE_F_DUP)) {
                 ++k;
@@ -318,7 +392,11 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
         w.close();
     }
     if (f != stdout) fclose(f);
-    if (verbose_)
+    if (verbose_ && on_device)
+        fprintf(stderr, "[openge] FileWriter: device bins + BGZF %.3f s (gpu, %.3f of %llu bytes), device->host %.3f s, write %.3f s\n",
+                t_dev, z.size() ? (double)z.size() / (double)std::max<uint64_t>(1, b.bytes()) : 0.0,
+                (unsigned long long)z.size(), t_d2h, sec(t2, clk()));
+    else if (verbose_)
         fprintf(stderr, "[openge] FileWriter: device->host %.3f s, bins %.3f s, BGZF %.3f s (%s)\n", sec(t0, t1), sec(t1, t2),
                 sec(t2, clk()), bgzf_codec_name());
     else fflush(stdout);

@@ -131,6 +131,7 @@ public:
     FileWriter() : AlgorithmModule("FileWriter") {}
     void setFilename(const std::string &f) { filename_ = f; }
     void setCompressionLevel(int l) { level_ = l; }
+    int compress_on_device(ChainContext &cc, ReadBatch &b, bytevec &z, double *t_dev, double *t_d2h);
     void addProgramLine(const std::string &cl) { program_line_ = cl; }
     int setFormat(const std::string &f);  // only "bam" is supported (SAM/FASTQ out of scope)
 protected:

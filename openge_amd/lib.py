@@ -204,6 +204,11 @@ def lib() -> C.CDLL:
         "oge_realign_result_free": (None, [vp]),
         "oge_realign_synth_defaults": (None, [vp]),
         "oge_synth_realign": (C.c_int, [vp, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
+        "oge_bgzf_bound": (u64, [u64]),
+        "oge_bgzf_deflate_dev": (C.c_int, [vp, vp, u64, C.c_int, vp, u64, C.POINTER(u64)]),
+        "oge_bgzf_deflate": (C.c_int, [vp, vp, u64, C.c_int, vp, u64, C.POINTER(u64)]),
+        "oge_fix_bins_dev": (C.c_int, [vp, vp, vp, u64]),
+        "oge_drop_flagged_dev": (C.c_int, [vp, vp, vp, u64, C.c_uint16, vp, vp, C.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)
@@ -394,6 +399,28 @@ class Context:
         t = C.c_int()
         check(lib().oge_radix_sort_pairs_dev(self.h, d_keys, d_vals, d_ktmp, d_vtmp, n, bit_mask, C.byref(t)), self.h)
         return bool(t.value)
+
+    def bgzf_deflate(self, data: bytes | np.ndarray, level: int = 6) -> bytes:
+        """BGZF-compress host bytes on the device (no EOF marker)."""
+        a = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, np.uint8)
+        cap = int(lib().oge_bgzf_bound(len(a)))
+        out = np.empty(max(cap, 1), dtype=np.uint8)
+        got = C.c_uint64()
+        check(lib().oge_bgzf_deflate(self.h, _ptr(a), len(a), level, _ptr(out), cap, C.byref(got)), self.h)
+        return out[:got.value].tobytes()
+
+    def bgzf_deflate_dev(self, d_src, n: int, level: int, d_dst, dst_cap: int) -> int:
+        got = C.c_uint64()
+        check(lib().oge_bgzf_deflate_dev(self.h, d_src, n, level, d_dst, dst_cap, C.byref(got)), self.h)
+        return got.value
+
+    def fix_bins_dev(self, d_recs, d_off, n: int) -> None:
+        check(lib().oge_fix_bins_dev(self.h, d_recs, d_off, n), self.h)
+
+    def drop_flagged_dev(self, d_recs, d_off, n: int, flag_mask: int, d_out, d_out_off) -> int:
+        m = C.c_uint64()
+        check(lib().oge_drop_flagged_dev(self.h, d_recs, d_off, n, flag_mask, d_out, d_out_off, C.byref(m)), self.h)
+        return m.value
 
     def markdup_dev(self, d_recs, d_off, n, opts: MarkdupOpts, d_dup, apply: bool = True) -> int:
         nd = C.c_uint64()

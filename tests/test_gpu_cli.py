@@ -130,3 +130,30 @@ def test_cli_errors_are_loud(tmp_path):
     r = subprocess.run([OPENGE, "mergesort", str(GOLDEN / "inputs" / "208.truncated.bam"), "-o", str(tmp_path / "t.bam")],
                        capture_output=True, text=True)
     assert r.returncode != 0 and "truncated" in r.stderr
+
+
+@pytest.mark.parametrize("cmd", [("mergesort", "-M"), ("dedup", "-r")])
+def test_cli_gpu_bgzf_equals_host_codec(tmp_path, cmd):
+    """The writer compresses device-resident records on the GPU by default; the decompressed file
+    must equal the host codec's (OGE_BGZF_CODEC=libdeflate) byte for byte, incl. -r (dups dropped
+    on the device) and the bins recomputed there."""
+    import gzip
+    import os
+    p = L.synth_params(60_000, preset="c2", seed=77)
+    recs, offs, hdr = L.synth_host(p)
+    src = tmp_path / "in.bam"
+    L.write_bam(str(src), hdr, recs, offs, len(offs) - 1, level=1)
+    out = {}
+    for codec in ("gpu", "libdeflate"):
+        env = dict(os.environ)
+        env.pop("OGE_BGZF_CODEC", None)
+        if codec != "gpu":
+            env["OGE_BGZF_CODEC"] = codec
+        dst = tmp_path / f"{codec}.bam"
+        r = subprocess.run([OPENGE, *cmd, "--nopg", "-v", str(src), "-o", str(dst)],
+                           capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr
+        assert ("(gpu," in r.stderr) == (codec == "gpu"), r.stderr
+        out[codec] = gzip.decompress(dst.read_bytes())
+    assert out["gpu"] == out["libdeflate"]
+    assert len(out["gpu"]) > 1_000_000

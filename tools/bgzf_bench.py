@@ -1,0 +1,57 @@
+"""Device BGZF compression throughput on C2-shaped records already resident in HBM.
+
+    python tools/bgzf_bench.py [reads=20000000] [reps=3]
+
+Prints one JSON line: payload GB/s (HIP-event time of the `bgzf_deflate` stage), compressed ratio,
+and the ratio of host libdeflate level 6 on a 64 MB sample of the same bytes for comparison."""
+import json
+import sys
+import time
+import zlib
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from openge_amd import lib as L  # noqa: E402
+
+
+def main():
+    reads = int(sys.argv[1]) if len(sys.argv) > 1 else 20_000_000
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    dev = torch.device("cuda", 0)
+    ctx = L.Context(0)
+    p = L.synth_params(reads // 2, preset="c2", seed=1234)
+    n = 2 * (reads // 2)
+    d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), None)
+    ctx.sync()
+    B = int(d_offs[-1].item())
+    d_recs = torch.empty(B + 64, dtype=torch.uint8, device=dev)
+    ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), d_recs.data_ptr())
+    ctx.sync()
+    cap = int(L.lib().oge_bgzf_bound(B))
+    d_z = torch.empty(cap, dtype=torch.uint8, device=dev)
+    ms, wall = [], []
+    zb = 0
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        zb = ctx.bgzf_deflate_dev(d_recs.data_ptr(), B, 6, d_z.data_ptr(), cap)
+        wall.append(time.perf_counter() - t0)
+        ms.append(ctx.timing("bgzf_deflate"))
+    ms, wall = ms[1:], wall[1:]
+    sample = d_recs[: min(B, 64 << 20)].cpu().numpy().tobytes()
+    host = sum(len(zlib.compress(sample[i:i + 65280], 6)) + 26 for i in range(0, len(sample), 65280))
+    print(json.dumps({
+        "reads": n, "payload_bytes": B, "compressed_bytes": zb, "ratio": round(zb / B, 4),
+        "zlib6_ratio_sample": round(host / len(sample), 4),
+        "ms": [round(x, 2) for x in ms], "wall_s": [round(x, 3) for x in wall],
+        "GBps": round(B / (min(ms) * 1e-3) / 1e9, 1),
+    }), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
