@@ -92,16 +92,28 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
     }
 }
 
+__device__ __forceinline__ uint32_t crc_mat(const uint32_t *M, uint32_t c) {  // GF(2) matrix x vector
+    uint32_t r = 0;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) r ^= (uint32_t)(-(int32_t)((c >> b) & 1)) & M[b];
+    return r;
+}
+
 // ------------------------------------------------------------------------------------ tokens
 // tok layout: [(blk * kNSub + sub) * kSeg + k] * kT + t  (u32: literal byte, or
 // 0x80000000 | (len - 3) << 16 | (dist - 1)); ntok[(blk * kNSub + sub) * kT + t].
+// zpow[k][32]: operator of feeding 2^k zero bytes through the (reflected) CRC-32 register.
 __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
-                                                    uint32_t *__restrict__ tok, uint8_t *__restrict__ ntok,
-                                                    uint32_t *__restrict__ freq_out) {
+                                                    const uint32_t *__restrict__ zpow, uint32_t *__restrict__ tok,
+                                                    uint8_t *__restrict__ ntok, uint32_t *__restrict__ freq_out,
+                                                    uint32_t *__restrict__ crc_out) {
     __shared__ uint32_t in[kPay / 4 + 4];
     __shared__ uint32_t htab[1 << kHashBits];
     __shared__ uint16_t cand[kSub];
     __shared__ uint32_t freq[kFreq];
+    __shared__ uint32_t crctab[4][256];
+    __shared__ uint32_t zp[16][32];
+    __shared__ uint32_t crcs[kT];
     const int t = threadIdx.x;
     const uint64_t blk = blk0 + blockIdx.x;
     const uint64_t start = blk * kPay;
@@ -116,20 +128,77 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
         const uint32_t nw = (len + 3) / 4;
         // words whose aligned source span stays inside the payload's bytes use dword loads
         const uint32_t safe = len / 4;  // words wholly inside the payload
-        for (uint32_t k = t; k < nw + 4; k += kT) {
+        constexpr int U = 8;  // loads in flight per thread
+        for (uint32_t k0 = t; k0 < safe; k0 += U * kT) {
+            uint32_t lo[U], hi[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const uint32_t k = min(k0 + j * kT, safe - 1);
+                lo[j] = W[k];
+                hi[j] = sh ? W[k + 1] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const uint32_t k = k0 + j * kT;
+                if (k < safe) in[k] = sh ? __builtin_amdgcn_alignbyte(hi[j], lo[j], sh) : lo[j];
+            }
+        }
+        for (uint32_t k = safe + t; k < nw + 4; k += kT) {
             uint32_t v = 0;
-            if (k < safe) {
-                v = sh ? __builtin_amdgcn_alignbyte(W[k + 1], W[k], sh) : W[k];
-            } else if (k < nw) {
+            if (k < nw)
                 for (int b = 0; b < 4; ++b)
                     if (4 * k + b < len) v |= (uint32_t)s[4 * k + b] << (8 * b);
-            }
             in[k] = v;
         }
     }
     for (int i = t; i < (1 << kHashBits); i += kT) htab[i] = 0;
     for (int i = t; i < kFreq; i += kT) freq[i] = 0;
+    if (t < 256) {  // slice-by-4 tables
+        auto byte_step = [](uint32_t c) {
+            for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (uint32_t)(-(int32_t)(c & 1)));
+            return c;
+        };
+        uint32_t c = byte_step(t);
+        crctab[0][t] = c;
+        for (int k = 1; k < 4; ++k) c = (c >> 8) ^ byte_step(c & 0xff), crctab[k][t] = c;
+    }
+    for (int i = t; i < 16 * 32; i += kT) zp[i >> 5][i & 31] = zpow[i];
     __syncthreads();
+
+    // CRC-32 of the payload: the data is right-aligned in a 65536-byte window (leading zeros leave a
+    // zero register unchanged); thread t owns window bytes [128t, 128t + 128); pairs of pieces are
+    // combined with crc(A || B) = Z_|B|(crc A) ^ crc B, and the whole with the 0xffffffff preset.
+    {
+        const uint32_t lead = kSlot - len, w0 = t * 128u;
+        uint32_t c = 0;
+        if (w0 >= lead) {
+            const uint32_t d0 = w0 - lead;
+#pragma unroll 4
+            for (int i = 0; i < 32; ++i) {
+                c ^= ld32(in, d0 + 4 * i);
+                c = crctab[3][c & 0xff] ^ crctab[2][(c >> 8) & 0xff] ^ crctab[1][(c >> 16) & 0xff] ^ crctab[0][c >> 24];
+            }
+        } else if (w0 + 128 > lead) {
+            for (uint32_t d = 0; d < w0 + 128 - lead; ++d)
+                c = crctab[0][(c ^ (in[d >> 2] >> (8 * (d & 3)))) & 0xff] ^ (c >> 8);
+        }
+        crcs[t] = c;
+    }
+    __syncthreads();
+    for (int lv = 0; lv < 9; ++lv) {
+        const int pairs = kT >> (lv + 1);
+        uint32_t v = 0;
+        if (t < pairs) v = crc_mat(zp[7 + lv], crcs[2 * t]) ^ crcs[2 * t + 1];
+        __syncthreads();
+        if (t < pairs) crcs[t] = v;
+        __syncthreads();
+    }
+    if (t == 0) {
+        uint32_t c = 0xffffffffu;
+        for (int k = 0; k < 16; ++k)
+            if ((len >> k) & 1) c = crc_mat(zp[k], c);
+        crc_out[blockIdx.x] = ~(c ^ crcs[0]);
+    }
 
     for (int sub = 0; sub < kNSub; ++sub) {
         const uint32_t base = sub * kSub;
@@ -459,24 +528,15 @@ __device__ __forceinline__ uint32_t tok_bits(uint32_t v, const uint32_t *lit, co
     return (lit[s] >> 16) + nb + (dist[s2] >> 16) + nb2;
 }
 
-__device__ __forceinline__ uint32_t crc_mat(const uint32_t *M, uint32_t c) {  // GF(2) matrix x vector
-    uint32_t r = 0;
-#pragma unroll
-    for (int b = 0; b < 32; ++b) r ^= (uint32_t)(-(int32_t)((c >> b) & 1)) & M[b];
-    return r;
-}
 
 // zpow[k][32]: operator of feeding 2^k zero bytes through the (reflected) CRC-32 register
 __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0, int level,
                                                   const uint32_t *__restrict__ tok, const uint8_t *__restrict__ ntok,
-                                                  const DeflTab *__restrict__ tabs, const uint32_t *__restrict__ zpow,
+                                                  const DeflTab *__restrict__ tabs, const uint32_t *__restrict__ crc_in,
                                                   uint8_t *__restrict__ slots, uint32_t *__restrict__ sizes) {
     __shared__ uint32_t lit[kLit], dist[kDist];
-    __shared__ uint32_t crctab[256];
-    __shared__ uint32_t zp[16][32];
     __shared__ uint32_t scan[kNSeg];
     __shared__ uint32_t wsum[kT / 64];
-    __shared__ uint32_t crcs[kT];
     __shared__ uint32_t sh_total, sh_stored;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint64_t blk = blk0 + blockIdx.x;
@@ -486,32 +546,7 @@ __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ sr
     const DeflTab &T = tabs[blockIdx.x];
     for (int i = t; i < kLit; i += kT) lit[i] = T.lit[i];
     for (int i = t; i < kDist; i += kT) dist[i] = T.dist[i];
-    if (t < 256) {
-        uint32_t c = t;
-        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (uint32_t)(-(int32_t)(c & 1)));
-        crctab[t] = c;
-    }
-    for (int i = t; i < 16 * 32; i += kT) zp[i >> 5][i & 31] = zpow[i];
     __syncthreads();
-
-    // CRC-32 of the payload: the data is right-aligned in a 65536-byte window (leading zeros do not
-    // change a zero-initialised register); thread t owns window bytes [128t, 128t + 128).
-    {
-        const uint32_t lead = kSlot - len;
-        uint32_t c = 0;
-        const uint32_t w0 = t * 128u;
-        for (uint32_t w = max(w0, lead); w < w0 + 128; ++w) c = crctab[(c ^ s[w - lead]) & 0xff] ^ (c >> 8);
-        crcs[t] = c;
-    }
-    __syncthreads();
-    for (int lv = 0; lv < 9; ++lv) {  // combine pairs: crc(A || B) = Z_|B|(crc A) ^ crc B
-        const int pairs = kT >> (lv + 1);
-        uint32_t v = 0;
-        if (t < pairs) v = crc_mat(zp[7 + lv], crcs[2 * t]) ^ crcs[2 * t + 1];
-        __syncthreads();
-        if (t < pairs) crcs[t] = v;
-        __syncthreads();
-    }
 
     // bit counts per segment, in stream order (sub-block 0 segments then sub-block 1)
     uint32_t cnt[kNSub];
@@ -519,7 +554,14 @@ __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ sr
         const uint32_t nt = ntok[((uint64_t)blockIdx.x * kNSub + sub) * kT + t];
         const uint32_t *tp = tok + ((uint64_t)blockIdx.x * kNSub + sub) * kSeg * kT + t;
         uint32_t b = 0;
-        for (uint32_t k = 0; k < nt; ++k) b += tok_bits(tp[(uint64_t)k * kT], lit, dist);
+        for (uint32_t k0 = 0; k0 < nt; k0 += 8) {  // every segment owns kSeg token slots: batch the loads
+            uint32_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = tp[(uint64_t)min(k0 + j, (uint32_t)kSeg - 1) * kT];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (k0 + j < nt) b += tok_bits(v[j], lit, dist);
+        }
         cnt[sub] = b;
         scan[sub * kT + t] = b;
     }
@@ -556,7 +598,8 @@ __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ sr
     uint32_t *ow = (uint32_t *)out;
     // zero what the block will occupy (atomicOr targets included)
     for (uint32_t i = t; i < (total + 15) / 16; i += kT) ((uint4 *)out)[i] = make_uint4(0, 0, 0, 0);
-    __threadfence();
+    // workgroup-scope release/acquire (in __syncthreads) orders these stores before the atomics of
+    // other waves; a device-scope __threadfence would write back the XCD's L2 on gfx950
     __syncthreads();
     if (t == 0) {
         ow[0] = 0x04088b1fu;  // ID1 ID2 CM=8 FLG=FEXTRA
@@ -564,15 +607,7 @@ __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ sr
         ow[2] = 0x0006ff00u;  // XFL=0 OS=255 XLEN=6
         ow[3] = 0x00024342u;  // 'B' 'C' SLEN=2
     }
-    // full CRC: ~raw(0xffffffff, data) = ~(Z_len(0xffffffff) ^ raw(0, data))
-    __shared__ uint32_t sh_crc;
-    if (t == 0) {
-        uint32_t c = 0xffffffffu;
-        for (int k = 0; k < 16; ++k)
-            if ((len >> k) & 1) c = crc_mat(zp[k], c);
-        sh_crc = ~(c ^ crcs[0]);
-    }
-    __syncthreads();
+    const uint32_t sh_crc = crc_in[blockIdx.x];
     const uint32_t bsize = total - 1;
     if (stored) {
         if (t == 0) {
@@ -603,8 +638,14 @@ __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ sr
             const uint32_t *tp = tok + ((uint64_t)blockIdx.x * kNSub + sub) * kSeg * kT + t;
             BitW w;
             w.init(bw, 16 + hb + scan[sub * kT + t]);
-            for (uint32_t k = 0; k < nt; ++k) {
-                const uint32_t v = tp[(uint64_t)k * kT];
+            for (uint32_t k0 = 0; k0 < nt; k0 += 8) {
+              uint32_t vv[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) vv[j] = tp[(uint64_t)min(k0 + j, (uint32_t)kSeg - 1) * kT];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                if (k0 + j >= nt) break;
+                const uint32_t v = vv[j];
                 if (!(v >> 31)) {
                     const uint32_t c = lit[v];
                     w.put(c & 0xffff, c >> 16);
@@ -618,6 +659,7 @@ __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ sr
                     const uint32_t d = dist[sy];
                     w.put((d & 0xffff) | (ev << (d >> 16)), (d >> 16) + nb);
                 }
+              }
             }
             w.finish();
         }
@@ -721,7 +763,8 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     uint32_t *offs = (uint32_t *)ctx->ws("defl_offs", chunk * 4 + 16);
     uint32_t *zpow = (uint32_t *)ctx->ws("defl_zpow", 16 * 32 * 4);
     uint64_t *base = (uint64_t *)ctx->ws("defl_base", 16);
-    if (!tok || !ntok || !freq || !tabs || !slots || !sizes || !offs || !zpow || !base) return OGE_ERR_HIP;
+    uint32_t *crc = (uint32_t *)ctx->ws("defl_crc", chunk * 4 + 16);
+    if (!tok || !ntok || !freq || !tabs || !slots || !sizes || !offs || !zpow || !base || !crc) return OGE_ERR_HIP;
     static uint32_t z[16][32];
     static bool zinit = false;
     if (!zinit) crc_zpow(z), zinit = true;
@@ -730,11 +773,11 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     OgeStageTimer *tm = ctx->begin_stage("bgzf_deflate");
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
-        k_defl_tokens<<<nb, kT, 0, ctx->stream>>>(d_src, n, b0, tok, ntok, freq);
+        k_defl_tokens<<<nb, kT, 0, ctx->stream>>>(d_src, n, b0, zpow, tok, ntok, freq, crc);
         OGE_LAUNCH_CHECK(ctx);
         k_defl_huff<<<nb, 64, 0, ctx->stream>>>(freq, tabs);
         OGE_LAUNCH_CHECK(ctx);
-        k_defl_emit<<<nb, kT, 0, ctx->stream>>>(d_src, n, b0, level, tok, ntok, tabs, zpow, slots, sizes);
+        k_defl_emit<<<nb, kT, 0, ctx->stream>>>(d_src, n, b0, level, tok, ntok, tabs, crc, slots, sizes);
         OGE_LAUNCH_CHECK(ctx);
         int rc = oge_exclusive_scan_u32(ctx, sizes, offs, nb);
         if (rc) return rc;
