@@ -248,6 +248,27 @@ int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t n, int lev
 /* Host-buffer form (uploads, compresses, downloads); dst_cap >= the compressed size. */
 int oge_bgzf_deflate(oge_ctx *ctx, const uint8_t *src, uint64_t n, int level, uint8_t *dst, uint64_t dst_cap,
                      uint64_t *out_bytes);
+/* ---- BGZF decompression and BAM record boundaries on the device (replaces BgzfInputStream,
+ * util/bgzf_input_stream.cpp:65-142,208-240, and BamDeserializer's record walk,
+ * util/bam_deserializer.h:143-193) ------------------------------------------------------ */
+/* Host: index the BGZF framing of z.  For each block with a non-empty payload (at most cap):
+ * d0/d1 = byte range of its deflate data in z, uoff = payload offset (uoff has cap + 1 entries;
+ * uoff[nblk] = total), crc = the stored CRC-32.  Any array may be NULL.  *nblk = block count
+ * (OGE_ERR_ARG when it exceeds cap). */
+int oge_bgzf_index(const uint8_t *z, uint64_t zbytes, uint64_t *d0, uint64_t *d1, uint64_t *uoff, uint32_t *crc,
+                   uint64_t cap, uint64_t *nblk);
+/* Inflate the indexed blocks of d_z (4-byte aligned) into d_out + uoff[i]; d_crc (may be NULL)
+ * checks every payload's CRC-32.  Fails with OGE_ERR_IO on corrupt data. */
+int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d_d0, const uint64_t *d_d1,
+                         const uint64_t *d_uoff, const uint32_t *d_crc, uint64_t nblk, uint8_t *d_out);
+/* Host-buffer form: the whole BGZF stream z -> out (out_cap >= payload total). */
+int oge_bgzf_inflate(oge_ctx *ctx, const uint8_t *z, uint64_t zbytes, uint8_t *out, uint64_t out_cap,
+                     uint64_t *out_bytes);
+/* Record boundaries of the decompressed BAM stream d_stream[rec_base, end): d_off[i] = absolute
+ * offset of record i, d_off[n] = end (cap >= n + 1; d_off NULL = count only).  Equals the sequential
+ * block_size walk; block_size outside [32, 10000] or a record past the end fails (OGE_ERR_IO). */
+int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream, uint64_t rec_base, uint64_t end, int32_t n_ref,
+                               uint64_t *d_off, uint64_t cap, uint64_t *n_out);
 /* Recompute every record's bin field in place (BamSerializer::write, util/bam_serializer.h:112-116). */
 int oge_fix_bins_dev(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n);
 /* Copy the records whose FLAG has none of flag_mask set, in order, to d_out / d_out_off (n_out

@@ -35,11 +35,11 @@
 #include "bam_layout.h"
 #include "oge_ctx.h"
 #include "records.h"
+#include "bgzf_dev.h"
 
 namespace {
 
-constexpr uint32_t kPay = 65280;          // BGZF payload per block
-constexpr uint32_t kSlot = 65536;         // max BGZF block size
+using namespace oge_bgzf;
 constexpr int kT = 512;                   // threads per workgroup (tokens / emit)
 constexpr int kSeg = 64;                  // bytes per thread segment
 constexpr int kSub = kT * kSeg;           // 32768 positions per sub-block
@@ -57,10 +57,6 @@ struct DeflTab {
     uint32_t hdr[kHdrWords];
 };
 
-__device__ __forceinline__ uint32_t ld32(const uint32_t *w, uint32_t p) {  // unaligned LDS read
-    const uint32_t a = w[p >> 2], b = w[(p >> 2) + 1];
-    return __builtin_amdgcn_alignbyte(b, a, p & 3);
-}
 
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashBits); }
 
@@ -92,12 +88,6 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
     }
 }
 
-__device__ __forceinline__ uint32_t crc_mat(const uint32_t *M, uint32_t c) {  // GF(2) matrix x vector
-    uint32_t r = 0;
-#pragma unroll
-    for (int b = 0; b < 32; ++b) r ^= (uint32_t)(-(int32_t)((c >> b) & 1)) & M[b];
-    return r;
-}
 
 // ------------------------------------------------------------------------------------ tokens
 // tok layout: [(blk * kNSub + sub) * kSeg + k] * kT + t  (u32: literal byte, or
@@ -112,7 +102,7 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
     __shared__ uint16_t cand[kSub];
     __shared__ uint32_t freq[kFreq];
     __shared__ uint32_t crctab[4][256];
-    __shared__ uint32_t zp[16][32];
+    __shared__ uint32_t zp[17][32];
     __shared__ uint32_t crcs[kT];
     const int t = threadIdx.x;
     const uint64_t blk = blk0 + blockIdx.x;
@@ -120,84 +110,14 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
     const uint32_t len = (uint32_t)min<uint64_t>(kPay, n - start);
     const uint8_t *s = src + start;
 
-    // stage the payload: aligned dword loads funnel-shifted to the payload's alignment
-    {
-        const uintptr_t a = (uintptr_t)s & ~(uintptr_t)3;
-        const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
-        const uint32_t *W = (const uint32_t *)a;
-        const uint32_t nw = (len + 3) / 4;
-        // words whose aligned source span stays inside the payload's bytes use dword loads
-        const uint32_t safe = len / 4;  // words wholly inside the payload
-        constexpr int U = 8;  // loads in flight per thread
-        for (uint32_t k0 = t; k0 < safe; k0 += U * kT) {
-            uint32_t lo[U], hi[U];
-#pragma unroll
-            for (int j = 0; j < U; ++j) {
-                const uint32_t k = min(k0 + j * kT, safe - 1);
-                lo[j] = W[k];
-                hi[j] = sh ? W[k + 1] : 0;
-            }
-#pragma unroll
-            for (int j = 0; j < U; ++j) {
-                const uint32_t k = k0 + j * kT;
-                if (k < safe) in[k] = sh ? __builtin_amdgcn_alignbyte(hi[j], lo[j], sh) : lo[j];
-            }
-        }
-        for (uint32_t k = safe + t; k < nw + 4; k += kT) {
-            uint32_t v = 0;
-            if (k < nw)
-                for (int b = 0; b < 4; ++b)
-                    if (4 * k + b < len) v |= (uint32_t)s[4 * k + b] << (8 * b);
-            in[k] = v;
-        }
-    }
+    stage_words<kT>(in, s, len, t);
     for (int i = t; i < (1 << kHashBits); i += kT) htab[i] = 0;
     for (int i = t; i < kFreq; i += kT) freq[i] = 0;
-    if (t < 256) {  // slice-by-4 tables
-        auto byte_step = [](uint32_t c) {
-            for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (uint32_t)(-(int32_t)(c & 1)));
-            return c;
-        };
-        uint32_t c = byte_step(t);
-        crctab[0][t] = c;
-        for (int k = 1; k < 4; ++k) c = (c >> 8) ^ byte_step(c & 0xff), crctab[k][t] = c;
-    }
-    for (int i = t; i < 16 * 32; i += kT) zp[i >> 5][i & 31] = zpow[i];
+    crc_setup<kT>(crctab, zp, zpow, t);
     __syncthreads();
-
-    // CRC-32 of the payload: the data is right-aligned in a 65536-byte window (leading zeros leave a
-    // zero register unchanged); thread t owns window bytes [128t, 128t + 128); pairs of pieces are
-    // combined with crc(A || B) = Z_|B|(crc A) ^ crc B, and the whole with the 0xffffffff preset.
     {
-        const uint32_t lead = kSlot - len, w0 = t * 128u;
-        uint32_t c = 0;
-        if (w0 >= lead) {
-            const uint32_t d0 = w0 - lead;
-#pragma unroll 4
-            for (int i = 0; i < 32; ++i) {
-                c ^= ld32(in, d0 + 4 * i);
-                c = crctab[3][c & 0xff] ^ crctab[2][(c >> 8) & 0xff] ^ crctab[1][(c >> 16) & 0xff] ^ crctab[0][c >> 24];
-            }
-        } else if (w0 + 128 > lead) {
-            for (uint32_t d = 0; d < w0 + 128 - lead; ++d)
-                c = crctab[0][(c ^ (in[d >> 2] >> (8 * (d & 3)))) & 0xff] ^ (c >> 8);
-        }
-        crcs[t] = c;
-    }
-    __syncthreads();
-    for (int lv = 0; lv < 9; ++lv) {
-        const int pairs = kT >> (lv + 1);
-        uint32_t v = 0;
-        if (t < pairs) v = crc_mat(zp[7 + lv], crcs[2 * t]) ^ crcs[2 * t + 1];
-        __syncthreads();
-        if (t < pairs) crcs[t] = v;
-        __syncthreads();
-    }
-    if (t == 0) {
-        uint32_t c = 0xffffffffu;
-        for (int k = 0; k < 16; ++k)
-            if ((len >> k) & 1) c = crc_mat(zp[k], c);
-        crc_out[blockIdx.x] = ~(c ^ crcs[0]);
+        const uint32_t c = crc_window512(in, len, crctab, zp, crcs, t);
+        if (t == 0) crc_out[blockIdx.x] = c;
     }
 
     for (int sub = 0; sub < kNSub; ++sub) {
@@ -718,22 +638,6 @@ __global__ void k_keep_perm(const uint32_t *__restrict__ keep, const uint32_t *_
     if (keep[i]) perm[pos[i]] = (uint32_t)i;
 }
 
-// host: zero-byte operators Z_{2^k}, k = 0..15 (columns = images of the 32 basis bits)
-static void crc_zpow(uint32_t z[16][32]) {
-    for (int b = 0; b < 32; ++b) {  // one zero byte
-        uint32_t c = 1u << b;
-        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (uint32_t)(-(int32_t)(c & 1)));
-        z[0][b] = c;
-    }
-    for (int k = 1; k < 16; ++k)
-        for (int b = 0; b < 32; ++b) {
-            uint32_t v = z[k - 1][b], r = 0;
-            for (int j = 0; j < 32; ++j)
-                if ((v >> j) & 1) r ^= z[k - 1][j];
-            z[k][b] = r;
-        }
-}
-
 }  // namespace
 
 int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
@@ -761,11 +665,11 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     uint8_t *slots = (uint8_t *)ctx->ws("defl_slots", chunk * kSlot);
     uint32_t *sizes = (uint32_t *)ctx->ws("defl_sizes", chunk * 4 + 16);
     uint32_t *offs = (uint32_t *)ctx->ws("defl_offs", chunk * 4 + 16);
-    uint32_t *zpow = (uint32_t *)ctx->ws("defl_zpow", 16 * 32 * 4);
+    uint32_t *zpow = (uint32_t *)ctx->ws("defl_zpow", 17 * 32 * 4);
     uint64_t *base = (uint64_t *)ctx->ws("defl_base", 16);
     uint32_t *crc = (uint32_t *)ctx->ws("defl_crc", chunk * 4 + 16);
     if (!tok || !ntok || !freq || !tabs || !slots || !sizes || !offs || !zpow || !base || !crc) return OGE_ERR_HIP;
-    static uint32_t z[16][32];
+    static uint32_t z[17][32];
     static bool zinit = false;
     if (!zinit) crc_zpow(z), zinit = true;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, z, sizeof(z), hipMemcpyHostToDevice, ctx->stream));

@@ -1,0 +1,123 @@
+// bgzf_dev.h -- device helpers shared by the BGZF deflate (bgzf.hip) and inflate (inflate.hip)
+// kernels: LDS payload staging, slice-by-4 CRC-32 with zero-operator combining.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace oge_bgzf {
+
+constexpr uint32_t kPay = 65280;   // BGZF payload per block written here
+constexpr uint32_t kSlot = 65536;  // max BGZF block size (and max payload accepted on input)
+
+__device__ __forceinline__ uint32_t ld32(const uint32_t *w, uint32_t p) {  // unaligned LDS read
+    const uint32_t a = w[p >> 2], b = w[(p >> 2) + 1];
+    return __builtin_amdgcn_alignbyte(b, a, p & 3);
+}
+
+__device__ __forceinline__ uint32_t crc_mat(const uint32_t *M, uint32_t c) {  // GF(2) matrix x vector
+    uint32_t r = 0;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) r ^= (uint32_t)(-(int32_t)((c >> b) & 1)) & M[b];
+    return r;
+}
+
+// Stage len bytes at s (any alignment) into LDS words in[0 .. (len+3)/4 + 4), zero padded.
+// Aligned dword loads, funnel-shifted, U loads in flight per thread.
+template <int NT>
+__device__ void stage_words(uint32_t *in, const uint8_t *s, uint32_t len, int t) {
+    const uintptr_t a = (uintptr_t)s & ~(uintptr_t)3;
+    const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
+    const uint32_t *W = (const uint32_t *)a;
+    const uint32_t nw = (len + 3) / 4;
+    const uint32_t safe = len / 4;  // words wholly inside the payload
+    constexpr int U = 8;
+    for (uint32_t k0 = t; k0 < safe; k0 += U * NT) {
+        uint32_t lo[U], hi[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t k = min(k0 + j * NT, safe - 1);
+            lo[j] = W[k];
+            hi[j] = sh ? W[k + 1] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t k = k0 + j * NT;
+            if (k < safe) in[k] = sh ? __builtin_amdgcn_alignbyte(hi[j], lo[j], sh) : lo[j];
+        }
+    }
+    for (uint32_t k = safe + t; k < nw + 4; k += NT) {
+        uint32_t v = 0;
+        if (k < nw)
+            for (int b = 0; b < 4; ++b)
+                if (4 * k + b < len) v |= (uint32_t)s[4 * k + b] << (8 * b);
+        in[k] = v;
+    }
+}
+
+// Slice-by-4 tables and the 2^k-zero-byte operators (zpow from the host, 17 x 32 words, k = 0..16).
+template <int NT>
+__device__ void crc_setup(uint32_t (*crctab)[256], uint32_t (*zp)[32], const uint32_t *zpow, int t) {
+    if (t < 256) {
+        auto byte_step = [](uint32_t c) {
+            for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (uint32_t)(-(int32_t)(c & 1)));
+            return c;
+        };
+        uint32_t c = byte_step(t);
+        crctab[0][t] = c;
+        for (int k = 1; k < 4; ++k) c = (c >> 8) ^ byte_step(c & 0xff), crctab[k][t] = c;
+    }
+    for (int i = t; i < 17 * 32; i += NT) zp[i >> 5][i & 31] = zpow[i];
+}
+
+// CRC-32 of the len (<= 65536) bytes staged in LDS; 512 threads; result valid in every thread.
+// The data is right-aligned in a 65536-byte window (leading zeros leave a zero register unchanged);
+// thread t owns window bytes [128t, 128t + 128); pairs of pieces are combined with
+// crc(A || B) = Z_|B|(crc A) ^ crc B, and the whole with the 0xffffffff preset.
+__device__ uint32_t crc_window512(const uint32_t *in, uint32_t len, const uint32_t (*crctab)[256], const uint32_t (*zp)[32],
+                                  uint32_t *crcs, int t) {
+    const uint32_t lead = kSlot - len, w0 = t * 128u;
+    uint32_t c = 0;
+    if (w0 >= lead) {
+        const uint32_t d0 = w0 - lead;
+#pragma unroll 4
+        for (int i = 0; i < 32; ++i) {
+            c ^= ld32(in, d0 + 4 * i);
+            c = crctab[3][c & 0xff] ^ crctab[2][(c >> 8) & 0xff] ^ crctab[1][(c >> 16) & 0xff] ^ crctab[0][c >> 24];
+        }
+    } else if (w0 + 128 > lead) {
+        for (uint32_t d = 0; d < w0 + 128 - lead; ++d) c = crctab[0][(c ^ (in[d >> 2] >> (8 * (d & 3)))) & 0xff] ^ (c >> 8);
+    }
+    crcs[t] = c;
+    __syncthreads();
+    for (int lv = 0; lv < 9; ++lv) {
+        const int pairs = 512 >> (lv + 1);
+        uint32_t v = 0;
+        if (t < pairs) v = crc_mat(zp[7 + lv], crcs[2 * t]) ^ crcs[2 * t + 1];
+        __syncthreads();
+        if (t < pairs) crcs[t] = v;
+        __syncthreads();
+    }
+    uint32_t r = 0xffffffffu;
+    for (int k = 0; k < 17; ++k)
+        if ((len >> k) & 1) r = crc_mat(zp[k], r);
+    return ~(r ^ crcs[0]);
+}
+
+// host: zero-byte operators Z_{2^k}, k = 0..16 (columns = images of the 32 basis bits)
+inline void crc_zpow(uint32_t z[17][32]) {
+    for (int b = 0; b < 32; ++b) {  // one zero byte
+        uint32_t c = 1u << b;
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (uint32_t)(-(int32_t)(c & 1)));
+        z[0][b] = c;
+    }
+    for (int k = 1; k < 17; ++k)
+        for (int b = 0; b < 32; ++b) {
+            uint32_t v = z[k - 1][b], r = 0;
+            for (int j = 0; j < 32; ++j)
+                if ((v >> j) & 1) r ^= z[k - 1][j];
+            z[k][b] = r;
+        }
+}
+
+}  // namespace oge_bgzf

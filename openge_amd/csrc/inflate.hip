@@ -1,0 +1,604 @@
+// inflate.hip -- BGZF decompression on the GPU, and the device-side BAM record boundary parse.
+//
+// Replaces `BgzfInputStream::decompress` (openge/src/util/bgzf_input_stream.cpp:65-142,208-240:
+// inflateInit2(-15) per block at :116-123) and the record walk of `BamDeserializer::read`
+// (util/bam_deserializer.h:143-193, block_size bounds at :160-163).  SURVEY §8f rows 1-2.
+//
+//   oge_bgzf_index (host)  walks the BGZF framing: per block the deflate byte range, the payload
+//                          offset (prefix sum of ISIZE) and the stored CRC-32.
+//   k_inflate              one wave per block.  The whole decoder runs wave-uniform (every lane
+//                          computes the same symbol), so its state lives in scalar registers; the
+//                          compressed bits stream through two VGPRs (256 bytes each, lane l holding
+//                          word l) read with v_readlane, decode tables (10-bit direct lookup + the
+//                          canonical count/offset walk for longer codes) sit in LDS, literals are
+//                          stored by lane 0 and back-references copied by all 64 lanes at once.
+//   k_crc_check            one 512-thread workgroup per block: the payload staged in LDS, slice-by-4
+//                          CRC-32 combined across threads; any mismatch fails the call.
+//   k_rec_walk             BAM record boundaries: one thread per 64 KiB chunk walks the block_size
+//                          chain from its chunk's first record start (found by a 16-record
+//                          plausibility chain); the host verifies that every chunk's walk ends where
+//                          the next one starts and re-walks from the true end when it does not, so
+//                          the result equals the sequential walk.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "bam_layout.h"
+#include "bgzf_dev.h"
+#include "oge_ctx.h"
+
+namespace {
+
+using namespace oge_bgzf;
+
+__constant__ uint16_t kLBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                    31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t kLExt[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t kDBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
+                                    193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t kDExt[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t kClOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// Wave-uniform LSB-first bit reader over the compressed bytes.
+struct Bits {
+    const uint32_t *zw;
+    uint64_t zwords;
+    uint64_t base;  // word index held by lane 0 of `cur`
+    uint64_t pos;   // absolute bit position
+    uint32_t cur, nxt;
+    __device__ __forceinline__ uint32_t ldw(uint64_t w) const { return w < zwords ? zw[w] : 0u; }
+    __device__ void seek(uint64_t bit) {
+        pos = bit;
+        base = bit >> 5;
+        const int l = threadIdx.x & 63;
+        cur = ldw(base + l);
+        nxt = ldw(base + 64 + l);
+    }
+    __device__ __forceinline__ uint32_t peek() const {
+        const uint32_t rel = (uint32_t)((pos >> 5) - base);
+        const uint32_t lo = __builtin_amdgcn_readlane(rel < 64 ? cur : nxt, rel & 63);
+        const uint32_t hi = __builtin_amdgcn_readlane(rel + 1 < 64 ? cur : nxt, (rel + 1) & 63);
+        return (uint32_t)((((uint64_t)hi << 32) | lo) >> (pos & 31));
+    }
+    __device__ __forceinline__ void skip(uint32_t n) {  // n <= 32
+        pos += n;
+        if ((pos >> 5) - base >= 64) {
+            cur = nxt;
+            base += 64;
+            nxt = ldw(base + 64 + (threadIdx.x & 63));
+        }
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t n) {  // n <= 31
+        const uint32_t v = n ? peek() & ((1u << n) - 1) : 0u;
+        skip(n);
+        return v;
+    }
+};
+
+// Canonical Huffman decode tables for one alphabet (RFC 1951 3.2.2): tab = 2^TB direct entries
+// (symbol | length << 9, 0 = longer code or unused), cnt[len] and sym[] (symbols ordered by (length,
+// value)) for the bit-by-bit walk.  Returns false for an over-subscribed code.
+template <int TB>
+__device__ bool build_table(const uint8_t *lens, int n, uint16_t *tab, uint32_t *cnt, uint16_t *sym, uint32_t *first,
+                            uint32_t *offs) {
+    const int lane = threadIdx.x;
+    for (int i = lane; i < (1 << TB); i += 64) tab[i] = 0;
+    uint32_t tot[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) tot[b] = 0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int s = c0 + lane;
+        const uint32_t L = s < n ? lens[s] : 0;
+#pragma unroll
+        for (int b = 1; b < 16; ++b) tot[b] += __popcll(__ballot(L == (uint32_t)b));
+    }
+    int left = 1;
+#pragma unroll
+    for (int b = 1; b < 16; ++b) {
+        left = 2 * left - (int)tot[b];
+        if (left < 0) return false;
+    }
+    if (lane == 0) {
+        uint32_t code = 0, off = 0;
+        cnt[0] = 0;
+#pragma unroll
+        for (int b = 1; b < 16; ++b) {
+            code = (code + (b > 1 ? tot[b - 1] : 0)) << (b > 1 ? 1 : 0);
+            first[b] = code;
+            offs[b] = off;
+            off += tot[b];
+            cnt[b] = tot[b];
+        }
+    }
+    __syncthreads();
+    uint32_t run[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) run[b] = 0;
+    const uint64_t lt = (1ull << lane) - 1;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int s = c0 + lane;
+        const uint32_t L = s < n ? lens[s] : 0;
+        uint32_t rank = 0;
+#pragma unroll
+        for (int b = 1; b < 16; ++b) {
+            const uint64_t m = __ballot(L == (uint32_t)b);
+            if (L == (uint32_t)b) rank = run[b] + __popcll(m & lt);
+            run[b] += __popcll(m);
+        }
+        if (L) {
+            const uint32_t code = first[L] + rank;
+            sym[offs[L] + rank] = (uint16_t)s;
+            if (L <= (uint32_t)TB) {
+                const uint32_t r = __builtin_bitreverse32(code) >> (32 - L);
+                const uint16_t e = (uint16_t)(s | (L << 9));
+                for (uint32_t k = 0; k < (1u << (TB - L)); ++k) tab[r | (k << L)] = e;
+            }
+        }
+    }
+    __syncthreads();
+    return true;
+}
+
+template <int TB>
+__device__ __forceinline__ int decode_sym(Bits &br, const uint16_t *tab, const uint32_t *cnt, const uint16_t *sym) {
+    const uint32_t v = br.peek();
+    const uint32_t e = tab[v & ((1u << TB) - 1)];
+    if (e) {
+        br.skip(e >> 9);
+        return (int)(e & 511);
+    }
+    int code = 0, first = 0, index = 0;
+    for (int len = 1; len <= 15; ++len) {
+        code |= (int)((v >> (len - 1)) & 1);
+        const int count = (int)cnt[len];
+        if (code - count < first) {
+            br.skip(len);
+            return sym[index + (code - first)];
+        }
+        index += count;
+        first += count;
+        first <<= 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+enum { E_STORED = 1, E_CODE = 2, E_OVERRUN = 3, E_LEN = 4, E_DIST = 5, E_FAR = 6, E_TYPE = 7, E_PAST = 8, E_SIZE = 9,
+       E_TABLE = 10, E_CRC = 11 };
+
+__device__ __forceinline__ void report(uint32_t *err, uint32_t code, uint64_t blk) {
+    atomicOr(err, 1u << code);
+    atomicMin(err + 1, (uint32_t)min<uint64_t>(blk, 0xffffffffull));
+}
+
+__global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ z, uint64_t zbytes, const uint64_t *__restrict__ d0,
+                                                const uint64_t *__restrict__ d1, const uint64_t *__restrict__ uoff,
+                                                uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
+    __shared__ uint16_t ltab[1024], dtab[1024], ctab[128];
+    __shared__ uint32_t lcnt[16], dcnt[16], ccnt[16], tfirst[16], toffs[16];
+    __shared__ uint16_t lsym[288], dsym[32], csym[19];
+    __shared__ uint8_t lens[320], cl[19];
+    const int lane = threadIdx.x;
+    const uint64_t b = blockIdx.x;
+    Bits br;
+    br.zw = (const uint32_t *)z;
+    br.zwords = (zbytes + 3) / 4;
+    br.seek(d0[b] * 8);
+    const uint64_t end_bit = d1[b] * 8;
+    uint8_t *o = out + uoff[b];
+    const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
+    uint32_t pos = 0;
+    int e = 0;
+    for (;;) {
+        const uint32_t h = br.get(3);
+        const uint32_t type = h >> 1;
+        if (type == 0) {
+            br.skip((8 - (uint32_t)(br.pos & 7)) & 7);
+            const uint32_t len = br.get(16), nlen = br.get(16);
+            const uint64_t src = br.pos >> 3;
+            if ((len ^ 0xffffu) != nlen || pos + len > osz || src + len > d1[b]) {
+                e = E_STORED;
+                break;
+            }
+            for (uint32_t i = lane; i < len; i += 64) o[pos + i] = z[src + i];
+            pos += len;
+            br.seek(br.pos + (uint64_t)len * 8);
+        } else if (type == 1 || type == 2) {
+            int hlit = 288, hdist = 30;
+            if (type == 1) {
+                for (int s = lane; s < 318; s += 64)
+                    lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+                __syncthreads();
+            } else {
+                hlit = (int)br.get(5) + 257;
+                hdist = (int)br.get(5) + 1;
+                const int hclen = (int)br.get(4) + 4;
+                if (hlit > 286 || hdist > 30) {
+                    e = E_TABLE;
+                    break;
+                }
+                if (lane < 19) cl[lane] = 0;
+                __syncthreads();
+                for (int i = 0; i < hclen; ++i) {
+                    const uint32_t v = br.get(3);
+                    if (lane == 0) cl[kClOrd[i]] = (uint8_t)v;
+                }
+                __syncthreads();
+                if (!build_table<7>(cl, 19, ctab, ccnt, csym, tfirst, toffs)) {
+                    e = E_TABLE;
+                    break;
+                }
+                const int total = hlit + hdist;
+                int i = 0;
+                uint32_t prev = 0;
+                while (i < total) {
+                    const int s = decode_sym<7>(br, ctab, ccnt, csym);
+                    if (s < 0) {
+                        e = E_CODE;
+                        break;
+                    }
+                    if (s < 16) {
+                        if (lane == 0) lens[i] = (uint8_t)s;
+                        prev = (uint32_t)s;
+                        ++i;
+                        continue;
+                    }
+                    uint32_t val = 0, rep;
+                    if (s == 16) {
+                        if (i == 0) {
+                            e = E_TABLE;
+                            break;
+                        }
+                        val = prev;
+                        rep = 3 + br.get(2);
+                    } else if (s == 17) {
+                        rep = 3 + br.get(3);
+                    } else {
+                        rep = 11 + br.get(7);
+                    }
+                    if (i + (int)rep > total) {
+                        e = E_TABLE;
+                        break;
+                    }
+                    if ((uint32_t)lane < rep) lens[i + lane] = (uint8_t)val;
+                    if (rep > 64 && (uint32_t)lane + 64 < rep) lens[i + 64 + lane] = (uint8_t)val;
+                    if (rep > 128 && (uint32_t)lane + 128 < rep) lens[i + 128 + lane] = (uint8_t)val;
+                    prev = val;
+                    i += (int)rep;
+                }
+                if (e) break;
+                __syncthreads();
+                if (lens[256] == 0) {
+                    e = E_TABLE;
+                    break;
+                }
+            }
+            // fixed codes: literal/length lens[0..288), distance lens[288..318)
+            const uint8_t *dl = type == 1 ? lens + 288 : lens + hlit;
+            if (!build_table<10>(lens, hlit, ltab, lcnt, lsym, tfirst, toffs) ||
+                !build_table<10>(dl, hdist, dtab, dcnt, dsym, tfirst, toffs)) {
+                e = E_TABLE;
+                break;
+            }
+            for (;;) {
+                int s = decode_sym<10>(br, ltab, lcnt, lsym);
+                if (s < 0) {
+                    e = E_CODE;
+                    break;
+                }
+                if (s < 256) {
+                    if (pos >= osz) {
+                        e = E_OVERRUN;
+                        break;
+                    }
+                    if (lane == 0) o[pos] = (uint8_t)s;
+                    ++pos;
+                    continue;
+                }
+                if (s == 256) break;
+                s -= 257;
+                if (s >= 29) {
+                    e = E_LEN;
+                    break;
+                }
+                const uint32_t L = kLBase[s] + br.get(kLExt[s]);
+                const int ds = decode_sym<10>(br, dtab, dcnt, dsym);
+                if (ds < 0 || ds >= 30) {
+                    e = E_DIST;
+                    break;
+                }
+                const uint32_t D = kDBase[ds] + br.get(kDExt[ds]);
+                if (D > pos || pos + L > osz) {
+                    e = E_FAR;
+                    break;
+                }
+                // this wave's earlier byte stores must be visible to the loads below
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                for (uint32_t i = lane; i < L; i += 64) o[pos + i] = o[pos - D + (D >= L ? i : i % D)];
+                pos += L;
+            }
+            if (e) break;
+        } else {
+            e = E_TYPE;
+            break;
+        }
+        if (br.pos > end_bit) {
+            e = E_PAST;
+            break;
+        }
+        if (h & 1) break;
+    }
+    if (!e && pos != osz) e = E_SIZE;
+    if (e && lane == 0) report(err, e, b);
+}
+
+__global__ void __launch_bounds__(512) k_crc_check(const uint8_t *__restrict__ out, const uint64_t *__restrict__ uoff,
+                                                   const uint32_t *__restrict__ crc, const uint32_t *__restrict__ zpow,
+                                                   uint32_t *__restrict__ err) {
+    __shared__ uint32_t in[kSlot / 4 + 4];
+    __shared__ uint32_t crctab[4][256];
+    __shared__ uint32_t zp[17][32];
+    __shared__ uint32_t crcs[512];
+    const int t = threadIdx.x;
+    const uint64_t b = blockIdx.x;
+    const uint32_t len = (uint32_t)(uoff[b + 1] - uoff[b]);
+    if (len > kSlot) {
+        if (t == 0) report(err, E_SIZE, b);
+        return;
+    }
+    stage_words<512>(in, out + uoff[b], len, t);
+    crc_setup<512>(crctab, zp, zpow, t);
+    __syncthreads();
+    const uint32_t c = crc_window512(in, len, crctab, zp, crcs, t);
+    if (t == 0 && c != crc[b]) report(err, E_CRC, b);
+}
+
+// ------------------------------------------------------------------------------ record boundaries
+__device__ __forceinline__ uint32_t rd32u(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// the reader's plausibility test for a record start (bamio.cpp plausible_record)
+__device__ bool plausible(const uint8_t *d, uint64_t s, uint64_t n, int32_t n_ref) {
+    if (s + 36 > n) return false;
+    const uint32_t bs = rd32u(d + s);
+    if (bs < 32 || bs > 10000 || s + 4 + bs > n) return false;
+    const int32_t ref = (int32_t)rd32u(d + s + 4), mref = (int32_t)rd32u(d + s + 24);
+    if (ref < -1 || ref >= n_ref || mref < -1 || mref >= n_ref) return false;
+    const uint32_t lname = d[s + 12], nc = d[s + 16] | (d[s + 17] << 8), lseq = rd32u(d + s + 20);
+    if (lname == 0 || d[s + 36 + lname - 1] != 0) return false;
+    return 32ull + lname + 4ull * nc + (lseq + 1ull) / 2 + lseq <= bs;
+}
+
+constexpr uint64_t kNone = ~0ull;
+
+// chunk c covers [p + c*CH, min(n, p + (c+1)*CH)); guess its first record start
+__global__ void k_rec_guess(const uint8_t *__restrict__ d, uint64_t p, uint64_t n, int32_t n_ref, uint64_t CH, uint64_t C,
+                            uint64_t *__restrict__ start) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    if (c == 0) {
+        start[0] = p;
+        return;
+    }
+    const uint64_t cut = p + c * CH, lim = min(n, cut + 20016);
+    for (uint64_t s = cut; s < lim; ++s) {
+        uint64_t q = s;
+        int k = 0;
+        for (; k < 16 && q < n && plausible(d, q, n, n_ref); ++k) q += 4 + rd32u(d + q);
+        if (k == 16 || (q == n && k > 0)) {
+            start[c] = s;
+            return;
+        }
+    }
+    start[c] = kNone;
+}
+
+// walk chunk c from start[c] to the first record start at or past the chunk end; with out != NULL
+// also write the (absolute) offsets from pos[c]
+__global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t n, uint64_t CH, uint64_t C,
+                           const uint64_t *__restrict__ start, uint64_t *__restrict__ stop, uint64_t *__restrict__ count,
+                           const uint64_t *__restrict__ pos, uint64_t *__restrict__ out) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const uint64_t end = min(n, p + (c + 1) * CH);
+    uint64_t q = start[c], k = 0;
+    if (q == kNone) {
+        stop[c] = kNone;
+        count[c] = 0;
+        return;
+    }
+    uint64_t *o = out ? out + pos[c] : nullptr;
+    while (q < end) {
+        if (q + 4 > n) break;
+        const uint32_t bs = rd32u(d + q);
+        if (bs < 32 || bs > 10000 || q + 4 + bs > n) break;
+        if (o) o[k] = q;
+        ++k;
+        q += 4 + bs;
+    }
+    stop[c] = q < end ? kNone - 1 : q;  // kNone - 1: invalid record inside the chunk
+    count[c] = k;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------ host side
+static inline uint16_t rd16h(const uint8_t *p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static inline uint32_t rd32h(const uint8_t *p) { return (uint32_t)p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
+
+extern "C" int oge_bgzf_index(const uint8_t *z, uint64_t zbytes, uint64_t *d0, uint64_t *d1, uint64_t *uoff, uint32_t *crc,
+                              uint64_t cap, uint64_t *nblk) {
+    if (!nblk || (zbytes && !z)) return oge_fail(nullptr, OGE_ERR_ARG, "null argument");
+    uint64_t p = 0, k = 0, total = 0;
+    while (p < zbytes) {
+        if (zbytes - p < 18 || z[p] != 31 || z[p + 1] != 139 || z[p + 2] != 8 || !(z[p + 3] & 4))
+            return oge_fail(nullptr, OGE_ERR_IO, "not a BGZF stream or truncated block header");
+        if (z[p + 3] & ~4u) return oge_fail(nullptr, OGE_ERR_IO, "unsupported gzip header flags in a BGZF block");
+        const uint16_t xlen = rd16h(z + p + 10);
+        uint64_t x = p + 12, xend = x + xlen, bsize = 0;
+        if (xend > zbytes) return oge_fail(nullptr, OGE_ERR_IO, "truncated BGZF extra field");
+        while (x + 4 <= xend) {
+            const uint16_t slen = rd16h(z + x + 2);
+            if (z[x] == 'B' && z[x + 1] == 'C' && slen == 2) bsize = (uint64_t)rd16h(z + x + 4) + 1;
+            x += 4 + slen;
+        }
+        if (!bsize) return oge_fail(nullptr, OGE_ERR_IO, "BGZF block without BC field");
+        if (p + bsize > zbytes || bsize < xend - p + 8) return oge_fail(nullptr, OGE_ERR_IO, "truncated BGZF block");
+        const uint32_t isize = rd32h(z + p + bsize - 4);
+        if (isize > kSlot) return oge_fail(nullptr, OGE_ERR_IO, "BGZF block payload larger than 64 KiB");
+        if (isize) {
+            if (k < cap) {
+                if (d0) d0[k] = xend;
+                if (d1) d1[k] = p + bsize - 8;
+                if (uoff) uoff[k] = total;
+                if (crc) crc[k] = rd32h(z + p + bsize - 8);
+            }
+            ++k;
+            total += isize;
+        }
+        p += bsize;
+    }
+    if (k <= cap && uoff) uoff[k] = total;
+    *nblk = k;
+    return k <= cap ? OGE_OK : oge_fail(nullptr, OGE_ERR_ARG, "index capacity too small");
+}
+
+extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d_d0,
+                                    const uint64_t *d_d1, const uint64_t *d_uoff, const uint32_t *d_crc, uint64_t nblk,
+                                    uint8_t *d_out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if (nblk && (!d_z || !d_d0 || !d_d1 || !d_uoff || !d_out)) return oge_fail(ctx, OGE_ERR_ARG, "null buffer");
+    if ((uintptr_t)d_z & 3) return oge_fail(ctx, OGE_ERR_ARG, "d_z must be 4-byte aligned");
+    hipSetDevice(ctx->device);
+    ctx->reset_timing();
+    if (!nblk) return OGE_OK;
+    uint32_t *err = (uint32_t *)ctx->ws("infl_err", 16);
+    uint32_t *zpow = (uint32_t *)ctx->ws("infl_zpow", 17 * 32 * 4);
+    if (!err || !zpow) return OGE_ERR_HIP;
+    static uint32_t zh[17][32];
+    static bool zinit = false;
+    if (!zinit) crc_zpow(zh), zinit = true;
+    const uint32_t init[2] = {0, 0xffffffffu};
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(err, init, 8, hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, zh, sizeof(zh), hipMemcpyHostToDevice, ctx->stream));
+    OgeStageTimer *tm = ctx->begin_stage("bgzf_inflate");
+    for (uint64_t b0 = 0; b0 < nblk; b0 += (1u << 30)) {
+        const uint32_t nb = (uint32_t)std::min<uint64_t>(nblk - b0, 1u << 30);
+        k_inflate<<<nb, 64, 0, ctx->stream>>>(d_z, zbytes, d_d0 + b0, d_d1 + b0, d_uoff + b0, d_out, err);
+        OGE_LAUNCH_CHECK(ctx);
+    }
+    ctx->end_stage(tm);
+    if (d_crc) {
+        OgeStageTimer *tc = ctx->begin_stage("bgzf_crc");
+        for (uint64_t b0 = 0; b0 < nblk; b0 += (1u << 30)) {
+            const uint32_t nb = (uint32_t)std::min<uint64_t>(nblk - b0, 1u << 30);
+            k_crc_check<<<nb, 512, 0, ctx->stream>>>(d_out, d_uoff + b0, d_crc + b0, zpow, err);
+            OGE_LAUNCH_CHECK(ctx);
+        }
+        ctx->end_stage(tc);
+    }
+    uint32_t got[2];
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(got, err, 8, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (got[0]) {
+        char msg[160];
+        snprintf(msg, sizeof msg, "BGZF block %u failed to inflate (%s; error bits 0x%x)", got[1],
+                 (got[0] >> E_CRC) & 1 ? "CRC mismatch" : "corrupt deflate data", got[0]);
+        return oge_fail(ctx, OGE_ERR_IO, msg);
+    }
+    return OGE_OK;
+}
+
+extern "C" int oge_bgzf_inflate(oge_ctx *ctx, const uint8_t *z, uint64_t zbytes, uint8_t *out, uint64_t out_cap,
+                                uint64_t *out_bytes) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if (!out_bytes) return oge_fail(ctx, OGE_ERR_ARG, "null out_bytes");
+    hipSetDevice(ctx->device);
+    *out_bytes = 0;
+    uint64_t nb = 0;
+    int rc = oge_bgzf_index(z, zbytes, nullptr, nullptr, nullptr, nullptr, 0, &nb);
+    if (rc != OGE_OK && rc != OGE_ERR_ARG) return oge_fail(ctx, rc, oge_last_error(nullptr));
+    std::vector<uint64_t> d0(nb), d1(nb), uo(nb + 1);
+    std::vector<uint32_t> crc(nb);
+    rc = oge_bgzf_index(z, zbytes, d0.data(), d1.data(), uo.data(), crc.data(), nb, &nb);
+    if (rc) return oge_fail(ctx, rc, oge_last_error(nullptr));
+    const uint64_t total = uo[nb];
+    if (total > out_cap) return oge_fail(ctx, OGE_ERR_ARG, "out_cap too small for the decompressed stream");
+    if (!nb) return OGE_OK;
+    uint8_t *dz = (uint8_t *)ctx->ws("infl_hz", zbytes + 16);
+    uint64_t *dd = (uint64_t *)ctx->ws("infl_hidx", (3 * nb + 1) * 8);
+    uint32_t *dc = (uint32_t *)ctx->ws("infl_hcrc", nb * 4);
+    uint8_t *dout = (uint8_t *)ctx->ws("infl_hout", total + 16);
+    if (!dz || !dd || !dc || !dout) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(dz, z, zbytes, hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(dd, d0.data(), nb * 8, hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(dd + nb, d1.data(), nb * 8, hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(dd + 2 * nb, uo.data(), (nb + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(dc, crc.data(), nb * 4, hipMemcpyHostToDevice, ctx->stream));
+    rc = oge_bgzf_inflate_dev(ctx, dz, zbytes, dd, dd + nb, dd + 2 * nb, dc, nb, dout);
+    if (rc) return rc;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *out_bytes = total;
+    return OGE_OK;
+}
+
+extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream, uint64_t rec_base, uint64_t end, int32_t n_ref,
+                                          uint64_t *d_off, uint64_t cap, uint64_t *n_out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if (!n_out || rec_base > end || (end > rec_base && !d_stream)) return oge_fail(ctx, OGE_ERR_ARG, "bad argument");
+    hipSetDevice(ctx->device);
+    *n_out = 0;
+    const uint64_t CH = 1ull << 16;
+    const uint64_t C = std::max<uint64_t>(1, (end - rec_base + CH - 1) / CH);
+    uint64_t *ws = (uint64_t *)ctx->ws("rec_walk", 4 * C * 8 + 64);
+    if (!ws) return OGE_ERR_HIP;
+    uint64_t *start = ws, *stop = ws + C, *count = ws + 2 * C, *pos = ws + 3 * C;
+    std::vector<uint64_t> hs(C), he(C), hc(C), hp(C);
+    if (end == rec_base) {
+        if (d_off && cap >= 1) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off, &end, 8, hipMemcpyHostToDevice, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return OGE_OK;
+    }
+    const uint32_t TB = 128, G = oge_ceil_div(C, TB);
+    k_rec_guess<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, n_ref, CH, C, start);
+    OGE_LAUNCH_CHECK(ctx);
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(hs.data(), start, C * 8, hipMemcpyDeviceToHost, ctx->stream));
+    // walk, then make every chunk start where its predecessor's walk stopped, until consistent
+    for (int it = 0;; ++it) {
+        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, nullptr, nullptr);
+        OGE_LAUNCH_CHECK(ctx);
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(he.data(), stop, C * 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(hc.data(), count, C * 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        bool changed = false;
+        for (uint64_t c = 0; c + 1 < C; ++c) {
+            if (he[c] >= kNone - 1) break;  // the chain broke before here: fixed on a later pass
+            if (hs[c + 1] != he[c]) hs[c + 1] = he[c], changed = true;
+        }
+        // the chain from chunk 0 is exact up to the first chunk whose start was not yet verified
+        if (!changed) break;
+        if (it > 64) return oge_fail(ctx, OGE_ERR_IO, "BAM record walk did not converge (corrupt stream?)");
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(start, hs.data(), C * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    for (uint64_t c = 0; c < C; ++c) {
+        const bool last = c + 1 == C;
+        if (he[c] >= kNone - 1 || (last && he[c] != end) || (!last && he[c] != hs[c + 1]))
+            return oge_fail(ctx, OGE_ERR_IO,
+                            "Invalid BAM record (block size out of range or record past the end of the stream)");
+    }
+    uint64_t n = 0;
+    for (uint64_t c = 0; c < C; ++c) hp[c] = n, n += hc[c];
+    *n_out = n;
+    if (!d_off) return OGE_OK;
+    if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(pos, hp.data(), C * 8, hipMemcpyHostToDevice, ctx->stream));
+    k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos, d_off);
+    OGE_LAUNCH_CHECK(ctx);
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &end, 8, hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return OGE_OK;
+}

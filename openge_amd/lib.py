@@ -208,6 +208,10 @@ def lib() -> C.CDLL:
         "oge_bgzf_deflate_dev": (C.c_int, [vp, vp, u64, C.c_int, vp, u64, C.POINTER(u64)]),
         "oge_bgzf_deflate": (C.c_int, [vp, vp, u64, C.c_int, vp, u64, C.POINTER(u64)]),
         "oge_fix_bins_dev": (C.c_int, [vp, vp, vp, u64]),
+        "oge_bgzf_index": (C.c_int, [vp, u64, vp, vp, vp, vp, u64, C.POINTER(u64)]),
+        "oge_bgzf_inflate_dev": (C.c_int, [vp, vp, u64, vp, vp, vp, vp, u64, vp]),
+        "oge_bgzf_inflate": (C.c_int, [vp, vp, u64, vp, u64, C.POINTER(u64)]),
+        "oge_bam_record_offsets_dev": (C.c_int, [vp, vp, u64, u64, i32, vp, u64, C.POINTER(u64)]),
         "oge_drop_flagged_dev": (C.c_int, [vp, vp, vp, u64, C.c_uint16, vp, vp, C.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
@@ -413,6 +417,25 @@ class Context:
         got = C.c_uint64()
         check(lib().oge_bgzf_deflate_dev(self.h, d_src, n, level, d_dst, dst_cap, C.byref(got)), self.h)
         return got.value
+
+    def bgzf_inflate(self, z: bytes, out_cap: int | None = None) -> bytes:
+        """Decompress a BGZF stream on the device (host buffers in and out)."""
+        a = np.frombuffer(z, dtype=np.uint8)
+        nb = C.c_uint64()
+        lib().oge_bgzf_index(_ptr(a), len(a), None, None, None, None, 0, C.byref(nb))
+        uo = np.zeros(nb.value + 1, dtype=np.uint64)
+        if nb.value:
+            check(lib().oge_bgzf_index(_ptr(a), len(a), None, None, _ptr(uo), None, nb.value, C.byref(nb)))
+        cap = int(uo[-1]) if out_cap is None else out_cap
+        out = np.empty(max(cap, 1), dtype=np.uint8)
+        got = C.c_uint64()
+        check(lib().oge_bgzf_inflate(self.h, _ptr(a), len(a), _ptr(out), cap, C.byref(got)), self.h)
+        return out[:got.value].tobytes()
+
+    def record_offsets_dev(self, d_stream, rec_base: int, end: int, n_ref: int, d_off=None, cap: int = 0) -> int:
+        n = C.c_uint64()
+        check(lib().oge_bam_record_offsets_dev(self.h, d_stream, rec_base, end, n_ref, d_off, cap, C.byref(n)), self.h)
+        return n.value
 
     def fix_bins_dev(self, d_recs, d_off, n: int) -> None:
         check(lib().oge_fix_bins_dev(self.h, d_recs, d_off, n), self.h)
