@@ -10,8 +10,10 @@
 //                          computes the same symbol), so its state lives in scalar registers; the
 //                          compressed bits stream through two VGPRs (256 bytes each, lane l holding
 //                          word l) read with v_readlane, decode tables (10-bit direct lookup + the
-//                          canonical count/offset walk for longer codes) sit in LDS, literals are
-//                          stored by lane 0 and back-references copied by all 64 lanes at once.
+//                          canonical count/offset walk for longer codes) sit in LDS.  Output goes
+//                          through a 4 KiB LDS ring (literals written by lane 0, back-references
+//                          copied by all 64 lanes at once) flushed to HBM 256 bytes at a time;
+//                          only references further back than the ring read HBM.
 //   k_crc_check            one 512-thread workgroup per block: the payload staged in LDS, slice-by-4
 //                          CRC-32 combined across threads; any mismatch fails the call.
 //   k_rec_walk             BAM record boundaries: one thread per 64 KiB chunk walks the block_size
@@ -41,37 +43,57 @@ __constant__ uint16_t kDBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   1
 __constant__ uint8_t kDExt[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t kClOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// Wave-uniform LSB-first bit reader over the compressed bytes.
+// Wave-uniform LSB-first bit reader over the compressed bytes: a 64-bit scalar bit buffer refilled
+// 32 bits at a time (v_readlane) from two 256-byte chunks held one word per lane.  All state is
+// wave-uniform and kept in SGPRs (table entries are readfirstlane'd), which keeps the per-symbol path
+// to a few scalar instructions.
 struct Bits {
     const uint32_t *zw;
     uint64_t zwords;
-    uint64_t base;  // word index held by lane 0 of `cur`
-    uint64_t pos;   // absolute bit position
+    uint64_t wbase;  // absolute word index of relative word 0
+    uint32_t widx;   // next relative word to enter the buffer
+    uint32_t cbase;  // relative word held by lane 0 of `cur`
     uint32_t cur, nxt;
-    __device__ __forceinline__ uint32_t ldw(uint64_t w) const { return w < zwords ? zw[w] : 0u; }
-    __device__ void seek(uint64_t bit) {
-        pos = bit;
-        base = bit >> 5;
-        const int l = threadIdx.x & 63;
-        cur = ldw(base + l);
-        nxt = ldw(base + 64 + l);
+    uint64_t buf;    // low `cnt` bits are the next bits of the stream
+    uint32_t cnt;
+    __device__ __forceinline__ uint32_t ldw(uint32_t rel) const {
+        const uint64_t w = wbase + rel;
+        return w < zwords ? zw[w] : 0u;
     }
-    __device__ __forceinline__ uint32_t peek() const {
-        const uint32_t rel = (uint32_t)((pos >> 5) - base);
-        const uint32_t lo = __builtin_amdgcn_readlane(rel < 64 ? cur : nxt, rel & 63);
-        const uint32_t hi = __builtin_amdgcn_readlane(rel + 1 < 64 ? cur : nxt, (rel + 1) & 63);
-        return (uint32_t)((((uint64_t)hi << 32) | lo) >> (pos & 31));
-    }
-    __device__ __forceinline__ void skip(uint32_t n) {  // n <= 32
-        pos += n;
-        if ((pos >> 5) - base >= 64) {
-            cur = nxt;
-            base += 64;
-            nxt = ldw(base + 64 + (threadIdx.x & 63));
+    __device__ __forceinline__ void refill() {
+        while (cnt <= 32) {
+            const uint32_t r = widx - cbase;
+            const uint32_t w = __builtin_amdgcn_readlane(r < 64 ? cur : nxt, r & 63);
+            buf |= (uint64_t)w << cnt;
+            cnt += 32;
+            ++widx;
+            if (widx - cbase >= 64) {
+                cur = nxt;
+                cbase += 64;
+                nxt = ldw(cbase + 64 + (threadIdx.x & 63));
+            }
         }
     }
+    __device__ void seek(uint64_t bit) {
+        wbase = bit >> 5;
+        widx = cbase = 0;
+        const uint32_t l = threadIdx.x & 63;
+        cur = ldw(l);
+        nxt = ldw(64 + l);
+        buf = 0;
+        cnt = 0;
+        refill();
+        skip((uint32_t)(bit & 31));
+    }
+    __device__ __forceinline__ uint64_t bitpos() const { return (wbase + widx) * 32 - cnt; }
+    __device__ __forceinline__ uint32_t peek() const { return (uint32_t)buf; }
+    __device__ __forceinline__ void skip(uint32_t n) {  // n <= 32
+        buf >>= n;
+        cnt -= n;
+        if (cnt <= 32) refill();
+    }
     __device__ __forceinline__ uint32_t get(uint32_t n) {  // n <= 31
-        const uint32_t v = n ? peek() & ((1u << n) - 1) : 0u;
+        const uint32_t v = (uint32_t)buf & ((1u << n) - 1);
         skip(n);
         return v;
     }
@@ -144,7 +166,7 @@ __device__ bool build_table(const uint8_t *lens, int n, uint16_t *tab, uint32_t 
 template <int TB>
 __device__ __forceinline__ int decode_sym(Bits &br, const uint16_t *tab, const uint32_t *cnt, const uint16_t *sym) {
     const uint32_t v = br.peek();
-    const uint32_t e = tab[v & ((1u << TB) - 1)];
+    const uint32_t e = __builtin_amdgcn_readfirstlane(tab[v & ((1u << TB) - 1)]);
     if (e) {
         br.skip(e >> 9);
         return (int)(e & 511);
@@ -152,10 +174,10 @@ __device__ __forceinline__ int decode_sym(Bits &br, const uint16_t *tab, const u
     int code = 0, first = 0, index = 0;
     for (int len = 1; len <= 15; ++len) {
         code |= (int)((v >> (len - 1)) & 1);
-        const int count = (int)cnt[len];
+        const int count = (int)__builtin_amdgcn_readfirstlane(cnt[len]);
         if (code - count < first) {
             br.skip(len);
-            return sym[index + (code - first)];
+            return (int)__builtin_amdgcn_readfirstlane(sym[index + (code - first)]);
         }
         index += count;
         first += count;
@@ -164,6 +186,8 @@ __device__ __forceinline__ int decode_sym(Bits &br, const uint16_t *tab, const u
     }
     return -1;
 }
+
+constexpr uint32_t kRing = 4096;
 
 enum { E_STORED = 1, E_CODE = 2, E_OVERRUN = 3, E_LEN = 4, E_DIST = 5, E_FAR = 6, E_TYPE = 7, E_PAST = 8, E_SIZE = 9,
        E_TABLE = 10, E_CRC = 11 };
@@ -180,6 +204,8 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ z, u
     __shared__ uint32_t lcnt[16], dcnt[16], ccnt[16], tfirst[16], toffs[16];
     __shared__ uint16_t lsym[288], dsym[32], csym[19];
     __shared__ uint8_t lens[320], cl[19];
+    // the most recent kRing output bytes; whole 256-byte chunks are flushed to `o` by the wave
+    __shared__ uint8_t ring[kRing];
     const int lane = threadIdx.x;
     const uint64_t b = blockIdx.x;
     Bits br;
@@ -189,22 +215,33 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ z, u
     const uint64_t end_bit = d1[b] * 8;
     uint8_t *o = out + uoff[b];
     const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
-    uint32_t pos = 0;
+    uint32_t pos = 0, flushed = 0;
     int e = 0;
+    auto flush = [&](uint32_t upto) {  // ring bytes [flushed, upto) -> o (byte stores, 64 lanes)
+        for (uint32_t q0 = flushed; q0 < upto; q0 += 64) {  // uniform trip count keeps pos/flushed scalar
+            const uint32_t q = q0 + lane;
+            if (q < upto) o[q] = ring[q & (kRing - 1)];
+        }
+        flushed = upto;
+    };
     for (;;) {
         const uint32_t h = br.get(3);
         const uint32_t type = h >> 1;
         if (type == 0) {
-            br.skip((8 - (uint32_t)(br.pos & 7)) & 7);
+            br.skip((8 - (uint32_t)(br.bitpos() & 7)) & 7);
             const uint32_t len = br.get(16), nlen = br.get(16);
-            const uint64_t src = br.pos >> 3;
+            const uint64_t src = br.bitpos() >> 3;
             if ((len ^ 0xffffu) != nlen || pos + len > osz || src + len > d1[b]) {
                 e = E_STORED;
                 break;
             }
-            for (uint32_t i = lane; i < len; i += 64) o[pos + i] = z[src + i];
-            pos += len;
-            br.seek(br.pos + (uint64_t)len * 8);
+            for (uint32_t i = 0; i < len; i += 64) {
+                const uint32_t m = min(64u, len - i);
+                if ((uint32_t)lane < m) ring[(pos + lane) & (kRing - 1)] = z[src + i + lane];
+                pos += m;
+                if (pos - flushed >= 256) flush(pos & ~255u);
+            }
+            br.seek(br.bitpos() + (uint64_t)len * 8);
         } else if (type == 1 || type == 2) {
             int hlit = 288, hdist = 30;
             if (type == 1) {
@@ -283,6 +320,8 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ z, u
                 break;
             }
             for (;;) {
+                pos = __builtin_amdgcn_readfirstlane(pos);
+                flushed = __builtin_amdgcn_readfirstlane(flushed);
                 int s = decode_sym<10>(br, ltab, lcnt, lsym);
                 if (s < 0) {
                     e = E_CODE;
@@ -293,8 +332,9 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ z, u
                         e = E_OVERRUN;
                         break;
                     }
-                    if (lane == 0) o[pos] = (uint8_t)s;
+                    ring[pos & (kRing - 1)] = (uint8_t)s;  // every lane stores the same byte
                     ++pos;
+                    if (pos - flushed >= 256) flush(pos & ~255u);
                     continue;
                 }
                 if (s == 256) break;
@@ -314,23 +354,36 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ z, u
                     e = E_FAR;
                     break;
                 }
-                // this wave's earlier byte stores must be visible to the loads below
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-                for (uint32_t i = lane; i < L; i += 64) o[pos + i] = o[pos - D + (D >= L ? i : i % D)];
+                if (D <= kRing - 1024) {  // source still in the ring (flushed >= pos - 255 - 258)
+                    for (uint32_t i = 0; i < L; i += 64) {
+                        const uint32_t j = i + lane;
+                        uint8_t v = 0;
+                        if (j < L) v = ring[(pos - D + (D >= L ? j : j % D)) & (kRing - 1)];
+                        if (j < L) ring[(pos + j) & (kRing - 1)] = v;
+                    }
+                } else {  // far source: flushed to `o`; make this wave's stores visible first
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                    for (uint32_t i = 0; i < L; i += 64) {
+                        const uint32_t j = i + lane;
+                        if (j < L) ring[(pos + j) & (kRing - 1)] = o[pos - D + j];
+                    }
+                }
                 pos += L;
+                if (pos - flushed >= 256) flush(pos & ~255u);
             }
             if (e) break;
         } else {
             e = E_TYPE;
             break;
         }
-        if (br.pos > end_bit) {
+        if (br.bitpos() > end_bit) {
             e = E_PAST;
             break;
         }
         if (h & 1) break;
     }
     if (!e && pos != osz) e = E_SIZE;
+    if (!e) flush(pos);
     if (e && lane == 0) report(err, e, b);
 }
 

@@ -42,6 +42,30 @@ def main():
         wall.append(time.perf_counter() - t0)
         ms.append(ctx.timing("bgzf_deflate"))
     ms, wall = ms[1:], wall[1:]
+    # inflate the same stream back on the device (index on the host, as the reader does)
+    import ctypes as C
+    zh = d_z[:zb].cpu().numpy()
+    nb = C.c_uint64()
+    L.lib().oge_bgzf_index(zh.ctypes.data, zb, None, None, None, None, 0, C.byref(nb))
+    idx = np.zeros(3 * nb.value + 1, dtype=np.uint64)
+    crc = np.zeros(nb.value, dtype=np.uint32)
+    i0 = idx.ctypes.data
+    L.check(L.lib().oge_bgzf_index(zh.ctypes.data, zb, i0, i0 + 8 * nb.value, i0 + 16 * nb.value, crc.ctypes.data,
+                                   nb.value, C.byref(nb)))
+    d_idx = torch.from_numpy(idx.view(np.int64)).to(dev)
+    d_crc = torch.from_numpy(crc.view(np.int32)).to(dev)
+    d_back = torch.empty(B + 64, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    inf_ms, crc_ms = [], []
+    k = nb.value
+    for _ in range(reps + 1):
+        p0 = d_idx.data_ptr()
+        L.check(L.lib().oge_bgzf_inflate_dev(ctx.h, d_z.data_ptr(), zb, p0, p0 + 8 * k, p0 + 16 * k, d_crc.data_ptr(), k,
+                                             d_back.data_ptr()), ctx.h)
+        inf_ms.append(ctx.timing("bgzf_inflate"))
+        crc_ms.append(ctx.timing("bgzf_crc"))
+    inf_ms, crc_ms = inf_ms[1:], crc_ms[1:]
+    assert torch.equal(d_back[:B], d_recs[:B])
     sample = d_recs[: min(B, 64 << 20)].cpu().numpy().tobytes()
     host = sum(len(zlib.compress(sample[i:i + 65280], 6)) + 26 for i in range(0, len(sample), 65280))
     print(json.dumps({
@@ -49,6 +73,8 @@ def main():
         "zlib6_ratio_sample": round(host / len(sample), 4),
         "ms": [round(x, 2) for x in ms], "wall_s": [round(x, 3) for x in wall],
         "GBps": round(B / (min(ms) * 1e-3) / 1e9, 1),
+        "inflate_ms": [round(x, 2) for x in inf_ms], "crc_ms": [round(x, 2) for x in crc_ms],
+        "inflate_GBps": round(B / ((min(inf_ms) + min(crc_ms)) * 1e-3) / 1e9, 1),
     }), flush=True)
     ctx.close()
 
