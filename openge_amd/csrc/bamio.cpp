@@ -476,10 +476,7 @@ static bool parse_offsets_parallel(const uint8_t *d, size_t p, size_t n, int32_t
     return true;
 }
 
-bool bam_parse(bytevec &&raw, BamFile &out, std::string &err, int threads) {
-    out.data = std::move(raw);
-    const uint8_t *d = out.data.data();
-    size_t n = out.data.size();
+bool bam_parse_header(const uint8_t *d, size_t n, BamFile &out, std::string &err, size_t *rec_base) {
     if (n < 12 || memcmp(d, "BAM\1", 4) != 0) { err = "Error reading BAM stream header magic bytes."; return false; }
     uint32_t l_text = rd32(d + 4);
     if (8 + (size_t)l_text + 4 > n) { err = "Error reading BAM stream header text."; return false; }
@@ -506,6 +503,17 @@ bool bam_parse(bytevec &&raw, BamFile &out, std::string &err, int threads) {
         }
     }
     out.rec_base = p;
+    *rec_base = p;
+    return true;
+}
+
+bool bam_parse(bytevec &&raw, BamFile &out, std::string &err, int threads) {
+    out.data = std::move(raw);
+    const uint8_t *d = out.data.data();
+    size_t n = out.data.size();
+    size_t p = 0;
+    if (!bam_parse_header(d, n, out, err, &p)) return false;
+    uint32_t n_ref = (uint32_t)out.ref_names.size();
     out.offsets.clear();
     if (threads > 1 && n - p >= (64ull << 20) && parse_offsets_parallel(d, p, n, (int32_t)n_ref, threads, out.offsets))
         return true;
@@ -523,13 +531,10 @@ bool bam_parse(bytevec &&raw, BamFile &out, std::string &err, int threads) {
     return true;
 }
 
-bool bam_read_file(const std::string &path, BamFile &out, int threads, std::string &err) {
-    static const bool dbg = getenv("OGE_IO_DEBUG") != nullptr;
-    auto clk = [] { return std::chrono::steady_clock::now(); };
-    const auto t0 = clk();
+bool read_file_bytes(const std::string &path, bytevec &comp, int threads, std::string &err) {
     FILE *f = (path == "-" || path == "stdin") ? stdin : fopen(path.c_str(), "rb");
     if (!f) { err = "cannot open " + path; return false; }
-    bytevec comp;
+    comp.clear();
     if (f != stdin && fseeko(f, 0, SEEK_END) == 0) {  // regular file: parallel preads into a sized buffer
         off_t sz = ftello(f);
         comp.reserve(sz > 0 ? (size_t)sz : 0);
@@ -560,6 +565,15 @@ bool bam_read_file(const std::string &path, BamFile &out, int threads, std::stri
         while ((r = fread(buf, 1, sizeof(buf), f)) > 0) comp.insert(comp.end(), buf, buf + r);
     }
     if (f != stdin) fclose(f);
+    return true;
+}
+
+bool bam_read_file(const std::string &path, BamFile &out, int threads, std::string &err) {
+    static const bool dbg = getenv("OGE_IO_DEBUG") != nullptr;
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = clk();
+    bytevec comp;
+    if (!read_file_bytes(path, comp, threads, err)) return false;
     const auto t1 = clk();
     bytevec raw;
     if (!bgzf_inflate_all(comp.data(), comp.size(), raw, threads, err)) return false;

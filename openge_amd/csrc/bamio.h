@@ -89,6 +89,10 @@ bool bam_read_file(const std::string &path, BamFile &out, int threads, std::stri
 // madvise(MADV_HUGEPAGE) over a large buffer before its first touch
 void want_huge_pages(void *p, size_t n);
 bool bam_parse(bytevec &&raw, BamFile &out, std::string &err, int threads = 1);
+// The whole file (parallel pread for regular files).
+bool read_file_bytes(const std::string &path, bytevec &comp, int threads, std::string &err);
+// Header text, @SQ / binary reference list of a decompressed stream prefix d[0, n) -> *rec_base.
+bool bam_parse_header(const uint8_t *d, size_t n, BamFile &out, std::string &err, size_t *rec_base);
 // Serialize header block (magic, text, reference list taken from the header @SQ lines, as
 // BamSerializer::open does at util/bam_serializer.h:54-76).
 std::vector<uint8_t> bam_encode_header(const BamHeaderModel &h);

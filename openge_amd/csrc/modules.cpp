@@ -84,9 +84,100 @@ int AlgorithmModule::runChain(ChainContext &cc) {
 }
 
 // ----------------------------------------------------------------------------------- FileReader
+int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &path) {
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
+        return std::chrono::duration<double>(z - a).count();
+    };
+    const auto t0 = clk();
+    const int threads = cc.threads > 0 ? cc.threads : 8;
+    bytevec comp;
+    std::string err;
+    if (!read_file_bytes(path, comp, threads, err)) {
+        fprintf(stderr, "openge: error reading %s: %s\n", path.c_str(), err.c_str());
+        return -1;
+    }
+    uint64_t nb = 0;
+    oge_bgzf_index(comp.data(), comp.size(), nullptr, nullptr, nullptr, nullptr, 0, &nb);
+    std::vector<uint64_t> idx(3 * nb + 1);
+    std::vector<uint32_t> crc(nb);
+    if (oge_bgzf_index(comp.data(), comp.size(), idx.data(), idx.data() + nb, idx.data() + 2 * nb, crc.data(), nb, &nb))
+        return 1;  // not BGZF / truncated: the host reader reports it
+    const uint64_t total = idx[3 * nb];
+    const auto t1 = clk();
+    void *dz = nullptr, *di = nullptr, *dc = nullptr, *dout = nullptr, *doff = nullptr;
+    auto release = [&]() {
+        for (void *p : {dz, di, dc, dout, doff})
+            if (p) oge_dev_free(cc.ctx, p);
+    };
+    if (oge_dev_alloc(cc.ctx, comp.size() + 16, &dz) || oge_dev_alloc(cc.ctx, idx.size() * 8, &di) ||
+        oge_dev_alloc(cc.ctx, crc.size() * 4 + 4, &dc) || oge_dev_alloc(cc.ctx, total + 64, &dout)) {
+        release();
+        return cc.fail("device allocation");
+    }
+    if (oge_memcpy(cc.ctx, dz, comp.data(), comp.size(), 1) || oge_memcpy(cc.ctx, di, idx.data(), idx.size() * 8, 1) ||
+        oge_memcpy(cc.ctx, dc, crc.data(), crc.size() * 4, 1)) {
+        release();
+        return cc.fail("host->device copy");
+    }
+    const auto t2 = clk();
+    const uint64_t *dd = (const uint64_t *)di;
+    if (nb && oge_bgzf_inflate_dev(cc.ctx, (const uint8_t *)dz, comp.size(), dd, dd + nb, dd + 2 * nb, (const uint32_t *)dc, nb,
+                                   (uint8_t *)dout)) {
+        release();
+        return 1;
+    }
+    oge_dev_free(cc.ctx, dz);
+    dz = nullptr;
+    comp = bytevec();
+    const auto t3 = clk();
+    // header from a prefix of the stream
+    BamFile f;
+    size_t rec_base = 0;
+    for (uint64_t pre = std::min<uint64_t>(total, 1 << 20);; pre = std::min<uint64_t>(total, pre * 8)) {
+        std::vector<uint8_t> h(pre);
+        if (pre && oge_memcpy(cc.ctx, h.data(), dout, pre, 2)) {
+            release();
+            return cc.fail("device->host copy");
+        }
+        f = BamFile();
+        if (bam_parse_header(h.data(), pre, f, err, &rec_base)) break;
+        if (pre == total) {
+            release();
+            return 1;
+        }
+    }
+    uint64_t n = 0;
+    if (oge_bam_record_offsets_dev(cc.ctx, (const uint8_t *)dout, rec_base, total, (int32_t)f.ref_names.size(), nullptr, 0, &n) ||
+        oge_dev_alloc(cc.ctx, (n + 1) * 8, &doff) ||
+        oge_bam_record_offsets_dev(cc.ctx, (const uint8_t *)dout, rec_base, total, (int32_t)f.ref_names.size(), (uint64_t *)doff,
+                                   n + 1, &n)) {
+        release();
+        return 1;
+    }
+    oge_dev_free(cc.ctx, di);
+    oge_dev_free(cc.ctx, dc);
+    b.header = f.header;
+    b.ref_names = f.ref_names;
+    b.n = n;
+    b.d_recs = (uint8_t *)dout;
+    b.d_offs = (uint64_t *)doff;
+    b.d_bytes = total;
+    b.dev_valid = true;
+    b.host_valid = false;
+    if (verbose_)
+        fprintf(stderr, "[openge] FileReader (device): file %.3f s, upload %.3f s, inflate %.3f s, records %.3f s\n", sec(t0, t1),
+                sec(t1, t2), sec(t2, t3), sec(t3, clk()));
+    return 0;
+}
+
 int FileReader::runInternal(ChainContext &cc, ReadBatch &b) {
-    (void)cc;
     if (files_.empty()) files_.push_back("stdin");
+    const char *rd = getenv("OGE_READER");
+    if (files_.size() == 1 && files_[0] != "stdin" && files_[0] != "-" && !(rd && std::string(rd) == "host")) {
+        const int r = read_device(cc, b, files_[0]);
+        if (r <= 0) return r;  // 1: fall through to the host reader (it reports format errors)
+    }
     for (size_t i = 0; i < files_.size(); ++i) {
         const std::string path = files_[i] == "stdin" ? "/dev/stdin" : files_[i];
         BamFile f;

@@ -81,6 +81,9 @@ public:
     void setLoadStringData(bool) {}  // the record arena always keeps the full record bytes
 protected:
     int runInternal(ChainContext &cc, ReadBatch &b) override;
+    // One BGZF file straight into HBM: inflate + record walk on the GPU (returns 1 when the host
+    // reader should take over, e.g. to report a format error with the reference's message).
+    int read_device(ChainContext &cc, ReadBatch &b, const std::string &path);
     std::vector<std::string> files_;
 };
 
