@@ -9,6 +9,7 @@
 #include <chrono>
 #include <unistd.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <cstring>
 #include <sstream>
 #include <thread>
@@ -271,7 +272,31 @@ void BgzfWriter::write_span(const uint8_t *data, size_t n) {
 void BgzfWriter::write_compressed(const uint8_t *z, size_t n) {
     flush_blocks(true);
     drain();
-    if (n) fwrite(z, 1, n, f_);
+    if (!n) return;
+    // regular files: parallel pwrite at the stream position (page-cache copies on all threads)
+    struct stat st;
+    fflush(f_);
+    const int fd = fileno(f_);
+    const off_t at = ftello(f_);
+    if (n >= (64ull << 20) && threads_ > 1 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && at >= 0) {
+        const size_t chunk = 32ull << 20, nch = (n + chunk - 1) / chunk;
+        std::atomic<bool> ok(true);
+        parallel_for(nch, threads_, [&](size_t c) {
+            size_t o = c * chunk;
+            const size_t e = std::min(n, o + chunk);
+            while (o < e) {
+                const ssize_t r = pwrite(fd, z + o, e - o, at + (off_t)o);
+                if (r <= 0) {
+                    ok = false;
+                    return;
+                }
+                o += (size_t)r;
+            }
+        });
+        if (ok && fseeko(f_, at + (off_t)n, SEEK_SET) == 0) return;
+        fseeko(f_, at, SEEK_SET);  // fall back to one sequential write
+    }
+    fwrite(z, 1, n, f_);
 }
 
 void BgzfWriter::close() {
