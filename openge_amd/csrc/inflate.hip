@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -354,14 +355,15 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ z, u
                     e = E_FAR;
                     break;
                 }
-                if (D <= kRing - 1024) {  // source still in the ring (flushed >= pos - 255 - 258)
+                if (D + 259 <= kRing) {  // the match cannot overwrite its own source slots
                     for (uint32_t i = 0; i < L; i += 64) {
                         const uint32_t j = i + lane;
                         uint8_t v = 0;
                         if (j < L) v = ring[(pos - D + (D >= L ? j : j % D)) & (kRing - 1)];
                         if (j < L) ring[(pos + j) & (kRing - 1)] = v;
                     }
-                } else {  // far source: flushed to `o`; make this wave's stores visible first
+                } else {  // far source: flush everything so far, then make the stores visible
+                    flush(pos);
                     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
                     for (uint32_t i = 0; i < L; i += 64) {
                         const uint32_t j = i + lane;
@@ -385,6 +387,351 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ z, u
     if (!e && pos != osz) e = E_SIZE;
     if (!e) flush(pos);
     if (e && lane == 0) report(err, e, b);
+}
+
+// ---------------------------------------------------------------- grouped (VALU) decoder
+// G lanes decode one block; a wave runs 64 / G blocks at once.  The decoder state is per lane
+// (uniform within the group), so it executes on the SIMD's vector ALU, four of which share the
+// CU's single scalar unit that bounds k_inflate.  Each group owns its decode tables and an R-byte
+// output ring in LDS; no workgroup barriers are used (one wave per workgroup, LDS is in order).
+template <int G, int R, int LTB, int DTB>
+struct GLds {
+    uint16_t ltab[1 << LTB];
+    uint16_t dtab[1 << DTB];
+    uint16_t ctab[128];
+    uint32_t lcnt[16], dcnt[16], ccnt[16];
+    uint16_t lsym[288], dsym[32], csym[20];
+    uint32_t aux[48];
+    uint8_t lens[320], cl[32];
+    uint8_t ring[R];
+};
+
+template <int G>
+struct GBits {
+    const uint32_t *zw;
+    uint64_t zwords;
+    uint64_t wbase;
+    uint32_t widx, cbase;
+    uint32_t cur, nxt;  // lane gl of the group holds words cbase + gl and cbase + G + gl
+    uint64_t buf;
+    uint32_t cnt;
+    uint32_t gl;
+    __device__ __forceinline__ uint32_t ldw(uint32_t rel) const {
+        const uint64_t w = wbase + rel;
+        return w < zwords ? zw[w] : 0u;
+    }
+    __device__ __forceinline__ void refill() {
+        while (cnt <= 32) {
+            const uint32_t r = widx - cbase;
+            const uint32_t w = (uint32_t)__shfl((int)(r < (uint32_t)G ? cur : nxt), (int)(r & (G - 1)), G);
+            buf |= (uint64_t)w << cnt;
+            cnt += 32;
+            ++widx;
+            if (widx - cbase >= (uint32_t)G) {
+                cur = nxt;
+                cbase += G;
+                nxt = ldw(cbase + G + gl);
+            }
+        }
+    }
+    __device__ void seek(uint64_t bit) {
+        wbase = bit >> 5;
+        widx = cbase = 0;
+        cur = ldw(gl);
+        nxt = ldw(G + gl);
+        buf = 0;
+        cnt = 0;
+        refill();
+        skip((uint32_t)(bit & 31));
+    }
+    __device__ __forceinline__ uint64_t bitpos() const { return (wbase + widx) * 32 - cnt; }
+    __device__ __forceinline__ void skip(uint32_t n) {
+        buf >>= n;
+        cnt -= n;
+        if (cnt <= 32) refill();
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t n) {
+        const uint32_t v = (uint32_t)buf & ((1u << n) - 1);
+        skip(n);
+        return v;
+    }
+};
+
+template <int G>
+__device__ __forceinline__ uint64_t gballot(bool p, uint32_t gbase) {
+    const uint64_t m = __ballot(p) >> gbase;
+    return G == 64 ? m : (m & ((1ull << G) - 1));
+}
+
+template <int G, int TB>
+__device__ bool gbuild(const uint8_t *lens, int n, uint16_t *tab, uint32_t *cnt, uint16_t *sym, uint32_t *aux, uint32_t gl,
+                       uint32_t gbase) {
+    // aux: 48 words of group scratch: first code [0,16), symbol offset [16,32), running rank [32,48).
+    // Per-length values live in LDS (lane gl holds length gl's count) to keep VGPR pressure low.
+    for (int i = gl; i < (1 << TB); i += G) tab[i] = 0;
+    uint32_t mine = 0;  // lane b (1..15): number of codes of length b
+    for (int c0 = 0; c0 < n; c0 += G) {
+        const int s = c0 + (int)gl;
+        const uint32_t L = s < n ? lens[s] : 0;
+        for (int b = 1; b < 16; ++b) {
+            const uint32_t c = __popcll(gballot<G>(L == (uint32_t)b, gbase));
+            if ((int)gl == b) mine += c;
+        }
+    }
+    for (uint32_t i = gl; i < 16; i += G) cnt[i] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (gl >= 1 && gl < 16) cnt[gl] = mine;
+    __builtin_amdgcn_wave_barrier();
+    int left = 1;
+    uint32_t code = 0, off = 0;
+    for (int b = 1; b < 16; ++b) {
+        const uint32_t t = cnt[b];
+        left = 2 * left - (int)t;
+        code = (code + (b > 1 ? cnt[b - 1] : 0)) << (b > 1 ? 1 : 0);
+        if ((int)gl == b) aux[b] = code, aux[16 + b] = off, aux[32 + b] = 0;
+        off += t;
+    }
+    if (left < 0) return false;
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t lt = (1ull << gl) - 1;
+    for (int c0 = 0; c0 < n; c0 += G) {
+        const int s = c0 + (int)gl;
+        const uint32_t L = s < n ? lens[s] : 0;
+        uint64_t my = 0;
+        uint32_t mc = 0;
+        for (int b = 1; b < 16; ++b) {
+            const uint64_t m = gballot<G>(L == (uint32_t)b, gbase);
+            if (L == (uint32_t)b) my = m;
+            if ((int)gl == b) mc = __popcll(m);
+        }
+        if (L) {
+            const uint32_t rank = aux[32 + L] + __popcll(my & lt);
+            sym[aux[16 + L] + rank] = (uint16_t)s;
+            if (L <= (uint32_t)TB) {
+                const uint32_t r = __builtin_bitreverse32(aux[L] + rank) >> (32 - L);
+                const uint16_t e = (uint16_t)(s | (L << 9));
+                for (uint32_t k = 0; k < (1u << (TB - L)); ++k) tab[r | (k << L)] = e;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (gl >= 1 && gl < 16) aux[32 + gl] += mc;
+        __builtin_amdgcn_wave_barrier();
+    }
+    __builtin_amdgcn_wave_barrier();
+    return true;
+}
+
+template <int G, int TB>
+__device__ __forceinline__ int gdecode(GBits<G> &br, const uint16_t *tab, const uint32_t *cnt, const uint16_t *sym) {
+    const uint32_t v = (uint32_t)br.buf;
+    const uint32_t e = tab[v & ((1u << TB) - 1)];
+    if (e) {
+        br.skip(e >> 9);
+        return (int)(e & 511);
+    }
+    int code = 0, first = 0, index = 0;
+    for (int len = 1; len <= 15; ++len) {
+        code |= (int)((v >> (len - 1)) & 1);
+        const int count = (int)cnt[len];
+        if (code - count < first) {
+            br.skip(len);
+            return sym[index + (code - first)];
+        }
+        index += count;
+        first += count;
+        first <<= 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+template <int G, int R, int LTB, int DTB>
+__global__ void __launch_bounds__(64) k_inflate_g(const uint8_t *__restrict__ z, uint64_t zbytes, const uint64_t *__restrict__ d0,
+                                                  const uint64_t *__restrict__ d1, const uint64_t *__restrict__ uoff, uint64_t nblk,
+                                                  uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
+    constexpr int NG = 64 / G;
+    __shared__ GLds<G, R, LTB, DTB> gs[NG];
+    const uint32_t lane = threadIdx.x, g = lane / G, gl = lane % G, gbase = g * G;
+    const uint64_t b = (uint64_t)blockIdx.x * NG + g;
+    if (b >= nblk) return;
+    GLds<G, R, LTB, DTB> &S = gs[g];
+    GBits<G> br;
+    br.gl = gl;
+    br.zw = (const uint32_t *)z;
+    br.zwords = (zbytes + 3) / 4;
+    br.seek(d0[b] * 8);
+    const uint64_t end_bit = d1[b] * 8;
+    uint8_t *o = out + uoff[b];
+    const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
+    uint32_t pos = 0, flushed = 0;
+    int e = 0;
+    auto flush = [&](uint32_t upto) {
+        for (uint32_t q0 = flushed; q0 < upto; q0 += G) {
+            const uint32_t q = q0 + gl;
+            if (q < upto) o[q] = S.ring[q & (R - 1)];
+        }
+        flushed = upto;
+    };
+    for (;;) {
+        const uint32_t h = br.get(3);
+        const uint32_t type = h >> 1;
+        if (type == 0) {
+            br.skip((8 - (uint32_t)(br.bitpos() & 7)) & 7);
+            const uint32_t len = br.get(16), nlen = br.get(16);
+            const uint64_t src = br.bitpos() >> 3;
+            if ((len ^ 0xffffu) != nlen || pos + len > osz || src + len > d1[b]) {
+                e = E_STORED;
+                break;
+            }
+            for (uint32_t i = 0; i < len; i += G) {
+                const uint32_t m = min((uint32_t)G, len - i);
+                if (gl < m) S.ring[(pos + gl) & (R - 1)] = z[src + i + gl];
+                pos += m;
+                if (pos - flushed >= 256) flush(pos & ~255u);
+            }
+            br.seek(br.bitpos() + (uint64_t)len * 8);
+        } else if (type == 1 || type == 2) {
+            int hlit = 288, hdist = 30;
+            if (type == 1) {
+                for (int s = gl; s < 318; s += G) S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+                __builtin_amdgcn_wave_barrier();
+            } else {
+                hlit = (int)br.get(5) + 257;
+                hdist = (int)br.get(5) + 1;
+                const int hclen = (int)br.get(4) + 4;
+                if (hlit > 286 || hdist > 30) {
+                    e = E_TABLE;
+                    break;
+                }
+                for (int i = gl; i < 19; i += G) S.cl[i] = 0;
+                __builtin_amdgcn_wave_barrier();
+                for (int i = 0; i < hclen; ++i) {
+                    const uint32_t v = br.get(3);
+                    S.cl[kClOrd[i]] = (uint8_t)v;  // every lane of the group stores the same byte
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (!gbuild<G, 7>(S.cl, 19, S.ctab, S.ccnt, S.csym, S.aux, gl, gbase)) {
+                    e = E_TABLE;
+                    break;
+                }
+                const int total = hlit + hdist;
+                int i = 0;
+                uint32_t prev = 0;
+                while (i < total) {
+                    const int sy = gdecode<G, 7>(br, S.ctab, S.ccnt, S.csym);
+                    if (sy < 0) {
+                        e = E_CODE;
+                        break;
+                    }
+                    if (sy < 16) {
+                        S.lens[i] = (uint8_t)sy;
+                        prev = (uint32_t)sy;
+                        ++i;
+                        continue;
+                    }
+                    uint32_t val = 0, rep;
+                    if (sy == 16) {
+                        if (i == 0) {
+                            e = E_TABLE;
+                            break;
+                        }
+                        val = prev;
+                        rep = 3 + br.get(2);
+                    } else if (sy == 17) {
+                        rep = 3 + br.get(3);
+                    } else {
+                        rep = 11 + br.get(7);
+                    }
+                    if (i + (int)rep > total) {
+                        e = E_TABLE;
+                        break;
+                    }
+                    for (uint32_t k = gl; k < rep; k += G) S.lens[i + k] = (uint8_t)val;
+                    prev = val;
+                    i += (int)rep;
+                }
+                if (e) break;
+                __builtin_amdgcn_wave_barrier();
+                if (S.lens[256] == 0) {
+                    e = E_TABLE;
+                    break;
+                }
+            }
+            const uint8_t *dl = type == 1 ? S.lens + 288 : S.lens + hlit;
+            if (!gbuild<G, LTB>(S.lens, hlit, S.ltab, S.lcnt, S.lsym, S.aux, gl, gbase) ||
+                !gbuild<G, DTB>(dl, hdist, S.dtab, S.dcnt, S.dsym, S.aux, gl, gbase)) {
+                e = E_TABLE;
+                break;
+            }
+            for (;;) {
+                int sy = gdecode<G, LTB>(br, S.ltab, S.lcnt, S.lsym);
+                if (sy < 0) {
+                    e = E_CODE;
+                    break;
+                }
+                if (sy < 256) {
+                    if (pos >= osz) {
+                        e = E_OVERRUN;
+                        break;
+                    }
+                    S.ring[pos & (R - 1)] = (uint8_t)sy;
+                    ++pos;
+                    if (pos - flushed >= 256) flush(pos & ~255u);
+                    continue;
+                }
+                if (sy == 256) break;
+                sy -= 257;
+                if (sy >= 29) {
+                    e = E_LEN;
+                    break;
+                }
+                const uint32_t L = kLBase[sy] + br.get(kLExt[sy]);
+                const int ds = gdecode<G, DTB>(br, S.dtab, S.dcnt, S.dsym);
+                if (ds < 0 || ds >= 30) {
+                    e = E_DIST;
+                    break;
+                }
+                const uint32_t D = kDBase[ds] + br.get(kDExt[ds]);
+                if (D > pos || pos + L > osz) {
+                    e = E_FAR;
+                    break;
+                }
+                // ring path iff the match cannot overwrite its own source slots (D + L <= R); a far
+                // source is read back from HBM after flushing everything written so far
+                if (D + 259 <= (uint32_t)R) {
+                    for (uint32_t i = 0; i < L; i += G) {
+                        const uint32_t j = i + gl;
+                        uint8_t v = 0;
+                        if (j < L) v = S.ring[(pos - D + (D >= L ? j : j % D)) & (R - 1)];
+                        __builtin_amdgcn_wave_barrier();
+                        if (j < L) S.ring[(pos + j) & (R - 1)] = v;
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                } else {
+                    flush(pos);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+                    for (uint32_t i = 0; i < L; i += G) {
+                        const uint32_t j = i + gl;
+                        if (j < L) S.ring[(pos + j) & (R - 1)] = o[pos - D + j];
+                    }
+                }
+                pos += L;
+                if (pos - flushed >= 256) flush(pos & ~255u);
+            }
+            if (e) break;
+        } else {
+            e = E_TYPE;
+            break;
+        }
+        if (br.bitpos() > end_bit) {
+            e = E_PAST;
+            break;
+        }
+        if (h & 1) break;
+    }
+    if (!e && pos != osz) e = E_SIZE;
+    if (!e) flush(pos);
+    if (e && gl == 0) report(err, e, b);
 }
 
 __global__ void __launch_bounds__(512) k_crc_check(const uint8_t *__restrict__ out, const uint64_t *__restrict__ uoff,
@@ -537,10 +884,23 @@ extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t z
     const uint32_t init[2] = {0, 0xffffffffu};
     OGE_HIP_TRY(ctx, hipMemcpyAsync(err, init, 8, hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, zh, sizeof(zh), hipMemcpyHostToDevice, ctx->stream));
+    // decoder: lanes per block -- 32 (default), 16, or 0 = the wave-uniform scalar decoder k_inflate.
+    // Measured on 20M C2 reads (5.68 GB): scalar 437 ms (bound by the CU's one scalar ALU), 32 lanes
+    // with a 1 KiB ring 254 ms, 16 lanes 268-296 ms (divergence between the wave's groups); larger
+    // rings or tables cost occupancy and were slower (2 KiB 327 ms, 8 KiB 591 ms).
+    static const int inflate_group = [] {
+        const char *v = getenv("OGE_INFLATE_GROUP");
+        return v && *v ? atoi(v) : 32;
+    }();
     OgeStageTimer *tm = ctx->begin_stage("bgzf_inflate");
     for (uint64_t b0 = 0; b0 < nblk; b0 += (1u << 30)) {
         const uint32_t nb = (uint32_t)std::min<uint64_t>(nblk - b0, 1u << 30);
-        k_inflate<<<nb, 64, 0, ctx->stream>>>(d_z, zbytes, d_d0 + b0, d_d1 + b0, d_uoff + b0, d_out, err);
+        const uint64_t *a0 = d_d0 + b0, *a1 = d_d1 + b0, *au = d_uoff + b0;
+        switch (inflate_group) {
+        case 0: k_inflate<<<nb, 64, 0, ctx->stream>>>(d_z, zbytes, a0, a1, au, d_out, err); break;
+        case 16: k_inflate_g<16, 1024, 9, 8><<<oge_ceil_div(nb, 4), 64, 0, ctx->stream>>>(d_z, zbytes, a0, a1, au, nb, d_out, err); break;
+        default: k_inflate_g<32, 1024, 10, 8><<<oge_ceil_div(nb, 2), 64, 0, ctx->stream>>>(d_z, zbytes, a0, a1, au, nb, d_out, err); break;
+        }
         OGE_LAUNCH_CHECK(ctx);
     }
     ctx->end_stage(tm);

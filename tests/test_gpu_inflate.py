@@ -146,3 +146,18 @@ def test_record_offsets_reject_bad_block_size(ctx):
     torch.cuda.synchronize()
     with pytest.raises(L.OgeError):
         ctx.record_offsets_dev(d.data_ptr(), base, len(bad), n_ref)
+
+
+@pytest.mark.parametrize("level", [1, 6, 9])
+def test_inflate_host_writer_streams(ctx, tmp_path, level):
+    """BGZF written by the host writer (libdeflate when present, else zlib) -- the CLI's own inputs."""
+    import gzip
+    from openge_amd import lib as L
+    # 240k reads (~68 MB, ~1000 blocks): enough back-references just beyond the decoder's LDS ring
+    # (the case a flush race once corrupted)
+    p = L.synth_params(120_000, preset="c2", seed=31)
+    recs, offs, hdr = L.synth_host(p, threads=8)
+    path = tmp_path / "w.bam"
+    L.write_bam(str(path), hdr, recs, offs, len(offs) - 1, level=level)
+    z = path.read_bytes()
+    assert ctx.bgzf_inflate(z) == gzip.decompress(z)
