@@ -12,7 +12,9 @@
 #include "oge_ctx.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 namespace {
 
@@ -144,11 +146,12 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t k, const Digit d) {
     return lo | (hi << d.w0);
 }
 
+template <int NB>
 __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restrict__ keys, uint64_t n, Digit dg,
                                                           uint32_t nbins, uint32_t *__restrict__ hist, uint32_t nblocks) {
-    __shared__ uint32_t h[kWaves][256];
+    __shared__ uint32_t h[kWaves][NB];
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    for (uint32_t i = tid; i < kWaves * 256; i += kThreads) (&h[0][0])[i] = 0;
+    for (uint32_t i = tid; i < kWaves * NB; i += kThreads) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)w * (kItems * 64);
 #pragma unroll 4
@@ -168,19 +171,20 @@ __global__ __launch_bounds__(kThreads) void k_radix_hist(const uint64_t *__restr
 // Stable scatter of one 4096-key tile.  Ranks come from 64-lane ballot peer masks per wave; the
 // tile is then re-ordered by digit in LDS so that the global writes of each digit bucket are
 // contiguous runs written by consecutive lanes (instead of 16 scattered 8-byte writes per bucket).
-template <bool HAS_V>
+template <bool HAS_V, int NB>
 __global__ __launch_bounds__(kThreads) void k_radix_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                              uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint64_t n,
                                                              Digit dg, uint32_t nbins, const uint32_t *__restrict__ offs,
                                                              uint32_t nblocks) {
+    constexpr int DPT = NB / kThreads > 0 ? NB / kThreads : 1;  // digits per thread in the digit scan
     __shared__ uint64_t sk[kTile];
     __shared__ uint32_t sv[HAS_V ? kTile : 1];
-    __shared__ uint32_t wcnt[kWaves][256];
-    __shared__ uint32_t dstart[256];
-    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t wcnt[kWaves][NB];
+    __shared__ uint32_t dstart[NB];
+    __shared__ uint32_t gbase[NB];
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint32_t nbits = dg.w0 + dg.w1;
-    for (uint32_t i = tid; i < kWaves * 256; i += kThreads) (&wcnt[0][0])[i] = 0;
+    for (uint32_t i = tid; i < kWaves * NB; i += kThreads) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint64_t tile0 = (uint64_t)blockIdx.x * kTile;
     const uint64_t base = tile0 + (uint64_t)w * (kItems * 64);
@@ -216,24 +220,37 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(const uint64_t *__re
         rank[j] = prev + below;
     }
     __syncthreads();
-    // per digit: tile total -> exclusive scan over digits (block-local bucket starts)
-    uint32_t tot = 0;
-    if (tid < nbins) {
+    // per digit: tile total -> exclusive scan over digits (block-local bucket starts); thread t owns
+    // digits [t*DPT, t*DPT + DPT)
+    uint32_t tot[DPT];
+    uint32_t tsum = 0;
 #pragma unroll
-        for (int i = 0; i < kWaves; ++i) tot += wcnt[i][tid];
+    for (int k = 0; k < DPT; ++k) {
+        const uint32_t d = tid * DPT + k;
+        tot[k] = 0;
+        if (d < nbins) {
+#pragma unroll
+            for (int i = 0; i < kWaves; ++i) tot[k] += wcnt[i][d];
+        }
+        tsum += tot[k];
     }
     uint32_t dummy;
-    const uint32_t ds = block_excl_scan(tot, &dummy);
-    if (tid < nbins) {
-        dstart[tid] = ds;
-        gbase[tid] = offs[(uint64_t)tid * nblocks + blockIdx.x];
-        uint32_t run = ds;
+    uint32_t ds = block_excl_scan(tsum, &dummy);
 #pragma unroll
-        for (int i = 0; i < kWaves; ++i) {
-            const uint32_t c = wcnt[i][tid];
-            wcnt[i][tid] = run;
-            run += c;
+    for (int k = 0; k < DPT; ++k) {
+        const uint32_t d = tid * DPT + k;
+        if (d < nbins) {
+            dstart[d] = ds;
+            gbase[d] = offs[(uint64_t)d * nblocks + blockIdx.x];
+            uint32_t run = ds;
+#pragma unroll
+            for (int i = 0; i < kWaves; ++i) {
+                const uint32_t c = wcnt[i][d];
+                wcnt[i][d] = run;
+                run += c;
+            }
         }
+        ds += tot[k];
     }
     __syncthreads();
 #pragma unroll
@@ -256,7 +273,7 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(const uint64_t *__re
     }
 }
 
-std::vector<Digit> plan_digits(uint64_t mask) {
+std::vector<Digit> plan_digits(uint64_t mask, uint32_t maxw) {
     // contiguous runs of set bits
     std::vector<std::pair<uint32_t, uint32_t>> runs;  // (start, width)
     for (uint32_t b = 0; b < 64;) {
@@ -269,7 +286,7 @@ std::vector<Digit> plan_digits(uint64_t mask) {
     for (auto &r : runs) total += r.second;
     std::vector<Digit> out;
     if (!total) return out;
-    uint32_t passes = (total + 7) / 8;
+    uint32_t passes = (total + maxw - 1) / maxw;
     uint32_t per = (total + passes - 1) / passes;  // balanced digit width
     size_t ri = 0;
     uint32_t roff = 0;
@@ -325,27 +342,45 @@ int oge_radix_sort_pairs(oge_ctx *ctx, uint64_t *keys, uint32_t *vals, uint64_t 
     if (n < 2 || bit_mask == 0) return OGE_OK;
     if (n > 0xFFFFFFFFull) return oge_fail(ctx, OGE_ERR_LIMIT, "radix sort: more than 2^32-1 elements");
     const bool has_v = vals != nullptr;
-    std::vector<Digit> digits = plan_digits(bit_mask);
+    // widest digit (OGE_RADIX_MAXW, 4..10).  8 is the measured optimum on C2 at 300M reads: 9- and
+    // 10-bit digits save passes but every 4096-key tile then spreads over 512/1024 buckets, the
+    // scatter's per-bucket runs shrink below a cache line, and the step got slower (185 -> 192 /
+    // 196 ms).  Both wide paths pass the parity suite.
+    static const uint32_t maxw = [] {
+        const char *e = getenv("OGE_RADIX_MAXW");
+        const int v = e && *e ? atoi(e) : 8;
+        return (uint32_t)std::min(10, std::max(4, v));
+    }();
+    std::vector<Digit> digits = plan_digits(bit_mask, maxw);
     const uint32_t nblocks = oge_ceil_div(n, kTile);
-    uint32_t *hist = (uint32_t *)ctx->ws("radix_hist", (size_t)256 * nblocks * sizeof(uint32_t));
+    uint32_t *hist = (uint32_t *)ctx->ws("radix_hist", (size_t)1024 * nblocks * sizeof(uint32_t));
     if (!hist) return OGE_ERR_HIP;
     uint64_t *ka = keys, *kb = ktmp;
     uint32_t *va = vals, *vb = vtmp;
     for (const Digit &d : digits) {
         const uint32_t nbins = 1u << (d.w0 + d.w1);
-        hipLaunchKernelGGL(k_radix_hist, dim3(nblocks), dim3(kThreads), 0, ctx->stream, (const uint64_t *)ka, n, d, nbins,
-                           hist, nblocks);
-        OGE_LAUNCH_CHECK(ctx);
-        int rc = oge_exclusive_scan_u32(ctx, hist, hist, (uint64_t)nbins * nblocks);
+        auto pass = [&](auto nb_tag) -> int {
+            constexpr int NB = decltype(nb_tag)::value;
+            hipLaunchKernelGGL(k_radix_hist<NB>, dim3(nblocks), dim3(kThreads), 0, ctx->stream, (const uint64_t *)ka, n, d,
+                               nbins, hist, nblocks);
+            OGE_LAUNCH_CHECK(ctx);
+            int rc = oge_exclusive_scan_u32(ctx, hist, hist, (uint64_t)nbins * nblocks);
+            if (rc) return rc;
+            if (has_v)
+                hipLaunchKernelGGL((k_radix_scatter<true, NB>), dim3(nblocks), dim3(kThreads), 0, ctx->stream,
+                                   (const uint64_t *)ka, (const uint32_t *)va, kb, vb, n, d, nbins, (const uint32_t *)hist,
+                                   nblocks);
+            else
+                hipLaunchKernelGGL((k_radix_scatter<false, NB>), dim3(nblocks), dim3(kThreads), 0, ctx->stream,
+                                   (const uint64_t *)ka, (const uint32_t *)nullptr, kb, (uint32_t *)nullptr, n, d, nbins,
+                                   (const uint32_t *)hist, nblocks);
+            OGE_LAUNCH_CHECK(ctx);
+            return OGE_OK;
+        };
+        int rc = nbins <= 256   ? pass(std::integral_constant<int, 256>())
+                 : nbins <= 512 ? pass(std::integral_constant<int, 512>())
+                                : pass(std::integral_constant<int, 1024>());
         if (rc) return rc;
-        if (has_v)
-            hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nblocks), dim3(kThreads), 0, ctx->stream, (const uint64_t *)ka,
-                               (const uint32_t *)va, kb, vb, n, d, nbins, (const uint32_t *)hist, nblocks);
-        else
-            hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nblocks), dim3(kThreads), 0, ctx->stream, (const uint64_t *)ka,
-                               (const uint32_t *)nullptr, kb, (uint32_t *)nullptr, n, d, nbins, (const uint32_t *)hist,
-                               nblocks);
-        OGE_LAUNCH_CHECK(ctx);
         std::swap(ka, kb);
         std::swap(va, vb);
     }
