@@ -116,3 +116,41 @@ def test_synth_shape_c2(built):
     assert sum(x["flag"] & 0x4 != 0 for x in f) / n == pytest.approx(0.0025, abs=0.002)
     assert len({x["refid"] for x in f}) == 24
     assert hdr.count("@RG") == 2
+
+
+def test_bgzf_index_matches_framing(built, tmp_path):
+    """oge_bgzf_index (host side of the GPU reader): deflate ranges, payload offsets and CRCs per
+    block, empty blocks skipped, truncation and non-BGZF input rejected."""
+    import zlib
+    data = np.random.default_rng(7).integers(0, 4, 200_000, dtype=np.uint8).tobytes()
+    blocks, want = [], []
+    pos = zpos = 0
+    for i in range(0, len(data), 65280):
+        chunk = data[i:i + 65280]
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        body = c.compress(chunk) + c.flush()
+        bsize = 18 + len(body) + 8
+        blk = (b"\x1f\x8b\x08\x04\0\0\0\0\0\xff\x06\0BC\x02\0" + struct.pack("<H", bsize - 1) + body +
+               struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
+        want.append((zpos + 18, zpos + bsize - 8, pos, zlib.crc32(chunk) & 0xFFFFFFFF))
+        blocks.append(blk)
+        pos += len(chunk)
+        zpos += bsize
+    eof = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    z = np.frombuffer(b"".join(blocks) + eof, dtype=np.uint8)
+    lib = L.lib()
+    nb = ctypes.c_uint64()
+    assert lib.oge_bgzf_index(z.ctypes.data, len(z), None, None, None, None, 0, ctypes.byref(nb)) == -1  # cap 0: count only
+    k = nb.value
+    assert k == len(want)
+    d0, d1, uo = (np.zeros(k + 1, dtype=np.uint64) for _ in range(3))
+    crc = np.zeros(k, dtype=np.uint32)
+    assert lib.oge_bgzf_index(z.ctypes.data, len(z), d0.ctypes.data, d1.ctypes.data, uo.ctypes.data, crc.ctypes.data, k,
+                              ctypes.byref(nb)) == 0
+    for i, (a, b, u, c) in enumerate(want):
+        assert (d0[i], d1[i], uo[i], crc[i]) == (a, b, u, c)
+    assert uo[k] == len(data)
+    bad = z[:-100].copy()
+    assert lib.oge_bgzf_index(bad.ctypes.data, len(bad), None, None, None, None, 0, ctypes.byref(nb)) != 0
+    notgz = np.frombuffer(b"BAM\x01" + bytes(100), dtype=np.uint8)
+    assert lib.oge_bgzf_index(notgz.ctypes.data, len(notgz), None, None, None, None, 0, ctypes.byref(nb)) != 0
