@@ -276,6 +276,42 @@ int oge_fix_bins_dev(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint6
 int oge_drop_flagged_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, uint16_t flag_mask,
                          uint8_t *d_out, uint64_t *d_out_off, uint64_t *n_out);
 
+/* ---- mergesort extras: Filter (-r region / -q mapq) and sort by name (-b) ----------- */
+/* Filter::runInternal's predicate (algorithms/filter.cpp:205-249) with the module's setters
+ * (filter.h:34-47).  len = l_seq (BamAlignment::getLength).  A record is kept when
+ *   mapq >= mapq_min && min_len <= len <= max_len && len > trim_total
+ *   [&& ref_id <= refID <= ref_id && pos + len >= left_pos && pos <= right_pos   if has_region]
+ * and at most count_limit records (the first ones kept, in input order) are kept. */
+typedef struct oge_filter_opts {
+    int32_t has_region;
+    int32_t ref_id;       /* region refID (Filter::ParseRegionString) */
+    int32_t left_pos;     /* region start, 0-based as the reference compares it */
+    int32_t right_pos;    /* region stop */
+    int32_t mapq_min;     /* setQualityLimit, default 0 */
+    int32_t min_len;      /* setMinimumReadLength, default 0 */
+    int32_t max_len;      /* setMaximumReadLength, default INT32_MAX */
+    int32_t trim_total;   /* trim_begin_length + trim_end_length, default 0 */
+    uint64_t count_limit; /* setCountLimit, default INT32_MAX */
+} oge_filter_opts;
+/* Defaults of Filter::Filter() (filter.cpp:185-194). */
+void oge_filter_opts_init(oge_filter_opts *o);
+/* Filter::ParseRegionString (filter.cpp:31-137): "chr", "chr:pos" or "chr:start..stop" against the
+ * header's sequence dictionary (ref_names = n_ref NUL-terminated names back to back, ref_len =
+ * their LN).  Fills has_region/ref_id/left_pos/right_pos; OGE_ERR_ARG with the reference's message
+ * (oge_last_error(NULL)) when the region does not parse or lies outside the sequence. */
+int oge_parse_region(const char *region, const char *ref_names, int32_t n_ref, const int64_t *ref_len,
+                     oge_filter_opts *o);
+/* Copy the records the filter keeps, in input order, to d_out / d_out_off (*n_out records). */
+int oge_filter_records_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
+                           const oge_filter_opts *o, uint8_t *d_out, uint64_t *d_out_off, uint64_t *n_out);
+/* Sort::ByName (util/bamtools/Sort.h:67-90) as ReadSorter uses it for SORT_QUERYNAME
+ * (algorithms/read_sorter.cpp:202-203): read names compared bytewise (std::string <); records
+ * with equal names keep input order (the reference's std::sort leaves their order
+ * implementation-defined).  d_perm (n) receives the input index of each output position. */
+int oge_sort_name_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, uint32_t *d_perm);
+int oge_sort_name(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const uint64_t *rec_off, uint64_t n,
+                  uint32_t *perm_out);
+
 #ifdef __cplusplus
 }
 #endif

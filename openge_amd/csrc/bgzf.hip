@@ -624,20 +624,6 @@ __global__ void k_fix_bins(uint8_t *__restrict__ recs, const uint64_t *__restric
     oge_wr_u16(r + OGE_OFF_BIN, oge_rec_bin(r));
 }
 
-__global__ void k_keep_flags(const uint8_t *__restrict__ recs, const uint64_t *__restrict__ off, uint64_t n, uint16_t mask,
-                             uint32_t *__restrict__ keep) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    keep[i] = (oge_rd_u16(recs + off[i] + OGE_OFF_FLAG) & mask) ? 0u : 1u;
-}
-
-__global__ void k_keep_perm(const uint32_t *__restrict__ keep, const uint32_t *__restrict__ pos, uint64_t n,
-                            uint32_t *__restrict__ perm) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (keep[i]) perm[pos[i]] = (uint32_t)i;
-}
-
 }  // namespace
 
 int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
@@ -729,35 +715,3 @@ extern "C" int oge_fix_bins_dev(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d
     return OGE_OK;
 }
 
-extern "C" int oge_drop_flagged_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, uint16_t flag_mask,
-                                    uint8_t *d_out, uint64_t *d_out_off, uint64_t *n_out) {
-    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
-    if (!n_out) return oge_fail(ctx, OGE_ERR_ARG, "null n_out");
-    if (n >= 0xffffffffull) return oge_fail(ctx, OGE_ERR_ARG, "too many records");
-    hipSetDevice(ctx->device);
-    *n_out = 0;
-    if (!n) return OGE_OK;
-    uint32_t *keep = (uint32_t *)ctx->ws("drop_keep", (n + 1) * 4);
-    uint32_t *pos = (uint32_t *)ctx->ws("drop_pos", (n + 1) * 4);
-    uint32_t *perm = (uint32_t *)ctx->ws("drop_perm", (n + 1) * 4);
-    if (!keep || !pos || !perm) return OGE_ERR_HIP;
-    k_keep_flags<<<oge_ceil_div(n, 256), 256, 0, ctx->stream>>>(d_recs, d_off, n, flag_mask, keep);
-    OGE_LAUNCH_CHECK(ctx);
-    int rc = oge_exclusive_scan_u32(ctx, keep, pos, n);
-    if (rc) return rc;
-    k_keep_perm<<<oge_ceil_div(n, 256), 256, 0, ctx->stream>>>(keep, pos, n, perm);
-    OGE_LAUNCH_CHECK(ctx);
-    uint32_t last[2];
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&last[0], pos + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&last[1], keep + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    const uint64_t m = (uint64_t)last[0] + last[1];
-    if (m) {
-        rc = oge_gather_with_sizes(ctx, d_recs, d_off, perm, nullptr, m, d_out, d_out_off, nullptr, nullptr);
-        if (rc) return rc;
-    } else {
-        OGE_HIP_TRY(ctx, hipMemsetAsync(d_out_off, 0, 8, ctx->stream));
-    }
-    *n_out = m;
-    return OGE_OK;
-}

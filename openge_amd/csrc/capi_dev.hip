@@ -228,6 +228,23 @@ int oge_sort_coord(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const 
     return OGE_OK;
 }
 
+int oge_sort_name(oge_ctx *ctx, const uint8_t *recs, uint64_t rec_bytes, const uint64_t *rec_off, uint64_t n,
+                  uint32_t *perm_out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    hipSetDevice(ctx->device);
+    uint8_t *dr;
+    uint64_t *dof;
+    int rc = upload(ctx, recs, rec_bytes, rec_off, n, &dr, &dof);
+    if (rc) return rc;
+    uint32_t *dp = (uint32_t *)ctx->ws("host_perm", (n + 1) * 4);
+    if (!dp) return OGE_ERR_HIP;
+    rc = oge_sort_name_dev(ctx, dr, dof, n, dp);
+    if (rc) return rc;
+    if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(perm_out, dp, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return OGE_OK;
+}
+
 // ---------------------------------------------------------------- markdup
 int oge_markdup_dev(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
                     uint8_t *d_dup, int apply, uint64_t *n_dup_out) {

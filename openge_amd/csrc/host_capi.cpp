@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -184,3 +185,62 @@ int oge_bam_write(const char *path, const char *header_text, uint64_t header_len
 }
 
 } // extern "C"
+
+// ----------------------------------------------------------------------------- Filter (mergesort -r/-q)
+extern "C" void oge_filter_opts_init(oge_filter_opts *o) {  // Filter::Filter (filter.cpp:185-194)
+    if (!o) return;
+    memset(o, 0, sizeof *o);
+    o->max_len = INT32_MAX;
+    o->count_limit = INT32_MAX;
+}
+
+// Filter::ParseRegionString (filter.cpp:31-137): the same parse (atoi on the pieces, so "chr:5-9"
+// reads as the single position 5), the last dictionary entry of that name, the same range checks.
+extern "C" int oge_parse_region(const char *region, const char *ref_names, int32_t n_ref, const int64_t *ref_len,
+                                oge_filter_opts *o) {
+    if (!region || !o || (n_ref > 0 && (!ref_names || !ref_len))) return oge_fail(nullptr, OGE_ERR_ARG, "null argument");
+    const std::string rs = region;
+    const std::string bad = "ERROR: could not parse region'" + rs + "'";
+    if (rs.empty()) return oge_fail(nullptr, OGE_ERR_ARG, bad.c_str());
+    std::string chrom;
+    int start, stop;
+    const size_t c1 = rs.find(':');
+    if (c1 == std::string::npos) {
+        chrom = rs;
+        start = 0;
+        stop = -1;
+    } else {
+        chrom = rs.substr(0, c1);
+        const size_t dots = rs.find("..", c1 + 1);
+        if (dots == std::string::npos) {
+            start = atoi(rs.substr(c1 + 1).c_str());
+            stop = start;
+        } else {
+            start = atoi(rs.substr(c1 + 1, dots - c1 - 1).c_str());
+            if (rs.find(':', dots + 1) != std::string::npos) return oge_fail(nullptr, OGE_ERR_ARG, bad.c_str());
+            stop = atoi(rs.substr(dots + 2).c_str());
+        }
+    }
+    int ref = -1;
+    const char *p = ref_names;
+    for (int i = 0; i < n_ref; ++i) {
+        if (chrom == p) ref = i;
+        p += strlen(p) + 1;
+    }
+    if (ref == -1) return oge_fail(nullptr, OGE_ERR_ARG, ("Can't find chromosome'" + chrom + "'").c_str());
+    const int len = (int)ref_len[ref];
+    if (start >= len)
+        return oge_fail(nullptr, OGE_ERR_ARG,
+                        ("Start position (" + std::to_string(start) + ") after end of the reference sequence (" +
+                         std::to_string(len) + ")").c_str());
+    if (stop > len)  // the reference's message says "Start" here too (filter.cpp:125)
+        return oge_fail(nullptr, OGE_ERR_ARG,
+                        ("Start position (" + std::to_string(stop) + ") after end of the reference sequence (" +
+                         std::to_string(len) + ")").c_str());
+    if (stop == -1) stop = len;
+    o->has_region = 1;
+    o->ref_id = ref;
+    o->left_pos = start;
+    o->right_pos = stop;
+    return OGE_OK;
+}

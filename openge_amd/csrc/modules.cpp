@@ -2,6 +2,7 @@
 #include "modules.h"
 
 #include <chrono>
+#include <climits>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -77,7 +78,9 @@ int AlgorithmModule::runChain(ChainContext &cc) {
             cc.free_device(b);
             return rc;
         }
-        if (dynamic_cast<ReadSorter *>(m) && dynamic_cast<MarkDuplicates *>(m->sink_)) marked = true;
+        if (dynamic_cast<ReadSorter *>(m) && static_cast<ReadSorter *>(m)->sortBy() == BamHeaderModel::COORDINATE &&
+            dynamic_cast<MarkDuplicates *>(m->sink_))
+            marked = true;
     }
     cc.free_device(b);
     return 0;
@@ -241,10 +244,83 @@ static void markdup_opts(const ReadBatch &b, bool compat, int split, MdOpts &m) 
     m.o.split_chains = split;
 }
 
+// ----------------------------------------------------------------------------------- Filter
+bool Filter::setReadLengths(const std::string &s) {
+    int a = 0, z = 0;
+    char junk;
+    bool ok;
+    if (!s.empty() && s[0] == '+') {
+        ok = sscanf(s.c_str(), "%c%d", &junk, &a) == 2;
+        z = INT32_MAX;
+    } else if (!s.empty() && s[0] == '-') {
+        ok = sscanf(s.c_str(), "%c%d", &junk, &z) == 2;
+        a = INT32_MIN;
+    } else if (s.find('-') != std::string::npos) {
+        ok = sscanf(s.c_str(), "%d%c%d", &a, &junk, &z) == 3;
+    } else {
+        ok = sscanf(s.c_str(), "%d", &a) == 1;
+        z = a;
+    }
+    if (!ok) {  // filter.cpp:179-182
+        fprintf(stderr, "Error parsing read length requirements. Aborting.\n"
+                        "Valid ranges look like: 64, or 64-72, or -64, or +64.\n");
+        exit(-1);
+    }
+    opts_.min_len = a;
+    opts_.max_len = z;
+    return true;
+}
+
+int Filter::runInternal(ChainContext &cc, ReadBatch &b) {
+    oge_filter_opts o = opts_;
+    if (has_region_) {
+        if (verbose_) fprintf(stderr, "Filtering to region %s\n", region_.c_str());
+        std::string names;
+        std::vector<int64_t> lens;
+        for (auto &sq : b.header.sq) {
+            names += sq.name;
+            names.push_back('\0');
+            lens.push_back(sq.length);
+        }
+        if (oge_parse_region(region_.c_str(), names.data(), (int32_t)lens.size(), lens.data(), &o)) {
+            // filter.cpp:243-247: the parse error, then the generic message, then exit(-1)
+            const std::string why = oge_last_error(nullptr);
+            if (why.rfind("ERROR: could not parse", 0) != 0) fprintf(stderr, "%s\n", why.c_str());
+            fprintf(stderr, "ERROR: could not parse region'%s'\n"
+                            "Check that region description is in valid format (see documentation) and that the "
+                            "coordinates are valid\n", region_.c_str());
+            return -1;
+        }
+    }
+    if (cc.to_device(b)) return -1;
+    void *out = nullptr, *out_off = nullptr;
+    if (oge_dev_alloc(cc.ctx, b.d_bytes + 64, &out) || oge_dev_alloc(cc.ctx, (b.n + 1) * 8, &out_off))
+        return cc.fail("device allocation");
+    uint64_t m = 0, bytes = 0;
+    int rc = oge_filter_records_dev(cc.ctx, b.d_recs, b.d_offs, b.n, &o, (uint8_t *)out, (uint64_t *)out_off, &m);
+    if (!rc) rc = oge_memcpy(cc.ctx, &bytes, (uint64_t *)out_off + m, 8, 2);
+    if (!rc) rc = oge_ctx_sync(cc.ctx);
+    if (rc) {
+        oge_dev_free(cc.ctx, out);
+        oge_dev_free(cc.ctx, out_off);
+        return cc.fail("Filter");
+    }
+    cc.free_device(b);
+    b.d_recs = (uint8_t *)out;
+    b.d_offs = (uint64_t *)out_off;
+    b.d_bytes = bytes;
+    b.n = m;
+    b.dev_valid = true;
+    b.host_valid = false;
+    kept = m;
+    if (verbose_) fprintf(stderr, "%llu alignments processed.\n", (unsigned long long)m);
+    return 0;
+}
+
 // ----------------------------------------------------------------------------------- ReadSorter
 int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
-    if (order_ != BamHeaderModel::COORDINATE) {
-        fprintf(stderr, "openge: sort by name (-b) is not provided by the GPU path\n");
+    if (order_ != BamHeaderModel::COORDINATE && order_ != BamHeaderModel::QUERYNAME) {
+        fprintf(stderr, "openge: unsupported sort order\n");
         return -1;
     }
     const auto t0 = std::chrono::steady_clock::now();
@@ -255,8 +331,11 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
         oge_dev_alloc(cc.ctx, (b.n + 1) * 8, &out_off))
         return cc.fail("device allocation");
     int rc;
-    MarkDuplicates *md = dynamic_cast<MarkDuplicates *>(sink_);
-    if (md) {  // mergesort -M: one fused device pipeline (sort, dedup, gather with 0x400 applied)
+    MarkDuplicates *md = order_ == BamHeaderModel::COORDINATE ? dynamic_cast<MarkDuplicates *>(sink_) : nullptr;
+    if (order_ == BamHeaderModel::QUERYNAME) {  // -b; a MarkDuplicates sink then runs on its own
+        rc = oge_sort_name_dev(cc.ctx, b.d_recs, b.d_offs, b.n, (uint32_t *)perm);
+        if (!rc) rc = oge_gather_records_dev(cc.ctx, b.d_recs, b.d_offs, (uint32_t *)perm, b.n, (uint8_t *)out, (uint64_t *)out_off);
+    } else if (md) {  // mergesort -M: one fused device pipeline (sort, dedup, gather with 0x400 applied)
         MdOpts m;
         markdup_opts(b, md->compatNonverbose, md->splitChains, m);
         uint64_t nd = 0;
@@ -283,7 +362,7 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
     b.d_offs = (uint64_t *)out_off;
     b.dev_valid = true;
     b.host_valid = false;
-    b.header.sort_order = BamHeaderModel::COORDINATE;  // read_sorter.cpp:257-258
+    b.header.sort_order = order_;  // read_sorter.cpp:257-258
     return 0;
 }
 

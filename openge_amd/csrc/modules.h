@@ -87,8 +87,32 @@ protected:
     std::vector<std::string> files_;
 };
 
-// ReadSorter (algorithms/read_sorter.h:32-105): coordinate sort on the GPU (oge_sort_coord_dev +
-// permutation gather).  The temp-file knobs are accepted for interface parity; one device sort
+// Filter (algorithms/filter.h:30-70, filter.cpp:185-249): mergesort's -r region / -q mapq, as a
+// device compaction (oge_filter_records_dev).  Trimming (setTrimBeginLength/EndLength) edits
+// records and is only reachable from the bpipe `filter` command, which is out of scope; its
+// length condition (len > trim total) is kept.
+class Filter : public AlgorithmModule {
+public:
+    Filter() : AlgorithmModule("Filter") { oge_filter_opts_init(&opts_); }
+    void setRegion(const std::string &region) { region_ = region; has_region_ = true; }
+    std::string getRegion() const { return region_; }
+    void setCountLimit(int ct) { opts_.count_limit = ct < 0 ? 0 : (uint64_t)ct; }
+    size_t getCountLimit() const { return opts_.count_limit; }
+    void setQualityLimit(int mapq) { opts_.mapq_min = mapq; }
+    int getQualityLimit() const { return opts_.mapq_min; }
+    void setMinimumReadLength(int l) { opts_.min_len = l; }
+    void setMaximumReadLength(int l) { opts_.max_len = l; }
+    bool setReadLengths(const std::string &s);  // "64", "64-72", "-64", "+64" (filter.cpp:150-183)
+    uint64_t kept = 0;
+protected:
+    int runInternal(ChainContext &cc, ReadBatch &b) override;
+    std::string region_;
+    bool has_region_ = false;
+    oge_filter_opts opts_;
+};
+
+// ReadSorter (algorithms/read_sorter.h:32-105): coordinate sort (oge_sort_coord_dev) or, with
+// setSortBy(QUERYNAME), name sort (oge_sort_name_dev) on the GPU, then the permutation gather.  The temp-file knobs are accepted for interface parity; one device sort
 // replaces the reference's spilled runs and k-way merge.
 class ReadSorter : public AlgorithmModule {
 public:
@@ -99,6 +123,8 @@ public:
 protected:
     int runInternal(ChainContext &cc, ReadBatch &b) override;
     BamHeaderModel::SortOrder order_ = BamHeaderModel::COORDINATE;
+public:
+    BamHeaderModel::SortOrder sortBy() const { return order_; }
 };
 
 // MarkDuplicates (algorithms/mark_duplicates.h:27-68): -v --nosplit semantics on the GPU.

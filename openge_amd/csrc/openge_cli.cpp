@@ -7,8 +7,10 @@
 // Deliberate differences: dedup defaults to `-v --nosplit` semantics (Q1, Q3).
 // --compat-nonverbose-dedup reproduces the non-verbose index bug; --split-chains K reproduces K
 // split-by-chromosome chains, and --compat-split the reference's own rule for them (without
-// --nosplit/--nothreads: K = min(12, threads / 2), command_dedup.cpp:46-48).  Sort-by-name (-b),
-// region/MAPQ filters (-r/-q) and SAM/FASTQ output are not provided and fail loudly.
+// --nosplit/--nothreads: K = min(12, threads / 2), command_dedup.cpp:46-48).  Sort by name (-b)
+// gives the true name order (the reference merges name-sorted temp runs by position,
+// util/read_stream_reader.h:94-97, so its output is name-sorted only within one run of -n reads).
+// SAM/FASTQ output is not provided and fails loudly.
 #include <sys/resource.h>
 #include <sys/time.h>
 
@@ -168,17 +170,21 @@ int main(int argc, const char **argv) {
 
     int ret = 0;
     if (cmd == "mergesort") {
-        if (p.count("region") || p.count("mapq")) {
-            fprintf(stderr, "openge: region/MAPQ filters (-r/-q) are not provided by the GPU path\n");
-            return -1;
-        }
         bool dedup = p.count("markduplicates") || p.count("removeduplicates");
+        Filter filter;
         ReadSorter sorter;
         MarkDuplicates md;
         sorter.setSortBy(p.count("byname") ? BamHeaderModel::QUERYNAME : BamHeaderModel::COORDINATE);
         sorter.setCompressTempFiles(p.count("compresstempfiles"));
         sorter.setAlignmentsPerTempfile(atoi(p.get("n", "500000").c_str()));
-        reader.addSink(&sorter);
+        if (p.count("region") || p.count("mapq")) {  // command_mergesort.cpp:82-92
+            if (p.count("region")) filter.setRegion(p.get("region", ""));
+            if (p.count("mapq")) filter.setQualityLimit(atoi(p.get("mapq", "0").c_str()));
+            reader.addSink(&filter);
+            filter.addSink(&sorter);
+        } else {
+            reader.addSink(&sorter);
+        }
         if (dedup) {
             md.removeDuplicates = p.count("removeduplicates");
             md.compatNonverbose = compat;

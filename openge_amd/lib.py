@@ -41,6 +41,13 @@ class MarkdupOpts(C.Structure):
     ]
 
 
+class FilterOpts(C.Structure):
+    """oge_filter_opts (include/openge_hip.h): Filter's settings (algorithms/filter.h:34-47)."""
+
+    _fields_ = [(k, C.c_int32) for k in ("has_region", "ref_id", "left_pos", "right_pos", "mapq_min", "min_len",
+                                         "max_len", "trim_total")] + [("count_limit", C.c_uint64)]
+
+
 class RealignSynthParams(C.Structure):
     """Mirror of oge_realign_synth_params (include/openge_hip.h)."""
 
@@ -213,6 +220,11 @@ def lib() -> C.CDLL:
         "oge_bgzf_inflate": (C.c_int, [vp, vp, u64, vp, u64, C.POINTER(u64)]),
         "oge_bam_record_offsets_dev": (C.c_int, [vp, vp, u64, u64, i32, vp, u64, C.POINTER(u64)]),
         "oge_drop_flagged_dev": (C.c_int, [vp, vp, vp, u64, C.c_uint16, vp, vp, C.POINTER(u64)]),
+        "oge_filter_opts_init": (None, [vp]),
+        "oge_parse_region": (C.c_int, [C.c_char_p, C.c_char_p, i32, vp, vp]),
+        "oge_filter_records_dev": (C.c_int, [vp, vp, vp, u64, vp, vp, vp, C.POINTER(u64)]),
+        "oge_sort_name_dev": (C.c_int, [vp, vp, vp, u64, vp]),
+        "oge_sort_name": (C.c_int, [vp, vp, u64, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)
@@ -221,6 +233,24 @@ def lib() -> C.CDLL:
         f.restype, f.argtypes = res, args
     _lib = L
     return L
+
+
+def filter_opts(**over) -> FilterOpts:
+    """Filter::Filter() defaults (algorithms/filter.cpp:185-194) with overrides."""
+    o = FilterOpts()
+    lib().oge_filter_opts_init(C.byref(o))
+    for k, v in over.items():
+        setattr(o, k, v)
+    return o
+
+
+def parse_region(region: str, refs: list[tuple[str, int]], opts: FilterOpts | None = None) -> FilterOpts:
+    """Filter::ParseRegionString through the C ABI; raises OgeError with the reference's message."""
+    o = opts if opts is not None else filter_opts()
+    names = b"".join(nm.encode() + b"\0" for nm, _ in refs)
+    lens = np.array([ln for _, ln in refs] or [0], dtype=np.int64)
+    check(lib().oge_parse_region(region.encode(), names, len(refs), _ptr(lens), C.byref(o)))
+    return o
 
 
 def exported_symbols() -> list[str]:
@@ -444,6 +474,20 @@ class Context:
         m = C.c_uint64()
         check(lib().oge_drop_flagged_dev(self.h, d_recs, d_off, n, flag_mask, d_out, d_out_off, C.byref(m)), self.h)
         return m.value
+
+    def filter_records_dev(self, d_recs, d_off, n: int, opts: "FilterOpts", d_out, d_out_off) -> int:
+        m = C.c_uint64()
+        check(lib().oge_filter_records_dev(self.h, d_recs, d_off, n, C.byref(opts), d_out, d_out_off, C.byref(m)),
+              self.h)
+        return m.value
+
+    def sort_name(self, recs: np.ndarray, offs: np.ndarray, n: int) -> np.ndarray:
+        perm = np.zeros(max(n, 1), dtype=np.uint32)
+        check(lib().oge_sort_name(self.h, _ptr(recs), recs.nbytes, _ptr(offs), n, _ptr(perm)), self.h)
+        return perm[:n]
+
+    def sort_name_dev(self, d_recs, d_off, n: int, d_perm) -> None:
+        check(lib().oge_sort_name_dev(self.h, d_recs, d_off, n, d_perm), self.h)
 
     def markdup_dev(self, d_recs, d_off, n, opts: MarkdupOpts, d_dup, apply: bool = True) -> int:
         nd = C.c_uint64()

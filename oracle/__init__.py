@@ -53,6 +53,11 @@ def _L():
         L.oracle_markdup_split.restype = C.c_int64
         L.oracle_markdup_split.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
                                            C.c_int32, C.c_int16, C.c_int, C.c_int, C.c_void_p]
+        L.oracle_filter.restype = C.c_uint64
+        L.oracle_filter.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int] + [C.c_int32] * 7 + [C.c_uint64,
+                                                                                               C.c_void_p]
+        L.oracle_sort_name.restype = C.c_int
+        L.oracle_sort_name.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
         L.oracle_markdup.restype = C.c_int64
         L.oracle_markdup.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
                                      C.c_int32, C.c_int16, C.c_int, C.c_void_p]
@@ -102,3 +107,65 @@ def realign_scan(cons, cons_off, bases, quals, read_off, pairs):
                                               np.asarray(read_off, np.uint64))]
     _L().oracle_realign_scan(*[a.ctypes.data for a in arrs], pairs.ctypes.data, n, bi.ctypes.data, bs.ctypes.data)
     return bi[:n], bs[:n]
+
+
+FILTER_DEFAULTS = dict(has_region=0, ref_id=-1, left_pos=0, right_pos=0, mapq_min=0, min_len=0, max_len=2**31 - 1,
+                       trim_total=0, count_limit=2**31 - 1)
+
+
+def filter_keep(recs: np.ndarray, offs: np.ndarray, n: int, **opts) -> np.ndarray:
+    """Filter::runInternal's kept-record mask (algorithms/filter.cpp:205-249), input order."""
+    o = dict(FILTER_DEFAULTS, **opts)
+    recs = np.ascontiguousarray(recs, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs[:n], dtype=np.uint64)
+    keep = np.zeros(max(n, 1), dtype=np.uint8)
+    _L().oracle_filter(recs.ctypes.data, offs.ctypes.data, n, o["has_region"], o["ref_id"], o["left_pos"],
+                       o["right_pos"], o["mapq_min"], o["min_len"], o["max_len"], o["trim_total"], o["count_limit"],
+                       keep.ctypes.data)
+    return keep[:n].astype(bool)
+
+
+def parse_region(region: str, refs: list[tuple[str, int]]) -> dict | None:
+    """Filter::ParseRegionString (algorithms/filter.cpp:31-137) in Python; None where it fails."""
+    if not region:
+        return None
+    c1 = region.find(":")
+
+    def atoi(t: str) -> int:
+        import re
+        m = re.match(r"\s*[+-]?\d+", t)
+        return int(m.group(0)) if m else 0
+
+    if c1 < 0:
+        chrom, start, stop = region, 0, -1
+    else:
+        chrom = region[:c1]
+        dots = region.find("..", c1 + 1)
+        if dots < 0:
+            start = stop = atoi(region[c1 + 1:])
+        else:
+            start = atoi(region[c1 + 1:dots])
+            if region.find(":", dots + 1) >= 0:
+                return None
+            stop = atoi(region[dots + 2:])
+    ref = -1
+    for i, (nm, _) in enumerate(refs):
+        if nm == chrom:
+            ref = i
+    if ref < 0:
+        return None
+    ln = refs[ref][1]
+    if start >= ln or stop > ln:
+        return None
+    if stop == -1:
+        stop = ln
+    return dict(has_region=1, ref_id=ref, left_pos=start, right_pos=stop)
+
+
+def sort_name_perm(recs: np.ndarray, offs: np.ndarray, n: int) -> np.ndarray:
+    """Sort::ByName order (util/bamtools/Sort.h:67-90), equal names in input order."""
+    recs = np.ascontiguousarray(recs, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs[:n], dtype=np.uint64)
+    perm = np.zeros(max(n, 1), dtype=np.uint32)
+    _L().oracle_sort_name(recs.ctypes.data, offs.ctypes.data, n, perm.ctypes.data)
+    return perm[:n]

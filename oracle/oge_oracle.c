@@ -565,3 +565,54 @@ int oracle_realign_scan(const uint8_t *cons, const uint64_t *cons_off, const uin
     }
     return 0;
 }
+
+/* ---------------------------------------------------------------------------------------
+ * mergesort extras.
+ *
+ * Filter::runInternal (algorithms/filter.cpp:205-249): keep[i] = 1 for the records the module
+ * passes on, in input order; at most count_limit are kept (the loop stops pulling at the limit).
+ * len = BamAlignment::getLength() = l_seq; the region test is refID in [L, R], pos + len >= left,
+ * pos <= right (filter.cpp:230-236).  Returns the number kept. */
+uint64_t oracle_filter(const uint8_t *recs, const uint64_t *offs, uint64_t n, int has_region, int32_t ref_id,
+                       int32_t left_pos, int32_t right_pos, int32_t mapq_min, int32_t min_len, int32_t max_len,
+                       int32_t trim_total, uint64_t count_limit, uint8_t *keep) {
+    uint64_t count = 0, i;
+    for (i = 0; i < n; ++i) {
+        const uint8_t *r = recs + offs[i];
+        int32_t len = rdi32(r + OFF_LSEQ), mapq = r[13], ok;
+        ok = mapq >= mapq_min && len >= min_len && len <= max_len && len > trim_total;
+        if (has_region) {
+            int32_t ref = rdi32(r + OFF_REFID), pos = rdi32(r + OFF_POS);
+            ok = ok && ref >= ref_id && (int32_t)((uint32_t)pos + (uint32_t)len) >= left_pos && ref <= ref_id &&
+                 pos <= right_pos;
+        }
+        ok = ok && count < count_limit;
+        keep[i] = (uint8_t)ok;
+        count += ok;
+    }
+    return count;
+}
+
+/* Sort::ByName (util/bamtools/Sort.h:67-90): std::string < on the read names (unsigned bytewise,
+ * shorter prefix first); equal names keep input order here (the reference's std::sort leaves
+ * them in an implementation-defined order). */
+static const rec_set *g_name_set;
+static int name_cmp(uint32_t a, uint32_t b) {
+    const uint8_t *ra = REC(g_name_set, a), *rb = REC(g_name_set, b);
+    int la = ra[OFF_LNAME] - 1, lb = rb[OFF_LNAME] - 1, m = la < lb ? la : lb;
+    int c = memcmp(ra + OFF_NAME, rb + OFF_NAME, (size_t)m);
+    if (c) return c;
+    if (la != lb) return la < lb ? -1 : 1;
+    return a < b ? -1 : a > b;
+}
+static int name_cmp_q(const void *x, const void *y) { return name_cmp(*(const uint32_t *)x, *(const uint32_t *)y); }
+
+int oracle_sort_name(const uint8_t *recs, const uint64_t *offs, uint64_t n, uint32_t *perm) {
+    rec_set s = {recs, offs};
+    uint64_t i;
+    for (i = 0; i < n; ++i) perm[i] = (uint32_t)i;
+    g_name_set = &s;
+    qsort(perm, n, sizeof(uint32_t), name_cmp_q);
+    g_name_set = 0;
+    return 0;
+}

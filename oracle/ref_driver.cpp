@@ -7,6 +7,8 @@
 //   dedup      : FileReader -> MarkDuplicates -> sink (cmd/command_dedup.cpp:48-69, --nosplit)
 //   sortdedup  : FileReader -> ReadSorter -> MarkDuplicates -> sink (command_mergesort.cpp:68-117, -M --nosplit)
 //   realign    : FileReader -> LocalRealignment -> sink (cmd/command_localrealign.cpp:37-75)
+// sort / sortdedup take mergesort's -r region / -q mapq (a Filter between reader and sorter,
+// command_mergesort.cpp:82-92) and -b (sort by name, :104).
 // With -K k (k > 1) dedup / sortdedup run the reference's default split-by-chromosome chain
 // instead (cmd/command_dedup.cpp:71-106, command_mergesort.cpp:118-170):
 //   ... -> SplitByChromosome -> k x MarkDuplicates -> SortedMerge -> sink
@@ -24,6 +26,7 @@
 #include "algorithms/local_realignment.h"
 #include "algorithms/split_by_chromosome.h"
 #include "algorithms/sorted_merge.h"
+#include "algorithms/filter.h"
 #include "util/bam_serializer.h"
 #include "util/bgzf_output_stream.h"
 
@@ -62,7 +65,7 @@ protected:
 static void usage() {
     fprintf(stderr,
             "usage: ref_driver sort|dedup|sortdedup|realign [-v] [-t N] [-n N] [-T tmpdir] [-c level] [-K chains]\n"
-            "                  [-R ref.fa -L intervals] in.bam out.bam\n");
+            "                  [-r region] [-q mapq] [-b] [-R ref.fa -L intervals] in.bam out.bam\n");
     exit(2);
 }
 
@@ -71,7 +74,9 @@ int main(int argc, char **argv) {
     std::string mode = argv[1];
     bool verbose = false;
     int threads = 8, per_tmp = 500000, level = 6, chains = 0;
-    std::string tmpdir = "/tmp", ref, intervals;
+    std::string tmpdir = "/tmp", ref, intervals, region;
+    int mapq = -1;
+    bool byname = false;
     std::vector<std::string> pos;
     for (int i = 2; i < argc; i++) {
         std::string a = argv[i];
@@ -83,6 +88,9 @@ int main(int argc, char **argv) {
         else if (a == "-K" && i + 1 < argc) chains = atoi(argv[++i]);
         else if (a == "-R" && i + 1 < argc) ref = argv[++i];
         else if (a == "-L" && i + 1 < argc) intervals = argv[++i];
+        else if (a == "-r" && i + 1 < argc) region = argv[++i];
+        else if (a == "-q" && i + 1 < argc) mapq = atoi(argv[++i]);
+        else if (a == "-b") byname = true;
         else pos.push_back(a);
     }
     if (pos.size() != 2) usage();
@@ -125,10 +133,18 @@ int main(int argc, char **argv) {
     } else if (mode == "sort" || mode == "sortdedup") {
         ReadSorter sorter(tmpdir);
         MarkDuplicates md(tmpdir);
-        sorter.setSortBy(BamHeader::SORT_COORDINATE);
+        Filter filter;
+        sorter.setSortBy(byname ? BamHeader::SORT_QUERYNAME : BamHeader::SORT_COORDINATE);
         sorter.setCompressTempFiles(false);
         sorter.setAlignmentsPerTempfile(per_tmp);
-        reader.addSink(&sorter);
+        if (!region.empty() || mapq >= 0) {
+            if (!region.empty()) filter.setRegion(region);
+            if (mapq >= 0) filter.setQualityLimit(mapq);
+            reader.addSink(&filter);
+            filter.addSink(&sorter);
+        } else {
+            reader.addSink(&sorter);
+        }
         if (mode == "sortdedup") {
             sorter.addSink(&md);
             md.addSink(&sink);
