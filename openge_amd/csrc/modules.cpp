@@ -1,6 +1,7 @@
 // modules.cpp -- AlgorithmModule chain over the C ABI (see modules.h).
 #include "modules.h"
 
+#include <algorithm>
 #include <chrono>
 #include <climits>
 #include <cstdio>
@@ -176,6 +177,7 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
 
 int FileReader::runInternal(ChainContext &cc, ReadBatch &b) {
     if (files_.empty()) files_.push_back("stdin");
+    std::vector<uint64_t> file_end;  // record count after each file
     const char *rd = getenv("OGE_READER");
     if (files_.size() == 1 && files_[0] != "stdin" && files_[0] != "-" && !(rd && std::string(rd) == "host")) {
         const int r = read_device(cc, b, files_[0]);
@@ -197,19 +199,102 @@ int FileReader::runInternal(ChainContext &cc, ReadBatch &b) {
             for (size_t k = 0; k < f.offsets.size(); ++k) b.offs[k] = base + f.offsets[k];
             b.recs = std::move(f.data);
         } else {
-            if (f.ref_names != b.ref_names) {
-                fprintf(stderr, "openge: %s has a different sequence dictionary than %s\n", files_[i].c_str(), files_[0].c_str());
-                return -1;
-            }
+            if (f.header.sq.size() != b.header.sq.size() || f.ref_names != b.ref_names)  // read_stream_reader.h:116-124
+                fprintf(stderr, "Warning; sequence headers vary between files. Data may be corrupt.\n");
             const uint64_t base = b.recs.size();
             b.recs.insert(b.recs.end(), f.recs(), f.recs() + f.rec_bytes());
             for (uint64_t o : f.offsets) b.offs.push_back(base + o);
         }
+        file_end.push_back(b.offs.size());
     }
     b.n = b.offs.size();
     b.offs.push_back(b.recs.size());
     b.recs.resize(b.recs.size() + 16, 0);
     b.host_valid = true;
+    if (files_.size() > 1 && !sink_sorts()) return merge_inputs(b, file_end, cc.threads);
+    return 0;
+}
+
+// True when the records go straight (or through a Filter) into a ReadSorter: the sort then makes
+// the MultiReader's interleaving irrelevant (records it would order differently are full ByPosition
+// ties, ordered by heap address in the reference).
+bool FileReader::sink_sorts() const {
+    const AlgorithmModule *m = sink_;
+    if (m && dynamic_cast<const Filter *>(m)) m = m->sink();
+    return m && dynamic_cast<const ReadSorter *>(m);
+}
+
+// Sort::ByPosition (util/bamtools/Sort.h:116-133) down to the flag, as a three-way compare; refID
+// -1 sorts last and is equivalent to every other refID -1 record.
+static int bypos_cmp(const uint8_t *a, const uint8_t *b) {
+    const int32_t ra = oge_rd_i32(a + 4), rb = oge_rd_i32(b + 4);
+    if (ra == -1 || rb == -1) return (ra == -1) - (rb == -1);
+    if (ra != rb) return ra < rb ? -1 : 1;
+    const int32_t pa = oge_rd_i32(a + 8), pb = oge_rd_i32(b + 8);
+    if (pa != pb) return pa < pb ? -1 : 1;
+    const uint16_t fa = oge_rd_u16(a + 18), fb = oge_rd_u16(b + 18);
+    const bool va = fa & 0x10, vb = fb & 0x10;
+    if (va != vb) return va ? 1 : -1;
+    const int la = a[12] - 1, lb = b[12] - 1;
+    const int c = memcmp(a + 36, b + 36, (size_t)std::min(la, lb));
+    if (c) return c < 0 ? -1 : 1;
+    if (la != lb) return la < lb ? -1 : 1;
+    if (fa != fb) return fa < fb ? -1 : 1;
+    return 0;
+}
+
+// MultiReader::read (util/read_stream_reader.h:132-153): the inputs are interleaved by a
+// std::multiset of one head per file ordered by ByPosition, so equivalent heads leave in insertion
+// order.  A binary heap keyed on (ByPosition, insertion number) reproduces it exactly, for sorted
+// and unsorted inputs alike (the reference's final address tie-break is replaced by insertion
+// order, Q10).  The arena is then rewritten in that order.
+int FileReader::merge_inputs(ReadBatch &b, const std::vector<uint64_t> &file_end, int threads) {
+    struct Head {
+        uint64_t rec, end, seq;
+    };
+    const uint8_t *base = b.recs.data();
+    auto later = [&](const Head &x, const Head &y) {  // heap "less": x leaves after y
+        const int c = bypos_cmp(base + b.offs[x.rec], base + b.offs[y.rec]);
+        return c ? c > 0 : x.seq > y.seq;
+    };
+    std::vector<Head> heap;
+    uint64_t seq = 0, begin = 0;
+    for (uint64_t e : file_end) {  // MultiReader::open: one read from each file, in file order
+        if (e > begin) heap.push_back({begin, e, seq++});
+        begin = e;
+    }
+    std::make_heap(heap.begin(), heap.end(), later);
+    std::vector<uint64_t> order;
+    order.reserve(b.n);
+    while (!heap.empty()) {
+        std::pop_heap(heap.begin(), heap.end(), later);
+        Head h = heap.back();
+        heap.pop_back();
+        order.push_back(h.rec);
+        if (++h.rec < h.end) {
+            h.seq = seq++;
+            heap.push_back(h);
+            std::push_heap(heap.begin(), heap.end(), later);
+        }
+    }
+    bytevec out;
+    out.resize(b.recs.size());
+    std::vector<uint64_t> offs(b.n + 1);
+    for (uint64_t k = 0; k < b.n; ++k) offs[k + 1] = offs[k] + (b.offs[order[k] + 1] - b.offs[order[k]]);
+    const uint64_t shift = b.offs[0];  // keep the reader's leading bytes (header) where they were
+    const int T = std::max(1, threads);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < T; ++t)
+        ts.emplace_back([&, t]() {
+            for (uint64_t k = (uint64_t)t; k < b.n; k += (uint64_t)T)
+                memcpy(out.data() + shift + offs[k], base + b.offs[order[k]], offs[k + 1] - offs[k]);
+        });
+    for (auto &t : ts) t.join();
+    memcpy(out.data(), base, shift);
+    memset(out.data() + shift + offs[b.n], 0, out.size() - shift - offs[b.n]);
+    for (auto &o : offs) o += shift;
+    b.recs = std::move(out);
+    b.offs = std::move(offs);
     return 0;
 }
 

@@ -59,6 +59,7 @@ public:
     static void setVerbose(bool v) { verbose_ = v; }
     static bool isVerbose() { return verbose_; }
     const char *name() const { return name_; }
+    AlgorithmModule *sink() const { return sink_; }
 
 protected:
     explicit AlgorithmModule(const char *name) : name_(name) {}
@@ -70,9 +71,10 @@ protected:
     friend class ReadSorter;
 };
 
-// FileReader (algorithms/file_reader.cpp:29-63): BAM input(s).  Several inputs are concatenated
-// in the order given (the reference's MultiReader interleaves them by position; for mergesort the
-// sort makes both equivalent).
+// FileReader (algorithms/file_reader.cpp:29-63): BAM input(s).  Several inputs are interleaved as
+// the reference's MultiReader does (a ByPosition merge of the file heads,
+// util/read_stream_reader.h:132-153) unless a ReadSorter follows, which makes the interleaving
+// irrelevant; the header is the first file's (a differing dictionary only warns, :116-124).
 class FileReader : public AlgorithmModule {
 public:
     FileReader() : AlgorithmModule("FileReader") {}
@@ -84,6 +86,8 @@ protected:
     // One BGZF file straight into HBM: inflate + record walk on the GPU (returns 1 when the host
     // reader should take over, e.g. to report a format error with the reference's message).
     int read_device(ChainContext &cc, ReadBatch &b, const std::string &path);
+    bool sink_sorts() const;
+    static int merge_inputs(ReadBatch &b, const std::vector<uint64_t> &file_end, int threads);
     std::vector<std::string> files_;
 };
 

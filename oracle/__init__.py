@@ -169,3 +169,37 @@ def sort_name_perm(recs: np.ndarray, offs: np.ndarray, n: int) -> np.ndarray:
     perm = np.zeros(max(n, 1), dtype=np.uint32)
     _L().oracle_sort_name(recs.ctypes.data, offs.ctypes.data, n, perm.ctypes.data)
     return perm[:n]
+
+
+def _bypos_key(recs: np.ndarray, off: int):
+    """Sort::ByPosition (util/bamtools/Sort.h:116-133) down to the flag; refID -1 -> one equivalence class."""
+    o = int(off)
+    ref = int.from_bytes(recs[o + 4:o + 8].tobytes(), "little", signed=True)
+    if ref == -1:
+        return (1,)
+    pos = int.from_bytes(recs[o + 8:o + 12].tobytes(), "little", signed=True)
+    flag = int(recs[o + 18]) | int(recs[o + 19]) << 8
+    name = recs[o + 36:o + 36 + int(recs[o + 12]) - 1].tobytes()
+    return (0, ref, pos, (flag >> 4) & 1, name, flag)
+
+
+def multireader_order(recs: np.ndarray, offs_per_file: list[np.ndarray]) -> list[tuple[int, int]]:
+    """MultiReader::open/read (util/read_stream_reader.h:24-61,132-153): the files' heads in a
+    std::multiset ordered by ByPosition; equivalent heads leave in insertion order (the reference's
+    address tie-break among full ties is replaced by insertion order).
+    -> (file, record index in file) in output order.  Pure Python: small cases only."""
+    import heapq
+    heap, seq = [], 0
+    for f, offs in enumerate(offs_per_file):
+        if len(offs):
+            heap.append((_bypos_key(recs, offs[0]), seq, f, 0))
+            seq += 1
+    heapq.heapify(heap)
+    out = []
+    while heap:
+        _, _, f, i = heapq.heappop(heap)
+        out.append((f, i))
+        if i + 1 < len(offs_per_file[f]):
+            heapq.heappush(heap, (_bypos_key(recs, offs_per_file[f][i + 1]), seq, f, i + 1))
+            seq += 1
+    return out

@@ -65,7 +65,7 @@ protected:
 static void usage() {
     fprintf(stderr,
             "usage: ref_driver sort|dedup|sortdedup|realign [-v] [-t N] [-n N] [-T tmpdir] [-c level] [-K chains]\n"
-            "                  [-r region] [-q mapq] [-b] [-R ref.fa -L intervals] in.bam out.bam\n");
+            "                  [-r region] [-q mapq] [-b] [-R ref.fa -L intervals] in.bam [in2.bam ...] out.bam\n");
     exit(2);
 }
 
@@ -93,7 +93,7 @@ int main(int argc, char **argv) {
         else if (a == "-b") byname = true;
         else pos.push_back(a);
     }
-    if (pos.size() != 2) usage();
+    if (pos.size() < 2) usage();  // in.bam [in2.bam ...] out.bam: several inputs go through MultiReader
     tmpdir += "/";
 
     OGEParallelismSettings::setNumberThreads(threads);
@@ -103,9 +103,9 @@ int main(int argc, char **argv) {
 
     FileReader reader;
     reader.setLoadStringData(false);
-    reader.addFile(pos[0]);
+    for (size_t k = 0; k + 1 < pos.size(); ++k) reader.addFile(pos[k]);
     CaptureSink sink;
-    sink.filename = pos[1];
+    sink.filename = pos.back();
     sink.level = level;
 
     if ((mode == "dedup" || mode == "sortdedup") && chains > 1) {

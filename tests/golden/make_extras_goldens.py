@@ -6,6 +6,8 @@ oracle/Makefile.ref).  Per case it runs
   sort -r REGION / -q MAPQ / both           (mergesort -r/-q)
   sortdedup -v -r REGION -q MAPQ            (mergesort -M --nosplit -r/-q)
   sort -b                                   (mergesort -b, one temp run)
+  dedup -v part0 part1 part2                (several inputs through MultiReader; unsorted and
+                                             sorted parts)
 and stores: for the filtered sorts the input index of every output record (perm) and digests of
 the output record stream; for dedup the 0x400 indices; for -b the output name sequence and a digest
 of the output with every run of equal names canonicalised (records sorted bytewise), since the
@@ -76,9 +78,44 @@ def canonical_name_stream(recs, offs) -> tuple[str, str]:
 
 
 def run(driver, mode, src, dst, *extra):
-    r = subprocess.run([str(driver), mode, *extra, "-T", str(dst.parent), str(src), str(dst)], capture_output=True,
+    srcs = [str(x) for x in src] if isinstance(src, (list, tuple)) else [str(src)]
+    r = subprocess.run([str(driver), mode, *extra, "-T", str(dst.parent), *srcs, str(dst)], capture_output=True,
                        timeout=600)
     return r.returncode
+
+
+MULTI_CASES = ["yhet208", "mix3k", "c2_20k"]
+MULTI_K = 3
+
+
+def split_inputs(tmp: Path, tag: str, header: str, refs, recs, offs, order) -> list[Path]:
+    """Records order[j] for j % K == k go to file k (each file keeps the order given)."""
+    paths = []
+    for k in range(MULTI_K):
+        path = tmp / f"{tag}.part{k}.bam"
+        bamutil.write_bam_py(path, header, refs, [bamutil.rec_bytes(recs, offs[i]) for i in order[k::MULTI_K]])
+        paths.append(path)
+    return paths
+
+
+def multi_goldens(driver, tmp: Path, name: str, src: Path, meta: dict, arrays: dict) -> None:
+    """MultiReader (util/read_stream_reader.h:132-153): dedup -v over K parts of the unsorted input and
+    over K parts of the reference-sorted input; output order (input index) and 0x400 indices."""
+    hdr, refs, irecs, ioffs = bamutil.read_bam(src)
+    s_path = tmp / f"{name}.msorted.bam"
+    assert run(driver, "sort", src, s_path) == 0
+    _, _, srecs, soffs = bamutil.read_bam(s_path)
+    sorted_order = bamutil.perm_of(srecs, soffs, irecs, ioffs)
+    meta["multi"] = {}
+    for tag, order in (("unsorted", np.arange(len(ioffs))), ("sorted", sorted_order)):
+        parts = split_inputs(tmp, f"{name}.{tag}", hdr, refs, irecs, ioffs, order)
+        dst = tmp / f"{name}.{tag}.multi.bam"
+        assert run(driver, "dedup", parts, dst, "-v") == 0
+        h, _, r, o = bamutil.read_bam(dst)
+        arrays[f"multi_{tag}_order"] = bamutil.perm_of(r, o, irecs, ioffs)
+        idx = np.nonzero(bamutil.flags_of(r, o) & 0x400)[0].astype(np.uint32)
+        arrays[f"multi_{tag}_dup"] = idx
+        meta["multi"][tag] = {"k": MULTI_K, "n_out": len(o), "n_dup": int(len(idx)), "header": h}
 
 
 def main():
@@ -113,6 +150,8 @@ def main():
             h, _, r, o = bamutil.read_bam(dst)
             hn, hc = canonical_name_stream(r, o)
             meta["byname"] = {"n_out": len(o), "header": h, "names_sha256": hn, "canonical_sha256": hc}
+            if name in MULTI_CASES:
+                multi_goldens(driver, tmp, name, src, meta, arrays)
             np.savez_compressed(OUT / f"{name}.npz", **arrays)
             (OUT / f"{name}.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
             print(name, {k: v["n_out"] for k, v in meta["filters"].items()}, "dups", meta["sortdedup"]["r_range_q30"]["n_dup"])

@@ -114,3 +114,26 @@ def test_oracle_filter_drops_empty_seq_and_honours_limits(built):
     keep = oracle.filter_keep(rr, oo, 60, mapq_min=30, count_limit=5)
     want = [i for i in range(60) if i % 3 and i % 70 >= 30][:5]
     assert np.nonzero(keep)[0].tolist() == want
+
+
+MULTI = ["yhet208", "mix3k", "c2_20k"]
+
+
+@pytest.mark.parametrize("name", MULTI)
+@pytest.mark.parametrize("tag", ["unsorted", "sorted"])
+def test_oracle_multireader_dedup_matches_reference(built, name, tag):
+    """dedup -v over 3 input files: MultiReader's interleaving, then MarkDuplicates on that stream."""
+    case, meta, arrays = load_extras(name)
+    g = meta["multi"][tag]
+    k = g["k"]
+    if tag == "unsorted":
+        order = np.arange(case.n)
+    else:
+        order = oracle.sort_perm(case.recs, case.offs, case.n)
+    parts = [order[f::k] for f in range(k)]
+    merged = oracle.multireader_order(case.recs, [case.offs[:-1][p] for p in parts])
+    out = np.array([parts[f][i] for f, i in merged], dtype=np.uint32)
+    assert np.array_equal(out, arrays[f"multi_{tag}_order"])
+    so = case.offs[:-1][out]
+    dup, _ = oracle.markdup(case.recs, so, case.n, case.header)
+    assert np.array_equal(final_dup_indices(case, so, dup), arrays[f"multi_{tag}_dup"])
