@@ -237,8 +237,13 @@ def main():
             del out, off
             return k
 
+    warmup_ms = []  # first-call costs (workspace growth, code-object load) stay out of the timed steps
     for _ in range(args.warmup):
+        torch.cuda.synchronize(dev)
+        tw = time.perf_counter()
         step()
+        torch.cuda.synchronize(dev)
+        warmup_ms.append(round((time.perf_counter() - tw) * 1e3, 2))
     shard_t.clear()
     stage_tot = {s: 0.0 for s in STAGES}
     if world > 1:
@@ -298,6 +303,7 @@ def main():
             out["pipeline"] = {"algorithmic_bytes": pipe_bytes, "achieved": round(pipe_gbs, 1), "unit": "GB/s",
                                "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)}
             out["stages_ms"] = stages_ms
+            out["warmup_ms"] = warmup_ms
             if not args.no_realign:
                 out["realign"] = realign_leg(ctx, args.realign_intervals)
             if not args.no_cpu_baseline:

@@ -432,10 +432,18 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
         if (!rc) rc = oge_gather_records_dev(cc.ctx, b.d_recs, b.d_offs, (uint32_t *)perm, b.n, (uint8_t *)out, (uint64_t *)out_off);
     }
     if (!rc) rc = oge_ctx_sync(cc.ctx);
-    if (verbose_)
+    if (verbose_) {
         fprintf(stderr, "[openge] ReadSorter: host->device %.3f s, device pipeline %.3f s\n",
                 std::chrono::duration<double>(t1 - t0).count(),
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
+        std::string st;  // HIP-event stage times of the device pipeline (ms)
+        for (const char *s : {"input_pass", "sort_radix", "sort_ties", "meta_gather", "md_matejoin", "md_pairs", "md_frags",
+                              "md_apply", "gather_offsets", "gather_records", "name_sort"}) {
+            double ms = -1;
+            if (!oge_ctx_timing(cc.ctx, s, &ms) && ms >= 0) st += std::string(" ") + s + "=" + std::to_string(ms).substr(0, 6);
+        }
+        fprintf(stderr, "[openge] ReadSorter stages (ms):%s\n", st.c_str());
+    }
     oge_dev_free(cc.ctx, perm);
     if (rc) {
         oge_dev_free(cc.ctx, out);

@@ -18,13 +18,17 @@ th = int(sys.argv[3]) if len(sys.argv) > 3 else 16
 out.mkdir(parents=True, exist_ok=True)
 src = out / f"c2_{n}.bam"
 if not src.exists():
+    t = time.perf_counter()
     p = L.synth_params(n // 2, preset="c2", seed=1234)
     recs, offs, hdr = L.synth_host(p, threads=th)
+    print(f"synth {n} reads in {time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
     L.write_bam(src, hdr, recs, offs, n, level=6, threads=th)
+    print(f"wrote {src} ({src.stat().st_size / 1e9:.2f} GB) in {time.perf_counter() - t:.1f} s", file=sys.stderr,
+          flush=True)
     del recs, offs
 t0 = time.perf_counter()
 r = subprocess.run([str(ROOT / "openge_amd/openge"), "mergesort", "-M", "--nopg", "-v", "-t", str(th), str(src), "-o",
                     str(out / "sorted_dedup.bam")], capture_output=True, text=True)
 dt = time.perf_counter() - t0
 print(json.dumps({"reads": n, "seconds": round(dt, 3), "mreads_per_s": round(n / dt / 1e6, 3), "threads": th,
-                  "rc": r.returncode, "stderr_tail": r.stderr[-600:], "in_bytes": src.stat().st_size}))
+                  "rc": r.returncode, "stderr_tail": r.stderr[-1500:], "in_bytes": src.stat().st_size}))
