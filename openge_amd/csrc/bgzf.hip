@@ -626,9 +626,6 @@ __global__ void k_fix_bins(uint8_t *__restrict__ recs, const uint64_t *__restric
 
 }  // namespace
 
-int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
-                          const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
-                          const RecMeta *smeta, const uint8_t *d_dup);
 
 extern "C" uint64_t oge_bgzf_bound(uint64_t n) { return ((n + kPay - 1) / kPay) * (uint64_t)kSlot; }
 

@@ -15,13 +15,10 @@ unsigned int *oge_sort_counts(oge_ctx *ctx);
 int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
                       bool keys_ready, uint64_t **kout, uint32_t **vout, const RecMeta *meta_in = nullptr,
                       RecMeta *meta_out = nullptr);
-int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
-                          const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
-                          const RecMeta *smeta, const uint8_t *d_dup);
 int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, const char *name, RecMeta **meta,
                         OgeRgTable *rg);
 int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
-                       const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out);
+                       const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out, uint64_t *d_desc, bool *desc_ok);
 int oge_meta_gather(oge_ctx *ctx, const RecMeta *in, const uint32_t *perm, uint64_t n, RecMeta *out);
 int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
                     uint8_t *d_dup, int apply, uint64_t *n_dup_out);
@@ -320,10 +317,13 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
     if (rc) return rc;
     if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_perm, v, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
     uint64_t nd = 0;
-    rc = oge_markdup_finish(ctx, (uint8_t *)d_recs, d_off, n, opts, meta, dd, 0, &nd);
+    uint64_t *desc = (uint64_t *)ctx->ws("sm_desc", (n + 1) * 8);
+    if (!desc) return OGE_ERR_HIP;
+    bool desc_ok = false;
+    rc = oge_markdup_finish(ctx, (uint8_t *)d_recs, d_off, n, opts, meta, dd, 0, &nd, desc, &desc_ok);
     if (rc) return rc;
     if (n_dup_out) *n_dup_out = nd;
-    return oge_gather_with_sizes(ctx, d_recs, d_off, v, k, n, d_out, d_out_off, meta, dd);
+    return oge_gather_with_sizes(ctx, d_recs, d_off, v, k, n, d_out, d_out_off, meta, dd, desc_ok ? desc : nullptr);
 }
 
 }  // extern "C"

@@ -53,10 +53,6 @@ __global__ void k_keep_perm(const uint32_t *__restrict__ keep, const uint32_t *_
 
 }  // namespace
 
-int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
-                          const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
-                          const RecMeta *smeta, const uint8_t *d_dup);
-
 // keep[] (n flags, already written on the stream) -> the first `limit` kept records, in order.
 static int compact_kept(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, uint32_t *keep,
                         uint64_t limit, uint8_t *d_out, uint64_t *d_out_off, uint64_t *n_out) {

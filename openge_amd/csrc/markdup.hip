@@ -311,25 +311,35 @@ __global__ __launch_bounds__(kT) void k_any(const uint8_t *__restrict__ dup, uin
     if (__ballot(i < n && dup[i]) && (threadIdx.x & 63) == 0) atomicOr(any, 1u);
 }
 
+// desc (optional, output order): the record gather's 8-byte descriptor -- source offset (40 bits),
+// bin (16), final FLAG high byte with 0x400 applied (8) -- so the gather reads 8 bytes per record
+// instead of the 64-byte summary and the dup byte.  A source offset past 40 bits sets *desc_ovf and
+// the caller gathers from the summaries instead.
 __global__ __launch_bounds__(kT) void k_apply(uint8_t *__restrict__ recs, const uint64_t *__restrict__ off, uint64_t n,
                                                const RecMeta *__restrict__ meta, uint8_t *__restrict__ dup, int apply,
                                                int compat, const unsigned int *__restrict__ any,
-                                               unsigned long long *__restrict__ ndup) {
+                                               unsigned long long *__restrict__ ndup, uint64_t *__restrict__ desc,
+                                               unsigned int *__restrict__ desc_ovf) {
     __shared__ uint32_t wsum[kT / 64];
     uint32_t mine = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kT) {
         const uint64_t m = meta[i].m;
         const uint8_t d = compat ? (uint8_t)(i == 0 && *any) : dup[i];
+        const uint8_t hi = (uint8_t)(m >> 40);
+        uint8_t nh = hi;
         if (!(m & OGE_M_PRIMARY)) {
             dup[i] = 2;
         } else {
             dup[i] = d;
             mine += d;
-            if (apply) {  // FLAG bit 0x400 is bit 2 of the flag's high byte (record byte 19)
-                const uint8_t hi = (uint8_t)(m >> 40);
-                const uint8_t nh = d ? (uint8_t)(hi | 0x04) : (uint8_t)(hi & ~0x04);
-                if (nh != hi) recs[off[i] + OGE_OFF_FLAG + 1] = nh;
-            }
+            // FLAG bit 0x400 is bit 2 of the flag's high byte (record byte 19)
+            nh = d ? (uint8_t)(hi | 0x04) : (uint8_t)(hi & ~0x04);
+            if (apply && nh != hi) recs[off[i] + OGE_OFF_FLAG + 1] = nh;
+        }
+        if (desc) {
+            const uint64_t src = meta[i].src;
+            if (src >> 40) atomicOr(desc_ovf, 1u);
+            desc[i] = (src & ((1ull << 40) - 1)) | ((m >> 48) << 40) | ((uint64_t)nh << 56);
         }
     }
     // one atomic per block: per-thread counts -> wave sums -> block sum
@@ -400,7 +410,9 @@ int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, 
 // dup[i] receives 1/0/2 (see oge_markdup); with apply, FLAG 0x400 is rewritten in place at
 // recs + off[i].
 int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
-                       const oge_markdup_opts *opts, const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out) {
+                       const oge_markdup_opts *opts, const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out,
+                       uint64_t *d_desc, bool *desc_ok) {
+    if (desc_ok) *desc_ok = false;
     int16_t maxlib = opts->unknown_lib;
     for (int32_t g = 0; g < opts->n_rg; ++g) maxlib = std::max(maxlib, opts->rg_lib[g]);
     if (opts->unknown_lib < 0) return oge_fail(ctx, OGE_ERR_ARG, "markdup: negative library id");
@@ -547,13 +559,16 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
         OGE_LAUNCH_CHECK(ctx);
     }
     hipLaunchKernelGGL(k_apply, dim3(std::min<uint32_t>(nb, 2048u)), dim3(kT), 0, ctx->stream, d_recs, d_off, n, meta, d_dup, apply,
-                       opts->compat_nonverbose_index, (const unsigned int *)(cnt + 1), ndup);
+                       opts->compat_nonverbose_index, (const unsigned int *)(cnt + 1), ndup, d_desc, cnt + 3);
     OGE_LAUNCH_CHECK(ctx);
     ctx->end_stage(t);
     unsigned long long h = 0;
+    unsigned int ovf = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&h, ndup, 8, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&ovf, cnt + 3, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     *n_dup_out = h;
+    if (desc_ok) *desc_ok = d_desc && !ovf;
     return OGE_OK;
 }
 
@@ -574,7 +589,7 @@ int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64
     rc = oge_input_pass(ctx, a);
     if (rc) return rc;
     ctx->end_stage(t);
-    return oge_markdup_finish(ctx, d_recs, d_off, n, opts, meta, d_dup, apply, n_dup_out);
+    return oge_markdup_finish(ctx, d_recs, d_off, n, opts, meta, d_dup, apply, n_dup_out, nullptr, nullptr);
 }
 
 namespace {

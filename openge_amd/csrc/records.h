@@ -59,6 +59,8 @@ struct OgePassArgs {
     const uint32_t *perm;
     const RecMeta *smeta;    // summaries in OUTPUT order (bin, flags, src offset), optional
     const uint8_t *dup;      // output order: 1 sets 0x400, 0 clears it (primary records only)
+    const uint64_t *desc;    // output order, replaces smeta + dup when given: src (40 bits) | bin << 40 |
+                             // final FLAG high byte << 56 (written by k_apply)
     uint8_t *out;
     const uint64_t *out_off; // n+1 output offsets
 };
@@ -66,3 +68,7 @@ struct OgePassArgs {
 struct oge_ctx;
 int oge_input_pass(oge_ctx *ctx, const OgePassArgs &a);
 int oge_gather_pass(oge_ctx *ctx, const OgePassArgs &a);
+// Output offsets (from the sorted keys' size payload, or from the records) + the record gather.
+int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
+                          const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
+                          const RecMeta *smeta, const uint8_t *d_dup, const uint64_t *desc = nullptr);

@@ -319,7 +319,9 @@ __device__ __forceinline__ GChunk gchunk_plan(const uint32_t *sdw, uint32_t cnt,
     return g;
 }
 
-template <bool SMETA>
+// MODE 0: source = off[perm[k]], bin/flags parsed from the record; 1: from the output-order summaries
+// (smeta) and dup[]; 2: from the 8-byte descriptors (desc).
+template <int MODE>
 __global__ __launch_bounds__(kT) void k_gather16(OgePassArgs a) {
     __shared__ uint32_t sd[kT / 64][65];   // per wave: output start of record j relative to the batch
     __shared__ uint64_t ss[kT / 64][64];   // source offset of record j
@@ -337,7 +339,13 @@ __global__ __launch_bounds__(kT) void k_gather16(OgePassArgs a) {
             uint64_t s;
             uint32_t bin, fhi;
             bool primary;
-            if (SMETA) {
+            if (MODE == 2) {
+                const uint64_t D = a.desc[rec];
+                s = D & ((1ull << 40) - 1);
+                bin = (uint32_t)(D >> 40) & 0xffff;
+                fhi = (uint32_t)(D >> 56);
+                primary = false;  // 0x400 already applied in the descriptor
+            } else if (MODE == 1) {
                 const RecMeta M = a.smeta[rec];
                 s = M.src;
                 bin = (uint32_t)(M.m >> 48);
@@ -426,10 +434,12 @@ int oge_gather_pass(oge_ctx *ctx, const OgePassArgs &a) {
         return (e && *e) ? std::max<uint64_t>(256, strtoull(e, nullptr, 10)) : 131072ull;
     }();
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, 64 * (kT / 64)), cap);
-    if (a.smeta)
-        hipLaunchKernelGGL(k_gather16<true>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
+    if (a.desc)
+        hipLaunchKernelGGL(k_gather16<2>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
+    else if (a.smeta)
+        hipLaunchKernelGGL(k_gather16<1>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
     else
-        hipLaunchKernelGGL(k_gather16<false>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
+        hipLaunchKernelGGL(k_gather16<0>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
     OGE_LAUNCH_CHECK(ctx);
     return OGE_OK;
 }

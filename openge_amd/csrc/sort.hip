@@ -367,7 +367,7 @@ unsigned int *oge_sort_counts(oge_ctx *ctx) { return (unsigned int *)ctx->ws("so
 // smeta (output-order summaries) and dup are optional (see OgePassArgs).
 int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
                           const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
-                          const RecMeta *smeta, const uint8_t *d_dup) {
+                          const RecMeta *smeta, const uint8_t *d_dup, const uint64_t *desc) {
     OgeStageTimer *t = ctx->begin_stage("gather_offsets");
     if (sorted_keys)
         hipLaunchKernelGGL(k_sizes_from_keys, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, sorted_keys, n,
@@ -388,8 +388,9 @@ int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d
     a.n = n;
     a.out = d_out;
     a.out_off = d_out_off;
-    a.smeta = smeta;
-    a.dup = d_dup;
+    a.smeta = desc ? nullptr : smeta;
+    a.dup = desc ? nullptr : d_dup;
+    a.desc = desc;
     rc = oge_gather_pass(ctx, a);
     if (rc) return rc;
     ctx->end_stage(t);
