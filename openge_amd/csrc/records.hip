@@ -31,14 +31,13 @@
 namespace {
 
 constexpr int kT = 256;
-constexpr uint32_t kTileRecs = 256;
-constexpr uint32_t kLdsCap = 76 * 1024;
 
 // --- byte readers over the LDS tile or global memory (x = absolute byte index) ---
 struct LdsRd {
     const uint8_t *b;  // LDS tile base (16-byte aligned)
     __device__ __forceinline__ uint32_t u8(uint64_t x) const { return b[x]; }
     __device__ __forceinline__ uint32_t a32(uint64_t x) const { return *(const uint32_t *)(b + x); }
+    __device__ __forceinline__ uint4 a128(uint64_t x) const { return *(const uint4 *)(b + x); }
     __device__ __forceinline__ uint32_t u32(uint64_t x) const {
         const uint32_t sh = (uint32_t)(x & 3) * 8;
         const uint32_t lo = a32(x & ~3ull);
@@ -49,8 +48,17 @@ struct GlbRd {
     const uint8_t *b;  // arena base
     __device__ __forceinline__ uint32_t u8(uint64_t x) const { return b[x]; }
     __device__ __forceinline__ uint32_t a32(uint64_t x) const { return *(const uint32_t *)(b + x); }
+    __device__ __forceinline__ uint4 a128(uint64_t x) const { return *(const uint4 *)(b + x); }
     __device__ __forceinline__ uint32_t u32(uint64_t x) const { return oge_ldu32(b + x); }
 };
+
+// getScore's per-byte term (b >= 15 ? b : 0) summed over the 4 bytes of w, plus acc: a SWAR
+// ">= 15" mask (no carries cross bytes: low 7 bits + 0x71 <= 0xf0; bytes >= 128 pass by their top
+// bit) and one v_sad_u8 against zero.
+__device__ __forceinline__ uint32_t qsum4(uint32_t w, uint32_t acc) {
+    const uint32_t ge = (((w & 0x7f7f7f7fu) + 0x71717171u) | w) & 0x80808080u;
+    return __builtin_amdgcn_sad_u8(w & ((ge >> 7) * 0xffu), 0u, acc);
+}
 
 // FNV-1a (64-bit) over the pair key, finished with the MurmurHash3 fmix64 avalanche so every bit
 // of the 48 kept is usable as a radix digit (the mate join sorts by as many bits as fit)
@@ -111,11 +119,10 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
         const uint64_t q0 = c + 4 * nc + (lseq + 1) / 2, q1 = q0 + lseq;
         uint32_t sc = 0;
         uint64_t x = q0;
-        for (; x < q1 && (x & 3); ++x) { const uint32_t b = rd.u8(x); sc += b >= 15 ? b : 0; }
-        for (; x + 4 <= q1; x += 4) {
-            const uint32_t w = rd.a32(x);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) { const uint32_t b = (w >> (8 * s)) & 0xff; sc += b >= 15 ? b : 0; }
+        for (; x < q1 && (x & 15); ++x) { const uint32_t b = rd.u8(x); sc += b >= 15 ? b : 0; }
+        for (; x + 16 <= q1; x += 16) {  // 16-byte aligned reads (LDS tile and arena are 16-aligned)
+            const uint4 v = rd.a128(x);
+            sc = qsum4(v.w, qsum4(v.z, qsum4(v.y, qsum4(v.x, sc))));
         }
         for (; x < q1; ++x) { const uint32_t b = rd.u8(x); sc += b >= 15 ? b : 0; }
         m |= (uint64_t)(uint16_t)sc;
@@ -208,26 +215,44 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
     a.meta[i] = M;
 }
 
-template <bool META, bool KEYS>
-__global__ __launch_bounds__(kT) void k_input_pass(OgePassArgs a) {
+// NT records per tile and NT threads per block; the tile window is NT x 304 bytes of LDS (76 KB at
+// NT = 256: 2 blocks per CU; 38 KB at 128: 4 blocks of 2 waves, so staging and parsing of different
+// blocks overlap more finely).
+template <bool META, bool KEYS, int NT>
+__global__ __launch_bounds__(NT) void k_input_pass(OgePassArgs a) {
+    constexpr uint32_t kTileRecs = NT;
+    constexpr uint32_t kLdsCap = NT * 304;
     __shared__ uint4 tile[kLdsCap / 16];
     __shared__ uint64_t tb[2];
     const uint8_t *lds = (const uint8_t *)tile;
-    for (uint64_t r0 = (uint64_t)blockIdx.x * kTileRecs; r0 < a.n; r0 += (uint64_t)gridDim.x * kTileRecs) {
+    // Tile window = [first record, next tile's first record); only a cache: every record is checked
+    // against it and parsed from global memory when it is not inside.  The window bounds (thread 0)
+    // and each thread's record offset for tile t+1 are loaded while tile t's LDS-DMA is in flight,
+    // so no tile starts with a dependent global-load round trip.
+    auto window = [&](uint64_t r0, uint64_t &wb0, uint64_t &wb1) {
+        const uint64_t r1 = (a.n - r0) < kTileRecs ? a.n : r0 + kTileRecs;
+        wb0 = a.off[r0] & ~15ull;
+        uint64_t e;
+        if (r1 < a.n) {
+            e = a.off[r1];
+        } else {
+            const uint64_t last = a.off[r1 - 1];
+            e = last + 4 + oge_ldu32(a.recs + last);
+        }
+        wb1 = (e > wb0 && e - wb0 <= kLdsCap) ? e : wb0;  // empty window: parse from global
+    };
+    const uint64_t stride = (uint64_t)gridDim.x * kTileRecs;
+    uint64_t r0 = (uint64_t)blockIdx.x * kTileRecs;
+    uint64_t wb0 = 0, wb1 = 0, my_off = 0;
+    if (r0 < a.n) {
+        if (threadIdx.x == 0) window(r0, wb0, wb1);
+        if (r0 + threadIdx.x < a.n) my_off = a.off[r0 + threadIdx.x];
+    }
+    for (; r0 < a.n; r0 += stride) {
         const uint64_t r1 = (a.n - r0) < kTileRecs ? a.n : r0 + kTileRecs;
         if (threadIdx.x == 0) {
-            // window = [first record, next tile's first record); only a cache: every record is
-            // checked against it below and parsed from global memory when it is not inside
-            const uint64_t b0 = a.off[r0] & ~15ull;
-            uint64_t e;
-            if (r1 < a.n) {
-                e = a.off[r1];
-            } else {
-                const uint64_t last = a.off[r1 - 1];
-                e = last + 4 + oge_ldu32(a.recs + last);
-            }
-            tb[0] = b0;
-            tb[1] = (e > b0 && e - b0 <= kLdsCap) ? e : b0;  // empty window: parse from global
+            tb[0] = wb0;
+            tb[1] = wb1;
         }
         __syncthreads();
         const uint64_t b0 = tb[0], b1 = tb[1];
@@ -235,15 +260,20 @@ __global__ __launch_bounds__(kT) void k_input_pass(OgePassArgs a) {
         const uint4 *g = (const uint4 *)(a.recs + b0);
         // LDS-DMA: every chunk load of the tile in flight at once, no VGPR round trip
         const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63;
-        for (uint64_t c0 = (uint64_t)wv * 64; c0 < nch; c0 += kT)
+        for (uint64_t c0 = (uint64_t)wv * 64; c0 < nch; c0 += NT)
             if (c0 + ln < nch)
                 __builtin_amdgcn_global_load_lds((const void *)(g + c0 + ln),
                                                  (__attribute__((address_space(3))) void *)(tile + c0), 16, 0, 0);
+        const uint64_t o = my_off;
+        const uint64_t n0 = r0 + stride;
+        if (n0 < a.n) {  // next tile's window and offsets, overlapping this tile's loads
+            if (threadIdx.x == 0) window(n0, wb0, wb1);
+            if (n0 + threadIdx.x < a.n) my_off = a.off[n0 + threadIdx.x];
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const uint64_t i = r0 + threadIdx.x;
         if (i < r1) {
-            const uint64_t o = a.off[i];
             const uint32_t bs = (o >= b0 && o + 4 <= b1) ? LdsRd{lds}.u32(o - b0) : 0u;
             if (bs && o + 4 + bs <= b1) parse_input<META, KEYS>(LdsRd{lds}, o - b0, i, o, a);
             else parse_input<META, KEYS>(GlbRd{a.recs}, o, i, o, a);
@@ -408,21 +438,31 @@ __global__ __launch_bounds__(kT) void k_gather16(OgePassArgs a) {
 
 }  // namespace
 
+template <int NT>
+static void launch_input_pass(oge_ctx *ctx, const OgePassArgs &a, uint64_t cap) {
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, NT), cap);
+    if (a.meta && a.keys)
+        hipLaunchKernelGGL((k_input_pass<true, true, NT>), dim3(blocks), dim3(NT), 0, ctx->stream, a);
+    else if (a.meta)
+        hipLaunchKernelGGL((k_input_pass<true, false, NT>), dim3(blocks), dim3(NT), 0, ctx->stream, a);
+    else
+        hipLaunchKernelGGL((k_input_pass<false, true, NT>), dim3(blocks), dim3(NT), 0, ctx->stream, a);
+}
+
 int oge_input_pass(oge_ctx *ctx, const OgePassArgs &a) {
-    if (!a.n) return OGE_OK;
-    static const uint64_t cap = [] {
+    if (!a.n || (!a.meta && !a.keys)) return OGE_OK;
+    static const int tile = [] {  // OGE_INPUT_TILE: records (= threads) per block, 64 / 128 / 256
+        const char *e = getenv("OGE_INPUT_TILE");
+        const int v = (e && *e) ? atoi(e) : 256;
+        return v <= 64 ? 64 : v <= 128 ? 128 : 256;
+    }();
+    static const uint64_t cap = [] {  // grid cap in 256-record units of work
         const char *e = getenv("OGE_INPUT_BLOCKS");
         return (e && *e) ? std::max<uint64_t>(256, strtoull(e, nullptr, 10)) : 256ull * 8u;
     }();
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, kTileRecs), cap);
-    if (a.meta && a.keys)
-        hipLaunchKernelGGL((k_input_pass<true, true>), dim3(blocks), dim3(kT), 0, ctx->stream, a);
-    else if (a.meta)
-        hipLaunchKernelGGL((k_input_pass<true, false>), dim3(blocks), dim3(kT), 0, ctx->stream, a);
-    else if (a.keys)
-        hipLaunchKernelGGL((k_input_pass<false, true>), dim3(blocks), dim3(kT), 0, ctx->stream, a);
-    else
-        return OGE_OK;
+    if (tile == 64) launch_input_pass<64>(ctx, a, cap * 4);
+    else if (tile == 128) launch_input_pass<128>(ctx, a, cap * 2);
+    else launch_input_pass<256>(ctx, a, cap);
     OGE_LAUNCH_CHECK(ctx);
     return OGE_OK;
 }
