@@ -30,11 +30,6 @@ constexpr int kT = 256;
 enum { RE_F = 1, RE_R = 2, RE_FF = 3, RE_RR = 4, RE_FR = 5, RE_RF = 6 };
 
 // --- compaction of pair candidates (order-preserving) ---
-__global__ __launch_bounds__(kT) void k_cand_flags(const RecMeta *__restrict__ meta, uint64_t n, uint32_t *__restrict__ f) {
-    uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i < n) f[i] = (meta[i].m & OGE_M_CAND) ? 1u : 0u;
-    else if (i == n) f[i] = 0;
-}
 // candidate key = top hb bits of the 48-bit pair-key hash << ib | record index (ib = bits for an
 // index, hb = min(48, 64 - ib)): the hash takes every key bit the index leaves free, so collision
 // runs (which fall to the exact slow path of k_pair_runs) stay rare at full-GPU sizes.  Only the hash
@@ -260,11 +255,7 @@ __global__ __launch_bounds__(kT) void k_pair_groups(const uint64_t *__restrict__
 
 // fragment key: bit 63 paired, bits [47,63) score, bit 46 "not a fragment",
 // lib << (sb+33) | refID << 33 | biased coord << 1 | reverse
-__global__ __launch_bounds__(kT) void k_frag_keys(const RecMeta *__restrict__ meta, uint64_t n, KeyLayout L,
-                                                   uint64_t *__restrict__ keys, uint32_t *__restrict__ vals) {
-    uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i >= n) return;
-    const RecMeta R = meta[i];
+__device__ __forceinline__ uint64_t frag_key(const RecMeta &R, KeyLayout L) {
     const uint64_t m = R.m;
     uint64_t k;
     if (!(m & OGE_M_FRAG)) {
@@ -275,8 +266,25 @@ __global__ __launch_bounds__(kT) void k_frag_keys(const RecMeta *__restrict__ me
             ((m & OGE_M_REV) ? 1ull : 0ull);
         k |= ((m & 0xFFFF) << 47) | ((m & OGE_M_PAIRED) ? (1ull << 63) : 0ull);
     }
-    keys[i] = k;
-    vals[i] = (uint32_t)i;
+    return k;
+}
+
+
+// One pass over the summaries for the two per-record products that need nothing else: the
+// mate-join candidate flag and the fragment key, so the 64-byte rows
+// are streamed once instead of twice.
+__global__ __launch_bounds__(kT) void k_cand_frag(const RecMeta *__restrict__ meta, uint64_t n, KeyLayout L,
+                                                   uint32_t *__restrict__ f, uint64_t *__restrict__ keys,
+                                                   uint32_t *__restrict__ vals) {
+    uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (i < n) {
+        const RecMeta R = meta[i];
+        f[i] = (R.m & OGE_M_CAND) ? 1u : 0u;
+        keys[i] = frag_key(R, L);
+        vals[i] = (uint32_t)i;
+    } else if (i == n) {
+        f[i] = 0;
+    }
 }
 
 __global__ __launch_bounds__(kT) void k_frag_groups(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
@@ -433,8 +441,10 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     // ---- mate join ----
     OgeStageTimer *t = ctx->begin_stage("md_matejoin");
     uint32_t *cpos = (uint32_t *)ctx->ws("md_cpos", (n + 1) * 4);
-    if (!cpos) return OGE_ERR_HIP;
-    hipLaunchKernelGGL(k_cand_flags, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, cpos);
+    uint64_t *fk = (uint64_t *)ctx->ws("md_fk", (n + 1) * 8);  // fragment keys, sorted in md_frags
+    uint32_t *fv = (uint32_t *)ctx->ws("md_fv", (n + 1) * 4);
+    if (!cpos || !fk || !fv) return OGE_ERR_HIP;
+    hipLaunchKernelGGL(k_cand_frag, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, L, cpos, fk, fv);
     OGE_LAUNCH_CHECK(ctx);
     int rc = oge_exclusive_scan_u32(ctx, cpos, cpos, n + 1);
     if (rc) return rc;
@@ -532,13 +542,9 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
 
     // ---- fragment groups ----
     t = ctx->begin_stage("md_frags");
-    uint64_t *fk = (uint64_t *)ctx->ws("md_fk", (n + 1) * 8);
-    uint32_t *fv = (uint32_t *)ctx->ws("md_fv", (n + 1) * 4);
     uint64_t *fk2 = (uint64_t *)ctx->ws("md_fk2", (n + 1) * 8);
     uint32_t *fv2 = (uint32_t *)ctx->ws("md_fv2", (n + 1) * 4);
-    if (!fk || !fv || !fk2 || !fv2) return OGE_ERR_HIP;
-    hipLaunchKernelGGL(k_frag_keys, dim3(nb), dim3(kT), 0, ctx->stream, meta, n, L, fk, fv);
-    OGE_LAUNCH_CHECK(ctx);
+    if (!fk2 || !fv2) return OGE_ERR_HIP;  // fk / fv were written by k_cand_frag
     {
         uint64_t o = 0, a = 0;
         rc = oge_reduce_or_and_u64(ctx, fk, n, (1ull << 47) - 1, &o, &a);
