@@ -41,12 +41,6 @@ struct CandKey {
     __host__ __device__ uint64_t idx_mask() const { return (1ull << ib) - 1; }
     __host__ __device__ uint64_t hash_of(uint64_t k) const { return k >> ib; }
 };
-__global__ __launch_bounds__(kT) void k_cand_scatter(const RecMeta *__restrict__ meta, uint64_t n,
-                                                      const uint32_t *__restrict__ pos, CandKey ck,
-                                                      uint64_t *__restrict__ ckey) {
-    uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i < n && (meta[i].m & OGE_M_CAND)) ckey[pos[i]] = ((oge_meta_hash48(meta[i]) >> (48 - ck.hb)) << ck.ib) | i;
-}
 
 __device__ bool pair_key_of(const uint8_t *r, const uint8_t **rg, uint32_t *rgl, uint32_t *nl) {
     const uint32_t bs = oge_ldu32(r);
@@ -273,18 +267,36 @@ __device__ __forceinline__ uint64_t frag_key(const RecMeta &R, KeyLayout L) {
 // One pass over the summaries for the two per-record products that need nothing else: the
 // mate-join candidate flag and the fragment key, so the 64-byte rows
 // are streamed once instead of twice.
-__global__ __launch_bounds__(kT) void k_cand_frag(const RecMeta *__restrict__ meta, uint64_t n, KeyLayout L,
+// Also written here, so later kernels stream 8 bytes per record instead of the 64-byte row:
+//   cval[i]  = the record's mate-join candidate key (see CandKey), scattered by k_cand_pack
+//   desc0[i] = src (39 bits) | primary << 39 | bin << 40 | FLAG high byte << 56 (optional), finished
+//              by k_apply_desc once the dup bits are known; a src past 39 bits sets *ovf.
+__global__ __launch_bounds__(kT) void k_cand_frag(const RecMeta *__restrict__ meta, uint64_t n, KeyLayout L, CandKey ck,
                                                    uint32_t *__restrict__ f, uint64_t *__restrict__ keys,
-                                                   uint32_t *__restrict__ vals) {
+                                                   uint32_t *__restrict__ vals, uint64_t *__restrict__ cval,
+                                                   uint64_t *__restrict__ desc0, unsigned int *__restrict__ ovf) {
     uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
     if (i < n) {
         const RecMeta R = meta[i];
         f[i] = (R.m & OGE_M_CAND) ? 1u : 0u;
         keys[i] = frag_key(R, L);
         vals[i] = (uint32_t)i;
+        cval[i] = ((oge_meta_hash48(R) >> (48 - ck.hb)) << ck.ib) | i;
+        if (desc0) {
+            if (R.src >> 39) atomicOr(ovf, 1u);
+            desc0[i] = (R.src & ((1ull << 39) - 1)) | ((R.m & OGE_M_PRIMARY) ? (1ull << 39) : 0ull) |
+                       ((R.m >> 48) << 40) | (((R.m >> 40) & 0xff) << 56);
+        }
     } else if (i == n) {
         f[i] = 0;
     }
+}
+
+// candidate i (flag = its exclusive-scan slot differs from the next one's) -> its compacted slot
+__global__ __launch_bounds__(kT) void k_cand_pack(const uint32_t *__restrict__ pos, const uint64_t *__restrict__ cval,
+                                                   uint64_t n, uint64_t *__restrict__ ckey) {
+    uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (i < n && pos[i + 1] != pos[i]) ckey[pos[i]] = cval[i];
 }
 
 __global__ __launch_bounds__(kT) void k_frag_groups(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
@@ -319,15 +331,10 @@ __global__ __launch_bounds__(kT) void k_any(const uint8_t *__restrict__ dup, uin
     if (__ballot(i < n && dup[i]) && (threadIdx.x & 63) == 0) atomicOr(any, 1u);
 }
 
-// desc (optional, output order): the record gather's 8-byte descriptor -- source offset (40 bits),
-// bin (16), final FLAG high byte with 0x400 applied (8) -- so the gather reads 8 bytes per record
-// instead of the 64-byte summary and the dup byte.  A source offset past 40 bits sets *desc_ovf and
-// the caller gathers from the summaries instead.
 __global__ __launch_bounds__(kT) void k_apply(uint8_t *__restrict__ recs, const uint64_t *__restrict__ off, uint64_t n,
                                                const RecMeta *__restrict__ meta, uint8_t *__restrict__ dup, int apply,
                                                int compat, const unsigned int *__restrict__ any,
-                                               unsigned long long *__restrict__ ndup, uint64_t *__restrict__ desc,
-                                               unsigned int *__restrict__ desc_ovf) {
+                                               unsigned long long *__restrict__ ndup) {
     __shared__ uint32_t wsum[kT / 64];
     uint32_t mine = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kT) {
@@ -344,13 +351,39 @@ __global__ __launch_bounds__(kT) void k_apply(uint8_t *__restrict__ recs, const 
             nh = d ? (uint8_t)(hi | 0x04) : (uint8_t)(hi & ~0x04);
             if (apply && nh != hi) recs[off[i] + OGE_OFF_FLAG + 1] = nh;
         }
-        if (desc) {
-            const uint64_t src = meta[i].src;
-            if (src >> 40) atomicOr(desc_ovf, 1u);
-            desc[i] = (src & ((1ull << 40) - 1)) | ((m >> 48) << 40) | ((uint64_t)nh << 56);
-        }
     }
     // one atomic per block: per-thread counts -> wave sums -> block sum
+    const uint32_t ws = oge_wave_sum(mine);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = ws;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int q = 0; q < kT / 64; ++q) t += wsum[q];
+        if (t) atomicAdd(ndup, (unsigned long long)t);
+    }
+}
+
+// k_apply for the fused pipeline from the 8-byte desc0 words (k_cand_frag): dup[] as k_apply leaves
+// it (apply = 0) and the gather descriptor with the final FLAG high byte.
+__global__ __launch_bounds__(kT) void k_apply_desc(const uint64_t *__restrict__ desc0, uint64_t n, uint8_t *__restrict__ dup,
+                                                    int compat, const unsigned int *__restrict__ any,
+                                                    unsigned long long *__restrict__ ndup, uint64_t *__restrict__ desc) {
+    __shared__ uint32_t wsum[kT / 64];
+    uint32_t mine = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kT) {
+        const uint64_t D = desc0[i];
+        const uint8_t d = compat ? (uint8_t)(i == 0 && *any) : dup[i];
+        const uint8_t hi = (uint8_t)(D >> 56);
+        uint8_t nh = hi;
+        if (!((D >> 39) & 1)) {
+            dup[i] = 2;
+        } else {
+            dup[i] = d;
+            mine += d;
+            nh = d ? (uint8_t)(hi | 0x04) : (uint8_t)(hi & ~0x04);
+        }
+        desc[i] = (D & ((1ull << 39) - 1)) | (D & (0xffffull << 40)) | ((uint64_t)nh << 56);
+    }
     const uint32_t ws = oge_wave_sum(mine);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = ws;
     __syncthreads();
@@ -443,14 +476,24 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     uint32_t *cpos = (uint32_t *)ctx->ws("md_cpos", (n + 1) * 4);
     uint64_t *fk = (uint64_t *)ctx->ws("md_fk", (n + 1) * 8);  // fragment keys, sorted in md_frags
     uint32_t *fv = (uint32_t *)ctx->ws("md_fv", (n + 1) * 4);
-    if (!cpos || !fk || !fv) return OGE_ERR_HIP;
-    hipLaunchKernelGGL(k_cand_frag, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, L, cpos, fk, fv);
+    uint64_t *cval = (uint64_t *)ctx->ws("md_cval", (n + 1) * 8);
+    uint64_t *desc0 = d_desc ? (uint64_t *)ctx->ws("md_desc0", (n + 1) * 8) : nullptr;
+    if (!cpos || !fk || !fv || !cval || (d_desc && !desc0)) return OGE_ERR_HIP;
+    CandKey ckl;
+    ckl.ib = bits_for(n - 1);
+    ckl.hb = std::min<uint32_t>(48, 64 - ckl.ib);
+    ckl.split_k = opts->split_chains;
+    if (opts->debug_hash_bits > 0 && (uint32_t)opts->debug_hash_bits < ckl.hb) ckl.hb = (uint32_t)opts->debug_hash_bits;
+    hipLaunchKernelGGL(k_cand_frag, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, L, ckl, cpos, fk, fv,
+                       cval, desc0, cnt + 3);
     OGE_LAUNCH_CHECK(ctx);
     int rc = oge_exclusive_scan_u32(ctx, cpos, cpos, n + 1);
     if (rc) return rc;
-    uint32_t nc = 0;
+    uint32_t nc = 0, desc_ovf = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&nc, cpos + n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&desc_ovf, cnt + 3, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const bool use_desc = d_desc && !desc_ovf;
     const uint64_t nc1 = (uint64_t)nc + 1;
     uint64_t *ck = (uint64_t *)ctx->ws("md_ck", nc1 * 8);
     uint64_t *ck2 = (uint64_t *)ctx->ws("md_ck2", nc1 * 8);
@@ -461,12 +504,7 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     uint64_t *pairs2 = (uint64_t *)ctx->ws("md_pairs2", (nc1 / 2 + 1) * 8);
     uint32_t *slow = (uint32_t *)ctx->ws("md_slow", nc1 * 4);
     if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !slow) return OGE_ERR_HIP;
-    CandKey ckl;
-    ckl.ib = bits_for(n - 1);
-    ckl.hb = std::min<uint32_t>(48, 64 - ckl.ib);
-    ckl.split_k = opts->split_chains;
-    if (opts->debug_hash_bits > 0 && (uint32_t)opts->debug_hash_bits < ckl.hb) ckl.hb = (uint32_t)opts->debug_hash_bits;
-    hipLaunchKernelGGL(k_cand_scatter, dim3(nb), dim3(kT), 0, ctx->stream, meta, n, (const uint32_t *)cpos, ckl, ck);
+    hipLaunchKernelGGL(k_cand_pack, dim3(nb), dim3(kT), 0, ctx->stream, (const uint32_t *)cpos, (const uint64_t *)cval, n, ck);
     OGE_LAUNCH_CHECK(ctx);
     uint64_t *sk;
     rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, ((1ull << ckl.hb) - 1) << ckl.ib, &sk, nullptr);
@@ -564,17 +602,19 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
         hipLaunchKernelGGL(k_any, dim3(nb), dim3(kT), 0, ctx->stream, (const uint8_t *)d_dup, n, cnt + 1);
         OGE_LAUNCH_CHECK(ctx);
     }
-    hipLaunchKernelGGL(k_apply, dim3(std::min<uint32_t>(nb, 2048u)), dim3(kT), 0, ctx->stream, d_recs, d_off, n, meta, d_dup, apply,
-                       opts->compat_nonverbose_index, (const unsigned int *)(cnt + 1), ndup, d_desc, cnt + 3);
+    if (use_desc && !apply)
+        hipLaunchKernelGGL(k_apply_desc, dim3(std::min<uint32_t>(nb, 2048u)), dim3(kT), 0, ctx->stream, (const uint64_t *)desc0,
+                           n, d_dup, opts->compat_nonverbose_index, (const unsigned int *)(cnt + 1), ndup, d_desc);
+    else
+        hipLaunchKernelGGL(k_apply, dim3(std::min<uint32_t>(nb, 2048u)), dim3(kT), 0, ctx->stream, d_recs, d_off, n, meta, d_dup,
+                           apply, opts->compat_nonverbose_index, (const unsigned int *)(cnt + 1), ndup);
     OGE_LAUNCH_CHECK(ctx);
     ctx->end_stage(t);
     unsigned long long h = 0;
-    unsigned int ovf = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&h, ndup, 8, hipMemcpyDeviceToHost, ctx->stream));
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&ovf, cnt + 3, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     *n_dup_out = h;
-    if (desc_ok) *desc_ok = d_desc && !ovf;
+    if (desc_ok) *desc_ok = use_desc && !apply;
     return OGE_OK;
 }
 
