@@ -59,6 +59,9 @@ int oge_dev_alloc(oge_ctx *ctx, uint64_t bytes, void **out);
 int oge_dev_free(oge_ctx *ctx, void *p);
 /* kind: 1 = host->device, 2 = device->host, 3 = device->device; synchronous on the ctx stream */
 int oge_memcpy(oge_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
+/* Page-locked host memory (DMA at full PCIe rate) for staging compressed output. */
+int oge_host_alloc(oge_ctx *ctx, uint64_t bytes, void **out);
+int oge_host_free(oge_ctx *ctx, void *p);
 
 /* ---- coordinate sort (ReadSorter + Sort::ByPosition) ------------------------------ */
 /* perm_out[k] = input index of the record at sorted position k.  Order: refID ascending with

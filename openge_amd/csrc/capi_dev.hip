@@ -167,6 +167,20 @@ int oge_dev_free(oge_ctx *ctx, void *p) {
     return OGE_OK;
 }
 
+int oge_host_alloc(oge_ctx *ctx, uint64_t bytes, void **out) {
+    if (!ctx || !out) return oge_fail(ctx, OGE_ERR_ARG, "oge_host_alloc: null argument");
+    hipSetDevice(ctx->device);
+    *out = nullptr;
+    OGE_HIP_TRY(ctx, hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return OGE_OK;
+}
+
+int oge_host_free(oge_ctx *ctx, void *p) {
+    if (!ctx) return oge_fail(ctx, OGE_ERR_ARG, "oge_host_free: null ctx");
+    if (p) OGE_HIP_TRY(ctx, hipHostFree(p));
+    return OGE_OK;
+}
+
 int oge_memcpy(oge_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind) {
     if (!ctx || (bytes && (!dst || !src))) return oge_fail(ctx, OGE_ERR_ARG, "oge_memcpy: null argument");
     hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;

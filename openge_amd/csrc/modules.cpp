@@ -529,18 +529,31 @@ static void fix_bins(ReadBatch &b, int threads) {
 // Device-resident records: drop duplicates (-r/-R), recompute bins and BGZF-compress on the GPU;
 // only the compressed stream crosses PCIe.  The records of a batch are back to back in its arena
 // (the reader's stream, a gather's output), so the stream is the byte range [off[0], off[n]).
-int FileWriter::compress_on_device(ChainContext &cc, ReadBatch &b, bytevec &z, double *t_dev, double *t_d2h) {
+// Device-resident records -> BGZF file.  Bins are recomputed on the device, then the stream is
+// deflated in segments of kSeg bytes (a multiple of the 65,280-byte block payload, so the blocks are
+// exactly those of one whole-stream deflate); each segment's compressed bytes come down into one of
+// two page-locked buffers and are written by a background thread while the next segment is
+// deflated and copied.  Timings: device deflate, device->host, and time spent waiting for the disk.
+int FileWriter::write_device(ChainContext &cc, ReadBatch &b, BgzfWriter &w, double *t_dev, double *t_d2h, double *t_wait) {
     auto clk = [] { return std::chrono::steady_clock::now(); };
-    const auto t0 = clk();
+    auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
+        return std::chrono::duration<double>(z - a).count();
+    };
+    *t_dev = *t_d2h = *t_wait = 0;
     uint8_t *recs = b.d_recs;
     uint64_t *offs = b.d_offs;
     uint64_t n = b.n;
-    void *kept = nullptr, *kept_off = nullptr, *dz = nullptr;
+    void *kept = nullptr, *kept_off = nullptr, *dz = nullptr, *hz[2] = {nullptr, nullptr};
+    std::thread wr;
     auto release = [&]() {
+        if (wr.joinable()) wr.join();
         if (kept) oge_dev_free(cc.ctx, kept);
         if (kept_off) oge_dev_free(cc.ctx, kept_off);
         if (dz) oge_dev_free(cc.ctx, dz);
+        for (void *h : hz)
+            if (h) oge_host_free(cc.ctx, h);
     };
+    auto t = clk();
     if (b.drop_duplicates && n) {
         if (oge_dev_alloc(cc.ctx, b.d_bytes + 64, &kept) || oge_dev_alloc(cc.ctx, (n + 1) * 8, &kept_off)) {
             release();
@@ -561,31 +574,44 @@ int FileWriter::compress_on_device(ChainContext &cc, ReadBatch &b, bytevec &z, d
         release();
         return cc.fail("FileWriter: bins");
     }
+    *t_dev += sec(t, clk());
     const uint64_t len = ends[1] - ends[0];
-    uint64_t zb = 0;
-    if (len) {
-        const uint64_t cap = oge_bgzf_bound(len);
-        if (oge_dev_alloc(cc.ctx, cap, &dz)) {
-            release();
-            return cc.fail("device allocation");
-        }
-        if (oge_bgzf_deflate_dev(cc.ctx, recs + ends[0], len, std::max(0, std::min(9, level_)), (uint8_t *)dz, cap, &zb) || oge_ctx_sync(cc.ctx)) {
+    const uint64_t kSeg = 65280ull * 32768;  // 2.14 GB of records per segment
+    const uint64_t seg = std::min(len, kSeg);
+    const uint64_t cap = oge_bgzf_bound(seg);
+    if (len && (oge_dev_alloc(cc.ctx, cap, &dz) || oge_host_alloc(cc.ctx, cap, &hz[0]) ||
+                (len > seg && oge_host_alloc(cc.ctx, cap, &hz[1])))) {
+        release();
+        return cc.fail("FileWriter: buffers");
+    }
+    w.write_compressed(nullptr, 0);  // flush the header as blocks of its own
+    int k = 0;
+    for (uint64_t s0 = 0; s0 < len; s0 += seg, k ^= 1) {
+        const uint64_t sl = std::min(seg, len - s0);
+        uint64_t zb = 0;
+        t = clk();
+        if (oge_bgzf_deflate_dev(cc.ctx, recs + ends[0] + s0, sl, std::max(0, std::min(9, level_)), (uint8_t *)dz, cap, &zb) ||
+            oge_ctx_sync(cc.ctx)) {
             release();
             return cc.fail("FileWriter: BGZF on the device");
         }
+        *t_dev += sec(t, clk());
+        t = clk();
+        if (wr.joinable()) wr.join();  // the buffer written two segments ago is free again
+        *t_wait += sec(t, clk());
+        t = clk();
+        if (zb && oge_memcpy(cc.ctx, hz[k], dz, zb, 2)) {
+            release();
+            return cc.fail("device->host copy");
+        }
+        *t_d2h += sec(t, clk());
+        const uint8_t *hp = (const uint8_t *)hz[k];
+        wr = std::thread([&w, hp, zb]() { w.write_compressed(hp, zb); });
     }
-    const auto t1 = clk();
-    z.clear();
-    z.reserve(zb + 16);
-    want_huge_pages(z.data(), zb + 16);
-    z.resize(zb);
-    if (zb && oge_memcpy(cc.ctx, z.data(), dz, zb, 2)) {
-        release();
-        return cc.fail("device->host copy");
-    }
+    t = clk();
+    if (wr.joinable()) wr.join();
+    *t_wait += sec(t, clk());
     release();
-    *t_dev = std::chrono::duration<double>(t1 - t0).count();
-    *t_d2h = std::chrono::duration<double>(clk() - t1).count();
     return 0;
 }
 
@@ -596,13 +622,8 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
     };
     const auto t0 = clk();
     const bool on_device = b.dev_valid && !b.host_valid && !bgzf_host_codec_forced();
-    bytevec z;
-    double t_dev = 0, t_d2h = 0;
-    if (on_device) {
-        if (compress_on_device(cc, b, z, &t_dev, &t_d2h)) return -1;
-    } else if (cc.to_host(b)) {
-        return -1;
-    }
+    double t_dev = 0, t_d2h = 0, t_wait = 0;
+    if (!on_device && cc.to_host(b)) return -1;
     const auto t1 = clk();
     if (!on_device) fix_bins(b, cc.threads);
     const auto t2 = clk();
@@ -630,7 +651,10 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
         std::vector<uint8_t> hb = bam_encode_header(h);
         w.write(hb.data(), hb.size());
         if (on_device) {
-            w.write_compressed(z.data(), z.size());
+            if (write_device(cc, b, w, &t_dev, &t_d2h, &t_wait)) {
+                if (f != stdout) fclose(f);
+                return -1;
+            }
             w.close();
         }
         // maximal runs of records that sit back to back in memory go out as spans (no copy)
@@ -656,9 +680,8 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
     }
     if (f != stdout) fclose(f);
     if (verbose_ && on_device)
-        fprintf(stderr, "[openge] FileWriter: device bins + BGZF %.3f s (gpu, %.3f of %llu bytes), device->host %.3f s, write %.3f s\n",
-                t_dev, z.size() ? (double)z.size() / (double)std::max<uint64_t>(1, b.bytes()) : 0.0,
-                (unsigned long long)z.size(), t_d2h, sec(t2, clk()));
+        fprintf(stderr, "[openge] FileWriter: device bins + BGZF %.3f s (gpu, 2.1 GB segments), device->host %.3f s, waiting on the disk %.3f s, "
+                "total %.3f s\n", t_dev, t_d2h, t_wait, sec(t2, clk()));
     else if (verbose_)
         fprintf(stderr, "[openge] FileWriter: device->host %.3f s, bins %.3f s, BGZF %.3f s (%s)\n", sec(t0, t1), sec(t1, t2),
                 sec(t2, clk()), bgzf_codec_name());

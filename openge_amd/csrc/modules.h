@@ -164,7 +164,7 @@ public:
     FileWriter() : AlgorithmModule("FileWriter") {}
     void setFilename(const std::string &f) { filename_ = f; }
     void setCompressionLevel(int l) { level_ = l; }
-    int compress_on_device(ChainContext &cc, ReadBatch &b, bytevec &z, double *t_dev, double *t_d2h);
+    int write_device(ChainContext &cc, ReadBatch &b, BgzfWriter &w, double *t_dev, double *t_d2h, double *t_wait);
     void addProgramLine(const std::string &cl) { program_line_ = cl; }
     int setFormat(const std::string &f);  // only "bam" is supported (SAM/FASTQ out of scope)
 protected:
