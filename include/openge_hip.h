@@ -59,6 +59,11 @@ int oge_dev_alloc(oge_ctx *ctx, uint64_t bytes, void **out);
 int oge_dev_free(oge_ctx *ctx, void *p);
 /* kind: 1 = host->device, 2 = device->host, 3 = device->device; synchronous on the ctx stream */
 int oge_memcpy(oge_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
+/* enable != 0: device buffers (oge_dev_alloc and the library's workspaces) come from the device's
+ * stream-ordered pool and freed memory stays reserved for the next allocation of this process
+ * (a module chain then reuses one module's buffers for the next).  Call before any allocation;
+ * buffers must be freed with the same setting. */
+int oge_ctx_set_pool(oge_ctx *ctx, int enable);
 /* Page-locked host memory (DMA at full PCIe rate) for staging compressed output. */
 int oge_host_alloc(oge_ctx *ctx, uint64_t bytes, void **out);
 int oge_host_free(oge_ctx *ctx, void *p);

@@ -32,18 +32,38 @@ int oge_fail(oge_ctx *ctx, int code, const char *msg) {
 }
 
 // ---------------------------------------------------------------- context
+// With `pool` (oge_ctx_set_pool), buffers come from the device's default stream-ordered pool with
+// an unlimited release threshold: memory one module frees is handed to the next module's buffers
+// without going back to the driver (each fresh hipMalloc of tens of GB maps new pages, which on
+// some boxes costs seconds in a CLI run).
+void *oge_ctx::alloc(size_t bytes) {
+    void *p = nullptr;
+    if (pool) {
+        if (hipMallocAsync(&p, bytes, stream) != hipSuccess) return nullptr;
+        return p;
+    }
+    return hipMalloc(&p, bytes) == hipSuccess ? p : nullptr;
+}
+
+void oge_ctx::release(void *p) {
+    if (!p) return;
+    if (pool) hipFreeAsync(p, stream);
+    else hipFree(p);
+}
+
 void *oge_ctx::ws(const char *name, size_t bytes) {
     Buf &b = bufs[name];
     if (bytes == 0) bytes = 1;
     if (b.cap >= bytes) return b.p;
     if (b.p) {
         hipStreamSynchronize(stream);
-        hipFree(b.p);
+        release(b.p);
         b.p = nullptr;
         b.cap = 0;
     }
     size_t cap = bytes + 64;  // slack so 4-byte over-reads at the end stay inside the allocation
-    hipError_t e = hipMalloc(&b.p, cap);
+    b.p = alloc(cap);
+    hipError_t e = b.p ? hipSuccess : hipErrorOutOfMemory;
     if (e != hipSuccess) {
         b.p = nullptr;
         std::string m = std::string("hipMalloc(") + name + ", " + std::to_string(cap) + " B): " + hipGetErrorString(e);
@@ -126,8 +146,8 @@ void oge_ctx_destroy(oge_ctx *ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
-    for (auto &kv : ctx->bufs)
-        if (kv.second.p) hipFree(kv.second.p);
+    for (auto &kv : ctx->bufs) ctx->release(kv.second.p);
+    hipStreamSynchronize(ctx->stream);
     for (auto &t : ctx->event_pool) {
         hipEventDestroy(t.start);
         hipEventDestroy(t.stop);
@@ -155,15 +175,29 @@ int oge_ctx_timing(oge_ctx *ctx, const char *stage, double *ms_out) {
 int oge_dev_alloc(oge_ctx *ctx, uint64_t bytes, void **out) {
     if (!ctx || !out) return oge_fail(ctx, OGE_ERR_ARG, "oge_dev_alloc: null argument");
     hipSetDevice(ctx->device);
-    *out = nullptr;
-    OGE_HIP_TRY(ctx, hipMalloc(out, bytes ? bytes : 1));
+    *out = ctx->alloc(bytes ? bytes : 1);
+    if (!*out) return oge_fail(ctx, OGE_ERR_HIP, ("oge_dev_alloc: out of device memory (" + std::to_string(bytes) + " B)").c_str());
     return OGE_OK;
 }
 
 int oge_dev_free(oge_ctx *ctx, void *p) {
     if (!ctx) return oge_fail(ctx, OGE_ERR_ARG, "oge_dev_free: null ctx");
     hipSetDevice(ctx->device);
-    if (p) OGE_HIP_TRY(ctx, hipFree(p));
+    ctx->release(p);
+    return OGE_OK;
+}
+
+int oge_ctx_set_pool(oge_ctx *ctx, int enable) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    hipSetDevice(ctx->device);
+    if (enable) {
+        hipMemPool_t mp;
+        OGE_HIP_TRY(ctx, hipDeviceGetDefaultMemPool(&mp, ctx->device));
+        uint64_t thr = ~0ull;
+        OGE_HIP_TRY(ctx, hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &thr));
+    }
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->pool = enable != 0;
     return OGE_OK;
 }
 

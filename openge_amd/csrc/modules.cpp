@@ -415,6 +415,8 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
     if (oge_dev_alloc(cc.ctx, b.n * 4 + 4, &perm) || oge_dev_alloc(cc.ctx, b.d_bytes + 64, &out) ||
         oge_dev_alloc(cc.ctx, (b.n + 1) * 8, &out_off))
         return cc.fail("device allocation");
+    if (verbose_) oge_ctx_sync(cc.ctx);
+    const auto t1a = std::chrono::steady_clock::now();
     int rc;
     MarkDuplicates *md = order_ == BamHeaderModel::COORDINATE ? dynamic_cast<MarkDuplicates *>(sink_) : nullptr;
     if (order_ == BamHeaderModel::QUERYNAME) {  // -b; a MarkDuplicates sink then runs on its own
@@ -433,9 +435,9 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
     }
     if (!rc) rc = oge_ctx_sync(cc.ctx);
     if (verbose_) {
-        fprintf(stderr, "[openge] ReadSorter: host->device %.3f s, device pipeline %.3f s\n",
-                std::chrono::duration<double>(t1 - t0).count(),
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
+        fprintf(stderr, "[openge] ReadSorter: host->device %.3f s, output allocation %.3f s, device pipeline %.3f s\n",
+                std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t1a - t1).count(),
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t1a).count());
         std::string st;  // HIP-event stage times of the device pipeline (ms)
         for (const char *s : {"input_pass", "sort_radix", "sort_ties", "meta_gather", "md_matejoin", "md_pairs", "md_frags",
                               "md_apply", "gather_offsets", "gather_records", "name_sort"}) {

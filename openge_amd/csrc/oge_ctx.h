@@ -26,6 +26,9 @@ struct oge_ctx {
     std::vector<OgeStageTimer> event_pool;
     size_t event_pool_used = 0;
     bool timing = true;
+    bool pool = false;  // allocate from the device's stream-ordered pool and keep freed memory in it
+    void *alloc(size_t bytes);
+    void release(void *p);
     bool last_scan_generic = false;  // realign scan fell back to the byte-wise kernel
     double scan_t[3] = {0, 0, 0};    // realign scan host timings: validate, upload, device + download
 

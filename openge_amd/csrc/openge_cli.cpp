@@ -159,6 +159,11 @@ int main(int argc, const char **argv) {
         fprintf(stderr, "openge: %s\n", oge_last_error(nullptr));
         return -1;
     }
+    const char *pool = getenv("OGE_POOL");  // default on: the chain's modules share one memory pool
+    if (!(pool && std::string(pool) == "0") && oge_ctx_set_pool(cc.ctx, 1)) {
+        fprintf(stderr, "openge: %s\n", oge_last_error(cc.ctx));
+        return -1;
+    }
 
     FileReader reader;
     FileWriter writer;

@@ -203,6 +203,7 @@ def lib() -> C.CDLL:
         "oge_dev_free": (C.c_int, [vp, vp]),
         "oge_memcpy": (C.c_int, [vp, vp, vp, u64, C.c_int]),
         "oge_host_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
+        "oge_ctx_set_pool": (C.c_int, [vp, C.c_int]),
         "oge_host_free": (C.c_int, [vp, vp]),
         "oge_realign_opts_init": (None, [vp]),
         "oge_localrealign": (C.c_int, [vp, C.c_char_p, u64, vp, vp, u64, C.c_char_p, C.c_char_p, vp, C.POINTER(vp)]),
