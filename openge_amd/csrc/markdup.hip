@@ -4,6 +4,8 @@
 //  readends     : per-record fragment ReadEnds fields (records.hip, k_records<*, META>): buildReadEnds
 //                 :147-164, getUnclippedStart/End :88-129, getScore :135-144, getLibraryId :282-318,
 //                 plus a 32-bit hash of the pair key RG ":" name (:210-213)
+//  k_cand_frag  : one pass over the sorted summaries -> candidate flags, candidate hash keys,
+//                 fragment sort keys and the gather descriptors (8-byte words for later passes)
 //  mate join    : pair candidates sorted by hash (stable, so record order inside a hash run);
 //                 k_pair_runs pairs consecutive occurrences of each exact key (the first-seen /
 //                 second-seen semantics of the ReadEndsMap at :214-245)
@@ -13,7 +15,8 @@
 //                 markDuplicatePairs / markDuplicateFragments (:488-540): best = first strict max
 //                 score in index order; fragments only when the chunk holds an unpaired end.
 //  k_apply      : every primary record gets 0x400 set/cleared, others untouched (:443-465); only
-//                 records whose flag byte changes are written.
+//                 records whose flag byte changes are written (standalone dedup); k_apply_desc
+//                 finishes the gather descriptors instead in the fused sort + dedup pipeline.
 #include "oge_ctx.h"
 #include "bam_layout.h"
 #include "dev_util.h"
