@@ -250,6 +250,73 @@ __global__ __launch_bounds__(kT) void k_pair_groups(const uint64_t *__restrict__
     }
 }
 
+// Pair chunks (markDuplicatePairs, :488-507) need equal (lib, r1Seq, r1Coord, orient, r2Seq, r2Coord)
+// contiguous, not ordered: the best of a chunk is chosen explicitly (max score, then smallest read1
+// index, which is the reference's "first strict max" in its index-ordered chunk).  So pairs are
+// sorted on 32 bits of a 64-bit hash of the full key (4 radix passes instead of 10 for the two
+// 48-bit key words) and every run of equal hash bits is split into its exact keys here.
+__device__ __forceinline__ uint64_t mix64(uint64_t h) {
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; return h ^ (h >> 33);
+}
+__global__ __launch_bounds__(kT) void k_pair_hash(const uint64_t *__restrict__ hi, const uint64_t *__restrict__ lo, uint32_t np,
+                                                   uint64_t *__restrict__ hk) {
+    const uint32_t p = blockIdx.x * kT + threadIdx.x;
+    if (p < np) hk[p] = mix64(mix64(hi[p] & ((1ull << 48) - 1)) ^ lo[p]);
+}
+
+__device__ __forceinline__ void pair_chunk(const uint32_t *__restrict__ sval, const uint64_t *__restrict__ hi,
+                                           const uint64_t *__restrict__ lo, const uint2 *__restrict__ idx, uint32_t q,
+                                           uint32_t e, uint64_t kh, uint64_t kl, uint8_t *__restrict__ dup) {
+    const uint64_t kmask = (1ull << 48) - 1;
+    uint32_t cnt = 0, best = 0xffffffffu, bi = 0;
+    int16_t bs = 0;
+    for (uint32_t x = q; x < e; ++x) {
+        const uint32_t v = sval[x];
+        const uint64_t h = hi[v];
+        if ((h & kmask) != kh || lo[v] != kl) continue;
+        ++cnt;
+        const int16_t s = (int16_t)(uint16_t)(h >> 48);
+        const uint32_t i1 = idx[v].x;
+        if (best == 0xffffffffu || s > bs || (s == bs && i1 < bi)) { best = x; bs = s; bi = i1; }
+    }
+    if (cnt < 2) return;
+    for (uint32_t x = q; x < e; ++x) {
+        const uint32_t v = sval[x];
+        if (x == best || (hi[v] & kmask) != kh || lo[v] != kl) continue;
+        const uint2 ii = idx[v];
+        dup[ii.x] = 1;
+        dup[ii.y] = 1;
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_pair_groups_h(const uint64_t *__restrict__ shk, const uint32_t *__restrict__ sval,
+                                                       const uint64_t *__restrict__ hi, const uint64_t *__restrict__ lo,
+                                                       const uint2 *__restrict__ idx, uint32_t np, uint64_t rmask,
+                                                       uint8_t *__restrict__ dup) {
+    const uint32_t q = blockIdx.x * kT + threadIdx.x;
+    if (q >= np) return;
+    const uint64_t top = shk[q] & rmask, kmask = (1ull << 48) - 1;
+    if (q > 0 && (shk[q - 1] & rmask) == top) return;  // one thread per run of equal sorted hash bits
+    uint32_t e = q + 1;
+    while (e < np && (shk[e] & rmask) == top) ++e;
+    if (e - q < 2) return;
+    const uint64_t qh = hi[sval[q]] & kmask, ql = lo[sval[q]];
+    bool pure = true;  // the common case: one exact key fills the run
+    for (uint32_t x = q + 1; x < e && pure; ++x) pure = (hi[sval[x]] & kmask) == qh && lo[sval[x]] == ql;
+    if (pure) {
+        if (!(ql >> 63)) pair_chunk(sval, hi, lo, idx, q, e, qh, ql, dup);
+        return;
+    }
+    for (uint32_t x = q; x < e; ++x) {  // each exact key once, at its first occurrence in the run
+        const uint32_t v = sval[x];
+        const uint64_t kh = hi[v] & kmask, kl = lo[v];
+        if (kl >> 63) continue;  // unconfirmed pair key (hash collision): not a pair
+        bool seen = false;
+        for (uint32_t y = q; y < x && !seen; ++y) seen = (hi[sval[y]] & kmask) == kh && lo[sval[y]] == kl;
+        if (!seen) pair_chunk(sval, hi, lo, idx, x, e, kh, kl, dup);
+    }
+}
+
 // fragment key: bit 63 paired, bits [47,63) score, bit 46 "not a fragment",
 // lib << (sb+33) | refID << 33 | biased coord << 1 | reverse
 __device__ __forceinline__ uint64_t frag_key(const RecMeta &R, KeyLayout L) {
@@ -554,29 +621,18 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
         hipLaunchKernelGGL(k_pair_build, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)spairs, np,
                            (const uint8_t *)d_recs, meta, L, hi, lo, pidx, pv);
         OGE_LAUNCH_CHECK(ctx);
-        // LSD over (hi, lo): sort by lo first (copy lo so the unsorted lo stays addressable by pair index)
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(lo2, lo, (uint64_t)np * 8, hipMemcpyDeviceToDevice, ctx->stream));
-        uint64_t o = 0, a = 0;
-        rc = oge_reduce_or_and_u64(ctx, lo2, np, ~0ull, &o, &a);
-        if (rc) return rc;
-        uint64_t *k1;
-        uint32_t *v1;
-        rc = oge_radix_sort_pairs(ctx, lo2, pv, hi2, pv2, np, o ^ a, &k1, &v1);
-        if (rc) return rc;
-        // gather hi in lo-sorted order, then stable sort by hi's key bits
-        uint64_t *hk = (k1 == lo2) ? hi2 : lo2;
-        hipLaunchKernelGGL(k_gather_u64, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)hi, (const uint32_t *)v1, np, hk);
+        // 32 bits of a hash of the whole chunk key group equal keys (k_pair_groups_h splits runs)
+        hipLaunchKernelGGL(k_pair_hash, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)hi, (const uint64_t *)lo, np, hi2);
         OGE_LAUNCH_CHECK(ctx);
-        rc = oge_reduce_or_and_u64(ctx, hk, np, (1ull << 48) - 1, &o, &a);
-        if (rc) return rc;
-        uint64_t *kt2 = (hk == lo2) ? hi2 : lo2;
-        uint32_t *vt2 = (v1 == pv) ? pv2 : pv;
         uint64_t *k2;
         uint32_t *v2;
-        rc = oge_radix_sort_pairs(ctx, hk, v1, kt2, vt2, np, (o ^ a) & ((1ull << 48) - 1), &k2, &v2);
+        // debug_hash_bits (tests) also narrows these bits, so runs holding several keys are exercised
+        const int rb = opts->debug_hash_bits > 0 ? std::min(32, opts->debug_hash_bits) : 32;
+        const uint64_t rmask = ~0ull << (64 - rb);
+        rc = oge_radix_sort_pairs(ctx, hi2, pv, lo2, pv2, np, rmask, &k2, &v2);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_pair_groups, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)k2, (const uint32_t *)v2,
-                           (const uint64_t *)lo, (const uint2 *)pidx, np, d_dup);
+        hipLaunchKernelGGL(k_pair_groups_h, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)k2, (const uint32_t *)v2,
+                           (const uint64_t *)hi, (const uint64_t *)lo, (const uint2 *)pidx, np, rmask, d_dup);
         OGE_LAUNCH_CHECK(ctx);
     }
     ctx->end_stage(t);

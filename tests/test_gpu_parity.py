@@ -118,3 +118,34 @@ def test_markdup_forced_hash_collisions(ctx, bits):
     dup, nd = ctx.markdup(recs, so, n, opts)
     odup, ond = oracle.markdup(recs, so, n, hdr)
     assert nd == ond and np.array_equal(dup, odup)
+
+
+@pytest.mark.parametrize("bits", [1, 12])
+def test_sort_markdup_forced_hash_collisions(ctx, bits):
+    """The fused pipeline with truncated hashes: mate-join runs and the pair-chunk runs (grouped on
+    hash bits, split into exact keys by k_pair_groups_h) hold many keys; FLAG bits must still equal
+    the oracle's."""
+    import torch
+    p = L.synth_params(4000, preset="mix", seed=23)
+    recs, offs, hdr = L.synth_host(p)
+    n = 8000
+    d_recs = torch.from_numpy(recs).cuda()
+    d_offs = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_perm = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_out = torch.zeros(recs.size, dtype=torch.uint8, device="cuda")
+    d_oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    opts.debug_hash_bits = bits
+    nd = ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(), d_out.data_ptr(),
+                              d_oo.data_ptr())
+    ctx.sync()
+    perm = d_perm.cpu().numpy().view(np.uint32)
+    operm = oracle.sort_perm(recs, offs, n)
+    assert np.array_equal(perm, operm)
+    odup, ond = oracle.markdup(recs, offs[:-1][operm], n, hdr)
+    assert nd == ond
+    out, oo = d_out.cpu().numpy(), d_oo.cpu().numpy().view(np.uint64)
+    for k in range(n):
+        f = int.from_bytes(out[int(oo[k]) + 18:int(oo[k]) + 20].tobytes(), "little")
+        if odup[k] != 2:
+            assert bool(f & 0x400) == bool(odup[k]), k
