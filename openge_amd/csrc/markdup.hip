@@ -300,11 +300,29 @@ __global__ __launch_bounds__(kT) void k_pair_groups_h(const uint64_t *__restrict
     uint32_t e = q + 1;
     while (e < np && (shk[e] & rmask) == top) ++e;
     if (e - q < 2) return;
-    const uint64_t qh = hi[sval[q]] & kmask, ql = lo[sval[q]];
-    bool pure = true;  // the common case: one exact key fills the run
-    for (uint32_t x = q + 1; x < e && pure; ++x) pure = (hi[sval[x]] & kmask) == qh && lo[sval[x]] == ql;
+    // the common case: one exact key fills the run.  Its best pair is found in the same walk that
+    // checks the keys (score, then read1 index, as pair_chunk), so each pair is gathered once.
+    const uint32_t v0 = sval[q];
+    const uint64_t h0 = hi[v0], qh = h0 & kmask, ql = lo[v0];
+    uint32_t best = q, bi = idx[v0].x;
+    int16_t bs = (int16_t)(uint16_t)(h0 >> 48);
+    bool pure = true;
+    for (uint32_t x = q + 1; x < e; ++x) {
+        const uint32_t v = sval[x];
+        const uint64_t h = hi[v];
+        if ((h & kmask) != qh || lo[v] != ql) { pure = false; break; }
+        const int16_t s = (int16_t)(uint16_t)(h >> 48);
+        const uint32_t i1 = idx[v].x;
+        if (s > bs || (s == bs && i1 < bi)) { best = x; bs = s; bi = i1; }
+    }
     if (pure) {
-        if (!(ql >> 63)) pair_chunk(sval, hi, lo, idx, q, e, qh, ql, dup);
+        if (ql >> 63) return;  // unconfirmed pair key (hash collision): not a pair
+        for (uint32_t x = q; x < e; ++x) {
+            if (x == best) continue;
+            const uint2 ii = idx[sval[x]];
+            dup[ii.x] = 1;
+            dup[ii.y] = 1;
+        }
         return;
     }
     for (uint32_t x = q; x < e; ++x) {  // each exact key once, at its first occurrence in the run
