@@ -105,6 +105,7 @@ __global__ __launch_bounds__(kT) void k_pair_runs(const uint64_t *__restrict__ c
     bool queue = false;
     if (p < nc) {
         uint32_t f = 0;
+        uint64_t sp = 0;
         const uint64_t kp = ckey[p];
         const uint64_t h = ck.hash_of(kp);
         if (p == 0 || ck.hash_of(ckey[p - 1]) != h) {
@@ -112,12 +113,13 @@ __global__ __launch_bounds__(kT) void k_pair_runs(const uint64_t *__restrict__ c
             while (e < nc && e - p <= 2 && ck.hash_of(ckey[e]) == h) ++e;
             if (e - p == 2) {
                 f = 1;
-                sparse[p] = ((kp & ck.idx_mask()) << 32) | (ckey[p + 1] & ck.idx_mask());
+                sp = ((kp & ck.idx_mask()) << 32) | (ckey[p + 1] & ck.idx_mask());
             } else if (e - p > 2) {
                 queue = true;
             }
         }
         flag[p] = f;
+        sparse[p] = sp;  // every slot written: whole-line stores, no partial-line read-modify-write
     } else if (p == nc) {
         flag[p] = 0;
     }
@@ -183,9 +185,15 @@ __device__ __forceinline__ int orient_byte(bool r1neg, bool r2neg) {
 // (same_pair_key); a hash-collision "pair" gets bit 63 of lo and is ignored by k_pair_groups.
 // hi = score(16) << 48 | lib << (sb+32) | r1Seq << 32 | biased r1Coord
 // lo = invalid << 63 | (orient-3) << (sb+32) | r2Seq << 32 | biased r2Coord
+// 64-bit mix of the whole chunk key (hi without score, lo): k_pair_groups_h's sort key
+__device__ __forceinline__ uint64_t mix64(uint64_t h) {
+    h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; return h ^ (h >> 33);
+}
+
 __global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ pairs, uint32_t np, const uint8_t *__restrict__ recs,
                                                     const RecMeta *__restrict__ meta, KeyLayout L, uint64_t *__restrict__ hi,
-                                                    uint64_t *__restrict__ lo, uint2 *__restrict__ idx, uint32_t *__restrict__ val) {
+                                                    uint64_t *__restrict__ lo, uint2 *__restrict__ idx, uint32_t *__restrict__ val,
+                                                    uint64_t *__restrict__ hk) {
     uint32_t p = blockIdx.x * kT + threadIdx.x;
     if (p >= np) return;
     uint32_t a = (uint32_t)(pairs[p] >> 32), b = (uint32_t)pairs[p];  // a seen first (smaller record index)
@@ -207,10 +215,12 @@ __global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ 
     }
     const uint16_t score = (uint16_t)((int16_t)(uint16_t)(ma & 0xFFFF) + (int16_t)(uint16_t)(mb & 0xFFFF));
     const uint64_t lib = (ma >> 16) & 0xFFFF;
-    hi[p] = ((uint64_t)score << 48) | (lib << (L.sb + 32)) | ((uint64_t)(uint32_t)r1s << 32) |
-            (uint64_t)((uint32_t)r1c ^ 0x80000000u);
-    lo[p] = bad | ((uint64_t)(o - RE_FF) << (L.sb + 32)) | ((uint64_t)(uint32_t)r2s << 32) |
-            (uint64_t)((uint32_t)r2c ^ 0x80000000u);
+    const uint64_t kh = (lib << (L.sb + 32)) | ((uint64_t)(uint32_t)r1s << 32) | (uint64_t)((uint32_t)r1c ^ 0x80000000u);
+    const uint64_t kl = bad | ((uint64_t)(o - RE_FF) << (L.sb + 32)) | ((uint64_t)(uint32_t)r2s << 32) |
+                        (uint64_t)((uint32_t)r2c ^ 0x80000000u);
+    hi[p] = ((uint64_t)score << 48) | kh;
+    lo[p] = kl;
+    hk[p] = mix64(mix64(kh) ^ kl);
     idx[p] = make_uint2(i1, i2);
     val[p] = p;
 }
@@ -255,14 +265,7 @@ __global__ __launch_bounds__(kT) void k_pair_groups(const uint64_t *__restrict__
 // index, which is the reference's "first strict max" in its index-ordered chunk).  So pairs are
 // sorted on 32 bits of a 64-bit hash of the full key (4 radix passes instead of 10 for the two
 // 48-bit key words) and every run of equal hash bits is split into its exact keys here.
-__device__ __forceinline__ uint64_t mix64(uint64_t h) {
-    h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; return h ^ (h >> 33);
-}
-__global__ __launch_bounds__(kT) void k_pair_hash(const uint64_t *__restrict__ hi, const uint64_t *__restrict__ lo, uint32_t np,
-                                                   uint64_t *__restrict__ hk) {
-    const uint32_t p = blockIdx.x * kT + threadIdx.x;
-    if (p < np) hk[p] = mix64(mix64(hi[p] & ((1ull << 48) - 1)) ^ lo[p]);
-}
+// (the pair's hash sort key, 32 bits of which group equal chunk keys, is written by k_pair_build)
 
 __device__ __forceinline__ void pair_chunk(const uint32_t *__restrict__ sval, const uint64_t *__restrict__ hi,
                                            const uint64_t *__restrict__ lo, const uint2 *__restrict__ idx, uint32_t q,
@@ -637,11 +640,9 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
         if (!hi || !lo || !lo2 || !hi2 || !pidx || !pv || !pv2) return OGE_ERR_HIP;
         const uint32_t pb = oge_ceil_div(np, kT);
         hipLaunchKernelGGL(k_pair_build, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)spairs, np,
-                           (const uint8_t *)d_recs, meta, L, hi, lo, pidx, pv);
+                           (const uint8_t *)d_recs, meta, L, hi, lo, pidx, pv, hi2);
         OGE_LAUNCH_CHECK(ctx);
-        // 32 bits of a hash of the whole chunk key group equal keys (k_pair_groups_h splits runs)
-        hipLaunchKernelGGL(k_pair_hash, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)hi, (const uint64_t *)lo, np, hi2);
-        OGE_LAUNCH_CHECK(ctx);
+        // 32 bits of a hash of the whole chunk key (hi2) group equal keys (k_pair_groups_h splits runs)
         uint64_t *k2;
         uint32_t *v2;
         // debug_hash_bits (tests) also narrows these bits, so runs holding several keys are exercised
