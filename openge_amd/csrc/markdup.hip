@@ -182,7 +182,7 @@ __device__ __forceinline__ int orient_byte(bool r1neg, bool r2neg) {
 }
 
 // Pairs (a << 32 | b, sorted by a) -> pair ReadEnds group keys.  The pair key is confirmed here
-// (same_pair_key); a hash-collision "pair" gets bit 63 of lo and is ignored by k_pair_groups.
+// (same_pair_key); a hash-collision "pair" gets bit 63 of lo and is ignored by k_pair_groups_h.
 // hi = score(16) << 48 | lib << (sb+32) | r1Seq << 32 | biased r1Coord
 // lo = invalid << 63 | (orient-3) << (sb+32) | r2Seq << 32 | biased r2Coord
 // 64-bit mix of the whole chunk key (hi without score, lo): k_pair_groups_h's sort key
@@ -223,41 +223,6 @@ __global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ 
     hk[p] = mix64(mix64(kh) ^ kl);
     idx[p] = make_uint2(i1, i2);
     val[p] = p;
-}
-
-__global__ __launch_bounds__(kT) void k_gather_u64(const uint64_t *__restrict__ src, const uint32_t *__restrict__ by,
-                                                    uint32_t n, uint64_t *__restrict__ dst) {
-    uint32_t p = blockIdx.x * kT + threadIdx.x;
-    if (p < n) dst[p] = src[by[p]];
-}
-
-// One thread per pair group (sorted by (hi, lo)): best = max score, ties -> smallest read1 index.
-__global__ __launch_bounds__(kT) void k_pair_groups(const uint64_t *__restrict__ shi, const uint32_t *__restrict__ sval,
-                                                     const uint64_t *__restrict__ lo, const uint2 *__restrict__ idx, uint32_t np,
-                                                     uint8_t *__restrict__ dup) {
-    uint32_t q = blockIdx.x * kT + threadIdx.x;
-    if (q >= np) return;
-    const uint64_t kmask = (1ull << 48) - 1;
-    const uint64_t h = shi[q] & kmask, l = lo[sval[q]];
-    if (l >> 63) return;  // unconfirmed pair key (hash collision): not a pair
-    if (q > 0 && (shi[q - 1] & kmask) == h && lo[sval[q - 1]] == l) return;
-    uint32_t e = q + 1;
-    while (e < np && (shi[e] & kmask) == h && lo[sval[e]] == l) ++e;
-    if (e - q < 2) return;
-    uint32_t best = q;
-    int16_t bs = (int16_t)(uint16_t)(shi[q] >> 48);
-    uint32_t bi = idx[sval[q]].x;
-    for (uint32_t x = q + 1; x < e; ++x) {
-        const int16_t s = (int16_t)(uint16_t)(shi[x] >> 48);
-        const uint32_t i1 = idx[sval[x]].x;
-        if (s > bs || (s == bs && i1 < bi)) { best = x; bs = s; bi = i1; }
-    }
-    for (uint32_t x = q; x < e; ++x) {
-        if (x == best) continue;
-        const uint2 ii = idx[sval[x]];
-        dup[ii.x] = 1;
-        dup[ii.y] = 1;
-    }
 }
 
 // Pair chunks (markDuplicatePairs, :488-507) need equal (lib, r1Seq, r1Coord, orient, r2Seq, r2Coord)
