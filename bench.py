@@ -2,31 +2,43 @@
 """bench.py -- OpenGE post-alignment hot path on MI355X.
 
 Metric (BASELINE.json): Mreads/s of sort+dedup (`openge mergesort -M --nosplit` semantics: coordinate
-sort, Picard MarkDuplicates with -v semantics, output records re-encoded with bin recompute and
-FLAG 0x400 applied).  Workload at N=1: configs[1]+[2] -- a 300M-read (150M pairs) 30x WGS-shaped
-synthetic read set (SURVEY.md §8d C2 generator, seed 1234), generated straight into HBM; one step =
-the whole device pipeline over the resident records (oge_sort_markdup_dev).
+sort, Picard MarkDuplicates with -v semantics, FLAG 0x400 applied, bins recomputed, header
+regenerated).  Workload at N=1: configs[1]+[2] -- a 300M-read (150M pairs) 30x WGS-shaped synthetic
+read set (SURVEY.md §8d C2 generator, seed 1234).
+
+value (SURVEY §8d timing rule, BAM in -> BAM out at BGZF level 6): one step is the whole
+`mergesort -M` chain over a BGZF BAM file resident in HBM when the timed region starts
+(oge_mergesort_bgzf_dev: framing index, inflate + CRC-32, record walk, sort + dedup, header,
+level-6 deflate, EOF block; the output BAM file ends in HBM).  The input file is made once before
+the timed region by the library's own GPU deflate at level 6 from the device generator.
+
+Also on the same JSON line:
+  kernel_step   -- the sort+dedup device pipeline alone over records already decoded in HBM
+                   (oge_sort_markdup_dev), the round-1 headline, with its stage times
+  pcie_inclusive-- one more e2e run with the compressed input uploaded from / the output downloaded
+                   to page-locked host memory inside the timed region (never `value`)
+  roofline      -- the e2e step's dominant kernel: algorithmic bytes per launch / its HIP-event time
+                   (events on the context stream), traffic from the committed rocprofv3 PMC summary
+  cpu_baseline  -- the REFERENCE itself (oracle/_ref/ref_driver: OpenGE's own ReadSorter +
+                   MarkDuplicates + BamSerializer modules compiled from its sources here, the
+                   mergesort -M --nosplit chain with -v) timed on this box's host cores on a bounded
+                   BAM-in/BAM-out sample of the same generator
+  realign       -- configs[4]: openge localrealign on the C5 set (50k indel intervals)
 
 Multi-GPU (torchrun, one rank per GPU): the same 300M-read sample split across N ranks (strong
 scaling); openge_amd/shard.py routes records to the rank owning their contig with an RCCL all-to-all
 over xGMI (ghost copies of cross-rank mates keep MarkDuplicates exact), each rank sorts + dedups its
-range, and the ranks' outputs concatenate into the single-GPU result.  value = reads / max-over-ranks
-wall time.
-
-Also reported on the same JSON line:
-  roofline     -- dominant kernel (the permutation gather, algorithmic bytes 2*B per launch, B = record
-                  bytes) timed live with HIP events on the stream it runs on; traffic from the committed
-                  rocprofv3 PMC summary when present (profiles/)
-  pipeline     -- the same for the whole step (algorithmic bytes of SURVEY §8d: sort 2B + dedup B-seq+2N)
-  cpu_baseline -- the oracle port (oracle/oge_oracle.c, single thread, in memory) timed on this box's host
-                  on a bounded C2-shaped sample
+range.  value = reads / max-over-ranks wall time.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import struct
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -35,34 +47,100 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mreads/sec sort+dedup (and realign intervals/sec), 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
-STAGES = ["input_pass", "sort_radix", "sort_ties", "meta_gather", "md_matejoin", "md_pairs", "md_frags", "md_apply",
-          "gather_offsets", "gather_records"]
+# int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md: SIMD-32, a wave64
+# VALU instruction issues over 2 cycles)
+VALU_INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+KERNEL_STAGES = ["input_pass", "sort_radix", "sort_ties", "meta_gather", "md_matejoin", "md_pairs", "md_frags",
+                 "md_apply", "gather_offsets", "gather_records"]
+E2E_STAGES = ["bgzf_index", "bgzf_inflate", "bgzf_crc", "rec_walk"] + KERNEL_STAGES + ["bgzf_deflate"]
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--pairs", type=int, default=150_000_000, help="read pairs per GPU (default 150M = 300M reads)")
-    ap.add_argument("--cpu-sample-reads", type=int, default=8_000_000)
+    ap.add_argument("--pairs", type=int, default=150_000_000, help="read pairs (default 150M = 300M reads)")
+    ap.add_argument("--level", type=int, default=6, help="BGZF level of the input file and of the output")
+    ap.add_argument("--kernel-steps", type=int, default=3, help="timed steps of the kernel-only leg")
+    ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the reference (box CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-realign", action="store_true", help="skip the localrealign (C5) leg")
+    ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--realign-intervals", type=int, default=50_000)
     ap.add_argument("--realign-only", action="store_true", help="profiling aid: only the C5 realign leg")
+    ap.add_argument("--e2e-only", action="store_true", help="profiling aid: skip every leg but the e2e steps")
     return ap.parse_args()
 
 
-VALU_INT32_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12  # CUs x SIMDs x lanes/clk x 2.4 GHz (MI355X_MICROARCH.md)
+def log(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+# ------------------------------------------------------------------------------------------- helpers
+def bam_header_bytes(header_text: str) -> bytes:
+    """BamSerializer::open's header block (util/bam_serializer.h:54-76): magic, text, reference list."""
+    refs = []
+    for ln in header_text.splitlines():
+        if ln.startswith("@SQ"):
+            f = dict(x.split(":", 1) for x in ln.split("\t")[1:])
+            refs.append((f["SN"], int(f["LN"])))
+    t = header_text.encode()
+    out = b"BAM\1" + struct.pack("<i", len(t)) + t + struct.pack("<i", len(refs))
+    for nm, ln in refs:
+        b = nm.encode() + b"\0"
+        out += struct.pack("<i", len(b)) + b + struct.pack("<i", ln)
+    return out
+
+
+def stage_ms(ctx, names) -> dict:
+    out = {}
+    for s in names:
+        v = ctx.timing(s)
+        if v >= 0:
+            out[s] = v
+    return out
+
+
+def pmc_traffic(kernel: str, rec_bytes: int) -> dict | None:
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*_pmc.json,
+    written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md).  Scaled by record bytes when the profiled workload
+    differed."""
+    files = sorted(f for f in (ROOT / "profiles").glob("r*_pmc.json") if "realign" not in f.name)
+    for fn in reversed(files):
+        try:
+            d = json.loads(fn.read_text())
+        except Exception:
+            continue
+        for name, v in d.get("kernels", {}).items():
+            if kernel in name:
+                w = d.get("workload", {})
+                b = w.get("record_bytes_rank0") or w.get("record_bytes_per_gpu") or rec_bytes
+                return {"bytes": v["hbm_bytes"] * rec_bytes / b, "source": fn.name}
+    return None
+
+
+# kernel per e2e stage (the launch the stage time belongs to) and its algorithmic bytes
+def stage_kernels(B: int, zin: int, zout: int, n: int, seq_bytes: int) -> dict:
+    return {
+        "bgzf_inflate": ("k_infl", "BGZF inflate: compressed bytes read + payload bytes written", zin + B),
+        "bgzf_deflate": ("k_defl", "BGZF deflate (level 6): payload read + compressed bytes written", B + zout),
+        "gather_records": ("k_gather16", "permutation gather + BAM re-encode: 2*B (SURVEY §8d sort bytes)", 2 * B),
+        "input_pass": ("k_input_pass", "record parse: B - packed bases (SURVEY §8d dedup bytes) + 2N",
+                       B - seq_bytes + 2 * n),
+        "bgzf_crc": ("k_crc_check", "CRC-32 of every payload: B", B),
+    }
+
+
+# --------------------------------------------------------------------------------------------- legs
 def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1) -> dict | None:
     """configs[4]: openge localrealign on the C5 synthetic set (50k indel intervals, 24 contigs).
     Host phases (binning, consensus generation, decisions, mate fixing) + the HIP offset scan; the
     records are decoded in host memory before the timed region (the module's input queue).  With
     world > 1 every rank realigns its contig range (openge_amd/realign_shard.py, no exchange); the
     time is the max over ranks between barriers.  Returns the result on rank 0 (None elsewhere)."""
-    import tempfile
     from openge_amd import lib as L
     from openge_amd import realign_shard as RS
 
@@ -102,6 +180,7 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1) -> dict | 
     valu = realign_pmc_valu()
     t_k = st["scan_kernel_ms"] / 1e3
     ach = valu["lane_ops"] / t_k / 1e12 if (valu and t_k > 0 and n_intervals == 50_000) else None
+    cmp_t = st["scan_ops"] / t_k / 1e12 if t_k > 0 else None
     return {"metric": "realign intervals/sec", "value": round(n_intervals / dt, 1), "unit": "intervals/s",
             "workload": f"C5: {n_intervals} indel intervals, 24 contigs, {b.n} reads (seed 1234)",
             "seconds": round(dt, 3), "host_threads": 16, "stats": st,
@@ -113,10 +192,11 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1) -> dict | 
                          "lane_ops": valu["lane_ops"] if valu else None,
                          "lane_ops_source": valu["source"] if valu else None, "avg_ms": st["scan_kernel_ms"],
                          "algorithmic_compares": st["scan_ops"],
-                         "compares_per_s_T": round(st["scan_ops"] / t_k / 1e12, 2) if t_k > 0 else None},
+                         "compares_per_s_T": round(cmp_t, 2) if cmp_t else None,
+                         "compares_frac": round(cmp_t / VALU_INT32_PEAK_TOPS, 4) if cmp_t else None},
             "cpu_reference_here": {"value": 1520.0, "unit": "intervals/s", "cores": 8,
                                    "note": "oracle/_ref/ref_driver realign -t 8 on the same C5 set in the build "
-                                           "container (32.9 s); the reference cannot run on the GPU box"}}
+                                           "container (32.9 s)"}}
 
 
 def realign_pmc_valu() -> dict | None:
@@ -133,40 +213,94 @@ def realign_pmc_valu() -> dict | None:
         return None
 
 
-def cpu_baseline(sample_reads: int) -> dict:
-    """The oracle port (TEST INFRASTRUCTURE, timed as the CPU baseline only) on a C2-shaped sample."""
-    import oracle
+def cpu_baseline_reference(sample_reads: int, threads: int) -> dict:
+    """The REFERENCE (TEST INFRASTRUCTURE, timed as the CPU baseline only): oracle/_ref/ref_driver is
+    OpenGE's own FileReader -> ReadSorter -> MarkDuplicates -> BamSerializer<BgzfOutputStream> chain
+    (command_mergesort.cpp:68-117 with -M --nosplit -v, n = 500,000 reads per run, level-0 temp runs,
+    level-6 dedup temp file and output) compiled from its sources by oracle/Makefile.ref.  Timed
+    BAM file in -> BAM file out on this box's host cores, on a bounded sample of the C2 generator."""
     from openge_amd import lib as L
 
-    p = L.synth_params(sample_reads // 2, preset="c2", seed=1234)
-    recs, offs, hdr = L.synth_host(p)
-    n = 2 * (sample_reads // 2)
-    t0 = time.perf_counter()
-    perm = oracle.sort_perm(recs, offs, n)
-    oracle.markdup(recs, offs[:-1][perm], n, hdr)
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt / 1e6, 4), "unit": "Mreads/s", "cores": 1, "kind": "port",
-            "sample": f"{n} reads of the C2 generator (seed 1234), in-memory oracle sort + markdup, 1 thread",
-            "seconds": round(dt, 2)}
+    drv = ROOT / "oracle" / "_ref" / "ref_driver"
+    if not drv.exists():
+        return {"value": None, "kind": "reference", "note": f"{drv} missing (built only where /root/reference exists)"}
+    n_pairs = sample_reads // 2
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        src, dst = os.path.join(td, "in.bam"), os.path.join(td, "out.bam")
+        p = L.synth_params(n_pairs, preset="c2", seed=1234)
+        recs, offs, hdr = L.synth_host(p, threads=threads)
+        L.write_bam(src, hdr, recs, offs, len(offs) - 1, level=6, threads=threads)
+        del recs, offs
+        t0 = time.perf_counter()
+        r = subprocess.run([str(drv), "sortdedup", "-v", "-t", str(threads), "-n", "500000", "-c", "6", "-T", td, src, dst],
+                           capture_output=True, text=True, timeout=900)
+        dt = time.perf_counter() - t0
+        if r.returncode != 0:
+            return {"value": None, "kind": "reference", "note": f"ref_driver exit {r.returncode}: {r.stderr[-300:]}"}
+        marked = [ln for ln in r.stderr.splitlines() if "uplicate" in ln][-1:]
+    n = 2 * n_pairs
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mreads/s", "cores": threads, "kind": "reference",
+            "sample": f"{n} reads of the C2 generator (seed 1234) as a level-6 BAM file -> OpenGE's own "
+                      f"mergesort -M --nosplit -v chain (oracle/_ref/ref_driver sortdedup -t {threads} -n 500000) "
+                      "-> level-6 BAM file, wall time",
+            "seconds": round(dt, 2), "reference_log_tail": marked}
 
 
-def pmc_traffic(kernel: str, rec_bytes: int) -> dict | None:
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*_pmc.json,
-    written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes).
-    When the profiled workload had a different record-byte total, the count is scaled by bytes."""
-    files = sorted(f for f in (ROOT / "profiles").glob("r*_pmc.json") if "realign" not in f.name)
-    if not files:
-        return None
-    try:
-        d = json.loads(files[-1].read_text())
-    except Exception:
-        return None
-    for name, v in d.get("kernels", {}).items():
-        if kernel in name:
-            w = d.get("workload", {})
-            b = w.get("record_bytes_rank0") or w.get("record_bytes_per_gpu") or rec_bytes
-            return {"bytes": v["hbm_bytes"] * rec_bytes / b, "source": files[-1].name}
-    return None
+def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, "torch.Tensor", int, object]:
+    """Records generated straight into HBM after a `hlen`-byte BAM header prefix (the buffer later
+    becomes the input file); the sort+dedup device pipeline alone over the resident records."""
+    d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), None)
+    ctx.sync()
+    B = int(d_offs[-1].item())
+    S = torch.empty(hlen + B + 64, dtype=torch.uint8, device=dev)
+    d_offs += hlen
+    ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), S.data_ptr())
+    ctx.sync()
+    import ctypes as C
+    buf = C.create_string_buffer(1 << 16)
+    L.check(L.lib().oge_synth_header_text(C.byref(p), buf, 1 << 16, None))
+    hdr_text = buf.value.decode()
+    opts, keep = L.markdup_opts_from_header(hdr_text, p.n_ref)
+    res = {"skipped": True}
+    if args.kernel_steps > 0:
+        d_out = torch.empty(B + 64, dtype=torch.uint8, device=dev)
+        d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        d_perm = torch.empty(n, dtype=torch.int32, device=dev)
+        step = lambda: ctx.sort_markdup_dev(S.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(),
+                                            d_out.data_ptr(), d_out_off.data_ptr())
+        step()  # first call: workspace growth, code-object load
+        torch.cuda.synchronize(dev)
+        tot = {s: 0.0 for s in KERNEL_STAGES}
+        t0 = time.perf_counter()
+        for _ in range(args.kernel_steps):
+            nd = step()
+            for s, v in stage_ms(ctx, KERNEL_STAGES).items():
+                tot[s] += v
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / args.kernel_steps
+        K = args.kernel_steps
+        sms = {s: round(v / K, 3) for s, v in tot.items()}
+        tg = sms["gather_records"] / 1e3
+        res = {"what": "oge_sort_markdup_dev over records already decoded in HBM (no codec)",
+               "ms_per_step": round(dt * 1e3, 2), "mreads_per_s": round(n / dt / 1e6, 1), "steps": K,
+               "duplicates_flagged": nd, "stages_ms": sms,
+               "gather_roofline": {"kernel": "k_gather16", "achieved_GBps": round(2 * B / tg / 1e9, 1) if tg else None,
+                                   "frac": round(2 * B / tg / 1e9 / HBM_PEAK_GBS, 4) if tg else None,
+                                   "algorithmic_bytes": 2 * B}}
+        del d_out, d_out_off, d_perm
+    del d_offs
+    return res, S, B, hdr_text
+
+
+def build_input(ctx, L, torch, dev, S, total: int, level: int) -> tuple["torch.Tensor", int]:
+    """The input BAM file in HBM: the library's GPU deflate of [header][records] at `level` plus the
+    EOF block, in a buffer of exactly its size (the bound-sized staging buffer is freed)."""
+    bound = int(L.lib().oge_bgzf_bound(total))
+    Z = torch.empty(bound + 64, dtype=torch.uint8, device=dev)
+    zb = ctx.bgzf_deflate_dev(S.data_ptr(), total, level, Z.data_ptr(), bound)
+    ctx.sync()
+    return Z, zb
 
 
 def main():
@@ -196,10 +330,141 @@ def main():
         ctx.close()
         return
 
-    # ---- inputs resident in HBM before the timed region.  One 300M-read sample (C2); with N ranks
-    # each holds 1/N of it (an arbitrary slice of the unsorted input: strong scaling).
     p = L.synth_params(args.pairs, preset="c2", seed=1234)
     n_all = 2 * args.pairs
+    if world > 1:
+        multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank)
+        ctx.close()
+        dist.destroy_process_group()
+        return
+
+    free0, total_mem = torch.cuda.mem_get_info(dev)
+    log(f"HBM free {free0 / 1e9:.1f} / {total_mem / 1e9:.1f} GB")
+    # ---- kernel-only leg; the generated records become the input file
+    import ctypes as C
+    buf = C.create_string_buffer(1 << 16)
+    L.check(L.lib().oge_synth_finalize(C.byref(p)))
+    L.check(L.lib().oge_synth_header_text(C.byref(p), buf, 1 << 16, None))
+    hb = bam_header_bytes(buf.value.decode())
+    n = n_all
+    kargs = argparse.Namespace(**vars(args))
+    if args.e2e_only:
+        kargs.kernel_steps = 0
+    kres, S, B, hdr_text = kernel_leg(ctx, L, torch, dev, p, n, len(hb), kargs)
+    log(f"kernel leg: {kres.get('ms_per_step')} ms/step; records {B / 1e9:.2f} GB")
+    S[:len(hb)].copy_(torch.frombuffer(bytearray(hb), dtype=torch.uint8).to(dev))
+    total = len(hb) + B
+    seq_bytes = n * ((p.read_len + 1) // 2)
+
+    # ---- the input BAM file in HBM (level-6 BGZF, GPU deflate), staging freed
+    Z, zb = build_input(ctx, L, torch, dev, S, total, args.level)
+    del S
+    torch.cuda.empty_cache()
+    d_z = torch.empty(zb + 28 + 64, dtype=torch.uint8, device=dev)
+    d_z[:zb].copy_(Z[:zb])
+    d_z[zb:zb + 28].copy_(torch.tensor(list(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")),
+                                       dtype=torch.uint8, device=dev))
+    zbytes = zb + 28
+    del Z
+    torch.cuda.empty_cache()
+    torch.cuda.synchronize(dev)
+    log(f"input BAM file in HBM: {zbytes / 1e9:.2f} GB (ratio {zbytes / total:.3f})")
+
+    # ---- e2e steps: BAM file in HBM -> mergesort -M chain -> BAM file in HBM
+    mopts = L.mergesort_opts(level=args.level, mark_duplicates=1)
+    step = lambda: ctx.mergesort_bgzf_dev(d_z.data_ptr(), zbytes, mopts)
+    warm = []
+    for _ in range(args.warmup):
+        torch.cuda.synchronize(dev)
+        tw = time.perf_counter()
+        step()
+        torch.cuda.synchronize(dev)
+        warm.append(round((time.perf_counter() - tw) * 1e3, 1))
+        log(f"warmup step {warm[-1]} ms")
+    tot = {}
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    out_bytes = nr = nd = 0
+    for _ in range(args.steps):
+        d_out, out_bytes, nr, nd = step()
+        for s, v in stage_ms(ctx, E2E_STAGES).items():
+            tot[s] = tot.get(s, 0.0) + v
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    K = args.steps
+    ms_step = dt / K * 1e3
+    value = n * K / dt / 1e6
+    sms = {s: round(v / K, 3) for s, v in tot.items()}
+    fr, _ = torch.cuda.mem_get_info(dev)
+    log(f"HBM free during e2e steps {fr / 1e9:.1f} GB")
+    log(f"e2e: {ms_step:.1f} ms/step = {value:.1f} Mreads/s; stages {sms}")
+    assert nr == n, (nr, n)
+
+    # roofline: the dominant kernel of the e2e step
+    kinfo = stage_kernels(B, zbytes, out_bytes, n, seq_bytes)
+    cand = [(sms.get(s, 0.0), s) for s in kinfo]
+    t_dom, s_dom = max(cand)
+    kname, what, abytes = kinfo[s_dom]
+    ach = abytes / (t_dom / 1e3) / 1e9 if t_dom > 0 else 0.0
+    pmc = pmc_traffic(kname, B)
+    roof = {"kernel": f"{kname} ({what})", "stage": s_dom, "bound": "hbm", "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": round(pmc["bytes"]) if pmc else None, "traffic_source": pmc["source"] if pmc else None,
+            "algorithmic_bytes": abytes, "avg_ms": t_dom}
+    others = []
+    for s, (kn, w, ab) in kinfo.items():
+        t = sms.get(s, 0.0)
+        if t > 0:
+            a = ab / (t / 1e3) / 1e9
+            others.append({"stage": s, "kernel": kn, "avg_ms": t, "achieved": round(a, 1), "frac": round(a / HBM_PEAK_GBS, 4)})
+
+    # ---- PCIe-inclusive run (compressed bytes only cross PCIe)
+    pcie = None
+    if not args.no_pcie and not args.e2e_only:
+        hz = torch.empty(zbytes, dtype=torch.uint8, pin_memory=True)
+        hz.copy_(d_z[:zbytes])
+        ho = torch.empty(max(out_bytes, 1) + (1 << 20), dtype=torch.uint8, pin_memory=True)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        d_z[:zbytes].copy_(hz, non_blocking=True)
+        d_out, ob, _, _ = step()
+        L.check(L.lib().oge_memcpy(ctx.h, ho.data_ptr(), d_out, ob, 2), ctx.h)
+        torch.cuda.synchronize(dev)
+        tp = time.perf_counter() - t1
+        pcie = {"what": "upload of the input BAM file from page-locked host memory + the e2e step + download of "
+                        "the output BAM file, one run", "seconds": round(tp, 3), "mreads_per_s": round(n / tp / 1e6, 1),
+                "bytes_up": zbytes, "bytes_down": ob}
+        del hz, ho
+
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "Mreads/s", "n_gpus": 1, "steps": K,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234, as a level-6 BGZF BAM file resident in HBM",
+        "config": {"workload": f"C2+C3 end to end: {n // 1000000}M-read BAM file -> mergesort -M --nosplit "
+                               f"(sort + dedup -v) -> BGZF level-{args.level} BAM file, in HBM",
+                   "reads_total": n, "record_bytes": B, "input_file_bytes": zbytes, "output_file_bytes": out_bytes,
+                   "duplicates_flagged": nd, "parallelism": "1 GPU"},
+        "roofline": roof, "roofline_stages": others, "stages_ms": sms, "warmup_ms": warm,
+        "kernel_step": kres, "pcie_inclusive": pcie,
+    }
+    del d_z
+    torch.cuda.empty_cache()
+    if not args.no_realign and not args.e2e_only:
+        log("realign leg")
+        out["realign"] = realign_leg(ctx, args.realign_intervals)
+    if not args.no_cpu_baseline and not args.e2e_only:
+        log("cpu baseline (reference)")
+        cb = cpu_baseline_reference(args.cpu_sample_reads, args.cpu_threads)
+        if cb.get("value"):
+            cb["gpu_speedup"] = round(value / cb["value"], 1)
+        out["cpu_baseline"] = cb
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
+    """N ranks: contig-sharded sort + dedup with the RCCL all-to-all (openge_amd/shard.py)."""
     s0, s1 = n_all * rank // world, n_all * (rank + 1) // world
     n = s1 - s0
     d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
@@ -208,117 +473,55 @@ def main():
     B = int(d_offs[-1].item())
     d_recs = torch.empty(B + 64, dtype=torch.uint8, device=dev)
     ctx.synth_range_dev(p, s0, n, d_offs.data_ptr(), d_recs.data_ptr())
-    hdr_len = 1 << 16
     import ctypes as C
-    buf = C.create_string_buffer(hdr_len)
-    L.check(L.lib().oge_synth_header_text(C.byref(p), buf, hdr_len, None))
+    buf = C.create_string_buffer(1 << 16)
+    L.check(L.lib().oge_synth_header_text(C.byref(p), buf, 1 << 16, None))
     opts, keep = L.markdup_opts_from_header(buf.value.decode(), p.n_ref)
     ctx.sync()
-
+    from openge_amd import shard
+    backend = shard.HipBackend(ctx)
+    owners = shard.contig_owners([int(p.ref_len[i]) for i in range(p.n_ref)], world)
     shard_t = {}
-    if world == 1:
-        d_out = torch.empty(B + 64, dtype=torch.uint8, device=dev)
-        d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        d_perm = torch.empty(n, dtype=torch.int32, device=dev)
 
-        def step():
-            return ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(),
-                                        d_out.data_ptr(), d_out_off.data_ptr())
-    else:
-        from openge_amd import shard
-        backend = shard.HipBackend(ctx)
-        owners = shard.contig_owners([int(p.ref_len[i]) for i in range(p.n_ref)], world)
+    def step():
+        T = {}
+        out, off, k = shard.sort_markdup_sharded(backend, d_recs, d_offs, n, p.n_ref, owners, opts, timings=T)
+        for key, v in T.items():
+            shard_t[key] = shard_t.get(key, 0.0) + v
+        del out, off
+        return k
 
-        def step():
-            T = {}
-            out, off, k = shard.sort_markdup_sharded(backend, d_recs, d_offs, n, p.n_ref, owners, opts, timings=T)
-            for key, v in T.items():
-                shard_t[key] = shard_t.get(key, 0.0) + v
-            del out, off
-            return k
-
-    warmup_ms = []  # first-call costs (workspace growth, code-object load) stay out of the timed steps
     for _ in range(args.warmup):
-        torch.cuda.synchronize(dev)
-        tw = time.perf_counter()
         step()
-        torch.cuda.synchronize(dev)
-        warmup_ms.append(round((time.perf_counter() - tw) * 1e3, 2))
     shard_t.clear()
-    stage_tot = {s: 0.0 for s in STAGES}
-    if world > 1:
-        dist.barrier()
+    dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    ndup = 0
     for _ in range(args.steps):
-        ndup = step()
-        if world == 1:
-            for s in STAGES:  # HIP events recorded around each stage on the context stream
-                stage_tot[s] += max(ctx.timing(s), 0.0)
+        step()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    dist.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
     realign_multi = None
-    if world > 1 and not args.no_realign:  # every rank realigns its contig range
+    if not args.no_realign:
         realign_multi = realign_leg(ctx, args.realign_intervals, rank, world)
-
     if rank == 0:
         K = args.steps
-        ms_step = dt / K * 1e3
-        value = n_all * K / dt / 1e6
-        out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Mreads/s", "n_gpus": world, "steps": K,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234; records resident in HBM",
-            "config": {"workload": f"C2+C3 sort+dedup (mergesort -M --nosplit semantics), {n_all // 1000000}M reads "
-                                   "in total" + (f", {world} contig-sharded ranks" if world > 1 else ""),
-                       "reads_total": n_all, "reads_rank0": n, "record_bytes_rank0": B,
-                       "parallelism": (f"{world} ranks: contig ownership + RCCL all-to-all + ghost mates"
-                                       if world > 1 else "1 GPU")},
-        }
-        if world == 1:
-            out["config"]["duplicates_flagged"] = ndup
-            stages_ms = {s: round(v / K, 3) for s, v in stage_tot.items()}
-            t_gather = stages_ms["gather_records"] / 1e3
-            gather_bytes = 2 * B  # sort = 2*B (each record read once, written once)
-            achieved = gather_bytes / t_gather / 1e9 if t_gather > 0 else 0.0
-            seq_bytes = n * ((p.read_len + 1) // 2)
-            pipe_bytes = 2 * B + (B - seq_bytes) + 2 * n
-            pipe_gbs = pipe_bytes / (ms_step / 1e3) / 1e9
-            pmc = pmc_traffic("k_gather16", B)
-            out["roofline"] = {"kernel": "k_gather_records (permutation gather + BAM re-encode)", "bound": "hbm",
-                               "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": round(achieved / HBM_PEAK_GBS, 4),
-                               "traffic": round(pmc["bytes"]) if pmc else None,
-                               "traffic_source": pmc["source"] if pmc else None,
-                               "algorithmic_bytes": gather_bytes, "avg_ms": stages_ms["gather_records"]}
-            out["pipeline"] = {"algorithmic_bytes": pipe_bytes, "achieved": round(pipe_gbs, 1), "unit": "GB/s",
-                               "frac": round(pipe_gbs / HBM_PEAK_GBS, 4)}
-            out["stages_ms"] = stages_ms
-            out["warmup_ms"] = warmup_ms
-            if not args.no_realign:
-                out["realign"] = realign_leg(ctx, args.realign_intervals)
-            if not args.no_cpu_baseline:
-                cb = cpu_baseline(args.cpu_sample_reads)
-                cb["gpu_speedup"] = round(value / cb["value"], 1)
-                out["cpu_baseline"] = cb
-        else:
-            out["shard_rank0_s_per_step"] = {k: (round(v / K, 4) if isinstance(v, float) else v // K)
-                                             for k, v in shard_t.items()}
-            if realign_multi is not None:
-                out["realign"] = realign_multi
+        out = {"metric": METRIC, "value": round(n_all * K / dt / 1e6, 2), "unit": "Mreads/s", "n_gpus": world,
+               "steps": K, "warmup": args.warmup, "ms_per_step": round(dt / K * 1e3, 2), "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+               "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234; records resident in HBM",
+               "config": {"workload": f"C2+C3 sort+dedup, {n_all // 1000000}M reads in total, {world} contig-sharded "
+                                      "ranks (records decoded in HBM)", "reads_total": n_all, "reads_rank0": n,
+                          "parallelism": f"{world} ranks: contig ownership + RCCL all-to-all + ghost mates"},
+               "shard_rank0_s_per_step": {k: (round(v / K, 4) if isinstance(v, float) else v // K)
+                                          for k, v in shard_t.items()}}
+        if realign_multi is not None:
+            out["realign"] = realign_multi
         print(json.dumps(out), flush=True)
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

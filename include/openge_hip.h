@@ -135,6 +135,26 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
                          const oge_markdup_opts *opts, uint32_t *d_perm, uint8_t *d_out, uint64_t *d_out_off,
                          uint64_t *n_dup_out);
 
+/* ---- the whole mergesort chain on a BAM file resident in HBM -------------------------- */
+/* FileReader -> ReadSorter -> [MarkDuplicates] -> FileWriter as MergeSortCommand::runCommand wires
+ * it (commands/command_mergesort.cpp:68-117), every stage on the device: BGZF framing index,
+ * inflate + CRC check, record walk, coordinate sort (+ duplicate marking, -M), optional removal
+ * (-R), header regeneration (SO:coordinate, @PG unless program_line is NULL = --nopg), BGZF
+ * deflate, EOF block.  d_z = the whole input file (4-byte aligned).  On success *d_out points at
+ * the whole output BAM file in HBM, valid until the next call on ctx. */
+typedef struct oge_mergesort_opts {
+    int32_t level;                   /* output BGZF level 0..9 (FileWriter -c; default 6) */
+    int32_t mark_duplicates;         /* -M */
+    int32_t remove_duplicates;       /* -R (with -M) */
+    int32_t compat_nonverbose_index; /* oge_markdup_opts field of the same name */
+    int32_t split_chains;            /* oge_markdup_opts field of the same name */
+    int32_t pad0;
+    const char *program_line;        /* @PG CL, or NULL (--nopg) */
+} oge_mergesort_opts;
+void oge_mergesort_opts_init(oge_mergesort_opts *o);
+int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *o,
+                           const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup);
+
 /* ---- multi-GPU contig sharding (replaces SplitByChromosome/SortedMerge) -------------- */
 /* Per record: d_dest = owner rank of its refID (d_owner has n_ref + 1 entries, the last one for
  * refID -1; it must be non-decreasing so rank outputs concatenate in sorted order); d_ghost = the
@@ -265,6 +285,12 @@ int oge_bgzf_deflate(oge_ctx *ctx, const uint8_t *src, uint64_t n, int level, ui
  * (OGE_ERR_ARG when it exceeds cap). */
 int oge_bgzf_index(const uint8_t *z, uint64_t zbytes, uint64_t *d0, uint64_t *d1, uint64_t *uoff, uint32_t *crc,
                    uint64_t cap, uint64_t *nblk);
+/* Device form of oge_bgzf_index for a stream resident in HBM (d_z 4-byte aligned): every byte
+ * position is tested for a block header in parallel and the candidates are accepted only when they
+ * form the exact block chain from offset 0 to zbytes (otherwise the host walk runs on a copy, with
+ * its error messages).  Same outputs and capacity rule as oge_bgzf_index, as device arrays. */
+int oge_bgzf_index_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t *d_d0, uint64_t *d_d1,
+                       uint64_t *d_uoff, uint32_t *d_crc, uint64_t cap, uint64_t *nblk);
 /* Inflate the indexed blocks of d_z (4-byte aligned) into d_out + uoff[i]; d_crc (may be NULL)
  * checks every payload's CRC-32.  Fails with OGE_ERR_IO on corrupt data. */
 int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d_d0, const uint64_t *d_d1,

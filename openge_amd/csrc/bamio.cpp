@@ -9,6 +9,7 @@
 #include <chrono>
 #include <unistd.h>
 #include <sys/mman.h>
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <cstring>
 #include <sstream>
@@ -188,8 +189,18 @@ void BgzfWriter::emit(std::vector<std::vector<uint8_t>> &&blocks) {
     drain();  // the previous batch goes out first
     writing_ = std::move(blocks);
     writer_ = std::thread([this]() {
-        for (auto &o : writing_) fwrite(o.data(), 1, o.size(), f_);
+        for (auto &o : writing_) put(o.data(), o.size());
     });
+}
+
+void BgzfWriter::put(const uint8_t *p, size_t n) {
+    if (n && fwrite(p, 1, n, f_) != n) failed_ = true;
+}
+
+void BgzfWriter::abandon() {
+    drain();
+    pending_.clear();
+    closed_ = true;
 }
 
 static void bgzf_block(const uint8_t *src, size_t n, int level, std::vector<uint8_t> &dst) {
@@ -224,6 +235,31 @@ static void bgzf_block(const uint8_t *src, size_t n, int level, std::vector<uint
     uint32_t isz = (uint32_t)n;
     memcpy(dst.data() + 18 + clen + 4, &isz, 4);
     dst.resize(bsize);
+}
+
+const uint8_t kBgzfEof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+std::vector<uint8_t> bgzf_compress_host(const uint8_t *src, size_t n, int level) {
+    std::vector<uint8_t> out, blk;
+    for (size_t o = 0; o < n; o += kBlockPayload) {
+        bgzf_block(src + o, std::min(kBlockPayload, n - o), level, blk);
+        out.insert(out.end(), blk.begin(), blk.end());
+    }
+    return out;
+}
+
+void add_program_record(BamHeaderModel &h, const std::string &cl) {
+    PgRecord pg;
+    pg.id = "openge";
+    auto has = [&](const std::string &id) {
+        for (auto &p : h.pg)
+            if (p.id == id) return true;
+        return false;
+    };
+    for (int i = 2; has(pg.id); i++) pg.id = "openge-" + std::to_string(i);
+    pg.vn = "0.3-dev";  // OPENGE_VERSION_STRING (oge/CMakeLists.txt:11-12)
+    pg.cl = cl;
+    h.pg.push_back(pg);
 }
 
 void BgzfWriter::write(const void *data, size_t n) {
@@ -278,7 +314,10 @@ void BgzfWriter::write_compressed(const uint8_t *z, size_t n) {
     fflush(f_);
     const int fd = fileno(f_);
     const off_t at = ftello(f_);
-    if (n >= (64ull << 20) && threads_ > 1 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && at >= 0) {
+    // pwrite ignores the offset on an O_APPEND descriptor (`>>` redirection): sequential there
+    const int fl = fcntl(fd, F_GETFL);
+    if (n >= (64ull << 20) && threads_ > 1 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && at >= 0 && fl >= 0 &&
+        !(fl & O_APPEND)) {
         const size_t chunk = 32ull << 20, nch = (n + chunk - 1) / chunk;
         std::atomic<bool> ok(true);
         parallel_for(nch, threads_, [&](size_t c) {
@@ -296,7 +335,7 @@ void BgzfWriter::write_compressed(const uint8_t *z, size_t n) {
         if (ok && fseeko(f_, at + (off_t)n, SEEK_SET) == 0) return;
         fseeko(f_, at, SEEK_SET);  // fall back to one sequential write
     }
-    fwrite(z, 1, n, f_);
+    put(z, n);
 }
 
 void BgzfWriter::close() {
@@ -305,8 +344,8 @@ void BgzfWriter::close() {
     drain();
     std::vector<uint8_t> eof;
     bgzf_block(nullptr, 0, level_, eof);
-    fwrite(eof.data(), 1, eof.size(), f_);
-    fflush(f_);
+    put(eof.data(), eof.size());
+    if (fflush(f_) != 0) failed_ = true;
     closed_ = true;
 }
 

@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -28,6 +29,11 @@ const char *bgzf_codec_name();  // "libdeflate" or "zlib"
 // OGE_BGZF_CODEC=zlib|libdeflate: compress on the host even when the records sit on the device.
 bool bgzf_host_codec_forced();
 
+// Compress n bytes into BGZF blocks (65280-byte payloads) in memory, no EOF marker.
+std::vector<uint8_t> bgzf_compress_host(const uint8_t *src, size_t n, int level);
+// The 28-byte empty BGZF block that ends every BAM file.
+extern const uint8_t kBgzfEof[28];
+
 class BgzfWriter {
 public:
     // level: zlib level 0..9; block payload is 65280 bytes (htslib framing; the reference uses
@@ -42,7 +48,13 @@ public:
     // block is flushed as a block of its own first, so block boundaries stay intact.
     void write_compressed(const uint8_t *z, size_t n);
     void close();  // flush + EOF marker
+    // Make the writer inert without touching the FILE (the caller is about to fclose it after a
+    // failure): a background write in flight is joined, pending bytes are dropped, no EOF block.
+    void abandon();
+    // false once any fwrite / pwrite / fflush failed (sticky); the caller turns it into an exit status
+    bool ok() const { return !failed_; }
 private:
+    void put(const uint8_t *p, size_t n);  // fwrite with the sticky error flag
     void flush_blocks(bool final);
     void emit(std::vector<std::vector<uint8_t>> &&blocks);  // ordered, written by a background thread
     void drain();                                          // wait for the background write
@@ -52,6 +64,7 @@ private:
     int level_, threads_;
     std::vector<uint8_t> pending_;
     bool closed_;
+    std::atomic<bool> failed_{false};
 };
 
 // ---------------- header model ----------------
@@ -71,6 +84,10 @@ struct BamHeaderModel {
     // Library id per read group in the order MarkDuplicates would discover them does not
     // matter; ids here: 1 + index of the distinct LB name, "Unknown Library" last.
 };
+
+// FileWriter's @PG line (algorithms/file_writer.cpp:76-89): ID openge, or openge-k when taken,
+// VN 0.3-dev (OPENGE_VERSION_STRING), CL = the command line.
+void add_program_record(BamHeaderModel &h, const std::string &cl);
 
 // ---------------- BAM ----------------
 struct BamFile {

@@ -93,6 +93,7 @@ void oge_ctx::end_stage(OgeStageTimer *t) {
 }
 
 void oge_ctx::reset_timing() {
+    if (timing_hold) return;
     stage_events.clear();
     event_pool_used = 0;
 }

@@ -823,6 +823,107 @@ __global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t n
     count[c] = k;
 }
 
+
+// ------------------------------------------------------------------------------ BGZF framing index
+// The framing walk of oge_bgzf_index done in parallel: every byte position is tested for a BGZF
+// member header (gzip magic, FLG = FEXTRA, a BC subfield; the same acceptance as the host walk),
+// candidates are compacted in stream order, and the candidate list is accepted only when it is the
+// exact chain 0 -> p + BSIZE -> ... -> end (a false candidate inside deflate data, or a corrupt
+// stream, fails the check and the caller falls back to the host walk, which reports errors).
+__device__ __forceinline__ uint32_t bgzf_head(const uint8_t *__restrict__ z, uint64_t zbytes, uint64_t p) {
+    if (p + 18 > zbytes || z[p] != 31 || z[p + 1] != 139 || z[p + 2] != 8 || z[p + 3] != 4) return 0;
+    const uint32_t xlen = z[p + 10] | ((uint32_t)z[p + 11] << 8);
+    const uint64_t xend = p + 12 + xlen;
+    if (xend > zbytes) return 0;
+    uint32_t bsize = 0;
+    for (uint64_t x = p + 12; x + 4 <= xend;) {
+        const uint32_t slen = z[x + 2] | ((uint32_t)z[x + 3] << 8);
+        if (z[x] == 'B' && z[x + 1] == 'C' && slen == 2 && x + 6 <= xend) bsize = (z[x + 4] | ((uint32_t)z[x + 5] << 8)) + 1;
+        x += 4 + slen;
+    }
+    if (!bsize || p + bsize > zbytes || bsize < 12 + xlen + 8) return 0;
+    return bsize;
+}
+
+constexpr int kIdxPos = 16;  // byte positions per thread
+
+template <bool EMIT>
+__global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z, uint64_t zbytes, uint32_t *__restrict__ cnt,
+                                                   const uint32_t *__restrict__ base, uint64_t *__restrict__ cpos,
+                                                   uint32_t *__restrict__ cbs) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t t = threadIdx.x;
+    const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + t) * kIdxPos;
+    uint32_t mine = 0;
+    if (p0 < zbytes) {
+        const uint32_t *w = (const uint32_t *)(z + p0);
+        uint32_t v[kIdxPos / 4];
+#pragma unroll
+        for (int k = 0; k < kIdxPos / 4; ++k) v[k] = p0 + 4 * k + 4 <= zbytes ? w[k] : 0;
+#pragma unroll
+        for (int k = 0; k < kIdxPos; ++k)
+            if (((v[k >> 2] >> (8 * (k & 3))) & 0xff) == 31 && p0 + k < zbytes && bgzf_head(z, zbytes, p0 + k)) ++mine;
+    }
+    // block-wide exclusive prefix of the per-thread counts
+    const uint32_t lane = t & 63, wv = t >> 6;
+    uint32_t incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t k = 0; k < 4; ++k) {
+        if (k < wv) before += wsum[k];
+        tot += wsum[k];
+    }
+    if (!EMIT) {
+        if (t == 0) cnt[blockIdx.x] = tot;
+        return;
+    }
+    if (!mine) return;
+    uint64_t o = base[blockIdx.x] + before + incl - mine;
+    for (int k = 0; k < kIdxPos; ++k) {
+        const uint64_t p = p0 + k;
+        if (p >= zbytes || z[p] != 31) continue;
+        const uint32_t bs = bgzf_head(z, zbytes, p);
+        if (bs) cpos[o] = p, cbs[o] = bs, ++o;
+    }
+}
+
+// chain check + per-block fields; nonempty[i] = payload size > 0
+__global__ void k_bgzf_chain(const uint8_t *__restrict__ z, uint64_t zbytes, const uint64_t *__restrict__ cpos,
+                             const uint32_t *__restrict__ cbs, uint64_t m, uint32_t *__restrict__ bad,
+                             uint32_t *__restrict__ isz) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t p = cpos[i], e = p + cbs[i];
+    const bool ok = (i == 0 ? p == 0 : cpos[i - 1] + cbs[i - 1] == p) && (i + 1 == m ? e == zbytes : true);
+    const uint32_t s = z[e - 4] | ((uint32_t)z[e - 3] << 8) | ((uint32_t)z[e - 2] << 16) | ((uint32_t)z[e - 1] << 24);
+    if (!ok || s > kSlot) atomicAdd(bad, 1u);
+    isz[i] = s;
+}
+
+__global__ void k_bgzf_fill(const uint8_t *__restrict__ z, const uint64_t *__restrict__ cpos, const uint32_t *__restrict__ cbs,
+                            const uint32_t *__restrict__ isz, const uint32_t *__restrict__ slot, uint64_t m,
+                            uint64_t *__restrict__ d0, uint64_t *__restrict__ d1, uint64_t *__restrict__ usz,
+                            uint32_t *__restrict__ crc) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m || !isz[i]) return;
+    const uint64_t p = cpos[i], e = p + cbs[i], k = slot[i];
+    d0[k] = p + 12 + (z[p + 10] | ((uint32_t)z[p + 11] << 8));
+    d1[k] = e - 8;
+    usz[k] = isz[i];
+    crc[k] = z[e - 8] | ((uint32_t)z[e - 7] << 8) | ((uint32_t)z[e - 6] << 16) | ((uint32_t)z[e - 5] << 24);
+}
+
+__global__ void k_nonzero_u32(const uint32_t *__restrict__ a, uint64_t n, uint32_t *__restrict__ f) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) f[i] = a[i] != 0;
+    else if (i == n) f[i] = 0;
+}
 }  // namespace
 
 // ------------------------------------------------------------------------------------ host side
@@ -864,6 +965,116 @@ extern "C" int oge_bgzf_index(const uint8_t *z, uint64_t zbytes, uint64_t *d0, u
     if (k <= cap && uoff) uoff[k] = total;
     *nblk = k;
     return k <= cap ? OGE_OK : oge_fail(nullptr, OGE_ERR_ARG, "index capacity too small");
+}
+
+
+// Device framing index into the context's workspace (pointers valid until the next call that uses
+// it).  Returns 1 (no error recorded) when the candidate chain is not exact: the caller then uses
+// the host walk, which also produces the reference-like error messages.
+int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzfIndex *ix) {
+    hipSetDevice(ctx->device);
+    ix->nblk = 0;
+    ix->total = 0;
+    if (!zbytes) return OGE_OK;
+    if ((uintptr_t)d_z & 3) return 1;
+    const uint64_t per_blk = 256ull * kIdxPos;
+    const uint64_t G = (zbytes + per_blk - 1) / per_blk;
+    if (G > 0xffffffffull) return 1;
+    uint32_t *cnt = (uint32_t *)ctx->ws("bix_cnt", (G + 1) * 4);
+    uint32_t *base = (uint32_t *)ctx->ws("bix_base", (G + 1) * 4);
+    uint32_t *bad = (uint32_t *)ctx->ws("bix_bad", 16);
+    if (!cnt || !base || !bad) return OGE_ERR_HIP;
+    k_bgzf_cand<false><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, cnt, nullptr, nullptr, nullptr);
+    OGE_LAUNCH_CHECK(ctx);
+    OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + G, 0, 4, ctx->stream));
+    int rc = oge_exclusive_scan_u32(ctx, cnt, base, G + 1);
+    if (rc) return rc;
+    uint32_t m32 = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&m32, base + G, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t m = m32;
+    if (!m) return 1;
+    uint64_t *cpos = (uint64_t *)ctx->ws("bix_cpos", m * 8);
+    uint32_t *cbs = (uint32_t *)ctx->ws("bix_cbs", m * 4);
+    uint32_t *isz = (uint32_t *)ctx->ws("bix_isz", (m + 1) * 4);
+    uint32_t *slot = (uint32_t *)ctx->ws("bix_slot", (m + 1) * 4);
+    if (!cpos || !cbs || !isz || !slot) return OGE_ERR_HIP;
+    k_bgzf_cand<true><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, cnt, base, cpos, cbs);
+    OGE_LAUNCH_CHECK(ctx);
+    OGE_HIP_TRY(ctx, hipMemsetAsync(bad, 0, 4, ctx->stream));
+    k_bgzf_chain<<<oge_ceil_div(m, 256), 256, 0, ctx->stream>>>(d_z, zbytes, cpos, cbs, m, bad, isz);
+    OGE_LAUNCH_CHECK(ctx);
+    k_nonzero_u32<<<oge_ceil_div(m + 1, 256), 256, 0, ctx->stream>>>(isz, m, slot);
+    OGE_LAUNCH_CHECK(ctx);
+    rc = oge_exclusive_scan_u32(ctx, slot, slot, m + 1);
+    if (rc) return rc;
+    uint32_t hb[2] = {0, 0};
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&hb[0], bad, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&hb[1], slot + m, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (hb[0]) return 1;
+    const uint64_t nb = hb[1];
+    uint64_t *ix64 = (uint64_t *)ctx->ws("bix_out", (3 * nb + 2) * 8);
+    uint32_t *crc = (uint32_t *)ctx->ws("bix_crc", (nb + 1) * 4);
+    if (!ix64 || !crc) return OGE_ERR_HIP;
+    uint64_t *d0 = ix64, *d1 = ix64 + nb, *uoff = ix64 + 2 * nb;
+    k_bgzf_fill<<<oge_ceil_div(m, 256), 256, 0, ctx->stream>>>(d_z, cpos, cbs, isz, slot, m, d0, d1, uoff, crc);
+    OGE_LAUNCH_CHECK(ctx);
+    OGE_HIP_TRY(ctx, hipMemsetAsync(uoff + nb, 0, 8, ctx->stream));
+    rc = oge_exclusive_scan_u64(ctx, uoff, uoff, nb + 1);
+    if (rc) return rc;
+    uint64_t total = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&total, uoff + nb, 8, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ix->d0 = d0;
+    ix->d1 = d1;
+    ix->uoff = uoff;
+    ix->crc = crc;
+    ix->nblk = nb;
+    ix->total = total;
+    return OGE_OK;
+}
+
+extern "C" int oge_bgzf_index_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t *d_d0, uint64_t *d_d1,
+                                  uint64_t *d_uoff, uint32_t *d_crc, uint64_t cap, uint64_t *nblk) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if (!nblk || (zbytes && !d_z)) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    hipSetDevice(ctx->device);
+    ctx->reset_timing();
+    OgeStageTimer *tm = ctx->begin_stage("bgzf_index");
+    OgeBgzfIndex ix;
+    int rc = oge_bgzf_index_ws(ctx, d_z, zbytes, &ix);
+    ctx->end_stage(tm);
+    if (rc == 1) {  // not an exact chain: the host walk (and its error messages)
+        std::vector<uint8_t> h(zbytes);
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(h.data(), d_z, zbytes, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        uint64_t nb = 0;
+        rc = oge_bgzf_index(h.data(), zbytes, nullptr, nullptr, nullptr, nullptr, 0, &nb);
+        if (rc != OGE_OK && rc != OGE_ERR_ARG) return oge_fail(ctx, rc, oge_last_error(nullptr));
+        std::vector<uint64_t> a(3 * nb + 1);
+        std::vector<uint32_t> c(nb + 1);
+        rc = oge_bgzf_index(h.data(), zbytes, a.data(), a.data() + nb, a.data() + 2 * nb, c.data(), nb, &nb);
+        if (rc) return oge_fail(ctx, rc, oge_last_error(nullptr));
+        *nblk = nb;
+        if (nb > cap) return oge_fail(ctx, OGE_ERR_ARG, "index capacity too small");
+        if (d_d0) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_d0, a.data(), nb * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (d_d1) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_d1, a.data() + nb, nb * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (d_uoff) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_uoff, a.data() + 2 * nb, (nb + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (d_crc) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_crc, c.data(), nb * 4, hipMemcpyHostToDevice, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return OGE_OK;
+    }
+    if (rc) return rc;
+    *nblk = ix.nblk;
+    if (ix.nblk > cap) return oge_fail(ctx, OGE_ERR_ARG, "index capacity too small");
+    const uint64_t nb = ix.nblk;
+    if (d_d0 && nb) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_d0, ix.d0, nb * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    if (d_d1 && nb) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_d1, ix.d1, nb * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    if (d_uoff) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_uoff, ix.uoff, (nb + 1) * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    if (d_crc && nb) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_crc, ix.crc, nb * 4, hipMemcpyDeviceToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return OGE_OK;
 }
 
 extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d_d0,

@@ -5,6 +5,7 @@
 #include <chrono>
 #include <climits>
 #include <cstdio>
+#include <cerrno>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -542,6 +543,10 @@ int FileWriter::write_device(ChainContext &cc, ReadBatch &b, BgzfWriter &w, doub
         return std::chrono::duration<double>(z - a).count();
     };
     *t_dev = *t_d2h = *t_wait = 0;
+    if (const char *f = getenv("OGE_TEST_FAIL"); f && !strcmp(f, "write_device")) {  // test hook: a failed device write
+        fprintf(stderr, "openge: FileWriter: injected failure (OGE_TEST_FAIL=write_device)\n");
+        return -1;
+    }
     uint8_t *recs = b.d_recs;
     uint64_t *offs = b.d_offs;
     uint64_t n = b.n;
@@ -630,30 +635,20 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
     if (!on_device) fix_bins(b, cc.threads);
     const auto t2 = clk();
     BamHeaderModel h = b.header;
-    if (!program_line_.empty()) {  // file_writer.cpp:76-89
-        PgRecord pg;
-        pg.id = "openge";
-        auto has = [&](const std::string &id) {
-            for (auto &p : h.pg)
-                if (p.id == id) return true;
-            return false;
-        };
-        for (int i = 2; has(pg.id); i++) pg.id = "openge-" + std::to_string(i);
-        pg.vn = "0.3-dev";  // OPENGE_VERSION_STRING (oge/CMakeLists.txt:11-12)
-        pg.cl = program_line_;
-        h.pg.push_back(pg);
-    }
+    if (!program_line_.empty()) add_program_record(h, program_line_);  // file_writer.cpp:76-89
     FILE *f = filename_ == "stdout" || filename_ == "-" ? stdout : fopen(filename_.c_str(), "wb");
     if (!f) {
         fprintf(stderr, "Error opening BAM file to write.\n");
         return -1;
     }
+    bool write_ok = true;
     {
         BgzfWriter w(f, level_, cc.threads > 0 ? cc.threads : 8);
         std::vector<uint8_t> hb = bam_encode_header(h);
         w.write(hb.data(), hb.size());
         if (on_device) {
             if (write_device(cc, b, w, &t_dev, &t_d2h, &t_wait)) {
+                w.abandon();  // no EOF block and no write into the FILE closed below
                 if (f != stdout) fclose(f);
                 return -1;
             }
@@ -679,8 +674,13 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
             w.write_span(b.recs.data() + s, e - s);
         }
         w.close();
+        write_ok = w.ok();
     }
-    if (f != stdout) fclose(f);
+    if (f != stdout ? fclose(f) != 0 : fflush(f) != 0) write_ok = false;
+    if (!write_ok) {  // a full disk or a closed pipe must not look like success
+        fprintf(stderr, "openge: error writing %s: %s\n", filename_.c_str(), strerror(errno));
+        return -1;
+    }
     if (verbose_ && on_device)
         fprintf(stderr, "[openge] FileWriter: device bins + BGZF %.3f s (gpu, 2.1 GB segments), device->host %.3f s, waiting on the disk %.3f s, "
                 "total %.3f s\n", t_dev, t_d2h, t_wait, sec(t2, clk()));

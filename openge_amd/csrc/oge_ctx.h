@@ -26,6 +26,7 @@ struct oge_ctx {
     std::vector<OgeStageTimer> event_pool;
     size_t event_pool_used = 0;
     bool timing = true;
+    int timing_hold = 0;  // > 0: a composite entry point (the pipeline) keeps its sub-calls' stage events
     bool pool = false;  // allocate from the device's stream-ordered pool and keep freed memory in it
     void *alloc(size_t bytes);
     void release(void *p);
@@ -65,3 +66,12 @@ int oge_radix_sort_pairs(oge_ctx *ctx, uint64_t *keys, uint32_t *vals, uint64_t 
                          uint64_t n, uint64_t bit_mask, uint64_t **kout, uint32_t **vout);
 // OR / AND reduction of a u64 array (for choosing the varying key bits).
 int oge_reduce_or_and_u64(oge_ctx *ctx, const uint64_t *in, uint64_t n, uint64_t mask, uint64_t *or_out, uint64_t *and_out);
+
+// ---- BGZF framing index on the device (inflate.hip) ----
+struct OgeBgzfIndex {
+    uint64_t *d0 = nullptr, *d1 = nullptr, *uoff = nullptr;  // nblk, nblk, nblk + 1 entries (device)
+    uint32_t *crc = nullptr;
+    uint64_t nblk = 0, total = 0;
+};
+// 0 = ok, 1 = candidates are not an exact block chain (use the host walk), < 0 = error
+int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzfIndex *ix);

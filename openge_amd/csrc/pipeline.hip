@@ -1,0 +1,198 @@
+// pipeline.hip -- the whole `openge mergesort [-M]` chain on a BGZF BAM resident in HBM.
+//
+// Replaces the module chain FileReader -> ReadSorter -> [MarkDuplicates] -> FileWriter that
+// MergeSortCommand::runCommand wires (openge/src/commands/command_mergesort.cpp:68-117): the
+// reader's BgzfInputStream + BamDeserializer (util/bgzf_input_stream.cpp:65-142,208-240,
+// util/bam_deserializer.h:143-193), the sorter and marker (algorithms/read_sorter.cpp:48-232,
+// algorithms/mark_duplicates.cpp:185-475) and the writer's BamSerializer + BgzfOutputStream
+// (util/bam_serializer.h:105-147, util/bgzf_output_stream.cpp:59-250, @PG at
+// algorithms/file_writer.cpp:76-89).  Every stage runs on the device; the host parses the BAM header
+// (a copy of the stream's first bytes) and compresses the output header block.
+//
+//   index    oge_bgzf_index_ws  (device framing walk)
+//   inflate  oge_bgzf_inflate_dev into X, CRC-32 checked
+//   records  oge_bam_record_offsets_dev (block_size walk)
+//   sort     oge_sort_markdup_dev (or sort + gather without -M) X -> Y, bins recomputed
+//   [-R]     oge_drop_flagged_dev Y -> X
+//   write    header block (host) + oge_bgzf_deflate_dev + EOF block into the free buffer
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "bamio.h"
+#include "oge_ctx.h"
+
+using namespace oge;
+
+namespace {
+
+struct Hold {  // keep every sub-call's stage events for the caller
+    oge_ctx *c;
+    explicit Hold(oge_ctx *x) : c(x) {
+        c->reset_timing();
+        c->timing_hold++;
+    }
+    ~Hold() { c->timing_hold--; }
+};
+
+// MarkDuplicates::getLibraryName (algorithms/mark_duplicates.cpp:301-318): the LB of the record's
+// @RG, "Unknown Library" when absent or empty; distinct names get distinct ids.
+struct LibTable {
+    std::string ids;
+    std::vector<int16_t> libs;
+    oge_markdup_opts o;
+    LibTable(const BamHeaderModel &h, int32_t n_ref, const oge_mergesort_opts *mo) {
+        std::map<std::string, int16_t> lib_ids;
+        int16_t next = 1;
+        for (auto &rg : h.rg) {
+            const std::string lib = rg.lb.empty() ? std::string("Unknown Library") : rg.lb;
+            auto it = lib_ids.find(lib);
+            if (it == lib_ids.end()) it = lib_ids.emplace(lib, next++).first;
+            libs.push_back(it->second);
+            ids += rg.id;
+            ids.push_back('\0');
+        }
+        auto unk = lib_ids.find("Unknown Library");
+        libs.push_back(0);
+        memset(&o, 0, sizeof o);
+        o.n_ref = n_ref;
+        o.rg_ids = ids.c_str();
+        o.rg_ids_bytes = ids.size();
+        o.rg_lib = libs.data();
+        o.n_rg = (int32_t)h.rg.size();
+        o.unknown_lib = unk != lib_ids.end() ? unk->second : next;
+        o.compat_nonverbose_index = mo->compat_nonverbose_index;
+        o.split_chains = mo->split_chains;
+    }
+};
+
+}  // namespace
+
+extern "C" void oge_mergesort_opts_init(oge_mergesort_opts *o) {
+    if (!o) return;
+    memset(o, 0, sizeof *o);
+    o->level = 6;  // FileWriter's default compression level (commands.cpp:129, -c)
+}
+
+extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *mo,
+                                      const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if (!mo || !d_out || !out_bytes || (zbytes && !d_z)) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    if (mo->level < 0 || mo->level > 9) return oge_fail(ctx, OGE_ERR_ARG, "level must be 0..9");
+    hipSetDevice(ctx->device);
+    Hold hold(ctx);
+    *d_out = nullptr;
+    *out_bytes = 0;
+
+    // ---- framing index (device; host walk of a copy when the chain is not exact)
+    OgeStageTimer *tm = ctx->begin_stage("bgzf_index");
+    OgeBgzfIndex ix;
+    int rc = oge_bgzf_index_ws(ctx, d_z, zbytes, &ix);
+    ctx->end_stage(tm);
+    if (rc < 0) return rc;
+    if (rc == 1) {
+        uint64_t nb = 0;
+        rc = oge_bgzf_index_dev(ctx, d_z, zbytes, nullptr, nullptr, nullptr, nullptr, 0, &nb);
+        if (rc != OGE_OK && rc != OGE_ERR_ARG) return rc;
+        uint64_t *a = (uint64_t *)ctx->ws("pipe_ix", (3 * nb + 2) * 8);
+        uint32_t *c = (uint32_t *)ctx->ws("pipe_ixc", (nb + 1) * 4);
+        if (!a || !c) return OGE_ERR_HIP;
+        rc = oge_bgzf_index_dev(ctx, d_z, zbytes, a, a + nb, a + 2 * nb, c, nb, &nb);
+        if (rc) return rc;
+        ix.d0 = a, ix.d1 = a + nb, ix.uoff = a + 2 * nb, ix.crc = c, ix.nblk = nb;
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&ix.total, ix.uoff + nb, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    const uint64_t total = ix.total;
+    if (!total) return oge_fail(ctx, OGE_ERR_IO, "empty BAM stream (no BAM magic)");
+
+    // ---- inflate into X (X is also the deflate target later: it must hold the bound)
+    const uint64_t cap = std::max<uint64_t>(total, oge_bgzf_bound(total) + (1u << 20)) + 64;
+    uint8_t *X = (uint8_t *)ctx->ws("pipe_x", cap);
+    if (!X) return OGE_ERR_HIP;
+    rc = oge_bgzf_inflate_dev(ctx, d_z, zbytes, ix.d0, ix.d1, ix.uoff, ix.crc, ix.nblk, X);
+    if (rc) return rc;
+
+    // ---- header (host parse of the stream's first bytes)
+    BamFile f;
+    std::string err;
+    size_t rec_base = 0;
+    for (uint64_t pre = std::min<uint64_t>(total, 1 << 20);; pre = std::min<uint64_t>(total, pre * 8)) {
+        std::vector<uint8_t> h(pre);
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(h.data(), X, pre, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        f = BamFile();
+        if (bam_parse_header(h.data(), pre, f, err, &rec_base)) break;
+        if (pre == total) return oge_fail(ctx, OGE_ERR_IO, ("BAM header: " + err).c_str());
+    }
+    const int32_t n_ref = (int32_t)f.ref_names.size();
+
+    // ---- record boundaries
+    tm = ctx->begin_stage("rec_walk");
+    uint64_t n = 0;
+    rc = oge_bam_record_offsets_dev(ctx, X, rec_base, total, n_ref, nullptr, 0, &n);
+    if (rc) return rc;
+    uint64_t *xoff = (uint64_t *)ctx->ws("pipe_xoff", (n + 1) * 8);
+    if (!xoff) return OGE_ERR_HIP;
+    rc = oge_bam_record_offsets_dev(ctx, X, rec_base, total, n_ref, xoff, n + 1, &n);
+    if (rc) return rc;
+    ctx->end_stage(tm);
+
+    // ---- sort (+ markdup), gathered into Y with bins recomputed and 0x400 applied
+    uint8_t *Y = (uint8_t *)ctx->ws("pipe_y", cap);
+    uint64_t *yoff = (uint64_t *)ctx->ws("pipe_yoff", (n + 1) * 8);
+    uint32_t *perm = (uint32_t *)ctx->ws("pipe_perm", (n + 1) * 4);
+    if (!Y || !yoff || !perm) return OGE_ERR_HIP;
+    uint64_t nd = 0;
+    LibTable lt(f.header, n_ref, mo);
+    if (mo->mark_duplicates) {
+        rc = oge_sort_markdup_dev(ctx, X, xoff, n, &lt.o, perm, Y, yoff, &nd);
+    } else {
+        rc = oge_sort_coord_dev(ctx, X, xoff, n, n_ref, perm);
+        if (!rc) rc = oge_gather_records_dev(ctx, X, xoff, perm, n, Y, yoff);
+    }
+    if (rc) return rc;
+    uint8_t *src = Y, *dst = X;
+    uint64_t *soff = yoff;
+    uint64_t m = n;
+    if (mo->mark_duplicates && mo->remove_duplicates) {  // -R: MarkDuplicates::runInternal :456-458
+        tm = ctx->begin_stage("drop_dups");
+        rc = oge_drop_flagged_dev(ctx, Y, yoff, n, 0x400, X, xoff, &m);
+        ctx->end_stage(tm);
+        if (rc) return rc;
+        src = X, dst = Y, soff = xoff;
+    }
+
+    // ---- output: header block(s) (host zlib/libdeflate, tiny), device deflate of the records, EOF
+    BamHeaderModel oh = f.header;
+    oh.sort_order = BamHeaderModel::COORDINATE;  // read_sorter.cpp:257-258
+    if (mo->program_line) add_program_record(oh, mo->program_line);
+    const std::vector<uint8_t> hb = bam_encode_header(oh);
+    const std::vector<uint8_t> hz = bgzf_compress_host(hb.data(), hb.size(), mo->level);
+    uint64_t ends[2] = {0, 0};
+    if (m) {
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&ends[0], soff, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&ends[1], soff + m, 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t len = ends[1] - ends[0];
+    if (hz.size() + oge_bgzf_bound(len) + 28 > cap) return oge_fail(ctx, OGE_ERR_LIMIT, "output buffer too small");
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(dst, hz.data(), hz.size(), hipMemcpyHostToDevice, ctx->stream));
+    uint64_t zb = 0;
+    if (len) {
+        rc = oge_bgzf_deflate_dev(ctx, src + ends[0], len, mo->level, dst + hz.size(), cap - hz.size() - 28, &zb);
+        if (rc) return rc;
+    }
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(dst + hz.size() + zb, kBgzfEof, 28, hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *d_out = dst;
+    *out_bytes = hz.size() + zb + 28;
+    if (n_reads) *n_reads = m;
+    if (n_dup) *n_dup = nd;
+    return OGE_OK;
+}

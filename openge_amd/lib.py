@@ -48,6 +48,21 @@ class FilterOpts(C.Structure):
                                          "max_len", "trim_total")] + [("count_limit", C.c_uint64)]
 
 
+class MergesortOpts(C.Structure):
+    """Mirror of oge_mergesort_opts (include/openge_hip.h)."""
+
+    _fields_ = [(k, C.c_int32) for k in ("level", "mark_duplicates", "remove_duplicates", "compat_nonverbose_index",
+                                         "split_chains", "pad0")] + [("program_line", C.c_char_p)]
+
+
+def mergesort_opts(**over) -> MergesortOpts:
+    o = MergesortOpts()
+    lib().oge_mergesort_opts_init(C.byref(o))
+    for k, v in over.items():
+        setattr(o, k, v)
+    return o
+
+
 class RealignSynthParams(C.Structure):
     """Mirror of oge_realign_synth_params (include/openge_hip.h)."""
 
@@ -228,6 +243,10 @@ def lib() -> C.CDLL:
         "oge_filter_records_dev": (C.c_int, [vp, vp, vp, u64, vp, vp, vp, C.POINTER(u64)]),
         "oge_sort_name_dev": (C.c_int, [vp, vp, vp, u64, vp]),
         "oge_sort_name": (C.c_int, [vp, vp, u64, vp, u64, vp]),
+        "oge_bgzf_index_dev": (C.c_int, [vp, vp, u64, vp, vp, vp, vp, u64, C.POINTER(u64)]),
+        "oge_mergesort_opts_init": (None, [vp]),
+        "oge_mergesort_bgzf_dev": (C.c_int, [vp, vp, u64, vp, C.POINTER(vp), C.POINTER(u64), C.POINTER(u64),
+                                             C.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)
@@ -464,6 +483,20 @@ class Context:
         got = C.c_uint64()
         check(lib().oge_bgzf_inflate(self.h, _ptr(a), len(a), _ptr(out), cap, C.byref(got)), self.h)
         return out[:got.value].tobytes()
+
+    def bgzf_index_dev(self, d_z, zbytes: int, d_d0=None, d_d1=None, d_uoff=None, d_crc=None, cap: int = 0) -> int:
+        nb = C.c_uint64()
+        check(lib().oge_bgzf_index_dev(self.h, d_z, zbytes, d_d0, d_d1, d_uoff, d_crc, cap, C.byref(nb)), self.h)
+        return nb.value
+
+    def mergesort_bgzf_dev(self, d_z, zbytes: int, opts: "MergesortOpts") -> tuple[int, int, int, int]:
+        """The whole mergesort [-M] chain on a BAM file resident in HBM -> (d_out, out_bytes, n_reads,
+        n_dup); d_out (device pointer) is valid until the next call on this context."""
+        d = C.c_void_p()
+        ob, nr, nd = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(lib().oge_mergesort_bgzf_dev(self.h, d_z, zbytes, C.byref(opts), C.byref(d), C.byref(ob), C.byref(nr),
+                                           C.byref(nd)), self.h)
+        return d.value or 0, ob.value, nr.value, nd.value
 
     def record_offsets_dev(self, d_stream, rec_base: int, end: int, n_ref: int, d_off=None, cap: int = 0) -> int:
         n = C.c_uint64()

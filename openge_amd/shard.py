@@ -206,6 +206,8 @@ def sort_markdup_sharded(backend, recs: torch.Tensor, offs: torch.Tensor, n: int
     final_ids = ids_sorted[owned]
     del out, out_off, ids_sorted, dest2, back
     if r_ids.numel():
+        if final_ids.numel() == 0:
+            raise RuntimeError("sharded dedup: an authority message names a record this rank does not own")
         sids, sorder = torch.sort(final_ids)
         pos = torch.searchsorted(sids, r_ids)
         pos = torch.clamp(pos, max=max(sids.numel() - 1, 0))

@@ -157,3 +157,18 @@ def test_cli_gpu_bgzf_equals_host_codec(tmp_path, cmd):
         out[codec] = gzip.decompress(dst.read_bytes())
     assert out["gpu"] == out["libdeflate"]
     assert len(out["gpu"]) > 1_000_000
+
+
+def test_cli_write_failures_exit_nonzero(tmp_path):
+    """a failed device write must leave the writer inert (no write into the closed FILE),
+    and a failed fwrite / fflush / fclose (full disk) must give a non-zero exit, not a truncated BAM
+    with status 0."""
+    import os
+    src = GOLDEN / "inputs" / "208.yhet.bam"
+    env = dict(os.environ, OGE_TEST_FAIL="write_device")
+    r = subprocess.run([OPENGE, "mergesort", "-M", str(src), "-o", str(tmp_path / "f.bam")], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode > 0 and "injected failure" in r.stderr, (r.returncode, r.stderr)
+    r = subprocess.run([OPENGE, "mergesort", "-M", str(src), "-o", "/dev/full"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode > 0 and "error writing" in r.stderr, (r.returncode, r.stderr)
