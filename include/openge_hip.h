@@ -288,7 +288,8 @@ int oge_bgzf_index(const uint8_t *z, uint64_t zbytes, uint64_t *d0, uint64_t *d1
 /* Device form of oge_bgzf_index for a stream resident in HBM (d_z 4-byte aligned): every byte
  * position is tested for a block header in parallel and the candidates are accepted only when they
  * form the exact block chain from offset 0 to zbytes (otherwise the host walk runs on a copy, with
- * its error messages).  Same outputs and capacity rule as oge_bgzf_index, as device arrays. */
+ * its error messages).  Same outputs and capacity rule as oge_bgzf_index, as device arrays; with every
+ * array NULL it only counts (*nblk). */
 int oge_bgzf_index_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t *d_d0, uint64_t *d_d1,
                        uint64_t *d_uoff, uint32_t *d_crc, uint64_t cap, uint64_t *nblk);
 /* Inflate the indexed blocks of d_z (4-byte aligned) into d_out + uoff[i]; d_crc (may be NULL)

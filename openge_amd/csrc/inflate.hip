@@ -1057,6 +1057,7 @@ extern "C" int oge_bgzf_index_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zby
         rc = oge_bgzf_index(h.data(), zbytes, a.data(), a.data() + nb, a.data() + 2 * nb, c.data(), nb, &nb);
         if (rc) return oge_fail(ctx, rc, oge_last_error(nullptr));
         *nblk = nb;
+        if (!d_d0 && !d_d1 && !d_uoff && !d_crc) return OGE_OK;  // count only
         if (nb > cap) return oge_fail(ctx, OGE_ERR_ARG, "index capacity too small");
         if (d_d0) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_d0, a.data(), nb * 8, hipMemcpyHostToDevice, ctx->stream));
         if (d_d1) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_d1, a.data() + nb, nb * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -1067,6 +1068,7 @@ extern "C" int oge_bgzf_index_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zby
     }
     if (rc) return rc;
     *nblk = ix.nblk;
+    if (!d_d0 && !d_d1 && !d_uoff && !d_crc) return OGE_OK;  // count only
     if (ix.nblk > cap) return oge_fail(ctx, OGE_ERR_ARG, "index capacity too small");
     const uint64_t nb = ix.nblk;
     if (d_d0 && nb) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_d0, ix.d0, nb * 8, hipMemcpyDeviceToDevice, ctx->stream));
