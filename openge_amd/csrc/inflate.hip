@@ -1097,14 +1097,21 @@ extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t z
     const uint32_t init[2] = {0, 0xffffffffu};
     OGE_HIP_TRY(ctx, hipMemcpyAsync(err, init, 8, hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, zh, sizeof(zh), hipMemcpyHostToDevice, ctx->stream));
-    // decoder: lanes per block -- 32 (default), 16, or 0 = the wave-uniform scalar decoder k_inflate.
+    // decoder: OGE_INFLATE_GROUP unset = one lane per block (inflate_lane.hip); else lanes per block of the
+    // grouped decoder -- 32, 16, or 0 = the wave-uniform scalar decoder k_inflate.
     // Measured on 20M C2 reads (5.68 GB): scalar 437 ms (bound by the CU's one scalar ALU), 32 lanes
     // with a 1 KiB ring 254 ms, 16 lanes 268-296 ms (divergence between the wave's groups); larger
     // rings or tables cost occupancy and were slower (2 KiB 327 ms, 8 KiB 591 ms).
     static const int inflate_group = [] {
         const char *v = getenv("OGE_INFLATE_GROUP");
-        return v && *v ? atoi(v) : 32;
+        return v && *v ? atoi(v) : -1;
     }();
+    if (inflate_group < 0) {  // default: the lane decoder (inflate_lane.hip), CRC fused into its phase 2
+        OgeStageTimer *tm = ctx->begin_stage("bgzf_inflate");
+        int rc = oge_inflate_lanes(ctx, d_z, zbytes, d_d0, d_d1, d_uoff, d_crc, nblk, d_out, err, zpow);
+        ctx->end_stage(tm);
+        if (rc) return rc;
+    } else {
     OgeStageTimer *tm = ctx->begin_stage("bgzf_inflate");
     for (uint64_t b0 = 0; b0 < nblk; b0 += (1u << 30)) {
         const uint32_t nb = (uint32_t)std::min<uint64_t>(nblk - b0, 1u << 30);
@@ -1125,6 +1132,7 @@ extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t z
             OGE_LAUNCH_CHECK(ctx);
         }
         ctx->end_stage(tc);
+    }
     }
     uint32_t got[2];
     OGE_HIP_TRY(ctx, hipMemcpyAsync(got, err, 8, hipMemcpyDeviceToHost, ctx->stream));

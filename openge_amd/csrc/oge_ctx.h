@@ -75,3 +75,7 @@ struct OgeBgzfIndex {
 };
 // 0 = ok, 1 = candidates are not an exact block chain (use the host walk), < 0 = error
 int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzfIndex *ix);
+// lane-per-block BGZF inflate (inflate_lane.hip); err/zpow as in oge_bgzf_inflate_dev
+int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d0, const uint64_t *d1,
+                      const uint64_t *uoff, const uint32_t *crc, uint64_t nblk, uint8_t *out, uint32_t *err,
+                      const uint32_t *zpow);

@@ -62,6 +62,66 @@ def test_inflate_fixed_codes_and_rle(ctx, name):
     assert ctx.bgzf_inflate(bgzf(data, 6, zlib.Z_HUFFMAN_ONLY)) == data
 
 
+def _bgzf_ragged(data: bytes, sizes, level=6) -> bytes:
+    out, i, k = [], 0, 0
+    while i < len(data):
+        n = sizes[k % len(sizes)]
+        k += 1
+        chunk = data[i:i + n]
+        i += n
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        body = c.compress(chunk) + c.flush()
+        out.append(b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" + struct.pack("<H", 18 + len(body) + 7) +
+                   body + struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("level", [0, 6])
+def test_inflate_ragged_payloads(ctx, level):
+    """Payload sizes that leave every block at a different byte alignment (the lane decoder writes
+    8-byte chunks and must not touch a neighbour's bytes), incl. 1-byte and 64 KiB payloads."""
+    rng = np.random.default_rng(11)
+    sizes = [1, 7, 65536, 3, 65279, 12345] + rng.integers(1, 65537, 40).tolist()
+    data = DATA["bam"] + DATA["random"] + DATA["text"]
+    assert ctx.bgzf_inflate(_bgzf_ragged(data, sizes, level)) == data
+
+
+def _libdeflate():
+    import ctypes as C
+    try:
+        ld = C.CDLL("libdeflate.so.0")
+    except OSError:
+        return None
+    ld.libdeflate_alloc_compressor.restype = C.c_void_p
+    ld.libdeflate_alloc_compressor.argtypes = [C.c_int]
+    ld.libdeflate_deflate_compress.restype = C.c_size_t
+    ld.libdeflate_deflate_compress.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t]
+    ld.libdeflate_free_compressor.argtypes = [C.c_void_p]
+    return ld
+
+
+@pytest.mark.parametrize("level", [1, 6, 9, 12])
+def test_inflate_libdeflate_streams(ctx, level):
+    """libdeflate (the host codec samtools-era writers use) emits one block per payload, with
+    different Huffman shapes than zlib; level 12 gives near-optimal parses with long codes."""
+    import ctypes as C
+    ld = _libdeflate()
+    if ld is None:
+        pytest.skip("libdeflate.so.0 not loadable")
+    comp = ld.libdeflate_alloc_compressor(level)
+    data = DATA["bam"] + DATA["acgt"] + DATA["text"]
+    out = []
+    for i in range(0, len(data), PAY):
+        chunk = data[i:i + PAY]
+        buf = C.create_string_buffer(PAY + 1024)
+        n = ld.libdeflate_deflate_compress(comp, chunk, len(chunk), buf, PAY + 1024)
+        body = buf.raw[:n]
+        out.append(b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" + struct.pack("<H", 18 + n + 7) + body +
+                   struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
+    ld.libdeflate_free_compressor(comp)
+    assert ctx.bgzf_inflate(b"".join(out)) == data
+
+
 def test_inflate_full_64k_payloads(ctx):
     data = DATA["acgt"][:200_000]
     assert ctx.bgzf_inflate(bgzf(data, 6, pay=65536)) == data
