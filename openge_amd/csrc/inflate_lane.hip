@@ -24,6 +24,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "bgzf_dev.h"
 #include "oge_ctx.h"
@@ -201,7 +204,7 @@ __device__ bool wbuild_ld(uint8_t *R, uint32_t hlit, uint32_t hdist, bool fixed)
 __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes, const uint64_t *__restrict__ d0a,
                                                   const uint64_t *__restrict__ d1a, const uint64_t *__restrict__ uoff, uint64_t b0,
                                                   uint64_t nb, uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
-                                                  uint32_t *__restrict__ err) {
+                                                  uint32_t *__restrict__ err, uint32_t *__restrict__ trace) {
     extern __shared__ __align__(16) uint8_t smem[];
     const uint32_t lane = threadIdx.x;
     uint8_t *const myR = smem + lane * kRegion;
@@ -376,6 +379,10 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
                 if (L == 15 && c15 >= *(const uint16_t *)(myR + R_LLIM15)) sym = 512;  // no such code
             }
             skip(L);
+            if (trace && b == 0 && trace[0] < 200000) {  // debug: symbol trace of block 0
+                const uint32_t k = trace[0]++;
+                trace[1 + 4 * k] = pos, trace[2 + 4 * k] = sym, trace[3 + 4 * k] = L, trace[4 + 4 * k] = (uint32_t)(bitpos() - ((uint64_t)(uintptr_t)z + d0a[0]) * 8);
+            }
             if (sym < 256) {
                 if (pos >= osz) {
                     fail(E_OVERRUN);
@@ -632,13 +639,27 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     const uint64_t chunk = std::min<uint64_t>(nblk, 262144);
     uint64_t *bitmap = (uint64_t *)ctx->ws("infl_bitmap", chunk * 1024 * 8);
     if (!bitmap) return OGE_ERR_HIP;
+    static const bool tr = getenv("OGE_INFLATE_TRACE") != nullptr;
+    uint32_t *trace = nullptr;
+    if (tr) {
+        trace = (uint32_t *)ctx->ws("infl_trace", 4 * (1 + 4 * 200000));
+        hipMemsetAsync(trace, 0, 4, ctx->stream);
+    }
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
         const uint64_t nb = std::min(chunk, nblk - b0);
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, (uint64_t)ncu * 4);
-        k_infl_huff<<<g1, 64, 64 * kRegion, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, err);
+        k_infl_huff<<<g1, 64, 64 * kRegion, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, err, b0 ? nullptr : trace);
         OGE_LAUNCH_CHECK(ctx);
         k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, b0, zpow, err);
         OGE_LAUNCH_CHECK(ctx);
+    }
+    if (tr) {
+        hipStreamSynchronize(ctx->stream);
+        uint32_t n = 0;
+        hipMemcpy(&n, trace, 4, hipMemcpyDeviceToHost);
+        std::vector<uint32_t> h(1 + 4 * (size_t)n);
+        hipMemcpy(h.data(), trace, h.size() * 4, hipMemcpyDeviceToHost);
+        if (FILE *f = fopen(getenv("OGE_INFLATE_TRACE"), "wb")) fwrite(h.data(), 4, h.size(), f), fclose(f);
     }
     return OGE_OK;
 }
