@@ -326,6 +326,11 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
                 const uint64_t c = (uint64_t)__builtin_amdgcn_readlane((uint32_t)clp, j) |
                                    ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(clp >> 32), j) << 32);
                 ok = wbuild_cl(Rj, c);
+                if (trace && lane == j && b == 0) {  // debug: the CL table and lengths of block 0
+                    uint32_t *d = trace + 1 + 4 * 200000;
+                    d[0] = (uint32_t)c, d[1] = (uint32_t)(c >> 32), d[2] = ok;
+                    for (int k = 0; k < 32; ++k) d[3 + k] = ((const uint32_t *)Rj)[k];
+                }
                 if (lane == j) {
                     if (ok) st = ST_CL, ci = 0, prev = 0;
                     else fail(E_TABLE);
@@ -441,6 +446,10 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
             const uint32_t s = e & 31, L = e >> 5;
             skip(L);
             const uint32_t total = hlit + hdist;
+            if (trace && b == 0 && trace[0] < 200000) {
+                const uint32_t k = trace[0]++;
+                trace[1 + 4 * k] = 0x80000000u | ci, trace[2 + 4 * k] = e, trace[3 + 4 * k] = (uint32_t)buf, trace[4 + 4 * k] = total;
+            }
             uint32_t rep = 1, val = s;
             if (!e) {
                 fail(E_CODE);
@@ -642,7 +651,7 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     static const bool tr = getenv("OGE_INFLATE_TRACE") != nullptr;
     uint32_t *trace = nullptr;
     if (tr) {
-        trace = (uint32_t *)ctx->ws("infl_trace", 4 * (1 + 4 * 200000));
+        trace = (uint32_t *)ctx->ws("infl_trace", 4 * (1 + 4 * 200000 + 64));
         hipMemsetAsync(trace, 0, 4, ctx->stream);
     }
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
@@ -657,7 +666,7 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         hipStreamSynchronize(ctx->stream);
         uint32_t n = 0;
         hipMemcpy(&n, trace, 4, hipMemcpyDeviceToHost);
-        std::vector<uint32_t> h(1 + 4 * (size_t)n);
+        std::vector<uint32_t> h(1 + 4 * 200000 + 64);
         hipMemcpy(h.data(), trace, h.size() * 4, hipMemcpyDeviceToHost);
         if (FILE *f = fopen(getenv("OGE_INFLATE_TRACE"), "wb")) fwrite(h.data(), 4, h.size(), f), fclose(f);
     }

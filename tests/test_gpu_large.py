@@ -1,0 +1,165 @@
+"""GPU: full-size parity pins (VERDICT r01 "pin full-size parity").
+
+* c2_4m / c5_50k -- digests of the REFERENCE's own outputs at config scale (tests/golden/large.json,
+  made by tests/golden/make_large_goldens.py with oracle/_ref): 4M C2 reads through sort and
+  `mergesort -M -v`, the whole 50,000-interval C5 realignment set.
+* 300M -- the bench workload itself (configs[1]/[2]): no reference run exists at that size (it would
+  take ~40 min on 8 cores), so the output is checked through size-independent properties of
+  mark_duplicates.cpp:326-475 / Sort.h:116-136: the output is a permutation of the input, its
+  ByPosition key (refID', pos, strand, name, flag) never decreases, and the duplicate count equals the
+  number of records carrying 0x400.
+"""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from goldens import GOLDEN
+from openge_amd import lib as L
+
+pytestmark = pytest.mark.gpu
+LARGE = json.loads((GOLDEN / "large.json").read_text())
+
+
+def _c2_input():
+    s = LARGE["c2_4m"]["spec"]
+    p = L.synth_params(s["n_pairs"], preset=s["preset"], seed=s["seed"])
+    recs, offs, hdr = L.synth_host(p, threads=16)
+    return p, recs, offs, hdr
+
+
+def _stream_sha(d_out, d_off, n):
+    end = int(d_off[n].item())
+    beg = int(d_off[0].item())
+    return hashlib.sha256(d_out[beg:end].cpu().numpy().tobytes()).hexdigest()
+
+
+def test_c2_4m_sort_and_sortdedup_match_reference(ctx):
+    p, recs, offs, hdr = _c2_input()
+    n = len(offs) - 1
+    d_recs = torch.from_numpy(recs).cuda()
+    d_offs = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_perm = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_out = torch.empty(recs.size, dtype=torch.uint8, device="cuda")
+    d_out_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    ctx.sort_coord_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, p.n_ref, d_perm.data_ptr())
+    ctx.gather_records_dev(d_recs.data_ptr(), d_offs.data_ptr(), d_perm.data_ptr(), n, d_out.data_ptr(),
+                           d_out_off.data_ptr())
+    ctx.sync()
+    assert _stream_sha(d_out, d_out_off, n) == LARGE["c2_4m"]["sort"]["stream_sha256"]
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    nd = ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(), d_out.data_ptr(),
+                              d_out_off.data_ptr())
+    ctx.sync()
+    g = LARGE["c2_4m"]["sortdedup_v"]
+    assert nd == g["n_dup"]
+    assert _stream_sha(d_out, d_out_off, n) == g["stream_sha256"]
+
+
+def test_c2_4m_bam_file_through_the_device_chain(ctx, tmp_path):
+    """The same 4M reads as a BAM file in HBM -> oge_mergesort_bgzf_dev -> BAM file: the records and
+    the regenerated header equal the reference's `mergesort -M` output."""
+    import gzip
+    import struct
+    p, recs, offs, hdr = _c2_input()
+    src = tmp_path / "c2.bam"
+    L.write_bam(src, hdr, recs, offs, len(offs) - 1, level=1, threads=16)
+    del recs, offs
+    z = src.read_bytes()
+    dz = torch.from_numpy(np.frombuffer(z + b"\0" * 8, np.uint8).copy()).cuda()
+    d, nb, nr, nd = ctx.mergesort_bgzf_dev(dz.data_ptr(), len(z), L.mergesort_opts(mark_duplicates=1))
+    out = np.empty(nb, np.uint8)
+    L.check(L.lib().oge_memcpy(ctx.h, out.ctypes.data, d, nb, 2), ctx.h)
+    raw = gzip.decompress(out.tobytes())
+    (lt,) = struct.unpack_from("<i", raw, 4)
+    q = 8 + lt
+    (nref,) = struct.unpack_from("<i", raw, q)
+    q += 4
+    for _ in range(nref):
+        q += 8 + struct.unpack_from("<i", raw, q)[0]
+    g = LARGE["c2_4m"]["sortdedup_v"]
+    assert raw[8:8 + lt].decode() == g["header"]
+    assert hashlib.sha256(raw[q:]).hexdigest() == g["stream_sha256"]
+    assert (nr, nd) == (g["n"], g["n_dup"])
+
+
+def test_c5_50k_realign_matches_reference(ctx, tmp_path):
+    """The whole C5 set (50,000 indel intervals, 4M reads): realigned records byte for byte."""
+    rp = L.realign_synth_params(**LARGE["c5_50k"]["spec"])
+    fa, iv, bam = L.synth_realign(rp, tmp_path, level=1, threads=16)
+    b = L.Bam(bam, threads=16)
+    offs = np.append(b.offs, np.uint64(b.recs.size))
+    out, oo, st = ctx.localrealign(b.header_text, b.recs, offs, b.n, fa, iv, L.realign_opts(threads=16))
+    g = LARGE["c5_50k"]["realign"]
+    assert len(oo) - 1 == g["n"]
+    assert hashlib.sha256(out[int(oo[0]):int(oo[-1])].tobytes()).hexdigest() == g["stream_sha256"]
+
+
+def _u32(buf, idx):
+    b = [buf[idx + k].to(torch.int64) for k in range(4)]
+    return b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24)
+
+
+def test_300m_read_properties():
+    """configs[1]+[2] at full size: 300M C2 reads generated in HBM, sorted and marked on the device."""
+    ctx = L.Context(0)
+    try:
+        pairs = 150_000_000
+        p = L.synth_params(pairs, preset="c2", seed=1234)
+        n = 2 * pairs
+        d_offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), None)
+        ctx.sync()
+        B = int(d_offs[-1].item())
+        d_recs = torch.empty(B + 64, dtype=torch.uint8, device="cuda")
+        ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), d_recs.data_ptr())
+        import ctypes as C
+        buf = C.create_string_buffer(1 << 16)
+        L.check(L.lib().oge_synth_header_text(C.byref(p), buf, 1 << 16, None))
+        opts, keep = L.markdup_opts_from_header(buf.value.decode(), p.n_ref)
+        d_out = torch.empty(B + 64, dtype=torch.uint8, device="cuda")
+        d_out_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        d_perm = torch.empty(n, dtype=torch.int32, device="cuda")
+        nd = ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(), d_out.data_ptr(),
+                                  d_out_off.data_ptr())
+        ctx.sync()
+        del d_recs
+        torch.cuda.empty_cache()
+        # a permutation of the input
+        sp, _ = torch.sort(d_perm)
+        assert torch.equal(sp, torch.arange(n, dtype=torch.int32, device="cuda"))
+        del sp
+        off = d_out_off[:n]
+        assert int(d_out_off[n].item()) - int(off[0].item()) == B
+        # ByPosition key, then name bytes, then flag never decrease between neighbours
+        ref = _u32(d_out, off + 4)
+        ref = torch.where(ref == 0xFFFFFFFF, torch.full_like(ref, 0x7FFFFFFF), ref)
+        pos = _u32(d_out, off + 8)
+        flag = d_out[off + 18].to(torch.int64) | (d_out[off + 19].to(torch.int64) << 8)
+        key = (ref << 33) | (((pos + 1) & 0xFFFFFFFF) << 1) | ((flag >> 4) & 1)
+        del ref, pos
+        dk = key[1:] - key[:-1]
+        assert bool((dk >= 0).all()), "coordinate order violated"
+        tie = torch.nonzero(dk == 0).squeeze(1)
+        del dk, key
+        # names "r%010llu" (11 bytes): big-endian over bytes 36..46 of tied neighbours
+        def name_key(i):
+            o = off[i] + 36
+            hi = torch.zeros_like(o)
+            lo = torch.zeros_like(o)
+            for k in range(8):
+                hi = (hi << 8) | d_out[o + k].to(torch.int64)
+            for k in range(8, 11):
+                lo = (lo << 8) | d_out[o + k].to(torch.int64)
+            return hi, lo
+        a_hi, a_lo = name_key(tie)
+        b_hi, b_lo = name_key(tie + 1)
+        ordered = (a_hi < b_hi) | ((a_hi == b_hi) & ((a_lo < b_lo) | ((a_lo == b_lo) & (flag[tie] <= flag[tie + 1]))))
+        assert bool(ordered.all()), "name / flag tie order violated"
+        # the duplicate count is the number of records carrying 0x400
+        assert int(((flag >> 10) & 1).sum().item()) == nd
+        assert 0.06 * n < nd < 0.10 * n  # 8% duplicate pairs
+    finally:
+        ctx.close()
