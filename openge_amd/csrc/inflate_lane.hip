@@ -323,8 +323,9 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
             const uint32_t sj = __builtin_amdgcn_readlane(st, j);
             bool ok;
             if (sj == ST_BCL) {
-                const uint64_t c = (uint64_t)__builtin_amdgcn_readlane((uint32_t)clp, j) |
-                                   ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(clp >> 32), j) << 32);
+                // readlane returns int: go through uint32_t so the low word is not sign-extended
+                const uint64_t c = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)clp, j) |
+                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(clp >> 32), j) << 32);
                 ok = wbuild_cl(Rj, c);
                 if (trace && lane == j && b == 0) {  // debug: the CL table and lengths of block 0
                     uint32_t *d = trace + 1 + 4 * 200000;
