@@ -133,4 +133,5 @@ def test_pipeline_program_line_and_levels(ctx, tmp_path):
         assert raw == ref
     (tmp_path / "p.bam").write_bytes(out)
     h = bamutil.read_bam(tmp_path / "p.bam")[0]
-    assert [l for l in h.splitlines() if l.startswith("@PG")] == ["@PG\tID:openge\tCL:openge mergesort -M x\tVN:0.3-dev"]
+    pg = [l for l in h.splitlines() if l.startswith("@PG")]
+    assert pg[-1] == "@PG\tID:openge\tCL:openge mergesort -M x\tVN:0.3-dev"  # after the input's own @PG lines
