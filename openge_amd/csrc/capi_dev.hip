@@ -74,6 +74,15 @@ void *oge_ctx::ws(const char *name, size_t bytes) {
     return b.p;
 }
 
+void *oge_ctx::scratch(const char *name, size_t bytes) {
+    const size_t a = (loan_used + 255) & ~(size_t)255;
+    if (loan_base && a + bytes + 64 <= loan_cap) {
+        loan_used = a + bytes + 64;
+        return loan_base + a;
+    }
+    return ws(name, bytes);
+}
+
 OgeStageTimer *oge_ctx::begin_stage(const char *name) {
     if (!timing) return nullptr;
     if (event_pool_used == event_pool.size()) {
@@ -333,6 +342,20 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
     if (!opts) return oge_fail(ctx, OGE_ERR_ARG, "sort_markdup: opts is NULL");
     hipSetDevice(ctx->device);
     ctx->reset_timing();
+    // d_out holds the records' byte total and is only written by the final gather: until then it is
+    // the scratch arena of the pipeline (input summaries, mate-join and group buffers), which keeps
+    // the 300M-read footprint at the two record arenas + ~30 GB
+    if (n) {
+        uint64_t span[2] = {0, 0};
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&span[0], d_off, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&span[1], d_off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        ctx->lend(d_out, span[1] - span[0]);
+    }
+    struct Loan {
+        oge_ctx *c;
+        ~Loan() { c->end_loan(); }
+    } loan{ctx};
     RecMeta *meta_in;
     OgeRgTable rg;
     int rc = oge_markdup_prepare(ctx, opts, n, "md_meta_in", &meta_in, &rg);
@@ -372,6 +395,7 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
     rc = oge_markdup_finish(ctx, (uint8_t *)d_recs, d_off, n, opts, meta, dd, 0, &nd, desc, &desc_ok);
     if (rc) return rc;
     if (n_dup_out) *n_dup_out = nd;
+    ctx->end_loan();  // the gather below writes d_out
     return oge_gather_with_sizes(ctx, d_recs, d_off, v, k, n, d_out, d_out_off, meta, dd, desc_ok ? desc : nullptr);
 }
 

@@ -476,7 +476,8 @@ int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, 
     if (opts->n_rg < 0 || (opts->n_rg && (!opts->rg_ids || !opts->rg_lib)))
         return oge_fail(ctx, OGE_ERR_ARG, "markdup: bad read-group table");
     if (opts->n_rg > OGE_MAX_RG) return oge_fail(ctx, OGE_ERR_LIMIT, "markdup: more than 32767 read groups");
-    *meta = (RecMeta *)ctx->ws(name, (n + 1) * sizeof(RecMeta));
+    *meta = (RecMeta *)(strcmp(name, "md_meta_in") ? ctx->ws(name, (n + 1) * sizeof(RecMeta))
+                                                   : ctx->scratch(name, (n + 1) * sizeof(RecMeta)));
     std::vector<uint32_t> offs(opts->n_rg + 1, 0);
     const char *p = opts->rg_ids;
     for (int32_t g = 0; g < opts->n_rg; ++g) {
@@ -529,11 +530,11 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
 
     // ---- mate join ----
     OgeStageTimer *t = ctx->begin_stage("md_matejoin");
-    uint32_t *cpos = (uint32_t *)ctx->ws("md_cpos", (n + 1) * 4);
-    uint64_t *fk = (uint64_t *)ctx->ws("md_fk", (n + 1) * 8);  // fragment keys, sorted in md_frags
-    uint32_t *fv = (uint32_t *)ctx->ws("md_fv", (n + 1) * 4);
-    uint64_t *cval = (uint64_t *)ctx->ws("md_cval", (n + 1) * 8);
-    uint64_t *desc0 = d_desc ? (uint64_t *)ctx->ws("md_desc0", (n + 1) * 8) : nullptr;
+    uint32_t *cpos = (uint32_t *)ctx->scratch("md_cpos", (n + 1) * 4);
+    uint64_t *fk = (uint64_t *)ctx->scratch("md_fk", (n + 1) * 8);  // fragment keys, sorted in md_frags
+    uint32_t *fv = (uint32_t *)ctx->scratch("md_fv", (n + 1) * 4);
+    uint64_t *cval = (uint64_t *)ctx->scratch("md_cval", (n + 1) * 8);
+    uint64_t *desc0 = d_desc ? (uint64_t *)ctx->scratch("md_desc0", (n + 1) * 8) : nullptr;
     if (!cpos || !fk || !fv || !cval || (d_desc && !desc0)) return OGE_ERR_HIP;
     CandKey ckl;
     ckl.ib = bits_for(n - 1);
@@ -551,14 +552,14 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     const bool use_desc = d_desc && !desc_ovf;
     const uint64_t nc1 = (uint64_t)nc + 1;
-    uint64_t *ck = (uint64_t *)ctx->ws("md_ck", nc1 * 8);
-    uint64_t *ck2 = (uint64_t *)ctx->ws("md_ck2", nc1 * 8);
-    uint8_t *used = (uint8_t *)ctx->ws("md_used", nc1);
-    uint32_t *pflag = (uint32_t *)ctx->ws("md_pflag", nc1 * 4);
-    uint64_t *sparse = (uint64_t *)ctx->ws("md_sparse", nc1 * 8);
-    uint64_t *pairs = (uint64_t *)ctx->ws("md_pairs", (nc1 / 2 + 1) * 8);
-    uint64_t *pairs2 = (uint64_t *)ctx->ws("md_pairs2", (nc1 / 2 + 1) * 8);
-    uint32_t *slow = (uint32_t *)ctx->ws("md_slow", nc1 * 4);
+    uint64_t *ck = (uint64_t *)ctx->scratch("md_ck", nc1 * 8);
+    uint64_t *ck2 = (uint64_t *)ctx->scratch("md_ck2", nc1 * 8);
+    uint8_t *used = (uint8_t *)ctx->scratch("md_used", nc1);
+    uint32_t *pflag = (uint32_t *)ctx->scratch("md_pflag", nc1 * 4);
+    uint64_t *sparse = (uint64_t *)ctx->scratch("md_sparse", nc1 * 8);
+    uint64_t *pairs = (uint64_t *)ctx->scratch("md_pairs", (nc1 / 2 + 1) * 8);
+    uint64_t *pairs2 = (uint64_t *)ctx->scratch("md_pairs2", (nc1 / 2 + 1) * 8);
+    uint32_t *slow = (uint32_t *)ctx->scratch("md_slow", nc1 * 4);
     if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !slow) return OGE_ERR_HIP;
     hipLaunchKernelGGL(k_cand_pack, dim3(nb), dim3(kT), 0, ctx->stream, (const uint32_t *)cpos, (const uint64_t *)cval, n, ck);
     OGE_LAUNCH_CHECK(ctx);
@@ -595,13 +596,13 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     // ---- pair groups ----
     t = ctx->begin_stage("md_pairs");
     if (np) {
-        uint64_t *hi = (uint64_t *)ctx->ws("md_hi", (uint64_t)np * 8);
-        uint64_t *lo = (uint64_t *)ctx->ws("md_lo", (uint64_t)np * 8);
-        uint64_t *lo2 = (uint64_t *)ctx->ws("md_lo2", (uint64_t)np * 8);
-        uint64_t *hi2 = (uint64_t *)ctx->ws("md_hi2", (uint64_t)np * 8);
-        uint2 *pidx = (uint2 *)ctx->ws("md_pidx", (uint64_t)np * sizeof(uint2));
-        uint32_t *pv = (uint32_t *)ctx->ws("md_pv", (uint64_t)np * 4);
-        uint32_t *pv2 = (uint32_t *)ctx->ws("md_pv2", (uint64_t)np * 4);
+        uint64_t *hi = (uint64_t *)ctx->scratch("md_hi", (uint64_t)np * 8);
+        uint64_t *lo = (uint64_t *)ctx->scratch("md_lo", (uint64_t)np * 8);
+        uint64_t *lo2 = (uint64_t *)ctx->scratch("md_lo2", (uint64_t)np * 8);
+        uint64_t *hi2 = (uint64_t *)ctx->scratch("md_hi2", (uint64_t)np * 8);
+        uint2 *pidx = (uint2 *)ctx->scratch("md_pidx", (uint64_t)np * sizeof(uint2));
+        uint32_t *pv = (uint32_t *)ctx->scratch("md_pv", (uint64_t)np * 4);
+        uint32_t *pv2 = (uint32_t *)ctx->scratch("md_pv2", (uint64_t)np * 4);
         if (!hi || !lo || !lo2 || !hi2 || !pidx || !pv || !pv2) return OGE_ERR_HIP;
         const uint32_t pb = oge_ceil_div(np, kT);
         hipLaunchKernelGGL(k_pair_build, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)spairs, np,
@@ -623,8 +624,8 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
 
     // ---- fragment groups ----
     t = ctx->begin_stage("md_frags");
-    uint64_t *fk2 = (uint64_t *)ctx->ws("md_fk2", (n + 1) * 8);
-    uint32_t *fv2 = (uint32_t *)ctx->ws("md_fv2", (n + 1) * 4);
+    uint64_t *fk2 = (uint64_t *)ctx->scratch("md_fk2", (n + 1) * 8);
+    uint32_t *fv2 = (uint32_t *)ctx->scratch("md_fv2", (n + 1) * 4);
     if (!fk2 || !fv2) return OGE_ERR_HIP;  // fk / fv were written by k_cand_frag
     {
         uint64_t o = 0, a = 0;

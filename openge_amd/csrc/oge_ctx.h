@@ -35,6 +35,14 @@ struct oge_ctx {
 
     // Grow-only named scratch buffer; contents are undefined between calls.
     void *ws(const char *name, size_t bytes);
+    // Loaned scratch: while a loan is active (lend), scratch() bump-allocates from the caller's buffer
+    // (the fused pipeline lends its output arena, which is only written by the final gather), else it
+    // is ws().  Only for buffers that are dead before the lender writes its buffer.
+    uint8_t *loan_base = nullptr;
+    size_t loan_cap = 0, loan_used = 0;
+    void *scratch(const char *name, size_t bytes);
+    void lend(void *p, size_t bytes) { loan_base = (uint8_t *)p; loan_cap = p ? bytes : 0; loan_used = 0; }
+    void end_loan() { loan_base = nullptr; loan_cap = loan_used = 0; }
     OgeStageTimer *begin_stage(const char *name);
     void end_stage(OgeStageTimer *t);
     void reset_timing();

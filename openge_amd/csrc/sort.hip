@@ -309,7 +309,7 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     // equal-coordinate runs -> (name, flag, index) order.  With summaries: gather them first and
     // order the small runs on them (k_ties_meta); long runs on the record bytes (k_tie_large), whose
     // rows are then re-gathered.
-    uint2 *large = (uint2 *)ctx->ws("sort_large", (n / 33 + 1) * sizeof(uint2));
+    uint2 *large = (uint2 *)ctx->scratch("sort_large", (n / 33 + 1) * sizeof(uint2));
     if (!large) return OGE_ERR_HIP;
     OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 8, ctx->stream));
     if (meta_out) {
@@ -342,9 +342,9 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
             so[i] = tot;
             tot += P;
         }
-        uint64_t *dso = (uint64_t *)ctx->ws("sort_large_off", nlarge * 8);
-        uint64_t *sk = (uint64_t *)ctx->ws("sort_large_k", tot * 8);
-        uint32_t *sv = (uint32_t *)ctx->ws("sort_large_v", tot * 4);
+        uint64_t *dso = (uint64_t *)ctx->scratch("sort_large_off", nlarge * 8);
+        uint64_t *sk = (uint64_t *)ctx->scratch("sort_large_k", tot * 8);
+        uint32_t *sv = (uint32_t *)ctx->scratch("sort_large_v", tot * 4);
         if (!dso || !sk || !sv) return OGE_ERR_HIP;
         OGE_HIP_TRY(ctx, hipMemcpyAsync(dso, so.data(), nlarge * 8, hipMemcpyHostToDevice, ctx->stream));
         hipLaunchKernelGGL(k_tie_large, dim3(nlarge), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout,
