@@ -5,22 +5,23 @@
 // Why this shape.  A BGZF block is an independent deflate stream of <= 64 KiB whose Huffman decode is
 // one long serial chain.  The grouped decoder (inflate.hip, k_inflate_g) runs one chain per 32 lanes,
 // so a wave64 instruction advances two blocks.  Here every lane is its own decoder: one wave
-// instruction advances 64 blocks, and the per-lane state (64-bit bit buffer, a 32-byte input
-// double-buffer in VGPRs, output accumulator) needs no cross-lane traffic.
+// instruction advances 64 blocks.  A lane's decode step is a dependent chain (table lookup -> shift
+// -> next lookup), so throughput comes from waves in flight: phase 1 keeps only the hot 6-bit
+// literal/length and 4-bit distance tables in LDS (144 B per lane, lane-interleaved so a wave's 64
+// lookups hit 64 different banks), holds the canonical limits of the longer codes in VGPRs and their
+// symbol lists in a per-lane global scratch (MALL-resident): 12 waves per CU (VGPR-bound).
 //
-// Phase 1 (k_infl_huff, persistent, 64-lane workgroups, 640 B of LDS per lane = 4 workgroups/CU):
-//   each lane decodes symbols of its block.  Literals are written at their output position (8-byte
-//   aligned chunks assembled in a register); a match (length L >= 3, distance D) leaves a hole of L
-//   bytes whose first three bytes receive the descriptor (L-3, D-1 in 23 bits) and sets the hole's
-//   start bit in the block's 65536-bit bitmap.  Decode tables live in the lane's LDS region: a 6-bit
-//   direct litlen table and 5-bit direct distance table, plus the canonical-code limits and the
-//   sorted symbol lists for longer codes.  Tables are built by the whole wave for one lane at a time
-//   (ballot counting, as the lanes reach a new dynamic block), so a lane's table build costs the
-//   wave ~hundreds of instructions, not thousands of serial ones.
+// Phase 1 (k_infl_huff, persistent 64-lane workgroups): each lane decodes the symbols of its blocks.
+//   Literals are written at their output position (8-byte chunks assembled in a register); a match
+//   (length L >= 3, distance D) leaves a hole of L bytes whose first three bytes receive the
+//   descriptor (L-3, D-1 in 23 bits) and sets the hole's start bit in the block's 65536-bit bitmap.
+//   Code tables are built by the whole wave for one lane at a time (ballot counting, when a lane
+//   reaches a new dynamic block).
 // Phase 2 (k_infl_lz, one 512-thread workgroup per block): refs[p] = p for every position, then
 //   refs[p + j] = p - D + j for every hole; pointer jumping (refs[q] = refs[refs[q]]) in LDS until
 //   every position points at a literal (log2 of the copy-chain depth rounds; BAM data: 5-7); the
-//   final bytes are gathered from the literal positions, staged in LDS, CRC-32 checked, written out.
+//   block's literal-filled bytes are then staged in LDS, every byte gathered from its root, CRC-32
+//   checked and written out.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -43,172 +44,137 @@ __device__ __forceinline__ void report(uint32_t *err, uint32_t code, uint64_t bl
     atomicMin(err + 1, (uint32_t)min<uint64_t>(blk, 0xffffffffull));
 }
 
-// ---------------------------------------------------------------------------- per-lane LDS region
-constexpr uint32_t kRegion = 640;
-constexpr uint32_t R_LT = 0;      // u16[64]  litlen direct table (6 bits): sym | L << 9, 0 = longer code
-                                  // u8[128]  during code-length decoding: CL table (7 bits), sym | L << 5
-constexpr uint32_t R_DT = 128;    // u8[32]   distance direct table (5 bits): sym | L << 5
-constexpr uint32_t R_LLIM = 160;  // u16[8]   litlen left-justified 15-bit limits, lengths 7..14
-constexpr uint32_t R_LLIM15 = 176;  // u16    limit of length 15
-constexpr uint32_t R_LIE = 180;   // u32[9]   lengths 7..15: (list index - first code) | end-of-literals << 16
-constexpr uint32_t R_DLIM = 224;  // u16[8]   distance limits, lengths 6..13; +16: u16 L=14, +18: u16 L=15
-constexpr uint32_t R_DIDX = 244;  // u16[10]  distance lengths 6..15: list index - first code
-constexpr uint32_t R_DS = 264;    // u8[32]   distance symbols with codes longer than 5 bits, canonical order
-constexpr uint32_t R_LS = 296;    // u8[288]  litlen symbols longer than 6 bits, canonical order (low 8 bits)
-constexpr uint32_t R_LENS = 128;  // u8[318]  code lengths while a dynamic header is decoded
-constexpr int TBL = 6, TBD = 5;
+constexpr int TBL = 6, TBD = 4;  // direct-table bits: literal/length, distance
+// per-wave LDS, lane-interleaved ([entry][lane]): element e of lane l at e * 64 + l
+struct P1Lds {
+    uint16_t lt[1 << TBL][64];  // sym | L << 9, 0 = longer code; while code lengths are decoded the same
+                                // 8 KB is the 7-bit code-length table, u8 [128][64]: sym | L << 5
+    uint8_t dt[1 << TBD][64];   // sym | L << 5, 0 = longer code
+    uint32_t cnt[16], lo[16], first[16], offl[16], run[16], lim[16], lie[16];  // the build's per-length values
+    uint64_t clp[64];           // a lane's code-length-code lengths between its header and its CL build
+};
+// per-lane global scratch
+constexpr uint32_t kScr = 640;
+constexpr uint32_t S_LENS = 0;   // u8[320] code lengths of the block being set up (zeroed by the CL build)
+constexpr uint32_t S_LS = 320;   // u8[288] literal/length symbols with codes longer than TBL, canonical order
+constexpr uint32_t S_DS = 608;   // u8[32]  distance symbols with codes longer than TBD
 
 __constant__ uint8_t kClOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 enum { ST_HDR = 0, ST_CL = 1, ST_SYM = 2, ST_STORED = 3, ST_BCL = 4, ST_BLD = 5, ST_NEXT = 6, ST_DONE = 7 };
 
+// the slow-path parameters of one lane, in VGPRs (u16 pairs)
+struct Slow {
+    uint32_t ll[4];   // litlen left-justified 15-bit limits, lengths 7..14
+    uint32_t l15;     // limit of length 15
+    uint32_t lie[9];  // lengths 7..15: (list index - first code) & 0xffff | end-of-literals << 16
+    uint32_t dl[6];   // distance limits, lengths 5..15 (slot 11 unused)
+    uint32_t di[6];   // distance lengths 5..15: list index - first code
+};
+
+template <int N>
+__device__ __forceinline__ uint32_t pick(const uint32_t (&a)[N], uint32_t i) {  // a[i], i < N, no scratch
+    uint32_t v = a[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k) v = i == (uint32_t)k ? a[k] : v;
+    return v;
+}
+__device__ __forceinline__ uint32_t u16of(const uint32_t (&a)[6], uint32_t i) {
+    return (pick(a, i >> 1) >> ((i & 1) * 16)) & 0xffff;
+}
+
 // ---------------------------------------------------------------------------- wave-cooperative builds
-// Canonical Huffman code (RFC 1951 3.2.2) of one alphabet for lane j's region R, the wave's 64
-// lanes holding the lengths of symbols lane, lane+64, ... in len[0..NR).  Direct table of TB bits for
-// codes <= TB; codes longer than TB: left-justified limits + list index per length, symbols in
-// canonical order.  Returns false for an over-subscribed code.
+// Canonical Huffman code (RFC 1951 3.2.2) of one alphabet for lane j, the wave's 64 lanes holding the
+// lengths of symbols lane, lane+64, ... in len[0..NR).  Codes <= TB bits go to lane j's column of the
+// direct table; longer codes to lane j's symbol list (global scratch).  Per length L (lane L of the
+// wave): left-justified 15-bit limit in S.lim[L], (list index - first code) | end-of-literals << 16 in
+// S.lie[L].  The per-length values pass through LDS so the build holds few scalars.
+// false = over-subscribed code.
 template <int NR, int TB, bool LIT>
-__device__ bool wbuild(uint8_t *R, const uint32_t (&len)[NR], uint32_t n) {
+__device__ bool wbuild(P1Lds &S, uint32_t j, uint8_t *list, const uint32_t (&len)[NR], uint32_t n) {
     const uint32_t lane = threadIdx.x;
     const uint64_t lt = (1ull << lane) - 1;
-    uint32_t cnt[16], lo[16];
-#pragma unroll
-    for (int L = 0; L < 16; ++L) cnt[L] = lo[L] = 0;
+    if (lane < 16) S.cnt[lane] = S.lo[lane] = S.run[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-#pragma unroll
-        for (int L = 1; L < 16; ++L) {
-            const uint32_t c = (uint32_t)__popcll(__ballot(len[r] == (uint32_t)L));
-            cnt[L] += c;
-            if (r < 4) lo[L] += c;  // litlen symbols < 256
+        const uint32_t L = len[r];
+        if (L && r * 64 + lane < n) {
+            atomicAdd(&S.cnt[L], 1u);
+            if (r < 4) atomicAdd(&S.lo[L], 1u);  // literal/length symbols < 256
         }
     }
-    int left = 1;
-#pragma unroll
-    for (int L = 1; L < 16; ++L) {
-        left = 2 * left - (int)cnt[L];
-        if (left < 0) return false;
+    __builtin_amdgcn_wave_barrier();
+    // lane L: first code, long-list offset, Kraft term of length L
+    uint32_t fst = 0, ofl = 0, kraft = 0;
+    if (lane >= 1 && lane < 16) {
+        for (uint32_t l = 1; l < lane; ++l) {
+            const uint32_t c = S.cnt[l];
+            fst += c << (lane - l);
+            if (l > (uint32_t)TB) ofl += c;
+        }
+        const uint32_t c = S.cnt[lane];
+        kraft = c << (15 - lane);
+        S.first[lane] = fst;
+        S.offl[lane] = ofl;
+        S.lim[lane] = min((fst + c) << (15 - lane), 65535u);
+        S.lie[lane] = ((ofl - fst) & 0xffff) | ((ofl + S.lo[lane]) << 16);
     }
-    uint32_t first[16], offl[16];  // canonical first code; index of the first symbol of length L in the long list
-    uint32_t code = 0, ol = 0;
-    first[0] = offl[0] = 0;
+    // over-subscribed iff the Kraft sum exceeds 2^15 (every prefix check of RFC 1951 follows from it)
+    uint32_t ks = kraft;
 #pragma unroll
-    for (int L = 1; L < 16; ++L) {
-        code = (code + cnt[L - 1]) << 1;
-        first[L] = code;
-        offl[L] = ol;
-        if (L > TB) ol += cnt[L];
+    for (int d = 1; d < 16; d <<= 1) ks += __shfl_xor(ks, d, 64);
+    ks = __builtin_amdgcn_readfirstlane(ks);
+    if (ks > 32768u) return false;
+    if (lane < (1u << TB)) {  // zero lane j's column of the direct table
+        if (LIT) S.lt[lane][j] = 0;
+        else S.dt[lane][j] = 0;
     }
-    // zero the direct table
-    constexpr uint32_t tbytes = LIT ? (2u << TB) : (1u << TB);
-    uint32_t *tw = (uint32_t *)(R + (LIT ? R_LT : R_DT));
-    if (lane < tbytes / 4) tw[lane] = 0;
-    uint32_t run[16];
-#pragma unroll
-    for (int L = 0; L < 16; ++L) run[L] = 0;
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const uint32_t myL = len[r], s = r * 64 + lane;
-        uint32_t rank = 0, fc = 0, ofl = 0;
+        const bool mine = myL && s < n;
+        const uint32_t base = mine ? S.run[myL] : 0u, fc = mine ? S.first[myL] : 0u, ol = mine ? S.offl[myL] : 0u;
+        uint32_t rank = 0, add = 0;
 #pragma unroll
         for (int L = 1; L < 16; ++L) {
-            const uint64_t m = __ballot(myL == (uint32_t)L);
-            if (myL == (uint32_t)L) rank = run[L] + (uint32_t)__popcll(m & lt), fc = first[L], ofl = offl[L];
-            run[L] += (uint32_t)__popcll(m);
+            const uint64_t m = __ballot(mine && myL == (uint32_t)L);
+            if (myL == (uint32_t)L) rank = (uint32_t)__popcll(m & lt);
+            if (lane == (uint32_t)L) add = (uint32_t)__popcll(m);
         }
-        if (myL && s < n) {
+        __builtin_amdgcn_wave_barrier();
+        if (lane >= 1 && lane < 16) S.run[lane] += add;
+        __builtin_amdgcn_wave_barrier();
+        if (mine) {
+            rank += base;
             if (myL <= (uint32_t)TB) {
                 const uint32_t rev = __builtin_bitreverse32(fc + rank) >> (32 - myL);
                 for (uint32_t k = 0; k < (1u << (TB - myL)); ++k) {
                     const uint32_t ix = rev | (k << myL);
-                    if (LIT) ((uint16_t *)(R + R_LT))[ix] = (uint16_t)(s | (myL << 9));
-                    else R[R_DT + ix] = (uint8_t)(s | (myL << 5));
+                    if (LIT) S.lt[ix][j] = (uint16_t)(s | (myL << 9));
+                    else S.dt[ix][j] = (uint8_t)(s | (myL << 5));
                 }
             } else {
-                R[(LIT ? R_LS : R_DS) + ofl + rank] = (uint8_t)s;
+                list[ol + rank] = (uint8_t)s;
             }
         }
     }
-    if (lane == 0) {
-        if (LIT) {
-            uint16_t *lim = (uint16_t *)(R + R_LLIM);
-            uint32_t *lie = (uint32_t *)(R + R_LIE);
-#pragma unroll
-            for (int L = 7; L < 16; ++L) {
-                const uint32_t v = (first[L] + cnt[L]) << (15 - L);
-                if (L < 15) lim[L - 7] = (uint16_t)v;
-                else *(uint16_t *)(R + R_LLIM15) = (uint16_t)min(v, 65535u);
-                lie[L - 7] = ((offl[L] - first[L]) & 0xffff) | ((offl[L] + lo[L]) << 16);
-            }
-        } else {
-            uint16_t *lim = (uint16_t *)(R + R_DLIM);
-            uint16_t *idx = (uint16_t *)(R + R_DIDX);
-#pragma unroll
-            for (int L = 6; L < 16; ++L) {
-                lim[L - 6] = (uint16_t)min((first[L] + cnt[L]) << (15 - L), 65535u);
-                idx[L - 6] = (uint16_t)((offl[L] - first[L]) & 0xffff);
-            }
-        }
-    }
-    return true;
-}
-
-// code-length code: 19 symbols, lengths 3 bits each packed in clp (symbol s at bits 3s), 7-bit table
-__device__ bool wbuild_cl(uint8_t *R, uint64_t clp) {
-    const uint32_t lane = threadIdx.x;
-    const uint32_t myL = lane < 19 ? (uint32_t)((clp >> (3 * lane)) & 7) : 0;
-    uint32_t cnt[8];
-#pragma unroll
-    for (int L = 0; L < 8; ++L) cnt[L] = L ? (uint32_t)__popcll(__ballot(myL == (uint32_t)L)) : 0;
-    int left = 1;
-#pragma unroll
-    for (int L = 1; L < 8; ++L) {
-        left = 2 * left - (int)cnt[L];
-        if (left < 0) return false;
-    }
-    uint32_t code = 0, fc = 0, rank = 0;
-    const uint64_t lt = (1ull << lane) - 1;
-#pragma unroll
-    for (int L = 1; L < 8; ++L) {
-        code = (code + cnt[L - 1]) << 1;
-        const uint64_t m = __ballot(myL == (uint32_t)L);
-        if (myL == (uint32_t)L) fc = code, rank = (uint32_t)__popcll(m & lt);
-    }
-    uint32_t *tw = (uint32_t *)(R + R_LT);
-    if (lane < 32) tw[lane] = 0;
-    if (myL) {
-        const uint32_t rev = __builtin_bitreverse32(fc + rank) >> (32 - myL);
-        for (uint32_t k = 0; k < (1u << (7 - myL)); ++k) R[R_LT + (rev | (k << myL))] = (uint8_t)(lane | (myL << 5));
-    }
-    return true;
-}
-
-// litlen + distance tables of lane j's dynamic (or fixed) block
-__device__ bool wbuild_ld(uint8_t *R, uint32_t hlit, uint32_t hdist, bool fixed) {
-    const uint32_t lane = threadIdx.x;
-    uint32_t ll[5], dl[1];
-    // every length is read before anything is written (the lengths share the region with the tables)
-#pragma unroll
-    for (int r = 0; r < 5; ++r) {
-        const uint32_t s = r * 64 + lane;
-        ll[r] = 0;
-        if (s < hlit) ll[r] = fixed ? (s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8) : R[R_LENS + s];
-    }
-    dl[0] = lane < hdist ? (fixed ? 5u : (uint32_t)R[R_LENS + hlit + lane]) : 0u;
     __builtin_amdgcn_wave_barrier();
-    if (!wbuild<5, TBL, true>(R, ll, hlit)) return false;
-    return wbuild<1, TBD, false>(R, dl, hdist);
+    return true;
 }
 
 // ---------------------------------------------------------------------------- phase 1
-__global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes, const uint64_t *__restrict__ d0a,
-                                                  const uint64_t *__restrict__ d1a, const uint64_t *__restrict__ uoff, uint64_t b0,
-                                                  uint64_t nb, uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
-                                                  uint32_t *__restrict__ err, uint32_t *__restrict__ trace) {
-    extern __shared__ __align__(16) uint8_t smem[];
+__global__ void __launch_bounds__(64, 3) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
+                                                     const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
+                                                     const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
+                                                     uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
+                                                     uint8_t *__restrict__ scratch, uint32_t *__restrict__ err) {
+    __shared__ P1Lds S;
     const uint32_t lane = threadIdx.x;
-    uint8_t *const myR = smem + lane * kRegion;
+    const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
     const uint64_t stride = (uint64_t)gridDim.x * 64;
+    uint8_t *const scr = scratch + gid * kScr;  // this lane's lens / long-code symbol lists
     const uintptr_t zend = (uintptr_t)z + zbytes;
 
     // input: 64-bit bit buffer + two 16-byte chunks (q being consumed, p loaded ahead)
@@ -273,14 +239,22 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
                 if (c + k >= obase && c + k < obase + osz) c[k] = (uint8_t)(acc >> (8 * k));
         }
     };
-    auto put = [&](uint32_t p, uint32_t v) {
+    auto put = [&](uint32_t p, uint32_t v, uint32_t nbytes) {  // nbytes (1..3) little-endian bytes of v at p
         const uintptr_t a = (uintptr_t)(obase + p);
-        if ((a >> 3) != oc) {
-            flush();
-            oc = a >> 3;
-            acc = 0;
+        const uint32_t sh = (uint32_t)(a & 7);
+        if ((a >> 3) == oc && sh + nbytes <= 8) {
+            acc |= (uint64_t)(v & ((1u << (8 * nbytes)) - 1)) << (8 * sh);
+            return;
         }
-        acc |= (uint64_t)(v & 0xff) << ((a & 7) * 8);
+        for (uint32_t k = 0; k < nbytes; ++k) {
+            const uintptr_t ak = a + k;
+            if ((ak >> 3) != oc) {
+                flush();
+                oc = ak >> 3;
+                acc = 0;
+            }
+            acc |= (uint64_t)((v >> (8 * k)) & 0xff) << ((ak & 7) * 8);
+        }
     };
     // match-start bitmap of the block (1024 words per block of the chunk)
     uint64_t *bmp = nullptr, bm = 0;
@@ -296,8 +270,16 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
         bm |= 1ull << (p & 63);
     };
 
-    uint32_t st = ST_NEXT, fin = 0, hlit = 0, hdist = 0, ci = 0, prev = 0, srem = 0, fixed = 0;
-    uint64_t clp = 0, b = b0 + lane + (uint64_t)blockIdx.x * 64, d1bit = 0;
+    Slow T;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) T.ll[k] = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) T.lie[k] = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) T.dl[k] = T.di[k] = 0;
+    T.l15 = 0;
+    uint32_t st = ST_NEXT, fin = 0, hlit = 0, hdist = 0, ci = 0, prev = 0, srem = 0, fixed = 0, l256 = 0;
+    uint64_t b = b0 + gid, d1bit = 0;
     bool first = true;
 
     auto fail = [&](uint32_t code) {
@@ -316,32 +298,76 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
     for (;;) {
         // ---- table builds, the whole wave for one lane at a time
         uint64_t need = __ballot(st == ST_BCL || st == ST_BLD);
+        if (need) __threadfence_block();  // lanes' code-length stores before the wave reads them
         while (need) {
             const uint32_t j = (uint32_t)__builtin_ctzll(need);
             need &= need - 1;
-            uint8_t *Rj = smem + j * kRegion;
-            const uint32_t sj = __builtin_amdgcn_readlane(st, j);
-            bool ok;
-            if (sj == ST_BCL) {
-                // readlane returns int: go through uint32_t so the low word is not sign-extended
-                const uint64_t c = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)clp, j) |
-                                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(clp >> 32), j) << 32);
-                ok = wbuild_cl(Rj, c);
-                if (trace && lane == j && b == 0) {  // debug: the CL table and lengths of block 0
-                    uint32_t *d = trace + 1 + 4 * 200000;
-                    d[0] = (uint32_t)c, d[1] = (uint32_t)(c >> 32), d[2] = ok;
-                    for (int k = 0; k < 32; ++k) d[3 + k] = ((const uint32_t *)Rj)[k];
+            uint8_t *sj = scratch + ((uint64_t)blockIdx.x * 64 + j) * kScr;
+            if (__builtin_amdgcn_readlane(st, j) == ST_BCL) {
+                // code-length code: 19 symbols, lengths 3 bits each (symbol s at bits 3s of S.clp[j])
+                const uint64_t c = S.clp[j];
+                const uint32_t myL = lane < 19 ? (uint32_t)((c >> (3 * lane)) & 7) : 0;
+                uint32_t cntl[8];
+#pragma unroll
+                for (int L = 0; L < 8; ++L) cntl[L] = L ? (uint32_t)__popcll(__ballot(myL == (uint32_t)L)) : 0;
+                int left = 1;
+                bool ok = true;
+#pragma unroll
+                for (int L = 1; L < 8; ++L) {
+                    left = 2 * left - (int)cntl[L];
+                    ok = ok && left >= 0;
                 }
+                uint32_t code = 0, fc = 0, rank = 0;
+                const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+                for (int L = 1; L < 8; ++L) {
+                    code = (code + cntl[L - 1]) << 1;
+                    const uint64_t m = __ballot(myL == (uint32_t)L);
+                    if (myL == (uint32_t)L) fc = code, rank = (uint32_t)__popcll(m & lt);
+                }
+                uint8_t *cl = (uint8_t *)&S.lt[0][0];  // [128][64] bytes
+                cl[lane * 64 + j] = 0;
+                cl[(lane + 64) * 64 + j] = 0;
+                if (ok && myL) {
+                    const uint32_t rev = __builtin_bitreverse32(fc + rank) >> (32 - myL);
+                    for (uint32_t k = 0; k < (1u << (7 - myL)); ++k) cl[(rev | (k << myL)) * 64 + j] = (uint8_t)(lane | (myL << 5));
+                }
+                if (lane < 80) ((uint32_t *)(sj + S_LENS))[lane] = 0;  // 17/18 runs then need no stores
                 if (lane == j) {
-                    if (ok) st = ST_CL, ci = 0, prev = 0;
+                    if (ok) st = ST_CL, ci = 0, prev = 0, l256 = 0;
                     else fail(E_TABLE);
                 }
             } else {
-                ok = wbuild_ld(Rj, __builtin_amdgcn_readlane(hlit, j), __builtin_amdgcn_readlane(hdist, j),
-                               __builtin_amdgcn_readlane(fixed, j) != 0);
+                const uint32_t hl = __builtin_amdgcn_readlane(hlit, j), hd = __builtin_amdgcn_readlane(hdist, j);
+                const bool fx = __builtin_amdgcn_readlane(fixed, j) != 0;
+                uint32_t ll[5], dl[1];
+#pragma unroll
+                for (int r = 0; r < 5; ++r) {
+                    const uint32_t s = r * 64 + lane;
+                    ll[r] = 0;
+                    if (s < hl) ll[r] = fx ? (s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8) : sj[S_LENS + s];
+                }
+                dl[0] = lane < hd ? (fx ? 5u : (uint32_t)sj[S_LENS + hl + lane]) : 0u;
+                bool ok = wbuild<5, TBL, true>(S, j, sj + S_LS, ll, hl);
+                if (ok && lane == j) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) T.ll[k] = S.lim[7 + 2 * k] | (S.lim[8 + 2 * k] << 16);
+                    T.l15 = S.lim[15];
+#pragma unroll
+                    for (int L = 7; L < 16; ++L) T.lie[L - 7] = S.lie[L];
+                }
+                ok = ok && wbuild<1, TBD, false>(S, j, sj + S_DS, dl, hd);
                 if (lane == j) {
-                    if (ok) st = ST_SYM;
-                    else fail(E_TABLE);
+                    if (!ok) {
+                        fail(E_TABLE);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 6; ++k) {
+                            T.dl[k] = S.lim[5 + 2 * k] | (k < 5 ? S.lim[6 + 2 * k] << 16 : 0u);
+                            T.di[k] = (S.lie[5 + 2 * k] & 0xffff) | (k < 5 ? S.lie[6 + 2 * k] << 16 : 0u);
+                        }
+                        st = ST_SYM;
+                    }
                 }
             }
         }
@@ -370,30 +396,26 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
         if (st == ST_SYM) {
             refill();
             const uint32_t v = (uint32_t)buf;
-            uint32_t e = ((const uint16_t *)(myR + R_LT))[v & ((1u << TBL) - 1)];
+            const uint32_t e = S.lt[v & ((1u << TBL) - 1)][lane];
             uint32_t sym, L;
             if (e) {
                 sym = e & 511, L = e >> 9;
-            } else {  // code longer than TBL bits: canonical limits
+            } else {  // code longer than TBL bits: canonical limits (VGPRs), symbol from the lane's list
                 const uint32_t c15 = __builtin_bitreverse32(v) >> 17;
-                const uint4 lm = *(const uint4 *)(myR + R_LLIM);
-                L = 7 + (c15 >= (lm.x & 0xffff)) + (c15 >= (lm.x >> 16)) + (c15 >= (lm.y & 0xffff)) + (c15 >= (lm.y >> 16)) +
-                    (c15 >= (lm.z & 0xffff)) + (c15 >= (lm.z >> 16)) + (c15 >= (lm.w & 0xffff)) + (c15 >= (lm.w >> 16));
-                const uint32_t lie = ((const uint32_t *)(myR + R_LIE))[L - 7];
+                L = 7;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) L += (c15 >= (T.ll[k] & 0xffff)) + (c15 >= (T.ll[k] >> 16));
+                const uint32_t lie = pick(T.lie, L - 7);
                 const uint32_t k = ((lie & 0xffff) + (c15 >> (15 - L))) & 0xffff;
-                sym = myR[R_LS + min(k, 287u)] + (k >= (lie >> 16) ? 256u : 0u);
-                if (L == 15 && c15 >= *(const uint16_t *)(myR + R_LLIM15)) sym = 512;  // no such code
+                sym = scr[S_LS + min(k, 287u)] + (k >= (lie >> 16) ? 256u : 0u);
+                if (L == 15 && c15 >= T.l15) sym = 512;  // no such code
             }
             skip(L);
-            if (trace && b == 0 && trace[0] < 200000) {  // debug: symbol trace of block 0
-                const uint32_t k = trace[0]++;
-                trace[1 + 4 * k] = pos, trace[2 + 4 * k] = sym, trace[3 + 4 * k] = L, trace[4 + 4 * k] = (uint32_t)(bitpos() - ((uint64_t)(uintptr_t)z + d0a[0]) * 8);
-            }
             if (sym < 256) {
                 if (pos >= osz) {
                     fail(E_OVERRUN);
                 } else {
-                    put(pos, sym);
+                    put(pos, sym, 1);
                     ++pos;
                 }
             } else if (sym == 256) {
@@ -408,20 +430,18 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
                 const uint32_t len = base + get(ext);
                 refill();
                 const uint32_t w = (uint32_t)buf;
-                const uint32_t de = myR[R_DT + (w & ((1u << TBD) - 1))];
+                const uint32_t de = S.dt[w & ((1u << TBD) - 1)][lane];
                 uint32_t ds, DL;
                 if (de) {
                     ds = de & 31, DL = de >> 5;
                 } else {
                     const uint32_t c15 = __builtin_bitreverse32(w) >> 17;
-                    const uint4 lm = *(const uint4 *)(myR + R_DLIM);
-                    const uint32_t l1415 = *(const uint32_t *)(myR + R_DLIM + 16);
-                    DL = 6 + (c15 >= (lm.x & 0xffff)) + (c15 >= (lm.x >> 16)) + (c15 >= (lm.y & 0xffff)) + (c15 >= (lm.y >> 16)) +
-                         (c15 >= (lm.z & 0xffff)) + (c15 >= (lm.z >> 16)) + (c15 >= (lm.w & 0xffff)) + (c15 >= (lm.w >> 16)) +
-                         (c15 >= (l1415 & 0xffff));
-                    const uint32_t k = (((const uint16_t *)(myR + R_DIDX))[DL - 6] + (c15 >> (15 - DL))) & 0xffff;
-                    ds = myR[R_DS + min(k, 31u)];
-                    if (DL == 15 && c15 >= (l1415 >> 16)) ds = 31;  // no such code
+                    DL = 5;
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) DL += (c15 >= (T.dl[k] & 0xffff)) + (c15 >= (T.dl[k] >> 16));
+                    const uint32_t k = (u16of(T.di, DL - 5) + (c15 >> (15 - DL))) & 0xffff;
+                    ds = scr[S_DS + min(k, 31u)];
+                    if (DL == 15 && c15 >= (T.dl[5] & 0xffff)) ds = 31;  // no such code
                 }
                 skip(DL);
                 if (ds >= 30) {
@@ -432,10 +452,7 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
                     if (dist > pos || pos + len > osz) {
                         fail(E_FAR);
                     } else {
-                        const uint32_t d = (len - 3) | ((dist - 1) << 8);  // descriptor in the hole's first bytes
-                        put(pos, d);
-                        put(pos + 1, d >> 8);
-                        put(pos + 2, d >> 16);
+                        put(pos, (len - 3) | ((dist - 1) << 8), 3);  // descriptor in the hole's first bytes
                         mark(pos);
                         pos += len;
                     }
@@ -443,14 +460,10 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
             }
         } else if (st == ST_CL) {
             refill();
-            const uint32_t e = myR[R_LT + ((uint32_t)buf & 127)];
+            const uint32_t e = ((const uint8_t *)&S.lt[0][0])[((uint32_t)buf & 127) * 64 + lane];
             const uint32_t s = e & 31, L = e >> 5;
             skip(L);
             const uint32_t total = hlit + hdist;
-            if (trace && b == 0 && trace[0] < 200000) {
-                const uint32_t k = trace[0]++;
-                trace[1 + 4 * k] = 0x80000000u | ci, trace[2 + 4 * k] = e, trace[3 + 4 * k] = (uint32_t)buf, trace[4 + 4 * k] = total;
-            }
             uint32_t rep = 1, val = s;
             if (!e) {
                 fail(E_CODE);
@@ -461,11 +474,13 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
                 if ((s == 16 && ci == 0) || ci + rep > total) {
                     fail(E_TABLE);
                 } else {
-                    for (uint32_t k = 0; k < rep; ++k) myR[R_LENS + ci + k] = (uint8_t)val;
+                    if (val)  // zero runs need no stores: the buffer was zeroed by the CL build
+                        for (uint32_t k = 0; k < rep; ++k) scr[S_LENS + ci + k] = (uint8_t)val;
+                    if (ci <= 256 && 256 < ci + rep) l256 = val;
                     prev = val;
                     ci += rep;
                     if (ci == total) {
-                        if (myR[R_LENS + 256] == 0) fail(E_TABLE);
+                        if (!l256) fail(E_TABLE);  // no end-of-block code
                         else st = ST_BLD;
                     }
                 }
@@ -491,7 +506,7 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
                 if (hlit > 286 || hdist > 30) {
                     fail(E_TABLE);
                 } else {
-                    clp = 0;
+                    uint64_t clp = 0;
 #pragma unroll
                     for (int i = 0; i < 19; ++i) {
                         if ((uint32_t)i < hclen) {
@@ -499,6 +514,7 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
                             clp |= (uint64_t)get(3) << (3 * kClOrd[i]);
                         }
                     }
+                    S.clp[lane] = clp;
                     fixed = 0;
                     st = ST_BCL;
                 }
@@ -508,7 +524,7 @@ __global__ void __launch_bounds__(64) k_infl_huff(const uint8_t *__restrict__ z,
         } else if (st == ST_STORED) {
             refill();
             const uint32_t k = min(srem, 4u);
-            for (uint32_t i = 0; i < k; ++i) put(pos + i, get(8));
+            for (uint32_t i = 0; i < k; ++i) put(pos + i, get(8), 1);
             pos += k;
             srem -= k;
             if (!srem) {
@@ -525,7 +541,7 @@ constexpr uint32_t kT2 = 512;
 __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, const uint64_t *__restrict__ uoff,
                                                  const uint32_t *__restrict__ crc, const uint64_t *__restrict__ bitmap,
                                                  uint64_t b0, const uint32_t *__restrict__ zpow, uint32_t *__restrict__ err) {
-    __shared__ __align__(16) uint16_t refs[kSlot + 16];  // after resolution: the block's bytes, right-aligned
+    __shared__ __align__(16) uint16_t refs[kSlot + 16];  // later the block's bytes (img)
     __shared__ uint32_t crctab[4][256];
     __shared__ uint32_t zp[17][32];
     __shared__ uint32_t crcs[kT2];
@@ -538,8 +554,22 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         return;
     }
     if (crc) crc_setup<kT2>(crctab, zp, zpow, t);
-    // 1. every position its own source
     const uint32_t q0 = 128 * t;
+    // 1. this thread's 128 literal-filled bytes [q0, q0 + 128) and the next word (descriptors may
+    //    straddle): aligned dword loads, funnel-shifted
+    uint32_t wv[33];
+    {
+        const uintptr_t a = (uintptr_t)(O + q0);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint32_t *W = (const uint32_t *)(a & ~(uintptr_t)3);
+        const uintptr_t lim = (uintptr_t)(O + osz);  // a dword starting below lim holds a block byte: readable
+        uint32_t raw[34];
+#pragma unroll
+        for (int k = 0; k < 34; ++k) raw[k] = (uintptr_t)(W + k) < lim ? W[k] : 0u;
+#pragma unroll
+        for (int k = 0; k < 33; ++k) wv[k] = sh ? __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh) : raw[k];
+    }
+    // 2. every position its own source
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
         const uint32_t p = q0 + 8 * k;
@@ -548,71 +578,72 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         *(uint4 *)(refs + p) = v;
     }
     __syncthreads();
-    // 2. holes: refs[p + j] = p - D + j
+    // 3. holes: refs[p + j] = p - D + j, descriptors read from the registers
     const uint64_t *bmp = bitmap + (b - b0) * 1024;
     const uint32_t nw = (osz + 63) >> 6;
-    for (uint32_t w = 2 * t; w < 2 * t + 2 && w < nw; ++w) {
-        uint64_t m = bmp[w];
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+        const uint32_t w = 2 * t + h;
+        uint64_t m = w < nw ? bmp[w] : 0;
         while (m) {
-            const uint32_t p = 64 * w + (uint32_t)__builtin_ctzll(m);
+            const uint32_t jb = 64 * h + (uint32_t)__builtin_ctzll(m);  // byte in the window
             m &= m - 1;
-            const uint32_t d = O[p] | ((uint32_t)O[p + 1] << 8) | ((uint32_t)O[p + 2] << 16);
-            const uint32_t len = (d & 0xff) + 3, dist = (d >> 8) + 1;
+            const uint32_t d = jb >> 2, sh = (jb & 3) * 8;
+            uint32_t lo = wv[0], hi = wv[1];
+#pragma unroll
+            for (uint32_t k = 1; k < 32; ++k) lo = d == k ? wv[k] : lo, hi = d == k ? wv[k + 1] : hi;
+            const uint32_t x = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+            const uint32_t p = q0 + jb, len = (x & 0xff) + 3, dist = ((x >> 8) & 0x7fff) + 1;
             const uint32_t e = min(p + len, osz);  // phase 1 checked it; a failed block must not write past the array
-            for (uint32_t j = p; j < e; ++j) refs[j] = (uint16_t)(j - dist);
+            for (uint32_t q = p; q < e; ++q) refs[q] = (uint16_t)(q - dist);
         }
     }
     __syncthreads();
-    // 3. pointer jumping until every position names a literal
+    // 4. pointer jumping until every position names a literal
     const uint32_t qe = min(q0 + 128, osz);
     for (int round = 0; round < 20; ++round) {
         int changed = 0;
         for (uint32_t q = q0; q < qe; q += 8) {
             const uint4 v = *(const uint4 *)(refs + q);
             const uint32_t r8[8] = {v.x & 0xffff, v.x >> 16, v.y & 0xffff, v.y >> 16, v.z & 0xffff, v.z >> 16, v.w & 0xffff, v.w >> 16};
+            uint32_t rr[8];
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) rr[i] = refs[r8[i]];  // all issued before any is used
 #pragma unroll
             for (uint32_t i = 0; i < 8; ++i) {
-                if (q + i < qe && r8[i] != q + i) {
-                    const uint32_t rr = refs[r8[i]];
-                    if (rr != r8[i]) refs[q + i] = (uint16_t)rr, changed = 1;
+                if (q + i < qe && rr[i] != r8[i]) {
+                    refs[q + i] = (uint16_t)rr[i];
+                    changed = 1;
                 }
             }
         }
         if (!__syncthreads_or(changed)) break;
     }
-    // 4. final bytes of [q0, q0 + 128): literal-filled bytes (aligned dword loads, funnel-shifted),
-    //    holes gathered from their literal sources
-    uint32_t wv[32];
-    {
-        const uintptr_t a = (uintptr_t)(O + q0);
-        const uint32_t sh = (uint32_t)(a & 3);
-        const uint32_t *W = (const uint32_t *)(a & ~(uintptr_t)3);
-        const uintptr_t lim = (uintptr_t)(O + osz);  // a dword starting below lim holds a block byte: readable
-        uint32_t raw[33];
+    // 5. own refs into registers, then the region becomes the byte image of the block
+    uint32_t rf[64];
 #pragma unroll
-        for (int k = 0; k < 33; ++k) raw[k] = (uintptr_t)(W + k) < lim ? W[k] : 0u;
-#pragma unroll
-        for (int k = 0; k < 32; ++k) wv[k] = sh ? __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh) : raw[k];
+    for (uint32_t k = 0; k < 16; ++k) {
+        const uint4 v = *(const uint4 *)(refs + q0 + 8 * k);
+        rf[4 * k] = v.x, rf[4 * k + 1] = v.y, rf[4 * k + 2] = v.z, rf[4 * k + 3] = v.w;
     }
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        const uint32_t q = q0 + 4 * k;
-        if (q >= qe) break;
-        const uint2 rv = *(const uint2 *)(refs + q);
-        const uint32_t r4[4] = {rv.x & 0xffff, rv.x >> 16, rv.y & 0xffff, rv.y >> 16};
-        uint32_t x = wv[k];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (q + i < qe && r4[i] != q + i) x = (x & ~(0xffu << (8 * i))) | ((uint32_t)O[min(r4[i], osz - 1)] << (8 * i));
-        wv[k] = x;
-    }
-    __syncthreads();  // refs no longer read: the region becomes the byte image
-    // 5. stage the bytes in LDS (crc_window512's layout: byte q at img + q), CRC, write out
+    __syncthreads();
     uint8_t *img = (uint8_t *)refs;
 #pragma unroll
-    for (int k = 0; k < 32; ++k)
-        if (q0 + 4 * k < osz) *(uint32_t *)(img + q0 + 4 * k) = wv[k];
+    for (int k = 0; k < 32; ++k) *(uint32_t *)(img + q0 + 4 * k) = wv[k];
     __syncthreads();
+    // 6. every byte from its root (a literal position of the image)
+    const uint32_t last = osz ? osz - 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t r0 = min(rf[2 * k] & 0xffff, last), r1 = min(rf[2 * k] >> 16, last);
+        const uint32_t r2 = min(rf[2 * k + 1] & 0xffff, last), r3 = min(rf[2 * k + 1] >> 16, last);
+        wv[k] = (uint32_t)img[r0] | ((uint32_t)img[r1] << 8) | ((uint32_t)img[r2] << 16) | ((uint32_t)img[r3] << 24);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) *(uint32_t *)(img + q0 + 4 * k) = wv[k];
+    __syncthreads();
+    // 7. CRC (crc_window512's layout: byte q at img + q) and the write-out at the block's alignment
     if (crc) {
         const uint32_t c = crc_window512((const uint32_t *)img, osz, crctab, zp, crcs, t);
         if (t == 0 && c != crc[b]) report(err, E_CRC, b);
@@ -647,29 +678,17 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         return n > 0 ? n : 256;
     }();
     const uint64_t chunk = std::min<uint64_t>(nblk, 262144);
+    const uint64_t wgs = std::min<uint64_t>((chunk + 63) / 64, (uint64_t)ncu * 12);
     uint64_t *bitmap = (uint64_t *)ctx->ws("infl_bitmap", chunk * 1024 * 8);
-    if (!bitmap) return OGE_ERR_HIP;
-    static const bool tr = getenv("OGE_INFLATE_TRACE") != nullptr;
-    uint32_t *trace = nullptr;
-    if (tr) {
-        trace = (uint32_t *)ctx->ws("infl_trace", 4 * (1 + 4 * 200000 + 64));
-        hipMemsetAsync(trace, 0, 4, ctx->stream);
-    }
+    uint8_t *scr = (uint8_t *)ctx->ws("infl_scratch", wgs * 64 * kScr);
+    if (!bitmap || !scr) return OGE_ERR_HIP;
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
         const uint64_t nb = std::min(chunk, nblk - b0);
-        const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, (uint64_t)ncu * 4);
-        k_infl_huff<<<g1, 64, 64 * kRegion, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, err, b0 ? nullptr : trace);
+        const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
+        k_infl_huff<<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         OGE_LAUNCH_CHECK(ctx);
         k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, b0, zpow, err);
         OGE_LAUNCH_CHECK(ctx);
-    }
-    if (tr) {
-        hipStreamSynchronize(ctx->stream);
-        uint32_t n = 0;
-        hipMemcpy(&n, trace, 4, hipMemcpyDeviceToHost);
-        std::vector<uint32_t> h(1 + 4 * 200000 + 64);
-        hipMemcpy(h.data(), trace, h.size() * 4, hipMemcpyDeviceToHost);
-        if (FILE *f = fopen(getenv("OGE_INFLATE_TRACE"), "wb")) fwrite(h.data(), 4, h.size(), f), fclose(f);
     }
     return OGE_OK;
 }
