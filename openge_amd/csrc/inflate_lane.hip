@@ -47,8 +47,8 @@ __device__ __forceinline__ void report(uint32_t *err, uint32_t code, uint64_t bl
 constexpr int TBL = 6, TBD = 4;  // direct-table bits: literal/length, distance
 // per-wave LDS, lane-interleaved ([entry][lane]): element e of lane l at e * 64 + l
 struct P1Lds {
-    uint16_t lt[1 << TBL][64];  // sym | L << 9, 0 = longer code; while code lengths are decoded the same
-                                // 8 KB is the 7-bit code-length table, u8 [128][64]: sym | L << 5
+    uint16_t lt[1 << TBL][64];  // sym | L << 9, 0 = longer code; while code lengths are decoded a lane's
+                                // column holds its 7-bit code-length table (cl_at): sym | L << 5
     uint8_t dt[1 << TBD][64];   // sym | L << 5, 0 = longer code
     uint32_t cnt[16], lo[16], first[16], offl[16], run[16], lim[16], lie[16];  // the build's per-length values
     uint64_t clp[64];           // a lane's code-length-code lengths between its header and its CL build
@@ -60,6 +60,10 @@ constexpr uint32_t S_LS = 320;   // u8[288] literal/length symbols with codes lo
 constexpr uint32_t S_DS = 608;   // u8[32]  distance symbols with codes longer than TBD
 
 __constant__ uint8_t kClOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// entry i (7-bit code) of lane l's code-length table: byte i & 1 of lane l's literal/length entry i >> 1,
+// so building one lane's table never touches another lane's column
+__device__ __forceinline__ uint32_t cl_at(uint32_t i, uint32_t l) { return ((i >> 1) * 64 + l) * 2 + (i & 1); }
 
 enum { ST_HDR = 0, ST_CL = 1, ST_SYM = 2, ST_STORED = 3, ST_BCL = 4, ST_BLD = 5, ST_NEXT = 6, ST_DONE = 7 };
 
@@ -325,14 +329,15 @@ __global__ void __launch_bounds__(64, 3) k_infl_huff(const uint8_t *__restrict__
                     const uint64_t m = __ballot(myL == (uint32_t)L);
                     if (myL == (uint32_t)L) fc = code, rank = (uint32_t)__popcll(m & lt);
                 }
-                uint8_t *cl = (uint8_t *)&S.lt[0][0];  // [128][64] bytes
-                cl[lane * 64 + j] = 0;
-                cl[(lane + 64) * 64 + j] = 0;
+                uint8_t *cl = (uint8_t *)&S.lt[0][0];
+                S.lt[lane][j] = 0;
+                __builtin_amdgcn_wave_barrier();
                 if (ok && myL) {
                     const uint32_t rev = __builtin_bitreverse32(fc + rank) >> (32 - myL);
-                    for (uint32_t k = 0; k < (1u << (7 - myL)); ++k) cl[(rev | (k << myL)) * 64 + j] = (uint8_t)(lane | (myL << 5));
+                    for (uint32_t k = 0; k < (1u << (7 - myL)); ++k) cl[cl_at(rev | (k << myL), j)] = (uint8_t)(lane | (myL << 5));
                 }
-                if (lane < 80) ((uint32_t *)(sj + S_LENS))[lane] = 0;  // 17/18 runs then need no stores
+                ((uint32_t *)(sj + S_LENS))[lane] = 0;  // all 320 bytes: 17/18 runs then need no stores
+                if (lane < 16) ((uint32_t *)(sj + S_LENS))[64 + lane] = 0;
                 if (lane == j) {
                     if (ok) st = ST_CL, ci = 0, prev = 0, l256 = 0;
                     else fail(E_TABLE);
@@ -460,7 +465,7 @@ __global__ void __launch_bounds__(64, 3) k_infl_huff(const uint8_t *__restrict__
             }
         } else if (st == ST_CL) {
             refill();
-            const uint32_t e = ((const uint8_t *)&S.lt[0][0])[((uint32_t)buf & 127) * 64 + lane];
+            const uint32_t e = ((const uint8_t *)&S.lt[0][0])[cl_at((uint32_t)buf & 127, lane)];
             const uint32_t s = e & 31, L = e >> 5;
             skip(L);
             const uint32_t total = hlit + hdist;
