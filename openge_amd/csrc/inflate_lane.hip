@@ -27,6 +27,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 #include "bgzf_dev.h"
@@ -76,11 +77,22 @@ struct Slow {
     uint32_t di[6];   // distance lengths 5..15: list index - first code
 };
 
+// Compile-time loop: f(integral_constant<K>) for K < N.  Register arrays (Slow) must only ever be indexed
+// by constants -- a '#pragma unroll' loop still indexes them by a variable when SROA runs, which sends
+// the whole array to scratch memory and turns pick() into a scratch load (a global-memory round trip
+// per long code).
+template <class F, int... K>
+__device__ __forceinline__ void sfor_(F &&f, std::integer_sequence<int, K...>) {
+    (f(std::integral_constant<int, K>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F &&f) {
+    sfor_(f, std::make_integer_sequence<int, N>{});
+}
 template <int N>
-__device__ __forceinline__ uint32_t pick(const uint32_t (&a)[N], uint32_t i) {  // a[i], i < N, no scratch
+__device__ __forceinline__ uint32_t pick(const uint32_t (&a)[N], uint32_t i) {  // a[i], i < N, in VGPRs
     uint32_t v = a[0];
-#pragma unroll
-    for (int k = 1; k < N; ++k) v = i == (uint32_t)k ? a[k] : v;
+    sfor<N>([&](auto k) { v = i == (uint32_t)k() ? a[k()] : v; });
     return v;
 }
 __device__ __forceinline__ uint32_t u16of(const uint32_t (&a)[6], uint32_t i) {
@@ -275,12 +287,9 @@ __global__ void __launch_bounds__(64, 3) k_infl_huff(const uint8_t *__restrict__
     };
 
     Slow T;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) T.ll[k] = 0;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) T.lie[k] = 0;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) T.dl[k] = T.di[k] = 0;
+    sfor<4>([&](auto k) { T.ll[k()] = 0; });
+    sfor<9>([&](auto k) { T.lie[k()] = 0; });
+    sfor<6>([&](auto k) { T.dl[k()] = T.di[k()] = 0; });
     T.l15 = 0;
     uint32_t st = ST_NEXT, fin = 0, hlit = 0, hdist = 0, ci = 0, prev = 0, srem = 0, fixed = 0, l256 = 0;
     uint64_t b = b0 + gid, d1bit = 0;
@@ -355,22 +364,19 @@ __global__ void __launch_bounds__(64, 3) k_infl_huff(const uint8_t *__restrict__
                 dl[0] = lane < hd ? (fx ? 5u : (uint32_t)sj[S_LENS + hl + lane]) : 0u;
                 bool ok = wbuild<5, TBL, true>(S, j, sj + S_LS, ll, hl);
                 if (ok && lane == j) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) T.ll[k] = S.lim[7 + 2 * k] | (S.lim[8 + 2 * k] << 16);
+                    sfor<4>([&](auto k) { T.ll[k()] = S.lim[7 + 2 * k()] | (S.lim[8 + 2 * k()] << 16); });
                     T.l15 = S.lim[15];
-#pragma unroll
-                    for (int L = 7; L < 16; ++L) T.lie[L - 7] = S.lie[L];
+                    sfor<9>([&](auto k) { T.lie[k()] = S.lie[7 + k()]; });
                 }
                 ok = ok && wbuild<1, TBD, false>(S, j, sj + S_DS, dl, hd);
                 if (lane == j) {
                     if (!ok) {
                         fail(E_TABLE);
                     } else {
-#pragma unroll
-                        for (int k = 0; k < 6; ++k) {
-                            T.dl[k] = S.lim[5 + 2 * k] | (k < 5 ? S.lim[6 + 2 * k] << 16 : 0u);
-                            T.di[k] = (S.lie[5 + 2 * k] & 0xffff) | (k < 5 ? S.lie[6 + 2 * k] << 16 : 0u);
-                        }
+                        sfor<6>([&](auto k) {
+                            T.dl[k()] = S.lim[5 + 2 * k()] | (k() < 5 ? S.lim[6 + 2 * k()] << 16 : 0u);
+                            T.di[k()] = (S.lie[5 + 2 * k()] & 0xffff) | (k() < 5 ? S.lie[6 + 2 * k()] << 16 : 0u);
+                        });
                         st = ST_SYM;
                     }
                 }
@@ -408,8 +414,7 @@ __global__ void __launch_bounds__(64, 3) k_infl_huff(const uint8_t *__restrict__
             } else {  // code longer than TBL bits: canonical limits (VGPRs), symbol from the lane's list
                 const uint32_t c15 = __builtin_bitreverse32(v) >> 17;
                 L = 7;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) L += (c15 >= (T.ll[k] & 0xffff)) + (c15 >= (T.ll[k] >> 16));
+                sfor<4>([&](auto k) { L += (c15 >= (T.ll[k()] & 0xffff)) + (c15 >= (T.ll[k()] >> 16)); });
                 const uint32_t lie = pick(T.lie, L - 7);
                 const uint32_t k = ((lie & 0xffff) + (c15 >> (15 - L))) & 0xffff;
                 sym = scr[S_LS + min(k, 287u)] + (k >= (lie >> 16) ? 256u : 0u);
@@ -442,8 +447,7 @@ __global__ void __launch_bounds__(64, 3) k_infl_huff(const uint8_t *__restrict__
                 } else {
                     const uint32_t c15 = __builtin_bitreverse32(w) >> 17;
                     DL = 5;
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) DL += (c15 >= (T.dl[k] & 0xffff)) + (c15 >= (T.dl[k] >> 16));
+                    sfor<5>([&](auto k) { DL += (c15 >= (T.dl[k()] & 0xffff)) + (c15 >= (T.dl[k()] >> 16)); });
                     const uint32_t k = (u16of(T.di, DL - 5) + (c15 >> (15 - DL))) & 0xffff;
                     ds = scr[S_DS + min(k, 31u)];
                     if (DL == 15 && c15 >= (T.dl[5] & 0xffff)) ds = 31;  // no such code
@@ -574,16 +578,18 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
 #pragma unroll
         for (int k = 0; k < 33; ++k) wv[k] = sh ? __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh) : raw[k];
     }
+    // Steps 2 and 4-6 walk the block in 8-position chunks c = 512 k + t: a wave's 64 lanes touch 64
+    // consecutive 16-byte (refs) or 8-byte (image) chunks, so the LDS accesses are conflict-free.
     // 2. every position its own source
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
-        const uint32_t p = q0 + 8 * k;
+        const uint32_t p = 8 * (512 * k + t);
         uint4 v;
         v.x = p | ((p + 1) << 16), v.y = (p + 2) | ((p + 3) << 16), v.z = (p + 4) | ((p + 5) << 16), v.w = (p + 6) | ((p + 7) << 16);
         *(uint4 *)(refs + p) = v;
     }
     __syncthreads();
-    // 3. holes: refs[p + j] = p - D + j, descriptors read from the registers
+    // 3. holes: refs[p + j] = p - D + j, descriptors read from this thread's window registers
     const uint64_t *bmp = bitmap + (b - b0) * 1024;
     const uint32_t nw = (osz + 63) >> 6;
 #pragma unroll
@@ -605,48 +611,66 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     }
     __syncthreads();
     // 4. pointer jumping until every position names a literal
-    const uint32_t qe = min(q0 + 128, osz);
     for (int round = 0; round < 20; ++round) {
         int changed = 0;
-        for (uint32_t q = q0; q < qe; q += 8) {
+#pragma unroll 2
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t q = 8 * (512 * k + t);
+            if (q >= osz) break;
             const uint4 v = *(const uint4 *)(refs + q);
             const uint32_t r8[8] = {v.x & 0xffff, v.x >> 16, v.y & 0xffff, v.y >> 16, v.z & 0xffff, v.z >> 16, v.w & 0xffff, v.w >> 16};
             uint32_t rr[8];
 #pragma unroll
             for (uint32_t i = 0; i < 8; ++i) rr[i] = refs[r8[i]];  // all issued before any is used
+            bool ch = false;
 #pragma unroll
-            for (uint32_t i = 0; i < 8; ++i) {
-                if (q + i < qe && rr[i] != r8[i]) {
-                    refs[q + i] = (uint16_t)rr[i];
-                    changed = 1;
-                }
+            for (uint32_t i = 0; i < 8; ++i) ch |= rr[i] != r8[i];
+            if (ch) {  // positions past the end point at themselves: never changed
+                uint4 o;
+                o.x = rr[0] | (rr[1] << 16), o.y = rr[2] | (rr[3] << 16), o.z = rr[4] | (rr[5] << 16), o.w = rr[6] | (rr[7] << 16);
+                *(uint4 *)(refs + q) = o;
+                changed = 1;
             }
         }
         if (!__syncthreads_or(changed)) break;
     }
-    // 5. own refs into registers, then the region becomes the byte image of the block
+    // 5. this thread's chunks' roots into registers, then the region becomes the byte image of the block
+    //    (the literal-filled bytes, coalesced from the output)
     uint32_t rf[64];
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
-        const uint4 v = *(const uint4 *)(refs + q0 + 8 * k);
+        const uint4 v = *(const uint4 *)(refs + 8 * (512 * k + t));
         rf[4 * k] = v.x, rf[4 * k + 1] = v.y, rf[4 * k + 2] = v.z, rf[4 * k + 3] = v.w;
     }
     __syncthreads();
     uint8_t *img = (uint8_t *)refs;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) *(uint32_t *)(img + q0 + 4 * k) = wv[k];
+    {
+        const uint32_t sh = (uint32_t)((uintptr_t)O & 3);
+        const uint32_t *W = (const uint32_t *)((uintptr_t)O & ~(uintptr_t)3);
+        const uintptr_t lim = (uintptr_t)(O + osz);
+        const uint32_t nd = (osz + 3) >> 2;
+#pragma unroll 4
+        for (uint32_t k = 0; k < 32; ++k) {
+            const uint32_t w = 512 * k + t;
+            if (w >= nd) break;
+            const uint32_t a0 = W[w], a1 = (uintptr_t)(W + w + 1) < lim ? W[w + 1] : 0u;
+            *(uint32_t *)(img + 4 * w) = sh ? __builtin_amdgcn_alignbyte(a1, a0, sh) : a0;
+        }
+    }
     __syncthreads();
     // 6. every byte from its root (a literal position of the image)
     const uint32_t last = osz ? osz - 1 : 0;
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        const uint32_t r0 = min(rf[2 * k] & 0xffff, last), r1 = min(rf[2 * k] >> 16, last);
-        const uint32_t r2 = min(rf[2 * k + 1] & 0xffff, last), r3 = min(rf[2 * k + 1] >> 16, last);
-        wv[k] = (uint32_t)img[r0] | ((uint32_t)img[r1] << 8) | ((uint32_t)img[r2] << 16) | ((uint32_t)img[r3] << 24);
+    for (int k = 0; k < 16; ++k) {
+        uint32_t r[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[2 * i] = min(rf[4 * k + i] & 0xffff, last), r[2 * i + 1] = min(rf[4 * k + i] >> 16, last);
+        wv[2 * k] = (uint32_t)img[r[0]] | ((uint32_t)img[r[1]] << 8) | ((uint32_t)img[r[2]] << 16) | ((uint32_t)img[r[3]] << 24);
+        wv[2 * k + 1] = (uint32_t)img[r[4]] | ((uint32_t)img[r[5]] << 8) | ((uint32_t)img[r[6]] << 16) | ((uint32_t)img[r[7]] << 24);
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 32; ++k) *(uint32_t *)(img + q0 + 4 * k) = wv[k];
+    for (int k = 0; k < 16; ++k) *(uint2 *)(img + 8 * (512 * k + t)) = make_uint2(wv[2 * k], wv[2 * k + 1]);
     __syncthreads();
     // 7. CRC (crc_window512's layout: byte q at img + q) and the write-out at the block's alignment
     if (crc) {
@@ -682,8 +706,12 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
         return n > 0 ? n : 256;
     }();
-    const uint64_t chunk = std::min<uint64_t>(nblk, 262144);
-    const uint64_t wgs = std::min<uint64_t>((chunk + 63) / 64, (uint64_t)ncu * 12);
+    // one block per lane per launch: a launch fills the 12 resident waves per CU once (a second, partial
+    // round of waves would run at a fraction of the occupancy); chunks are balanced
+    const uint64_t lanes = (uint64_t)ncu * 12 * 64;
+    const uint64_t nchunks = std::max<uint64_t>(1, (nblk + lanes - 1) / lanes);
+    const uint64_t chunk = std::max<uint64_t>(1, (nblk + nchunks - 1) / nchunks);
+    const uint64_t wgs = (chunk + 63) / 64;
     uint64_t *bitmap = (uint64_t *)ctx->ws("infl_bitmap", chunk * 1024 * 8);
     uint8_t *scr = (uint8_t *)ctx->ws("infl_scratch", wgs * 64 * kScr);
     if (!bitmap || !scr) return OGE_ERR_HIP;
