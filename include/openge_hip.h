@@ -155,16 +155,37 @@ void oge_mergesort_opts_init(oge_mergesort_opts *o);
 int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *o,
                            const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup);
 
-/* ---- multi-GPU contig sharding (replaces SplitByChromosome/SortedMerge) -------------- */
-/* Per record: d_dest = owner rank of its refID (d_owner has n_ref + 1 entries, the last one for
- * refID -1; it must be non-decreasing so rank outputs concatenate in sorted order); d_ghost = the
- * mate's owner when the record is a mate-join candidate whose mate is owned by another rank, else
- * -1; d_back = d_dest when my_rank holds the record as a ghost whose mate is the pair's read1
- * (mate refID < refID), else -1.  Any output may be NULL.  Replaces
- * algorithms/split_by_chromosome.cpp:30-58 + algorithms/sorted_merge.cpp:66-101. */
-int oge_shard_route_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
-                        const int32_t *d_owner, int32_t n_ref, int32_t my_rank, int32_t *d_dest,
-                        int32_t *d_ghost, int32_t *d_back);
+/* ---- multi-GPU sort + duplicate marking (replaces SplitByChromosome / SortedMerge) ------ */
+/* One rank per GPU.  The reference parallelises mergesort -M / dedup by routing refID % K to K
+ * MarkDuplicates chains and re-merging them (alg/split_by_chromosome.cpp:30-58,
+ * alg/sorted_merge.cpp:66-101, wired by cmd/command_mergesort.cpp:118-179 and
+ * cmd/command_dedup.cpp:70-113); here G ranks split the ByPosition key range with sampled
+ * splitters, exchange records over RCCL (xGMI), and mark duplicates exactly (= --nosplit on one
+ * GPU) with hash-routed mate-join and pair-group exchanges.  Every call below is collective: all
+ * ranks of a communicator make it, in the same order. */
+typedef struct oge_comm oge_comm;
+/* RCCL unique id for oge_comm_init_rank (made by one rank, shared by the caller) */
+uint64_t oge_comm_unique_id_bytes(void);
+int oge_comm_unique_id(uint8_t *id_out, uint64_t bytes);
+/* one process per GPU: rank `rank` of `nranks`, RCCL over xGMI */
+int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, oge_comm **out);
+/* one process, n contexts (one thread per rank afterwards): RCCL when the contexts' devices are
+ * distinct, else (or with OGE_COMM=local) an in-process transport of device-to-device copies.
+ * out[0..n) receives one communicator per context. */
+int oge_comm_init(oge_ctx **ctxs, int n, oge_comm **out);
+void oge_comm_destroy(oge_comm *comm);
+int oge_comm_rank(const oge_comm *comm);
+int oge_comm_size(const oge_comm *comm);
+const char *oge_comm_transport(const oge_comm *comm); /* "rccl" or "local" */
+/* This rank's shard of the input (any split; contiguous input ranges in rank order keep the
+ * reference's input-order tie-break) -> this rank's slice of the globally sorted output, with bin
+ * recomputed and, when opts != NULL, 0x400 set/cleared exactly as oge_sort_markdup_dev does on the
+ * whole input (compat_nonverbose_index unsupported).  Concatenating the slices in rank order gives
+ * the one-GPU output.  *d_out / *d_out_off (*n_out + 1 offsets) are owned by the rank's context and
+ * valid until its next call; *n_dup_total = 0x400 records over all ranks. */
+int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+                          const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
+                          uint64_t *n_dup_total);
 /* Device synthetic generation of the slot range [slot0, slot0 + nslots) of a data set (one rank's
  * shard of a multi-GPU input). */
 int oge_synth_offsets_range_dev(oge_ctx *ctx, const void *params, uint64_t slot0, uint64_t nslots, uint64_t *d_offs);

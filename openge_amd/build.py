@@ -22,7 +22,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 ARCH = "gfx950"
 
-HIP_SRCS = ["prims.hip", "sort.hip", "records.hip", "markdup.hip", "capi_dev.hip", "realign.hip", "shard.hip", "bgzf.hip", "inflate.hip", "inflate_lane.hip", "filter.hip", "sort_name.hip", "pipeline.hip"]
+HIP_SRCS = ["prims.hip", "sort.hip", "records.hip", "markdup.hip", "capi_dev.hip", "realign.hip", "bgzf.hip", "inflate.hip", "inflate_lane.hip", "filter.hip", "sort_name.hip", "pipeline.hip", "dist.hip"]
 HOST_SRCS = ["bamio.cpp", "host_capi.cpp", "realign.cpp", "realign_synth.cpp"]
 CLI_SRCS = ["openge_cli.cpp", "modules.cpp"]
 
@@ -69,7 +69,7 @@ def build(verbose: bool = False) -> Path:
         list(ex.map(lambda j: _compile(*j), jobs))
     objs = [j[1] for j in jobs]
     if _stale(LIB, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs), "-lz", "-lpthread", "-ldl"])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-o", str(LIB), *map(str, objs), "-L/opt/rocm/lib", "-lrccl", "-lz", "-lpthread", "-ldl"])
         if verbose:
             print(f"built {LIB}")
     cli_srcs = [CSRC / s for s in CLI_SRCS if (CSRC / s).exists()]

@@ -102,6 +102,9 @@ void oge_ctx::end_stage(OgeStageTimer *t) {
 }
 
 void oge_ctx::reset_timing() {
+    // every top-level entry point starts here: drop a sticky error some other HIP user of this thread
+    // left behind (torch in a worker thread, say), so OGE_LAUNCH_CHECK reports only our launches
+    (void)hipGetLastError();
     if (timing_hold) return;
     stage_events.clear();
     event_pool_used = 0;

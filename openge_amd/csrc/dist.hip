@@ -1,0 +1,853 @@
+// dist.hip -- sort + duplicate marking over G GPUs (one rank per GPU), the MI355X replacement of the
+// reference's split-by-chromosome parallelism (alg/split_by_chromosome.cpp:30-58 routes refID % K to
+// K MarkDuplicates chains, alg/sorted_merge.cpp:66-101 re-merges them; driven from
+// cmd/command_mergesort.cpp:118-179 and cmd/command_dedup.cpp:70-113).  The result equals the one-GPU
+// `mergesort [-M] --nosplit` result record for record, for any G and any input split.
+//
+// Each rank enters with any shard of the input (contiguous input ranges in rank order keep the
+// reference's input-order tie-break); the collectives go through an OgeTransport: RCCL over xGMI
+// between processes or GPUs, or the in-process hub (dist_local.h) between contexts of one process.
+//
+//  1 range split   packed ByPosition keys (refID', pos, strand) of every record, kSamples per rank
+//                  pooled into G-1 splitters (dist_plan.h); record -> owner of its key
+//  2 exchange      records (stable by input order within each source), sizes; local sort of the
+//                  received records = this rank's slice of the global order (ties share a key, so
+//                  name/flag tie order is decided on one rank)
+//  3 dedup         ReadEnds of the sorted slice (records.hip input pass), global index = padded
+//                  (rank * stride + sorted position), monotone in the global sorted position:
+//     fragments    routed by the owner of their 5' (refID, coord): a fragment group (equal lib,
+//                  r1Seq, r1Coord, orient) lands on one rank, nearly always its own
+//     mate join    every candidate end (paired, mate mapped: mark_duplicates.cpp:205-245) goes to
+//                  hash(RG:name)'s rank with a minimal record (name + RG tag) for exact key compares;
+//                  arrival order = global index order, so the ReadEndsMap pairs consecutive ends of a
+//                  name exactly as on one GPU, for any number of primaries per name (0x800 included)
+//     pair groups  completed pair ReadEnds go to the rank of a hash of their chunk key
+//     reduce       dup marks, written at padded global indices, meet in a max reduce-scatter
+//  4 gather        the slice written once with bin recomputed and 0x400 applied
+#include "oge_ctx.h"
+#include "bam_layout.h"
+#include "dev_util.h"
+#include "dist_local.h"
+#include "dist_plan.h"
+#include "markdup_stages.h"
+#include "records.h"
+#include "rec_parse.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, const char *name, RecMeta **meta,
+                        OgeRgTable *rg);
+int oge_sort_buffers(oge_ctx *ctx, uint64_t n, uint64_t **keys, uint32_t **vals);
+unsigned int *oge_sort_counts(oge_ctx *ctx);
+int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+                      bool keys_ready, uint64_t **kout, uint32_t **vout, const RecMeta *meta_in, RecMeta *meta_out);
+
+// ----------------------------------------------------------------------------------------- transport
+struct OgeTransport {
+    int rank = 0, size = 1;
+    virtual ~OgeTransport() {}
+    virtual const char *name() const = 0;
+    // device buffers, stream-ordered on ctx->stream and complete on return
+    virtual int alltoallv(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
+                          const uint64_t *rbytes, const uint64_t *roff) = 0;
+    virtual int allgather_host(oge_ctx *ctx, const void *in, void *out, size_t bytes) = 0;
+    virtual int reduce_scatter_max_u8(oge_ctx *ctx, const uint8_t *in, uint8_t *out, size_t chunk) = 0;
+};
+
+struct oge_comm {
+    oge_ctx *ctx = nullptr;
+    std::unique_ptr<OgeTransport> tr;
+};
+
+namespace {
+
+constexpr int kT = 256;
+
+int dist_hip_fail(oge_ctx *ctx, int line) {
+    const hipError_t e = hipGetLastError();
+    return oge_fail(ctx, OGE_ERR_HIP, ("dist.hip:" + std::to_string(line) + ": " + hipGetErrorString(e)).c_str());
+}
+
+__global__ __launch_bounds__(kT) void k_max_into(uint8_t *__restrict__ acc, const uint8_t *__restrict__ src, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kT) acc[i] = max(acc[i], src[i]);
+}
+
+// the in-process hub's memory operations on HBM
+struct HipOps {
+    oge_ctx *ctx;
+    int copy(void *dst, const void *src, size_t n) {
+        return hipMemcpyAsync(dst, src, n, hipMemcpyDefault, ctx->stream) == hipSuccess ? 0 : -1;
+    }
+    int sync() { return hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : -1; }
+    int max_into(uint8_t *acc, const uint8_t *src, size_t n) {  // src may live on another GPU: stage it
+        uint8_t *tmp = (uint8_t *)ctx->ws("comm_max_tmp", n);
+        if (!tmp || copy(tmp, src, n)) return -1;
+        hipLaunchKernelGGL(k_max_into, dim3(std::min<uint32_t>(oge_ceil_div(n, kT), 4096u)), dim3(kT), 0, ctx->stream, acc,
+                           (const uint8_t *)tmp, (uint64_t)n);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+};
+
+struct LocalTransport : OgeTransport {
+    std::shared_ptr<oge_dist::Hub> hub;
+    const char *name() const override { return "local"; }
+    int alltoallv(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv, const uint64_t *rbytes,
+                  const uint64_t *roff) override {
+        HipOps ops{ctx};
+        oge_dist::LocalColl<HipOps> c{*hub, rank, ops};
+        return c.alltoallv(send, sbytes, soff, recv, rbytes, roff) ? oge_fail(ctx, OGE_ERR_HIP, "local transport: all-to-all failed")
+                                                                   : OGE_OK;
+    }
+    int allgather_host(oge_ctx *ctx, const void *in, void *out, size_t bytes) override {
+        HipOps ops{ctx};
+        oge_dist::LocalColl<HipOps> c{*hub, rank, ops};
+        return c.allgather_host(in, out, bytes);
+    }
+    int reduce_scatter_max_u8(oge_ctx *ctx, const uint8_t *in, uint8_t *out, size_t chunk) override {
+        HipOps ops{ctx};
+        oge_dist::LocalColl<HipOps> c{*hub, rank, ops};
+        return c.reduce_scatter_max_u8(in, out, chunk) ? oge_fail(ctx, OGE_ERR_HIP, "local transport: reduce-scatter failed")
+                                                       : OGE_OK;
+    }
+};
+
+#define OGE_NCCL_TRY(ctx, expr)                                                                              \
+    do {                                                                                                     \
+        ncclResult_t _r = (expr);                                                                            \
+        if (_r != ncclSuccess) return oge_fail((ctx), OGE_ERR_HIP, (std::string(#expr) + ": " + ncclGetErrorString(_r)).c_str()); \
+    } while (0)
+
+struct RcclTransport : OgeTransport {
+    ncclComm_t comm = nullptr;
+    ~RcclTransport() override {
+        if (comm) ncclCommDestroy(comm);
+    }
+    const char *name() const override { return "rccl"; }
+    int alltoallv(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv, const uint64_t *rbytes,
+                  const uint64_t *roff) override {
+        OGE_NCCL_TRY(ctx, ncclGroupStart());
+        for (int p = 0; p < size; ++p) {
+            if (sbytes[p]) OGE_NCCL_TRY(ctx, ncclSend((const uint8_t *)send + soff[p], sbytes[p], ncclUint8, p, comm, ctx->stream));
+            if (rbytes[p]) OGE_NCCL_TRY(ctx, ncclRecv((uint8_t *)recv + roff[p], rbytes[p], ncclUint8, p, comm, ctx->stream));
+        }
+        OGE_NCCL_TRY(ctx, ncclGroupEnd());
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return OGE_OK;
+    }
+    int allgather_host(oge_ctx *ctx, const void *in, void *out, size_t bytes) override {
+        uint8_t *d = (uint8_t *)ctx->ws("comm_allgather", bytes * size);
+        if (!d) return OGE_ERR_HIP;
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(d + bytes * rank, in, bytes, hipMemcpyHostToDevice, ctx->stream));
+        OGE_NCCL_TRY(ctx, ncclAllGather(d + bytes * rank, d, bytes, ncclUint8, comm, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(out, d, bytes * size, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return OGE_OK;
+    }
+    int reduce_scatter_max_u8(oge_ctx *ctx, const uint8_t *in, uint8_t *out, size_t chunk) override {
+        if (chunk) OGE_NCCL_TRY(ctx, ncclReduceScatter(in, out, chunk, ncclUint8, ncclMax, comm, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return OGE_OK;
+    }
+};
+
+// ------------------------------------------------------------------------------------------ kernels
+// ByPosition key (sort.hip's k_keypack without the size payload)
+__global__ __launch_bounds__(kT) void k_dist_keys(const uint8_t *__restrict__ recs, const uint64_t *__restrict__ off, uint64_t n,
+                                                  int32_t n_ref, uint64_t *__restrict__ keys) {
+    const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *r = recs + off[i];
+    const int32_t ref = oge_rd_i32(r + OGE_OFF_REFID), pos = oge_rd_i32(r + OGE_OFF_POS);
+    const uint32_t rev = (oge_rd_u16(r + OGE_OFF_FLAG) >> 4) & 1u;
+    keys[i] = ref == -1 ? (uint64_t)(uint32_t)n_ref << 33
+                        : ((uint64_t)(uint32_t)ref << 33) | ((uint64_t)(uint32_t)(pos + 1) << 1) | rev;
+}
+
+__global__ __launch_bounds__(kT) void k_sample(const uint64_t *__restrict__ keys, uint64_t n, uint32_t m, uint64_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * kT + threadIdx.x;
+    if (i < m) out[i] = keys[oge_dist::sample_pos(n, m, i)];
+}
+
+// destination of each record by its key; G = excluded
+__global__ __launch_bounds__(kT) void k_dest_range(const uint64_t *__restrict__ keys, uint64_t n, const uint64_t *__restrict__ spl,
+                                                   uint32_t nspl, uint64_t *__restrict__ dkey, uint32_t *__restrict__ dval) {
+    const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    dkey[i] = oge_dist::owner_of(keys[i] & OGE_SORT_KEY_MASK, spl, nspl);
+    dval[i] = (uint32_t)i;
+}
+
+// fragment ReadEnds -> owner of the 5' coordinate's key; other records excluded (G)
+__global__ __launch_bounds__(kT) void k_dest_frag(const RecMeta *__restrict__ meta, uint64_t n, const uint64_t *__restrict__ spl,
+                                                  uint32_t nspl, uint32_t G, uint64_t *__restrict__ dkey, uint32_t *__restrict__ dval) {
+    const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const RecMeta &M = meta[i];
+    uint32_t d = G;
+    if (M.m & OGE_M_FRAG) {
+        const int64_t c1 = (int64_t)M.coord + 1;
+        const uint64_t cpos = c1 < 0 ? 0 : (uint64_t)c1;
+        d = oge_dist::owner_of(((uint64_t)(uint32_t)M.seq << 33) | ((cpos > 0xffffffffull ? 0xffffffffull : cpos) << 1), spl, nspl);
+    }
+    dkey[i] = d;
+    dval[i] = (uint32_t)i;
+}
+
+// mate-join candidates -> owner of their RG:name hash; other records excluded (G)
+__global__ __launch_bounds__(kT) void k_dest_cand(const RecMeta *__restrict__ meta, uint64_t n, uint32_t G,
+                                                  uint64_t *__restrict__ dkey, uint32_t *__restrict__ dval) {
+    const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const RecMeta &M = meta[i];
+    dkey[i] = (M.m & OGE_M_CAND) ? oge_dist::hash_owner(oge_meta_hash48(M), G) : G;
+    dval[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(kT) void k_dest_pairs(const uint64_t *__restrict__ hk, uint32_t np, uint32_t G, uint64_t *__restrict__ dkey,
+                                                   uint32_t *__restrict__ dval) {
+    const uint32_t i = blockIdx.x * kT + threadIdx.x;
+    if (i >= np) return;
+    dkey[i] = oge_dist::hash_owner(hk[i], G);
+    dval[i] = i;
+}
+
+__global__ __launch_bounds__(kT) void k_count_dest(const uint64_t *__restrict__ dkey, uint64_t n, uint32_t G,
+                                                   unsigned long long *__restrict__ cnt) {
+    __shared__ unsigned int c[65];
+    for (uint32_t g = threadIdx.x; g <= G; g += kT) c[g] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kT) atomicAdd(&c[dkey[i]], 1u);
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g <= G; g += kT)
+        if (c[g]) atomicAdd(cnt + g, (unsigned long long)c[g]);
+}
+
+// out[k] = in[perm[k]] for elements of W 4-byte words
+template <int W>
+__global__ __launch_bounds__(kT) void k_gather_words(const uint32_t *__restrict__ in, const uint32_t *__restrict__ perm, uint64_t n,
+                                                     uint32_t *__restrict__ out) {
+    const uint64_t k = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (k >= n) return;
+    const uint64_t s = perm[k];
+#pragma unroll
+    for (int w = 0; w < W; ++w) out[k * W + w] = in[s * W + w];
+}
+
+__global__ __launch_bounds__(kT) void k_sizes_u32(const uint64_t *__restrict__ off, uint64_t n, uint32_t *__restrict__ sz) {
+    const uint64_t k = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (k < n) sz[k] = (uint32_t)(off[k + 1] - off[k]);
+}
+
+__global__ __launch_bounds__(kT) void k_off_from_u32(const uint32_t *__restrict__ sz, uint64_t n, uint64_t *__restrict__ off) {
+    const uint64_t k = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (k < n) off[k] = sz[k];
+    else if (k == n) off[k] = 0;
+}
+
+// Minimal record for an exact pair-key compare on another rank: the 36-byte core with l_read_name,
+// n_cigar = 0, l_seq = 0, the name, and the record's RG tag (type and value bytes) when it has one --
+// what pair_key_of / same_pair_key (markdup.hip) read.
+__device__ __forceinline__ uint32_t minirec_size(const uint8_t *r, const uint8_t **rg, uint32_t *rgl) {
+    const uint32_t bs = oge_ldu32(r);
+    const uint32_t lname = r[OGE_OFF_LNAME], nc = oge_ldu16(r + OGE_OFF_NCIGAR), lseq = oge_ldu32(r + OGE_OFF_LSEQ);
+    const uint8_t *tags = r + OGE_OFF_NAME + lname + 4 * nc + (lseq + 1) / 2 + lseq;
+    if (!find_rg(tags, r + 4 + bs, rg, rgl)) *rgl = 0xffffffffu;
+    return OGE_OFF_NAME + lname + (*rgl != 0xffffffffu ? 3 + *rgl + 1 : 0);
+}
+
+__global__ __launch_bounds__(kT) void k_minirec_sizes(const uint8_t *__restrict__ recs, const RecMeta *__restrict__ cm, uint64_t n,
+                                                      uint64_t *__restrict__ sz) {
+    const uint64_t k = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (k < n) {
+        const uint8_t *rg;
+        uint32_t rgl;
+        sz[k] = minirec_size(recs + cm[k].src, &rg, &rgl);
+    } else if (k == n) {
+        sz[k] = 0;
+    }
+}
+
+// writes the minimal records and points each summary's src at its record, relative to the byte chunk
+// of its destination (chunk0[d]: first byte of destination d's chunk; dend[d]: its first entry after)
+__global__ __launch_bounds__(kT) void k_minirec_write(const uint8_t *__restrict__ recs, RecMeta *__restrict__ cm, uint64_t n,
+                                                      const uint64_t *__restrict__ moff, const uint64_t *__restrict__ dend,
+                                                      uint32_t G, uint8_t *__restrict__ out) {
+    const uint64_t k = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (k >= n) return;
+    const uint8_t *r = recs + cm[k].src;
+    const uint8_t *rg;
+    uint32_t rgl;
+    const uint32_t sz = minirec_size(r, &rg, &rgl);
+    uint8_t *o = out + moff[k];
+    const uint32_t lname = r[OGE_OFF_LNAME];
+    for (uint32_t b = 0; b < 4; ++b) o[b] = (uint8_t)((sz - 4) >> (8 * b));
+    for (uint32_t b = 4; b < OGE_OFF_NAME; ++b) o[b] = 0;
+    o[OGE_OFF_LNAME] = (uint8_t)lname;
+    for (uint32_t b = 0; b < lname; ++b) o[OGE_OFF_NAME + b] = r[OGE_OFF_NAME + b];
+    if (rgl != 0xffffffffu) {
+        uint8_t *t = o + OGE_OFF_NAME + lname;
+        for (uint32_t b = 0; b < 3; ++b) t[b] = rg[(int)b - 3];
+        for (uint32_t b = 0; b < rgl; ++b) t[3 + b] = rg[b];
+        t[3 + rgl] = 0;
+    }
+    uint32_t d = 0;
+    while (d + 1 < G && k >= dend[d]) ++d;
+    cm[k].src = moff[k] - (d ? moff[dend[d - 1]] : 0);
+}
+
+// received summaries from source s start at rcnt_off[s]; their records at rbyte_off[s]
+__global__ __launch_bounds__(kT) void k_minirec_fix(RecMeta *__restrict__ cm, uint64_t n, const uint64_t *__restrict__ rcnt_off,
+                                                    const uint64_t *__restrict__ rbyte_off, uint32_t G) {
+    const uint64_t k = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (k >= n) return;
+    uint32_t s = 0;
+    while (s + 1 < G && k >= rcnt_off[s + 1]) ++s;
+    cm[k].src += rbyte_off[s];
+}
+
+__global__ __launch_bounds__(kT) void k_padded_index(const uint32_t *__restrict__ local, uint64_t n, uint32_t base,
+                                                     uint32_t *__restrict__ out) {
+    const uint64_t k = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (k < n) out[k] = base + local[k];
+}
+
+__global__ __launch_bounds__(kT) void k_map_pair_idx(uint2 *__restrict__ idx, uint32_t np, const uint32_t *__restrict__ gidx) {
+    const uint32_t p = blockIdx.x * kT + threadIdx.x;
+    if (p < np) idx[p] = make_uint2(gidx[idx[p].x], gidx[idx[p].y]);
+}
+
+// ------------------------------------------------------------------------------------------- driver
+struct Dist {
+    oge_comm *comm;
+    oge_ctx *ctx;
+    int G, rank;
+
+    // device -> host, ordered after this rank's stream (the context's stream does not synchronise
+    // with the null stream a plain hipMemcpy uses)
+    int d2h(void *h, const void *d, size_t bytes) {
+        if (hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return oge_fail(ctx, OGE_ERR_HIP, (std::string("multi-GPU: device->host copy: ") + hipGetErrorString(hipGetLastError())).c_str());
+        return OGE_OK;
+    }
+
+    int agree(int rc) {  // every rank learns whether any rank failed; keeps the collectives in step
+        std::vector<int> all(G);
+        int r2 = comm->tr->allgather_host(ctx, &rc, all.data(), sizeof(int));
+        if (r2) return r2;
+        for (int g = 0; g < G; ++g)
+            if (all[g]) return rc ? rc : oge_fail(ctx, OGE_ERR_HIP, ("multi-GPU: rank " + std::to_string(g) + " failed").c_str());
+        return OGE_OK;
+    }
+
+    // stable partition of n entries by destination (dkey in [0, G], G = not sent):
+    // perm = entry order grouped by destination, cnt[G] = entries per destination
+    int partition(uint64_t *dkey, uint32_t *dval, uint64_t n, const char *tag, uint32_t **perm, std::vector<uint64_t> &cnt) {
+        cnt.assign(G, 0);
+        *perm = dval;
+        if (!n) return OGE_OK;
+        unsigned long long *dc = (unsigned long long *)ctx->ws("dist_cnt", 8 * (G + 1));
+        uint64_t *k2 = (uint64_t *)ctx->ws((std::string("dist_pk_") + tag).c_str(), n * 8);
+        uint32_t *v2 = (uint32_t *)ctx->ws((std::string("dist_pv_") + tag).c_str(), n * 4);
+        if (!dc || !k2 || !v2) return OGE_ERR_HIP;
+        OGE_HIP_TRY(ctx, hipMemsetAsync(dc, 0, 8 * (G + 1), ctx->stream));
+        hipLaunchKernelGGL(k_count_dest, dim3(std::min<uint32_t>(oge_ceil_div(n, kT), 1024u)), dim3(kT), 0, ctx->stream,
+                           (const uint64_t *)dkey, n, (uint32_t)G, dc);
+        OGE_LAUNCH_CHECK(ctx);
+        uint32_t b = 0;
+        while ((1u << b) <= (uint32_t)G) ++b;
+        uint64_t *ko;
+        uint32_t *vo;
+        int rc = oge_radix_sort_pairs(ctx, dkey, dval, k2, v2, n, (1ull << b) - 1, &ko, &vo);
+        if (rc) return rc;
+        std::vector<unsigned long long> h(G + 1);
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(h.data(), dc, 8 * (G + 1), hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        for (int g = 0; g < G; ++g) cnt[g] = h[g];
+        *perm = vo;
+        return OGE_OK;
+    }
+
+    // exchange plan for per-destination element counts
+    int plan(const std::vector<uint64_t> &cnt, oge_dist::Plan *p) {
+        std::vector<uint64_t> all((size_t)G * G);
+        int rc = comm->tr->allgather_host(ctx, cnt.data(), all.data(), G * 8);
+        if (rc) return rc;
+        *p = oge_dist::plan_from_counts(all, G, rank);
+        return OGE_OK;
+    }
+
+    // all-to-all of `elem`-byte elements laid out by the plan
+    int a2a(const oge_dist::Plan &p, size_t elem, const void *send, void *recv) {
+        std::vector<uint64_t> sb(G), so(G), rb(G), ro(G);
+        for (int g = 0; g < G; ++g) {
+            sb[g] = p.scnt[g] * elem;
+            so[g] = p.soff[g] * elem;
+            rb[g] = p.rcnt[g] * elem;
+            ro[g] = p.roff[g] * elem;
+        }
+        return comm->tr->alltoallv(ctx, send, sb.data(), so.data(), recv, rb.data(), ro.data());
+    }
+
+    template <int W>
+    int gather_words(const void *in, const uint32_t *perm, uint64_t n, void *out) {
+        if (!n) return OGE_OK;
+        hipLaunchKernelGGL(k_gather_words<W>, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)in, perm, n,
+                           (uint32_t *)out);
+        OGE_LAUNCH_CHECK(ctx);
+        return OGE_OK;
+    }
+};
+
+}  // namespace
+
+static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+                    const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out, uint64_t *n_dup_total) {
+    oge_ctx *ctx = comm->ctx;
+    Dist D{comm, ctx, comm->tr->size, comm->tr->rank};
+    const int G = D.G;
+    const uint32_t nspl = (uint32_t)G - 1;
+    int rc = OGE_OK;
+    if (opts && opts->compat_nonverbose_index) rc = oge_fail(ctx, OGE_ERR_ARG, "multi-GPU dedup: compat_nonverbose_index is one-GPU only");
+    if (n > 0xFFFFFFFEull) rc = oge_fail(ctx, OGE_ERR_LIMIT, "multi-GPU: more than 2^32-2 records on one rank");
+    if ((rc = D.agree(rc))) return rc;
+
+    // ---- 1. range split
+    OgeStageTimer *t = ctx->begin_stage("dist_split");
+    uint64_t *keys = (uint64_t *)ctx->ws("dist_keys", (n + 1) * 8);
+    uint64_t *samp = (uint64_t *)ctx->ws("dist_samp", oge_dist::kSamples * 8);
+    if (!keys || !samp) rc = OGE_ERR_HIP;
+    const uint32_t m = (uint32_t)std::min<uint64_t>(n, oge_dist::kSamples);
+    std::vector<uint64_t> hs(oge_dist::kSamples, 0);
+    if (!rc && n) {
+        hipLaunchKernelGGL(k_dist_keys, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off, n, n_ref, keys);
+        hipLaunchKernelGGL(k_sample, dim3(oge_ceil_div(m, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)keys, n, m, samp);
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(hs.data(), samp, m * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            rc = oge_fail(ctx, OGE_ERR_HIP, "multi-GPU: key sampling failed");
+    }
+    if ((rc = D.agree(rc))) return rc;
+    std::vector<uint64_t> allsamp((size_t)G * oge_dist::kSamples), alln(G);
+    const uint64_t mm[2] = {n, m};
+    std::vector<uint64_t> allmm(2 * G);
+    if ((rc = comm->tr->allgather_host(ctx, hs.data(), allsamp.data(), oge_dist::kSamples * 8))) return rc;
+    if ((rc = comm->tr->allgather_host(ctx, mm, allmm.data(), 16))) return rc;
+    std::vector<std::vector<uint64_t>> per(G);
+    for (int g = 0; g < G; ++g) {
+        alln[g] = allmm[2 * g];
+        per[g].assign(allsamp.begin() + (size_t)g * oge_dist::kSamples, allsamp.begin() + (size_t)g * oge_dist::kSamples + allmm[2 * g + 1]);
+    }
+    const std::vector<uint64_t> spl = oge_dist::choose_splitters(per, alln, G);
+    uint64_t *d_spl = (uint64_t *)ctx->ws("dist_spl", 8 * (nspl + 1));
+    uint64_t *dkey = (uint64_t *)ctx->ws("dist_dkey", (n + 1) * 8);
+    uint32_t *dval = (uint32_t *)ctx->ws("dist_dval", (n + 1) * 4);
+    uint32_t *perm = nullptr;
+    std::vector<uint64_t> cnt;
+    if (!d_spl || !dkey || !dval) rc = OGE_ERR_HIP;
+    if (!rc && nspl) rc = hipMemcpyAsync(d_spl, spl.data(), 8 * nspl, hipMemcpyHostToDevice, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    if (!rc && n) {
+        hipLaunchKernelGGL(k_dest_range, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)keys, n,
+                           (const uint64_t *)d_spl, nspl, dkey, dval);
+        rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    }
+    if (!rc) rc = D.partition(dkey, dval, n, "rec", &perm, cnt);
+    // send buffer: records grouped by destination (stable), their sizes
+    uint64_t total = 0;
+    if (!rc && n) rc = D.d2h(&total, d_off + n, 8);
+    uint64_t first = 0;
+    if (!rc && n) rc = D.d2h(&first, d_off, 8);
+    uint8_t *sbuf = (uint8_t *)ctx->ws("dist_sbuf", total - first + 64);
+    uint64_t *soff = (uint64_t *)ctx->ws("dist_soff", (n + 1) * 8);
+    uint32_t *ssz = (uint32_t *)ctx->ws("dist_ssz", (n + 1) * 4);
+    if (!rc && (!sbuf || !soff || !ssz)) rc = OGE_ERR_HIP;
+    if (!rc && n) rc = oge_gather_with_sizes(ctx, d_recs, d_off, perm, nullptr, n, sbuf, soff, nullptr, nullptr);
+    if (!rc && n) {
+        hipLaunchKernelGGL(k_sizes_u32, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)soff, n, ssz);
+        rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    }
+    // bytes per destination from the send offsets at the count boundaries
+    std::vector<uint64_t> bcnt(G, 0);
+    if (!rc) {
+        std::vector<uint64_t> bnd(G + 1, 0);
+        uint64_t c = 0;
+        for (int g = 0; g <= G && !rc; ++g) {
+            if (n) rc = D.d2h(&bnd[g], soff + c, 8);
+            if (g < G) c += cnt[g];
+        }
+        for (int g = 0; g < G; ++g) bcnt[g] = bnd[g + 1] - bnd[g];
+    }
+    ctx->end_stage(t);
+    if ((rc = D.agree(rc))) return rc;
+
+    // ---- 2. exchange + local sort
+    t = ctx->begin_stage("dist_exchange");
+    oge_dist::Plan pr, pb;
+    if ((rc = D.plan(cnt, &pr)) || (rc = D.plan(bcnt, &pb))) return rc;
+    const uint64_t R = pr.rtot, RB = pb.rtot;
+    uint8_t *rbuf = (uint8_t *)ctx->ws("dist_rbuf", RB + 64);
+    uint32_t *rsz = (uint32_t *)ctx->ws("dist_rsz", (R + 1) * 4);
+    uint64_t *roff = (uint64_t *)ctx->ws("dist_roff", (R + 1) * 8);
+    if (!rbuf || !rsz || !roff) rc = OGE_ERR_HIP;
+    if ((rc = D.agree(rc))) return rc;
+    if ((rc = D.a2a(pb, 1, sbuf, rbuf))) return rc;
+    if ((rc = D.a2a(pr, 4, ssz, rsz))) return rc;
+    hipLaunchKernelGGL(k_off_from_u32, dim3(oge_ceil_div(R + 1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)rsz, R, roff);
+    OGE_LAUNCH_CHECK(ctx);
+    rc = oge_exclusive_scan_u64(ctx, roff, roff, R + 1);
+    ctx->end_stage(t);
+    if ((rc = D.agree(rc))) return rc;
+    if (R > 0xFFFFFFFEull) rc = oge_fail(ctx, OGE_ERR_LIMIT, "multi-GPU: more than 2^32-2 records on one rank after the exchange");
+    uint8_t *out = (uint8_t *)ctx->ws("dist_out", RB + 64);
+    uint64_t *out_off = (uint64_t *)ctx->ws("dist_out_off", (R + 1) * 8);
+    if (!out || !out_off) rc = OGE_ERR_HIP;
+    if ((rc = D.agree(rc))) return rc;
+
+    uint64_t *k = nullptr;
+    uint32_t *v = nullptr;
+    if (!opts) {  // sort only
+        rc = oge_sort_keys_dev(ctx, rbuf, roff, R, n_ref, false, &k, &v, nullptr, nullptr);
+        if (!rc) rc = oge_gather_with_sizes(ctx, rbuf, roff, v, k, R, out, out_off, nullptr, nullptr);
+        if (!rc) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+        if ((rc = D.agree(rc))) return rc;
+        *d_out = out;
+        *d_out_off = out_off;
+        *n_out = R;
+        if (n_dup_total) *n_dup_total = 0;
+        return OGE_OK;
+    }
+
+    RecMeta *meta_in = nullptr, *meta = nullptr;
+    OgeRgTable rg;
+    rc = oge_markdup_prepare(ctx, opts, R, "md_meta_in", &meta_in, &rg);
+    uint64_t *skeys = nullptr;
+    uint32_t *svals = nullptr;
+    unsigned int *counts = oge_sort_counts(ctx);
+    if (!rc && (oge_sort_buffers(ctx, R, &skeys, &svals) || !counts)) rc = OGE_ERR_HIP;
+    meta = (RecMeta *)ctx->ws("md_meta", (R + 1) * sizeof(RecMeta));
+    if (!rc && !meta) rc = OGE_ERR_HIP;
+    if (!rc) {
+        OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 16, ctx->stream));
+        t = ctx->begin_stage("input_pass");
+        OgePassArgs a = {};
+        a.recs = rbuf;
+        a.off = roff;
+        a.n = R;
+        a.meta = meta_in;
+        a.rg = rg;
+        a.keys = skeys;
+        a.vals = svals;
+        a.n_ref = n_ref;
+        a.bad = counts + 2;
+        rc = oge_input_pass(ctx, a);
+        ctx->end_stage(t);
+    }
+    if (!rc) rc = oge_sort_keys_dev(ctx, rbuf, roff, R, n_ref, true, &k, &v, meta_in, meta);
+    if ((rc = D.agree(rc))) return rc;
+
+    // ---- 3. dedup: global indices
+    std::vector<uint64_t> allR(G);
+    if ((rc = comm->tr->allgather_host(ctx, &R, allR.data(), 8))) return rc;
+    uint64_t stride = 1, Ntot = 0;
+    for (int g = 0; g < G; ++g) stride = std::max<uint64_t>(stride, allR[g]), Ntot += allR[g];
+    if ((uint64_t)G * stride > 0xFFFFFFFFull)
+        return oge_fail(ctx, OGE_ERR_LIMIT, "multi-GPU dedup: G x the largest slice exceeds 2^32 records");
+    const uint32_t base = (uint32_t)((uint64_t)D.rank * stride);
+    (void)Ntot;
+    uint8_t *dup_pad = (uint8_t *)ctx->ws("dist_dup_pad", (size_t)G * stride);
+    uint8_t *dup = (uint8_t *)ctx->ws("dist_dup", stride + 1);
+    uint64_t *desc = (uint64_t *)ctx->ws("dist_desc", (R + 1) * 8);
+    uint64_t *desc0 = (uint64_t *)ctx->ws("dist_desc0", (R + 1) * 8);
+    if (!dup_pad || !dup || !desc || !desc0) rc = OGE_ERR_HIP;
+    if (!rc) rc = hipMemsetAsync(dup_pad, 0, (size_t)G * stride, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    OgeMdFrags F;
+    t = ctx->begin_stage("dist_frags");
+    if (!rc) rc = oge_md_cand_frag(ctx, opts, meta, R, true, &F);
+    if (!rc && F.desc_ovf) rc = oge_fail(ctx, OGE_ERR_LIMIT, "multi-GPU dedup: a record offset exceeds 2^39");
+    if (!rc && R) rc = hipMemcpyAsync(desc0, F.desc0, R * 8, hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    if ((rc = D.agree(rc))) return rc;
+
+    // fragments -> owner of their 5' coordinate
+    {
+        uint64_t *fdk = (uint64_t *)ctx->ws("dist_fdk", (R + 1) * 8);
+        uint32_t *fdv = (uint32_t *)ctx->ws("dist_fdv", (R + 1) * 4);
+        uint64_t *fks = (uint64_t *)ctx->ws("dist_fks", (R + 1) * 8);
+        uint32_t *fvs = (uint32_t *)ctx->ws("dist_fvs", (R + 1) * 4);
+        if (!fdk || !fdv || !fks || !fvs) rc = OGE_ERR_HIP;
+        if (!rc && R) {
+            hipLaunchKernelGGL(k_dest_frag, dim3(oge_ceil_div(R, kT)), dim3(kT), 0, ctx->stream, (const RecMeta *)meta, R,
+                               (const uint64_t *)d_spl, nspl, (uint32_t)G, fdk, fdv);
+            rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+        }
+        uint32_t *fperm = nullptr;
+        std::vector<uint64_t> fc;
+        if (!rc) rc = D.partition(fdk, fdv, R, "frag", &fperm, fc);
+        uint64_t ns = 0;
+        for (uint64_t c : fc) ns += c;
+        if (!rc && ns) {  // fragment keys and padded global indices in destination order
+            rc = D.gather_words<2>(F.fk, fperm, ns, fks);
+            if (!rc) {
+                hipLaunchKernelGGL(k_padded_index, dim3(oge_ceil_div(ns, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)fperm, ns, base,
+                                   fvs);
+                rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+            }
+        }
+        if ((rc = D.agree(rc))) return rc;
+        oge_dist::Plan pf;
+        if ((rc = D.plan(fc, &pf))) return rc;
+        uint64_t *fkr = (uint64_t *)ctx->ws("dist_fkr", (pf.rtot + 1) * 8);
+        uint32_t *fvr = (uint32_t *)ctx->ws("dist_fvr", (pf.rtot + 1) * 4);
+        if (!fkr || !fvr) rc = OGE_ERR_HIP;
+        if ((rc = D.agree(rc))) return rc;
+        if ((rc = D.a2a(pf, 8, fks, fkr)) || (rc = D.a2a(pf, 4, fvs, fvr))) return rc;
+        rc = oge_md_frag_groups(ctx, fkr, fvr, pf.rtot, dup_pad);
+        if ((rc = D.agree(rc))) return rc;
+    }
+    ctx->end_stage(t);
+
+    // mate-join candidates -> owner of their RG:name hash, with their minimal records
+    t = ctx->begin_stage("dist_join");
+    OgeMdPairs P;
+    {
+        uint64_t *cdk = (uint64_t *)ctx->ws("dist_cdk", (R + 1) * 8);
+        uint32_t *cdv = (uint32_t *)ctx->ws("dist_cdv", (R + 1) * 4);
+        if (!cdk || !cdv) rc = OGE_ERR_HIP;
+        if (!rc && R) {
+            hipLaunchKernelGGL(k_dest_cand, dim3(oge_ceil_div(R, kT)), dim3(kT), 0, ctx->stream, (const RecMeta *)meta, R, (uint32_t)G,
+                               cdk, cdv);
+            rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+        }
+        uint32_t *cperm = nullptr;
+        std::vector<uint64_t> cc;
+        if (!rc) rc = D.partition(cdk, cdv, R, "cand", &cperm, cc);
+        uint64_t ns = 0;
+        for (uint64_t c : cc) ns += c;
+        RecMeta *cms = (RecMeta *)ctx->ws("dist_cms", (ns + 1) * sizeof(RecMeta));
+        uint32_t *cgs = (uint32_t *)ctx->ws("dist_cgs", (ns + 1) * 4);
+        uint64_t *moff = (uint64_t *)ctx->ws("dist_moff", (ns + 1) * 8);
+        uint64_t *dend = (uint64_t *)ctx->ws("dist_dend", 8 * (G + 1));
+        if (!cms || !cgs || !moff || !dend) rc = OGE_ERR_HIP;
+        std::vector<uint64_t> mb(G, 0);
+        if (!rc && ns) {
+            rc = D.gather_words<sizeof(RecMeta) / 4>(meta, cperm, ns, cms);
+            if (!rc) {
+                hipLaunchKernelGGL(k_padded_index, dim3(oge_ceil_div(ns, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)cperm, ns, base,
+                                   cgs);
+                hipLaunchKernelGGL(k_minirec_sizes, dim3(oge_ceil_div(ns + 1, kT)), dim3(kT), 0, ctx->stream, rbuf, (const RecMeta *)cms,
+                                   ns, moff);
+                rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+            }
+            if (!rc) rc = oge_exclusive_scan_u64(ctx, moff, moff, ns + 1);
+            std::vector<uint64_t> de(G), mo(G + 1, 0);
+            uint64_t c = 0;
+            for (int g = 0; g < G; ++g) c += cc[g], de[g] = c;
+            for (int g = 0; g <= G && !rc; ++g) {
+                const uint64_t at = g ? de[g - 1] : 0;
+                rc = D.d2h(&mo[g], moff + at, 8);
+            }
+            for (int g = 0; g < G; ++g) mb[g] = mo[g + 1] - mo[g];
+            uint8_t *mrec = nullptr;
+            if (!rc) {
+                mrec = (uint8_t *)ctx->ws("dist_mrec", mo[G] + 64);
+                if (!mrec) rc = OGE_ERR_HIP;
+            }
+            if (!rc) rc = hipMemcpyAsync(dend, de.data(), 8 * G, hipMemcpyHostToDevice, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+            if (!rc) {
+                hipLaunchKernelGGL(k_minirec_write, dim3(oge_ceil_div(ns, kT)), dim3(kT), 0, ctx->stream, rbuf, cms, ns,
+                                   (const uint64_t *)moff, (const uint64_t *)dend, (uint32_t)G, mrec);
+                rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+            }
+            // `de` (the source of the dend upload) leaves scope here
+            if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = dist_hip_fail(ctx, __LINE__);
+        }
+        if ((rc = D.agree(rc))) return rc;
+        oge_dist::Plan pc, pm;
+        if ((rc = D.plan(cc, &pc)) || (rc = D.plan(mb, &pm))) return rc;
+        const uint64_t nr = pc.rtot;
+        RecMeta *cmr = (RecMeta *)ctx->ws("dist_cmr", (nr + 1) * sizeof(RecMeta));
+        uint32_t *cgr = (uint32_t *)ctx->ws("dist_cgr", (nr + 1) * 4);
+        uint8_t *mrr = (uint8_t *)ctx->ws("dist_mrr", pm.rtot + 64);
+        uint64_t *rco = (uint64_t *)ctx->ws("dist_rco", 8 * (G + 1));
+        uint64_t *rbo = (uint64_t *)ctx->ws("dist_rbo", 8 * (G + 1));
+        if (!cmr || !cgr || !mrr || !rco || !rbo) rc = OGE_ERR_HIP;
+        if ((rc = D.agree(rc))) return rc;
+        uint8_t *mrec = (uint8_t *)ctx->ws("dist_mrec", 64);
+        if ((rc = D.a2a(pc, sizeof(RecMeta), cms, cmr)) || (rc = D.a2a(pc, 4, cgs, cgr)) || (rc = D.a2a(pm, 1, mrec, mrr))) return rc;
+        if (nr) {
+            OGE_HIP_TRY(ctx, hipMemcpyAsync(rco, pc.roff.data(), 8 * (G + 1), hipMemcpyHostToDevice, ctx->stream));
+            OGE_HIP_TRY(ctx, hipMemcpyAsync(rbo, pm.roff.data(), 8 * (G + 1), hipMemcpyHostToDevice, ctx->stream));
+            hipLaunchKernelGGL(k_minirec_fix, dim3(oge_ceil_div(nr, kT)), dim3(kT), 0, ctx->stream, cmr, nr, (const uint64_t *)rco,
+                               (const uint64_t *)rbo, (uint32_t)G);
+            OGE_LAUNCH_CHECK(ctx);
+        }
+        // the owner's join: arrival order (source rank, then sorted position) = global order
+        OgeMdFrags F2;
+        rc = oge_md_cand_frag(ctx, opts, cmr, nr, false, &F2);
+        if (!rc) rc = oge_md_join_build(ctx, opts, mrr, cmr, nr, F2, &P);
+        if (!rc && P.np) {
+            hipLaunchKernelGGL(k_map_pair_idx, dim3(oge_ceil_div(P.np, kT)), dim3(kT), 0, ctx->stream, P.idx, P.np, (const uint32_t *)cgr);
+            rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+        }
+        if ((rc = D.agree(rc))) return rc;
+    }
+    ctx->end_stage(t);
+
+    // pair ReadEnds -> owner of their chunk-key hash
+    t = ctx->begin_stage("dist_pairs");
+    {
+        const uint32_t np = P.np;
+        uint64_t *pdk = (uint64_t *)ctx->ws("dist_pdk", ((uint64_t)np + 1) * 8);
+        uint32_t *pdv = (uint32_t *)ctx->ws("dist_pdv", ((uint64_t)np + 1) * 4);
+        uint64_t *shi = (uint64_t *)ctx->ws("dist_shi", ((uint64_t)np + 1) * 8);
+        uint64_t *slo = (uint64_t *)ctx->ws("dist_slo", ((uint64_t)np + 1) * 8);
+        uint2 *sidx = (uint2 *)ctx->ws("dist_sidx", ((uint64_t)np + 1) * 8);
+        if (!pdk || !pdv || !shi || !slo || !sidx) rc = OGE_ERR_HIP;
+        if (!rc && np) {
+            hipLaunchKernelGGL(k_dest_pairs, dim3(oge_ceil_div(np, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)P.hk, np, (uint32_t)G,
+                               pdk, pdv);
+            rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+        }
+        uint32_t *pperm = nullptr;
+        std::vector<uint64_t> pc2;
+        if (!rc) rc = D.partition(pdk, pdv, np, "pair", &pperm, pc2);
+        if (!rc && np) {
+            rc = D.gather_words<2>(P.hi, pperm, np, shi);
+            if (!rc) rc = D.gather_words<2>(P.lo, pperm, np, slo);
+            if (!rc) rc = D.gather_words<2>(P.idx, pperm, np, sidx);
+        }
+        if ((rc = D.agree(rc))) return rc;
+        oge_dist::Plan pp;
+        if ((rc = D.plan(pc2, &pp))) return rc;
+        OgeMdPairs Q;
+        Q.np = (uint32_t)pp.rtot;
+        Q.hi = (uint64_t *)ctx->ws("dist_rhi", (pp.rtot + 1) * 8);
+        Q.lo = (uint64_t *)ctx->ws("dist_rlo", (pp.rtot + 1) * 8);
+        Q.idx = (uint2 *)ctx->ws("dist_ridx", (pp.rtot + 1) * 8);
+        if (!Q.hi || !Q.lo || !Q.idx) rc = OGE_ERR_HIP;
+        if ((rc = D.agree(rc))) return rc;
+        if ((rc = D.a2a(pp, 8, shi, Q.hi)) || (rc = D.a2a(pp, 8, slo, Q.lo)) || (rc = D.a2a(pp, 8, sidx, Q.idx))) return rc;
+        rc = oge_md_pairs_rehash(ctx, &Q);
+        if (!rc) rc = oge_md_pair_groups(ctx, opts, Q, dup_pad);
+        if ((rc = D.agree(rc))) return rc;
+    }
+    ctx->end_stage(t);
+
+    // ---- dup marks meet; 4. apply + gather
+    t = ctx->begin_stage("dist_reduce");
+    if ((rc = comm->tr->reduce_scatter_max_u8(ctx, dup_pad, dup, stride))) return rc;
+    ctx->end_stage(t);
+    t = ctx->begin_stage("md_apply");
+    uint64_t nd = 0;
+    rc = oge_md_apply_desc(ctx, desc0, R, dup, desc, &nd);
+    ctx->end_stage(t);
+    if (!rc) rc = oge_gather_with_sizes(ctx, rbuf, roff, v, k, R, out, out_off, meta, dup, desc);
+    if (!rc) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    if ((rc = D.agree(rc))) return rc;
+    std::vector<uint64_t> alld(G);
+    if ((rc = comm->tr->allgather_host(ctx, &nd, alld.data(), 8))) return rc;
+    uint64_t tot = 0;
+    for (uint64_t x : alld) tot += x;
+    *d_out = out;
+    *d_out_off = out_off;
+    *n_out = R;
+    if (n_dup_total) *n_dup_total = tot;
+    return OGE_OK;
+}
+
+// ---------------------------------------------------------------------------------------------- ABI
+extern "C" {
+
+int oge_comm_unique_id(uint8_t *id_out, uint64_t bytes) {
+    if (!id_out || bytes < sizeof(ncclUniqueId)) return oge_fail(nullptr, OGE_ERR_ARG, "oge_comm_unique_id: buffer too small");
+    ncclUniqueId id;
+    ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return oge_fail(nullptr, OGE_ERR_HIP, ncclGetErrorString(r));
+    memcpy(id_out, &id, sizeof id);
+    return OGE_OK;
+}
+
+uint64_t oge_comm_unique_id_bytes(void) { return sizeof(ncclUniqueId); }
+
+int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, oge_comm **out) {
+    if (!ctx || !id || !out || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
+        return oge_fail(ctx, OGE_ERR_ARG, "oge_comm_init_rank: bad arguments");
+    (void)hipSetDevice(ctx->device);
+    auto t = std::make_unique<RcclTransport>();
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof uid);
+    ncclResult_t r = ncclCommInitRank(&t->comm, nranks, uid, rank);
+    if (r != ncclSuccess) return oge_fail(ctx, OGE_ERR_HIP, (std::string("ncclCommInitRank: ") + ncclGetErrorString(r)).c_str());
+    t->rank = rank;
+    t->size = nranks;
+    oge_comm *c = new oge_comm();
+    c->ctx = ctx;
+    c->tr = std::move(t);
+    *out = c;
+    return OGE_OK;
+}
+
+int oge_comm_init(oge_ctx **ctxs, int n, oge_comm **out) {
+    if (!ctxs || !out || n < 1 || n > 64) return oge_fail(nullptr, OGE_ERR_ARG, "oge_comm_init: bad arguments");
+    for (int g = 0; g < n; ++g)
+        if (!ctxs[g]) return oge_fail(nullptr, OGE_ERR_ARG, "oge_comm_init: null context");
+    bool distinct = true;
+    for (int a = 0; a < n; ++a)
+        for (int b = a + 1; b < n; ++b) distinct = distinct && ctxs[a]->device != ctxs[b]->device;
+    const char *e = getenv("OGE_COMM");
+    const bool local = !distinct || n == 1 || (e && !strcmp(e, "local"));
+    if (local) {  // contexts sharing a GPU (or forced): the in-process hub
+        auto hub = std::make_shared<oge_dist::Hub>(n);
+        for (int g = 0; g < n; ++g) {
+            auto t = std::make_unique<LocalTransport>();
+            t->hub = hub;
+            t->rank = g;
+            t->size = n;
+            out[g] = new oge_comm();
+            out[g]->ctx = ctxs[g];
+            out[g]->tr = std::move(t);
+        }
+        return OGE_OK;
+    }
+    std::vector<ncclComm_t> cs(n);
+    std::vector<int> devs(n);
+    for (int g = 0; g < n; ++g) devs[g] = ctxs[g]->device;
+    ncclResult_t r = ncclCommInitAll(cs.data(), n, devs.data());
+    if (r != ncclSuccess) return oge_fail(nullptr, OGE_ERR_HIP, (std::string("ncclCommInitAll: ") + ncclGetErrorString(r)).c_str());
+    for (int g = 0; g < n; ++g) {
+        auto t = std::make_unique<RcclTransport>();
+        t->comm = cs[g];
+        t->rank = g;
+        t->size = n;
+        out[g] = new oge_comm();
+        out[g]->ctx = ctxs[g];
+        out[g]->tr = std::move(t);
+    }
+    return OGE_OK;
+}
+
+void oge_comm_destroy(oge_comm *c) { delete c; }
+
+int oge_comm_rank(const oge_comm *c) { return c ? c->tr->rank : -1; }
+int oge_comm_size(const oge_comm *c) { return c ? c->tr->size : -1; }
+const char *oge_comm_transport(const oge_comm *c) { return c ? c->tr->name() : ""; }
+
+int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+                          const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
+                          uint64_t *n_dup_total) {
+    if (!comm || !d_out || !d_out_off || !n_out || (n && (!d_recs || !d_off)))
+        return oge_fail(comm ? comm->ctx : nullptr, OGE_ERR_ARG, "oge_sort_markdup_dist: bad arguments");
+    oge_ctx *ctx = comm->ctx;
+    (void)hipSetDevice(ctx->device);
+    ctx->reset_timing();
+    if (opts && opts->n_ref != n_ref) return oge_fail(ctx, OGE_ERR_ARG, "oge_sort_markdup_dist: opts->n_ref differs from n_ref");
+    return dist_run(comm, d_recs, d_off, n, n_ref, opts, d_out, d_out_off, n_out, n_dup_total);
+}
+
+}  // extern "C"

@@ -22,6 +22,7 @@
 #include "dev_util.h"
 #include "records.h"
 #include "rec_parse.h"
+#include "markdup_stages.h"
 
 #include <algorithm>
 #include <cstring>
@@ -503,54 +504,92 @@ int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, 
     return OGE_OK;
 }
 
-// Everything after the per-record ReadEnds pass.  meta[i] describes record i of the stream
-// (record index = i); its bytes are at recs + meta[i].src (only read to confirm pair keys).
-// dup[i] receives 1/0/2 (see oge_markdup); with apply, FLAG 0x400 is rewritten in place at
-// recs + off[i].
-int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
-                       const oge_markdup_opts *opts, const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out,
-                       uint64_t *d_desc, bool *desc_ok) {
-    if (desc_ok) *desc_ok = false;
+namespace {
+__global__ __launch_bounds__(kT) void k_pair_rehash(const uint64_t *__restrict__ hi, const uint64_t *__restrict__ lo, uint32_t np,
+                                                     uint64_t *__restrict__ hk, uint32_t *__restrict__ val) {
+    const uint32_t p = blockIdx.x * kT + threadIdx.x;
+    if (p >= np) return;
+    hk[p] = mix64(mix64(hi[p] & ((1ull << 48) - 1)) ^ lo[p]);
+    val[p] = p;
+}
+}  // namespace
+
+int oge_md_pairs_rehash(oge_ctx *ctx, OgeMdPairs *P) {
+    if (!P->np) return OGE_OK;
+    P->hk = (uint64_t *)ctx->scratch("md_hi2", (uint64_t)P->np * 8);
+    P->val = (uint32_t *)ctx->scratch("md_pv", (uint64_t)P->np * 4);
+    if (!P->hk || !P->val) return OGE_ERR_HIP;
+    hipLaunchKernelGGL(k_pair_rehash, dim3(oge_ceil_div(P->np, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)P->hi,
+                       (const uint64_t *)P->lo, P->np, P->hk, P->val);
+    OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}
+
+// ------------------------------------------------------------------------------------ stages
+// oge_markdup_finish is the sequence cand_frag -> join_build -> pair_groups -> frag_groups -> apply;
+// the multi-GPU path (dist.hip) runs the same stages on ReadEnds exchanged between ranks.
+
+static int md_layout(oge_ctx *ctx, const oge_markdup_opts *opts, KeyLayout *L) {
     int16_t maxlib = opts->unknown_lib;
     for (int32_t g = 0; g < opts->n_rg; ++g) maxlib = std::max(maxlib, opts->rg_lib[g]);
     if (opts->unknown_lib < 0) return oge_fail(ctx, OGE_ERR_ARG, "markdup: negative library id");
     for (int32_t g = 0; g < opts->n_rg; ++g)
         if (opts->rg_lib[g] < 0) return oge_fail(ctx, OGE_ERR_ARG, "markdup: negative library id");
-    const KeyLayout L{bits_for((uint64_t)std::max(opts->n_ref, 1)), bits_for((uint64_t)maxlib), opts->split_chains};
-    if (L.sb + L.lb + 34 > 47 || L.sb + L.lb > 16)
+    *L = KeyLayout{bits_for((uint64_t)std::max(opts->n_ref, 1)), bits_for((uint64_t)maxlib), opts->split_chains};
+    if (L->sb + L->lb + 34 > 47 || L->sb + L->lb > 16)
         return oge_fail(ctx, OGE_ERR_LIMIT, "markdup: too many references x libraries for the packed group key");
-    unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
-    unsigned long long *ndup = (unsigned long long *)ctx->ws("md_ndup", 8);
-    if (!cnt || !ndup) return OGE_ERR_HIP;
-    OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 16, ctx->stream));
-    OGE_HIP_TRY(ctx, hipMemsetAsync(ndup, 0, 8, ctx->stream));
-    OGE_HIP_TRY(ctx, hipMemsetAsync(d_dup, 0, n ? n : 1, ctx->stream));
-    if (!n) { *n_dup_out = 0; return OGE_OK; }
-    const uint32_t nb = oge_ceil_div(n, kT);
+    return OGE_OK;
+}
 
-    // ---- mate join ----
-    OgeStageTimer *t = ctx->begin_stage("md_matejoin");
-    uint32_t *cpos = (uint32_t *)ctx->scratch("md_cpos", (n + 1) * 4);
-    uint64_t *fk = (uint64_t *)ctx->scratch("md_fk", (n + 1) * 8);  // fragment keys, sorted in md_frags
-    uint32_t *fv = (uint32_t *)ctx->scratch("md_fv", (n + 1) * 4);
-    uint64_t *cval = (uint64_t *)ctx->scratch("md_cval", (n + 1) * 8);
-    uint64_t *desc0 = d_desc ? (uint64_t *)ctx->scratch("md_desc0", (n + 1) * 8) : nullptr;
-    if (!cpos || !fk || !fv || !cval || (d_desc && !desc0)) return OGE_ERR_HIP;
+static CandKey md_candkey(const oge_markdup_opts *opts, uint64_t n) {
     CandKey ckl;
-    ckl.ib = bits_for(n - 1);
+    ckl.ib = bits_for(n ? n - 1 : 0);
     ckl.hb = std::min<uint32_t>(48, 64 - ckl.ib);
     ckl.split_k = opts->split_chains;
     if (opts->debug_hash_bits > 0 && (uint32_t)opts->debug_hash_bits < ckl.hb) ckl.hb = (uint32_t)opts->debug_hash_bits;
-    hipLaunchKernelGGL(k_cand_frag, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, L, ckl, cpos, fk, fv,
-                       cval, desc0, cnt + 3);
-    OGE_LAUNCH_CHECK(ctx);
-    int rc = oge_exclusive_scan_u32(ctx, cpos, cpos, n + 1);
+    return ckl;
+}
+
+int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
+                     OgeMdFrags *f) {
+    KeyLayout L;
+    int rc = md_layout(ctx, opts, &L);
     if (rc) return rc;
-    uint32_t nc = 0, desc_ovf = 0;
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&nc, cpos + n, 4, hipMemcpyDeviceToHost, ctx->stream));
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&desc_ovf, cnt + 3, 4, hipMemcpyDeviceToHost, ctx->stream));
+    *f = OgeMdFrags{};
+    unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
+    if (!cnt) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 16, ctx->stream));
+    f->cpos = (uint32_t *)ctx->scratch("md_cpos", (n + 1) * 4);
+    f->fk = (uint64_t *)ctx->scratch("md_fk", (n + 1) * 8);
+    f->fv = (uint32_t *)ctx->scratch("md_fv", (n + 1) * 4);
+    f->cval = (uint64_t *)ctx->scratch("md_cval", (n + 1) * 8);
+    f->desc0 = want_desc ? (uint64_t *)ctx->scratch("md_desc0", (n + 1) * 8) : nullptr;
+    if (!f->cpos || !f->fk || !f->fv || !f->cval || (want_desc && !f->desc0)) return OGE_ERR_HIP;
+    const CandKey ckl = md_candkey(opts, n);
+    hipLaunchKernelGGL(k_cand_frag, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, L, ckl, f->cpos, f->fk,
+                       f->fv, f->cval, f->desc0, cnt + 3);
+    OGE_LAUNCH_CHECK(ctx);
+    rc = oge_exclusive_scan_u32(ctx, f->cpos, f->cpos, n + 1);
+    if (rc) return rc;
+    uint32_t nc = 0, ovf = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&nc, f->cpos + n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&ovf, cnt + 3, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    const bool use_desc = d_desc && !desc_ovf;
+    f->nc = nc;
+    f->desc_ovf = ovf != 0;
+    return OGE_OK;
+}
+
+int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t *recs, const RecMeta *meta, uint64_t n,
+                      const OgeMdFrags &f, OgeMdPairs *P) {
+    KeyLayout L;
+    int rc = md_layout(ctx, opts, &L);
+    if (rc) return rc;
+    *P = OgeMdPairs{};
+    unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
+    if (!cnt) return OGE_ERR_HIP;
+    const CandKey ckl = md_candkey(opts, n);
+    const uint32_t nc = f.nc;
     const uint64_t nc1 = (uint64_t)nc + 1;
     uint64_t *ck = (uint64_t *)ctx->scratch("md_ck", nc1 * 8);
     uint64_t *ck2 = (uint64_t *)ctx->scratch("md_ck2", nc1 * 8);
@@ -561,11 +600,15 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     uint64_t *pairs2 = (uint64_t *)ctx->scratch("md_pairs2", (nc1 / 2 + 1) * 8);
     uint32_t *slow = (uint32_t *)ctx->scratch("md_slow", nc1 * 4);
     if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !slow) return OGE_ERR_HIP;
-    hipLaunchKernelGGL(k_cand_pack, dim3(nb), dim3(kT), 0, ctx->stream, (const uint32_t *)cpos, (const uint64_t *)cval, n, ck);
-    OGE_LAUNCH_CHECK(ctx);
+    if (n) {
+        hipLaunchKernelGGL(k_cand_pack, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)f.cpos,
+                           (const uint64_t *)f.cval, n, ck);
+        OGE_LAUNCH_CHECK(ctx);
+    }
     uint64_t *sk;
     rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, ((1ull << ckl.hb) - 1) << ckl.ib, &sk, nullptr);
     if (rc) return rc;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + 2, 0, 4, ctx->stream));
     hipLaunchKernelGGL(k_pair_runs, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)sk, (uint64_t)nc, ckl,
                        pflag, sparse, slow, cnt + 2);
     OGE_LAUNCH_CHECK(ctx);
@@ -574,8 +617,8 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (nslow) {
         OGE_HIP_TRY(ctx, hipMemsetAsync(used, 0, nc1, ctx->stream));
-        hipLaunchKernelGGL(k_pair_runs_slow, dim3(oge_ceil_div(nslow, kT)), dim3(kT), 0, ctx->stream, (const uint8_t *)d_recs,
-                           meta, (const uint64_t *)sk, (uint64_t)nc, ckl, (const uint32_t *)slow, nslow, used, pflag, sparse);
+        hipLaunchKernelGGL(k_pair_runs_slow, dim3(oge_ceil_div(nslow, kT)), dim3(kT), 0, ctx->stream, recs, meta,
+                           (const uint64_t *)sk, (uint64_t)nc, ckl, (const uint32_t *)slow, nslow, used, pflag, sparse);
         OGE_LAUNCH_CHECK(ctx);
     }
     rc = oge_exclusive_scan_u32(ctx, pflag, pflag, nc1);
@@ -591,63 +634,126 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     uint64_t *spairs = pairs;
     rc = oge_radix_sort_pairs(ctx, pairs, nullptr, pairs2, nullptr, np, bits_mask_hi32(n), &spairs, nullptr);
     if (rc) return rc;
+    P->np = np;
+    if (!np) return OGE_OK;
+    P->hi = (uint64_t *)ctx->scratch("md_hi", (uint64_t)np * 8);
+    P->lo = (uint64_t *)ctx->scratch("md_lo", (uint64_t)np * 8);
+    P->hk = (uint64_t *)ctx->scratch("md_hi2", (uint64_t)np * 8);
+    P->idx = (uint2 *)ctx->scratch("md_pidx", (uint64_t)np * sizeof(uint2));
+    P->val = (uint32_t *)ctx->scratch("md_pv", (uint64_t)np * 4);
+    if (!P->hi || !P->lo || !P->hk || !P->idx || !P->val) return OGE_ERR_HIP;
+    hipLaunchKernelGGL(k_pair_build, dim3(oge_ceil_div(np, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)spairs, np, recs,
+                       meta, L, P->hi, P->lo, P->idx, P->val, P->hk);
+    OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}
+
+int oge_md_pair_groups(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &P, uint8_t *dup) {
+    const uint32_t np = P.np;
+    if (!np) return OGE_OK;
+    uint64_t *lo2 = (uint64_t *)ctx->scratch("md_lo2", (uint64_t)np * 8);
+    uint32_t *pv2 = (uint32_t *)ctx->scratch("md_pv2", (uint64_t)np * 4);
+    if (!lo2 || !pv2) return OGE_ERR_HIP;
+    // 32 bits of a hash of the whole chunk key (hk) group equal keys (k_pair_groups_h splits runs);
+    // debug_hash_bits (tests) also narrows these bits, so runs holding several keys are exercised
+    uint64_t *k2;
+    uint32_t *v2;
+    const int rb = opts->debug_hash_bits > 0 ? std::min(32, opts->debug_hash_bits) : 32;
+    const uint64_t rmask = ~0ull << (64 - rb);
+    int rc = oge_radix_sort_pairs(ctx, P.hk, P.val, lo2, pv2, np, rmask, &k2, &v2);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_pair_groups_h, dim3(oge_ceil_div(np, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)k2,
+                       (const uint32_t *)v2, (const uint64_t *)P.hi, (const uint64_t *)P.lo, (const uint2 *)P.idx, np, rmask, dup);
+    OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}
+
+int oge_md_frag_groups(oge_ctx *ctx, uint64_t *fk, uint32_t *fv, uint64_t n, uint8_t *dup) {
+    if (!n) return OGE_OK;
+    uint64_t *fk2 = (uint64_t *)ctx->scratch("md_fk2", (n + 1) * 8);
+    uint32_t *fv2 = (uint32_t *)ctx->scratch("md_fv2", (n + 1) * 4);
+    if (!fk2 || !fv2) return OGE_ERR_HIP;
+    uint64_t o = 0, a = 0;
+    int rc = oge_reduce_or_and_u64(ctx, fk, n, (1ull << 47) - 1, &o, &a);
+    if (rc) return rc;
+    uint64_t *k;
+    uint32_t *v;
+    rc = oge_radix_sort_pairs(ctx, fk, fv, fk2, fv2, n, (o ^ a) & ((1ull << 47) - 1), &k, &v);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_frag_groups, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)k, (const uint32_t *)v, n,
+                       dup);
+    OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}
+
+int oge_md_apply_desc(oge_ctx *ctx, const uint64_t *desc0, uint64_t n, uint8_t *dup, uint64_t *desc, uint64_t *n_dup_out) {
+    unsigned long long *ndup = (unsigned long long *)ctx->ws("md_ndup", 8);
+    unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
+    if (!ndup || !cnt) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(ndup, 0, 8, ctx->stream));
+    if (n) {
+        hipLaunchKernelGGL(k_apply_desc, dim3(std::min<uint32_t>(oge_ceil_div(n, kT), 2048u)), dim3(kT), 0, ctx->stream, desc0, n, dup, 0,
+                           (const unsigned int *)(cnt + 1), ndup, desc);
+        OGE_LAUNCH_CHECK(ctx);
+    }
+    unsigned long long h = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&h, ndup, 8, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *n_dup_out = h;
+    return OGE_OK;
+}
+
+// Everything after the per-record ReadEnds pass.  meta[i] describes record i of the stream
+// (record index = i); its bytes are at recs + meta[i].src (only read to confirm pair keys).
+// dup[i] receives 1/0/2 (see oge_markdup); with apply, FLAG 0x400 is rewritten in place at
+// recs + off[i].
+int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
+                       const oge_markdup_opts *opts, const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out,
+                       uint64_t *d_desc, bool *desc_ok) {
+    if (desc_ok) *desc_ok = false;
+    KeyLayout L;
+    int rc = md_layout(ctx, opts, &L);
+    if (rc) return rc;
+    unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
+    unsigned long long *ndup = (unsigned long long *)ctx->ws("md_ndup", 8);
+    if (!cnt || !ndup) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(d_dup, 0, n ? n : 1, ctx->stream));
+    if (!n) { *n_dup_out = 0; return OGE_OK; }
+    const uint32_t nb = oge_ceil_div(n, kT);
+
+    // ---- mate join ----
+    OgeStageTimer *t = ctx->begin_stage("md_matejoin");
+    OgeMdFrags F;
+    rc = oge_md_cand_frag(ctx, opts, meta, n, d_desc != nullptr, &F);
+    if (rc) return rc;
+    const bool use_desc = d_desc && !F.desc_ovf;
+    OgeMdPairs P;
+    rc = oge_md_join_build(ctx, opts, d_recs, meta, n, F, &P);
+    if (rc) return rc;
     ctx->end_stage(t);
 
     // ---- pair groups ----
     t = ctx->begin_stage("md_pairs");
-    if (np) {
-        uint64_t *hi = (uint64_t *)ctx->scratch("md_hi", (uint64_t)np * 8);
-        uint64_t *lo = (uint64_t *)ctx->scratch("md_lo", (uint64_t)np * 8);
-        uint64_t *lo2 = (uint64_t *)ctx->scratch("md_lo2", (uint64_t)np * 8);
-        uint64_t *hi2 = (uint64_t *)ctx->scratch("md_hi2", (uint64_t)np * 8);
-        uint2 *pidx = (uint2 *)ctx->scratch("md_pidx", (uint64_t)np * sizeof(uint2));
-        uint32_t *pv = (uint32_t *)ctx->scratch("md_pv", (uint64_t)np * 4);
-        uint32_t *pv2 = (uint32_t *)ctx->scratch("md_pv2", (uint64_t)np * 4);
-        if (!hi || !lo || !lo2 || !hi2 || !pidx || !pv || !pv2) return OGE_ERR_HIP;
-        const uint32_t pb = oge_ceil_div(np, kT);
-        hipLaunchKernelGGL(k_pair_build, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)spairs, np,
-                           (const uint8_t *)d_recs, meta, L, hi, lo, pidx, pv, hi2);
-        OGE_LAUNCH_CHECK(ctx);
-        // 32 bits of a hash of the whole chunk key (hi2) group equal keys (k_pair_groups_h splits runs)
-        uint64_t *k2;
-        uint32_t *v2;
-        // debug_hash_bits (tests) also narrows these bits, so runs holding several keys are exercised
-        const int rb = opts->debug_hash_bits > 0 ? std::min(32, opts->debug_hash_bits) : 32;
-        const uint64_t rmask = ~0ull << (64 - rb);
-        rc = oge_radix_sort_pairs(ctx, hi2, pv, lo2, pv2, np, rmask, &k2, &v2);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_pair_groups_h, dim3(pb), dim3(kT), 0, ctx->stream, (const uint64_t *)k2, (const uint32_t *)v2,
-                           (const uint64_t *)hi, (const uint64_t *)lo, (const uint2 *)pidx, np, rmask, d_dup);
-        OGE_LAUNCH_CHECK(ctx);
-    }
+    rc = oge_md_pair_groups(ctx, opts, P, d_dup);
+    if (rc) return rc;
     ctx->end_stage(t);
 
     // ---- fragment groups ----
     t = ctx->begin_stage("md_frags");
-    uint64_t *fk2 = (uint64_t *)ctx->scratch("md_fk2", (n + 1) * 8);
-    uint32_t *fv2 = (uint32_t *)ctx->scratch("md_fv2", (n + 1) * 4);
-    if (!fk2 || !fv2) return OGE_ERR_HIP;  // fk / fv were written by k_cand_frag
-    {
-        uint64_t o = 0, a = 0;
-        rc = oge_reduce_or_and_u64(ctx, fk, n, (1ull << 47) - 1, &o, &a);
-        if (rc) return rc;
-        uint64_t *k;
-        uint32_t *v;
-        rc = oge_radix_sort_pairs(ctx, fk, fv, fk2, fv2, n, (o ^ a) & ((1ull << 47) - 1), &k, &v);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_frag_groups, dim3(nb), dim3(kT), 0, ctx->stream, (const uint64_t *)k, (const uint32_t *)v, n, d_dup);
-        OGE_LAUNCH_CHECK(ctx);
-    }
+    rc = oge_md_frag_groups(ctx, F.fk, F.fv, n, d_dup);  // fk / fv were written by k_cand_frag
+    if (rc) return rc;
     ctx->end_stage(t);
 
     // ---- apply ----
     t = ctx->begin_stage("md_apply");
+    OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 16, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemsetAsync(ndup, 0, 8, ctx->stream));
     if (opts->compat_nonverbose_index) {
         hipLaunchKernelGGL(k_any, dim3(nb), dim3(kT), 0, ctx->stream, (const uint8_t *)d_dup, n, cnt + 1);
         OGE_LAUNCH_CHECK(ctx);
     }
     if (use_desc && !apply)
-        hipLaunchKernelGGL(k_apply_desc, dim3(std::min<uint32_t>(nb, 2048u)), dim3(kT), 0, ctx->stream, (const uint64_t *)desc0,
+        hipLaunchKernelGGL(k_apply_desc, dim3(std::min<uint32_t>(nb, 2048u)), dim3(kT), 0, ctx->stream, (const uint64_t *)F.desc0,
                            n, d_dup, opts->compat_nonverbose_index, (const unsigned int *)(cnt + 1), ndup, d_desc);
     else
         hipLaunchKernelGGL(k_apply, dim3(std::min<uint32_t>(nb, 2048u)), dim3(kT), 0, ctx->stream, d_recs, d_off, n, meta, d_dup,

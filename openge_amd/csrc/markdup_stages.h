@@ -1,0 +1,44 @@
+// markdup_stages.h -- the stages of the device MarkDuplicates (markdup.hip), callable one by one so
+// the multi-GPU path (dist.hip) can run them on ReadEnds exchanged between ranks:
+//
+//   cand_frag   per-record pass over the sorted summaries: mate-join candidate keys, fragment group
+//               keys (fk/fv), gather descriptors (mark_duplicates.cpp:147-164,185-205)
+//   join_build  ReadEndsMap pairing of consecutive occurrences of each RG:name key and the pair
+//               ReadEnds (read1/read2 choice, orientation, int16 score sum; :210-245)
+//   pair_groups markDuplicatePairs over equal (lib, r1Seq, r1Coord, orient, r2Seq, r2Coord) (:488-507)
+//   frag_groups markDuplicateFragments over equal (lib, r1Seq, r1Coord, orient) (:515-540)
+//   apply_desc  0x400 set / cleared on primaries, counted (:443-465)
+//
+// dup[] is indexed by whatever the stage's index arrays hold: the record index on one GPU, a padded
+// global index (home rank * stride + sorted position) on several.
+#pragma once
+#include "oge_ctx.h"
+#include "records.h"
+
+struct OgeMdFrags {
+    uint32_t *cpos = nullptr;   // n + 1: exclusive scan of the candidate flags
+    uint64_t *fk = nullptr;     // n fragment group keys (bit 46: not a fragment; bit 63: paired)
+    uint32_t *fv = nullptr;     // n record indices
+    uint64_t *cval = nullptr;   // n candidate keys (hash bits << ib | index)
+    uint64_t *desc0 = nullptr;  // n gather descriptors (optional)
+    uint32_t nc = 0;            // candidates
+    bool desc_ovf = false;      // a record offset does not fit the descriptor
+};
+
+struct OgeMdPairs {  // pair ReadEnds, np entries (see k_pair_build for the packing of hi / lo)
+    uint64_t *hi = nullptr, *lo = nullptr, *hk = nullptr;
+    uint2 *idx = nullptr;  // (read1 index, read2 index)
+    uint32_t *val = nullptr;
+    uint32_t np = 0;
+};
+
+int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
+                     OgeMdFrags *f);
+// recs: the bytes RecMeta.src points into (only read for names that do not fit the summary)
+int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t *recs, const RecMeta *meta, uint64_t n,
+                      const OgeMdFrags &f, OgeMdPairs *p);
+int oge_md_pair_groups(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &p, uint8_t *dup);
+int oge_md_frag_groups(oge_ctx *ctx, uint64_t *fk, uint32_t *fv, uint64_t n, uint8_t *dup);
+int oge_md_apply_desc(oge_ctx *ctx, const uint64_t *desc0, uint64_t n, uint8_t *dup, uint64_t *desc, uint64_t *n_dup_out);
+// hk (the chunk-key hash k_pair_build writes) and val = 0..np-1 for pairs received from other ranks
+int oge_md_pairs_rehash(oge_ctx *ctx, OgeMdPairs *p);

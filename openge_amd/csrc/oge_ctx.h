@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <string>
 #include <vector>
@@ -23,7 +24,7 @@ struct oge_ctx {
     std::map<std::string, Buf> bufs;
     // stage -> list of (start, stop) event pairs recorded during the last pipeline call
     std::map<std::string, std::vector<OgeStageTimer>> stage_events;
-    std::vector<OgeStageTimer> event_pool;
+    std::deque<OgeStageTimer> event_pool;  // deque: begin_stage's pointers stay valid while stages nest
     size_t event_pool_used = 0;
     bool timing = true;
     int timing_hold = 0;  // > 0: a composite entry point (the pipeline) keeps its sub-calls' stage events
@@ -57,8 +58,17 @@ struct oge_ctx {
         }                                                                                          \
     } while (0)
 
-// Launch-error check after a kernel launch.
-#define OGE_LAUNCH_CHECK(ctx) OGE_HIP_TRY(ctx, hipGetLastError())
+// Launch-error check after a kernel launch (names the launch site).
+#define OGE_STR2(x) #x
+#define OGE_STR(x) OGE_STR2(x)
+#define OGE_LAUNCH_CHECK(ctx)                                                                      \
+    do {                                                                                           \
+        hipError_t _e = hipGetLastError();                                                         \
+        if (_e != hipSuccess)                                                                      \
+            return oge_fail((ctx), OGE_ERR_HIP,                                                    \
+                            (std::string("kernel launch at " __FILE__ ":" OGE_STR(__LINE__) ": ") + \
+                             hipGetErrorString(_e)).c_str());                                      \
+    } while (0)
 
 static inline uint32_t oge_ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 

@@ -298,7 +298,8 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     int rc = oge_reduce_or_and_u64(ctx, keys, n, kSortKeyMask, &o, &a);
     if (rc) return rc;
     unsigned int bad = 0;
-    OGE_HIP_TRY(ctx, hipMemcpy(&bad, counts + 2, 4, hipMemcpyDeviceToHost));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&bad, counts + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (bad & 1) return oge_fail(ctx, OGE_ERR_ARG, "sort: record with refID outside [-1, n_ref) or pos < -1");
     if (bad & 2) return oge_fail(ctx, OGE_ERR_ARG, "sort: record block_size outside [32, 10000] (util/bam_deserializer.h:160)");
     OgeStageTimer *t = ctx->begin_stage("sort_radix");
@@ -333,7 +334,8 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (nlarge) {
         std::vector<uint2> h(nlarge);
-        OGE_HIP_TRY(ctx, hipMemcpy(h.data(), large, nlarge * sizeof(uint2), hipMemcpyDeviceToHost));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(h.data(), large, nlarge * sizeof(uint2), hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         std::vector<uint64_t> so(nlarge);
         uint64_t tot = 0;
         for (unsigned i = 0; i < nlarge; ++i) {

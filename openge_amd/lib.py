@@ -211,7 +211,16 @@ def lib() -> C.CDLL:
         "oge_bam_markdup_opts": (C.c_int, [vp, vp, C.POINTER(vp), C.POINTER(vp)]),
         "oge_bam_write": (C.c_int, [C.c_char_p, C.c_char_p, u64, C.c_int, vp, vp, u64, vp, vp, C.c_int, C.c_int]),
         "oge_realign_scan": (C.c_int, [vp, vp, vp, vp]),
-        "oge_shard_route_dev": (C.c_int, [vp, vp, vp, u64, vp, i32, i32, vp, vp, vp]),
+        "oge_comm_unique_id_bytes": (u64, []),
+        "oge_comm_unique_id": (C.c_int, [vp, u64]),
+        "oge_comm_init_rank": (C.c_int, [vp, C.c_int, C.c_int, vp, C.POINTER(vp)]),
+        "oge_comm_init": (C.c_int, [vp, C.c_int, vp]),
+        "oge_comm_destroy": (None, [vp]),
+        "oge_comm_rank": (C.c_int, [vp]),
+        "oge_comm_size": (C.c_int, [vp]),
+        "oge_comm_transport": (C.c_char_p, [vp]),
+        "oge_sort_markdup_dist": (C.c_int, [vp, vp, vp, u64, i32, vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64),
+                                            C.POINTER(u64)]),
         "oge_synth_offsets_range_dev": (C.c_int, [vp, vp, u64, u64, vp]),
         "oge_synth_records_range_dev": (C.c_int, [vp, vp, u64, u64, vp, vp]),
         "oge_dev_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
@@ -590,3 +599,62 @@ class Context:
             check(L.oge_synth_offsets_dev(self.h, C.byref(p), d_offs), self.h)
         if d_out:
             check(L.oge_synth_records_dev(self.h, C.byref(p), d_offs, d_out), self.h)
+
+
+# ------------------------------------------------------------------------- multi-GPU (oge_comm)
+class Comm:
+    """One rank of a multi-GPU communicator (oge_comm_*): RCCL over xGMI, or the in-process
+    transport when several contexts share a GPU.  Every method is collective."""
+
+    def __init__(self, h: C.c_void_p, ctx: "Context"):
+        self.h, self.ctx = h, ctx
+
+    @property
+    def rank(self) -> int:
+        return lib().oge_comm_rank(self.h)
+
+    @property
+    def size(self) -> int:
+        return lib().oge_comm_size(self.h)
+
+    @property
+    def transport(self) -> str:
+        return lib().oge_comm_transport(self.h).decode()
+
+    def sort_markdup_dist(self, d_recs: int, d_off: int, n: int, n_ref: int, opts: "MarkdupOpts | None"):
+        """This rank's shard -> its slice of the sorted (and, with opts, duplicate-marked) output:
+        (d_out pointer, d_out_off pointer, records in the slice, duplicates over all ranks).  The
+        pointers are owned by the rank's context (valid until its next call)."""
+        d, do = C.c_void_p(), C.c_void_p()
+        no, nd = C.c_uint64(), C.c_uint64()
+        check(lib().oge_sort_markdup_dist(self.h, d_recs, d_off, n, n_ref, C.byref(opts) if opts is not None else None,
+                                          C.byref(d), C.byref(do), C.byref(no), C.byref(nd)), self.ctx.h)
+        return d.value or 0, do.value or 0, no.value, nd.value
+
+    def close(self):
+        if self.h:
+            lib().oge_comm_destroy(self.h)
+            self.h = None
+
+
+def comm_init(ctxs: list["Context"]) -> list[Comm]:
+    """One process, one rank per context (call each rank's methods from its own thread)."""
+    n = len(ctxs)
+    arr = (C.c_void_p * n)(*[c.h for c in ctxs])
+    out = (C.c_void_p * n)()
+    check(lib().oge_comm_init(arr, n, out))
+    return [Comm(C.c_void_p(out[i]), ctxs[i]) for i in range(n)]
+
+
+def comm_unique_id() -> bytes:
+    nb = lib().oge_comm_unique_id_bytes()
+    buf = C.create_string_buffer(nb)
+    check(lib().oge_comm_unique_id(buf, nb))
+    return buf.raw
+
+
+def comm_init_rank(ctx: "Context", nranks: int, rank: int, uid: bytes) -> Comm:
+    """One process per GPU (RCCL): uid from comm_unique_id() on one rank, shared by the caller."""
+    h = C.c_void_p()
+    check(lib().oge_comm_init_rank(ctx.h, nranks, rank, uid, C.byref(h)), ctx.h)
+    return Comm(h, ctx)

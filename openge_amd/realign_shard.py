@@ -5,7 +5,7 @@ contig: a read bin never spans contigs (ReadBin::add, algorithms/local_realignme
 intervals are walked in order (map_func :455-553), and the mate-fixing writer flushes and forgets
 its mate map whenever a read of another contig arrives (ConstrainedMateFixingManager::
 addReadInternal, util/gatk/ConstrainedMateFixingManager.cpp:312-330).  So rank r realigns the
-records of its contig range (the same contiguous partition as the sort, ``shard.contig_owners``)
+records of its contig range (contiguous refID ranges, ``contig_owners``)
 with the whole interval list, and the rank outputs concatenate into the single-process output.
 
 The one coupling the writer has across a contig boundary -- a flush that finds
@@ -17,7 +17,34 @@ from __future__ import annotations
 import numpy as np
 
 from . import lib as L
-from .shard import contig_owners
+
+
+def contig_owners(ref_lens: list[int], world: int) -> list[int]:
+    """Owner rank of each refID (+ one trailing entry for refID -1, on the last rank).
+
+    Contiguous refID ranges (so rank outputs concatenate in sorted order) minimising the largest
+    range's total length: binary search on the capacity with a greedy fill (linear partition)."""
+    lens = [float(x) for x in ref_lens]
+
+    def fill(cap):
+        owners, r, acc = [], 0, 0.0
+        for ln in lens:
+            if acc > 0 and acc + ln > cap:
+                r, acc = r + 1, 0.0
+            owners.append(r)
+            acc += ln
+        return owners
+
+    lo, hi = max(lens, default=0.0), sum(lens)
+    for _ in range(100):
+        mid = (lo + hi) / 2
+        if fill(mid)[-1:] and fill(mid)[-1] >= world:
+            lo = mid
+        else:
+            hi = mid
+    owners = fill(hi) if lens else []
+    owners = [min(o, world - 1) for o in owners]
+    return owners + [world - 1]
 
 
 def record_refids(recs: np.ndarray, offs: np.ndarray, n: int) -> np.ndarray:

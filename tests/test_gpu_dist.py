@@ -1,0 +1,176 @@
+"""GPU: multi-GPU sort + duplicate marking through the C ABI (oge_comm_init / oge_sort_markdup_dist,
+openge_amd/csrc/dist.hip) equals the one-GPU `mergesort [-M] --nosplit` output record for record.
+
+On the one-GPU test box G ranks are G contexts on device 0, one thread each, joined by the
+in-process transport (the same schedule RCCL runs between GPUs).  Inputs: the reference-made golden
+cases, C2/mix synthetic sets, and C2 with supplementary (0x800, counted as primary by the reference,
+bt/BamAlignment.cpp:493-495) copies on other contigs, so names carry 3 and 4 primaries whose
+ReadEndsMap pairing (mark_duplicates.cpp:213-245) depends on the global order of their ends --
+checked against the oracle restatement as well.  Shards are contiguous input ranges (one of them
+empty in one case) and, separately, an interleaved split."""
+import struct
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import bamutil
+import oracle
+from goldens import CASE_NAMES, load_case
+from openge_amd import lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _single(ctx, recs, offs, n, n_ref, opts):
+    d_recs = torch.from_numpy(recs).cuda()
+    d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_perm = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+    d_out = torch.empty(recs.size, dtype=torch.uint8, device="cuda")
+    d_oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    nd = 0
+    if opts is not None:
+        nd = ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(), d_out.data_ptr(),
+                                  d_oo.data_ptr())
+    else:
+        ctx.sort_coord_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, n_ref, d_perm.data_ptr())
+        ctx.gather_records_dev(d_recs.data_ptr(), d_offs.data_ptr(), d_perm.data_ptr(), n, d_out.data_ptr(), d_oo.data_ptr())
+    ctx.sync()
+    oo = d_oo.cpu().numpy()
+    return d_out[int(oo[0]):int(oo[n])].cpu().numpy().tobytes(), nd
+
+
+def _shards(recs, offs, cuts):
+    """contiguous input ranges [cuts[g], cuts[g+1]) as (record bytes, offsets from 0)"""
+    out = []
+    for g in range(len(cuts) - 1):
+        lo, hi = cuts[g], cuts[g + 1]
+        b0, b1 = int(offs[lo]), int(offs[hi])
+        out.append((np.concatenate([recs[b0:b1], np.zeros(64, np.uint8)]), (offs[lo:hi + 1] - b0).astype(np.int64)))
+    return out
+
+
+def run_dist(shards, n_ref, opts):
+    """One rank per shard, all on device 0; returns (concatenated output stream, per-rank counts, dups)."""
+    G = len(shards)
+    ctxs = [L.Context(0) for _ in range(G)]
+    comms = L.comm_init(ctxs)
+    assert comms[0].transport == "local" and comms[0].size == G
+    res, errs = [None] * G, []
+
+    def work(g):
+        try:
+            recs, offs = shards[g]
+            n = len(offs) - 1
+            d_recs = torch.from_numpy(recs).cuda()
+            d_offs = torch.from_numpy(offs).cuda()
+            torch.cuda.synchronize()
+            d, do, no, nd = comms[g].sort_markdup_dist(d_recs.data_ptr(), d_offs.data_ptr(), n, n_ref, opts)
+            oo = np.empty(no + 1, np.uint64)
+            L.check(L.lib().oge_memcpy(ctxs[g].h, oo.ctypes.data, do, 8 * (no + 1), 2), ctxs[g].h)
+            out = np.empty(int(oo[no] - oo[0]), np.uint8)
+            if out.size:
+                L.check(L.lib().oge_memcpy(ctxs[g].h, out.ctypes.data, d + int(oo[0]), out.size, 2), ctxs[g].h)
+            res[g] = (out.tobytes(), no, nd)
+        except Exception as e:  # noqa: BLE001
+            errs.append((g, e))
+
+    ts = [threading.Thread(target=work, args=(g,)) for g in range(G)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    for c in comms:
+        c.close()
+    for c in ctxs:
+        c.close()
+    if errs:
+        raise errs[0][1]
+    assert len({r[2] for r in res}) == 1  # every rank reports the same total
+    return b"".join(r[0] for r in res), [r[1] for r in res], res[0][2]
+
+
+def _check(ctx, recs, offs, n_ref, header, G, cuts=None, sort_only=False):
+    n = len(offs) - 1
+    opts = None
+    if not sort_only:
+        opts, keep = L.markdup_opts_from_header(header, n_ref)
+    want, nd = _single(ctx, recs, offs, n, n_ref, opts)
+    cuts = cuts or [n * g // G for g in range(G + 1)]
+    got, counts, gd = run_dist(_shards(recs, offs, cuts), n_ref, opts)
+    assert sum(counts) == n
+    assert got == want
+    assert gd == nd
+    return counts, nd
+
+
+@pytest.mark.parametrize("name", CASE_NAMES)
+@pytest.mark.parametrize("G", [2, 3])
+def test_dist_equals_single_on_goldens(ctx, name, G):
+    c = load_case(name)
+    _check(ctx, c.recs, c.offs, c.n_ref, c.header, G)
+    if G == 3:  # sort only (mergesort without -M)
+        _check(ctx, c.recs, c.offs, c.n_ref, c.header, G, sort_only=True)
+
+
+@pytest.mark.parametrize("preset,pairs,seed,G", [("c2", 40000, 11, 2), ("c2", 40000, 12, 3), ("mix", 6000, 5, 3),
+                                                  ("c2", 60000, 13, 5)])
+def test_dist_equals_single_synthetic(ctx, preset, pairs, seed, G):
+    p = L.synth_params(pairs, preset=preset, seed=seed)
+    recs, offs, hdr = L.synth_host(p)
+    counts, nd = _check(ctx, recs, offs, p.n_ref, hdr, G)
+    assert nd > 0
+    if preset == "c2":  # range splitters balance the slices (sampling error only)
+        assert max(counts) / (sum(counts) / G) < 1.05
+
+
+def test_dist_uneven_and_empty_shards(ctx):
+    p = L.synth_params(8000, preset="c2", seed=21)
+    recs, offs, hdr = L.synth_host(p)
+    n = len(offs) - 1
+    _check(ctx, recs, offs, p.n_ref, hdr, 3, cuts=[0, 0, n // 5, n])
+    _check(ctx, recs, offs, p.n_ref, hdr, 2, cuts=[0, n, n])
+
+
+def _with_supplementaries(recs, offs, n_ref, ref_len, seed):
+    """C2 records plus 0x800 copies of ~4% of the reads on another contig (a few names get two),
+    mate fields unchanged: 3- and 4-primary names for the ReadEndsMap."""
+    rng = np.random.default_rng(seed)
+    n = len(offs) - 1
+    out = [bamutil.rec_bytes(recs, offs[i]) for i in range(n)]
+    pick = rng.choice(n, size=n // 25, replace=False)
+    extra = []
+    for k, i in enumerate(pick):
+        for _ in range(2 if k % 7 == 0 else 1):
+            b = bytearray(out[i])
+            (flag,) = struct.unpack_from("<H", b, 18)
+            ref = int(rng.integers(0, n_ref))
+            pos = int(rng.integers(0, max(1, ref_len[ref] - 200)))
+            struct.pack_into("<iI", b, 4, ref, pos)
+            struct.pack_into("<H", b, 18, (flag | 0x800) & ~0x400)
+            extra.append(bytes(b))
+    allr = out + extra
+    order = rng.permutation(len(allr))
+    return bamutil.pack_records([allr[j] for j in order])
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_dist_supplementary_names_exact(ctx, G):
+    p = L.synth_params(15000, preset="c2", seed=31)
+    recs0, offs0, hdr = L.synth_host(p)
+    lens = [int(p.ref_len[i]) for i in range(p.n_ref)]
+    recs, offs = _with_supplementaries(recs0, offs0, p.n_ref, lens, 32)
+    n = len(offs) - 1
+    # the one-GPU path against the oracle restatement of mark_duplicates.cpp on the sorted stream
+    perm = oracle.sort_perm(recs, offs, n)
+    srecs, soffs = bamutil.pack_records([bamutil.rec_bytes(recs, offs[i]) for i in perm])
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    dup, nd = ctx.markdup(srecs, soffs, n, opts)
+    odup, ond = oracle.markdup(srecs, soffs, n, hdr)
+    assert nd == ond and np.array_equal(dup, odup)
+    # the multi-GPU path against the one-GPU path, contiguous and interleaved input splits
+    _check(ctx, recs, offs, p.n_ref, hdr, G)
+    inter = np.concatenate([np.arange(g, n, G) for g in range(G)])
+    irecs, ioffs = bamutil.pack_records([bamutil.rec_bytes(recs, offs[i]) for i in inter])
+    _check(ctx, irecs, ioffs, p.n_ref, hdr, G)
