@@ -43,6 +43,8 @@ typedef struct oge_ctx oge_ctx;
 
 /* ---- context ---------------------------------------------------------------------- */
 int oge_ctx_create(int device, oge_ctx **out);
+/* number of HIP devices visible to the process (0 when there is none) */
+int oge_device_count(void);
 /* stream: a hipStream_t (0 = the context's own non-blocking stream) */
 int oge_ctx_set_stream(oge_ctx *ctx, void *stream);
 void *oge_ctx_stream(oge_ctx *ctx);
@@ -57,7 +59,8 @@ const char *oge_version(void);
 /* ---- device buffers (for host code that stages records in HBM without HIP headers) ---- */
 int oge_dev_alloc(oge_ctx *ctx, uint64_t bytes, void **out);
 int oge_dev_free(oge_ctx *ctx, void *p);
-/* kind: 1 = host->device, 2 = device->host, 3 = device->device; synchronous on the ctx stream */
+/* kind: 1 = host->device, 2 = device->host, 3 = device->device, 4 = any (also between two GPUs'
+ * HBM); synchronous on the ctx stream */
 int oge_memcpy(oge_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind);
 /* enable != 0: device buffers (oge_dev_alloc and the library's workspaces) come from the device's
  * stream-ordered pool and freed memory stays reserved for the next allocation of this process
@@ -177,13 +180,22 @@ void oge_comm_destroy(oge_comm *comm);
 int oge_comm_rank(const oge_comm *comm);
 int oge_comm_size(const oge_comm *comm);
 const char *oge_comm_transport(const oge_comm *comm); /* "rccl" or "local" */
-/* This rank's shard of the input (any split; contiguous input ranges in rank order keep the
- * reference's input-order tie-break) -> this rank's slice of the globally sorted output, with bin
- * recomputed and, when opts != NULL, 0x400 set/cleared exactly as oge_sort_markdup_dev does on the
- * whole input (compat_nonverbose_index unsupported).  Concatenating the slices in rank order gives
- * the one-GPU output.  *d_out / *d_out_off (*n_out + 1 offsets) are owned by the rank's context and
- * valid until its next call; *n_dup_total = 0x400 records over all ranks. */
-int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+/* This rank's shard of the input: contiguous input ranges in rank order (any sizes, empty ones
+ * included).  sort != 0 (mergesort [-M]): -> this rank's slice of the globally sorted output, with
+ * bin recomputed and, when opts != NULL, 0x400 set/cleared exactly as oge_sort_markdup_dev does on
+ * the whole input.  sort == 0 (dedup): the shard keeps its records and their order, marked exactly
+ * as oge_markdup_dev marks the whole input (record index = input position).  compat_nonverbose_index
+ * is one-GPU only.  Concatenating the slices in rank order gives the one-GPU output.  *d_out /
+ * *d_out_off (*n_out + 1 offsets) are owned by the rank's context and valid until its next call;
+ * *n_dup_total = 0x400 records over all ranks.  d_off[i] are byte offsets from d_recs. */
+/* The whole mergesort [-M] [-R] chain (oge_mergesort_bgzf_dev) over the communicator's ranks: rank g
+ * passes its own input BAM file (resident in its HBM; the output header is rank 0's file's, as
+ * MultiReader takes the first file's), and *d_out receives rank g's slice of the one output file --
+ * rank 0's begins with the header, the last rank's ends with the EOF block, so the slices concatenate
+ * in rank order (valid until the rank's next call).  *n_reads_total: records written by all ranks. */
+int oge_mergesort_bgzf_dist(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *o,
+                            const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads_total, uint64_t *n_dup_total);
+int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref, int sort,
                           const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
                           uint64_t *n_dup_total);
 /* Device synthetic generation of the slot range [slot0, slot0 + nslots) of a data set (one rank's

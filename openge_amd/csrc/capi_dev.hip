@@ -116,6 +116,11 @@ const char *oge_version(void) { return "openge_amd 0.1 (gfx950)"; }
 
 const char *oge_last_error(const oge_ctx *ctx) { return ctx ? ctx->err.c_str() : g_last_error.c_str(); }
 
+int oge_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 int oge_ctx_create(int device, oge_ctx **out) {
     if (!out) return oge_fail(nullptr, OGE_ERR_ARG, "oge_ctx_create: out is NULL");
     int ndev = 0;
@@ -230,8 +235,9 @@ int oge_host_free(oge_ctx *ctx, void *p) {
 
 int oge_memcpy(oge_ctx *ctx, void *dst, const void *src, uint64_t bytes, int kind) {
     if (!ctx || (bytes && (!dst || !src))) return oge_fail(ctx, OGE_ERR_ARG, "oge_memcpy: null argument");
-    hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-    if (kind < 1 || kind > 3) return oge_fail(ctx, OGE_ERR_ARG, "oge_memcpy: bad kind");
+    hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost
+                    : kind == 3 ? hipMemcpyDeviceToDevice : hipMemcpyDefault;
+    if (kind < 1 || kind > 4) return oge_fail(ctx, OGE_ERR_ARG, "oge_memcpy: bad kind");
     hipSetDevice(ctx->device);
     if (bytes) OGE_HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, k, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -319,6 +319,11 @@ __global__ __launch_bounds__(kT) void k_padded_index(const uint32_t *__restrict_
     if (k < n) out[k] = base + local[k];
 }
 
+__global__ __launch_bounds__(kT) void k_iota(uint64_t n, uint32_t *__restrict__ v) {
+    const uint64_t k = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (k < n) v[k] = (uint32_t)k;
+}
+
 __global__ __launch_bounds__(kT) void k_map_pair_idx(uint2 *__restrict__ idx, uint32_t np, const uint32_t *__restrict__ gidx) {
     const uint32_t p = blockIdx.x * kT + threadIdx.x;
     if (p < np) idx[p] = make_uint2(gidx[idx[p].x], gidx[idx[p].y]);
@@ -409,7 +414,11 @@ struct Dist {
 
 }  // namespace
 
-static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, uint64_t RB, int32_t n_ref, const uint64_t *d_spl,
+                      bool sorted, const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
+                      uint64_t *n_dup_total);
+
+static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref, int sort,
                     const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out, uint64_t *n_dup_total) {
     oge_ctx *ctx = comm->ctx;
     Dist D{comm, ctx, comm->tr->size, comm->tr->rank};
@@ -418,6 +427,7 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     int rc = OGE_OK;
     if (opts && opts->compat_nonverbose_index) rc = oge_fail(ctx, OGE_ERR_ARG, "multi-GPU dedup: compat_nonverbose_index is one-GPU only");
     if (n > 0xFFFFFFFEull) rc = oge_fail(ctx, OGE_ERR_LIMIT, "multi-GPU: more than 2^32-2 records on one rank");
+    if (!sort && !opts) rc = oge_fail(ctx, OGE_ERR_ARG, "multi-GPU: nothing to do (no sort, no duplicate marking)");
     if ((rc = D.agree(rc))) return rc;
 
     // ---- 1. range split
@@ -447,12 +457,22 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     }
     const std::vector<uint64_t> spl = oge_dist::choose_splitters(per, alln, G);
     uint64_t *d_spl = (uint64_t *)ctx->ws("dist_spl", 8 * (nspl + 1));
+    if (!d_spl) rc = OGE_ERR_HIP;
+    if (!rc && nspl) rc = hipMemcpyAsync(d_spl, spl.data(), 8 * nspl, hipMemcpyHostToDevice, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    uint64_t total = 0, first = 0;
+    if (!rc && n) rc = D.d2h(&total, d_off + n, 8);
+    if (!rc && n) rc = D.d2h(&first, d_off, 8);
+    if (!sort) {  // dedup: records stay where they are, in input order (record index = input position)
+        ctx->end_stage(t);
+        if ((rc = D.agree(rc))) return rc;
+        return dist_dedup(D, const_cast<uint8_t *>(d_recs), d_off, n, total - first, n_ref, d_spl, false, opts, d_out, d_out_off,
+                          n_out, n_dup_total);
+    }
     uint64_t *dkey = (uint64_t *)ctx->ws("dist_dkey", (n + 1) * 8);
     uint32_t *dval = (uint32_t *)ctx->ws("dist_dval", (n + 1) * 4);
     uint32_t *perm = nullptr;
     std::vector<uint64_t> cnt;
-    if (!d_spl || !dkey || !dval) rc = OGE_ERR_HIP;
-    if (!rc && nspl) rc = hipMemcpyAsync(d_spl, spl.data(), 8 * nspl, hipMemcpyHostToDevice, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    if (!dkey || !dval) rc = OGE_ERR_HIP;
     if (!rc && n) {
         hipLaunchKernelGGL(k_dest_range, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)keys, n,
                            (const uint64_t *)d_spl, nspl, dkey, dval);
@@ -460,10 +480,6 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     }
     if (!rc) rc = D.partition(dkey, dval, n, "rec", &perm, cnt);
     // send buffer: records grouped by destination (stable), their sizes
-    uint64_t total = 0;
-    if (!rc && n) rc = D.d2h(&total, d_off + n, 8);
-    uint64_t first = 0;
-    if (!rc && n) rc = D.d2h(&first, d_off, 8);
     uint8_t *sbuf = (uint8_t *)ctx->ws("dist_sbuf", total - first + 64);
     uint64_t *soff = (uint64_t *)ctx->ws("dist_soff", (n + 1) * 8);
     uint32_t *ssz = (uint32_t *)ctx->ws("dist_ssz", (n + 1) * 4);
@@ -524,9 +540,28 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
         return OGE_OK;
     }
 
+    return dist_dedup(D, rbuf, roff, R, RB, n_ref, d_spl, true, opts, d_out, d_out_off, n_out, n_dup_total);
+}
+
+// Duplicate marking of this rank's records (its sorted slice when `sorted`, else its input shard in
+// input order), then the gather of the records with bin recomputed and 0x400 applied.
+static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, uint64_t RB, int32_t n_ref, const uint64_t *d_spl,
+                      bool sorted, const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
+                      uint64_t *n_dup_total) {
+    oge_comm *comm = D.comm;
+    oge_ctx *ctx = D.ctx;
+    const int G = D.G;
+    const uint32_t nspl = (uint32_t)G - 1;
+    int rc = OGE_OK;
+    OgeStageTimer *t = nullptr;
+    uint8_t *out = (uint8_t *)ctx->ws("dist_out", RB + 64);
+    uint64_t *out_off = (uint64_t *)ctx->ws("dist_out_off", (R + 1) * 8);
+    if (!out || !out_off) rc = OGE_ERR_HIP;
+    uint64_t *k = nullptr;
+    uint32_t *v = nullptr;
     RecMeta *meta_in = nullptr, *meta = nullptr;
     OgeRgTable rg;
-    rc = oge_markdup_prepare(ctx, opts, R, "md_meta_in", &meta_in, &rg);
+    if (!rc) rc = oge_markdup_prepare(ctx, opts, R, "md_meta_in", &meta_in, &rg);
     uint64_t *skeys = nullptr;
     uint32_t *svals = nullptr;
     unsigned int *counts = oge_sort_counts(ctx);
@@ -542,14 +577,24 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
         a.n = R;
         a.meta = meta_in;
         a.rg = rg;
-        a.keys = skeys;
-        a.vals = svals;
+        a.keys = sorted ? skeys : nullptr;
+        a.vals = sorted ? svals : nullptr;
         a.n_ref = n_ref;
         a.bad = counts + 2;
         rc = oge_input_pass(ctx, a);
         ctx->end_stage(t);
     }
-    if (!rc) rc = oge_sort_keys_dev(ctx, rbuf, roff, R, n_ref, true, &k, &v, meta_in, meta);
+    if (sorted) {
+        if (!rc) rc = oge_sort_keys_dev(ctx, rbuf, roff, R, n_ref, true, &k, &v, meta_in, meta);
+    } else {  // input order: the summaries as they are, the identity permutation for the gather
+        v = svals;
+        if (!rc && R) rc = hipMemcpyAsync(meta, meta_in, R * sizeof(RecMeta), hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess
+                               ? 0 : dist_hip_fail(ctx, __LINE__);
+        if (!rc && R) {
+            hipLaunchKernelGGL(k_iota, dim3(oge_ceil_div(R, kT)), dim3(kT), 0, ctx->stream, R, v);
+            rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+        }
+    }
     if ((rc = D.agree(rc))) return rc;
 
     // ---- 3. dedup: global indices
@@ -561,6 +606,7 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
         return oge_fail(ctx, OGE_ERR_LIMIT, "multi-GPU dedup: G x the largest slice exceeds 2^32 records");
     const uint32_t base = (uint32_t)((uint64_t)D.rank * stride);
     (void)Ntot;
+    (void)nspl;
     uint8_t *dup_pad = (uint8_t *)ctx->ws("dist_dup_pad", (size_t)G * stride);
     uint8_t *dup = (uint8_t *)ctx->ws("dist_dup", stride + 1);
     uint64_t *desc = (uint64_t *)ctx->ws("dist_desc", (R + 1) * 8);
@@ -761,6 +807,20 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     return OGE_OK;
 }
 
+oge_ctx *oge_comm_ctx(oge_comm *comm) { return comm ? comm->ctx : nullptr; }
+
+int oge_comm_sum_u64(oge_comm *comm, uint64_t *v, int count) {
+    const int G = comm->tr->size;
+    std::vector<uint64_t> all((size_t)G * count);
+    const int rc = comm->tr->allgather_host(comm->ctx, v, all.data(), 8 * (size_t)count);
+    if (rc) return rc;
+    for (int k = 0; k < count; ++k) {
+        v[k] = 0;
+        for (int g = 0; g < G; ++g) v[k] += all[(size_t)g * count + k];
+    }
+    return OGE_OK;
+}
+
 // ---------------------------------------------------------------------------------------------- ABI
 extern "C" {
 
@@ -838,7 +898,7 @@ int oge_comm_rank(const oge_comm *c) { return c ? c->tr->rank : -1; }
 int oge_comm_size(const oge_comm *c) { return c ? c->tr->size : -1; }
 const char *oge_comm_transport(const oge_comm *c) { return c ? c->tr->name() : ""; }
 
-int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref, int sort,
                           const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
                           uint64_t *n_dup_total) {
     if (!comm || !d_out || !d_out_off || !n_out || (n && (!d_recs || !d_off)))
@@ -847,7 +907,7 @@ int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t 
     (void)hipSetDevice(ctx->device);
     ctx->reset_timing();
     if (opts && opts->n_ref != n_ref) return oge_fail(ctx, OGE_ERR_ARG, "oge_sort_markdup_dist: opts->n_ref differs from n_ref");
-    return dist_run(comm, d_recs, d_off, n, n_ref, opts, d_out, d_out_off, n_out, n_dup_total);
+    return dist_run(comm, d_recs, d_off, n, n_ref, sort, opts, d_out, d_out_off, n_out, n_dup_total);
 }
 
 }  // extern "C"

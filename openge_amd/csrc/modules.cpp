@@ -59,6 +59,93 @@ void ChainContext::free_device(ReadBatch &b) {
     b.dev_valid = false;
 }
 
+int ChainContext::init_ranks() {
+    if (gpus <= 1 || !comms.empty()) return 0;
+    const int ndev = oge_device_count();
+    if (ndev < 1) return fail("--gpus");
+    rank_ctx.assign(gpus, nullptr);
+    rank_ctx[0] = ctx;
+    for (int g = 1; g < gpus; ++g) {
+        if (oge_ctx_create((device + g) % ndev, &rank_ctx[g])) {
+            rank_ctx.resize(g);
+            return fail("--gpus: context");
+        }
+        const char *pool = getenv("OGE_POOL");
+        if (!(pool && std::string(pool) == "0")) oge_ctx_set_pool(rank_ctx[g], 1);
+    }
+    comms.assign(gpus, nullptr);
+    if (oge_comm_init(rank_ctx.data(), gpus, comms.data())) {
+        comms.clear();
+        return fail("--gpus: communicator");
+    }
+    if (verbose)
+        fprintf(stderr, "[openge] %d ranks on %d device(s), transport %s\n", gpus, std::min(gpus, ndev), oge_comm_transport(comms[0]));
+    return 0;
+}
+
+void ChainContext::close_ranks() {
+    for (oge_comm *c : comms) oge_comm_destroy(c);
+    comms.clear();
+    for (size_t g = 1; g < rank_ctx.size(); ++g) oge_ctx_destroy(rank_ctx[g]);
+    rank_ctx.clear();
+}
+
+// Cut the batch into G contiguous input ranges and run oge_sort_markdup_dist on every rank (one host
+// thread each).  A rank whose own preparation failed still joins the collectives with an empty shard
+// so the others finish, and the failure is reported.
+int run_ranks(ChainContext &cc, ReadBatch &b, bool sort, const oge_markdup_opts *opts, uint64_t *n_dup) {
+    if (cc.init_ranks() || cc.to_device(b)) return -1;
+    const int G = cc.gpus;
+    const uint64_t n = b.n;
+    const int32_t n_ref = (int32_t)b.ref_names.size();
+    std::vector<uint64_t> cut(G + 1), boff(G + 1);
+    for (int g = 0; g <= G; ++g) {
+        cut[g] = n * (uint64_t)g / (uint64_t)G;
+        if (oge_memcpy(cc.ctx, &boff[g], b.d_offs + cut[g], 8, 2)) return cc.fail("device->host copy");
+    }
+    std::vector<ReadBatch::Slice> sl(G);
+    std::vector<int> rcs(G, 0);
+    std::vector<uint64_t> nds(G, 0);
+    std::vector<std::string> why(G);
+    std::vector<std::thread> ts;
+    for (int g = 0; g < G; ++g)
+        ts.emplace_back([&, g]() {
+            oge_ctx *c = cc.rank_ctx[g];
+            const uint64_t lo = cut[g], m = cut[g + 1] - lo, bytes = boff[g + 1] - boff[g];
+            void *r = nullptr, *o = nullptr;
+            int rc = oge_dev_alloc(c, bytes + 64, &r);
+            if (!rc) rc = oge_dev_alloc(c, (m + 1) * 8, &o);
+            if (!rc && bytes) rc = oge_memcpy(c, r, b.d_recs + boff[g], bytes, 4);
+            if (!rc) rc = oge_memcpy(c, o, b.d_offs + lo, (m + 1) * 8, 4);
+            if (rc) why[g] = oge_last_error(c);
+            uint8_t *dout = nullptr;
+            uint64_t *doff = nullptr, no = 0, nd = 0;
+            // the offsets stay absolute: the records pointer is shifted back by the range's first one
+            const int rd = rc ? oge_sort_markdup_dist(cc.comms[g], nullptr, nullptr, 0, n_ref, sort ? 1 : 0, opts, &dout, &doff, &no, &nd)
+                              : oge_sort_markdup_dist(cc.comms[g], (const uint8_t *)r - boff[g], (const uint64_t *)o, m, n_ref,
+                                                      sort ? 1 : 0, opts, &dout, &doff, &no, &nd);
+            if (!rc && rd) why[g] = oge_last_error(c);
+            rcs[g] = rc ? rc : rd;
+            if (r) oge_dev_free(c, r);
+            if (o) oge_dev_free(c, o);
+            sl[g] = {c, dout, doff, no};
+            nds[g] = nd;
+        });
+    for (auto &t : ts) t.join();
+    for (int g = 0; g < G; ++g)
+        if (rcs[g]) {
+            fprintf(stderr, "openge: rank %d: %s\n", g, why[g].c_str());
+            return -1;
+        }
+    cc.free_device(b);
+    b.slices = sl;
+    b.n = 0;
+    for (auto &x : sl) b.n += x.n;
+    b.host_valid = false;
+    *n_dup = nds[0];
+    return 0;
+}
+
 int AlgorithmModule::runChain(ChainContext &cc) {
     AlgorithmModule *head = this;
     while (head->source_) head = head->source_;
@@ -409,6 +496,20 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
         fprintf(stderr, "openge: unsupported sort order\n");
         return -1;
     }
+    MarkDuplicates *md = order_ == BamHeaderModel::COORDINATE ? dynamic_cast<MarkDuplicates *>(sink_) : nullptr;
+    if (cc.gpus > 1 && order_ == BamHeaderModel::COORDINATE) {  // --gpus G: range-split sort (+ dedup) over G ranks
+        MdOpts m;
+        if (md) markdup_opts(b, md->compatNonverbose, md->splitChains, m);
+        uint64_t nd = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (run_ranks(cc, b, true, md ? &m.o : nullptr, &nd)) return -1;
+        if (md) md->duplicates = nd;
+        b.header.sort_order = order_;
+        if (verbose_)
+            fprintf(stderr, "[openge] ReadSorter: %d ranks, %.3f s\n", cc.gpus,
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        return 0;
+    }
     const auto t0 = std::chrono::steady_clock::now();
     if (cc.to_device(b)) return -1;
     const auto t1 = std::chrono::steady_clock::now();
@@ -419,7 +520,6 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
     if (verbose_) oge_ctx_sync(cc.ctx);
     const auto t1a = std::chrono::steady_clock::now();
     int rc;
-    MarkDuplicates *md = order_ == BamHeaderModel::COORDINATE ? dynamic_cast<MarkDuplicates *>(sink_) : nullptr;
     if (order_ == BamHeaderModel::QUERYNAME) {  // -b; a MarkDuplicates sink then runs on its own
         rc = oge_sort_name_dev(cc.ctx, b.d_recs, b.d_offs, b.n, (uint32_t *)perm);
         if (!rc) rc = oge_gather_records_dev(cc.ctx, b.d_recs, b.d_offs, (uint32_t *)perm, b.n, (uint8_t *)out, (uint64_t *)out_off);
@@ -464,6 +564,19 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
 
 // ----------------------------------------------------------------------------------- MarkDuplicates
 int MarkDuplicates::runInternal(ChainContext &cc, ReadBatch &b) {
+    if (cc.gpus > 1) {  // --gpus G: every rank marks its input range in place order
+        if (compatNonverbose) {
+            fprintf(stderr, "openge: --compat-nonverbose-dedup is one-GPU only\n");
+            return -1;
+        }
+        MdOpts m;
+        markdup_opts(b, false, splitChains, m);
+        uint64_t nd = 0;
+        if (run_ranks(cc, b, false, &m.o, &nd)) return -1;
+        duplicates = nd;
+        b.drop_duplicates = removeDuplicates;
+        return 0;
+    }
     if (cc.to_device(b)) return -1;
     void *dup = nullptr;
     if (oge_dev_alloc(cc.ctx, b.n + 1, &dup)) return cc.fail("device allocation");
@@ -481,13 +594,95 @@ int MarkDuplicates::runInternal(ChainContext &cc, ReadBatch &b) {
 }
 
 // ----------------------------------------------------------------------------------- LocalRealignment
+// --gpus G: realignment shards by contig -- a read bin, the interval walk and the mate
+// fixer's state never span contigs (alg/local_realignment.cpp:263-275,455-553,
+// gatk/ConstrainedMateFixingManager.cpp:312-330) -- so rank g realigns a contiguous range of whole
+// contigs of the coordinate-sorted input (ranges balanced by record count) and the outputs concatenate.
+static int realign_ranks(ChainContext &cc, ReadBatch &b, const std::string &ht, const std::string &ref, const std::string &iv,
+                         bool verbose) {
+    if (cc.init_ranks()) return -1;
+    const int G = cc.gpus;
+    const uint64_t n = b.n;
+    std::vector<int64_t> rid(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        const int32_t r = oge_rd_i32(b.recs.data() + b.offs[i] + OGE_OFF_REFID);
+        rid[i] = r < 0 ? INT64_MAX : r;
+        if (i && rid[i] < rid[i - 1]) {
+            fprintf(stderr, "openge: localrealign --gpus needs coordinate-sorted input\n");
+            return -1;
+        }
+    }
+    std::vector<uint64_t> cut(G + 1, n);  // cuts at contig boundaries nearest the equal-count targets
+    cut[0] = 0;
+    for (int g = 1; g < G; ++g) {
+        uint64_t c = std::max<uint64_t>(cut[g - 1], n * (uint64_t)g / (uint64_t)G);
+        while (c > cut[g - 1] && c < n && rid[c] == rid[c - 1]) --c;  // back to the contig's first record
+        if (c == cut[g - 1]) {                                          // or forward past it
+            c = n * (uint64_t)g / (uint64_t)G;
+            while (c < n && c > 0 && rid[c] == rid[c - 1]) ++c;
+        }
+        cut[g] = std::max(c, cut[g - 1]);
+    }
+    std::vector<oge_realign_result *> res(G, nullptr);
+    std::vector<std::string> why(G);
+    std::vector<std::thread> ts;
+    for (int g = 0; g < G; ++g)
+        ts.emplace_back([&, g]() {
+            oge_realign_opts o;
+            oge_realign_opts_init(&o);
+            o.threads = std::max(1, cc.threads / G);
+            if (oge_localrealign(cc.rank_ctx[g], ht.data(), ht.size(), b.recs.data(), b.offs.data() + cut[g], cut[g + 1] - cut[g],
+                                 ref.c_str(), iv.c_str(), &o, &res[g]))
+                why[g] = oge_last_error(cc.rank_ctx[g]);
+        });
+    for (auto &t : ts) t.join();
+    int ret = 0;
+    bytevec recs;
+    std::vector<uint64_t> offs(1, 0);
+    for (int g = 0; g < G && !ret; ++g) {
+        if (!res[g]) {
+            fprintf(stderr, "openge: LocalRealignment rank %d: %s\n", g, why[g].c_str());
+            ret = -1;
+            break;
+        }
+        const char *st = oge_realign_result_stats(res[g]);
+        const char *tw = strstr(st, "\"tail_waiting\": ");
+        oge_realign_opts d;
+        oge_realign_opts_init(&d);
+        if (g + 1 < G && tw && strtoull(tw + 16, nullptr, 10) >= (uint64_t)d.max_records_in_memory) {
+            // the mate fixer flushed with maxRecordsInMemory reads waiting: that flush keeps its modified
+            // mate entries across the contig boundary, so the ranks would not concatenate exactly
+            fprintf(stderr, "openge: localrealign --gpus: the mate fixer held >= %d reads at a shard boundary; run on one GPU\n",
+                    d.max_records_in_memory);
+            ret = -1;
+            break;
+        }
+        if (verbose) fprintf(stderr, "[openge] LocalRealignment rank %d: %s\n", g, st);
+        uint64_t bytes = 0;
+        const uint8_t *rp = oge_realign_result_records(res[g], &bytes);
+        const uint64_t *op = oge_realign_result_offsets(res[g]);
+        const uint64_t m = oge_realign_result_count(res[g]), base = recs.size();
+        recs.insert(recs.end(), rp + op[0], rp + op[m]);
+        for (uint64_t k = 1; k <= m; ++k) offs.push_back(base + op[k] - op[0]);
+    }
+    for (auto *r : res)
+        if (r) oge_realign_result_free(r);
+    if (ret) return ret;
+    b.n = offs.size() - 1;
+    recs.resize(recs.size() + 16, 0);
+    b.recs = std::move(recs);
+    b.offs = std::move(offs);
+    return 0;
+}
+
 int LocalRealignment::runInternal(ChainContext &cc, ReadBatch &b) {
     if (cc.to_host(b)) return -1;
     cc.free_device(b);
+    const std::string ht = b.header.to_string();
+    if (cc.gpus > 1) return realign_ranks(cc, b, ht, reference_, intervals_, verbose);
     oge_realign_opts o;
     oge_realign_opts_init(&o);
     o.threads = cc.threads;
-    const std::string ht = b.header.to_string();
     oge_realign_result *r = nullptr;
     if (oge_localrealign(cc.ctx, ht.data(), ht.size(), b.recs.data(), b.offs.data(), b.n, reference_.c_str(),
                          intervals_.c_str(), &o, &r))
@@ -622,13 +817,75 @@ int FileWriter::write_device(ChainContext &cc, ReadBatch &b, BgzfWriter &w, doub
     return 0;
 }
 
+// --gpus G: every rank drops its duplicates (-r / -R) and BGZF-compresses its own slice on its own
+// GPU, concurrently; the compressed slices go to the file in rank order (a slice's last block may be
+// short, the decompressed stream is the one-GPU stream).
+int FileWriter::write_slices(ChainContext &cc, ReadBatch &b, BgzfWriter &w) {
+    const int G = (int)b.slices.size();
+    struct Out {
+        void *host = nullptr;
+        uint64_t zb = 0;
+        int rc = 0;
+        std::string why;
+    };
+    std::vector<Out> outs(G);
+    const int level = std::max(0, std::min(9, level_));
+    const bool drop = b.drop_duplicates;
+    std::vector<std::thread> ts;
+    for (int g = 0; g < G; ++g)
+        ts.emplace_back([&, g]() {
+            const ReadBatch::Slice &s = b.slices[g];
+            Out &o = outs[g];
+            oge_ctx *c = s.ctx;
+            uint8_t *recs = s.d_recs;
+            uint64_t *offs = s.d_offs, n = s.n;
+            void *kept = nullptr, *kept_off = nullptr, *dz = nullptr;
+            int rc = 0;
+            if (drop && n) {
+                rc = oge_dev_alloc(c, (n + 1) * 8, &kept_off);
+                uint64_t e = 0, m = 0;
+                if (!rc) rc = oge_memcpy(c, &e, offs + n, 8, 2);
+                if (!rc) rc = oge_dev_alloc(c, e + 64, &kept);
+                if (!rc) rc = oge_drop_flagged_dev(c, recs, offs, n, OGE_F_DUP, (uint8_t *)kept, (uint64_t *)kept_off, &m);
+                recs = (uint8_t *)kept;
+                offs = (uint64_t *)kept_off;
+                n = m;
+            }
+            uint64_t ends[2] = {0, 0};
+            if (!rc && n) rc = oge_memcpy(c, &ends[0], offs, 8, 2) || oge_memcpy(c, &ends[1], offs + n, 8, 2);
+            const uint64_t len = ends[1] - ends[0], cap = oge_bgzf_bound(len);
+            if (!rc && len) rc = oge_dev_alloc(c, cap, &dz);
+            if (!rc && len) rc = oge_bgzf_deflate_dev(c, recs + ends[0], len, level, (uint8_t *)dz, cap, &o.zb);
+            if (!rc && o.zb) rc = oge_host_alloc(c, o.zb, &o.host);
+            if (!rc && o.zb) rc = oge_memcpy(c, o.host, dz, o.zb, 2);
+            if (rc) o.why = oge_last_error(c);
+            o.rc = rc;
+            for (void *p : {kept, kept_off, dz})
+                if (p) oge_dev_free(c, p);
+        });
+    w.write_compressed(nullptr, 0);  // the header's blocks first
+    int ret = 0;
+    for (int g = 0; g < G; ++g) {
+        ts[g].join();
+        if (outs[g].rc) {
+            fprintf(stderr, "openge: FileWriter: rank %d: %s\n", g, outs[g].why.c_str());
+            ret = -1;
+        } else if (!ret && outs[g].zb) {
+            w.write_compressed((const uint8_t *)outs[g].host, outs[g].zb);
+        }
+        if (outs[g].host) oge_host_free(b.slices[g].ctx, outs[g].host);
+    }
+    return ret;
+}
+
 int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
     auto clk = [] { return std::chrono::steady_clock::now(); };
     auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
         return std::chrono::duration<double>(z - a).count();
     };
     const auto t0 = clk();
-    const bool on_device = b.dev_valid && !b.host_valid && !bgzf_host_codec_forced();
+    const bool sliced = !b.slices.empty();
+    const bool on_device = sliced || (b.dev_valid && !b.host_valid && !bgzf_host_codec_forced());
     double t_dev = 0, t_d2h = 0, t_wait = 0;
     if (!on_device && cc.to_host(b)) return -1;
     const auto t1 = clk();
@@ -647,7 +904,7 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
         std::vector<uint8_t> hb = bam_encode_header(h);
         w.write(hb.data(), hb.size());
         if (on_device) {
-            if (write_device(cc, b, w, &t_dev, &t_d2h, &t_wait)) {
+            if (sliced ? write_slices(cc, b, w) : write_device(cc, b, w, &t_dev, &t_d2h, &t_wait)) {
                 w.abandon();  // no EOF block and no write into the FILE closed below
                 if (f != stdout) fclose(f);
                 return -1;

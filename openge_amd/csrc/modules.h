@@ -33,6 +33,15 @@ struct ReadBatch {
     bool dev_valid = false;
     // dedup output applied by the writer (-r / -R: records carrying 0x400 are not written)
     bool drop_duplicates = false;
+    // multi-GPU (--gpus G): the records as G slices in rank order, each in its rank's HBM (owned by
+    // the rank's context); when set, the host and device forms above are unused
+    struct Slice {
+        oge_ctx *ctx;
+        uint8_t *d_recs;
+        uint64_t *d_offs;  // n + 1 byte offsets from d_recs
+        uint64_t n;
+    };
+    std::vector<Slice> slices;
 
     uint64_t bytes() const { return host_valid ? offs[n] : d_bytes; }
 };
@@ -42,6 +51,13 @@ struct ChainContext {
     int device = 0;
     int threads = 0;
     bool verbose = false;
+    // --gpus G: rank contexts (rank 0 = ctx, rank g on device (device + g) % devices; ranks share a
+    // device when there are fewer devices than ranks) and their communicators
+    int gpus = 1;
+    std::vector<oge_ctx *> rank_ctx;
+    std::vector<oge_comm *> comms;
+    int init_ranks();
+    void close_ranks();
     int fail(const std::string &where);  // prints oge_last_error, returns -1
     int to_device(ReadBatch &b);
     int to_host(ReadBatch &b);
@@ -157,6 +173,10 @@ protected:
     std::string reference_, intervals_;
 };
 
+// The multi-GPU form of ReadSorter (+ MarkDuplicates) and of a standalone MarkDuplicates: the batch
+// is cut into G contiguous input ranges, one per rank, and oge_sort_markdup_dist leaves b.slices.
+int run_ranks(ChainContext &cc, ReadBatch &b, bool sort, const oge_markdup_opts *opts, uint64_t *n_dup);
+
 // FileWriter (algorithms/file_writer.cpp:69-196): BAM output, @PG record unless --nopg, BGZF at the
 // given level, bin recomputed on every record.
 class FileWriter : public AlgorithmModule {
@@ -165,6 +185,7 @@ public:
     void setFilename(const std::string &f) { filename_ = f; }
     void setCompressionLevel(int l) { level_ = l; }
     int write_device(ChainContext &cc, ReadBatch &b, BgzfWriter &w, double *t_dev, double *t_d2h, double *t_wait);
+    int write_slices(ChainContext &cc, ReadBatch &b, BgzfWriter &w);
     void addProgramLine(const std::string &cl) { program_line_ = cl; }
     int setFormat(const std::string &f);  // only "bam" is supported (SAM/FASTQ out of scope)
 protected:

@@ -97,3 +97,8 @@ int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzf
 int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d0, const uint64_t *d1,
                       const uint64_t *uoff, const uint32_t *crc, uint64_t nblk, uint8_t *out, uint32_t *err,
                       const uint32_t *zpow);
+
+// ---- multi-GPU internals (dist.hip)
+oge_ctx *oge_comm_ctx(oge_comm *comm);
+// in place: v[0..count) = the sum over the communicator's ranks (collective, host values)
+int oge_comm_sum_u64(oge_comm *comm, uint64_t *v, int count);

@@ -38,7 +38,7 @@ const Opt kGlobal[] = {{"v", "verbose", false}, {"t", "threads", true}, {"d", "n
                        {"T", "tmpdir", true},   {"", "nosplit", false},  {"i", "in", true},
                        {"F", "format", true},   {"c", "compression", true}, {"", "nopg", false},
                        {"", "device", true},    {"", "compat-nonverbose-dedup", false},
-                       {"", "split-chains", true}, {"", "compat-split", false}};
+                       {"", "split-chains", true}, {"", "compat-split", false}, {"", "gpus", true}};
 const Opt kMergesort[] = {{"o", "out", true}, {"r", "region", true},  {"q", "mapq", true},
                           {"b", "byname", false}, {"n", "n", true}, {"C", "compresstempfiles", false},
                           {"M", "markduplicates", false}, {"R", "removeduplicates", false}};
@@ -144,6 +144,7 @@ int main(int argc, const char **argv) {
     cc.verbose = p.count("verbose");
     cc.threads = atoi(p.get("threads", std::to_string(std::max(1u, std::thread::hardware_concurrency()))).c_str());
     cc.device = atoi(p.get("device", "0").c_str());
+    cc.gpus = std::max(1, atoi(p.get("gpus", "1").c_str()));  // ranks over RCCL / xGMI
     AlgorithmModule::setVerbose(cc.verbose);
     const int level = atoi(p.get("compression", "6").c_str());
     const bool compat = p.count("compat-nonverbose-dedup");
@@ -227,6 +228,7 @@ int main(int argc, const char **argv) {
         lr.addSink(&writer);
         ret = writer.runChain(cc);
     }
+    cc.close_ranks();
     oge_ctx_destroy(cc.ctx);
     if (cc.verbose) {  // commands.cpp:91-108
         rusage r;

@@ -15,6 +15,9 @@
 //   sort     oge_sort_markdup_dev (or sort + gather without -M) X -> Y, bins recomputed
 //   [-R]     oge_drop_flagged_dev Y -> X
 //   write    header block (host) + oge_bgzf_deflate_dev + EOF block into the free buffer
+//
+// oge_mergesort_bgzf_dist runs the same chain over G ranks (one input file per rank, the sort and
+// dedup through oge_sort_markdup_dist, every rank deflating its own output slice).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -79,16 +82,9 @@ extern "C" void oge_mergesort_opts_init(oge_mergesort_opts *o) {
     o->level = 6;  // FileWriter's default compression level (commands.cpp:129, -c)
 }
 
-extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *mo,
-                                      const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup) {
-    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
-    if (!mo || !d_out || !out_bytes || (zbytes && !d_z)) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
-    if (mo->level < 0 || mo->level > 9) return oge_fail(ctx, OGE_ERR_ARG, "level must be 0..9");
-    hipSetDevice(ctx->device);
-    Hold hold(ctx);
-    *d_out = nullptr;
-    *out_bytes = 0;
-
+// The reader half: framing index, inflate into X (ws "pipe_x", *cap bytes), header parse, record walk.
+static int decode(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint8_t **Xo, uint64_t *cap_out, uint64_t **xoff_o,
+                  uint64_t *n_o, BamFile *f) {
     // ---- framing index (device; host walk of a copy when the chain is not exact)
     OgeStageTimer *tm = ctx->begin_stage("bgzf_index");
     OgeBgzfIndex ix;
@@ -119,18 +115,17 @@ extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t
     if (rc) return rc;
 
     // ---- header (host parse of the stream's first bytes)
-    BamFile f;
     std::string err;
     size_t rec_base = 0;
     for (uint64_t pre = std::min<uint64_t>(total, 1 << 20);; pre = std::min<uint64_t>(total, pre * 8)) {
         std::vector<uint8_t> h(pre);
         OGE_HIP_TRY(ctx, hipMemcpyAsync(h.data(), X, pre, hipMemcpyDeviceToHost, ctx->stream));
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        f = BamFile();
-        if (bam_parse_header(h.data(), pre, f, err, &rec_base)) break;
+        *f = BamFile();
+        if (bam_parse_header(h.data(), pre, *f, err, &rec_base)) break;
         if (pre == total) return oge_fail(ctx, OGE_ERR_IO, ("BAM header: " + err).c_str());
     }
-    const int32_t n_ref = (int32_t)f.ref_names.size();
+    const int32_t n_ref = (int32_t)f->ref_names.size();
 
     // ---- record boundaries
     tm = ctx->begin_stage("rec_walk");
@@ -142,6 +137,60 @@ extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t
     rc = oge_bam_record_offsets_dev(ctx, X, rec_base, total, n_ref, xoff, n + 1, &n);
     if (rc) return rc;
     ctx->end_stage(tm);
+    *Xo = X;
+    *cap_out = cap;
+    *xoff_o = xoff;
+    *n_o = n;
+    return OGE_OK;
+}
+
+// The writer half: [header block(s)] + device deflate of records [soff[0], soff[m]) of src + [EOF]
+// into dst (dst_cap bytes).
+static int encode(oge_ctx *ctx, const uint8_t *src, const uint64_t *soff, uint64_t m, const std::vector<uint8_t> *header,
+                  bool eof, int level, uint8_t *dst, uint64_t dst_cap, uint64_t *out_bytes) {
+    const std::vector<uint8_t> hz = header ? bgzf_compress_host(header->data(), header->size(), level) : std::vector<uint8_t>();
+    uint64_t ends[2] = {0, 0};
+    if (m) {
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&ends[0], soff, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&ends[1], soff + m, 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t len = ends[1] - ends[0];
+    if (hz.size() + oge_bgzf_bound(len) + 28 > dst_cap) return oge_fail(ctx, OGE_ERR_LIMIT, "output buffer too small");
+    if (!hz.empty()) OGE_HIP_TRY(ctx, hipMemcpyAsync(dst, hz.data(), hz.size(), hipMemcpyHostToDevice, ctx->stream));
+    uint64_t zb = 0;
+    if (len) {
+        const int rc = oge_bgzf_deflate_dev(ctx, src + ends[0], len, level, dst + hz.size(), dst_cap - hz.size() - 28, &zb);
+        if (rc) return rc;
+    }
+    if (eof) OGE_HIP_TRY(ctx, hipMemcpyAsync(dst + hz.size() + zb, kBgzfEof, 28, hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *out_bytes = hz.size() + zb + (eof ? 28 : 0);
+    return OGE_OK;
+}
+
+static std::vector<uint8_t> out_header(const BamFile &f, const oge_mergesort_opts *mo) {
+    BamHeaderModel oh = f.header;
+    oh.sort_order = BamHeaderModel::COORDINATE;  // read_sorter.cpp:257-258
+    if (mo->program_line) add_program_record(oh, mo->program_line);
+    return bam_encode_header(oh);
+}
+
+extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *mo,
+                                      const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if (!mo || !d_out || !out_bytes || (zbytes && !d_z)) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    if (mo->level < 0 || mo->level > 9) return oge_fail(ctx, OGE_ERR_ARG, "level must be 0..9");
+    (void)hipSetDevice(ctx->device);
+    Hold hold(ctx);
+    *d_out = nullptr;
+    *out_bytes = 0;
+    uint8_t *X;
+    uint64_t cap, *xoff, n;
+    BamFile f;
+    int rc = decode(ctx, d_z, zbytes, &X, &cap, &xoff, &n, &f);
+    if (rc) return rc;
+    const int32_t n_ref = (int32_t)f.ref_names.size();
 
     // ---- sort (+ markdup), gathered into Y with bins recomputed and 0x400 applied
     uint8_t *Y = (uint8_t *)ctx->ws("pipe_y", cap);
@@ -161,7 +210,7 @@ extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t
     uint64_t *soff = yoff;
     uint64_t m = n;
     if (mo->mark_duplicates && mo->remove_duplicates) {  // -R: MarkDuplicates::runInternal :456-458
-        tm = ctx->begin_stage("drop_dups");
+        OgeStageTimer *tm = ctx->begin_stage("drop_dups");
         rc = oge_drop_flagged_dev(ctx, Y, yoff, n, 0x400, X, xoff, &m);
         ctx->end_stage(tm);
         if (rc) return rc;
@@ -169,30 +218,87 @@ extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t
     }
 
     // ---- output: header block(s) (host zlib/libdeflate, tiny), device deflate of the records, EOF
-    BamHeaderModel oh = f.header;
-    oh.sort_order = BamHeaderModel::COORDINATE;  // read_sorter.cpp:257-258
-    if (mo->program_line) add_program_record(oh, mo->program_line);
-    const std::vector<uint8_t> hb = bam_encode_header(oh);
-    const std::vector<uint8_t> hz = bgzf_compress_host(hb.data(), hb.size(), mo->level);
-    uint64_t ends[2] = {0, 0};
-    if (m) {
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(&ends[0], soff, 8, hipMemcpyDeviceToHost, ctx->stream));
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(&ends[1], soff + m, 8, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    const uint64_t len = ends[1] - ends[0];
-    if (hz.size() + oge_bgzf_bound(len) + 28 > cap) return oge_fail(ctx, OGE_ERR_LIMIT, "output buffer too small");
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(dst, hz.data(), hz.size(), hipMemcpyHostToDevice, ctx->stream));
-    uint64_t zb = 0;
-    if (len) {
-        rc = oge_bgzf_deflate_dev(ctx, src + ends[0], len, mo->level, dst + hz.size(), cap - hz.size() - 28, &zb);
-        if (rc) return rc;
-    }
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(dst + hz.size() + zb, kBgzfEof, 28, hipMemcpyHostToDevice, ctx->stream));
-    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const std::vector<uint8_t> hb = out_header(f, mo);
+    uint64_t ob = 0;
+    rc = encode(ctx, src, soff, m, &hb, true, mo->level, dst, cap, &ob);
+    if (rc) return rc;
     *d_out = dst;
-    *out_bytes = hz.size() + zb + 28;
+    *out_bytes = ob;
     if (n_reads) *n_reads = m;
     if (n_dup) *n_dup = nd;
+    return OGE_OK;
+}
+
+// The same chain over G ranks: rank g's input is its own BAM file (mergesort's inputs, one per rank;
+// the header of rank 0's file is the output's, as MultiReader takes the first file's), the records
+// meet in oge_sort_markdup_dist, and rank g's output is its slice of the one output file: rank 0's
+// starts with the header, the last rank's ends with the EOF block, so the slices concatenate.
+extern "C" int oge_mergesort_bgzf_dist(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *mo,
+                                       const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads_total, uint64_t *n_dup_total) {
+    if (!comm) return oge_fail(nullptr, OGE_ERR_ARG, "null communicator");
+    oge_ctx *ctx = oge_comm_ctx(comm);
+    if (!mo || !d_out || !out_bytes || (zbytes && !d_z)) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    if (mo->level < 0 || mo->level > 9) return oge_fail(ctx, OGE_ERR_ARG, "level must be 0..9");
+    (void)hipSetDevice(ctx->device);
+    Hold hold(ctx);
+    *d_out = nullptr;
+    *out_bytes = 0;
+    const int rank = oge_comm_rank(comm), G = oge_comm_size(comm);
+    uint8_t *X = nullptr;
+    uint64_t cap = 0, *xoff = nullptr, n = 0;
+    BamFile f;
+    // a rank whose decode fails still joins the collectives (with no records), and reports its error
+    int rc = decode(ctx, d_z, zbytes, &X, &cap, &xoff, &n, &f);
+    std::string why = rc ? ctx->err : std::string();
+    const int32_t n_ref = (int32_t)f.ref_names.size();
+    LibTable lt(f.header, n_ref, mo);
+    uint8_t *dout = nullptr;
+    uint64_t *doff = nullptr, no = 0, nd = 0;
+    const int rd = oge_sort_markdup_dist(comm, rc ? nullptr : X, rc ? nullptr : xoff, rc ? 0 : n, n_ref, 1,
+                                         mo->mark_duplicates ? &lt.o : nullptr, &dout, &doff, &no, &nd);
+    if (rc) return oge_fail(ctx, rc, why.c_str());
+    if (rd) return rd;
+    const uint8_t *src = dout;
+    const uint64_t *soff = doff;
+    uint64_t m = no;
+    uint8_t *Y = (uint8_t *)ctx->ws("pipe_y", std::max<uint64_t>(cap, 64));
+    uint64_t *yoff = (uint64_t *)ctx->ws("pipe_yoff", (no + 1) * 8);
+    if (!Y || !yoff) return OGE_ERR_HIP;
+    if (mo->mark_duplicates && mo->remove_duplicates) {
+        uint64_t bytes = 0;
+        if (no) {
+            OGE_HIP_TRY(ctx, hipMemcpyAsync(&bytes, doff + no, 8, hipMemcpyDeviceToHost, ctx->stream));
+            OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        Y = (uint8_t *)ctx->ws("pipe_y", bytes + 64);
+        if (!Y) return OGE_ERR_HIP;
+        OgeStageTimer *tm = ctx->begin_stage("drop_dups");
+        rc = oge_drop_flagged_dev(ctx, dout, doff, no, 0x400, Y, yoff, &m);
+        ctx->end_stage(tm);
+        if (rc) return rc;
+        src = Y, soff = yoff;
+    }
+    uint64_t len = 0;
+    if (m) {
+        uint64_t e[2];
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&e[0], soff, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&e[1], soff + m, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        len = e[1] - e[0];
+    }
+    const std::vector<uint8_t> hb = out_header(f, mo);
+    const uint64_t zcap = oge_bgzf_bound(len) + (rank == 0 ? bgzf_compress_host(hb.data(), hb.size(), mo->level).size() : 0) + 64;
+    uint8_t *Z = (uint8_t *)ctx->ws("pipe_z", zcap);
+    if (!Z) return OGE_ERR_HIP;
+    uint64_t ob = 0;
+    rc = encode(ctx, src, soff, m, rank == 0 ? &hb : nullptr, rank == G - 1, mo->level, Z, zcap, &ob);
+    if (rc) return rc;
+    *d_out = Z;
+    *out_bytes = ob;
+    uint64_t tot = m;  // records written over all ranks
+    rc = oge_comm_sum_u64(comm, &tot, 1);
+    if (rc) return rc;
+    if (n_reads_total) *n_reads_total = tot;
+    if (n_dup_total) *n_dup_total = nd;
     return OGE_OK;
 }

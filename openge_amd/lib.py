@@ -219,7 +219,9 @@ def lib() -> C.CDLL:
         "oge_comm_rank": (C.c_int, [vp]),
         "oge_comm_size": (C.c_int, [vp]),
         "oge_comm_transport": (C.c_char_p, [vp]),
-        "oge_sort_markdup_dist": (C.c_int, [vp, vp, vp, u64, i32, vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64),
+        "oge_mergesort_bgzf_dist": (C.c_int, [vp, vp, u64, vp, C.POINTER(vp), C.POINTER(u64), C.POINTER(u64),
+                                              C.POINTER(u64)]),
+        "oge_sort_markdup_dist": (C.c_int, [vp, vp, vp, u64, i32, C.c_int, vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64),
                                             C.POINTER(u64)]),
         "oge_synth_offsets_range_dev": (C.c_int, [vp, vp, u64, u64, vp]),
         "oge_synth_records_range_dev": (C.c_int, [vp, vp, u64, u64, vp, vp]),
@@ -621,15 +623,26 @@ class Comm:
     def transport(self) -> str:
         return lib().oge_comm_transport(self.h).decode()
 
-    def sort_markdup_dist(self, d_recs: int, d_off: int, n: int, n_ref: int, opts: "MarkdupOpts | None"):
-        """This rank's shard -> its slice of the sorted (and, with opts, duplicate-marked) output:
-        (d_out pointer, d_out_off pointer, records in the slice, duplicates over all ranks).  The
-        pointers are owned by the rank's context (valid until its next call)."""
+    def sort_markdup_dist(self, d_recs: int, d_off: int, n: int, n_ref: int, opts: "MarkdupOpts | None", sort: bool = True):
+        """This rank's shard -> its slice of the sorted (and, with opts, duplicate-marked) output, or
+        with sort=False its shard marked in place order (dedup): (d_out pointer, d_out_off pointer,
+        records in the slice, duplicates over all ranks).  The pointers are owned by the rank's
+        context (valid until its next call)."""
         d, do = C.c_void_p(), C.c_void_p()
         no, nd = C.c_uint64(), C.c_uint64()
-        check(lib().oge_sort_markdup_dist(self.h, d_recs, d_off, n, n_ref, C.byref(opts) if opts is not None else None,
+        check(lib().oge_sort_markdup_dist(self.h, d_recs, d_off, n, n_ref, 1 if sort else 0,
+                                          C.byref(opts) if opts is not None else None,
                                           C.byref(d), C.byref(do), C.byref(no), C.byref(nd)), self.ctx.h)
         return d.value or 0, do.value or 0, no.value, nd.value
+
+    def mergesort_bgzf_dist(self, d_z: int, zbytes: int, opts: "MergesortOpts"):
+        """Rank's input BAM file in HBM -> (its slice of the output file: device pointer, bytes; records
+        written by all ranks; duplicates flagged by all ranks)."""
+        d = C.c_void_p()
+        ob, nr, nd = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(lib().oge_mergesort_bgzf_dist(self.h, d_z, zbytes, C.byref(opts), C.byref(d), C.byref(ob), C.byref(nr),
+                                            C.byref(nd)), self.ctx.h)
+        return d.value or 0, ob.value, nr.value, nd.value
 
     def close(self):
         if self.h:

@@ -172,3 +172,37 @@ def test_cli_write_failures_exit_nonzero(tmp_path):
     r = subprocess.run([OPENGE, "mergesort", "-M", str(src), "-o", "/dev/full"], capture_output=True, text=True,
                        timeout=300)
     assert r.returncode > 0 and "error writing" in r.stderr, (r.returncode, r.stderr)
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_cli_gpus_matches_reference(case, tmp_path, G):
+    """`--gpus G` (replacing SplitByChromosome/SortedMerge, cmd/command_mergesort.cpp:118-179,
+    cmd/command_dedup.cpp:70-113): the same reference outputs as one GPU -- mergesort -M, sort, and
+    dedup of the sorted file, with -R dropping the flagged records.  On a one-GPU box the G ranks
+    share the GPU through the in-process transport."""
+    src = case_input(case, tmp_path)
+    r = run("mergesort", "-M", "--nopg", "-v", "--gpus", G, src, "-o", tmp_path / "o.bam")
+    assert f"{G} ranks" in r.stderr
+    h, m, t = digests(tmp_path / "o.bam")
+    g = case.meta["sortdedup_v"]
+    assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
+    run("sort", "--nopg", "--gpus", G, src, "-o", tmp_path / "s.bam")
+    h, m, t = digests(tmp_path / "s.bam")
+    assert h == case.meta["sorted_header"] and m == case.meta["sort"]["mapped_sha256"]
+    run("dedup", "--nopg", "--gpus", G, tmp_path / "s.bam", "-o", tmp_path / "d.bam")
+    h, m, t = digests(tmp_path / "d.bam")
+    g = case.meta["dedup_sorted_v"]
+    assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
+    run("mergesort", "-R", "--nopg", "--gpus", G, src, "-o", tmp_path / "r.bam")
+    _, _, recs, offs = bamutil.read_bam(tmp_path / "r.bam")
+    assert len(offs) == case.n - case.meta["sortdedup_v"]["n_dup"]
+
+
+@pytest.mark.parametrize("name", ["rl_small", "rl_edge"])
+def test_cli_localrealign_gpus_matches_reference(name, tmp_path):
+    """localrealign --gpus 2: contig-range shards (whole contigs per rank), concatenated."""
+    meta, arrays, h, recs, offs, fa, iv = load_rl_case(name, tmp_path)
+    run("localrealign", "--nopg", "--gpus", 2, "-R", fa, "-L", iv, tmp_path / "reads.bam", "-o", tmp_path / "rl.bam")
+    oh, _, orecs, ooffs = bamutil.read_bam(tmp_path / "rl.bam")
+    assert oh == meta["output_header"]
+    check_output(meta, arrays, orecs, np.append(ooffs, np.uint64(len(orecs))))

@@ -51,7 +51,7 @@ def _shards(recs, offs, cuts):
     return out
 
 
-def run_dist(shards, n_ref, opts):
+def run_dist(shards, n_ref, opts, sort=True):
     """One rank per shard, all on device 0; returns (concatenated output stream, per-rank counts, dups)."""
     G = len(shards)
     ctxs = [L.Context(0) for _ in range(G)]
@@ -66,7 +66,7 @@ def run_dist(shards, n_ref, opts):
             d_recs = torch.from_numpy(recs).cuda()
             d_offs = torch.from_numpy(offs).cuda()
             torch.cuda.synchronize()
-            d, do, no, nd = comms[g].sort_markdup_dist(d_recs.data_ptr(), d_offs.data_ptr(), n, n_ref, opts)
+            d, do, no, nd = comms[g].sort_markdup_dist(d_recs.data_ptr(), d_offs.data_ptr(), n, n_ref, opts, sort)
             oo = np.empty(no + 1, np.uint64)
             L.check(L.lib().oge_memcpy(ctxs[g].h, oo.ctypes.data, do, 8 * (no + 1), 2), ctxs[g].h)
             out = np.empty(int(oo[no] - oo[0]), np.uint8)
@@ -174,3 +174,89 @@ def test_dist_supplementary_names_exact(ctx, G):
     inter = np.concatenate([np.arange(g, n, G) for g in range(G)])
     irecs, ioffs = bamutil.pack_records([bamutil.rec_bytes(recs, offs[i]) for i in inter])
     _check(ctx, irecs, ioffs, p.n_ref, hdr, G)
+
+
+def _unbin(stream: bytes) -> bytes:
+    """the record stream with every bin field zeroed (dedup leaves bins as read; the gather recomputes)"""
+    b, q = bytearray(stream), 0
+    while q < len(b):
+        (bs,) = struct.unpack_from("<I", b, q)
+        b[q + 14:q + 16] = b"\0\0"
+        q += 4 + bs
+    return bytes(b)
+
+
+@pytest.mark.parametrize("name,G", [("yhet208", 2), ("c2_20k", 3), ("mix3k", 2), ("edge", 3)])
+def test_dist_dedup_keeps_input_order(ctx, name, G):
+    """`dedup --gpus G`: each rank marks its input shard in place order, exactly as one GPU marks the
+    whole stream (oge_markdup_dev, record index = input position)."""
+    c = load_case(name)
+    opts, keep = L.markdup_opts_from_header(c.header, c.n_ref)
+    d_recs = torch.from_numpy(c.recs.copy()).cuda()
+    d_offs = torch.from_numpy(c.offs.astype(np.int64)).cuda()
+    d_dup = torch.empty(c.n + 1, dtype=torch.uint8, device="cuda")
+    nd = ctx.markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), c.n, opts, d_dup.data_ptr(), apply=1)
+    ctx.sync()
+    want = d_recs[int(c.offs[0]):int(c.offs[c.n])].cpu().numpy().tobytes()
+    got, counts, gd = run_dist(_shards(c.recs, c.offs, [c.n * g // G for g in range(G + 1)]), c.n_ref, opts, sort=False)
+    assert gd == nd and sum(counts) == c.n
+    assert _unbin(got) == _unbin(want)
+
+
+@pytest.mark.parametrize("G,level,flags", [(2, 6, {"mark_duplicates": 1}), (3, 1, {"mark_duplicates": 1, "remove_duplicates": 1}),
+                                           (2, 6, {})])
+def test_dist_bgzf_chain_equals_single(ctx, tmp_path, G, level, flags):
+    """oge_mergesort_bgzf_dist: G input BAM files (contiguous ranges of one input, same header) -> G
+    output slices that concatenate into one BAM file whose decompressed bytes equal the one-GPU
+    oge_mergesort_bgzf_dev output's."""
+    import gzip
+    p = L.synth_params(30000, preset="c2", seed=41)
+    recs, offs, hdr = L.synth_host(p)
+    n = len(offs) - 1
+    src = tmp_path / "all.bam"
+    L.write_bam(src, hdr, recs, offs, n, level=1)
+    z = src.read_bytes()
+    opts = L.mergesort_opts(level=level, program_line=b"openge mergesort x", **flags)
+    dz = torch.from_numpy(np.frombuffer(z + b"\0" * 8, np.uint8).copy()).cuda()
+    d, nb, nr, nd = ctx.mergesort_bgzf_dev(dz.data_ptr(), len(z), opts)
+    want = np.empty(nb, np.uint8)
+    L.check(L.lib().oge_memcpy(ctx.h, want.ctypes.data, d, nb, 2), ctx.h)
+    files = []
+    for g in range(G):
+        lo, hi = n * g // G, n * (g + 1) // G
+        fg = tmp_path / f"part{g}.bam"
+        r0, r1 = int(offs[lo]), int(offs[hi])
+        part = np.concatenate([recs[r0:r1], np.zeros(16, np.uint8)])
+        L.write_bam(fg, hdr, part, (offs[lo:hi + 1] - r0).astype(np.uint64), hi - lo, level=1)
+        files.append(fg.read_bytes())
+    ctxs = [L.Context(0) for _ in range(G)]
+    comms = L.comm_init(ctxs)
+    res, errs = [None] * G, []
+
+    def work(g):
+        try:
+            b = files[g]
+            t = torch.from_numpy(np.frombuffer(b + b"\0" * 8, np.uint8).copy()).cuda()
+            torch.cuda.synchronize()
+            d, ob, tr, td = comms[g].mergesort_bgzf_dist(t.data_ptr(), len(b), opts)
+            h = np.empty(ob, np.uint8)
+            L.check(L.lib().oge_memcpy(ctxs[g].h, h.ctypes.data, d, ob, 2), ctxs[g].h)
+            res[g] = (h.tobytes(), tr, td)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(g,)) for g in range(G)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    for c in comms:
+        c.close()
+    for c in ctxs:
+        c.close()
+    if errs:
+        raise errs[0]
+    out = b"".join(r[0] for r in res)
+    assert out[-28:] == bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    assert gzip.decompress(out) == gzip.decompress(want.tobytes())
+    assert {(r[1], r[2]) for r in res} == {(nr, nd)}
