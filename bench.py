@@ -165,7 +165,7 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1) -> dict | 
         out, oo, st = run()
         dt = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([dt], dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+            t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
             if rank != 0:
@@ -314,8 +314,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        # RCCL on ROCm: all-to-all over xGMI.  OGE_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs.
-        dist.init_process_group(os.environ.get("OGE_DIST_BACKEND", "nccl"))
+        # torch.distributed only bootstraps the library's RCCL communicator and times the steps (host
+        # values): gloo.  The records move through oge_comm (RCCL over xGMI).
+        dist.init_process_group(os.environ.get("OGE_DIST_BACKEND", "gloo"))
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -463,48 +464,72 @@ def main():
     ctx.close()
 
 
+DIST_STAGES = ["bgzf_index", "bgzf_inflate", "rec_walk", "dist_split", "dist_exchange", "input_pass", "sort_radix",
+               "sort_ties", "meta_gather", "dist_frags", "dist_join", "dist_pairs", "dist_reduce", "md_apply",
+               "gather_offsets", "gather_records", "bgzf_deflate"]
+
+
 def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
-    """N ranks: contig-sharded sort + dedup with the RCCL all-to-all (openge_amd/shard.py)."""
+    """N ranks, one process per GPU, RCCL over xGMI through the library's own communicator
+    (oge_comm_init_rank; torch.distributed only bootstraps it and times the steps, on gloo).  Rank g
+    holds one input BAM file in its HBM: the C2 data set's slots [n*g/N, n*(g+1)/N) behind the common
+    header, BGZF level 6 (mergesort's several input files, one per rank).  A step is the whole
+    `mergesort -M --nosplit` chain over the N files (oge_mergesort_bgzf_dist): inflate, record walk,
+    range-split exchange of the records, local sort, exact distributed dedup, and every rank deflating
+    its slice of the one output file.  Strong scaling: the 300M reads are split over the N ranks."""
+    import ctypes as C
     s0, s1 = n_all * rank // world, n_all * (rank + 1) // world
     n = s1 - s0
+    buf = C.create_string_buffer(1 << 16)
+    L.check(L.lib().oge_synth_finalize(C.byref(p)))
+    L.check(L.lib().oge_synth_header_text(C.byref(p), buf, 1 << 16, None))
+    hb = bam_header_bytes(buf.value.decode())
     d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
     ctx.synth_range_dev(p, s0, n, d_offs.data_ptr(), None)
     ctx.sync()
     B = int(d_offs[-1].item())
-    d_recs = torch.empty(B + 64, dtype=torch.uint8, device=dev)
-    ctx.synth_range_dev(p, s0, n, d_offs.data_ptr(), d_recs.data_ptr())
-    import ctypes as C
-    buf = C.create_string_buffer(1 << 16)
-    L.check(L.lib().oge_synth_header_text(C.byref(p), buf, 1 << 16, None))
-    opts, keep = L.markdup_opts_from_header(buf.value.decode(), p.n_ref)
-    ctx.sync()
-    from openge_amd import shard
-    backend = shard.HipBackend(ctx)
-    owners = shard.contig_owners([int(p.ref_len[i]) for i in range(p.n_ref)], world)
-    shard_t = {}
-
-    def step():
-        T = {}
-        out, off, k = shard.sort_markdup_sharded(backend, d_recs, d_offs, n, p.n_ref, owners, opts, timings=T)
-        for key, v in T.items():
-            shard_t[key] = shard_t.get(key, 0.0) + v
-        del out, off
-        return k
-
+    S = torch.empty(len(hb) + B + 64, dtype=torch.uint8, device=dev)
+    ctx.synth_range_dev(p, s0, n, d_offs.data_ptr(), S.data_ptr() + len(hb))
+    S[:len(hb)].copy_(torch.frombuffer(bytearray(hb), dtype=torch.uint8).to(dev))
+    del d_offs
+    Z, zb = build_input(ctx, L, torch, dev, S, len(hb) + B, args.level)
+    del S
+    d_z = torch.empty(zb + 28 + 64, dtype=torch.uint8, device=dev)
+    d_z[:zb].copy_(Z[:zb])
+    d_z[zb:zb + 28].copy_(torch.tensor(list(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")),
+                                       dtype=torch.uint8, device=dev))
+    zbytes = zb + 28
+    del Z
+    torch.cuda.empty_cache()
+    torch.cuda.synchronize(dev)
+    obj = [L.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    comm = L.comm_init_rank(ctx, world, rank, obj[0])
+    log(f"rank {rank}: {n} reads, input file {zbytes / 1e9:.2f} GB, transport {comm.transport}")
+    mopts = L.mergesort_opts(level=args.level, mark_duplicates=1)
+    step = lambda: comm.mergesort_bgzf_dist(d_z.data_ptr(), zbytes, mopts)
     for _ in range(args.warmup):
         step()
-    shard_t.clear()
-    dist.barrier()
     torch.cuda.synchronize(dev)
+    dist.barrier()
     t0 = time.perf_counter()
+    tot, nr, nd, ob = {}, 0, 0, 0
     for _ in range(args.steps):
-        step()
+        _, ob, nr, nd = step()
+        for s_, v in stage_ms(ctx, DIST_STAGES).items():
+            tot[s_] = tot.get(s_, 0.0) + v
     torch.cuda.synchronize(dev)
     dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    sizes = [None] * world
+    dist.all_gather_object(sizes, (n, ob))
+    assert nr == n_all, (nr, n_all)
+    comm.close()
+    del d_z
+    torch.cuda.empty_cache()
     realign_multi = None
     if not args.no_realign:
         realign_multi = realign_leg(ctx, args.realign_intervals, rank, world)
@@ -513,12 +538,16 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
         out = {"metric": METRIC, "value": round(n_all * K / dt / 1e6, 2), "unit": "Mreads/s", "n_gpus": world,
                "steps": K, "warmup": args.warmup, "ms_per_step": round(dt / K * 1e3, 2), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "u8",
-               "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234; records resident in HBM",
-               "config": {"workload": f"C2+C3 sort+dedup, {n_all // 1000000}M reads in total, {world} contig-sharded "
-                                      "ranks (records decoded in HBM)", "reads_total": n_all, "reads_rank0": n,
-                          "parallelism": f"{world} ranks: contig ownership + RCCL all-to-all + ghost mates"},
-               "shard_rank0_s_per_step": {k: (round(v / K, 4) if isinstance(v, float) else v // K)
-                                          for k, v in shard_t.items()}}
+               "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234, one level-6 BGZF input file per "
+                       "rank resident in its HBM",
+               "config": {"workload": f"C2+C3 end to end over {world} GPUs: {n_all // 1000000}M reads in {world} BAM "
+                                      "files -> mergesort -M --nosplit (range-split sort + exact distributed dedup) -> "
+                                      f"one BGZF level-{args.level} BAM file as {world} rank slices, in HBM",
+                          "reads_total": n_all, "duplicates_flagged": nd,
+                          "rank_reads_and_output_bytes": sizes,
+                          "parallelism": f"{world} ranks (one process per GPU), RCCL all-to-all over xGMI via "
+                                         "oge_comm_init_rank"},
+               "stages_ms_rank0": {k: round(v / K, 3) for k, v in tot.items()}}
         if realign_multi is not None:
             out["realign"] = realign_multi
         print(json.dumps(out), flush=True)
