@@ -1,0 +1,60 @@
+// gpu_chain_main.cpp -- `openge mergesort -M --nopg` as cmd/command_mergesort.cpp:68-117 wires it,
+// with the two GPU modules (gpu_modules.h) in place of ReadSorter and MarkDuplicates, the
+// reference's own FileReader in front, and at the end a sink writing through the reference's
+// BamSerializer<BgzfOutputStream> -- the serializer its FileWriter uses (alg/file_writer.cpp:144-166;
+// FileWriter itself needs the CMake-generated openge_constants.h, which this image cannot make).
+//   gpu_chain IN.bam OUT.bam [-R]
+#include <stdlib.h>
+#include <string.h>
+
+#include <iostream>
+
+#include "algorithms/file_reader.h"
+#include "gpu_modules.h"
+#include "util/bam_serializer.h"
+#include "util/bgzf_output_stream.h"
+#include "util/thread_pool.h"
+
+class BamFileSink : public AlgorithmModule {
+public:
+    std::string filename;
+protected:
+    virtual int runInternal() {
+        BamSerializer<BgzfOutputStream> w;
+        w.getOutputStream().setCompressionLevel(6);
+        if (!w.open(filename, getHeader())) {
+            std::cerr << "Error opening BAM file to write." << std::endl;
+            exit(-1);
+        }
+        for (OGERead *r; (r = getInputAlignment()) != NULL;) {
+            w.write(*r);
+            putOutputAlignment(r);
+        }
+        w.close();
+        return 0;
+    }
+};
+
+int main(int argc, char **argv) {
+    if (argc < 3) {
+        std::cerr << "usage: gpu_chain IN.bam OUT.bam [-R]" << std::endl;
+        return 2;
+    }
+    OGEParallelismSettings::setNumberThreads(8);  // as cmd/commands.cpp:67-84 sets up the pool
+    OGEParallelismSettings::enableMultithreading();
+    AlgorithmModule::setNothreads(false);
+    AlgorithmModule::setVerbose(false);
+    FileReader reader;
+    GpuReadSorter sorter;
+    GpuMarkDuplicates md;
+    BamFileSink sink;
+    reader.addFile(argv[1]);
+    sink.filename = argv[2];
+    md.removeDuplicates = argc > 3 && !strcmp(argv[3], "-R");
+    reader.addSink(&sorter);
+    sorter.addSink(&md);
+    md.addSink(&sink);
+    const int rc = reader.runChain();
+    std::cerr << "Marked " << md.duplicates << " records as duplicates." << std::endl;
+    return rc;
+}

@@ -17,7 +17,8 @@
 // no @PG line (the `--nopg` behaviour).  Global settings mirror
 // cmd/commands.cpp:67-84.
 //
-// It is never shipped and never runs on the GPU box.
+// It is never shipped; on the GPU box it runs only as bench.py's cpu_baseline (the reference's own
+// chain timed beside the GPU path).
 
 #include "algorithms/algorithm_module.h"
 #include "algorithms/file_reader.h"
