@@ -18,7 +18,7 @@ def test_gpu_modules_build_against_reference_headers(built):
     assert oracle.build_ref(), "reference objects (oracle/_ref) could not be built"
     r = subprocess.run(["make", "-f", str(ROOT / "integration" / "Makefile")], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
-    exe = ROOT / "integration" / "_build" / "gpu_chain"
+    exe = ROOT / "oracle" / "_ref" / "integration" / "gpu_chain"
     assert exe.exists()
     syms = subprocess.run(["nm", "-D", "--undefined-only", str(exe)], capture_output=True, text=True).stdout
     for s in ("oge_ctx_create", "oge_sort_coord", "oge_markdup", "oge_last_error"):
