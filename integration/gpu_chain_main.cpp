@@ -69,8 +69,9 @@ int main(int argc, char **argv) {
     md.addSink(&sink);
     const int rc = reader.runChain();
     std::cerr << "Marked " << md.duplicates << " records as duplicates." << std::endl;
-    // leave without static destructors: the reference's shared thread pool is a static whose workers
-    // are still parked at exit, and tearing it down under them aborted one run in four here
+    // leave without static destructors: one run aborted after this point ("double free or
+    // corruption" during teardown; the reference's shared thread pool is a static whose workers are
+    // still parked at exit), after the output was complete
     fflush(stdout);
     _exit(rc);
 }
