@@ -158,6 +158,23 @@ void oge_mergesort_opts_init(oge_mergesort_opts *o);
 int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *o,
                            const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup);
 
+/* ---- inputs larger than HBM (replaces ReadSorter's spilled runs + k-way merge) ---------- */
+/* Receives one output range: n records in HBM (d_off: n + 1 offsets from d_recs), valid during the
+ * call; ranges arrive in output order.  Non-zero return aborts the sort with that status. */
+typedef int (*oge_range_cb)(void *user, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n);
+/* mergesort [-M] of records in HOST memory of any size on one GPU (alg/read_sorter.cpp:48-190,
+ * util/read_stream_reader.h:132-153): sorted runs of <= chunk_bytes (0 = sized from free HBM) are
+ * written back over the input arena (h_recs is the spill space and holds the runs afterwards;
+ * h_off[0..n] is read-only), key ranges that fit HBM are cut from the runs and sorted on the device,
+ * and with opts != NULL the duplicate marks of the whole input are computed on a device-resident
+ * summary array first (64 B/read + ~140 B/read of scratch).  Output = oge_sort_markdup_dev's, handed
+ * to cb range by range.  *n_runs / *n_ranges (optional) report the cut. */
+int oge_sort_markdup_chunked(oge_ctx *ctx, uint8_t *h_recs, const uint64_t *h_off, uint64_t n, int32_t n_ref,
+                             const oge_markdup_opts *opts, uint64_t chunk_bytes, oge_range_cb cb, void *user,
+                             uint64_t *n_dup, uint64_t *n_runs, uint64_t *n_ranges);
+/* free / total bytes of the context's device memory */
+int oge_mem_info(oge_ctx *ctx, uint64_t *free_bytes, uint64_t *total_bytes);
+
 /* ---- multi-GPU sort + duplicate marking (replaces SplitByChromosome / SortedMerge) ------ */
 /* One rank per GPU.  The reference parallelises mergesort -M / dedup by routing refID % K to K
  * MarkDuplicates chains and re-merging them (alg/split_by_chromosome.cpp:30-58,

@@ -205,6 +205,16 @@ int oge_dev_free(oge_ctx *ctx, void *p) {
     return OGE_OK;
 }
 
+int oge_mem_info(oge_ctx *ctx, uint64_t *free_bytes, uint64_t *total_bytes) {
+    if (!ctx || !free_bytes || !total_bytes) return oge_fail(ctx, OGE_ERR_ARG, "oge_mem_info: null argument");
+    (void)hipSetDevice(ctx->device);
+    size_t f = 0, t = 0;
+    OGE_HIP_TRY(ctx, hipMemGetInfo(&f, &t));
+    *free_bytes = f;
+    *total_bytes = t;
+    return OGE_OK;
+}
+
 int oge_ctx_set_pool(oge_ctx *ctx, int enable) {
     if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
     hipSetDevice(ctx->device);

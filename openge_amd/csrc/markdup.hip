@@ -703,6 +703,26 @@ int oge_md_apply_desc(oge_ctx *ctx, const uint64_t *desc0, uint64_t n, uint8_t *
     return OGE_OK;
 }
 
+// 0x400 set / cleared in place on the primaries of n records (record k at recs + off[k], summary
+// meta[k], mark dup[k]); dup[k] becomes 1/0/2 as in oge_markdup.  *n_dup_out: records flagged.
+int oge_md_apply_inplace(oge_ctx *ctx, uint8_t *recs, const uint64_t *off, uint64_t n, const RecMeta *meta, uint8_t *dup,
+                         uint64_t *n_dup_out) {
+    unsigned long long *ndup = (unsigned long long *)ctx->ws("md_ndup", 8);
+    unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
+    if (!ndup || !cnt) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(ndup, 0, 8, ctx->stream));
+    if (n) {
+        hipLaunchKernelGGL(k_apply, dim3(std::min<uint32_t>(oge_ceil_div(n, kT), 2048u)), dim3(kT), 0, ctx->stream, recs, off, n, meta,
+                           dup, 1, 0, (const unsigned int *)(cnt + 1), ndup);
+        OGE_LAUNCH_CHECK(ctx);
+    }
+    unsigned long long h = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&h, ndup, 8, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *n_dup_out = h;
+    return OGE_OK;
+}
+
 // Everything after the per-record ReadEnds pass.  meta[i] describes record i of the stream
 // (record index = i); its bytes are at recs + meta[i].src (only read to confirm pair keys).
 // dup[i] receives 1/0/2 (see oge_markdup); with apply, FLAG 0x400 is rewritten in place at

@@ -39,6 +39,8 @@ int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t 
                       const OgeMdFrags &f, OgeMdPairs *p);
 int oge_md_pair_groups(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &p, uint8_t *dup);
 int oge_md_frag_groups(oge_ctx *ctx, uint64_t *fk, uint32_t *fv, uint64_t n, uint8_t *dup);
+int oge_md_apply_inplace(oge_ctx *ctx, uint8_t *recs, const uint64_t *off, uint64_t n, const RecMeta *meta, uint8_t *dup,
+                         uint64_t *n_dup_out);
 int oge_md_apply_desc(oge_ctx *ctx, const uint64_t *desc0, uint64_t n, uint8_t *dup, uint64_t *desc, uint64_t *n_dup_out);
 // hk (the chunk-key hash k_pair_build writes) and val = 0..np-1 for pairs received from other ranks
 int oge_md_pairs_rehash(oge_ctx *ctx, OgeMdPairs *p);

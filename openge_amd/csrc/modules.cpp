@@ -9,6 +9,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <functional>
 #include <atomic>
 #include <thread>
 
@@ -196,6 +197,10 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
     if (oge_bgzf_index(comp.data(), comp.size(), idx.data(), idx.data() + nb, idx.data() + 2 * nb, crc.data(), nb, &nb))
         return 1;  // not BGZF / truncated: the host reader reports it
     const uint64_t total = idx[3 * nb];
+    if (sink_sorts()) {  // larger than HBM (or the chunked test knob): the sorter works from host memory
+        uint64_t fr = 0, tot = 0;
+        if (getenv("OGE_CHUNK_BYTES") || (!oge_mem_info(cc.ctx, &fr, &tot) && total / 10 * 25 > fr)) return 1;
+    }
     const auto t1 = clk();
     void *dz = nullptr, *di = nullptr, *dc = nullptr, *dout = nullptr, *doff = nullptr;
     auto release = [&]() {
@@ -491,6 +496,17 @@ int Filter::runInternal(ChainContext &cc, ReadBatch &b) {
 }
 
 // ----------------------------------------------------------------------------------- ReadSorter
+// One GPU, and the chain's records (+ the sort's second arena and workspace) do not fit free HBM,
+// or OGE_CHUNK_BYTES forces the chunked path (tests).
+static bool use_chunked(ChainContext &cc, const ReadBatch &b) {
+    if (cc.gpus > 1) return false;
+    if (getenv("OGE_CHUNK_BYTES")) return true;
+    if (b.dev_valid) return false;  // the reader already holds them in HBM
+    uint64_t fr = 0, tot = 0;
+    if (oge_mem_info(cc.ctx, &fr, &tot)) return false;
+    return b.bytes() / 10 * 25 + b.n * 100 > fr;
+}
+
 int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
     if (order_ != BamHeaderModel::COORDINATE && order_ != BamHeaderModel::QUERYNAME) {
         fprintf(stderr, "openge: unsupported sort order\n");
@@ -508,6 +524,38 @@ int ReadSorter::runInternal(ChainContext &cc, ReadBatch &b) {
         if (verbose_)
             fprintf(stderr, "[openge] ReadSorter: %d ranks, %.3f s\n", cc.gpus,
                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        return 0;
+    }
+    if (order_ == BamHeaderModel::COORDINATE && use_chunked(cc, b)) {
+        // larger than HBM: sorted runs spilled into the host arena, key ranges sorted on the device,
+        // produced range by range when the writer asks (oge_sort_markdup_chunked)
+        if (cc.to_host(b)) return -1;
+        cc.free_device(b);
+        auto arena = std::make_shared<ReadBatch>();
+        arena->recs = std::move(b.recs);
+        arena->offs = std::move(b.offs);
+        auto mo = std::make_shared<MdOpts>();
+        if (md) markdup_opts(b, md->compatNonverbose, md->splitChains, *mo);
+        const char *ce = getenv("OGE_CHUNK_BYTES");
+        const uint64_t chunk = ce ? strtoull(ce, nullptr, 10) : 0, n = b.n;
+        const int32_t n_ref = (int32_t)b.ref_names.size();
+        b.produce = [arena, mo, md, chunk, n, n_ref](ChainContext &c, const ReadBatch::RangeSink &sink) -> int {
+            struct Tramp {
+                const ReadBatch::RangeSink *s;
+                static int call(void *u, const uint8_t *r, const uint64_t *o, uint64_t m) { return (*((Tramp *)u)->s)(r, o, m); }
+            } tr{&sink};
+            uint64_t nd = 0, runs = 0, ranges = 0;
+            const int rc = oge_sort_markdup_chunked(c.ctx, arena->recs.data(), arena->offs.data(), n, n_ref, md ? &mo->o : nullptr,
+                                                    chunk, &Tramp::call, &tr, &nd, &runs, &ranges);
+            if (rc) return c.fail("ReadSorter (chunked)");
+            if (md) md->duplicates = nd;
+            if (verbose_)
+                fprintf(stderr, "[openge] ReadSorter: %llu records in %llu sorted runs, output in %llu key ranges\n",
+                        (unsigned long long)n, (unsigned long long)runs, (unsigned long long)ranges);
+            return 0;
+        };
+        b.host_valid = false;
+        b.header.sort_order = order_;
         return 0;
     }
     const auto t0 = std::chrono::steady_clock::now();
@@ -878,14 +926,67 @@ int FileWriter::write_slices(ChainContext &cc, ReadBatch &b, BgzfWriter &w) {
     return ret;
 }
 
+// Inputs larger than HBM: every output range the sorter produces is (with -r / -R) compacted, BGZF
+// compressed on the device and written before the next range is made.
+int FileWriter::write_ranges(ChainContext &cc, ReadBatch &b, BgzfWriter &w) {
+    w.write_compressed(nullptr, 0);  // the header's blocks first
+    const int level = std::max(0, std::min(9, level_));
+    const bool drop = b.drop_duplicates;
+    struct Buf {
+        oge_ctx *c;
+        void *p = nullptr;
+        uint64_t cap = 0;
+        bool host = false;
+        int need(uint64_t bytes) {
+            if (bytes <= cap) return 0;
+            if (p) host ? oge_host_free(c, p) : oge_dev_free(c, p);
+            p = nullptr;
+            cap = 0;
+            const int rc = host ? oge_host_alloc(c, bytes, &p) : oge_dev_alloc(c, bytes, &p);
+            if (!rc) cap = bytes;
+            return rc;
+        }
+        ~Buf() {
+            if (p) host ? oge_host_free(c, p) : oge_dev_free(c, p);
+        }
+    } kept{cc.ctx}, kept_off{cc.ctx}, dz{cc.ctx}, hz{cc.ctx};
+    hz.host = true;
+    auto sink = [&](const uint8_t *recs, const uint64_t *offs, uint64_t n) -> int {
+        uint64_t ends[2] = {0, 0};
+        if (n && (oge_memcpy(cc.ctx, &ends[0], offs, 8, 2) || oge_memcpy(cc.ctx, &ends[1], offs + n, 8, 2))) return -1;
+        if (drop && n) {
+            uint64_t m = 0;
+            if (kept.need(ends[1] + 64) || kept_off.need((n + 1) * 8) ||
+                oge_drop_flagged_dev(cc.ctx, recs, offs, n, OGE_F_DUP, (uint8_t *)kept.p, (uint64_t *)kept_off.p, &m))
+                return -1;
+            recs = (const uint8_t *)kept.p;
+            offs = (const uint64_t *)kept_off.p;
+            n = m;
+            ends[0] = ends[1] = 0;
+            if (n && (oge_memcpy(cc.ctx, &ends[0], offs, 8, 2) || oge_memcpy(cc.ctx, &ends[1], offs + n, 8, 2))) return -1;
+        }
+        const uint64_t len = ends[1] - ends[0];
+        if (!len) return 0;
+        const uint64_t cap = oge_bgzf_bound(len);
+        uint64_t zb = 0;
+        if (dz.need(cap) || oge_bgzf_deflate_dev(cc.ctx, recs + ends[0], len, level, (uint8_t *)dz.p, cap, &zb) || hz.need(zb) ||
+            oge_memcpy(cc.ctx, hz.p, dz.p, zb, 2))
+            return -1;
+        w.write_compressed((const uint8_t *)hz.p, zb);
+        return 0;
+    };
+    if (b.produce(cc, sink)) return -1;
+    return 0;
+}
+
 int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
     auto clk = [] { return std::chrono::steady_clock::now(); };
     auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
         return std::chrono::duration<double>(z - a).count();
     };
     const auto t0 = clk();
-    const bool sliced = !b.slices.empty();
-    const bool on_device = sliced || (b.dev_valid && !b.host_valid && !bgzf_host_codec_forced());
+    const bool sliced = !b.slices.empty(), produced = (bool)b.produce;
+    const bool on_device = sliced || produced || (b.dev_valid && !b.host_valid && !bgzf_host_codec_forced());
     double t_dev = 0, t_d2h = 0, t_wait = 0;
     if (!on_device && cc.to_host(b)) return -1;
     const auto t1 = clk();
@@ -904,7 +1005,7 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
         std::vector<uint8_t> hb = bam_encode_header(h);
         w.write(hb.data(), hb.size());
         if (on_device) {
-            if (sliced ? write_slices(cc, b, w) : write_device(cc, b, w, &t_dev, &t_d2h, &t_wait)) {
+            if (produced ? write_ranges(cc, b, w) : sliced ? write_slices(cc, b, w) : write_device(cc, b, w, &t_dev, &t_d2h, &t_wait)) {
                 w.abandon();  // no EOF block and no write into the FILE closed below
                 if (f != stdout) fclose(f);
                 return -1;

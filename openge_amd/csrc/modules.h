@@ -9,6 +9,7 @@
 // link against, and it contains no HIP code of its own.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -16,6 +17,8 @@
 #include "bamio.h"
 
 namespace oge {
+
+struct ChainContext;
 
 // Records of one chain, resident in host memory, HBM, or both.
 struct ReadBatch {
@@ -42,6 +45,10 @@ struct ReadBatch {
         uint64_t n;
     };
     std::vector<Slice> slices;
+    // inputs larger than HBM: the output is produced range by range when the writer asks for it
+    // (oge_sort_markdup_chunked); each range is handed to `sink` in output order
+    using RangeSink = std::function<int(const uint8_t *d_recs, const uint64_t *d_offs, uint64_t n)>;
+    std::function<int(ChainContext &, const RangeSink &)> produce;
 
     uint64_t bytes() const { return host_valid ? offs[n] : d_bytes; }
 };
@@ -186,6 +193,7 @@ public:
     void setCompressionLevel(int l) { level_ = l; }
     int write_device(ChainContext &cc, ReadBatch &b, BgzfWriter &w, double *t_dev, double *t_d2h, double *t_wait);
     int write_slices(ChainContext &cc, ReadBatch &b, BgzfWriter &w);
+    int write_ranges(ChainContext &cc, ReadBatch &b, BgzfWriter &w);
     void addProgramLine(const std::string &cl) { program_line_ = cl; }
     int setFormat(const std::string &f);  // only "bam" is supported (SAM/FASTQ out of scope)
 protected:

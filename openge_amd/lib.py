@@ -211,6 +211,10 @@ def lib() -> C.CDLL:
         "oge_bam_markdup_opts": (C.c_int, [vp, vp, C.POINTER(vp), C.POINTER(vp)]),
         "oge_bam_write": (C.c_int, [C.c_char_p, C.c_char_p, u64, C.c_int, vp, vp, u64, vp, vp, C.c_int, C.c_int]),
         "oge_realign_scan": (C.c_int, [vp, vp, vp, vp]),
+        "oge_sort_markdup_chunked": (C.c_int, [vp, vp, vp, u64, i32, vp, u64, vp, vp, C.POINTER(u64), C.POINTER(u64),
+                                               C.POINTER(u64)]),
+        "oge_mem_info": (C.c_int, [vp, C.POINTER(u64), C.POINTER(u64)]),
+        "oge_device_count": (C.c_int, []),
         "oge_comm_unique_id_bytes": (u64, []),
         "oge_comm_unique_id": (C.c_int, [vp, u64]),
         "oge_comm_init_rank": (C.c_int, [vp, C.c_int, C.c_int, vp, C.POINTER(vp)]),
@@ -671,3 +675,34 @@ def comm_init_rank(ctx: "Context", nranks: int, rank: int, uid: bytes) -> Comm:
     h = C.c_void_p()
     check(lib().oge_comm_init_rank(ctx.h, nranks, rank, uid, C.byref(h)), ctx.h)
     return Comm(h, ctx)
+
+
+RANGE_CB = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
+
+
+def sort_markdup_chunked(ctx: "Context", recs: np.ndarray, offs: np.ndarray, n: int, n_ref: int,
+                         opts: "MarkdupOpts | None", chunk_bytes: int = 0):
+    """Out-of-core mergesort [-M] of host records (oge_sort_markdup_chunked).  `recs` is used as the
+    spill space (it holds the sorted runs afterwards).  Returns (output record stream bytes,
+    duplicates, runs, ranges)."""
+    parts = []
+
+    def on_range(user, d_recs, d_off, m):
+        try:
+            oo = np.empty(m + 1, np.uint64)
+            check(lib().oge_memcpy(ctx.h, oo.ctypes.data, d_off, 8 * (m + 1), 2), ctx.h)
+            b = np.empty(int(oo[m] - oo[0]), np.uint8)
+            if b.size:
+                check(lib().oge_memcpy(ctx.h, b.ctypes.data, d_recs + int(oo[0]), b.size, 2), ctx.h)
+            parts.append(b.tobytes())
+            return 0
+        except Exception:  # noqa: BLE001
+            return -1
+
+    cb = RANGE_CB(on_range)
+    nd, nr, ng = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    check(lib().oge_sort_markdup_chunked(ctx.h, recs.ctypes.data, offs.ctypes.data, n, n_ref,
+                                         C.byref(opts) if opts is not None else None, chunk_bytes, cb, None,
+                                         C.byref(nd), C.byref(nr), C.byref(ng)), ctx.h)
+    return b"".join(parts), nd.value, nr.value, ng.value

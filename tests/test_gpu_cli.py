@@ -206,3 +206,29 @@ def test_cli_localrealign_gpus_matches_reference(name, tmp_path):
     oh, _, orecs, ooffs = bamutil.read_bam(tmp_path / "rl.bam")
     assert oh == meta["output_header"]
     check_output(meta, arrays, orecs, np.append(ooffs, np.uint64(len(orecs))))
+
+
+def test_cli_chunked_matches_reference(case, tmp_path):
+    """Inputs larger than HBM take the chunked path (sorted runs spilled into host memory, key ranges
+    sorted and written one by one); OGE_CHUNK_BYTES forces it with tiny chunks: the reference's
+    mergesort -M / sort / -R outputs."""
+    import os
+    src = case_input(case, tmp_path)
+    env = dict(os.environ, OGE_CHUNK_BYTES="200000")
+    r = subprocess.run([OPENGE, "mergesort", "-M", "--nopg", "-v", str(src), "-o", str(tmp_path / "o.bam")],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert "sorted runs" in r.stderr
+    h, m, t = digests(tmp_path / "o.bam")
+    g = case.meta["sortdedup_v"]
+    assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
+    r = subprocess.run([OPENGE, "sort", "--nopg", str(src), "-o", str(tmp_path / "s.bam")], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    h, m, t = digests(tmp_path / "s.bam")
+    assert h == case.meta["sorted_header"] and m == case.meta["sort"]["mapped_sha256"]
+    r = subprocess.run([OPENGE, "mergesort", "-R", "--nopg", str(src), "-o", str(tmp_path / "r.bam")], capture_output=True,
+                       text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    _, _, recs, offs = bamutil.read_bam(tmp_path / "r.bam")
+    assert len(offs) == case.n - case.meta["sortdedup_v"]["n_dup"]
