@@ -30,6 +30,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "bam_layout.h"
@@ -97,9 +98,12 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
                                                     const uint32_t *__restrict__ zpow, uint32_t *__restrict__ tok,
                                                     uint8_t *__restrict__ ntok, uint32_t *__restrict__ freq_out,
                                                     uint32_t *__restrict__ crc_out) {
-    __shared__ uint32_t in[kPay / 4 + 4];
+    // padded layouts (bgzf_dev.h pw): every thread's 64-byte segment of `in` and its 64 candidates
+    // start in distinct banks for the greedy parse
+    constexpr int PS = 4;
+    __shared__ uint32_t in[kPay / 4 + 4 + (kPay / 4 + 4) / 16 + 1];
     __shared__ uint32_t htab[1 << kHashBits];
-    __shared__ uint16_t cand[kSub];
+    __shared__ uint16_t cand[kSub + 2 * (kSub / 64)];
     __shared__ uint32_t freq[kFreq];
     __shared__ uint32_t crctab[4][256];
     __shared__ uint32_t zp[17][32];
@@ -110,13 +114,14 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
     const uint32_t len = (uint32_t)min<uint64_t>(kPay, n - start);
     const uint8_t *s = src + start;
 
-    stage_words<kT>(in, s, len, t);
+    stage_words<kT, PS>(in, s, len, t);
+    auto cix = [](uint32_t q) { return q + 2 * (q >> 6); };  // candidate q of the sub-block
     for (int i = t; i < (1 << kHashBits); i += kT) htab[i] = 0;
     for (int i = t; i < kFreq; i += kT) freq[i] = 0;
     crc_setup<kT>(crctab, zp, zpow, t);
     __syncthreads();
     {
-        const uint32_t c = crc_window512(in, len, crctab, zp, crcs, t);
+        const uint32_t c = crc_window512<PS>(in, len, crctab, zp, crcs, t);
         if (t == 0) crc_out[blockIdx.x] = c;
     }
 
@@ -133,12 +138,12 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
             uint32_t h = 0, c = 0;
             const bool ok = p + 4 <= len;
             if (ok) {
-                const uint32_t w = ld32(in, p);
+                const uint32_t w = ld32p<PS>(in, p);
                 h = hash4(w);
                 const uint32_t j1 = htab[h];
-                if (j1 && p - (j1 - 1) <= 32768 && ld32(in, j1 - 1) == w) c = j1;
+                if (j1 && p - (j1 - 1) <= 32768 && ld32p<PS>(in, j1 - 1) == w) c = j1;
             }
-            if (p < end) cand[p - base] = (uint16_t)c;
+            if (p < end) cand[cix(p - base)] = (uint16_t)c;
             __syncthreads();
             if (ok) atomicMax(&htab[h], p + 1);
             __syncthreads();
@@ -148,14 +153,14 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
         uint32_t k = 0;
         uint32_t *tp = tok + ((uint64_t)blockIdx.x * kNSub + sub) * kSeg * kT + t;
         for (uint32_t p = s0; p < s1;) {
-            const uint32_t c = p < s1 ? cand[p - base] : 0;
+            const uint32_t c = p < s1 ? cand[cix(p - base)] : 0;
             uint32_t L = 0;
             if (c) {
                 const uint32_t j = c - 1;
                 const uint32_t maxL = min(258u, s1 - p);
                 L = min(4u, maxL);
                 while (L < maxL) {
-                    const uint32_t x = ld32(in, p + L) ^ ld32(in, j + L);
+                    const uint32_t x = ld32p<PS>(in, p + L) ^ ld32p<PS>(in, j + L);
                     if (x == 0) {
                         L += 4;
                     } else {
@@ -176,7 +181,7 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
                 atomicAdd(&freq[kLit + sym], 1u);
                 p += L;
             } else {
-                const uint32_t b = (in[p >> 2] >> (8 * (p & 3))) & 0xff;
+                const uint32_t b = byte_at<PS>(in, p);
                 tokv = b;
                 atomicAdd(&freq[b], 1u);
                 p += 1;
@@ -612,6 +617,34 @@ __global__ void __launch_bounds__(256) k_defl_compact(const uint8_t *__restrict_
     for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) d[i] = s[i];
 }
 
+// exclusive scan of n <= 2048 block sizes, one 1024-thread workgroup (the per-chunk offsets; runs on
+// the chunk's own stream)
+__global__ void __launch_bounds__(1024) k_scan2048(const uint32_t *__restrict__ in, uint32_t n, uint32_t *__restrict__ out) {
+    __shared__ uint32_t ws[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t a = 2 * t < n ? in[2 * t] : 0u, b = 2 * t + 1 < n ? in[2 * t + 1] : 0u;
+    uint32_t v = a + b, x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) ws[w] = x;
+    __syncthreads();
+    if (t < 16) {
+        uint32_t s = ws[t], z = s;
+        for (int d = 1; d < 16; d <<= 1) {
+            const uint32_t y = __shfl_up(z, d, 16);
+            if ((t & 15) >= (uint32_t)d) z += y;
+        }
+        ws[t] = z - s;
+    }
+    __syncthreads();
+    const uint32_t excl = ws[w] + x - v;
+    if (2 * t < n) out[2 * t] = excl;
+    if (2 * t + 1 < n) out[2 * t + 1] = excl + a;
+}
+
 __global__ void k_defl_advance(uint64_t *base, const uint32_t *offs, const uint32_t *sizes, uint32_t nb) {
     if (threadIdx.x == 0 && blockIdx.x == 0) *base += (uint64_t)offs[nb - 1] + sizes[nb - 1];
 }
@@ -641,38 +674,72 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     if (!n) return OGE_OK;
     const uint64_t nblk = (n + kPay - 1) / kPay;
     const uint64_t chunk = std::min<uint64_t>(nblk, 2048);
-    uint32_t *tok = (uint32_t *)ctx->ws("defl_tok", chunk * kNSub * kSeg * kT * 4);
-    uint8_t *ntok = (uint8_t *)ctx->ws("defl_ntok", chunk * kNSeg);
-    uint32_t *freq = (uint32_t *)ctx->ws("defl_freq", chunk * kFreq * 4);
-    DeflTab *tabs = (DeflTab *)ctx->ws("defl_tabs", chunk * sizeof(DeflTab));
-    uint8_t *slots = (uint8_t *)ctx->ws("defl_slots", chunk * kSlot);
-    uint32_t *sizes = (uint32_t *)ctx->ws("defl_sizes", chunk * 4 + 16);
-    uint32_t *offs = (uint32_t *)ctx->ws("defl_offs", chunk * 4 + 16);
+    // Chunks go round-robin over S streams: one chunk's Huffman and emit kernels (small LDS) run on
+    // the CUs beside another chunk's tokens workgroups (153 KiB of LDS, one per CU); only the
+    // compaction, which advances the running output offset, is ordered chunk after chunk (events).
+    const int S = nblk > chunk ? 3 : 1;
+    struct Bufs {
+        uint32_t *tok, *freq, *sizes, *offs, *crc;
+        uint8_t *ntok, *slots;
+        DeflTab *tabs;
+        hipStream_t st;
+    } B[3];
+    for (int s = 0; s < S; ++s) {
+        const std::string x = std::to_string(s);
+        B[s].tok = (uint32_t *)ctx->ws(("defl_tok" + x).c_str(), chunk * kNSub * kSeg * kT * 4);
+        B[s].ntok = (uint8_t *)ctx->ws(("defl_ntok" + x).c_str(), chunk * kNSeg);
+        B[s].freq = (uint32_t *)ctx->ws(("defl_freq" + x).c_str(), chunk * kFreq * 4);
+        B[s].tabs = (DeflTab *)ctx->ws(("defl_tabs" + x).c_str(), chunk * sizeof(DeflTab));
+        B[s].slots = (uint8_t *)ctx->ws(("defl_slots" + x).c_str(), chunk * kSlot);
+        B[s].sizes = (uint32_t *)ctx->ws(("defl_sizes" + x).c_str(), chunk * 4 + 16);
+        B[s].offs = (uint32_t *)ctx->ws(("defl_offs" + x).c_str(), chunk * 4 + 16);
+        B[s].crc = (uint32_t *)ctx->ws(("defl_crc" + x).c_str(), chunk * 4 + 16);
+        B[s].st = S == 1 ? ctx->stream : ctx->side_stream(s);
+        if (!B[s].tok || !B[s].ntok || !B[s].freq || !B[s].tabs || !B[s].slots || !B[s].sizes || !B[s].offs || !B[s].crc ||
+            !B[s].st)
+            return OGE_ERR_HIP;
+    }
     uint32_t *zpow = (uint32_t *)ctx->ws("defl_zpow", 17 * 32 * 4);
     uint64_t *base = (uint64_t *)ctx->ws("defl_base", 16);
-    uint32_t *crc = (uint32_t *)ctx->ws("defl_crc", chunk * 4 + 16);
-    if (!tok || !ntok || !freq || !tabs || !slots || !sizes || !offs || !zpow || !base || !crc) return OGE_ERR_HIP;
+    if (!zpow || !base) return OGE_ERR_HIP;
     static uint32_t z[17][32];
     static bool zinit = false;
     if (!zinit) crc_zpow(z), zinit = true;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, z, sizeof(z), hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(base, 0, 8, ctx->stream));
     OgeStageTimer *tm = ctx->begin_stage("bgzf_deflate");
-    for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
+    hipEvent_t ev[4];
+    for (auto &e : ev) OGE_HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    struct Evs {
+        hipEvent_t *e;
+        ~Evs() {
+            for (int i = 0; i < 4; ++i) hipEventDestroy(e[i]);
+        }
+    } evs{ev};
+    OGE_HIP_TRY(ctx, hipEventRecord(ev[3], ctx->stream));  // inputs ready for the side streams
+    for (int s = 0; s < S; ++s)
+        if (B[s].st != ctx->stream) OGE_HIP_TRY(ctx, hipStreamWaitEvent(B[s].st, ev[3], 0));
+    uint64_t k = 0;
+    for (uint64_t b0 = 0; b0 < nblk; b0 += chunk, ++k) {
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
-        k_defl_tokens<<<nb, kT, 0, ctx->stream>>>(d_src, n, b0, zpow, tok, ntok, freq, crc);
+        Bufs &u = B[k % S];
+        k_defl_tokens<<<nb, kT, 0, u.st>>>(d_src, n, b0, zpow, u.tok, u.ntok, u.freq, u.crc);
         OGE_LAUNCH_CHECK(ctx);
-        k_defl_huff<<<nb, 64, 0, ctx->stream>>>(freq, tabs);
+        k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs);
         OGE_LAUNCH_CHECK(ctx);
-        k_defl_emit<<<nb, kT, 0, ctx->stream>>>(d_src, n, b0, level, tok, ntok, tabs, crc, slots, sizes);
+        k_defl_emit<<<nb, kT, 0, u.st>>>(d_src, n, b0, level, u.tok, u.ntok, u.tabs, u.crc, u.slots, u.sizes);
         OGE_LAUNCH_CHECK(ctx);
-        int rc = oge_exclusive_scan_u32(ctx, sizes, offs, nb);
-        if (rc) return rc;
-        k_defl_compact<<<nb, 256, 0, ctx->stream>>>(slots, sizes, offs, base, d_dst);
+        k_scan2048<<<1, 1024, 0, u.st>>>(u.sizes, nb, u.offs);
         OGE_LAUNCH_CHECK(ctx);
-        k_defl_advance<<<1, 64, 0, ctx->stream>>>(base, offs, sizes, nb);
+        if (k) OGE_HIP_TRY(ctx, hipStreamWaitEvent(u.st, ev[(k - 1) % S], 0));  // previous chunk's offset advance
+        k_defl_compact<<<nb, 256, 0, u.st>>>(u.slots, u.sizes, u.offs, base, d_dst);
         OGE_LAUNCH_CHECK(ctx);
+        k_defl_advance<<<1, 64, 0, u.st>>>(base, u.offs, u.sizes, nb);
+        OGE_LAUNCH_CHECK(ctx);
+        OGE_HIP_TRY(ctx, hipEventRecord(ev[k % S], u.st));
     }
+    // the last chunk's advance follows every earlier compaction: the context stream waits for it
+    if (S > 1) OGE_HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[(k - 1) % S], 0));
     ctx->end_stage(tm);
     uint64_t total = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&total, base, 8, hipMemcpyDeviceToHost, ctx->stream));

@@ -15,6 +15,22 @@ __device__ __forceinline__ uint32_t ld32(const uint32_t *w, uint32_t p) {  // un
     return __builtin_amdgcn_alignbyte(b, a, p & 3);
 }
 
+// Padded LDS byte layouts: one spare word after every 2^PS words, so word w lives at w + (w >> PS).
+// Threads that each walk their own 2^PS-word (or 2^(PS+1)-word) piece then start in different banks
+// (a 64- or 128-byte stride otherwise puts a wave's 64 lanes on 2-4 banks).  PS = 31: no padding.
+template <int PS>
+__device__ __forceinline__ uint32_t pw(uint32_t w) { return PS >= 31 ? w : w + (w >> PS); }
+template <int PS>
+__device__ __forceinline__ uint32_t ld32p(const uint32_t *in, uint32_t p) {
+    const uint32_t w = p >> 2, a = in[pw<PS>(w)];
+    if (!(p & 3)) return a;
+    return __builtin_amdgcn_alignbyte(in[pw<PS>(w + 1)], a, p & 3);
+}
+template <int PS>
+__device__ __forceinline__ uint32_t byte_at(const uint32_t *in, uint32_t p) {
+    return (in[pw<PS>(p >> 2)] >> (8 * (p & 3))) & 0xff;
+}
+
 __device__ __forceinline__ uint32_t crc_mat(const uint32_t *M, uint32_t c) {  // GF(2) matrix x vector
     uint32_t r = 0;
 #pragma unroll
@@ -24,7 +40,7 @@ __device__ __forceinline__ uint32_t crc_mat(const uint32_t *M, uint32_t c) {  //
 
 // Stage len bytes at s (any alignment) into LDS words in[0 .. (len+3)/4 + 4), zero padded.
 // Aligned dword loads, funnel-shifted, U loads in flight per thread.
-template <int NT>
+template <int NT, int PS = 31>
 __device__ void stage_words(uint32_t *in, const uint8_t *s, uint32_t len, int t) {
     const uintptr_t a = (uintptr_t)s & ~(uintptr_t)3;
     const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
@@ -43,7 +59,7 @@ __device__ void stage_words(uint32_t *in, const uint8_t *s, uint32_t len, int t)
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const uint32_t k = k0 + j * NT;
-            if (k < safe) in[k] = sh ? __builtin_amdgcn_alignbyte(hi[j], lo[j], sh) : lo[j];
+            if (k < safe) in[pw<PS>(k)] = sh ? __builtin_amdgcn_alignbyte(hi[j], lo[j], sh) : lo[j];
         }
     }
     for (uint32_t k = safe + t; k < nw + 4; k += NT) {
@@ -51,7 +67,7 @@ __device__ void stage_words(uint32_t *in, const uint8_t *s, uint32_t len, int t)
         if (k < nw)
             for (int b = 0; b < 4; ++b)
                 if (4 * k + b < len) v |= (uint32_t)s[4 * k + b] << (8 * b);
-        in[k] = v;
+        in[pw<PS>(k)] = v;
     }
 }
 
@@ -74,6 +90,7 @@ __device__ void crc_setup(uint32_t (*crctab)[256], uint32_t (*zp)[32], const uin
 // The data is right-aligned in a 65536-byte window (leading zeros leave a zero register unchanged);
 // thread t owns window bytes [128t, 128t + 128); pairs of pieces are combined with
 // crc(A || B) = Z_|B|(crc A) ^ crc B, and the whole with the 0xffffffff preset.
+template <int PS = 31>
 __device__ uint32_t crc_window512(const uint32_t *in, uint32_t len, const uint32_t (*crctab)[256], const uint32_t (*zp)[32],
                                   uint32_t *crcs, int t) {
     const uint32_t lead = kSlot - len, w0 = t * 128u;
@@ -82,11 +99,11 @@ __device__ uint32_t crc_window512(const uint32_t *in, uint32_t len, const uint32
         const uint32_t d0 = w0 - lead;
 #pragma unroll 4
         for (int i = 0; i < 32; ++i) {
-            c ^= ld32(in, d0 + 4 * i);
+            c ^= ld32p<PS>(in, d0 + 4 * i);
             c = crctab[3][c & 0xff] ^ crctab[2][(c >> 8) & 0xff] ^ crctab[1][(c >> 16) & 0xff] ^ crctab[0][c >> 24];
         }
     } else if (w0 + 128 > lead) {
-        for (uint32_t d = 0; d < w0 + 128 - lead; ++d) c = crctab[0][(c ^ (in[d >> 2] >> (8 * (d & 3)))) & 0xff] ^ (c >> 8);
+        for (uint32_t d = 0; d < w0 + 128 - lead; ++d) c = crctab[0][(c ^ byte_at<PS>(in, d)) & 0xff] ^ (c >> 8);
     }
     crcs[t] = c;
     __syncthreads();

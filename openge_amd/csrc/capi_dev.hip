@@ -74,6 +74,11 @@ void *oge_ctx::ws(const char *name, size_t bytes) {
     return b.p;
 }
 
+hipStream_t oge_ctx::side_stream(int i) {
+    if (!side[i] && hipStreamCreateWithFlags(&side[i], hipStreamNonBlocking) != hipSuccess) side[i] = nullptr;
+    return side[i];
+}
+
 void *oge_ctx::scratch(const char *name, size_t bytes) {
     const size_t a = (loan_used + 255) & ~(size_t)255;
     if (loan_base && a + bytes + 64 <= loan_cap) {
@@ -170,6 +175,8 @@ void oge_ctx_destroy(oge_ctx *ctx) {
         hipEventDestroy(t.start);
         hipEventDestroy(t.stop);
     }
+    for (hipStream_t s : ctx->side)
+        if (s) hipStreamDestroy(s);
     if (ctx->own_stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }

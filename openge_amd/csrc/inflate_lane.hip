@@ -181,7 +181,8 @@ __device__ bool wbuild(P1Lds &S, uint32_t j, uint8_t *list, const uint32_t (&len
 }
 
 // ---------------------------------------------------------------------------- phase 1
-__global__ void __launch_bounds__(64, 3) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
+template <int WPS>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
+__global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
                                                      const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
                                                      const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
                                                      uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
@@ -643,7 +644,12 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         rf[4 * k] = v.x, rf[4 * k + 1] = v.y, rf[4 * k + 2] = v.z, rf[4 * k + 3] = v.w;
     }
     __syncthreads();
+    // the image is padded (bgzf_dev.h pw<5>: a spare word per 128 bytes) so the CRC's 128-byte pieces,
+    // one per thread, start in distinct banks; byte q lives at ib(q)
+    constexpr int PS = 5;
     uint8_t *img = (uint8_t *)refs;
+    uint32_t *img32 = (uint32_t *)refs;
+    auto ib = [](uint32_t q) { return q + ((q >> 7) << 2); };
     {
         const uint32_t sh = (uint32_t)((uintptr_t)O & 3);
         const uint32_t *W = (const uint32_t *)((uintptr_t)O & ~(uintptr_t)3);
@@ -654,7 +660,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
             const uint32_t w = 512 * k + t;
             if (w >= nd) break;
             const uint32_t a0 = W[w], a1 = (uintptr_t)(W + w + 1) < lim ? W[w + 1] : 0u;
-            *(uint32_t *)(img + 4 * w) = sh ? __builtin_amdgcn_alignbyte(a1, a0, sh) : a0;
+            img32[pw<PS>(w)] = sh ? __builtin_amdgcn_alignbyte(a1, a0, sh) : a0;
         }
     }
     __syncthreads();
@@ -665,16 +671,22 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         uint32_t r[8];
 #pragma unroll
         for (int i = 0; i < 4; ++i) r[2 * i] = min(rf[4 * k + i] & 0xffff, last), r[2 * i + 1] = min(rf[4 * k + i] >> 16, last);
-        wv[2 * k] = (uint32_t)img[r[0]] | ((uint32_t)img[r[1]] << 8) | ((uint32_t)img[r[2]] << 16) | ((uint32_t)img[r[3]] << 24);
-        wv[2 * k + 1] = (uint32_t)img[r[4]] | ((uint32_t)img[r[5]] << 8) | ((uint32_t)img[r[6]] << 16) | ((uint32_t)img[r[7]] << 24);
+        wv[2 * k] = (uint32_t)img[ib(r[0])] | ((uint32_t)img[ib(r[1])] << 8) | ((uint32_t)img[ib(r[2])] << 16) |
+                    ((uint32_t)img[ib(r[3])] << 24);
+        wv[2 * k + 1] = (uint32_t)img[ib(r[4])] | ((uint32_t)img[ib(r[5])] << 8) | ((uint32_t)img[ib(r[6])] << 16) |
+                        ((uint32_t)img[ib(r[7])] << 24);
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; ++k) *(uint2 *)(img + 8 * (512 * k + t)) = make_uint2(wv[2 * k], wv[2 * k + 1]);
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t w = 2 * (512 * k + t);  // w, w + 1: same 32-word group
+        img32[pw<PS>(w)] = wv[2 * k];
+        img32[pw<PS>(w) + 1] = wv[2 * k + 1];
+    }
     __syncthreads();
-    // 7. CRC (crc_window512's layout: byte q at img + q) and the write-out at the block's alignment
+    // 7. CRC and the write-out at the block's alignment
     if (crc) {
-        const uint32_t c = crc_window512((const uint32_t *)img, osz, crctab, zp, crcs, t);
+        const uint32_t c = crc_window512<PS>(img32, osz, crctab, zp, crcs, t);
         if (t == 0 && c != crc[b]) report(err, E_CRC, b);
     }
     const uint32_t sh = (uint32_t)((uintptr_t)O & 3);
@@ -683,11 +695,11 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     for (uint32_t g = t; g < nwords; g += kT2) {
         const int32_t r0 = (int32_t)(4 * g) - (int32_t)sh;  // relative position of the word's first byte
         if (r0 >= 0 && r0 + 4 <= (int32_t)osz) {
-            A[g] = ld32((const uint32_t *)img, (uint32_t)r0);
+            A[g] = ld32p<PS>(img32, (uint32_t)r0);
         } else {
             for (int i = 0; i < 4; ++i) {
                 const int32_t r = r0 + i;
-                if (r >= 0 && r < (int32_t)osz) ((uint8_t *)(A + g))[i] = img[r];
+                if (r >= 0 && r < (int32_t)osz) ((uint8_t *)(A + g))[i] = img[ib((uint32_t)r)];
             }
         }
     }
@@ -708,7 +720,12 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     }();
     // one block per lane per launch: a launch fills the 12 resident waves per CU once (a second, partial
     // round of waves would run at a fraction of the occupancy); chunks are balanced
-    const uint64_t lanes = (uint64_t)ncu * 12 * 64;
+    // OGE_INFL_WAVES=4: the 128-VGPR build (16 workgroups per CU, 10 KiB of LDS each) instead of 12
+    static const int wps = [] {
+        const char *e = getenv("OGE_INFL_WAVES");
+        return (e && atoi(e) == 4) ? 4 : 3;
+    }();
+    const uint64_t lanes = (uint64_t)ncu * 4 * wps * 64;
     const uint64_t nchunks = std::max<uint64_t>(1, (nblk + lanes - 1) / lanes);
     const uint64_t chunk = std::max<uint64_t>(1, (nblk + nchunks - 1) / nchunks);
     const uint64_t wgs = (chunk + 63) / 64;
@@ -718,7 +735,8 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
         const uint64_t nb = std::min(chunk, nblk - b0);
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
-        k_infl_huff<<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        if (wps == 4) k_infl_huff<4><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else k_infl_huff<3><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         OGE_LAUNCH_CHECK(ctx);
         k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, b0, zpow, err);
         OGE_LAUNCH_CHECK(ctx);

@@ -29,6 +29,8 @@ struct oge_ctx {
     bool timing = true;
     int timing_hold = 0;  // > 0: a composite entry point (the pipeline) keeps its sub-calls' stage events
     bool pool = false;  // allocate from the device's stream-ordered pool and keep freed memory in it
+    hipStream_t side[4] = {nullptr, nullptr, nullptr, nullptr};  // extra streams a stage pipelines over
+    hipStream_t side_stream(int i);
     void *alloc(size_t bytes);
     void release(void *p);
     bool last_scan_generic = false;  // realign scan fell back to the byte-wise kernel
