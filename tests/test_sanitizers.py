@@ -3,6 +3,7 @@ its thread pool) built with AddressSanitizer and, separately, ThreadSanitizer (t
 sanitize_main.cpp), run on the reference-made realignment cases; the output must still be the
 reference's and no sanitizer may report.  The multi-GPU hub is covered under TSan by
 test_dist_plan.py."""
+import fcntl
 import os
 import subprocess
 from pathlib import Path
@@ -21,15 +22,24 @@ FLAGS = {"asan": ["-fsanitize=address", "-fno-omit-frame-pointer"], "tsan": ["-f
 
 def _build(kind: str) -> Path:
     out = NATIVE / "_build" / f"sanitize_{kind}"
+    out.parent.mkdir(exist_ok=True)
+    # pytest-xdist workers may ask for the same binary at once: build under a lock, publish atomically
+    with open(out.parent / f".sanitize_{kind}.lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        return _build_locked(kind, out)
+
+
+def _build_locked(kind: str, out: Path) -> Path:
     deps = SRCS + list((ROOT / "openge_amd/csrc").glob("*.h")) + [ROOT / "oracle/oge_oracle.c"]
     if out.exists() and all(d.stat().st_mtime <= out.stat().st_mtime for d in deps):
         return out
-    out.parent.mkdir(exist_ok=True)
     obj = out.parent / f"oge_oracle_{kind}.o"
+    tmp = out.with_suffix(".tmp")
     subprocess.run(["gcc", "-O1", "-g", "-std=c99", *FLAGS[kind], "-c", str(ROOT / "oracle/oge_oracle.c"), "-o", str(obj)],
                    check=True)
-    subprocess.run(["g++", "-O1", "-g", "-std=c++17", *FLAGS[kind], f"-I{ROOT / 'include'}", "-o", str(out),
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", *FLAGS[kind], f"-I{ROOT / 'include'}", "-o", str(tmp),
                     *map(str, SRCS), str(obj), "-lz", "-lpthread", "-ldl"], check=True)
+    os.replace(tmp, out)
     return out
 
 
