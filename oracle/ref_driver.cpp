@@ -20,6 +20,8 @@
 // It is never shipped; on the GPU box it runs only as bench.py's cpu_baseline (the reference's own
 // chain timed beside the GPU path).
 
+#include <cstdlib>
+
 #include "algorithms/algorithm_module.h"
 #include "algorithms/file_reader.h"
 #include "algorithms/read_sorter.h"
@@ -66,7 +68,7 @@ protected:
 static void usage() {
     fprintf(stderr,
             "usage: ref_driver sort|dedup|sortdedup|realign [-v] [-t N] [-n N] [-T tmpdir] [-c level] [-K chains]\n"
-            "                  [-r region] [-q mapq] [-b] [-R ref.fa -L intervals] in.bam [in2.bam ...] out.bam\n");
+            "                  [-r region] [-q mapq] [-b] [-S seed] [-R ref.fa -L intervals] in.bam [in2.bam ...] out.bam\n");
     exit(2);
 }
 
@@ -92,6 +94,8 @@ int main(int argc, char **argv) {
         else if (a == "-r" && i + 1 < argc) region = argv[++i];
         else if (a == "-q" && i + 1 < argc) mapq = atoi(argv[++i]);
         else if (a == "-b") byname = true;
+        else if (a == "-S" && i + 1 < argc) srand((unsigned)atoi(argv[++i]));  // harness only: the realigner's
+                                  // random_shuffle of tied consensuses draws from rand()
         else pos.push_back(a);
     }
     if (pos.size() < 2) usage();  // in.bam [in2.bam ...] out.bam: several inputs go through MultiReader

@@ -54,5 +54,10 @@ int main(int argc, char **argv) {
     }
     if (fclose(o)) return 1;
     printf("%zu records in, %zu out\n", f.offsets.size(), oo.size() - 1);
+    if (getenv("OGE_REALIGN_STATS"))  // phase times of the host code (the scan here is the oracle's)
+        printf("bin %.3f (fasta %.3f decode %.3f) prepare %.3f scan %.3f (build %.3f) decide %.3f emit %.3f (mate %.3f) "
+               "release %.3f run %.3f\n",
+               st.t_bin, st.t_fasta, st.t_decode, st.t_prepare, st.t_scan, st.t_scan_build, st.t_decide, st.t_emit,
+               st.t_mate, st.t_release, st.t_run);
     return 0;
 }

@@ -2,7 +2,9 @@
 
 * c2_4m / c5_50k -- digests of the REFERENCE's own outputs at config scale (tests/golden/large.json,
   made by tests/golden/make_large_goldens.py with oracle/_ref): 4M C2 reads through sort and
-  `mergesort -M -v`, the whole 50,000-interval C5 realignment set.
+  `mergesort -M -v`; the whole 50,000-interval C5 realignment set, tie-aware
+  (tests/golden/make_c5_variants.py: the reference breaks consensus ties at random, so a handful of
+  record windows have several valid reference outputs).
 * 300M -- the bench workload itself (configs[1]/[2]): no reference run exists at that size (it would
   take ~40 min on 8 cores), so the output is checked through size-independent properties of
   mark_duplicates.cpp:326-475 / Sort.h:116-136: the output is a permutation of the input, its
@@ -94,7 +96,25 @@ def test_c5_50k_realign_matches_reference(ctx, tmp_path):
     out, oo, st = ctx.localrealign(b.header_text, b.recs, offs, b.n, fa, iv, L.realign_opts(threads=16))
     g = LARGE["c5_50k"]["realign"]
     assert len(oo) - 1 == g["n"]
-    assert hashlib.sha256(out[int(oo[0]):int(oo[-1])].tobytes()).hexdigest() == g["stream_sha256"]
+    check_c5_windows(out, oo, g)
+
+
+def check_c5_windows(out, oo, g):
+    """Tie-aware comparison with the reference (tests/golden/make_c5_variants.py): outside the windows
+    where the reference's own runs disagree (consensus ties broken by random_shuffle) the
+    records equal the reference's; inside each window they equal one of the reference's variants."""
+    h = hashlib.sha256()
+    prev = 0
+    bad = []
+    for w in g["windows"]:
+        lo, hi = w["lo"], w["hi"]
+        h.update(out[int(oo[prev]):int(oo[lo])].tobytes())
+        if hashlib.sha256(out[int(oo[lo]):int(oo[hi + 1])].tobytes()).hexdigest() not in w["variants"]:
+            bad.append((lo, hi))
+        prev = hi + 1
+    h.update(out[int(oo[prev]):int(oo[-1])].tobytes())
+    assert not bad, f"tie windows matching none of the reference's variants: {bad}"
+    assert h.hexdigest() == g["stable_sha256"]
 
 
 def _u32(buf, idx):
@@ -156,7 +176,9 @@ def test_300m_read_properties():
             return hi, lo
         a_hi, a_lo = name_key(tie)
         b_hi, b_lo = name_key(tie + 1)
-        ordered = (a_hi < b_hi) | ((a_hi == b_hi) & ((a_lo < b_lo) | ((a_lo == b_lo) & (flag[tie] <= flag[tie + 1]))))
+        # the sort saw the input's FLAG; 0x400 is set afterwards by the duplicate marking
+        fa, fb = flag[tie] & ~0x400, flag[tie + 1] & ~0x400
+        ordered = (a_hi < b_hi) | ((a_hi == b_hi) & ((a_lo < b_lo) | ((a_lo == b_lo) & (fa <= fb))))
         assert bool(ordered.all()), "name / flag tie order violated"
         # the duplicate count is the number of records carrying 0x400
         assert int(((flag >> 10) & 1).sum().item()) == nd

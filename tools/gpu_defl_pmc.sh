@@ -2,7 +2,7 @@
 # BGZF deflate: SQ counters of the k_defl_* kernels (two passes) + kernel stats on a 2M-read stream
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-OUT=gpurun_out/r02/deflpmc
+OUT=gpurun_out/${PMC_TAG:-r02}/deflpmc
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d $OUT/ks -o run --output-format csv -- python3 tools/bgzf_bench.py 2000000 2 > $OUT/ks.json 2> $OUT/ks.err || { tail -20 $OUT/ks.err; exit 1; }

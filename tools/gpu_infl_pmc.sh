@@ -2,7 +2,7 @@
 # lane inflate: SQ counters of k_infl_huff / k_infl_lz (two passes) on a 2M-read stream
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-OUT=gpurun_out/r02/inflpmc
+OUT=gpurun_out/${PMC_TAG:-r02}/inflpmc
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD --kernel-include-regex "k_infl" -d $OUT/p1 -o run --output-format csv -- python3 tools/bgzf_bench.py 2000000 1 > $OUT/p1.json 2> $OUT/p1.err || { tail -20 $OUT/p1.err; exit 1; }
