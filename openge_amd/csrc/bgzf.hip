@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -617,13 +618,19 @@ __global__ void __launch_bounds__(256) k_defl_compact(const uint8_t *__restrict_
     for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) d[i] = s[i];
 }
 
-// exclusive scan of n <= 2048 block sizes, one 1024-thread workgroup (the per-chunk offsets; runs on
-// the chunk's own stream)
-__global__ void __launch_bounds__(1024) k_scan2048(const uint32_t *__restrict__ in, uint32_t n, uint32_t *__restrict__ out) {
+// exclusive scan of n <= 8192 block sizes, one 1024-thread workgroup, 8 consecutive entries per thread
+// (the per-chunk offsets; runs on the chunk's own stream)
+constexpr uint32_t kMaxChunk = 8192;
+__global__ void __launch_bounds__(1024) k_scan_chunk(const uint32_t *__restrict__ in, uint32_t n, uint32_t *__restrict__ out) {
     __shared__ uint32_t ws[16];
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint32_t a = 2 * t < n ? in[2 * t] : 0u, b = 2 * t + 1 < n ? in[2 * t + 1] : 0u;
-    uint32_t v = a + b, x = v;
+    uint32_t a[8], v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        a[i] = 8 * t + i < n ? in[8 * t + i] : 0u;
+        v += a[i];
+    }
+    uint32_t x = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(x, d, 64);
@@ -640,9 +647,12 @@ __global__ void __launch_bounds__(1024) k_scan2048(const uint32_t *__restrict__ 
         ws[t] = z - s;
     }
     __syncthreads();
-    const uint32_t excl = ws[w] + x - v;
-    if (2 * t < n) out[2 * t] = excl;
-    if (2 * t + 1 < n) out[2 * t + 1] = excl + a;
+    uint32_t excl = ws[w] + x - v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (8 * t + i < n) out[8 * t + i] = excl;
+        excl += a[i];
+    }
 }
 
 __global__ void k_defl_advance(uint64_t *base, const uint32_t *offs, const uint32_t *sizes, uint32_t nb) {
@@ -673,7 +683,15 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     *out_bytes = 0;
     if (!n) return OGE_OK;
     const uint64_t nblk = (n + kPay - 1) / kPay;
-    const uint64_t chunk = std::min<uint64_t>(nblk, 2048);
+    // payloads per chunk: one launch of each kernel.  The Huffman kernel is one serial chain per payload
+    // (latency-bound, little LDS): more payloads per launch amortise that latency.  OGE_DEFL_CHUNK
+    // overrides (256..8192).
+    static const uint64_t chunk_max = [] {
+        const char *e = getenv("OGE_DEFL_CHUNK");
+        const long v = e ? atol(e) : 4096;
+        return (uint64_t)std::min<long>(std::max<long>(v, 256), kMaxChunk);
+    }();
+    const uint64_t chunk = std::min<uint64_t>(nblk, chunk_max);
     // Chunks go round-robin over S streams: one chunk's Huffman and emit kernels (small LDS) run on
     // the CUs beside another chunk's tokens workgroups (153 KiB of LDS, one per CU); only the
     // compaction, which advances the running output offset, is ordered chunk after chunk (events).
@@ -729,7 +747,7 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
         OGE_LAUNCH_CHECK(ctx);
         k_defl_emit<<<nb, kT, 0, u.st>>>(d_src, n, b0, level, u.tok, u.ntok, u.tabs, u.crc, u.slots, u.sizes);
         OGE_LAUNCH_CHECK(ctx);
-        k_scan2048<<<1, 1024, 0, u.st>>>(u.sizes, nb, u.offs);
+        k_scan_chunk<<<1, 1024, 0, u.st>>>(u.sizes, nb, u.offs);
         OGE_LAUNCH_CHECK(ctx);
         if (k) OGE_HIP_TRY(ctx, hipStreamWaitEvent(u.st, ev[(k - 1) % S], 0));  // previous chunk's offset advance
         k_defl_compact<<<nb, 256, 0, u.st>>>(u.slots, u.sizes, u.offs, base, d_dst);

@@ -46,13 +46,23 @@ __device__ __forceinline__ void report(uint32_t *err, uint32_t code, uint64_t bl
 }
 
 constexpr int TBL = 6, TBD = 4;  // direct-table bits: literal/length, distance
+// Long-code symbol lists: the first SLL (literal/length) and SLD (distance) entries of a lane's canonical
+// list live in LDS, the rest in its global scratch.  About 10% (synthetic) to 40% (real quality
+// alphabets) of symbols have codes longer than TBL bits; with 64 lanes some lane needs a list entry on
+// almost every step, so a list in global memory puts a memory round trip into every step of the wave.
+// Sizes that fill the LDS left at WPS waves per SIMD (4 SIMDs, 512-byte allocation granules): WPS 3 ->
+// 36 + 13 (13312 B per wave), WPS 2 -> 136 + 24 (20416 B per wave).
 // per-wave LDS, lane-interleaved ([entry][lane]): element e of lane l at e * 64 + l
+template <int SLL, int SLD>
 struct P1Lds {
+    static constexpr uint32_t kSLL = SLL, kSLD = SLD;
     uint16_t lt[1 << TBL][64];  // sym | L << 9, 0 = longer code; while code lengths are decoded a lane's
                                 // column holds its 7-bit code-length table (cl_at): sym | L << 5
     uint8_t dt[1 << TBD][64];   // sym | L << 5, 0 = longer code
     uint32_t cnt[16], lo[16], first[16], offl[16], run[16], lim[16], lie[16];  // the build's per-length values
     uint64_t clp[64];           // a lane's code-length-code lengths between its header and its CL build
+    uint8_t ll[SLL > 0 ? SLL : 1][64];  // head of the literal/length long-code list
+    uint8_t dl[SLD > 0 ? SLD : 1][64];  // head of the distance long-code list
 };
 // per-lane global scratch
 constexpr uint32_t kScr = 640;
@@ -106,8 +116,8 @@ __device__ __forceinline__ uint32_t u16of(const uint32_t (&a)[6], uint32_t i) {
 // wave): left-justified 15-bit limit in S.lim[L], (list index - first code) | end-of-literals << 16 in
 // S.lie[L].  The per-length values pass through LDS so the build holds few scalars.
 // false = over-subscribed code.
-template <int NR, int TB, bool LIT>
-__device__ bool wbuild(P1Lds &S, uint32_t j, uint8_t *list, const uint32_t (&len)[NR], uint32_t n) {
+template <int NR, int TB, bool LIT, class Lds>
+__device__ bool wbuild(Lds &S, uint32_t j, uint8_t *list, const uint32_t (&len)[NR], uint32_t n) {
     const uint32_t lane = threadIdx.x;
     const uint64_t lt = (1ull << lane) - 1;
     if (lane < 16) S.cnt[lane] = S.lo[lane] = S.run[lane] = 0;
@@ -172,7 +182,14 @@ __device__ bool wbuild(P1Lds &S, uint32_t j, uint8_t *list, const uint32_t (&len
                     else S.dt[ix][j] = (uint8_t)(s | (myL << 5));
                 }
             } else {
-                list[ol + rank] = (uint8_t)s;
+                const uint32_t k = ol + rank;
+                constexpr uint32_t H = LIT ? Lds::kSLL : Lds::kSLD;
+                if (k < H) {
+                    if (LIT) S.ll[k][j] = (uint8_t)s;
+                    else S.dl[k][j] = (uint8_t)s;
+                } else {
+                    list[k] = (uint8_t)s;
+                }
             }
         }
     }
@@ -181,13 +198,16 @@ __device__ bool wbuild(P1Lds &S, uint32_t j, uint8_t *list, const uint32_t (&len
 }
 
 // ---------------------------------------------------------------------------- phase 1
-template <int WPS>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
+// MODE: one Huffman code per loop step (a literal/length code, or the distance code of the pending match:
+// `md`), so a step has one refill, one extra-bits read and one output write whichever code it is;
+// otherwise a step decodes a whole symbol (a match's length and distance codes in the same step).
+template <int WPS, int SLL, int SLD, bool MODE>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
 __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
                                                      const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
                                                      const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
                                                      uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
                                                      uint8_t *__restrict__ scratch, uint32_t *__restrict__ err) {
-    __shared__ P1Lds S;
+    __shared__ P1Lds<SLL, SLD> S;
     const uint32_t lane = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
     const uint64_t stride = (uint64_t)gridDim.x * 64;
@@ -293,6 +313,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
     sfor<6>([&](auto k) { T.dl[k()] = T.di[k()] = 0; });
     T.l15 = 0;
     uint32_t st = ST_NEXT, fin = 0, hlit = 0, hdist = 0, ci = 0, prev = 0, srem = 0, fixed = 0, l256 = 0;
+    uint32_t md = 0, plen = 0;  // MODE: distance code next / the pending match's length
     uint64_t b = b0 + gid, d1bit = 0;
     bool first = true;
 
@@ -405,7 +426,66 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
         }
         if (__ballot(st != ST_DONE) == 0) break;
 
-        if (st == ST_SYM) {
+        if (MODE && st == ST_SYM) {
+            refill();  // >= 33 bits: a code (<= 15) and its extra bits (<= 13)
+            const uint32_t v = (uint32_t)buf;
+            const uint32_t e0 = S.lt[v & ((1u << TBL) - 1)][lane];
+            const uint32_t d0 = S.dt[v & ((1u << TBD) - 1)][lane];
+            uint32_t sym = md ? (d0 & 31) : (e0 & 511), L = md ? (d0 >> 5) : (e0 >> 9);
+            if (!(md ? d0 : e0)) {  // code longer than the direct table
+                const uint32_t c15 = __builtin_bitreverse32(v) >> 17;
+                if (!md) {
+                    L = 7;
+                    sfor<4>([&](auto k) { L += (c15 >= (T.ll[k()] & 0xffff)) + (c15 >= (T.ll[k()] >> 16)); });
+                    const uint32_t lie = pick(T.lie, L - 7);
+                    const uint32_t k = ((lie & 0xffff) + (c15 >> (15 - L))) & 0xffff;
+                    uint32_t sb;
+                    if (SLL > 0 && k < (uint32_t)SLL) sb = S.ll[min(k, (uint32_t)max(SLL - 1, 0))][lane];
+                    else sb = scr[S_LS + min(k, 287u)];
+                    sym = sb + (k >= (lie >> 16) ? 256u : 0u);
+                    if (L == 15 && c15 >= T.l15) sym = 512;  // no such code
+                } else {
+                    L = 5;
+                    sfor<5>([&](auto k) { L += (c15 >= (T.dl[k()] & 0xffff)) + (c15 >= (T.dl[k()] >> 16)); });
+                    const uint32_t k = (u16of(T.di, L - 5) + (c15 >> (15 - L))) & 0xffff;
+                    if (SLD > 0 && k < (uint32_t)SLD) sym = S.dl[min(k, (uint32_t)max(SLD - 1, 0))][lane];
+                    else sym = scr[S_DS + min(k, 31u)];
+                    if (L == 15 && c15 >= (T.dl[5] & 0xffff)) sym = 31;  // no such code
+                }
+            }
+            skip(L);
+            // extra bits: length code sym 257..285 (md = 0) or distance code sym 0..29 (md = 1)
+            const uint32_t c = sym - 257;
+            const uint32_t lext = c < 8 ? 0u : c < 28 ? (c - 4) >> 2 : 0u;
+            const uint32_t lbase = c < 8 ? c + 3 : c < 28 ? ((4 + (c & 3)) << lext) + 3 : 258u;
+            const uint32_t dext = sym < 4 ? 0u : (sym - 2) >> 1;
+            const uint32_t dbase = sym < 4 ? sym + 1 : ((2 + (sym & 1)) << dext) + 1;
+            const uint32_t ext = md ? dext : lext;
+            const uint32_t val = (md ? dbase : lbase) + get(ext);
+            uint32_t pv = 0, pn = 0, adv = 0;
+            if (!md) {
+                if (sym < 256) {
+                    if (pos >= osz) fail(E_OVERRUN);
+                    else pv = sym, pn = 1, adv = 1;
+                } else if (sym == 256) {
+                    if (fin) block_end();
+                    else st = ST_HDR;
+                } else if (sym > 285) {
+                    fail(sym == 512 ? E_CODE : E_LEN);
+                } else {
+                    plen = val, md = 1;
+                }
+            } else {
+                md = 0;
+                if (sym >= 30) fail(E_DIST);
+                else if (val > pos || pos + plen > osz) fail(E_FAR);
+                else pv = (plen - 3) | ((val - 1) << 8), pn = 3, adv = plen, mark(pos);  // descriptor in the hole
+            }
+            if (pn) {
+                put(pos, pv, pn);
+                pos += adv;
+            }
+        } else if (!MODE && st == ST_SYM) {
             refill();
             const uint32_t v = (uint32_t)buf;
             const uint32_t e = S.lt[v & ((1u << TBL) - 1)][lane];
@@ -418,7 +498,10 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 sfor<4>([&](auto k) { L += (c15 >= (T.ll[k()] & 0xffff)) + (c15 >= (T.ll[k()] >> 16)); });
                 const uint32_t lie = pick(T.lie, L - 7);
                 const uint32_t k = ((lie & 0xffff) + (c15 >> (15 - L))) & 0xffff;
-                sym = scr[S_LS + min(k, 287u)] + (k >= (lie >> 16) ? 256u : 0u);
+                uint32_t sb;
+                if (SLL > 0 && k < (uint32_t)SLL) sb = S.ll[min(k, (uint32_t)max(SLL - 1, 0))][lane];
+                else sb = scr[S_LS + min(k, 287u)];
+                sym = sb + (k >= (lie >> 16) ? 256u : 0u);
                 if (L == 15 && c15 >= T.l15) sym = 512;  // no such code
             }
             skip(L);
@@ -450,7 +533,8 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                     DL = 5;
                     sfor<5>([&](auto k) { DL += (c15 >= (T.dl[k()] & 0xffff)) + (c15 >= (T.dl[k()] >> 16)); });
                     const uint32_t k = (u16of(T.di, DL - 5) + (c15 >> (15 - DL))) & 0xffff;
-                    ds = scr[S_DS + min(k, 31u)];
+                    if (SLD > 0 && k < (uint32_t)SLD) ds = S.dl[min(k, (uint32_t)max(SLD - 1, 0))][lane];
+                    else ds = scr[S_DS + min(k, 31u)];
                     if (DL == 15 && c15 >= (T.dl[5] & 0xffff)) ds = 31;  // no such code
                 }
                 skip(DL);
@@ -497,6 +581,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
             }
         } else if (st == ST_HDR) {
             refill();
+            md = 0;
             const uint32_t h = get(3);
             fin = h & 1;
             const uint32_t type = h >> 1;
@@ -611,14 +696,28 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         }
     }
     __syncthreads();
-    // 4. pointer jumping until every position names a literal
+    // 4. pointer jumping until every position names a literal.  A chunk of literals only (every ref its
+    //    own position) or one whose refs all name roots never changes again: `act` drops it, so later
+    //    rounds only touch the chunks still inside unresolved copies.
+    auto ident = [](uint4 v, uint32_t q) {
+        return v.x == (q | ((q + 1) << 16)) && v.y == ((q + 2) | ((q + 3) << 16)) && v.z == ((q + 4) | ((q + 5) << 16)) &&
+               v.w == ((q + 6) | ((q + 7) << 16));
+    };
+    uint32_t act = 0;
+    for (uint32_t k = 0; k < 16; ++k)
+        if (8 * (512 * k + t) < osz) act |= 1u << k;
     for (int round = 0; round < 20; ++round) {
         int changed = 0;
-#pragma unroll 2
-        for (uint32_t k = 0; k < 16; ++k) {
+        uint32_t m = act;
+        while (m) {
+            const uint32_t k = __builtin_ctz(m);
+            m &= m - 1;
             const uint32_t q = 8 * (512 * k + t);
-            if (q >= osz) break;
             const uint4 v = *(const uint4 *)(refs + q);
+            if (ident(v, q)) {
+                act &= ~(1u << k);
+                continue;
+            }
             const uint32_t r8[8] = {v.x & 0xffff, v.x >> 16, v.y & 0xffff, v.y >> 16, v.z & 0xffff, v.z >> 16, v.w & 0xffff, v.w >> 16};
             uint32_t rr[8];
 #pragma unroll
@@ -631,6 +730,8 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
                 o.x = rr[0] | (rr[1] << 16), o.y = rr[2] | (rr[3] << 16), o.z = rr[4] | (rr[5] << 16), o.w = rr[6] | (rr[7] << 16);
                 *(uint4 *)(refs + q) = o;
                 changed = 1;
+            } else {
+                act &= ~(1u << k);
             }
         }
         if (!__syncthreads_or(changed)) break;
@@ -638,10 +739,13 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     // 5. this thread's chunks' roots into registers, then the region becomes the byte image of the block
     //    (the literal-filled bytes, coalesced from the output)
     uint32_t rf[64];
+    uint32_t cp = 0;  // chunks holding copied bytes (a ref other than its own position)
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) {
-        const uint4 v = *(const uint4 *)(refs + 8 * (512 * k + t));
+        const uint32_t q = 8 * (512 * k + t);
+        const uint4 v = *(const uint4 *)(refs + q);
         rf[4 * k] = v.x, rf[4 * k + 1] = v.y, rf[4 * k + 2] = v.z, rf[4 * k + 3] = v.w;
+        if (!ident(v, q)) cp |= 1u << k;
     }
     __syncthreads();
     // the image is padded (bgzf_dev.h pw<5>: a spare word per 128 bytes) so the CRC's 128-byte pieces,
@@ -664,10 +768,12 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         }
     }
     __syncthreads();
-    // 6. every byte from its root (a literal position of the image)
+    // 6. every copied byte from its root (a literal position of the image); literal-only chunks are
+    //    already in place
     const uint32_t last = osz ? osz - 1 : 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
+        if (!((cp >> k) & 1)) continue;
         uint32_t r[8];
 #pragma unroll
         for (int i = 0; i < 4; ++i) r[2 * i] = min(rf[4 * k + i] & 0xffff, last), r[2 * i + 1] = min(rf[4 * k + i] >> 16, last);
@@ -679,6 +785,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
+        if (!((cp >> k) & 1)) continue;
         const uint32_t w = 2 * (512 * k + t);  // w, w + 1: same 32-word group
         img32[pw<PS>(w)] = wv[2 * k];
         img32[pw<PS>(w) + 1] = wv[2 * k + 1];
@@ -720,11 +827,15 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     }();
     // one block per lane per launch: a launch fills the 12 resident waves per CU once (a second, partial
     // round of waves would run at a fraction of the occupancy); chunks are balanced
-    // OGE_INFL_WAVES=4: the 128-VGPR build (16 workgroups per CU, 10 KiB of LDS each) instead of 12
-    static const int wps = [] {
-        const char *e = getenv("OGE_INFL_WAVES");
-        return (e && atoi(e) == 4) ? 4 : 3;
+    // OGE_INFL_CFG (experiments): 0 = 12 waves per CU with the long-code lists in global scratch only,
+    // 1 = 12 waves with list heads in LDS, 3 = the same with one code per step (MODE), 2 = 8 waves with
+    // longer list heads in LDS (MODE), 4 = 16 waves
+    static const int cfg = [] {
+        const char *e = getenv("OGE_INFL_CFG");
+        const int c = e ? atoi(e) : 1;
+        return (c >= 0 && c <= 4) ? c : 1;
     }();
+    const int wps = cfg == 4 ? 4 : cfg == 2 ? 2 : 3;
     const uint64_t lanes = (uint64_t)ncu * 4 * wps * 64;
     const uint64_t nchunks = std::max<uint64_t>(1, (nblk + lanes - 1) / lanes);
     const uint64_t chunk = std::max<uint64_t>(1, (nblk + nchunks - 1) / nchunks);
@@ -735,8 +846,11 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
         const uint64_t nb = std::min(chunk, nblk - b0);
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
-        if (wps == 4) k_infl_huff<4><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else k_infl_huff<3><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        if (cfg == 4) k_infl_huff<4, 0, 0, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 2) k_infl_huff<2, 136, 24, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 0) k_infl_huff<3, 0, 0, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 3) k_infl_huff<3, 36, 13, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else k_infl_huff<3, 36, 13, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         OGE_LAUNCH_CHECK(ctx);
         k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, b0, zpow, err);
         OGE_LAUNCH_CHECK(ctx);
