@@ -17,14 +17,15 @@
 //                  deterministic); each thread then greedily parses its own 64-byte segment into
 //                  literal / (length, distance) tokens (matches end at the segment edge) and counts
 //                  symbol frequencies.  Tokens go to global scratch, interleaved so every store of a
-//                  wave is one contiguous line.
+//                  wave is one contiguous line.  (152 KiB of LDS: one per CU, with room beside it for an
+//                  emit or Huffman workgroup of the chunk another stream is on.)
 //   k_defl_huff    one wave per payload: length-limited Huffman code lengths for the literal/length
 //                  (15 bits), distance (15) and code-length (7) alphabets, canonical bit-reversed
 //                  codes, and the block header bit string.
 //   k_defl_emit    one 512-thread workgroup per payload: per-segment bit counts, a block scan for
 //                  the bit offsets, then every thread writes its own bits (interior words with plain
-//                  stores, the two edge words with atomicOr); CRC-32 from per-segment CRCs combined
-//                  with zero-run operators; BGZF header and footer.
+//                  stores, the two edge words with atomicOr); the payload's CRC-32 from 128-byte pieces
+//                  read from global memory, combined with zero-run operators; BGZF header and footer.
 //   k_defl_compact copies the variable-size blocks from their 64 KiB slots to their final offsets.
 #include <hip/hip_runtime.h>
 
@@ -95,20 +96,18 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
 // tok layout: [(blk * kNSub + sub) * kSeg + k] * kT + t  (u32: literal byte, or
 // 0x80000000 | (len - 3) << 16 | (dist - 1)); ntok[(blk * kNSub + sub) * kT + t].
 // zpow[k][32]: operator of feeding 2^k zero bytes through the (reflected) CRC-32 register.
+// PS: padded layouts (bgzf_dev.h pw) -- every thread's 64-byte segment of `in` starts in its own bank
+// for the greedy parse (PS = 4), or none (PS = 31).  The payload CRC is computed by k_defl_emit, so this
+// kernel's LDS (one workgroup per CU) leaves room for an emit or Huffman workgroup of another chunk.
+template <int PS>
 __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
-                                                    const uint32_t *__restrict__ zpow, uint32_t *__restrict__ tok,
-                                                    uint8_t *__restrict__ ntok, uint32_t *__restrict__ freq_out,
-                                                    uint32_t *__restrict__ crc_out) {
-    // padded layouts (bgzf_dev.h pw): every thread's 64-byte segment of `in` and its 64 candidates
-    // start in distinct banks for the greedy parse
-    constexpr int PS = 4;
-    __shared__ uint32_t in[kPay / 4 + 4 + (kPay / 4 + 4) / 16 + 1];
+                                                    uint32_t *__restrict__ tok, uint8_t *__restrict__ ntok,
+                                                    uint32_t *__restrict__ freq_out) {
+    constexpr uint32_t kInW = kPay / 4 + 4 + (PS < 31 ? (kPay / 4 + 4) / (1u << PS) + 1 : 0);
+    __shared__ uint32_t in[kInW];
     __shared__ uint32_t htab[1 << kHashBits];
     __shared__ uint16_t cand[kSub + 2 * (kSub / 64)];
     __shared__ uint32_t freq[kFreq];
-    __shared__ uint32_t crctab[4][256];
-    __shared__ uint32_t zp[17][32];
-    __shared__ uint32_t crcs[kT];
     const int t = threadIdx.x;
     const uint64_t blk = blk0 + blockIdx.x;
     const uint64_t start = blk * kPay;
@@ -119,12 +118,7 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
     auto cix = [](uint32_t q) { return q + 2 * (q >> 6); };  // candidate q of the sub-block
     for (int i = t; i < (1 << kHashBits); i += kT) htab[i] = 0;
     for (int i = t; i < kFreq; i += kT) freq[i] = 0;
-    crc_setup<kT>(crctab, zp, zpow, t);
     __syncthreads();
-    {
-        const uint32_t c = crc_window512<PS>(in, len, crctab, zp, crcs, t);
-        if (t == 0) crc_out[blockIdx.x] = c;
-    }
 
     for (int sub = 0; sub < kNSub; ++sub) {
         const uint32_t base = sub * kSub;
@@ -458,12 +452,15 @@ __device__ __forceinline__ uint32_t tok_bits(uint32_t v, const uint32_t *lit, co
 // zpow[k][32]: operator of feeding 2^k zero bytes through the (reflected) CRC-32 register
 __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0, int level,
                                                   const uint32_t *__restrict__ tok, const uint8_t *__restrict__ ntok,
-                                                  const DeflTab *__restrict__ tabs, const uint32_t *__restrict__ crc_in,
+                                                  const DeflTab *__restrict__ tabs, const uint32_t *__restrict__ zpow,
                                                   uint8_t *__restrict__ slots, uint32_t *__restrict__ sizes) {
     __shared__ uint32_t lit[kLit], dist[kDist];
     __shared__ uint32_t scan[kNSeg];
     __shared__ uint32_t wsum[kT / 64];
-    __shared__ uint32_t sh_total, sh_stored;
+    __shared__ uint32_t sh_total, sh_stored, sh_crc;
+    __shared__ uint32_t crctab[1][256];
+    __shared__ uint32_t zp[17][32];
+    __shared__ uint32_t crcs[kT / 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint64_t blk = blk0 + blockIdx.x;
     const uint64_t start = blk * kPay;
@@ -472,7 +469,12 @@ __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ sr
     const DeflTab &T = tabs[blockIdx.x];
     for (int i = t; i < kLit; i += kT) lit[i] = T.lit[i];
     for (int i = t; i < kDist; i += kT) dist[i] = T.dist[i];
+    crc_setup<kT, 1>(crctab, zp, zpow, t);
     __syncthreads();
+    {  // payload CRC-32 from global memory (the tokens kernel keeps its LDS for the match search)
+        const uint32_t c = crc_global512(s, len, crctab, zp, crcs, t);
+        if (t == 0) sh_crc = c;
+    }
 
     // bit counts per segment, in stream order (sub-block 0 segments then sub-block 1)
     uint32_t cnt[kNSub];
@@ -533,7 +535,6 @@ __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ sr
         ow[2] = 0x0006ff00u;  // XFL=0 OS=255 XLEN=6
         ow[3] = 0x00024342u;  // 'B' 'C' SLEN=2
     }
-    const uint32_t sh_crc = crc_in[blockIdx.x];
     const uint32_t bsize = total - 1;
     if (stored) {
         if (t == 0) {
@@ -692,12 +693,16 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
         return (uint64_t)std::min<long>(std::max<long>(v, 256), kMaxChunk);
     }();
     const uint64_t chunk = std::min<uint64_t>(nblk, chunk_max);
+    static const bool pad = [] {  // OGE_DEFL_PAD=0: unpadded tokens LDS layout (A/B)
+        const char *e = getenv("OGE_DEFL_PAD");
+        return !(e && atoi(e) == 0);
+    }();
     // Chunks go round-robin over S streams: one chunk's Huffman and emit kernels (small LDS) run on
     // the CUs beside another chunk's tokens workgroups (153 KiB of LDS, one per CU); only the
     // compaction, which advances the running output offset, is ordered chunk after chunk (events).
     const int S = nblk > chunk ? 3 : 1;
     struct Bufs {
-        uint32_t *tok, *freq, *sizes, *offs, *crc;
+        uint32_t *tok, *freq, *sizes, *offs;
         uint8_t *ntok, *slots;
         DeflTab *tabs;
         hipStream_t st;
@@ -711,9 +716,8 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
         B[s].slots = (uint8_t *)ctx->ws(("defl_slots" + x).c_str(), chunk * kSlot);
         B[s].sizes = (uint32_t *)ctx->ws(("defl_sizes" + x).c_str(), chunk * 4 + 16);
         B[s].offs = (uint32_t *)ctx->ws(("defl_offs" + x).c_str(), chunk * 4 + 16);
-        B[s].crc = (uint32_t *)ctx->ws(("defl_crc" + x).c_str(), chunk * 4 + 16);
         B[s].st = S == 1 ? ctx->stream : ctx->side_stream(s);
-        if (!B[s].tok || !B[s].ntok || !B[s].freq || !B[s].tabs || !B[s].slots || !B[s].sizes || !B[s].offs || !B[s].crc ||
+        if (!B[s].tok || !B[s].ntok || !B[s].freq || !B[s].tabs || !B[s].slots || !B[s].sizes || !B[s].offs ||
             !B[s].st)
             return OGE_ERR_HIP;
     }
@@ -741,11 +745,12 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk, ++k) {
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
         Bufs &u = B[k % S];
-        k_defl_tokens<<<nb, kT, 0, u.st>>>(d_src, n, b0, zpow, u.tok, u.ntok, u.freq, u.crc);
+        if (pad) k_defl_tokens<4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        else k_defl_tokens<31><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         OGE_LAUNCH_CHECK(ctx);
         k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs);
         OGE_LAUNCH_CHECK(ctx);
-        k_defl_emit<<<nb, kT, 0, u.st>>>(d_src, n, b0, level, u.tok, u.ntok, u.tabs, u.crc, u.slots, u.sizes);
+        k_defl_emit<<<nb, kT, 0, u.st>>>(d_src, n, b0, level, u.tok, u.ntok, u.tabs, zpow, u.slots, u.sizes);
         OGE_LAUNCH_CHECK(ctx);
         k_scan_chunk<<<1, 1024, 0, u.st>>>(u.sizes, nb, u.offs);
         OGE_LAUNCH_CHECK(ctx);

@@ -5,6 +5,11 @@
 
 #include <cstdint>
 
+// Global-address-space pointers.  A pointer rebuilt from an integer is a generic (flat) pointer, and on
+// gfx9 a flat load or store also counts in lgkmcnt: every later wait for an LDS read then waits for
+// that HBM access too.  Kernels that mix LDS table lookups with in-flight global traffic cast to this.
+#define OGE_G __attribute__((address_space(1)))
+
 namespace oge_bgzf {
 
 constexpr uint32_t kPay = 65280;   // BGZF payload per block written here
@@ -44,7 +49,7 @@ template <int NT, int PS = 31>
 __device__ void stage_words(uint32_t *in, const uint8_t *s, uint32_t len, int t) {
     const uintptr_t a = (uintptr_t)s & ~(uintptr_t)3;
     const uint32_t sh = (uint32_t)((uintptr_t)s & 3);
-    const uint32_t *W = (const uint32_t *)a;
+    const OGE_G uint32_t *W = (const OGE_G uint32_t *)a;
     const uint32_t nw = (len + 3) / 4;
     const uint32_t safe = len / 4;  // words wholly inside the payload
     constexpr int U = 8;
@@ -66,13 +71,14 @@ __device__ void stage_words(uint32_t *in, const uint8_t *s, uint32_t len, int t)
         uint32_t v = 0;
         if (k < nw)
             for (int b = 0; b < 4; ++b)
-                if (4 * k + b < len) v |= (uint32_t)s[4 * k + b] << (8 * b);
+                if (4 * k + b < len) v |= (uint32_t)((const OGE_G uint8_t *)s)[4 * k + b] << (8 * b);
         in[pw<PS>(k)] = v;
     }
 }
 
-// Slice-by-4 tables and the 2^k-zero-byte operators (zpow from the host, 17 x 32 words, k = 0..16).
-template <int NT>
+// Slice-by-NSL tables (NSL = 4, or 1 for the byte table only) and the 2^k-zero-byte operators (zpow
+// from the host, 17 x 32 words, k = 0..16).
+template <int NT, int NSL = 4>
 __device__ void crc_setup(uint32_t (*crctab)[256], uint32_t (*zp)[32], const uint32_t *zpow, int t) {
     if (t < 256) {
         auto byte_step = [](uint32_t c) {
@@ -81,15 +87,46 @@ __device__ void crc_setup(uint32_t (*crctab)[256], uint32_t (*zp)[32], const uin
         };
         uint32_t c = byte_step(t);
         crctab[0][t] = c;
-        for (int k = 1; k < 4; ++k) c = (c >> 8) ^ byte_step(c & 0xff), crctab[k][t] = c;
+        for (int k = 1; k < NSL; ++k) c = (c >> 8) ^ byte_step(c & 0xff), crctab[k][t] = c;
     }
     for (int i = t; i < 17 * 32; i += NT) zp[i >> 5][i & 31] = zpow[i];
 }
 
-// CRC-32 of the len (<= 65536) bytes staged in LDS; 512 threads; result valid in every thread.
+// CRC-32 of a payload of len (<= 65536) bytes with 512 threads; the result is valid in thread 0.
 // The data is right-aligned in a 65536-byte window (leading zeros leave a zero register unchanged);
-// thread t owns window bytes [128t, 128t + 128); pairs of pieces are combined with
-// crc(A || B) = Z_|B|(crc A) ^ crc B, and the whole with the 0xffffffff preset.
+// thread t owns window bytes [128t, 128t + 128) and passes the CRC of its piece (zero register start) to
+// crc_combine512, which combines pieces pairwise with crc(A || B) = Z_|B|(crc A) ^ crc B -- six levels
+// inside each wave by shuffles, the last three over the eight wave results (one barrier) -- and the
+// whole with the 0xffffffff preset.
+__device__ __forceinline__ uint32_t crc_word(const uint32_t (*crctab)[256], uint32_t c) {
+    return crctab[3][c & 0xff] ^ crctab[2][(c >> 8) & 0xff] ^ crctab[1][(c >> 16) & 0xff] ^ crctab[0][c >> 24];
+}
+
+__device__ inline uint32_t crc_combine512(uint32_t c, uint32_t len, const uint32_t (*zp)[32], uint32_t *crcs, int t) {
+    const uint32_t lane = t & 63;
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {  // pieces of 128 << lv bytes, pairs inside the wave
+        const uint32_t o = __shfl_down(c, 1u << lv, 64);
+        if (!(lane & ((2u << lv) - 1))) c = crc_mat(zp[7 + lv], c) ^ o;
+    }
+    if (lane == 0) crcs[t >> 6] = c;
+    __syncthreads();
+    uint32_t r = 0xffffffffu;
+    if (t < 64) {
+        c = t < 8 ? crcs[t] : 0u;
+#pragma unroll
+        for (int lv = 0; lv < 3; ++lv) {  // 8192-byte wave pieces
+            const uint32_t o = __shfl_down(c, 1u << lv, 64);
+            if (!(t & ((2u << lv) - 1))) c = crc_mat(zp[13 + lv], c) ^ o;
+        }
+        if (t == 0)
+            for (int k = 0; k < 17; ++k)
+                if ((len >> k) & 1) r = crc_mat(zp[k], r);
+    }
+    return ~(r ^ c);
+}
+
+// the payload staged in LDS (padded layout PS)
 template <int PS = 31>
 __device__ uint32_t crc_window512(const uint32_t *in, uint32_t len, const uint32_t (*crctab)[256], const uint32_t (*zp)[32],
                                   uint32_t *crcs, int t) {
@@ -98,27 +135,38 @@ __device__ uint32_t crc_window512(const uint32_t *in, uint32_t len, const uint32
     if (w0 >= lead) {
         const uint32_t d0 = w0 - lead;
 #pragma unroll 4
-        for (int i = 0; i < 32; ++i) {
-            c ^= ld32p<PS>(in, d0 + 4 * i);
-            c = crctab[3][c & 0xff] ^ crctab[2][(c >> 8) & 0xff] ^ crctab[1][(c >> 16) & 0xff] ^ crctab[0][c >> 24];
-        }
+        for (int i = 0; i < 32; ++i) c = crc_word(crctab, c ^ ld32p<PS>(in, d0 + 4 * i));
     } else if (w0 + 128 > lead) {
         for (uint32_t d = 0; d < w0 + 128 - lead; ++d) c = crctab[0][(c ^ byte_at<PS>(in, d)) & 0xff] ^ (c >> 8);
     }
-    crcs[t] = c;
-    __syncthreads();
-    for (int lv = 0; lv < 9; ++lv) {
-        const int pairs = 512 >> (lv + 1);
-        uint32_t v = 0;
-        if (t < pairs) v = crc_mat(zp[7 + lv], crcs[2 * t]) ^ crcs[2 * t + 1];
-        __syncthreads();
-        if (t < pairs) crcs[t] = v;
-        __syncthreads();
+    return crc_combine512(c, len, zp, crcs, t);
+}
+
+// the payload read from global memory at s (any alignment): aligned dword loads, funnel-shifted;
+// the byte table only (crctab[0]), so a caller needs 1 KiB of LDS for it
+__device__ inline uint32_t crc_global512(const uint8_t *s, uint32_t len, const uint32_t (*crctab)[256],
+                                         const uint32_t (*zp)[32], uint32_t *crcs, int t) {
+    const uint32_t lead = kSlot - len, w0 = t * 128u;
+    uint32_t c = 0;
+    if (w0 >= lead) {
+        const uint32_t d0 = w0 - lead;  // the piece is payload bytes [d0, d0 + 128)
+        const uintptr_t a = (uintptr_t)(s + d0);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const OGE_G uint32_t *W = (const OGE_G uint32_t *)(a & ~(uintptr_t)3);
+        uint32_t raw[33];
+#pragma unroll
+        for (int k = 0; k < 33; ++k) raw[k] = (k < 32 || sh) ? W[k] : 0u;  // a 33rd word only when unaligned
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            c ^= sh ? __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh) : raw[i];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) c = crctab[0][c & 0xff] ^ (c >> 8);
+        }
+    } else if (w0 + 128 > lead) {
+        const OGE_G uint8_t *b = (const OGE_G uint8_t *)s;
+        for (uint32_t d = 0; d < w0 + 128 - lead; ++d) c = crctab[0][(c ^ b[d]) & 0xff] ^ (c >> 8);
     }
-    uint32_t r = 0xffffffffu;
-    for (int k = 0; k < 17; ++k)
-        if ((len >> k) & 1) r = crc_mat(zp[k], r);
-    return ~(r ^ crcs[0]);
+    return crc_combine512(c, len, zp, crcs, t);
 }
 
 // host: zero-byte operators Z_{2^k}, k = 0..16 (columns = images of the 32 basis bits)

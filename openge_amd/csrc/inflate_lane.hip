@@ -117,7 +117,7 @@ __device__ __forceinline__ uint32_t u16of(const uint32_t (&a)[6], uint32_t i) {
 // S.lie[L].  The per-length values pass through LDS so the build holds few scalars.
 // false = over-subscribed code.
 template <int NR, int TB, bool LIT, class Lds>
-__device__ bool wbuild(Lds &S, uint32_t j, uint8_t *list, const uint32_t (&len)[NR], uint32_t n) {
+__device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (&len)[NR], uint32_t n) {
     const uint32_t lane = threadIdx.x;
     const uint64_t lt = (1ull << lane) - 1;
     if (lane < 16) S.cnt[lane] = S.lo[lane] = S.run[lane] = 0;
@@ -201,7 +201,8 @@ __device__ bool wbuild(Lds &S, uint32_t j, uint8_t *list, const uint32_t (&len)[
 // MODE: one Huffman code per loop step (a literal/length code, or the distance code of the pending match:
 // `md`), so a step has one refill, one extra-bits read and one output write whichever code it is;
 // otherwise a step decodes a whole symbol (a match's length and distance codes in the same step).
-template <int WPS, int SLL, int SLD, bool MODE>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
+// DIRECT: every output byte is its own byte store (no 8-byte accumulator to keep and flush).
+template <int WPS, int SLL, int SLD, bool MODE, bool DIRECT = false>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
 __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
                                                      const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
                                                      const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
@@ -211,7 +212,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
     const uint32_t lane = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
     const uint64_t stride = (uint64_t)gridDim.x * 64;
-    uint8_t *const scr = scratch + gid * kScr;  // this lane's lens / long-code symbol lists
+    OGE_G uint8_t *const scr = (OGE_G uint8_t *)(scratch + gid * kScr);  // this lane's lens / long-code symbol lists
     const uintptr_t zend = (uintptr_t)z + zbytes;
 
     // input: 64-bit bit buffer + two 16-byte chunks (q being consumed, p loaded ahead)
@@ -220,7 +221,8 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
     uintptr_t cp = 0;
     auto load16 = [&](uintptr_t a, uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t &x3) {
         if (a < zend) {  // a 16-byte aligned chunk holding at least one stream byte never leaves its page
-            const uint4 v = *(const uint4 *)a;
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 v = *(const OGE_G u32x4 *)a;
             x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
         } else {
             x0 = x1 = x2 = x3 = 0;
@@ -268,15 +270,22 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
     uint64_t oc = ~0ull, acc = 0;
     auto flush = [&]() {
         if (oc == ~0ull) return;
-        uint8_t *c = (uint8_t *)(oc << 3);
-        if (c >= obase && c + 8 <= obase + osz) {
-            *(uint64_t *)c = acc;
+        const uintptr_t c = oc << 3, ob = (uintptr_t)obase;
+        if (c >= ob && c + 8 <= ob + osz) {
+            *(OGE_G uint64_t *)c = acc;
         } else {
             for (uint32_t k = 0; k < 8; ++k)
-                if (c + k >= obase && c + k < obase + osz) c[k] = (uint8_t)(acc >> (8 * k));
+                if (c + k >= ob && c + k < ob + osz) ((OGE_G uint8_t *)c)[k] = (uint8_t)(acc >> (8 * k));
         }
     };
     auto put = [&](uint32_t p, uint32_t v, uint32_t nbytes) {  // nbytes (1..3) little-endian bytes of v at p
+        if (DIRECT) {
+            OGE_G uint8_t *o = (OGE_G uint8_t *)(obase + p);
+            o[0] = (uint8_t)v;
+            if (nbytes > 1) o[1] = (uint8_t)(v >> 8);
+            if (nbytes > 2) o[2] = (uint8_t)(v >> 16);
+            return;
+        }
         const uintptr_t a = (uintptr_t)(obase + p);
         const uint32_t sh = (uint32_t)(a & 7);
         if ((a >> 3) == oc && sh + nbytes <= 8) {
@@ -294,7 +303,8 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
         }
     };
     // match-start bitmap of the block (1024 words per block of the chunk)
-    uint64_t *bmp = nullptr, bm = 0;
+    OGE_G uint64_t *bmp = nullptr;
+    uint64_t bm = 0;
     uint32_t bw = 0;
     auto mark = [&](uint32_t p) {
         const uint32_t w = p >> 6;
@@ -337,7 +347,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
         while (need) {
             const uint32_t j = (uint32_t)__builtin_ctzll(need);
             need &= need - 1;
-            uint8_t *sj = scratch + ((uint64_t)blockIdx.x * 64 + j) * kScr;
+            OGE_G uint8_t *sj = (OGE_G uint8_t *)(scratch + ((uint64_t)blockIdx.x * 64 + j) * kScr);
             if (__builtin_amdgcn_readlane(st, j) == ST_BCL) {
                 // code-length code: 19 symbols, lengths 3 bits each (symbol s at bits 3s of S.clp[j])
                 const uint64_t c = S.clp[j];
@@ -367,8 +377,8 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                     const uint32_t rev = __builtin_bitreverse32(fc + rank) >> (32 - myL);
                     for (uint32_t k = 0; k < (1u << (7 - myL)); ++k) cl[cl_at(rev | (k << myL), j)] = (uint8_t)(lane | (myL << 5));
                 }
-                ((uint32_t *)(sj + S_LENS))[lane] = 0;  // all 320 bytes: 17/18 runs then need no stores
-                if (lane < 16) ((uint32_t *)(sj + S_LENS))[64 + lane] = 0;
+                ((OGE_G uint32_t *)(sj + S_LENS))[lane] = 0;  // all 320 bytes: 17/18 runs then need no stores
+                if (lane < 16) ((OGE_G uint32_t *)(sj + S_LENS))[64 + lane] = 0;
                 if (lane == j) {
                     if (ok) st = ST_CL, ci = 0, prev = 0, l256 = 0;
                     else fail(E_TABLE);
@@ -416,7 +426,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 pos = 0;
                 oc = ~0ull;
                 acc = 0;
-                bmp = bitmap + (b - b0) * 1024;
+                bmp = (OGE_G uint64_t *)(bitmap + (b - b0) * 1024);
                 bm = 0;
                 bw = 0;
                 d1bit = ((uint64_t)(uintptr_t)z + d1a[b]) * 8;
@@ -656,7 +666,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     {
         const uintptr_t a = (uintptr_t)(O + q0);
         const uint32_t sh = (uint32_t)(a & 3);
-        const uint32_t *W = (const uint32_t *)(a & ~(uintptr_t)3);
+        const OGE_G uint32_t *W = (const OGE_G uint32_t *)(a & ~(uintptr_t)3);
         const uintptr_t lim = (uintptr_t)(O + osz);  // a dword starting below lim holds a block byte: readable
         uint32_t raw[34];
 #pragma unroll
@@ -676,7 +686,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     }
     __syncthreads();
     // 3. holes: refs[p + j] = p - D + j, descriptors read from this thread's window registers
-    const uint64_t *bmp = bitmap + (b - b0) * 1024;
+    const OGE_G uint64_t *bmp = (const OGE_G uint64_t *)(bitmap + (b - b0) * 1024);
     const uint32_t nw = (osz + 63) >> 6;
 #pragma unroll
     for (uint32_t h = 0; h < 2; ++h) {
@@ -756,7 +766,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     auto ib = [](uint32_t q) { return q + ((q >> 7) << 2); };
     {
         const uint32_t sh = (uint32_t)((uintptr_t)O & 3);
-        const uint32_t *W = (const uint32_t *)((uintptr_t)O & ~(uintptr_t)3);
+        const OGE_G uint32_t *W = (const OGE_G uint32_t *)((uintptr_t)O & ~(uintptr_t)3);
         const uintptr_t lim = (uintptr_t)(O + osz);
         const uint32_t nd = (osz + 3) >> 2;
 #pragma unroll 4
@@ -797,7 +807,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         if (t == 0 && c != crc[b]) report(err, E_CRC, b);
     }
     const uint32_t sh = (uint32_t)((uintptr_t)O & 3);
-    uint32_t *A = (uint32_t *)((uintptr_t)O & ~(uintptr_t)3);
+    OGE_G uint32_t *A = (OGE_G uint32_t *)((uintptr_t)O & ~(uintptr_t)3);
     const uint32_t nwords = (osz + sh + 3) / 4;
     for (uint32_t g = t; g < nwords; g += kT2) {
         const int32_t r0 = (int32_t)(4 * g) - (int32_t)sh;  // relative position of the word's first byte
@@ -806,7 +816,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         } else {
             for (int i = 0; i < 4; ++i) {
                 const int32_t r = r0 + i;
-                if (r >= 0 && r < (int32_t)osz) ((uint8_t *)(A + g))[i] = img[ib((uint32_t)r)];
+                if (r >= 0 && r < (int32_t)osz) ((OGE_G uint8_t *)(A + g))[i] = img[ib((uint32_t)r)];
             }
         }
     }
@@ -829,11 +839,11 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     // round of waves would run at a fraction of the occupancy); chunks are balanced
     // OGE_INFL_CFG (experiments): 0 = 12 waves per CU with the long-code lists in global scratch only,
     // 1 = 12 waves with list heads in LDS, 3 = the same with one code per step (MODE), 2 = 8 waves with
-    // longer list heads in LDS (MODE), 4 = 16 waves
+    // longer list heads in LDS (MODE), 4 = 16 waves, 5 / 6 = 1 / 3 with byte stores (DIRECT)
     static const int cfg = [] {
         const char *e = getenv("OGE_INFL_CFG");
         const int c = e ? atoi(e) : 1;
-        return (c >= 0 && c <= 4) ? c : 1;
+        return (c >= 0 && c <= 6) ? c : 1;
     }();
     const int wps = cfg == 4 ? 4 : cfg == 2 ? 2 : 3;
     const uint64_t lanes = (uint64_t)ncu * 4 * wps * 64;
@@ -850,6 +860,8 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         else if (cfg == 2) k_infl_huff<2, 136, 24, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 0) k_infl_huff<3, 0, 0, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 3) k_infl_huff<3, 36, 13, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 5) k_infl_huff<3, 36, 13, false, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 6) k_infl_huff<3, 36, 13, true, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else k_infl_huff<3, 36, 13, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         OGE_LAUNCH_CHECK(ctx);
         k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, b0, zpow, err);
