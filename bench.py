@@ -52,6 +52,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measur
 VALU_INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 KERNEL_STAGES = ["input_pass", "sort_radix", "sort_ties", "meta_gather", "md_matejoin", "md_pairs", "md_frags",
                  "md_apply", "gather_offsets", "gather_records"]
+SUB_STAGES = ["md_pair_win", "md_frag_win", "md_pair_ovf", "md_frag_ovf"]  # nested in md_pairs / md_frags: which group path ran
 E2E_STAGES = ["bgzf_index", "bgzf_inflate", "bgzf_crc", "rec_walk"] + KERNEL_STAGES + ["bgzf_deflate"]
 
 
@@ -71,6 +72,7 @@ def parse():
     ap.add_argument("--realign-intervals", type=int, default=50_000)
     ap.add_argument("--realign-only", action="store_true", help="profiling aid: only the C5 realign leg")
     ap.add_argument("--e2e-only", action="store_true", help="profiling aid: skip every leg but the e2e steps")
+    ap.add_argument("--kernel-only", action="store_true", help="profiling aid: only the kernel-only leg")
     return ap.parse_args()
 
 
@@ -271,11 +273,11 @@ def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, "torch.Tenso
                                             d_out.data_ptr(), d_out_off.data_ptr())
         step()  # first call: workspace growth, code-object load
         torch.cuda.synchronize(dev)
-        tot = {s: 0.0 for s in KERNEL_STAGES}
+        tot = {s: 0.0 for s in KERNEL_STAGES + SUB_STAGES}
         t0 = time.perf_counter()
         for _ in range(args.kernel_steps):
             nd = step()
-            for s, v in stage_ms(ctx, KERNEL_STAGES).items():
+            for s, v in stage_ms(ctx, KERNEL_STAGES + SUB_STAGES).items():
                 tot[s] += v
         torch.cuda.synchronize(dev)
         dt = (time.perf_counter() - t0) / args.kernel_steps
@@ -353,6 +355,10 @@ def main():
         kargs.kernel_steps = 0
     kres, S, B, hdr_text = kernel_leg(ctx, L, torch, dev, p, n, len(hb), kargs)
     log(f"kernel leg: {kres.get('ms_per_step')} ms/step; records {B / 1e9:.2f} GB")
+    if args.kernel_only:
+        print(json.dumps(kres), flush=True)
+        ctx.close()
+        return
     S[:len(hb)].copy_(torch.frombuffer(bytearray(hb), dtype=torch.uint8).to(dev))
     total = len(hb) + B
     seq_bytes = n * ((p.read_len + 1) // 2)

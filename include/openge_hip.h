@@ -105,7 +105,9 @@ typedef struct oge_markdup_opts {
     const int16_t *rg_lib;
     int32_t n_rg;
     int16_t unknown_lib;
-    int16_t pad0;
+    /* Test knob: 1 = group fragments / pairs with the sort-based stages even where the windowed
+     * ones apply (records in sorted order on one GPU).  Results must not change. */
+    int16_t debug_sort_groups;
     /* Reproduce the reference's non-verbose index bug: the record index only
      * advances under -v, so every ReadEnds carries index 0.  Default 0 = -v semantics. */
     int32_t compat_nonverbose_index;

@@ -191,12 +191,71 @@ __device__ __forceinline__ uint64_t mix64(uint64_t h) {
     h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; return h ^ (h >> 33);
 }
 
+// ---- windowed grouping support (records in ByPosition order, one GPU) ----
+// A record's 5' coordinate (its fragment / pair group coordinate) lies within a few read lengths of
+// its sort position, so in sorted order every group's members sit inside a short window.  Positions
+// are compared as X(ref, v) = ref * 2^34 + v + 2^32 (v = pos + 1 or 5' coordinate + 1, |v| < 2^32).
+__device__ __forceinline__ int64_t win_x(uint32_t ref, int64_t v) { return ((int64_t)ref << 34) + v + (1ll << 32); }
+// the anchor of a sorted record: (refID', pos + 1) of its coordinate sort key (records.hip)
+__device__ __forceinline__ int64_t anchor_of_key(uint64_t k) {
+    return win_x((uint32_t)(k >> 33) & 0x1ffffu, (int64_t)((k >> 1) & 0xffffffffu));
+}
+constexpr int64_t kDevBias = 1ll << 40;  // deviations are kept as D + 2^40 (0 = none seen)
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t o = ((uint64_t)__shfl_xor((unsigned)(v >> 32), d, 64) << 32) | (uint64_t)__shfl_xor((unsigned)v, d, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+// max(anchor - coord) and max(coord - anchor) over the items, reduced per block into slot
+// (blockIdx & 255) of dev[0..511] (pairs of words); k_dev_fold folds the slots.  A single word
+// would serialise millions of atomics at one L2 channel.  Every thread of the block must call it.
+constexpr int kDevSlots = 256;
+__device__ __forceinline__ void win_dev_update(bool has, int64_t a, int64_t c, unsigned long long *dev) {
+    __shared__ uint64_t wd[2][kT / 64];
+    const uint64_t d0 = wave_max_u64(has ? (uint64_t)(a - c + kDevBias) : 0ull);
+    const uint64_t d1 = wave_max_u64(has ? (uint64_t)(c - a + kDevBias) : 0ull);
+    if ((threadIdx.x & 63) == 0) {
+        wd[0][threadIdx.x >> 6] = d0;
+        wd[1][threadIdx.x >> 6] = d1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        uint64_t m = 0;
+        for (int w = 0; w < kT / 64; ++w) m = max(m, wd[threadIdx.x][w]);
+        if (m) atomicMax(dev + 2 * (blockIdx.x & (kDevSlots - 1)) + threadIdx.x, (unsigned long long)m);
+    }
+}
+// out[0..1] = the maxima over the slots
+__global__ __launch_bounds__(kDevSlots) void k_dev_fold(const unsigned long long *__restrict__ slots,
+                                                        unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long m[2][kDevSlots];
+    m[0][threadIdx.x] = slots[2 * threadIdx.x];
+    m[1][threadIdx.x] = slots[2 * threadIdx.x + 1];
+    __syncthreads();
+    for (int h = kDevSlots / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) {
+            m[0][threadIdx.x] = max(m[0][threadIdx.x], m[0][threadIdx.x + h]);
+            m[1][threadIdx.x] = max(m[1][threadIdx.x], m[1][threadIdx.x + h]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 2) out[threadIdx.x] = m[threadIdx.x][0];
+}
+
+// skeys (optional, records in sorted order): pax[p] = anchor of the pair's first record a (pairs
+// arrive sorted by a) and the deviation of read1's 5' coordinate from it into dev[0..1].
 __global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ pairs, uint32_t np, const uint8_t *__restrict__ recs,
                                                     const RecMeta *__restrict__ meta, KeyLayout L, uint64_t *__restrict__ hi,
                                                     uint64_t *__restrict__ lo, uint2 *__restrict__ idx, uint32_t *__restrict__ val,
-                                                    uint64_t *__restrict__ hk) {
+                                                    uint64_t *__restrict__ hk, const uint64_t *__restrict__ skeys,
+                                                    int64_t *__restrict__ pax, unsigned long long *__restrict__ dev) {
     uint32_t p = blockIdx.x * kT + threadIdx.x;
-    if (p >= np) return;
+    bool has = false;
+    int64_t ax = 0, cx = 0;
+    if (p < np) {
     uint32_t a = (uint32_t)(pairs[p] >> 32), b = (uint32_t)pairs[p];  // a seen first (smaller record index)
     if (a > b) { uint32_t t = a; a = b; b = t; }
     const RecMeta A = meta[a], B = meta[b];
@@ -224,6 +283,14 @@ __global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ 
     hk[p] = mix64(mix64(kh) ^ kl);
     idx[p] = make_uint2(i1, i2);
     val[p] = p;
+    if (skeys) {
+        ax = anchor_of_key(skeys[a]);
+        cx = win_x((uint32_t)r1s, (int64_t)r1c + 1);
+        pax[p] = ax;
+        has = !bad;
+    }
+    }
+    if (skeys) win_dev_update(has, ax, cx, dev);
 }
 
 // Pair chunks (markDuplicatePairs, :488-507) need equal (lib, r1Seq, r1Coord, orient, r2Seq, r2Coord)
@@ -328,11 +395,16 @@ __device__ __forceinline__ uint64_t frag_key(const RecMeta &R, KeyLayout L) {
 //   cval[i]  = the record's mate-join candidate key (see CandKey), scattered by k_cand_pack
 //   desc0[i] = src (39 bits) | primary << 39 | bin << 40 | FLAG high byte << 56 (optional), finished
 //              by k_apply_desc once the dup bits are known; a src past 39 bits sets *ovf.
+// skeys (optional): the records' sorted coordinate keys; then the fragment coordinates' deviation
+// from the anchors is reduced into dev[0..1] for the windowed fragment groups.
 __global__ __launch_bounds__(kT) void k_cand_frag(const RecMeta *__restrict__ meta, uint64_t n, KeyLayout L, CandKey ck,
                                                    uint32_t *__restrict__ f, uint64_t *__restrict__ keys,
                                                    uint32_t *__restrict__ vals, uint64_t *__restrict__ cval,
-                                                   uint64_t *__restrict__ desc0, unsigned int *__restrict__ ovf) {
+                                                   uint64_t *__restrict__ desc0, unsigned int *__restrict__ ovf,
+                                                   const uint64_t *__restrict__ skeys, unsigned long long *__restrict__ dev) {
     uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    bool has = false;
+    int64_t ax = 0, cx = 0;
     if (i < n) {
         const RecMeta R = meta[i];
         f[i] = (R.m & OGE_M_CAND) ? 1u : 0u;
@@ -344,9 +416,15 @@ __global__ __launch_bounds__(kT) void k_cand_frag(const RecMeta *__restrict__ me
             desc0[i] = (R.src & ((1ull << 39) - 1)) | ((R.m & OGE_M_PRIMARY) ? (1ull << 39) : 0ull) |
                        ((R.m >> 48) << 40) | (((R.m >> 40) & 0xff) << 56);
         }
+        if (skeys && (R.m & OGE_M_FRAG)) {
+            has = true;
+            ax = anchor_of_key(skeys[i]);
+            cx = win_x((uint32_t)R.seq, (int64_t)R.coord + 1);
+        }
     } else if (i == n) {
         f[i] = 0;
     }
+    if (skeys) win_dev_update(has, ax, cx, dev);
 }
 
 // candidate i (flag = its exclusive-scan slot differs from the next one's) -> its compacted slot
@@ -373,14 +451,224 @@ __global__ __launch_bounds__(kT) void k_frag_groups(const uint64_t *__restrict__
             if (!(keys[x] >> 63)) dup[vals[x]] = 1;
         return;
     }
+    // best = max score, then smallest record index (the reference's first strict max in index
+    // order; explicit, so the group's order in the array does not matter)
     uint64_t best = q;
     int16_t bs = (int16_t)(uint16_t)((keys[q] >> 47) & 0xFFFF);
+    uint32_t bv = vals[q];
     for (uint64_t x = q + 1; x < e; ++x) {
         const int16_t s = (int16_t)(uint16_t)((keys[x] >> 47) & 0xFFFF);
-        if (s > bs) { best = x; bs = s; }
+        const uint32_t v = vals[x];
+        if (s > bs || (s == bs && v < bv)) { best = x; bs = s; bv = v; }
     }
     for (uint64_t x = q; x < e; ++x)
         if (x != best) dup[vals[x]] = 1;
+}
+
+// ---- windowed groups: markDuplicateFragments / markDuplicatePairs without a global sort ----
+// Items (records, or pairs ordered by their first record) are in anchor order; each has a group
+// coordinate C (5' coordinate of the fragment / of read1) with D1 >= A - C and D2 >= C - A (exact
+// maxima reduced by k_cand_frag / k_pair_build).  Tile t (items [tT, tT+T)) owns the groups whose C
+// lies in [A(tT), A(tT+T)) (first tile from -inf, last to +inf): every group has one owner, and all
+// its members lie in the window of items whose anchors are in [A(tT) - D2, A(tT+T) + D1).  The
+// owner builds the groups in an LDS hash table (best = max score, then smallest read1 / record
+// index: the reference's first strict max in index order) and marks the duplicates.  A window
+// larger than the tile's table (a pile of reads at one position) sends the whole stage to the
+// sort-based kernels above.
+constexpr uint32_t kWinTile = 512;   // items per tile
+constexpr uint32_t kFragCap = 2048;  // window items per fragment tile (LDS table of 2 x cap slots)
+constexpr uint32_t kPairCap = 1024;  // window items per pair tile
+
+__device__ __forceinline__ int64_t win_anchor(const uint64_t *__restrict__ skeys, const int64_t *__restrict__ ax, uint64_t i) {
+    return skeys ? anchor_of_key(skeys[i]) : ax[i];
+}
+// first i in [lo, hi) with anchor(i) >= v (hi if none)
+__device__ uint64_t win_lower_bound(const uint64_t *__restrict__ skeys, const int64_t *__restrict__ ax, uint64_t lo,
+                                    uint64_t hi, int64_t v) {
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (win_anchor(skeys, ax, mid) < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+struct WinTile {
+    int64_t lo, hi;  // owned group coordinates [lo, hi)
+    bool first, last;
+};
+__device__ __forceinline__ WinTile win_tile(const uint64_t *__restrict__ skeys, const int64_t *__restrict__ ax, uint64_t n,
+                                            uint64_t t) {
+    WinTile w;
+    const uint64_t b0 = t * kWinTile, b1 = b0 + kWinTile;
+    w.first = t == 0;
+    w.last = b1 >= n;
+    w.lo = w.first ? INT64_MIN : win_anchor(skeys, ax, b0);
+    w.hi = w.last ? INT64_MAX : win_anchor(skeys, ax, b1);
+    return w;
+}
+// one thread per tile: its window [s, e) of items (empty when it owns nothing); *ovf when a window
+// exceeds cap
+// amax: no item's group coordinate reaches it, and items from the first anchor >= amax on (the
+// unmapped tail of the sorted records) never join a window.
+__global__ __launch_bounds__(kT) void k_win_bounds(const uint64_t *__restrict__ skeys, const int64_t *__restrict__ ax, uint64_t n,
+                                                    uint32_t ntiles, uint32_t cap, const unsigned long long *__restrict__ dev,
+                                                    int64_t amax, uint2 *__restrict__ bounds, uint32_t *__restrict__ ovl,
+                                                    unsigned int *__restrict__ novf, unsigned long long *__restrict__ ovf_items) {
+    const uint32_t t = blockIdx.x * kT + threadIdx.x;
+    uint64_t s = 0, e = 0;
+    if (t < ntiles) {
+        const int64_t D1 = max((int64_t)dev[0] - kDevBias, (int64_t)0), D2 = max((int64_t)dev[1] - kDevBias, (int64_t)0);
+        const WinTile w = win_tile(skeys, ax, n, t);
+        const uint64_t b0 = (uint64_t)t * kWinTile;
+        if ((w.first || w.last || w.lo < w.hi) && w.lo < amax) {
+            s = w.first ? 0 : win_lower_bound(skeys, ax, 0, b0 + 1, w.lo - D2);
+            e = win_lower_bound(skeys, ax, b0, n, w.last ? amax : min(w.hi + D1, amax));
+        }
+        bounds[t] = make_uint2((uint32_t)s, (uint32_t)e);
+    }
+    // tiles whose window exceeds cap (a pile of reads at one position): listed for the sort path
+    const bool over = e - s > cap;
+    const uint32_t slot = oge_wave_append(over, novf);
+    if (over) {
+        ovl[slot] = t;
+        atomicAdd(ovf_items, (unsigned long long)(e - s));
+    }
+}
+
+// items owned by the overflowing tiles ovl[] -> (key, value) lists for the sort-based stages
+// (fragments: fk / fv; pairs: hk / pair index).  One block per listed tile.
+template <bool PAIRS>
+__global__ __launch_bounds__(kT) void k_win_collect(const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                                     const uint64_t *__restrict__ hi, const uint64_t *__restrict__ lo,
+                                                     const uint64_t *__restrict__ skeys, const int64_t *__restrict__ ax,
+                                                     uint64_t n, KeyLayout L, const uint2 *__restrict__ bounds,
+                                                     const uint32_t *__restrict__ ovl, uint64_t *__restrict__ ok,
+                                                     uint32_t *__restrict__ ov, unsigned int *__restrict__ cnt) {
+    const uint32_t t = ovl[blockIdx.x];
+    const uint2 b = bounds[t];
+    const WinTile w = win_tile(skeys, ax, n, t);
+    const uint64_t smask = (1ull << L.sb) - 1;
+    for (uint64_t base = b.x; base < b.y; base += kT) {  // uniform trip count: oge_wave_append is convergent
+        const uint64_t i = base + threadIdx.x;
+        bool own = false;
+        if (i < b.y) {
+            if (PAIRS) {
+                const uint64_t h = hi[i];
+                const int64_t c = win_x((uint32_t)((h >> 32) & smask), (int64_t)(int32_t)((uint32_t)h ^ 0x80000000u) + 1);
+                own = !(lo[i] >> 63) && c >= w.lo && c < w.hi;
+            } else {
+                const uint64_t k = keys[i];
+                const int64_t c = win_x((uint32_t)((k >> 33) & smask), (int64_t)(int32_t)((uint32_t)(k >> 1) ^ 0x80000000u) + 1);
+                own = !(k & (1ull << 46)) && c >= w.lo && c < w.hi;
+            }
+        }
+        const uint32_t slot = oge_wave_append(own, cnt);
+        if (own) {
+            ok[slot] = keys[i];
+            ov[slot] = PAIRS ? (uint32_t)i : vals[i];
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t win_hash(uint64_t k) { return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 32); }
+__device__ __forceinline__ uint32_t win_slots(uint32_t m) {  // power of two >= 2m, >= 64
+    uint32_t h = 64;
+    while (h < 2 * m) h <<= 1;
+    return h;
+}
+
+// fragments: items = records (fk / fv from k_cand_frag), anchors = the sorted coordinate keys.
+// Table slot: group key (47 bits; bit 63 = the group holds a paired end) + packed best of the
+// unpaired ends ((score + 2^15) << 32 | ~record index).
+__global__ __launch_bounds__(kT) void k_frag_win(const uint64_t *__restrict__ fk, const uint32_t *__restrict__ fv,
+                                                  const uint64_t *__restrict__ skeys, uint64_t n, KeyLayout L,
+                                                  const uint2 *__restrict__ bounds, uint8_t *__restrict__ dup) {
+    __shared__ unsigned long long skey[2 * kFragCap], sbest[2 * kFragCap];
+    const uint2 b = bounds[blockIdx.x];
+    if (b.x >= b.y || b.y - b.x > kFragCap) return;  // owns nothing / overflow: k_win_collect's list
+    const WinTile w = win_tile(skeys, nullptr, n, blockIdx.x);
+    const uint32_t H = win_slots(b.y - b.x);
+    constexpr unsigned long long kEmpty = ~0ull, kPaired = 1ull << 63;
+    const uint64_t gmask = (1ull << 47) - 1, smask = (1ull << L.sb) - 1;
+    for (uint32_t j = threadIdx.x; j < H; j += kT) { skey[j] = kEmpty; sbest[j] = 0; }
+    __syncthreads();
+    for (uint32_t i = b.x + threadIdx.x; i < b.y; i += kT) {
+        const uint64_t k = fk[i];
+        if (k & (1ull << 46)) continue;  // not a fragment
+        const int64_t c = win_x((uint32_t)((k >> 33) & smask), (int64_t)(int32_t)((uint32_t)(k >> 1) ^ 0x80000000u) + 1);
+        if (c < w.lo || c >= w.hi) continue;
+        const uint64_t g = k & gmask;
+        uint32_t h = win_hash(g) & (H - 1);
+        for (;;) {
+            const unsigned long long cur = atomicCAS(&skey[h], kEmpty, (unsigned long long)g);
+            if (cur == kEmpty || (cur & ~kPaired) == g) break;
+            h = (h + 1) & (H - 1);
+        }
+        if (k >> 63) atomicOr(&skey[h], kPaired);
+        else atomicMax(&sbest[h], ((unsigned long long)(((k >> 47) & 0xFFFF) ^ 0x8000) << 32) | (0xFFFFFFFFu - fv[i]));
+    }
+    __syncthreads();
+    for (uint32_t i = b.x + threadIdx.x; i < b.y; i += kT) {
+        const uint64_t k = fk[i];
+        if (k & ((1ull << 46) | (1ull << 63))) continue;  // not a fragment / a paired end: never marked here
+        const int64_t c = win_x((uint32_t)((k >> 33) & smask), (int64_t)(int32_t)((uint32_t)(k >> 1) ^ 0x80000000u) + 1);
+        if (c < w.lo || c >= w.hi) continue;
+        const uint64_t g = k & gmask;
+        uint32_t h = win_hash(g) & (H - 1);
+        while ((skey[h] & ~kPaired) != g) h = (h + 1) & (H - 1);
+        const uint32_t v = fv[i];
+        const unsigned long long mine = ((unsigned long long)(((k >> 47) & 0xFFFF) ^ 0x8000) << 32) | (0xFFFFFFFFu - v);
+        if ((skey[h] & kPaired) || sbest[h] != mine) dup[v] = 1;
+    }
+}
+
+// pairs: items = pair ReadEnds in first-record order (k_pair_build), anchors pax.  The window's
+// owned keys are staged in LDS; a slot holds the window index of its group's first inserted pair
+// and the packed best ((score + 2^15) << 32 | ~read1 index).
+__global__ __launch_bounds__(kT) void k_pair_win(const uint64_t *__restrict__ hi, const uint64_t *__restrict__ lo,
+                                                  const uint2 *__restrict__ idx, const int64_t *__restrict__ pax, uint64_t np,
+                                                  KeyLayout L, const uint2 *__restrict__ bounds, uint8_t *__restrict__ dup) {
+    __shared__ unsigned long long ikh[kPairCap], ikl[kPairCap], sbest[2 * kPairCap];
+    __shared__ uint32_t srep[2 * kPairCap];
+    __shared__ uint16_t islot[kPairCap];
+    const uint2 b = bounds[blockIdx.x];
+    if (b.x >= b.y || b.y - b.x > kPairCap) return;  // owns nothing / overflow: k_win_collect's list
+    const WinTile w = win_tile(nullptr, pax, np, blockIdx.x);
+    const uint32_t m = b.y - b.x, H = win_slots(m);
+    const uint64_t kmask = (1ull << 48) - 1, smask = (1ull << L.sb) - 1;
+    constexpr unsigned long long kNone = ~0ull;
+    for (uint32_t j = threadIdx.x; j < H; j += kT) { srep[j] = 0xFFFFFFFFu; sbest[j] = 0; }
+    for (uint32_t x = threadIdx.x; x < m; x += kT) {
+        const uint64_t h = hi[b.x + x], l = lo[b.x + x];
+        const int64_t c = win_x((uint32_t)((h >> 32) & smask), (int64_t)(int32_t)((uint32_t)h ^ 0x80000000u) + 1);
+        const bool own = !(l >> 63) && c >= w.lo && c < w.hi;  // bit 63 of lo: unconfirmed, not a pair
+        ikh[x] = h & kmask;
+        ikl[x] = own ? l : kNone;
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < m; x += kT) {
+        const unsigned long long kl = ikl[x];
+        if (kl == kNone) continue;
+        const unsigned long long kh = ikh[x];
+        uint32_t h = win_hash(kh ^ (kl * 0xff51afd7ed558ccdull)) & (H - 1);
+        for (;;) {
+            const uint32_t cur = atomicCAS(&srep[h], 0xFFFFFFFFu, x);
+            if (cur == 0xFFFFFFFFu || (ikh[cur] == kh && ikl[cur] == kl)) break;
+            h = (h + 1) & (H - 1);
+        }
+        islot[x] = (uint16_t)h;
+        atomicMax(&sbest[h], ((unsigned long long)((hi[b.x + x] >> 48) ^ 0x8000) << 32) | (0xFFFFFFFFu - idx[b.x + x].x));
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < m; x += kT) {
+        if (ikl[x] == kNone) continue;
+        const uint2 ii = idx[b.x + x];
+        const unsigned long long mine = ((unsigned long long)((hi[b.x + x] >> 48) ^ 0x8000) << 32) | (0xFFFFFFFFu - ii.x);
+        if (sbest[islot[x]] != mine) {
+            dup[ii.x] = 1;
+            dup[ii.y] = 1;
+        }
+    }
 }
 
 __global__ __launch_bounds__(kT) void k_any(const uint8_t *__restrict__ dup, uint64_t n, unsigned int *__restrict__ any) {
@@ -551,7 +839,7 @@ static CandKey md_candkey(const oge_markdup_opts *opts, uint64_t n) {
 }
 
 int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
-                     OgeMdFrags *f) {
+                     OgeMdFrags *f, const uint64_t *skeys) {
     KeyLayout L;
     int rc = md_layout(ctx, opts, &L);
     if (rc) return rc;
@@ -566,8 +854,15 @@ int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *
     f->desc0 = want_desc ? (uint64_t *)ctx->scratch("md_desc0", (n + 1) * 8) : nullptr;
     if (!f->cpos || !f->fk || !f->fv || !f->cval || (want_desc && !f->desc0)) return OGE_ERR_HIP;
     const CandKey ckl = md_candkey(opts, n);
+    if (skeys) {
+        f->skeys = skeys;
+        // per-block deviation maxima: kDevSlots word pairs for the fragments, as many for the pairs
+        f->dev = (unsigned long long *)ctx->ws("md_devslots", 4 * kDevSlots * sizeof(unsigned long long));
+        if (!f->dev) return OGE_ERR_HIP;
+        OGE_HIP_TRY(ctx, hipMemsetAsync(f->dev, 0, 4 * kDevSlots * sizeof(unsigned long long), ctx->stream));
+    }
     hipLaunchKernelGGL(k_cand_frag, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, L, ckl, f->cpos, f->fk,
-                       f->fv, f->cval, f->desc0, cnt + 3);
+                       f->fv, f->cval, f->desc0, cnt + 3, skeys, f->dev);
     OGE_LAUNCH_CHECK(ctx);
     rc = oge_exclusive_scan_u32(ctx, f->cpos, f->cpos, n + 1);
     if (rc) return rc;
@@ -642,30 +937,21 @@ int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t 
     P->idx = (uint2 *)ctx->scratch("md_pidx", (uint64_t)np * sizeof(uint2));
     P->val = (uint32_t *)ctx->scratch("md_pv", (uint64_t)np * 4);
     if (!P->hi || !P->lo || !P->hk || !P->idx || !P->val) return OGE_ERR_HIP;
+    if (f.skeys) {
+        P->pax = (int64_t *)ctx->scratch("md_pax", (uint64_t)np * 8);
+        P->dev = f.dev + 2 * kDevSlots;
+        if (!P->pax) return OGE_ERR_HIP;
+    }
     hipLaunchKernelGGL(k_pair_build, dim3(oge_ceil_div(np, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)spairs, np, recs,
-                       meta, L, P->hi, P->lo, P->idx, P->val, P->hk);
+                       meta, L, P->hi, P->lo, P->idx, P->val, P->hk, f.skeys, P->pax, P->dev);
     OGE_LAUNCH_CHECK(ctx);
     return OGE_OK;
 }
 
+static int pair_groups_sorted(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t *hk, uint32_t *val, uint32_t m,
+                              const OgeMdPairs &P, uint8_t *dup);
 int oge_md_pair_groups(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &P, uint8_t *dup) {
-    const uint32_t np = P.np;
-    if (!np) return OGE_OK;
-    uint64_t *lo2 = (uint64_t *)ctx->scratch("md_lo2", (uint64_t)np * 8);
-    uint32_t *pv2 = (uint32_t *)ctx->scratch("md_pv2", (uint64_t)np * 4);
-    if (!lo2 || !pv2) return OGE_ERR_HIP;
-    // 32 bits of a hash of the whole chunk key (hk) group equal keys (k_pair_groups_h splits runs);
-    // debug_hash_bits (tests) also narrows these bits, so runs holding several keys are exercised
-    uint64_t *k2;
-    uint32_t *v2;
-    const int rb = opts->debug_hash_bits > 0 ? std::min(32, opts->debug_hash_bits) : 32;
-    const uint64_t rmask = ~0ull << (64 - rb);
-    int rc = oge_radix_sort_pairs(ctx, P.hk, P.val, lo2, pv2, np, rmask, &k2, &v2);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_pair_groups_h, dim3(oge_ceil_div(np, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)k2,
-                       (const uint32_t *)v2, (const uint64_t *)P.hi, (const uint64_t *)P.lo, (const uint2 *)P.idx, np, rmask, dup);
-    OGE_LAUNCH_CHECK(ctx);
-    return OGE_OK;
+    return pair_groups_sorted(ctx, opts, P.hk, P.val, P.np, P, dup);
 }
 
 int oge_md_frag_groups(oge_ctx *ctx, uint64_t *fk, uint32_t *fv, uint64_t n, uint8_t *dup) {
@@ -683,6 +969,144 @@ int oge_md_frag_groups(oge_ctx *ctx, uint64_t *fk, uint32_t *fv, uint64_t n, uin
     hipLaunchKernelGGL(k_frag_groups, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)k, (const uint32_t *)v, n,
                        dup);
     OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}
+
+// window bounds of every tile into scratch, and the list of tiles whose window exceeds cap
+struct WinPlan {
+    uint2 *bounds = nullptr;
+    uint32_t ntiles = 0;
+    uint32_t *ovl = nullptr;  // overflowing tiles (device)
+    uint32_t novf = 0;
+    uint64_t ovf_items = 0;   // window items of the overflowing tiles (bounds the owned items)
+};
+static int md_win_bounds(oge_ctx *ctx, const uint64_t *skeys, const int64_t *ax, uint64_t n, uint32_t cap,
+                         const unsigned long long *dev_slots, int64_t amax, WinPlan *W) {
+    W->ntiles = oge_ceil_div(n, kWinTile);
+    W->bounds = (uint2 *)ctx->scratch("md_winb", (uint64_t)W->ntiles * sizeof(uint2));
+    W->ovl = (uint32_t *)ctx->scratch("md_winovl", (uint64_t)W->ntiles * 4);
+    // cnt[0] = overflowing tiles, cnt[1..2] = their window items (u64)
+    unsigned int *cnt = (unsigned int *)ctx->ws("md_winovf", 16);
+    unsigned long long *dev = (unsigned long long *)ctx->ws("md_windev", 2 * sizeof(unsigned long long));
+    if (!W->bounds || !W->ovl || !cnt || !dev) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 16, ctx->stream));
+    hipLaunchKernelGGL(k_dev_fold, dim3(1), dim3(kDevSlots), 0, ctx->stream, dev_slots, dev);
+    OGE_LAUNCH_CHECK(ctx);
+    hipLaunchKernelGGL(k_win_bounds, dim3(oge_ceil_div(W->ntiles, kT)), dim3(kT), 0, ctx->stream, skeys, ax, n, W->ntiles, cap,
+                       (const unsigned long long *)dev, amax, W->bounds, W->ovl, cnt, (unsigned long long *)(cnt + 2));
+    OGE_LAUNCH_CHECK(ctx);
+    uint32_t h[4] = {0, 0, 0, 0};
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(h, cnt, 16, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    W->novf = h[0];
+    W->ovf_items = (uint64_t)h[2] | ((uint64_t)h[3] << 32);
+    return OGE_OK;
+}
+
+// OGE_MD_WINDOW=0 forces the sort-based group stages (A/B and tests)
+static bool md_window_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("OGE_MD_WINDOW");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
+// sort-based pair groups over (hk, val) lists of m pairs: hk's top rb bits group equal chunk keys,
+// k_pair_groups_h splits the runs into exact keys and picks each chunk's best explicitly
+static int pair_groups_sorted(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t *hk, uint32_t *val, uint32_t m,
+                              const OgeMdPairs &P, uint8_t *dup) {
+    if (!m) return OGE_OK;
+    uint64_t *lo2 = (uint64_t *)ctx->scratch("md_lo2", (uint64_t)m * 8);
+    uint32_t *pv2 = (uint32_t *)ctx->scratch("md_pv2", (uint64_t)m * 4);
+    if (!lo2 || !pv2) return OGE_ERR_HIP;
+    // 32 bits of a hash of the whole chunk key (hk) group equal keys (k_pair_groups_h splits runs);
+    // debug_hash_bits (tests) also narrows these bits, so runs holding several keys are exercised
+    uint64_t *k2;
+    uint32_t *v2;
+    const int rb = opts->debug_hash_bits > 0 ? std::min(32, opts->debug_hash_bits) : 32;
+    const uint64_t rmask = ~0ull << (64 - rb);
+    int rc = oge_radix_sort_pairs(ctx, hk, val, lo2, pv2, m, rmask, &k2, &v2);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_pair_groups_h, dim3(oge_ceil_div(m, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)k2,
+                       (const uint32_t *)v2, (const uint64_t *)P.hi, (const uint64_t *)P.lo, (const uint2 *)P.idx, m, rmask, dup);
+    OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}
+
+int oge_md_frag_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdFrags &f, uint64_t n, uint8_t *dup,
+                           bool *done) {
+    *done = false;
+    if (!f.skeys || !f.dev || !md_window_enabled() || opts->debug_sort_groups) return OGE_OK;
+    if (!n) { *done = true; return OGE_OK; }
+    KeyLayout L;
+    int rc = md_layout(ctx, opts, &L);
+    if (rc) return rc;
+    OgeStageTimer *t = ctx->begin_stage("md_frag_win");  // nested in md_frags: shows which path ran
+    // the unmapped tail (refID' = n_ref) holds no fragment
+    const int64_t amax = ((int64_t)opts->n_ref << 34) + (1ll << 32);
+    WinPlan W;
+    if ((rc = md_win_bounds(ctx, f.skeys, nullptr, n, kFragCap, f.dev, amax, &W))) return rc;
+    hipLaunchKernelGGL(k_frag_win, dim3(W.ntiles), dim3(kT), 0, ctx->stream, (const uint64_t *)f.fk, (const uint32_t *)f.fv,
+                       f.skeys, n, L, (const uint2 *)W.bounds, dup);
+    OGE_LAUNCH_CHECK(ctx);
+    ctx->end_stage(t);
+    if (W.novf) {  // the overflowing tiles' fragments through the sort-based stage
+        t = ctx->begin_stage("md_frag_ovf");
+        uint64_t *ok = (uint64_t *)ctx->scratch("md_ofk", W.ovf_items * 8 + 8);
+        uint32_t *ov = (uint32_t *)ctx->scratch("md_ofv", W.ovf_items * 4 + 4);
+        unsigned int *cnt = (unsigned int *)ctx->ws("md_ocnt", 4);
+        if (!ok || !ov || !cnt) return OGE_ERR_HIP;
+        OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 4, ctx->stream));
+        hipLaunchKernelGGL(k_win_collect<false>, dim3(W.novf), dim3(kT), 0, ctx->stream, (const uint64_t *)f.fk,
+                           (const uint32_t *)f.fv, (const uint64_t *)nullptr, (const uint64_t *)nullptr, f.skeys,
+                           (const int64_t *)nullptr, n, L, (const uint2 *)W.bounds, (const uint32_t *)W.ovl, ok, ov, cnt);
+        OGE_LAUNCH_CHECK(ctx);
+        unsigned int m = 0;
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&m, cnt, 4, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if ((rc = oge_md_frag_groups(ctx, ok, ov, m, dup))) return rc;
+        ctx->end_stage(t);
+    }
+    *done = true;
+    return OGE_OK;
+}
+
+int oge_md_pair_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &P, uint8_t *dup, bool *done) {
+    *done = false;
+    if (!P.pax || !P.dev || !md_window_enabled() || opts->debug_sort_groups) return OGE_OK;
+    if (!P.np) { *done = true; return OGE_OK; }
+    // debug_hash_bits narrows the sort-based path's hash to exercise its collision handling: keep it
+    if (opts->debug_hash_bits > 0) return OGE_OK;
+    KeyLayout L;
+    int rc = md_layout(ctx, opts, &L);
+    if (rc) return rc;
+    OgeStageTimer *t = ctx->begin_stage("md_pair_win");  // nested in md_pairs
+    WinPlan W;
+    if ((rc = md_win_bounds(ctx, nullptr, P.pax, P.np, kPairCap, P.dev, INT64_MAX, &W))) return rc;
+    hipLaunchKernelGGL(k_pair_win, dim3(W.ntiles), dim3(kT), 0, ctx->stream, (const uint64_t *)P.hi, (const uint64_t *)P.lo,
+                       (const uint2 *)P.idx, (const int64_t *)P.pax, (uint64_t)P.np, L, (const uint2 *)W.bounds, dup);
+    OGE_LAUNCH_CHECK(ctx);
+    ctx->end_stage(t);
+    if (W.novf) {  // the overflowing tiles' pairs through the sort-based stage
+        t = ctx->begin_stage("md_pair_ovf");
+        uint64_t *ok = (uint64_t *)ctx->scratch("md_ohk", W.ovf_items * 8 + 8);
+        uint32_t *ov = (uint32_t *)ctx->scratch("md_opv", W.ovf_items * 4 + 4);
+        unsigned int *cnt = (unsigned int *)ctx->ws("md_ocnt", 4);
+        if (!ok || !ov || !cnt) return OGE_ERR_HIP;
+        OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 4, ctx->stream));
+        hipLaunchKernelGGL(k_win_collect<true>, dim3(W.novf), dim3(kT), 0, ctx->stream, (const uint64_t *)P.hk,
+                           (const uint32_t *)nullptr, (const uint64_t *)P.hi, (const uint64_t *)P.lo,
+                           (const uint64_t *)nullptr, (const int64_t *)P.pax, (uint64_t)P.np, L, (const uint2 *)W.bounds,
+                           (const uint32_t *)W.ovl, ok, ov, cnt);
+        OGE_LAUNCH_CHECK(ctx);
+        unsigned int m = 0;
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&m, cnt, 4, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if ((rc = pair_groups_sorted(ctx, opts, ok, ov, m, P, dup))) return rc;
+        ctx->end_stage(t);
+    }
+    *done = true;
     return OGE_OK;
 }
 
@@ -729,7 +1153,7 @@ int oge_md_apply_inplace(oge_ctx *ctx, uint8_t *recs, const uint64_t *off, uint6
 // recs + off[i].
 int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
                        const oge_markdup_opts *opts, const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out,
-                       uint64_t *d_desc, bool *desc_ok) {
+                       uint64_t *d_desc, bool *desc_ok, const uint64_t *skeys) {
     if (desc_ok) *desc_ok = false;
     KeyLayout L;
     int rc = md_layout(ctx, opts, &L);
@@ -744,7 +1168,7 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     // ---- mate join ----
     OgeStageTimer *t = ctx->begin_stage("md_matejoin");
     OgeMdFrags F;
-    rc = oge_md_cand_frag(ctx, opts, meta, n, d_desc != nullptr, &F);
+    rc = oge_md_cand_frag(ctx, opts, meta, n, d_desc != nullptr, &F, skeys);
     if (rc) return rc;
     const bool use_desc = d_desc && !F.desc_ovf;
     OgeMdPairs P;
@@ -754,13 +1178,16 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
 
     // ---- pair groups ----
     t = ctx->begin_stage("md_pairs");
-    rc = oge_md_pair_groups(ctx, opts, P, d_dup);
+    bool done = false;
+    rc = oge_md_pair_groups_win(ctx, opts, P, d_dup, &done);
+    if (!rc && !done) rc = oge_md_pair_groups(ctx, opts, P, d_dup);
     if (rc) return rc;
     ctx->end_stage(t);
 
     // ---- fragment groups ----
     t = ctx->begin_stage("md_frags");
-    rc = oge_md_frag_groups(ctx, F.fk, F.fv, n, d_dup);  // fk / fv were written by k_cand_frag
+    rc = oge_md_frag_groups_win(ctx, opts, F, n, d_dup, &done);
+    if (!rc && !done) rc = oge_md_frag_groups(ctx, F.fk, F.fv, n, d_dup);  // fk / fv were written by k_cand_frag
     if (rc) return rc;
     ctx->end_stage(t);
 
@@ -805,7 +1232,7 @@ int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64
     rc = oge_input_pass(ctx, a);
     if (rc) return rc;
     ctx->end_stage(t);
-    return oge_markdup_finish(ctx, d_recs, d_off, n, opts, meta, d_dup, apply, n_dup_out, nullptr, nullptr);
+    return oge_markdup_finish(ctx, d_recs, d_off, n, opts, meta, d_dup, apply, n_dup_out, nullptr, nullptr, nullptr);
 }
 
 namespace {

@@ -23,22 +23,34 @@ struct OgeMdFrags {
     uint64_t *desc0 = nullptr;  // n gather descriptors (optional)
     uint32_t nc = 0;            // candidates
     bool desc_ovf = false;      // a record offset does not fit the descriptor
+    const uint64_t *skeys = nullptr;  // sorted coordinate keys (windowed fragment groups), optional
+    unsigned long long *dev = nullptr;  // per-block maxima of the fragment (then pair) coordinates' deviation from the anchors
 };
 
 struct OgeMdPairs {  // pair ReadEnds, np entries (see k_pair_build for the packing of hi / lo)
     uint64_t *hi = nullptr, *lo = nullptr, *hk = nullptr;
     uint2 *idx = nullptr;  // (read1 index, read2 index)
     uint32_t *val = nullptr;
+    int64_t *pax = nullptr;  // anchor of each pair's first record (windowed pair groups), optional
+    unsigned long long *dev = nullptr;
     uint32_t np = 0;
 };
 
+// skeys (optional): the records' coordinate sort keys when meta is in that sorted order; enables the
+// windowed group stages (oge_md_*_groups_win)
 int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
-                     OgeMdFrags *f);
+                     OgeMdFrags *f, const uint64_t *skeys = nullptr);
 // recs: the bytes RecMeta.src points into (only read for names that do not fit the summary)
 int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t *recs, const RecMeta *meta, uint64_t n,
                       const OgeMdFrags &f, OgeMdPairs *p);
 int oge_md_pair_groups(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &p, uint8_t *dup);
 int oge_md_frag_groups(oge_ctx *ctx, uint64_t *fk, uint32_t *fv, uint64_t n, uint8_t *dup);
+// The same two stages without a global sort, for items in sorted order (see k_frag_win / k_pair_win);
+// *done = false (nothing written) when a window overflows or the anchors are missing: run the sort
+// based stage instead.
+int oge_md_frag_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdFrags &f, uint64_t n, uint8_t *dup,
+                           bool *done);
+int oge_md_pair_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &p, uint8_t *dup, bool *done);
 int oge_md_apply_inplace(oge_ctx *ctx, uint8_t *recs, const uint64_t *off, uint64_t n, const RecMeta *meta, uint8_t *dup,
                          uint64_t *n_dup_out);
 int oge_md_apply_desc(oge_ctx *ctx, const uint64_t *desc0, uint64_t n, uint8_t *dup, uint64_t *desc, uint64_t *n_dup_out);

@@ -35,7 +35,7 @@ class MarkdupOpts(C.Structure):
 
     _fields_ = [
         ("n_ref", C.c_int32), ("rg_ids", C.c_void_p), ("rg_ids_bytes", C.c_uint64), ("rg_lib", C.c_void_p),
-        ("n_rg", C.c_int32), ("unknown_lib", C.c_int16), ("pad0", C.c_int16),
+        ("n_rg", C.c_int32), ("unknown_lib", C.c_int16), ("debug_sort_groups", C.c_int16),
         ("compat_nonverbose_index", C.c_int32), ("remove_duplicates", C.c_int32), ("debug_hash_bits", C.c_int32),
         ("split_chains", C.c_int32),
     ]

@@ -149,3 +149,48 @@ def test_sort_markdup_forced_hash_collisions(ctx, bits):
         f = int.from_bytes(out[int(oo[k]) + 18:int(oo[k]) + 20].tobytes(), "little")
         if odup[k] != 2:
             assert bool(f & 0x400) == bool(odup[k]), k
+
+
+def _fused_dup_flags(ctx, recs, offs, n, opts):
+    import torch
+    d_recs = torch.from_numpy(recs).cuda()
+    d_offs = torch.from_numpy(offs.view(np.int64)).cuda()
+    d_perm = torch.empty(n, dtype=torch.int32, device="cuda")
+    d_out = torch.zeros(recs.size + 16, dtype=torch.uint8, device="cuda")
+    d_oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    nd = ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(), d_out.data_ptr(),
+                              d_oo.data_ptr())
+    ctx.sync()
+    win = (ctx.timing("md_frag_win") >= 0, ctx.timing("md_pair_win") >= 0)
+    out, oo = d_out.cpu().numpy(), d_oo.cpu().numpy().view(np.uint64)
+    fl = np.array([int.from_bytes(out[int(oo[k]) + 18:int(oo[k]) + 20].tobytes(), "little") for k in range(n)])
+    return nd, fl, d_perm.cpu().numpy().view(np.uint32), win
+
+
+# (preset, pairs, seed, overrides, piles expected): the last case packs 40k pairs onto 3 kb of one
+# contig (~27 reads per position), so the fragment windows overflow and those tiles' fragments go
+# through the sort-based stage (k_win_collect)
+WIN_CASES = [("c2", 30000, 5, {}, False), ("mix", 4000, 17, {}, False), ("c1", 20000, 8, {"clip_ppm": 300_000}, False),
+             ("c1", 40000, 9, {"ref_len": [3000], "dup_ppm": 300_000}, True)]
+
+
+@pytest.mark.parametrize("preset,npairs,seed,over,windowed", WIN_CASES)
+def test_fused_windowed_groups_equal_sorted_groups(ctx, preset, npairs, seed, over, windowed):
+    """The windowed fragment / pair group stages (k_frag_win, k_pair_win) against the sort-based
+    ones (debug_sort_groups) and the oracle; dense piles overflow the windows and must fall back."""
+    p = L.synth_params(npairs, preset=preset, seed=seed, **over)
+    recs, offs, hdr = L.synth_host(p)
+    n = 2 * npairs
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    nd_w, fl_w, perm, win = _fused_dup_flags(ctx, recs, offs, n, opts)
+    assert win == (True, True)
+    assert (ctx.timing("md_frag_ovf") >= 0) == windowed
+    opts.debug_sort_groups = 1
+    nd_s, fl_s, perm_s, win_s = _fused_dup_flags(ctx, recs, offs, n, opts)
+    assert win_s == (False, False)
+    assert np.array_equal(perm, perm_s) and nd_w == nd_s and np.array_equal(fl_w, fl_s)
+    operm = oracle.sort_perm(recs, offs, n)
+    odup, ond = oracle.markdup(recs, offs[:-1][operm], n, hdr)
+    assert nd_w == ond
+    prim = odup != 2
+    assert np.array_equal((fl_w[prim] & 0x400) != 0, odup[prim] == 1)

@@ -26,9 +26,20 @@ if not src.exists():
     print(f"wrote {src} ({src.stat().st_size / 1e9:.2f} GB) in {time.perf_counter() - t:.1f} s", file=sys.stderr,
           flush=True)
     del recs, offs
-t0 = time.perf_counter()
-r = subprocess.run([str(ROOT / "openge_amd/openge"), "mergesort", "-M", "--nopg", "-v", "-t", str(th), str(src), "-o",
-                    str(out / "sorted_dedup.bam")], capture_output=True, text=True)
-dt = time.perf_counter() - t0
-print(json.dumps({"reads": n, "seconds": round(dt, 3), "mreads_per_s": round(n / dt / 1e6, 3), "threads": th,
-                  "rc": r.returncode, "stderr_tail": r.stderr[-1500:], "in_bytes": src.stat().st_size}))
+import os  # noqa: E402
+
+# E2E_POOL="1,0": one run per setting of OGE_POOL (the CLI's device memory pool), output removed between
+for pool in os.environ.get("E2E_POOL", "default").split(","):
+    env = dict(os.environ)
+    if pool != "default":
+        env["OGE_POOL"] = pool
+    dst = out / "sorted_dedup.bam"
+    if dst.exists():
+        dst.unlink()
+    t0 = time.perf_counter()
+    r = subprocess.run([str(ROOT / "openge_amd/openge"), "mergesort", "-M", "--nopg", "-v", "-t", str(th), str(src), "-o",
+                        str(dst)], capture_output=True, text=True, env=env)
+    dt = time.perf_counter() - t0
+    print(json.dumps({"reads": n, "pool": pool, "seconds": round(dt, 3), "mreads_per_s": round(n / dt / 1e6, 3),
+                      "threads": th, "rc": r.returncode, "stderr_tail": r.stderr[-1500:],
+                      "in_bytes": src.stat().st_size}), flush=True)
