@@ -476,8 +476,12 @@ __global__ __launch_bounds__(kT) void k_frag_groups(const uint64_t *__restrict__
 // larger than the tile's table (a pile of reads at one position) sends the whole stage to the
 // sort-based kernels above.
 constexpr uint32_t kWinTile = 512;   // items per tile
-constexpr uint32_t kFragCap = 2048;  // window items per fragment tile (LDS table of 2 x cap slots)
-constexpr uint32_t kPairCap = 1024;  // window items per pair tile
+// window items per tile, powers of two (a window of m items uses the smallest power of two >= 2m
+// table slots).  LDS: fragments 16 B x 2 cap = 32 KiB (4 blocks per CU), pairs 42 B x cap = 42 KiB;
+// C2 windows hold ~560 items.
+constexpr uint32_t kFragCap = 1024;
+constexpr uint32_t kPairCap = 1024;
+static_assert((kFragCap & (kFragCap - 1)) == 0 && (kPairCap & (kPairCap - 1)) == 0, "caps must be powers of two");
 
 __device__ __forceinline__ int64_t win_anchor(const uint64_t *__restrict__ skeys, const int64_t *__restrict__ ax, uint64_t i) {
     return skeys ? anchor_of_key(skeys[i]) : ax[i];
@@ -582,10 +586,10 @@ __device__ __forceinline__ uint32_t win_slots(uint32_t m) {  // power of two >= 
 // unpaired ends ((score + 2^15) << 32 | ~record index).
 __global__ __launch_bounds__(kT) void k_frag_win(const uint64_t *__restrict__ fk, const uint32_t *__restrict__ fv,
                                                   const uint64_t *__restrict__ skeys, uint64_t n, KeyLayout L,
-                                                  const uint2 *__restrict__ bounds, uint8_t *__restrict__ dup) {
+                                                  const uint2 *__restrict__ bounds, uint32_t cap, uint8_t *__restrict__ dup) {
     __shared__ unsigned long long skey[2 * kFragCap], sbest[2 * kFragCap];
     const uint2 b = bounds[blockIdx.x];
-    if (b.x >= b.y || b.y - b.x > kFragCap) return;  // owns nothing / overflow: k_win_collect's list
+    if (b.x >= b.y || b.y - b.x > cap) return;  // owns nothing / overflow (cap <= kFragCap): k_win_collect's list
     const WinTile w = win_tile(skeys, nullptr, n, blockIdx.x);
     const uint32_t H = win_slots(b.y - b.x);
     constexpr unsigned long long kEmpty = ~0ull, kPaired = 1ull << 63;
@@ -627,12 +631,13 @@ __global__ __launch_bounds__(kT) void k_frag_win(const uint64_t *__restrict__ fk
 // and the packed best ((score + 2^15) << 32 | ~read1 index).
 __global__ __launch_bounds__(kT) void k_pair_win(const uint64_t *__restrict__ hi, const uint64_t *__restrict__ lo,
                                                   const uint2 *__restrict__ idx, const int64_t *__restrict__ pax, uint64_t np,
-                                                  KeyLayout L, const uint2 *__restrict__ bounds, uint8_t *__restrict__ dup) {
+                                                  KeyLayout L, const uint2 *__restrict__ bounds, uint32_t cap,
+                                                  uint8_t *__restrict__ dup) {
     __shared__ unsigned long long ikh[kPairCap], ikl[kPairCap], sbest[2 * kPairCap];
     __shared__ uint32_t srep[2 * kPairCap];
     __shared__ uint16_t islot[kPairCap];
     const uint2 b = bounds[blockIdx.x];
-    if (b.x >= b.y || b.y - b.x > kPairCap) return;  // owns nothing / overflow: k_win_collect's list
+    if (b.x >= b.y || b.y - b.x > cap) return;  // owns nothing / overflow (cap <= kPairCap): k_win_collect's list
     const WinTile w = win_tile(nullptr, pax, np, blockIdx.x);
     const uint32_t m = b.y - b.x, H = win_slots(m);
     const uint64_t kmask = (1ull << 48) - 1, smask = (1ull << L.sb) - 1;
@@ -1003,13 +1008,16 @@ static int md_win_bounds(oge_ctx *ctx, const uint64_t *skeys, const int64_t *ax,
     return OGE_OK;
 }
 
-// OGE_MD_WINDOW=0 forces the sort-based group stages (A/B and tests)
+// OGE_MD_WINDOW=0 forces the sort-based group stages (A/B); OGE_MD_WINCAP=k (tests) lowers the window
+// caps so that most tiles overflow and take the collect + sort path.  Read per call.
 static bool md_window_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("OGE_MD_WINDOW");
-        return !(e && *e == '0');
-    }();
-    return on;
+    const char *e = getenv("OGE_MD_WINDOW");
+    return !(e && *e == '0');
+}
+static uint32_t md_win_cap(uint32_t cap) {
+    const char *e = getenv("OGE_MD_WINCAP");
+    const long v = e && *e ? atol(e) : 0;
+    return v > 0 && (uint64_t)v < cap ? (uint32_t)v : cap;
 }
 
 // sort-based pair groups over (hk, val) lists of m pairs: hk's top rb bits group equal chunk keys,
@@ -1046,9 +1054,10 @@ int oge_md_frag_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const Oge
     // the unmapped tail (refID' = n_ref) holds no fragment
     const int64_t amax = ((int64_t)opts->n_ref << 34) + (1ll << 32);
     WinPlan W;
-    if ((rc = md_win_bounds(ctx, f.skeys, nullptr, n, kFragCap, f.dev, amax, &W))) return rc;
+    const uint32_t cap = md_win_cap(kFragCap);
+    if ((rc = md_win_bounds(ctx, f.skeys, nullptr, n, cap, f.dev, amax, &W))) return rc;
     hipLaunchKernelGGL(k_frag_win, dim3(W.ntiles), dim3(kT), 0, ctx->stream, (const uint64_t *)f.fk, (const uint32_t *)f.fv,
-                       f.skeys, n, L, (const uint2 *)W.bounds, dup);
+                       f.skeys, n, L, (const uint2 *)W.bounds, cap, dup);
     OGE_LAUNCH_CHECK(ctx);
     ctx->end_stage(t);
     if (W.novf) {  // the overflowing tiles' fragments through the sort-based stage
@@ -1083,9 +1092,10 @@ int oge_md_pair_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const Oge
     if (rc) return rc;
     OgeStageTimer *t = ctx->begin_stage("md_pair_win");  // nested in md_pairs
     WinPlan W;
-    if ((rc = md_win_bounds(ctx, nullptr, P.pax, P.np, kPairCap, P.dev, INT64_MAX, &W))) return rc;
+    const uint32_t cap = md_win_cap(kPairCap);
+    if ((rc = md_win_bounds(ctx, nullptr, P.pax, P.np, cap, P.dev, INT64_MAX, &W))) return rc;
     hipLaunchKernelGGL(k_pair_win, dim3(W.ntiles), dim3(kT), 0, ctx->stream, (const uint64_t *)P.hi, (const uint64_t *)P.lo,
-                       (const uint2 *)P.idx, (const int64_t *)P.pax, (uint64_t)P.np, L, (const uint2 *)W.bounds, dup);
+                       (const uint2 *)P.idx, (const int64_t *)P.pax, (uint64_t)P.np, L, (const uint2 *)W.bounds, cap, dup);
     OGE_LAUNCH_CHECK(ctx);
     ctx->end_stage(t);
     if (W.novf) {  // the overflowing tiles' pairs through the sort-based stage

@@ -224,6 +224,9 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
         release();
         return 1;
     }
+    double t_kern = -1;
+    if (verbose_) oge_ctx_timing(cc.ctx, "bgzf_inflate", &t_kern);  // synchronises: the kernels' own time
+    const auto t2b = clk();
     oge_dev_free(cc.ctx, dz);
     dz = nullptr;
     comp = bytevec();
@@ -263,8 +266,10 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
     b.dev_valid = true;
     b.host_valid = false;
     if (verbose_)
-        fprintf(stderr, "[openge] FileReader (device): file %.3f s, upload %.3f s, inflate %.3f s, records %.3f s\n", sec(t0, t1),
-                sec(t1, t2), sec(t2, t3), sec(t3, clk()));
+        fprintf(stderr,
+                "[openge] FileReader (device): file %.3f s, upload %.3f s, inflate %.3f s (kernels %.3f s, release of the "
+                "compressed copies %.3f s), records %.3f s\n",
+                sec(t0, t1), sec(t1, t2), sec(t2, t3), t_kern / 1e3, sec(t2b, t3), sec(t3, clk()));
     return 0;
 }
 

@@ -194,3 +194,23 @@ def test_fused_windowed_groups_equal_sorted_groups(ctx, preset, npairs, seed, ov
     assert nd_w == ond
     prim = odup != 2
     assert np.array_equal((fl_w[prim] & 0x400) != 0, odup[prim] == 1)
+
+
+@pytest.mark.parametrize("cap", ["1", "300"])
+def test_fused_windowed_groups_overflow_path(ctx, monkeypatch, cap):
+    """OGE_MD_WINCAP shrinks the window caps: (nearly) every tile overflows, so the fragment and pair
+    groups go through k_win_collect + the sort-based kernels; the result must not change."""
+    p = L.synth_params(6000, preset="mix", seed=31)
+    recs, offs, hdr = L.synth_host(p)
+    n = 12000
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    monkeypatch.setenv("OGE_MD_WINCAP", cap)
+    nd_w, fl_w, perm, win = _fused_dup_flags(ctx, recs, offs, n, opts)
+    assert win == (True, True)
+    assert ctx.timing("md_frag_ovf") >= 0 and ctx.timing("md_pair_ovf") >= 0
+    monkeypatch.delenv("OGE_MD_WINCAP")
+    operm = oracle.sort_perm(recs, offs, n)
+    odup, ond = oracle.markdup(recs, offs[:-1][operm], n, hdr)
+    assert nd_w == ond
+    prim = odup != 2
+    assert np.array_equal((fl_w[prim] & 0x400) != 0, odup[prim] == 1)
