@@ -856,13 +856,25 @@ __global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z
     const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + t) * kIdxPos;
     uint32_t mine = 0;
     if (p0 < zbytes) {
+        // the thread's 16 positions + 4 bytes of look-ahead in registers (one 16-byte load + one dword):
+        // only a position whose 4 bytes are the gzip/deflate/FEXTRA signature 1f 8b 08 04 goes on to
+        // bgzf_head's global loads (a bare 0x1f byte every 256 stalled the wave on dependent loads)
         const uint32_t *w = (const uint32_t *)(z + p0);
-        uint32_t v[kIdxPos / 4];
+        uint32_t v[kIdxPos / 4 + 1];
+        if (p0 + kIdxPos <= zbytes) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 q = *(const u32x4 *)w;
+            v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+        } else {
 #pragma unroll
-        for (int k = 0; k < kIdxPos / 4; ++k) v[k] = p0 + 4 * k + 4 <= zbytes ? w[k] : 0;
+            for (int k = 0; k < kIdxPos / 4; ++k) v[k] = p0 + 4 * k + 4 <= zbytes ? w[k] : 0;
+        }
+        v[kIdxPos / 4] = p0 + kIdxPos + 4 <= zbytes ? w[kIdxPos / 4] : 0;
 #pragma unroll
-        for (int k = 0; k < kIdxPos; ++k)
-            if (((v[k >> 2] >> (8 * (k & 3))) & 0xff) == 31 && p0 + k < zbytes && bgzf_head(z, zbytes, p0 + k)) ++mine;
+        for (int k = 0; k < kIdxPos; ++k) {
+            const uint32_t sig = (k & 3) ? __builtin_amdgcn_alignbyte(v[(k >> 2) + 1], v[k >> 2], k & 3) : v[k >> 2];
+            if (sig == 0x04088b1fu && p0 + k < zbytes && bgzf_head(z, zbytes, p0 + k)) ++mine;
+        }
     }
     // block-wide exclusive prefix of the per-thread counts
     const uint32_t lane = t & 63, wv = t >> 6;
@@ -1198,6 +1210,26 @@ extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream,
         return OGE_OK;
     }
     const uint32_t TB = 128, G = oge_ceil_div(C, TB);
+    auto &RW = ctx->recwalk;
+    if (d_off && RW.stream == d_stream && RW.base == rec_base && RW.end == end && RW.n_ref == n_ref && RW.pos.size() == C) {
+        // the count-only call on this stream converged just before: fill from its chunk starts
+        const uint64_t n = RW.n;
+        RW.stream = nullptr;
+        if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(pos, RW.pos.data(), C * 8, hipMemcpyHostToDevice, ctx->stream));
+        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos, d_off);
+        OGE_LAUNCH_CHECK(ctx);
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &end, 8, hipMemcpyHostToDevice, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(he.data(), stop, C * 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(hc.data(), count, C * 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (he == RW.stop && hc == RW.count) {
+            *n_out = n;
+            return OGE_OK;
+        }
+        // the stream changed between the calls: the full walk below
+    }
+    RW.stream = nullptr;
     k_rec_guess<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, n_ref, CH, C, start);
     OGE_LAUNCH_CHECK(ctx);
     OGE_HIP_TRY(ctx, hipMemcpyAsync(hs.data(), start, C * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1227,7 +1259,11 @@ extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream,
     uint64_t n = 0;
     for (uint64_t c = 0; c < C; ++c) hp[c] = n, n += hc[c];
     *n_out = n;
-    if (!d_off) return OGE_OK;
+    if (!d_off) {
+        RW.stream = d_stream, RW.base = rec_base, RW.end = end, RW.n_ref = n_ref, RW.n = n;
+        RW.stop = he, RW.count = hc, RW.pos = hp;
+        return OGE_OK;
+    }
     if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
     OGE_HIP_TRY(ctx, hipMemcpyAsync(pos, hp.data(), C * 8, hipMemcpyHostToDevice, ctx->stream));
     k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos, d_off);

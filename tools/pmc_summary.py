@@ -14,12 +14,28 @@ import sys
 from pathlib import Path
 
 
-def per_kernel(path):
+def per_kernel(path, totals=None):
     agg = {}
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
         agg.setdefault(k, []).append(float(r["Counter_Value"]) * 1024.0)
+    if totals is not None:
+        totals.update({k: sum(v) for k, v in agg.items()})
     return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+# stages made of several kernels / launches (STAGES="k_defl=2,k_infl=1": the prefix and how many times
+# the stage ran in the profiled command): one entry per stage with its bytes per run, listed first so
+# bench.py's pmc_traffic finds the stage before any single kernel of it
+def stage_entries(ft, wt, spec):
+    out = {}
+    for item in filter(None, spec.split(",")):
+        pre, runs = item.split("=")
+        f = sum(v for k, v in ft.items() if pre + "_" in k) / float(runs)
+        w = sum(v for k, v in wt.items() if pre + "_" in k) / float(runs)
+        out[f"{pre} (stage: all {pre}_* launches of one run)"] = {"fetch_size_bytes": f, "write_size_bytes": w,
+                                                                  "hbm_bytes": 2 * f + w}
+    return out
 
 
 def main():
@@ -35,9 +51,12 @@ def main():
     write = src / "pmc_WRITE_SIZE" / "run_counter_collection.csv"
     if not (fetch.exists() and write.exists()):
         return
-    f, w = per_kernel(fetch), per_kernel(write)
+    import os
+    ft, wt = {}, {}
+    f, w = per_kernel(fetch, ft), per_kernel(write, wt)
     bench = json.loads((src / "pmc_FETCH_SIZE.json").read_text())
-    out = {"workload": bench["config"], "note": "bytes per launch; hbm = 2*FETCH_SIZE + WRITE_SIZE", "kernels": {}}
+    out = {"workload": bench["config"], "note": "bytes per launch; hbm = 2*FETCH_SIZE + WRITE_SIZE",
+           "kernels": stage_entries(ft, wt, os.environ.get("STAGES", ""))}
     for k in sorted(set(f) | set(w), key=lambda k: -(2 * f.get(k, 0) + w.get(k, 0))):
         out["kernels"][k] = {"fetch_size_bytes": f.get(k), "write_size_bytes": w.get(k),
                              "hbm_bytes": 2 * f.get(k, 0) + w.get(k, 0)}
