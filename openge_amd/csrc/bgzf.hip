@@ -99,7 +99,10 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
 // PS: padded layouts (bgzf_dev.h pw) -- every thread's 64-byte segment of `in` starts in its own bank
 // for the greedy parse (PS = 4), or none (PS = 31).  The payload CRC is computed by k_defl_emit, so this
 // kernel's LDS (one workgroup per CU) leaves room for an emit or Huffman workgroup of another chunk.
-template <int PS>
+// R: positions per thread per candidate round (rounds of R * 512 consecutive positions; a position
+// sees the hash table as the earlier rounds left it).  Fewer, fuller rounds cut the barriers per
+// payload (128 at R = 1) at the price of not seeing the rest of its own round.
+template <int PS, int R>
 __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
                                                     uint32_t *__restrict__ tok, uint8_t *__restrict__ ntok,
                                                     uint32_t *__restrict__ freq_out) {
@@ -127,20 +130,28 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
             continue;
         }
         const uint32_t end = min(len, base + kSub);
-        // candidates, one round of kT consecutive positions at a time
-        for (uint32_t r = base; r < end; r += kT) {
-            const uint32_t p = r + t;
-            uint32_t h = 0, c = 0;
-            const bool ok = p + 4 <= len;
-            if (ok) {
-                const uint32_t w = ld32p<PS>(in, p);
-                h = hash4(w);
-                const uint32_t j1 = htab[h];
-                if (j1 && p - (j1 - 1) <= 32768 && ld32p<PS>(in, j1 - 1) == w) c = j1;
+        // candidates, one round of R * kT consecutive positions at a time
+        for (uint32_t r = base; r < end; r += R * kT) {
+            uint32_t hh[R];
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const uint32_t p = r + k * kT + t;
+                uint32_t h = 0, c = 0;
+                if (p + 4 <= len) {
+                    const uint32_t w = ld32p<PS>(in, p);
+                    h = hash4(w);
+                    const uint32_t j1 = htab[h];
+                    if (j1 && p - (j1 - 1) <= 32768 && ld32p<PS>(in, j1 - 1) == w) c = j1;
+                }
+                hh[k] = h;
+                if (p < end) cand[cix(p - base)] = (uint16_t)c;
             }
-            if (p < end) cand[cix(p - base)] = (uint16_t)c;
             __syncthreads();
-            if (ok) atomicMax(&htab[h], p + 1);
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const uint32_t p = r + k * kT + t;
+                if (p + 4 <= len && p < end) atomicMax(&htab[hh[k]], p + 1);
+            }
             __syncthreads();
         }
         // greedy parse of this thread's segment
@@ -693,6 +704,12 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
         return (uint64_t)std::min<long>(std::max<long>(v, 256), kMaxChunk);
     }();
     const uint64_t chunk = std::min<uint64_t>(nblk, chunk_max);
+    // OGE_DEFL_CAND_R = 1 | 2 | 4: positions per thread per candidate round.  20M C2 reads: 70.0 / 72.2 /
+    // 72.5 GB/s at ratio 0.6991 / 0.7007 / 0.7030 (profiles/r02s3_defl_r.json): 2 by default
+    static const int cand_r = [] {
+        const char *e = getenv("OGE_DEFL_CAND_R");
+        return e && *e ? atoi(e) : 2;
+    }();
     static const bool pad = [] {  // OGE_DEFL_PAD=0: unpadded tokens LDS layout (A/B)
         const char *e = getenv("OGE_DEFL_PAD");
         return !(e && atoi(e) == 0);
@@ -745,8 +762,10 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk, ++k) {
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
         Bufs &u = B[k % S];
-        if (pad) k_defl_tokens<4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else k_defl_tokens<31><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        if (!pad) k_defl_tokens<31, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        else if (cand_r >= 4) k_defl_tokens<4, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        else if (cand_r == 2) k_defl_tokens<4, 2><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        else k_defl_tokens<4, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         OGE_LAUNCH_CHECK(ctx);
         k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs);
         OGE_LAUNCH_CHECK(ctx);

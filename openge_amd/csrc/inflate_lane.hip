@@ -840,10 +840,13 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     // OGE_INFL_CFG (experiments): 0 = 12 waves per CU with the long-code lists in global scratch only,
     // 1 = 12 waves with list heads in LDS, 3 = the same with one code per step (MODE), 2 = 8 waves with
     // longer list heads in LDS (MODE), 4 = 16 waves, 5 / 6 = 1 / 3 with byte stores (DIRECT)
+    // Default 0: in the 300M-read chain (7 launches of 196,608 blocks) it inflates in 1157 ms against
+    // 1615 ms for 1 and 1629 ms for 3 (profiles/r02s3_infl_cfg.json); the 150M codec A/B that had
+    // picked 1 ran shorter launches on its own.
     static const int cfg = [] {
         const char *e = getenv("OGE_INFL_CFG");
-        const int c = e ? atoi(e) : 1;
-        return (c >= 0 && c <= 6) ? c : 1;
+        const int c = e ? atoi(e) : 0;
+        return (c >= 0 && c <= 6) ? c : 0;
     }();
     const int wps = cfg == 4 ? 4 : cfg == 2 ? 2 : 3;
     const uint64_t lanes = (uint64_t)ncu * 4 * wps * 64;
