@@ -102,7 +102,11 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
 // R: positions per thread per candidate round (rounds of R * 512 consecutive positions; a position
 // sees the hash table as the earlier rounds left it).  Fewer, fuller rounds cut the barriers per
 // payload (128 at R = 1) at the price of not seeing the rest of its own round.
-template <int PS, int R>
+// LB: literals per parse step.  A position without a candidate is a literal, and so are the
+// candidate-free positions right after it: a lane emits up to LB of them in one step, so a wave's
+// step count (the maximum over its 64 segments) drops for literal-heavy payload (BAM qualities)
+// while the tokens stay those of the one-symbol parse.
+template <int PS, int R, int LB>
 __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
                                                     uint32_t *__restrict__ tok, uint8_t *__restrict__ ntok,
                                                     uint32_t *__restrict__ freq_out) {
@@ -160,6 +164,18 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
         uint32_t *tp = tok + ((uint64_t)blockIdx.x * kNSub + sub) * kSeg * kT + t;
         for (uint32_t p = s0; p < s1;) {
             const uint32_t c = p < s1 ? cand[cix(p - base)] : 0;
+            if (LB > 1 && !c) {
+#pragma unroll
+                for (int q = 0; q < LB; ++q) {
+                    if (q > 0 && (p >= s1 || cand[cix(p - base)] != 0)) break;
+                    const uint32_t b = byte_at<PS>(in, p);
+                    atomicAdd(&freq[b], 1u);
+                    tp[(uint64_t)k * kT] = b;
+                    ++k;
+                    ++p;
+                }
+                continue;
+            }
             uint32_t L = 0;
             if (c) {
                 const uint32_t j = c - 1;
@@ -710,6 +726,10 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
         const char *e = getenv("OGE_DEFL_CAND_R");
         return e && *e ? atoi(e) : 2;
     }();
+    static const int lit_batch = [] {  // OGE_DEFL_LITB = 1 | 2 | 4: literals per parse step (with R = 2)
+        const char *e = getenv("OGE_DEFL_LITB");
+        return e && *e ? atoi(e) : 1;
+    }();
     static const bool pad = [] {  // OGE_DEFL_PAD=0: unpadded tokens LDS layout (A/B)
         const char *e = getenv("OGE_DEFL_PAD");
         return !(e && atoi(e) == 0);
@@ -762,10 +782,12 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk, ++k) {
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
         Bufs &u = B[k % S];
-        if (!pad) k_defl_tokens<31, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (cand_r >= 4) k_defl_tokens<4, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (cand_r == 2) k_defl_tokens<4, 2><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else k_defl_tokens<4, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        if (!pad) k_defl_tokens<31, 1, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        else if (lit_batch >= 4) k_defl_tokens<4, 2, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        else if (lit_batch == 2) k_defl_tokens<4, 2, 2><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        else if (cand_r >= 4) k_defl_tokens<4, 4, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        else if (cand_r == 2) k_defl_tokens<4, 2, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        else k_defl_tokens<4, 1, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         OGE_LAUNCH_CHECK(ctx);
         k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs);
         OGE_LAUNCH_CHECK(ctx);
