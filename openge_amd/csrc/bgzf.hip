@@ -181,13 +181,29 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
                 const uint32_t j = c - 1;
                 const uint32_t maxL = min(258u, s1 - p);
                 L = min(4u, maxL);
-                while (L < maxL) {
-                    const uint32_t x = ld32p<PS>(in, p + L) ^ ld32p<PS>(in, j + L);
-                    if (x == 0) {
-                        L += 4;
-                    } else {
-                        L += __builtin_ctz(x) >> 3;
-                        break;
+                if (LB > 1) {  // 8 bytes per step
+                    while (L < maxL) {
+                        const uint32_t x0 = ld32p<PS>(in, p + L) ^ ld32p<PS>(in, j + L);
+                        const uint32_t x1 = ld32p<PS>(in, p + L + 4) ^ ld32p<PS>(in, j + L + 4);
+                        if (x0) {
+                            L += __builtin_ctz(x0) >> 3;
+                            break;
+                        }
+                        if (x1) {
+                            L += 4 + (__builtin_ctz(x1) >> 3);
+                            break;
+                        }
+                        L += 8;
+                    }
+                } else {
+                    while (L < maxL) {
+                        const uint32_t x = ld32p<PS>(in, p + L) ^ ld32p<PS>(in, j + L);
+                        if (x == 0) {
+                            L += 4;
+                        } else {
+                            L += __builtin_ctz(x) >> 3;
+                            break;
+                        }
                     }
                 }
                 L = min(L, maxL);
