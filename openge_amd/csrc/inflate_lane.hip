@@ -202,7 +202,12 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
 // `md`), so a step has one refill, one extra-bits read and one output write whichever code it is;
 // otherwise a step decodes a whole symbol (a match's length and distance codes in the same step).
 // DIRECT: every output byte is its own byte store (no 8-byte accumulator to keep and flush).
-template <int WPS, int SLL, int SLD, bool MODE, bool DIRECT = false>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
+// LB (one-code-per-step path): a literal decoded from the direct table may be followed, in the same
+// step, by up to LB - 1 more literals whose codes also sit in the direct table (<= 6 bits each: the
+// >= 33 buffered bits cover four, then a refill); a wave's step count is the maximum over its 64
+// blocks' symbol counts, so literal runs (BAM qualities, bases) take fewer steps.  300M reads in the
+// chain: LB = 1 / 2 / 4 -> 1152 / 941 / 792 ms (profiles/r02s3_infl_litb.json).
+template <int WPS, int SLL, int SLD, bool MODE, bool DIRECT = false, int LB = 1>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
 __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
                                                      const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
                                                      const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
@@ -521,6 +526,17 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 } else {
                     put(pos, sym, 1);
                     ++pos;
+                    if (LB > 1 && e) {  // more direct-table literals in this step
+#pragma unroll
+                        for (int q = 1; q < LB; ++q) {
+                            if (q % 4 == 0) refill();  // >= 33 bits again for the next four
+                            const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TBL) - 1)][lane];
+                            if (!e2 || (e2 & 511) >= 256 || pos >= osz) break;
+                            skip(e2 >> 9);
+                            put(pos, e2 & 511, 1);
+                            ++pos;
+                        }
+                    }
                 }
             } else if (sym == 256) {
                 if (fin) block_end();
@@ -848,6 +864,10 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         const int c = e ? atoi(e) : 0;
         return (c >= 0 && c <= 6) ? c : 0;
     }();
+    static const int litb = [] {  // OGE_INFL_LITB = 1 | 2 | 4 | 6 | 8: literals per step (cfg 0)
+        const char *e = getenv("OGE_INFL_LITB");
+        return e && *e ? atoi(e) : 4;
+    }();
     const int wps = cfg == 4 ? 4 : cfg == 2 ? 2 : 3;
     const uint64_t lanes = (uint64_t)ncu * 4 * wps * 64;
     const uint64_t nchunks = std::max<uint64_t>(1, (nblk + lanes - 1) / lanes);
@@ -861,6 +881,10 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
         if (cfg == 4) k_infl_huff<4, 0, 0, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 2) k_infl_huff<2, 136, 24, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 0 && litb >= 8) k_infl_huff<3, 0, 0, false, false, 8><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 0 && litb >= 6) k_infl_huff<3, 0, 0, false, false, 6><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 0 && litb >= 4) k_infl_huff<3, 0, 0, false, false, 4><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 0 && litb >= 2) k_infl_huff<3, 0, 0, false, false, 2><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 0) k_infl_huff<3, 0, 0, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 3) k_infl_huff<3, 36, 13, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 5) k_infl_huff<3, 36, 13, false, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
