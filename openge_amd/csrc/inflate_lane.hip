@@ -53,12 +53,12 @@ constexpr int TBL = 6, TBD = 4;  // direct-table bits: literal/length, distance
 // Sizes that fill the LDS left at WPS waves per SIMD (4 SIMDs, 512-byte allocation granules): WPS 3 ->
 // 36 + 13 (13312 B per wave), WPS 2 -> 136 + 24 (20416 B per wave).
 // per-wave LDS, lane-interleaved ([entry][lane]): element e of lane l at e * 64 + l
-template <int SLL, int SLD>
+template <int SLL, int SLD, int TL = TBL, int TD = TBD>
 struct P1Lds {
     static constexpr uint32_t kSLL = SLL, kSLD = SLD;
-    uint16_t lt[1 << TBL][64];  // sym | L << 9, 0 = longer code; while code lengths are decoded a lane's
+    uint16_t lt[1 << TL][64];  // sym | L << 9, 0 = longer code; while code lengths are decoded a lane's
                                 // column holds its 7-bit code-length table (cl_at): sym | L << 5
-    uint8_t dt[1 << TBD][64];   // sym | L << 5, 0 = longer code
+    uint8_t dt[1 << TD][64];    // sym | L << 5, 0 = longer code
     uint32_t cnt[16], lo[16], first[16], offl[16], run[16], lim[16], lie[16];  // the build's per-length values
     uint64_t clp[64];           // a lane's code-length-code lengths between its header and its CL build
     uint8_t ll[SLL > 0 ? SLL : 1][64];  // head of the literal/length long-code list
@@ -152,9 +152,9 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
     for (int d = 1; d < 16; d <<= 1) ks += __shfl_xor(ks, d, 64);
     ks = __builtin_amdgcn_readfirstlane(ks);
     if (ks > 32768u) return false;
-    if (lane < (1u << TB)) {  // zero lane j's column of the direct table
-        if (LIT) S.lt[lane][j] = 0;
-        else S.dt[lane][j] = 0;
+    for (uint32_t r = lane; r < (1u << TB); r += 64) {  // zero lane j's column of the direct table
+        if (LIT) S.lt[r][j] = 0;
+        else S.dt[r][j] = 0;
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -207,13 +207,16 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
 // >= 33 buffered bits cover four, then a refill); a wave's step count is the maximum over its 64
 // blocks' symbol counts, so literal runs (BAM qualities, bases) take fewer steps.  300M reads in the
 // chain: LB = 1 / 2 / 4 -> 1152 / 941 / 792 ms (profiles/r02s3_infl_litb.json).
-template <int WPS, int SLL, int SLD, bool MODE, bool DIRECT = false, int LB = 1>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
+// TL / TD: direct-table bits of the literal/length and distance codes (the slow paths count the
+// canonical limits from lengths 7 and 5 up, which holds for any TL <= 7, TD <= 5: a code longer than
+// the table is at or past every shorter length's limit).
+template <int WPS, int SLL, int SLD, bool MODE, bool DIRECT = false, int LB = 1, int TL = TBL, int TD = TBD>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
 __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
                                                      const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
                                                      const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
                                                      uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
                                                      uint8_t *__restrict__ scratch, uint32_t *__restrict__ err) {
-    __shared__ P1Lds<SLL, SLD> S;
+    __shared__ P1Lds<SLL, SLD, TL, TD> S;
     const uint32_t lane = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
     const uint64_t stride = (uint64_t)gridDim.x * 64;
@@ -399,13 +402,13 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                     if (s < hl) ll[r] = fx ? (s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8) : sj[S_LENS + s];
                 }
                 dl[0] = lane < hd ? (fx ? 5u : (uint32_t)sj[S_LENS + hl + lane]) : 0u;
-                bool ok = wbuild<5, TBL, true>(S, j, sj + S_LS, ll, hl);
+                bool ok = wbuild<5, TL, true>(S, j, sj + S_LS, ll, hl);
                 if (ok && lane == j) {
                     sfor<4>([&](auto k) { T.ll[k()] = S.lim[7 + 2 * k()] | (S.lim[8 + 2 * k()] << 16); });
                     T.l15 = S.lim[15];
                     sfor<9>([&](auto k) { T.lie[k()] = S.lie[7 + k()]; });
                 }
-                ok = ok && wbuild<1, TBD, false>(S, j, sj + S_DS, dl, hd);
+                ok = ok && wbuild<1, TD, false>(S, j, sj + S_DS, dl, hd);
                 if (lane == j) {
                     if (!ok) {
                         fail(E_TABLE);
@@ -444,8 +447,8 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
         if (MODE && st == ST_SYM) {
             refill();  // >= 33 bits: a code (<= 15) and its extra bits (<= 13)
             const uint32_t v = (uint32_t)buf;
-            const uint32_t e0 = S.lt[v & ((1u << TBL) - 1)][lane];
-            const uint32_t d0 = S.dt[v & ((1u << TBD) - 1)][lane];
+            const uint32_t e0 = S.lt[v & ((1u << TL) - 1)][lane];
+            const uint32_t d0 = S.dt[v & ((1u << TD) - 1)][lane];
             uint32_t sym = md ? (d0 & 31) : (e0 & 511), L = md ? (d0 >> 5) : (e0 >> 9);
             if (!(md ? d0 : e0)) {  // code longer than the direct table
                 const uint32_t c15 = __builtin_bitreverse32(v) >> 17;
@@ -503,7 +506,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
         } else if (!MODE && st == ST_SYM) {
             refill();
             const uint32_t v = (uint32_t)buf;
-            const uint32_t e = S.lt[v & ((1u << TBL) - 1)][lane];
+            const uint32_t e = S.lt[v & ((1u << TL) - 1)][lane];
             uint32_t sym, L;
             if (e) {
                 sym = e & 511, L = e >> 9;
@@ -530,7 +533,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
 #pragma unroll
                         for (int q = 1; q < LB; ++q) {
                             if (q % 4 == 0) refill();  // >= 33 bits again for the next four
-                            const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TBL) - 1)][lane];
+                            const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
                             if (!e2 || (e2 & 511) >= 256 || pos >= osz) break;
                             skip(e2 >> 9);
                             put(pos, e2 & 511, 1);
@@ -550,7 +553,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 const uint32_t len = base + get(ext);
                 refill();
                 const uint32_t w = (uint32_t)buf;
-                const uint32_t de = S.dt[w & ((1u << TBD) - 1)][lane];
+                const uint32_t de = S.dt[w & ((1u << TD) - 1)][lane];
                 uint32_t ds, DL;
                 if (de) {
                     ds = de & 31, DL = de >> 5;
@@ -855,20 +858,21 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     // round of waves would run at a fraction of the occupancy); chunks are balanced
     // OGE_INFL_CFG (experiments): 0 = 12 waves per CU with the long-code lists in global scratch only,
     // 1 = 12 waves with list heads in LDS, 3 = the same with one code per step (MODE), 2 = 8 waves with
-    // longer list heads in LDS (MODE), 4 = 16 waves, 5 / 6 = 1 / 3 with byte stores (DIRECT)
+    // longer list heads in LDS (MODE), 4 = 16 waves, 5 / 6 = 1 / 3 with byte stores (DIRECT),
+    // 7 = 0 with a 5-bit distance table, 8 = 8 waves with a 7-bit literal/length table (both batched)
     // Default 0: in the 300M-read chain (7 launches of 196,608 blocks) it inflates in 1157 ms against
     // 1615 ms for 1 and 1629 ms for 3 (profiles/r02s3_infl_cfg.json); the 150M codec A/B that had
     // picked 1 ran shorter launches on its own.
     static const int cfg = [] {
         const char *e = getenv("OGE_INFL_CFG");
         const int c = e ? atoi(e) : 0;
-        return (c >= 0 && c <= 6) ? c : 0;
+        return (c >= 0 && c <= 8) ? c : 0;
     }();
     static const int litb = [] {  // OGE_INFL_LITB = 1 | 2 | 4 | 6 | 8: literals per step (cfg 0)
         const char *e = getenv("OGE_INFL_LITB");
         return e && *e ? atoi(e) : 4;
     }();
-    const int wps = cfg == 4 ? 4 : cfg == 2 ? 2 : 3;
+    const int wps = cfg == 4 ? 4 : (cfg == 2 || cfg == 8) ? 2 : 3;
     const uint64_t lanes = (uint64_t)ncu * 4 * wps * 64;
     const uint64_t nchunks = std::max<uint64_t>(1, (nblk + lanes - 1) / lanes);
     const uint64_t chunk = std::max<uint64_t>(1, (nblk + nchunks - 1) / nchunks);
@@ -881,6 +885,8 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
         if (cfg == 4) k_infl_huff<4, 0, 0, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 2) k_infl_huff<2, 136, 24, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 7) k_infl_huff<3, 0, 0, false, false, 4, 6, 5><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        else if (cfg == 8) k_infl_huff<2, 0, 0, false, false, 4, 7, 4><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 0 && litb >= 8) k_infl_huff<3, 0, 0, false, false, 8><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 0 && litb >= 6) k_infl_huff<3, 0, 0, false, false, 6><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 0 && litb >= 4) k_infl_huff<3, 0, 0, false, false, 4><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
