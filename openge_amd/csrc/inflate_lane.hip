@@ -799,19 +799,10 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     uint8_t *img = (uint8_t *)refs;
     uint32_t *img32 = (uint32_t *)refs;
     auto ib = [](uint32_t q) { return q + ((q >> 7) << 2); };
-    {
-        const uint32_t sh = (uint32_t)((uintptr_t)O & 3);
-        const OGE_G uint32_t *W = (const OGE_G uint32_t *)((uintptr_t)O & ~(uintptr_t)3);
-        const uintptr_t lim = (uintptr_t)(O + osz);
-        const uint32_t nd = (osz + 3) >> 2;
-#pragma unroll 4
-        for (uint32_t k = 0; k < 32; ++k) {
-            const uint32_t w = 512 * k + t;
-            if (w >= nd) break;
-            const uint32_t a0 = W[w], a1 = (uintptr_t)(W + w + 1) < lim ? W[w + 1] : 0u;
-            img32[pw<PS>(w)] = sh ? __builtin_amdgcn_alignbyte(a1, a0, sh) : a0;
-        }
-    }
+    // from the registers of step 1: this thread's 128 bytes [q0, q0 + 128) are words 32 t .. 32 t + 31,
+    // padded to 33 t + k (a lane's words at a 33-word stride: distinct banks), no second global read
+#pragma unroll
+    for (uint32_t k = 0; k < 32; ++k) img32[33 * t + k] = wv[k];
     __syncthreads();
     // 6. every copied byte from its root (a literal position of the image); literal-only chunks are
     //    already in place
