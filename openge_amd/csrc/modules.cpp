@@ -12,6 +12,9 @@
 #include <functional>
 #include <atomic>
 #include <thread>
+#include <unistd.h>
+#include <sys/stat.h>
+#include <fcntl.h>
 
 #include "bam_layout.h"
 
@@ -177,6 +180,78 @@ int AlgorithmModule::runChain(ChainContext &cc) {
 }
 
 // ----------------------------------------------------------------------------------- FileReader
+// The file streamed into HBM through two page-locked buffers (parallel preads of one while the other
+// is copied), indexed on the device: no host copy of the whole file to allocate, fault in and unmap
+// (a 29 GB file's unmap alone took 1.5 s).  Returns 2 when it does not apply (small files, inputs
+// close to the HBM size, a framing the device index rejects) -- the caller then takes the host path.
+static int stream_to_device(ChainContext &cc, const std::string &path, int threads, void **dz_out, uint64_t *zbytes) {
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) return 2;
+    struct stat stt;
+    const char *mn = getenv("OGE_STREAM_MIN");  // smallest file streamed (bytes; tests lower it)
+    const long long smin = mn && *mn ? atoll(mn) : (64ll << 20);
+    if (fstat(fd, &stt) || !S_ISREG(stt.st_mode) || stt.st_size < smin || stt.st_size < 1) {
+        close(fd);
+        return 2;
+    }
+    const uint64_t Z = (uint64_t)stt.st_size;
+    uint64_t fr = 0, tot = 0;
+    if (oge_mem_info(cc.ctx, &fr, &tot) || Z / 10 * 40 > fr) {  // leave the host path to size what follows
+        close(fd);
+        return 2;
+    }
+    void *dz = nullptr, *hb[2] = {nullptr, nullptr};
+    const uint64_t CH = getenv("OGE_STREAM_MIN") ? (64ull << 10) : (256ull << 20);  // tests: many small chunks
+    auto cleanup = [&]() {
+        for (void *h : hb)
+            if (h) oge_host_free(cc.ctx, h);
+        close(fd);
+    };
+    if (oge_dev_alloc(cc.ctx, Z + 16, &dz) || oge_host_alloc(cc.ctx, CH, &hb[0]) || oge_host_alloc(cc.ctx, CH, &hb[1])) {
+        if (dz) oge_dev_free(cc.ctx, dz);
+        cleanup();
+        return 2;
+    }
+    const uint64_t nch = (Z + CH - 1) / CH;
+    std::atomic<bool> bad(false);
+    auto read_chunk = [&](uint64_t c) {  // chunk c into hb[c & 1], 8 preads of 32 MB in parallel
+        const uint64_t o0 = c * CH, e0 = std::min(Z, o0 + CH);
+        const uint64_t sl = 32ull << 20, ns = (e0 - o0 + sl - 1) / sl;
+        std::vector<std::thread> ts;
+        for (uint64_t k = 0; k < ns; ++k)
+            ts.emplace_back([&, k]() {
+                uint64_t o = o0 + k * sl;
+                const uint64_t e = std::min(e0, o + sl);
+                while (o < e) {
+                    const ssize_t r = pread(fd, (uint8_t *)hb[c & 1] + (o - o0), e - o, (off_t)o);
+                    if (r <= 0) {
+                        bad = true;
+                        return;
+                    }
+                    o += (uint64_t)r;
+                }
+            });
+        for (auto &t : ts) t.join();
+    };
+    (void)threads;
+    read_chunk(0);
+    for (uint64_t c = 0; c < nch && !bad; ++c) {
+        std::thread next;
+        if (c + 1 < nch) next = std::thread(read_chunk, c + 1);
+        const uint64_t o = c * CH, len = std::min(Z, o + CH) - o;
+        if (oge_memcpy(cc.ctx, (uint8_t *)dz + o, hb[c & 1], len, 1)) bad = true;
+        if (next.joinable()) next.join();
+    }
+    cleanup();
+    if (bad) {
+        oge_dev_free(cc.ctx, dz);
+        return 2;
+    }
+    *dz_out = dz;
+    *zbytes = Z;
+    return 0;
+}
+
 int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &path) {
     auto clk = [] { return std::chrono::steady_clock::now(); };
     auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
@@ -186,40 +261,69 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
     const int threads = cc.threads > 0 ? cc.threads : 8;
     bytevec comp;
     std::string err;
-    if (!read_file_bytes(path, comp, threads, err)) {
-        fprintf(stderr, "openge: error reading %s: %s\n", path.c_str(), err.c_str());
-        return -1;
-    }
-    uint64_t nb = 0;
-    oge_bgzf_index(comp.data(), comp.size(), nullptr, nullptr, nullptr, nullptr, 0, &nb);
-    std::vector<uint64_t> idx(3 * nb + 1);
-    std::vector<uint32_t> crc(nb);
-    if (oge_bgzf_index(comp.data(), comp.size(), idx.data(), idx.data() + nb, idx.data() + 2 * nb, crc.data(), nb, &nb))
-        return 1;  // not BGZF / truncated: the host reader reports it
-    const uint64_t total = idx[3 * nb];
-    if (sink_sorts()) {  // larger than HBM (or the chunked test knob): the sorter works from host memory
-        uint64_t fr = 0, tot = 0;
-        if (getenv("OGE_CHUNK_BYTES") || (!oge_mem_info(cc.ctx, &fr, &tot) && total / 10 * 25 > fr)) return 1;
-    }
-    const auto t1 = clk();
     void *dz = nullptr, *di = nullptr, *dc = nullptr, *dout = nullptr, *doff = nullptr;
     auto release = [&]() {
         for (void *p : {dz, di, dc, dout, doff})
             if (p) oge_dev_free(cc.ctx, p);
     };
-    if (oge_dev_alloc(cc.ctx, comp.size() + 16, &dz) || oge_dev_alloc(cc.ctx, idx.size() * 8, &di) ||
-        oge_dev_alloc(cc.ctx, crc.size() * 4 + 4, &dc) || oge_dev_alloc(cc.ctx, total + 64, &dout)) {
+    uint64_t nb = 0, total = 0, zbytes = 0;
+    bool streamed = false;
+    if (!getenv("OGE_CHUNK_BYTES") && !(getenv("OGE_READER") && std::string(getenv("OGE_READER")) == "hostcopy") &&
+        stream_to_device(cc, path, threads, &dz, &zbytes) == 0) {
+        // framing index on the device (count, then fill); anything it rejects goes to the host path
+        streamed = oge_bgzf_index_dev(cc.ctx, (const uint8_t *)dz, zbytes, nullptr, nullptr, nullptr, nullptr, 0, &nb) == 0 &&
+                   oge_dev_alloc(cc.ctx, (3 * nb + 1) * 8, &di) == 0 && oge_dev_alloc(cc.ctx, nb * 4 + 4, &dc) == 0;
+        if (streamed) {
+            uint64_t *dd = (uint64_t *)di;
+            streamed = oge_bgzf_index_dev(cc.ctx, (const uint8_t *)dz, zbytes, dd, dd + nb, dd + 2 * nb, (uint32_t *)dc, nb, &nb) == 0 &&
+                       oge_memcpy(cc.ctx, &total, dd + 3 * nb, 8, 2) == 0;
+        }
+        if (streamed && sink_sorts()) {
+            uint64_t fr = 0, tot = 0;
+            if (oge_mem_info(cc.ctx, &fr, &tot) || total / 10 * 25 > fr) streamed = false;
+        }
+        if (!streamed) {
+            release();
+            dz = di = dc = nullptr;
+            nb = total = 0;
+        }
+    }
+    auto t1 = clk();
+    if (!streamed) {
+        if (!read_file_bytes(path, comp, threads, err)) {
+            fprintf(stderr, "openge: error reading %s: %s\n", path.c_str(), err.c_str());
+            return -1;
+        }
+        oge_bgzf_index(comp.data(), comp.size(), nullptr, nullptr, nullptr, nullptr, 0, &nb);
+        std::vector<uint64_t> idx(3 * nb + 1);
+        std::vector<uint32_t> crc(nb);
+        if (oge_bgzf_index(comp.data(), comp.size(), idx.data(), idx.data() + nb, idx.data() + 2 * nb, crc.data(), nb, &nb))
+            return 1;  // not BGZF / truncated: the host reader reports it
+        total = idx[3 * nb];
+        if (sink_sorts()) {  // larger than HBM (or the chunked test knob): the sorter works from host memory
+            uint64_t fr = 0, tot = 0;
+            if (getenv("OGE_CHUNK_BYTES") || (!oge_mem_info(cc.ctx, &fr, &tot) && total / 10 * 25 > fr)) return 1;
+        }
+        t1 = clk();
+        zbytes = comp.size();
+        if (oge_dev_alloc(cc.ctx, comp.size() + 16, &dz) || oge_dev_alloc(cc.ctx, idx.size() * 8, &di) ||
+            oge_dev_alloc(cc.ctx, crc.size() * 4 + 4, &dc)) {
+            release();
+            return cc.fail("device allocation");
+        }
+        if (oge_memcpy(cc.ctx, dz, comp.data(), comp.size(), 1) || oge_memcpy(cc.ctx, di, idx.data(), idx.size() * 8, 1) ||
+            oge_memcpy(cc.ctx, dc, crc.data(), crc.size() * 4, 1)) {
+            release();
+            return cc.fail("host->device copy");
+        }
+    }
+    if (oge_dev_alloc(cc.ctx, total + 64, &dout)) {
         release();
         return cc.fail("device allocation");
     }
-    if (oge_memcpy(cc.ctx, dz, comp.data(), comp.size(), 1) || oge_memcpy(cc.ctx, di, idx.data(), idx.size() * 8, 1) ||
-        oge_memcpy(cc.ctx, dc, crc.data(), crc.size() * 4, 1)) {
-        release();
-        return cc.fail("host->device copy");
-    }
     const auto t2 = clk();
     const uint64_t *dd = (const uint64_t *)di;
-    if (nb && oge_bgzf_inflate_dev(cc.ctx, (const uint8_t *)dz, comp.size(), dd, dd + nb, dd + 2 * nb, (const uint32_t *)dc, nb,
+    if (nb && oge_bgzf_inflate_dev(cc.ctx, (const uint8_t *)dz, zbytes, dd, dd + nb, dd + 2 * nb, (const uint32_t *)dc, nb,
                                    (uint8_t *)dout)) {
         release();
         return 1;
@@ -229,9 +333,9 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
     const auto t2b = clk();
     oge_dev_free(cc.ctx, dz);
     dz = nullptr;
-    // the compressed file's host copy (29 GB at 150M reads) takes ~1.5 s to unmap: on a thread of its
-    // own, beside the device stages that follow
-    std::thread([](bytevec v) { v = bytevec(); }, std::move(comp)).detach();
+    // the host path's copy of the compressed file (29 GB at 150M reads) takes ~1.5 s to unmap: on a
+    // thread of its own, beside the device stages that follow
+    if (!comp.empty()) std::thread([](bytevec v) { v = bytevec(); }, std::move(comp)).detach();
     comp = bytevec();
     const auto t3 = clk();
     // header from a prefix of the stream
@@ -270,9 +374,10 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
     b.host_valid = false;
     if (verbose_)
         fprintf(stderr,
-                "[openge] FileReader (device): file %.3f s, upload %.3f s, inflate %.3f s (kernels %.3f s, release of the "
+                "[openge] FileReader (device%s): file %.3f s, upload %.3f s, inflate %.3f s (kernels %.3f s, release of the "
                 "compressed copies %.3f s), records %.3f s\n",
-                sec(t0, t1), sec(t1, t2), sec(t2, t3), t_kern / 1e3, sec(t2b, t3), sec(t3, clk()));
+                streamed ? ", streamed + device index" : "", sec(t0, t1), sec(t1, t2), sec(t2, t3), t_kern / 1e3, sec(t2b, t3),
+                sec(t3, clk()));
     return 0;
 }
 

@@ -232,3 +232,19 @@ def test_cli_chunked_matches_reference(case, tmp_path):
     assert r.returncode == 0, r.stderr
     _, _, recs, offs = bamutil.read_bam(tmp_path / "r.bam")
     assert len(offs) == case.n - case.meta["sortdedup_v"]["n_dup"]
+
+
+def test_cli_streamed_reader_matches_reference(case, tmp_path):
+    """Files are streamed into HBM through page-locked buffers and indexed on the device
+    (OGE_STREAM_MIN lowers the size threshold and the chunk to 64 KiB, so the golden inputs take that
+    path in many chunks): the reference's mergesort -M outputs."""
+    import os
+    src = case_input(case, tmp_path)
+    env = dict(os.environ, OGE_STREAM_MIN="1")
+    r = subprocess.run([OPENGE, "mergesort", "-M", "--nopg", "-v", str(src), "-o", str(tmp_path / "o.bam")],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert "streamed + device index" in r.stderr
+    h, m, t = digests(tmp_path / "o.bam")
+    g = case.meta["sortdedup_v"]
+    assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
