@@ -737,7 +737,19 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
             const uint32_t x = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
             const uint32_t p = q0 + jb, len = (x & 0xff) + 3, dist = ((x >> 8) & 0x7fff) + 1;
             const uint32_t e = min(p + len, osz);  // phase 1 checked it; a failed block must not write past the array
-            for (uint32_t q = p; q < e; ++q) refs[q] = (uint16_t)(q - dist);
+            // refs[q] = q - dist over [p, e): single entries up to the next 8-aligned position, then
+            // 8 entries per 16-byte store, then the tail
+            uint32_t q = p;
+            const uint32_t a8 = min((p + 7) & ~7u, e);
+            for (; q < a8; ++q) refs[q] = (uint16_t)(q - dist);
+            for (; q + 8 <= e; q += 8) {
+                const uint32_t r = q - dist;
+                uint4 v;
+                v.x = (r & 0xffff) | (((r + 1) & 0xffff) << 16), v.y = ((r + 2) & 0xffff) | (((r + 3) & 0xffff) << 16);
+                v.z = ((r + 4) & 0xffff) | (((r + 5) & 0xffff) << 16), v.w = ((r + 6) & 0xffff) | (((r + 7) & 0xffff) << 16);
+                *(uint4 *)(refs + q) = v;
+            }
+            for (; q < e; ++q) refs[q] = (uint16_t)(q - dist);
         }
     }
     __syncthreads();
