@@ -106,7 +106,7 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
 // candidate-free positions right after it: a lane emits up to LB of them in one step, so a wave's
 // step count (the maximum over its 64 segments) drops for literal-heavy payload (BAM qualities)
 // while the tokens stay those of the one-symbol parse.
-template <int PS, int R, int LB, bool AFTER = false>
+template <int PS, int R, int LB>
 __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
                                                     uint32_t *__restrict__ tok, uint8_t *__restrict__ ntok,
                                                     uint32_t *__restrict__ freq_out) {
@@ -218,20 +218,6 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
                 dist_code(d, sym, nb, ev);
                 atomicAdd(&freq[kLit + sym], 1u);
                 p += L;
-                if (AFTER) {  // candidate-free positions right after the match: literals of this step
-                    tp[(uint64_t)k * kT] = tokv;
-                    ++k;
-#pragma unroll
-                    for (int q = 0; q < LB - 1; ++q) {
-                        if (p >= s1 || cand[cix(p - base)] != 0) break;
-                        const uint32_t b = byte_at<PS>(in, p);
-                        atomicAdd(&freq[b], 1u);
-                        tp[(uint64_t)k * kT] = b;
-                        ++k;
-                        ++p;
-                    }
-                    continue;
-                }
             } else {
                 const uint32_t b = byte_at<PS>(in, p);
                 tokv = b;
@@ -763,10 +749,6 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
         const char *e = getenv("OGE_DEFL_LITB");
         return e && *e ? atoi(e) : 4;
     }();
-    static const bool after = [] {  // OGE_DEFL_AFTER=1: the literal batch also follows matches
-        const char *e = getenv("OGE_DEFL_AFTER");
-        return e && *e == '1';
-    }();
     static const bool pad = [] {  // OGE_DEFL_PAD=0: unpadded tokens LDS layout (A/B)
         const char *e = getenv("OGE_DEFL_PAD");
         return !(e && atoi(e) == 0);
@@ -822,7 +804,6 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
         if (!pad) k_defl_tokens<31, 1, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch >= 16) k_defl_tokens<4, 2, 16><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch >= 8) k_defl_tokens<4, 2, 8><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (lit_batch >= 4 && after) k_defl_tokens<4, 2, 4, true><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch >= 4 && cand_r >= 4) k_defl_tokens<4, 4, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch >= 4) k_defl_tokens<4, 2, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch == 2) k_defl_tokens<4, 2, 2><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);

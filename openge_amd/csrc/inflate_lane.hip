@@ -210,8 +210,7 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
 // TL / TD: direct-table bits of the literal/length and distance codes (the slow paths count the
 // canonical limits from lengths 7 and 5 up, which holds for any TL <= 7, TD <= 5: a code longer than
 // the table is at or past every shorter length's limit).
-template <int WPS, int SLL, int SLD, bool MODE, bool DIRECT = false, int LB = 1, int TL = TBL, int TD = TBD,
-          bool AFTER = false>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
+template <int WPS, int SLL, int SLD, bool MODE, bool DIRECT = false, int LB = 1, int TL = TBL, int TD = TBD>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
 __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
                                                      const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
                                                      const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
@@ -524,14 +523,13 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 if (L == 15 && c15 >= T.l15) sym = 512;  // no such code
             }
             skip(L);
-            bool more = false;  // AFTER: a literal batch also follows a cleanly decoded match
             if (sym < 256) {
                 if (pos >= osz) {
                     fail(E_OVERRUN);
                 } else {
                     put(pos, sym, 1);
                     ++pos;
-                    if (LB > 1 && e && !AFTER) {  // more direct-table literals in this step
+                    if (LB > 1 && e) {  // more direct-table literals in this step
 #pragma unroll
                         for (int q = 1; q < LB; ++q) {
                             if (q % 4 == 0) refill();  // >= 33 bits again for the next four
@@ -542,7 +540,6 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                             ++pos;
                         }
                     }
-                    more = true;
                 }
             } else if (sym == 256) {
                 if (fin) block_end();
@@ -581,20 +578,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                         put(pos, (len - 3) | ((dist - 1) << 8), 3);  // descriptor in the hole's first bytes
                         mark(pos);
                         pos += len;
-                        more = true;
                     }
-                }
-            }
-            if (LB > 1 && AFTER && more) {  // direct-table literals after any symbol of this step
-                refill();  // a match may have left fewer than 24 bits
-#pragma unroll
-                for (int q = 1; q < LB; ++q) {
-                    if (q % 4 == 0) refill();
-                    const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
-                    if (!e2 || (e2 & 511) >= 256 || pos >= osz) break;
-                    skip(e2 >> 9);
-                    put(pos, e2 & 511, 1);
-                    ++pos;
                 }
             }
         } else if (st == ST_CL) {
@@ -891,10 +875,6 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         const char *e = getenv("OGE_INFL_LITB");
         return e && *e ? atoi(e) : 4;
     }();
-    static const bool after = [] {  // OGE_INFL_AFTER=1: the literal batch also follows matches
-        const char *e = getenv("OGE_INFL_AFTER");
-        return e && *e == '1';
-    }();
     const int wps = cfg == 4 ? 4 : (cfg == 2 || cfg == 8) ? 2 : 3;
     const uint64_t lanes = (uint64_t)ncu * 4 * wps * 64;
     const uint64_t nchunks = std::max<uint64_t>(1, (nblk + lanes - 1) / lanes);
@@ -908,7 +888,6 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
         if (cfg == 4) k_infl_huff<4, 0, 0, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 2) k_infl_huff<2, 136, 24, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 0 && litb >= 4 && after) k_infl_huff<3, 0, 0, false, false, 4, TBL, TBD, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 7) k_infl_huff<3, 0, 0, false, false, 4, 6, 5><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 8) k_infl_huff<2, 0, 0, false, false, 4, 7, 4><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         else if (cfg == 0 && litb >= 8) k_infl_huff<3, 0, 0, false, false, 8><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
