@@ -529,7 +529,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 } else {
                     put(pos, sym, 1);
                     ++pos;
-                    if (LB > 1 && e) {  // more direct-table literals in this step
+                    if (LB > 1) {  // more direct-table literals in this step (after a long code too: >= 18 bits left)
 #pragma unroll
                         for (int q = 1; q < LB; ++q) {
                             if (q % 4 == 0) refill();  // >= 33 bits again for the next four
