@@ -823,6 +823,27 @@ __global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t n
     count[c] = k;
 }
 
+// chunk c + 1 starts where chunk c's walk stopped; *st bit 0: a start moved, bit 1: a stop that is
+// invalid (or the last chunk's not at the end)
+__global__ void k_rec_join(const uint64_t *__restrict__ stop, uint64_t *__restrict__ start, uint64_t C, uint64_t n,
+                           unsigned int *__restrict__ st) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const uint64_t e = stop[c];
+    if (e >= kNone - 1) {
+        atomicOr(st, 2u);
+        return;
+    }
+    if (c + 1 < C) {
+        if (start[c + 1] != e) {
+            start[c + 1] = e;
+            atomicOr(st, 1u);
+        }
+    } else if (e != n) {
+        atomicOr(st, 2u);
+    }
+}
+
 
 // ------------------------------------------------------------------------------ BGZF framing index
 // The framing walk of oge_bgzf_index done in parallel: every byte position is tested for a BGZF
@@ -1200,72 +1221,79 @@ extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream,
     *n_out = 0;
     const uint64_t CH = 1ull << 16;
     const uint64_t C = std::max<uint64_t>(1, (end - rec_base + CH - 1) / CH);
-    uint64_t *ws = (uint64_t *)ctx->ws("rec_walk", 4 * C * 8 + 64);
+    uint64_t *ws = (uint64_t *)ctx->ws("rec_walk", (5 * C + 4) * 8 + 64);
     if (!ws) return OGE_ERR_HIP;
-    uint64_t *start = ws, *stop = ws + C, *count = ws + 2 * C, *pos = ws + 3 * C;
-    std::vector<uint64_t> hs(C), he(C), hc(C), hp(C);
+    // start[C], stop[C], count[C + 1], pos[C + 1], pos2[C + 1], st
+    uint64_t *start = ws, *stop = ws + C, *count = ws + 2 * C, *pos = ws + 3 * C + 1, *pos2 = ws + 4 * C + 2;
+    unsigned int *st = (unsigned int *)(ws + 5 * C + 3);
     if (end == rec_base) {
         if (d_off && cap >= 1) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off, &end, 8, hipMemcpyHostToDevice, ctx->stream));
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         return OGE_OK;
     }
     const uint32_t TB = 128, G = oge_ceil_div(C, TB);
+    // one walk + join pass: *st bit 0 = a start moved, bit 1 = an invalid or unjoined stop
+    auto walk_join = [&](uint64_t *pos_arg, uint64_t *out, unsigned int *h) -> int {
+        OGE_HIP_TRY(ctx, hipMemsetAsync(st, 0, 4, ctx->stream));
+        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos_arg, out);
+        OGE_LAUNCH_CHECK(ctx);
+        k_rec_join<<<G, TB, 0, ctx->stream>>>(stop, start, C, end, st);
+        OGE_LAUNCH_CHECK(ctx);
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(h, st, 4, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return OGE_OK;
+    };
+    // n = the sum of the chunk counts, pos = their exclusive scan
+    auto scan_counts = [&](uint64_t *dst, uint64_t *n) -> int {
+        OGE_HIP_TRY(ctx, hipMemsetAsync(count + C, 0, 8, ctx->stream));  // count[C] = 0 (pos[C] = total)
+        int rc = oge_exclusive_scan_u64(ctx, count, dst, C + 1);
+        if (rc) return rc;
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(n, dst + C, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return OGE_OK;
+    };
     auto &RW = ctx->recwalk;
-    if (d_off && RW.stream == d_stream && RW.base == rec_base && RW.end == end && RW.n_ref == n_ref && RW.pos.size() == C) {
-        // the count-only call on this stream converged just before: fill from its chunk starts
+    if (d_off && RW.stream == d_stream && RW.base == rec_base && RW.end == end && RW.n_ref == n_ref && RW.C == C) {
+        // the count-only call on this stream converged just before: fill from its chunk starts and
+        // offsets (still in the workspace), then check the walk joined and counted the same
         const uint64_t n = RW.n;
         RW.stream = nullptr;
         if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(pos, RW.pos.data(), C * 8, hipMemcpyHostToDevice, ctx->stream));
-        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos, d_off);
-        OGE_LAUNCH_CHECK(ctx);
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &end, 8, hipMemcpyHostToDevice, ctx->stream));
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(he.data(), stop, C * 8, hipMemcpyDeviceToHost, ctx->stream));
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(hc.data(), count, C * 8, hipMemcpyDeviceToHost, ctx->stream));
-        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        if (he == RW.stop && hc == RW.count) {
+        unsigned int h = 0;
+        uint64_t n2 = 0;
+        int rc = walk_join(pos, d_off, &h);
+        if (rc) return rc;
+        if (!h && !(rc = scan_counts(pos2, &n2)) && n2 == n) {
+            OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &end, 8, hipMemcpyHostToDevice, ctx->stream));
+            OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
             *n_out = n;
             return OGE_OK;
         }
+        if (rc) return rc;
         // the stream changed between the calls: the full walk below
     }
     RW.stream = nullptr;
     k_rec_guess<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, n_ref, CH, C, start);
     OGE_LAUNCH_CHECK(ctx);
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(hs.data(), start, C * 8, hipMemcpyDeviceToHost, ctx->stream));
-    // walk, then make every chunk start where its predecessor's walk stopped, until consistent
+    // walk, then every chunk starts where its predecessor's walk stopped (k_rec_join), until no start
+    // moves: the chain from chunk 0 then equals the sequential walk
+    unsigned int h = 0;
     for (int it = 0;; ++it) {
-        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, nullptr, nullptr);
-        OGE_LAUNCH_CHECK(ctx);
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(he.data(), stop, C * 8, hipMemcpyDeviceToHost, ctx->stream));
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(hc.data(), count, C * 8, hipMemcpyDeviceToHost, ctx->stream));
-        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        bool changed = false;
-        for (uint64_t c = 0; c + 1 < C; ++c) {
-            if (he[c] >= kNone - 1) break;  // the chain broke before here: fixed on a later pass
-            if (hs[c + 1] != he[c]) hs[c + 1] = he[c], changed = true;
-        }
-        // the chain from chunk 0 is exact up to the first chunk whose start was not yet verified
-        if (!changed) break;
+        int rc = walk_join(nullptr, nullptr, &h);
+        if (rc) return rc;
+        if (!(h & 1)) break;
         if (it > 64) return oge_fail(ctx, OGE_ERR_IO, "BAM record walk did not converge (corrupt stream?)");
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(start, hs.data(), C * 8, hipMemcpyHostToDevice, ctx->stream));
     }
-    for (uint64_t c = 0; c < C; ++c) {
-        const bool last = c + 1 == C;
-        if (he[c] >= kNone - 1 || (last && he[c] != end) || (!last && he[c] != hs[c + 1]))
-            return oge_fail(ctx, OGE_ERR_IO,
-                            "Invalid BAM record (block size out of range or record past the end of the stream)");
-    }
+    if (h) return oge_fail(ctx, OGE_ERR_IO, "Invalid BAM record (block size out of range or record past the end of the stream)");
     uint64_t n = 0;
-    for (uint64_t c = 0; c < C; ++c) hp[c] = n, n += hc[c];
+    int rc = scan_counts(pos, &n);
+    if (rc) return rc;
     *n_out = n;
     if (!d_off) {
-        RW.stream = d_stream, RW.base = rec_base, RW.end = end, RW.n_ref = n_ref, RW.n = n;
-        RW.stop = he, RW.count = hc, RW.pos = hp;
+        RW.stream = d_stream, RW.base = rec_base, RW.end = end, RW.n_ref = n_ref, RW.n = n, RW.C = C;
         return OGE_OK;
     }
     if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(pos, hp.data(), C * 8, hipMemcpyHostToDevice, ctx->stream));
     k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos, d_off);
     OGE_LAUNCH_CHECK(ctx);
     OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &end, 8, hipMemcpyHostToDevice, ctx->stream));

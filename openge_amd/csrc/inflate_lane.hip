@@ -203,8 +203,9 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
 // otherwise a step decodes a whole symbol (a match's length and distance codes in the same step).
 // DIRECT: every output byte is its own byte store (no 8-byte accumulator to keep and flush).
 // LB (one-code-per-step path): a literal decoded from the direct table may be followed, in the same
-// step, by up to LB - 1 more literals whose codes also sit in the direct table (<= 6 bits each: the
-// >= 33 buffered bits cover four, then a refill); a wave's step count is the maximum over its 64
+// step, by up to LB - 1 more literals whose codes also sit in the direct table (<= 6 bits each: a
+// refill leaves >= 32 bits, enough for four such codes; then another refill); a wave's step count is
+// the maximum over its 64
 // blocks' symbol counts, so literal runs (BAM qualities, bases) take fewer steps.  300M reads in the
 // chain: LB = 1 / 2 / 4 -> 1152 / 941 / 792 ms (profiles/r02s3_infl_litb.json).
 // TL / TD: direct-table bits of the literal/length and distance codes (the slow paths count the
@@ -529,7 +530,10 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 } else {
                     put(pos, sym, 1);
                     ++pos;
-                    if (LB > 1) {  // more direct-table literals in this step (after a long code too: >= 18 bits left)
+                    if (LB > 1 && e) {  // more direct-table literals in this step
+                        // the step's refill leaves >= 32 bits: 26 after a direct-table code cover three
+                        // more (after a long code, with a second refill, measured slower: 72.9 vs 68.9 ms
+                        // at 20M reads)
 #pragma unroll
                         for (int q = 1; q < LB; ++q) {
                             if (q % 4 == 0) refill();  // >= 33 bits again for the next four

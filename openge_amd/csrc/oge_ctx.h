@@ -33,14 +33,13 @@ struct oge_ctx {
     hipStream_t side_stream(int i);
     void *alloc(size_t bytes);
     void release(void *p);
-    // the last count-only oge_bam_record_offsets_dev call: its converged chunk starts stay in the
-    // "rec_walk" workspace, so the offsets call that follows (same stream and range) goes straight to
-    // the fill walk, whose per-chunk stops and counts are checked against these
+    // the last count-only oge_bam_record_offsets_dev call: its converged chunk starts and offsets stay
+    // in the "rec_walk" workspace, so the offsets call that follows (same stream and range) goes
+    // straight to the fill walk, which is checked to join and count the same
     struct RecWalk {
         const void *stream = nullptr;
-        uint64_t base = 0, end = 0, n = 0;
+        uint64_t base = 0, end = 0, n = 0, C = 0;
         int32_t n_ref = 0;
-        std::vector<uint64_t> stop, count, pos;
     } recwalk;
     bool last_scan_generic = false;  // realign scan fell back to the byte-wise kernel
     double scan_t[3] = {0, 0, 0};    // realign scan host timings: validate, upload, device + download
