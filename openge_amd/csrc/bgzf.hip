@@ -804,7 +804,6 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
         if (!pad) k_defl_tokens<31, 1, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch >= 16) k_defl_tokens<4, 2, 16><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch >= 8) k_defl_tokens<4, 2, 8><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (lit_batch >= 4 && cand_r == 1) k_defl_tokens<4, 1, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch >= 4 && cand_r >= 4) k_defl_tokens<4, 4, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch >= 4) k_defl_tokens<4, 2, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
         else if (lit_batch == 2) k_defl_tokens<4, 2, 2><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
