@@ -868,10 +868,14 @@ __device__ __forceinline__ uint32_t bgzf_head(const uint8_t *__restrict__ z, uin
 
 constexpr int kIdxPos = 16;  // byte positions per thread
 
+constexpr uint32_t kStash = 4;  // candidate slots per 4096-position block in the counting pass
+
 template <bool EMIT>
 __global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z, uint64_t zbytes, uint32_t *__restrict__ cnt,
                                                    const uint32_t *__restrict__ base, uint64_t *__restrict__ cpos,
-                                                   uint32_t *__restrict__ cbs) {
+                                                   uint32_t *__restrict__ cbs, uint64_t *__restrict__ stash_pos = nullptr,
+                                                   uint32_t *__restrict__ stash_bs = nullptr,
+                                                   unsigned int *__restrict__ ovf = nullptr) {
     __shared__ uint32_t wsum[4];
     const uint32_t t = threadIdx.x;
     const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + t) * kIdxPos;
@@ -914,6 +918,22 @@ __global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z
     }
     if (!EMIT) {
         if (t == 0) cnt[blockIdx.x] = tot;
+        // stash: a block's candidates (nearly always 0 or 1 per 4096 bytes) in its kStash slots, so the
+        // compaction needs no second scan of the file; a fuller block raises the overflow word
+        if (stash_pos) {
+            if (tot > kStash) {
+                if (t == 0) atomicOr(ovf, 1u);
+                return;
+            }
+            if (!mine) return;
+            uint64_t o = (uint64_t)blockIdx.x * kStash + before + incl - mine;
+            for (int k = 0; k < kIdxPos; ++k) {
+                const uint64_t p = p0 + k;
+                if (p >= zbytes || z[p] != 31) continue;
+                const uint32_t bs = bgzf_head(z, zbytes, p);
+                if (bs) stash_pos[o] = p, stash_bs[o] = bs, ++o;
+            }
+        }
         return;
     }
     if (!mine) return;
@@ -1004,6 +1024,16 @@ extern "C" int oge_bgzf_index(const uint8_t *z, uint64_t zbytes, uint64_t *d0, u
 // Device framing index into the context's workspace (pointers valid until the next call that uses
 // it).  Returns 1 (no error recorded) when the candidate chain is not exact: the caller then uses
 // the host walk, which also produces the reference-like error messages.
+// the stashed candidates of every block into stream order
+__global__ void k_bgzf_unstash(const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ base, uint64_t G,
+                               const uint64_t *__restrict__ stash_pos, const uint32_t *__restrict__ stash_bs,
+                               uint64_t *__restrict__ cpos, uint32_t *__restrict__ cbs) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= G) return;
+    const uint32_t c = cnt[b], o = base[b];
+    for (uint32_t j = 0; j < c; ++j) cpos[o + j] = stash_pos[b * kStash + j], cbs[o + j] = stash_bs[b * kStash + j];
+}
+
 int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzfIndex *ix) {
     hipSetDevice(ctx->device);
     ix->nblk = 0;
@@ -1016,14 +1046,19 @@ int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzf
     uint32_t *cnt = (uint32_t *)ctx->ws("bix_cnt", (G + 1) * 4);
     uint32_t *base = (uint32_t *)ctx->ws("bix_base", (G + 1) * 4);
     uint32_t *bad = (uint32_t *)ctx->ws("bix_bad", 16);
-    if (!cnt || !base || !bad) return OGE_ERR_HIP;
-    k_bgzf_cand<false><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, cnt, nullptr, nullptr, nullptr);
+    uint64_t *stash_pos = (uint64_t *)ctx->ws("bix_stash_pos", G * kStash * 8);
+    uint32_t *stash_bs = (uint32_t *)ctx->ws("bix_stash_bs", G * kStash * 4);
+    if (!cnt || !base || !bad || !stash_pos || !stash_bs) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(bad + 1, 0, 4, ctx->stream));
+    k_bgzf_cand<false><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, cnt, nullptr, nullptr, nullptr, stash_pos, stash_bs,
+                                                              bad + 1);
     OGE_LAUNCH_CHECK(ctx);
     OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + G, 0, 4, ctx->stream));
     int rc = oge_exclusive_scan_u32(ctx, cnt, base, G + 1);
     if (rc) return rc;
-    uint32_t m32 = 0;
+    uint32_t m32 = 0, stash_ovf = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&m32, base + G, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&stash_ovf, bad + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     const uint64_t m = m32;
     if (!m) return 1;
@@ -1032,7 +1067,10 @@ int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzf
     uint32_t *isz = (uint32_t *)ctx->ws("bix_isz", (m + 1) * 4);
     uint32_t *slot = (uint32_t *)ctx->ws("bix_slot", (m + 1) * 4);
     if (!cpos || !cbs || !isz || !slot) return OGE_ERR_HIP;
-    k_bgzf_cand<true><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, cnt, base, cpos, cbs);
+    if (stash_ovf)  // a block with more than kStash candidates: the second scan places them
+        k_bgzf_cand<true><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, cnt, base, cpos, cbs);
+    else
+        k_bgzf_unstash<<<oge_ceil_div(G, 256), 256, 0, ctx->stream>>>(cnt, base, G, stash_pos, stash_bs, cpos, cbs);
     OGE_LAUNCH_CHECK(ctx);
     OGE_HIP_TRY(ctx, hipMemsetAsync(bad, 0, 4, ctx->stream));
     k_bgzf_chain<<<oge_ceil_div(m, 256), 256, 0, ctx->stream>>>(d_z, zbytes, cpos, cbs, m, bad, isz);

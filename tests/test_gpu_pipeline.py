@@ -66,6 +66,10 @@ def _streams():
     # the host walk decides
     fake = struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, ord("B"), ord("C"), 2, 40) + b"\0" * 30
     yield "planted", bamutil.bgzf_blocks(raw[:70_000] + fake + raw[70_000:150_000], 0)
+    # hundreds of tiny blocks: more candidates per 4096-byte scan block than the counting pass stashes
+    # (kStash), so the second scan places them; and runs of them next to ordinary blocks
+    tiny = b"".join(bamutil.bgzf_blocks(raw[i:i + 3], 6)[:-28] for i in range(0, 3000, 3))
+    yield "tiny_blocks", tiny + bamutil.bgzf_blocks(raw[:100_000], 6)
     for name in ("simple.bam", "208.yhet.bam"):
         yield name, (GOLDEN / "inputs" / name).read_bytes()
 
