@@ -93,8 +93,9 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
 
 
 // ------------------------------------------------------------------------------------ tokens
-// tok layout: [(blk * kNSub + sub) * kSeg + k] * kT + t  (u32: literal byte, or
-// 0x80000000 | (len - 3) << 16 | (dist - 1)); ntok[(blk * kNSub + sub) * kT + t].
+// tok layout: [(blk * kNSub + sub) * kSeg + k] * kT + t  (u32: literal byte, or a match at symbol
+// level: 0x80000000 | (length symbol - 257) << 26 | length extra value << 21 | distance symbol << 16 |
+// distance extra value, so k_defl_emit only looks codes up); ntok[(blk * kNSub + sub) * kT + t].
 // zpow[k][32]: operator of feeding 2^k zero bytes through the (reflected) CRC-32 register.
 // PS: padded layouts (bgzf_dev.h pw) -- every thread's 64-byte segment of `in` starts in its own bank
 // for the greedy parse (PS = 4), or none (PS = 31).  The payload CRC is computed by k_defl_emit, so this
@@ -211,12 +212,12 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
             uint32_t tokv;
             if (L >= 3) {
                 const uint32_t d = p - (c - 1);
-                tokv = 0x80000000u | ((L - 3) << 16) | (d - 1);
-                uint32_t sym, nb, ev;
+                uint32_t sym, nb, ev, dsym, dnb, dev;
                 len_code(L, sym, nb, ev);
                 atomicAdd(&freq[sym], 1u);
-                dist_code(d, sym, nb, ev);
-                atomicAdd(&freq[kLit + sym], 1u);
+                dist_code(d, dsym, dnb, dev);
+                atomicAdd(&freq[kLit + dsym], 1u);
+                tokv = 0x80000000u | ((sym - 257) << 26) | (ev << 21) | (dsym << 16) | dev;
                 p += L;
             } else {
                 const uint32_t b = byte_at<PS>(in, p);
@@ -482,13 +483,14 @@ struct BitW {
     }
 };
 
+// extra-bit counts of a length symbol - 257 (0..28) and of a distance symbol (0..29)
+__device__ __forceinline__ uint32_t len_extra(uint32_t ls) { return ls < 8 ? 0u : ls < 28 ? (ls - 4) >> 2 : 0u; }
+__device__ __forceinline__ uint32_t dist_extra(uint32_t ds) { return ds < 4 ? 0u : (ds - 2) >> 1; }
+
 __device__ __forceinline__ uint32_t tok_bits(uint32_t v, const uint32_t *lit, const uint32_t *dist) {
     if (!(v >> 31)) return lit[v] >> 16;
-    const uint32_t L = ((v >> 16) & 0x7fff) + 3, D = (v & 0xffff) + 1;
-    uint32_t s, nb, ev, s2, nb2, ev2;
-    len_code(L, s, nb, ev);
-    dist_code(D, s2, nb2, ev2);
-    return (lit[s] >> 16) + nb + (dist[s2] >> 16) + nb2;
+    const uint32_t ls = (v >> 26) & 31, ds = (v >> 16) & 31;
+    return (lit[257 + ls] >> 16) + len_extra(ls) + (dist[ds] >> 16) + dist_extra(ds);
 }
 
 
@@ -620,14 +622,11 @@ __global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ sr
                     const uint32_t c = lit[v];
                     w.put(c & 0xffff, c >> 16);
                 } else {
-                    const uint32_t L = ((v >> 16) & 0x7fff) + 3, D = (v & 0xffff) + 1;
-                    uint32_t sy, nb, ev;
-                    len_code(L, sy, nb, ev);
-                    const uint32_t c = lit[sy];
-                    w.put((c & 0xffff) | (ev << (c >> 16)), (c >> 16) + nb);
-                    dist_code(D, sy, nb, ev);
-                    const uint32_t d = dist[sy];
-                    w.put((d & 0xffff) | (ev << (d >> 16)), (d >> 16) + nb);
+                    const uint32_t ls = (v >> 26) & 31, ds = (v >> 16) & 31;
+                    const uint32_t c = lit[257 + ls];
+                    w.put((c & 0xffff) | (((v >> 21) & 31) << (c >> 16)), (c >> 16) + len_extra(ls));
+                    const uint32_t d = dist[ds];
+                    w.put((d & 0xffff) | ((v & 0x1fff) << (d >> 16)), (d >> 16) + dist_extra(ds));
                 }
               }
             }
