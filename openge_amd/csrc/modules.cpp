@@ -184,7 +184,7 @@ int AlgorithmModule::runChain(ChainContext &cc) {
 // is copied), indexed on the device: no host copy of the whole file to allocate, fault in and unmap
 // (a 29 GB file's unmap alone took 1.5 s).  Returns 2 when it does not apply (small files, inputs
 // close to the HBM size, a framing the device index rejects) -- the caller then takes the host path.
-static int stream_to_device(ChainContext &cc, const std::string &path, int threads, void **dz_out, uint64_t *zbytes) {
+static int stream_to_device(ChainContext &cc, const std::string &path, void **dz_out, uint64_t *zbytes) {
     const int fd = open(path.c_str(), O_RDONLY);
     if (fd < 0) return 2;
     struct stat stt;
@@ -233,7 +233,6 @@ static int stream_to_device(ChainContext &cc, const std::string &path, int threa
             });
         for (auto &t : ts) t.join();
     };
-    (void)threads;
     read_chunk(0);
     for (uint64_t c = 0; c < nch && !bad; ++c) {
         std::thread next;
@@ -269,7 +268,7 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
     uint64_t nb = 0, total = 0, zbytes = 0;
     bool streamed = false;
     if (!getenv("OGE_CHUNK_BYTES") && !(getenv("OGE_READER") && std::string(getenv("OGE_READER")) == "hostcopy") &&
-        stream_to_device(cc, path, threads, &dz, &zbytes) == 0) {
+        stream_to_device(cc, path, &dz, &zbytes) == 0) {
         // framing index on the device (count, then fill); anything it rejects goes to the host path
         streamed = oge_bgzf_index_dev(cc.ctx, (const uint8_t *)dz, zbytes, nullptr, nullptr, nullptr, nullptr, 0, &nb) == 0 &&
                    oge_dev_alloc(cc.ctx, (3 * nb + 1) * 8, &di) == 0 && oge_dev_alloc(cc.ctx, nb * 4 + 4, &dc) == 0;
