@@ -26,9 +26,11 @@ Also on the same JSON line:
   realign       -- configs[4]: openge localrealign on the C5 set (50k indel intervals)
 
 Multi-GPU (torchrun, one rank per GPU): the same 300M-read sample split across N ranks (strong
-scaling); openge_amd/shard.py routes records to the rank owning their contig with an RCCL all-to-all
-over xGMI (ghost copies of cross-rank mates keep MarkDuplicates exact), each rank sorts + dedups its
-range.  value = reads / max-over-ranks wall time.
+scaling), one input BAM file per rank; oge_mergesort_bgzf_dist range-splits the ByPosition keys with
+sampled splitters, exchanges the records with an all-to-all (RCCL over xGMI between GPUs; the
+host-staged transport when ranks share a GPU), sorts each rank's slice and marks duplicates exactly
+with hash-routed mate-join / pair-group exchanges.  value = reads / max-over-ranks wall
+time.  --dump-dir writes every rank's output slice (tests/test_gpu_multiproc.py concatenates them).
 """
 from __future__ import annotations
 
@@ -53,7 +55,7 @@ VALU_INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 KERNEL_STAGES = ["input_pass", "sort_radix", "sort_ties", "meta_gather", "md_matejoin", "md_pairs", "md_frags",
                  "md_apply", "gather_offsets", "gather_records"]
 SUB_STAGES = ["md_pair_win", "md_frag_win", "md_pair_ovf", "md_frag_ovf"]  # nested in md_pairs / md_frags: which group path ran
-E2E_STAGES = ["bgzf_index", "bgzf_inflate", "bgzf_crc", "rec_walk"] + KERNEL_STAGES + ["bgzf_deflate"]
+E2E_STAGES = ["bgzf_index", "bgzf_inflate", "rec_walk"] + KERNEL_STAGES + ["bgzf_deflate"]
 
 
 def parse():
@@ -62,6 +64,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--pairs", type=int, default=150_000_000, help="read pairs (default 150M = 300M reads)")
+    ap.add_argument("--seed", type=int, default=1234, help="C2 generator seed")
+    ap.add_argument("--dump-dir", default=None, help="multi-GPU: write each rank's output slice here (tests)")
     ap.add_argument("--level", type=int, default=6, help="BGZF level of the input file and of the output")
     ap.add_argument("--kernel-steps", type=int, default=3, help="timed steps of the kernel-only leg")
     ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
@@ -124,20 +128,56 @@ def pmc_traffic(kernel: str, rec_bytes: int) -> dict | None:
     return None
 
 
-# kernel per e2e stage (the launch the stage time belongs to) and its algorithmic bytes
+# kernel per e2e stage (the launch the stage time belongs to), its algorithmic bytes and what bounds it:
+# the gather and the record parse stream HBM; the codec kernels are serial per-block chains (Huffman
+# decode, greedy parse, bit emission) bound by VALU issue and latency, not by HBM bandwidth
 def stage_kernels(B: int, zin: int, zout: int, n: int, seq_bytes: int) -> dict:
     return {
-        "bgzf_inflate": ("k_infl", "BGZF inflate: compressed bytes read + payload bytes written", zin + B),
-        "bgzf_deflate": ("k_defl", "BGZF deflate (level 6): payload read + compressed bytes written", B + zout),
-        "gather_records": ("k_gather16", "permutation gather + BAM re-encode: 2*B (SURVEY §8d sort bytes)", 2 * B),
+        "bgzf_inflate": ("k_infl", "BGZF inflate: compressed bytes read + payload bytes written", zin + B, "valu"),
+        "bgzf_deflate": ("k_defl", "BGZF deflate (level 6): payload read + compressed bytes written", B + zout, "valu"),
+        "gather_records": ("k_gather16", "permutation gather + BAM re-encode: 2*B (SURVEY §8d sort bytes)", 2 * B, "hbm"),
         "input_pass": ("k_input_pass", "record parse: B - packed bases (SURVEY §8d dedup bytes) + 2N",
-                       B - seq_bytes + 2 * n),
-        "bgzf_crc": ("k_crc_check", "CRC-32 of every payload: B", B),
+                       B - seq_bytes + 2 * n, "hbm"),
     }
 
 
+def pmc_valu(kernel: str, rec_bytes: int) -> dict | None:
+    """VALU lane-instructions per launch of a stage's kernels (SQ_INSTS_VALU x 64) from the newest
+    committed PMC summary that has them, scaled by record bytes like pmc_traffic."""
+    files = sorted(f for f in (ROOT / "profiles").glob("r*_pmc.json") if "realign" not in f.name)
+    for fn in reversed(files):
+        try:
+            d = json.loads(fn.read_text())
+        except Exception:
+            continue
+        for name, v in d.get("kernels", {}).items():
+            if kernel in name and v.get("valu_insts"):
+                w = d.get("workload", {})
+                b = w.get("record_bytes_rank0") or w.get("record_bytes_per_gpu") or rec_bytes
+                return {"lane_ops": 64 * v["valu_insts"] * rec_bytes / b, "source": fn.name}
+    return None
+
+
+def roofline_entry(stage: str, info: tuple, t_ms: float, B: int) -> dict:
+    kname, what, abytes, bound = info
+    ach = abytes / (t_ms / 1e3) / 1e9 if t_ms > 0 else 0.0
+    pmc = pmc_traffic(kname, B)
+    r = {"kernel": f"{kname} ({what})", "stage": stage, "bound": bound, "achieved": round(ach, 1),
+         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+         "traffic": round(pmc["bytes"]) if pmc else None, "traffic_source": pmc["source"] if pmc else None,
+         "traffic_ratio": round(pmc["bytes"] / abytes, 2) if pmc else None,
+         "algorithmic_bytes": abytes, "avg_ms": t_ms}
+    if bound == "valu":
+        v = pmc_valu(kname, B)
+        if v and t_ms > 0:
+            a = v["lane_ops"] / (t_ms / 1e3) / 1e12
+            r["valu"] = {"achieved": round(a, 2), "peak": round(VALU_INT32_PEAK_TOPS, 1), "unit": "T lane-ops/s",
+                         "frac": round(a / VALU_INT32_PEAK_TOPS, 4), "source": v["source"]}
+    return r
+
+
 # --------------------------------------------------------------------------------------------- legs
-def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1) -> dict | None:
+def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1, cpu_threads: int = 0) -> dict | None:
     """configs[4]: openge localrealign on the C5 synthetic set (50k indel intervals, 24 contigs).
     Host phases (binning, consensus generation, decisions, mate fixing) + the HIP offset scan; the
     records are decoded in host memory before the timed region (the module's input queue).  With
@@ -159,6 +199,9 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1) -> dict | 
         run = lambda: RS.localrealign_slice(ctx, b.header_text, b.recs, offs, lo, hi, fa, iv, opts,
                                             last=(rank == world - 1))
         run()  # warm-up (first-touch, kernel load)
+        ref_cpu = None
+        if world == 1 and cpu_threads:  # the reference's own realigner on the same files, this box's host
+            ref_cpu = cpu_baseline_realign(fa, iv, bam, n_intervals, cpu_threads, td)
         if world > 1:
             import torch
             import torch.distributed as dist
@@ -196,9 +239,28 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1) -> dict | 
                          "algorithmic_compares": st["scan_ops"],
                          "compares_per_s_T": round(cmp_t, 2) if cmp_t else None,
                          "compares_frac": round(cmp_t / VALU_INT32_PEAK_TOPS, 4) if cmp_t else None},
-            "cpu_reference_here": {"value": 1520.0, "unit": "intervals/s", "cores": 8,
-                                   "note": "oracle/_ref/ref_driver realign -t 8 on the same C5 set in the build "
-                                           "container (32.9 s)"}}
+            "cpu_baseline": ref_cpu}
+
+
+def cpu_baseline_realign(fa: str, iv: str, bam: str, n_intervals: int, threads: int, td: str) -> dict:
+    """The REFERENCE's LocalRealignment chain (oracle/_ref/ref_driver realign: FileReader ->
+    LocalRealignment -> BamSerializer, cmd/command_localrealign.cpp:37-75, compiled from its sources)
+    on the same C5 files, timed on this box's host cores in the same run (TEST INFRASTRUCTURE, the CPU
+    baseline only)."""
+    drv = ROOT / "oracle" / "_ref" / "ref_driver"
+    if not drv.exists():
+        return {"value": None, "kind": "reference", "note": f"{drv} missing (built only where /root/reference exists)"}
+    out = os.path.join(td, "ref_realigned.bam")
+    t0 = time.perf_counter()
+    r = subprocess.run([str(drv), "realign", "-t", str(threads), "-R", fa, "-L", iv, bam, out], capture_output=True,
+                       text=True, timeout=900)
+    dt = time.perf_counter() - t0
+    if r.returncode != 0:
+        return {"value": None, "kind": "reference", "note": f"ref_driver exit {r.returncode}: {r.stderr[-300:]}"}
+    return {"value": round(n_intervals / dt, 1), "unit": "intervals/s", "cores": threads, "kind": "reference",
+            "sample": f"the same C5 set ({n_intervals} intervals), OpenGE's own localrealign chain "
+                      f"(oracle/_ref/ref_driver realign -t {threads}), BAM file in -> BAM file out, wall time",
+            "seconds": round(dt, 2)}
 
 
 def realign_pmc_valu() -> dict | None:
@@ -244,7 +306,9 @@ def cpu_baseline_reference(sample_reads: int, threads: int) -> dict:
     return {"value": round(n / dt / 1e6, 4), "unit": "Mreads/s", "cores": threads, "kind": "reference",
             "sample": f"{n} reads of the C2 generator (seed 1234) as a level-6 BAM file -> OpenGE's own "
                       f"mergesort -M --nosplit -v chain (oracle/_ref/ref_driver sortdedup -t {threads} -n 500000) "
-                      "-> level-6 BAM file, wall time",
+                      "-> level-6 BAM file, wall time.  SIZE DIFFERS from the GPU leg (300M reads): at 300M the "
+                      "reference merges 600 spilled runs through a std::multiset (util/read_stream_reader.h:132-153), "
+                      "so its per-read cost there is higher and gpu_speedup is conservative",
             "seconds": round(dt, 2), "reference_log_tail": marked}
 
 
@@ -329,11 +393,12 @@ def main():
     ctx = L.Context(local, stream=stream.cuda_stream)
 
     if args.realign_only:
-        print(json.dumps(realign_leg(ctx, args.realign_intervals)), flush=True)
+        print(json.dumps(realign_leg(ctx, args.realign_intervals,
+                                     cpu_threads=0 if args.no_cpu_baseline else args.cpu_threads)), flush=True)
         ctx.close()
         return
 
-    p = L.synth_params(args.pairs, preset="c2", seed=1234)
+    p = L.synth_params(args.pairs, preset="c2", seed=args.seed)
     n_all = 2 * args.pairs
     if world > 1:
         multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank)
@@ -407,23 +472,11 @@ def main():
     log(f"e2e: {ms_step:.1f} ms/step = {value:.1f} Mreads/s; stages {sms}")
     assert nr == n, (nr, n)
 
-    # roofline: the dominant kernel of the e2e step
+    # roofline: the dominant kernel of the e2e step (bound per stage; VALU fraction for the codec)
     kinfo = stage_kernels(B, zbytes, out_bytes, n, seq_bytes)
-    cand = [(sms.get(s, 0.0), s) for s in kinfo]
-    t_dom, s_dom = max(cand)
-    kname, what, abytes = kinfo[s_dom]
-    ach = abytes / (t_dom / 1e3) / 1e9 if t_dom > 0 else 0.0
-    pmc = pmc_traffic(kname, B)
-    roof = {"kernel": f"{kname} ({what})", "stage": s_dom, "bound": "hbm", "achieved": round(ach, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": round(pmc["bytes"]) if pmc else None, "traffic_source": pmc["source"] if pmc else None,
-            "algorithmic_bytes": abytes, "avg_ms": t_dom}
-    others = []
-    for s, (kn, w, ab) in kinfo.items():
-        t = sms.get(s, 0.0)
-        if t > 0:
-            a = ab / (t / 1e3) / 1e9
-            others.append({"stage": s, "kernel": kn, "avg_ms": t, "achieved": round(a, 1), "frac": round(a / HBM_PEAK_GBS, 4)})
+    t_dom, s_dom = max((sms.get(s, 0.0), s) for s in kinfo)
+    roof = roofline_entry(s_dom, kinfo[s_dom], t_dom, B)
+    others = [roofline_entry(s, kinfo[s], sms[s], B) for s in kinfo if sms.get(s, 0.0) > 0]
 
     # ---- PCIe-inclusive run (compressed bytes only cross PCIe)
     pcie = None
@@ -459,7 +512,11 @@ def main():
     torch.cuda.empty_cache()
     if not args.no_realign and not args.e2e_only:
         log("realign leg")
-        out["realign"] = realign_leg(ctx, args.realign_intervals)
+        out["realign"] = realign_leg(ctx, args.realign_intervals,
+                                     cpu_threads=0 if args.no_cpu_baseline else args.cpu_threads)
+        rc_ = (out["realign"] or {}).get("cpu_baseline") or {}
+        if rc_.get("value"):
+            rc_["gpu_speedup"] = round(out["realign"]["value"] / rc_["value"], 1)
     if not args.no_cpu_baseline and not args.e2e_only:
         log("cpu baseline (reference)")
         cb = cpu_baseline_reference(args.cpu_sample_reads, args.cpu_threads)
@@ -519,9 +576,9 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
     torch.cuda.synchronize(dev)
     dist.barrier()
     t0 = time.perf_counter()
-    tot, nr, nd, ob = {}, 0, 0, 0
+    tot, nr, nd, ob, d_last = {}, 0, 0, 0, 0
     for _ in range(args.steps):
-        _, ob, nr, nd = step()
+        d_last, ob, nr, nd = step()
         for s_, v in stage_ms(ctx, DIST_STAGES).items():
             tot[s_] = tot.get(s_, 0.0) + v
     torch.cuda.synchronize(dev)
@@ -533,6 +590,12 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
     sizes = [None] * world
     dist.all_gather_object(sizes, (n, ob))
     assert nr == n_all, (nr, n_all)
+    transport = comm.transport
+    if args.dump_dir:  # this rank's slice of the output file (valid until the rank's next call)
+        ob_last = ob
+        hs = torch.empty(max(ob_last, 1), dtype=torch.uint8)
+        L.check(L.lib().oge_memcpy(ctx.h, hs.data_ptr(), d_last, ob_last, 2), ctx.h)
+        Path(args.dump_dir, f"slice_{rank}.bam").write_bytes(hs[:ob_last].numpy().tobytes())
     comm.close()
     del d_z
     torch.cuda.empty_cache()
@@ -551,8 +614,8 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
                                       f"one BGZF level-{args.level} BAM file as {world} rank slices, in HBM",
                           "reads_total": n_all, "duplicates_flagged": nd,
                           "rank_reads_and_output_bytes": sizes,
-                          "parallelism": f"{world} ranks (one process per GPU), RCCL all-to-all over xGMI via "
-                                         "oge_comm_init_rank"},
+                          "parallelism": f"{world} ranks (one process per GPU), all-to-all via oge_comm_init_rank",
+                          "transport": transport},
                "stages_ms_rank0": {k: round(v / K, 3) for k, v in tot.items()}}
         if realign_multi is not None:
             out["realign"] = realign_multi

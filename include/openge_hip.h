@@ -186,19 +186,25 @@ int oge_mem_info(oge_ctx *ctx, uint64_t *free_bytes, uint64_t *total_bytes);
  * GPU) with hash-routed mate-join and pair-group exchanges.  Every call below is collective: all
  * ranks of a communicator make it, in the same order. */
 typedef struct oge_comm oge_comm;
-/* RCCL unique id for oge_comm_init_rank (made by one rank, shared by the caller) */
+/* Communicator id for oge_comm_init_rank (made by one rank, shared by the caller): RCCL's unique id
+ * plus a random nonce naming the node-local meeting of ranks that share a GPU. */
 uint64_t oge_comm_unique_id_bytes(void);
 int oge_comm_unique_id(uint8_t *id_out, uint64_t bytes);
-/* one process per GPU: rank `rank` of `nranks`, RCCL over xGMI */
+/* One rank per process (or per host thread): rank `rank` of `nranks`, every rank with the same id,
+ * concurrently.  Transport (OGE_COMM = auto | rccl | host, default auto): RCCL over xGMI between
+ * distinct GPUs; "host" (device -> shared host segment -> device, dist_shm.h) when ranks share a GPU,
+ * which RCCL refuses -- so the same bootstrap runs on a one-GPU box.  auto takes RCCL when the
+ * process sees >= nranks devices, else compares the ranks' PCI bus ids in the shared segment
+ * (OGE_COMM_DIR, default /dev/shm or /tmp; OGE_COMM_STAGE_MB per-rank staging, default 32). */
 int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, oge_comm **out);
-/* one process, n contexts (one thread per rank afterwards): RCCL when the contexts' devices are
- * distinct, else (or with OGE_COMM=local) an in-process transport of device-to-device copies.
- * out[0..n) receives one communicator per context. */
+/* One process, n contexts in one call (test harness): RCCL when the contexts' devices are distinct,
+ * else (or with OGE_COMM=local) an in-process hub of device-to-device copies.  out[0..n) receives one
+ * communicator per context.  The CLI uses oge_comm_init_rank from one thread per rank instead. */
 int oge_comm_init(oge_ctx **ctxs, int n, oge_comm **out);
 void oge_comm_destroy(oge_comm *comm);
 int oge_comm_rank(const oge_comm *comm);
 int oge_comm_size(const oge_comm *comm);
-const char *oge_comm_transport(const oge_comm *comm); /* "rccl" or "local" */
+const char *oge_comm_transport(const oge_comm *comm); /* "rccl", "host" or "local" */
 /* This rank's shard of the input: contiguous input ranges in rank order (any sizes, empty ones
  * included).  sort != 0 (mergesort [-M]): -> this rank's slice of the globally sorted output, with
  * bin recomputed and, when opts != NULL, 0x400 set/cleared exactly as oge_sort_markdup_dev does on

@@ -4,6 +4,9 @@
 // BamSerializer<BgzfOutputStream> -- the serializer its FileWriter uses (alg/file_writer.cpp:144-166;
 // FileWriter itself needs the CMake-generated openge_constants.h, which this image cannot make).
 //   gpu_chain IN.bam OUT.bam [-R]
+// and `openge localrealign` as cmd/command_localrealign.cpp:37-75 wires it, with GpuLocalRealignment in
+// place of LocalRealignment:
+//   gpu_chain realign REF.fa INTERVALS IN.bam OUT.bam
 #include <execinfo.h>
 #include <signal.h>
 #include <stdlib.h>
@@ -49,8 +52,9 @@ static void on_abort(int sig) {  // where an abort came from, for the test log
 int main(int argc, char **argv) {
     signal(SIGABRT, on_abort);
     signal(SIGSEGV, on_abort);
-    if (argc < 3) {
-        std::cerr << "usage: gpu_chain IN.bam OUT.bam [-R]" << std::endl;
+    const bool realign = argc > 1 && !strcmp(argv[1], "realign");
+    if (argc < 3 || (realign && argc < 6)) {
+        std::cerr << "usage: gpu_chain IN.bam OUT.bam [-R] | gpu_chain realign REF.fa INTERVALS IN.bam OUT.bam" << std::endl;
         return 2;
     }
     OGEParallelismSettings::setNumberThreads(8);  // as cmd/commands.cpp:67-84 sets up the pool
@@ -58,20 +62,30 @@ int main(int argc, char **argv) {
     AlgorithmModule::setNothreads(false);
     AlgorithmModule::setVerbose(false);
     FileReader reader;
-    GpuReadSorter sorter;
-    GpuMarkDuplicates md;
     BamFileSink sink;
-    reader.addFile(argv[1]);
-    sink.filename = argv[2];
-    md.removeDuplicates = argc > 3 && !strcmp(argv[3], "-R");
-    reader.addSink(&sorter);
-    sorter.addSink(&md);
-    md.addSink(&sink);
-    const int rc = reader.runChain();
-    std::cerr << "Marked " << md.duplicates << " records as duplicates." << std::endl;
-    // leave without static destructors: one run aborted after this point ("double free or
-    // corruption" during teardown; the reference's shared thread pool is a static whose workers are
-    // still parked at exit), after the output was complete
-    fflush(stdout);
-    _exit(rc);
+    int rc;
+    if (realign) {
+        GpuLocalRealignment lr;
+        reader.addFile(argv[4]);
+        sink.filename = argv[5];
+        reader.addSink(&lr);
+        lr.addSink(&sink);
+        lr.setReferenceFilename(argv[2]);
+        lr.setIntervalsFilename(argv[3]);
+        rc = reader.runChain();
+    } else {
+        GpuReadSorter sorter;
+        GpuMarkDuplicates md;
+        reader.addFile(argv[1]);
+        sink.filename = argv[2];
+        md.removeDuplicates = argc > 3 && !strcmp(argv[3], "-R");
+        reader.addSink(&sorter);
+        sorter.addSink(&md);
+        md.addSink(&sink);
+        rc = reader.runChain();
+        std::cerr << "Marked " << md.duplicates << " records as duplicates." << std::endl;
+    }
+    OGERead::clearCachedAllocations();
+    ThreadPool::closeSharedPool();
+    return rc;
 }

@@ -8,6 +8,7 @@
 
 #include <iostream>
 #include <map>
+#include <sstream>
 
 namespace {
 
@@ -43,6 +44,26 @@ void finish(std::string &arena, std::vector<uint64_t> &off) {
 void fail(const char *what, oge_ctx *ctx) {
     std::cerr << what << ": " << oge_last_error(ctx) << std::endl;  // the reference's I/O error style
     exit(-1);
+}
+
+// An OGERead holding one BAM record (block_size + core + data), filled as BamDeserializer::read fills
+// the records it reads (util/bam_deserializer.h:143-193).
+OGERead *read_from_bam_record(const uint8_t *r) {
+    uint32_t w[9];
+    memcpy(w, r, sizeof w);
+    OGERead *al = OGERead::allocate();
+    al->setRefID((int32_t)w[1]);
+    al->setPosition((int32_t)w[2]);
+    const uint32_t lname = w[3] & 0xff;
+    al->setMapQuality((w[3] >> 8) & 0xff);
+    al->setBin(w[3] >> 16);
+    const uint32_t ncig = w[4] & 0xffff;
+    al->setAlignmentFlag(w[4] >> 16);
+    al->setMateRefID((int32_t)w[6]);
+    al->setMatePosition((int32_t)w[7]);
+    al->setInsertSize((int32_t)w[8]);
+    al->setBamStringData((const char *)r + 36, w[0] - 32, ncig, w[5], lname);
+    return al;
 }
 
 }  // namespace
@@ -112,12 +133,51 @@ int GpuMarkDuplicates::runInternal() {
     oge_ctx_destroy(ctx);
     duplicates = nd;
     // the apply phase (alg/mark_duplicates.cpp:443-465): primaries get 0x400 set or cleared,
-    // -r / -R drops the flagged ones (the receiver owns what it is handed; dropped reads are freed)
+    // -r / -R drops every record whose FLAG then carries 0x400 -- non-primaries keep the bit they came
+    // with (:456) -- (the receiver owns what it is handed; dropped reads are freed)
     for (size_t i = 0; i < reads.size(); i++) {
         OGERead *r = reads[i];
         if (dup[i] != 2) r->SetIsDuplicate(dup[i] == 1);
-        if (removeDuplicates && dup[i] == 1) OGERead::deallocate(r);
+        if (removeDuplicates && r->IsDuplicate()) OGERead::deallocate(r);
         else putOutputAlignment(r);
     }
+    return 0;
+}
+
+int GpuLocalRealignment::runInternal() {
+    // the sequence dictionary the realigner needs, as SAM header text (LocalRealignment::runInternal reads
+    // getHeader().getSequences(), alg/local_realignment.cpp:1464)
+    const BamHeader &h = getHeader();
+    std::ostringstream ht;
+    for (BamSequenceRecords::const_iterator sq = h.getSequences().begin(); sq != h.getSequences().end(); ++sq)
+        ht << "@SQ\tSN:" << sq->getName() << "\tLN:" << sq->getLength() << "\n";
+    const std::string hts = ht.str();
+    // drain the input (coordinate-sorted, as the reference module requires); the module owns what it
+    // is handed, so the input reads are freed once their bytes are in the arena
+    std::string arena;
+    std::vector<uint64_t> off;
+    for (OGERead *r; (r = getInputAlignment()) != NULL;) {
+        off.push_back(arena.size());
+        append_bam_record(arena, *r);
+        OGERead::deallocate(r);
+    }
+    const uint64_t n = off.size();
+    finish(arena, off);
+    oge_ctx *ctx = NULL;
+    if (oge_ctx_create(device, &ctx)) fail("GpuLocalRealignment", NULL);
+    oge_realign_opts o;
+    oge_realign_opts_init(&o);
+    oge_realign_result *res = NULL;
+    if (oge_localrealign(ctx, hts.c_str(), hts.size(), (const uint8_t *)arena.data(), &off[0], n, reference_filename.c_str(),
+                         intervals_filename.c_str(), &o, &res))
+        fail("GpuLocalRealignment", ctx);
+    if (verbose) std::cerr << "GpuLocalRealignment: " << oge_realign_result_stats(res) << std::endl;
+    const uint64_t m = oge_realign_result_count(res);
+    uint64_t nb = 0;
+    const uint8_t *out = oge_realign_result_records(res, &nb);
+    const uint64_t *oo = oge_realign_result_offsets(res);
+    for (uint64_t k = 0; k < m; k++) putOutputAlignment(read_from_bam_record(out + oo[k]));
+    oge_realign_result_free(res);
+    oge_ctx_destroy(ctx);
     return 0;
 }

@@ -1,5 +1,5 @@
-// gpu_modules.h -- the modules an OpenGE maintainer adds to openge/src/algorithms to run the sort and
-// duplicate marking on MI355X: AlgorithmModule subclasses (alg/algorithm_module.h:33-107) that drain
+// gpu_modules.h -- the modules an OpenGE maintainer adds to openge/src/algorithms to run the sort,
+// duplicate marking and local realignment on MI355X: AlgorithmModule subclasses (alg/algorithm_module.h:33-107) that drain
 // their input queue into a BAM-record arena, make one call into libopenge_hip.so
 // (include/openge_hip.h), and emit the same OGERead objects in the new order / with the new flags,
 // keeping the module contract (ownership passes on with putOutputAlignment; header via getHeader).
@@ -28,6 +28,23 @@ protected:
     int device;
     BamHeader header;
     bool header_ready;
+};
+
+// Drop-in for LocalRealignment (alg/local_realignment.h:67-527, wired by
+// cmd/command_localrealign.cpp:37-75): the same setters and public `verbose`; oge_localrealign runs
+// the whole module (binning, consensuses, the offset scan on the GPU, decisions, CIGAR / tag updates,
+// mate fixing) over the drained records and the realigned records are emitted in the module's order.
+class GpuLocalRealignment : public AlgorithmModule {
+public:
+    explicit GpuLocalRealignment(int device = 0) : verbose(false), device(device) {}
+    bool verbose;
+    void setReferenceFilename(const std::string &filename) { reference_filename = filename; }
+    void setIntervalsFilename(const std::string &filename) { intervals_filename = filename; }
+
+protected:
+    virtual int runInternal();
+    int device;
+    std::string reference_filename, intervals_filename;
 };
 
 // Drop-in for MarkDuplicates (alg/mark_duplicates.h:27-68, -v --nosplit semantics): oge_markdup.

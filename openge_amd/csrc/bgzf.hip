@@ -9,24 +9,19 @@
 //
 // Layout: the input is cut into 65,280-byte payloads (htslib's framing, as the host writer uses).
 // Each payload becomes one BGZF block holding one final deflate block with dynamic Huffman codes
-// (or a stored block when that is smaller).  Three launches per chunk of blocks:
+// (or a stored block when that is smaller).  Per chunk of 4096 payloads:
 //
-//   k_defl_tokens  one 512-thread workgroup per payload.  The payload is staged in LDS.  Match
-//                  candidates come from a 4096-bucket hash of 4-byte prefixes, filled in rounds of
-//                  512 consecutive positions (a position sees every earlier round, so the result is
-//                  deterministic); each thread then greedily parses its own 64-byte segment into
-//                  literal / (length, distance) tokens (matches end at the segment edge) and counts
-//                  symbol frequencies.  Tokens go to global scratch, interleaved so every store of a
-//                  wave is one contiguous line.  (152 KiB of LDS: one per CU, with room beside it for an
-//                  emit or Huffman workgroup of the chunk another stream is on.)
+//   k_defl_parse   one 512-thread workgroup per payload, the payload in LDS: hash-table match candidates
+//                  in rounds, a greedy parse of every 64-byte segment by its thread (literal runs
+//                  skipped by mask), symbol frequencies; out: per segment a literal mask + its matches.
 //   k_defl_huff    one wave per payload: length-limited Huffman code lengths for the literal/length
 //                  (15 bits), distance (15) and code-length (7) alphabets, canonical bit-reversed
-//                  codes, and the block header bit string.
-//   k_defl_emit    one 512-thread workgroup per payload: per-segment bit counts, a block scan for
-//                  the bit offsets, then every thread writes its own bits (interior words with plain
-//                  stores, the two edge words with atomicOr); the payload's CRC-32 from 128-byte pieces
-//                  read from global memory, combined with zero-run operators; BGZF header and footer.
-//   k_defl_compact copies the variable-size blocks from their 64 KiB slots to their final offsets.
+//                  codes, the block header bit string, and the exact block size (stored or dynamic).
+//   k_scan_chunk / k_defl_advance   the blocks' offsets in the output stream.
+//   k_defl_emit    one 512-thread workgroup per payload: segment bit counts, block scan, bits written
+//                  into an LDS image of the whole BGZF block, CRC-32, then the block out at its final
+//                  offset with coalesced stores.
+// Deterministic: the same input gives the same bytes (the candidate rounds fix what each position sees).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -43,7 +38,7 @@
 namespace {
 
 using namespace oge_bgzf;
-constexpr int kT = 512;                   // threads per workgroup (tokens / emit)
+constexpr int kT = 512;                   // threads per workgroup (parse / emit)
 constexpr int kSeg = 64;                  // bytes per thread segment
 constexpr int kSub = kT * kSeg;           // 32768 positions per sub-block
 constexpr int kNSub = 2;                  // sub-blocks per payload
@@ -57,6 +52,8 @@ struct DeflTab {
     uint32_t lit[kLit];    // bit-reversed code | length << 16
     uint32_t dist[kDist];
     uint32_t hdr_bits;
+    uint32_t stored;       // 1: the block is written as one stored block
+    uint32_t total;        // bytes of the whole BGZF block (header, deflate data, footer)
     uint32_t hdr[kHdrWords];
 };
 
@@ -92,68 +89,79 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
 }
 
 
-// ------------------------------------------------------------------------------------ tokens
-// tok layout: [(blk * kNSub + sub) * kSeg + k] * kT + t  (u32: literal byte, or a match at symbol
-// level: 0x80000000 | (length symbol - 257) << 26 | length extra value << 21 | distance symbol << 16 |
-// distance extra value, so k_defl_emit only looks codes up); ntok[(blk * kNSub + sub) * kT + t].
-// zpow[k][32]: operator of feeding 2^k zero bytes through the (reflected) CRC-32 register.
-// PS: padded layouts (bgzf_dev.h pw) -- every thread's 64-byte segment of `in` starts in its own bank
-// for the greedy parse (PS = 4), or none (PS = 31).  The payload CRC is computed by k_defl_emit, so this
-// kernel's LDS (one workgroup per CU) leaves room for an emit or Huffman workgroup of another chunk.
-// R: positions per thread per candidate round (rounds of R * 512 consecutive positions; a position
-// sees the hash table as the earlier rounds left it).  Fewer, fuller rounds cut the barriers per
-// payload (128 at R = 1) at the price of not seeing the rest of its own round.
-// LB: literals per parse step.  A position without a candidate is a literal, and so are the
-// candidate-free positions right after it: a lane emits up to LB of them in one step, so a wave's
-// step count (the maximum over its 64 segments) drops for literal-heavy payload (BAM qualities)
-// while the tokens stay those of the one-symbol parse.
-template <int PS, int R, int LB>
-__global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
-                                                    uint32_t *__restrict__ tok, uint8_t *__restrict__ ntok,
-                                                    uint32_t *__restrict__ freq_out) {
-    constexpr uint32_t kInW = kPay / 4 + 4 + (PS < 31 ? (kPay / 4 + 4) / (1u << PS) + 1 : 0);
-    __shared__ uint32_t in[kInW];
+// ------------------------------------------------------------------------------------ parse
+// One 512-thread workgroup per payload, the payload staged in LDS (unpadded).  Per sub-block of 32768
+// positions (two per payload):
+//   candidates  rounds of R * 512 consecutive positions: position p looks up the 4096-bucket hash of its
+//               4-byte prefix (the table as the earlier rounds left it: deterministic), keeps the
+//               candidate only if the 4 bytes match within 32 KiB, then the round's positions enter the
+//               table (atomicMax: the latest position wins).  A wave's 64 lanes hold 64 consecutive
+//               positions = one 64-byte segment, so one ballot gives the segment's candidate mask.
+//   parse       each thread greedily parses its own segment: literal runs are skipped with the mask
+//               (ctz to the next candidate: no per-literal work in the serial chain); at a candidate the
+//               match is extended 8 bytes per step and taken when >= 3 bytes (matches end at the segment
+//               edge).  The same tokens as a one-symbol-at-a-time greedy parse.
+//   counts      literal frequencies from the segment's literal mask (16-byte LDS reads, unrolled), length
+//               and distance symbol frequencies at each match.
+// Output per segment s (stream order: sub-block 0's 512 segments, then sub-block 1's): lmask[s] (bit i =
+// byte i of the segment is a literal), nmatch[s], and the matches mlist[k][s] (k < nmatch[s]):
+// offset in the segment << 23 | (length - 3) << 15 | (distance - 1).  About 8 B per payload byte less
+// than a token per symbol (r02: 4-byte tokens written here and read twice by the emitter).
+constexpr int kMaxM = 21;   // matches per 64-byte segment (each >= 3 bytes)
+constexpr int kR = 2;       // positions per thread per candidate round (r02: R = 1 / 2 / 4 -> ratio 0.6991 /
+                            // 0.7007 / 0.7030, 70.0 / 72.2 / 72.5 GB/s at 20M reads)
+
+__device__ __forceinline__ uint64_t bits_below(uint32_t q) { return q >= 64 ? ~0ull : ((1ull << q) - 1); }
+
+__global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
+                                                   uint64_t *__restrict__ lmask, uint8_t *__restrict__ nmatch,
+                                                   uint32_t *__restrict__ mlist, uint32_t *__restrict__ freq_out) {
+    __shared__ __align__(16) uint32_t in[kPay / 4 + 4];
     __shared__ uint32_t htab[1 << kHashBits];
-    __shared__ uint16_t cand[kSub + 2 * (kSub / 64)];
+    __shared__ uint16_t cand[kSub];
+    __shared__ uint64_t cmask[kT];
     __shared__ uint32_t freq[kFreq];
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint64_t blk = blk0 + blockIdx.x;
     const uint64_t start = blk * kPay;
     const uint32_t len = (uint32_t)min<uint64_t>(kPay, n - start);
-    const uint8_t *s = src + start;
 
-    stage_words<kT, PS>(in, s, len, t);
-    auto cix = [](uint32_t q) { return q + 2 * (q >> 6); };  // candidate q of the sub-block
+    stage_words<kT>(in, src + start, len, t);
     for (int i = t; i < (1 << kHashBits); i += kT) htab[i] = 0;
     for (int i = t; i < kFreq; i += kT) freq[i] = 0;
     __syncthreads();
 
+    const uint64_t seg_base = (uint64_t)blockIdx.x * kNSeg;
     for (int sub = 0; sub < kNSub; ++sub) {
         const uint32_t base = sub * kSub;
+        const uint64_t sg = seg_base + (uint64_t)sub * kT + t;  // this thread's segment, stream order
         if (base >= len) {
-            ntok[((uint64_t)blockIdx.x * kNSub + sub) * kT + t] = 0;
+            lmask[sg] = 0;
+            nmatch[sg] = 0;
             continue;
         }
         const uint32_t end = min(len, base + kSub);
-        // candidates, one round of R * kT consecutive positions at a time
-        for (uint32_t r = base; r < end; r += R * kT) {
-            uint32_t hh[R];
+        // candidates, one round of kR * kT consecutive positions at a time
+        for (uint32_t r = base; r < end; r += kR * kT) {
+            uint32_t hh[kR];
 #pragma unroll
-            for (int k = 0; k < R; ++k) {
+            for (int k = 0; k < kR; ++k) {
                 const uint32_t p = r + k * kT + t;
                 uint32_t h = 0, c = 0;
                 if (p + 4 <= len) {
-                    const uint32_t w = ld32p<PS>(in, p);
+                    const uint32_t w = ld32(in, p);
                     h = hash4(w);
                     const uint32_t j1 = htab[h];
-                    if (j1 && p - (j1 - 1) <= 32768 && ld32p<PS>(in, j1 - 1) == w) c = j1;
+                    if (j1 && p - (j1 - 1) <= 32768 && ld32(in, j1 - 1) == w) c = j1;
                 }
                 hh[k] = h;
-                if (p < end) cand[cix(p - base)] = (uint16_t)c;
+                const uint64_t m = __ballot(c != 0 && p < end);
+                if (p < end) cand[p - base] = (uint16_t)c;
+                if (lane == 0 && r + k * kT + 64 * wv < end) cmask[(r + k * kT + 64 * wv - base) >> 6] = m;
             }
             __syncthreads();
 #pragma unroll
-            for (int k = 0; k < R; ++k) {
+            for (int k = 0; k < kR; ++k) {
                 const uint32_t p = r + k * kT + t;
                 if (p + 4 <= len && p < end) atomicMax(&htab[hh[k]], p + 1);
             }
@@ -161,75 +169,63 @@ __global__ void __launch_bounds__(kT) k_defl_tokens(const uint8_t *__restrict__ 
         }
         // greedy parse of this thread's segment
         const uint32_t s0 = base + t * kSeg, s1 = min(end, s0 + kSeg);
-        uint32_t k = 0;
-        uint32_t *tp = tok + ((uint64_t)blockIdx.x * kNSub + sub) * kSeg * kT + t;
-        for (uint32_t p = s0; p < s1;) {
-            const uint32_t c = p < s1 ? cand[cix(p - base)] : 0;
-            if (LB > 1 && !c) {
-#pragma unroll
-                for (int q = 0; q < LB; ++q) {
-                    if (q > 0 && (p >= s1 || cand[cix(p - base)] != 0)) break;
-                    const uint32_t b = byte_at<PS>(in, p);
-                    atomicAdd(&freq[b], 1u);
-                    tp[(uint64_t)k * kT] = b;
-                    ++k;
-                    ++p;
-                }
-                continue;
-            }
-            uint32_t L = 0;
-            if (c) {
-                const uint32_t j = c - 1;
-                const uint32_t maxL = min(258u, s1 - p);
-                L = min(4u, maxL);
-                if (LB > 1) {  // 8 bytes per step
-                    while (L < maxL) {
-                        const uint32_t x0 = ld32p<PS>(in, p + L) ^ ld32p<PS>(in, j + L);
-                        const uint32_t x1 = ld32p<PS>(in, p + L + 4) ^ ld32p<PS>(in, j + L + 4);
-                        if (x0) {
-                            L += __builtin_ctz(x0) >> 3;
-                            break;
-                        }
-                        if (x1) {
-                            L += 4 + (__builtin_ctz(x1) >> 3);
-                            break;
-                        }
-                        L += 8;
+        uint64_t lit = 0;
+        uint32_t nm = 0;
+        if (s0 < s1) {
+            const uint32_t sl = s1 - s0;
+            const uint64_t cm = cmask[t] & bits_below(sl);
+            uint32_t *mp = mlist + ((uint64_t)blockIdx.x * kMaxM) * kNSeg + (uint64_t)sub * kT + t;
+            for (uint32_t p = 0; p < sl;) {
+                const uint64_t m = cm & ~bits_below(p);
+                const uint32_t q = m ? (uint32_t)__builtin_ctzll(m) : sl;
+                lit |= bits_below(q) & ~bits_below(p);  // literals [p, q)
+                if (q >= sl) break;
+                const uint32_t j = cand[s0 + q - base] - 1, pq = s0 + q;
+                const uint32_t maxL = min(258u, sl - q);
+                uint32_t L = min(4u, maxL);
+                while (L < maxL) {  // 8 bytes per step
+                    const uint32_t x0 = ld32(in, pq + L) ^ ld32(in, j + L);
+                    const uint32_t x1 = ld32(in, pq + L + 4) ^ ld32(in, j + L + 4);
+                    if (x0) {
+                        L += __builtin_ctz(x0) >> 3;
+                        break;
                     }
-                } else {
-                    while (L < maxL) {
-                        const uint32_t x = ld32p<PS>(in, p + L) ^ ld32p<PS>(in, j + L);
-                        if (x == 0) {
-                            L += 4;
-                        } else {
-                            L += __builtin_ctz(x) >> 3;
-                            break;
-                        }
+                    if (x1) {
+                        L += 4 + (__builtin_ctz(x1) >> 3);
+                        break;
                     }
+                    L += 8;
                 }
                 L = min(L, maxL);
+                if (L >= 3) {
+                    const uint32_t d = pq - j;
+                    uint32_t sym, nb, ev, dsym, dnb, dev;
+                    len_code(L, sym, nb, ev);
+                    dist_code(d, dsym, dnb, dev);
+                    atomicAdd(&freq[sym], 1u);
+                    atomicAdd(&freq[kLit + dsym], 1u);
+                    mp[(uint64_t)nm * kNSeg] = (q << 23) | ((L - 3) << 15) | (d - 1);
+                    ++nm;
+                    p = q + L;
+                } else {
+                    lit |= 1ull << q;
+                    p = q + 1;
+                }
             }
-            uint32_t tokv;
-            if (L >= 3) {
-                const uint32_t d = p - (c - 1);
-                uint32_t sym, nb, ev, dsym, dnb, dev;
-                len_code(L, sym, nb, ev);
-                atomicAdd(&freq[sym], 1u);
-                dist_code(d, dsym, dnb, dev);
-                atomicAdd(&freq[kLit + dsym], 1u);
-                tokv = 0x80000000u | ((sym - 257) << 26) | (ev << 21) | (dsym << 16) | dev;
-                p += L;
-            } else {
-                const uint32_t b = byte_at<PS>(in, p);
-                tokv = b;
-                atomicAdd(&freq[b], 1u);
-                p += 1;
+            // literal frequencies: the segment's 64 bytes in four 16-byte LDS reads
+            const uint4 *v4 = (const uint4 *)(in + s0 / 4);
+#pragma unroll
+            for (int w4 = 0; w4 < 4; ++w4) {
+                const uint4 v = v4[w4];
+                const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if ((lit >> (16 * w4 + k)) & 1) atomicAdd(&freq[(ww[k >> 2] >> (8 * (k & 3))) & 0xff], 1u);
             }
-            tp[(uint64_t)k * kT] = tokv;
-            ++k;
         }
-        ntok[((uint64_t)blockIdx.x * kNSub + sub) * kT + t] = (uint8_t)k;
-        __syncthreads();  // cand is reused by the next sub-block
+        lmask[sg] = lit;
+        nmatch[sg] = (uint8_t)nm;
+        __syncthreads();  // cand / cmask are reused by the next sub-block
     }
     for (int i = t; i < kFreq; i += kT) freq_out[(uint64_t)blockIdx.x * kFreq + i] = freq[i];
 }
@@ -342,7 +338,14 @@ __device__ void huff_codes(const uint8_t *len, int n, uint32_t *out) {
 
 __constant__ uint8_t kClOrder[kCl] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-__global__ void __launch_bounds__(64) k_defl_huff(const uint32_t *__restrict__ freq_in, DeflTab *__restrict__ tabs) {
+// extra-bit counts of a length symbol - 257 (0..28) and of a distance symbol (0..29)
+__device__ __forceinline__ uint32_t len_extra(uint32_t ls) { return ls < 8 ? 0u : ls < 28 ? (ls - 4) >> 2 : 0u; }
+__device__ __forceinline__ uint32_t dist_extra(uint32_t ds) { return ds < 4 ? 0u : (ds - 2) >> 1; }
+
+// Also the exact size of the block (sizes[]): header bits + sum over symbols of frequency x (code length +
+// extra bits), so the compressed blocks get their final offsets before they are emitted.
+__global__ void __launch_bounds__(64) k_defl_huff(const uint32_t *__restrict__ freq_in, DeflTab *__restrict__ tabs, uint64_t n,
+                                                 uint64_t blk0, int level, uint32_t *__restrict__ sizes) {
     __shared__ uint32_t f[kFreq];
     __shared__ uint8_t lens[kFreq];
     __shared__ uint32_t fcl[kCl];
@@ -453,20 +456,51 @@ __global__ void __launch_bounds__(64) k_defl_huff(const uint32_t *__restrict__ f
         }
         if (nacc) T.hdr[wi++] = (uint32_t)acc;
         T.hdr_bits = total;
+        ncl = total;  // the header's bit count, for the size below
+    }
+    __syncthreads();
+    uint32_t bits = 0;
+    for (int i = lane; i < kFreq; i += 64) {
+        const uint32_t fr = freq_in[(uint64_t)blockIdx.x * kFreq + i] + (i == 256);  // the real counts + end of block
+        const uint32_t ex = i < 257 ? 0u : i < kLit ? len_extra(i - 257) : dist_extra(i - kLit);
+        bits += fr * (lens[i] + ex);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) bits += __shfl_xor(bits, o, 64);
+    if (lane == 0) {
+        const uint64_t start = (blk0 + blockIdx.x) * kPay;
+        const uint32_t len = (uint32_t)min<uint64_t>(kPay, n - start);
+        const uint32_t dbytes = (ncl + bits + 7) / 8;
+        const uint32_t stored = level == 0 || dbytes > len + 5;
+        const uint32_t total = stored ? 18 + 5 + len + 8 : 18 + dbytes + 8;
+        T.stored = stored;
+        T.total = total;
+        sizes[blockIdx.x] = total;
     }
 }
 
 // ------------------------------------------------------------------------------------ emit
-struct BitW {
+// One 512-thread workgroup per payload (two per CU: 74 KiB of LDS).  The whole BGZF block is assembled in
+// LDS -- header, deflate bits, footer -- and written once, with coalesced dword stores, straight to its
+// final place in the output stream (offset = the chunk's base + the scan of the block sizes k_defl_huff
+// computed): no 64 KiB slot per block and no compaction copy (r02: each lane stored 4-byte words into its
+// own segment's bit range in global memory, 64 lines per wave store, then k_defl_compact copied the block).
+//   1. per segment (the thread's two: sub-block 0 and 1): its 64 payload bytes in registers, the literal
+//      mask and the match list from k_defl_parse; bit count = code lengths of its literals + its matches
+//   2. block scan of the 1024 counts -> every segment's bit offset
+//   3. every thread writes its segments' bits into the LDS image (plain stores inside its range, LDS
+//      atomicOr on the two edge words shared with its neighbours); header bits, end-of-block code,
+//      CRC-32 (from the payload in global memory, slice-by-1 per 128-byte piece, pieces combined) and
+//      ISIZE likewise
+//   4. the image [0, total) goes out at the block's byte offset: aligned dwords inside it, single bytes
+//      at the two ends (the neighbouring blocks own the other bytes of those dwords)
+struct LdsBits {  // LSB-first bit writer into LDS words; its first and last words are shared
     uint32_t *base;
     uint64_t acc;
-    uint32_t nacc;
-    uint32_t wpos;
+    uint32_t nacc, wpos;
     bool first;
-    __device__ void init(uint32_t *b, uint32_t bit) {
-        base = b, acc = 0, nacc = bit & 31, wpos = bit >> 5, first = true;
-    }
-    __device__ __forceinline__ void put(uint32_t v, uint32_t nb) {
+    __device__ __forceinline__ void init(uint32_t *b, uint32_t bit) { base = b, acc = 0, nacc = bit & 31, wpos = bit >> 5, first = true; }
+    __device__ __forceinline__ void put(uint32_t v, uint32_t nb) {  // nb <= 32, nacc < 32 on entry
         acc |= (uint64_t)v << nacc;
         nacc += nb;
         if (nacc >= 32) {
@@ -478,187 +512,196 @@ struct BitW {
             nacc -= 32;
         }
     }
-    __device__ void finish() {
+    __device__ __forceinline__ void finish() {
         if (nacc && (uint32_t)acc) atomicOr(base + wpos, (uint32_t)acc);
     }
 };
 
-// extra-bit counts of a length symbol - 257 (0..28) and of a distance symbol (0..29)
-__device__ __forceinline__ uint32_t len_extra(uint32_t ls) { return ls < 8 ? 0u : ls < 28 ? (ls - 4) >> 2 : 0u; }
-__device__ __forceinline__ uint32_t dist_extra(uint32_t ds) { return ds < 4 ? 0u : (ds - 2) >> 1; }
-
-__device__ __forceinline__ uint32_t tok_bits(uint32_t v, const uint32_t *lit, const uint32_t *dist) {
-    if (!(v >> 31)) return lit[v] >> 16;
-    const uint32_t ls = (v >> 26) & 31, ds = (v >> 16) & 31;
-    return (lit[257 + ls] >> 16) + len_extra(ls) + (dist[ds] >> 16) + dist_extra(ds);
+__device__ __forceinline__ uint32_t match_bits(uint32_t m, const uint32_t *lit, const uint32_t *dist) {
+    const uint32_t L = ((m >> 15) & 255) + 3, D = (m & 0x7fff) + 1;
+    uint32_t sym, nb, ev, dsym, dnb, dev;
+    len_code(L, sym, nb, ev);
+    dist_code(D, dsym, dnb, dev);
+    return (lit[sym] >> 16) + nb + (dist[dsym] >> 16) + dnb;
 }
 
+// a segment's 64 payload bytes (zero past len) into registers
+__device__ __forceinline__ void seg_load(const uint8_t *s, uint32_t s0, uint32_t len, uint32_t (&w)[16]) {
+    if (s0 + kSeg <= len && !((uintptr_t)(s + s0) & 15)) {
+        const uint4 *g = (const uint4 *)(s + s0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = g[k];
+            w[4 * k] = v.x, w[4 * k + 1] = v.y, w[4 * k + 2] = v.z, w[4 * k + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (s0 + 4 * k + b < len) v |= (uint32_t)s[s0 + 4 * k + b] << (8 * b);
+            w[k] = v;
+        }
+    }
+}
 
-// zpow[k][32]: operator of feeding 2^k zero bytes through the (reflected) CRC-32 register
-__global__ void __launch_bounds__(kT) k_defl_emit(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0, int level,
-                                                  const uint32_t *__restrict__ tok, const uint8_t *__restrict__ ntok,
-                                                  const DeflTab *__restrict__ tabs, const uint32_t *__restrict__ zpow,
-                                                  uint8_t *__restrict__ slots, uint32_t *__restrict__ sizes) {
+__device__ __forceinline__ uint32_t seg_bits(const uint32_t (&w)[16], uint64_t lm, uint32_t nm, const uint32_t *mp,
+                                             const uint32_t *lit, const uint32_t *dist) {
+    uint32_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < 64; ++i)
+        if ((lm >> i) & 1) bits += lit[(w[i >> 2] >> (8 * (i & 3))) & 0xff] >> 16;
+    for (uint32_t k = 0; k < nm; ++k) bits += match_bits(mp[(uint64_t)k * kNSeg], lit, dist);
+    return bits;
+}
+
+__device__ __forceinline__ void seg_emit(const uint32_t (&w)[16], uint64_t lm, uint32_t nm, const uint32_t *mp,
+                                         const uint32_t *lit, const uint32_t *dist, uint32_t *img, uint32_t bit) {
+    uint32_t k = 0, m = nm ? mp[0] : 0, moff = nm ? (m >> 23) : 64u;
+    LdsBits bw;
+    bw.init(img, bit);
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        if ((lm >> i) & 1) {
+            const uint32_t c = lit[(w[i >> 2] >> (8 * (i & 3))) & 0xff];
+            bw.put(c & 0xffff, c >> 16);
+        } else if ((uint32_t)i == moff) {
+            const uint32_t L = ((m >> 15) & 255) + 3, D = (m & 0x7fff) + 1;
+            uint32_t sym, nb, ev, dsym, dnb, dev;
+            len_code(L, sym, nb, ev);
+            dist_code(D, dsym, dnb, dev);
+            const uint32_t c = lit[sym];
+            bw.put((c & 0xffff) | (ev << (c >> 16)), (c >> 16) + nb);
+            const uint32_t dc = dist[dsym];
+            bw.put((dc & 0xffff) | (dev << (dc >> 16)), (dc >> 16) + dnb);
+            ++k;
+            if (k < nm) {
+                m = mp[(uint64_t)k * kNSeg];
+                moff = m >> 23;
+            } else {
+                moff = 64;
+            }
+        }
+    }
+    bw.finish();
+}
+
+__global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
+                                                     const uint64_t *__restrict__ lmask, const uint8_t *__restrict__ nmatch,
+                                                     const uint32_t *__restrict__ mlist, const DeflTab *__restrict__ tabs,
+                                                     const uint32_t *__restrict__ zpow, const uint32_t *__restrict__ offs,
+                                                     const uint64_t *__restrict__ cbase, uint8_t *__restrict__ dst) {
+    __shared__ __align__(16) uint32_t img[kSlot / 4 + 4];
     __shared__ uint32_t lit[kLit], dist[kDist];
     __shared__ uint32_t scan[kNSeg];
     __shared__ uint32_t wsum[kT / 64];
-    __shared__ uint32_t sh_total, sh_stored, sh_crc;
     __shared__ uint32_t crctab[1][256];
     __shared__ uint32_t zp[17][32];
     __shared__ uint32_t crcs[kT / 64];
+    __shared__ uint32_t sh_crc;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint64_t blk = blk0 + blockIdx.x;
     const uint64_t start = blk * kPay;
     const uint32_t len = (uint32_t)min<uint64_t>(kPay, n - start);
     const uint8_t *s = src + start;
     const DeflTab &T = tabs[blockIdx.x];
+    const uint32_t total = T.total, stored = T.stored, hb = T.hdr_bits;
     for (int i = t; i < kLit; i += kT) lit[i] = T.lit[i];
     for (int i = t; i < kDist; i += kT) dist[i] = T.dist[i];
     crc_setup<kT, 1>(crctab, zp, zpow, t);
+    for (uint32_t i = t; i < (total + 15) / 16; i += kT) ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    {  // payload CRC-32 from global memory (the tokens kernel keeps its LDS for the match search)
+    {
         const uint32_t c = crc_global512(s, len, crctab, zp, crcs, t);
         if (t == 0) sh_crc = c;
     }
-
-    // bit counts per segment, in stream order (sub-block 0 segments then sub-block 1)
-    uint32_t cnt[kNSub];
-    for (int sub = 0; sub < kNSub; ++sub) {
-        const uint32_t nt = ntok[((uint64_t)blockIdx.x * kNSub + sub) * kT + t];
-        const uint32_t *tp = tok + ((uint64_t)blockIdx.x * kNSub + sub) * kSeg * kT + t;
-        uint32_t b = 0;
-        for (uint32_t k0 = 0; k0 < nt; k0 += 8) {  // every segment owns kSeg token slots: batch the loads
-            uint32_t v[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = tp[(uint64_t)min(k0 + j, (uint32_t)kSeg - 1) * kT];
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (k0 + j < nt) b += tok_bits(v[j], lit, dist);
-        }
-        cnt[sub] = b;
-        scan[sub * kT + t] = b;
-    }
-    __syncthreads();
-    // exclusive scan of scan[0..kNSeg): thread t owns entries 2t, 2t + 1
-    {
-        const uint32_t a = scan[2 * t], b = scan[2 * t + 1];
-        uint32_t x = a + b, inc = x;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o);
-            if (lane >= o) inc += y;
-        }
-        if (lane == 63) wsum[wv] = inc;
-        __syncthreads();
-        uint32_t pre = 0;
-        for (int w = 0; w < wv; ++w) pre += wsum[w];
-        const uint32_t ex = pre + inc - x;
-        __syncthreads();
-        scan[2 * t] = ex;
-        scan[2 * t + 1] = ex + a;
-        if (t == kT - 1) {
-            const uint32_t body = ex + x;
-            const uint32_t bits = T.hdr_bits + body + (lit[256] >> 16);
-            const uint32_t dbytes = (bits + 7) / 8;
-            sh_stored = level == 0 || dbytes > len + 5;
-            sh_total = sh_stored ? 18 + 5 + len + 8 : 18 + dbytes + 8;
-        }
-    }
-    __syncthreads();
-    const uint32_t total = sh_total;
-    const bool stored = sh_stored;
-    uint8_t *out = slots + (uint64_t)blockIdx.x * kSlot;
-    uint32_t *ow = (uint32_t *)out;
-    // zero what the block will occupy (atomicOr targets included)
-    for (uint32_t i = t; i < (total + 15) / 16; i += kT) ((uint4 *)out)[i] = make_uint4(0, 0, 0, 0);
-    // workgroup-scope release/acquire (in __syncthreads) orders these stores before the atomics of
-    // other waves; a device-scope __threadfence would write back the XCD's L2 on gfx950
-    __syncthreads();
-    if (t == 0) {
-        ow[0] = 0x04088b1fu;  // ID1 ID2 CM=8 FLG=FEXTRA
-        ow[1] = 0;            // MTIME
-        ow[2] = 0x0006ff00u;  // XFL=0 OS=255 XLEN=6
-        ow[3] = 0x00024342u;  // 'B' 'C' SLEN=2
-    }
     const uint32_t bsize = total - 1;
     if (stored) {
-        if (t == 0) {
-            out[16] = (uint8_t)bsize, out[17] = (uint8_t)(bsize >> 8);
-            out[18] = 1;
-            out[19] = (uint8_t)len, out[20] = (uint8_t)(len >> 8);
-            out[21] = (uint8_t)~len, out[22] = (uint8_t)(~len >> 8);
-        }
-        for (uint32_t i = t; i < len; i += kT) out[23 + i] = s[i];
-        if (t == 0) {
-            const uint32_t q = 23 + len;
-            const uint32_t c = sh_crc;
-            for (int b = 0; b < 4; ++b) out[q + b] = (uint8_t)(c >> (8 * b)), out[q + 4 + b] = (uint8_t)(len >> (8 * b));
-        }
+        for (uint32_t i = t; i < len; i += kT) ((uint8_t *)img)[23 + i] = s[i];
     } else {
-        uint32_t *bw = ow + 4;  // stream bit 0 = bit 16 of word 4 (byte 18)
-        if (t == 0) atomicOr(ow + 4, bsize & 0xffff);
-        // header bits
-        const uint32_t hb = T.hdr_bits;
-        for (uint32_t i = t; i < (hb + 31) / 32; i += kT) {
-            const uint32_t v = T.hdr[i];
-            atomicOr(bw + i, v << 16);
-            if (v >> 16) atomicOr(bw + i + 1, v >> 16);
-        }
-        for (int sub = 0; sub < kNSub; ++sub) {
-            if (!cnt[sub]) continue;
-            const uint32_t nt = ntok[((uint64_t)blockIdx.x * kNSub + sub) * kT + t];
-            const uint32_t *tp = tok + ((uint64_t)blockIdx.x * kNSub + sub) * kSeg * kT + t;
-            BitW w;
-            w.init(bw, 16 + hb + scan[sub * kT + t]);
-            for (uint32_t k0 = 0; k0 < nt; k0 += 8) {
-              uint32_t vv[8];
+        // 1. the thread's two segments (sub-block 0 and 1): bytes, literal masks, bit counts
+        const uint32_t s0a = t * kSeg, s0b = kSub + t * kSeg;
+        const uint64_t sga = (uint64_t)blockIdx.x * kNSeg + t, sgb = sga + kT;
+        const uint64_t lma = s0a < len ? lmask[sga] : 0, lmb = s0b < len ? lmask[sgb] : 0;
+        const uint32_t nma = s0a < len ? nmatch[sga] : 0, nmb = s0b < len ? nmatch[sgb] : 0;
+        const uint32_t *mpa = mlist + ((uint64_t)blockIdx.x * kMaxM) * kNSeg + t, *mpb = mpa + kT;
+        uint32_t wa[16], wb[16];
+        seg_load(s, s0a, len, wa);
+        seg_load(s, s0b, len, wb);
+        const uint32_t ca = seg_bits(wa, lma, nma, mpa, lit, dist), cb = seg_bits(wb, lmb, nmb, mpb, lit, dist);
+        scan[t] = ca;
+        scan[kT + t] = cb;
+        __syncthreads();
+        // 2. exclusive scan of scan[0..kNSeg): thread t owns entries 2t, 2t + 1
+        {
+            const uint32_t a = scan[2 * t], b = scan[2 * t + 1];
+            uint32_t x = a + b, inc = x;
 #pragma unroll
-              for (int j = 0; j < 8; ++j) vv[j] = tp[(uint64_t)min(k0 + j, (uint32_t)kSeg - 1) * kT];
-#pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                if (k0 + j >= nt) break;
-                const uint32_t v = vv[j];
-                if (!(v >> 31)) {
-                    const uint32_t c = lit[v];
-                    w.put(c & 0xffff, c >> 16);
-                } else {
-                    const uint32_t ls = (v >> 26) & 31, ds = (v >> 16) & 31;
-                    const uint32_t c = lit[257 + ls];
-                    w.put((c & 0xffff) | (((v >> 21) & 31) << (c >> 16)), (c >> 16) + len_extra(ls));
-                    const uint32_t d = dist[ds];
-                    w.put((d & 0xffff) | ((v & 0x1fff) << (d >> 16)), (d >> 16) + dist_extra(ds));
-                }
-              }
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
             }
-            w.finish();
+            if (lane == 63) wsum[wv] = inc;
+            __syncthreads();
+            uint32_t pre = 0;
+            for (int q = 0; q < wv; ++q) pre += wsum[q];
+            const uint32_t ex = pre + inc - x;
+            __syncthreads();
+            scan[2 * t] = ex;
+            scan[2 * t + 1] = ex + a;
         }
-        if (t == kT - 1) {
-            const uint32_t body_end = 16 + hb + scan[kNSeg - 1] + cnt[kNSub - 1];
-            BitW w;
-            w.init(bw, body_end);
+        __syncthreads();
+        // 3. bits into the image: stream bit 0 = byte 18 = bit 144
+        for (uint32_t i = t; i < (hb + 31) / 32; i += kT) {  // the header bit string
+            const uint32_t v = T.hdr[i];
+            atomicOr(img + 4 + i, v << 16);
+            if (v >> 16) atomicOr(img + 5 + i, v >> 16);
+        }
+        if (ca) seg_emit(wa, lma, nma, mpa, lit, dist, img, 144 + hb + scan[t]);
+        if (cb) seg_emit(wb, lmb, nmb, mpb, lit, dist, img, 144 + hb + scan[kT + t]);
+        if (t == kT - 1) {  // end of block after the last segment
+            const uint32_t body_end = 144 + hb + scan[kNSeg - 1] + cb;
+            LdsBits bw;
+            bw.init(img, body_end);
             const uint32_t c = lit[256];
-            w.put(c & 0xffff, c >> 16);  // first flush of a BitW is an atomicOr, as is finish()
-            w.finish();
-            // footer: CRC32, ISIZE right after the last (zero-padded) deflate byte
-            const uint32_t q = 18 + (body_end - 16 + (c >> 16) + 7) / 8;
-            const uint64_t v = (uint64_t)sh_crc | ((uint64_t)len << 32);
-            const uint32_t wi = q >> 2, shb = (q & 3) * 8;
-            const uint64_t sv = v << shb;
-            atomicOr(ow + wi, (uint32_t)sv);
-            atomicOr(ow + wi + 1, (uint32_t)(sv >> 32));
-            if (shb) atomicOr(ow + wi + 2, (uint32_t)(v >> (64 - shb)));
+            bw.put(c & 0xffff, c >> 16);
+            bw.finish();
         }
     }
-    if (t == 0) sizes[blockIdx.x] = total;
-}
-
-__global__ void __launch_bounds__(256) k_defl_compact(const uint8_t *__restrict__ slots, const uint32_t *__restrict__ sizes,
-                                                      const uint32_t *__restrict__ offs, const uint64_t *__restrict__ base,
-                                                      uint8_t *__restrict__ dst) {
-    const uint8_t *s = slots + (uint64_t)blockIdx.x * kSlot;
-    uint8_t *d = dst + *base + offs[blockIdx.x];
-    const uint32_t sz = sizes[blockIdx.x];
-    for (uint32_t i = threadIdx.x; i < sz; i += blockDim.x) d[i] = s[i];
+    __syncthreads();
+    uint8_t *ib = (uint8_t *)img;
+    if (t == 0) {  // BGZF header (the stream's first bits are already in bytes 18, 19) and footer
+        img[0] = 0x04088b1fu;  // ID1 ID2 CM=8 FLG=FEXTRA
+        img[1] = 0;            // MTIME
+        img[2] = 0x0006ff00u;  // XFL=0 OS=255 XLEN=6
+        img[3] = 0x00024342u;  // 'B' 'C' SLEN=2
+        ib[16] = (uint8_t)bsize, ib[17] = (uint8_t)(bsize >> 8);
+        if (stored) {
+            ib[18] = 1;
+            ib[19] = (uint8_t)len, ib[20] = (uint8_t)(len >> 8);
+            ib[21] = (uint8_t)~len, ib[22] = (uint8_t)(~len >> 8);
+        }
+        const uint32_t q = total - 8;
+        for (int b = 0; b < 4; ++b) ib[q + b] = (uint8_t)(sh_crc >> (8 * b)), ib[q + 4 + b] = (uint8_t)(len >> (8 * b));
+    }
+    __syncthreads();
+    // 4. out at the block's final offset
+    uint8_t *D = dst + *cbase + offs[blockIdx.x];
+    const uint32_t sh = (uint32_t)((uintptr_t)D & 3);
+    OGE_G uint32_t *A = (OGE_G uint32_t *)((uintptr_t)D & ~(uintptr_t)3);
+    const uint32_t nwords = (total + sh + 3) / 4;
+    for (uint32_t g = t; g < nwords; g += kT) {
+        const int32_t r0 = (int32_t)(4 * g) - (int32_t)sh;  // block byte of the dword's first byte
+        if (r0 >= 0 && r0 + 4 <= (int32_t)total) {
+            A[g] = ld32(img, (uint32_t)r0);
+        } else {
+            for (int i = 0; i < 4; ++i) {
+                const int32_t r = r0 + i;
+                if (r >= 0 && r < (int32_t)total) ((OGE_G uint8_t *)(A + g))[i] = ib[r];
+            }
+        }
+    }
 }
 
 // exclusive scan of n <= 8192 block sizes, one 1024-thread workgroup, 8 consecutive entries per thread
@@ -670,7 +713,7 @@ __global__ void __launch_bounds__(1024) k_scan_chunk(const uint32_t *__restrict_
     uint32_t a[8], v = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        a[i] = 8 * t + i < n ? in[8 * t + i] : 0u;
+        a[i] = 8 * t + i < n ? in[8 * t + i] : 0;
         v += a[i];
     }
     uint32_t x = v;
@@ -698,8 +741,13 @@ __global__ void __launch_bounds__(1024) k_scan_chunk(const uint32_t *__restrict_
     }
 }
 
-__global__ void k_defl_advance(uint64_t *base, const uint32_t *offs, const uint32_t *sizes, uint32_t nb) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) *base += (uint64_t)offs[nb - 1] + sizes[nb - 1];
+// the chunk's base in the output stream (*cbase) and the running end for the next chunk (*base)
+__global__ void k_defl_advance(uint64_t *base, uint64_t *cbase, const uint32_t *offs, const uint32_t *sizes, uint32_t nb) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        const uint64_t b = *base;
+        *cbase = b;
+        *base = b + (uint64_t)offs[nb - 1] + sizes[nb - 1];
+    }
 }
 
 // ------------------------------------------------------------------------------------ records
@@ -726,54 +774,33 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     *out_bytes = 0;
     if (!n) return OGE_OK;
     const uint64_t nblk = (n + kPay - 1) / kPay;
-    // payloads per chunk: one launch of each kernel.  The Huffman kernel is one serial chain per payload
-    // (latency-bound, little LDS): more payloads per launch amortise that latency.  OGE_DEFL_CHUNK
-    // overrides (256..8192).
-    static const uint64_t chunk_max = [] {
-        const char *e = getenv("OGE_DEFL_CHUNK");
-        const long v = e ? atol(e) : 4096;
-        return (uint64_t)std::min<long>(std::max<long>(v, 256), kMaxChunk);
-    }();
-    const uint64_t chunk = std::min<uint64_t>(nblk, chunk_max);
-    // OGE_DEFL_CAND_R = 1 | 2 | 4: positions per thread per candidate round.  20M C2 reads: 70.0 / 72.2 /
-    // 72.5 GB/s at ratio 0.6991 / 0.7007 / 0.7030 (profiles/r02s3_defl_r.json): 2 by default
-    static const int cand_r = [] {
-        const char *e = getenv("OGE_DEFL_CAND_R");
-        return e && *e ? atoi(e) : 2;
-    }();
-    // OGE_DEFL_LITB = 1 | 2 | 4 | 8 | 16: literals per parse step (with R = 2; > 1 also extends matches 8
-    // bytes per step).  The tokens are the same for every setting.  20M reads: 72.6 / 75.3 / 79.8 / 78.5 /
-    // 72.6 GB/s for 1 / 2 / 4 / 8 / 16 (profiles/r02s3_defl_litb.json): 4 by default
-    static const int lit_batch = [] {
-        const char *e = getenv("OGE_DEFL_LITB");
-        return e && *e ? atoi(e) : 4;
-    }();
-    static const bool pad = [] {  // OGE_DEFL_PAD=0: unpadded tokens LDS layout (A/B)
-        const char *e = getenv("OGE_DEFL_PAD");
-        return !(e && atoi(e) == 0);
-    }();
-    // Chunks go round-robin over S streams: one chunk's Huffman and emit kernels (small LDS) run on
-    // the CUs beside another chunk's tokens workgroups (153 KiB of LDS, one per CU); only the
-    // compaction, which advances the running output offset, is ordered chunk after chunk (events).
+    // payloads per chunk: one launch of each kernel (4096 measured best in r02: 2048 / 4096 / 8192,
+    // profiles/r02_ab/codec_k*.json)
+    const uint64_t chunk = std::min<uint64_t>(nblk, 4096);
+    // Chunks go round-robin over S streams: one chunk's Huffman and emit kernels run on the CUs beside
+    // another chunk's parse workgroups (150 KiB of LDS, one per CU); only the offset advance, which
+    // gives each chunk its base in the output stream, is ordered chunk after chunk (events).
     const int S = nblk > chunk ? 3 : 1;
     struct Bufs {
-        uint32_t *tok, *freq, *sizes, *offs;
-        uint8_t *ntok, *slots;
+        uint64_t *lmask, *cbase;
+        uint32_t *mlist, *freq, *sizes, *offs;
+        uint8_t *nmatch;
         DeflTab *tabs;
         hipStream_t st;
     } B[3];
     for (int s = 0; s < S; ++s) {
         const std::string x = std::to_string(s);
-        B[s].tok = (uint32_t *)ctx->ws(("defl_tok" + x).c_str(), chunk * kNSub * kSeg * kT * 4);
-        B[s].ntok = (uint8_t *)ctx->ws(("defl_ntok" + x).c_str(), chunk * kNSeg);
+        B[s].lmask = (uint64_t *)ctx->ws(("defl_lmask" + x).c_str(), chunk * kNSeg * 8);
+        B[s].nmatch = (uint8_t *)ctx->ws(("defl_nmatch" + x).c_str(), chunk * kNSeg);
+        B[s].mlist = (uint32_t *)ctx->ws(("defl_mlist" + x).c_str(), chunk * kMaxM * kNSeg * 4);
         B[s].freq = (uint32_t *)ctx->ws(("defl_freq" + x).c_str(), chunk * kFreq * 4);
         B[s].tabs = (DeflTab *)ctx->ws(("defl_tabs" + x).c_str(), chunk * sizeof(DeflTab));
-        B[s].slots = (uint8_t *)ctx->ws(("defl_slots" + x).c_str(), chunk * kSlot);
         B[s].sizes = (uint32_t *)ctx->ws(("defl_sizes" + x).c_str(), chunk * 4 + 16);
         B[s].offs = (uint32_t *)ctx->ws(("defl_offs" + x).c_str(), chunk * 4 + 16);
+        B[s].cbase = (uint64_t *)ctx->ws(("defl_cbase" + x).c_str(), 16);
         B[s].st = S == 1 ? ctx->stream : ctx->side_stream(s);
-        if (!B[s].tok || !B[s].ntok || !B[s].freq || !B[s].tabs || !B[s].slots || !B[s].sizes || !B[s].offs ||
-            !B[s].st)
+        if (!B[s].lmask || !B[s].nmatch || !B[s].mlist || !B[s].freq || !B[s].tabs || !B[s].sizes || !B[s].offs ||
+            !B[s].cbase || !B[s].st)
             return OGE_ERR_HIP;
     }
     uint32_t *zpow = (uint32_t *)ctx->ws("defl_zpow", 17 * 32 * 4);
@@ -800,31 +827,26 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk, ++k) {
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
         Bufs &u = B[k % S];
-        if (!pad) k_defl_tokens<31, 1, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (lit_batch >= 16) k_defl_tokens<4, 2, 16><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (lit_batch >= 8) k_defl_tokens<4, 2, 8><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (lit_batch >= 4 && cand_r >= 4) k_defl_tokens<4, 4, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (lit_batch >= 4) k_defl_tokens<4, 2, 4><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (lit_batch == 2) k_defl_tokens<4, 2, 2><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (cand_r >= 4) k_defl_tokens<4, 4, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else if (cand_r == 2) k_defl_tokens<4, 2, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
-        else k_defl_tokens<4, 1, 1><<<nb, kT, 0, u.st>>>(d_src, n, b0, u.tok, u.ntok, u.freq);
+        k_defl_parse<<<nb, kT, 0, u.st>>>(d_src, n, b0, u.lmask, u.nmatch, u.mlist, u.freq);
         OGE_LAUNCH_CHECK(ctx);
-        k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs);
-        OGE_LAUNCH_CHECK(ctx);
-        k_defl_emit<<<nb, kT, 0, u.st>>>(d_src, n, b0, level, u.tok, u.ntok, u.tabs, zpow, u.slots, u.sizes);
+        k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs, n, b0, level, u.sizes);
         OGE_LAUNCH_CHECK(ctx);
         k_scan_chunk<<<1, 1024, 0, u.st>>>(u.sizes, nb, u.offs);
         OGE_LAUNCH_CHECK(ctx);
         if (k) OGE_HIP_TRY(ctx, hipStreamWaitEvent(u.st, ev[(k - 1) % S], 0));  // previous chunk's offset advance
-        k_defl_compact<<<nb, 256, 0, u.st>>>(u.slots, u.sizes, u.offs, base, d_dst);
-        OGE_LAUNCH_CHECK(ctx);
-        k_defl_advance<<<1, 64, 0, u.st>>>(base, u.offs, u.sizes, nb);
+        k_defl_advance<<<1, 64, 0, u.st>>>(base, u.cbase, u.offs, u.sizes, nb);
         OGE_LAUNCH_CHECK(ctx);
         OGE_HIP_TRY(ctx, hipEventRecord(ev[k % S], u.st));
+        k_defl_emit<<<nb, kT, 0, u.st>>>(d_src, n, b0, u.lmask, u.nmatch, u.mlist, u.tabs, zpow, u.offs, u.cbase, d_dst);
+        OGE_LAUNCH_CHECK(ctx);
     }
-    // the last chunk's advance follows every earlier compaction: the context stream waits for it
-    if (S > 1) OGE_HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[(k - 1) % S], 0));
+    // every chunk's emit: the context stream waits for all side streams
+    if (S > 1) {
+        for (int s = 0; s < S; ++s) {
+            OGE_HIP_TRY(ctx, hipEventRecord(ev[s], B[s].st));
+            OGE_HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[s], 0));
+        }
+    }
     ctx->end_stage(tm);
     uint64_t total = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&total, base, 8, hipMemcpyDeviceToHost, ctx->stream));

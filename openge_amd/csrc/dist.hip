@@ -29,6 +29,7 @@
 #include "dev_util.h"
 #include "dist_local.h"
 #include "dist_plan.h"
+#include "dist_shm.h"
 #include "markdup_stages.h"
 #include "records.h"
 #include "rec_parse.h"
@@ -37,6 +38,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <random>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -117,6 +119,41 @@ struct LocalTransport : OgeTransport {
         oge_dist::LocalColl<HipOps> c{*hub, rank, ops};
         return c.reduce_scatter_max_u8(in, out, chunk) ? oge_fail(ctx, OGE_ERR_HIP, "local transport: reduce-scatter failed")
                                                        : OGE_OK;
+    }
+};
+
+// the host-staged transport's memory operations (dist_shm.h), on the context stream
+struct StageOps {
+    oge_ctx *ctx;
+    int d2h(void *h, const void *d, size_t n) { return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess ? 0 : -1; }
+    int h2d(void *d, const void *h, size_t n) { return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, ctx->stream) == hipSuccess ? 0 : -1; }
+    int d2d(void *d, const void *s, size_t n) { return hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess ? 0 : -1; }
+    int sync() { return hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : -1; }
+};
+
+struct ShmTransport : OgeTransport {
+    std::unique_ptr<oge_dist::ShmSeg> seg;
+    const char *name() const override { return "host"; }
+    int alltoallv(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv, const uint64_t *rbytes,
+                  const uint64_t *roff) override {
+        StageOps ops{ctx};
+        oge_dist::ShmColl<StageOps> c{*seg, ops};
+        const int rc = c.alltoallv(send, sbytes, soff, recv, rbytes, roff);
+        return rc ? oge_fail(ctx, OGE_ERR_HIP, rc == -2 ? "host transport: all-to-all timed out (a rank did not arrive)"
+                                                       : "host transport: all-to-all failed")
+                  : OGE_OK;
+    }
+    int allgather_host(oge_ctx *ctx, const void *in, void *out, size_t bytes) override {
+        StageOps ops{ctx};
+        oge_dist::ShmColl<StageOps> c{*seg, ops};
+        return c.allgather_host(in, out, bytes) ? oge_fail(ctx, OGE_ERR_HIP, "host transport: allgather timed out") : OGE_OK;
+    }
+    int reduce_scatter_max_u8(oge_ctx *ctx, const uint8_t *in, uint8_t *out, size_t chunk) override {
+        StageOps ops{ctx};
+        oge_dist::ShmColl<StageOps> c{*seg, ops};
+        const int rc = c.reduce_scatter_max_u8(in, out, chunk);
+        return rc ? oge_fail(ctx, OGE_ERR_HIP, rc == -2 ? "host transport: reduce-scatter timed out" : "host transport: reduce-scatter failed")
+                  : OGE_OK;
     }
 };
 
@@ -463,11 +500,14 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     uint64_t *roff = (uint64_t *)ctx->ws("dist_roff", (R + 1) * 8);
     if (!rbuf || !rsz || !roff) rc = OGE_ERR_HIP;
     if ((rc = D.agree(rc))) return rc;
-    if ((rc = D.a2a(pb, 1, sbuf, rbuf))) return rc;
-    if ((rc = D.a2a(pr, 4, ssz, rsz))) return rc;
-    hipLaunchKernelGGL(k_off_from_u32, dim3(oge_ceil_div(R + 1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)rsz, R, roff);
-    OGE_LAUNCH_CHECK(ctx);
-    rc = oge_exclusive_scan_u64(ctx, roff, roff, R + 1);
+    // every rank makes both exchanges; a failure goes to the agree() below, never straight out
+    rc = D.a2a(pb, 1, sbuf, rbuf);
+    if (const int r2 = D.a2a(pr, 4, ssz, rsz)) rc = rc ? rc : r2;
+    if (!rc) {
+        hipLaunchKernelGGL(k_off_from_u32, dim3(oge_ceil_div(R + 1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)rsz, R, roff);
+        rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    }
+    if (!rc) rc = oge_exclusive_scan_u64(ctx, roff, roff, R + 1);
     ctx->end_stage(t);
     if ((rc = D.agree(rc))) return rc;
     if (R > 0xFFFFFFFEull) rc = oge_fail(ctx, OGE_ERR_LIMIT, "multi-GPU: more than 2^32-2 records on one rank after the exchange");
@@ -518,8 +558,8 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
     if (!rc && (oge_sort_buffers(ctx, R, &skeys, &svals) || !counts)) rc = OGE_ERR_HIP;
     meta = (RecMeta *)ctx->ws("md_meta", (R + 1) * sizeof(RecMeta));
     if (!rc && !meta) rc = OGE_ERR_HIP;
+    if (!rc) rc = hipMemsetAsync(counts, 0, 16, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
     if (!rc) {
-        OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 16, ctx->stream));
         t = ctx->begin_stage("input_pass");
         OgePassArgs a = {};
         a.recs = rbuf;
@@ -602,8 +642,9 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
         uint32_t *fvr = (uint32_t *)ctx->ws("dist_fvr", (pf.rtot + 1) * 4);
         if (!fkr || !fvr) rc = OGE_ERR_HIP;
         if ((rc = D.agree(rc))) return rc;
-        if ((rc = D.a2a(pf, 8, fks, fkr)) || (rc = D.a2a(pf, 4, fvs, fvr))) return rc;
-        rc = oge_md_frag_groups(ctx, fkr, fvr, pf.rtot, dup_pad);
+        rc = D.a2a(pf, 8, fks, fkr);
+        if (const int r2 = D.a2a(pf, 4, fvs, fvr)) rc = rc ? rc : r2;
+        if (!rc) rc = oge_md_frag_groups(ctx, fkr, fvr, pf.rtot, dup_pad);
         if ((rc = D.agree(rc))) return rc;
     }
     ctx->end_stage(t);
@@ -675,17 +716,22 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
         if (!cmr || !cgr || !mrr || !rco || !rbo) rc = OGE_ERR_HIP;
         if ((rc = D.agree(rc))) return rc;
         uint8_t *mrec = (uint8_t *)ctx->ws("dist_mrec", 64);
-        if ((rc = D.a2a(pc, sizeof(RecMeta), cms, cmr)) || (rc = D.a2a(pc, 4, cgs, cgr)) || (rc = D.a2a(pm, 1, mrec, mrr))) return rc;
-        if (nr) {
-            OGE_HIP_TRY(ctx, hipMemcpyAsync(rco, pc.roff.data(), 8 * (G + 1), hipMemcpyHostToDevice, ctx->stream));
-            OGE_HIP_TRY(ctx, hipMemcpyAsync(rbo, pm.roff.data(), 8 * (G + 1), hipMemcpyHostToDevice, ctx->stream));
-            hipLaunchKernelGGL(k_minirec_fix, dim3(oge_ceil_div(nr, kT)), dim3(kT), 0, ctx->stream, cmr, nr, (const uint64_t *)rco,
-                               (const uint64_t *)rbo, (uint32_t)G);
-            OGE_LAUNCH_CHECK(ctx);
+        rc = D.a2a(pc, sizeof(RecMeta), cms, cmr);
+        if (const int r2 = D.a2a(pc, 4, cgs, cgr)) rc = rc ? rc : r2;
+        if (const int r3 = D.a2a(pm, 1, mrec, mrr)) rc = rc ? rc : r3;
+        if (!rc && nr) {
+            if (hipMemcpyAsync(rco, pc.roff.data(), 8 * (G + 1), hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+                hipMemcpyAsync(rbo, pm.roff.data(), 8 * (G + 1), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+                rc = dist_hip_fail(ctx, __LINE__);
+            if (!rc) {
+                hipLaunchKernelGGL(k_minirec_fix, dim3(oge_ceil_div(nr, kT)), dim3(kT), 0, ctx->stream, cmr, nr, (const uint64_t *)rco,
+                                   (const uint64_t *)rbo, (uint32_t)G);
+                rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+            }
         }
         // the owner's join: arrival order (source rank, then sorted position) = global order
         OgeMdFrags F2;
-        rc = oge_md_cand_frag(ctx, opts, cmr, nr, false, &F2);
+        if (!rc) rc = oge_md_cand_frag(ctx, opts, cmr, nr, false, &F2);
         if (!rc) rc = oge_md_join_build(ctx, opts, mrr, cmr, nr, F2, &P);
         if (!rc && P.np) {
             hipLaunchKernelGGL(k_map_pair_idx, dim3(oge_ceil_div(P.np, kT)), dim3(kT), 0, ctx->stream, P.idx, P.np, (const uint32_t *)cgr);
@@ -728,8 +774,10 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
         Q.idx = (uint2 *)ctx->ws("dist_ridx", (pp.rtot + 1) * 8);
         if (!Q.hi || !Q.lo || !Q.idx) rc = OGE_ERR_HIP;
         if ((rc = D.agree(rc))) return rc;
-        if ((rc = D.a2a(pp, 8, shi, Q.hi)) || (rc = D.a2a(pp, 8, slo, Q.lo)) || (rc = D.a2a(pp, 8, sidx, Q.idx))) return rc;
-        rc = oge_md_pairs_rehash(ctx, &Q);
+        rc = D.a2a(pp, 8, shi, Q.hi);
+        if (const int r2 = D.a2a(pp, 8, slo, Q.lo)) rc = rc ? rc : r2;
+        if (const int r3 = D.a2a(pp, 8, sidx, Q.idx)) rc = rc ? rc : r3;
+        if (!rc) rc = oge_md_pairs_rehash(ctx, &Q);
         if (!rc) rc = oge_md_pair_groups(ctx, opts, Q, dup_pad);
         if ((rc = D.agree(rc))) return rc;
     }
@@ -737,11 +785,11 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
 
     // ---- dup marks meet; 4. apply + gather
     t = ctx->begin_stage("dist_reduce");
-    if ((rc = comm->tr->reduce_scatter_max_u8(ctx, dup_pad, dup, stride))) return rc;
+    rc = comm->tr->reduce_scatter_max_u8(ctx, dup_pad, dup, stride);
     ctx->end_stage(t);
     t = ctx->begin_stage("md_apply");
     uint64_t nd = 0;
-    rc = oge_md_apply_desc(ctx, desc0, R, dup, desc, &nd);
+    if (!rc) rc = oge_md_apply_desc(ctx, desc0, R, dup, desc, &nd);
     ctx->end_stage(t);
     if (!rc) rc = oge_gather_with_sizes(ctx, rbuf, roff, v, k, R, out, out_off, meta, dup, desc);
     if (!rc) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
@@ -774,31 +822,78 @@ int oge_comm_sum_u64(oge_comm *comm, uint64_t *v, int count) {
 // ---------------------------------------------------------------------------------------------- ABI
 extern "C" {
 
+// The id = RCCL's unique id + 16 random bytes that name the node-local meeting of ranks sharing a GPU.
+constexpr size_t kIdNonce = 16;
+
 int oge_comm_unique_id(uint8_t *id_out, uint64_t bytes) {
-    if (!id_out || bytes < sizeof(ncclUniqueId)) return oge_fail(nullptr, OGE_ERR_ARG, "oge_comm_unique_id: buffer too small");
+    if (!id_out || bytes < sizeof(ncclUniqueId) + kIdNonce) return oge_fail(nullptr, OGE_ERR_ARG, "oge_comm_unique_id: buffer too small");
     ncclUniqueId id;
     ncclResult_t r = ncclGetUniqueId(&id);
     if (r != ncclSuccess) return oge_fail(nullptr, OGE_ERR_HIP, ncclGetErrorString(r));
     memcpy(id_out, &id, sizeof id);
+    std::random_device rd;
+    for (size_t i = 0; i < kIdNonce; i += 4) {
+        const uint32_t v = rd();
+        memcpy(id_out + sizeof id + i, &v, 4);
+    }
     return OGE_OK;
 }
 
-uint64_t oge_comm_unique_id_bytes(void) { return sizeof(ncclUniqueId); }
+uint64_t oge_comm_unique_id_bytes(void) { return sizeof(ncclUniqueId) + kIdNonce; }
 
+// Transport of one rank (OGE_COMM = rccl | host | auto, default auto): RCCL when the ranks' devices are
+// distinct, the host-staged transport (dist_shm.h) when ranks share one.  auto: a process that sees at
+// least `nranks` devices takes RCCL at once (bench.py / the CLI give rank r device r % count); with fewer
+// visible devices than ranks the ranks meet in the shared segment named by the id and compare their
+// devices' PCI bus ids -- all distinct (e.g. one visible device per process) -> RCCL, else host.
 int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, oge_comm **out) {
     if (!ctx || !id || !out || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
         return oge_fail(ctx, OGE_ERR_ARG, "oge_comm_init_rank: bad arguments");
     (void)hipSetDevice(ctx->device);
-    auto t = std::make_unique<RcclTransport>();
-    ncclUniqueId uid;
-    memcpy(&uid, id, sizeof uid);
-    ncclResult_t r = ncclCommInitRank(&t->comm, nranks, uid, rank);
-    if (r != ncclSuccess) return oge_fail(ctx, OGE_ERR_HIP, (std::string("ncclCommInitRank: ") + ncclGetErrorString(r)).c_str());
-    t->rank = rank;
-    t->size = nranks;
+    const char *e = getenv("OGE_COMM");
+    std::string mode = e && *e ? e : "auto";
+    if (mode == "local") mode = "host";  // oge_comm_init's in-process name for "ranks share a GPU"
+    if (mode != "auto" && mode != "rccl" && mode != "host")
+        return oge_fail(ctx, OGE_ERR_ARG, "OGE_COMM must be auto, rccl or host");
+    int ndev = 0;
+    (void)hipGetDeviceCount(&ndev);
+    std::unique_ptr<oge_dist::ShmSeg> seg;
+    if (mode == "host" || (mode == "auto" && ndev < nranks)) {
+        char bus[64] = {0};
+        (void)hipDeviceGetPCIBusId(bus, sizeof bus - 1, ctx->device);
+        uint64_t h = 1469598103934665603ull;  // FNV-1a of the whole id names the meeting
+        for (size_t i = 0; i < sizeof(ncclUniqueId) + kIdNonce; ++i) h = (h ^ id[i]) * 1099511628211ull;
+        char name[64];
+        snprintf(name, sizeof name, "oge_comm_%016llx", (unsigned long long)h);
+        std::string err;
+        seg.reset(oge_dist::ShmSeg::open(name, nranks, rank, oge_dist::ShmSeg::default_stage_bytes(), bus, &err));
+        if (!seg) return oge_fail(ctx, OGE_ERR_HIP, err.c_str());
+        bool shared = false;
+        for (int a = 0; a < nranks; ++a)
+            for (int b = a + 1; b < nranks; ++b) shared = shared || !strcmp(seg->post(a).bus, seg->post(b).bus);
+        if (mode == "auto" && !shared) seg.reset();  // distinct GPUs: RCCL after all
+    }
     oge_comm *c = new oge_comm();
     c->ctx = ctx;
-    c->tr = std::move(t);
+    if (seg) {
+        auto t = std::make_unique<ShmTransport>();
+        t->seg = std::move(seg);
+        t->rank = rank;
+        t->size = nranks;
+        c->tr = std::move(t);
+    } else {
+        auto t = std::make_unique<RcclTransport>();
+        ncclUniqueId uid;
+        memcpy(&uid, id, sizeof uid);
+        ncclResult_t r = ncclCommInitRank(&t->comm, nranks, uid, rank);
+        if (r != ncclSuccess) {
+            delete c;
+            return oge_fail(ctx, OGE_ERR_HIP, (std::string("ncclCommInitRank: ") + ncclGetErrorString(r)).c_str());
+        }
+        t->rank = rank;
+        t->size = nranks;
+        c->tr = std::move(t);
+    }
     *out = c;
     return OGE_OK;
 }

@@ -6,16 +6,8 @@
 //
 //   oge_bgzf_index (host)  walks the BGZF framing: per block the deflate byte range, the payload
 //                          offset (prefix sum of ISIZE) and the stored CRC-32.
-//   k_inflate              one wave per block.  The whole decoder runs wave-uniform (every lane
-//                          computes the same symbol), so its state lives in scalar registers; the
-//                          compressed bits stream through two VGPRs (256 bytes each, lane l holding
-//                          word l) read with v_readlane, decode tables (10-bit direct lookup + the
-//                          canonical count/offset walk for longer codes) sit in LDS.  Output goes
-//                          through a 4 KiB LDS ring (literals written by lane 0, back-references
-//                          copied by all 64 lanes at once) flushed to HBM 256 bytes at a time;
-//                          only references further back than the ring read HBM.
-//   k_crc_check            one 512-thread workgroup per block: the payload staged in LDS, slice-by-4
-//                          CRC-32 combined across threads; any mismatch fails the call.
+//   inflate itself          inflate_lane.hip: one lane per BGZF block (Huffman decode), then one
+//                          workgroup per block (LZ77 resolution, CRC-32 check, write-out).
 //   k_rec_walk             BAM record boundaries: one thread per 64 KiB chunk walks the block_size
 //                          chain from its chunk's first record start (found by a 16-record
 //                          plausibility chain); the host verifies that every chunk's walk ends where
@@ -35,725 +27,6 @@
 namespace {
 
 using namespace oge_bgzf;
-
-__constant__ uint16_t kLBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                    31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t kLExt[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t kDBase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
-                                    193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t kDExt[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-__constant__ uint8_t kClOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
-
-// Wave-uniform LSB-first bit reader over the compressed bytes: a 64-bit scalar bit buffer refilled
-// 32 bits at a time (v_readlane) from two 256-byte chunks held one word per lane.  All state is
-// wave-uniform and kept in SGPRs (table entries are readfirstlane'd), which keeps the per-symbol path
-// to a few scalar instructions.
-struct Bits {
-    const uint32_t *zw;
-    uint64_t zwords;
-    uint64_t wbase;  // absolute word index of relative word 0
-    uint32_t widx;   // next relative word to enter the buffer
-    uint32_t cbase;  // relative word held by lane 0 of `cur`
-    uint32_t cur, nxt;
-    uint64_t buf;    // low `cnt` bits are the next bits of the stream
-    uint32_t cnt;
-    __device__ __forceinline__ uint32_t ldw(uint32_t rel) const {
-        const uint64_t w = wbase + rel;
-        return w < zwords ? zw[w] : 0u;
-    }
-    __device__ __forceinline__ void refill() {
-        while (cnt <= 32) {
-            const uint32_t r = widx - cbase;
-            const uint32_t w = __builtin_amdgcn_readlane(r < 64 ? cur : nxt, r & 63);
-            buf |= (uint64_t)w << cnt;
-            cnt += 32;
-            ++widx;
-            if (widx - cbase >= 64) {
-                cur = nxt;
-                cbase += 64;
-                nxt = ldw(cbase + 64 + (threadIdx.x & 63));
-            }
-        }
-    }
-    __device__ void seek(uint64_t bit) {
-        wbase = bit >> 5;
-        widx = cbase = 0;
-        const uint32_t l = threadIdx.x & 63;
-        cur = ldw(l);
-        nxt = ldw(64 + l);
-        buf = 0;
-        cnt = 0;
-        refill();
-        skip((uint32_t)(bit & 31));
-    }
-    __device__ __forceinline__ uint64_t bitpos() const { return (wbase + widx) * 32 - cnt; }
-    __device__ __forceinline__ uint32_t peek() const { return (uint32_t)buf; }
-    __device__ __forceinline__ void skip(uint32_t n) {  // n <= 32
-        buf >>= n;
-        cnt -= n;
-        if (cnt <= 32) refill();
-    }
-    __device__ __forceinline__ uint32_t get(uint32_t n) {  // n <= 31
-        const uint32_t v = (uint32_t)buf & ((1u << n) - 1);
-        skip(n);
-        return v;
-    }
-};
-
-// Canonical Huffman decode tables for one alphabet (RFC 1951 3.2.2): tab = 2^TB direct entries
-// (symbol | length << 9, 0 = longer code or unused), cnt[len] and sym[] (symbols ordered by (length,
-// value)) for the bit-by-bit walk.  Returns false for an over-subscribed code.
-template <int TB>
-__device__ bool build_table(const uint8_t *lens, int n, uint16_t *tab, uint32_t *cnt, uint16_t *sym, uint32_t *first,
-                            uint32_t *offs) {
-    const int lane = threadIdx.x;
-    for (int i = lane; i < (1 << TB); i += 64) tab[i] = 0;
-    uint32_t tot[16];
-#pragma unroll
-    for (int b = 0; b < 16; ++b) tot[b] = 0;
-    for (int c0 = 0; c0 < n; c0 += 64) {
-        const int s = c0 + lane;
-        const uint32_t L = s < n ? lens[s] : 0;
-#pragma unroll
-        for (int b = 1; b < 16; ++b) tot[b] += __popcll(__ballot(L == (uint32_t)b));
-    }
-    int left = 1;
-#pragma unroll
-    for (int b = 1; b < 16; ++b) {
-        left = 2 * left - (int)tot[b];
-        if (left < 0) return false;
-    }
-    if (lane == 0) {
-        uint32_t code = 0, off = 0;
-        cnt[0] = 0;
-#pragma unroll
-        for (int b = 1; b < 16; ++b) {
-            code = (code + (b > 1 ? tot[b - 1] : 0)) << (b > 1 ? 1 : 0);
-            first[b] = code;
-            offs[b] = off;
-            off += tot[b];
-            cnt[b] = tot[b];
-        }
-    }
-    __syncthreads();
-    uint32_t run[16];
-#pragma unroll
-    for (int b = 0; b < 16; ++b) run[b] = 0;
-    const uint64_t lt = (1ull << lane) - 1;
-    for (int c0 = 0; c0 < n; c0 += 64) {
-        const int s = c0 + lane;
-        const uint32_t L = s < n ? lens[s] : 0;
-        uint32_t rank = 0;
-#pragma unroll
-        for (int b = 1; b < 16; ++b) {
-            const uint64_t m = __ballot(L == (uint32_t)b);
-            if (L == (uint32_t)b) rank = run[b] + __popcll(m & lt);
-            run[b] += __popcll(m);
-        }
-        if (L) {
-            const uint32_t code = first[L] + rank;
-            sym[offs[L] + rank] = (uint16_t)s;
-            if (L <= (uint32_t)TB) {
-                const uint32_t r = __builtin_bitreverse32(code) >> (32 - L);
-                const uint16_t e = (uint16_t)(s | (L << 9));
-                for (uint32_t k = 0; k < (1u << (TB - L)); ++k) tab[r | (k << L)] = e;
-            }
-        }
-    }
-    __syncthreads();
-    return true;
-}
-
-template <int TB>
-__device__ __forceinline__ int decode_sym(Bits &br, const uint16_t *tab, const uint32_t *cnt, const uint16_t *sym) {
-    const uint32_t v = br.peek();
-    const uint32_t e = __builtin_amdgcn_readfirstlane(tab[v & ((1u << TB) - 1)]);
-    if (e) {
-        br.skip(e >> 9);
-        return (int)(e & 511);
-    }
-    int code = 0, first = 0, index = 0;
-    for (int len = 1; len <= 15; ++len) {
-        code |= (int)((v >> (len - 1)) & 1);
-        const int count = (int)__builtin_amdgcn_readfirstlane(cnt[len]);
-        if (code - count < first) {
-            br.skip(len);
-            return (int)__builtin_amdgcn_readfirstlane(sym[index + (code - first)]);
-        }
-        index += count;
-        first += count;
-        first <<= 1;
-        code <<= 1;
-    }
-    return -1;
-}
-
-constexpr uint32_t kRing = 4096;
-
-enum { E_STORED = 1, E_CODE = 2, E_OVERRUN = 3, E_LEN = 4, E_DIST = 5, E_FAR = 6, E_TYPE = 7, E_PAST = 8, E_SIZE = 9,
-       E_TABLE = 10, E_CRC = 11 };
-
-__device__ __forceinline__ void report(uint32_t *err, uint32_t code, uint64_t blk) {
-    atomicOr(err, 1u << code);
-    atomicMin(err + 1, (uint32_t)min<uint64_t>(blk, 0xffffffffull));
-}
-
-__global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ z, uint64_t zbytes, const uint64_t *__restrict__ d0,
-                                                const uint64_t *__restrict__ d1, const uint64_t *__restrict__ uoff,
-                                                uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
-    __shared__ uint16_t ltab[1024], dtab[1024], ctab[128];
-    __shared__ uint32_t lcnt[16], dcnt[16], ccnt[16], tfirst[16], toffs[16];
-    __shared__ uint16_t lsym[288], dsym[32], csym[19];
-    __shared__ uint8_t lens[320], cl[19];
-    // the most recent kRing output bytes; whole 256-byte chunks are flushed to `o` by the wave
-    __shared__ uint8_t ring[kRing];
-    const int lane = threadIdx.x;
-    const uint64_t b = blockIdx.x;
-    Bits br;
-    br.zw = (const uint32_t *)z;
-    br.zwords = (zbytes + 3) / 4;
-    br.seek(d0[b] * 8);
-    const uint64_t end_bit = d1[b] * 8;
-    uint8_t *o = out + uoff[b];
-    const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
-    uint32_t pos = 0, flushed = 0;
-    int e = 0;
-    auto flush = [&](uint32_t upto) {  // ring bytes [flushed, upto) -> o (byte stores, 64 lanes)
-        for (uint32_t q0 = flushed; q0 < upto; q0 += 64) {  // uniform trip count keeps pos/flushed scalar
-            const uint32_t q = q0 + lane;
-            if (q < upto) o[q] = ring[q & (kRing - 1)];
-        }
-        flushed = upto;
-    };
-    for (;;) {
-        const uint32_t h = br.get(3);
-        const uint32_t type = h >> 1;
-        if (type == 0) {
-            br.skip((8 - (uint32_t)(br.bitpos() & 7)) & 7);
-            const uint32_t len = br.get(16), nlen = br.get(16);
-            const uint64_t src = br.bitpos() >> 3;
-            if ((len ^ 0xffffu) != nlen || pos + len > osz || src + len > d1[b]) {
-                e = E_STORED;
-                break;
-            }
-            for (uint32_t i = 0; i < len; i += 64) {
-                const uint32_t m = min(64u, len - i);
-                if ((uint32_t)lane < m) ring[(pos + lane) & (kRing - 1)] = z[src + i + lane];
-                pos += m;
-                if (pos - flushed >= 256) flush(pos & ~255u);
-            }
-            br.seek(br.bitpos() + (uint64_t)len * 8);
-        } else if (type == 1 || type == 2) {
-            int hlit = 288, hdist = 30;
-            if (type == 1) {
-                for (int s = lane; s < 318; s += 64)
-                    lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
-                __syncthreads();
-            } else {
-                hlit = (int)br.get(5) + 257;
-                hdist = (int)br.get(5) + 1;
-                const int hclen = (int)br.get(4) + 4;
-                if (hlit > 286 || hdist > 30) {
-                    e = E_TABLE;
-                    break;
-                }
-                if (lane < 19) cl[lane] = 0;
-                __syncthreads();
-                for (int i = 0; i < hclen; ++i) {
-                    const uint32_t v = br.get(3);
-                    if (lane == 0) cl[kClOrd[i]] = (uint8_t)v;
-                }
-                __syncthreads();
-                if (!build_table<7>(cl, 19, ctab, ccnt, csym, tfirst, toffs)) {
-                    e = E_TABLE;
-                    break;
-                }
-                const int total = hlit + hdist;
-                int i = 0;
-                uint32_t prev = 0;
-                while (i < total) {
-                    const int s = decode_sym<7>(br, ctab, ccnt, csym);
-                    if (s < 0) {
-                        e = E_CODE;
-                        break;
-                    }
-                    if (s < 16) {
-                        if (lane == 0) lens[i] = (uint8_t)s;
-                        prev = (uint32_t)s;
-                        ++i;
-                        continue;
-                    }
-                    uint32_t val = 0, rep;
-                    if (s == 16) {
-                        if (i == 0) {
-                            e = E_TABLE;
-                            break;
-                        }
-                        val = prev;
-                        rep = 3 + br.get(2);
-                    } else if (s == 17) {
-                        rep = 3 + br.get(3);
-                    } else {
-                        rep = 11 + br.get(7);
-                    }
-                    if (i + (int)rep > total) {
-                        e = E_TABLE;
-                        break;
-                    }
-                    if ((uint32_t)lane < rep) lens[i + lane] = (uint8_t)val;
-                    if (rep > 64 && (uint32_t)lane + 64 < rep) lens[i + 64 + lane] = (uint8_t)val;
-                    if (rep > 128 && (uint32_t)lane + 128 < rep) lens[i + 128 + lane] = (uint8_t)val;
-                    prev = val;
-                    i += (int)rep;
-                }
-                if (e) break;
-                __syncthreads();
-                if (lens[256] == 0) {
-                    e = E_TABLE;
-                    break;
-                }
-            }
-            // fixed codes: literal/length lens[0..288), distance lens[288..318)
-            const uint8_t *dl = type == 1 ? lens + 288 : lens + hlit;
-            if (!build_table<10>(lens, hlit, ltab, lcnt, lsym, tfirst, toffs) ||
-                !build_table<10>(dl, hdist, dtab, dcnt, dsym, tfirst, toffs)) {
-                e = E_TABLE;
-                break;
-            }
-            for (;;) {
-                pos = __builtin_amdgcn_readfirstlane(pos);
-                flushed = __builtin_amdgcn_readfirstlane(flushed);
-                int s = decode_sym<10>(br, ltab, lcnt, lsym);
-                if (s < 0) {
-                    e = E_CODE;
-                    break;
-                }
-                if (s < 256) {
-                    if (pos >= osz) {
-                        e = E_OVERRUN;
-                        break;
-                    }
-                    ring[pos & (kRing - 1)] = (uint8_t)s;  // every lane stores the same byte
-                    ++pos;
-                    if (pos - flushed >= 256) flush(pos & ~255u);
-                    continue;
-                }
-                if (s == 256) break;
-                s -= 257;
-                if (s >= 29) {
-                    e = E_LEN;
-                    break;
-                }
-                const uint32_t L = kLBase[s] + br.get(kLExt[s]);
-                const int ds = decode_sym<10>(br, dtab, dcnt, dsym);
-                if (ds < 0 || ds >= 30) {
-                    e = E_DIST;
-                    break;
-                }
-                const uint32_t D = kDBase[ds] + br.get(kDExt[ds]);
-                if (D > pos || pos + L > osz) {
-                    e = E_FAR;
-                    break;
-                }
-                if (D + 259 <= kRing) {  // the match cannot overwrite its own source slots
-                    for (uint32_t i = 0; i < L; i += 64) {
-                        const uint32_t j = i + lane;
-                        uint8_t v = 0;
-                        if (j < L) v = ring[(pos - D + (D >= L ? j : j % D)) & (kRing - 1)];
-                        if (j < L) ring[(pos + j) & (kRing - 1)] = v;
-                    }
-                } else {  // far source: flush everything so far, then make the stores visible
-                    flush(pos);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-                    for (uint32_t i = 0; i < L; i += 64) {
-                        const uint32_t j = i + lane;
-                        if (j < L) ring[(pos + j) & (kRing - 1)] = o[pos - D + j];
-                    }
-                }
-                pos += L;
-                if (pos - flushed >= 256) flush(pos & ~255u);
-            }
-            if (e) break;
-        } else {
-            e = E_TYPE;
-            break;
-        }
-        if (br.bitpos() > end_bit) {
-            e = E_PAST;
-            break;
-        }
-        if (h & 1) break;
-    }
-    if (!e && pos != osz) e = E_SIZE;
-    if (!e) flush(pos);
-    if (e && lane == 0) report(err, e, b);
-}
-
-// ---------------------------------------------------------------- grouped (VALU) decoder
-// G lanes decode one block; a wave runs 64 / G blocks at once.  The decoder state is per lane
-// (uniform within the group), so it executes on the SIMD's vector ALU, four of which share the
-// CU's single scalar unit that bounds k_inflate.  Each group owns its decode tables and an R-byte
-// output ring in LDS; no workgroup barriers are used (one wave per workgroup, LDS is in order).
-template <int G, int R, int LTB, int DTB>
-struct GLds {
-    uint16_t ltab[1 << LTB];
-    uint16_t dtab[1 << DTB];
-    uint16_t ctab[128];
-    uint32_t lcnt[16], dcnt[16], ccnt[16];
-    uint16_t lsym[288], dsym[32], csym[20];
-    uint32_t aux[48];
-    uint8_t lens[320], cl[32];
-    uint8_t ring[R];
-};
-
-template <int G>
-struct GBits {
-    const uint32_t *zw;
-    uint64_t zwords;
-    uint64_t wbase;
-    uint32_t widx, cbase;
-    uint32_t cur, nxt;  // lane gl of the group holds words cbase + gl and cbase + G + gl
-    uint64_t buf;
-    uint32_t cnt;
-    uint32_t gl;
-    __device__ __forceinline__ uint32_t ldw(uint32_t rel) const {
-        const uint64_t w = wbase + rel;
-        return w < zwords ? zw[w] : 0u;
-    }
-    __device__ __forceinline__ void refill() {
-        while (cnt <= 32) {
-            const uint32_t r = widx - cbase;
-            const uint32_t w = (uint32_t)__shfl((int)(r < (uint32_t)G ? cur : nxt), (int)(r & (G - 1)), G);
-            buf |= (uint64_t)w << cnt;
-            cnt += 32;
-            ++widx;
-            if (widx - cbase >= (uint32_t)G) {
-                cur = nxt;
-                cbase += G;
-                nxt = ldw(cbase + G + gl);
-            }
-        }
-    }
-    __device__ void seek(uint64_t bit) {
-        wbase = bit >> 5;
-        widx = cbase = 0;
-        cur = ldw(gl);
-        nxt = ldw(G + gl);
-        buf = 0;
-        cnt = 0;
-        refill();
-        skip((uint32_t)(bit & 31));
-    }
-    __device__ __forceinline__ uint64_t bitpos() const { return (wbase + widx) * 32 - cnt; }
-    __device__ __forceinline__ void skip(uint32_t n) {
-        buf >>= n;
-        cnt -= n;
-        if (cnt <= 32) refill();
-    }
-    __device__ __forceinline__ uint32_t get(uint32_t n) {
-        const uint32_t v = (uint32_t)buf & ((1u << n) - 1);
-        skip(n);
-        return v;
-    }
-};
-
-template <int G>
-__device__ __forceinline__ uint64_t gballot(bool p, uint32_t gbase) {
-    const uint64_t m = __ballot(p) >> gbase;
-    return G == 64 ? m : (m & ((1ull << G) - 1));
-}
-
-template <int G, int TB>
-__device__ bool gbuild(const uint8_t *lens, int n, uint16_t *tab, uint32_t *cnt, uint16_t *sym, uint32_t *aux, uint32_t gl,
-                       uint32_t gbase) {
-    // aux: 48 words of group scratch: first code [0,16), symbol offset [16,32), running rank [32,48).
-    // Per-length values live in LDS (lane gl holds length gl's count) to keep VGPR pressure low.
-    for (int i = gl; i < (1 << TB); i += G) tab[i] = 0;
-    uint32_t mine = 0;  // lane b (1..15): number of codes of length b
-    for (int c0 = 0; c0 < n; c0 += G) {
-        const int s = c0 + (int)gl;
-        const uint32_t L = s < n ? lens[s] : 0;
-        for (int b = 1; b < 16; ++b) {
-            const uint32_t c = __popcll(gballot<G>(L == (uint32_t)b, gbase));
-            if ((int)gl == b) mine += c;
-        }
-    }
-    for (uint32_t i = gl; i < 16; i += G) cnt[i] = 0;
-    __builtin_amdgcn_wave_barrier();
-    if (gl >= 1 && gl < 16) cnt[gl] = mine;
-    __builtin_amdgcn_wave_barrier();
-    int left = 1;
-    uint32_t code = 0, off = 0;
-    for (int b = 1; b < 16; ++b) {
-        const uint32_t t = cnt[b];
-        left = 2 * left - (int)t;
-        code = (code + (b > 1 ? cnt[b - 1] : 0)) << (b > 1 ? 1 : 0);
-        if ((int)gl == b) aux[b] = code, aux[16 + b] = off, aux[32 + b] = 0;
-        off += t;
-    }
-    if (left < 0) return false;
-    __builtin_amdgcn_wave_barrier();
-    const uint64_t lt = (1ull << gl) - 1;
-    for (int c0 = 0; c0 < n; c0 += G) {
-        const int s = c0 + (int)gl;
-        const uint32_t L = s < n ? lens[s] : 0;
-        uint64_t my = 0;
-        uint32_t mc = 0;
-        for (int b = 1; b < 16; ++b) {
-            const uint64_t m = gballot<G>(L == (uint32_t)b, gbase);
-            if (L == (uint32_t)b) my = m;
-            if ((int)gl == b) mc = __popcll(m);
-        }
-        if (L) {
-            const uint32_t rank = aux[32 + L] + __popcll(my & lt);
-            sym[aux[16 + L] + rank] = (uint16_t)s;
-            if (L <= (uint32_t)TB) {
-                const uint32_t r = __builtin_bitreverse32(aux[L] + rank) >> (32 - L);
-                const uint16_t e = (uint16_t)(s | (L << 9));
-                for (uint32_t k = 0; k < (1u << (TB - L)); ++k) tab[r | (k << L)] = e;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (gl >= 1 && gl < 16) aux[32 + gl] += mc;
-        __builtin_amdgcn_wave_barrier();
-    }
-    __builtin_amdgcn_wave_barrier();
-    return true;
-}
-
-template <int G, int TB>
-__device__ __forceinline__ int gdecode(GBits<G> &br, const uint16_t *tab, const uint32_t *cnt, const uint16_t *sym) {
-    const uint32_t v = (uint32_t)br.buf;
-    const uint32_t e = tab[v & ((1u << TB) - 1)];
-    if (e) {
-        br.skip(e >> 9);
-        return (int)(e & 511);
-    }
-    int code = 0, first = 0, index = 0;
-    for (int len = 1; len <= 15; ++len) {
-        code |= (int)((v >> (len - 1)) & 1);
-        const int count = (int)cnt[len];
-        if (code - count < first) {
-            br.skip(len);
-            return sym[index + (code - first)];
-        }
-        index += count;
-        first += count;
-        first <<= 1;
-        code <<= 1;
-    }
-    return -1;
-}
-
-template <int G, int R, int LTB, int DTB>
-__global__ void __launch_bounds__(64) k_inflate_g(const uint8_t *__restrict__ z, uint64_t zbytes, const uint64_t *__restrict__ d0,
-                                                  const uint64_t *__restrict__ d1, const uint64_t *__restrict__ uoff, uint64_t nblk,
-                                                  uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
-    constexpr int NG = 64 / G;
-    __shared__ GLds<G, R, LTB, DTB> gs[NG];
-    const uint32_t lane = threadIdx.x, g = lane / G, gl = lane % G, gbase = g * G;
-    const uint64_t b = (uint64_t)blockIdx.x * NG + g;
-    if (b >= nblk) return;
-    GLds<G, R, LTB, DTB> &S = gs[g];
-    GBits<G> br;
-    br.gl = gl;
-    br.zw = (const uint32_t *)z;
-    br.zwords = (zbytes + 3) / 4;
-    br.seek(d0[b] * 8);
-    const uint64_t end_bit = d1[b] * 8;
-    uint8_t *o = out + uoff[b];
-    const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
-    uint32_t pos = 0, flushed = 0;
-    int e = 0;
-    auto flush = [&](uint32_t upto) {
-        for (uint32_t q0 = flushed; q0 < upto; q0 += G) {
-            const uint32_t q = q0 + gl;
-            if (q < upto) o[q] = S.ring[q & (R - 1)];
-        }
-        flushed = upto;
-    };
-    for (;;) {
-        const uint32_t h = br.get(3);
-        const uint32_t type = h >> 1;
-        if (type == 0) {
-            br.skip((8 - (uint32_t)(br.bitpos() & 7)) & 7);
-            const uint32_t len = br.get(16), nlen = br.get(16);
-            const uint64_t src = br.bitpos() >> 3;
-            if ((len ^ 0xffffu) != nlen || pos + len > osz || src + len > d1[b]) {
-                e = E_STORED;
-                break;
-            }
-            for (uint32_t i = 0; i < len; i += G) {
-                const uint32_t m = min((uint32_t)G, len - i);
-                if (gl < m) S.ring[(pos + gl) & (R - 1)] = z[src + i + gl];
-                pos += m;
-                if (pos - flushed >= 256) flush(pos & ~255u);
-            }
-            br.seek(br.bitpos() + (uint64_t)len * 8);
-        } else if (type == 1 || type == 2) {
-            int hlit = 288, hdist = 30;
-            if (type == 1) {
-                for (int s = gl; s < 318; s += G) S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
-                __builtin_amdgcn_wave_barrier();
-            } else {
-                hlit = (int)br.get(5) + 257;
-                hdist = (int)br.get(5) + 1;
-                const int hclen = (int)br.get(4) + 4;
-                if (hlit > 286 || hdist > 30) {
-                    e = E_TABLE;
-                    break;
-                }
-                for (int i = gl; i < 19; i += G) S.cl[i] = 0;
-                __builtin_amdgcn_wave_barrier();
-                for (int i = 0; i < hclen; ++i) {
-                    const uint32_t v = br.get(3);
-                    S.cl[kClOrd[i]] = (uint8_t)v;  // every lane of the group stores the same byte
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (!gbuild<G, 7>(S.cl, 19, S.ctab, S.ccnt, S.csym, S.aux, gl, gbase)) {
-                    e = E_TABLE;
-                    break;
-                }
-                const int total = hlit + hdist;
-                int i = 0;
-                uint32_t prev = 0;
-                while (i < total) {
-                    const int sy = gdecode<G, 7>(br, S.ctab, S.ccnt, S.csym);
-                    if (sy < 0) {
-                        e = E_CODE;
-                        break;
-                    }
-                    if (sy < 16) {
-                        S.lens[i] = (uint8_t)sy;
-                        prev = (uint32_t)sy;
-                        ++i;
-                        continue;
-                    }
-                    uint32_t val = 0, rep;
-                    if (sy == 16) {
-                        if (i == 0) {
-                            e = E_TABLE;
-                            break;
-                        }
-                        val = prev;
-                        rep = 3 + br.get(2);
-                    } else if (sy == 17) {
-                        rep = 3 + br.get(3);
-                    } else {
-                        rep = 11 + br.get(7);
-                    }
-                    if (i + (int)rep > total) {
-                        e = E_TABLE;
-                        break;
-                    }
-                    for (uint32_t k = gl; k < rep; k += G) S.lens[i + k] = (uint8_t)val;
-                    prev = val;
-                    i += (int)rep;
-                }
-                if (e) break;
-                __builtin_amdgcn_wave_barrier();
-                if (S.lens[256] == 0) {
-                    e = E_TABLE;
-                    break;
-                }
-            }
-            const uint8_t *dl = type == 1 ? S.lens + 288 : S.lens + hlit;
-            if (!gbuild<G, LTB>(S.lens, hlit, S.ltab, S.lcnt, S.lsym, S.aux, gl, gbase) ||
-                !gbuild<G, DTB>(dl, hdist, S.dtab, S.dcnt, S.dsym, S.aux, gl, gbase)) {
-                e = E_TABLE;
-                break;
-            }
-            for (;;) {
-                int sy = gdecode<G, LTB>(br, S.ltab, S.lcnt, S.lsym);
-                if (sy < 0) {
-                    e = E_CODE;
-                    break;
-                }
-                if (sy < 256) {
-                    if (pos >= osz) {
-                        e = E_OVERRUN;
-                        break;
-                    }
-                    S.ring[pos & (R - 1)] = (uint8_t)sy;
-                    ++pos;
-                    if (pos - flushed >= 256) flush(pos & ~255u);
-                    continue;
-                }
-                if (sy == 256) break;
-                sy -= 257;
-                if (sy >= 29) {
-                    e = E_LEN;
-                    break;
-                }
-                const uint32_t L = kLBase[sy] + br.get(kLExt[sy]);
-                const int ds = gdecode<G, DTB>(br, S.dtab, S.dcnt, S.dsym);
-                if (ds < 0 || ds >= 30) {
-                    e = E_DIST;
-                    break;
-                }
-                const uint32_t D = kDBase[ds] + br.get(kDExt[ds]);
-                if (D > pos || pos + L > osz) {
-                    e = E_FAR;
-                    break;
-                }
-                // ring path iff the match cannot overwrite its own source slots (D + L <= R); a far
-                // source is read back from HBM after flushing everything written so far
-                if (D + 259 <= (uint32_t)R) {
-                    for (uint32_t i = 0; i < L; i += G) {
-                        const uint32_t j = i + gl;
-                        uint8_t v = 0;
-                        if (j < L) v = S.ring[(pos - D + (D >= L ? j : j % D)) & (R - 1)];
-                        __builtin_amdgcn_wave_barrier();
-                        if (j < L) S.ring[(pos + j) & (R - 1)] = v;
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                } else {
-                    flush(pos);
-                    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-                    for (uint32_t i = 0; i < L; i += G) {
-                        const uint32_t j = i + gl;
-                        if (j < L) S.ring[(pos + j) & (R - 1)] = o[pos - D + j];
-                    }
-                }
-                pos += L;
-                if (pos - flushed >= 256) flush(pos & ~255u);
-            }
-            if (e) break;
-        } else {
-            e = E_TYPE;
-            break;
-        }
-        if (br.bitpos() > end_bit) {
-            e = E_PAST;
-            break;
-        }
-        if (h & 1) break;
-    }
-    if (!e && pos != osz) e = E_SIZE;
-    if (!e) flush(pos);
-    if (e && gl == 0) report(err, e, b);
-}
-
-__global__ void __launch_bounds__(512) k_crc_check(const uint8_t *__restrict__ out, const uint64_t *__restrict__ uoff,
-                                                   const uint32_t *__restrict__ crc, const uint32_t *__restrict__ zpow,
-                                                   uint32_t *__restrict__ err) {
-    __shared__ uint32_t in[kSlot / 4 + 4];
-    __shared__ uint32_t crctab[4][256];
-    __shared__ uint32_t zp[17][32];
-    __shared__ uint32_t crcs[512];
-    const int t = threadIdx.x;
-    const uint64_t b = blockIdx.x;
-    const uint32_t len = (uint32_t)(uoff[b + 1] - uoff[b]);
-    if (len > kSlot) {
-        if (t == 0) report(err, E_SIZE, b);
-        return;
-    }
-    stage_words<512>(in, out + uoff[b], len, t);
-    crc_setup<512>(crctab, zp, zpow, t);
-    __syncthreads();
-    const uint32_t c = crc_window512(in, len, crctab, zp, crcs, t);
-    if (t == 0 && c != crc[b]) report(err, E_CRC, b);
-}
 
 // ------------------------------------------------------------------------------ record boundaries
 __device__ __forceinline__ uint32_t rd32u(const uint8_t *p) {
@@ -1168,43 +441,11 @@ extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t z
     const uint32_t init[2] = {0, 0xffffffffu};
     OGE_HIP_TRY(ctx, hipMemcpyAsync(err, init, 8, hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, zh, sizeof(zh), hipMemcpyHostToDevice, ctx->stream));
-    // decoder: OGE_INFLATE_GROUP unset = one lane per block (inflate_lane.hip); else lanes per block of the
-    // grouped decoder -- 32, 16, or 0 = the wave-uniform scalar decoder k_inflate.
-    // Measured on 20M C2 reads (5.68 GB): scalar 437 ms (bound by the CU's one scalar ALU), 32 lanes
-    // with a 1 KiB ring 254 ms, 16 lanes 268-296 ms (divergence between the wave's groups); larger
-    // rings or tables cost occupancy and were slower (2 KiB 327 ms, 8 KiB 591 ms).
-    static const int inflate_group = [] {
-        const char *v = getenv("OGE_INFLATE_GROUP");
-        return v && *v ? atoi(v) : -1;
-    }();
-    if (inflate_group < 0) {  // default: the lane decoder (inflate_lane.hip), CRC fused into its phase 2
-        OgeStageTimer *tm = ctx->begin_stage("bgzf_inflate");
-        int rc = oge_inflate_lanes(ctx, d_z, zbytes, d_d0, d_d1, d_uoff, d_crc, nblk, d_out, err, zpow);
-        ctx->end_stage(tm);
-        if (rc) return rc;
-    } else {
+    // the lane decoder (inflate_lane.hip), CRC fused into its phase 2
     OgeStageTimer *tm = ctx->begin_stage("bgzf_inflate");
-    for (uint64_t b0 = 0; b0 < nblk; b0 += (1u << 30)) {
-        const uint32_t nb = (uint32_t)std::min<uint64_t>(nblk - b0, 1u << 30);
-        const uint64_t *a0 = d_d0 + b0, *a1 = d_d1 + b0, *au = d_uoff + b0;
-        switch (inflate_group) {
-        case 0: k_inflate<<<nb, 64, 0, ctx->stream>>>(d_z, zbytes, a0, a1, au, d_out, err); break;
-        case 16: k_inflate_g<16, 1024, 9, 8><<<oge_ceil_div(nb, 4), 64, 0, ctx->stream>>>(d_z, zbytes, a0, a1, au, nb, d_out, err); break;
-        default: k_inflate_g<32, 1024, 10, 8><<<oge_ceil_div(nb, 2), 64, 0, ctx->stream>>>(d_z, zbytes, a0, a1, au, nb, d_out, err); break;
-        }
-        OGE_LAUNCH_CHECK(ctx);
-    }
+    const int rc = oge_inflate_lanes(ctx, d_z, zbytes, d_d0, d_d1, d_uoff, d_crc, nblk, d_out, err, zpow);
     ctx->end_stage(tm);
-    if (d_crc) {
-        OgeStageTimer *tc = ctx->begin_stage("bgzf_crc");
-        for (uint64_t b0 = 0; b0 < nblk; b0 += (1u << 30)) {
-            const uint32_t nb = (uint32_t)std::min<uint64_t>(nblk - b0, 1u << 30);
-            k_crc_check<<<nb, 512, 0, ctx->stream>>>(d_out, d_uoff + b0, d_crc + b0, zpow, err);
-            OGE_LAUNCH_CHECK(ctx);
-        }
-        ctx->end_stage(tc);
-    }
-    }
+    if (rc) return rc;
     uint32_t got[2];
     OGE_HIP_TRY(ctx, hipMemcpyAsync(got, err, 8, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -3,9 +3,9 @@
 // zlib inflate per BGZF block on the pool) -- the same RFC 1951 decode, laid out for wave64.
 //
 // Why this shape.  A BGZF block is an independent deflate stream of <= 64 KiB whose Huffman decode is
-// one long serial chain.  The grouped decoder (inflate.hip, k_inflate_g) runs one chain per 32 lanes,
-// so a wave64 instruction advances two blocks.  Here every lane is its own decoder: one wave
-// instruction advances 64 blocks.  A lane's decode step is a dependent chain (table lookup -> shift
+// one long serial chain.  The r01 grouped decoder (one chain per 32 lanes: 19.7 GB/s at 20M reads,
+// removed in r03) let a wave64 instruction advance two blocks.  Here every lane is its own decoder:
+// one wave instruction advances 64 blocks (46.5 GB/s at 20M reads, profiles/r02_inflate_20m*).  A lane's decode step is a dependent chain (table lookup -> shift
 // -> next lookup), so throughput comes from waves in flight: phase 1 keeps only the hot 6-bit
 // literal/length and 4-bit distance tables in LDS (144 B per lane, lane-interleaved so a wave's 64
 // lookups hit 64 different banks), holds the canonical limits of the longer codes in VGPRs and their
@@ -37,32 +37,24 @@ namespace {
 
 using namespace oge_bgzf;
 
-enum { E_STORED = 1, E_CODE = 2, E_OVERRUN = 3, E_LEN = 4, E_DIST = 5, E_FAR = 6, E_TYPE = 7, E_PAST = 8, E_SIZE = 9,
-       E_TABLE = 10, E_CRC = 11 };
-
 __device__ __forceinline__ void report(uint32_t *err, uint32_t code, uint64_t blk) {
     atomicOr(err, 1u << code);
     atomicMin(err + 1, (uint32_t)min<uint64_t>(blk, 0xffffffffull));
 }
 
-constexpr int TBL = 6, TBD = 4;  // direct-table bits: literal/length, distance
-// Long-code symbol lists: the first SLL (literal/length) and SLD (distance) entries of a lane's canonical
-// list live in LDS, the rest in its global scratch.  About 10% (synthetic) to 40% (real quality
-// alphabets) of symbols have codes longer than TBL bits; with 64 lanes some lane needs a list entry on
-// almost every step, so a list in global memory puts a memory round trip into every step of the wave.
-// Sizes that fill the LDS left at WPS waves per SIMD (4 SIMDs, 512-byte allocation granules): WPS 3 ->
-// 36 + 13 (13312 B per wave), WPS 2 -> 136 + 24 (20416 B per wave).
+constexpr int TL = 6, TD = 4;  // direct-table bits: literal/length, distance
+constexpr int kWps = 3;        // waves per SIMD (VGPR budget 512 / 3)
+constexpr int LB = 4;          // literals per decode step (see the ST_SYM path)
+// Codes longer than the direct tables take their symbol from the lane's canonical list in its global
+// scratch (MALL-resident); list heads in LDS (r02 cfg 1-3) measured slower in the 300M chain: 1615 vs
+// 1157 ms (profiles/r02s3_infl_cfg.json).
 // per-wave LDS, lane-interleaved ([entry][lane]): element e of lane l at e * 64 + l
-template <int SLL, int SLD, int TL = TBL, int TD = TBD>
 struct P1Lds {
-    static constexpr uint32_t kSLL = SLL, kSLD = SLD;
     uint16_t lt[1 << TL][64];  // sym | L << 9, 0 = longer code; while code lengths are decoded a lane's
                                 // column holds its 7-bit code-length table (cl_at): sym | L << 5
     uint8_t dt[1 << TD][64];    // sym | L << 5, 0 = longer code
     uint32_t cnt[16], lo[16], first[16], offl[16], run[16], lim[16], lie[16];  // the build's per-length values
     uint64_t clp[64];           // a lane's code-length-code lengths between its header and its CL build
-    uint8_t ll[SLL > 0 ? SLL : 1][64];  // head of the literal/length long-code list
-    uint8_t dl[SLD > 0 ? SLD : 1][64];  // head of the distance long-code list
 };
 // per-lane global scratch
 constexpr uint32_t kScr = 640;
@@ -182,14 +174,7 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
                     else S.dt[ix][j] = (uint8_t)(s | (myL << 5));
                 }
             } else {
-                const uint32_t k = ol + rank;
-                constexpr uint32_t H = LIT ? Lds::kSLL : Lds::kSLD;
-                if (k < H) {
-                    if (LIT) S.ll[k][j] = (uint8_t)s;
-                    else S.dl[k][j] = (uint8_t)s;
-                } else {
-                    list[k] = (uint8_t)s;
-                }
+                list[ol + rank] = (uint8_t)s;
             }
         }
     }
@@ -198,26 +183,24 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
 }
 
 // ---------------------------------------------------------------------------- phase 1
-// MODE: one Huffman code per loop step (a literal/length code, or the distance code of the pending match:
-// `md`), so a step has one refill, one extra-bits read and one output write whichever code it is;
-// otherwise a step decodes a whole symbol (a match's length and distance codes in the same step).
-// DIRECT: every output byte is its own byte store (no 8-byte accumulator to keep and flush).
-// LB (one-code-per-step path): a literal decoded from the direct table may be followed, in the same
-// step, by up to LB - 1 more literals whose codes also sit in the direct table (<= 6 bits each: a
-// refill leaves >= 32 bits, enough for four such codes; then another refill); a wave's step count is
-// the maximum over its 64
-// blocks' symbol counts, so literal runs (BAM qualities, bases) take fewer steps.  300M reads in the
-// chain: LB = 1 / 2 / 4 -> 1152 / 941 / 792 ms (profiles/r02s3_infl_litb.json).
-// TL / TD: direct-table bits of the literal/length and distance codes (the slow paths count the
-// canonical limits from lengths 7 and 5 up, which holds for any TL <= 7, TD <= 5: a code longer than
-// the table is at or past every shorter length's limit).
-template <int WPS, int SLL, int SLD, bool MODE, bool DIRECT = false, int LB = 1, int TL = TBL, int TD = TBD>  // waves per SIMD the kernel is compiled for (VGPR budget 512 / WPS)
-__global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
-                                                     const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
-                                                     const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
-                                                     uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
-                                                     uint8_t *__restrict__ scratch, uint32_t *__restrict__ err) {
-    __shared__ P1Lds<SLL, SLD, TL, TD> S;
+// A step decodes one whole symbol (a match's length and distance codes in the same step).  A literal
+// decoded from the direct table may be followed, in the same step, by up to LB - 1 more literals whose
+// codes also sit in the direct table: a step starts with >= 32 bits in the buffer (refill tops up to
+// 32..64), a direct code takes <= TL = 6 bits, so 4 direct codes (<= 24 bits) always fit.  Not after a
+// long (7..15-bit) code: 15 + 3 * 6 = 33 > 32 (r02 commit 3941758 allowed it and corrupted a block at
+// 300M reads; tests/test_gpu_inflate.py::test_long_codes_before_direct_literal_runs pins it).  A wave's
+// step count is the maximum over its 64 blocks' symbol counts, so literal runs (BAM qualities, bases)
+// take fewer steps: 300M reads in the chain, LB = 1 / 2 / 4 -> 1152 / 941 / 792 ms
+// (profiles/r02s3_infl_litb.json).
+// Bit-budget guard (always on): every skip of more bits than the buffer holds sets `under`, and the
+// block fails with E_BITS instead of decoding from zero bits.
+__global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
+                                                      const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
+                                                      const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
+                                                      uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
+                                                      uint8_t *__restrict__ scratch, uint32_t *__restrict__ err) {
+    static_assert(LB <= 4 && TL * LB <= 32, "a step's literal batch must fit the 32 bits a refill guarantees");
+    __shared__ P1Lds S;
     const uint32_t lane = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
     const uint64_t stride = (uint64_t)gridDim.x * 64;
@@ -226,6 +209,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
 
     // input: 64-bit bit buffer + two 16-byte chunks (q being consumed, p loaded ahead)
     uint64_t buf = 0;
+    uint32_t under = 0;  // a skip past the buffered bits happened in this block (the guard)
     uint32_t cnt = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, qn = 0;
     uintptr_t cp = 0;
     auto load16 = [&](uintptr_t a, uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t &x3) {
@@ -250,6 +234,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
         }
     };
     auto skip = [&](uint32_t k) {
+        under |= k > cnt;
         buf >>= k;
         cnt -= k;
     };
@@ -288,13 +273,6 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
         }
     };
     auto put = [&](uint32_t p, uint32_t v, uint32_t nbytes) {  // nbytes (1..3) little-endian bytes of v at p
-        if (DIRECT) {
-            OGE_G uint8_t *o = (OGE_G uint8_t *)(obase + p);
-            o[0] = (uint8_t)v;
-            if (nbytes > 1) o[1] = (uint8_t)(v >> 8);
-            if (nbytes > 2) o[2] = (uint8_t)(v >> 16);
-            return;
-        }
         const uintptr_t a = (uintptr_t)(obase + p);
         const uint32_t sh = (uint32_t)(a & 7);
         if ((a >> 3) == oc && sh + nbytes <= 8) {
@@ -332,7 +310,6 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
     sfor<6>([&](auto k) { T.dl[k()] = T.di[k()] = 0; });
     T.l15 = 0;
     uint32_t st = ST_NEXT, fin = 0, hlit = 0, hdist = 0, ci = 0, prev = 0, srem = 0, fixed = 0, l256 = 0;
-    uint32_t md = 0, plen = 0;  // MODE: distance code next / the pending match's length
     uint64_t b = b0 + gid, d1bit = 0;
     bool first = true;
 
@@ -341,6 +318,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
         st = ST_NEXT;
     };
     auto block_end = [&]() {  // last deflate block of the BGZF block consumed
+        if (under) return fail(E_BITS);
         if (pos != osz) return fail(E_SIZE);
         if (bitpos() > d1bit) return fail(E_PAST);
         flush();
@@ -440,71 +418,13 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 bw = 0;
                 d1bit = ((uint64_t)(uintptr_t)z + d1a[b]) * 8;
                 seek((uintptr_t)z + d0a[b]);
+                under = 0;
                 st = ST_HDR;
             }
         }
         if (__ballot(st != ST_DONE) == 0) break;
 
-        if (MODE && st == ST_SYM) {
-            refill();  // >= 33 bits: a code (<= 15) and its extra bits (<= 13)
-            const uint32_t v = (uint32_t)buf;
-            const uint32_t e0 = S.lt[v & ((1u << TL) - 1)][lane];
-            const uint32_t d0 = S.dt[v & ((1u << TD) - 1)][lane];
-            uint32_t sym = md ? (d0 & 31) : (e0 & 511), L = md ? (d0 >> 5) : (e0 >> 9);
-            if (!(md ? d0 : e0)) {  // code longer than the direct table
-                const uint32_t c15 = __builtin_bitreverse32(v) >> 17;
-                if (!md) {
-                    L = 7;
-                    sfor<4>([&](auto k) { L += (c15 >= (T.ll[k()] & 0xffff)) + (c15 >= (T.ll[k()] >> 16)); });
-                    const uint32_t lie = pick(T.lie, L - 7);
-                    const uint32_t k = ((lie & 0xffff) + (c15 >> (15 - L))) & 0xffff;
-                    uint32_t sb;
-                    if (SLL > 0 && k < (uint32_t)SLL) sb = S.ll[min(k, (uint32_t)max(SLL - 1, 0))][lane];
-                    else sb = scr[S_LS + min(k, 287u)];
-                    sym = sb + (k >= (lie >> 16) ? 256u : 0u);
-                    if (L == 15 && c15 >= T.l15) sym = 512;  // no such code
-                } else {
-                    L = 5;
-                    sfor<5>([&](auto k) { L += (c15 >= (T.dl[k()] & 0xffff)) + (c15 >= (T.dl[k()] >> 16)); });
-                    const uint32_t k = (u16of(T.di, L - 5) + (c15 >> (15 - L))) & 0xffff;
-                    if (SLD > 0 && k < (uint32_t)SLD) sym = S.dl[min(k, (uint32_t)max(SLD - 1, 0))][lane];
-                    else sym = scr[S_DS + min(k, 31u)];
-                    if (L == 15 && c15 >= (T.dl[5] & 0xffff)) sym = 31;  // no such code
-                }
-            }
-            skip(L);
-            // extra bits: length code sym 257..285 (md = 0) or distance code sym 0..29 (md = 1)
-            const uint32_t c = sym - 257;
-            const uint32_t lext = c < 8 ? 0u : c < 28 ? (c - 4) >> 2 : 0u;
-            const uint32_t lbase = c < 8 ? c + 3 : c < 28 ? ((4 + (c & 3)) << lext) + 3 : 258u;
-            const uint32_t dext = sym < 4 ? 0u : (sym - 2) >> 1;
-            const uint32_t dbase = sym < 4 ? sym + 1 : ((2 + (sym & 1)) << dext) + 1;
-            const uint32_t ext = md ? dext : lext;
-            const uint32_t val = (md ? dbase : lbase) + get(ext);
-            uint32_t pv = 0, pn = 0, adv = 0;
-            if (!md) {
-                if (sym < 256) {
-                    if (pos >= osz) fail(E_OVERRUN);
-                    else pv = sym, pn = 1, adv = 1;
-                } else if (sym == 256) {
-                    if (fin) block_end();
-                    else st = ST_HDR;
-                } else if (sym > 285) {
-                    fail(sym == 512 ? E_CODE : E_LEN);
-                } else {
-                    plen = val, md = 1;
-                }
-            } else {
-                md = 0;
-                if (sym >= 30) fail(E_DIST);
-                else if (val > pos || pos + plen > osz) fail(E_FAR);
-                else pv = (plen - 3) | ((val - 1) << 8), pn = 3, adv = plen, mark(pos);  // descriptor in the hole
-            }
-            if (pn) {
-                put(pos, pv, pn);
-                pos += adv;
-            }
-        } else if (!MODE && st == ST_SYM) {
+        if (st == ST_SYM) {
             refill();
             const uint32_t v = (uint32_t)buf;
             const uint32_t e = S.lt[v & ((1u << TL) - 1)][lane];
@@ -517,10 +437,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 sfor<4>([&](auto k) { L += (c15 >= (T.ll[k()] & 0xffff)) + (c15 >= (T.ll[k()] >> 16)); });
                 const uint32_t lie = pick(T.lie, L - 7);
                 const uint32_t k = ((lie & 0xffff) + (c15 >> (15 - L))) & 0xffff;
-                uint32_t sb;
-                if (SLL > 0 && k < (uint32_t)SLL) sb = S.ll[min(k, (uint32_t)max(SLL - 1, 0))][lane];
-                else sb = scr[S_LS + min(k, 287u)];
-                sym = sb + (k >= (lie >> 16) ? 256u : 0u);
+                sym = scr[S_LS + min(k, 287u)] + (k >= (lie >> 16) ? 256u : 0u);
                 if (L == 15 && c15 >= T.l15) sym = 512;  // no such code
             }
             skip(L);
@@ -530,13 +447,9 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                 } else {
                     put(pos, sym, 1);
                     ++pos;
-                    if (LB > 1 && e) {  // more direct-table literals in this step
-                        // the step's refill leaves >= 32 bits: 26 after a direct-table code cover three
-                        // more (after a long code, with a second refill, measured slower: 72.9 vs 68.9 ms
-                        // at 20M reads)
+                    if (e) {  // more direct-table literals in this step (>= 26 bits left: three more)
 #pragma unroll
                         for (int q = 1; q < LB; ++q) {
-                            if (q % 4 == 0) refill();  // >= 33 bits again for the next four
                             const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
                             if (!e2 || (e2 & 511) >= 256 || pos >= osz) break;
                             skip(e2 >> 9);
@@ -566,8 +479,7 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
                     DL = 5;
                     sfor<5>([&](auto k) { DL += (c15 >= (T.dl[k()] & 0xffff)) + (c15 >= (T.dl[k()] >> 16)); });
                     const uint32_t k = (u16of(T.di, DL - 5) + (c15 >> (15 - DL))) & 0xffff;
-                    if (SLD > 0 && k < (uint32_t)SLD) ds = S.dl[min(k, (uint32_t)max(SLD - 1, 0))][lane];
-                    else ds = scr[S_DS + min(k, 31u)];
+                    ds = scr[S_DS + min(k, 31u)];
                     if (DL == 15 && c15 >= (T.dl[5] & 0xffff)) ds = 31;  // no such code
                 }
                 skip(DL);
@@ -614,7 +526,6 @@ __global__ void __launch_bounds__(64, WPS) k_infl_huff(const uint8_t *__restrict
             }
         } else if (st == ST_HDR) {
             refill();
-            md = 0;
             const uint32_t h = get(3);
             fin = h & 1;
             const uint32_t type = h >> 1;
@@ -857,30 +768,13 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
                       const uint32_t *zpow) {
     static int ncu = [] {
         int d = 0, n = 0;
-        hipGetDevice(&d);
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
+        (void)hipGetDevice(&d);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
         return n > 0 ? n : 256;
     }();
     // one block per lane per launch: a launch fills the 12 resident waves per CU once (a second, partial
     // round of waves would run at a fraction of the occupancy); chunks are balanced
-    // OGE_INFL_CFG (experiments): 0 = 12 waves per CU with the long-code lists in global scratch only,
-    // 1 = 12 waves with list heads in LDS, 3 = the same with one code per step (MODE), 2 = 8 waves with
-    // longer list heads in LDS (MODE), 4 = 16 waves, 5 / 6 = 1 / 3 with byte stores (DIRECT),
-    // 7 = 0 with a 5-bit distance table, 8 = 8 waves with a 7-bit literal/length table (both batched)
-    // Default 0: in the 300M-read chain (7 launches of 196,608 blocks) it inflates in 1157 ms against
-    // 1615 ms for 1 and 1629 ms for 3 (profiles/r02s3_infl_cfg.json); the 150M codec A/B that had
-    // picked 1 ran shorter launches on its own.
-    static const int cfg = [] {
-        const char *e = getenv("OGE_INFL_CFG");
-        const int c = e ? atoi(e) : 0;
-        return (c >= 0 && c <= 8) ? c : 0;
-    }();
-    static const int litb = [] {  // OGE_INFL_LITB = 1 | 2 | 4 | 6 | 8: literals per step (cfg 0)
-        const char *e = getenv("OGE_INFL_LITB");
-        return e && *e ? atoi(e) : 4;
-    }();
-    const int wps = cfg == 4 ? 4 : (cfg == 2 || cfg == 8) ? 2 : 3;
-    const uint64_t lanes = (uint64_t)ncu * 4 * wps * 64;
+    const uint64_t lanes = (uint64_t)ncu * 4 * kWps * 64;
     const uint64_t nchunks = std::max<uint64_t>(1, (nblk + lanes - 1) / lanes);
     const uint64_t chunk = std::max<uint64_t>(1, (nblk + nchunks - 1) / nchunks);
     const uint64_t wgs = (chunk + 63) / 64;
@@ -890,19 +784,7 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
         const uint64_t nb = std::min(chunk, nblk - b0);
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
-        if (cfg == 4) k_infl_huff<4, 0, 0, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 2) k_infl_huff<2, 136, 24, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 7) k_infl_huff<3, 0, 0, false, false, 4, 6, 5><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 8) k_infl_huff<2, 0, 0, false, false, 4, 7, 4><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 0 && litb >= 8) k_infl_huff<3, 0, 0, false, false, 8><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 0 && litb >= 6) k_infl_huff<3, 0, 0, false, false, 6><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 0 && litb >= 4) k_infl_huff<3, 0, 0, false, false, 4><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 0 && litb >= 2) k_infl_huff<3, 0, 0, false, false, 2><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 0) k_infl_huff<3, 0, 0, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 3) k_infl_huff<3, 36, 13, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 5) k_infl_huff<3, 36, 13, false, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else if (cfg == 6) k_infl_huff<3, 36, 13, true, true><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
-        else k_infl_huff<3, 36, 13, false><<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        k_infl_huff<<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
         OGE_LAUNCH_CHECK(ctx);
         k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, b0, zpow, err);
         OGE_LAUNCH_CHECK(ctx);

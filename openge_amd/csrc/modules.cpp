@@ -77,11 +77,30 @@ int ChainContext::init_ranks() {
         const char *pool = getenv("OGE_POOL");
         if (!(pool && std::string(pool) == "0")) oge_ctx_set_pool(rank_ctx[g], 1);
     }
+    // the multi-process route of bench.py / a torchrun launch, one host thread per rank: one id, every
+    // rank joins concurrently (RCCL between distinct GPUs, the host-staged transport when they share one)
+    std::vector<uint8_t> id(oge_comm_unique_id_bytes());
+    if (oge_comm_unique_id(id.data(), id.size())) return fail("--gpus: communicator id");
     comms.assign(gpus, nullptr);
-    if (oge_comm_init(rank_ctx.data(), gpus, comms.data())) {
-        comms.clear();
-        return fail("--gpus: communicator");
+    std::vector<int> rcs(gpus, 0);
+    std::vector<std::string> why(gpus);
+    {
+        std::vector<std::thread> ts;
+        for (int g = 0; g < gpus; ++g)
+            ts.emplace_back([&, g]() {
+                rcs[g] = oge_comm_init_rank(rank_ctx[g], gpus, g, id.data(), &comms[g]);
+                if (rcs[g]) why[g] = oge_last_error(rank_ctx[g]);
+            });
+        for (auto &t : ts) t.join();
     }
+    for (int g = 0; g < gpus; ++g)
+        if (rcs[g]) {
+            fprintf(stderr, "openge: --gpus: rank %d communicator: %s\n", g, why[g].c_str());
+            for (oge_comm *c : comms)
+                if (c) oge_comm_destroy(c);
+            comms.clear();
+            return -1;
+        }
     if (verbose)
         fprintf(stderr, "[openge] %d ranks on %d device(s), transport %s\n", gpus, std::min(gpus, ndev), oge_comm_transport(comms[0]));
     return 0;

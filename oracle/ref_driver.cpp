@@ -17,8 +17,9 @@
 // no @PG line (the `--nopg` behaviour).  Global settings mirror
 // cmd/commands.cpp:67-84.
 //
-// It is never shipped; on the GPU box it runs only as bench.py's cpu_baseline (the reference's own
-// chain timed beside the GPU path).
+// It is never part of the product.  The built binary travels to the GPU box with the snapshot and
+// runs there only as test infrastructure: bench.py's cpu_baseline legs (the reference's own chains
+// timed beside the GPU path) and -m gpu tests that compare against the reference chain's output.
 
 #include <cstdlib>
 
@@ -67,7 +68,7 @@ protected:
 
 static void usage() {
     fprintf(stderr,
-            "usage: ref_driver sort|dedup|sortdedup|realign [-v] [-t N] [-n N] [-T tmpdir] [-c level] [-K chains]\n"
+            "usage: ref_driver sort|dedup|sortdedup|realign [-v] [-D] [-t N] [-n N] [-T tmpdir] [-c level] [-K chains]\n"
             "                  [-r region] [-q mapq] [-b] [-S seed] [-R ref.fa -L intervals] in.bam [in2.bam ...] out.bam\n");
     exit(2);
 }
@@ -79,7 +80,7 @@ int main(int argc, char **argv) {
     int threads = 8, per_tmp = 500000, level = 6, chains = 0;
     std::string tmpdir = "/tmp", ref, intervals, region;
     int mapq = -1;
-    bool byname = false;
+    bool byname = false, remove_dups = false;
     std::vector<std::string> pos;
     for (int i = 2; i < argc; i++) {
         std::string a = argv[i];
@@ -94,6 +95,7 @@ int main(int argc, char **argv) {
         else if (a == "-r" && i + 1 < argc) region = argv[++i];
         else if (a == "-q" && i + 1 < argc) mapq = atoi(argv[++i]);
         else if (a == "-b") byname = true;
+        else if (a == "-D") remove_dups = true;  // MarkDuplicates::removeDuplicates (mergesort/dedup -R)
         else if (a == "-S" && i + 1 < argc) srand((unsigned)atoi(argv[++i]));  // harness only: the realigner's
                                   // random_shuffle of tied consensuses draws from rand()
         else pos.push_back(a);
@@ -130,6 +132,7 @@ int main(int argc, char **argv) {
         merge.addSink(&sink);
         for (int c = 0; c < chains; ++c) {
             md.push_back(new MarkDuplicates(tmpdir));
+            md.back()->removeDuplicates = remove_dups;
             merge.addSource(md.back());
             split.addSink(md.back());
         }
@@ -138,6 +141,7 @@ int main(int argc, char **argv) {
     } else if (mode == "sort" || mode == "sortdedup") {
         ReadSorter sorter(tmpdir);
         MarkDuplicates md(tmpdir);
+        md.removeDuplicates = remove_dups;
         Filter filter;
         sorter.setSortBy(byname ? BamHeader::SORT_QUERYNAME : BamHeader::SORT_COORDINATE);
         sorter.setCompressTempFiles(false);
@@ -159,6 +163,7 @@ int main(int argc, char **argv) {
         sink.runChain();
     } else if (mode == "dedup") {
         MarkDuplicates md(tmpdir);
+        md.removeDuplicates = remove_dups;
         reader.addSink(&md);
         md.addSink(&sink);
         sink.runChain();

@@ -74,3 +74,30 @@ def test_skewed_keys_still_exact(tmp_path):
     k.tofile(f)
     r = subprocess.run([str(exe), str(f), "2", "4", "8"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
+
+
+def test_host_staged_transport_across_processes(keys_file, tmp_path):
+    """The host-staged transport (openge_amd/csrc/dist_shm.h: device -> shared host segment -> device,
+    what oge_comm_init_rank picks when ranks share a GPU) run by G forked processes with memcpy ops and
+    a 1 MB staging area, so every exchange takes many rounds: the same global order and balance."""
+    import os
+    exe = _build(tmp_path / "dist_selftest")
+    env = dict(os.environ, OGE_COMM_STAGE_MB="1", OGE_COMM_TIMEOUT="60", OGE_COMM_DIR=str(tmp_path))
+    r = subprocess.run([str(exe), "--shm", str(keys_file), "1", "2", "3", "5", "8"], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    bal = json.loads(r.stdout)
+    for g, b in bal.items():
+        assert b <= 1.05, (g, b)
+    assert not list(tmp_path.glob("oge_comm_*")), "the meeting file must be unlinked once every rank joined"
+
+
+def test_failing_rank_returns_on_every_rank(tmp_path):
+    """One rank's copy operations fail inside the collectives: over the in-process hub and
+    over the host-staged transport, every rank still returns (no rank waits in a collective the failing
+    one left), and the failing rank reports the failure."""
+    import os
+    exe = _build(tmp_path / "dist_selftest")
+    env = dict(os.environ, OGE_COMM_TIMEOUT="60", OGE_COMM_DIR=str(tmp_path))
+    r = subprocess.run([str(exe), "--fail-copy", "2", "3", "5"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr

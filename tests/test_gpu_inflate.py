@@ -222,3 +222,16 @@ def test_inflate_host_writer_streams(ctx, tmp_path, level):
     L.write_bam(str(path), hdr, recs, offs, len(offs) - 1, level=level)
     z = path.read_bytes()
     assert ctx.bgzf_inflate(z) == gzip.decompress(z)
+
+
+def test_long_codes_before_direct_literal_runs(ctx):
+    """Dynamic-Huffman blocks with explicit code lengths (tests/deflate_craft.py): 15-bit literal codes
+    mixed at random with 6-bit ones, so a long code followed by three direct-table (<= 6-bit) literals
+    starts a decode step at every fill level of the lane decoder's bit buffer, including a buffer
+    refilled to exactly 32 bits.  A literal batch after a long code needs 15 + 3 * 6 = 33 bits (VERDICT
+    r02: commit 3941758 allowed it and corrupted a block at 300M reads; only the CRC caught it); the
+    decode must be exact and the always-on bit-budget guard silent."""
+    import deflate_craft as D
+    for seed in (7, 8):
+        data, z = D.long_short_stream(130, seed=seed)  # two waves' worth of blocks
+        assert ctx.bgzf_inflate(z) == data
