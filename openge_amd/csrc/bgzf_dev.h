@@ -130,6 +130,49 @@ __device__ inline uint32_t crc_combine512(uint32_t c, uint32_t len, const uint32
     return ~(r ^ c);
 }
 
+// The same for NT = 1024 threads (pieces of 64 bytes, sixteen waves): six in-wave levels, four over
+// the wave results.
+__device__ inline uint32_t crc_combine1024(uint32_t c, uint32_t len, const uint32_t (*zp)[32], uint32_t *crcs, int t) {
+    const uint32_t lane = t & 63;
+#pragma unroll
+    for (int lv = 0; lv < 6; ++lv) {  // pieces of 64 << lv bytes, pairs inside the wave
+        const uint32_t o = __shfl_down(c, 1u << lv, 64);
+        if (!(lane & ((2u << lv) - 1))) c = crc_mat(zp[6 + lv], c) ^ o;
+    }
+    if (lane == 0) crcs[t >> 6] = c;
+    __syncthreads();
+    uint32_t r = 0xffffffffu;
+    if (t < 64) {
+        c = t < 16 ? crcs[t] : 0u;
+#pragma unroll
+        for (int lv = 0; lv < 4; ++lv) {  // 4096-byte wave pieces
+            const uint32_t o = __shfl_down(c, 1u << lv, 64);
+            if (!(t & ((2u << lv) - 1))) c = crc_mat(zp[12 + lv], c) ^ o;
+        }
+        if (t == 0)
+            for (int k = 0; k < 17; ++k)
+                if ((len >> k) & 1) r = crc_mat(zp[k], r);
+    }
+    return ~(r ^ c);
+}
+
+// 1024 threads over the payload staged in LDS (padded layout PS): thread t owns window bytes
+// [64t, 64t + 64) of the right-aligned 65536-byte window
+template <int PS = 31>
+__device__ uint32_t crc_window1024(const uint32_t *in, uint32_t len, const uint32_t (*crctab)[256], const uint32_t (*zp)[32],
+                                   uint32_t *crcs, int t) {
+    const uint32_t lead = kSlot - len, w0 = t * 64u;
+    uint32_t c = 0;
+    if (w0 >= lead) {
+        const uint32_t d0 = w0 - lead;
+#pragma unroll 4
+        for (int i = 0; i < 16; ++i) c = crc_word(crctab, c ^ ld32p<PS>(in, d0 + 4 * i));
+    } else if (w0 + 64 > lead) {
+        for (uint32_t d = 0; d < w0 + 64 - lead; ++d) c = crctab[0][(c ^ byte_at<PS>(in, d)) & 0xff] ^ (c >> 8);
+    }
+    return crc_combine1024(c, len, zp, crcs, t);
+}
+
 // the payload staged in LDS (padded layout PS)
 template <int PS = 31>
 __device__ uint32_t crc_window512(const uint32_t *in, uint32_t len, const uint32_t (*crctab)[256], const uint32_t (*zp)[32],

@@ -17,7 +17,7 @@
 //   descriptor (L-3, D-1 in 23 bits) and sets the hole's start bit in the block's 65536-bit bitmap.
 //   Code tables are built by the whole wave for one lane at a time (ballot counting, when a lane
 //   reaches a new dynamic block).
-// Phase 2 (k_infl_lz, one 512-thread workgroup per block): refs[p] = p for every position, then
+// Phase 2 (k_infl_lz, one 1024-thread workgroup per block): refs[p] = p for every position, then
 //   refs[p + j] = p - D + j for every hole; pointer jumping (refs[q] = refs[refs[q]]) in LDS until
 //   every position points at a literal (log2 of the copy-chain depth rounds; BAM data: 5-7); the
 //   block's literal-filled bytes are then staged in LDS, every byte gathered from its root, CRC-32
@@ -575,7 +575,12 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
 }
 
 // ---------------------------------------------------------------------------- phase 2
-constexpr uint32_t kT2 = 512;
+// One 1024-thread workgroup per block (r02: 512 threads; the refs array keeps it to one workgroup per
+// CU, so sixteen waves instead of eight hide the LDS and barrier latency of the pointer-jumping rounds).
+// Thread t owns the block's bytes [64t, 64t + 64) for the hole descriptors and the CRC, and the
+// 8-position chunks c = 1024 k + t (k < 8) for the refs / image passes (a wave's 64 lanes touch 64
+// consecutive chunks: conflict-free LDS).
+constexpr uint32_t kT2 = 1024;
 
 __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, const uint64_t *__restrict__ uoff,
                                                  const uint32_t *__restrict__ crc, const uint64_t *__restrict__ bitmap,
@@ -583,7 +588,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     __shared__ __align__(16) uint16_t refs[kSlot + 16];  // later the block's bytes (img)
     __shared__ uint32_t crctab[4][256];
     __shared__ uint32_t zp[17][32];
-    __shared__ uint32_t crcs[kT2];
+    __shared__ uint32_t crcs[kT2 / 64];
     const uint32_t t = threadIdx.x;
     const uint64_t b = b0 + blockIdx.x;
     const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
@@ -593,27 +598,25 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         return;
     }
     if (crc) crc_setup<kT2>(crctab, zp, zpow, t);
-    const uint32_t q0 = 128 * t;
-    // 1. this thread's 128 literal-filled bytes [q0, q0 + 128) and the next word (descriptors may
+    const uint32_t q0 = 64 * t;
+    // 1. this thread's 64 literal-filled bytes [q0, q0 + 64) and the next word (descriptors may
     //    straddle): aligned dword loads, funnel-shifted
-    uint32_t wv[33];
+    uint32_t wv[17];
     {
         const uintptr_t a = (uintptr_t)(O + q0);
         const uint32_t sh = (uint32_t)(a & 3);
         const OGE_G uint32_t *W = (const OGE_G uint32_t *)(a & ~(uintptr_t)3);
         const uintptr_t lim = (uintptr_t)(O + osz);  // a dword starting below lim holds a block byte: readable
-        uint32_t raw[34];
+        uint32_t raw[18];
 #pragma unroll
-        for (int k = 0; k < 34; ++k) raw[k] = (uintptr_t)(W + k) < lim ? W[k] : 0u;
+        for (int k = 0; k < 18; ++k) raw[k] = (uintptr_t)(W + k) < lim ? W[k] : 0u;
 #pragma unroll
-        for (int k = 0; k < 33; ++k) wv[k] = sh ? __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh) : raw[k];
+        for (int k = 0; k < 17; ++k) wv[k] = sh ? __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh) : raw[k];
     }
-    // Steps 2 and 4-6 walk the block in 8-position chunks c = 512 k + t: a wave's 64 lanes touch 64
-    // consecutive 16-byte (refs) or 8-byte (image) chunks, so the LDS accesses are conflict-free.
     // 2. every position its own source
 #pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) {
-        const uint32_t p = 8 * (512 * k + t);
+    for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t p = 8 * (kT2 * k + t);
         uint4 v;
         v.x = p | ((p + 1) << 16), v.y = (p + 2) | ((p + 3) << 16), v.z = (p + 4) | ((p + 5) << 16), v.w = (p + 6) | ((p + 7) << 16);
         *(uint4 *)(refs + p) = v;
@@ -622,17 +625,15 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     // 3. holes: refs[p + j] = p - D + j, descriptors read from this thread's window registers
     const OGE_G uint64_t *bmp = (const OGE_G uint64_t *)(bitmap + (b - b0) * 1024);
     const uint32_t nw = (osz + 63) >> 6;
-#pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {
-        const uint32_t w = 2 * t + h;
-        uint64_t m = w < nw ? bmp[w] : 0;
+    {
+        uint64_t m = t < nw ? bmp[t] : 0;
         while (m) {
-            const uint32_t jb = 64 * h + (uint32_t)__builtin_ctzll(m);  // byte in the window
+            const uint32_t jb = (uint32_t)__builtin_ctzll(m);  // byte in the window
             m &= m - 1;
             const uint32_t d = jb >> 2, sh = (jb & 3) * 8;
             uint32_t lo = wv[0], hi = wv[1];
 #pragma unroll
-            for (uint32_t k = 1; k < 32; ++k) lo = d == k ? wv[k] : lo, hi = d == k ? wv[k + 1] : hi;
+            for (uint32_t k = 1; k < 16; ++k) lo = d == k ? wv[k] : lo, hi = d == k ? wv[k + 1] : hi;
             const uint32_t x = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
             const uint32_t p = q0 + jb, len = (x & 0xff) + 3, dist = ((x >> 8) & 0x7fff) + 1;
             const uint32_t e = min(p + len, osz);  // phase 1 checked it; a failed block must not write past the array
@@ -660,15 +661,15 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
                v.w == ((q + 6) | ((q + 7) << 16));
     };
     uint32_t act = 0;
-    for (uint32_t k = 0; k < 16; ++k)
-        if (8 * (512 * k + t) < osz) act |= 1u << k;
+    for (uint32_t k = 0; k < 8; ++k)
+        if (8 * (kT2 * k + t) < osz) act |= 1u << k;
     for (int round = 0; round < 20; ++round) {
         int changed = 0;
         uint32_t m = act;
         while (m) {
             const uint32_t k = __builtin_ctz(m);
             m &= m - 1;
-            const uint32_t q = 8 * (512 * k + t);
+            const uint32_t q = 8 * (kT2 * k + t);
             const uint4 v = *(const uint4 *)(refs + q);
             if (ident(v, q)) {
                 act &= ~(1u << k);
@@ -693,54 +694,54 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         if (!__syncthreads_or(changed)) break;
     }
     // 5. this thread's chunks' roots into registers, then the region becomes the byte image of the block
-    //    (the literal-filled bytes, coalesced from the output)
-    uint32_t rf[64];
+    //    (the literal-filled bytes, from the registers of step 1: no second global read)
+    uint32_t rf[32];
     uint32_t cp = 0;  // chunks holding copied bytes (a ref other than its own position)
 #pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) {
-        const uint32_t q = 8 * (512 * k + t);
+    for (uint32_t k = 0; k < 8; ++k) {
+        const uint32_t q = 8 * (kT2 * k + t);
         const uint4 v = *(const uint4 *)(refs + q);
         rf[4 * k] = v.x, rf[4 * k + 1] = v.y, rf[4 * k + 2] = v.z, rf[4 * k + 3] = v.w;
         if (!ident(v, q)) cp |= 1u << k;
     }
     __syncthreads();
-    // the image is padded (bgzf_dev.h pw<5>: a spare word per 128 bytes) so the CRC's 128-byte pieces,
+    // the image is padded (bgzf_dev.h pw<4>: a spare word per 64 bytes) so the CRC's 64-byte pieces,
     // one per thread, start in distinct banks; byte q lives at ib(q)
-    constexpr int PS = 5;
+    constexpr int PS = 4;
     uint8_t *img = (uint8_t *)refs;
     uint32_t *img32 = (uint32_t *)refs;
-    auto ib = [](uint32_t q) { return q + ((q >> 7) << 2); };
-    // from the registers of step 1: this thread's 128 bytes [q0, q0 + 128) are words 32 t .. 32 t + 31,
-    // padded to 33 t + k (a lane's words at a 33-word stride: distinct banks), no second global read
+    auto ib = [](uint32_t q) { return q + ((q >> 6) << 2); };
 #pragma unroll
-    for (uint32_t k = 0; k < 32; ++k) img32[33 * t + k] = wv[k];
+    for (uint32_t k = 0; k < 16; ++k) img32[17 * t + k] = wv[k];
     __syncthreads();
     // 6. every copied byte from its root (a literal position of the image); literal-only chunks are
     //    already in place
     const uint32_t last = osz ? osz - 1 : 0;
+    uint32_t cw[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < 8; ++k) {
+        cw[2 * k] = cw[2 * k + 1] = 0;
         if (!((cp >> k) & 1)) continue;
         uint32_t r[8];
 #pragma unroll
         for (int i = 0; i < 4; ++i) r[2 * i] = min(rf[4 * k + i] & 0xffff, last), r[2 * i + 1] = min(rf[4 * k + i] >> 16, last);
-        wv[2 * k] = (uint32_t)img[ib(r[0])] | ((uint32_t)img[ib(r[1])] << 8) | ((uint32_t)img[ib(r[2])] << 16) |
+        cw[2 * k] = (uint32_t)img[ib(r[0])] | ((uint32_t)img[ib(r[1])] << 8) | ((uint32_t)img[ib(r[2])] << 16) |
                     ((uint32_t)img[ib(r[3])] << 24);
-        wv[2 * k + 1] = (uint32_t)img[ib(r[4])] | ((uint32_t)img[ib(r[5])] << 8) | ((uint32_t)img[ib(r[6])] << 16) |
+        cw[2 * k + 1] = (uint32_t)img[ib(r[4])] | ((uint32_t)img[ib(r[5])] << 8) | ((uint32_t)img[ib(r[6])] << 16) |
                         ((uint32_t)img[ib(r[7])] << 24);
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < 8; ++k) {
         if (!((cp >> k) & 1)) continue;
-        const uint32_t w = 2 * (512 * k + t);  // w, w + 1: same 32-word group
-        img32[pw<PS>(w)] = wv[2 * k];
-        img32[pw<PS>(w) + 1] = wv[2 * k + 1];
+        const uint32_t w = 2 * (kT2 * k + t);  // w, w + 1: same 16-word group
+        img32[pw<PS>(w)] = cw[2 * k];
+        img32[pw<PS>(w) + 1] = cw[2 * k + 1];
     }
     __syncthreads();
     // 7. CRC and the write-out at the block's alignment
     if (crc) {
-        const uint32_t c = crc_window512<PS>(img32, osz, crctab, zp, crcs, t);
+        const uint32_t c = crc_window1024<PS>(img32, osz, crctab, zp, crcs, t);
         if (t == 0 && c != crc[b]) report(err, E_CRC, b);
     }
     const uint32_t sh = (uint32_t)((uintptr_t)O & 3);

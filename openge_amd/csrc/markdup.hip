@@ -1008,12 +1008,8 @@ static int md_win_bounds(oge_ctx *ctx, const uint64_t *skeys, const int64_t *ax,
     return OGE_OK;
 }
 
-// OGE_MD_WINDOW=0 forces the sort-based group stages (A/B); OGE_MD_WINCAP=k (tests) lowers the window
-// caps so that most tiles overflow and take the collect + sort path.  Read per call.
-static bool md_window_enabled() {
-    const char *e = getenv("OGE_MD_WINDOW");
-    return !(e && *e == '0');
-}
+// OGE_MD_WINCAP=k (tests) lowers the window caps so that most tiles overflow and take the collect + sort
+// path.  Read per call.
 static uint32_t md_win_cap(uint32_t cap) {
     const char *e = getenv("OGE_MD_WINCAP");
     const long v = e && *e ? atol(e) : 0;
@@ -1045,7 +1041,7 @@ static int pair_groups_sorted(oge_ctx *ctx, const oge_markdup_opts *opts, uint64
 int oge_md_frag_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdFrags &f, uint64_t n, uint8_t *dup,
                            bool *done) {
     *done = false;
-    if (!f.skeys || !f.dev || !md_window_enabled() || opts->debug_sort_groups) return OGE_OK;
+    if (!f.skeys || !f.dev || opts->debug_sort_groups) return OGE_OK;
     if (!n) { *done = true; return OGE_OK; }
     KeyLayout L;
     int rc = md_layout(ctx, opts, &L);
@@ -1083,7 +1079,7 @@ int oge_md_frag_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const Oge
 
 int oge_md_pair_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &P, uint8_t *dup, bool *done) {
     *done = false;
-    if (!P.pax || !P.dev || !md_window_enabled() || opts->debug_sort_groups) return OGE_OK;
+    if (!P.pax || !P.dev || opts->debug_sort_groups) return OGE_OK;
     if (!P.np) { *done = true; return OGE_OK; }
     // debug_hash_bits narrows the sort-based path's hash to exercise its collision handling: keep it
     if (opts->debug_hash_bits > 0) return OGE_OK;

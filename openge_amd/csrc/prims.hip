@@ -342,15 +342,10 @@ int oge_radix_sort_pairs(oge_ctx *ctx, uint64_t *keys, uint32_t *vals, uint64_t 
     if (n < 2 || bit_mask == 0) return OGE_OK;
     if (n > 0xFFFFFFFFull) return oge_fail(ctx, OGE_ERR_LIMIT, "radix sort: more than 2^32-1 elements");
     const bool has_v = vals != nullptr;
-    // widest digit (OGE_RADIX_MAXW, 4..10).  8 is the measured optimum on C2 at 300M reads: 9- and
-    // 10-bit digits save passes but every 4096-key tile then spreads over 512/1024 buckets, the
-    // scatter's per-bucket runs shrink below a cache line, and the step got slower (185 -> 192 /
-    // 196 ms).  Both wide paths pass the parity suite.
-    static const uint32_t maxw = [] {
-        const char *e = getenv("OGE_RADIX_MAXW");
-        const int v = e && *e ? atoi(e) : 8;
-        return (uint32_t)std::min(10, std::max(4, v));
-    }();
+    // widest digit 8 bits: the measured optimum on C2 at 300M reads (r01: 9- and 10-bit digits save
+    // passes but every 4096-key tile then spreads over 512/1024 buckets, the scatter's per-bucket runs
+    // shrink below a cache line, and the step got slower: 185 -> 192 / 196 ms)
+    constexpr uint32_t maxw = 8;
     std::vector<Digit> digits = plan_digits(bit_mask, maxw);
     const uint32_t nblocks = oge_ceil_div(n, kTile);
     uint32_t *hist = (uint32_t *)ctx->ws("radix_hist", (size_t)1024 * nblocks * sizeof(uint32_t));

@@ -157,6 +157,19 @@ std::string RRead::quals_ascii() const {
 
 static inline uint32_t rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
 
+// the same strings into a caller's (thread-local, reused) buffers: no allocation per read
+static void bases_into(const RRead &r, std::string &s) {
+    s.resize(r.l_seq);
+    char *o = &s[0];
+    const uint32_t full = r.l_seq >> 1;
+    for (uint32_t k = 0; k < full; ++k) memcpy(o + 2 * k, kSeqPairs.p[(uint8_t)r.seq4[k]], 2);
+    if (r.l_seq & 1) o[r.l_seq - 1] = kSeqPairs.p[(uint8_t)r.seq4[full]][0];
+}
+static void quals_ascii_into(const RRead &r, std::string &q) {
+    q.assign(r.qual.data(), r.qual.size());
+    for (auto &c : q) c = (char)(c + 33);
+}
+
 bool rread_decode(const uint8_t *rec, RRead &r, std::string &err) {
     uint32_t bs = rd32(rec);
     if (bs < 32 || bs > 10000) {  // BamDeserializer::read rejects these (util/bam_deserializer.h:160-163)
@@ -556,27 +569,49 @@ static inline bool is_regular(char b) {  // BaseUtils::isRegularBase (util/gatk/
     return b == 'A' || b == 'C' || b == 'G' || b == 'T' || b == 'a' || b == 'c' || b == 'g' || b == 't' || b == '*';
 }
 
+// bytes of getUnclippedBases (:137-164) -- the M and I operations of the ORIGINAL cigar, each clipped
+// to the read -- for the interval's arena
+static size_t unclipped_len(const RRead &r) {
+    size_t from = 0, n = 0;
+    for (auto &ce : r.cigar) {
+        if (ce.t == 'S') from += ce.n;
+        else if (ce.t == 'M' || ce.t == 'I') {
+            if (from < r.l_seq) n += std::min<size_t>(ce.n, r.l_seq - from);
+            from += ce.n;
+        }
+    }
+    return n;
+}
+
 struct AlignedRead {
     RRead *read;
-    std::string bases, quals;  // getUnclippedBases (:137-164): M and I of the ORIGINAL cigar
+    std::string_view bases, quals;  // getUnclippedBases (:137-164), in the interval's arena
     Cigar newCigar;
     int newStart = -1;
     int misRef = 0;
     long aligner = 0;
 
-    explicit AlignedRead(RRead *r) : read(r) {
-        const std::string ab = r->bases(), aq = r->quals_ascii();
-        size_t from = 0;
+    // decodes the unclipped bases and their ASCII qualities into arena[0 .. 2 * unclipped_len(*r))
+    AlignedRead(RRead *r, char *arena) : read(r) {
+        const size_t n = unclipped_len(*r);
+        char *b = arena, *q = arena + n;
+        size_t from = 0, k = 0;
         for (auto &ce : r->cigar) {
             if (ce.t == 'S') from += ce.n;
             else if (ce.t == 'M' || ce.t == 'I') {
-                if (from < ab.size()) {
-                    bases.append(ab, from, ce.n);
-                    quals.append(aq, from, ce.n);
+                if (from < r->l_seq) {
+                    const size_t m = std::min<size_t>(ce.n, r->l_seq - from);
+                    for (size_t j = 0; j < m; ++j, ++k) {
+                        const size_t i = from + j;
+                        b[k] = kSeqChars[((uint8_t)r->seq4[i >> 1] >> ((i & 1) ? 0 : 4)) & 15];
+                        q[k] = (char)(r->qual[i] + 33);
+                    }
                 }
                 from += ce.n;
             }
         }
+        bases = std::string_view(b, n);
+        quals = std::string_view(q, n);
     }
     int read_length() const { return bases.empty() ? (int)read->l_seq : (int)bases.size(); }
     const Cigar &cigar() const { return newCigar.empty() ? read->cigar : newCigar; }
@@ -601,7 +636,7 @@ struct AlignedRead {
 
 // mismatchQualitySumIgnoreCigar (:641-679) with quit = INT_MAX (the raw mismatch score)
 static int mismatch_sum_ignore_cigar(const AlignedRead &a, const std::string &ref, int refIndex) {
-    const std::string &rs = a.bases, &q = a.quals;
+    const std::string_view rs = a.bases, q = a.quals;
     const int64_t L = (int64_t)rs.size(), R = (int64_t)ref.size();
     int sum = 0;
     for (int64_t i = 0; i < L; ++i) {
@@ -623,7 +658,9 @@ static long mismatching_qualities(const RRead &r, const std::string &ref, int re
     long mq = 0;
     int readIdx = 0;
     const int endOnRead = (int)r.l_seq - 1;
-    const std::string rs = r.bases(), qa = r.quals_ascii();
+    thread_local std::string rs, qa;
+    bases_into(r, rs);
+    quals_ascii_into(r, qa);
     for (auto &ce : r.cigar) {
         if (readIdx > endOnRead) break;
         switch (ce.t) {
@@ -652,7 +689,7 @@ struct Consensus {
 };
 
 // createAlternateConsensus from a read (:1022-1088)
-static bool create_consensus(int indexOnRef, const Cigar &c, const std::string &ref, const std::string &readStr, Consensus &out) {
+static bool create_consensus(int indexOnRef, const Cigar &c, const std::string &ref, std::string_view readStr, Consensus &out) {
     if (indexOnRef < 0) return false;
     if (c.size() == 1 && c[0].t == 'M') return false;
     std::string sb;
@@ -766,18 +803,17 @@ static bool update_read(const Cigar &alt, int altPosOnRef, int myPosOnAlt, Align
 }
 
 // alternateReducesEntropy (:1274-1391)
-static bool reduces_entropy(const std::vector<std::unique_ptr<AlignedRead>> &reads, const std::string &ref, int leftmost,
+static bool reduces_entropy(const std::vector<AlignedRead> &reads, const std::string &ref, int leftmost,
                             double mismatchThreshold) {
     const size_t n = ref.size();
     std::vector<int> om(n, 0), cm(n, 0), to(n, 0), tc(n, 0);
-    for (auto &ap : reads) {
-        const AlignedRead &a = *ap;
+    for (const AlignedRead &a : reads) {
         int blocks = 0;
         for (auto &c : a.read->cigar)
             if (c.t == 'M' || c.t == '=' || c.t == 'X') blocks++;
         if (blocks > 1) continue;
         int refIdx = a.read->pos - leftmost;
-        const std::string &rs = a.bases, &q = a.quals;
+        const std::string_view rs = a.bases, q = a.quals;
         for (size_t j = 0; j < rs.size(); ++j, ++refIdx) {
             if (refIdx < 0 || refIdx >= (int)n) break;
             int w = (int)(signed char)q[j] - 33;
@@ -827,7 +863,9 @@ static inline bool bases_equal(char l, char r) {  // SequenceUtil::basesEqual (S
 // SequenceUtil::calculateSamNmTag / sumQualitiesOfMismatches (SequenceUtil.cpp:134-228) over the
 // read's alignment blocks (getAlignmentBlocks :55-88).  UQ sums ASCII qualities (Q23).
 static void nm_uq(const RRead &r, const std::string &ref, int leftmost, int *nm, int *uq) {
-    const std::string rs = r.bases(), qa = r.quals_ascii();
+    thread_local std::string rs, qa;
+    bases_into(r, rs);
+    quals_ascii_into(r, qa);
     int readBase = 0, refBase = r.pos - leftmost, mis = 0, qs = 0;
     auto refc = [&](int k) -> char { return (k >= 0 && k < (int)ref.size()) ? ref[k] : '\0'; };
     auto readc = [&](int k) -> char { return (k >= 0 && k < (int)rs.size()) ? rs[k] : '\0'; };
@@ -866,7 +904,8 @@ struct IntervalData {
     std::string reference;
     int leftmost = 0;
     long totalRaw = 0;
-    std::vector<std::unique_ptr<AlignedRead>> alt;
+    std::vector<AlignedRead> alt;        // altReads, bases / qualities in `arena`
+    std::vector<char> arena;
     std::vector<Consensus> cons;
     uint64_t pairBase = 0;
     std::vector<std::pair<RRead *, RRead>> pending;  // read -> updated copy (applied in phase E)
@@ -1400,25 +1439,33 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         for (auto &c : d.reference) c = (char)toupper((unsigned char)c);
         d.leftmost = padLeft;
         const std::string &ref = d.reference;
+        size_t abytes = 0;
+        for (RRead *r : d.toClean)
+            if (!r->cigar.empty()) abytes += 2 * unclipped_len(*r);
+        d.arena.resize(abytes);  // sized once: the altReads' views into it stay valid
+        char *ap = d.arena.data();
+        thread_local std::string rb;
         for (RRead *r : d.toClean) {
             if (r->cigar.empty()) continue;  // refReads
-            std::unique_ptr<AlignedRead> a(new AlignedRead(r));
+            AlignedRead a(r, ap);
+            ap += 2 * a.bases.size();
             int blocks = 0;
             for (auto &c : r->cigar)
                 if (c.t == 'M' || c.t == '=' || c.t == 'X') blocks++;
             if (blocks == 2) {
-                Cigar nc = left_align_indel(unclip_cigar(r->cigar), ref, r->bases(), r->pos - d.leftmost, 0);
-                a->set_cigar(nc, false);
+                bases_into(*r, rb);
+                Cigar nc = left_align_indel(unclip_cigar(r->cigar), ref, rb, r->pos - d.leftmost, 0);
+                a.set_cigar(nc, false);
             }
             const int startOnRef = r->pos - d.leftmost;
-            const int raw = mismatch_sum_ignore_cigar(*a, ref, startOnRef);
+            const int raw = mismatch_sum_ignore_cigar(a, ref, startOnRef);
             if (raw > 0) {
                 if (!r->dup()) d.totalRaw += raw;
-                a->misRef = raw;
-                a->aligner = mismatching_qualities(*r, ref, startOnRef);
+                a.misRef = raw;
+                a.aligner = mismatching_qualities(*r, ref, startOnRef);
                 if (blocks == 2) {
                     Consensus c;
-                    if (create_consensus(startOnRef, a->cigar(), ref, a->bases, c)) {
+                    if (create_consensus(startOnRef, a.cigar(), ref, a.bases, c)) {
                         c.hash = std::hash<std::string>()(c.str);
                         bool exists = false;
                         for (auto &o : d.cons)
@@ -1448,7 +1495,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         const bool on = !d.cons.empty();
         if (on) {
             for (auto &c : d.cons) cb += c.str.size();
-            for (auto &a : d.alt) rb += a->bases.size();
+            for (auto &a : d.alt) rb += a.bases.size();
         }
         xc[w + 1] = xc[w] + (on ? d.cons.size() : 0);
         xcb[w + 1] = xcb[w] + cb;
@@ -1477,7 +1524,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         }
         uint64_t rb = xrb[w], ri0 = xr[w];
         for (size_t j = 0; j < d.alt.size(); ++j) {
-            const AlignedRead &a = *d.alt[j];
+            const AlignedRead &a = d.alt[j];
             memcpy(B.bases.data() + rb, a.bases.data(), a.bases.size());
             for (size_t k = 0; k < a.quals.size(); ++k) B.quals[rb + k] = (uint8_t)(a.quals[k] - 33);
             rb += a.bases.size();
@@ -1487,7 +1534,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         for (uint32_t c = 0; c < d.cons.size(); ++c) {
             const int consLen = (int)d.cons[c].str.size();
             for (uint32_t j = 0; j < d.alt.size(); ++j) {
-                const AlignedRead &a = *d.alt[j];
+                const AlignedRead &a = d.alt[j];
                 ScanPair &sp = B.pairs[pi++];
                 sp.cons = (uint32_t)(ci0 + c);
                 sp.read = (uint32_t)(ri0 + j);
@@ -1522,7 +1569,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         for (auto &c : d.cons) {  // deterministic consensus order (Q19: the reference shuffles)
             c.sum = 0;
             for (size_t j = 0; j < d.alt.size(); ++j, ++pi) {
-                AlignedRead &a = *d.alt[j];
+                AlignedRead &a = d.alt[j];
                 int my = bscore[pi];
                 if (my > a.aligner || my >= a.misRef) my = a.misRef;
                 else c.readIndexes.push_back(std::make_pair((int)j, (int)bidx[pi]));
@@ -1534,14 +1581,14 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         if (!(improvement >= P.lod_threshold)) return;
         best->cigar = left_align_indel(best->cigar, d.reference, best->str, best->pos, best->pos);
         for (auto &ip : best->readIndexes)
-            if (!update_read(best->cigar, best->pos, ip.second, *d.alt[ip.first], d.leftmost)) return;
+            if (!update_read(best->cigar, best->pos, ip.second, d.alt[ip.first], d.leftmost)) return;
         if (!reduces_entropy(d.alt, d.reference, d.leftmost, P.mismatch_threshold)) return;
         std::string reference = d.reference;
         int leftmost = d.leftmost;
         const std::string &contig = ref_names[ivs[d.interval].contig];
         const std::string *fseq = fa.get(contig);
         for (auto &ip : best->readIndexes) {
-            AlignedRead &a = *d.alt[ip.first];
+            AlignedRead &a = d.alt[ip.first];
             // constizeUpdate (:218-241)
             if (a.newCigar.empty()) continue;
             RRead u = *a.read;
@@ -1684,14 +1731,25 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         err = "internal: emitted " + std::to_string(order.size()) + " of " + std::to_string(n) + " records";
         return -1;
     }
+    // output offsets: sizes and per-chunk sums in parallel, the chunk prefix serially, then the adds
+    const uint64_t chunk = 4096;
     out_off.assign(n + 1, 0);
-    for (uint64_t i = 0; i < n; ++i) out_off[i + 1] = rread_encoded_size(*order[i]);
-    for (uint64_t i = 0; i < n; ++i) out_off[i + 1] += out_off[i];
+    const uint64_t nch = (n + chunk - 1) / chunk;
+    std::vector<uint64_t> csum(nch + 1, 0);
+    pool.run_chunks(n, chunk, [&](size_t b, size_t e) {
+        uint64_t s = 0;
+        for (size_t i = b; i < e; ++i) s += (out_off[i + 1] = rread_encoded_size(*order[i]));
+        csum[b / chunk + 1] = s;
+    });
+    for (uint64_t c = 0; c < nch; ++c) csum[c + 1] += csum[c];
+    pool.run_chunks(n, chunk, [&](size_t b, size_t e) {
+        uint64_t run = csum[b / chunk];
+        for (size_t i = b; i < e; ++i) run = (out_off[i + 1] += run);
+    });
     if (!out.alloc(out_off[n])) {
         err = "out of host memory for the output records";
         return -1;
     }
-    const uint64_t chunk = 4096;
     pool.run_chunks(n, chunk, [&](size_t b, size_t e) {
         for (size_t i = b; i < e; ++i) rread_encode_to(*order[i], out.data() + out_off[i]);
     });
