@@ -157,10 +157,21 @@ int plan_ranges(oge_ctx *ctx, const std::vector<Run> &runs, uint64_t total, uint
         uint64_t mid = keys[keys.size() / 2];
         if (mid == iv.a) {  // the lower half is one key: cut just above it
             auto it = std::upper_bound(keys.begin(), keys.end(), mid);
-            if (it == keys.end())
-                return oge_fail(ctx, OGE_ERR_LIMIT, ("chunked sort: " + std::to_string(R.n) + " records share one sort key (" +
-                                                     std::to_string(R.bytes) + " bytes), more than the chunk size").c_str());
-            mid = *it;
+            if (it != keys.end()) {
+                mid = *it;
+            } else {  // no larger key among the samples: the smallest larger key of any run's whole segment
+                uint64_t nxt = ~0ull;
+                bool found = false;
+                for (size_t j = 0; j < runs.size(); ++j) {
+                    const uint64_t *b = runs[j].keys.data() + R.lo[j], *e = runs[j].keys.data() + R.hi[j];
+                    const uint64_t *u = std::upper_bound(b, e, mid);
+                    if (u != e) nxt = std::min(nxt, *u), found = true;
+                }
+                if (!found)
+                    return oge_fail(ctx, OGE_ERR_LIMIT, ("chunked sort: " + std::to_string(R.n) + " records share one sort key (" +
+                                                         std::to_string(R.bytes) + " bytes), more than the chunk size").c_str());
+                mid = nxt;
+            }
         }
         work.insert(work.begin(), {mid, iv.b, iv.last});
         work.insert(work.begin(), {iv.a, mid, false});

@@ -70,10 +70,11 @@ __global__ void k_rec_guess(const uint8_t *__restrict__ d, uint64_t p, uint64_t 
 }
 
 // walk chunk c from start[c] to the first record start at or past the chunk end; with out != NULL
-// also write the (absolute) offsets from pos[c]
+// also write the (absolute) offsets from pos[c], never at or past out[cap] (a stream that changed since
+// the counts in pos were made may hold more records: the caller then detects it and walks again)
 __global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t n, uint64_t CH, uint64_t C,
                            const uint64_t *__restrict__ start, uint64_t *__restrict__ stop, uint64_t *__restrict__ count,
-                           const uint64_t *__restrict__ pos, uint64_t *__restrict__ out) {
+                           const uint64_t *__restrict__ pos, uint64_t *__restrict__ out, uint64_t cap) {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     const uint64_t end = min(n, p + (c + 1) * CH);
@@ -83,12 +84,12 @@ __global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t n
         count[c] = 0;
         return;
     }
-    uint64_t *o = out ? out + pos[c] : nullptr;
+    const uint64_t o0 = out ? pos[c] : 0;
     while (q < end) {
         if (q + 4 > n) break;
         const uint32_t bs = rd32u(d + q);
         if (bs < 32 || bs > 10000 || q + 4 + bs > n) break;
-        if (o) o[k] = q;
+        if (out && o0 + k < cap) out[o0 + k] = q;
         ++k;
         q += 4 + bs;
     }
@@ -514,7 +515,7 @@ extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream,
     // one walk + join pass: *st bit 0 = a start moved, bit 1 = an invalid or unjoined stop
     auto walk_join = [&](uint64_t *pos_arg, uint64_t *out, unsigned int *h) -> int {
         OGE_HIP_TRY(ctx, hipMemsetAsync(st, 0, 4, ctx->stream));
-        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos_arg, out);
+        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos_arg, out, cap);
         OGE_LAUNCH_CHECK(ctx);
         k_rec_join<<<G, TB, 0, ctx->stream>>>(stop, start, C, end, st);
         OGE_LAUNCH_CHECK(ctx);
@@ -573,7 +574,7 @@ extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream,
         return OGE_OK;
     }
     if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
-    k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos, d_off);
+    k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos, d_off, cap);
     OGE_LAUNCH_CHECK(ctx);
     OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &end, 8, hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
