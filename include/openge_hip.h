@@ -354,9 +354,6 @@ int oge_bgzf_index_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64
  * checks every payload's CRC-32.  Fails with OGE_ERR_IO on corrupt data. */
 int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d_d0, const uint64_t *d_d1,
                          const uint64_t *d_uoff, const uint32_t *d_crc, uint64_t nblk, uint8_t *d_out);
-/* Test/measurement only: pick the inflate implementation of this context (0 = workgroup-per-block
- * segment decoder, the default; 1 = the r02 lane-per-block decoder). */
-int oge_debug_set_inflate(oge_ctx *ctx, int impl);
 /* Host-buffer form: the whole BGZF stream z -> out (out_cap >= payload total). */
 int oge_bgzf_inflate(oge_ctx *ctx, const uint8_t *z, uint64_t zbytes, uint8_t *out, uint64_t out_cap,
                      uint64_t *out_bytes);

@@ -17,8 +17,7 @@ constexpr uint32_t kSlot = 65536;  // max BGZF block size (and max payload accep
 
 // inflate error bits (err[0] |= 1 << code; err[1] = the first failing block)
 enum InflErr { E_STORED = 1, E_CODE = 2, E_OVERRUN = 3, E_LEN = 4, E_DIST = 5, E_FAR = 6, E_TYPE = 7, E_PAST = 8, E_SIZE = 9,
-               E_TABLE = 10, E_CRC = 11, E_BITS = 12,
-               E_SEG = 13, E_LZ = 14 };  // segment decoder: pass counts disagree / copies left unresolved
+               E_TABLE = 10, E_CRC = 11, E_BITS = 12 };
 
 __device__ __forceinline__ uint32_t ld32(const uint32_t *w, uint32_t p) {  // unaligned LDS read
     const uint32_t a = w[p >> 2], b = w[(p >> 2) + 1];

@@ -442,10 +442,9 @@ extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t z
     const uint32_t init[2] = {0, 0xffffffffu};
     OGE_HIP_TRY(ctx, hipMemcpyAsync(err, init, 8, hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, zh, sizeof(zh), hipMemcpyHostToDevice, ctx->stream));
-    // the segment decoder (inflate_seg.hip), CRC fused; the lane decoder (inflate_lane.hip) for A/B
+    // the lane decoder (inflate_lane.hip), CRC fused into its phase 2
     OgeStageTimer *tm = ctx->begin_stage("bgzf_inflate");
-    const int rc = ctx->inflate_impl == 1 ? oge_inflate_lanes(ctx, d_z, zbytes, d_d0, d_d1, d_uoff, d_crc, nblk, d_out, err, zpow)
-                                          : oge_inflate_seg(ctx, d_z, zbytes, d_d0, d_d1, d_uoff, d_crc, nblk, d_out, err, zpow);
+    const int rc = oge_inflate_lanes(ctx, d_z, zbytes, d_d0, d_d1, d_uoff, d_crc, nblk, d_out, err, zpow);
     ctx->end_stage(tm);
     if (rc) return rc;
     uint32_t got[2];
@@ -457,12 +456,6 @@ extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t z
                  (got[0] >> E_CRC) & 1 ? "CRC mismatch" : "corrupt deflate data", got[0]);
         return oge_fail(ctx, OGE_ERR_IO, msg);
     }
-    return OGE_OK;
-}
-
-extern "C" int oge_debug_set_inflate(oge_ctx *ctx, int impl) {
-    if (!ctx || impl < 0 || impl > 1) return oge_fail(ctx, OGE_ERR_ARG, "inflate impl must be 0 (segments) or 1 (lanes)");
-    ctx->inflate_impl = impl;
     return OGE_OK;
 }
 

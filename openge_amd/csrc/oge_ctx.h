@@ -41,7 +41,6 @@ struct oge_ctx {
         uint64_t base = 0, end = 0, n = 0, C = 0;
         int32_t n_ref = 0;
     } recwalk;
-    int inflate_impl = 0;  // 0 = workgroup-per-block segment decoder, 1 = lane decoder (oge_debug_set_inflate, A/B)
     bool last_scan_generic = false;  // realign scan fell back to the byte-wise kernel
     double scan_t[3] = {0, 0, 0};    // realign scan host timings: validate, upload, device + download
 
@@ -108,10 +107,6 @@ int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzf
 int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d0, const uint64_t *d1,
                       const uint64_t *uoff, const uint32_t *crc, uint64_t nblk, uint8_t *out, uint32_t *err,
                       const uint32_t *zpow);
-// workgroup-per-block segment-parallel BGZF inflate (inflate_seg.hip); same arguments
-int oge_inflate_seg(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d0, const uint64_t *d1,
-                    const uint64_t *uoff, const uint32_t *crc, uint64_t nblk, uint8_t *out, uint32_t *err,
-                    const uint32_t *zpow);
 
 // ---- multi-GPU internals (dist.hip)
 oge_ctx *oge_comm_ctx(oge_comm *comm);

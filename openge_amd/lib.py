@@ -251,7 +251,6 @@ def lib() -> C.CDLL:
         "oge_bgzf_index": (C.c_int, [vp, u64, vp, vp, vp, vp, u64, C.POINTER(u64)]),
         "oge_bgzf_inflate_dev": (C.c_int, [vp, vp, u64, vp, vp, vp, vp, u64, vp]),
         "oge_bgzf_inflate": (C.c_int, [vp, vp, u64, vp, u64, C.POINTER(u64)]),
-        "oge_debug_set_inflate": (C.c_int, [vp, C.c_int]),
         "oge_bam_record_offsets_dev": (C.c_int, [vp, vp, u64, u64, i32, vp, u64, C.POINTER(u64)]),
         "oge_drop_flagged_dev": (C.c_int, [vp, vp, vp, u64, C.c_uint16, vp, vp, C.POINTER(u64)]),
         "oge_filter_opts_init": (None, [vp]),
@@ -485,10 +484,6 @@ class Context:
         got = C.c_uint64()
         check(lib().oge_bgzf_deflate_dev(self.h, d_src, n, level, d_dst, dst_cap, C.byref(got)), self.h)
         return got.value
-
-    def set_inflate(self, impl: int) -> None:
-        """Test/measurement only: 0 = segment decoder (default), 1 = lane decoder."""
-        check(lib().oge_debug_set_inflate(self.h, impl), self.h)
 
     def bgzf_inflate(self, z: bytes, out_cap: int | None = None) -> bytes:
         """Decompress a BGZF stream on the device (host buffers in and out)."""
