@@ -546,41 +546,76 @@ __device__ __forceinline__ void seg_load(const uint8_t *s, uint32_t s0, uint32_t
     }
 }
 
+// Latency, not work, bounds these two: a code lookup or a match-token load inside a data-dependent branch
+// is waited for on the spot.  So the segment's literal codes are looked up 16 at a time without branches
+// (independent LDS reads in flight together) and its first kMPre match tokens are loaded at once.
+constexpr int kMPre = 8;
+__device__ __forceinline__ void seg_tokens(const uint32_t *mp, uint32_t nm, uint32_t (&m)[kMPre]) {
+    const uint32_t last = nm ? nm - 1 : 0;  // (clamped: every load is a real address, no branch around it)
+#pragma unroll
+    for (int k = 0; k < kMPre; ++k) m[k] = mp[(uint64_t)min((uint32_t)k, last) * kNSeg];
+}
+
 __device__ __forceinline__ uint32_t seg_bits(const uint32_t (&w)[16], uint64_t lm, uint32_t nm, const uint32_t *mp,
-                                             const uint32_t *lit, const uint32_t *dist) {
+                                             const uint32_t (&m)[kMPre], const uint32_t *lit, const uint32_t *dist) {
     uint32_t bits = 0;
 #pragma unroll
-    for (int i = 0; i < 64; ++i)
-        if ((lm >> i) & 1) bits += lit[(w[i >> 2] >> (8 * (i & 3))) & 0xff] >> 16;
-    for (uint32_t k = 0; k < nm; ++k) bits += match_bits(mp[(uint64_t)k * kNSeg], lit, dist);
+    for (int g = 0; g < 4; ++g) {
+        uint32_t c[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c[i] = lit[(w[4 * g + (i >> 2)] >> (8 * (i & 3))) & 0xff];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) bits += (lm >> (16 * g + i)) & 1 ? c[i] >> 16 : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kMPre; ++k)
+        if ((uint32_t)k < nm) bits += match_bits(m[k], lit, dist);
+    for (uint32_t k = kMPre; k < nm; ++k) bits += match_bits(mp[(uint64_t)k * kNSeg], lit, dist);
     return bits;
 }
 
 __device__ __forceinline__ void seg_emit(const uint32_t (&w)[16], uint64_t lm, uint32_t nm, const uint32_t *mp,
-                                         const uint32_t *lit, const uint32_t *dist, uint32_t *img, uint32_t bit) {
-    uint32_t k = 0, m = nm ? mp[0] : 0, moff = nm ? (m >> 23) : 64u;
+                                         uint32_t (&m)[kMPre], const uint32_t *lit, const uint32_t *dist, uint32_t *img,
+                                         uint32_t bit) {
+    // the next match's length / distance codes are looked up one match ahead (software pipelined): at a
+    // match start the codes are already in registers, and the lookups for the following match overlap
+    // the literals in between
+    uint32_t k = 0, cur = m[0], moff = nm ? (cur >> 23) : 64u;
+    uint32_t ev, nb, dev, dnb, lc, dc;
+    auto look = [&](uint32_t tok) {
+        const uint32_t L = ((tok >> 15) & 255) + 3, D = (tok & 0x7fff) + 1;
+        uint32_t sym, dsym;
+        len_code(L, sym, nb, ev);
+        dist_code(D, dsym, dnb, dev);
+        lc = lit[sym];
+        dc = dist[dsym];
+    };
+    look(cur);
     LdsBits bw;
     bw.init(img, bit);
 #pragma unroll
-    for (int i = 0; i < 64; ++i) {
-        if ((lm >> i) & 1) {
-            const uint32_t c = lit[(w[i >> 2] >> (8 * (i & 3))) & 0xff];
-            bw.put(c & 0xffff, c >> 16);
-        } else if ((uint32_t)i == moff) {
-            const uint32_t L = ((m >> 15) & 255) + 3, D = (m & 0x7fff) + 1;
-            uint32_t sym, nb, ev, dsym, dnb, dev;
-            len_code(L, sym, nb, ev);
-            dist_code(D, dsym, dnb, dev);
-            const uint32_t c = lit[sym];
-            bw.put((c & 0xffff) | (ev << (c >> 16)), (c >> 16) + nb);
-            const uint32_t dc = dist[dsym];
-            bw.put((dc & 0xffff) | (dev << (dc >> 16)), (dc >> 16) + dnb);
-            ++k;
-            if (k < nm) {
-                m = mp[(uint64_t)k * kNSeg];
-                moff = m >> 23;
-            } else {
-                moff = 64;
+    for (int g = 0; g < 4; ++g) {
+        uint32_t c[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) c[i] = lit[(w[4 * g + (i >> 2)] >> (8 * (i & 3))) & 0xff];
+#pragma unroll
+        for (int i0 = 0; i0 < 16; ++i0) {
+            const int i = 16 * g + i0;
+            if ((lm >> i) & 1) {
+                bw.put(c[i0] & 0xffff, c[i0] >> 16);
+            } else if ((uint32_t)i == moff) {
+                bw.put((lc & 0xffff) | (ev << (lc >> 16)), (lc >> 16) + nb);
+                bw.put((dc & 0xffff) | (dev << (dc >> 16)), (dc >> 16) + dnb);
+                ++k;
+#pragma unroll
+                for (int q = 0; q + 1 < kMPre; ++q) m[q] = m[q + 1];  // the next token to the front
+                if (k < nm) {
+                    cur = k < (uint32_t)kMPre ? m[0] : mp[(uint64_t)k * kNSeg];
+                    moff = cur >> 23;
+                    look(cur);
+                } else {
+                    moff = 64;
+                }
             }
         }
     }
@@ -596,7 +631,7 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
     __shared__ uint32_t lit[kLit], dist[kDist];
     __shared__ uint32_t scan[kNSeg];
     __shared__ uint32_t wsum[kT / 64];
-    __shared__ uint32_t crctab[1][256];
+    __shared__ uint32_t crctab[4][256];
     __shared__ uint32_t zp[17][32];
     __shared__ uint32_t crcs[kT / 64];
     __shared__ uint32_t sh_crc;
@@ -609,11 +644,11 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
     const uint32_t total = T.total, stored = T.stored, hb = T.hdr_bits;
     for (int i = t; i < kLit; i += kT) lit[i] = T.lit[i];
     for (int i = t; i < kDist; i += kT) dist[i] = T.dist[i];
-    crc_setup<kT, 1>(crctab, zp, zpow, t);
+    crc_setup<kT>(crctab, zp, zpow, t);
     for (uint32_t i = t; i < (total + 15) / 16; i += kT) ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     {
-        const uint32_t c = crc_global512(s, len, crctab, zp, crcs, t);
+        const uint32_t c = crc_global512x4(s, len, crctab, zp, crcs, t);
         if (t == 0) sh_crc = c;
     }
     const uint32_t bsize = total - 1;
@@ -626,10 +661,18 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
         const uint64_t lma = s0a < len ? lmask[sga] : 0, lmb = s0b < len ? lmask[sgb] : 0;
         const uint32_t nma = s0a < len ? nmatch[sga] : 0, nmb = s0b < len ? nmatch[sgb] : 0;
         const uint32_t *mpa = mlist + ((uint64_t)blockIdx.x * kMaxM) * kNSeg + t, *mpb = mpa + kT;
-        uint32_t wa[16], wb[16];
-        seg_load(s, s0a, len, wa);
-        seg_load(s, s0b, len, wb);
-        const uint32_t ca = seg_bits(wa, lma, nma, mpa, lit, dist), cb = seg_bits(wb, lmb, nmb, mpb, lit, dist);
+        // (the bytes and tokens are loaded again for the emit below -- L2 hits -- rather than held in
+        // registers across the scan)
+        uint32_t ca, cb;
+        {
+            uint32_t w[16], m[kMPre];
+            seg_load(s, s0a, len, w);
+            seg_tokens(mpa, nma, m);
+            ca = seg_bits(w, lma, nma, mpa, m, lit, dist);
+            seg_load(s, s0b, len, w);
+            seg_tokens(mpb, nmb, m);
+            cb = seg_bits(w, lmb, nmb, mpb, m, lit, dist);
+        }
         scan[t] = ca;
         scan[kT + t] = cb;
         __syncthreads();
@@ -658,8 +701,19 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
             atomicOr(img + 4 + i, v << 16);
             if (v >> 16) atomicOr(img + 5 + i, v >> 16);
         }
-        if (ca) seg_emit(wa, lma, nma, mpa, lit, dist, img, 144 + hb + scan[t]);
-        if (cb) seg_emit(wb, lmb, nmb, mpb, lit, dist, img, 144 + hb + scan[kT + t]);
+        {
+            uint32_t w[16], m[kMPre];
+            if (ca) {
+                seg_load(s, s0a, len, w);
+                seg_tokens(mpa, nma, m);
+                seg_emit(w, lma, nma, mpa, m, lit, dist, img, 144 + hb + scan[t]);
+            }
+            if (cb) {
+                seg_load(s, s0b, len, w);
+                seg_tokens(mpb, nmb, m);
+                seg_emit(w, lmb, nmb, mpb, m, lit, dist, img, 144 + hb + scan[kT + t]);
+            }
+        }
         if (t == kT - 1) {  // end of block after the last segment
             const uint32_t body_end = 144 + hb + scan[kNSeg - 1] + cb;
             LdsBits bw;

@@ -216,6 +216,29 @@ __device__ inline uint32_t crc_global512(const uint8_t *s, uint32_t len, const u
     return crc_combine512(c, len, zp, crcs, t);
 }
 
+// the same with the slice-by-4 tables (crctab[0..3]): four independent lookups per word, so a thread's
+// 32-word chain is 32 table round trips instead of 128
+__device__ inline uint32_t crc_global512x4(const uint8_t *s, uint32_t len, const uint32_t (*crctab)[256],
+                                           const uint32_t (*zp)[32], uint32_t *crcs, int t) {
+    const uint32_t lead = kSlot - len, w0 = t * 128u;
+    uint32_t c = 0;
+    if (w0 >= lead) {
+        const uint32_t d0 = w0 - lead;
+        const uintptr_t a = (uintptr_t)(s + d0);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const OGE_G uint32_t *W = (const OGE_G uint32_t *)(a & ~(uintptr_t)3);
+        uint32_t raw[33];
+#pragma unroll
+        for (int k = 0; k < 33; ++k) raw[k] = (k < 32 || sh) ? W[k] : 0u;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) c = crc_word(crctab, c ^ (sh ? __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh) : raw[i]));
+    } else if (w0 + 128 > lead) {
+        const OGE_G uint8_t *b = (const OGE_G uint8_t *)s;
+        for (uint32_t d = 0; d < w0 + 128 - lead; ++d) c = crctab[0][(c ^ b[d]) & 0xff] ^ (c >> 8);
+    }
+    return crc_combine512(c, len, zp, crcs, t);
+}
+
 // host: zero-byte operators Z_{2^k}, k = 0..16 (columns = images of the 32 basis bits)
 inline void crc_zpow(uint32_t z[17][32]) {
     for (int b = 0; b < 32; ++b) {  // one zero byte
