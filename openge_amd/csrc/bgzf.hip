@@ -237,12 +237,15 @@ __global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ s
 // handed out longest-first to the least frequent symbols.
 struct HuffScratch {
     uint16_t sorted[kLit];
-    uint32_t w[2 * kLit];
-    uint16_t parent[2 * kLit];
+    uint32_t w[2 * kLit];      // node weights, later the node depths
+    uint16_t parent[2 * kLit]; // parent node, later the pointer-jumping ancestor
     uint32_t cnt[16];
     uint32_t m;
 };
 
+// One wave, everything but the two-queue merge lane-parallel (r03: the r02 version ran the depth walk,
+// the depth counts and the length hand-out as serial lane-0 loops over LDS, one LDS round trip per step;
+// the same lengths, so the same compressed bytes).
 __device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, HuffScratch &hs) {
     const int lane = threadIdx.x;
     uint32_t m = 0;
@@ -261,48 +264,111 @@ __device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, Huff
         m += __popcll(__ballot(fi != 0));
     }
     __syncthreads();
-    if (lane == 0) {
-        if (m == 1) {
-            len[hs.sorted[0]] = 1;
-        } else if (m > 1) {
-            for (uint32_t k = 0; k < m; ++k) hs.w[k] = f[hs.sorted[k]];
-            uint32_t i = 0, j = m, nx = m;
-            for (uint32_t c = 0; c + 1 < m; ++c) {
-                uint32_t a, b;
-                if (i < m && (j >= nx || hs.w[i] <= hs.w[j])) a = i++; else a = j++;
-                if (i < m && (j >= nx || hs.w[i] <= hs.w[j])) b = i++; else b = j++;
-                hs.w[nx] = hs.w[a] + hs.w[b];
-                hs.parent[a] = (uint16_t)nx;
-                hs.parent[b] = (uint16_t)nx;
-                ++nx;
+    if (m == 0) return;
+    if (m == 1) {
+        if (lane == 0) len[hs.sorted[0]] = 1;
+        __syncthreads();
+        return;
+    }
+    for (uint32_t k = lane; k < m; k += 64) hs.w[k] = f[hs.sorted[k]];
+    __syncthreads();
+    const uint32_t root = 2 * m - 2;
+    if (lane == 0) {  // two-queue merge: the two queue heads are kept in registers, one LDS read per pick
+        uint32_t i = 0, j = m, nx = m, wi = hs.w[0], wj = 0;
+        for (uint32_t c = 0; c + 1 < m; ++c) {
+            uint32_t a, b, wa, wb;
+            if (i < m && (j >= nx || wi <= wj)) {
+                a = i, wa = wi;
+                ++i;
+                wi = i < m ? hs.w[i] : 0u;
+            } else {
+                a = j, wa = wj;
+                ++j;
+                wj = j < nx ? hs.w[j] : 0u;
             }
-            // depths, root first (w is reused for the depth)
-            const uint32_t root = 2 * m - 2;
-            hs.w[root] = 0;
-            for (int x = (int)root - 1; x >= 0; --x) hs.w[x] = hs.w[hs.parent[x]] + 1;
-            for (int b = 0; b < 16; ++b) hs.cnt[b] = 0;
-            for (uint32_t k = 0; k < m; ++k) hs.cnt[min(hs.w[k], (uint32_t)M)]++;
-            const uint32_t one = 1u << M;
-            uint32_t K = 0;
-            for (int b = 1; b <= M; ++b) K += hs.cnt[b] << (M - b);
-            while (K > one) {  // over-subscribed after clamping: lengthen the longest code < M
-                int b = M - 1;
-                while (hs.cnt[b] == 0) --b;
-                hs.cnt[b]--;
-                hs.cnt[b + 1]++;
-                K -= 1u << (M - b - 1);
+            if (i < m && (j >= nx || wi <= wj)) {
+                b = i, wb = wi;
+                ++i;
+                wi = i < m ? hs.w[i] : 0u;
+            } else {
+                b = j, wb = wj;
+                ++j;
+                wj = j < nx ? hs.w[j] : 0u;
             }
-            while (K < one) {  // under-subscribed: shorten the longest code that still fits
-                int b = M;
-                while (hs.cnt[b] == 0 || K + (1u << (M - b)) > one) --b;
-                hs.cnt[b]--;
-                hs.cnt[b - 1]++;
-                K += 1u << (M - b);
-            }
-            uint32_t k = 0;
-            for (int b = M; b >= 1; --b)
-                for (uint32_t c = 0; c < hs.cnt[b]; ++c) len[hs.sorted[k++]] = (uint8_t)b;
+            const uint32_t sw = wa + wb;
+            hs.w[nx] = sw;
+            hs.parent[a] = (uint16_t)nx;
+            hs.parent[b] = (uint16_t)nx;
+            if (j == nx) wj = sw;  // the internal queue was empty: the new node is its head
+            ++nx;
         }
+        hs.parent[root] = (uint16_t)root;
+    }
+    __syncthreads();
+    // depths by pointer jumping over the parent tree: d[x] = edges to the root (<= 10 doublings)
+    for (uint32_t x = lane; x <= root; x += 64) hs.w[x] = x == root ? 0u : 1u;
+    __syncthreads();
+    for (int round = 0; round < 10; ++round) {
+        uint32_t nd[9], na[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            const uint32_t x = lane + 64 * q;
+            nd[q] = 0, na[q] = 0;
+            if (x <= root) {
+                const uint32_t a = hs.parent[x];
+                nd[q] = hs.w[x] + (a != root ? hs.w[a] : 0u);
+                na[q] = hs.parent[a];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            const uint32_t x = lane + 64 * q;
+            if (x <= root) hs.w[x] = nd[q], hs.parent[x] = (uint16_t)na[q];
+        }
+        __syncthreads();
+    }
+    // leaves per clamped depth (ballots), Kraft repair (lane 0, <= 15 entries), lengths handed out
+    // longest-first to the least frequent symbols: rank k gets the b whose range holds k
+    if (lane < 16) hs.cnt[lane] = 0;
+    __syncthreads();
+    for (uint32_t k0 = 0; k0 < m; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const uint32_t dk = k < m ? min(hs.w[k], (uint32_t)M) : 0u;
+        for (int b = 1; b <= M; ++b) {
+            const uint32_t c = (uint32_t)__popcll(__ballot(k < m && dk == (uint32_t)b));
+            if (lane == 0 && c) hs.cnt[b] += c;
+        }
+    }
+    __syncthreads();
+    if (lane == 0) {
+        const uint32_t one = 1u << M;
+        uint32_t K = 0;
+        for (int b = 1; b <= M; ++b) K += hs.cnt[b] << (M - b);
+        while (K > one) {  // over-subscribed after clamping: lengthen the longest code < M
+            int b = M - 1;
+            while (hs.cnt[b] == 0) --b;
+            hs.cnt[b]--;
+            hs.cnt[b + 1]++;
+            K -= 1u << (M - b - 1);
+        }
+        while (K < one) {  // under-subscribed: shorten the longest code that still fits
+            int b = M;
+            while (hs.cnt[b] == 0 || K + (1u << (M - b)) > one) --b;
+            hs.cnt[b]--;
+            hs.cnt[b - 1]++;
+            K += 1u << (M - b);
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = lane; k < m; k += 64) {
+        uint32_t acc = 0, b = M;
+        for (int bb = M; bb >= 1; --bb) {  // ranks [acc, acc + cnt[bb]) get length bb
+            const uint32_t c = hs.cnt[bb];
+            if (k >= acc && k < acc + c) b = bb;
+            acc += c;
+        }
+        len[hs.sorted[k]] = (uint8_t)b;
     }
     __syncthreads();
 }

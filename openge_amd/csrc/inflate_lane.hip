@@ -198,12 +198,12 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                                                       const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
                                                       const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
                                                       uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
-                                                      uint8_t *__restrict__ scratch, uint32_t *__restrict__ err) {
+                                                      uint8_t *__restrict__ scratch, uint32_t *__restrict__ err,
+                                                      unsigned long long *__restrict__ next) {
     static_assert(LB <= 4 && TL * LB <= 32, "a step's literal batch must fit the 32 bits a refill guarantees");
     __shared__ P1Lds S;
     const uint32_t lane = threadIdx.x;
     const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
-    const uint64_t stride = (uint64_t)gridDim.x * 64;
     OGE_G uint8_t *const scr = (OGE_G uint8_t *)(scratch + gid * kScr);  // this lane's lens / long-code symbol lists
     const uintptr_t zend = (uintptr_t)z + zbytes;
 
@@ -310,8 +310,7 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
     sfor<6>([&](auto k) { T.dl[k()] = T.di[k()] = 0; });
     T.l15 = 0;
     uint32_t st = ST_NEXT, fin = 0, hlit = 0, hdist = 0, ci = 0, prev = 0, srem = 0, fixed = 0, l256 = 0;
-    uint64_t b = b0 + gid, d1bit = 0;
-    bool first = true;
+    uint64_t b = 0, d1bit = 0;
 
     auto fail = [&](uint32_t code) {
         report(err, code, b);
@@ -401,10 +400,18 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 }
             }
         }
-        // ---- next block for lanes that finished theirs
+        // ---- next block for lanes that finished theirs: taken from the launch's queue (one atomic per
+        // wave), so a lane never idles while blocks are left -- the launch ends when the queue drains,
+        // not when the slowest of a fixed block-per-lane assignment does
+        const uint64_t want = __ballot(st == ST_NEXT);
+        if (want) {
+            const uint32_t leader = (uint32_t)__builtin_ctzll(want);
+            unsigned long long q = 0;
+            if (lane == leader) q = atomicAdd(next, (unsigned long long)__popcll(want));
+            q = ((unsigned long long)__shfl((unsigned)(q >> 32), (int)leader, 64) << 32) | (unsigned)__shfl((unsigned)q, (int)leader, 64);
+            b = b0 + q + (uint64_t)__popcll(want & ((1ull << lane) - 1));
+        }
         if (st == ST_NEXT) {
-            if (!first) b += stride;
-            first = false;
             if (b >= b0 + nb) {
                 st = ST_DONE;
             } else {
@@ -773,19 +780,25 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
         return n > 0 ? n : 256;
     }();
-    // one block per lane per launch: a launch fills the 12 resident waves per CU once (a second, partial
-    // round of waves would run at a fraction of the occupancy); chunks are balanced
+    // persistent lanes (the 12 resident waves per CU) take blocks from a queue; a chunk is as many
+    // blocks as a quarter of the free device memory holds bitmaps for (8 KiB per block), at least one
+    // block per lane
     const uint64_t lanes = (uint64_t)ncu * 4 * kWps * 64;
-    const uint64_t nchunks = std::max<uint64_t>(1, (nblk + lanes - 1) / lanes);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
+    const uint64_t budget = std::max<uint64_t>(lanes, (uint64_t)(fr / 4) / (1024 * 8));
+    const uint64_t nchunks = std::max<uint64_t>(1, (nblk + budget - 1) / budget);
     const uint64_t chunk = std::max<uint64_t>(1, (nblk + nchunks - 1) / nchunks);
-    const uint64_t wgs = (chunk + 63) / 64;
+    const uint64_t wgs = std::min<uint64_t>((chunk + 63) / 64, lanes / 64);
     uint64_t *bitmap = (uint64_t *)ctx->ws("infl_bitmap", chunk * 1024 * 8);
     uint8_t *scr = (uint8_t *)ctx->ws("infl_scratch", wgs * 64 * kScr);
-    if (!bitmap || !scr) return OGE_ERR_HIP;
+    unsigned long long *next = (unsigned long long *)ctx->ws("infl_next", 8);
+    if (!bitmap || !scr || !next) return OGE_ERR_HIP;
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
         const uint64_t nb = std::min(chunk, nblk - b0);
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
-        k_infl_huff<<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err);
+        OGE_HIP_TRY(ctx, hipMemsetAsync(next, 0, 8, ctx->stream));
+        k_infl_huff<<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err, next);
         OGE_LAUNCH_CHECK(ctx);
         k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, b0, zpow, err);
         OGE_LAUNCH_CHECK(ctx);

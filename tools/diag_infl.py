@@ -1,0 +1,38 @@
+"""Diagnostic: inflate stage time of the 20M codec stream with an alternative library build (argv[1] = .so
+path; errors are reported, not raised: diagnostic builds may drop work)."""
+import ctypes as C, sys
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import numpy as np, torch
+from openge_amd import lib as L
+if len(sys.argv) > 1:
+    L.LIB_PATH = Path(sys.argv[1])
+reads = 20_000_000
+dev = torch.device("cuda", 0)
+ctx = L.Context(0)
+p = L.synth_params(reads // 2, preset="c2", seed=1234)
+n = 2 * (reads // 2)
+d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), None); ctx.sync()
+B = int(d_offs[-1].item())
+d_recs = torch.empty(B + 64, dtype=torch.uint8, device=dev)
+ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), d_recs.data_ptr()); ctx.sync()
+cap = int(L.lib().oge_bgzf_bound(B))
+d_z = torch.empty(cap, dtype=torch.uint8, device=dev)
+zb = ctx.bgzf_deflate_dev(d_recs.data_ptr(), B, 6, d_z.data_ptr(), cap)
+zh = d_z[:zb].cpu().numpy()
+nb = C.c_uint64()
+L.lib().oge_bgzf_index(zh.ctypes.data, zb, None, None, None, None, 0, C.byref(nb))
+k = nb.value
+idx = np.zeros(3 * k + 1, dtype=np.uint64); crc = np.zeros(k, dtype=np.uint32)
+i0 = idx.ctypes.data
+L.check(L.lib().oge_bgzf_index(zh.ctypes.data, zb, i0, i0 + 8 * k, i0 + 16 * k, crc.ctypes.data, k, C.byref(nb)))
+d_idx = torch.from_numpy(idx.view(np.int64)).to(dev); d_crc = torch.from_numpy(crc.view(np.int32)).to(dev)
+d_back = torch.zeros(B + 64, dtype=torch.uint8, device=dev)
+torch.cuda.synchronize()
+ms = []
+for _ in range(4):
+    p0 = d_idx.data_ptr()
+    rc = L.lib().oge_bgzf_inflate_dev(ctx.h, d_z.data_ptr(), zb, p0, p0 + 8 * k, p0 + 16 * k, d_crc.data_ptr(), k, d_back.data_ptr())
+    ms.append(round(ctx.timing("bgzf_inflate"), 2))
+print(sys.argv[1:] or ["default"], "inflate ms", ms[1:], "rc", rc, flush=True)
