@@ -96,6 +96,19 @@ __device__ void crc_setup(uint32_t (*crctab)[256], uint32_t (*zp)[32], const uin
     for (int i = t; i < 17 * 32; i += NT) zp[i >> 5][i & 31] = zpow[i];
 }
 
+// The 0xffffffff preset carried over len zero bytes: Z_len(0xffffffff) from the 2^k operators, one GF(2)
+// matrix-vector product per set bit of len (each 32 dependent LDS reads) -- except for the 65,280-byte
+// payload of every full BGZF block, whose value is a constant (python: 32-bit CRC register 0xffffffff
+// stepped over 65,280 zero bytes, reflected polynomial 0xEDB88320).
+constexpr uint32_t kPresetFull = 0x012c2d38u;
+__device__ __forceinline__ uint32_t crc_preset(uint32_t len, const uint32_t (*zp)[32]) {
+    if (len == kPay) return kPresetFull;
+    uint32_t r = 0xffffffffu;
+    for (int k = 0; k < 17; ++k)
+        if ((len >> k) & 1) r = crc_mat(zp[k], r);
+    return r;
+}
+
 // CRC-32 of a payload of len (<= 65536) bytes with 512 threads; the result is valid in thread 0.
 // The data is right-aligned in a 65536-byte window (leading zeros leave a zero register unchanged);
 // thread t owns window bytes [128t, 128t + 128) and passes the CRC of its piece (zero register start) to
@@ -123,9 +136,7 @@ __device__ inline uint32_t crc_combine512(uint32_t c, uint32_t len, const uint32
             const uint32_t o = __shfl_down(c, 1u << lv, 64);
             if (!(t & ((2u << lv) - 1))) c = crc_mat(zp[13 + lv], c) ^ o;
         }
-        if (t == 0)
-            for (int k = 0; k < 17; ++k)
-                if ((len >> k) & 1) r = crc_mat(zp[k], r);
+        if (t == 0) r = crc_preset(len, zp);
     }
     return ~(r ^ c);
 }
@@ -149,9 +160,7 @@ __device__ inline uint32_t crc_combine1024(uint32_t c, uint32_t len, const uint3
             const uint32_t o = __shfl_down(c, 1u << lv, 64);
             if (!(t & ((2u << lv) - 1))) c = crc_mat(zp[12 + lv], c) ^ o;
         }
-        if (t == 0)
-            for (int k = 0; k < 17; ++k)
-                if ((len >> k) & 1) r = crc_mat(zp[k], r);
+        if (t == 0) r = crc_preset(len, zp);
     }
     return ~(r ^ c);
 }
