@@ -143,7 +143,9 @@ __global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ s
         const uint32_t end = min(len, base + kSub);
         // candidates, one round of kR * kT consecutive positions at a time
         for (uint32_t r = base; r < end; r += kR * kT) {
-            uint32_t hh[kR];
+            // the kR lookup chains (prefix word -> bucket -> candidate's word) of a thread run side by side;
+            // the ballots come after all of them (a ballot between them would serialise the chains)
+            uint32_t hh[kR], cc[kR];
 #pragma unroll
             for (int k = 0; k < kR; ++k) {
                 const uint32_t p = r + k * kT + t;
@@ -155,6 +157,11 @@ __global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ s
                     if (j1 && p - (j1 - 1) <= 32768 && ld32(in, j1 - 1) == w) c = j1;
                 }
                 hh[k] = h;
+                cc[k] = c;
+            }
+#pragma unroll
+            for (int k = 0; k < kR; ++k) {
+                const uint32_t p = r + k * kT + t, c = cc[k];
                 const uint64_t m = __ballot(c != 0 && p < end);
                 if (p < end) cand[p - base] = (uint16_t)c;
                 if (lane == 0 && r + k * kT + 64 * wv < end) cmask[(r + k * kT + 64 * wv - base) >> 6] = m;
