@@ -177,7 +177,8 @@ def roofline_entry(stage: str, info: tuple, t_ms: float, B: int) -> dict:
 
 
 # --------------------------------------------------------------------------------------------- legs
-def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1, cpu_threads: int = 0) -> dict | None:
+def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1, cpu_threads: int = 0,
+                dump_dir: str | None = None) -> dict | None:
     """configs[4]: openge localrealign on the C5 synthetic set (50k indel intervals, 24 contigs).
     Host phases (binning, consensus generation, decisions, mate fixing) + the HIP offset scan; the
     records are decoded in host memory before the timed region (the module's input queue).  With
@@ -198,7 +199,9 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1, cpu_thread
         lo, hi = RS.contig_slices(b.recs, offs, b.n, ref_lens, world)[rank]
         run = lambda: RS.localrealign_slice(ctx, b.header_text, b.recs, offs, lo, hi, fa, iv, opts,
                                             last=(rank == world - 1))
-        run()  # warm-up (first-touch, kernel load)
+        w_out, w_oo, _ = run()  # warm-up (first-touch, kernel load)
+        if dump_dir:  # this rank's realigned records (tests concatenate the ranks' parts)
+            Path(dump_dir, f"realign_{rank}.bin").write_bytes(np.asarray(w_out[:int(w_oo[-1])]).tobytes())
         ref_cpu = None
         if world == 1 and cpu_threads:  # the reference's own realigner on the same files, this box's host
             ref_cpu = cpu_baseline_realign(fa, iv, bam, n_intervals, cpu_threads, td)
@@ -394,7 +397,8 @@ def main():
 
     if args.realign_only:
         print(json.dumps(realign_leg(ctx, args.realign_intervals,
-                                     cpu_threads=0 if args.no_cpu_baseline else args.cpu_threads)), flush=True)
+                                     cpu_threads=0 if args.no_cpu_baseline else args.cpu_threads,
+                                     dump_dir=args.dump_dir)), flush=True)
         ctx.close()
         return
 
@@ -532,6 +536,23 @@ DIST_STAGES = ["bgzf_index", "bgzf_inflate", "rec_walk", "dist_split", "dist_exc
                "gather_offsets", "gather_records", "bgzf_deflate"]
 
 
+def exchange_summary(per_rank: list) -> dict:
+    """The last step's collectives (oge_comm_stats_json of every rank): per tag, bytes that crossed
+    between ranks (sum over ranks of bytes sent), bytes kept on their rank, calls, and the slowest
+    rank's time (host wall time of the collective calls, waiting for peers included), plus each rank's
+    own list."""
+    tags: dict = {}
+    for r in per_rank:
+        for x in r["exchanges"]:
+            t = tags.setdefault(x["tag"], {"calls": x["calls"], "bytes_between_ranks": 0, "bytes_kept": 0, "max_ms": 0.0})
+            t["bytes_between_ranks"] += x["bytes_sent"]
+            t["bytes_kept"] += x["bytes_self"]
+            t["max_ms"] = round(max(t["max_ms"], x["ms"]), 3)
+    return {"by_tag": tags, "per_rank": [r["exchanges"] for r in per_rank],
+            "what": "last timed step; bytes_between_ranks = sum over ranks of bytes sent to other ranks; "
+                    "ms = host wall time of the tag's collectives on a rank (peers' skew included)"}
+
+
 def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
     """N ranks, one process per GPU, RCCL over xGMI through the library's own communicator
     (oge_comm_init_rank; torch.distributed only bootstraps it and times the steps, on gloo).  Rank g
@@ -589,6 +610,11 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
     dt = float(t.item())
     sizes = [None] * world
     dist.all_gather_object(sizes, (n, ob))
+    # per-rank record of the last step: every exchange's bytes and time, every stage's time
+    K = args.steps
+    mine = {"exchanges": comm.exchange_stats(), "stages_ms": {k: round(v / K, 3) for k, v in tot.items()}}
+    per_rank = [None] * world
+    dist.all_gather_object(per_rank, mine)
     assert nr == n_all, (nr, n_all)
     transport = comm.transport
     if args.dump_dir:  # this rank's slice of the output file (valid until the rank's next call)
@@ -601,9 +627,8 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
     torch.cuda.empty_cache()
     realign_multi = None
     if not args.no_realign:
-        realign_multi = realign_leg(ctx, args.realign_intervals, rank, world)
+        realign_multi = realign_leg(ctx, args.realign_intervals, rank, world, dump_dir=args.dump_dir)
     if rank == 0:
-        K = args.steps
         out = {"metric": METRIC, "value": round(n_all * K / dt / 1e6, 2), "unit": "Mreads/s", "n_gpus": world,
                "steps": K, "warmup": args.warmup, "ms_per_step": round(dt / K * 1e3, 2), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "u8",
@@ -616,7 +641,9 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
                           "rank_reads_and_output_bytes": sizes,
                           "parallelism": f"{world} ranks (one process per GPU), all-to-all via oge_comm_init_rank",
                           "transport": transport},
-               "stages_ms_rank0": {k: round(v / K, 3) for k, v in tot.items()}}
+               "stages_ms_rank0": {k: round(v / K, 3) for k, v in tot.items()},
+               "stages_ms_per_rank": [r["stages_ms"] for r in per_rank],
+               "exchanges": exchange_summary(per_rank)}
         if realign_multi is not None:
             out["realign"] = realign_multi
         print(json.dumps(out), flush=True)

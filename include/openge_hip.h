@@ -197,6 +197,17 @@ int oge_comm_unique_id(uint8_t *id_out, uint64_t bytes);
  * process sees >= nranks devices, else compares the ranks' PCI bus ids in the shared segment
  * (OGE_COMM_DIR, default /dev/shm or /tmp; OGE_COMM_STAGE_MB per-rank staging, default 32). */
 int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, oge_comm **out);
+/* The same with the transport chosen by the caller (mode "auto" | "rccl" | "host"; NULL = OGE_COMM).
+ * In auto mode with fewer visible devices than ranks, the shared-segment meeting is tried only when
+ * the launcher says every rank is on this node (LOCAL_WORLD_SIZE / OMPI_COMM_WORLD_LOCAL_SIZE /
+ * MPI_LOCALNRANKS == nranks); otherwise RCCL, the only transport that reaches other hosts.  The CLI,
+ * whose ranks are threads of one process, passes "host" when they share a device. */
+int oge_comm_init_rank_mode(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, const char *mode, oge_comm **out);
+/* Per-exchange record of the communicator's last oge_sort_markdup_dist / oge_mergesort_bgzf_dist call:
+ * a JSON array of {tag, calls, bytes_sent, bytes_recv, bytes_self, ms} (bytes to / from other ranks and
+ * kept on this rank; host wall time of the collectives, waiting for peers included).  Returns the JSON
+ * length; writes it (NUL-terminated) when cap > length. */
+int64_t oge_comm_stats_json(const oge_comm *comm, char *buf, uint64_t cap);
 /* One process, n contexts in one call (test harness): RCCL when the contexts' devices are distinct,
  * else (or with OGE_COMM=local) an in-process hub of device-to-device copies.  out[0..n) receives one
  * communicator per context.  The CLI uses oge_comm_init_rank from one thread per rank instead. */

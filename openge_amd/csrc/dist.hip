@@ -38,6 +38,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <random>
 #include <cstdio>
 #include <cstdlib>
@@ -65,9 +66,66 @@ struct OgeTransport {
     virtual int reduce_scatter_max_u8(oge_ctx *ctx, const uint8_t *in, uint8_t *out, size_t chunk) = 0;
 };
 
+// One exchange site of a step: bytes this rank sent to / received from other ranks (and kept), and the
+// host wall time of its collectives (a transport call returns when its data is complete on this rank, so
+// the time includes waiting for the slowest peer).  `calls` collectives were made under the tag.
+struct OgeXchg {
+    std::string tag;
+    uint64_t sent = 0, recv = 0, self = 0, calls = 0;
+    double ms = 0;
+};
+
 struct oge_comm {
     oge_ctx *ctx = nullptr;
     std::unique_ptr<OgeTransport> tr;
+    std::vector<OgeXchg> stats;  // since the last oge_sort_markdup_dist / oge_mergesort_bgzf_dist call
+    OgeXchg &stat(const char *tag) {
+        for (auto &x : stats)
+            if (x.tag == tag) return x;
+        stats.push_back(OgeXchg());
+        stats.back().tag = tag;
+        return stats.back();
+    }
+    // the collectives, recorded per tag
+    int alltoallv(const char *tag, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
+                  const uint64_t *rbytes, const uint64_t *roff) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = tr->alltoallv(ctx, send, sbytes, soff, recv, rbytes, roff);
+        OgeXchg &x = stat(tag);
+        x.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        x.calls++;
+        for (int p = 0; p < tr->size; ++p) {
+            if (p == tr->rank) {
+                x.self += sbytes[p];
+            } else {
+                x.sent += sbytes[p];
+                x.recv += rbytes[p];
+            }
+        }
+        return rc;
+    }
+    int allgather_host(const char *tag, const void *in, void *out, size_t bytes) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = tr->allgather_host(ctx, in, out, bytes);
+        OgeXchg &x = stat(tag);
+        x.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        x.calls++;
+        x.sent += bytes * (tr->size - 1);
+        x.recv += bytes * (tr->size - 1);
+        x.self += bytes;
+        return rc;
+    }
+    int reduce_scatter_max_u8(const char *tag, const uint8_t *in, uint8_t *out, size_t chunk) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = tr->reduce_scatter_max_u8(ctx, in, out, chunk);
+        OgeXchg &x = stat(tag);
+        x.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        x.calls++;
+        x.sent += chunk * (tr->size - 1);
+        x.recv += chunk * (tr->size - 1);
+        x.self += chunk;
+        return rc;
+    }
 };
 
 namespace {
@@ -333,7 +391,7 @@ struct Dist {
 
     int agree(int rc) {  // every rank learns whether any rank failed; keeps the collectives in step
         std::vector<int> all(G);
-        int r2 = comm->tr->allgather_host(ctx, &rc, all.data(), sizeof(int));
+        int r2 = comm->allgather_host("status", &rc, all.data(), sizeof(int));
         if (r2) return r2;
         for (int g = 0; g < G; ++g)
             if (all[g]) return rc ? rc : oge_fail(ctx, OGE_ERR_HIP, ("multi-GPU: rank " + std::to_string(g) + " failed").c_str());
@@ -371,14 +429,14 @@ struct Dist {
     // exchange plan for per-destination element counts
     int plan(const std::vector<uint64_t> &cnt, oge_dist::Plan *p) {
         std::vector<uint64_t> all((size_t)G * G);
-        int rc = comm->tr->allgather_host(ctx, cnt.data(), all.data(), G * 8);
+        int rc = comm->allgather_host("plans", cnt.data(), all.data(), G * 8);
         if (rc) return rc;
         *p = oge_dist::plan_from_counts(all, G, rank);
         return OGE_OK;
     }
 
     // all-to-all of `elem`-byte elements laid out by the plan
-    int a2a(const oge_dist::Plan &p, size_t elem, const void *send, void *recv) {
+    int a2a(const char *tag, const oge_dist::Plan &p, size_t elem, const void *send, void *recv) {
         std::vector<uint64_t> sb(G), so(G), rb(G), ro(G);
         for (int g = 0; g < G; ++g) {
             sb[g] = p.scnt[g] * elem;
@@ -386,7 +444,7 @@ struct Dist {
             rb[g] = p.rcnt[g] * elem;
             ro[g] = p.roff[g] * elem;
         }
-        return comm->tr->alltoallv(ctx, send, sb.data(), so.data(), recv, rb.data(), ro.data());
+        return comm->alltoallv(tag, send, sb.data(), so.data(), recv, rb.data(), ro.data());
     }
 
     template <int W>
@@ -435,8 +493,8 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     std::vector<uint64_t> allsamp((size_t)G * oge_dist::kSamples), alln(G);
     const uint64_t mm[2] = {n, m};
     std::vector<uint64_t> allmm(2 * G);
-    if ((rc = comm->tr->allgather_host(ctx, hs.data(), allsamp.data(), oge_dist::kSamples * 8))) return rc;
-    if ((rc = comm->tr->allgather_host(ctx, mm, allmm.data(), 16))) return rc;
+    if ((rc = comm->allgather_host("splitter_samples", hs.data(), allsamp.data(), oge_dist::kSamples * 8))) return rc;
+    if ((rc = comm->allgather_host("splitter_samples", mm, allmm.data(), 16))) return rc;
     std::vector<std::vector<uint64_t>> per(G);
     for (int g = 0; g < G; ++g) {
         alln[g] = allmm[2 * g];
@@ -501,8 +559,8 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     if (!rbuf || !rsz || !roff) rc = OGE_ERR_HIP;
     if ((rc = D.agree(rc))) return rc;
     // every rank makes both exchanges; a failure goes to the agree() below, never straight out
-    rc = D.a2a(pb, 1, sbuf, rbuf);
-    if (const int r2 = D.a2a(pr, 4, ssz, rsz)) rc = rc ? rc : r2;
+    rc = D.a2a("records", pb, 1, sbuf, rbuf);
+    if (const int r2 = D.a2a("record_sizes", pr, 4, ssz, rsz)) rc = rc ? rc : r2;
     if (!rc) {
         hipLaunchKernelGGL(k_off_from_u32, dim3(oge_ceil_div(R + 1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)rsz, R, roff);
         rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
@@ -589,7 +647,7 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
 
     // ---- 3. dedup: global indices
     std::vector<uint64_t> allR(G);
-    if ((rc = comm->tr->allgather_host(ctx, &R, allR.data(), 8))) return rc;
+    if ((rc = comm->allgather_host("plans", &R, allR.data(), 8))) return rc;
     uint64_t stride = 1, Ntot = 0;
     for (int g = 0; g < G; ++g) stride = std::max<uint64_t>(stride, allR[g]), Ntot += allR[g];
     if ((uint64_t)G * stride > 0xFFFFFFFFull)
@@ -642,8 +700,8 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
         uint32_t *fvr = (uint32_t *)ctx->ws("dist_fvr", (pf.rtot + 1) * 4);
         if (!fkr || !fvr) rc = OGE_ERR_HIP;
         if ((rc = D.agree(rc))) return rc;
-        rc = D.a2a(pf, 8, fks, fkr);
-        if (const int r2 = D.a2a(pf, 4, fvs, fvr)) rc = rc ? rc : r2;
+        rc = D.a2a("fragments", pf, 8, fks, fkr);
+        if (const int r2 = D.a2a("fragments", pf, 4, fvs, fvr)) rc = rc ? rc : r2;
         if (!rc) rc = oge_md_frag_groups(ctx, fkr, fvr, pf.rtot, dup_pad);
         if ((rc = D.agree(rc))) return rc;
     }
@@ -716,9 +774,9 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
         if (!cmr || !cgr || !mrr || !rco || !rbo) rc = OGE_ERR_HIP;
         if ((rc = D.agree(rc))) return rc;
         uint8_t *mrec = (uint8_t *)ctx->ws("dist_mrec", 64);
-        rc = D.a2a(pc, sizeof(RecMeta), cms, cmr);
-        if (const int r2 = D.a2a(pc, 4, cgs, cgr)) rc = rc ? rc : r2;
-        if (const int r3 = D.a2a(pm, 1, mrec, mrr)) rc = rc ? rc : r3;
+        rc = D.a2a("matejoin_candidates", pc, sizeof(RecMeta), cms, cmr);
+        if (const int r2 = D.a2a("matejoin_candidates", pc, 4, cgs, cgr)) rc = rc ? rc : r2;
+        if (const int r3 = D.a2a("matejoin_minirecs", pm, 1, mrec, mrr)) rc = rc ? rc : r3;
         if (!rc && nr) {
             if (hipMemcpyAsync(rco, pc.roff.data(), 8 * (G + 1), hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
                 hipMemcpyAsync(rbo, pm.roff.data(), 8 * (G + 1), hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
@@ -774,9 +832,9 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
         Q.idx = (uint2 *)ctx->ws("dist_ridx", (pp.rtot + 1) * 8);
         if (!Q.hi || !Q.lo || !Q.idx) rc = OGE_ERR_HIP;
         if ((rc = D.agree(rc))) return rc;
-        rc = D.a2a(pp, 8, shi, Q.hi);
-        if (const int r2 = D.a2a(pp, 8, slo, Q.lo)) rc = rc ? rc : r2;
-        if (const int r3 = D.a2a(pp, 8, sidx, Q.idx)) rc = rc ? rc : r3;
+        rc = D.a2a("pair_ends", pp, 8, shi, Q.hi);
+        if (const int r2 = D.a2a("pair_ends", pp, 8, slo, Q.lo)) rc = rc ? rc : r2;
+        if (const int r3 = D.a2a("pair_ends", pp, 8, sidx, Q.idx)) rc = rc ? rc : r3;
         if (!rc) rc = oge_md_pairs_rehash(ctx, &Q);
         if (!rc) rc = oge_md_pair_groups(ctx, opts, Q, dup_pad);
         if ((rc = D.agree(rc))) return rc;
@@ -785,7 +843,7 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
 
     // ---- dup marks meet; 4. apply + gather
     t = ctx->begin_stage("dist_reduce");
-    rc = comm->tr->reduce_scatter_max_u8(ctx, dup_pad, dup, stride);
+    rc = comm->reduce_scatter_max_u8("dup_marks", dup_pad, dup, stride);
     ctx->end_stage(t);
     t = ctx->begin_stage("md_apply");
     uint64_t nd = 0;
@@ -795,7 +853,7 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
     if (!rc) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
     if ((rc = D.agree(rc))) return rc;
     std::vector<uint64_t> alld(G);
-    if ((rc = comm->tr->allgather_host(ctx, &nd, alld.data(), 8))) return rc;
+    if ((rc = comm->allgather_host("status", &nd, alld.data(), 8))) return rc;
     uint64_t tot = 0;
     for (uint64_t x : alld) tot += x;
     *d_out = out;
@@ -810,7 +868,7 @@ oge_ctx *oge_comm_ctx(oge_comm *comm) { return comm ? comm->ctx : nullptr; }
 int oge_comm_sum_u64(oge_comm *comm, uint64_t *v, int count) {
     const int G = comm->tr->size;
     std::vector<uint64_t> all((size_t)G * count);
-    const int rc = comm->tr->allgather_host(comm->ctx, v, all.data(), 8 * (size_t)count);
+    const int rc = comm->allgather_host("status", v, all.data(), 8 * (size_t)count);
     if (rc) return rc;
     for (int k = 0; k < count; ++k) {
         v[k] = 0;
@@ -841,16 +899,29 @@ int oge_comm_unique_id(uint8_t *id_out, uint64_t bytes) {
 
 uint64_t oge_comm_unique_id_bytes(void) { return sizeof(ncclUniqueId) + kIdNonce; }
 
-// Transport of one rank (OGE_COMM = rccl | host | auto, default auto): RCCL when the ranks' devices are
-// distinct, the host-staged transport (dist_shm.h) when ranks share one.  auto: a process that sees at
-// least `nranks` devices takes RCCL at once (bench.py / the CLI give rank r device r % count); with fewer
-// visible devices than ranks the ranks meet in the shared segment named by the id and compare their
-// devices' PCI bus ids -- all distinct (e.g. one visible device per process) -> RCCL, else host.
-int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, oge_comm **out) {
+// Number of ranks the launcher placed on this node, when it says (torchrun LOCAL_WORLD_SIZE, Open MPI,
+// MPICH / Hydra); 0 = unknown.
+static int launcher_local_ranks() {
+    for (const char *v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"}) {
+        const char *e = getenv(v);
+        if (e && *e) return atoi(e);
+    }
+    return 0;
+}
+
+// Transport of one rank.  mode: "rccl", "host" or "auto" (nullptr / "": OGE_COMM, default auto).  RCCL
+// between distinct GPUs, the host-staged transport (dist_shm.h) when ranks share one.  auto: a process
+// that sees at least `nranks` devices takes RCCL at once (bench.py / the CLI give rank r device r %
+// count).  With fewer visible devices than ranks, the shared-segment meeting (which compares the ranks'
+// PCI bus ids: all distinct -> RCCL, else host) is only tried when every rank is known to be on this
+// node -- the launcher's local rank count equals nranks (torchrun's LOCAL_WORLD_SIZE, ...), or the caller
+// runs every rank itself (the CLI's threads pass "host"); otherwise (a multi-node job, 2 x 8 GPUs with a
+// device-isolating launcher) RCCL, which is the only transport that reaches other hosts.
+static int comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, const char *want, oge_comm **out) {
     if (!ctx || !id || !out || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
         return oge_fail(ctx, OGE_ERR_ARG, "oge_comm_init_rank: bad arguments");
     (void)hipSetDevice(ctx->device);
-    const char *e = getenv("OGE_COMM");
+    const char *e = want && *want ? want : getenv("OGE_COMM");
     std::string mode = e && *e ? e : "auto";
     if (mode == "local") mode = "host";  // oge_comm_init's in-process name for "ranks share a GPU"
     if (mode != "auto" && mode != "rccl" && mode != "host")
@@ -858,7 +929,8 @@ int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, og
     int ndev = 0;
     (void)hipGetDeviceCount(&ndev);
     std::unique_ptr<oge_dist::ShmSeg> seg;
-    if (mode == "host" || (mode == "auto" && ndev < nranks)) {
+    const bool one_node = launcher_local_ranks() == nranks;
+    if (mode == "host" || (mode == "auto" && ndev < nranks && one_node)) {
         char bus[64] = {0};
         (void)hipDeviceGetPCIBusId(bus, sizeof bus - 1, ctx->device);
         uint64_t h = 1469598103934665603ull;  // FNV-1a of the whole id names the meeting
@@ -867,7 +939,10 @@ int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, og
         snprintf(name, sizeof name, "oge_comm_%016llx", (unsigned long long)h);
         std::string err;
         seg.reset(oge_dist::ShmSeg::open(name, nranks, rank, oge_dist::ShmSeg::default_stage_bytes(), bus, &err));
-        if (!seg) return oge_fail(ctx, OGE_ERR_HIP, err.c_str());
+        if (!seg) {
+            err += " (the host transport meets node-local ranks only: a job spanning several hosts needs OGE_COMM=rccl)";
+            return oge_fail(ctx, OGE_ERR_HIP, err.c_str());
+        }
         bool shared = false;
         for (int a = 0; a < nranks; ++a)
             for (int b = a + 1; b < nranks; ++b) shared = shared || !strcmp(seg->post(a).bus, seg->post(b).bus);
@@ -896,6 +971,14 @@ int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, og
     }
     *out = c;
     return OGE_OK;
+}
+
+int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, oge_comm **out) {
+    return comm_init_rank(ctx, nranks, rank, id, nullptr, out);
+}
+
+int oge_comm_init_rank_mode(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, const char *mode, oge_comm **out) {
+    return comm_init_rank(ctx, nranks, rank, id, mode, out);
 }
 
 int oge_comm_init(oge_ctx **ctxs, int n, oge_comm **out) {
@@ -943,6 +1026,22 @@ int oge_comm_rank(const oge_comm *c) { return c ? c->tr->rank : -1; }
 int oge_comm_size(const oge_comm *c) { return c ? c->tr->size : -1; }
 const char *oge_comm_transport(const oge_comm *c) { return c ? c->tr->name() : ""; }
 
+int64_t oge_comm_stats_json(const oge_comm *c, char *buf, uint64_t cap) {
+    if (!c) return -1;
+    std::string j = "[";
+    char tmp[256];
+    for (size_t i = 0; i < c->stats.size(); ++i) {
+        const OgeXchg &x = c->stats[i];
+        snprintf(tmp, sizeof tmp, "%s{\"tag\":\"%s\",\"calls\":%llu,\"bytes_sent\":%llu,\"bytes_recv\":%llu,\"bytes_self\":%llu,\"ms\":%.3f}",
+                 i ? "," : "", x.tag.c_str(), (unsigned long long)x.calls, (unsigned long long)x.sent, (unsigned long long)x.recv,
+                 (unsigned long long)x.self, x.ms);
+        j += tmp;
+    }
+    j += "]";
+    if (buf && cap > j.size()) memcpy(buf, j.c_str(), j.size() + 1);
+    return (int64_t)j.size();
+}
+
 int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref, int sort,
                           const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
                           uint64_t *n_dup_total) {
@@ -951,6 +1050,7 @@ int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t 
     oge_ctx *ctx = comm->ctx;
     (void)hipSetDevice(ctx->device);
     ctx->reset_timing();
+    comm->stats.clear();
     if (opts && opts->n_ref != n_ref) return oge_fail(ctx, OGE_ERR_ARG, "oge_sort_markdup_dist: opts->n_ref differs from n_ref");
     return dist_run(comm, d_recs, d_off, n, n_ref, sort, opts, d_out, d_out_off, n_out, n_dup_total);
 }

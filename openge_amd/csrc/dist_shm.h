@@ -17,6 +17,8 @@
 #pragma once
 #include <fcntl.h>
 #include <sched.h>
+#include <signal.h>
+#include <cerrno>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/statvfs.h>
@@ -82,10 +84,13 @@ public:
         const long mb = e && *e ? atol(e) : 32;
         return (uint64_t)std::min<long>(std::max<long>(mb, 1), 4096) << 20;
     }
+    // A wait ends early when a peer process is gone (its posted pid no longer exists); the wall-clock
+    // limit (OGE_COMM_TIMEOUT, default 1800 s) is only the backstop for a live peer that never arrives,
+    // so a slow rank (a larger input, a GPU under contention) does not break the communicator.
     static double timeout_s() {
         const char *e = getenv("OGE_COMM_TIMEOUT");
-        const double t = e && *e ? atof(e) : 300.0;
-        return t > 0 ? t : 300.0;
+        const double t = e && *e ? atof(e) : 1800.0;
+        return t > 0 ? t : 1800.0;
     }
 
     // Every rank calls open with the same name; returns after all G ranks have joined (or nullptr on a
@@ -178,7 +183,15 @@ private:
         }
         std::this_thread::sleep_for(std::chrono::microseconds(50));
         if ((it & 1023) != 0) return false;
+        if (peer_gone()) return true;
         return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s();
+    }
+    bool peer_gone() const {  // a rank that posted its pid and whose process has exited
+        for (int r = 0; r < G_; ++r) {
+            const int64_t pid = ctl_->post[r].pid;
+            if (pid > 0 && kill((pid_t)pid, 0) != 0 && errno == ESRCH) return true;
+        }
+        return false;
     }
 
     int G_ = 0, rank_ = 0;
@@ -199,6 +212,12 @@ template <class Ops>
 struct ShmColl {
     ShmSeg &seg;
     Ops &ops;
+
+    // wait for every copy queued so far, whatever happened before; rc keeps the first error
+    void drain(int &rc) {
+        const int s = ops.sync();
+        if (!rc) rc = s;
+    }
 
     // device buffers: rank r's bytes for rank p are send + soff[p], sbytes[p]; they land at recv + roff[r]
     // of rank p.  0 = ok, -1 = this rank's copies failed or the byte counts disagree, -2 = the protocol
@@ -227,16 +246,16 @@ struct ShmColl {
                 const uint64_t n = p == r ? 0 : shm_part(sbytes[p], k, S);
                 if (n) rc = ops.d2h(seg.slot(r, p), (const uint8_t *)send + soff[p] + k * S, n);
             }
-            if (!rc) rc = ops.sync();  // the slot is filled before the peers read it
+            drain(rc);  // the slot is filled before the peers read it (always: no copy outlives its round)
             if (seg.barrier()) return -2;
             for (int p = 0; p < G && !rc; ++p) {
                 const uint64_t n = p == r ? 0 : shm_part(rbytes[p], k, S);
                 if (n) rc = ops.h2d((uint8_t *)recv + roff[p] + k * S, seg.slot(p, r), n);
             }
-            if (!rc) rc = ops.sync();  // read out before the sender refills the slot
+            drain(rc);  // read out before the sender refills the slot
             if (seg.barrier()) return -2;
         }
-        if (!rc) rc = ops.sync();
+        drain(rc);
         if (seg.barrier()) return -2;  // every rank has read the posts before the next collective rewrites them
         return rc;
     }
@@ -265,7 +284,7 @@ struct ShmColl {
         for (uint64_t k = 0; k * S < chunk; ++k) {
             const uint64_t n = shm_part(chunk, k, S);
             for (int p = 0; p < G && !rc; ++p) rc = ops.d2h(seg.slot(r, p), in + (size_t)p * chunk + k * S, n);
-            if (!rc) rc = ops.sync();
+            drain(rc);
             if (seg.barrier()) return -2;
             if (!rc) {
                 memcpy(acc.data(), seg.slot(0, r), n);
@@ -274,8 +293,8 @@ struct ShmColl {
                     for (uint64_t i = 0; i < n; ++i) acc[i] = std::max(acc[i], s[i]);
                 }
                 rc = ops.h2d(out + k * S, acc.data(), n);
-                if (!rc) rc = ops.sync();
             }
+            drain(rc);  // acc and the slots are reused next round
             if (seg.barrier()) return -2;
         }
         return rc;

@@ -444,7 +444,12 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 sfor<4>([&](auto k) { L += (c15 >= (T.ll[k()] & 0xffff)) + (c15 >= (T.ll[k()] >> 16)); });
                 const uint32_t lie = pick(T.lie, L - 7);
                 const uint32_t k = ((lie & 0xffff) + (c15 >> (15 - L))) & 0xffff;
+#if OGE_EXP == 1  // timing experiment: a long literal's byte is not looked up (wrong output, same bit stream)
+                if (k < (lie >> 16)) sym = k & 255;
+                else sym = scr[S_LS + min(k, 287u)] + 256u;
+#else
                 sym = scr[S_LS + min(k, 287u)] + (k >= (lie >> 16) ? 256u : 0u);
+#endif
                 if (L == 15 && c15 >= T.l15) sym = 512;  // no such code
             }
             skip(L);
@@ -780,13 +785,14 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
         return n > 0 ? n : 256;
     }();
-    // persistent lanes (the 12 resident waves per CU) take blocks from a queue; a chunk is as many
-    // blocks as a quarter of the free device memory holds bitmaps for (8 KiB per block), at least one
-    // block per lane
+    // persistent lanes (the 12 resident waves per CU) take blocks from a queue; a chunk is at most 4
+    // blocks per lane (the queue keeps the lanes busy, so a larger chunk gains nothing: 300M reads = 2
+    // launches, a 6.4 GB bitmap workspace that lives as long as the context), and no more than a
+    // quarter of the free device memory holds bitmaps for (8 KiB per block), at least one block per lane
     const uint64_t lanes = (uint64_t)ncu * 4 * kWps * 64;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
-    const uint64_t budget = std::max<uint64_t>(lanes, (uint64_t)(fr / 4) / (1024 * 8));
+    const uint64_t budget = std::max<uint64_t>(lanes, std::min<uint64_t>(4 * lanes, (uint64_t)(fr / 4) / (1024 * 8)));
     const uint64_t nchunks = std::max<uint64_t>(1, (nblk + budget - 1) / budget);
     const uint64_t chunk = std::max<uint64_t>(1, (nblk + nchunks - 1) / nchunks);
     const uint64_t wgs = std::min<uint64_t>((chunk + 63) / 64, lanes / 64);

@@ -88,7 +88,9 @@ int ChainContext::init_ranks() {
         std::vector<std::thread> ts;
         for (int g = 0; g < gpus; ++g)
             ts.emplace_back([&, g]() {
-                rcs[g] = oge_comm_init_rank(rank_ctx[g], gpus, g, id.data(), &comms[g]);
+                // every rank is a thread of this process: the shared-segment meeting is node-local by
+                // construction, so ranks sharing a device take the host transport
+                rcs[g] = oge_comm_init_rank_mode(rank_ctx[g], gpus, g, id.data(), gpus > ndev ? "host" : nullptr, &comms[g]);
                 if (rcs[g]) why[g] = oge_last_error(rank_ctx[g]);
             });
         for (auto &t : ts) t.join();

@@ -218,6 +218,8 @@ def lib() -> C.CDLL:
         "oge_comm_unique_id_bytes": (u64, []),
         "oge_comm_unique_id": (C.c_int, [vp, u64]),
         "oge_comm_init_rank": (C.c_int, [vp, C.c_int, C.c_int, vp, C.POINTER(vp)]),
+        "oge_comm_init_rank_mode": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_char_p, C.POINTER(vp)]),
+        "oge_comm_stats_json": (C.c_int64, [vp, C.c_char_p, u64]),
         "oge_comm_init": (C.c_int, [vp, C.c_int, vp]),
         "oge_comm_destroy": (None, [vp]),
         "oge_comm_rank": (C.c_int, [vp]),
@@ -648,6 +650,16 @@ class Comm:
                                             C.byref(nd)), self.ctx.h)
         return d.value or 0, ob.value, nr.value, nd.value
 
+    def exchange_stats(self) -> list:
+        """This rank's per-exchange record of its last sort_markdup_dist / mergesort_bgzf_dist call:
+        [{tag, calls, bytes_sent, bytes_recv, bytes_self, ms}] (bytes to / from other ranks, kept here;
+        host wall time of the collectives, waiting for peers included)."""
+        import json
+        n = lib().oge_comm_stats_json(self.h, None, 0)
+        buf = C.create_string_buffer(n + 1)
+        lib().oge_comm_stats_json(self.h, buf, n + 1)
+        return json.loads(buf.value.decode())
+
     def close(self):
         if self.h:
             lib().oge_comm_destroy(self.h)
@@ -670,10 +682,14 @@ def comm_unique_id() -> bytes:
     return buf.raw
 
 
-def comm_init_rank(ctx: "Context", nranks: int, rank: int, uid: bytes) -> Comm:
-    """One process per GPU (RCCL): uid from comm_unique_id() on one rank, shared by the caller."""
+def comm_init_rank(ctx: "Context", nranks: int, rank: int, uid: bytes, mode: str | None = None) -> Comm:
+    """One process per GPU (RCCL): uid from comm_unique_id() on one rank, shared by the caller.  mode:
+    "auto" | "rccl" | "host" (None = OGE_COMM)."""
     h = C.c_void_p()
-    check(lib().oge_comm_init_rank(ctx.h, nranks, rank, uid, C.byref(h)), ctx.h)
+    if mode is None:
+        check(lib().oge_comm_init_rank(ctx.h, nranks, rank, uid, C.byref(h)), ctx.h)
+    else:
+        check(lib().oge_comm_init_rank_mode(ctx.h, nranks, rank, uid, mode.encode(), C.byref(h)), ctx.h)
     return Comm(h, ctx)
 
 

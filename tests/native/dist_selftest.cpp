@@ -13,6 +13,8 @@
 //   dist_selftest KEYS_FILE G...          (KEYS_FILE: little-endian u64 ByPosition keys in input order)
 //   dist_selftest --shm KEYS_FILE G...
 //   dist_selftest --fail-copy G...
+//   dist_selftest --dead-rank G...        (the last rank's process exits after joining: the others must
+//                                          return with an error long before OGE_COMM_TIMEOUT)
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -149,7 +151,7 @@ static int run(const std::vector<uint64_t> &keys, int G, double *balance, int fa
 }
 
 // G forked processes over the host-staged transport (shared file mapping); results come back in files
-static int run_shm(const std::vector<uint64_t> &keys, int G, double *balance, int fail_rank = -1) {
+static int run_shm(const std::vector<uint64_t> &keys, int G, double *balance, int fail_rank = -1, int dead_rank = -1) {
     char dir[] = "/tmp/oge_shm_selftestXXXXXX";
     if (!mkdtemp(dir)) return perror("mkdtemp"), 1;
     char name[64];
@@ -166,6 +168,7 @@ static int run_shm(const std::vector<uint64_t> &keys, int G, double *balance, in
                 fprintf(stderr, "rank %d: %s\n", r, err.c_str());
                 _exit(3);
             }
+            if (r == dead_rank) _exit(7);  // gone before the first collective
             HostOps ops;
             ops.fail = r == fail_rank;
             ShmColl<HostOps> c{*seg, ops};
@@ -185,10 +188,11 @@ static int run_shm(const std::vector<uint64_t> &keys, int G, double *balance, in
         kids.push_back(pid);
     }
     std::vector<int> status(G);
-    for (int r = 0; r < G; ++r) {
+    for (int k = 0; k < G; ++k) {  // reap in exit order (a launcher does: an exited rank is no zombie)
         int st = 0;
-        waitpid(kids[r], &st, 0);
-        status[r] = WIFEXITED(st) ? WEXITSTATUS(st) : 128;
+        const pid_t pid = waitpid(-1, &st, 0);
+        for (int r = 0; r < G; ++r)
+            if (kids[r] == pid) status[r] = WIFEXITED(st) ? WEXITSTATUS(st) : 128;
     }
     std::vector<std::vector<uint64_t>> slices(G);
     std::vector<std::vector<uint8_t>> rs_out(G);
@@ -209,6 +213,12 @@ static int run_shm(const std::vector<uint64_t> &keys, int G, double *balance, in
     if (fail_rank >= 0) {
         for (int r = 0; r < G; ++r)
             if (status[r] != (r == fail_rank ? 4 : 0))
+                return fprintf(stderr, "shm: rank %d exited %d\n", r, status[r]), 1;
+        return 0;
+    }
+    if (dead_rank >= 0) {
+        for (int r = 0; r < G; ++r)
+            if (status[r] != (r == dead_rank ? 7 : 4))
                 return fprintf(stderr, "shm: rank %d exited %d\n", r, status[r]), 1;
         return 0;
     }
@@ -237,6 +247,18 @@ int main(int argc, char **argv) {
             const int G = atoi(argv[a]);
             double bal = 0;
             if (run(keys, G, &bal, G - 1) || run_shm(keys, G, &bal, G - 1)) return 1;
+        }
+        printf("{}\n");
+        return 0;
+    }
+    if (!strcmp(argv[1], "--dead-rank")) {
+        std::vector<uint64_t> keys(50000);
+        std::mt19937_64 rng(6);
+        for (auto &k : keys) k = rng() >> 20;
+        for (int a = 2; a < argc; ++a) {
+            const int G = atoi(argv[a]);
+            double bal = 0;
+            if (run_shm(keys, G, &bal, -1, G - 1)) return 1;
         }
         printf("{}\n");
         return 0;

@@ -101,3 +101,17 @@ def test_failing_rank_returns_on_every_rank(tmp_path):
     env = dict(os.environ, OGE_COMM_TIMEOUT="60", OGE_COMM_DIR=str(tmp_path))
     r = subprocess.run([str(exe), "--fail-copy", "2", "3", "5"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
+
+
+def test_dead_peer_ends_the_wait(tmp_path):
+    """A rank's process exits after joining the host-staged meeting (time out on a dead peer,
+    not a slow one): the other ranks see its posted pid gone and return with an error within seconds,
+    although the wall-clock backstop (OGE_COMM_TIMEOUT) is ten minutes."""
+    import os
+    import time
+    exe = _build(tmp_path / "dist_selftest")
+    env = dict(os.environ, OGE_COMM_TIMEOUT="600", OGE_COMM_DIR=str(tmp_path))
+    t0 = time.time()
+    r = subprocess.run([str(exe), "--dead-rank", "2", "4"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert time.time() - t0 < 60

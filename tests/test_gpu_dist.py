@@ -115,7 +115,7 @@ def test_dist_equals_single_on_goldens(ctx, name, G):
 
 
 @pytest.mark.parametrize("preset,pairs,seed,G", [("c2", 40000, 11, 2), ("c2", 40000, 12, 3), ("mix", 6000, 5, 3),
-                                                  ("c2", 60000, 13, 5)])
+                                                  ("c2", 60000, 13, 5), ("c2", 40000, 14, 4), ("c2", 60000, 15, 8)])
 def test_dist_equals_single_synthetic(ctx, preset, pairs, seed, G):
     p = L.synth_params(pairs, preset=preset, seed=seed)
     recs, offs, hdr = L.synth_host(p)
@@ -260,3 +260,40 @@ def test_dist_bgzf_chain_equals_single(ctx, tmp_path, G, level, flags):
     assert out[-28:] == bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
     assert gzip.decompress(out) == gzip.decompress(want.tobytes())
     assert {(r[1], r[2]) for r in res} == {(nr, nd)}
+
+
+def _pile(recs, offs, frac, seed):
+    """C2 records with a fraction moved onto ONE coordinate (refID 0, pos 1000, forward strand): a
+    uniform-key pile.  Equal ByPosition keys never straddle ranks, so the splitters degenerate -- with
+    frac = 1 every record has the same key and all of them land on one rank, the others get nothing."""
+    rng = np.random.default_rng(seed)
+    n = len(offs) - 1
+    out = [bytearray(bamutil.rec_bytes(recs, offs[i])) for i in range(n)]
+    pick = np.arange(n) if frac >= 1 else rng.choice(n, size=int(n * frac), replace=False)
+    for i in pick:
+        b = out[i]
+        (flag,) = struct.unpack_from("<H", b, 18)
+        struct.pack_into("<iI", b, 4, 0, 1000)
+        struct.pack_into("<H", b, 18, flag & ~0x10 & ~0x400)
+    return bamutil.pack_records([bytes(b) for b in out])
+
+
+@pytest.mark.parametrize("frac,G", [(0.6, 8), (1.0, 8), (1.0, 4)])
+def test_dist_uniform_key_pile(ctx, frac, G):
+    """Splitter degeneracy at the node's rank counts: a pile of identical ByPosition keys (60% of the
+    reads, then all of them).  The one-GPU marks are pinned to the oracle restatement first (the pile
+    takes the windowed dedup's overflow path), then the G-rank output must equal the one-GPU output."""
+    p = L.synth_params(6000, preset="c2", seed=51)
+    recs0, offs0, hdr = L.synth_host(p)
+    recs, offs = _pile(recs0, offs0, frac, 52)
+    n = len(offs) - 1
+    perm = oracle.sort_perm(recs, offs, n)
+    srecs, soffs = bamutil.pack_records([bamutil.rec_bytes(recs, offs[i]) for i in perm])
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    dup, nd = ctx.markdup(srecs, soffs, n, opts)
+    odup, ond = oracle.markdup(srecs, soffs, n, hdr)
+    assert nd == ond and np.array_equal(dup, odup)
+    counts, nd2 = _check(ctx, recs, offs, p.n_ref, hdr, G)
+    assert nd2 == nd
+    if frac >= 1:  # one rank holds the whole pile
+        assert sorted(counts)[-1] == n and sum(1 for c in counts if c) == 1

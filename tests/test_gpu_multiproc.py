@@ -25,6 +25,19 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
 
 
+def _header_bytes(stream: bytes) -> int:
+    """bytes of the BAM header block at the start of a decompressed BAM stream (magic, text, refs)"""
+    import struct
+    (lt,) = struct.unpack_from("<i", stream, 4)
+    q = 8 + lt
+    (nref,) = struct.unpack_from("<i", stream, q)
+    q += 4
+    for _ in range(nref):
+        (ln,) = struct.unpack_from("<i", stream, q)
+        q += 4 + ln + 4
+    return q
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -50,20 +63,54 @@ def one_gpu_c2_20k(built, tmp_path_factory):
     return case, gzip.decompress(h.tobytes()), nr, nd
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_bench_multiprocess_bootstrap_matches_reference(world, tmp_path, one_gpu_c2_20k):
+RL_INTERVALS = 1500  # C5 generator, small enough for 8 ranks that each generate the whole set
+
+
+@pytest.fixture(scope="module")
+def one_gpu_realign(built, tmp_path_factory):
+    """bench.py's realign leg in one process (world 1) on the small C5 set: its realigned records."""
+    d = tmp_path_factory.mktemp("rl1")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--realign-only", "--realign-intervals", str(RL_INTERVALS),
+           "--no-cpu-baseline", "--dump-dir", str(d)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-4000:]
+    return (d / "realign_0.bin").read_bytes()
+
+
+@pytest.mark.parametrize("world,realign", [(2, False), (3, False), (4, True), (8, False)])
+def test_bench_multiprocess_bootstrap_matches_reference(world, realign, tmp_path, one_gpu_c2_20k, request):
+    """world 4 and 8 are the rank counts of the 8-GPU node's scaling run (config 4), here as processes
+    sharing the one GPU; world 4 also runs the realign leg (contig-range shards, no exchange), whose
+    concatenated rank outputs must equal the one-process realign output byte for byte."""
     case, want, nr1, nd1 = one_gpu_c2_20k
     env = dict(os.environ, OGE_COMM_DIR=str(tmp_path), OGE_COMM_TIMEOUT="120", MASTER_ADDR="127.0.0.1",
-               OMP_NUM_THREADS="4")
+               OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            str(ROOT / "bench.py"), "--gpus", str(world), "--pairs", "20000", "--seed", "99", "--steps", "1",
-           "--warmup", "1", "--no-realign", "--dump-dir", str(tmp_path)]
+           "--warmup", "1", "--dump-dir", str(tmp_path)]
+    cmd += ["--realign-intervals", str(RL_INTERVALS)] if realign else ["--no-realign"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(ROOT))
     assert r.returncode == 0, r.stderr[-4000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == world
     assert line["config"]["transport"] == "host"
+    # the diagnosable breakdown: every rank's exchanges (bytes and times) and stage times
+    ex = line["exchanges"]
+    assert len(ex["per_rank"]) == world and len(line["stages_ms_per_rank"]) == world
+    by = ex["by_tag"]
+    for tag in ("records", "record_sizes", "fragments", "matejoin_candidates", "matejoin_minirecs", "pair_ends",
+                "dup_marks", "plans", "status"):
+        assert tag in by, tag
+    # every record moves to its range owner or stays: sent + kept = the record bytes of the input
+    rec_bytes = by["records"]["bytes_between_ranks"] + by["records"]["bytes_kept"]
+    assert rec_bytes == int(np.frombuffer(want, np.uint8).size) - _header_bytes(want)
+    assert by["record_sizes"]["bytes_between_ranks"] + by["record_sizes"]["bytes_kept"] == 4 * nr1
+    if realign:
+        rl = line["realign"]
+        assert rl["n_gpus"] == world and rl["value"] > 0
+        got = b"".join((tmp_path / f"realign_{g}.bin").read_bytes() for g in range(world))
+        assert got == request.getfixturevalue("one_gpu_realign")
     assert line["config"]["duplicates_flagged"] == case.meta["sortdedup_v"]["n_dup"] == nd1
     out = b"".join((tmp_path / f"slice_{g}.bam").read_bytes() for g in range(world))
     assert out[-28:] == bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
