@@ -6,11 +6,13 @@ sort, Picard MarkDuplicates with -v semantics, FLAG 0x400 applied, bins recomput
 regenerated).  Workload at N=1: configs[1]+[2] -- a 300M-read (150M pairs) 30x WGS-shaped synthetic
 read set (SURVEY.md §8d C2 generator, seed 1234).
 
-value (SURVEY §8d timing rule, BAM in -> BAM out at BGZF level 6): one step is the whole
+value (SURVEY §8d timing rule, BAM in -> BAM out, BGZF at -c 6): one step is the whole
 `mergesort -M` chain over a BGZF BAM file resident in HBM when the timed region starts
 (oge_mergesort_bgzf_dev: framing index, inflate + CRC-32, record walk, sort + dedup, header,
-level-6 deflate, EOF block; the output BAM file ends in HBM).  The input file is made once before
-the timed region by the library's own GPU deflate at level 6 from the device generator.
+GPU deflate, EOF block; the output BAM file ends in HBM).  The input file is made once before the
+timed region by the library's own GPU deflate from the device generator.  The GPU deflate is a greedy
+single-candidate parse (DEFLATE_SEARCH below), not zlib's level-6 lazy hash-chain search: its output is
+~3% larger; config.deflate carries both ratios.
 
 Also on the same JSON line:
   kernel_step   -- the sort+dedup device pipeline alone over records already decoded in HBM
@@ -134,7 +136,7 @@ def pmc_traffic(kernel: str, rec_bytes: int) -> dict | None:
 def stage_kernels(B: int, zin: int, zout: int, n: int, seq_bytes: int) -> dict:
     return {
         "bgzf_inflate": ("k_infl", "BGZF inflate: compressed bytes read + payload bytes written", zin + B, "valu"),
-        "bgzf_deflate": ("k_defl", "BGZF deflate (level 6): payload read + compressed bytes written", B + zout, "valu"),
+        "bgzf_deflate": ("k_defl", "BGZF deflate (greedy single-candidate, -c 6): payload read + compressed bytes written", B + zout, "valu"),
         "gather_records": ("k_gather16", "permutation gather + BAM re-encode: 2*B (SURVEY §8d sort bytes)", 2 * B, "hbm"),
         "input_pass": ("k_input_pass", "record parse: B - packed bases (SURVEY §8d dedup bytes) + 2N",
                        B - seq_bytes + 2 * n, "hbm"),
@@ -362,6 +364,27 @@ def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, "torch.Tenso
     return res, S, B, hdr_text
 
 
+DEFLATE_SEARCH = ("GPU deflate (bgzf.hip): greedy parse, ONE hash candidate per position (4-byte prefix, 4096 "
+                  "buckets, filled in rounds of 1024 positions), matches cut at 64-byte segment edges, no lazy "
+                  "matching; one dynamic-Huffman block per 65,280-byte payload (length-limited to 15 bits). "
+                  "The level number selects stored (0) or this mode (1-9): it is not zlib's level-6 search")
+
+
+def zlib6_sample_ratio(S, off: int, nbytes: int, sample: int = 32 << 20) -> dict:
+    """zlib level 6 (OpenGE's writer: util/bgzf_output_stream.cpp:74-79) over the first `sample` bytes of the
+    record stream in 65,280-byte BGZF payloads (18 + 8 bytes of BGZF framing each), for comparison with the
+    GPU deflate's ratio."""
+    import zlib
+    from concurrent.futures import ThreadPoolExecutor
+    pay = 65280
+    n = max(pay, min(nbytes, sample) // pay * pay)
+    h = S[off:off + n].cpu().numpy().tobytes()
+    with ThreadPoolExecutor(16) as ex:
+        z = sum(ex.map(lambda i: len(zlib.compress(h[i:i + pay], 6)) - 6 + 26, range(0, len(h), pay)))
+    return {"ratio": round(z / len(h), 4), "sample_bytes": len(h),
+            "what": "zlib level 6 per 65,280-byte payload + BGZF framing, first bytes of the same record stream"}
+
+
 def build_input(ctx, L, torch, dev, S, total: int, level: int) -> tuple["torch.Tensor", int]:
     """The input BAM file in HBM: the library's GPU deflate of [header][records] at `level` plus the
     EOF block, in a buffer of exactly its size (the bound-sized staging buffer is freed)."""
@@ -433,6 +456,7 @@ def main():
     seq_bytes = n * ((p.read_len + 1) // 2)
 
     # ---- the input BAM file in HBM (level-6 BGZF, GPU deflate), staging freed
+    zref = zlib6_sample_ratio(S, len(hb), B)
     Z, zb = build_input(ctx, L, torch, dev, S, total, args.level)
     del S
     torch.cuda.empty_cache()
@@ -506,9 +530,12 @@ def main():
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234, as a level-6 BGZF BAM file resident in HBM",
         "config": {"workload": f"C2+C3 end to end: {n // 1000000}M-read BAM file -> mergesort -M --nosplit "
-                               f"(sort + dedup -v) -> BGZF level-{args.level} BAM file, in HBM",
+                               f"(sort + dedup -v) -> BGZF BAM file (-c {args.level}: GPU greedy single-candidate "
+                               "deflate, see config.deflate), in HBM",
                    "reads_total": n, "record_bytes": B, "input_file_bytes": zbytes, "output_file_bytes": out_bytes,
-                   "duplicates_flagged": nd, "parallelism": "1 GPU"},
+                   "duplicates_flagged": nd, "parallelism": "1 GPU",
+                   "deflate": {"search": DEFLATE_SEARCH, "gpu_ratio_input_file": round(zbytes / total, 4),
+                               "gpu_ratio_output_file": round(out_bytes / total, 4), "zlib6_sample": zref}},
         "roofline": roof, "roofline_stages": others, "stages_ms": sms, "warmup_ms": warm,
         "kernel_step": kres, "pcie_inclusive": pcie,
     }

@@ -3,27 +3,35 @@
 // zlib inflate per BGZF block on the pool) -- the same RFC 1951 decode, laid out for wave64.
 //
 // Why this shape.  A BGZF block is an independent deflate stream of <= 64 KiB whose Huffman decode is
-// one long serial chain.  The r01 grouped decoder (one chain per 32 lanes: 19.7 GB/s at 20M reads,
-// removed in r03) let a wave64 instruction advance two blocks.  Here every lane is its own decoder:
-// one wave instruction advances 64 blocks (46.5 GB/s at 20M reads, profiles/r02_inflate_20m*).  A lane's decode step is a dependent chain (table lookup -> shift
-// -> next lookup), so throughput comes from waves in flight: phase 1 keeps only the hot 6-bit
-// literal/length and 4-bit distance tables in LDS (144 B per lane, lane-interleaved so a wave's 64
-// lookups hit 64 different banks), holds the canonical limits of the longer codes in VGPRs and their
-// symbol lists in a per-lane global scratch (MALL-resident): 12 waves per CU (VGPR-bound).
+// one long serial chain.  Every lane is its own decoder: one wave instruction advances 64 blocks.  A
+// lane's decode step is a dependent chain (table lookup -> shift -> next lookup), and a wave executes
+// the UNION of its 64 lanes' paths every step (some lane is nearly always on each rare path: a long
+// code, a match, a long distance code), so the rare paths must be cheap and must not wait on memory:
+//
+//   * Only LDS and registers in the chain.  The hot 6-bit literal/length and 4-bit distance direct
+//     tables, the long LENGTH codes' symbols and the long DISTANCE codes' symbols live in LDS
+//     (lane-interleaved [entry][lane]: a wave's 64 lookups hit 64 banks); the canonical limits of the
+//     longer codes in VGPRs.  A long LITERAL code (7..15 bits: ~7% of BAM literals) needs no symbol to
+//     continue the bit stream -- its length comes from the limits and the literal/length split from
+//     the code's canonical index -- so phase 1 writes the index (< 256) in place of the byte, marks the
+//     position in a second bitmap, and phase 2 translates it through the table's list (written once
+//     per table to a per-block area).  r03 looked the symbol up in a per-lane global scratch in the
+//     chain: a global load per step that also waited (vmcnt counts stores too) for every output store
+//     in flight.
+//   * Wave-wide work (table builds, the block queue, the exit test) every kInner steps instead of every
+//     step; a lane waiting for it idles at most kInner steps (a few per BGZF block).
 //
 // Phase 1 (k_infl_huff, persistent 64-lane workgroups): each lane decodes the symbols of its blocks.
 //   Literals are written at their output position (8-byte chunks assembled in a register); a match
 //   (length L >= 3, distance D) leaves a hole of L bytes whose first three bytes receive the
-//   descriptor (L-3, D-1 in 23 bits) and sets the hole's start bit in the block's 65536-bit bitmap.
-//   Code tables are built by the whole wave for one lane at a time (ballot counting, when a lane
-//   reaches a new dynamic block).
-// Phase 2 (k_infl_lz, one 1024-thread workgroup per block): refs[p] = p for every position, then
-//   refs[p + j] = p - D + j for every hole; pointer jumping (refs[q] = refs[refs[q]]) in LDS until
-//   every position points at a literal (log2 of the copy-chain depth rounds; BAM data: 5-7); the
-//   block's literal-filled bytes are then staged in LDS, every byte gathered from its root, CRC-32
-//   checked and written out.
+//   descriptor (L-3, D-1 in 23 bits) and sets the hole's start bit in the block's bitmap.
+// Phase 2 (k_infl_lz, one 1024-thread workgroup per block): deferred literals translated; refs[p] = p for
+//   every position, then refs[p + j] = p - D + j for every hole; pointer jumping (refs[q] = refs[refs[q]])
+//   in LDS until every position points at a literal; the block's bytes are then staged in LDS, every
+//   byte gathered from its root, CRC-32 checked and written out.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -45,22 +53,29 @@ __device__ __forceinline__ void report(uint32_t *err, uint32_t code, uint64_t bl
 constexpr int TL = 6, TD = 4;  // direct-table bits: literal/length, distance
 constexpr int kWps = 3;        // waves per SIMD (VGPR budget 512 / 3)
 constexpr int LB = 4;          // literals per decode step (see the ST_SYM path)
-// Codes longer than the direct tables take their symbol from the lane's canonical list in its global
-// scratch (MALL-resident); list heads in LDS (r02 cfg 1-3) measured slower in the 300M chain: 1615 vs
-// 1157 ms (profiles/r02s3_infl_cfg.json).
-// per-wave LDS, lane-interleaved ([entry][lane]): element e of lane l at e * 64 + l
+constexpr int kInner = 16;     // decode steps between the wave-wide phases
+constexpr int kNT = 4;         // tables per BGZF block whose long literals phase 2 translates
+constexpr uint32_t kXList = 288;                 // a table's canonical list of long codes (bytes)
+constexpr uint32_t kXTab = 1280;                 // per block: kNT lists, then kNT u32 start positions
+constexpr uint32_t kXStart = kNT * kXList;       // offset of the start positions
+constexpr uint32_t kDefer = 0x1000;              // sym: a long literal whose byte phase 2 looks up
+
+// per-wave LDS, lane-interleaved ([entry][lane]): element e of lane l at e * 64 + l.  13,312 bytes: 12
+// waves per CU fit the 160 KiB.
 struct P1Lds {
     uint16_t lt[1 << TL][64];  // sym | L << 9, 0 = longer code; while code lengths are decoded a lane's
                                 // column holds its 7-bit code-length table (cl_at): sym | L << 5
-    uint8_t dt[1 << TD][64];    // sym | L << 5, 0 = longer code
-    uint32_t cnt[16], lo[16], first[16], offl[16], run[16], lim[16], lie[16];  // the build's per-length values
-    uint64_t clp[64];           // a lane's code-length-code lengths between its header and its CL build
+    uint8_t dt[1 << TD][64];   // sym | L << 5, 0 = longer code
+    uint8_t ll[32][64];        // long length codes (and end of block): symbol - 256, by long-length index
+                               // (32: the fixed code's 286 / 287 have codes too)
+    uint8_t dl[30][64];        // long distance codes: symbol, by long-distance index
+    uint32_t cnt[16], lo[16];  // a build's per-length counts (all / literal symbols)
 };
 // per-lane global scratch
 constexpr uint32_t kScr = 640;
 constexpr uint32_t S_LENS = 0;   // u8[320] code lengths of the block being set up (zeroed by the CL build)
-constexpr uint32_t S_LS = 320;   // u8[288] literal/length symbols with codes longer than TBL, canonical order
-constexpr uint32_t S_DS = 608;   // u8[32]  distance symbols with codes longer than TBD
+constexpr uint32_t S_LS = 320;   // u8[288] the long-code list of a table whose literals are not deferred
+constexpr uint32_t S_CLP = 608;  // u64: the code-length code's lengths between a header and its build
 
 __constant__ uint8_t kClOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
@@ -74,7 +89,8 @@ enum { ST_HDR = 0, ST_CL = 1, ST_SYM = 2, ST_STORED = 3, ST_BCL = 4, ST_BLD = 5,
 struct Slow {
     uint32_t ll[4];   // litlen left-justified 15-bit limits, lengths 7..14
     uint32_t l15;     // limit of length 15
-    uint32_t lie[9];  // lengths 7..15: (list index - first code) & 0xffff | end-of-literals << 16
+    uint32_t pk[9];   // lengths 7..15: (list index - first code) & 0xffff | end of literals << 16 | long
+                      // length codes before this length << 25
     uint32_t dl[6];   // distance limits, lengths 5..15 (slot 11 unused)
     uint32_t di[6];   // distance lengths 5..15: list index - first code
 };
@@ -104,56 +120,63 @@ __device__ __forceinline__ uint32_t u16of(const uint32_t (&a)[6], uint32_t i) {
 // ---------------------------------------------------------------------------- wave-cooperative builds
 // Canonical Huffman code (RFC 1951 3.2.2) of one alphabet for lane j, the wave's 64 lanes holding the
 // lengths of symbols lane, lane+64, ... in len[0..NR).  Codes <= TB bits go to lane j's column of the
-// direct table; longer codes to lane j's symbol list (global scratch).  Per length L (lane L of the
-// wave): left-justified 15-bit limit in S.lim[L], (list index - first code) | end-of-literals << 16 in
-// S.lie[L].  The per-length values pass through LDS so the build holds few scalars.
-// false = over-subscribed code.
-template <int NR, int TB, bool LIT, class Lds>
-__device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (&len)[NR], uint32_t n) {
+// direct table.  Longer codes, in canonical order (length, then symbol): LIT -- the literal/length
+// alphabet -- all of them to `list` (the lane's scratch) and, when `xl` is given and there are at most
+// 256 of them (a list index then fits the byte phase 1 writes), to xl (phase 2's translation list); the
+// length codes among them also to lane j's column of S.ll.  !LIT (distances): to lane j's column of S.dl.
+// Returns lane L's (L < 16) left-justified 15-bit limit in *lim and its list parameters in *pk (see
+// Slow), the number of long codes in *nlong; false = over-subscribed code.
+template <int NR, int TB, bool LIT>
+__device__ bool wbuild(P1Lds &S, uint32_t j, OGE_G uint8_t *list, OGE_G uint8_t *xl, const uint32_t (&len)[NR], uint32_t n,
+                       uint32_t *lim, uint32_t *pk, uint32_t *nlong) {
     const uint32_t lane = threadIdx.x;
     const uint64_t lt = (1ull << lane) - 1;
-    if (lane < 16) S.cnt[lane] = S.lo[lane] = S.run[lane] = 0;
+    if (lane < 16) S.cnt[lane] = S.lo[lane] = 0;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const uint32_t L = len[r];
         if (L && r * 64 + lane < n) {
             atomicAdd(&S.cnt[L], 1u);
-            if (r < 4) atomicAdd(&S.lo[L], 1u);  // literal/length symbols < 256
+            if (LIT && r < 4) atomicAdd(&S.lo[L], 1u);  // literal symbols < 256
         }
     }
     __builtin_amdgcn_wave_barrier();
-    // lane L: first code, long-list offset, Kraft term of length L
-    uint32_t fst = 0, ofl = 0, kraft = 0;
+    // lane L: first code, long-list offset, long literals before it, Kraft term of length L
+    uint32_t fst = 0, ofl = 0, litb = 0, kraft = 0, c = 0, lo = 0;
     if (lane >= 1 && lane < 16) {
         for (uint32_t l = 1; l < lane; ++l) {
-            const uint32_t c = S.cnt[l];
-            fst += c << (lane - l);
-            if (l > (uint32_t)TB) ofl += c;
+            const uint32_t cl = S.cnt[l];
+            fst += cl << (lane - l);
+            if (l > (uint32_t)TB) ofl += cl, litb += S.lo[l];
         }
-        const uint32_t c = S.cnt[lane];
+        c = S.cnt[lane];
+        lo = S.lo[lane];
         kraft = c << (15 - lane);
-        S.first[lane] = fst;
-        S.offl[lane] = ofl;
-        S.lim[lane] = min((fst + c) << (15 - lane), 65535u);
-        S.lie[lane] = ((ofl - fst) & 0xffff) | ((ofl + S.lo[lane]) << 16);
     }
+    *lim = min((fst + c) << (15 - (lane & 15)), 65535u);
+    *pk = ((ofl - fst) & 0xffff) | ((ofl + lo) << 16) | ((ofl - litb) << 25);
     // over-subscribed iff the Kraft sum exceeds 2^15 (every prefix check of RFC 1951 follows from it)
-    uint32_t ks = kraft;
+    uint32_t ks = kraft, nl = lane > (uint32_t)TB && lane < 16 ? c : 0u;
 #pragma unroll
-    for (int d = 1; d < 16; d <<= 1) ks += __shfl_xor(ks, d, 64);
+    for (int d = 1; d < 16; d <<= 1) ks += __shfl_xor(ks, d, 64), nl += __shfl_xor(nl, d, 64);
     ks = __builtin_amdgcn_readfirstlane(ks);
+    *nlong = __builtin_amdgcn_readfirstlane(nl);
     if (ks > 32768u) return false;
+    const bool wx = xl != nullptr && *nlong <= 256;
     for (uint32_t r = lane; r < (1u << TB); r += 64) {  // zero lane j's column of the direct table
         if (LIT) S.lt[r][j] = 0;
         else S.dt[r][j] = 0;
     }
     __builtin_amdgcn_wave_barrier();
+    uint32_t run = 0;  // lane L: symbols of length L placed so far
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         const uint32_t myL = len[r], s = r * 64 + lane;
         const bool mine = myL && s < n;
-        const uint32_t base = mine ? S.run[myL] : 0u, fc = mine ? S.first[myL] : 0u, ol = mine ? S.offl[myL] : 0u;
+        const uint32_t src = mine ? myL : 0u;
+        const uint32_t base = __shfl(run, src, 64), fc = __shfl(fst, src, 64), ol = __shfl(ofl, src, 64);
+        const uint32_t lob = LIT ? __shfl(lo, src, 64) : 0u, lenb = LIT ? __shfl(ofl - litb, src, 64) : 0u;
         uint32_t rank = 0, add = 0;
 #pragma unroll
         for (int L = 1; L < 16; ++L) {
@@ -161,9 +184,7 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
             if (myL == (uint32_t)L) rank = (uint32_t)__popcll(m & lt);
             if (lane == (uint32_t)L) add = (uint32_t)__popcll(m);
         }
-        __builtin_amdgcn_wave_barrier();
-        if (lane >= 1 && lane < 16) S.run[lane] += add;
-        __builtin_amdgcn_wave_barrier();
+        run += add;
         if (mine) {
             rank += base;
             if (myL <= (uint32_t)TB) {
@@ -173,8 +194,12 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
                     if (LIT) S.lt[ix][j] = (uint16_t)(s | (myL << 9));
                     else S.dt[ix][j] = (uint8_t)(s | (myL << 5));
                 }
-            } else {
+            } else if (LIT) {
                 list[ol + rank] = (uint8_t)s;
+                if (wx) xl[ol + rank] = (uint8_t)s;
+                if (s >= 256) S.ll[min(lenb + rank - lob, 31u)][j] = (uint8_t)(s - 256);
+            } else {
+                S.dl[min(ol + rank, 29u)][j] = (uint8_t)s;
             }
         }
     }
@@ -194,17 +219,21 @@ __device__ bool wbuild(Lds &S, uint32_t j, OGE_G uint8_t *list, const uint32_t (
 // (profiles/r02s3_infl_litb.json).
 // Bit-budget guard (always on): every skip of more bits than the buffer holds sets `under`, and the
 // block fails with E_BITS instead of decoding from zero bits.
+// Output: bytes go through a 64-bit shift register (the newest byte enters at the top) that is stored
+// when it holds a whole 8-byte chunk of the output; the block's first and last chunk (shared with the
+// neighbouring blocks) are stored byte by byte.  Bitmap words (holes, deferred literals) per 64
+// positions, zeroed before the launch, stored when a lane leaves a word that has bits.
 __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
                                                       const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
                                                       const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
                                                       uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
-                                                      uint8_t *__restrict__ scratch, uint32_t *__restrict__ err,
-                                                      unsigned long long *__restrict__ next) {
+                                                      uint8_t *__restrict__ xtab, uint8_t *__restrict__ scratch,
+                                                      uint32_t *__restrict__ err, unsigned long long *__restrict__ next) {
     static_assert(LB <= 4 && TL * LB <= 32, "a step's literal batch must fit the 32 bits a refill guarantees");
+    static_assert(sizeof(P1Lds) <= 13312, "12 waves per CU");
     __shared__ P1Lds S;
     const uint32_t lane = threadIdx.x;
-    const uint64_t gid = (uint64_t)blockIdx.x * 64 + lane;
-    OGE_G uint8_t *const scr = (OGE_G uint8_t *)(scratch + gid * kScr);  // this lane's lens / long-code symbol lists
+    auto scr = [&]() { return (OGE_G uint8_t *)(scratch + ((uint64_t)blockIdx.x * 64 + threadIdx.x) * kScr); };  // lens / list
     const uintptr_t zend = (uintptr_t)z + zbytes;
 
     // input: 64-bit bit buffer + two 16-byte chunks (q being consumed, p loaded ahead)
@@ -258,59 +287,60 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
         skip((uint32_t)(a & 3) * 8);
     };
 
-    // output: 8-byte chunk accumulator; the block's first/last chunk are written byte by byte
-    uint8_t *obase = nullptr;
-    uint32_t osz = 0, pos = 0;
-    uint64_t oc = ~0ull, acc = 0;
-    auto flush = [&]() {
-        if (oc == ~0ull) return;
-        const uintptr_t c = oc << 3, ob = (uintptr_t)obase;
-        if (c >= ob && c + 8 <= ob + osz) {
-            *(OGE_G uint64_t *)c = acc;
-        } else {
-            for (uint32_t k = 0; k < 8; ++k)
-                if (c + k >= ob && c + k < ob + osz) ((OGE_G uint8_t *)c)[k] = (uint8_t)(acc >> (8 * k));
-        }
-    };
-    auto put = [&](uint32_t p, uint32_t v, uint32_t nbytes) {  // nbytes (1..3) little-endian bytes of v at p
-        const uintptr_t a = (uintptr_t)(obase + p);
-        const uint32_t sh = (uint32_t)(a & 7);
-        if ((a >> 3) == oc && sh + nbytes <= 8) {
-            acc |= (uint64_t)(v & ((1u << (8 * nbytes)) - 1)) << (8 * sh);
-            return;
-        }
-        for (uint32_t k = 0; k < nbytes; ++k) {
-            const uintptr_t ak = a + k;
-            if ((ak >> 3) != oc) {
-                flush();
-                oc = ak >> 3;
-                acc = 0;
+    // output: position q = pos + al from the 8-aligned base ob8; the shift register acc holds the last
+    // 8 bytes put (oldest in the low byte), so at a chunk boundary it IS the chunk
+    OGE_G uint8_t *ob8 = nullptr;
+    uint32_t al = 0, osz = 0, pos = 0, clast = 0;
+    uint64_t acc = 0;
+    auto store_chunk = [&](uint32_t c, uint64_t v) {  // chunk c (8 bytes at ob8 + 8c) = v
+        OGE_G uint64_t *A = (OGE_G uint64_t *)ob8 + c;
+        if ((c == 0 && al) || (c == clast && ((al + osz) & 7))) {  // shared with a neighbouring block
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t q = 8 * c + k;
+                if (q >= al && q < al + osz) ((OGE_G uint8_t *)A)[k] = (uint8_t)(v >> (8 * k));
             }
-            acc |= (uint64_t)((v >> (8 * k)) & 0xff) << ((ak & 7) * 8);
+        } else {
+            *A = v;
         }
     };
-    // match-start bitmap of the block (1024 words per block of the chunk)
-    OGE_G uint64_t *bmp = nullptr;
-    uint64_t bm = 0;
-    uint32_t bw = 0;
-    auto mark = [&](uint32_t p) {
+    auto put = [&](uint32_t v) {  // one byte at pos
+        acc = (acc >> 8) | ((uint64_t)(v & 0xff) << 56);
+        const uint32_t q = pos + al + 1;
+        ++pos;
+        if (!(q & 7)) store_chunk((q >> 3) - 1, acc);
+    };
+    auto flush_partial = [&]() {  // the chunk holding the last byte put, when it is not complete
+        const uint32_t q = pos + al;
+        if (q & 7) store_chunk(q >> 3, acc >> (8 * (8 - (q & 7))));
+    };
+    // hole and deferred-literal bitmaps of the block (1024 word pairs per block of the chunk)
+    uint64_t bm = 0, lm = 0;
+    uint32_t bw = 0, bi = 0;  // word, block index in the chunk
+    auto word = [&](uint32_t p) {
         const uint32_t w = p >> 6;
         if (w != bw) {
-            bmp[bw] = bm;
-            for (uint32_t k = bw + 1; k < w; ++k) bmp[k] = 0;
-            bm = 0;
+            if (bm | lm) {
+                typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+                u64x2 v;
+                v.x = bm, v.y = lm;
+                *(OGE_G u64x2 *)(bitmap + (uint64_t)bi * 2048 + 2 * bw) = v;
+            }
+            bm = lm = 0;
             bw = w;
         }
-        bm |= 1ull << (p & 63);
     };
+    // tables built in this block << 1 | the current table's long literals are deferred to phase 2
+    uint32_t tabs = 0;
 
     Slow T;
     sfor<4>([&](auto k) { T.ll[k()] = 0; });
-    sfor<9>([&](auto k) { T.lie[k()] = 0; });
+    sfor<9>([&](auto k) { T.pk[k()] = 0; });
     sfor<6>([&](auto k) { T.dl[k()] = T.di[k()] = 0; });
     T.l15 = 0;
-    uint32_t st = ST_NEXT, fin = 0, hlit = 0, hdist = 0, ci = 0, prev = 0, srem = 0, fixed = 0, l256 = 0;
-    uint64_t b = 0, d1bit = 0;
+    // hl: hlit | hdist << 16; aux: the code-length walk (ci | prev << 16 | l256 << 24) or a stored block's
+    // bytes left; flg: the block header's BFINAL (1) and fixed-codes (2) bits
+    uint32_t st = ST_NEXT, hl = 0, aux = 0, flg = 0;
+    uint32_t b = 0;  // block index (a chunk of a launch holds < 2^32 blocks)
 
     auto fail = [&](uint32_t code) {
         report(err, code, b);
@@ -319,10 +349,9 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
     auto block_end = [&]() {  // last deflate block of the BGZF block consumed
         if (under) return fail(E_BITS);
         if (pos != osz) return fail(E_SIZE);
-        if (bitpos() > d1bit) return fail(E_PAST);
-        flush();
-        bmp[bw] = bm;
-        for (uint32_t k = bw + 1; k < (osz + 63) >> 6; ++k) bmp[k] = 0;
+        if (bitpos() > ((uint64_t)(uintptr_t)z + d1a[b]) * 8) return fail(E_PAST);
+        flush_partial();
+        word(0xffffffffu);
         st = ST_NEXT;
     };
 
@@ -335,8 +364,8 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
             need &= need - 1;
             OGE_G uint8_t *sj = (OGE_G uint8_t *)(scratch + ((uint64_t)blockIdx.x * 64 + j) * kScr);
             if (__builtin_amdgcn_readlane(st, j) == ST_BCL) {
-                // code-length code: 19 symbols, lengths 3 bits each (symbol s at bits 3s of S.clp[j])
-                const uint64_t c = S.clp[j];
+                // code-length code: 19 symbols, lengths 3 bits each (symbol s at bits 3s of lane j's clp)
+                const uint64_t c = *(const OGE_G uint64_t *)(sj + S_CLP);  // lane j's, stored at its header
                 const uint32_t myL = lane < 19 ? (uint32_t)((c >> (3 * lane)) & 7) : 0;
                 uint32_t cntl[8];
 #pragma unroll
@@ -366,12 +395,13 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 ((OGE_G uint32_t *)(sj + S_LENS))[lane] = 0;  // all 320 bytes: 17/18 runs then need no stores
                 if (lane < 16) ((OGE_G uint32_t *)(sj + S_LENS))[64 + lane] = 0;
                 if (lane == j) {
-                    if (ok) st = ST_CL, ci = 0, prev = 0, l256 = 0;
+                    if (ok) st = ST_CL, aux = 0;
                     else fail(E_TABLE);
                 }
             } else {
-                const uint32_t hl = __builtin_amdgcn_readlane(hlit, j), hd = __builtin_amdgcn_readlane(hdist, j);
-                const bool fx = __builtin_amdgcn_readlane(fixed, j) != 0;
+                const uint32_t hlj = __builtin_amdgcn_readlane(hl, j), hd = hlj >> 16, hl = hlj & 0xffff;
+                const bool fx = (__builtin_amdgcn_readlane(flg, j) & 2) != 0;
+                const uint32_t nt = __builtin_amdgcn_readlane(tabs, j) >> 1;
                 uint32_t ll[5], dl[1];
 #pragma unroll
                 for (int r = 0; r < 5; ++r) {
@@ -380,21 +410,39 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                     if (s < hl) ll[r] = fx ? (s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8) : sj[S_LENS + s];
                 }
                 dl[0] = lane < hd ? (fx ? 5u : (uint32_t)sj[S_LENS + hl + lane]) : 0u;
-                bool ok = wbuild<5, TL, true>(S, j, sj + S_LS, ll, hl);
-                if (ok && lane == j) {
-                    sfor<4>([&](auto k) { T.ll[k()] = S.lim[7 + 2 * k()] | (S.lim[8 + 2 * k()] << 16); });
-                    T.l15 = S.lim[15];
-                    sfor<9>([&](auto k) { T.lie[k()] = S.lie[7 + k()]; });
+                // the long-code list: the lane's scratch, and the block's translation area while it has a
+                // free table slot (else the table's long literals are looked up in the chain, as r03 did)
+                OGE_G uint8_t *xj = (OGE_G uint8_t *)(xtab + (uint64_t)__builtin_amdgcn_readlane(bi, j) * kXTab);
+                uint32_t lim, pk, nlong;
+                bool ok = wbuild<5, TL, true>(S, j, sj + S_LS, nt < kNT ? xj + nt * kXList : nullptr, ll, hl, &lim, &pk, &nlong);
+                const uint32_t dfr = ok && nt < kNT && nlong <= 256;
+                sfor<4>([&](auto k) {
+                    const uint32_t v = (uint32_t)__shfl(lim, 7 + 2 * k(), 64) | ((uint32_t)__shfl(lim, 8 + 2 * k(), 64) << 16);
+                    if (lane == j) T.ll[k()] = v;
+                });
+                {
+                    const uint32_t v = (uint32_t)__shfl(lim, 15, 64);
+                    if (lane == j) T.l15 = v;
                 }
-                ok = ok && wbuild<1, TD, false>(S, j, sj + S_DS, dl, hd);
+                sfor<9>([&](auto k) {
+                    const uint32_t v = (uint32_t)__shfl(pk, 7 + k(), 64);
+                    if (lane == j) T.pk[k()] = v;
+                });
+                ok = ok && wbuild<1, TD, false>(S, j, nullptr, nullptr, dl, hd, &lim, &pk, &nlong);
+                sfor<6>([&](auto k) {
+                    const uint32_t a = (uint32_t)__shfl(lim, 5 + 2 * k(), 64), c2 = (uint32_t)__shfl(lim, 6 + 2 * k(), 64);
+                    const uint32_t pa = (uint32_t)__shfl(pk, 5 + 2 * k(), 64), pc = (uint32_t)__shfl(pk, 6 + 2 * k(), 64);
+                    if (lane == j) {
+                        T.dl[k()] = a | (k() < 5 ? c2 << 16 : 0u);
+                        T.di[k()] = (pa & 0xffff) | (k() < 5 ? pc << 16 : 0u);
+                    }
+                });
                 if (lane == j) {
                     if (!ok) {
                         fail(E_TABLE);
                     } else {
-                        sfor<6>([&](auto k) {
-                            T.dl[k()] = S.lim[5 + 2 * k()] | (k() < 5 ? S.lim[6 + 2 * k()] << 16 : 0u);
-                            T.di[k()] = (S.lie[5 + 2 * k()] & 0xffff) | (k() < 5 ? S.lie[6 + 2 * k()] << 16 : 0u);
-                        });
+                        if (dfr) ((OGE_G uint32_t *)(xj + kXStart))[nt] = pos;  // the table's first position
+                        tabs = ((nt + 1) << 1) | dfr;
                         st = ST_SYM;
                     }
                 }
@@ -409,21 +457,25 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
             unsigned long long q = 0;
             if (lane == leader) q = atomicAdd(next, (unsigned long long)__popcll(want));
             q = ((unsigned long long)__shfl((unsigned)(q >> 32), (int)leader, 64) << 32) | (unsigned)__shfl((unsigned)q, (int)leader, 64);
-            b = b0 + q + (uint64_t)__popcll(want & ((1ull << lane) - 1));
+            if (st == ST_NEXT) b = (uint32_t)(b0 + q) + (uint32_t)__popcll(want & ((1ull << lane) - 1));
         }
         if (st == ST_NEXT) {
-            if (b >= b0 + nb) {
+            if ((uint64_t)b >= b0 + nb) {
                 st = ST_DONE;
             } else {
-                obase = out + uoff[b];
+                const uintptr_t ob = (uintptr_t)(out + uoff[b]);
                 osz = (uint32_t)(uoff[b + 1] - uoff[b]);
+                al = (uint32_t)(ob & 7);
+                ob8 = (OGE_G uint8_t *)(ob - al);
+                clast = (al + osz + 7) / 8 - 1;
                 pos = 0;
-                oc = ~0ull;
                 acc = 0;
-                bmp = (OGE_G uint64_t *)(bitmap + (b - b0) * 1024);
-                bm = 0;
+                bi = (uint32_t)(b - b0);
+                bm = lm = 0;
                 bw = 0;
-                d1bit = ((uint64_t)(uintptr_t)z + d1a[b]) * 8;
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                *(OGE_G u32x4 *)(xtab + (uint64_t)bi * kXTab + kXStart) = u32x4{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+                tabs = 0;
                 seek((uintptr_t)z + d0a[b]);
                 under = 0;
                 st = ST_HDR;
@@ -431,156 +483,174 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
         }
         if (__ballot(st != ST_DONE) == 0) break;
 
-        if (st == ST_SYM) {
-            refill();
-            const uint32_t v = (uint32_t)buf;
-            const uint32_t e = S.lt[v & ((1u << TL) - 1)][lane];
-            uint32_t sym, L;
-            if (e) {
-                sym = e & 511, L = e >> 9;
-            } else {  // code longer than TBL bits: canonical limits (VGPRs), symbol from the lane's list
-                const uint32_t c15 = __builtin_bitreverse32(v) >> 17;
-                L = 7;
-                sfor<4>([&](auto k) { L += (c15 >= (T.ll[k()] & 0xffff)) + (c15 >= (T.ll[k()] >> 16)); });
-                const uint32_t lie = pick(T.lie, L - 7);
-                const uint32_t k = ((lie & 0xffff) + (c15 >> (15 - L))) & 0xffff;
-#if OGE_EXP == 1  // timing experiment: a long literal's byte is not looked up (wrong output, same bit stream)
-                if (k < (lie >> 16)) sym = k & 255;
-                else sym = scr[S_LS + min(k, 287u)] + 256u;
-#else
-                sym = scr[S_LS + min(k, 287u)] + (k >= (lie >> 16) ? 256u : 0u);
-#endif
-                if (L == 15 && c15 >= T.l15) sym = 512;  // no such code
-            }
-            skip(L);
-            if (sym < 256) {
-                if (pos >= osz) {
-                    fail(E_OVERRUN);
-                } else {
-                    put(pos, sym, 1);
-                    ++pos;
-                    if (e) {  // more direct-table literals in this step (>= 26 bits left: three more)
-#pragma unroll
-                        for (int q = 1; q < LB; ++q) {
-                            const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
-                            if (!e2 || (e2 & 511) >= 256 || pos >= osz) break;
-                            skip(e2 >> 9);
-                            put(pos, e2 & 511, 1);
-                            ++pos;
-                        }
-                    }
-                }
-            } else if (sym == 256) {
-                if (fin) block_end();
-                else st = ST_HDR;
-            } else if (sym > 285) {
-                fail(sym == 512 ? E_CODE : E_LEN);
-            } else {
-                const uint32_t c = sym - 257;
-                const uint32_t ext = c < 8 ? 0u : c < 28 ? (c - 4) >> 2 : 0u;
-                const uint32_t base = c < 8 ? c + 3 : c < 28 ? ((4 + (c & 3)) << ext) + 3 : 258u;
-                const uint32_t len = base + get(ext);
+        // ---- kInner decode steps; a lane that reaches a wave-wide state (build, next block) idles
+        for (int it = 0; it < kInner; ++it) {
+            if (st == ST_SYM) {
                 refill();
-                const uint32_t w = (uint32_t)buf;
-                const uint32_t de = S.dt[w & ((1u << TD) - 1)][lane];
-                uint32_t ds, DL;
-                if (de) {
-                    ds = de & 31, DL = de >> 5;
-                } else {
-                    const uint32_t c15 = __builtin_bitreverse32(w) >> 17;
-                    DL = 5;
-                    sfor<5>([&](auto k) { DL += (c15 >= (T.dl[k()] & 0xffff)) + (c15 >= (T.dl[k()] >> 16)); });
-                    const uint32_t k = (u16of(T.di, DL - 5) + (c15 >> (15 - DL))) & 0xffff;
-                    ds = scr[S_DS + min(k, 31u)];
-                    if (DL == 15 && c15 >= (T.dl[5] & 0xffff)) ds = 31;  // no such code
+                const uint32_t v = (uint32_t)buf;
+                const uint32_t e = S.lt[v & ((1u << TL) - 1)][lane];
+                uint32_t sym, L;
+                if (e) {
+                    sym = e & 511, L = e >> 9;
+                } else {  // code longer than TL bits: canonical limits (VGPRs)
+                    const uint32_t c15 = __builtin_bitreverse32(v) >> 17;
+                    L = 7;
+                    sfor<4>([&](auto k) { L += (c15 >= (T.ll[k()] & 0xffff)) + (c15 >= (T.ll[k()] >> 16)); });
+                    const uint32_t pk = pick(T.pk, L - 7);
+                    const uint32_t k = ((pk & 0xffff) + (c15 >> (15 - L))) & 0xffff;
+                    const uint32_t litend = (pk >> 16) & 511;
+                    if (k < litend) {  // a literal: its byte later (phase 2), or now from the lane's scratch
+                        sym = (tabs & 1) ? kDefer | k : (uint32_t)scr()[S_LS + min(k, 287u)];
+                    } else {  // a length code or end of block: LDS
+                        sym = 256u + S.ll[min(k - litend + (pk >> 25), 31u)][lane];
+                    }
+                    if (L == 15 && c15 >= T.l15) sym = 512;  // no such code
                 }
-                skip(DL);
-                if (ds >= 30) {
-                    fail(E_DIST);
-                } else {
-                    const uint32_t dext = ds < 4 ? 0u : (ds - 2) >> 1;
-                    const uint32_t dist = (ds < 4 ? ds + 1 : ((2 + (ds & 1)) << dext) + 1) + get(dext);
-                    if (dist > pos || pos + len > osz) {
-                        fail(E_FAR);
+                skip(L);
+                if (sym < 256 || sym >= kDefer) {
+                    if (pos >= osz) {
+                        fail(E_OVERRUN);
                     } else {
-                        put(pos, (len - 3) | ((dist - 1) << 8), 3);  // descriptor in the hole's first bytes
-                        mark(pos);
-                        pos += len;
-                    }
-                }
-            }
-        } else if (st == ST_CL) {
-            refill();
-            const uint32_t e = ((const uint8_t *)&S.lt[0][0])[cl_at((uint32_t)buf & 127, lane)];
-            const uint32_t s = e & 31, L = e >> 5;
-            skip(L);
-            const uint32_t total = hlit + hdist;
-            uint32_t rep = 1, val = s;
-            if (!e) {
-                fail(E_CODE);
-            } else {
-                if (s == 16) rep = 3 + get(2), val = prev;
-                else if (s == 17) rep = 3 + get(3), val = 0;
-                else if (s == 18) rep = 11 + get(7), val = 0;
-                if ((s == 16 && ci == 0) || ci + rep > total) {
-                    fail(E_TABLE);
-                } else {
-                    if (val)  // zero runs need no stores: the buffer was zeroed by the CL build
-                        for (uint32_t k = 0; k < rep; ++k) scr[S_LENS + ci + k] = (uint8_t)val;
-                    if (ci <= 256 && 256 < ci + rep) l256 = val;
-                    prev = val;
-                    ci += rep;
-                    if (ci == total) {
-                        if (!l256) fail(E_TABLE);  // no end-of-block code
-                        else st = ST_BLD;
-                    }
-                }
-            }
-        } else if (st == ST_HDR) {
-            refill();
-            const uint32_t h = get(3);
-            fin = h & 1;
-            const uint32_t type = h >> 1;
-            if (type == 0) {
-                skip((8 - (uint32_t)(bitpos() & 7)) & 7);
-                refill();
-                const uint32_t len = get(16), nlen = get(16);
-                if ((len ^ 0xffffu) != nlen) fail(E_STORED);
-                else if (pos + len > osz) fail(E_OVERRUN);
-                else srem = len, st = ST_STORED;
-            } else if (type == 1) {
-                fixed = 1, hlit = 288, hdist = 30, st = ST_BLD;
-            } else if (type == 2) {
-                hlit = get(5) + 257;
-                hdist = get(5) + 1;
-                const uint32_t hclen = get(4) + 4;
-                if (hlit > 286 || hdist > 30) {
-                    fail(E_TABLE);
-                } else {
-                    uint64_t clp = 0;
+                        if (sym >= kDefer) {
+                            word(pos);
+                            lm |= 1ull << (pos & 63);
+                        }
+                        put(sym);
+                        if (e) {  // more direct-table literals in this step (>= 26 bits left: three more)
 #pragma unroll
-                    for (int i = 0; i < 19; ++i) {
-                        if ((uint32_t)i < hclen) {
-                            refill();
-                            clp |= (uint64_t)get(3) << (3 * kClOrd[i]);
+                            for (int q = 1; q < LB; ++q) {
+                                const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
+                                if (!e2 || (e2 & 511) >= 256 || pos >= osz) break;
+                                skip(e2 >> 9);
+                                put(e2 & 511);
+                            }
                         }
                     }
-                    S.clp[lane] = clp;
-                    fixed = 0;
-                    st = ST_BCL;
+                } else if (sym == 256) {
+                    if (flg & 1) block_end();
+                    else st = ST_HDR;
+                } else if (sym > 285) {
+                    fail(sym == 512 ? E_CODE : E_LEN);
+                } else {
+                    const uint32_t c = sym - 257;
+                    const uint32_t ext = c < 8 ? 0u : c < 28 ? (c - 4) >> 2 : 0u;
+                    const uint32_t base = c < 8 ? c + 3 : c < 28 ? ((4 + (c & 3)) << ext) + 3 : 258u;
+                    const uint32_t len = base + get(ext);
+                    refill();
+                    const uint32_t w = (uint32_t)buf;
+                    const uint32_t de = S.dt[w & ((1u << TD) - 1)][lane];
+                    uint32_t ds, DL;
+                    if (de) {
+                        ds = de & 31, DL = de >> 5;
+                    } else {
+                        const uint32_t c15 = __builtin_bitreverse32(w) >> 17;
+                        DL = 5;
+                        sfor<5>([&](auto k) { DL += (c15 >= (T.dl[k()] & 0xffff)) + (c15 >= (T.dl[k()] >> 16)); });
+                        const uint32_t k = (u16of(T.di, DL - 5) + (c15 >> (15 - DL))) & 0xffff;
+                        ds = S.dl[min(k, 29u)][lane];
+                        if (DL == 15 && c15 >= (T.dl[5] & 0xffff)) ds = 31;  // no such code
+                    }
+                    skip(DL);
+                    if (ds >= 30) {
+                        fail(E_DIST);
+                    } else {
+                        const uint32_t dext = ds < 4 ? 0u : (ds - 2) >> 1;
+                        const uint32_t dist = (ds < 4 ? ds + 1 : ((2 + (ds & 1)) << dext) + 1) + get(dext);
+                        if (dist > pos || pos + len > osz) {
+                            fail(E_FAR);
+                        } else {
+                            word(pos);
+                            bm |= 1ull << (pos & 63);
+                            const uint32_t dsc = (len - 3) | ((dist - 1) << 8);  // descriptor in the hole's first bytes
+                            put(dsc);
+                            put(dsc >> 8);
+                            put(dsc >> 16);
+                            // the rest of the hole: the shift register moves on with it (a chunk it leaves
+                            // half-written is stored now; hole bytes are don't-care)
+                            const uint32_t q = pos + al, qe = q + len - 3;
+                            if ((qe >> 3) == (q >> 3)) {
+                                acc >>= 8 * (qe - q);
+                            } else {
+                                flush_partial();
+                            }
+                            pos += len - 3;
+                        }
+                    }
                 }
-            } else {
-                fail(E_TYPE);
-            }
-        } else if (st == ST_STORED) {
-            refill();
-            const uint32_t k = min(srem, 4u);
-            for (uint32_t i = 0; i < k; ++i) put(pos + i, get(8), 1);
-            pos += k;
-            srem -= k;
-            if (!srem) {
-                if (fin) block_end();
-                else st = ST_HDR;
+            } else if (st == ST_CL) {
+                refill();
+                const uint32_t e = ((const uint8_t *)&S.lt[0][0])[cl_at((uint32_t)buf & 127, lane)];
+                const uint32_t s = e & 31, L = e >> 5;
+                skip(L);
+                const uint32_t total = (hl & 0xffff) + (hl >> 16);
+                uint32_t ci = aux & 0xffff, prev = (aux >> 16) & 0xff, l256 = aux >> 24;
+                uint32_t rep = 1, val = s;
+                if (!e) {
+                    fail(E_CODE);
+                } else {
+                    if (s == 16) rep = 3 + get(2), val = prev;
+                    else if (s == 17) rep = 3 + get(3), val = 0;
+                    else if (s == 18) rep = 11 + get(7), val = 0;
+                    if ((s == 16 && ci == 0) || ci + rep > total) {
+                        fail(E_TABLE);
+                    } else {
+                        if (val)  // zero runs need no stores: the buffer was zeroed by the CL build
+                            for (uint32_t k = 0; k < rep; ++k) scr()[S_LENS + ci + k] = (uint8_t)val;
+                        if (ci <= 256 && 256 < ci + rep) l256 = val;
+                        prev = val;
+                        ci += rep;
+                        aux = ci | (prev << 16) | (l256 << 24);
+                        if (ci == total) {
+                            if (!l256) fail(E_TABLE);  // no end-of-block code
+                            else st = ST_BLD;
+                        }
+                    }
+                }
+            } else if (st == ST_HDR) {
+                refill();
+                const uint32_t h = get(3);
+                flg = h & 1;
+                const uint32_t type = h >> 1;
+                if (type == 0) {
+                    skip((8 - (uint32_t)(bitpos() & 7)) & 7);
+                    refill();
+                    const uint32_t len = get(16), nlen = get(16);
+                    if ((len ^ 0xffffu) != nlen) fail(E_STORED);
+                    else if (pos + len > osz) fail(E_OVERRUN);
+                    else aux = len, st = ST_STORED;
+                } else if (type == 1) {
+                    flg |= 2, hl = 288 | (30 << 16), st = ST_BLD;
+                } else if (type == 2) {
+                    const uint32_t hlit = get(5) + 257;
+                    const uint32_t hdist = get(5) + 1;
+                    hl = hlit | (hdist << 16);
+                    const uint32_t hclen = get(4) + 4;
+                    if (hlit > 286 || hdist > 30) {
+                        fail(E_TABLE);
+                    } else {
+                        uint64_t c = 0;
+#pragma unroll
+                        for (int i = 0; i < 19; ++i) {
+                            if ((uint32_t)i < hclen) {
+                                refill();
+                                c |= (uint64_t)get(3) << (3 * kClOrd[i]);
+                            }
+                        }
+                        *(OGE_G uint64_t *)(scr() + S_CLP) = c;
+                        st = ST_BCL;
+                    }
+                } else {
+                    fail(E_TYPE);
+                }
+            } else if (st == ST_STORED) {
+                refill();
+                const uint32_t k = min(aux, 4u);
+                for (uint32_t i = 0; i < k; ++i) put(get(8));
+                aux -= k;
+                if (!aux) {
+                    if (flg & 1) block_end();
+                    else st = ST_HDR;
+                }
             }
         }
     }
@@ -596,7 +666,8 @@ constexpr uint32_t kT2 = 1024;
 
 __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, const uint64_t *__restrict__ uoff,
                                                  const uint32_t *__restrict__ crc, const uint64_t *__restrict__ bitmap,
-                                                 uint64_t b0, const uint32_t *__restrict__ zpow, uint32_t *__restrict__ err) {
+                                                 const uint8_t *__restrict__ xtab, uint64_t b0, const uint32_t *__restrict__ zpow,
+                                                 uint32_t *__restrict__ err) {
     __shared__ __align__(16) uint16_t refs[kSlot + 16];  // later the block's bytes (img)
     __shared__ uint32_t crctab[4][256];
     __shared__ uint32_t zp[17][32];
@@ -635,10 +706,16 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     }
     __syncthreads();
     // 3. holes: refs[p + j] = p - D + j, descriptors read from this thread's window registers
-    const OGE_G uint64_t *bmp = (const OGE_G uint64_t *)(bitmap + (b - b0) * 1024);
+    const OGE_G uint64_t *bmp = (const OGE_G uint64_t *)(bitmap + (b - b0) * 2048);
     const uint32_t nw = (osz + 63) >> 6;
+    uint64_t dm = 0;  // this window's deferred literals
     {
-        uint64_t m = t < nw ? bmp[t] : 0;
+        uint64_t m = 0;
+        if (t < nw) {
+            typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+            const u64x2 hv = *(const OGE_G u64x2 *)(bmp + 2 * t);
+            m = hv.x, dm = hv.y;
+        }
         while (m) {
             const uint32_t jb = (uint32_t)__builtin_ctzll(m);  // byte in the window
             m &= m - 1;
@@ -725,6 +802,19 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     auto ib = [](uint32_t q) { return q + ((q >> 6) << 2); };
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) img32[17 * t + k] = wv[k];
+    // deferred literals of this window: the byte phase 1 wrote is the code's index in its table's
+    // canonical long-code list; the table is the last one whose first position is <= the literal's
+    if (dm) {
+        const OGE_G uint8_t *xb = (const OGE_G uint8_t *)(xtab + (b - b0) * kXTab);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 xs = *(const OGE_G u32x4 *)(xb + kXStart);
+        while (dm) {
+            const uint32_t p = q0 + (uint32_t)__builtin_ctzll(dm);
+            dm &= dm - 1;
+            const uint32_t tb = (p >= xs.w ? 3u : p >= xs.z ? 2u : p >= xs.y ? 1u : 0u);
+            img[ib(p)] = xb[tb * kXList + img[ib(p)]];
+        }
+    }
     __syncthreads();
     // 6. every copied byte from its root (a literal position of the image); literal-only chunks are
     //    already in place
@@ -787,26 +877,29 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     }();
     // persistent lanes (the 12 resident waves per CU) take blocks from a queue; a chunk is at most 4
     // blocks per lane (the queue keeps the lanes busy, so a larger chunk gains nothing: 300M reads = 2
-    // launches, a 6.4 GB bitmap workspace that lives as long as the context), and no more than a
-    // quarter of the free device memory holds bitmaps for (8 KiB per block), at least one block per lane
+    // launches, a 14 GB workspace that lives as long as the context), and no more than a quarter of the
+    // free device memory holds bitmaps and lists for (17.3 KiB per block), at least one block per lane
     const uint64_t lanes = (uint64_t)ncu * 4 * kWps * 64;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
-    const uint64_t budget = std::max<uint64_t>(lanes, std::min<uint64_t>(4 * lanes, (uint64_t)(fr / 4) / (1024 * 8)));
+    constexpr uint64_t kPerBlk = 2048 * 8 + kXTab;  // bitmaps + translation lists
+    const uint64_t budget = std::max<uint64_t>(lanes, std::min<uint64_t>(4 * lanes, (uint64_t)(fr / 4) / kPerBlk));
     const uint64_t nchunks = std::max<uint64_t>(1, (nblk + budget - 1) / budget);
     const uint64_t chunk = std::max<uint64_t>(1, (nblk + nchunks - 1) / nchunks);
     const uint64_t wgs = std::min<uint64_t>((chunk + 63) / 64, lanes / 64);
-    uint64_t *bitmap = (uint64_t *)ctx->ws("infl_bitmap", chunk * 1024 * 8);
+    uint64_t *bitmap = (uint64_t *)ctx->ws("infl_bitmap", chunk * 2048 * 8);
+    uint8_t *xtab = (uint8_t *)ctx->ws("infl_xtab", chunk * kXTab);
     uint8_t *scr = (uint8_t *)ctx->ws("infl_scratch", wgs * 64 * kScr);
     unsigned long long *next = (unsigned long long *)ctx->ws("infl_next", 8);
-    if (!bitmap || !scr || !next) return OGE_ERR_HIP;
+    if (!bitmap || !xtab || !scr || !next) return OGE_ERR_HIP;
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
         const uint64_t nb = std::min(chunk, nblk - b0);
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
         OGE_HIP_TRY(ctx, hipMemsetAsync(next, 0, 8, ctx->stream));
-        k_infl_huff<<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, scr, err, next);
+        OGE_HIP_TRY(ctx, hipMemsetAsync(bitmap, 0, nb * 2048 * 8, ctx->stream));  // phase 1 stores only words with bits
+        k_infl_huff<<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, xtab, scr, err, next);
         OGE_LAUNCH_CHECK(ctx);
-        k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, b0, zpow, err);
+        k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, xtab, b0, zpow, err);
         OGE_LAUNCH_CHECK(ctx);
     }
     return OGE_OK;

@@ -162,3 +162,64 @@ def test_fix_bins_and_drop_flagged(ctx):
     keep = np.nonzero(~dup)[0]
     want = b"".join(recs[offs[i]:offs[i + 1]].tobytes() for i in keep)
     assert got == want
+
+
+def _fib_bytes(n, seed):
+    """bytes whose frequencies follow the Fibonacci numbers (22 symbols): plain Huffman depths reach ~21,
+    so the 15-bit limit, the clamp and the Kraft repair of the GPU's length builder all run"""
+    f, a, b = [], 1, 1
+    for _ in range(22):
+        f.append(a)
+        a, b = b, a + b
+    sym = np.repeat(np.arange(22, dtype=np.uint8) * 7 + 3, f)
+    rng = np.random.default_rng(seed)
+    return bytes(rng.permutation(np.resize(sym, n)))
+
+
+HUFF_CASES = {
+    "c2_records": lambda: _bam_bytes(6_000),
+    "fibonacci": lambda: _fib_bytes(3 * PAY, 1),
+    "geometric": lambda: bytes(np.minimum(np.random.default_rng(7).geometric(0.18, 2 * PAY), 255).astype(np.uint8)),
+    "runs": lambda: CASES["runs"],
+    "short_text": lambda: CASES["short_text"],
+}
+
+
+@pytest.mark.parametrize("name", sorted(HUFF_CASES))
+def test_deflate_header_equals_restated_builder(ctx, name):
+    """every dynamic block's transmitted code lengths (literal/length, distance and
+    code-length code) equal the CPU restatement of k_defl_huff (tests/deflate_parse.py) applied to the
+    symbol counts the block's body uses -- the length-limited two-queue Huffman with Kraft repair pinned
+    independently of round trips."""
+    import deflate_parse as DP
+    data = HUFF_CASES[name]()
+    z = ctx.bgzf_deflate(data, 6)
+    n_dyn = 0
+    for payload, body in check_roundtrip(data, z):
+        blocks = DP.parse_block(body)
+        assert blocks[-1]["out"] == payload
+        for b in blocks:
+            if b["type"] != 2:
+                continue
+            n_dyn += 1
+            lit, dist, cl = DP.header_lengths(b["lit_count"], b["dist_count"])
+            assert b["lit"] == lit and b["dist"] == dist and b["cl"] == cl
+    assert n_dyn > 0
+
+
+def test_deflate_bytes_pinned(ctx):
+    """The GPU deflate's exact output bytes on a fixed input (the C2 generator, 20,000 pairs, seed 99 --
+    the c2_20k golden set -- as one record stream, level 6) against a committed sha256
+    (tests/golden/deflate_sha.json, written by tools/deflate_sha.py on the GPU box): "same bytes" claims
+    about deflate changes are this test."""
+    import hashlib
+    import json
+    from pathlib import Path
+    from openge_amd import lib as L
+    p = L.synth_params(20_000, preset="c2", seed=99)
+    recs, offs, _ = L.synth_host(p)
+    data = recs[:int(offs[-1])].tobytes()
+    z = ctx.bgzf_deflate(data, 6)
+    want = json.loads((Path(__file__).parent / "golden" / "deflate_sha.json").read_text())
+    assert len(data) == want["input_bytes"]
+    assert len(z) == want["output_bytes"] and hashlib.sha256(z).hexdigest() == want["sha256"]

@@ -269,7 +269,13 @@ def test_300m_bgzf_chain_equals_kernel_path():
         assert ctx.bgzf_index_dev(d, ob, d0.data_ptr(), d1.data_ptr(), uo.data_ptr(), crc.data_ptr(), nblk) == nblk
         ctx.sync()
         uoh = uo.cpu().numpy()
+        d0h, d1h = d0.cpu().numpy(), d1.cpu().numpy()
         total = int(uoh[nblk])
+        # an independent decoder on a deterministic sample: >= 1,000 of the output
+        # file's blocks are inflated by host zlib and compared with the GPU inflate's window
+        stride = max(1, nblk // 1200)
+        sample = set(range(0, nblk, stride)) | {nblk - 1}
+        zchecked = 0
         win = torch.empty((4 << 30) + 65536, dtype=torch.uint8, device="cuda")
         got, q, b0 = [0, 0], None, 0
         while b0 < nblk:
@@ -282,6 +288,15 @@ def test_300m_bgzf_chain_equals_kernel_path():
                                                  win.data_ptr() - int(uoh[b0])), ctx.h)
             ctx.sync()
             u0, u1 = int(uoh[b0]), int(uoh[b1])
+            import zlib
+            for b in sorted(x for x in sample if b0 <= x < b1):
+                zb_ = int(d1h[b] - d0h[b])
+                raw = np.empty(zb_, np.uint8)
+                L.check(L.lib().oge_memcpy(ctx.h, raw.ctypes.data, d + int(d0h[b]), zb_, 2), ctx.h)
+                ref = zlib.decompress(raw.tobytes(), -15)
+                assert len(ref) == int(uoh[b + 1] - uoh[b]), b
+                assert win[int(uoh[b]) - u0:int(uoh[b + 1]) - u0].cpu().numpy().tobytes() == ref, f"block {b}"
+                zchecked += 1
             if q is None:  # the header: magic, text, reference list
                 hv = win[:min(u1 - u0, 1 << 20)].cpu().numpy().tobytes()
                 (lt,) = struct.unpack_from("<i", hv, 4)
@@ -296,6 +311,7 @@ def test_300m_bgzf_chain_equals_kernel_path():
                 _byte_checksum(win[lo - u0:u1 - u0], lo - q, got)
             b0 = b1
         assert total - q == B
+        assert zchecked >= 1000
         assert got == want, "the BGZF chain's records differ from the kernel path's"
     finally:
         ctx.close()

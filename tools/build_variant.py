@@ -2,6 +2,7 @@
 recompiled with extra defines, e.g.
 
     python tools/build_variant.py nolonglit inflate_lane.hip -DOGE_EXP=1
+    python tools/build_variant.py r03 inflate_lane.hip=openge_amd/_var/inflate_lane_r03.hip
 
 tools/diag_infl.py <path to .so> then times the inflate stage with it.  The _var directory is git-ignored
 and deleted when the experiment is recorded."""
@@ -14,11 +15,15 @@ sys.path.insert(0, str(ROOT))
 from openge_amd import build as B  # noqa: E402
 
 name, src, *defs = sys.argv[1:]
+# src: a file in openge_amd/csrc (recompiled with defs), or SRC=PATH:a replacement for that file
+repl = None
+if "=" in src:
+    src, repl = src.split("=", 1)
 B.build()
 var = ROOT / "openge_amd" / "_var"
 var.mkdir(exist_ok=True)
 obj = var / f"{Path(src).stem}_{name}.o"
-subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-x", "hip", *B.COMMON, *defs, f"-I{B.CSRC}", "-c", str(B.CSRC / src),
+subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-x", "hip", *B.COMMON, *defs, f"-I{B.CSRC}", "-c", repl or str(B.CSRC / src),
                 "-o", str(obj)], check=True)
 objs = [str(B.BUILD / (s + ".o")) for s in B.HIP_SRCS if s != src]
 objs += [str(B.BUILD / (s + ".o")) for s in B.HOST_SRCS]
