@@ -108,12 +108,20 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
 // offset in the segment << 23 | (length - 3) << 15 | (distance - 1).  About 8 B per payload byte less
 // than a token per symbol (r02: 4-byte tokens written here and read twice by the emitter).
 constexpr int kMaxM = 21;   // matches per 64-byte segment (each >= 3 bytes)
-constexpr int kR = 2;       // positions per thread per candidate round (r02: R = 1 / 2 / 4 -> ratio 0.6991 /
-                            // 0.7007 / 0.7030, 70.0 / 72.2 / 72.5 GB/s at 20M reads)
+#ifndef OGE_DEFL_TP
+#define OGE_DEFL_TP 1024
+#endif
+// parse workgroup: 1024 threads (r04: 16 waves per CU instead of 8 hide the candidate rounds' chains of
+// dependent LDS reads and their barriers; the same rounds of 1024 positions, so the same bytes: 20M reads
+// 42.6 -> 37.8 ms); threads >= kT only take part in the staging and the candidate rounds
+constexpr int kTP = OGE_DEFL_TP;  // a candidate round is kR * kTP = 1024 positions
+constexpr int kR = 1024 / kTP;    // positions per thread per candidate round (r02: rounds of 512 / 1024 / 2048
+                                  // positions -> ratio 0.6991 / 0.7007 / 0.7030)
+static_assert(kR * kTP == 1024 && kTP >= kT, "round size and segment threads");
 
 __device__ __forceinline__ uint64_t bits_below(uint32_t q) { return q >= 64 ? ~0ull : ((1ull << q) - 1); }
 
-__global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
+__global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
                                                    uint64_t *__restrict__ lmask, uint8_t *__restrict__ nmatch,
                                                    uint32_t *__restrict__ mlist, uint32_t *__restrict__ freq_out) {
     __shared__ __align__(16) uint32_t in[kPay / 4 + 4];
@@ -126,9 +134,9 @@ __global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ s
     const uint64_t start = blk * kPay;
     const uint32_t len = (uint32_t)min<uint64_t>(kPay, n - start);
 
-    stage_words<kT>(in, src + start, len, t);
-    for (int i = t; i < (1 << kHashBits); i += kT) htab[i] = 0;
-    for (int i = t; i < kFreq; i += kT) freq[i] = 0;
+    stage_words<kTP>(in, src + start, len, t);
+    for (int i = t; i < (1 << kHashBits); i += kTP) htab[i] = 0;
+    for (int i = t; i < kFreq; i += kTP) freq[i] = 0;
     __syncthreads();
 
     const uint64_t seg_base = (uint64_t)blockIdx.x * kNSeg;
@@ -136,19 +144,18 @@ __global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ s
         const uint32_t base = sub * kSub;
         const uint64_t sg = seg_base + (uint64_t)sub * kT + t;  // this thread's segment, stream order
         if (base >= len) {
-            lmask[sg] = 0;
-            nmatch[sg] = 0;
+            if (t < kT) lmask[sg] = 0, nmatch[sg] = 0;
             continue;
         }
         const uint32_t end = min(len, base + kSub);
         // candidates, one round of kR * kT consecutive positions at a time
-        for (uint32_t r = base; r < end; r += kR * kT) {
+        for (uint32_t r = base; r < end; r += kR * kTP) {
             // the kR lookup chains (prefix word -> bucket -> candidate's word) of a thread run side by side;
             // the ballots come after all of them (a ballot between them would serialise the chains)
             uint32_t hh[kR], cc[kR];
 #pragma unroll
             for (int k = 0; k < kR; ++k) {
-                const uint32_t p = r + k * kT + t;
+                const uint32_t p = r + k * kTP + t;
                 uint32_t h = 0, c = 0;
                 if (p + 4 <= len) {
                     const uint32_t w = ld32(in, p);
@@ -161,15 +168,15 @@ __global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ s
             }
 #pragma unroll
             for (int k = 0; k < kR; ++k) {
-                const uint32_t p = r + k * kT + t, c = cc[k];
+                const uint32_t p = r + k * kTP + t, c = cc[k];
                 const uint64_t m = __ballot(c != 0 && p < end);
                 if (p < end) cand[p - base] = (uint16_t)c;
-                if (lane == 0 && r + k * kT + 64 * wv < end) cmask[(r + k * kT + 64 * wv - base) >> 6] = m;
+                if (lane == 0 && r + k * kTP + 64 * wv < end) cmask[(r + k * kTP + 64 * wv - base) >> 6] = m;
             }
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < kR; ++k) {
-                const uint32_t p = r + k * kT + t;
+                const uint32_t p = r + k * kTP + t;
                 if (p + 4 <= len && p < end) atomicMax(&htab[hh[k]], p + 1);
             }
             __syncthreads();
@@ -178,7 +185,7 @@ __global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ s
         const uint32_t s0 = base + t * kSeg, s1 = min(end, s0 + kSeg);
         uint64_t lit = 0;
         uint32_t nm = 0;
-        if (s0 < s1) {
+        if (t < kT && s0 < s1) {
             const uint32_t sl = s1 - s0;
             const uint64_t cm = cmask[t] & bits_below(sl);
             uint32_t *mp = mlist + ((uint64_t)blockIdx.x * kMaxM) * kNSeg + (uint64_t)sub * kT + t;
@@ -230,11 +237,10 @@ __global__ void __launch_bounds__(kT) k_defl_parse(const uint8_t *__restrict__ s
                     if ((lit >> (16 * w4 + k)) & 1) atomicAdd(&freq[(ww[k >> 2] >> (8 * (k & 3))) & 0xff], 1u);
             }
         }
-        lmask[sg] = lit;
-        nmatch[sg] = (uint8_t)nm;
+        if (t < kT) lmask[sg] = lit, nmatch[sg] = (uint8_t)nm;
         __syncthreads();  // cand / cmask are reused by the next sub-block
     }
-    for (int i = t; i < kFreq; i += kT) freq_out[(uint64_t)blockIdx.x * kFreq + i] = freq[i];
+    for (int i = t; i < kFreq; i += kTP) freq_out[(uint64_t)blockIdx.x * kFreq + i] = freq[i];
 }
 
 // ------------------------------------------------------------------------------------ Huffman
@@ -954,7 +960,7 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk, ++k) {
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
         Bufs &u = B[k % S];
-        k_defl_parse<<<nb, kT, 0, u.st>>>(d_src, n, b0, u.lmask, u.nmatch, u.mlist, u.freq);
+        k_defl_parse<<<nb, kTP, 0, u.st>>>(d_src, n, b0, u.lmask, u.nmatch, u.mlist, u.freq);
         OGE_LAUNCH_CHECK(ctx);
         k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs, n, b0, level, u.sizes);
         OGE_LAUNCH_CHECK(ctx);

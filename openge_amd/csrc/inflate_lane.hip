@@ -208,15 +208,15 @@ __device__ bool wbuild(P1Lds &S, uint32_t j, OGE_G uint8_t *list, OGE_G uint8_t 
 }
 
 // ---------------------------------------------------------------------------- phase 1
-// A step decodes one whole symbol (a match's length and distance codes in the same step).  A literal
-// decoded from the direct table may be followed, in the same step, by up to LB - 1 more literals whose
-// codes also sit in the direct table: a step starts with >= 32 bits in the buffer (refill tops up to
-// 32..64), a direct code takes <= TL = 6 bits, so 4 direct codes (<= 24 bits) always fit.  Not after a
-// long (7..15-bit) code: 15 + 3 * 6 = 33 > 32 (r02 commit 3941758 allowed it and corrupted a block at
-// 300M reads; tests/test_gpu_inflate.py::test_long_codes_before_direct_literal_runs pins it).  A wave's
-// step count is the maximum over its 64 blocks' symbol counts, so literal runs (BAM qualities, bases)
-// take fewer steps: 300M reads in the chain, LB = 1 / 2 / 4 -> 1152 / 941 / 792 ms
-// (profiles/r02s3_infl_litb.json).
+// An iteration (ST_SYM) decodes up to LB literals from the direct table, then one symbol of any kind (a
+// long-code literal, end of block, or a match with its length and distance codes), then up to LB direct
+// literals again; every part starts with a refill, which leaves >= 32 bits in the buffer: LB = 4 direct
+// codes take <= 24 bits, a literal/length code + its extra bits <= 20, a distance code + its extra bits
+// <= 28.  (r02 commit 3941758 let a batch follow a long code without a refill -- 15 + 3 * 6 = 33 > 32 --
+// and corrupted a block at 300M reads; tests/test_gpu_inflate.py::test_long_codes_before_direct_literal_runs
+// pins it.)  A wave's iteration count is the maximum over its 64 blocks, and it runs the union of their
+// paths, so a lane makes as much progress per iteration as the union costs: C2 BGZF blocks take 11.5k
+// iterations of this shape instead of 19.8k one-symbol-or-literal-batch steps (r03).
 // Bit-budget guard (always on): every skip of more bits than the buffer holds sets `under`, and the
 // block fails with E_BITS instead of decoding from zero bits.
 // Output: bytes go through a 64-bit shift register (the newest byte enters at the top) that is stored
@@ -235,29 +235,44 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
     const uint32_t lane = threadIdx.x;
     auto scr = [&]() { return (OGE_G uint8_t *)(scratch + ((uint64_t)blockIdx.x * 64 + threadIdx.x) * kScr); };  // lens / list
     const uintptr_t zend = (uintptr_t)z + zbytes;
+    const uintptr_t zlast = (zend - 1) & ~(uintptr_t)15;  // the stream's last 16-byte chunk
 
     // input: 64-bit bit buffer + two 16-byte chunks (q being consumed, p loaded ahead)
     uint64_t buf = 0;
     uint32_t under = 0;  // a skip past the buffered bits happened in this block (the guard)
-    uint32_t cnt = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0, p0 = 0, p1 = 0, p2 = 0, p3 = 0, qn = 0;
+    // q: the chunk being consumed (q.x next), p: the next chunk, loaded ahead.  Both are 4-register tuples:
+    // a load lands in p's own registers (four scalar u32s made the compiler load into a temporary tuple
+    // and copy it out at once -- a wait for the load right where it was issued)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 q = {0, 0, 0, 0}, p = {0, 0, 0, 0};
+    uint32_t cnt = 0, qn = 0;
     uintptr_t cp = 0;
-    auto load16 = [&](uintptr_t a, uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t &x3) {
-        if (a < zend) {  // a 16-byte aligned chunk holding at least one stream byte never leaves its page
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 v = *(const OGE_G u32x4 *)a;
-            x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
-        } else {
-            x0 = x1 = x2 = x3 = 0;
-        }
-    };
+    // A 16-byte aligned chunk holding at least one stream byte never leaves its page; past the end the
+    // last chunk is loaded again (only a corrupt stream reads those bits, and it fails E_PAST / E_BITS).
+    // No branch around the load: a value merged after a branch is waited for on the spot, and the
+    // prefetch one chunk ahead would wait for its HBM round trip -- and, vmcnt counting stores too, for
+    // every output store in flight -- at every fourth refill.
+    auto load16 = [&](uintptr_t a) { return *(const OGE_G u32x4 *)(a < zend ? a : zlast); };
+#if OGE_EXP == 2  // timing experiment: cycles spent taking the prefetched chunk (its wait) vs the decode loop
+    uint64_t x_wait = 0, x_loop = 0, x_steps = 0;
+#endif
     auto refill = [&]() {
         if (cnt <= 32) {
-            buf |= (uint64_t)q0 << cnt;
+            buf |= (uint64_t)q.x << cnt;
             cnt += 32;
-            q0 = q1, q1 = q2, q2 = q3;
+            q.x = q.y, q.y = q.z, q.z = q.w;
             if (--qn == 0) {
-                q0 = p0, q1 = p1, q2 = p2, q3 = p3, qn = 4;
-                load16(cp, p0, p1, p2, p3);
+#if OGE_EXP == 2
+                const uint64_t c0 = __builtin_readcyclecounter();
+                q = p, qn = 4;
+                __asm__ volatile("" ::"v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w));
+                x_wait += __builtin_readcyclecounter() - c0;
+#else
+                q = p, qn = 4;
+                // q takes p's values before the next load is issued, so the load can land in p's registers
+                __asm__ volatile("" : "+v"(q.x), "+v"(q.y), "+v"(q.z), "+v"(q.w)::"memory");
+#endif
+                p = load16(cp);
                 cp += 16;
             }
         }
@@ -275,11 +290,11 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
     auto bitpos = [&]() -> uint64_t { return (uint64_t)(cp - 16 - 4 * qn) * 8 - cnt; };
     auto seek = [&](uintptr_t a) {  // start reading at byte address a
         const uintptr_t al = a & ~(uintptr_t)15;
-        load16(al, q0, q1, q2, q3);
-        load16(al + 16, p0, p1, p2, p3);
+        q = load16(al);
+        p = load16(al + 16);
         cp = al + 32;
         qn = 4;
-        for (uint32_t k = 0; k < (uint32_t)((a - al) >> 2); ++k) q0 = q1, q1 = q2, q2 = q3, --qn;
+        for (uint32_t k = 0; k < (uint32_t)((a - al) >> 2); ++k) q.x = q.y, q.y = q.z, q.z = q.w, --qn;
         buf = 0;
         cnt = 0;
         refill();
@@ -312,6 +327,19 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
     auto flush_partial = [&]() {  // the chunk holding the last byte put, when it is not complete
         const uint32_t q = pos + al;
         if (q & 7) store_chunk(q >> 3, acc >> (8 * (8 - (q & 7))));
+    };
+    // Up to LB literals whose codes sit in the direct table (sym < 256: bit 8 of the entry clear).  After
+    // the refill >= 32 bits are buffered and LB direct codes take <= 24, so no budget check is needed.
+    auto lit_batch = [&]() {
+        refill();
+#pragma unroll
+        for (int k = 0; k < LB; ++k) {
+            const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
+            if (!e2 || (e2 & 0x100) || pos >= osz) break;
+            buf >>= e2 >> 9;
+            cnt -= e2 >> 9;
+            put(e2 & 0xff);
+        }
     };
     // hole and deferred-literal bitmaps of the block (1024 word pairs per block of the chunk)
     uint64_t bm = 0, lm = 0;
@@ -481,11 +509,30 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 st = ST_HDR;
             }
         }
-        if (__ballot(st != ST_DONE) == 0) break;
+        if (__ballot(st != ST_DONE) == 0) {
+#if OGE_EXP == 2
+            uint64_t w = x_wait;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) w = max(w, (uint64_t)__shfl_xor((unsigned long long)w, d, 64));
+            if (lane == 0 && blockIdx.x < 8)
+                printf("infl-exp wave %u: loop cycles %llu, steps %llu, max lane wait cycles %llu\n", blockIdx.x,
+                       (unsigned long long)x_loop, (unsigned long long)x_steps, (unsigned long long)w);
+#endif
+            break;
+        }
 
         // ---- kInner decode steps; a lane that reaches a wave-wide state (build, next block) idles
+#if OGE_EXP == 2
+        const uint64_t l0 = __builtin_readcyclecounter();
+        x_steps += kInner;
+#endif
         for (int it = 0; it < kInner; ++it) {
             if (st == ST_SYM) {
+                // an iteration: up to LB direct literals, one symbol of any kind, up to LB direct literals.
+                // A wave runs the union of its lanes' paths, so a lane should make as much progress per
+                // iteration as the union costs: a match and the literals around it in one pass (C2 blocks:
+                // 11.5k iterations per BGZF block instead of 19.8k one-symbol steps; tools/ana policy)
+                lit_batch();
                 refill();
                 const uint32_t v = (uint32_t)buf;
                 const uint32_t e = S.lt[v & ((1u << TL) - 1)][lane];
@@ -516,15 +563,6 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                             lm |= 1ull << (pos & 63);
                         }
                         put(sym);
-                        if (e) {  // more direct-table literals in this step (>= 26 bits left: three more)
-#pragma unroll
-                            for (int q = 1; q < LB; ++q) {
-                                const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
-                                if (!e2 || (e2 & 511) >= 256 || pos >= osz) break;
-                                skip(e2 >> 9);
-                                put(e2 & 511);
-                            }
-                        }
                     }
                 } else if (sym == 256) {
                     if (flg & 1) block_end();
@@ -577,6 +615,7 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                         }
                     }
                 }
+                if (st == ST_SYM) lit_batch();
             } else if (st == ST_CL) {
                 refill();
                 const uint32_t e = ((const uint8_t *)&S.lt[0][0])[cl_at((uint32_t)buf & 127, lane)];
@@ -653,6 +692,9 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 }
             }
         }
+#if OGE_EXP == 2
+        x_loop += __builtin_readcyclecounter() - l0;
+#endif
     }
 }
 

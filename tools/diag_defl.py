@@ -1,4 +1,7 @@
-"""Diagnostic: run the GPU deflate of a 2M-read C2 stream with an alternative library build (argv[1])."""
+"""Diagnostic: GPU deflate stage time of the 20M-read C2 stream (the codec bench size) with the default
+library or an alternative build (argv[1]); prints the stage times of 3 runs after a warm-up, the
+compressed size and the sha256 of the output (same bytes = same sha)."""
+import hashlib
 import sys
 from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
@@ -6,7 +9,7 @@ import torch
 from openge_amd import lib as L
 if len(sys.argv) > 1:
     L.LIB_PATH = Path(sys.argv[1])
-reads = 2_000_000
+reads = 20_000_000
 dev = torch.device("cuda", 0)
 ctx = L.Context(0)
 p = L.synth_params(reads // 2, preset="c2", seed=1234)
@@ -18,6 +21,9 @@ d_recs = torch.empty(B + 64, dtype=torch.uint8, device=dev)
 ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), d_recs.data_ptr()); ctx.sync()
 cap = int(L.lib().oge_bgzf_bound(B))
 d_z = torch.empty(cap, dtype=torch.uint8, device=dev)
-for _ in range(2):
+ms = []
+for _ in range(4):
     zb = ctx.bgzf_deflate_dev(d_recs.data_ptr(), B, 6, d_z.data_ptr(), cap)
-    print("deflate ms", ctx.timing("bgzf_deflate"), "bytes", zb, flush=True)
+    ms.append(round(ctx.timing("bgzf_deflate"), 2))
+sha = hashlib.sha256(d_z[:zb].cpu().numpy().tobytes()).hexdigest()[:16]
+print(sys.argv[1:] or ["default"], "deflate ms", ms[1:], "bytes", zb, "ratio", round(zb / B, 4), "sha", sha, flush=True)

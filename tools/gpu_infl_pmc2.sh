@@ -23,7 +23,9 @@ res = {}
 for f in glob.glob(d + "/*/p*/**/*counter_collection.csv", recursive=True):
     lib = f[len(d) + 1:].split("/")[0]
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].split("::")[-1]
+        import re
+        m = re.search(r"(k_infl_\w+)", r["Kernel_Name"])
+        k = m.group(1) if m else r["Kernel_Name"][:40]
         res.setdefault(lib, {}).setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 out = {lib: {k: {c: sum(v) / len(v) * 0 + sum(v) for c, v in kv.items()} for k, kv in ks.items()} for lib, ks in res.items()}
 print(json.dumps(out, indent=1))
