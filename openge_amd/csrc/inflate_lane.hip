@@ -63,7 +63,8 @@ constexpr uint32_t kDefer = 0x1000;              // sym: a long literal whose by
 // per-wave LDS, lane-interleaved ([entry][lane]): element e of lane l at e * 64 + l.  13,312 bytes: 12
 // waves per CU fit the 160 KiB.
 struct P1Lds {
-    uint16_t lt[1 << TL][64];  // sym | L << 9, 0 = longer code; while code lengths are decoded a lane's
+    uint16_t lt[1 << TL][64];  // sym | L << 9, 0x100 = longer code (bit 8 set: not a literal, L = 0); while
+                                // code lengths are decoded a lane's
                                 // column holds its 7-bit code-length table (cl_at): sym | L << 5
     uint8_t dt[1 << TD][64];   // sym | L << 5, 0 = longer code
     uint8_t ll[32][64];        // long length codes (and end of block): symbol - 256, by long-length index
@@ -164,8 +165,8 @@ __device__ bool wbuild(P1Lds &S, uint32_t j, OGE_G uint8_t *list, OGE_G uint8_t 
     *nlong = __builtin_amdgcn_readfirstlane(nl);
     if (ks > 32768u) return false;
     const bool wx = xl != nullptr && *nlong <= 256;
-    for (uint32_t r = lane; r < (1u << TB); r += 64) {  // zero lane j's column of the direct table
-        if (LIT) S.lt[r][j] = 0;
+    for (uint32_t r = lane; r < (1u << TB); r += 64) {  // clear lane j's column of the direct table
+        if (LIT) S.lt[r][j] = 0x100;
         else S.dt[r][j] = 0;
     }
     __builtin_amdgcn_wave_barrier();
@@ -335,7 +336,7 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
 #pragma unroll
         for (int k = 0; k < LB; ++k) {
             const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
-            if (!e2 || (e2 & 0x100) || pos >= osz) break;
+            if ((e2 & 0x100) || pos >= osz) break;  // bit 8: a length code, end of block or a longer code
             buf >>= e2 >> 9;
             cnt -= e2 >> 9;
             put(e2 & 0xff);
@@ -537,13 +538,20 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 const uint32_t v = (uint32_t)buf;
                 const uint32_t e = S.lt[v & ((1u << TL) - 1)][lane];
                 uint32_t sym, L;
-                if (e) {
+                if (e >> 9) {
                     sym = e & 511, L = e >> 9;
                 } else {  // code longer than TL bits: canonical limits (VGPRs)
                     const uint32_t c15 = __builtin_bitreverse32(v) >> 17;
+                    // L = 7 + the limits <= c15 (limits never decrease with the length); the same tests pick
+                    // the length's list parameters
                     L = 7;
-                    sfor<4>([&](auto k) { L += (c15 >= (T.ll[k()] & 0xffff)) + (c15 >= (T.ll[k()] >> 16)); });
-                    const uint32_t pk = pick(T.pk, L - 7);
+                    uint32_t pk = T.pk[0];
+                    sfor<4>([&](auto k) {
+                        const bool g0 = c15 >= (T.ll[k()] & 0xffff), g1 = c15 >= (T.ll[k()] >> 16);
+                        L += g0 + g1;
+                        pk = g0 ? T.pk[2 * k() + 1] : pk;
+                        pk = g1 ? T.pk[2 * k() + 2] : pk;
+                    });
                     const uint32_t k = ((pk & 0xffff) + (c15 >> (15 - L))) & 0xffff;
                     const uint32_t litend = (pk >> 16) & 511;
                     if (k < litend) {  // a literal: its byte later (phase 2), or now from the lane's scratch
@@ -583,8 +591,14 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                     } else {
                         const uint32_t c15 = __builtin_bitreverse32(w) >> 17;
                         DL = 5;
-                        sfor<5>([&](auto k) { DL += (c15 >= (T.dl[k()] & 0xffff)) + (c15 >= (T.dl[k()] >> 16)); });
-                        const uint32_t k = (u16of(T.di, DL - 5) + (c15 >> (15 - DL))) & 0xffff;
+                        uint32_t di = T.di[0] & 0xffff;
+                        sfor<5>([&](auto k) {
+                            const bool g0 = c15 >= (T.dl[k()] & 0xffff), g1 = c15 >= (T.dl[k()] >> 16);
+                            DL += g0 + g1;
+                            di = g0 ? T.di[k()] >> 16 : di;
+                            di = g1 ? T.di[k() + 1] & 0xffff : di;
+                        });
+                        const uint32_t k = (di + (c15 >> (15 - DL))) & 0xffff;
                         ds = S.dl[min(k, 29u)][lane];
                         if (DL == 15 && c15 >= (T.dl[5] & 0xffff)) ds = 31;  // no such code
                     }
