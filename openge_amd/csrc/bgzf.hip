@@ -435,6 +435,14 @@ __global__ void __launch_bounds__(64) k_defl_huff(const uint32_t *__restrict__ f
     __shared__ HuffScratch hs;
     const int lane = threadIdx.x;
     DeflTab &T = tabs[blockIdx.x];
+#if OGE_EXP == 3  // timing experiment: phase clocks of one wave
+    uint64_t xc[10];
+    int xn = 0;
+#define XCLK() (xc[xn++] = __builtin_readcyclecounter())
+#else
+#define XCLK()
+#endif
+    XCLK();
     for (int i = lane; i < kFreq; i += 64) f[i] = freq_in[(uint64_t)blockIdx.x * kFreq + i];
     __syncthreads();
     if (lane == 0) {
@@ -450,10 +458,14 @@ __global__ void __launch_bounds__(64) k_defl_huff(const uint32_t *__restrict__ f
             if (!f[kLit + i]) f[kLit + i] = 1, ++nz;
     }
     __syncthreads();
+    XCLK();
     huff_lengths(f, kLit, 15, lens, hs);
+    XCLK();
     huff_lengths(f + kLit, kDist, 15, lens + kLit, hs);
+    XCLK();
     huff_codes(lens, kLit, T.lit);
     huff_codes(lens + kLit, kDist, T.dist);
+    XCLK();
 
     // run-length code the two length sequences separately (RFC 1951 3.2.7)
     __shared__ uint32_t hlit, hdist;
@@ -503,8 +515,10 @@ __global__ void __launch_bounds__(64) k_defl_huff(const uint32_t *__restrict__ f
             if (!fcl[i]) fcl[i] = 1, ++nz;
     }
     __syncthreads();
+    XCLK();
     huff_lengths(fcl, kCl, 7, lcl, hs);
     huff_codes(lcl, kCl, ccl);
+    XCLK();
     if (lane == 0) {
         int hclen = kCl;
         while (hclen > 4 && lcl[kClOrder[hclen - 1]] == 0) --hclen;
@@ -556,6 +570,14 @@ __global__ void __launch_bounds__(64) k_defl_huff(const uint32_t *__restrict__ f
         T.total = total;
         sizes[blockIdx.x] = total;
     }
+#if OGE_EXP == 3
+    XCLK();
+    if (lane == 0 && blockIdx.x < 4 && blk0 == 0)
+        printf("huff-exp blk %u: load %llu lit-lengths %llu dist-lengths %llu codes %llu rle %llu cl %llu header+size %llu\n",
+               blockIdx.x, (unsigned long long)(xc[1] - xc[0]), (unsigned long long)(xc[2] - xc[1]), (unsigned long long)(xc[3] - xc[2]),
+               (unsigned long long)(xc[4] - xc[3]), (unsigned long long)(xc[5] - xc[4]), (unsigned long long)(xc[6] - xc[5]),
+               (unsigned long long)(xc[7] - xc[6]));
+#endif
 }
 
 // ------------------------------------------------------------------------------------ emit
@@ -913,7 +935,10 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     // Chunks go round-robin over S streams: one chunk's Huffman and emit kernels run on the CUs beside
     // another chunk's parse workgroups (150 KiB of LDS, one per CU); only the offset advance, which
     // gives each chunk its base in the output stream, is ordered chunk after chunk (events).
-    const int S = nblk > chunk ? 3 : 1;
+#ifndef OGE_DEFL_STREAMS
+#define OGE_DEFL_STREAMS 3
+#endif
+    const int S = nblk > chunk ? OGE_DEFL_STREAMS : 1;
     struct Bufs {
         uint64_t *lmask, *cbase;
         uint32_t *mlist, *freq, *sizes, *offs;

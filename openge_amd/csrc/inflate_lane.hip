@@ -371,8 +371,12 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
     uint32_t st = ST_NEXT, hl = 0, aux = 0, flg = 0;
     uint32_t b = 0;  // block index (a chunk of a launch holds < 2^32 blocks)
 
+    // a failing block: the lane stops decoding it at once, the error is reported (atomics on err) in the
+    // next wave-wide phase, before the lane takes another block -- no atomics inlined into the decode
+    // loop at each of its error sites
+    uint32_t ferr = 0;
     auto fail = [&](uint32_t code) {
-        report(err, code, b);
+        ferr = code;
         st = ST_NEXT;
     };
     auto block_end = [&]() {  // last deflate block of the BGZF block consumed
@@ -385,6 +389,10 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
     };
 
     for (;;) {
+        if (ferr) {
+            report(err, ferr, b);
+            ferr = 0;
+        }
         // ---- table builds, the whole wave for one lane at a time
         uint64_t need = __ballot(st == ST_BCL || st == ST_BLD);
         if (need) __threadfence_block();  // lanes' code-length stores before the wave reads them
