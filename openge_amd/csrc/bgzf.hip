@@ -250,32 +250,47 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
 // handed out longest-first to the least frequent symbols.
 struct HuffScratch {
     uint16_t sorted[kLit];
-    uint32_t w[2 * kLit];      // node weights, later the node depths
+    uint32_t w[2 * kLit];      // node weights, later the node depths; first the sort keys (512)
     uint16_t parent[2 * kLit]; // parent node, later the pointer-jumping ancestor
     uint32_t cnt[16];
     uint32_t m;
 };
+static_assert(2 * kLit >= 512, "the sort keys live in HuffScratch::w");
 
 // One wave, everything but the two-queue merge lane-parallel (r03: the r02 version ran the depth walk,
 // the depth counts and the length hand-out as serial lane-0 loops over LDS, one LDS round trip per step;
 // the same lengths, so the same compressed bytes).
 __device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, HuffScratch &hs) {
     const int lane = threadIdx.x;
+    // the used symbols ranked by (frequency, symbol): keys f << 9 | symbol (f <= 65281), unused slots
+    // 0xffffffff, bitonic-sorted in LDS by the wave (literal/length alphabet: 512 slots, 45 stages; r03
+    // counted, for every symbol, the keys below it -- n^2 / 64 LDS reads per lane)
     uint32_t m = 0;
-    for (int i0 = 0; i0 < n; i0 += 64) {
+    uint32_t *key = hs.w;
+    const uint32_t S = n <= 32 ? 32u : n <= 64 ? 64u : n <= 128 ? 128u : n <= 256 ? 256u : 512u;  // sorted slots
+    for (int i0 = 0; i0 < (int)S; i0 += 64) {  // every lane takes part in every ballot: m is wave-uniform
         const int i = i0 + lane;
         const uint32_t fi = i < n ? f[i] : 0;
         if (i < n) len[i] = 0;
-        if (fi) {
-            uint32_t r = 0;
-            for (int j = 0; j < n; ++j) {
-                const uint32_t fj = f[j];
-                r += fj && (fj < fi || (fj == fi && j < i));
-            }
-            hs.sorted[r] = (uint16_t)i;
-        }
+        if (i < (int)S) key[i] = fi ? (fi << 9) | (uint32_t)i : 0xffffffffu;
         m += __popcll(__ballot(fi != 0));
     }
+    __syncthreads();
+    for (uint32_t k = 2; k <= S; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // S / 2 compare-exchange pairs, up to four per lane
+                const uint32_t p = (uint32_t)lane + 64 * q;
+                if (p >= S / 2) break;
+                const uint32_t a = ((p & ~(j - 1)) << 1) | (p & (j - 1)), b = a | j;
+                const uint32_t x = key[a], y = key[b];
+                const bool up = (a & k) == 0;
+                if ((x > y) == up) key[a] = y, key[b] = x;
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t r = lane; r < m; r += 64) hs.sorted[r] = (uint16_t)(key[r] & 511);
     __syncthreads();
     if (m == 0) return;
     if (m == 1) {
@@ -387,30 +402,40 @@ __device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, Huff
 }
 
 // canonical codes, bit-reversed for LSB-first emission: out[i] = rcode | len << 16
+// (lengths counted and symbols ranked inside their length by ballots: r03 counted on lane 0 and ranked each
+// symbol by a walk over the symbols before it)
 __device__ void huff_codes(const uint8_t *len, int n, uint32_t *out) {
     const int lane = threadIdx.x;
-    __shared__ uint32_t first[16];
-    if (lane == 0) {
-        uint32_t cnt[16] = {0};
-        for (int i = 0; i < n; ++i) cnt[len[i]]++;
-        cnt[0] = 0;
-        uint32_t code = 0;
+    const uint64_t lt = (1ull << lane) - 1;
+    uint32_t cnt = 0;  // lane L: codes of length L
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t L = i0 + lane < n ? len[i0 + lane] : 0u;
+#pragma unroll
         for (int b = 1; b < 16; ++b) {
-            code = (code + cnt[b - 1]) << 1;
-            first[b] = code;
+            const uint32_t c = (uint32_t)__popcll(__ballot(L == (uint32_t)b));
+            if (lane == b) cnt += c;
         }
     }
-    __syncthreads();
-    for (int i = lane; i < n; i += 64) {
-        const uint32_t L = len[i];
-        uint32_t v = 0;
-        if (L) {
-            uint32_t r = 0;
-            for (int j = 0; j < i; ++j) r += len[j] == L;
-            const uint32_t code = first[L] + r;
-            v = (__builtin_bitreverse32(code) >> (32 - L)) | (L << 16);
+    uint32_t first = 0, code = 0;  // lane L: the first code of length L
+#pragma unroll
+    for (int b = 1; b < 16; ++b) {
+        code = (code + (b > 1 ? (uint32_t)__shfl(cnt, b - 1, 64) : 0u)) << 1;
+        if (lane == b) first = code;
+    }
+    uint32_t run = 0;  // lane L: codes of length L handed out so far
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        const uint32_t L = i < n ? len[i] : 0u;
+        const uint32_t base = (uint32_t)__shfl(run, (int)L, 64) + (uint32_t)__shfl(first, (int)L, 64);
+        uint32_t r = 0, add = 0;
+#pragma unroll
+        for (int b = 1; b < 16; ++b) {
+            const uint64_t mk = __ballot(L == (uint32_t)b);
+            if (L == (uint32_t)b) r = (uint32_t)__popcll(mk & lt);
+            if (lane == b) add = (uint32_t)__popcll(mk);
         }
-        out[i] = v;
+        run += add;
+        if (i < n) out[i] = L ? (__builtin_bitreverse32(base + r) >> (32 - L)) | (L << 16) : 0u;
     }
     __syncthreads();
 }
