@@ -134,10 +134,19 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
     const uint64_t start = blk * kPay;
     const uint32_t len = (uint32_t)min<uint64_t>(kPay, n - start);
 
+#if OGE_EXP == 4  // timing experiment: phase clocks of a parse workgroup (thread 0)
+    uint64_t pc[12];
+    int pn = 0;
+#define PCLK() (pc[pn++] = __builtin_readcyclecounter())
+#else
+#define PCLK()
+#endif
+    PCLK();
     stage_words<kTP>(in, src + start, len, t);
     for (int i = t; i < (1 << kHashBits); i += kTP) htab[i] = 0;
     for (int i = t; i < kFreq; i += kTP) freq[i] = 0;
     __syncthreads();
+    PCLK();
 
     const uint64_t seg_base = (uint64_t)blockIdx.x * kNSeg;
     for (int sub = 0; sub < kNSub; ++sub) {
@@ -148,7 +157,9 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
             continue;
         }
         const uint32_t end = min(len, base + kSub);
-        // candidates, one round of kR * kT consecutive positions at a time
+        // candidates, one round of kR * kT consecutive positions at a time (r04: an LDS compare-and-swap
+        // bucket holding the latest position and the latest from an earlier round, one barrier per round,
+        // measured slower -- 60k vs 36k cycles per sub-block: repeated prefixes contend for one bucket)
         for (uint32_t r = base; r < end; r += kR * kTP) {
             // the kR lookup chains (prefix word -> bucket -> candidate's word) of a thread run side by side;
             // the ballots come after all of them (a ballot between them would serialise the chains)
@@ -181,6 +192,7 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
             }
             __syncthreads();
         }
+        PCLK();
         // greedy parse of this thread's segment
         const uint32_t s0 = base + t * kSeg, s1 = min(end, s0 + kSeg);
         uint64_t lit = 0;
@@ -239,8 +251,15 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
         }
         if (t < kT) lmask[sg] = lit, nmatch[sg] = (uint8_t)nm;
         __syncthreads();  // cand / cmask are reused by the next sub-block
+        PCLK();
     }
     for (int i = t; i < kFreq; i += kTP) freq_out[(uint64_t)blockIdx.x * kFreq + i] = freq[i];
+#if OGE_EXP == 4
+    if (t == 0 && blockIdx.x < 4 && blk0 == 0)
+        printf("parse-exp blk %u: stage %llu | sub0 rounds %llu parse+counts %llu | sub1 rounds %llu parse+counts %llu\n", blockIdx.x,
+               (unsigned long long)(pc[1] - pc[0]), (unsigned long long)(pc[2] - pc[1]), (unsigned long long)(pc[3] - pc[2]),
+               (unsigned long long)(pc[4] - pc[3]), (unsigned long long)(pc[5] - pc[4]));
+#endif
 }
 
 // ------------------------------------------------------------------------------------ Huffman
@@ -492,89 +511,150 @@ __global__ void __launch_bounds__(64) k_defl_huff(const uint32_t *__restrict__ f
     huff_codes(lens + kLit, kDist, T.dist);
     XCLK();
 
-    // run-length code the two length sequences separately (RFC 1951 3.2.7)
+    // run-length code the two length sequences separately (RFC 1951 3.2.7), the whole wave at once (r03 walked
+    // them on lane 0: ~150k cycles of dependent LDS reads per block, then ~100k for the header bit string).
+    // A run of v of length R (maximal, inside one sequence) always becomes the same tokens:
+    //   v = 0: floor(R / 138) x 18(138), then the rest r = R % 138 as one 17 / 18 if r >= 3, else r zeros;
+    //   v > 0: v, floor((R - 1) / 6) x 16(6), then the rest r = (R - 1) % 6 as one 16(r) if r >= 3, else r x v
+    // (tests/deflate_parse.py restates the sequential walk; tests/test_gpu_bgzf.py pins the headers to it).
     __shared__ uint32_t hlit, hdist;
-    if (lane == 0) {
-        int a = kLit;
-        while (a > 257 && lens[a - 1] == 0) --a;
-        int b = kDist;
-        while (b > 1 && lens[kLit + b - 1] == 0) --b;
-        hlit = a;
-        hdist = b;
-        for (int i = 0; i < kCl; ++i) fcl[i] = 0;
-        uint32_t q = 0;
-        for (int part = 0; part < 2; ++part) {
-            const uint8_t *L = part ? lens + kLit : lens;
-            const int N = part ? b : a;
-            for (int i = 0; i < N;) {
-                const uint8_t v = L[i];
-                int run = 1;
-                while (i + run < N && L[i + run] == v) ++run;
-                if (v == 0 && run >= 3) {
-                    const int r = min(run, 138);
-                    if (r >= 11) cl_sym[q] = 18, cl_ext[q] = (uint8_t)(r - 11);
-                    else cl_sym[q] = 17, cl_ext[q] = (uint8_t)(r - 3);
-                    fcl[cl_sym[q]]++;
-                    ++q;
-                    i += r;
-                    continue;
+    __shared__ uint32_t hw[kHdrWords];
+    {
+        // one past the last used code: at least 257 / 1
+        uint32_t la = 0, lb = 0;
+        for (int r = 0; r < 5; ++r) {
+            const int i = 64 * r + lane;
+            const uint64_t mk = __ballot(i < kLit && lens[i] != 0);
+            if (mk) la = 64 * r + 64 - __builtin_clzll(mk);
+        }
+        const uint64_t mkd = __ballot(lane < kDist && lens[kLit + lane] != 0);
+        if (mkd) lb = 64 - __builtin_clzll(mkd);
+        const uint32_t a = max(la, 257u), b = max(lb, 1u), N = a + b;
+        auto val = [&](uint32_t p) -> uint32_t { return p < a ? lens[p] : lens[kLit + p - a]; };
+        // run starts, as five wave masks over positions 64 r + lane
+        uint64_t st[5];
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const uint32_t p = 64 * r + lane;
+            st[r] = __ballot(p < N && (p == 0 || p == a || val(p) != val(p - 1)));
+        }
+        if (lane < kCl) fcl[lane] = 0;
+        if (lane == 0) hlit = a, hdist = b;
+        __syncthreads();
+        // tokens per run, their exclusive prefix in position order, then each run writes its tokens
+        uint32_t base = 0;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            const uint32_t p = 64 * r + lane;
+            const bool start = (st[r] >> lane) & 1;
+            uint32_t R = 0, v = 0, ntok = 0;
+            if (start) {
+                uint32_t nx = N;  // the next run start after p
+                const uint64_t rest = lane < 63 ? st[r] & (~0ull << (lane + 1)) : 0ull;
+                if (rest) {
+                    nx = 64 * r + __builtin_ctzll(rest);
+                } else {
+#pragma unroll
+                    for (int r2 = 4; r2 > r; --r2)
+                        if (st[r2]) nx = 64 * r2 + __builtin_ctzll(st[r2]);
                 }
-                cl_sym[q] = v, cl_ext[q] = 0, fcl[v]++, ++q;
-                ++i;
-                int rest = run - 1;
-                if (v != 0) {
-                    while (rest >= 3) {
-                        const int r = min(rest, 6);
-                        cl_sym[q] = 16, cl_ext[q] = (uint8_t)(r - 3), fcl[16]++, ++q;
-                        rest -= r;
-                        i += r;
-                    }
+                R = min(nx, N) - p;
+                v = val(p);
+                if (v == 0) {
+                    const uint32_t rm = R % 138;
+                    ntok = R / 138 + (rm >= 3 ? 1 : rm);
+                } else {
+                    const uint32_t rm = (R - 1) % 6;
+                    ntok = 1 + (R - 1) / 6 + (rm >= 3 ? 1 : rm);
                 }
-                // the (< 3) remaining equal values go round the loop as plain lengths
+            }
+            uint32_t inc = ntok;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o, 64);
+                if (lane >= (uint32_t)o) inc += y;
+            }
+            uint32_t k = base + inc - ntok;
+            base += __shfl(inc, 63, 64);
+            if (start) {
+                auto tok = [&](uint32_t sym, uint32_t ext) {
+                    cl_sym[k] = (uint8_t)sym;
+                    cl_ext[k] = (uint8_t)ext;
+                    atomicAdd(&fcl[sym], 1u);
+                    ++k;
+                };
+                if (v == 0) {
+                    for (uint32_t q = 0; q < R / 138; ++q) tok(18, 127);
+                    const uint32_t rm = R % 138;
+                    if (rm >= 11) tok(18, rm - 11);
+                    else if (rm >= 3) tok(17, rm - 3);
+                    else
+                        for (uint32_t q = 0; q < rm; ++q) tok(0, 0);
+                } else {
+                    tok(v, 0);
+                    for (uint32_t q = 0; q < (R - 1) / 6; ++q) tok(16, 3);
+                    const uint32_t rm = (R - 1) % 6;
+                    if (rm >= 3) tok(16, rm - 3);
+                    else
+                        for (uint32_t q = 0; q < rm; ++q) tok(v, 0);
+                }
             }
         }
-        ncl = q;
-        uint32_t nz = 0;
-        for (int i = 0; i < kCl; ++i) nz += fcl[i] != 0;
-        for (int i = 0; nz < 2 && i < kCl; ++i)
-            if (!fcl[i]) fcl[i] = 1, ++nz;
+        __syncthreads();
+        if (lane == 0) {
+            ncl = base;
+            uint32_t nz = 0;
+            for (int i = 0; i < kCl; ++i) nz += fcl[i] != 0;
+            for (int i = 0; nz < 2 && i < kCl; ++i)
+                if (!fcl[i]) fcl[i] = 1, ++nz;
+        }
     }
     __syncthreads();
     XCLK();
     huff_lengths(fcl, kCl, 7, lcl, hs);
     huff_codes(lcl, kCl, ccl);
     XCLK();
-    if (lane == 0) {
-        int hclen = kCl;
-        while (hclen > 4 && lcl[kClOrder[hclen - 1]] == 0) --hclen;
-        uint64_t acc = 0;
-        uint32_t nacc = 0, wi = 0, total = 0;
-        auto put = [&](uint32_t v, uint32_t nb) {
-            acc |= (uint64_t)v << nacc;
-            nacc += nb;
-            total += nb;
-            if (nacc >= 32) {
-                T.hdr[wi++] = (uint32_t)acc;
-                acc >>= 32;
-                nacc -= 32;
-            }
+    {
+        // the header bit string: 17 fixed bits, HCLEN x 3 bits, then every token's code and extra bits at the
+        // prefix sum of the token lengths, OR-ed into LDS words (a token spans at most two)
+        for (int i = lane; i < kHdrWords; i += 64) hw[i] = 0;
+        const uint64_t mh = __ballot(lane >= 4 && lane < kCl && lcl[kClOrder[lane]] != 0);
+        const uint32_t hclen = mh ? 64 - __builtin_clzll(mh) : 4u;
+        __syncthreads();
+        auto orbits = [&](uint32_t at, uint32_t v, uint32_t nb) {  // nb <= 32
+            if (!nb) return;
+            const uint32_t w = at >> 5, sh = at & 31;
+            atomicOr(&hw[w], v << sh);
+            if (sh + nb > 32) atomicOr(&hw[w + 1], v >> (32 - sh));
         };
-        put(1, 1);  // BFINAL
-        put(2, 2);  // BTYPE = dynamic
-        put(hlit - 257, 5);
-        put(hdist - 1, 5);
-        put(hclen - 4, 4);
-        for (int i = 0; i < hclen; ++i) put(lcl[kClOrder[i]], 3);
-        for (uint32_t i = 0; i < ncl; ++i) {
-            const uint32_t s = cl_sym[i], c = ccl[s];
-            put(c & 0xffff, c >> 16);
-            if (s == 16) put(cl_ext[i], 2);
-            else if (s == 17) put(cl_ext[i], 3);
-            else if (s == 18) put(cl_ext[i], 7);
+        if (lane == 0) orbits(0, 1u | (2u << 1) | ((hlit - 257) << 3) | ((hdist - 1) << 8) | ((hclen - 4) << 13), 17);
+        if ((uint32_t)lane < hclen) orbits(17 + 3 * lane, lcl[kClOrder[lane]], 3);
+        const uint32_t n = ncl;
+        uint32_t at = 17 + 3 * hclen;
+        for (uint32_t t0 = 0; t0 < n; t0 += 64) {
+            const uint32_t t = t0 + lane;
+            uint32_t nb = 0, v = 0;
+            if (t < n) {
+                const uint32_t sym = cl_sym[t], c = ccl[sym], cb = c >> 16;
+                const uint32_t eb = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
+                nb = cb + eb;
+                v = (c & 0xffff) | ((uint32_t)cl_ext[t] << cb);
+            }
+            uint32_t inc = nb;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o, 64);
+                if (lane >= (uint32_t)o) inc += y;
+            }
+            orbits(at + inc - nb, v, nb);
+            at += __shfl(inc, 63, 64);
         }
-        if (nacc) T.hdr[wi++] = (uint32_t)acc;
-        T.hdr_bits = total;
-        ncl = total;  // the header's bit count, for the size below
+        __syncthreads();
+        for (uint32_t i = lane; i < (at + 31) / 32; i += 64) T.hdr[i] = hw[i];
+        if (lane == 0) {
+            T.hdr_bits = at;
+            ncl = at;  // the header's bit count, for the size below
+        }
     }
     __syncthreads();
     uint32_t bits = 0;

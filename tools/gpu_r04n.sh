@@ -13,3 +13,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/dprof -o run --output
 grep "deflate ms" $OUT/defl_s1.txt
 timeout -k 10 200 python tools/diag_defl.py openge_amd/_var/lib_hx2.so > $OUT/hx2.txt 2>&1 || { tail -20 $OUT/hx2.txt; exit 1; }
 grep "huff-exp" $OUT/hx2.txt | head -4
+timeout -k 10 200 python tools/diag_defl.py openge_amd/_var/lib_px.so > $OUT/px.txt 2>&1 || { tail -20 $OUT/px.txt; exit 1; }
+grep "parse-exp" $OUT/px.txt | head -4
