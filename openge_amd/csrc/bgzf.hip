@@ -320,33 +320,32 @@ __device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, Huff
     for (uint32_t k = lane; k < m; k += 64) hs.w[k] = f[hs.sorted[k]];
     __syncthreads();
     const uint32_t root = 2 * m - 2;
-    if (lane == 0) {  // two-queue merge: the two queue heads are kept in registers, one LDS read per pick
-        uint32_t i = 0, j = m, nx = m, wi = hs.w[0], wj = 0;
+    if (lane == 0) {  // two-queue merge (lane 0).  A step's two picks can only take the next two entries
+        // of either queue, so those four are read together at the start of the step (one LDS round trip per
+        // step instead of one per pick; entries not yet created are never taken: nodes are made in order)
+        uint32_t i = 0, j = m, nx = m;
         for (uint32_t c = 0; c + 1 < m; ++c) {
+            // unconditional reads (both pairs in one LDS round trip); an entry past its queue's end is read
+            // but never picked
+            const uint32_t l0 = hs.w[i], l1 = hs.w[i + 1], n0 = hs.w[j], n1 = hs.w[j + 1];
             uint32_t a, b, wa, wb;
-            if (i < m && (j >= nx || wi <= wj)) {
-                a = i, wa = wi;
-                ++i;
-                wi = i < m ? hs.w[i] : 0u;
+            if (i < m && (j >= nx || l0 <= n0)) {  // first pick
+                a = i, wa = l0;
+                const bool leaf = i + 1 < m && (j >= nx || l1 <= n0);  // second pick
+                b = leaf ? i + 1 : j, wb = leaf ? l1 : n0;
+                i += leaf ? 2 : 1;
+                j += leaf ? 0 : 1;
             } else {
-                a = j, wa = wj;
-                ++j;
-                wj = j < nx ? hs.w[j] : 0u;
-            }
-            if (i < m && (j >= nx || wi <= wj)) {
-                b = i, wb = wi;
-                ++i;
-                wi = i < m ? hs.w[i] : 0u;
-            } else {
-                b = j, wb = wj;
-                ++j;
-                wj = j < nx ? hs.w[j] : 0u;
+                a = j, wa = n0;
+                const bool leaf = i < m && (j + 1 >= nx || l0 <= n1);
+                b = leaf ? i : j + 1, wb = leaf ? l0 : n1;
+                i += leaf ? 1 : 0;
+                j += leaf ? 1 : 2;
             }
             const uint32_t sw = wa + wb;
             hs.w[nx] = sw;
             hs.parent[a] = (uint16_t)nx;
             hs.parent[b] = (uint16_t)nx;
-            if (j == nx) wj = sw;  // the internal queue was empty: the new node is its head
             ++nx;
         }
         hs.parent[root] = (uint16_t)root;
@@ -752,6 +751,10 @@ __device__ __forceinline__ void seg_load(const uint8_t *s, uint32_t s0, uint32_t
     }
 }
 
+// (r04: a wave-per-segment emitter -- lane i = byte i, the segment's match tokens gathered to their start
+// lanes by rank, a DPP prefix sum of the bit counts, LDS atomicOr into the image -- measured slower: 13.3k
+// vs 10.3k VALU per wave (it does ~80 VALU per segment per wave, this one ~16 per position per lane with
+// 64 segments side by side), 20M deflate 36.5-37.6 vs 32.8 ms; same bytes)
 // Latency, not work, bounds these two: a code lookup or a match-token load inside a data-dependent branch
 // is waited for on the spot.  So the segment's literal codes are looked up 16 at a time without branches
 // (independent LDS reads in flight together) and its first kMPre match tokens are loaded at once.
