@@ -1,13 +1,14 @@
-"""Diagnostic: inflate stage time of the 20M codec stream with an alternative library build (argv[1] = .so
-path; errors are reported, not raised: diagnostic builds may drop work)."""
-import ctypes as C, sys
+"""Diagnostic: inflate stage time of the 20M codec stream (DIAG_READS overrides the read count) with an
+alternative library build (argv[1] = .so path; errors are reported, not raised: diagnostic builds may drop
+work); the last run's output is compared with the records."""
+import ctypes as C, os, sys
 from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import numpy as np, torch
 from openge_amd import lib as L
 if len(sys.argv) > 1:
     L.LIB_PATH = Path(sys.argv[1])
-reads = 20_000_000
+reads = int(os.environ.get("DIAG_READS", 20_000_000))
 dev = torch.device("cuda", 0)
 ctx = L.Context(0)
 p = L.synth_params(reads // 2, preset="c2", seed=1234)
@@ -35,4 +36,5 @@ for _ in range(4):
     p0 = d_idx.data_ptr()
     rc = L.lib().oge_bgzf_inflate_dev(ctx.h, d_z.data_ptr(), zb, p0, p0 + 8 * k, p0 + 16 * k, d_crc.data_ptr(), k, d_back.data_ptr())
     ms.append(round(ctx.timing("bgzf_inflate"), 2))
-print(sys.argv[1:] or ["default"], "inflate ms", ms[1:], "rc", rc, flush=True)
+same = bool(torch.equal(d_back[:B], d_recs[:B]))
+print(sys.argv[1:] or ["default"], "reads", reads, "blocks", k, "inflate ms", ms[1:], "rc", rc, "same", same, flush=True)

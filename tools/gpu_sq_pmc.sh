@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 KRE=${KRE:-k_infl}
 DIAG=${DIAG:-tools/diag_infl.py}
-OUT=gpurun_out/${PMC_TAG:-r04}/${KRE}pmc
+OUT=gpurun_out/${PMC_TAG:-sq}/${KRE}pmc
 mkdir -p $OUT
 export TMPDIR=/tmp
 G1="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH"
