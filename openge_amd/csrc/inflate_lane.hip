@@ -35,6 +35,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -52,6 +53,14 @@ __device__ __forceinline__ void report(uint32_t *err, uint32_t code, uint64_t bl
 
 constexpr int TL = 6, TD = 4;  // direct-table bits: literal/length, distance
 constexpr int kWps = 3;        // waves per SIMD (VGPR budget 512 / 3)
+#ifndef OGE_INFL_STREAMS
+#define OGE_INFL_STREAMS 2
+#endif
+#ifndef OGE_INFL_CHUNK
+#define OGE_INFL_CHUNK 1
+#endif
+constexpr int kStreams = OGE_INFL_STREAMS;     // chunk pipelines (see oge_inflate_lanes)
+constexpr uint64_t kChunkLanes = OGE_INFL_CHUNK;  // blocks per lane per chunk, at most
 constexpr int LB = 4;          // literals per decode step (see the ST_SYM path)
 constexpr int kInner = 16;     // decode steps between the wave-wide phases
 constexpr int kNT = 4;         // tables per BGZF block whose long literals phase 2 translates
@@ -746,6 +755,14 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     }
     if (crc) crc_setup<kT2>(crctab, zp, zpow, t);
     const uint32_t q0 = 64 * t;
+#if OGE_EXP == 7  // timing experiment: phase clocks of a phase-2 workgroup (thread 0) and its rounds
+    uint64_t zc[10];
+    int zn = 0, zr = 0;
+#define ZCLK() (zc[zn++] = __builtin_readcyclecounter())
+#else
+#define ZCLK()
+#endif
+    ZCLK();
     // 1. this thread's 64 literal-filled bytes [q0, q0 + 64) and the next word (descriptors may
     //    straddle): aligned dword loads, funnel-shifted
     uint32_t wv[17];
@@ -760,6 +777,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
 #pragma unroll
         for (int k = 0; k < 17; ++k) wv[k] = sh ? __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh) : raw[k];
     }
+    ZCLK();
     // 2. every position its own source
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) {
@@ -769,6 +787,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         *(uint4 *)(refs + p) = v;
     }
     __syncthreads();
+    ZCLK();
     // 3. holes: refs[p + j] = p - D + j, descriptors read from this thread's window registers
     const OGE_G uint64_t *bmp = (const OGE_G uint64_t *)(bitmap + (b - b0) * 2048);
     const uint32_t nw = (osz + 63) >> 6;
@@ -790,22 +809,45 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
             const uint32_t x = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
             const uint32_t p = q0 + jb, len = (x & 0xff) + 3, dist = ((x >> 8) & 0x7fff) + 1;
             const uint32_t e = min(p + len, osz);  // phase 1 checked it; a failed block must not write past the array
-            // refs[q] = q - dist over [p, e): single entries up to the next 8-aligned position, then
-            // 8 entries per 16-byte store, then the tail
+            // refs over [p, e): single entries up to the next 8-aligned position, then 8 entries per 16-byte
+            // store, then the tail
             uint32_t q = p;
             const uint32_t a8 = min((p + 7) & ~7u, e);
-            for (; q < a8; ++q) refs[q] = (uint16_t)(q - dist);
-            for (; q + 8 <= e; q += 8) {
-                const uint32_t r = q - dist;
-                uint4 v;
-                v.x = (r & 0xffff) | (((r + 1) & 0xffff) << 16), v.y = ((r + 2) & 0xffff) | (((r + 3) & 0xffff) << 16);
-                v.z = ((r + 4) & 0xffff) | (((r + 5) & 0xffff) << 16), v.w = ((r + 6) & 0xffff) | (((r + 7) & 0xffff) << 16);
-                *(uint4 *)(refs + q) = v;
+            if (dist >= len) {  // refs[q] = q - dist: the source lies before the copy
+                for (; q < a8; ++q) refs[q] = (uint16_t)(q - dist);
+                for (; q + 8 <= e; q += 8) {
+                    const uint32_t r = q - dist;
+                    uint4 v;
+                    v.x = (r & 0xffff) | (((r + 1) & 0xffff) << 16), v.y = ((r + 2) & 0xffff) | (((r + 3) & 0xffff) << 16);
+                    v.z = ((r + 4) & 0xffff) | (((r + 5) & 0xffff) << 16), v.w = ((r + 6) & 0xffff) | (((r + 7) & 0xffff) << 16);
+                    *(uint4 *)(refs + q) = v;
+                }
+                for (; q < e; ++q) refs[q] = (uint16_t)(q - dist);
+            } else {  // an overlapping copy repeats its first dist bytes: refs[p + j] = p - dist + j mod dist,
+                      // always before p (r03 chained q -> q - dist inside the copy: len / dist levels of
+                      // pointer jumping for a run)
+                const uint32_t r0 = p - dist;
+                uint32_t k = 0;
+                auto nx = [&]() {
+                    const uint32_t r = r0 + k;
+                    k = k + 1 == dist ? 0u : k + 1;
+                    return r & 0xffff;
+                };
+                for (; q < a8; ++q) refs[q] = (uint16_t)nx();
+                for (; q + 8 <= e; q += 8) {
+                    uint4 v;
+                    v.x = nx(), v.x |= nx() << 16;
+                    v.y = nx(), v.y |= nx() << 16;
+                    v.z = nx(), v.z |= nx() << 16;
+                    v.w = nx(), v.w |= nx() << 16;
+                    *(uint4 *)(refs + q) = v;
+                }
+                for (; q < e; ++q) refs[q] = (uint16_t)nx();
             }
-            for (; q < e; ++q) refs[q] = (uint16_t)(q - dist);
         }
     }
     __syncthreads();
+    ZCLK();
     // 4. pointer jumping until every position names a literal.  A chunk of literals only (every ref its
     //    own position) or one whose refs all name roots never changes again: `act` drops it, so later
     //    rounds only touch the chunks still inside unresolved copies.
@@ -844,8 +886,12 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
                 act &= ~(1u << k);
             }
         }
+#if OGE_EXP == 7
+        zr = round + 1;
+#endif
         if (!__syncthreads_or(changed)) break;
     }
+    ZCLK();
     // 5. this thread's chunks' roots into registers, then the region becomes the byte image of the block
     //    (the literal-filled bytes, from the registers of step 1: no second global read)
     uint32_t rf[32];
@@ -880,6 +926,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         }
     }
     __syncthreads();
+    ZCLK();
     // 6. every copied byte from its root (a literal position of the image); literal-only chunks are
     //    already in place
     const uint32_t last = osz ? osz - 1 : 0;
@@ -905,6 +952,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         img32[pw<PS>(w) + 1] = cw[2 * k + 1];
     }
     __syncthreads();
+    ZCLK();
     // 7. CRC and the write-out at the block's alignment
     if (crc) {
         const uint32_t c = crc_window1024<PS>(img32, osz, crctab, zp, crcs, t);
@@ -924,6 +972,15 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
             }
         }
     }
+#if OGE_EXP == 7
+    ZCLK();
+    if (t == 0 && blockIdx.x % 4096 == 7)
+        printf("lz-exp blk %u: load %llu init %llu holes %llu jump %llu (%d rounds) roots+defer %llu gather %llu crc+out %llu\n",
+               blockIdx.x, (unsigned long long)(zc[1] - zc[0]), (unsigned long long)(zc[2] - zc[1]),
+               (unsigned long long)(zc[3] - zc[2]), (unsigned long long)(zc[4] - zc[3]), zr, (unsigned long long)(zc[5] - zc[4]),
+               (unsigned long long)(zc[6] - zc[5]), (unsigned long long)(zc[7] - zc[6]));
+#endif
+#undef ZCLK
 }
 
 }  // namespace
@@ -939,32 +996,70 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
         return n > 0 ? n : 256;
     }();
-    // persistent lanes (the 12 resident waves per CU) take blocks from a queue; a chunk is at most 4
-    // blocks per lane (the queue keeps the lanes busy, so a larger chunk gains nothing: 300M reads = 2
-    // launches, a 14 GB workspace that lives as long as the context), and no more than a quarter of the
-    // free device memory holds bitmaps and lists for (17.3 KiB per block), at least one block per lane
+    // persistent lanes (the 12 resident waves per CU) take blocks from a queue; a chunk is at most
+    // kChunkLanes blocks per lane, and no more than a quarter of the free device memory holds bitmaps and
+    // lists for (17.3 KiB per block), at least one block per lane.  Chunks alternate over kStreams streams
+    // with a buffer set each: chunk k + 1's phase 1 starts while chunk k's lanes drain (a wave ends when
+    // its last lane's block does) and while chunk k's phase 2 runs, so the tails overlap.  100M reads
+    // (435k blocks), A/B in one run on two boxes: one chunk on one stream 225.2 / 225.4 ms, three chunks
+    // of one block per lane on two streams 209.1 / 217.5 (three streams: no better); the workspace is
+    // 2 x 196k blocks x 17.3 KiB = 6.8 GB (r03: up to 4 blocks per lane in one set, 14 GB).
     const uint64_t lanes = (uint64_t)ncu * 4 * kWps * 64;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
     constexpr uint64_t kPerBlk = 2048 * 8 + kXTab;  // bitmaps + translation lists
-    const uint64_t budget = std::max<uint64_t>(lanes, std::min<uint64_t>(4 * lanes, (uint64_t)(fr / 4) / kPerBlk));
+    constexpr int S = kStreams;
+    const uint64_t budget =
+        std::max<uint64_t>(lanes, std::min<uint64_t>(kChunkLanes * lanes, (uint64_t)(fr / 4) / (S * kPerBlk)));
     const uint64_t nchunks = std::max<uint64_t>(1, (nblk + budget - 1) / budget);
     const uint64_t chunk = std::max<uint64_t>(1, (nblk + nchunks - 1) / nchunks);
     const uint64_t wgs = std::min<uint64_t>((chunk + 63) / 64, lanes / 64);
-    uint64_t *bitmap = (uint64_t *)ctx->ws("infl_bitmap", chunk * 2048 * 8);
-    uint8_t *xtab = (uint8_t *)ctx->ws("infl_xtab", chunk * kXTab);
-    uint8_t *scr = (uint8_t *)ctx->ws("infl_scratch", wgs * 64 * kScr);
-    unsigned long long *next = (unsigned long long *)ctx->ws("infl_next", 8);
-    if (!bitmap || !xtab || !scr || !next) return OGE_ERR_HIP;
-    for (uint64_t b0 = 0; b0 < nblk; b0 += chunk) {
+    struct Set {
+        uint64_t *bitmap;
+        uint8_t *xtab, *scr;
+        unsigned long long *next;
+        hipStream_t st;
+    } B[S];
+    for (int k = 0; k < S; ++k) {
+        const std::string x = std::to_string(k);
+        B[k].bitmap = (uint64_t *)ctx->ws(("infl_bitmap" + x).c_str(), chunk * 2048 * 8);
+        B[k].xtab = (uint8_t *)ctx->ws(("infl_xtab" + x).c_str(), chunk * kXTab);
+        B[k].scr = (uint8_t *)ctx->ws(("infl_scratch" + x).c_str(), wgs * 64 * kScr);
+        B[k].next = (unsigned long long *)ctx->ws(("infl_next" + x).c_str(), 8);
+        B[k].st = S == 1 ? ctx->stream : ctx->side_stream(k);
+        if (!B[k].bitmap || !B[k].xtab || !B[k].scr || !B[k].next || !B[k].st) return OGE_ERR_HIP;
+    }
+    hipEvent_t ev[S + 1];
+    int nev = 0;
+    struct Evs {
+        hipEvent_t *e;
+        int &n;
+        ~Evs() {
+            for (int i = 0; i < n; ++i) (void)hipEventDestroy(e[i]);
+        }
+    } evs{ev, nev};
+    for (; nev < S + 1; ++nev) OGE_HIP_TRY(ctx, hipEventCreateWithFlags(&ev[nev], hipEventDisableTiming));
+    if (S > 1) {  // inputs ready for the side streams
+        OGE_HIP_TRY(ctx, hipEventRecord(ev[S], ctx->stream));
+        for (int k = 0; k < S; ++k) OGE_HIP_TRY(ctx, hipStreamWaitEvent(B[k].st, ev[S], 0));
+    }
+    uint64_t k = 0;
+    for (uint64_t b0 = 0; b0 < nblk; b0 += chunk, ++k) {
         const uint64_t nb = std::min(chunk, nblk - b0);
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
-        OGE_HIP_TRY(ctx, hipMemsetAsync(next, 0, 8, ctx->stream));
-        OGE_HIP_TRY(ctx, hipMemsetAsync(bitmap, 0, nb * 2048 * 8, ctx->stream));  // phase 1 stores only words with bits
-        k_infl_huff<<<g1, 64, 0, ctx->stream>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, bitmap, xtab, scr, err, next);
+        const Set &u = B[k % S];
+        OGE_HIP_TRY(ctx, hipMemsetAsync(u.next, 0, 8, u.st));
+        OGE_HIP_TRY(ctx, hipMemsetAsync(u.bitmap, 0, nb * 2048 * 8, u.st));  // phase 1 stores only words with bits
+        k_infl_huff<<<g1, 64, 0, u.st>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, u.bitmap, u.xtab, u.scr, err, u.next);
         OGE_LAUNCH_CHECK(ctx);
-        k_infl_lz<<<(uint32_t)nb, kT2, 0, ctx->stream>>>(out, uoff, crc, bitmap, xtab, b0, zpow, err);
+        k_infl_lz<<<(uint32_t)nb, kT2, 0, u.st>>>(out, uoff, crc, u.bitmap, u.xtab, b0, zpow, err);
         OGE_LAUNCH_CHECK(ctx);
+    }
+    if (S > 1) {  // the context stream waits for every chunk
+        for (int j = 0; j < S; ++j) {
+            OGE_HIP_TRY(ctx, hipEventRecord(ev[j], B[j].st));
+            OGE_HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ev[j], 0));
+        }
     }
     return OGE_OK;
 }
