@@ -21,6 +21,7 @@
 #include <memory>
 #include <mutex>
 #include <sys/mman.h>
+#include <unistd.h>
 #include <new>
 #include <set>
 #include <thread>
@@ -116,6 +117,32 @@ private:
     bool stop_ = false;
 };
 
+// Pools outlive the call: a worker set of the same size is taken from this cache and handed back at the
+// end (r03 started and joined 16 threads per call: ~20 ms on the GPU box); concurrent calls each get
+// their own.
+static std::mutex g_pool_mu;
+static std::vector<std::unique_ptr<Pool>> g_pools;
+struct PoolLease {
+    std::unique_ptr<Pool> p;
+    explicit PoolLease(int threads) {
+        if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+        {
+            std::lock_guard<std::mutex> g(g_pool_mu);
+            for (auto it = g_pools.begin(); it != g_pools.end(); ++it)
+                if ((*it)->size() == threads) {
+                    p = std::move(*it);
+                    g_pools.erase(it);
+                    break;
+                }
+        }
+        if (!p) p.reset(new Pool(threads));
+    }
+    ~PoolLease() {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        g_pools.push_back(std::move(p));
+    }
+};
+
 // Hand the pages of a large block about to be freed back to the kernel from all workers: one
 // munmap of ~1 GB frees its pages serially.
 static void release_pages(Pool &pool, void *p, size_t bytes) {
@@ -164,10 +191,6 @@ static void bases_into(const RRead &r, std::string &s) {
     const uint32_t full = r.l_seq >> 1;
     for (uint32_t k = 0; k < full; ++k) memcpy(o + 2 * k, kSeqPairs.p[(uint8_t)r.seq4[k]], 2);
     if (r.l_seq & 1) o[r.l_seq - 1] = kSeqPairs.p[(uint8_t)r.seq4[full]][0];
-}
-static void quals_ascii_into(const RRead &r, std::string &q) {
-    q.assign(r.qual.data(), r.qual.size());
-    for (auto &c : q) c = (char)(c + 33);
 }
 
 bool rread_decode(const uint8_t *rec, RRead &r, std::string &err) {
@@ -376,12 +399,29 @@ struct Fasta {
             return false;
         }
         std::string data;
-        if (fseek(f, 0, SEEK_END) == 0) {
-            long sz = ftell(f);
+        if (fseeko(f, 0, SEEK_END) == 0) {  // regular file: 8 MiB preads on the workers
+            const off_t sz = ftello(f);
             if (sz > 0) {
                 data.resize((size_t)sz);
-                fseek(f, 0, SEEK_SET);
-                data.resize(fread(&data[0], 1, (size_t)sz, f));
+                const int fd = fileno(f);
+                const size_t chunk = 8ull << 20;
+                std::atomic<bool> shortr(false);
+                pool.run_chunks((size_t)sz, chunk, [&](size_t o, size_t e) {
+                    while (o < e) {
+                        const ssize_t r = pread(fd, &data[o], e - o, (off_t)o);
+                        if (r <= 0) {
+                            shortr = true;
+                            return;
+                        }
+                        o += (size_t)r;
+                    }
+                });
+                if (shortr) {
+                    fclose(f);
+                    err = "short read on reference FASTA " + path;
+                    return false;
+                }
+                fseeko(f, sz, SEEK_SET);
             }
         }
         char buf[1 << 16];
@@ -658,9 +698,9 @@ static long mismatching_qualities(const RRead &r, const std::string &ref, int re
     long mq = 0;
     int readIdx = 0;
     const int endOnRead = (int)r.l_seq - 1;
-    thread_local std::string rs, qa;
-    bases_into(r, rs);
-    quals_ascii_into(r, qa);
+    // bases and ASCII qualities read in place (the packed base's character, the phred byte + 33 as a
+    // signed char: what getQueryBases / getQualities would hold), no per-read strings
+    const uint8_t *s4 = (const uint8_t *)r.seq4.data(), *qp = (const uint8_t *)r.qual.data();
     for (auto &ce : r.cigar) {
         if (readIdx > endOnRead) break;
         switch (ce.t) {
@@ -668,7 +708,8 @@ static long mismatching_qualities(const RRead &r, const std::string &ref, int re
                 for (uint32_t j = 0; j < ce.n; ++j, ++refIndex, ++readIdx) {
                     if (refIndex < 0 || refIndex >= (int)ref.size()) continue;
                     if (readIdx > endOnRead) break;
-                    if (rs[readIdx] != ref[refIndex]) mq += (int)(signed char)qa[readIdx] - 33;
+                    const char b = kSeqChars[(s4[readIdx >> 1] >> ((readIdx & 1) ? 0 : 4)) & 15];
+                    if (b != ref[refIndex]) mq += (int)(signed char)(char)(qp[readIdx] + 33) - 33;
                 }
                 break;
             case 'I': case 'S': readIdx += ce.n; break;
@@ -863,12 +904,12 @@ static inline bool bases_equal(char l, char r) {  // SequenceUtil::basesEqual (S
 // SequenceUtil::calculateSamNmTag / sumQualitiesOfMismatches (SequenceUtil.cpp:134-228) over the
 // read's alignment blocks (getAlignmentBlocks :55-88).  UQ sums ASCII qualities (Q23).
 static void nm_uq(const RRead &r, const std::string &ref, int leftmost, int *nm, int *uq) {
-    thread_local std::string rs, qa;
-    bases_into(r, rs);
-    quals_ascii_into(r, qa);
+    // bases and ASCII qualities read in place (as in mismatching_qualities)
+    const uint8_t *s4 = (const uint8_t *)r.seq4.data(), *qp = (const uint8_t *)r.qual.data();
+    const int nseq = (int)r.l_seq, nq = (int)r.qual.size();
     int readBase = 0, refBase = r.pos - leftmost, mis = 0, qs = 0;
     auto refc = [&](int k) -> char { return (k >= 0 && k < (int)ref.size()) ? ref[k] : '\0'; };
-    auto readc = [&](int k) -> char { return (k >= 0 && k < (int)rs.size()) ? rs[k] : '\0'; };
+    auto readc = [&](int k) -> char { return (k >= 0 && k < nseq) ? kSeqChars[(s4[k >> 1] >> ((k & 1) ? 0 : 4)) & 15] : '\0'; };
     for (auto &e : r.cigar) {
         switch (e.t) {
             case 'S': case 'I': readBase += (int)e.n; break;
@@ -878,7 +919,7 @@ static void nm_uq(const RRead &r, const std::string &ref, int leftmost, int *nm,
                     const int k = readBase + (int)i;
                     if (!bases_equal(readc(k), refc(refBase + (int)i))) {
                         mis++;
-                        qs += (int)(signed char)(k < (int)qa.size() ? qa[k] : 0);
+                        qs += (int)(signed char)(k < nq ? (char)(qp[k] + 33) : 0);
                     }
                 }
                 readBase += (int)e.n;
@@ -1267,11 +1308,27 @@ static bool do_not_clean(const RRead &r, const RealignParams &P) {
     return !r.mapped() || (r.flag & 0x100) || (r.flag & 0x200) || r.mapq == 0 || r.pos == -1 || tooBig || is454;
 }
 
+// per-worker busy seconds of a run_static phase (index i runs on worker i % threads): max and mean say
+// how well the phase's work is balanced
+struct Busy {
+    std::vector<double> t;
+    explicit Busy(int threads) : t((size_t)std::max(threads, 1), 0.0) {}
+    void add(size_t i, double s) { t[i % t.size()] += s; }  // each worker only touches its own slot
+    void report(RealignStats &st, const char *name) const {
+        double mx = 0, sum = 0;
+        for (double x : t) mx = std::max(mx, x), sum += x;
+        st.more.emplace_back(std::string(name) + "_busy_max", mx);
+        st.more.emplace_back(std::string(name) + "_busy_avg", sum / (double)t.size());
+    }
+};
+
 int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, const uint64_t *offs, uint64_t n,
                 const std::string &fasta_path, const std::string &intervals_path, const RealignParams &P, const ScanFn &scan,
                 ByteBuf &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err) {
     double t0 = now_s();
-    Pool pool(P.threads);
+    PoolLease lease(P.threads);
+    Pool &pool = *lease.p;
+    st.more.emplace_back("t_pool", now_s() - t0);
     Fasta fa;
     if (!fa.load(fasta_path, err, pool)) return -4;
     std::vector<GLoc> ivs;
@@ -1422,7 +1479,15 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         if (e.t == EV_CLEAN && !e.id->toClean.empty()) work.push_back(e.id);
     std::atomic<bool> ferr(false);
     std::string fmsg;
+    Busy bprep(pool.size());
     pool.run_static(work.size(), [&](size_t w) {
+        const double tb = now_s();
+        struct Acc {
+            Busy &b;
+            size_t w;
+            double t;
+            ~Acc() { b.add(w, now_s() - t); }
+        } acc{bprep, w, tb};
         IntervalData &d = *work[w];
         const std::string &contig = ref_names[d.binLoc.contig];
         const std::string *seq = fa.get(contig);
@@ -1483,6 +1548,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     }
     double t2 = now_s();
     st.t_prepare = t2 - t1;
+    bprep.report(st, "t_prepare");
 
     // ---------------------------------------------------------------- C: offset scan (GPU)
     // batch layout: per-interval extents, prefix sums, then a parallel fill
@@ -1561,7 +1627,14 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     st.t_scan = t3 - t2;
 
     // ---------------------------------------------------------------- D: decide (:713-892)
+    Busy bdec(pool.size());
     pool.run_static(work.size(), [&](size_t w) {
+        struct Acc {
+            Busy &b;
+            size_t w;
+            double t;
+            ~Acc() { b.add(w, now_s() - t); }
+        } acc{bdec, w, now_s()};
         IntervalData &d = *work[w];
         if (d.cons.empty()) return;
         Consensus *best = nullptr;
@@ -1623,6 +1696,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     });
     double t4 = now_s();
     st.t_decide = t4 - t3;
+    bdec.report(st, "t_decide");
 
     // ---------------------------------------------------------------- E: emit + mate fixing
     // The writer (ConstrainedMateFixingManager) flushes everything waiting and forgets its mate map
@@ -1668,6 +1742,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         uint64_t cl = 0, rr = 0;
         size_t left = 0;
     };
+    const double tm0 = now_s();
     std::vector<Seg> segs;
     bool mixed = false;
     {
@@ -1698,11 +1773,19 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         }
     }
     bool sequential = mixed || segs.size() <= 1 || P.mate_sequential;
+    st.more.emplace_back("t_mate_build", now_s() - tm0);
     if (!sequential) {
+        std::vector<double> segt(segs.size(), 0.0);
         pool.run(segs.size(), [&](size_t k) {
+            const double ts = now_s();
             Seg &g = segs[k];
             g.left = emit_events(g.e0, g.e1, g.add0, g.ord, g.cl, g.rr);
+            segt[k] = now_s() - ts;
         });
+        double smax = 0, ssum = 0;
+        for (double x : segt) smax = std::max(smax, x), ssum += x;
+        st.more.emplace_back("t_mate_seg_max", smax);
+        st.more.emplace_back("t_mate_seg_sum", ssum);
         for (size_t k = 0; k + 1 < segs.size(); ++k)
             if (segs[k].left >= (size_t)P.max_records_in_memory) sequential = true;
         if (sequential) {  // undo: fresh records, then the one-writer path
@@ -1716,14 +1799,21 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     if (sequential) {
         order.reserve(n);
         st.tail_waiting = emit_events(0, ev.size(), 0, order, st.intervals_cleaned, st.reads_realigned);
-    } else {
-        order.reserve(n);
-        st.tail_waiting = segs.back().left;
-        for (auto &g : segs) {
-            order.insert(order.end(), g.ord.begin(), g.ord.end());
-            st.intervals_cleaned += g.cl;
-            st.reads_realigned += g.rr;
+    } else {  // the segments' orders side by side (copied by the workers)
+        const double tc = now_s();
+        std::vector<size_t> at(segs.size() + 1, 0);
+        for (size_t k = 0; k < segs.size(); ++k) {
+            at[k + 1] = at[k] + segs[k].ord.size();
+            st.intervals_cleaned += segs[k].cl;
+            st.reads_realigned += segs[k].rr;
         }
+        st.tail_waiting = segs.back().left;
+        order.resize(at.back());
+        pool.run(segs.size(), [&](size_t k) {
+            std::copy(segs[k].ord.begin(), segs[k].ord.end(), order.begin() + (ptrdiff_t)at[k]);
+            std::vector<RRead *>().swap(segs[k].ord);
+        });
+        st.more.emplace_back("t_mate_concat", now_s() - tc);
     }
     st.mate_segments = sequential ? 1 : segs.size();
     st.t_mate = now_s() - t4;
@@ -1755,15 +1845,42 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     });
     st.t_emit = now_s() - t4;
     const double t5 = now_s();
+    st.more.emplace_back("t_encode", t5 - t4 - st.t_mate);
     // teardown on the workers that allocated (run_static, same mapping as prepare/decide)
     pool.run_static(work.size(), [&](size_t w) {
         IntervalData &d = *work[w];
         for (auto &pu : d.pending) std::string().swap(pu.first->tags_own);
         *work[w] = IntervalData();
     });
+    const double t6 = now_s();
     ids.clear();
+    const double t7 = now_s();
     reads.release();
     st.t_release = now_s() - t5;
+    st.more.emplace_back("t_release_intervals", t6 - t5);
+    st.more.emplace_back("t_release_ids", t7 - t6);
+    st.more.emplace_back("t_release_reads", now_s() - t7);
+    // the large temporaries freed on the workers side by side (r03: by their destructors at return,
+    // one after another on this thread -- ~0.14 s of munmap on the GPU box)
+    const double t8 = now_s();
+    {
+        std::vector<std::function<void()>> jobs = {
+            [&] { decltype(ev)().swap(ev); },
+            [&] { ScanBatch tmp = std::move(B); },
+            [&] { decltype(bidx)().swap(bidx); },
+            [&] { decltype(bscore)().swap(bscore); },
+            [&] { decltype(segs)().swap(segs); },
+            [&] { decltype(order)().swap(order); },
+            [&] { decltype(lstop)().swap(lstop); },
+            [&] { decltype(dnc)().swap(dnc); },
+            [&] { decltype(work)().swap(work); },
+            [&] { decltype(fa.seq) tmp = std::move(fa.seq); },
+        };
+        pool.run(jobs.size(), [&](size_t i) { jobs[i](); });
+    }
+    st.more.emplace_back("t_release_temps", now_s() - t8);
+    st.t_release = now_s() - t5;
+    st.more.emplace_back("t_at_return", now_s() - t0);  // t_run minus this: the locals' destructors
     return 0;
 }
 

@@ -202,6 +202,7 @@ struct RealignStats {
     double t_bin = 0, t_prepare = 0, t_scan = 0, t_decide = 0, t_emit = 0, t_run = 0;
     double t_fasta = 0, t_decode = 0, t_mate = 0, t_release = 0;  // parts of t_bin / t_emit; teardown
     double t_scan_build = 0;                                       // part of t_scan: batch assembly
+    std::vector<std::pair<std::string, double>> more;              // finer timers (name, seconds), in the stats JSON
 };
 
 // Output record bytes: malloc'ed without zero-fill so the parallel encoder's first touch is the only

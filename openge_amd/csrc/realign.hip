@@ -527,6 +527,14 @@ int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len,
              st.t_scan, st.t_decide, st.t_emit, st.t_run, st.t_fasta, st.t_decode, st.t_mate, st.t_release, st.t_scan_build, ctx->scan_t[0], ctx->scan_t[1], ctx->scan_t[2],
              (unsigned long long)st.mate_segments, (unsigned long long)st.tail_waiting, ctx->last_scan_generic ? "k_realign_scan (byte-wise)" : "k_planes + k_scan_bp");
     r->stats = buf;
+    if (!st.more.empty()) {  // the finer timers, appended before the closing brace
+        r->stats.pop_back();
+        for (auto &m : st.more) {
+            snprintf(buf, sizeof buf, ", \"%s\": %.4f", m.first.c_str(), m.second);
+            r->stats += buf;
+        }
+        r->stats += "}";
+    }
     *out = r.release();
     return OGE_OK;
 }

@@ -42,8 +42,31 @@ void *realign_cpu(const char *header, uint64_t hlen, const uint8_t *recs, const 
     oge::ScanFn scan = [](const oge::ScanBatch &B, std::vector<int32_t> &bi, std::vector<int32_t> &bs) {
         bi.resize(B.pairs.size());
         bs.resize(B.pairs.size());
-        return oracle_realign_scan(B.cons.data(), B.cons_off.data(), B.bases.data(), B.quals.data(), B.read_off.data(),
-                                   (const int32_t *)B.pairs.data(), B.pairs.size(), bi.data(), bs.data());
+        // OGE_TEST_SCAN_CACHE=path (host-phase timing runs, tools/realign_prof.py): the scan's results
+        // for this batch are kept in a file keyed by the pair count and reused, so the literal scan
+        // (minutes at C5 size) runs once
+        const char *cache = std::getenv("OGE_TEST_SCAN_CACHE");
+        const uint64_t np = B.pairs.size();
+        if (cache) {
+            if (FILE *f = std::fopen(cache, "rb")) {
+                uint64_t k = 0;
+                bool ok = std::fread(&k, 8, 1, f) == 1 && k == np && std::fread(bi.data(), 4, np, f) == np &&
+                          std::fread(bs.data(), 4, np, f) == np;
+                std::fclose(f);
+                if (ok) return 0;
+            }
+        }
+        int rc = oracle_realign_scan(B.cons.data(), B.cons_off.data(), B.bases.data(), B.quals.data(), B.read_off.data(),
+                                     (const int32_t *)B.pairs.data(), np, bi.data(), bs.data());
+        if (!rc && cache) {
+            if (FILE *f = std::fopen(cache, "wb")) {
+                std::fwrite(&np, 8, 1, f);
+                std::fwrite(bi.data(), 4, np, f);
+                std::fwrite(bs.data(), 4, np, f);
+                std::fclose(f);
+            }
+        }
+        return rc;
     };
     oge::RealignStats st;
     std::string err;
@@ -56,6 +79,14 @@ void *realign_cpu(const char *header, uint64_t hlen, const uint8_t *recs, const 
              st.t_bin, st.t_prepare, st.t_scan, st.t_decide, st.t_emit, st.t_run, st.t_fasta, st.t_decode, st.t_mate, st.t_release, (unsigned long long)st.scan_pairs,
              (unsigned long long)st.mate_segments, (unsigned long long)st.tail_waiting);
     o->stats = b;
+    if (!st.more.empty()) {  // the product's finer timers
+        o->stats.pop_back();
+        for (auto &m : st.more) {
+            snprintf(b, sizeof b, ", \"%s\": %.4f", m.first.c_str(), m.second);
+            o->stats += b;
+        }
+        o->stats += "}";
+    }
     return o;
 }
 const char *realign_cpu_error(void *h) { return ((Out *)h)->msg.c_str(); }
