@@ -117,32 +117,6 @@ private:
     bool stop_ = false;
 };
 
-// Pools outlive the call: a worker set of the same size is taken from this cache and handed back at the
-// end (r03 started and joined 16 threads per call: ~20 ms on the GPU box); concurrent calls each get
-// their own.
-static std::mutex g_pool_mu;
-static std::vector<std::unique_ptr<Pool>> g_pools;
-struct PoolLease {
-    std::unique_ptr<Pool> p;
-    explicit PoolLease(int threads) {
-        if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
-        {
-            std::lock_guard<std::mutex> g(g_pool_mu);
-            for (auto it = g_pools.begin(); it != g_pools.end(); ++it)
-                if ((*it)->size() == threads) {
-                    p = std::move(*it);
-                    g_pools.erase(it);
-                    break;
-                }
-        }
-        if (!p) p.reset(new Pool(threads));
-    }
-    ~PoolLease() {
-        std::lock_guard<std::mutex> g(g_pool_mu);
-        g_pools.push_back(std::move(p));
-    }
-};
-
 // Hand the pages of a large block about to be freed back to the kernel from all workers: one
 // munmap of ~1 GB frees its pages serially.
 static void release_pages(Pool &pool, void *p, size_t bytes) {
@@ -390,6 +364,7 @@ static void tag_edit_i32(std::string &t, const char *tag, int32_t v) {
 // the raw bytes (case preserved).
 struct Fasta {
     std::unordered_map<std::string, std::string> seq;
+    std::string data;  // the file (kept, like the sequences' storage, for the next load: see Scratch)
     // Whole file in one read; contigs (">" lines) located serially, their bodies de-lined in
     // parallel.  Line handling as FastaReader: name up to the first blank, CR before LF dropped.
     bool load(const std::string &path, std::string &err, Pool &pool) {
@@ -398,7 +373,7 @@ struct Fasta {
             err = "cannot open reference FASTA " + path;
             return false;
         }
-        std::string data;
+        data.clear();
         if (fseeko(f, 0, SEEK_END) == 0) {  // regular file: 8 MiB preads on the workers
             const off_t sz = ftello(f);
             if (sz > 0) {
@@ -432,15 +407,30 @@ struct Fasta {
         const char *b = data.data(), *e = b + data.size();
         for (const char *q = b; q < e && (q = (const char *)memchr(q, '>', (size_t)(e - q))); ++q)
             if (q == b || q[-1] == '\n') hs.push_back((size_t)(q - b));
-        std::vector<std::string> names(hs.size()), bodies(hs.size());
-        pool.run(hs.size(), [&](size_t c) {
+        // names first (serially: the map's entries are made here, the last of a repeated name wins),
+        // then the bodies into the entries' strings (their storage reused across loads)
+        std::vector<std::string> names(hs.size());
+        std::vector<size_t> les(hs.size());
+        for (size_t c = 0; c < hs.size(); ++c) {
             const size_t h = hs[c], stop = c + 1 < hs.size() ? hs[c + 1] : data.size();
             size_t le = data.find('\n', h);
             if (le == std::string::npos || le > stop) le = stop;
             size_t ne = h + 1;
             while (ne < le && data[ne] != ' ' && data[ne] != '\t' && data[ne] != '\r') ++ne;
             names[c].assign(data, h + 1, ne - h - 1);
-            std::string &out = bodies[c];
+            les[c] = le;
+        }
+        std::unordered_map<std::string, size_t> last;
+        for (size_t c = 0; c < hs.size(); ++c) last[names[c]] = c;
+        for (auto it = seq.begin(); it != seq.end();)  // contigs of an earlier file that this one lacks
+            it = last.count(it->first) ? std::next(it) : seq.erase(it);
+        std::vector<std::string *> bodies(hs.size(), nullptr);
+        for (auto &kv : last) bodies[kv.second] = &seq[kv.first];
+        pool.run(hs.size(), [&](size_t c) {
+            if (!bodies[c]) return;  // a repeated name: a later entry holds it
+            const size_t stop = c + 1 < hs.size() ? hs[c + 1] : data.size(), le = les[c];
+            std::string &out = *bodies[c];
+            out.clear();
             out.reserve(stop > le ? stop - le : 0);
             size_t p = le + 1;
             while (p < stop) {
@@ -452,7 +442,6 @@ struct Fasta {
                 p = q + 1;
             }
         });
-        for (size_t c = 0; c < hs.size(); ++c) seq[names[c]] = std::move(bodies[c]);
         if (seq.empty()) {
             err = "no sequences in reference FASTA " + path;
             return false;
@@ -951,6 +940,19 @@ struct IntervalData {
     uint64_t pairBase = 0;
     std::vector<std::pair<RRead *, RRead>> pending;  // read -> updated copy (applied in phase E)
     bool cleanable = false;
+    // back to a fresh interval, keeping the containers' capacity (the objects are reused across calls)
+    void reset(int iv) {
+        interval = iv;
+        toClean.clear(), notToClean.clear();
+        binLoc = GLoc();
+        hasLoc = false;
+        reference.clear();
+        leftmost = 0;
+        totalRaw = 0;
+        alt.clear(), arena.clear(), cons.clear(), pending.clear();
+        pairBase = 0;
+        cleanable = false;
+    }
 };
 
 enum EvType { EV_READ, EV_CLEAN, EV_LIST };
@@ -1308,6 +1310,55 @@ static bool do_not_clean(const RRead &r, const RealignParams &P) {
     return !r.mapped() || (r.flag & 0x100) || (r.flag & 0x200) || r.mapq == 0 || r.pos == -1 || tooBig || is454;
 }
 
+// A worker pool and the run's large containers, kept across calls (taken from this cache and handed
+// back at the end; concurrent calls each get their own).  r03 started and joined 16 threads per call
+// (~20 ms on the GPU box), allocated the record array, the event list, the scan batch and 50k interval
+// objects afresh -- first touch of every page -- and freed them at return (~0.15 s of destructors and
+// munmap).  Reused containers are cleared, not freed: their capacity carries over.
+struct Scratch {
+    std::unique_ptr<Pool> pool;
+    RRead *rmem = nullptr;  // the decoded records: [0, rlive) constructed and kept across calls (the decode
+    uint64_t rcap = 0, rlive = 0;  // overwrites every field; cigar / owned-tag storage is reused)
+    std::vector<int32_t> lstop;
+    std::vector<uint8_t> dnc;
+    std::vector<std::unique_ptr<IntervalData>> ids;
+    std::vector<Event> ev;
+    std::vector<IntervalData *> work;
+    ScanBatch B;
+    std::vector<int32_t> bidx, bscore;
+    std::vector<RRead *> order;
+    Fasta fa;
+    ~Scratch() {
+        for (uint64_t i = 0; i < rlive; ++i) rmem[i].~RRead();
+        std::free(rmem);
+    }
+};
+static std::mutex g_scratch_mu;
+static std::vector<std::unique_ptr<Scratch>> g_scratch;
+struct ScratchLease {
+    std::unique_ptr<Scratch> s;
+    explicit ScratchLease(int threads) {
+        if (threads <= 0) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+        {
+            std::lock_guard<std::mutex> g(g_scratch_mu);
+            for (auto it = g_scratch.begin(); it != g_scratch.end(); ++it)
+                if ((*it)->pool->size() == threads) {
+                    s = std::move(*it);
+                    g_scratch.erase(it);
+                    break;
+                }
+        }
+        if (!s) {
+            s.reset(new Scratch());
+            s->pool.reset(new Pool(threads));
+        }
+    }
+    ~ScratchLease() {
+        std::lock_guard<std::mutex> g(g_scratch_mu);
+        g_scratch.push_back(std::move(s));
+    }
+};
+
 // per-worker busy seconds of a run_static phase (index i runs on worker i % threads): max and mean say
 // how well the phase's work is balanced
 struct Busy {
@@ -1326,10 +1377,11 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
                 const std::string &fasta_path, const std::string &intervals_path, const RealignParams &P, const ScanFn &scan,
                 ByteBuf &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err) {
     double t0 = now_s();
-    PoolLease lease(P.threads);
-    Pool &pool = *lease.p;
+    ScratchLease lease(P.threads);
+    Scratch &S = *lease.s;
+    Pool &pool = *S.pool;
     st.more.emplace_back("t_pool", now_s() - t0);
-    Fasta fa;
+    Fasta &fa = S.fa;
     if (!fa.load(fasta_path, err, pool)) return -4;
     std::vector<GLoc> ivs;
     if (!parse_intervals(intervals_path, ref_names, ivs, err)) return -1;
@@ -1342,34 +1394,40 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         RRead *p;
         uint64_t n;
         Pool &pool;
-        ~ReadArray() { release(); }
-        void release() {
-            pool.run_chunks(n, dchunk, [&](size_t b, size_t e) {
-                for (size_t i = b; i < e; ++i) p[i].~RRead();
-            });
-            if (p) release_pages(pool, p, n * sizeof(RRead));
-            std::free(p);
-            p = nullptr;
-            n = 0;
-        }
         RRead &operator[](uint64_t i) { return p[i]; }
     };
-    RRead *rmem = (RRead *)std::malloc(std::max<uint64_t>(n, 1) * sizeof(RRead));
-    if (!rmem) {
-        err = "out of host memory for the decoded records";
-        return -1;
+    if (S.rcap < std::max<uint64_t>(n, 1)) {
+        pool.run_chunks(S.rlive, dchunk, [&](size_t b, size_t e) {
+            for (size_t i = b; i < e; ++i) S.rmem[i].~RRead();
+        });
+        S.rlive = 0;
+        std::free(S.rmem);
+        S.rcap = 0;
+        S.rmem = (RRead *)std::malloc(std::max<uint64_t>(n, 1) * sizeof(RRead));
+        if (!S.rmem) {
+            err = "out of host memory for the decoded records";
+            return -1;
+        }
+        S.rcap = std::max<uint64_t>(n, 1);
     }
+    RRead *rmem = S.rmem;
     ReadArray reads{rmem, 0, pool};
-    pool.run_chunks(n, dchunk, [&](size_t b, size_t e) {
-        for (size_t i = b; i < e; ++i) new (&rmem[i]) RRead();
-    });
+    if (S.rlive < n) {
+        const uint64_t r0 = S.rlive;
+        pool.run_chunks(n - r0, dchunk, [&](size_t b, size_t e) {
+            for (size_t i = r0 + b; i < r0 + e; ++i) new (&rmem[i]) RRead();
+        });
+        S.rlive = n;
+    }
     reads.n = n;
     std::atomic<bool> bad(false);
     std::mutex emu;
     std::string derr;
     // decode, plus what binning asks of every read (its GenomeLoc stop, doNotTryToClean)
-    std::vector<int32_t> lstop(n);
-    std::vector<uint8_t> dnc(n);
+    std::vector<int32_t> &lstop = S.lstop;  // (every entry written by the decode below)
+    std::vector<uint8_t> &dnc = S.dnc;
+    lstop.resize(n);
+    dnc.resize(n);
     pool.run_chunks(n, dchunk, [&](size_t b, size_t end) {
         std::string e;
         for (size_t i = b; i < end; ++i) {
@@ -1399,12 +1457,15 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     st.t_fasta = tf - t0;
     st.t_decode = td - tf;
     // ---------------------------------------------------------------- A: map_func (:455-553)
-    std::vector<std::unique_ptr<IntervalData>> ids;
-    std::vector<Event> ev;
+    std::vector<std::unique_ptr<IntervalData>> &ids = S.ids;  // objects reused across calls
+    size_t nids = 0;
+    std::vector<Event> &ev = S.ev;
+    ev.clear();
     auto new_id = [&](int interval) {
-        ids.emplace_back(new IntervalData());
-        ids.back()->interval = interval;
-        return ids.back().get();
+        if (nids == ids.size()) ids.emplace_back(new IntervalData());
+        IntervalData *d = ids[nids++].get();
+        d->reset(interval);
+        return d;
     };
     size_t it = 0;
     IntervalData *loading = new_id(ivs.empty() ? -1 : 0);
@@ -1474,7 +1535,8 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     st.t_bin = t1 - t0;
 
     // ---------------------------------------------------------------- B: prepare (:681-700, :918-999)
-    std::vector<IntervalData *> work;
+    std::vector<IntervalData *> &work = S.work;
+    work.clear();
     for (auto &e : ev)
         if (e.t == EV_CLEAN && !e.id->toClean.empty()) work.push_back(e.id);
     std::atomic<bool> ferr(false);
@@ -1552,7 +1614,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
 
     // ---------------------------------------------------------------- C: offset scan (GPU)
     // batch layout: per-interval extents, prefix sums, then a parallel fill
-    ScanBatch B;
+    ScanBatch &B = S.B;  // (resized below; every byte written)
     const size_t nw = work.size();
     std::vector<uint64_t> xc(nw + 1, 0), xcb(nw + 1, 0), xr(nw + 1, 0), xrb(nw + 1, 0), xp(nw + 1, 0);
     for (size_t w = 0; w < nw; ++w) {
@@ -1615,7 +1677,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     for (uint64_t o : wops) st.scan_ops += o;
     st.scan_pairs = B.pairs.size();
     st.t_scan_build = now_s() - t2;
-    std::vector<int32_t> bidx, bscore;
+    std::vector<int32_t> &bidx = S.bidx, &bscore = S.bscore;
     if (!B.pairs.empty()) {
         int rc = scan(B, bidx, bscore);
         if (rc) {
@@ -1795,7 +1857,8 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
             });
         }
     }
-    std::vector<RRead *> order;
+    std::vector<RRead *> &order = S.order;
+    order.clear();
     if (sequential) {
         order.reserve(n);
         st.tail_waiting = emit_events(0, ev.size(), 0, order, st.intervals_cleaned, st.reads_realigned);
@@ -1846,40 +1909,14 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     st.t_emit = now_s() - t4;
     const double t5 = now_s();
     st.more.emplace_back("t_encode", t5 - t4 - st.t_mate);
-    // teardown on the workers that allocated (run_static, same mapping as prepare/decide)
-    pool.run_static(work.size(), [&](size_t w) {
-        IntervalData &d = *work[w];
-        for (auto &pu : d.pending) std::string().swap(pu.first->tags_own);
-        *work[w] = IntervalData();
-    });
+    // teardown: the intervals reset on the workers (their containers keep their capacity for the next
+    // call); the records and the large containers stay with the scratch (see Scratch)
+    pool.run(nids, [&](size_t k) { ids[k]->reset(-1); });
     const double t6 = now_s();
-    ids.clear();
-    const double t7 = now_s();
-    reads.release();
+    for (auto &g : segs) std::vector<RRead *>().swap(g.ord);
     st.t_release = now_s() - t5;
     st.more.emplace_back("t_release_intervals", t6 - t5);
-    st.more.emplace_back("t_release_ids", t7 - t6);
-    st.more.emplace_back("t_release_reads", now_s() - t7);
-    // the large temporaries freed on the workers side by side (r03: by their destructors at return,
-    // one after another on this thread -- ~0.14 s of munmap on the GPU box)
-    const double t8 = now_s();
-    {
-        std::vector<std::function<void()>> jobs = {
-            [&] { decltype(ev)().swap(ev); },
-            [&] { ScanBatch tmp = std::move(B); },
-            [&] { decltype(bidx)().swap(bidx); },
-            [&] { decltype(bscore)().swap(bscore); },
-            [&] { decltype(segs)().swap(segs); },
-            [&] { decltype(order)().swap(order); },
-            [&] { decltype(lstop)().swap(lstop); },
-            [&] { decltype(dnc)().swap(dnc); },
-            [&] { decltype(work)().swap(work); },
-            [&] { decltype(fa.seq) tmp = std::move(fa.seq); },
-        };
-        pool.run(jobs.size(), [&](size_t i) { jobs[i](); });
-    }
-    st.more.emplace_back("t_release_temps", now_s() - t8);
-    st.t_release = now_s() - t5;
+    st.more.emplace_back("t_release_reads", now_s() - t6);
     st.more.emplace_back("t_at_return", now_s() - t0);  // t_run minus this: the locals' destructors
     return 0;
 }
