@@ -32,9 +32,12 @@
 namespace oge {
 
 // =====================================================================================  threads
-// Persistent workers for one realign_run.  run_static maps index i to worker i % size() in every
-// phase, so what a worker allocates for interval i (prepare, decide) it also frees (teardown): the
-// frees stay in that thread's malloc arena instead of contending for other threads' arena locks.
+// Persistent workers (kept across calls with the run's Scratch).  run_static maps index i to worker
+// i % size(); run hands indices out one at a time (prepare and decide: intervals differ in size; r03
+// mapped them statically so each interval's frees stayed in its allocating thread's arena -- the
+// interval objects are now reused instead of freed).
+static thread_local int tl_worker = 0;  // the Pool worker running the current job (0 = the caller)
+
 class Pool {
 public:
     explicit Pool(int threads) {
@@ -58,6 +61,7 @@ public:
             return;
         }
         exec([&](int t) {
+            tl_worker = t;
             for (size_t i = (size_t)t; i < n; i += (size_t)n_) f(i);
         });
     }
@@ -68,7 +72,8 @@ public:
             return;
         }
         std::atomic<size_t> next(0);
-        exec([&](int) {
+        exec([&](int t) {
+            tl_worker = t;
             for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
         });
     }
@@ -1359,12 +1364,11 @@ struct ScratchLease {
     }
 };
 
-// per-worker busy seconds of a run_static phase (index i runs on worker i % threads): max and mean say
-// how well the phase's work is balanced
+// per-worker busy seconds of a parallel phase: max and mean say how well its work is balanced
 struct Busy {
     std::vector<double> t;
     explicit Busy(int threads) : t((size_t)std::max(threads, 1), 0.0) {}
-    void add(size_t i, double s) { t[i % t.size()] += s; }  // each worker only touches its own slot
+    void add(size_t, double s) { t[(size_t)tl_worker % t.size()] += s; }  // each worker only touches its own slot
     void report(RealignStats &st, const char *name) const {
         double mx = 0, sum = 0;
         for (double x : t) mx = std::max(mx, x), sum += x;
@@ -1542,7 +1546,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     std::atomic<bool> ferr(false);
     std::string fmsg;
     Busy bprep(pool.size());
-    pool.run_static(work.size(), [&](size_t w) {
+    pool.run(work.size(), [&](size_t w) {  // (dynamic: intervals differ in size)
         const double tb = now_s();
         struct Acc {
             Busy &b;
@@ -1690,7 +1694,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
 
     // ---------------------------------------------------------------- D: decide (:713-892)
     Busy bdec(pool.size());
-    pool.run_static(work.size(), [&](size_t w) {
+    pool.run(work.size(), [&](size_t w) {
         struct Acc {
             Busy &b;
             size_t w;
