@@ -1812,37 +1812,70 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     std::vector<Seg> segs;
     bool mixed = false;
     {
+        // each event's contig and record count, chunk by chunk on the workers (an interval's lists are
+        // walked: a bin whose records span two contigs sends the phase to the sequential path); then a
+        // segment starts at every event with records whose contig differs from the previous such event
+        struct Cut {
+            size_t k;
+            int32_t ref;
+            uint64_t adds;  // records of the chunk before event k
+        };
+        struct Part {
+            std::vector<Cut> cuts;  // events with records whose contig differs from the chunk's previous one
+            uint64_t adds = 0;
+            bool mixed = false;
+        };
+        const size_t echunk = 16384, nch = (ev.size() + echunk - 1) / echunk;
+        std::vector<Part> parts(nch);
+        pool.run(nch, [&](size_t c) {
+            Part &pt = parts[c];
+            int32_t cur = INT32_MIN;
+            for (size_t k = c * echunk, ke = std::min(ev.size(), k + echunk); k < ke; ++k) {
+                const Event &e = ev[k];
+                int32_t ref = INT32_MIN;
+                uint64_t cnt = 0;
+                if (e.t == EV_READ) {
+                    ref = e.read->ref;
+                    cnt = 1;
+                } else {
+                    const IntervalData &d = *e.id;
+                    for (const auto *v : {&d.notToClean, &d.toClean})
+                        for (RRead *r : *v) {
+                            if (ref == INT32_MIN) ref = r->ref;
+                            else if (r->ref != ref) pt.mixed = true;
+                            cnt++;
+                        }
+                }
+                if (cnt && ref != cur) {
+                    pt.cuts.push_back(Cut{k, ref, pt.adds});
+                    cur = ref;
+                }
+                pt.adds += cnt;
+            }
+        });
         uint64_t adds = 0;
         int32_t cur = INT32_MIN;
-        for (size_t k = 0; k < ev.size(); ++k) {
-            const Event &e = ev[k];
-            int32_t ref = INT32_MIN;
-            uint64_t cnt = 0;
-            if (e.t == EV_READ) {
-                ref = e.read->ref;
-                cnt = 1;
-            } else {
-                const IntervalData &d = *e.id;
-                for (const auto *v : {&d.notToClean, &d.toClean})
-                    for (RRead *r : *v) {
-                        if (ref == INT32_MIN) ref = r->ref;
-                        else if (r->ref != ref) mixed = true;
-                        cnt++;
-                    }
+        for (auto &pt : parts) {
+            mixed |= pt.mixed;
+            for (auto &ct : pt.cuts) {
+                if (ct.ref == cur) continue;  // (a chunk's first cut continues the previous chunk's contig)
+                if (!segs.empty()) segs.back().e1 = ct.k;
+                segs.push_back(Seg{segs.empty() ? 0 : ct.k, ev.size(), adds + ct.adds, {}, 0, 0, 0});
+                cur = ct.ref;
             }
-            if (cnt && ref != cur) {
-                if (!segs.empty()) segs.back().e1 = k;
-                segs.push_back(Seg{segs.empty() ? 0 : k, ev.size(), adds, {}, 0, 0, 0});
-                cur = ref;
-            }
-            adds += cnt;
+            adds += pt.adds;
         }
     }
     bool sequential = mixed || segs.size() <= 1 || P.mate_sequential;
     st.more.emplace_back("t_mate_build", now_s() - tm0);
     if (!sequential) {
         std::vector<double> segt(segs.size(), 0.0);
-        pool.run(segs.size(), [&](size_t k) {
+        std::vector<size_t> big(segs.size());  // the largest segments handed out first
+        for (size_t k = 0; k < segs.size(); ++k) big[k] = k;
+        auto recs_in = [&](size_t k) { return (k + 1 < segs.size() ? segs[k + 1].add0 : (uint64_t)n) - segs[k].add0; };
+        std::stable_sort(big.begin(), big.end(), [&](size_t a, size_t b) { return recs_in(a) > recs_in(b); });
+        pool.run(segs.size(), [&](size_t j) {
+            const size_t k = big[j];
             const double ts = now_s();
             Seg &g = segs[k];
             g.left = emit_events(g.e0, g.e1, g.add0, g.ord, g.cl, g.rr);
@@ -1906,6 +1939,12 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     if (!out.alloc(out_off[n])) {
         err = "out of host memory for the output records";
         return -1;
+    }
+    {  // fresh pages for ~1 GB of output: 2 MiB pages where the kernel allows them (512x fewer faults
+       // in the parallel encode below)
+        const uintptr_t a = ((uintptr_t)out.data() + (2ull << 20) - 1) & ~(uintptr_t)((2ull << 20) - 1);
+        const uintptr_t e = ((uintptr_t)out.data() + out_off[n]) & ~(uintptr_t)((2ull << 20) - 1);
+        if (e > a) madvise((void *)a, e - a, MADV_HUGEPAGE);
     }
     pool.run_chunks(n, chunk, [&](size_t b, size_t e) {
         for (size_t i = b; i < e; ++i) rread_encode_to(*order[i], out.data() + out_off[i]);
