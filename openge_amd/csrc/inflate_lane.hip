@@ -745,6 +745,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     __shared__ uint32_t crctab[4][256];
     __shared__ uint32_t zp[17][32];
     __shared__ uint32_t crcs[kT2 / 64];
+    __shared__ __align__(16) uint8_t xl[kXTab];
     const uint32_t t = threadIdx.x;
     const uint64_t b = b0 + blockIdx.x;
     const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
@@ -763,6 +764,16 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
 #define ZCLK()
 #endif
     ZCLK();
+    // 0. this window's hole / deferred-literal bitmap pair, loaded first so its latency overlaps the
+    //    block loads below (r03 loaded it after the refs-init barrier: a second exposed round trip)
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    u64x2 hv = {0, 0};
+    if (t < ((osz + 63) >> 6)) hv = *(const OGE_G u64x2 *)((const OGE_G uint64_t *)(bitmap + (b - b0) * 2048) + 2 * t);
+    // the block's long-literal translation lists (1,280 B), staged in LDS with the refs init below:
+    // the deferred literals of step 5 then look their bytes up without a global round trip each
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 xv = {0, 0, 0, 0};
+    if (t < kXTab / 16) xv = *(const OGE_G u32x4 *)(xtab + (b - b0) * kXTab + 16 * t);
     // 1. this thread's 64 literal-filled bytes [q0, q0 + 64) and the next word (descriptors may
     //    straddle): aligned dword loads, funnel-shifted
     uint32_t wv[17];
@@ -778,6 +789,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         for (int k = 0; k < 17; ++k) wv[k] = sh ? __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh) : raw[k];
     }
     ZCLK();
+    if (t < kXTab / 16) *(u32x4 *)(xl + 16 * t) = xv;
     // 2. every position its own source
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) {
@@ -789,16 +801,9 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     __syncthreads();
     ZCLK();
     // 3. holes: refs[p + j] = p - D + j, descriptors read from this thread's window registers
-    const OGE_G uint64_t *bmp = (const OGE_G uint64_t *)(bitmap + (b - b0) * 2048);
-    const uint32_t nw = (osz + 63) >> 6;
-    uint64_t dm = 0;  // this window's deferred literals
+    uint64_t dm = hv.y;  // this window's deferred literals
     {
-        uint64_t m = 0;
-        if (t < nw) {
-            typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-            const u64x2 hv = *(const OGE_G u64x2 *)(bmp + 2 * t);
-            m = hv.x, dm = hv.y;
-        }
+        uint64_t m = hv.x;
         while (m) {
             const uint32_t jb = (uint32_t)__builtin_ctzll(m);  // byte in the window
             m &= m - 1;
@@ -915,14 +920,12 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     // deferred literals of this window: the byte phase 1 wrote is the code's index in its table's
     // canonical long-code list; the table is the last one whose first position is <= the literal's
     if (dm) {
-        const OGE_G uint8_t *xb = (const OGE_G uint8_t *)(xtab + (b - b0) * kXTab);
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 xs = *(const OGE_G u32x4 *)(xb + kXStart);
+        const u32x4 xs = *(const u32x4 *)(xl + kXStart);
         while (dm) {
             const uint32_t p = q0 + (uint32_t)__builtin_ctzll(dm);
             dm &= dm - 1;
             const uint32_t tb = (p >= xs.w ? 3u : p >= xs.z ? 2u : p >= xs.y ? 1u : 0u);
-            img[ib(p)] = xb[tb * kXList + img[ib(p)]];
+            img[ib(p)] = xl[tb * kXList + img[ib(p)]];
         }
     }
     __syncthreads();
