@@ -722,12 +722,35 @@ struct LdsBits {  // LSB-first bit writer into LDS words; its first and last wor
     }
 };
 
-__device__ __forceinline__ uint32_t match_bits(uint32_t m, const uint32_t *lit, const uint32_t *dist) {
-    const uint32_t L = ((m >> 15) & 255) + 3, D = (m & 0x7fff) + 1;
-    uint32_t sym, nb, ev, dsym, dnb, dev;
-    len_code(L, sym, nb, ev);
-    dist_code(D, dsym, dnb, dev);
-    return (lit[sym] >> 16) + nb + (dist[dsym] >> 16) + dnb;
+// The emitter's symbol table ct[512] (LDS, built per payload): ct[b] (b < 256) = literal b, ct[256 + L - 3]
+// = match length L with its extra bits -- bit-reversed code | extra << code length in the low 24 bits,
+// total bit count << 24: one lookup for either, no length-symbol arithmetic per match (r03 looked the
+// length symbol up through len_code, branches the whole wave ran at every match position).
+__device__ __forceinline__ uint32_t ct_entry(uint32_t i, const uint32_t *tlit) {
+    if (i < 256) {
+        const uint32_t c = tlit[i];
+        return (c & 0xffff) | (c >> 16) << 24;
+    }
+    uint32_t sym, nb, ev;
+    len_code(i - 256 + 3, sym, nb, ev);
+    const uint32_t c = tlit[sym];
+    return ((c & 0xffff) | (ev << (c >> 16))) | ((c >> 16) + nb) << 24;
+}
+// distance 1..32768 -> code | extra << code length, bit count (branch-free; dist_code's cases as selects)
+__device__ __forceinline__ void dist_bits(uint32_t D, const uint32_t *dist, uint32_t &v, uint32_t &n) {
+    const uint32_t d = D - 1, lg = 31 - __builtin_clz(d | 1);
+    const bool small = d < 4;
+    const uint32_t dnb = small ? 0u : lg - 1;
+    const uint32_t dsym = small ? d : 2 * lg + ((d >> ((lg - 1) & 31)) & 1);
+    const uint32_t dev = d & ((1u << dnb) - 1);
+    const uint32_t c = dist[dsym];
+    v = (c & 0xffff) | (dev << (c >> 16));
+    n = (c >> 16) + dnb;
+}
+__device__ __forceinline__ uint32_t match_bits(uint32_t m, const uint32_t *ct, const uint32_t *dist) {
+    uint32_t dv, dn;
+    dist_bits((m & 0x7fff) + 1, dist, dv, dn);
+    return (ct[256 + ((m >> 15) & 255)] >> 24) + dn;
 }
 
 // a segment's 64 payload bytes (zero past len) into registers
@@ -766,38 +789,34 @@ __device__ __forceinline__ void seg_tokens(const uint32_t *mp, uint32_t nm, uint
 }
 
 __device__ __forceinline__ uint32_t seg_bits(const uint32_t (&w)[16], uint64_t lm, uint32_t nm, const uint32_t *mp,
-                                             const uint32_t (&m)[kMPre], const uint32_t *lit, const uint32_t *dist) {
+                                             const uint32_t (&m)[kMPre], const uint32_t *ct, const uint32_t *dist) {
     uint32_t bits = 0;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         uint32_t c[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) c[i] = lit[(w[4 * g + (i >> 2)] >> (8 * (i & 3))) & 0xff];
+        for (int i = 0; i < 16; ++i) c[i] = ct[(w[4 * g + (i >> 2)] >> (8 * (i & 3))) & 0xff];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) bits += (lm >> (16 * g + i)) & 1 ? c[i] >> 16 : 0u;
+        for (int i = 0; i < 16; ++i) bits += (lm >> (16 * g + i)) & 1 ? c[i] >> 24 : 0u;
     }
 #pragma unroll
     for (int k = 0; k < kMPre; ++k)
-        if ((uint32_t)k < nm) bits += match_bits(m[k], lit, dist);
-    for (uint32_t k = kMPre; k < nm; ++k) bits += match_bits(mp[(uint64_t)k * kNSeg], lit, dist);
+        if ((uint32_t)k < nm) bits += match_bits(m[k], ct, dist);
+    for (uint32_t k = kMPre; k < nm; ++k) bits += match_bits(mp[(uint64_t)k * kNSeg], ct, dist);
     return bits;
 }
 
 __device__ __forceinline__ void seg_emit(const uint32_t (&w)[16], uint64_t lm, uint32_t nm, const uint32_t *mp,
-                                         uint32_t (&m)[kMPre], const uint32_t *lit, const uint32_t *dist, uint32_t *img,
+                                         uint32_t (&m)[kMPre], const uint32_t *ct, const uint32_t *dist, uint32_t *img,
                                          uint32_t bit) {
     // the next match's length / distance codes are looked up one match ahead (software pipelined): at a
     // match start the codes are already in registers, and the lookups for the following match overlap
     // the literals in between
     uint32_t k = 0, cur = m[0], moff = nm ? (cur >> 23) : 64u;
-    uint32_t ev, nb, dev, dnb, lc, dc;
+    uint32_t lc, dv, dn;
     auto look = [&](uint32_t tok) {
-        const uint32_t L = ((tok >> 15) & 255) + 3, D = (tok & 0x7fff) + 1;
-        uint32_t sym, dsym;
-        len_code(L, sym, nb, ev);
-        dist_code(D, dsym, dnb, dev);
-        lc = lit[sym];
-        dc = dist[dsym];
+        lc = ct[256 + ((tok >> 15) & 255)];
+        dist_bits((tok & 0x7fff) + 1, dist, dv, dn);
     };
     look(cur);
     LdsBits bw;
@@ -806,15 +825,15 @@ __device__ __forceinline__ void seg_emit(const uint32_t (&w)[16], uint64_t lm, u
     for (int g = 0; g < 4; ++g) {
         uint32_t c[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) c[i] = lit[(w[4 * g + (i >> 2)] >> (8 * (i & 3))) & 0xff];
+        for (int i = 0; i < 16; ++i) c[i] = ct[(w[4 * g + (i >> 2)] >> (8 * (i & 3))) & 0xff];
 #pragma unroll
         for (int i0 = 0; i0 < 16; ++i0) {
             const int i = 16 * g + i0;
             if ((lm >> i) & 1) {
-                bw.put(c[i0] & 0xffff, c[i0] >> 16);
+                bw.put(c[i0] & 0xffffff, c[i0] >> 24);
             } else if ((uint32_t)i == moff) {
-                bw.put((lc & 0xffff) | (ev << (lc >> 16)), (lc >> 16) + nb);
-                bw.put((dc & 0xffff) | (dev << (dc >> 16)), (dc >> 16) + dnb);
+                bw.put(lc & 0xffffff, lc >> 24);
+                bw.put(dv, dn);
                 ++k;
 #pragma unroll
                 for (int q = 0; q + 1 < kMPre; ++q) m[q] = m[q + 1];  // the next token to the front
@@ -837,7 +856,7 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
                                                      const uint32_t *__restrict__ zpow, const uint32_t *__restrict__ offs,
                                                      const uint64_t *__restrict__ cbase, uint8_t *__restrict__ dst) {
     __shared__ __align__(16) uint32_t img[kSlot / 4 + 4];
-    __shared__ uint32_t lit[kLit], dist[kDist];
+    __shared__ uint32_t ct[512], dist[kDist];
     __shared__ uint32_t scan[kNSeg];
     __shared__ uint32_t wsum[kT / 64];
     __shared__ uint32_t crctab[4][256];
@@ -851,7 +870,7 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
     const uint8_t *s = src + start;
     const DeflTab &T = tabs[blockIdx.x];
     const uint32_t total = T.total, stored = T.stored, hb = T.hdr_bits;
-    for (int i = t; i < kLit; i += kT) lit[i] = T.lit[i];
+    for (int i = t; i < 512; i += kT) ct[i] = ct_entry(i, T.lit);
     for (int i = t; i < kDist; i += kT) dist[i] = T.dist[i];
     crc_setup<kT>(crctab, zp, zpow, t);
     for (uint32_t i = t; i < (total + 15) / 16; i += kT) ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
@@ -877,10 +896,10 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
             uint32_t w[16], m[kMPre];
             seg_load(s, s0a, len, w);
             seg_tokens(mpa, nma, m);
-            ca = seg_bits(w, lma, nma, mpa, m, lit, dist);
+            ca = seg_bits(w, lma, nma, mpa, m, ct, dist);
             seg_load(s, s0b, len, w);
             seg_tokens(mpb, nmb, m);
-            cb = seg_bits(w, lmb, nmb, mpb, m, lit, dist);
+            cb = seg_bits(w, lmb, nmb, mpb, m, ct, dist);
         }
         scan[t] = ca;
         scan[kT + t] = cb;
@@ -915,19 +934,19 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
             if (ca) {
                 seg_load(s, s0a, len, w);
                 seg_tokens(mpa, nma, m);
-                seg_emit(w, lma, nma, mpa, m, lit, dist, img, 144 + hb + scan[t]);
+                seg_emit(w, lma, nma, mpa, m, ct, dist, img, 144 + hb + scan[t]);
             }
             if (cb) {
                 seg_load(s, s0b, len, w);
                 seg_tokens(mpb, nmb, m);
-                seg_emit(w, lmb, nmb, mpb, m, lit, dist, img, 144 + hb + scan[kT + t]);
+                seg_emit(w, lmb, nmb, mpb, m, ct, dist, img, 144 + hb + scan[kT + t]);
             }
         }
         if (t == kT - 1) {  // end of block after the last segment
             const uint32_t body_end = 144 + hb + scan[kNSeg - 1] + cb;
             LdsBits bw;
             bw.init(img, body_end);
-            const uint32_t c = lit[256];
+            const uint32_t c = T.lit[256];
             bw.put(c & 0xffff, c >> 16);
             bw.finish();
         }
