@@ -54,10 +54,10 @@ __device__ __forceinline__ void report(uint32_t *err, uint32_t code, uint64_t bl
 constexpr int TL = 6, TD = 4;  // direct-table bits: literal/length, distance
 constexpr int kWps = 3;        // waves per SIMD (VGPR budget 512 / 3)
 #ifndef OGE_INFL_STREAMS
-#define OGE_INFL_STREAMS 2
+#define OGE_INFL_STREAMS 1
 #endif
 #ifndef OGE_INFL_CHUNK
-#define OGE_INFL_CHUNK 1
+#define OGE_INFL_CHUNK 4
 #endif
 constexpr int kStreams = OGE_INFL_STREAMS;     // chunk pipelines (see oge_inflate_lanes)
 constexpr uint64_t kChunkLanes = OGE_INFL_CHUNK;  // blocks per lane per chunk, at most
@@ -1001,12 +1001,14 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     }();
     // persistent lanes (the 12 resident waves per CU) take blocks from a queue; a chunk is at most
     // kChunkLanes blocks per lane, and no more than a quarter of the free device memory holds bitmaps and
-    // lists for (17.3 KiB per block), at least one block per lane.  Chunks alternate over kStreams streams
-    // with a buffer set each: chunk k + 1's phase 1 starts while chunk k's lanes drain (a wave ends when
-    // its last lane's block does) and while chunk k's phase 2 runs, so the tails overlap.  100M reads
-    // (435k blocks), A/B in one run on two boxes: one chunk on one stream 225.2 / 225.4 ms, three chunks
-    // of one block per lane on two streams 209.1 / 217.5 (three streams: no better); the workspace is
-    // 2 x 196k blocks x 17.3 KiB = 6.8 GB (r03: up to 4 blocks per lane in one set, 14 GB).
+    // lists for (17.3 KiB per block), at least one block per lane.  With kStreams > 1, chunks alternate
+    // over that many streams with a buffer set each, so one chunk's phase-1 drain and phase 2 can overlap
+    // the next chunk.  Measured (r04): standalone at 100M reads (435k blocks) three chunks of one block
+    // per lane on two streams beat one chunk on one stream (209-218 vs 225 ms) and at 200M two chunks of
+    // four on two streams did (400 vs 434 ms); but inside the 300M chain -- the number that counts --
+    // one stream with chunks of four blocks per lane is fastest: 649 ms against 695 (two streams, one
+    // per lane), 715 (two, two) and 728 (two, four): concurrent phase-1 launches on two streams share the
+    // CUs and the L2 and both finish late.  So one stream by default (a 14 GB workspace at 300M).
     const uint64_t lanes = (uint64_t)ncu * 4 * kWps * 64;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;

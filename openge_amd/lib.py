@@ -13,7 +13,7 @@ from pathlib import Path
 import numpy as np
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "libopenge_hip.so"
+LIB_PATH = Path(os.environ["OGE_LIB"]) if os.environ.get("OGE_LIB") else PKG / "libopenge_hip.so"  # OGE_LIB: an A/B build
 
 MAX_REF = 64
 
