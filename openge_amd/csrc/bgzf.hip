@@ -124,12 +124,12 @@ __device__ __forceinline__ uint64_t bits_below(uint32_t q) { return q >= 64 ? ~0
 __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
                                                    uint64_t *__restrict__ lmask, uint8_t *__restrict__ nmatch,
                                                    uint32_t *__restrict__ mlist, uint32_t *__restrict__ freq_out) {
+    // 163,600 B of LDS: the payload, two hash tables, the sub-block's candidates (the symbol counts live
+    // in the table not in use while a sub-block is parsed; the candidate masks are read back from cand)
     __shared__ __align__(16) uint32_t in[kPay / 4 + 4];
-    __shared__ uint32_t htab[1 << kHashBits];
-    __shared__ uint16_t cand[kSub];
-    __shared__ uint64_t cmask[kT];
-    __shared__ uint32_t freq[kFreq];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    __shared__ uint32_t htab[2][1 << kHashBits];
+    __shared__ __align__(16) uint16_t cand[kSub];
+    const int t = threadIdx.x;
     const uint64_t blk = blk0 + blockIdx.x;
     const uint64_t start = blk * kPay;
     const uint32_t len = (uint32_t)min<uint64_t>(kPay, n - start);
@@ -143,11 +143,22 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
 #endif
     PCLK();
     stage_words<kTP>(in, src + start, len, t);
-    for (int i = t; i < (1 << kHashBits); i += kTP) htab[i] = 0;
-    for (int i = t; i < kFreq; i += kTP) freq[i] = 0;
+    for (int i = t; i < 2 << kHashBits; i += kTP) (&htab[0][0])[i] = 0;
     __syncthreads();
     PCLK();
 
+    // Candidate rounds with one barrier each (r04; r03 had two: lookups, barrier, inserts, barrier).  Round
+    // g looks up in htab[g & 1] and inserts into htab[(g + 1) & 1] both its own positions and round g - 1's:
+    // at the start of round g, htab[g & 1] holds every position of the rounds before g (what r03's single
+    // table held) and htab[(g + 1) & 1] those before g - 1, so the lookups see exactly r03's table -- the
+    // same candidates, the same bytes -- while the inserts go to the other table.  20M reads: 32.24 ->
+    // 32.09 ms only: a round is bound by its chain of dependent LDS reads and the bank conflicts of the
+    // random bucket / candidate reads and atomics, not by its barriers.
+    uint32_t g = 0;
+    uint32_t hp[kR], vp[kR];  // the previous round's buckets and positions + 1 (0: nothing to insert)
+#pragma unroll
+    for (int k = 0; k < kR; ++k) hp[k] = 0, vp[k] = 0;
+    uint32_t f0 = 0;  // symbol t's count in sub-block 0 (kept while sub-block 1 reuses the table it was in)
     const uint64_t seg_base = (uint64_t)blockIdx.x * kNSeg;
     for (int sub = 0; sub < kNSub; ++sub) {
         const uint32_t base = sub * kSub;
@@ -157,12 +168,17 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
             continue;
         }
         const uint32_t end = min(len, base + kSub);
-        // candidates, one round of kR * kT consecutive positions at a time (r04: an LDS compare-and-swap
-        // bucket holding the latest position and the latest from an earlier round, one barrier per round,
-        // measured slower -- 60k vs 36k cycles per sub-block: repeated prefixes contend for one bucket)
-        for (uint32_t r = base; r < end; r += kR * kTP) {
-            // the kR lookup chains (prefix word -> bucket -> candidate's word) of a thread run side by side;
-            // the ballots come after all of them (a ballot between them would serialise the chains)
+        if (sub > 0) {  // the spare table held sub-block 0's counts: keep them, then make it a copy of the full one
+            uint32_t *F = htab[(g + 1) & 1];
+            if (t < kFreq) f0 = F[t];
+            __syncthreads();
+            for (int i = t; i < (1 << kHashBits); i += kTP) F[i] = htab[g & 1][i];
+            __syncthreads();
+        }
+        for (uint32_t r = base; r < end; r += kR * kTP, ++g) {
+            const uint32_t *A = htab[g & 1];
+            uint32_t *B = htab[(g + 1) & 1];
+            // the kR lookup chains (prefix word -> bucket -> candidate's word) of a thread run side by side
             uint32_t hh[kR], cc[kR];
 #pragma unroll
             for (int k = 0; k < kR; ++k) {
@@ -171,7 +187,7 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
                 if (p + 4 <= len) {
                     const uint32_t w = ld32(in, p);
                     h = hash4(w);
-                    const uint32_t j1 = htab[h];
+                    const uint32_t j1 = A[h];
                     if (j1 && p - (j1 - 1) <= 32768 && ld32(in, j1 - 1) == w) c = j1;
                 }
                 hh[k] = h;
@@ -179,27 +195,40 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
             }
 #pragma unroll
             for (int k = 0; k < kR; ++k) {
-                const uint32_t p = r + k * kTP + t, c = cc[k];
-                const uint64_t m = __ballot(c != 0 && p < end);
-                if (p < end) cand[p - base] = (uint16_t)c;
-                if (lane == 0 && r + k * kTP + 64 * wv < end) cmask[(r + k * kTP + 64 * wv - base) >> 6] = m;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < kR; ++k) {
                 const uint32_t p = r + k * kTP + t;
-                if (p + 4 <= len && p < end) atomicMax(&htab[hh[k]], p + 1);
+                if (p < end) cand[p - base] = (uint16_t)cc[k];
+                if (vp[k]) atomicMax(&B[hp[k]], vp[k]);
+                const bool ins = p + 4 <= len && p < end;
+                if (ins) atomicMax(&B[hh[k]], p + 1);
+                hp[k] = hh[k];
+                vp[k] = ins ? p + 1 : 0u;
             }
             __syncthreads();
         }
         PCLK();
+        // the symbol counts of this sub-block go to the spare table (it is rebuilt before it is read again)
+        uint32_t *freq = htab[(g + 1) & 1];
+        for (int i = t; i < kFreq; i += kTP) freq[i] = 0;
+        __syncthreads();
         // greedy parse of this thread's segment
         const uint32_t s0 = base + t * kSeg, s1 = min(end, s0 + kSeg);
         uint64_t lit = 0;
         uint32_t nm = 0;
         if (t < kT && s0 < s1) {
             const uint32_t sl = s1 - s0;
-            const uint64_t cm = cmask[t] & bits_below(sl);
+            uint64_t cm = 0;  // the segment's candidate mask, from its 64 cand entries (eight 16-byte reads)
+            {
+                const uint4 *cv = (const uint4 *)(cand + (s0 - base));
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint4 v = cv[q];
+                    const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        cm |= (uint64_t)(((ww[i >> 1] >> (16 * (i & 1))) & 0xffff) != 0) << (8 * q + i);
+                }
+                cm &= bits_below(sl);
+            }
             uint32_t *mp = mlist + ((uint64_t)blockIdx.x * kMaxM) * kNSeg + (uint64_t)sub * kT + t;
             for (uint32_t p = 0; p < sl;) {
                 const uint64_t m = cm & ~bits_below(p);
@@ -250,16 +279,19 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
             }
         }
         if (t < kT) lmask[sg] = lit, nmatch[sg] = (uint8_t)nm;
-        __syncthreads();  // cand / cmask are reused by the next sub-block
+        __syncthreads();  // cand and the counts are reused by the next sub-block
         PCLK();
     }
-    for (int i = t; i < kFreq; i += kTP) freq_out[(uint64_t)blockIdx.x * kFreq + i] = freq[i];
+    // counts: sub-block 0's (kept in f0 when sub-block 1 ran) + those in the spare table
+    static_assert(kFreq <= kTP, "one count per thread");
+    if (t < kFreq) freq_out[(uint64_t)blockIdx.x * kFreq + t] = f0 + htab[(g + 1) & 1][t];
 #if OGE_EXP == 4
     if (t == 0 && blockIdx.x < 4 && blk0 == 0)
         printf("parse-exp blk %u: stage %llu | sub0 rounds %llu parse+counts %llu | sub1 rounds %llu parse+counts %llu\n", blockIdx.x,
                (unsigned long long)(pc[1] - pc[0]), (unsigned long long)(pc[2] - pc[1]), (unsigned long long)(pc[3] - pc[2]),
                (unsigned long long)(pc[4] - pc[3]), (unsigned long long)(pc[5] - pc[4]));
 #endif
+#undef PCLK
 }
 
 // ------------------------------------------------------------------------------------ Huffman
