@@ -1339,7 +1339,9 @@ struct Scratch {
     }
 };
 static std::mutex g_scratch_mu;
-static std::vector<std::unique_ptr<Scratch>> g_scratch;
+// never destroyed: no static destructor joins worker threads at exit (a forked child that exits
+// through them would join threads it does not have)
+static std::vector<std::unique_ptr<Scratch>> &g_scratch = *new std::vector<std::unique_ptr<Scratch>>();
 struct ScratchLease {
     std::unique_ptr<Scratch> s;
     explicit ScratchLease(int threads) {
