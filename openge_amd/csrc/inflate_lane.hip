@@ -62,7 +62,10 @@ constexpr int kWps = 3;        // waves per SIMD (VGPR budget 512 / 3)
 constexpr int kStreams = OGE_INFL_STREAMS;     // chunk pipelines (see oge_inflate_lanes)
 constexpr uint64_t kChunkLanes = OGE_INFL_CHUNK;  // blocks per lane per chunk, at most
 constexpr int LB = 4;          // literals per decode step (see the ST_SYM path)
-constexpr int kInner = 16;     // decode steps between the wave-wide phases
+#ifndef OGE_INFL_INNER
+#define OGE_INFL_INNER 16
+#endif
+constexpr int kInner = OGE_INFL_INNER;  // decode steps between the wave-wide phases
 constexpr int kNT = 4;         // tables per BGZF block whose long literals phase 2 translates
 constexpr uint32_t kXList = 288;                 // a table's canonical list of long codes (bytes)
 constexpr uint32_t kXTab = 1280;                 // per block: kNT lists, then kNT u32 start positions
