@@ -297,3 +297,72 @@ def test_dist_uniform_key_pile(ctx, frac, G):
     assert nd2 == nd
     if frac >= 1:  # one rank holds the whole pile
         assert sorted(counts)[-1] == n and sum(1 for c in counts if c) == 1
+
+
+@pytest.mark.parametrize("sort", [True, False])
+def test_rccl_transport_world1(ctx, sort):
+    """RcclTransport's three methods on the one-GPU box: a one-rank communicator forced onto RCCL
+    (oge_comm_init_rank_mode "rccl": ncclCommInitRank with one rank) runs the whole distributed step --
+    all-to-all-v as grouped ncclSend / ncclRecv to itself, ncclAllGather for the plans and samples,
+    ncclReduceScatter(max) for the marks -- and must equal the one-GPU output (sort + dedup, and the
+    in-place dedup mode).  More ranks need more GPUs (RCCL refuses two ranks on one device)."""
+    p = L.synth_params(20000, preset="c2", seed=31)
+    recs, offs, hdr = L.synth_host(p)
+    n = len(offs) - 1
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    c1 = L.Context(0)
+    comm = L.comm_init_rank(c1, 1, 0, L.comm_unique_id(), mode="rccl")
+    try:
+        assert comm.transport == "rccl" and comm.size == 1
+        (srecs, soffs), = _shards(recs, offs, [0, n])
+        d_recs = torch.from_numpy(srecs).cuda()
+        d_offs = torch.from_numpy(soffs).cuda()
+        torch.cuda.synchronize()
+        d, do, no, nd = comm.sort_markdup_dist(d_recs.data_ptr(), d_offs.data_ptr(), n, p.n_ref, opts, sort)
+        assert no == n and nd > 0
+        oo = np.empty(no + 1, np.uint64)
+        L.check(L.lib().oge_memcpy(c1.h, oo.ctypes.data, do, 8 * (no + 1), 2), c1.h)
+        got = np.empty(int(oo[no] - oo[0]), np.uint8)
+        L.check(L.lib().oge_memcpy(c1.h, got.ctypes.data, d + int(oo[0]), got.size, 2), c1.h)
+        ex = {e["tag"]: e for e in comm.exchange_stats()}
+        assert ex and all(e["calls"] >= 1 for e in ex.values())
+    finally:
+        comm.close()
+        c1.close()
+    if sort:
+        want, wd = _single(ctx, recs, offs, n, p.n_ref, opts)
+        assert got.tobytes() == want and nd == wd
+    else:  # dedup mode: the input order, the same marks as the in-process two-rank run
+        want, counts, wd = run_dist(_shards(recs, offs, [0, n // 2, n]), p.n_ref, opts, sort=False)
+        assert got.tobytes() == want and nd == wd
+
+
+def test_rccl_transport_world1_bgzf_chain(ctx, tmp_path):
+    """bench.py --gpus N's call (oge_mergesort_bgzf_dist) over a one-rank RCCL communicator: the output
+    file inflates to the one-GPU chain's bytes, with the same record and duplicate counts."""
+    import gzip
+    p = L.synth_params(20000, preset="c2", seed=43)
+    recs, offs, hdr = L.synth_host(p)
+    n = len(offs) - 1
+    src = tmp_path / "all.bam"
+    L.write_bam(src, hdr, recs, offs, n, level=1)
+    z = src.read_bytes()
+    opts = L.mergesort_opts(level=6, program_line=b"openge mergesort x", mark_duplicates=1)
+    dz = torch.from_numpy(np.frombuffer(z + b"\0" * 8, np.uint8).copy()).cuda()
+    d, nb, nr, nd = ctx.mergesort_bgzf_dev(dz.data_ptr(), len(z), opts)
+    want = np.empty(nb, np.uint8)
+    L.check(L.lib().oge_memcpy(ctx.h, want.ctypes.data, d, nb, 2), ctx.h)
+    c1 = L.Context(0)
+    comm = L.comm_init_rank(c1, 1, 0, L.comm_unique_id(), mode="rccl")
+    try:
+        assert comm.transport == "rccl"
+        t = torch.from_numpy(np.frombuffer(z + b"\0" * 8, np.uint8).copy()).cuda()
+        torch.cuda.synchronize()
+        d2, ob, tr, td = comm.mergesort_bgzf_dist(t.data_ptr(), len(z), opts)
+        got = np.empty(ob, np.uint8)
+        L.check(L.lib().oge_memcpy(c1.h, got.ctypes.data, d2, ob, 2), c1.h)
+    finally:
+        comm.close()
+        c1.close()
+    assert (tr, td) == (nr, nd)
+    assert gzip.decompress(got.tobytes()) == gzip.decompress(want.tobytes())
