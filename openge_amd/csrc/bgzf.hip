@@ -858,12 +858,14 @@ __device__ __forceinline__ void seg_emit(const uint32_t (&w)[16], uint64_t lm, u
         uint32_t c[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) c[i] = ct[(w[4 * g + (i >> 2)] >> (8 * (i & 3))) & 0xff];
+        // positions in pairs: the pair's literal codes (<= 30 bits) go out in one put; a match can start at
+        // only one of the two (it covers >= 3 positions), after the literal that may precede it
 #pragma unroll
-        for (int i0 = 0; i0 < 16; ++i0) {
+        for (int i0 = 0; i0 < 16; i0 += 2) {
             const int i = 16 * g + i0;
-            if ((lm >> i) & 1) {
-                bw.put(c[i0] & 0xffffff, c[i0] >> 24);
-            } else if ((uint32_t)i == moff) {
+            const uint32_t a = (lm >> i) & 1 ? c[i0] : 0u, b = (lm >> (i + 1)) & 1 ? c[i0 + 1] : 0u;
+            bw.put((a & 0xffffff) | ((b & 0xffffff) << (a >> 24)), (a >> 24) + (b >> 24));
+            if (((uint32_t)i | 1u) == (moff | 1u)) {  // a match starts at i or i + 1
                 bw.put(lc & 0xffffff, lc >> 24);
                 bw.put(dv, dn);
                 ++k;
