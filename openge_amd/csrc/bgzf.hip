@@ -813,7 +813,10 @@ __device__ __forceinline__ void seg_load(const uint8_t *s, uint32_t s0, uint32_t
 // Latency, not work, bounds these two: a code lookup or a match-token load inside a data-dependent branch
 // is waited for on the spot.  So the segment's literal codes are looked up 16 at a time without branches
 // (independent LDS reads in flight together) and its first kMPre match tokens are loaded at once.
-constexpr int kMPre = 8;
+#ifndef OGE_EMIT_MPRE  // (20M deflate with 2 / 4 / 8 / 12 / 16: 30.6 / 29.6 / 28.8 / 29.0 / 29.2 ms)
+#define OGE_EMIT_MPRE 8
+#endif
+constexpr int kMPre = OGE_EMIT_MPRE;
 __device__ __forceinline__ void seg_tokens(const uint32_t *mp, uint32_t nm, uint32_t (&m)[kMPre]) {
     const uint32_t last = nm ? nm - 1 : 0;  // (clamped: every load is a real address, no branch around it)
 #pragma unroll
@@ -866,6 +869,12 @@ __device__ __forceinline__ void seg_emit(const uint32_t (&w)[16], uint64_t lm, u
             const uint32_t a = (lm >> i) & 1 ? c[i0] : 0u, b = (lm >> (i + 1)) & 1 ? c[i0 + 1] : 0u;
             bw.put((a & 0xffffff) | ((b & 0xffffff) << (a >> 24)), (a >> 24) + (b >> 24));
             if (((uint32_t)i | 1u) == (moff | 1u)) {  // a match starts at i or i + 1
+#if OGE_EXP == 8  // timing experiment: matches not emitted (wrong bytes)
+                ++k;
+#pragma unroll
+                for (int q = 0; q + 1 < kMPre; ++q) m[q] = m[q + 1];
+                moff = k < nm && k < (uint32_t)kMPre ? m[0] >> 23 : 64u;
+#else
                 bw.put(lc & 0xffffff, lc >> 24);
                 bw.put(dv, dn);
                 ++k;
@@ -878,6 +887,7 @@ __device__ __forceinline__ void seg_emit(const uint32_t (&w)[16], uint64_t lm, u
                 } else {
                     moff = 64;
                 }
+#endif
             }
         }
     }
