@@ -1111,6 +1111,8 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
 #ifndef OGE_DEFL_STREAMS
 #define OGE_DEFL_STREAMS 3
 #endif
+    // B[] below holds three buffer sets; 300M chain: 2 streams 423.6 ms, 3 streams 417.4 ms (r04)
+    static_assert(OGE_DEFL_STREAMS >= 1 && OGE_DEFL_STREAMS <= 3, "deflate: 1-3 streams");
     const int S = nblk > chunk ? OGE_DEFL_STREAMS : 1;
     struct Bufs {
         uint64_t *lmask, *cbase;
