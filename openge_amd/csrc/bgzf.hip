@@ -907,6 +907,7 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
     __shared__ uint32_t wsum[kT / 64];
     __shared__ uint32_t crctab[4][256];
     __shared__ uint32_t zp[17][32];
+    __shared__ uint32_t zl[32][16];  // the CRC's per-lane combine operators (crc_combine512l)
     __shared__ uint32_t crcs[kT / 64];
     __shared__ uint32_t sh_crc;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -919,10 +920,11 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
     for (int i = t; i < 512; i += kT) ct[i] = ct_entry(i, T.lit);
     for (int i = t; i < kDist; i += kT) dist[i] = T.dist[i];
     crc_setup<kT>(crctab, zp, zpow, t);
+    for (int i = t; i < 32 * 16; i += kT) zl[i >> 4][i & 15] = zpow[17 * 32 + i];
     for (uint32_t i = t; i < (total + 15) / 16; i += kT) ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     {
-        const uint32_t c = crc_global512x4(s, len, crctab, zp, crcs, t);
+        const uint32_t c = crc_global512x4l(s, len, crctab, zl, zp, crcs, t);
         if (t == 0) sh_crc = c;
     }
     const uint32_t bsize = total - 1;
@@ -1136,13 +1138,19 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
             !B[s].cbase || !B[s].st)
             return OGE_ERR_HIP;
     }
-    uint32_t *zpow = (uint32_t *)ctx->ws("defl_zpow", 17 * 32 * 4);
+    // the 2^k zero-byte operators, then the emit's 16-lane combine operators (crc_zlane, 128-byte pieces)
+    uint32_t *zpow = (uint32_t *)ctx->ws("defl_zpow", (17 * 32 + 32 * 16) * 4);
     uint64_t *base = (uint64_t *)ctx->ws("defl_base", 16);
     if (!zpow || !base) return OGE_ERR_HIP;
-    static uint32_t z[17][32];
-    static bool zinit = false;
-    if (!zinit) crc_zpow(z), zinit = true;
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, z, sizeof(z), hipMemcpyHostToDevice, ctx->stream));
+    static struct {
+        uint32_t z[17][32], zl[32][16];
+    } zh = [] {
+        decltype(zh) v;
+        crc_zpow(v.z);
+        crc_zlane<16>(v.z, 128, &v.zl[0][0]);
+        return v;
+    }();
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, &zh, sizeof(zh), hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(base, 0, 8, ctx->stream));
     OgeStageTimer *tm = ctx->begin_stage("bgzf_deflate");
     hipEvent_t ev[4];

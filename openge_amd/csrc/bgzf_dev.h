@@ -141,6 +141,38 @@ __device__ inline uint32_t crc_combine512(uint32_t c, uint32_t len, const uint32
     return ~(r ^ c);
 }
 
+// 512 threads with per-lane operators of 16 lanes (2 KiB of LDS: the deflate emit's two workgroups per CU
+// leave no room for 64): lane l carries its 128-byte piece's register over 128 (15 - l % 16) bytes with
+// zl[.][l % 16], the 16-lane groups XOR, two levels join the four 2048-byte group pieces of a wave, three
+// the eight wave pieces -- three matrix-vector products per lane instead of six before the barrier
+__device__ inline uint32_t crc_combine512l(uint32_t c, uint32_t len, const uint32_t (*zl)[16], const uint32_t (*zp)[32],
+                                           uint32_t *crcs, int t) {
+    const uint32_t lane = t & 63;
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) v ^= (uint32_t)(-(int32_t)((c >> b) & 1)) & zl[b][lane & 15];
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) v ^= __shfl_xor(v, d, 64);
+#pragma unroll
+    for (int lv = 0; lv < 2; ++lv) {  // 2048-byte group pieces
+        const uint32_t o = __shfl_down(v, 16u << lv, 64);
+        if (!(lane & ((32u << lv) - 1))) v = crc_mat(zp[11 + lv], v) ^ o;
+    }
+    if (lane == 0) crcs[t >> 6] = v;
+    __syncthreads();
+    uint32_t r = 0xffffffffu;
+    if (t < 64) {
+        c = t < 8 ? crcs[t] : 0u;
+#pragma unroll
+        for (int lv = 0; lv < 3; ++lv) {  // 8192-byte wave pieces
+            const uint32_t o = __shfl_down(c, 1u << lv, 64);
+            if (!(t & ((2u << lv) - 1))) c = crc_mat(zp[13 + lv], c) ^ o;
+        }
+        if (t == 0) r = crc_preset(len, zp);
+    }
+    return ~(r ^ c);
+}
+
 // The same for NT = 1024 threads (pieces of 64 bytes, sixteen waves): six in-wave levels, four over
 // the wave results.
 __device__ inline uint32_t crc_combine1024(uint32_t c, uint32_t len, const uint32_t (*zp)[32], uint32_t *crcs, int t) {
@@ -151,6 +183,33 @@ __device__ inline uint32_t crc_combine1024(uint32_t c, uint32_t len, const uint3
         if (!(lane & ((2u << lv) - 1))) c = crc_mat(zp[6 + lv], c) ^ o;
     }
     if (lane == 0) crcs[t >> 6] = c;
+    __syncthreads();
+    uint32_t r = 0xffffffffu;
+    if (t < 64) {
+        c = t < 16 ? crcs[t] : 0u;
+#pragma unroll
+        for (int lv = 0; lv < 4; ++lv) {  // 4096-byte wave pieces
+            const uint32_t o = __shfl_down(c, 1u << lv, 64);
+            if (!(t & ((2u << lv) - 1))) c = crc_mat(zp[12 + lv], c) ^ o;
+        }
+        if (t == 0) r = crc_preset(len, zp);
+    }
+    return ~(r ^ c);
+}
+
+// The same with per-lane operators (r04): lane l's register is carried over the 64 (63 - l) bytes that
+// follow its piece inside the wave's 4096 bytes by its own matrix zl[.][l] (zl = [bit][lane], a wave's 64
+// reads hit 64 banks) and the wave XORs the results -- one matrix-vector product per lane instead of six
+// shuffle levels of them (crc_zlane builds zl on the host)
+__device__ inline uint32_t crc_combine1024l(uint32_t c, uint32_t len, const uint32_t (*zl)[64], const uint32_t (*zp)[32],
+                                            uint32_t *crcs, int t) {
+    const uint32_t lane = t & 63;
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) v ^= (uint32_t)(-(int32_t)((c >> b) & 1)) & zl[b][lane];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v ^= __shfl_xor(v, d, 64);
+    if (lane == 0) crcs[t >> 6] = v;
     __syncthreads();
     uint32_t r = 0xffffffffu;
     if (t < 64) {
@@ -180,6 +239,20 @@ __device__ uint32_t crc_window1024(const uint32_t *in, uint32_t len, const uint3
         for (uint32_t d = 0; d < w0 + 64 - lead; ++d) c = crctab[0][(c ^ byte_at<PS>(in, d)) & 0xff] ^ (c >> 8);
     }
     return crc_combine1024(c, len, zp, crcs, t);
+}
+template <int PS = 31>
+__device__ uint32_t crc_window1024l(const uint32_t *in, uint32_t len, const uint32_t (*crctab)[256], const uint32_t (*zl)[64],
+                                    const uint32_t (*zp)[32], uint32_t *crcs, int t) {
+    const uint32_t lead = kSlot - len, w0 = t * 64u;
+    uint32_t c = 0;
+    if (w0 >= lead) {
+        const uint32_t d0 = w0 - lead;
+#pragma unroll 4
+        for (int i = 0; i < 16; ++i) c = crc_word(crctab, c ^ ld32p<PS>(in, d0 + 4 * i));
+    } else if (w0 + 64 > lead) {
+        for (uint32_t d = 0; d < w0 + 64 - lead; ++d) c = crctab[0][(c ^ byte_at<PS>(in, d)) & 0xff] ^ (c >> 8);
+    }
+    return crc_combine1024l(c, len, zl, zp, crcs, t);
 }
 
 // the payload staged in LDS (padded layout PS)
@@ -247,6 +320,26 @@ __device__ inline uint32_t crc_global512x4(const uint8_t *s, uint32_t len, const
     }
     return crc_combine512(c, len, zp, crcs, t);
 }
+__device__ inline uint32_t crc_global512x4l(const uint8_t *s, uint32_t len, const uint32_t (*crctab)[256], const uint32_t (*zl)[16],
+                                            const uint32_t (*zp)[32], uint32_t *crcs, int t) {
+    const uint32_t lead = kSlot - len, w0 = t * 128u;
+    uint32_t c = 0;
+    if (w0 >= lead) {
+        const uint32_t d0 = w0 - lead;
+        const uintptr_t a = (uintptr_t)(s + d0);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const OGE_G uint32_t *W = (const OGE_G uint32_t *)(a & ~(uintptr_t)3);
+        uint32_t raw[33];
+#pragma unroll
+        for (int k = 0; k < 33; ++k) raw[k] = (k < 32 || sh) ? W[k] : 0u;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) c = crc_word(crctab, c ^ (sh ? __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh) : raw[i]));
+    } else if (w0 + 128 > lead) {
+        const OGE_G uint8_t *b = (const OGE_G uint8_t *)s;
+        for (uint32_t d = 0; d < w0 + 128 - lead; ++d) c = crctab[0][(c ^ b[d]) & 0xff] ^ (c >> 8);
+    }
+    return crc_combine512l(c, len, zl, zp, crcs, t);
+}
 
 // host: zero-byte operators Z_{2^k}, k = 0..16 (columns = images of the 32 basis bits)
 inline void crc_zpow(uint32_t z[17][32]) {
@@ -262,6 +355,25 @@ inline void crc_zpow(uint32_t z[17][32]) {
                 if ((v >> j) & 1) r ^= z[k - 1][j];
             z[k][b] = r;
         }
+}
+
+// host: the per-lane operators of crc_combine1024l (W = 64) / crc_combine512l (W = 16) for pieces of P = 2^k
+// bytes: zl[b * W + l] = column b of Z_{P (W - 1 - l)}
+template <int W>
+inline void crc_zlane(const uint32_t z[17][32], uint32_t P, uint32_t *zl) {
+    int k = 0;
+    while ((1u << k) < P) ++k;
+    uint32_t M[32];
+    for (int b = 0; b < 32; ++b) M[b] = 1u << b;  // Z_0
+    for (int j = 0; j < W; ++j) {               // M = Z_{P j}
+        for (int b = 0; b < 32; ++b) zl[b * W + W - 1 - j] = M[b];
+        for (int b = 0; b < 32; ++b) {
+            uint32_t r = 0;
+            for (int i = 0; i < 32; ++i)
+                if ((M[b] >> i) & 1) r ^= z[k][i];
+            M[b] = r;
+        }
+    }
 }
 
 }  // namespace oge_bgzf

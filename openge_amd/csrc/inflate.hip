@@ -439,14 +439,20 @@ extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t z
     ctx->reset_timing();
     if (!nblk) return OGE_OK;
     uint32_t *err = (uint32_t *)ctx->ws("infl_err", 16);
-    uint32_t *zpow = (uint32_t *)ctx->ws("infl_zpow", 17 * 32 * 4);
+    // the 2^k zero-byte operators, then phase 2's per-lane combine operators (crc_zlane, 64-byte pieces)
+    uint32_t *zpow = (uint32_t *)ctx->ws("infl_zpow", (17 * 32 + 32 * 64) * 4);
     if (!err || !zpow) return OGE_ERR_HIP;
-    static uint32_t zh[17][32];
-    static bool zinit = false;
-    if (!zinit) crc_zpow(zh), zinit = true;
+    static struct {
+        uint32_t z[17][32], zl[32][64];
+    } zh = [] {
+        decltype(zh) v;
+        crc_zpow(v.z);
+        crc_zlane<64>(v.z, 64, &v.zl[0][0]);
+        return v;
+    }();
     const uint32_t init[2] = {0, 0xffffffffu};
     OGE_HIP_TRY(ctx, hipMemcpyAsync(err, init, 8, hipMemcpyHostToDevice, ctx->stream));
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, zh, sizeof(zh), hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(zpow, &zh, sizeof(zh), hipMemcpyHostToDevice, ctx->stream));
     // the lane decoder (inflate_lane.hip), CRC fused into its phase 2
     OgeStageTimer *tm = ctx->begin_stage("bgzf_inflate");
     const int rc = oge_inflate_lanes(ctx, d_z, zbytes, d_d0, d_d1, d_uoff, d_crc, nblk, d_out, err, zpow);

@@ -25,7 +25,8 @@
 //   Literals are written at their output position (8-byte chunks assembled in a register); a match
 //   (length L >= 3, distance D) leaves a hole of L bytes whose first three bytes receive the
 //   descriptor (L-3, D-1 in 23 bits) and sets the hole's start bit in the block's bitmap.
-// Phase 2 (k_infl_lz, one 1024-thread workgroup per block): deferred literals translated; refs[p] = p for
+// Phase 2 (k_infl_lz, persistent 1024-thread workgroups, one block at a time, the next block's bytes loaded
+//   under this block's CRC): deferred literals translated; refs[p] = p for
 //   every position, then refs[p + j] = p - D + j for every hole; pointer jumping (refs[q] = refs[refs[q]])
 //   in LDS until every position points at a literal; the block's bytes are then staged in LDS, every
 //   byte gathered from its root, CRC-32 checked and written out.
@@ -337,22 +338,40 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
         ++pos;
         if (!(q & 7)) store_chunk((q >> 3) - 1, acc);
     };
+    // n (<= 5) bytes at pos, the first in the low byte of v: one shift-or into the register and at most one
+    // chunk store (the batch completes the current chunk when it brings its m missing bytes)
+    auto put_n = [&](uint64_t v, uint32_t n) {
+        const uint32_t q0 = pos + al, m = 8 - (q0 & 7);
+        const uint32_t mm = min(m, 5u), nn = max(n, 1u);  // shifts stay below 64 on the paths not taken
+        if (n >= m) store_chunk(q0 >> 3, (acc >> (8 * mm)) | (v << (64 - 8 * mm)));
+        if (n) acc = (acc >> (8 * nn)) | (v << (64 - 8 * nn));
+        pos += n;
+    };
     auto flush_partial = [&]() {  // the chunk holding the last byte put, when it is not complete
         const uint32_t q = pos + al;
         if (q & 7) store_chunk(q >> 3, acc >> (8 * (8 - (q & 7))));
     };
     // Up to LB literals whose codes sit in the direct table (sym < 256: bit 8 of the entry clear).  After
     // the refill >= 32 bits are buffered and LB direct codes take <= 24, so no budget check is needed.
-    auto lit_batch = [&]() {
+    // Branch-free: the lookup chain (entry -> shift -> next entry) carries only selects, and the batch's
+    // bytes go out in one put_n (r04: a put per literal, whose chunk-store branch sat in that chain).
+    // np (0 or 1) pending bytes in pb -- the literal of the iteration's main symbol -- go out with the batch
+    auto lit_batch = [&](uint32_t pb, uint32_t np) {
         refill();
+        uint64_t bytes = pb;
+        uint32_t n = np;
+        bool go = true;
 #pragma unroll
         for (int k = 0; k < LB; ++k) {
             const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
-            if ((e2 & 0x100) || pos >= osz) break;  // bit 8: a length code, end of block or a longer code
-            buf >>= e2 >> 9;
-            cnt -= e2 >> 9;
-            put(e2 & 0xff);
+            go = go && !(e2 & 0x100) && pos + n < osz;  // bit 8: a length code, end of block or a longer code
+            const uint32_t L = go ? e2 >> 9 : 0u;
+            buf >>= L;
+            cnt -= L;
+            bytes |= go ? (uint64_t)(e2 & 0xff) << (8 * n) : 0ull;
+            n += go;
         }
+        put_n(bytes, n);
     };
     // hole and deferred-literal bitmaps of the block (1024 word pairs per block of the chunk)
     uint64_t bm = 0, lm = 0;
@@ -553,8 +572,9 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 // A wave runs the union of its lanes' paths, so a lane should make as much progress per
                 // iteration as the union costs: a match and the literals around it in one pass (C2 blocks:
                 // 11.5k iterations per BGZF block instead of 19.8k one-symbol steps; tools/ana policy)
-                lit_batch();
+                lit_batch(0, 0);
                 refill();
+                uint32_t pb = 0, np = 0;  // a literal main symbol: put with the second batch
                 const uint32_t v = (uint32_t)buf;
                 const uint32_t e = S.lt[v & ((1u << TL) - 1)][lane];
                 uint32_t sym, L;
@@ -590,7 +610,7 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                             word(pos);
                             lm |= 1ull << (pos & 63);
                         }
-                        put(sym);
+                        pb = sym & 0xff, np = 1;
                     }
                 } else if (sym == 256) {
                     if (flg & 1) block_end();
@@ -634,9 +654,7 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                             word(pos);
                             bm |= 1ull << (pos & 63);
                             const uint32_t dsc = (len - 3) | ((dist - 1) << 8);  // descriptor in the hole's first bytes
-                            put(dsc);
-                            put(dsc >> 8);
-                            put(dsc >> 16);
+                            put_n(dsc, 3);
                             // the rest of the hole: the shift register moves on with it (a chunk it leaves
                             // half-written is stored now; hole bytes are don't-care)
                             const uint32_t q = pos + al, qe = q + len - 3;
@@ -649,7 +667,7 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                         }
                     }
                 }
-                if (st == ST_SYM) lit_batch();
+                if (st == ST_SYM) lit_batch(pb, np);  // a failed block drops its pending byte
             } else if (st == ST_CL) {
                 refill();
                 const uint32_t e = ((const uint8_t *)&S.lt[0][0])[cl_at((uint32_t)buf & 127, lane)];
@@ -733,8 +751,11 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
 }
 
 // ---------------------------------------------------------------------------- phase 2
-// One 1024-thread workgroup per block (r02: 512 threads; the refs array keeps it to one workgroup per
-// CU, so sixteen waves instead of eight hide the LDS and barrier latency of the pointer-jumping rounds).
+// 1024-thread workgroups (r02: 512 threads; the refs array keeps it to one workgroup per CU, so sixteen
+// waves instead of eight hide the LDS and barrier latency of the pointer-jumping rounds), persistent since
+// r04 (see the block loop).  Tried in r04 and not kept: hole refs filled chunk by chunk by every thread
+// (owners mark their holes' positions in an LDS bitmap and write the start refs only; each 8-position chunk
+// then finds its covering hole's start) instead of by the window's owner: 20M reads 46.5 -> 47.9 ms.
 // Thread t owns the block's bytes [64t, 64t + 64) for the hole descriptors and the CRC, and the
 // 8-position chunks c = 1024 k + t (k < 8) for the refs / image passes (a wave's 64 lanes touch 64
 // consecutive chunks: conflict-free LDS).
@@ -742,23 +763,73 @@ constexpr uint32_t kT2 = 1024;
 
 __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, const uint64_t *__restrict__ uoff,
                                                  const uint32_t *__restrict__ crc, const uint64_t *__restrict__ bitmap,
-                                                 const uint8_t *__restrict__ xtab, uint64_t b0, const uint32_t *__restrict__ zpow,
-                                                 uint32_t *__restrict__ err) {
+                                                 const uint8_t *__restrict__ xtab, uint64_t b0, uint64_t nb,
+                                                 const uint32_t *__restrict__ zpow, uint32_t *__restrict__ err) {
     __shared__ __align__(16) uint16_t refs[kSlot + 16];  // later the block's bytes (img)
     __shared__ uint32_t crctab[4][256];
     __shared__ uint32_t zp[17][32];
     __shared__ uint32_t crcs[kT2 / 64];
     __shared__ __align__(16) uint8_t xl[kXTab];
+    __shared__ uint32_t zl[32][64];  // the CRC's per-lane combine operators (crc_combine1024l)
     const uint32_t t = threadIdx.x;
-    const uint64_t b = b0 + blockIdx.x;
+    if (crc) {  // once per workgroup (r04: once per block)
+        crc_setup<kT2>(crctab, zp, zpow, t);
+        for (uint32_t i = t; i < 32 * 64; i += kT2) zl[i >> 6][i & 63] = zpow[17 * 32 + i];
+    }
+    const uint32_t q0 = 64 * t;
+    // A persistent workgroup walks blocks i = blockIdx.x, + gridDim.x, ... (its 139 KiB of LDS make it the
+    // CU's only one).  Block i + gridDim.x's global inputs are loaded into registers while block i's CRC is
+    // computed, so a block starts with its bytes at hand (r04: one workgroup per block, whose loads -- and
+    // the refs-init barrier waiting on them -- were ~14k of its ~117k cycles with the CU otherwise idle).
+    //  hv: this window's hole / deferred-literal bitmap pair; xv: the block's long-literal translation
+    //  lists (1,280 B, staged in LDS: the deferred literals of step 5 look their bytes up without a global
+    //  round trip each); raw: this thread's 64 literal-filled bytes [q0, q0 + 64) and the next word
+    //  (descriptors may straddle), aligned dwords, funnel-shifted at use.
+    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u64x2 hv = {0, 0};
+    u32x4 xv = {0, 0, 0, 0};
+    uint32_t raw[18];
+    auto fetch = [&](uint64_t i) {
+        const uint64_t b = b0 + i;
+        const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
+        const uint8_t *O = out + uoff[b];
+        hv = u64x2{0, 0};
+        if (t < ((osz + 63) >> 6)) hv = *(const OGE_G u64x2 *)((const OGE_G uint64_t *)(bitmap + i * 2048) + 2 * t);
+        xv = u32x4{0, 0, 0, 0};
+        if (t < kXTab / 16) xv = *(const OGE_G u32x4 *)(xtab + i * kXTab + 16 * t);
+        const OGE_G uint32_t *W = (const OGE_G uint32_t *)((uintptr_t)(O + q0) & ~(uintptr_t)3);
+        const uintptr_t lim = (uintptr_t)(O + osz);  // a dword starting below lim holds a block byte: readable
+#pragma unroll
+        for (int k = 0; k < 18; ++k) raw[k] = (uintptr_t)(W + k) < lim ? W[k] : 0u;
+    };
+    // past the last block: registers defined without a load (else the compiler keeps the consumed values
+    // of the previous block alive across the loop for that path, and spills)
+    auto fetch_or_clear = [&](uint64_t i) {
+        if (i < nb) {
+            fetch(i);
+        } else {
+            hv = u64x2{0, 0}, xv = u32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < 18; ++k) raw[k] = 0;
+        }
+    };
+    fetch_or_clear(blockIdx.x);
+    const uint32_t t_ = t;
+    for (uint64_t i = blockIdx.x; i < nb; i += gridDim.x) {
+    // the thread index laundered per block: the per-block index math below (the refs-init values alone
+    // are 32 registers) must not be hoisted out of the loop -- hoisted, it spilled 14 VGPRs
+    uint32_t t = t_;
+    __asm__ volatile("" : "+v"(t));
+    const uint32_t q0 = 64 * t;
+    const uint64_t b = b0 + i;
     const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
     uint8_t *const O = out + uoff[b];
-    if (osz > kSlot) {
+    if (osz > kSlot) {  // uniform: no LDS touched for this block
         if (t == 0) report(err, E_SIZE, b);
-        return;
+        fetch_or_clear(i + gridDim.x);
+        continue;
     }
-    if (crc) crc_setup<kT2>(crctab, zp, zpow, t);
-    const uint32_t q0 = 64 * t;
 #if OGE_EXP == 7  // timing experiment: phase clocks of a phase-2 workgroup (thread 0) and its rounds
     uint64_t zc[10];
     int zn = 0, zr = 0;
@@ -767,27 +838,10 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
 #define ZCLK()
 #endif
     ZCLK();
-    // 0. this window's hole / deferred-literal bitmap pair, loaded first so its latency overlaps the
-    //    block loads below (r03 loaded it after the refs-init barrier: a second exposed round trip)
-    typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-    u64x2 hv = {0, 0};
-    if (t < ((osz + 63) >> 6)) hv = *(const OGE_G u64x2 *)((const OGE_G uint64_t *)(bitmap + (b - b0) * 2048) + 2 * t);
-    // the block's long-literal translation lists (1,280 B), staged in LDS with the refs init below:
-    // the deferred literals of step 5 then look their bytes up without a global round trip each
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 xv = {0, 0, 0, 0};
-    if (t < kXTab / 16) xv = *(const OGE_G u32x4 *)(xtab + (b - b0) * kXTab + 16 * t);
-    // 1. this thread's 64 literal-filled bytes [q0, q0 + 64) and the next word (descriptors may
-    //    straddle): aligned dword loads, funnel-shifted
+    // 1. the prefetched window bytes
     uint32_t wv[17];
     {
-        const uintptr_t a = (uintptr_t)(O + q0);
-        const uint32_t sh = (uint32_t)(a & 3);
-        const OGE_G uint32_t *W = (const OGE_G uint32_t *)(a & ~(uintptr_t)3);
-        const uintptr_t lim = (uintptr_t)(O + osz);  // a dword starting below lim holds a block byte: readable
-        uint32_t raw[18];
-#pragma unroll
-        for (int k = 0; k < 18; ++k) raw[k] = (uintptr_t)(W + k) < lim ? W[k] : 0u;
+        const uint32_t sh = (uint32_t)((uintptr_t)(O + q0) & 3);
 #pragma unroll
         for (int k = 0; k < 17; ++k) wv[k] = sh ? __builtin_amdgcn_alignbyte(raw[k + 1], raw[k], sh) : raw[k];
     }
@@ -803,8 +857,8 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     }
     __syncthreads();
     ZCLK();
-    // 3. holes: refs[p + j] = p - D + j, descriptors read from this thread's window registers
     uint64_t dm = hv.y;  // this window's deferred literals
+    // 3. holes: refs[p + j] = p - D + j, descriptors read from this thread's window registers
     {
         uint64_t m = hv.x;
         while (m) {
@@ -959,9 +1013,11 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     }
     __syncthreads();
     ZCLK();
-    // 7. CRC and the write-out at the block's alignment
+    // 7. the next block's inputs (registers free again: hv, xv and raw were consumed by steps 1-5), then
+    //    the CRC and the write-out at the block's alignment
+    fetch_or_clear(i + gridDim.x);
     if (crc) {
-        const uint32_t c = crc_window1024<PS>(img32, osz, crctab, zp, crcs, t);
+        const uint32_t c = crc_window1024l<PS>(img32, osz, crctab, zl, zp, crcs, t);
         if (t == 0 && c != crc[b]) report(err, E_CRC, b);
     }
     const uint32_t sh = (uint32_t)((uintptr_t)O & 3);
@@ -987,6 +1043,8 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
                (unsigned long long)(zc[6] - zc[5]), (unsigned long long)(zc[7] - zc[6]));
 #endif
 #undef ZCLK
+    __syncthreads();  // the write-out's LDS reads before the next block's refs
+    }
 }
 
 }  // namespace
@@ -1060,7 +1118,8 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         OGE_HIP_TRY(ctx, hipMemsetAsync(u.bitmap, 0, nb * 2048 * 8, u.st));  // phase 1 stores only words with bits
         k_infl_huff<<<g1, 64, 0, u.st>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, u.bitmap, u.xtab, u.scr, err, u.next);
         OGE_LAUNCH_CHECK(ctx);
-        k_infl_lz<<<(uint32_t)nb, kT2, 0, u.st>>>(out, uoff, crc, u.bitmap, u.xtab, b0, zpow, err);
+        k_infl_lz<<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)ncu), kT2, 0, u.st>>>(out, uoff, crc, u.bitmap, u.xtab, b0, nb,
+                                                                                   zpow, err);
         OGE_LAUNCH_CHECK(ctx);
     }
     if (S > 1) {  // the context stream waits for every chunk
