@@ -572,7 +572,9 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 // A wave runs the union of its lanes' paths, so a lane should make as much progress per
                 // iteration as the union costs: a match and the literals around it in one pass (C2 blocks:
                 // 11.5k iterations per BGZF block instead of 19.8k one-symbol steps; tools/ana policy)
+#if OGE_INFL_ITER != 1
                 lit_batch(0, 0);
+#endif
                 refill();
                 uint32_t pb = 0, np = 0;  // a literal main symbol: put with the second batch
                 const uint32_t v = (uint32_t)buf;
@@ -668,6 +670,9 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                     }
                 }
                 if (st == ST_SYM) lit_batch(pb, np);  // a failed block drops its pending byte
+#if OGE_INFL_ITER >= 1
+                if (st == ST_SYM) lit_batch(0, 0);
+#endif
             } else if (st == ST_CL) {
                 refill();
                 const uint32_t e = ((const uint8_t *)&S.lt[0][0])[cl_at((uint32_t)buf & 127, lane)];
@@ -825,13 +830,14 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     const uint64_t b = b0 + i;
     const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
     uint8_t *const O = out + uoff[b];
+    const uint32_t want = crc ? crc[b] : 0u;  // loaded now, compared after step 7's CRC (no round trip there)
     if (osz > kSlot) {  // uniform: no LDS touched for this block
         if (t == 0) report(err, E_SIZE, b);
         fetch_or_clear(i + gridDim.x);
         continue;
     }
 #if OGE_EXP == 7  // timing experiment: phase clocks of a phase-2 workgroup (thread 0) and its rounds
-    uint64_t zc[10];
+    uint64_t zc[12];
     int zn = 0, zr = 0;
 #define ZCLK() (zc[zn++] = __builtin_readcyclecounter())
 #else
@@ -1016,10 +1022,12 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     // 7. the next block's inputs (registers free again: hv, xv and raw were consumed by steps 1-5), then
     //    the CRC and the write-out at the block's alignment
     fetch_or_clear(i + gridDim.x);
+    ZCLK();
     if (crc) {
         const uint32_t c = crc_window1024l<PS>(img32, osz, crctab, zl, zp, crcs, t);
-        if (t == 0 && c != crc[b]) report(err, E_CRC, b);
+        if (t == 0 && c != want) report(err, E_CRC, b);
     }
+    ZCLK();
     const uint32_t sh = (uint32_t)((uintptr_t)O & 3);
     OGE_G uint32_t *A = (OGE_G uint32_t *)((uintptr_t)O & ~(uintptr_t)3);
     const uint32_t nwords = (osz + sh + 3) / 4;
@@ -1036,11 +1044,14 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
     }
 #if OGE_EXP == 7
     ZCLK();
-    if (t == 0 && blockIdx.x % 4096 == 7)
+    if (t == 0 && blockIdx.x == 7 && (i / gridDim.x) % 64 == 3)
         printf("lz-exp blk %u: load %llu init %llu holes %llu jump %llu (%d rounds) roots+defer %llu gather %llu crc+out %llu\n",
                blockIdx.x, (unsigned long long)(zc[1] - zc[0]), (unsigned long long)(zc[2] - zc[1]),
                (unsigned long long)(zc[3] - zc[2]), (unsigned long long)(zc[4] - zc[3]), zr, (unsigned long long)(zc[5] - zc[4]),
-               (unsigned long long)(zc[6] - zc[5]), (unsigned long long)(zc[7] - zc[6]));
+               (unsigned long long)(zc[6] - zc[5]), (unsigned long long)(zc[9] - zc[6]));
+    if (t == 0 && blockIdx.x == 7 && (i / gridDim.x) % 64 == 3)
+        printf("lz-exp blk %u: fetch %llu crc %llu out %llu\n", blockIdx.x, (unsigned long long)(zc[7] - zc[6]),
+               (unsigned long long)(zc[8] - zc[7]), (unsigned long long)(zc[9] - zc[8]));
 #endif
 #undef ZCLK
     __syncthreads();  // the write-out's LDS reads before the next block's refs
