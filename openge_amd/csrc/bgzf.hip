@@ -121,7 +121,13 @@ static_assert(kR * kTP == 1024 && kTP >= kT, "round size and segment threads");
 
 __device__ __forceinline__ uint64_t bits_below(uint32_t q) { return q >= 64 ? ~0ull : ((1ull << q) - 1); }
 
-__global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0,
+// Persistent (r04): workgroup blockIdx.x parses payloads i = blockIdx.x, + gridDim.x, ... < nb of the chunk,
+// and loads payload i + gridDim.x's words into registers while payload i's last sub-block is parsed, so
+// a payload's staging is a register -> LDS copy (r04: one workgroup per payload, ~8k of its ~112k cycles
+// staging from HBM with the CU otherwise idle).
+constexpr uint32_t kPre = kPay / 4 / kTP + 1;  // prefetched words per thread (16 for a full payload)
+
+__global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0, uint64_t nb,
                                                    uint64_t *__restrict__ lmask, uint8_t *__restrict__ nmatch,
                                                    uint32_t *__restrict__ mlist, uint32_t *__restrict__ freq_out) {
     // 163,600 B of LDS: the payload, two hash tables, the sub-block's candidates (the symbol counts live
@@ -129,8 +135,34 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
     __shared__ __align__(16) uint32_t in[kPay / 4 + 4];
     __shared__ uint32_t htab[2][1 << kHashBits];
     __shared__ __align__(16) uint16_t cand[kSub];
-    const int t = threadIdx.x;
-    const uint64_t blk = blk0 + blockIdx.x;
+    const int t_ = threadIdx.x;
+    // the payload's whole words when it starts 4-byte aligned (every payload does when src does: kPay is a
+    // multiple of 4); otherwise stage_words reads them at the payload's start
+    const bool al4 = ((uintptr_t)src & 3) == 0;
+    uint32_t pre[kPre];
+    auto fetch = [&](uint64_t i) {
+        const uint64_t st0 = (blk0 + i) * kPay;
+        const uint32_t ln = (uint32_t)min<uint64_t>(kPay, n - st0);
+        const OGE_G uint32_t *W = (const OGE_G uint32_t *)(src + st0);
+#pragma unroll
+        for (uint32_t j = 0; j < kPre; ++j) {
+            const uint32_t k = t_ + j * kTP;
+            pre[j] = al4 && k < ln / 4 ? W[k] : 0u;
+        }
+    };
+    auto fetch_or_clear = [&](uint64_t i) {  // registers defined on every path (see k_infl_lz)
+        if (i < nb) {
+            fetch(i);
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kPre; ++j) pre[j] = 0;
+        }
+    };
+    fetch_or_clear(blockIdx.x);
+    for (uint64_t pi = blockIdx.x; pi < nb; pi += gridDim.x) {
+    int t = t_;
+    __asm__ volatile("" : "+v"(t));  // per-payload index math stays in the loop (see k_infl_lz)
+    const uint64_t blk = blk0 + pi;
     const uint64_t start = blk * kPay;
     const uint32_t len = (uint32_t)min<uint64_t>(kPay, n - start);
 
@@ -142,7 +174,23 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
 #define PCLK()
 #endif
     PCLK();
-    stage_words<kTP>(in, src + start, len, t);
+    if (al4) {  // the prefetched words, then the zero-padded tail (as stage_words leaves it)
+        const uint32_t safe = len / 4, nw = (len + 3) / 4;
+#pragma unroll
+        for (uint32_t j = 0; j < kPre; ++j) {
+            const uint32_t k = t + j * kTP;
+            if (k < safe) in[k] = pre[j];
+        }
+        for (uint32_t k = safe + t; k < nw + 4; k += kTP) {
+            uint32_t v = 0;
+            if (k < nw)
+                for (int b = 0; b < 4; ++b)
+                    if (4 * k + b < len) v |= (uint32_t)src[start + 4 * k + b] << (8 * b);
+            in[k] = v;
+        }
+    } else {
+        stage_words<kTP>(in, src + start, len, t);
+    }
     for (int i = t; i < 2 << kHashBits; i += kTP) (&htab[0][0])[i] = 0;
     __syncthreads();
     PCLK();
@@ -159,7 +207,7 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
 #pragma unroll
     for (int k = 0; k < kR; ++k) hp[k] = 0, vp[k] = 0;
     uint32_t f0 = 0;  // symbol t's count in sub-block 0 (kept while sub-block 1 reuses the table it was in)
-    const uint64_t seg_base = (uint64_t)blockIdx.x * kNSeg;
+    const uint64_t seg_base = pi * kNSeg;
     for (int sub = 0; sub < kNSub; ++sub) {
         const uint32_t base = sub * kSub;
         const uint64_t sg = seg_base + (uint64_t)sub * kT + t;  // this thread's segment, stream order
@@ -206,6 +254,7 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
             __syncthreads();
         }
         PCLK();
+        if (sub == kNSub - 1 || base + kSub >= len) fetch_or_clear(pi + gridDim.x);  // under the last parse
         // the symbol counts of this sub-block go to the spare table (it is rebuilt before it is read again)
         uint32_t *freq = htab[(g + 1) & 1];
         for (int i = t; i < kFreq; i += kTP) freq[i] = 0;
@@ -229,7 +278,7 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
                 }
                 cm &= bits_below(sl);
             }
-            uint32_t *mp = mlist + ((uint64_t)blockIdx.x * kMaxM) * kNSeg + (uint64_t)sub * kT + t;
+            uint32_t *mp = mlist + (pi * kMaxM) * kNSeg + (uint64_t)sub * kT + t;
             for (uint32_t p = 0; p < sl;) {
                 const uint64_t m = cm & ~bits_below(p);
                 const uint32_t q = m ? (uint32_t)__builtin_ctzll(m) : sl;
@@ -284,7 +333,7 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
     }
     // counts: sub-block 0's (kept in f0 when sub-block 1 ran) + those in the spare table
     static_assert(kFreq <= kTP, "one count per thread");
-    if (t < kFreq) freq_out[(uint64_t)blockIdx.x * kFreq + t] = f0 + htab[(g + 1) & 1][t];
+    if (t < kFreq) freq_out[pi * kFreq + t] = f0 + htab[(g + 1) & 1][t];
 #if OGE_EXP == 4
     if (t == 0 && blockIdx.x < 4 && blk0 == 0)
         printf("parse-exp blk %u: stage %llu | sub0 rounds %llu parse+counts %llu | sub1 rounds %llu parse+counts %llu\n", blockIdx.x,
@@ -292,6 +341,8 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
                (unsigned long long)(pc[4] - pc[3]), (unsigned long long)(pc[5] - pc[4]));
 #endif
 #undef PCLK
+    __syncthreads();  // the counts read out of htab before the next payload clears it
+    }
 }
 
 // ------------------------------------------------------------------------------------ Huffman
@@ -1104,6 +1155,12 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     *out_bytes = 0;
     if (!n) return OGE_OK;
     const uint64_t nblk = (n + kPay - 1) / kPay;
+    static int ncu = [] {  // persistent parse workgroups: one per CU
+        int d = 0, c = 0;
+        (void)hipGetDevice(&d);
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d);
+        return c > 0 ? c : 256;
+    }();
     // payloads per chunk: one launch of each kernel (4096 measured best in r02: 2048 / 4096 / 8192,
     // profiles/r02_ab/codec_k*.json)
     const uint64_t chunk = std::min<uint64_t>(nblk, 4096);
@@ -1168,7 +1225,8 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk, ++k) {
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
         Bufs &u = B[k % S];
-        k_defl_parse<<<nb, kTP, 0, u.st>>>(d_src, n, b0, u.lmask, u.nmatch, u.mlist, u.freq);
+        k_defl_parse<<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)ncu), kTP, 0, u.st>>>(d_src, n, b0, nb, u.lmask, u.nmatch,
+                                                                                      u.mlist, u.freq);
         OGE_LAUNCH_CHECK(ctx);
         k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs, n, b0, level, u.sizes);
         OGE_LAUNCH_CHECK(ctx);
