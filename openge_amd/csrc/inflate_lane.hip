@@ -62,7 +62,11 @@ constexpr int kWps = 3;        // waves per SIMD (VGPR budget 512 / 3)
 #endif
 constexpr int kStreams = OGE_INFL_STREAMS;     // chunk pipelines (see oge_inflate_lanes)
 constexpr uint64_t kChunkLanes = OGE_INFL_CHUNK;  // blocks per lane per chunk, at most
-constexpr int LB = 4;          // literals per decode step (see the ST_SYM path)
+#ifndef OGE_INFL_LB
+#define OGE_INFL_LB 6
+#endif
+constexpr int LB = OGE_INFL_LB;  // literals per batch (see the ST_SYM path; 20M reads, LB 3 / 4 / 5 / 6:
+                                 // 48.1 / 45.1 / 43.5 / 43.2 ms)
 #ifndef OGE_INFL_INNER
 #define OGE_INFL_INNER 16
 #endif
@@ -224,9 +228,9 @@ __device__ bool wbuild(P1Lds &S, uint32_t j, OGE_G uint8_t *list, OGE_G uint8_t 
 // ---------------------------------------------------------------------------- phase 1
 // An iteration (ST_SYM) decodes up to LB literals from the direct table, then one symbol of any kind (a
 // long-code literal, end of block, or a match with its length and distance codes), then up to LB direct
-// literals again; every part starts with a refill, which leaves >= 32 bits in the buffer: LB = 4 direct
-// codes take <= 24 bits, a literal/length code + its extra bits <= 20, a distance code + its extra bits
-// <= 28.  (r02 commit 3941758 let a batch follow a long code without a refill -- 15 + 3 * 6 = 33 > 32 --
+// literals again; every part starts with a refill, which leaves >= 33 bits in the buffer: five direct codes
+// take <= 30 bits (a sixth is taken only when its length fits the bits left), a literal/length code + its
+// extra bits <= 20, a distance code + its extra bits <= 28.  (r02 commit 3941758 let a batch follow a long code without a refill -- 15 + 3 * 6 = 33 > 32 --
 // and corrupted a block at 300M reads; tests/test_gpu_inflate.py::test_long_codes_before_direct_literal_runs
 // pins it.)  A wave's iteration count is the maximum over its 64 blocks, and it runs the union of their
 // paths, so a lane makes as much progress per iteration as the union costs: C2 BGZF blocks take 11.5k
@@ -243,7 +247,7 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                                                       uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
                                                       uint8_t *__restrict__ xtab, uint8_t *__restrict__ scratch,
                                                       uint32_t *__restrict__ err, unsigned long long *__restrict__ next) {
-    static_assert(LB <= 4 && TL * LB <= 32, "a step's literal batch must fit the 32 bits a refill guarantees");
+    static_assert(LB + 1 < 8, "a batch and the pending literal: fewer bytes than the 8-byte register (put_n shifts < 64)");
     static_assert(sizeof(P1Lds) <= 13312, "12 waves per CU");
     __shared__ P1Lds S;
     const uint32_t lane = threadIdx.x;
@@ -338,11 +342,11 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
         ++pos;
         if (!(q & 7)) store_chunk((q >> 3) - 1, acc);
     };
-    // n (<= 5) bytes at pos, the first in the low byte of v: one shift-or into the register and at most one
-    // chunk store (the batch completes the current chunk when it brings its m missing bytes)
+    // n (<= LB + 1) bytes at pos, the first in the low byte of v: one shift-or into the register and at most
+    // one chunk store (the batch completes the current chunk when it brings its m missing bytes)
     auto put_n = [&](uint64_t v, uint32_t n) {
         const uint32_t q0 = pos + al, m = 8 - (q0 & 7);
-        const uint32_t mm = min(m, 5u), nn = max(n, 1u);  // shifts stay below 64 on the paths not taken
+        const uint32_t mm = min(m, (uint32_t)LB + 1), nn = max(n, 1u);  // shifts stay below 64 on the paths not taken
         if (n >= m) store_chunk(q0 >> 3, (acc >> (8 * mm)) | (v << (64 - 8 * mm)));
         if (n) acc = (acc >> (8 * nn)) | (v << (64 - 8 * nn));
         pos += n;
@@ -352,7 +356,8 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
         if (q & 7) store_chunk(q >> 3, acc >> (8 * (8 - (q & 7))));
     };
     // Up to LB literals whose codes sit in the direct table (sym < 256: bit 8 of the entry clear).  After
-    // the refill >= 32 bits are buffered and LB direct codes take <= 24, so no budget check is needed.
+    // the refill >= 33 bits are buffered: five direct codes (<= 30 bits) need no budget check, a sixth or
+    // seventh stops the batch when its length exceeds the bits left.
     // Branch-free: the lookup chain (entry -> shift -> next entry) carries only selects, and the batch's
     // bytes go out in one put_n (r04: a put per literal, whose chunk-store branch sat in that chain).
     // np (0 or 1) pending bytes in pb -- the literal of the iteration's main symbol -- go out with the batch
@@ -365,6 +370,8 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
         for (int k = 0; k < LB; ++k) {
             const uint32_t e2 = S.lt[(uint32_t)buf & ((1u << TL) - 1)][lane];
             go = go && !(e2 & 0x100) && pos + n < osz;  // bit 8: a length code, end of block or a longer code
+            // a refill guarantees 33 bits: TL * 5 of them; longer batches stop where the buffered bits end
+            if (TL * (k + 1) > 32) go = go && (e2 >> 9) <= cnt;  // folded at compile time (k unrolled)
             const uint32_t L = go ? e2 >> 9 : 0u;
             buf >>= L;
             cnt -= L;
