@@ -571,13 +571,16 @@ def exchange_summary(per_rank: list) -> dict:
     tags: dict = {}
     for r in per_rank:
         for x in r["exchanges"]:
-            t = tags.setdefault(x["tag"], {"calls": x["calls"], "bytes_between_ranks": 0, "bytes_kept": 0, "max_ms": 0.0})
+            t = tags.setdefault(x["tag"], {"calls": x["calls"], "bytes_between_ranks": 0, "bytes_kept": 0, "max_ms": 0.0,
+                                           "mode": x.get("mode", "blocking")})
             t["bytes_between_ranks"] += x["bytes_sent"]
             t["bytes_kept"] += x["bytes_self"]
             t["max_ms"] = round(max(t["max_ms"], x["ms"]), 3)
     return {"by_tag": tags, "per_rank": [r["exchanges"] for r in per_rank],
             "what": "last timed step; bytes_between_ranks = sum over ranks of bytes sent to other ranks; "
-                    "ms = host wall time of the tag's collectives on a rank (peers' skew included)"}
+                    "ms = host wall time of the tag's collectives on a rank (peers' skew included); mode side_stream = "
+                    "the peers' parts moved on a side stream while the rank's own records went through the input "
+                    "pass (RCCL: ms is the time to queue them)"}
 
 
 def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):

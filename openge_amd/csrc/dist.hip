@@ -64,6 +64,15 @@ struct OgeTransport {
                           const uint64_t *rbytes, const uint64_t *roff) = 0;
     virtual int allgather_host(oge_ctx *ctx, const void *in, void *out, size_t bytes) = 0;
     virtual int reduce_scatter_max_u8(oge_ctx *ctx, const uint8_t *in, uint8_t *out, size_t chunk) = 0;
+    // The peers' parts of an all-to-all (the caller moves its own part), ordered after everything already on
+    // stream st.  On return the exchange is either complete (host-driven transports: their copies run on st
+    // while ctx->stream keeps executing what was queued on it -- the overlap) or queued on st (RCCL); the
+    // caller makes ctx->stream wait for st.  Default: the blocking all-to-all on ctx->stream (no overlap).
+    virtual int alltoallv_peers(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
+                                const uint64_t *rbytes, const uint64_t *roff, hipStream_t st) {
+        (void)st;
+        return alltoallv(ctx, send, sbytes, soff, recv, rbytes, roff);
+    }
 };
 
 // One exchange site of a step: bytes this rank sent to / received from other ranks (and kept), and the
@@ -73,6 +82,10 @@ struct OgeXchg {
     std::string tag;
     uint64_t sent = 0, recv = 0, self = 0, calls = 0;
     double ms = 0;
+    // "blocking": ms covers the data movement; "side_stream": the peers' parts moved on a side stream beside
+    // the caller's own work (host transport: ms covers the staged copies, which ran beside it; RCCL: ms is
+    // the time to queue them)
+    const char *mode = "blocking";
 };
 
 struct oge_comm {
@@ -102,6 +115,21 @@ struct oge_comm {
                 x.recv += rbytes[p];
             }
         }
+        return rc;
+    }
+    // the peers' parts only (sbytes / rbytes of this rank's own part are ignored), see OgeTransport
+    int alltoallv_peers(const char *tag, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
+                        const uint64_t *rbytes, const uint64_t *roff, hipStream_t st) {
+        std::vector<uint64_t> sb(sbytes, sbytes + tr->size), rb(rbytes, rbytes + tr->size);
+        sb[tr->rank] = rb[tr->rank] = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = tr->alltoallv_peers(ctx, send, sb.data(), soff, recv, rb.data(), roff, st);
+        OgeXchg &x = stat(tag);
+        x.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        x.calls++;
+        x.mode = "side_stream";
+        x.self += sbytes[tr->rank];
+        for (int p = 0; p < tr->size; ++p) x.sent += sb[p], x.recv += rb[p];
         return rc;
     }
     int allgather_host(const char *tag, const void *in, void *out, size_t bytes) {
@@ -183,10 +211,12 @@ struct LocalTransport : OgeTransport {
 // the host-staged transport's memory operations (dist_shm.h), on the context stream
 struct StageOps {
     oge_ctx *ctx;
-    int d2h(void *h, const void *d, size_t n) { return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess ? 0 : -1; }
-    int h2d(void *d, const void *h, size_t n) { return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, ctx->stream) == hipSuccess ? 0 : -1; }
-    int d2d(void *d, const void *s, size_t n) { return hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, ctx->stream) == hipSuccess ? 0 : -1; }
-    int sync() { return hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : -1; }
+    hipStream_t st = nullptr;  // null: the context stream
+    hipStream_t s() const { return st ? st : ctx->stream; }
+    int d2h(void *h, const void *d, size_t n) { return hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s()) == hipSuccess ? 0 : -1; }
+    int h2d(void *d, const void *h, size_t n) { return hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s()) == hipSuccess ? 0 : -1; }
+    int d2d(void *d, const void *s_, size_t n) { return hipMemcpyAsync(d, s_, n, hipMemcpyDeviceToDevice, s()) == hipSuccess ? 0 : -1; }
+    int sync() { return hipStreamSynchronize(s()) == hipSuccess ? 0 : -1; }
 };
 
 struct ShmTransport : OgeTransport {
@@ -194,7 +224,15 @@ struct ShmTransport : OgeTransport {
     const char *name() const override { return "host"; }
     int alltoallv(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv, const uint64_t *rbytes,
                   const uint64_t *roff) override {
-        StageOps ops{ctx};
+        return a2a_on(ctx, send, sbytes, soff, recv, rbytes, roff, nullptr);
+    }
+    int alltoallv_peers(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
+                        const uint64_t *rbytes, const uint64_t *roff, hipStream_t st) override {
+        return a2a_on(ctx, send, sbytes, soff, recv, rbytes, roff, st);  // staged copies on st
+    }
+    int a2a_on(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv, const uint64_t *rbytes,
+               const uint64_t *roff, hipStream_t st) {
+        StageOps ops{ctx, st};
         oge_dist::ShmColl<StageOps> c{*seg, ops};
         const int rc = c.alltoallv(send, sbytes, soff, recv, rbytes, roff);
         return rc ? oge_fail(ctx, OGE_ERR_HIP, rc == -2 ? "host transport: all-to-all timed out (a rank did not arrive)"
@@ -236,6 +274,17 @@ struct RcclTransport : OgeTransport {
         }
         OGE_NCCL_TRY(ctx, ncclGroupEnd());
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        return OGE_OK;
+    }
+    int alltoallv_peers(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
+                        const uint64_t *rbytes, const uint64_t *roff, hipStream_t st) override {
+        OGE_NCCL_TRY(ctx, ncclGroupStart());  // queued on st, not waited for: the caller joins st
+        for (int p = 0; p < size; ++p) {
+            if (p == rank) continue;
+            if (sbytes[p]) OGE_NCCL_TRY(ctx, ncclSend((const uint8_t *)send + soff[p], sbytes[p], ncclUint8, p, comm, st));
+            if (rbytes[p]) OGE_NCCL_TRY(ctx, ncclRecv((uint8_t *)recv + roff[p], rbytes[p], ncclUint8, p, comm, st));
+        }
+        OGE_NCCL_TRY(ctx, ncclGroupEnd());
         return OGE_OK;
     }
     int allgather_host(oge_ctx *ctx, const void *in, void *out, size_t bytes) override {
@@ -459,9 +508,15 @@ struct Dist {
 
 }  // namespace
 
+// The record exchange still to be made when dist_dedup starts (sort + dedup): the byte plan, the send
+// buffer and the record plan (which records of rbuf came from which rank)
+struct RecXchg {
+    const oge_dist::Plan *pb, *pr;
+    const uint8_t *sbuf;
+};
 static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, uint64_t RB, int32_t n_ref, const uint64_t *d_spl,
                       bool sorted, const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
-                      uint64_t *n_dup_total);
+                      uint64_t *n_dup_total, const RecXchg *xr = nullptr);
 
 static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref, int sort,
                     const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out, uint64_t *n_dup_total) {
@@ -558,9 +613,11 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     uint64_t *roff = (uint64_t *)ctx->ws("dist_roff", (R + 1) * 8);
     if (!rbuf || !rsz || !roff) rc = OGE_ERR_HIP;
     if ((rc = D.agree(rc))) return rc;
-    // every rank makes both exchanges; a failure goes to the agree() below, never straight out
-    rc = D.a2a("records", pb, 1, sbuf, rbuf);
-    if (const int r2 = D.a2a("record_sizes", pr, 4, ssz, rsz)) rc = rc ? rc : r2;
+    // every rank makes both exchanges; a failure goes to the agree() below, never straight out.  With
+    // duplicate marking the records follow inside dist_dedup, overlapped with the local input pass.
+    rc = D.a2a("record_sizes", pr, 4, ssz, rsz);
+    if (!opts)
+        if (const int r2 = D.a2a("records", pb, 1, sbuf, rbuf)) rc = rc ? rc : r2;
     if (!rc) {
         hipLaunchKernelGGL(k_off_from_u32, dim3(oge_ceil_div(R + 1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)rsz, R, roff);
         rc = hipGetLastError() == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
@@ -588,14 +645,15 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
         return OGE_OK;
     }
 
-    return dist_dedup(D, rbuf, roff, R, RB, n_ref, d_spl, true, opts, d_out, d_out_off, n_out, n_dup_total);
+    const RecXchg xr{&pb, &pr, sbuf};
+    return dist_dedup(D, rbuf, roff, R, RB, n_ref, d_spl, true, opts, d_out, d_out_off, n_out, n_dup_total, &xr);
 }
 
 // Duplicate marking of this rank's records (its sorted slice when `sorted`, else its input shard in
 // input order), then the gather of the records with bin recomputed and 0x400 applied.
 static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, uint64_t RB, int32_t n_ref, const uint64_t *d_spl,
                       bool sorted, const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
-                      uint64_t *n_dup_total) {
+                      uint64_t *n_dup_total, const RecXchg *xr) {
     oge_comm *comm = D.comm;
     oge_ctx *ctx = D.ctx;
     const int G = D.G;
@@ -617,19 +675,58 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
     meta = (RecMeta *)ctx->ws("md_meta", (R + 1) * sizeof(RecMeta));
     if (!rc && !meta) rc = OGE_ERR_HIP;
     if (!rc) rc = hipMemsetAsync(counts, 0, 16, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
-    if (!rc) {
-        t = ctx->begin_stage("input_pass");
+    // the ReadEnds / key pass over records [r0, r1) of rbuf
+    auto pass = [&](uint64_t r0, uint64_t r1) {
+        if (rc || r1 <= r0) return;
         OgePassArgs a = {};
         a.recs = rbuf;
-        a.off = roff;
-        a.n = R;
-        a.meta = meta_in;
+        a.off = roff + r0;
+        a.n = r1 - r0;
+        a.ibase = r0;
+        a.meta = meta_in + r0;
         a.rg = rg;
-        a.keys = sorted ? skeys : nullptr;
-        a.vals = sorted ? svals : nullptr;
+        a.keys = sorted ? skeys + r0 : nullptr;
+        a.vals = sorted ? svals + r0 : nullptr;
         a.n_ref = n_ref;
         a.bad = counts + 2;
         rc = oge_input_pass(ctx, a);
+    };
+    if (xr) {
+        // Records still to exchange: this rank's own records are copied and passed on
+        // the context stream while the peers' parts move on a side stream (RCCL: queued there; the host
+        // transport: its staged copies run there while this stream executes the pass), then the pass covers
+        // the received records.  Every rank makes the exchange whatever happened before (agree() below).
+        t = ctx->begin_stage("input_pass");
+        const int me = D.rank;
+        const oge_dist::Plan &pb = *xr->pb, &pr = *xr->pr;
+        hipStream_t side = ctx->side_stream(0);
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        for (auto &e : ev)
+            if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = dist_hip_fail(ctx, __LINE__);
+        if (!rc && !side) rc = OGE_ERR_HIP;
+        // the send buffer (gathered on the context stream) before the side stream reads it
+        if (!rc && (hipEventRecord(ev[0], ctx->stream) != hipSuccess || hipStreamWaitEvent(side, ev[0], 0) != hipSuccess))
+            rc = dist_hip_fail(ctx, __LINE__);
+        if (!rc && pb.scnt[me] &&
+            hipMemcpyAsync(rbuf + pb.roff[me], xr->sbuf + pb.soff[me], pb.scnt[me], hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
+            rc = dist_hip_fail(ctx, __LINE__);
+        pass(pr.roff[me], pr.roff[me] + pr.rcnt[me]);
+        std::vector<uint64_t> sb(D.G), so(D.G), rb(D.G), ro(D.G);
+        for (int g = 0; g < D.G; ++g) sb[g] = pb.scnt[g], so[g] = pb.soff[g], rb[g] = pb.rcnt[g], ro[g] = pb.roff[g];
+        const int rx = comm->alltoallv_peers("records", xr->sbuf, sb.data(), so.data(), rbuf, rb.data(), ro.data(),
+                                             side ? side : ctx->stream);
+        if (!rc) rc = rx;
+        if (!rc && (hipEventRecord(ev[1], side) != hipSuccess || hipStreamWaitEvent(ctx->stream, ev[1], 0) != hipSuccess))
+            rc = dist_hip_fail(ctx, __LINE__);
+        pass(0, pr.roff[me]);
+        pass(pr.roff[me] + pr.rcnt[me], R);
+        if (side) (void)hipStreamSynchronize(side);  // the events may go: nothing is left on the side stream
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        ctx->end_stage(t);
+    } else if (!rc) {
+        t = ctx->begin_stage("input_pass");
+        pass(0, R);
         ctx->end_stage(t);
     }
     if (sorted) {
@@ -1029,12 +1126,14 @@ const char *oge_comm_transport(const oge_comm *c) { return c ? c->tr->name() : "
 int64_t oge_comm_stats_json(const oge_comm *c, char *buf, uint64_t cap) {
     if (!c) return -1;
     std::string j = "[";
-    char tmp[256];
+    char tmp[384];
     for (size_t i = 0; i < c->stats.size(); ++i) {
         const OgeXchg &x = c->stats[i];
-        snprintf(tmp, sizeof tmp, "%s{\"tag\":\"%s\",\"calls\":%llu,\"bytes_sent\":%llu,\"bytes_recv\":%llu,\"bytes_self\":%llu,\"ms\":%.3f}",
+        snprintf(tmp, sizeof tmp,
+                 "%s{\"tag\":\"%s\",\"calls\":%llu,\"bytes_sent\":%llu,\"bytes_recv\":%llu,\"bytes_self\":%llu,\"ms\":%.3f,"
+                 "\"mode\":\"%s\"}",
                  i ? "," : "", x.tag.c_str(), (unsigned long long)x.calls, (unsigned long long)x.sent, (unsigned long long)x.recv,
-                 (unsigned long long)x.self, x.ms);
+                 (unsigned long long)x.self, x.ms, x.mode);
         j += tmp;
     }
     j += "]";

@@ -52,7 +52,8 @@ struct OgePassArgs {
     RecMeta *meta;           // summary of input record i
     OgeRgTable rg;
     uint64_t *keys;          // coordinate sort key of input record i (+ byte size payload)
-    uint32_t *vals;          // = i
+    uint32_t *vals;          // = ibase + i
+    uint64_t ibase;          // index of the pass's first record in a larger array (a pass over a sub-range)
     int32_t n_ref;
     unsigned int *bad;       // bit 0: refID/pos out of range, bit 1: block_size out of [32, 10000]
     // gather pass: output record k = input record perm[k] (or meta[k].src when smeta is given)

@@ -87,7 +87,7 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
         }
         if (bs < 32 || bs > 10000) atomicOr(a.bad, 2u);
         a.keys[i] = k | ((uint64_t)(bs + 4) << 50);
-        a.vals[i] = (uint32_t)i;
+        a.vals[i] = (uint32_t)(a.ibase + i);
     }
     if (!META) return;
     const uint64_t c = r + OGE_OFF_NAME + lname;

@@ -106,6 +106,8 @@ def test_bench_multiprocess_bootstrap_matches_reference(world, realign, tmp_path
     rec_bytes = by["records"]["bytes_between_ranks"] + by["records"]["bytes_kept"]
     assert rec_bytes == int(np.frombuffer(want, np.uint8).size) - _header_bytes(want)
     assert by["record_sizes"]["bytes_between_ranks"] + by["record_sizes"]["bytes_kept"] == 4 * nr1
+    # the record exchange ran on a side stream beside the own records' input pass
+    assert by["records"]["mode"] == "side_stream" and by["record_sizes"]["mode"] == "blocking"
     if realign:
         rl = line["realign"]
         assert rl["n_gpus"] == world and rl["value"] > 0
