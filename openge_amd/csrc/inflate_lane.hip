@@ -67,6 +67,9 @@ constexpr uint64_t kChunkLanes = OGE_INFL_CHUNK;  // blocks per lane per chunk, 
 #endif
 constexpr int LB = OGE_INFL_LB;  // literals per batch (see the ST_SYM path; 20M reads, LB 3 / 4 / 5 / 6:
                                  // 48.1 / 45.1 / 43.5 / 43.2 ms)
+#ifndef OGE_INFL_ITER  // iteration shape (build knob): 0 batch + symbol + batch, 1 symbol + 2 batches, 2 batch +
+#define OGE_INFL_ITER 0  // symbol + 2 batches; 20M reads (LB 6): 43.8 / 43.6 / 45.6 ms
+#endif
 #ifndef OGE_INFL_INNER
 #define OGE_INFL_INNER 16
 #endif
