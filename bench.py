@@ -27,9 +27,10 @@ Also on the same JSON line:
                    BAM-in/BAM-out sample of the same generator
   realign       -- configs[4]: openge localrealign on the C5 set (50k indel intervals)
 
-Multi-GPU (torchrun, one rank per GPU): the same 300M-read sample split across N ranks (strong
-scaling), one input BAM file per rank; oge_mergesort_bgzf_dist range-splits the ByPosition keys with
-sampled splitters, exchanges the records with an all-to-all (RCCL over xGMI between GPUs; the
+Multi-GPU (torchrun, one rank per GPU): ONE 300M-read input BAM file split by byte range across the N
+ranks (strong scaling); oge_mergesort_bgzf_shard has every rank inflate only the BGZF blocks of its
+range (block and record boundaries joined with the neighbouring ranks), range-splits the ByPosition
+keys with sampled splitters, exchanges the records with an all-to-all (RCCL over xGMI between GPUs; the
 host-staged transport when ranks share a GPU), sorts each rank's slice and marks duplicates exactly
 with hash-routed mate-join / pair-group exchanges.  value = reads / max-over-ranks wall
 time.  --dump-dir writes every rank's output slice (tests/test_gpu_multiproc.py concatenates them).
@@ -558,7 +559,7 @@ def main():
     ctx.close()
 
 
-DIST_STAGES = ["bgzf_index", "bgzf_inflate", "rec_walk", "dist_split", "dist_exchange", "input_pass", "sort_radix",
+DIST_STAGES = ["bgzf_index", "bgzf_inflate", "shard_edges", "rec_walk", "dist_split", "dist_exchange", "input_pass", "sort_radix",
                "sort_ties", "meta_gather", "dist_frags", "dist_join", "dist_pairs", "dist_reduce", "md_apply",
                "gather_offsets", "gather_records", "bgzf_deflate"]
 
@@ -585,43 +586,47 @@ def exchange_summary(per_rank: list) -> dict:
 
 def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
     """N ranks, one process per GPU, RCCL over xGMI through the library's own communicator
-    (oge_comm_init_rank; torch.distributed only bootstraps it and times the steps, on gloo).  Rank g
-    holds one input BAM file in its HBM: the C2 data set's slots [n*g/N, n*(g+1)/N) behind the common
-    header, BGZF level 6 (mergesort's several input files, one per rank).  A step is the whole
-    `mergesort -M --nosplit` chain over the N files (oge_mergesort_bgzf_dist): inflate, record walk,
-    range-split exchange of the records, local sort, exact distributed dedup, and every rank deflating
-    its slice of the one output file.  Strong scaling: the 300M reads are split over the N ranks."""
+    (oge_comm_init_rank; torch.distributed only bootstraps it and times the steps, on gloo).  ONE input
+    BAM file (config 4: the node sorts one file): the C2 data set behind its header, BGZF level 6, made
+    by the same seeded generator and deterministic GPU deflate on every rank before the timed region;
+    rank g keeps only its byte range of it in its HBM (lib.shard_ranges: the blocks that start in
+    [a_g, a_g + own_g), plus up to 64 KiB of the next range for its last block).  A step is the whole
+    `mergesort -M --nosplit` chain over the one file (oge_mergesort_bgzf_shard): every rank indexes and
+    inflates only its own blocks, the ranks join their block and record boundaries and hand over the
+    records that straddle them, then the range-split exchange of the records, local sort, exact
+    distributed dedup, and every rank deflating its slice of the one output file.  Strong scaling: the
+    300M reads of the file are split over the N ranks."""
     import ctypes as C
-    s0, s1 = n_all * rank // world, n_all * (rank + 1) // world
-    n = s1 - s0
     buf = C.create_string_buffer(1 << 16)
     L.check(L.lib().oge_synth_finalize(C.byref(p)))
     L.check(L.lib().oge_synth_header_text(C.byref(p), buf, 1 << 16, None))
     hb = bam_header_bytes(buf.value.decode())
-    d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    ctx.synth_range_dev(p, s0, n, d_offs.data_ptr(), None)
+    d_offs = torch.empty(n_all + 1, dtype=torch.int64, device=dev)
+    ctx.synth_range_dev(p, 0, n_all, d_offs.data_ptr(), None)
     ctx.sync()
     B = int(d_offs[-1].item())
     S = torch.empty(len(hb) + B + 64, dtype=torch.uint8, device=dev)
-    ctx.synth_range_dev(p, s0, n, d_offs.data_ptr(), S.data_ptr() + len(hb))
+    ctx.synth_range_dev(p, 0, n_all, d_offs.data_ptr(), S.data_ptr() + len(hb))
     S[:len(hb)].copy_(torch.frombuffer(bytearray(hb), dtype=torch.uint8).to(dev))
     del d_offs
     Z, zb = build_input(ctx, L, torch, dev, S, len(hb) + B, args.level)
     del S
-    d_z = torch.empty(zb + 28 + 64, dtype=torch.uint8, device=dev)
-    d_z[:zb].copy_(Z[:zb])
-    d_z[zb:zb + 28].copy_(torch.tensor(list(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")),
-                                       dtype=torch.uint8, device=dev))
-    zbytes = zb + 28
+    Z[zb:zb + 28].copy_(torch.tensor(list(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")),
+                                     dtype=torch.uint8, device=dev))
+    zfile = zb + 28
+    a, own, end = L.shard_ranges(zfile, world)[rank]
+    d_z = torch.empty(end - a + 64, dtype=torch.uint8, device=dev)
+    d_z[:end - a].copy_(Z[a:end])
+    zbytes = end - a
     del Z
     torch.cuda.empty_cache()
     torch.cuda.synchronize(dev)
     obj = [L.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     comm = L.comm_init_rank(ctx, world, rank, obj[0])
-    log(f"rank {rank}: {n} reads, input file {zbytes / 1e9:.2f} GB, transport {comm.transport}")
+    log(f"rank {rank}: file bytes [{a}, {a + own}) of {zfile} ({zbytes} held), transport {comm.transport}")
     mopts = L.mergesort_opts(level=args.level, mark_duplicates=1)
-    step = lambda: comm.mergesort_bgzf_dist(d_z.data_ptr(), zbytes, mopts)
+    step = lambda: comm.mergesort_bgzf_shard(d_z.data_ptr(), zbytes, own, mopts)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -638,20 +643,20 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
     t = torch.tensor([dt], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    sizes = [None] * world
-    dist.all_gather_object(sizes, (n, ob))
-    # per-rank record of the last step: every exchange's bytes and time, every stage's time
+    # per-rank record of the last step: every exchange's bytes and time, every stage's time, the share of
+    # the file this rank decoded
     K = args.steps
-    mine = {"exchanges": comm.exchange_stats(), "stages_ms": {k: round(v / K, 3) for k, v in tot.items()}}
+    shard = {k: ctx.counter(k) for k in ("shard_blocks", "shard_zbytes", "shard_bytes", "shard_records")}
+    shard.update({"file_range": [a, a + own], "output_bytes": ob})
+    mine = {"exchanges": comm.exchange_stats(), "stages_ms": {k: round(v / K, 3) for k, v in tot.items()}, "shard": shard}
     per_rank = [None] * world
     dist.all_gather_object(per_rank, mine)
     assert nr == n_all, (nr, n_all)
     transport = comm.transport
     if args.dump_dir:  # this rank's slice of the output file (valid until the rank's next call)
-        ob_last = ob
-        hs = torch.empty(max(ob_last, 1), dtype=torch.uint8)
-        L.check(L.lib().oge_memcpy(ctx.h, hs.data_ptr(), d_last, ob_last, 2), ctx.h)
-        Path(args.dump_dir, f"slice_{rank}.bam").write_bytes(hs[:ob_last].numpy().tobytes())
+        hs = torch.empty(max(ob, 1), dtype=torch.uint8)
+        L.check(L.lib().oge_memcpy(ctx.h, hs.data_ptr(), d_last, ob, 2), ctx.h)
+        Path(args.dump_dir, f"slice_{rank}.bam").write_bytes(hs[:ob].numpy().tobytes())
     comm.close()
     del d_z
     torch.cuda.empty_cache()
@@ -662,13 +667,14 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
         out = {"metric": METRIC, "value": round(n_all * K / dt / 1e6, 2), "unit": "Mreads/s", "n_gpus": world,
                "steps": K, "warmup": args.warmup, "ms_per_step": round(dt / K * 1e3, 2), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "u8",
-               "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234, one level-6 BGZF input file per "
-                       "rank resident in its HBM",
-               "config": {"workload": f"C2+C3 end to end over {world} GPUs: {n_all // 1000000}M reads in {world} BAM "
-                                      "files -> mergesort -M --nosplit (range-split sort + exact distributed dedup) -> "
-                                      f"one BGZF level-{args.level} BAM file as {world} rank slices, in HBM",
-                          "reads_total": n_all, "duplicates_flagged": nd,
-                          "rank_reads_and_output_bytes": sizes,
+               "data": "synthetic: C2 generator (SURVEY §8d) on device, seed 1234, ONE level-6 BGZF input file; rank g "
+                       "holds its byte range of it in its HBM",
+               "config": {"workload": f"C2+C3 end to end over {world} GPUs: one {n_all // 1000000}M-read BAM file, "
+                                      "each rank decoding the BGZF blocks of its byte range -> mergesort -M --nosplit "
+                                      "(range-split sort + exact distributed dedup) -> one BGZF "
+                                      f"level-{args.level} BAM file as {world} rank slices, in HBM",
+                          "reads_total": n_all, "input_file_bytes": zfile, "duplicates_flagged": nd,
+                          "shard_per_rank": [r["shard"] for r in per_rank],
                           "parallelism": f"{world} ranks (one process per GPU), all-to-all via oge_comm_init_rank",
                           "transport": transport},
                "stages_ms_rank0": {k: round(v / K, 3) for k, v in tot.items()},

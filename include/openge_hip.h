@@ -53,6 +53,10 @@ void oge_ctx_destroy(oge_ctx *ctx);
 const char *oge_last_error(const oge_ctx *ctx);   /* ctx may be NULL (thread-local last error) */
 /* last pipeline's kernel timings in ms, measured with HIP events on the context stream */
 int oge_ctx_timing(oge_ctx *ctx, const char *stage, double *ms_out);
+/* A work count of the context's last pipeline call (e.g. "shard_blocks", "shard_zbytes",
+ * "shard_bytes", "shard_records" of oge_bgzf_decode_shard: this rank's BGZF blocks, their compressed
+ * and decompressed bytes, its records).  OGE_ERR_ARG when the call recorded no such count. */
+int oge_ctx_counter(oge_ctx *ctx, const char *name, uint64_t *value);
 /* version string of the library, gfx target it was built for */
 const char *oge_version(void);
 
@@ -203,7 +207,8 @@ int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, og
  * MPI_LOCALNRANKS == nranks); otherwise RCCL, the only transport that reaches other hosts.  The CLI,
  * whose ranks are threads of one process, passes "host" when they share a device. */
 int oge_comm_init_rank_mode(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, const char *mode, oge_comm **out);
-/* Per-exchange record of the communicator's last oge_sort_markdup_dist / oge_mergesort_bgzf_dist call:
+/* Per-exchange record of the communicator's last oge_sort_markdup_dist / oge_mergesort_bgzf_dist /
+ * oge_mergesort_bgzf_shard / oge_bgzf_decode_shard call:
  * a JSON array of {tag, calls, bytes_sent, bytes_recv, bytes_self, ms} (bytes to / from other ranks and
  * kept on this rank; host wall time of the collectives, waiting for peers included).  Returns the JSON
  * length; writes it (NUL-terminated) when cap > length. */
@@ -234,6 +239,26 @@ int oge_mergesort_bgzf_dist(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes,
 int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref, int sort,
                           const oge_markdup_opts *opts, uint8_t **d_out, uint64_t **d_out_off, uint64_t *n_out,
                           uint64_t *n_dup_total);
+/* ONE BGZF BAM file read by every rank from its own byte range (config 4 on the node; replaces the
+ * reader thread of BgzfInputStream util/bgzf_input_stream.cpp:180-206 + BamDeserializer::read
+ * util/bam_deserializer.h:143-193 feeding SplitByChromosome, cmd/command_mergesort.cpp:118-179).  Rank g
+ * holds the file's bytes [a_g, a_g + zbytes) in HBM, a_g = the sum of the earlier ranks' own_bytes, and
+ * decodes the BGZF blocks that START in [a_g, a_g + own_bytes): the buffer must hold them whole (own_bytes
+ * + 65536 bytes, or up to the end of the file, which the last rank's buffer ends at; zbytes >= own_bytes).
+ * The ranks confirm their first block / first record with their predecessors' walk exits (allgathers)
+ * and fetch the <= 16 KiB tail of the record that straddles their part's end from the next ranks (an
+ * all-to-all).  Out: this rank's records -- those that START in its part of the decompressed stream, in
+ * file order, complete in its HBM (*d_off: n + 1 offsets into *d_recs, library workspace valid until the
+ * next call on the rank's context) -- and the raw BAM header (rank 0's, shared), copied to hdr_out when
+ * hdr_cap holds it (*hdr_len = its length; OGE_ERR_LIMIT otherwise).  The rank shards are contiguous
+ * input ranges in rank order: oge_sort_markdup_dist's input.  Collective. */
+int oge_bgzf_decode_shard(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, uint64_t own_bytes, const uint8_t **d_recs,
+                          const uint64_t **d_off, uint64_t *n, uint8_t *hdr_out, uint64_t hdr_cap, uint64_t *hdr_len);
+/* oge_mergesort_bgzf_dist over ONE input file sharded by byte range as oge_bgzf_decode_shard takes it:
+ * every rank inflates ~1/G of the blocks, then the range-split sort + exact dedup, then every rank
+ * deflates its slice of the output file (rank 0's with the header, the last rank's with the EOF block). */
+int oge_mergesort_bgzf_shard(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, uint64_t own_bytes, const oge_mergesort_opts *o,
+                             const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads_total, uint64_t *n_dup_total);
 /* Device synthetic generation of the slot range [slot0, slot0 + nslots) of a data set (one rank's
  * shard of a multi-GPU input). */
 int oge_synth_offsets_range_dev(oge_ctx *ctx, const void *params, uint64_t slot0, uint64_t nslots, uint64_t *d_offs);

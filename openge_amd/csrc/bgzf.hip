@@ -206,6 +206,7 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
     uint32_t hp[kR], vp[kR];  // the previous round's buckets and positions + 1 (0: nothing to insert)
 #pragma unroll
     for (int k = 0; k < kR; ++k) hp[k] = 0, vp[k] = 0;
+    static_assert(kNSub == 2, "f0 holds sub-block 0's counts while sub-block 1 reuses their table: two sub-blocks only");
     uint32_t f0 = 0;  // symbol t's count in sub-block 0 (kept while sub-block 1 reuses the table it was in)
     const uint64_t seg_base = pi * kNSeg;
     for (int sub = 0; sub < kNSub; ++sub) {
@@ -1155,12 +1156,7 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     *out_bytes = 0;
     if (!n) return OGE_OK;
     const uint64_t nblk = (n + kPay - 1) / kPay;
-    static int ncu = [] {  // persistent parse workgroups: one per CU
-        int d = 0, c = 0;
-        (void)hipGetDevice(&d);
-        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d);
-        return c > 0 ? c : 256;
-    }();
+    const int ncu = ctx->cu_count();  // persistent parse workgroups: one per CU of this context's device
     // payloads per chunk: one launch of each kernel (4096 measured best in r02: 2048 / 4096 / 8192,
     // profiles/r02_ab/codec_k*.json)
     const uint64_t chunk = std::min<uint64_t>(nblk, 4096);

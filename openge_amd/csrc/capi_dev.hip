@@ -113,6 +113,7 @@ void oge_ctx::reset_timing() {
     (void)hipGetLastError();
     if (timing_hold) return;
     stage_events.clear();
+    counters.clear();
     event_pool_used = 0;
 }
 
@@ -180,6 +181,14 @@ void oge_ctx_destroy(oge_ctx *ctx) {
         if (s) hipStreamDestroy(s);
     if (ctx->own_stream) hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+int oge_ctx_counter(oge_ctx *ctx, const char *name, uint64_t *value) {
+    if (!ctx || !name || !value) return oge_fail(ctx, OGE_ERR_ARG, "oge_ctx_counter: null argument");
+    auto it = ctx->counters.find(name);
+    if (it == ctx->counters.end()) return OGE_ERR_ARG;
+    *value = it->second;
+    return OGE_OK;
 }
 
 int oge_ctx_timing(oge_ctx *ctx, const char *stage, double *ms_out) {

@@ -73,6 +73,8 @@ struct OgeTransport {
         (void)st;
         return alltoallv(ctx, send, sbytes, soff, recv, rbytes, roff);
     }
+    // whether alltoallv_peers really runs beside the context stream (the default above does not)
+    virtual bool overlaps() const { return false; }
 };
 
 // One exchange site of a step: bytes this rank sent to / received from other ranks (and kept), and the
@@ -127,7 +129,7 @@ struct oge_comm {
         OgeXchg &x = stat(tag);
         x.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         x.calls++;
-        x.mode = "side_stream";
+        x.mode = tr->overlaps() ? "side_stream" : "blocking";
         x.self += sbytes[tr->rank];
         for (int p = 0; p < tr->size; ++p) x.sent += sb[p], x.recv += rb[p];
         return rc;
@@ -230,6 +232,7 @@ struct ShmTransport : OgeTransport {
                         const uint64_t *rbytes, const uint64_t *roff, hipStream_t st) override {
         return a2a_on(ctx, send, sbytes, soff, recv, rbytes, roff, st);  // staged copies on st
     }
+    bool overlaps() const override { return true; }
     int a2a_on(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv, const uint64_t *rbytes,
                const uint64_t *roff, hipStream_t st) {
         StageOps ops{ctx, st};
@@ -287,6 +290,7 @@ struct RcclTransport : OgeTransport {
         OGE_NCCL_TRY(ctx, ncclGroupEnd());
         return OGE_OK;
     }
+    bool overlaps() const override { return true; }
     int allgather_host(oge_ctx *ctx, const void *in, void *out, size_t bytes) override {
         uint8_t *d = (uint8_t *)ctx->ws("comm_allgather", bytes * size);
         if (!d) return OGE_ERR_HIP;
@@ -614,9 +618,12 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     if (!rbuf || !rsz || !roff) rc = OGE_ERR_HIP;
     if ((rc = D.agree(rc))) return rc;
     // every rank makes both exchanges; a failure goes to the agree() below, never straight out.  With
-    // duplicate marking the records follow inside dist_dedup, overlapped with the local input pass.
+    // duplicate marking the records follow inside dist_dedup, overlapped with the local input pass
+    // (OGE_DIST_RECORDS=blocking: before it, on the context stream -- the A/B and fallback of the overlap)
+    const char *rmode = getenv("OGE_DIST_RECORDS");
+    const bool overlap = opts && !(rmode && !strcmp(rmode, "blocking"));
     rc = D.a2a("record_sizes", pr, 4, ssz, rsz);
-    if (!opts)
+    if (!overlap)
         if (const int r2 = D.a2a("records", pb, 1, sbuf, rbuf)) rc = rc ? rc : r2;
     if (!rc) {
         hipLaunchKernelGGL(k_off_from_u32, dim3(oge_ceil_div(R + 1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)rsz, R, roff);
@@ -646,7 +653,7 @@ static int dist_run(oge_comm *comm, const uint8_t *d_recs, const uint64_t *d_off
     }
 
     const RecXchg xr{&pb, &pr, sbuf};
-    return dist_dedup(D, rbuf, roff, R, RB, n_ref, d_spl, true, opts, d_out, d_out_off, n_out, n_dup_total, &xr);
+    return dist_dedup(D, rbuf, roff, R, RB, n_ref, d_spl, true, opts, d_out, d_out_off, n_out, n_dup_total, overlap ? &xr : nullptr);
 }
 
 // Duplicate marking of this rank's records (its sorted slice when `sorted`, else its input shard in
@@ -974,6 +981,17 @@ int oge_comm_sum_u64(oge_comm *comm, uint64_t *v, int count) {
     return OGE_OK;
 }
 
+int oge_comm_allgather(oge_comm *comm, const char *tag, const void *in, void *out, size_t bytes) {
+    return comm->allgather_host(tag, in, out, bytes);
+}
+
+int oge_comm_alltoallv_dev(oge_comm *comm, const char *tag, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
+                           const uint64_t *rbytes, const uint64_t *roff) {
+    return comm->alltoallv(tag, send, sbytes, soff, recv, rbytes, roff);
+}
+
+void oge_comm_reset_stats(oge_comm *comm) { comm->stats.clear(); }
+
 // ---------------------------------------------------------------------------------------------- ABI
 extern "C" {
 
@@ -999,7 +1017,8 @@ uint64_t oge_comm_unique_id_bytes(void) { return sizeof(ncclUniqueId) + kIdNonce
 // Number of ranks the launcher placed on this node, when it says (torchrun LOCAL_WORLD_SIZE, Open MPI,
 // MPICH / Hydra); 0 = unknown.
 static int launcher_local_ranks() {
-    for (const char *v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS"}) {
+    for (const char *v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "SLURM_NTASKS_PER_NODE",
+                          "SLURM_STEP_TASKS_PER_NODE"}) {
         const char *e = getenv(v);
         if (e && *e) return atoi(e);
     }
@@ -1060,7 +1079,10 @@ static int comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id,
         ncclResult_t r = ncclCommInitRank(&t->comm, nranks, uid, rank);
         if (r != ncclSuccess) {
             delete c;
-            return oge_fail(ctx, OGE_ERR_HIP, (std::string("ncclCommInitRank: ") + ncclGetErrorString(r)).c_str());
+            std::string m = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+            if (mode == "auto" && ndev < nranks)  // ranks that may share a device, started by a launcher we do not know
+                m += " (fewer visible devices than ranks: ranks sharing a GPU need the host transport, OGE_COMM=host)";
+            return oge_fail(ctx, OGE_ERR_HIP, m.c_str());
         }
         t->rank = rank;
         t->size = nranks;
@@ -1149,7 +1171,7 @@ int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t 
     oge_ctx *ctx = comm->ctx;
     (void)hipSetDevice(ctx->device);
     ctx->reset_timing();
-    comm->stats.clear();
+    if (!ctx->timing_hold) comm->stats.clear();  // a composite entry point (pipeline.hip) keeps its earlier exchanges
     if (opts && opts->n_ref != n_ref) return oge_fail(ctx, OGE_ERR_ARG, "oge_sort_markdup_dist: opts->n_ref differs from n_ref");
     return dist_run(comm, d_recs, d_off, n, n_ref, sort, opts, d_out, d_out_off, n_out, n_dup_total);
 }

@@ -42,10 +42,12 @@ constexpr int kShmMaxRanks = 64;
 struct ShmRankPost {
     char bus[64];         // PCI bus id of the rank's device (the meeting's question)
     int64_t pid;
+    uint64_t pidns;       // inode of the rank's /proc/self/ns/pid: its pid means something here only if equal
+    std::atomic<uint64_t> beat;  // bumped by the rank's heartbeat thread while its segment is open
     uint64_t stage_bytes; // W as this rank computed it (must agree)
     uint64_t maxb;        // largest byte count this rank sends to another rank in the current collective
     uint64_t sb[kShmMaxRanks];  // bytes for each destination in the current collective
-    uint8_t pad[64];
+    uint8_t pad[48];
 };
 
 struct ShmCtl {
@@ -60,6 +62,8 @@ struct ShmCtl {
 class ShmSeg {
 public:
     ~ShmSeg() {
+        stop_.store(true);
+        if (hb_.joinable()) hb_.join();
         if (base_) munmap(base_, size_);
     }
     int size() const { return G_; }
@@ -84,9 +88,20 @@ public:
         const long mb = e && *e ? atol(e) : 32;
         return (uint64_t)std::min<long>(std::max<long>(mb, 1), 4096) << 20;
     }
-    // A wait ends early when a peer process is gone (its posted pid no longer exists); the wall-clock
-    // limit (OGE_COMM_TIMEOUT, default 1800 s) is only the backstop for a live peer that never arrives,
-    // so a slow rank (a larger input, a GPU under contention) does not break the communicator.
+    // A wait ends early when a peer process is gone: its posted pid no longer exists (only trusted when the
+    // peer posted this process's pid namespace), or -- for a peer in another pid namespace (containers
+    // sharing one IPC namespace) -- its heartbeat has not moved for OGE_COMM_STALE_S seconds.  The wall-clock
+    // limit (OGE_COMM_TIMEOUT, default 1800 s) is only the backstop for a live peer that never arrives, so
+    // a slow rank (a larger input, a GPU under contention) does not break the communicator.
+    static double stale_beat_s() {  // OGE_COMM_STALE_S (default 20)
+        const char *e = getenv("OGE_COMM_STALE_S");
+        const double t = e && *e ? atof(e) : 20.0;
+        return t > 0 ? t : 20.0;
+    }
+    static uint64_t pid_namespace() {
+        struct stat st;
+        return stat("/proc/self/ns/pid", &st) == 0 ? (uint64_t)st.st_ino : 0;
+    }
     static double timeout_s() {
         const char *e = getenv("OGE_COMM_TIMEOUT");
         const double t = e && *e ? atof(e) : 1800.0;
@@ -133,11 +148,22 @@ public:
         ShmRankPost &me = s->ctl_->post[rank];
         snprintf(me.bus, sizeof me.bus, "%s", bus ? bus : "");
         me.pid = (int64_t)getpid();
+        me.pidns = pid_namespace();
         me.stage_bytes = W;
+        s->my_ns_ = me.pidns;
+        s->seen_.assign(G, {0, std::chrono::steady_clock::now()});
+        s->hb_ = std::thread([s, rank]() {  // liveness for peers that cannot check this rank's pid
+            while (!s->stop_.load()) {
+                s->ctl_->post[rank].beat.fetch_add(1, std::memory_order_relaxed);
+                std::this_thread::sleep_for(std::chrono::milliseconds(100));
+            }
+        });
         s->ctl_->joined.fetch_add(1, std::memory_order_acq_rel);
         const auto t0 = std::chrono::steady_clock::now();
         for (uint64_t it = 0; s->ctl_->joined.load(std::memory_order_acquire) < (uint32_t)G; ++it) {
-            if (s->waited_too_long(t0, it)) {
+            // a rank that joined last and exited at once is not a failure of the meeting (the next
+            // barrier sees it): re-check the count after a failed wait
+            if (s->waited_too_long(t0, it) && s->ctl_->joined.load(std::memory_order_acquire) < (uint32_t)G) {
                 if (rank == 0) unlink(path.c_str());
                 *err = "host transport: not every rank joined " + path + " in time";
                 delete s;
@@ -167,7 +193,7 @@ public:
         const auto t0 = std::chrono::steady_clock::now();
         for (uint64_t it = 0; ctl_->gen.load(std::memory_order_acquire) == g; ++it) {
             if (ctl_->broken.load(std::memory_order_acquire)) return -2;
-            if (waited_too_long(t0, it)) {
+            if (waited_too_long(t0, it) && ctl_->gen.load(std::memory_order_acquire) == g) {
                 ctl_->broken.store(1, std::memory_order_release);
                 return -2;
             }
@@ -186,14 +212,39 @@ private:
         if (peer_gone()) return true;
         return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s();
     }
-    bool peer_gone() const {  // a rank that posted its pid and whose process has exited
+    bool peer_gone() {  // a rank that posted its pid and whose process has exited
+        const auto now = std::chrono::steady_clock::now();
         for (int r = 0; r < G_; ++r) {
-            const int64_t pid = ctl_->post[r].pid;
-            if (pid > 0 && kill((pid_t)pid, 0) != 0 && errno == ESRCH) return true;
+            if (r == rank_) continue;
+            const ShmRankPost &p = ctl_->post[r];
+            if (p.pid <= 0) continue;  // not joined yet
+            if (my_ns_ && p.pidns == my_ns_) {
+                if (kill((pid_t)p.pid, 0) != 0 && errno == ESRCH) return true;
+                continue;
+            }
+            const uint64_t b = p.beat.load(std::memory_order_relaxed);  // another pid namespace: the heartbeat
+            if (b != seen_[r].first) {
+                seen_[r] = {b, now};
+            } else if (std::chrono::duration<double>(now - seen_[r].second).count() > stale_beat_s()) {
+                return true;
+            }
         }
         return false;
     }
 
+public:
+    // test hook (tests/native/dist_selftest.cpp --foreign-pid): post a pid that does not exist here, under
+    // another pid namespace, as a rank of a container sharing the segment would
+    void pose_as_foreign() {
+        ctl_->post[rank_].pidns = my_ns_ + 1;
+        ctl_->post[rank_].pid = 0x7ffffff0;
+    }
+
+private:
+    uint64_t my_ns_ = 0;
+    std::vector<std::pair<uint64_t, std::chrono::steady_clock::time_point>> seen_;
+    std::thread hb_;
+    std::atomic<bool> stop_{false};
     int G_ = 0, rank_ = 0;
     uint64_t W_ = 0, S_ = 0;
     size_t hdr_ = 0, size_ = 0;

@@ -47,37 +47,56 @@ __device__ bool plausible(const uint8_t *d, uint64_t s, uint64_t n, int32_t n_re
 
 constexpr uint64_t kNone = ~0ull;
 
-// chunk c covers [p + c*CH, min(n, p + (c+1)*CH)); guess its first record start
-__global__ void k_rec_guess(const uint8_t *__restrict__ d, uint64_t p, uint64_t n, int32_t n_ref, uint64_t CH, uint64_t C,
-                            uint64_t *__restrict__ start) {
+// a 16-record plausibility chain starts at s (or the chain reaches the stream's end, at_end: n is it)
+__device__ bool chain_at(const uint8_t *d, uint64_t s, uint64_t n, bool at_end, int32_t n_ref) {
+    uint64_t q = s;
+    int k = 0;
+    for (; k < 16 && q < n && plausible(d, q, n, n_ref); ++k) q += 4 + rd32u(d + q);
+    return k == 16 || (at_end && q == n && k > 0);
+}
+
+// chunk c covers [p + c*CH, min(lim, p + (c+1)*CH)) (bytes readable up to n); guess its first record start
+__global__ void k_rec_guess(const uint8_t *__restrict__ d, uint64_t p, uint64_t lim, uint64_t n, bool at_end, int32_t n_ref,
+                            uint64_t CH, uint64_t C, uint64_t *__restrict__ start) {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
     if (c == 0) {
         start[0] = p;
         return;
     }
-    const uint64_t cut = p + c * CH, lim = min(n, cut + 20016);
-    for (uint64_t s = cut; s < lim; ++s) {
-        uint64_t q = s;
-        int k = 0;
-        for (; k < 16 && q < n && plausible(d, q, n, n_ref); ++k) q += 4 + rd32u(d + q);
-        if (k == 16 || (q == n && k > 0)) {
+    const uint64_t cut = p + c * CH, ls = min(n, cut + 20016);
+    for (uint64_t s = cut; s < ls; ++s)
+        if (chain_at(d, s, n, at_end, n_ref)) {
             start[c] = s;
             return;
         }
-    }
     start[c] = kNone;
+}
+
+// the first plausible record start in [0, lim): one workgroup, thread t tries t, t + 256, ...
+__global__ void __launch_bounds__(256) k_rec_guess_first(const uint8_t *__restrict__ d, uint64_t lim, uint64_t n, bool at_end,
+                                                         int32_t n_ref, unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long best;
+    if (threadIdx.x == 0) best = kNone;
+    __syncthreads();
+    for (uint64_t base = 0; base < lim; base += 256) {
+        const uint64_t s = base + threadIdx.x;
+        if (s < lim && s < best && chain_at(d, s, n, at_end, n_ref)) atomicMin(&best, (unsigned long long)s);
+        __syncthreads();
+        if (best != kNone) break;
+    }
+    if (threadIdx.x == 0) *out = best;
 }
 
 // walk chunk c from start[c] to the first record start at or past the chunk end; with out != NULL
 // also write the (absolute) offsets from pos[c], never at or past out[cap] (a stream that changed since
 // the counts in pos were made may hold more records: the caller then detects it and walks again)
-__global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t n, uint64_t CH, uint64_t C,
+__global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t lim, uint64_t n, uint64_t CH, uint64_t C,
                            const uint64_t *__restrict__ start, uint64_t *__restrict__ stop, uint64_t *__restrict__ count,
                            const uint64_t *__restrict__ pos, uint64_t *__restrict__ out, uint64_t cap) {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    const uint64_t end = min(n, p + (c + 1) * CH);
+    const uint64_t end = min(lim, p + (c + 1) * CH);
     uint64_t q = start[c], k = 0;
     if (q == kNone) {
         stop[c] = kNone;
@@ -98,8 +117,8 @@ __global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t n
 }
 
 // chunk c + 1 starts where chunk c's walk stopped; *st bit 0: a start moved, bit 1: a stop that is
-// invalid (or the last chunk's not at the end)
-__global__ void k_rec_join(const uint64_t *__restrict__ stop, uint64_t *__restrict__ start, uint64_t C, uint64_t n,
+// invalid (or the last chunk's short of the window's end)
+__global__ void k_rec_join(const uint64_t *__restrict__ stop, uint64_t *__restrict__ start, uint64_t C, uint64_t lim,
                            unsigned int *__restrict__ st) {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
@@ -113,7 +132,7 @@ __global__ void k_rec_join(const uint64_t *__restrict__ stop, uint64_t *__restri
             start[c + 1] = e;
             atomicOr(st, 1u);
         }
-    } else if (e != n) {
+    } else if (e < lim) {
         atomicOr(st, 2u);
     }
 }
@@ -147,7 +166,8 @@ constexpr int kIdxPos = 64;  // byte positions per thread (300M reads, 60 GB fil
 constexpr uint32_t kStash = 4;  // candidate slots per 256 * kIdxPos-position block in the counting pass
 
 template <bool EMIT>
-__global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z, uint64_t zbytes, uint32_t *__restrict__ cnt,
+__global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z, uint64_t zbytes, uint64_t plim,
+                                                   uint32_t *__restrict__ cnt,
                                                    const uint32_t *__restrict__ base, uint64_t *__restrict__ cpos,
                                                    uint32_t *__restrict__ cbs, uint64_t *__restrict__ stash_pos = nullptr,
                                                    uint32_t *__restrict__ stash_bs = nullptr,
@@ -156,7 +176,7 @@ __global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z
     const uint32_t t = threadIdx.x;
     const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + t) * kIdxPos;
     uint32_t mine = 0;
-    if (p0 < zbytes) {
+    if (p0 < plim) {
         // the thread's kIdxPos positions + 4 bytes of look-ahead in registers (16-byte loads + one dword):
         // only a position whose 4 bytes are the gzip/deflate/FEXTRA signature 1f 8b 08 04 goes on to
         // bgzf_head's global loads (a bare 0x1f byte every 256 stalled the wave on dependent loads)
@@ -177,7 +197,7 @@ __global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z
 #pragma unroll
         for (int k = 0; k < kIdxPos; ++k) {
             const uint32_t sig = (k & 3) ? __builtin_amdgcn_alignbyte(v[(k >> 2) + 1], v[k >> 2], k & 3) : v[k >> 2];
-            if (sig == 0x04088b1fu && p0 + k < zbytes && bgzf_head(z, zbytes, p0 + k)) ++mine;
+            if (sig == 0x04088b1fu && p0 + k < plim && bgzf_head(z, zbytes, p0 + k)) ++mine;
         }
     }
     // block-wide exclusive prefix of the per-thread counts
@@ -208,7 +228,7 @@ __global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z
             uint64_t o = (uint64_t)blockIdx.x * kStash + before + incl - mine;
             for (int k = 0; k < kIdxPos; ++k) {
                 const uint64_t p = p0 + k;
-                if (p >= zbytes || z[p] != 31) continue;
+                if (p >= plim || z[p] != 31) continue;
                 const uint32_t bs = bgzf_head(z, zbytes, p);
                 if (bs) stash_pos[o] = p, stash_bs[o] = bs, ++o;
             }
@@ -219,23 +239,31 @@ __global__ void __launch_bounds__(256) k_bgzf_cand(const uint8_t *__restrict__ z
     uint64_t o = base[blockIdx.x] + before + incl - mine;
     for (int k = 0; k < kIdxPos; ++k) {
         const uint64_t p = p0 + k;
-        if (p >= zbytes || z[p] != 31) continue;
+        if (p >= plim || z[p] != 31) continue;
         const uint32_t bs = bgzf_head(z, zbytes, p);
         if (bs) cpos[o] = p, cbs[o] = bs, ++o;
     }
 }
 
-// chain check + per-block fields; nonempty[i] = payload size > 0
-__global__ void k_bgzf_chain(const uint8_t *__restrict__ z, uint64_t zbytes, const uint64_t *__restrict__ cpos,
-                             const uint32_t *__restrict__ cbs, uint64_t m, uint32_t *__restrict__ bad,
-                             uint32_t *__restrict__ isz) {
+// chain check + per-block fields over the candidates at or past s (positions below s get isz 0 and
+// are left out): the first is s itself, every later one starts where its predecessor ends, and the
+// last ends at or past `own` (the end of the range whose block starts are indexed; for a whole file
+// own = zbytes, so the chain ends exactly at the end).  *xend = that end.
+__global__ void k_bgzf_chain(const uint8_t *__restrict__ z, uint64_t zbytes, uint64_t s, uint64_t own,
+                             const uint64_t *__restrict__ cpos, const uint32_t *__restrict__ cbs, uint64_t m,
+                             uint32_t *__restrict__ bad, uint32_t *__restrict__ isz, unsigned long long *__restrict__ xend) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     const uint64_t p = cpos[i], e = p + cbs[i];
-    const bool ok = (i == 0 ? p == 0 : cpos[i - 1] + cbs[i - 1] == p) && (i + 1 == m ? e == zbytes : true);
-    const uint32_t s = z[e - 4] | ((uint32_t)z[e - 3] << 8) | ((uint32_t)z[e - 2] << 16) | ((uint32_t)z[e - 1] << 24);
-    if (!ok || s > kSlot) atomicAdd(bad, 1u);
-    isz[i] = s;
+    if (p < s) {
+        isz[i] = 0;
+        return;
+    }
+    const bool ok = (p == s || (i > 0 && cpos[i - 1] >= s && cpos[i - 1] + cbs[i - 1] == p)) && (i + 1 == m ? e >= own : true);
+    if (i + 1 == m) atomicMax(xend, (unsigned long long)e);
+    const uint32_t sz = z[e - 4] | ((uint32_t)z[e - 3] << 8) | ((uint32_t)z[e - 2] << 16) | ((uint32_t)z[e - 1] << 24);
+    if (!ok || sz > kSlot) atomicAdd(bad, 1u);
+    isz[i] = sz;
 }
 
 __global__ void k_bgzf_fill(const uint8_t *__restrict__ z, const uint64_t *__restrict__ cpos, const uint32_t *__restrict__ cbs,
@@ -313,23 +341,25 @@ __global__ void k_bgzf_unstash(const uint32_t *__restrict__ cnt, const uint32_t 
     for (uint32_t j = 0; j < c; ++j) cpos[o + j] = stash_pos[b * kStash + j], cbs[o + j] = stash_bs[b * kStash + j];
 }
 
-int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzfIndex *ix) {
+int oge_bgzf_index_range_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t s, uint64_t own, OgeBgzfIndex *ix,
+                            uint64_t *s_used, uint64_t *xend) {
     hipSetDevice(ctx->device);
     ix->nblk = 0;
     ix->total = 0;
-    if (!zbytes) return OGE_OK;
+    if (own > zbytes || (s != kIndexFirst && s >= own)) return 2;
     if ((uintptr_t)d_z & 3) return 1;
     const uint64_t per_blk = 256ull * kIdxPos;
-    const uint64_t G = (zbytes + per_blk - 1) / per_blk;
+    const uint64_t G = (own + per_blk - 1) / per_blk;
+    if (!G) return 2;
     if (G > 0xffffffffull) return 1;
     uint32_t *cnt = (uint32_t *)ctx->ws("bix_cnt", (G + 1) * 4);
     uint32_t *base = (uint32_t *)ctx->ws("bix_base", (G + 1) * 4);
-    uint32_t *bad = (uint32_t *)ctx->ws("bix_bad", 16);
+    uint32_t *bad = (uint32_t *)ctx->ws("bix_bad", 32);
     uint64_t *stash_pos = (uint64_t *)ctx->ws("bix_stash_pos", G * kStash * 8);
     uint32_t *stash_bs = (uint32_t *)ctx->ws("bix_stash_bs", G * kStash * 4);
     if (!cnt || !base || !bad || !stash_pos || !stash_bs) return OGE_ERR_HIP;
-    OGE_HIP_TRY(ctx, hipMemsetAsync(bad + 1, 0, 4, ctx->stream));
-    k_bgzf_cand<false><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, cnt, nullptr, nullptr, nullptr, stash_pos, stash_bs,
+    OGE_HIP_TRY(ctx, hipMemsetAsync(bad, 0, 32, ctx->stream));
+    k_bgzf_cand<false><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, own, cnt, nullptr, nullptr, nullptr, stash_pos, stash_bs,
                                                               bad + 1);
     OGE_LAUNCH_CHECK(ctx);
     OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + G, 0, 4, ctx->stream));
@@ -340,29 +370,37 @@ int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzf
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&stash_ovf, bad + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     const uint64_t m = m32;
-    if (!m) return 1;
+    if (!m) return s == kIndexFirst ? 2 : 1;
     uint64_t *cpos = (uint64_t *)ctx->ws("bix_cpos", m * 8);
     uint32_t *cbs = (uint32_t *)ctx->ws("bix_cbs", m * 4);
     uint32_t *isz = (uint32_t *)ctx->ws("bix_isz", (m + 1) * 4);
     uint32_t *slot = (uint32_t *)ctx->ws("bix_slot", (m + 1) * 4);
     if (!cpos || !cbs || !isz || !slot) return OGE_ERR_HIP;
     if (stash_ovf)  // a block with more than kStash candidates: the second scan places them
-        k_bgzf_cand<true><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, cnt, base, cpos, cbs);
+        k_bgzf_cand<true><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, own, cnt, base, cpos, cbs);
     else
         k_bgzf_unstash<<<oge_ceil_div(G, 256), 256, 0, ctx->stream>>>(cnt, base, G, stash_pos, stash_bs, cpos, cbs);
     OGE_LAUNCH_CHECK(ctx);
-    OGE_HIP_TRY(ctx, hipMemsetAsync(bad, 0, 4, ctx->stream));
-    k_bgzf_chain<<<oge_ceil_div(m, 256), 256, 0, ctx->stream>>>(d_z, zbytes, cpos, cbs, m, bad, isz);
+    if (s == kIndexFirst) {  // the range's first candidate
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&s, cpos, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    if (s_used) *s_used = s;
+    unsigned long long *dx = (unsigned long long *)(bad + 4);
+    k_bgzf_chain<<<oge_ceil_div(m, 256), 256, 0, ctx->stream>>>(d_z, zbytes, s, own, cpos, cbs, m, bad, isz, dx);
     OGE_LAUNCH_CHECK(ctx);
     k_nonzero_u32<<<oge_ceil_div(m + 1, 256), 256, 0, ctx->stream>>>(isz, m, slot);
     OGE_LAUNCH_CHECK(ctx);
     rc = oge_exclusive_scan_u32(ctx, slot, slot, m + 1);
     if (rc) return rc;
     uint32_t hb[2] = {0, 0};
+    unsigned long long xe = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&hb[0], bad, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&hb[1], slot + m, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&xe, dx, 8, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (hb[0]) return 1;
+    if (xend) *xend = xe;
     const uint64_t nb = hb[1];
     uint64_t *ix64 = (uint64_t *)ctx->ws("bix_out", (3 * nb + 2) * 8);
     uint32_t *crc = (uint32_t *)ctx->ws("bix_crc", (nb + 1) * 4);
@@ -383,6 +421,14 @@ int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzf
     ix->nblk = nb;
     ix->total = total;
     return OGE_OK;
+}
+
+int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzfIndex *ix) {
+    ix->nblk = 0;
+    ix->total = 0;
+    if (!zbytes) return OGE_OK;
+    const int rc = oge_bgzf_index_range_ws(ctx, d_z, zbytes, 0, zbytes, ix, nullptr, nullptr);
+    return rc == 2 ? 1 : rc;  // no candidate at all: the host walk reports it
 }
 
 extern "C" int oge_bgzf_index_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t *d_d0, uint64_t *d_d1,
@@ -504,21 +550,35 @@ extern "C" int oge_bgzf_inflate(oge_ctx *ctx, const uint8_t *z, uint64_t zbytes,
     return OGE_OK;
 }
 
-extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream, uint64_t rec_base, uint64_t end, int32_t n_ref,
-                                          uint64_t *d_off, uint64_t cap, uint64_t *n_out) {
-    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
-    if (!n_out || rec_base > end || (end > rec_base && !d_stream)) return oge_fail(ctx, OGE_ERR_ARG, "bad argument");
+int oge_record_guess(oge_ctx *ctx, const uint8_t *d, uint64_t lim, uint64_t bufend, bool at_end, int32_t n_ref, uint64_t *out) {
+    *out = kNone;
+    if (!lim) return OGE_OK;
+    unsigned long long *w = (unsigned long long *)ctx->ws("rec_guess", 16);
+    if (!w) return OGE_ERR_HIP;
+    k_rec_guess_first<<<1, 256, 0, ctx->stream>>>(d, std::min<uint64_t>(lim, 20016), bufend, at_end, n_ref, w);
+    OGE_LAUNCH_CHECK(ctx);
+    unsigned long long h = kNone;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&h, w, 8, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *out = h;
+    return OGE_OK;
+}
+
+int oge_record_walk(oge_ctx *ctx, const uint8_t *d_stream, uint64_t rec_base, uint64_t limit, uint64_t end, bool at_end,
+                    int32_t n_ref, uint64_t *d_off, uint64_t cap, uint64_t *n_out, uint64_t *exit) {
+    if (!n_out || rec_base > limit || limit > end || (end > rec_base && !d_stream)) return oge_fail(ctx, OGE_ERR_ARG, "bad argument");
     hipSetDevice(ctx->device);
     *n_out = 0;
+    *exit = rec_base;
     const uint64_t CH = 1ull << 16;
-    const uint64_t C = std::max<uint64_t>(1, (end - rec_base + CH - 1) / CH);
+    const uint64_t C = std::max<uint64_t>(1, (limit - rec_base + CH - 1) / CH);
     uint64_t *ws = (uint64_t *)ctx->ws("rec_walk", (5 * C + 4) * 8 + 64);
     if (!ws) return OGE_ERR_HIP;
     // start[C], stop[C], count[C + 1], pos[C + 1], pos2[C + 1], st
     uint64_t *start = ws, *stop = ws + C, *count = ws + 2 * C, *pos = ws + 3 * C + 1, *pos2 = ws + 4 * C + 2;
     unsigned int *st = (unsigned int *)(ws + 5 * C + 3);
-    if (end == rec_base) {
-        if (d_off && cap >= 1) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off, &end, 8, hipMemcpyHostToDevice, ctx->stream));
+    if (limit == rec_base) {
+        if (d_off && cap >= 1) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off, &rec_base, 8, hipMemcpyHostToDevice, ctx->stream));
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         return OGE_OK;
     }
@@ -526,45 +586,48 @@ extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream,
     // one walk + join pass: *st bit 0 = a start moved, bit 1 = an invalid or unjoined stop
     auto walk_join = [&](uint64_t *pos_arg, uint64_t *out, unsigned int *h) -> int {
         OGE_HIP_TRY(ctx, hipMemsetAsync(st, 0, 4, ctx->stream));
-        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos_arg, out, cap);
+        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, limit, end, CH, C, start, stop, count, pos_arg, out, cap);
         OGE_LAUNCH_CHECK(ctx);
-        k_rec_join<<<G, TB, 0, ctx->stream>>>(stop, start, C, end, st);
+        k_rec_join<<<G, TB, 0, ctx->stream>>>(stop, start, C, limit, st);
         OGE_LAUNCH_CHECK(ctx);
         OGE_HIP_TRY(ctx, hipMemcpyAsync(h, st, 4, hipMemcpyDeviceToHost, ctx->stream));
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         return OGE_OK;
     };
-    // n = the sum of the chunk counts, pos = their exclusive scan
-    auto scan_counts = [&](uint64_t *dst, uint64_t *n) -> int {
+    // n = the sum of the chunk counts, pos = their exclusive scan; *x = the last chunk's stop
+    auto scan_counts = [&](uint64_t *dst, uint64_t *n, uint64_t *x) -> int {
         OGE_HIP_TRY(ctx, hipMemsetAsync(count + C, 0, 8, ctx->stream));  // count[C] = 0 (pos[C] = total)
         int rc = oge_exclusive_scan_u64(ctx, count, dst, C + 1);
         if (rc) return rc;
         OGE_HIP_TRY(ctx, hipMemcpyAsync(n, dst + C, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(x, stop + C - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         return OGE_OK;
     };
     auto &RW = ctx->recwalk;
-    if (d_off && RW.stream == d_stream && RW.base == rec_base && RW.end == end && RW.n_ref == n_ref && RW.C == C) {
+    if (d_off && RW.stream == d_stream && RW.base == rec_base && RW.limit == limit && RW.end == end && RW.n_ref == n_ref &&
+        RW.C == C) {
         // the count-only call on this stream converged just before: fill from its chunk starts and
         // offsets (still in the workspace), then check the walk joined and counted the same
         const uint64_t n = RW.n;
         RW.stream = nullptr;
         if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
         unsigned int h = 0;
-        uint64_t n2 = 0;
+        uint64_t n2 = 0, x = 0;
         int rc = walk_join(pos, d_off, &h);
         if (rc) return rc;
-        if (!h && !(rc = scan_counts(pos2, &n2)) && n2 == n) {
-            OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &end, 8, hipMemcpyHostToDevice, ctx->stream));
+        if (!h && !(rc = scan_counts(pos2, &n2, &x)) && n2 == n) {
+            OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &x, 8, hipMemcpyHostToDevice, ctx->stream));
             OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
             *n_out = n;
+            *exit = x;
             return OGE_OK;
         }
         if (rc) return rc;
         // the stream changed between the calls: the full walk below
     }
     RW.stream = nullptr;
-    k_rec_guess<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, n_ref, CH, C, start);
+    k_rec_guess<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, limit, end, at_end, n_ref, CH, C, start);
     OGE_LAUNCH_CHECK(ctx);
     // walk, then every chunk starts where its predecessor's walk stopped (k_rec_join), until no start
     // moves: the chain from chunk 0 then equals the sequential walk
@@ -576,18 +639,27 @@ extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream,
         if (it > 64) return oge_fail(ctx, OGE_ERR_IO, "BAM record walk did not converge (corrupt stream?)");
     }
     if (h) return oge_fail(ctx, OGE_ERR_IO, "Invalid BAM record (block size out of range or record past the end of the stream)");
-    uint64_t n = 0;
-    int rc = scan_counts(pos, &n);
+    uint64_t n = 0, x = 0;
+    int rc = scan_counts(pos, &n, &x);
     if (rc) return rc;
     *n_out = n;
+    *exit = x;
     if (!d_off) {
-        RW.stream = d_stream, RW.base = rec_base, RW.end = end, RW.n_ref = n_ref, RW.n = n, RW.C = C;
+        RW.stream = d_stream, RW.base = rec_base, RW.limit = limit, RW.end = end, RW.n_ref = n_ref, RW.n = n, RW.C = C;
         return OGE_OK;
     }
     if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
-    k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, end, CH, C, start, stop, count, pos, d_off, cap);
+    k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, limit, end, CH, C, start, stop, count, pos, d_off, cap);
     OGE_LAUNCH_CHECK(ctx);
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &end, 8, hipMemcpyHostToDevice, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &x, 8, hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return OGE_OK;
+}
+
+extern "C" int oge_bam_record_offsets_dev(oge_ctx *ctx, const uint8_t *d_stream, uint64_t rec_base, uint64_t end, int32_t n_ref,
+                                          uint64_t *d_off, uint64_t cap, uint64_t *n_out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if (!n_out || rec_base > end || (end > rec_base && !d_stream)) return oge_fail(ctx, OGE_ERR_ARG, "bad argument");
+    uint64_t x = 0;
+    return oge_record_walk(ctx, d_stream, rec_base, end, end, true, n_ref, d_off, cap, n_out, &x);
 }

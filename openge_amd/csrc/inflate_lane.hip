@@ -1075,12 +1075,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
 int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d0, const uint64_t *d1,
                       const uint64_t *uoff, const uint32_t *crc, uint64_t nblk, uint8_t *out, uint32_t *err,
                       const uint32_t *zpow) {
-    static int ncu = [] {
-        int d = 0, n = 0;
-        (void)hipGetDevice(&d);
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
-        return n > 0 ? n : 256;
-    }();
+    const int ncu = ctx->cu_count();
     // persistent lanes (the 12 resident waves per CU) take blocks from a queue; a chunk is at most
     // kChunkLanes blocks per lane, and no more than a quarter of the free device memory holds bitmaps and
     // lists for (17.3 KiB per block), at least one block per lane.  With kStreams > 1, chunks alternate

@@ -119,12 +119,13 @@ void ChainContext::close_ranks() {
 // thread each).  A rank whose own preparation failed still joins the collectives with an empty shard
 // so the others finish, and the failure is reported.
 int run_ranks(ChainContext &cc, ReadBatch &b, bool sort, const oge_markdup_opts *opts, uint64_t *n_dup) {
-    if (cc.init_ranks() || cc.to_device(b)) return -1;
+    const bool sharded = !b.shards.empty();  // the reader left every rank its own input shard
+    if (cc.init_ranks() || (!sharded && cc.to_device(b))) return -1;
     const int G = cc.gpus;
     const uint64_t n = b.n;
     const int32_t n_ref = (int32_t)b.ref_names.size();
     std::vector<uint64_t> cut(G + 1), boff(G + 1);
-    for (int g = 0; g <= G; ++g) {
+    for (int g = 0; g <= G && !sharded; ++g) {
         cut[g] = n * (uint64_t)g / (uint64_t)G;
         if (oge_memcpy(cc.ctx, &boff[g], b.d_offs + cut[g], 8, 2)) return cc.fail("device->host copy");
     }
@@ -136,6 +137,16 @@ int run_ranks(ChainContext &cc, ReadBatch &b, bool sort, const oge_markdup_opts 
     for (int g = 0; g < G; ++g)
         ts.emplace_back([&, g]() {
             oge_ctx *c = cc.rank_ctx[g];
+            uint8_t *dout = nullptr;
+            uint64_t *doff = nullptr, no = 0, nd = 0;
+            if (sharded) {  // the rank's own shard, in its HBM already
+                const ReadBatch::Slice &s = b.shards[g];
+                rcs[g] = oge_sort_markdup_dist(cc.comms[g], s.d_recs, s.d_offs, s.n, n_ref, sort ? 1 : 0, opts, &dout, &doff, &no, &nd);
+                if (rcs[g]) why[g] = oge_last_error(c);
+                sl[g] = {c, dout, doff, no};
+                nds[g] = nd;
+                return;
+            }
             const uint64_t lo = cut[g], m = cut[g + 1] - lo, bytes = boff[g + 1] - boff[g];
             void *r = nullptr, *o = nullptr;
             int rc = oge_dev_alloc(c, bytes + 64, &r);
@@ -143,8 +154,6 @@ int run_ranks(ChainContext &cc, ReadBatch &b, bool sort, const oge_markdup_opts 
             if (!rc && bytes) rc = oge_memcpy(c, r, b.d_recs + boff[g], bytes, 4);
             if (!rc) rc = oge_memcpy(c, o, b.d_offs + lo, (m + 1) * 8, 4);
             if (rc) why[g] = oge_last_error(c);
-            uint8_t *dout = nullptr;
-            uint64_t *doff = nullptr, no = 0, nd = 0;
             // the offsets stay absolute: the records pointer is shifted back by the range's first one
             const int rd = rc ? oge_sort_markdup_dist(cc.comms[g], nullptr, nullptr, 0, n_ref, sort ? 1 : 0, opts, &dout, &doff, &no, &nd)
                               : oge_sort_markdup_dist(cc.comms[g], (const uint8_t *)r - boff[g], (const uint64_t *)o, m, n_ref,
@@ -163,6 +172,7 @@ int run_ranks(ChainContext &cc, ReadBatch &b, bool sort, const oge_markdup_opts 
             return -1;
         }
     cc.free_device(b);
+    b.shards.clear();
     b.slices = sl;
     b.n = 0;
     for (auto &x : sl) b.n += x.n;
@@ -401,10 +411,152 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
     return 0;
 }
 
+// Bytes [off, off + len) of the open file into device memory dst (rank ctx's stream): parallel preads
+// into one of two page-locked buffers while the other is copied.  0 = ok.
+static int read_range_to_device(oge_ctx *ctx, int fd, uint64_t off, uint64_t len, uint8_t *dst) {
+    if (!len) return 0;
+    const uint64_t CH = std::min<uint64_t>(len, 128ull << 20);
+    void *hb[2] = {nullptr, nullptr};
+    if (oge_host_alloc(ctx, CH, &hb[0]) || oge_host_alloc(ctx, CH, &hb[1])) {
+        for (void *h : hb)
+            if (h) oge_host_free(ctx, h);
+        return -1;
+    }
+    std::atomic<bool> bad(false);
+    const uint64_t nch = (len + CH - 1) / CH;
+    auto read_chunk = [&](uint64_t c) {
+        const uint64_t o0 = c * CH, e0 = std::min(len, o0 + CH), sl = 16ull << 20, ns = (e0 - o0 + sl - 1) / sl;
+        std::vector<std::thread> ts;
+        for (uint64_t k = 0; k < ns; ++k)
+            ts.emplace_back([&, k]() {
+                uint64_t o = o0 + k * sl;
+                const uint64_t e = std::min(e0, o + sl);
+                while (o < e) {
+                    const ssize_t r = pread(fd, (uint8_t *)hb[c & 1] + (o - o0), e - o, (off_t)(off + o));
+                    if (r <= 0) {
+                        bad = true;
+                        return;
+                    }
+                    o += (uint64_t)r;
+                }
+            });
+        for (auto &t : ts) t.join();
+    };
+    read_chunk(0);
+    for (uint64_t c = 0; c < nch && !bad; ++c) {
+        std::thread next;
+        if (c + 1 < nch) next = std::thread(read_chunk, c + 1);
+        const uint64_t o = c * CH, l = std::min(len, o + CH) - o;
+        if (oge_memcpy(ctx, dst + o, hb[c & 1], l, 1)) bad = true;
+        if (next.joinable()) next.join();
+    }
+    for (void *h : hb) oge_host_free(ctx, h);
+    return bad ? -1 : 0;
+}
+
+// True when the next module takes per-rank input shards (run_ranks: the coordinate ReadSorter, or a
+// standalone MarkDuplicates).
+bool FileReader::sink_takes_shards() const {
+    if (auto *rs = dynamic_cast<const ReadSorter *>(sink_)) return rs->sortBy() == BamHeaderModel::COORDINATE;
+    return dynamic_cast<const MarkDuplicates *>(sink_) != nullptr;
+}
+
+// --gpus G with one input file (config 4): rank g reads the file's bytes [a_g, min(size, b_g + 64 KiB))
+// into its own HBM and decodes the BGZF blocks that start in [a_g, b_g) (oge_bgzf_decode_shard: block and
+// record boundaries joined with the neighbouring ranks), so the G ranks share the codec instead of rank 0
+// inflating the whole file.  Returns 1 when the file cannot be opened or decoded this way (the
+// whole-file readers take over and report it).
+int FileReader::read_sharded(ChainContext &cc, ReadBatch &b, const std::string &path) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int fd = open(path.c_str(), O_RDONLY);
+    struct stat stt;
+    if (fd < 0) return 1;
+    if (fstat(fd, &stt) || !S_ISREG(stt.st_mode)) {
+        close(fd);
+        return 1;
+    }
+    if (cc.init_ranks()) {
+        close(fd);
+        return -1;
+    }
+    const int G = cc.gpus;
+    const uint64_t Z = (uint64_t)stt.st_size;
+    std::vector<ReadBatch::Slice> sh(G);
+    std::vector<int> rcs(G, 0);
+    std::vector<std::string> why(G);
+    std::vector<uint8_t> hdr(1 << 22);
+    uint64_t hlen = 0;
+    std::vector<double> t_read(G, 0), t_dec(G, 0);
+    std::vector<std::thread> ts;
+    for (int g = 0; g < G; ++g)
+        ts.emplace_back([&, g]() {
+            oge_ctx *c = cc.rank_ctx[g];
+            const uint64_t a = Z * (uint64_t)g / (uint64_t)G, bnd = Z * (uint64_t)(g + 1) / (uint64_t)G;
+            const uint64_t end = std::min<uint64_t>(Z, bnd + 65536), len = end - a;
+            void *dz = nullptr;
+            const auto r0 = std::chrono::steady_clock::now();
+            int rc = oge_dev_alloc(c, len + 64, &dz);
+            if (!rc && read_range_to_device(c, fd, a, len, (uint8_t *)dz)) rc = OGE_ERR_IO;
+            if (rc) why[g] = rc == OGE_ERR_IO ? std::string("read failed") : std::string(oge_last_error(c));
+            const auto r1 = std::chrono::steady_clock::now();
+            const uint8_t *recs = nullptr;
+            const uint64_t *offs = nullptr;
+            uint64_t n = 0, hl = 0;
+            // a rank whose read failed still takes part, with no buffer: its argument error fails every rank
+            const int rd = oge_bgzf_decode_shard(cc.comms[g], rc ? nullptr : (const uint8_t *)dz, len, bnd - a, &recs, &offs, &n,
+                                                 g == 0 ? hdr.data() : nullptr, g == 0 ? hdr.size() : 0, g == 0 ? &hl : nullptr);
+            if (!rc && rd) why[g] = oge_last_error(c);
+            rcs[g] = rc ? rc : rd;
+            if (g == 0) hlen = hl;
+            if (dz) oge_dev_free(c, dz);
+            sh[g] = {c, const_cast<uint8_t *>(recs), const_cast<uint64_t *>(offs), n};
+            t_read[g] = std::chrono::duration<double>(r1 - r0).count();
+            t_dec[g] = std::chrono::duration<double>(std::chrono::steady_clock::now() - r1).count();
+        });
+    for (auto &t : ts) t.join();
+    close(fd);
+    // a file the sharded decode rejects goes to the whole-file readers, which report format errors with
+    // the reference's messages (the ranks failed together, so their communicators are still in step)
+    for (int g = 0; g < G; ++g)
+        if (rcs[g]) {
+            if (verbose_) fprintf(stderr, "[openge] FileReader: sharded decode failed on rank %d (%s); reading the whole file\n", g, why[g].c_str());
+            return 1;
+        }
+    BamFile f;
+    std::string err;
+    size_t rec_base = 0;
+    if (!bam_parse_header(hdr.data(), hlen, f, err, &rec_base)) return 1;
+    b.header = f.header;
+    b.ref_names = f.ref_names;
+    b.shards = sh;
+    b.n = 0;
+    for (auto &s : sh) b.n += s.n;
+    b.dev_valid = b.host_valid = false;
+    if (verbose_) {
+        std::string per;
+        for (int g = 0; g < G; ++g) {
+            uint64_t nb = 0;
+            oge_ctx_counter(cc.rank_ctx[g], "shard_blocks", &nb);
+            char tmp[160];
+            snprintf(tmp, sizeof tmp, " [rank %d: read %.3f s, decode %.3f s, %llu blocks, %llu records]", g, t_read[g], t_dec[g],
+                     (unsigned long long)nb, (unsigned long long)sh[g].n);
+            per += tmp;
+        }
+        fprintf(stderr, "[openge] FileReader (sharded over %d ranks): %.3f s%s\n", G,
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), per.c_str());
+    }
+    return 0;
+}
+
 int FileReader::runInternal(ChainContext &cc, ReadBatch &b) {
     if (files_.empty()) files_.push_back("stdin");
     std::vector<uint64_t> file_end;  // record count after each file
     const char *rd = getenv("OGE_READER");
+    if (cc.gpus > 1 && files_.size() == 1 && files_[0] != "stdin" && files_[0] != "-" && sink_takes_shards() &&
+        !(rd && (std::string(rd) == "host" || std::string(rd) == "whole"))) {
+        const int r = read_sharded(cc, b, files_[0]);
+        if (r <= 0) return r;  // 1: the host reader reports why the file cannot be read
+    }
     if (files_.size() == 1 && files_[0] != "stdin" && files_[0] != "-" && !(rd && std::string(rd) == "host")) {
         const int r = read_device(cc, b, files_[0]);
         if (r <= 0) return r;  // 1: fall through to the host reader (it reports format errors)

@@ -45,6 +45,10 @@ struct ReadBatch {
         uint64_t n;
     };
     std::vector<Slice> slices;
+    // multi-GPU input (--gpus G, one BAM file): the records as G input shards in rank order (contiguous
+    // ranges of the file's records, each decoded by its rank from its own byte range of the file,
+    // oge_bgzf_decode_shard), owned by the ranks' contexts; run_ranks takes them as they are
+    std::vector<Slice> shards;
     // inputs larger than HBM: the output is produced range by range when the writer asks for it
     // (oge_sort_markdup_chunked); each range is handed to `sink` in output order
     using RangeSink = std::function<int(const uint8_t *d_recs, const uint64_t *d_offs, uint64_t n)>;
@@ -109,6 +113,9 @@ protected:
     // One BGZF file straight into HBM: inflate + record walk on the GPU (returns 1 when the host
     // reader should take over, e.g. to report a format error with the reference's message).
     int read_device(ChainContext &cc, ReadBatch &b, const std::string &path);
+    // --gpus G: every rank reads and decodes its own byte range of the one input file (b.shards)
+    int read_sharded(ChainContext &cc, ReadBatch &b, const std::string &path);
+    bool sink_takes_shards() const;
     bool sink_sorts() const;
     static int merge_inputs(ReadBatch &b, const std::vector<uint64_t> &file_end, int threads);
     std::vector<std::string> files_;

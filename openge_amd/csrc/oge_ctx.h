@@ -31,6 +31,15 @@ struct oge_ctx {
     bool pool = false;  // allocate from the device's stream-ordered pool and keep freed memory in it
     hipStream_t side[4] = {nullptr, nullptr, nullptr, nullptr};  // extra streams a stage pipelines over
     hipStream_t side_stream(int i);
+    int ncu = 0;  // compute units of `device` (persistent grids), looked up once per context
+    int cu_count() {
+        if (!ncu) {
+            int c = 0;
+            (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, device);
+            ncu = c > 0 ? c : 256;
+        }
+        return ncu;
+    }
     void *alloc(size_t bytes);
     void release(void *p);
     // the last count-only oge_bam_record_offsets_dev call: its converged chunk starts and offsets stay
@@ -38,9 +47,10 @@ struct oge_ctx {
     // straight to the fill walk, which is checked to join and count the same
     struct RecWalk {
         const void *stream = nullptr;
-        uint64_t base = 0, end = 0, n = 0, C = 0;
+        uint64_t base = 0, limit = 0, end = 0, n = 0, C = 0;
         int32_t n_ref = 0;
     } recwalk;
+    std::map<std::string, uint64_t> counters;  // per call: work counts a stage reports (oge_ctx_counter)
     bool last_scan_generic = false;  // realign scan fell back to the byte-wise kernel
     double scan_t[3] = {0, 0, 0};    // realign scan host timings: validate, upload, device + download
 
@@ -103,6 +113,21 @@ struct OgeBgzfIndex {
 };
 // 0 = ok, 1 = candidates are not an exact block chain (use the host walk), < 0 = error
 int oge_bgzf_index_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, OgeBgzfIndex *ix);
+// The blocks that start in [s, own) of d_z (zbytes >= own bytes readable: the last block may end past
+// own): s = kIndexFirst takes the range's first candidate (*s_used), else s must be a candidate; the
+// chain must be exact from s to its last block, whose end (>= own) goes to *xend.  0 = ok, 1 = not an
+// exact chain, 2 = no candidate in the range (or s >= own: no block), < 0 = error.
+constexpr uint64_t kIndexFirst = ~0ull;
+int oge_bgzf_index_range_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t s, uint64_t own, OgeBgzfIndex *ix,
+                            uint64_t *s_used, uint64_t *xend);
+// The record walk of oge_bam_record_offsets_dev generalised to a window: records that start in
+// [start, limit) of d (bytes readable up to bufend, so the last record may end past limit); at_end says
+// bufend is the end of the stream (a guess chain may stop there).  *exit = the end of the last record
+// (= the first record start at or past limit); d_off (cap >= n + 1) gets the offsets and d_off[n] = *exit.
+int oge_record_walk(oge_ctx *ctx, const uint8_t *d, uint64_t start, uint64_t limit, uint64_t bufend, bool at_end, int32_t n_ref,
+                    uint64_t *d_off, uint64_t cap, uint64_t *n_out, uint64_t *exit);
+// The first plausible record start in [0, lim) of d (bufend readable) as k_rec_guess judges it, or ~0.
+int oge_record_guess(oge_ctx *ctx, const uint8_t *d, uint64_t lim, uint64_t bufend, bool at_end, int32_t n_ref, uint64_t *out);
 // lane-per-block BGZF inflate (inflate_lane.hip); err/zpow as in oge_bgzf_inflate_dev
 int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d0, const uint64_t *d1,
                       const uint64_t *uoff, const uint32_t *crc, uint64_t nblk, uint8_t *out, uint32_t *err,
@@ -112,3 +137,13 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
 oge_ctx *oge_comm_ctx(oge_comm *comm);
 // in place: v[0..count) = the sum over the communicator's ranks (collective, host values)
 int oge_comm_sum_u64(oge_comm *comm, uint64_t *v, int count);
+// host allgather (every rank `bytes` bytes, out = G * bytes in rank order) and the device all-to-all-v,
+// recorded under `tag` in the communicator's exchange statistics
+int oge_comm_allgather(oge_comm *comm, const char *tag, const void *in, void *out, size_t bytes);
+int oge_comm_alltoallv_dev(oge_comm *comm, const char *tag, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
+                           const uint64_t *rbytes, const uint64_t *roff);
+void oge_comm_reset_stats(oge_comm *comm);
+// shard.hip: this rank's records of one BGZF BAM file decoded by byte range (see oge_bgzf_decode_shard);
+// *X / *xoff are workspace ("pipe_x", "pipe_xoff"), *header the raw BAM header bytes.  Collective.
+int oge_decode_shard(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, uint64_t own, uint8_t **X, uint64_t **xoff, uint64_t *n,
+                     std::vector<uint8_t> *header);

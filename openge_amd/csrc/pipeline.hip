@@ -17,7 +17,8 @@
 //   write    header block (host) + oge_bgzf_deflate_dev + EOF block into the free buffer
 //
 // oge_mergesort_bgzf_dist runs the same chain over G ranks (one input file per rank, the sort and
-// dedup through oge_sort_markdup_dist, every rank deflating its own output slice).
+// dedup through oge_sort_markdup_dist, every rank deflating its own output slice);
+// oge_mergesort_bgzf_shard does it for ONE input file whose byte ranges the ranks decode (shard.hip).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -229,27 +230,15 @@ extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t
     return OGE_OK;
 }
 
-// The same chain over G ranks: rank g's input is its own BAM file (mergesort's inputs, one per rank;
-// the header of rank 0's file is the output's, as MultiReader takes the first file's), the records
-// meet in oge_sort_markdup_dist, and rank g's output is its slice of the one output file: rank 0's
+// The sort + dedup + write half of the multi-rank chains: this rank's decoded records (its input
+// shard; a rank whose decode failed passes rc != 0 and still joins the collectives with no records,
+// then reports its error) through oge_sort_markdup_dist, then its slice of the one output file: rank 0's
 // starts with the header, the last rank's ends with the EOF block, so the slices concatenate.
-extern "C" int oge_mergesort_bgzf_dist(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *mo,
-                                       const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads_total, uint64_t *n_dup_total) {
-    if (!comm) return oge_fail(nullptr, OGE_ERR_ARG, "null communicator");
+static int dist_sort_write(oge_comm *comm, int rc, const std::string &why, uint8_t *X, uint64_t *xoff, uint64_t n, const BamFile &f,
+                           const oge_mergesort_opts *mo, const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads_total,
+                           uint64_t *n_dup_total) {
     oge_ctx *ctx = oge_comm_ctx(comm);
-    if (!mo || !d_out || !out_bytes || (zbytes && !d_z)) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
-    if (mo->level < 0 || mo->level > 9) return oge_fail(ctx, OGE_ERR_ARG, "level must be 0..9");
-    (void)hipSetDevice(ctx->device);
-    Hold hold(ctx);
-    *d_out = nullptr;
-    *out_bytes = 0;
     const int rank = oge_comm_rank(comm), G = oge_comm_size(comm);
-    uint8_t *X = nullptr;
-    uint64_t cap = 0, *xoff = nullptr, n = 0;
-    BamFile f;
-    // a rank whose decode fails still joins the collectives (with no records), and reports its error
-    int rc = decode(ctx, d_z, zbytes, &X, &cap, &xoff, &n, &f);
-    std::string why = rc ? ctx->err : std::string();
     const int32_t n_ref = (int32_t)f.ref_names.size();
     LibTable lt(f.header, n_ref, mo);
     uint8_t *dout = nullptr;
@@ -261,9 +250,9 @@ extern "C" int oge_mergesort_bgzf_dist(oge_comm *comm, const uint8_t *d_z, uint6
     const uint8_t *src = dout;
     const uint64_t *soff = doff;
     uint64_t m = no;
-    uint8_t *Y = (uint8_t *)ctx->ws("pipe_y", std::max<uint64_t>(cap, 64));
+    uint8_t *Y = nullptr;
     uint64_t *yoff = (uint64_t *)ctx->ws("pipe_yoff", (no + 1) * 8);
-    if (!Y || !yoff) return OGE_ERR_HIP;
+    if (!yoff) return OGE_ERR_HIP;
     if (mo->mark_duplicates && mo->remove_duplicates) {
         uint64_t bytes = 0;
         if (no) {
@@ -301,4 +290,53 @@ extern "C" int oge_mergesort_bgzf_dist(oge_comm *comm, const uint8_t *d_z, uint6
     if (n_reads_total) *n_reads_total = tot;
     if (n_dup_total) *n_dup_total = nd;
     return OGE_OK;
+}
+
+static int dist_args(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *mo, const uint8_t **d_out,
+                     uint64_t *out_bytes) {
+    if (!comm) return oge_fail(nullptr, OGE_ERR_ARG, "null communicator");
+    oge_ctx *ctx = oge_comm_ctx(comm);
+    if (!mo || !d_out || !out_bytes || (zbytes && !d_z)) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    if (mo->level < 0 || mo->level > 9) return oge_fail(ctx, OGE_ERR_ARG, "level must be 0..9");
+    (void)hipSetDevice(ctx->device);
+    *d_out = nullptr;
+    *out_bytes = 0;
+    return OGE_OK;
+}
+
+// The same chain over G ranks: rank g's input is its own BAM file (mergesort's inputs, one per rank;
+// the header of rank 0's file is the output's, as MultiReader takes the first file's).
+extern "C" int oge_mergesort_bgzf_dist(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *mo,
+                                       const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads_total, uint64_t *n_dup_total) {
+    if (const int rc = dist_args(comm, d_z, zbytes, mo, d_out, out_bytes)) return rc;
+    oge_ctx *ctx = oge_comm_ctx(comm);
+    Hold hold(ctx);
+    oge_comm_reset_stats(comm);
+    uint8_t *X = nullptr;
+    uint64_t cap = 0, *xoff = nullptr, n = 0;
+    BamFile f;
+    // a rank whose decode fails still joins the collectives (with no records), and reports its error
+    const int rc = decode(ctx, d_z, zbytes, &X, &cap, &xoff, &n, &f);
+    return dist_sort_write(comm, rc, rc ? ctx->err : std::string(), X, xoff, n, f, mo, d_out, out_bytes, n_reads_total, n_dup_total);
+}
+
+// ONE input file over G ranks (config 4): rank g holds the file's bytes from a_g on and decodes the
+// blocks that start in its own_bytes (shard.hip), then the same sort + dedup + write half.
+extern "C" int oge_mergesort_bgzf_shard(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, uint64_t own_bytes,
+                                        const oge_mergesort_opts *mo, const uint8_t **d_out, uint64_t *out_bytes,
+                                        uint64_t *n_reads_total, uint64_t *n_dup_total) {
+    if (const int rc = dist_args(comm, d_z, zbytes, mo, d_out, out_bytes)) return rc;
+    oge_ctx *ctx = oge_comm_ctx(comm);
+    Hold hold(ctx);
+    oge_comm_reset_stats(comm);
+    uint8_t *X = nullptr;
+    uint64_t *xoff = nullptr, n = 0;
+    std::vector<uint8_t> h;
+    int rc = oge_decode_shard(comm, d_z, zbytes, own_bytes, &X, &xoff, &n, &h);
+    if (rc) return rc;  // collective: every rank failed together
+    BamFile f;
+    std::string err;
+    size_t rec_base = 0;
+    if (!bam_parse_header(h.data(), h.size(), f, err, &rec_base)) return oge_fail(ctx, OGE_ERR_IO, ("BAM header: " + err).c_str());
+    return dist_sort_write(comm, OGE_OK, std::string(), X, xoff, n, f, mo, d_out, out_bytes, n_reads_total, n_dup_total);
 }

@@ -186,6 +186,7 @@ def lib() -> C.CDLL:
         "oge_ctx_destroy": (None, [vp]),
         "oge_last_error": (C.c_char_p, [vp]),
         "oge_ctx_timing": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_double)]),
+        "oge_ctx_counter": (C.c_int, [vp, C.c_char_p, C.POINTER(u64)]),
         "oge_version": (C.c_char_p, []),
         "oge_sort_coord": (C.c_int, [vp, vp, u64, vp, u64, i32, vp]),
         "oge_sort_coord_dev": (C.c_int, [vp, vp, vp, u64, i32, vp]),
@@ -228,6 +229,10 @@ def lib() -> C.CDLL:
         "oge_mergesort_bgzf_dist": (C.c_int, [vp, vp, u64, vp, C.POINTER(vp), C.POINTER(u64), C.POINTER(u64),
                                               C.POINTER(u64)]),
         "oge_sort_markdup_dist": (C.c_int, [vp, vp, vp, u64, i32, C.c_int, vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64),
+                                            C.POINTER(u64)]),
+        "oge_mergesort_bgzf_shard": (C.c_int, [vp, vp, u64, u64, vp, C.POINTER(vp), C.POINTER(u64), C.POINTER(u64),
+                                               C.POINTER(u64)]),
+        "oge_bgzf_decode_shard": (C.c_int, [vp, vp, u64, u64, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64), vp, u64,
                                             C.POINTER(u64)]),
         "oge_synth_offsets_range_dev": (C.c_int, [vp, vp, u64, u64, vp]),
         "oge_synth_records_range_dev": (C.c_int, [vp, vp, u64, u64, vp, vp]),
@@ -441,6 +446,11 @@ class Context:
     def sync(self):
         check(lib().oge_ctx_sync(self.h), self.h)
 
+    def counter(self, name: str) -> int | None:
+        """A work count of the last pipeline call (oge_ctx_counter), None when it recorded none."""
+        v = C.c_uint64()
+        return v.value if lib().oge_ctx_counter(self.h, name.encode(), C.byref(v)) == 0 else None
+
     def timing(self, stage: str) -> float:
         ms = C.c_double()
         check(lib().oge_ctx_timing(self.h, stage.encode(), C.byref(ms)), self.h)
@@ -650,6 +660,26 @@ class Comm:
                                             C.byref(nd)), self.ctx.h)
         return d.value or 0, ob.value, nr.value, nd.value
 
+    def mergesort_bgzf_shard(self, d_z: int, zbytes: int, own_bytes: int, opts: "MergesortOpts"):
+        """ONE input file over the ranks: this rank holds the file's bytes from a_g on (a_g = the earlier
+        ranks' own_bytes summed) and decodes the blocks that start in its own_bytes -> (its slice of the
+        output file: device pointer, bytes; records written by all ranks; duplicates flagged by all)."""
+        d = C.c_void_p()
+        ob, nr, nd = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(lib().oge_mergesort_bgzf_shard(self.h, d_z, zbytes, own_bytes, C.byref(opts), C.byref(d), C.byref(ob),
+                                             C.byref(nr), C.byref(nd)), self.ctx.h)
+        return d.value or 0, ob.value, nr.value, nd.value
+
+    def decode_shard(self, d_z: int, zbytes: int, own_bytes: int, hdr_cap: int = 1 << 22):
+        """oge_bgzf_decode_shard: this rank's records of one sharded BGZF file -> (d_recs pointer, d_off
+        pointer (n + 1 offsets), n, raw BAM header bytes)."""
+        dr, do = C.c_void_p(), C.c_void_p()
+        n, hl = C.c_uint64(), C.c_uint64()
+        hb = C.create_string_buffer(hdr_cap)
+        check(lib().oge_bgzf_decode_shard(self.h, d_z, zbytes, own_bytes, C.byref(dr), C.byref(do), C.byref(n), hb, hdr_cap,
+                                          C.byref(hl)), self.ctx.h)
+        return dr.value or 0, do.value or 0, n.value, hb.raw[:hl.value]
+
     def exchange_stats(self) -> list:
         """This rank's per-exchange record of its last sort_markdup_dist / mergesort_bgzf_dist call:
         [{tag, calls, bytes_sent, bytes_recv, bytes_self, ms}] (bytes to / from other ranks, kept here;
@@ -664,6 +694,21 @@ class Comm:
         if self.h:
             lib().oge_comm_destroy(self.h)
             self.h = None
+
+
+BGZF_MAX_BLOCK = 65536  # BSIZE - 1 is a u16 (SAM spec 4.1): no block is longer
+
+
+def shard_ranges(file_bytes: int, world: int) -> list[tuple[int, int, int]]:
+    """Byte ranges of ONE BGZF file for `world` ranks (oge_bgzf_decode_shard / Comm.mergesort_bgzf_shard):
+    (a_g, own_g, end_g) -- rank g decodes the blocks that start in [a_g, a_g + own_g) and holds the file's
+    bytes [a_g, end_g) (its last block may run up to 64 KiB past its range; the last rank's ends at the
+    end of the file)."""
+    out = []
+    for g in range(world):
+        a, b = file_bytes * g // world, file_bytes * (g + 1) // world
+        out.append((a, b - a, min(file_bytes, b + BGZF_MAX_BLOCK)))
+    return out
 
 
 def comm_init(ctxs: list["Context"]) -> list[Comm]:

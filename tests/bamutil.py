@@ -116,10 +116,10 @@ def pack_records(recs: list[bytes]) -> tuple[np.ndarray, np.ndarray]:
     return np.frombuffer(b"".join(recs) + b"\0" * 16, dtype=np.uint8).copy(), np.array(offs + [acc], dtype=np.uint64)
 
 
-def bgzf_blocks(data: bytes, level: int = 6) -> bytes:
+def bgzf_blocks(data: bytes, level: int = 6, payload: int = 65280) -> bytes:
     out = bytearray()
-    for i in range(0, max(len(data), 1), 65280):
-        chunk = data[i:i + 65280]
+    for i in range(0, max(len(data), 1), payload):
+        chunk = data[i:i + payload]
         co = zlib.compressobj(level, zlib.DEFLATED, -15)
         c = co.compress(chunk) + co.flush()
         bsize = 18 + len(c) + 8

@@ -151,7 +151,8 @@ static int run(const std::vector<uint64_t> &keys, int G, double *balance, int fa
 }
 
 // G forked processes over the host-staged transport (shared file mapping); results come back in files
-static int run_shm(const std::vector<uint64_t> &keys, int G, double *balance, int fail_rank = -1, int dead_rank = -1) {
+static int run_shm(const std::vector<uint64_t> &keys, int G, double *balance, int fail_rank = -1, int dead_rank = -1,
+                   int foreign_rank = -1) {
     char dir[] = "/tmp/oge_shm_selftestXXXXXX";
     if (!mkdtemp(dir)) return perror("mkdtemp"), 1;
     char name[64];
@@ -167,6 +168,10 @@ static int run_shm(const std::vector<uint64_t> &keys, int G, double *balance, in
             if (!seg) {
                 fprintf(stderr, "rank %d: %s\n", r, err.c_str());
                 _exit(3);
+            }
+            if (r == foreign_rank) {  // a rank in another pid namespace: its posted pid does not exist here
+                seg->pose_as_foreign();
+                usleep(1500 * 1000);  // the others wait (and check liveness) long enough to have judged it
             }
             if (r == dead_rank) _exit(7);  // gone before the first collective
             HostOps ops;
@@ -247,6 +252,21 @@ int main(int argc, char **argv) {
             const int G = atoi(argv[a]);
             double bal = 0;
             if (run(keys, G, &bal, G - 1) || run_shm(keys, G, &bal, G - 1)) return 1;
+        }
+        printf("{}\n");
+        return 0;
+    }
+    if (!strcmp(argv[1], "--foreign-pid") || !strcmp(argv[1], "--foreign-dead")) {
+        // a live rank posting a pid that does not exist in this namespace must not be taken for dead; a
+        // foreign rank that exits is found by its stopped heartbeat (OGE_COMM_STALE_S)
+        const bool dies = !strcmp(argv[1], "--foreign-dead");
+        std::vector<uint64_t> keys(50000);
+        std::mt19937_64 rng(7);
+        for (auto &k : keys) k = rng() >> 20;
+        for (int a = 2; a < argc; ++a) {
+            const int G = atoi(argv[a]);
+            double bal = 0;
+            if (run_shm(keys, G, &bal, -1, dies ? G - 1 : -1, G - 1)) return 1;
         }
         printf("{}\n");
         return 0;

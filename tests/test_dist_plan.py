@@ -115,3 +115,19 @@ def test_dead_peer_ends_the_wait(tmp_path):
     r = subprocess.run([str(exe), "--dead-rank", "2", "4"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
     assert time.time() - t0 < 60
+
+
+def test_foreign_pid_namespace_peer_is_not_dead(tmp_path):
+    """a rank whose posted pid means nothing in this pid namespace (a container sharing the
+    segment) is alive while its heartbeat moves -- the schedule completes and verifies; when such a rank
+    exits, its stopped heartbeat ends the others' waits (OGE_COMM_STALE_S) long before the backstop."""
+    import os
+    import time
+    exe = _build(tmp_path / "dist_selftest")
+    env = dict(os.environ, OGE_COMM_TIMEOUT="600", OGE_COMM_DIR=str(tmp_path), OGE_COMM_STALE_S="3")
+    r = subprocess.run([str(exe), "--foreign-pid", "2", "4"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    t0 = time.time()
+    r = subprocess.run([str(exe), "--foreign-dead", "3"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    assert time.time() - t0 < 60

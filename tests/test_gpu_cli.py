@@ -130,6 +130,10 @@ def test_cli_errors_are_loud(tmp_path):
     r = subprocess.run([OPENGE, "mergesort", str(GOLDEN / "inputs" / "208.truncated.bam"), "-o", str(tmp_path / "t.bam")],
                        capture_output=True, text=True)
     assert r.returncode != 0 and "truncated" in r.stderr
+    # --gpus: the sharded reader rejects the file on every rank and the whole-file reader reports it
+    r = subprocess.run([OPENGE, "mergesort", "--gpus", "2", str(GOLDEN / "inputs" / "208.truncated.bam"), "-o",
+                        str(tmp_path / "t2.bam")], capture_output=True, text=True)
+    assert r.returncode != 0 and "truncated" in r.stderr
 
 
 @pytest.mark.parametrize("cmd", [("mergesort", "-M"), ("dedup", "-r")])
@@ -174,15 +178,17 @@ def test_cli_write_failures_exit_nonzero(tmp_path):
     assert r.returncode > 0 and "error writing" in r.stderr, (r.returncode, r.stderr)
 
 
-@pytest.mark.parametrize("G", [2, 3])
+@pytest.mark.parametrize("G", [2, 3, 8])
 def test_cli_gpus_matches_reference(case, tmp_path, G):
     """`--gpus G` (replacing SplitByChromosome/SortedMerge, cmd/command_mergesort.cpp:118-179,
     cmd/command_dedup.cpp:70-113): the same reference outputs as one GPU -- mergesort -M, sort, and
-    dedup of the sorted file, with -R dropping the flagged records.  On a one-GPU box the G ranks
-    share the GPU through the in-process transport."""
+    dedup of the sorted file, with -R dropping the flagged records.  The one input file is read by the
+    G ranks from their own byte ranges (FileReader::read_sharded, oge_bgzf_decode_shard).  On a one-GPU
+    box the G ranks share the GPU through the host-staged transport."""
     src = case_input(case, tmp_path)
     r = run("mergesort", "-M", "--nopg", "-v", "--gpus", G, src, "-o", tmp_path / "o.bam")
     assert f"{G} ranks" in r.stderr
+    assert f"FileReader (sharded over {G} ranks)" in r.stderr
     h, m, t = digests(tmp_path / "o.bam")
     g = case.meta["sortdedup_v"]
     assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]

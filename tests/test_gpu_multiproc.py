@@ -77,14 +77,20 @@ def one_gpu_realign(built, tmp_path_factory):
     return (d / "realign_0.bin").read_bytes()
 
 
-@pytest.mark.parametrize("world,realign", [(2, False), (3, False), (4, True), (8, False)])
-def test_bench_multiprocess_bootstrap_matches_reference(world, realign, tmp_path, one_gpu_c2_20k, request):
-    """world 4 and 8 are the rank counts of the 8-GPU node's scaling run (config 4), here as processes
-    sharing the one GPU; world 4 also runs the realign leg (contig-range shards, no exchange), whose
-    concatenated rank outputs must equal the one-process realign output byte for byte."""
+@pytest.mark.parametrize("world,realign,records", [(2, False, "overlap"), (3, False, "overlap"), (4, True, "overlap"),
+                                                  (8, False, "overlap"), (2, False, "blocking")])
+def test_bench_multiprocess_bootstrap_matches_reference(world, realign, records, tmp_path, one_gpu_c2_20k, request):
+    """ONE input file (the c2_20k golden input's records behind its header), every rank decoding the BGZF
+    blocks of its byte range (oge_mergesort_bgzf_shard).  world 4 and 8 are the rank counts of the 8-GPU
+    node's scaling run (config 4), here as processes sharing the one GPU; world 4 also runs the realign
+    leg (contig-range shards, no exchange), whose concatenated rank outputs must equal the one-process
+    realign output byte for byte.  records=blocking: the record exchange before the input pass
+    (OGE_DIST_RECORDS=blocking, the fallback of the side-stream overlap), same output."""
     case, want, nr1, nd1 = one_gpu_c2_20k
     env = dict(os.environ, OGE_COMM_DIR=str(tmp_path), OGE_COMM_TIMEOUT="120", MASTER_ADDR="127.0.0.1",
                OMP_NUM_THREADS="2")
+    if records == "blocking":
+        env["OGE_DIST_RECORDS"] = "blocking"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            str(ROOT / "bench.py"), "--gpus", str(world), "--pairs", "20000", "--seed", "99", "--steps", "1",
@@ -100,14 +106,23 @@ def test_bench_multiprocess_bootstrap_matches_reference(world, realign, tmp_path
     assert len(ex["per_rank"]) == world and len(line["stages_ms_per_rank"]) == world
     by = ex["by_tag"]
     for tag in ("records", "record_sizes", "fragments", "matejoin_candidates", "matejoin_minirecs", "pair_ends",
-                "dup_marks", "plans", "status"):
+                "dup_marks", "plans", "status", "shard_framing", "shard_edges", "shard_records"):
         assert tag in by, tag
+    # the codec is split: every rank inflated the blocks of its own byte range (~1/G of the file), the
+    # parts add up to the whole file and stream
+    sh = line["config"]["shard_per_rank"]
+    assert len(sh) == world
+    nblk = sum(s["shard_blocks"] for s in sh)
+    assert sum(s["shard_zbytes"] for s in sh) == line["config"]["input_file_bytes"]
+    assert max(s["shard_blocks"] for s in sh) <= nblk // world + 2
+    assert sum(s["shard_records"] for s in sh) == nr1
     # every record moves to its range owner or stays: sent + kept = the record bytes of the input
     rec_bytes = by["records"]["bytes_between_ranks"] + by["records"]["bytes_kept"]
     assert rec_bytes == int(np.frombuffer(want, np.uint8).size) - _header_bytes(want)
     assert by["record_sizes"]["bytes_between_ranks"] + by["record_sizes"]["bytes_kept"] == 4 * nr1
     # the record exchange ran on a side stream beside the own records' input pass
-    assert by["records"]["mode"] == "side_stream" and by["record_sizes"]["mode"] == "blocking"
+    assert by["records"]["mode"] == ("side_stream" if records == "overlap" else "blocking")
+    assert by["record_sizes"]["mode"] == "blocking"
     if realign:
         rl = line["realign"]
         assert rl["n_gpus"] == world and rl["value"] > 0
