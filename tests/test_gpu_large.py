@@ -8,8 +8,9 @@
 * 300M -- the bench workload itself (configs[1]/[2]): no reference run exists at that size (it would
   take ~40 min on 8 cores), so the output is checked through size-independent properties of
   mark_duplicates.cpp:326-475 / Sort.h:116-136: the output is a permutation of the input, its
-  ByPosition key (refID', pos, strand, name, flag) never decreases, and the duplicate count equals the
-  number of records carrying 0x400.
+  ByPosition key (refID', pos, strand, name, flag) never decreases, the duplicate count equals the
+  number of records carrying 0x400, and every record's 0x400 bit equals the one an independent torch
+  restatement of MarkDuplicates (tests/dupcheck.py, pinned to the reference on the goldens) gives it.
 """
 import hashlib
 import json
@@ -138,7 +139,8 @@ def test_300m_read_properties():
         import ctypes as C
         buf = C.create_string_buffer(1 << 16)
         L.check(L.lib().oge_synth_header_text(C.byref(p), buf, 1 << 16, None))
-        opts, keep = L.markdup_opts_from_header(buf.value.decode(), p.n_ref)
+        hdr_text = buf.value.decode()
+        opts, keep = L.markdup_opts_from_header(hdr_text, p.n_ref)
         d_out = torch.empty(B + 64, dtype=torch.uint8, device="cuda")
         d_out_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
         d_perm = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -183,6 +185,20 @@ def test_300m_read_properties():
         # the duplicate count is the number of records carrying 0x400
         assert int(((flag >> 10) & 1).sum().item()) == nd
         assert 0.06 * n < nd < 0.10 * n  # 8% duplicate pairs
+        del a_hi, a_lo, b_hi, b_lo, fa, fb, ordered, tie
+        # WHICH records carry 0x400: the torch restatement of MarkDuplicates
+        # (tests/dupcheck.py, pinned to the reference's dup sets on every golden case by
+        # tests/test_dupcheck.py) recomputes the pair and fragment chunks from the output records --
+        # every pair chunk keeps exactly its first strict max, fragment chunks follow the paired /
+        # unpaired rule -- and must give every one of the 300M records the bit the product gave it
+        import dupcheck
+        got = ((flag >> 10) & 1).bool()
+        del flag
+        torch.cuda.empty_cache()
+        primary, want = dupcheck.expected_dups(d_out, off, hdr_text)
+        assert bool(primary.all())
+        bad = int((want != got).sum().item())
+        assert bad == 0, f"{bad} of {n} records carry a 0x400 bit the restated MarkDuplicates does not give"
     finally:
         ctx.close()
 
