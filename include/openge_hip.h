@@ -163,6 +163,14 @@ typedef struct oge_mergesort_opts {
 void oge_mergesort_opts_init(oge_mergesort_opts *o);
 int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *o,
                            const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup);
+/* The same chain on a BAM file in HOST memory with the PCIe transfers overlapped (replaces the reader and
+ * writer threads of BgzfInputStream / BgzfOutputStream, util/bgzf_input_stream.cpp:180-206,
+ * util/bgzf_output_stream.cpp:252-285): h_z goes up in chunks on a copy stream while the host indexes its
+ * framing and the chunks already up are inflated; after the sort the output is deflated in block-aligned
+ * segments whose copies down into h_out (out_cap bytes) run while the next segment is compressed.  The
+ * output bytes equal oge_mergesort_bgzf_dev's.  h_z and h_out should be page-locked (oge_host_alloc). */
+int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_t zbytes, const oge_mergesort_opts *o, uint8_t *h_out,
+                            uint64_t out_cap, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup);
 
 /* ---- inputs larger than HBM (replaces ReadSorter's spilled runs + k-way merge) ---------- */
 /* Receives one output range: n records in HBM (d_off: n + 1 offsets from d_recs), valid during the

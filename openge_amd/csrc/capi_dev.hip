@@ -1,5 +1,6 @@
 // capi_dev.hip -- C-ABI entry points that run on the GPU, the context implementation, and the
 // device-side synthetic generator.
+#include <chrono>
 #include "oge_ctx.h"
 #include "bam_layout.h"
 #include "synth.h"
@@ -56,6 +57,22 @@ void *oge_ctx::ws(const char *name, size_t bytes) {
     Buf &b = bufs[name];
     if (bytes == 0) bytes = 1;
     if (b.cap >= bytes) return b.p;
+    // host time of (re)allocations, per call (oge_ctx_counter "ws_alloc_us" / "ws_allocs"); OGE_TRACE_ALLOC
+    // prints each one
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Note {
+        oge_ctx *c;
+        const char *nm;
+        size_t sz;
+        std::chrono::steady_clock::time_point t0;
+        ~Note() {
+            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            c->counters["ws_alloc_us"] += (uint64_t)us;
+            c->counters["ws_allocs"] += 1;
+            static const bool tr = getenv("OGE_TRACE_ALLOC") != nullptr;
+            if (tr) fprintf(stderr, "[oge ws] %s %.3f GB: %.1f ms\n", nm, sz / 1e9, us / 1e3);
+        }
+    } note{this, name, bytes, t0};
     if (b.p) {
         hipStreamSynchronize(stream);
         release(b.p);

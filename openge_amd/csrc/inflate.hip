@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "bam_layout.h"
@@ -327,6 +328,99 @@ extern "C" int oge_bgzf_index(const uint8_t *z, uint64_t zbytes, uint64_t *d0, u
     return k <= cap ? OGE_OK : oge_fail(nullptr, OGE_ERR_ARG, "index capacity too small");
 }
 
+
+// The same framing walk on the host with T threads (oge_mergesort_bgzf_host indexes a host file while its
+// first chunks upload): thread t walks the blocks that start in [zbytes t / T, zbytes (t + 1) / T) from the
+// first position there that begins a chain of valid headers (three blocks, or to the end of the stream);
+// each walk must start where its predecessor's ended (a wrong guess is walked again from that exit).  The
+// output equals oge_bgzf_index's (nonempty blocks only); returns false on anything it cannot walk (the
+// caller then takes the sequential walk, which reports the error).
+static uint32_t host_bgzf_head(const uint8_t *z, uint64_t zbytes, uint64_t p) {
+    if (zbytes - p < 18 || z[p] != 31 || z[p + 1] != 139 || z[p + 2] != 8 || z[p + 3] != 4) return 0;
+    const uint64_t xend = p + 12 + rd16h(z + p + 10);
+    if (xend > zbytes) return 0;
+    uint32_t bs = 0;
+    for (uint64_t x = p + 12; x + 4 <= xend;) {
+        const uint32_t sl = rd16h(z + x + 2);
+        if (z[x] == 'B' && z[x + 1] == 'C' && sl == 2) bs = (uint32_t)rd16h(z + x + 4) + 1;
+        x += 4 + sl;
+    }
+    if (!bs || p + bs > zbytes || bs < xend - p + 8) return 0;
+    if (rd32h(z + p + bs - 4) > kSlot) return 0;
+    return bs;
+}
+
+bool oge_bgzf_index_host_mt(const uint8_t *z, uint64_t zbytes, int T, std::vector<uint64_t> &d0, std::vector<uint64_t> &d1,
+                            std::vector<uint64_t> &uoff, std::vector<uint32_t> &crc) {
+    T = std::max(1, std::min(T, 64));
+    if (zbytes < (uint64_t)T * (1u << 20)) T = 1;
+    struct Part {
+        uint64_t s = 0, x = 0;
+        bool ok = false;
+        std::vector<uint64_t> pos;  // block starts (every block, empty ones included)
+    };
+    std::vector<Part> P(T);
+    auto walk = [&](Part &w, uint64_t s, uint64_t lim) {
+        w.s = s, w.pos.clear(), w.ok = false;
+        uint64_t p = s;
+        while (p < lim) {
+            const uint32_t bs = host_bgzf_head(z, zbytes, p);
+            if (!bs) return;
+            w.pos.push_back(p);
+            p += bs;
+        }
+        w.x = p;
+        w.ok = true;
+    };
+    auto guess = [&](uint64_t a, uint64_t lim) -> uint64_t {  // first position in [a, lim) starting a valid chain
+        for (uint64_t p = a; p < lim; ++p) {
+            if (z[p] != 31) continue;
+            uint64_t q = p;
+            int k = 0;
+            for (; k < 3 && q < zbytes; ++k) {
+                const uint32_t bs = host_bgzf_head(z, zbytes, q);
+                if (!bs) break;
+                q += bs;
+            }
+            if (k == 3 || q == zbytes) return p;
+        }
+        return lim;
+    };
+    std::vector<std::thread> ts;
+    for (int t = 0; t < T; ++t)
+        ts.emplace_back([&, t]() {
+            const uint64_t a = zbytes * (uint64_t)t / (uint64_t)T, b = zbytes * (uint64_t)(t + 1) / (uint64_t)T;
+            walk(P[t], t ? guess(a, std::min(zbytes, a + (1u << 20))) : 0, b);
+        });
+    for (auto &t : ts) t.join();
+    for (int t = 0; t < T; ++t) {  // the join: every part starts where the previous one ended
+        const uint64_t b = zbytes * (uint64_t)(t + 1) / (uint64_t)T;
+        const uint64_t want = t ? P[t - 1].x : 0;
+        if (!P[t].ok || P[t].s != want) {
+            if (want >= b) {  // no block starts in this part
+                P[t].s = P[t].x = want, P[t].pos.clear(), P[t].ok = true;
+                continue;
+            }
+            walk(P[t], want, b);
+            if (!P[t].ok) return false;
+        }
+    }
+    if (P[T - 1].x != zbytes) return false;
+    d0.clear(), d1.clear(), uoff.clear(), crc.clear();
+    uint64_t total = 0;
+    for (auto &w : P)
+        for (uint64_t p : w.pos) {
+            const uint32_t bs = host_bgzf_head(z, zbytes, p), isize = rd32h(z + p + bs - 4);
+            if (!isize) continue;
+            d0.push_back(p + 12 + rd16h(z + p + 10));
+            d1.push_back(p + bs - 8);
+            uoff.push_back(total);
+            crc.push_back(rd32h(z + p + bs - 8));
+            total += isize;
+        }
+    uoff.push_back(total);
+    return true;
+}
 
 // Device framing index into the context's workspace (pointers valid until the next call that uses
 // it).  Returns 1 (no error recorded) when the candidate chain is not exact: the caller then uses

@@ -128,6 +128,9 @@ int oge_record_walk(oge_ctx *ctx, const uint8_t *d, uint64_t start, uint64_t lim
                     uint64_t *d_off, uint64_t cap, uint64_t *n_out, uint64_t *exit);
 // The first plausible record start in [0, lim) of d (bufend readable) as k_rec_guess judges it, or ~0.
 int oge_record_guess(oge_ctx *ctx, const uint8_t *d, uint64_t lim, uint64_t bufend, bool at_end, int32_t n_ref, uint64_t *out);
+// the framing walk of a host buffer with T threads (inflate.hip); false: use oge_bgzf_index
+bool oge_bgzf_index_host_mt(const uint8_t *z, uint64_t zbytes, int T, std::vector<uint64_t> &d0, std::vector<uint64_t> &d1,
+                            std::vector<uint64_t> &uoff, std::vector<uint32_t> &crc);
 // lane-per-block BGZF inflate (inflate_lane.hip); err/zpow as in oge_bgzf_inflate_dev
 int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const uint64_t *d0, const uint64_t *d1,
                       const uint64_t *uoff, const uint32_t *crc, uint64_t nblk, uint8_t *out, uint32_t *err,

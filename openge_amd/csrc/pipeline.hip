@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "bamio.h"
+#include "bgzf_dev.h"
 #include "oge_ctx.h"
 
 using namespace oge;
@@ -83,6 +84,8 @@ extern "C" void oge_mergesort_opts_init(oge_mergesort_opts *o) {
     o->level = 6;  // FileWriter's default compression level (commands.cpp:129, -c)
 }
 
+static int decode_records(oge_ctx *ctx, uint8_t *X, uint64_t total, uint64_t **xoff_o, uint64_t *n_o, BamFile *f);
+
 // The reader half: framing index, inflate into X (ws "pipe_x", *cap bytes), header parse, record walk.
 static int decode(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint8_t **Xo, uint64_t *cap_out, uint64_t **xoff_o,
                   uint64_t *n_o, BamFile *f) {
@@ -115,6 +118,16 @@ static int decode(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint8_t **X
     rc = oge_bgzf_inflate_dev(ctx, d_z, zbytes, ix.d0, ix.d1, ix.uoff, ix.crc, ix.nblk, X);
     if (rc) return rc;
 
+    *Xo = X;
+    *cap_out = cap;
+    return decode_records(ctx, X, total, xoff_o, n_o, f);
+}
+
+// The reader's second half on the decompressed stream X[0, total): header parse (host, a copy of the
+// first bytes), record walk.
+static int decode_records(oge_ctx *ctx, uint8_t *X, uint64_t total, uint64_t **xoff_o, uint64_t *n_o, BamFile *f) {
+    int rc = OGE_OK;
+    OgeStageTimer *tm = nullptr;
     // ---- header (host parse of the stream's first bytes)
     std::string err;
     size_t rec_base = 0;
@@ -138,8 +151,6 @@ static int decode(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint8_t **X
     rc = oge_bam_record_offsets_dev(ctx, X, rec_base, total, n_ref, xoff, n + 1, &n);
     if (rc) return rc;
     ctx->end_stage(tm);
-    *Xo = X;
-    *cap_out = cap;
     *xoff_o = xoff;
     *n_o = n;
     return OGE_OK;
@@ -177,6 +188,36 @@ static std::vector<uint8_t> out_header(const BamFile &f, const oge_mergesort_opt
     return bam_encode_header(oh);
 }
 
+// sort (+ markdup) X -> Y (ws "pipe_y", cap bytes) with bins recomputed and 0x400 applied; with -R the
+// kept records go back into X.  *src / *soff / *m: the records to write; *spare: the other buffer.
+static int sort_stage(oge_ctx *ctx, uint8_t *X, uint64_t *xoff, uint64_t n, uint64_t cap, const BamFile &f, const oge_mergesort_opts *mo,
+                      uint8_t **src, uint64_t **soff, uint64_t *m, uint64_t *nd, uint8_t **spare) {
+    const int32_t n_ref = (int32_t)f.ref_names.size();
+    uint8_t *Y = (uint8_t *)ctx->ws("pipe_y", cap);
+    uint64_t *yoff = (uint64_t *)ctx->ws("pipe_yoff", (n + 1) * 8);
+    uint32_t *perm = (uint32_t *)ctx->ws("pipe_perm", (n + 1) * 4);
+    if (!Y || !yoff || !perm) return OGE_ERR_HIP;
+    *nd = 0;
+    LibTable lt(f.header, n_ref, mo);
+    int rc;
+    if (mo->mark_duplicates) {
+        rc = oge_sort_markdup_dev(ctx, X, xoff, n, &lt.o, perm, Y, yoff, nd);
+    } else {
+        rc = oge_sort_coord_dev(ctx, X, xoff, n, n_ref, perm);
+        if (!rc) rc = oge_gather_records_dev(ctx, X, xoff, perm, n, Y, yoff);
+    }
+    if (rc) return rc;
+    *src = Y, *spare = X, *soff = yoff, *m = n;
+    if (mo->mark_duplicates && mo->remove_duplicates) {  // -R: MarkDuplicates::runInternal :456-458
+        OgeStageTimer *tm = ctx->begin_stage("drop_dups");
+        rc = oge_drop_flagged_dev(ctx, Y, yoff, n, 0x400, X, xoff, m);
+        ctx->end_stage(tm);
+        if (rc) return rc;
+        *src = X, *spare = Y, *soff = xoff;
+    }
+    return OGE_OK;
+}
+
 extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *mo,
                                       const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup) {
     if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
@@ -191,32 +232,10 @@ extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t
     BamFile f;
     int rc = decode(ctx, d_z, zbytes, &X, &cap, &xoff, &n, &f);
     if (rc) return rc;
-    const int32_t n_ref = (int32_t)f.ref_names.size();
-
-    // ---- sort (+ markdup), gathered into Y with bins recomputed and 0x400 applied
-    uint8_t *Y = (uint8_t *)ctx->ws("pipe_y", cap);
-    uint64_t *yoff = (uint64_t *)ctx->ws("pipe_yoff", (n + 1) * 8);
-    uint32_t *perm = (uint32_t *)ctx->ws("pipe_perm", (n + 1) * 4);
-    if (!Y || !yoff || !perm) return OGE_ERR_HIP;
-    uint64_t nd = 0;
-    LibTable lt(f.header, n_ref, mo);
-    if (mo->mark_duplicates) {
-        rc = oge_sort_markdup_dev(ctx, X, xoff, n, &lt.o, perm, Y, yoff, &nd);
-    } else {
-        rc = oge_sort_coord_dev(ctx, X, xoff, n, n_ref, perm);
-        if (!rc) rc = oge_gather_records_dev(ctx, X, xoff, perm, n, Y, yoff);
-    }
+    uint8_t *src, *dst;
+    uint64_t *soff, m, nd;
+    rc = sort_stage(ctx, X, xoff, n, cap, f, mo, &src, &soff, &m, &nd, &dst);
     if (rc) return rc;
-    uint8_t *src = Y, *dst = X;
-    uint64_t *soff = yoff;
-    uint64_t m = n;
-    if (mo->mark_duplicates && mo->remove_duplicates) {  // -R: MarkDuplicates::runInternal :456-458
-        OgeStageTimer *tm = ctx->begin_stage("drop_dups");
-        rc = oge_drop_flagged_dev(ctx, Y, yoff, n, 0x400, X, xoff, &m);
-        ctx->end_stage(tm);
-        if (rc) return rc;
-        src = X, dst = Y, soff = xoff;
-    }
 
     // ---- output: header block(s) (host zlib/libdeflate, tiny), device deflate of the records, EOF
     const std::vector<uint8_t> hb = out_header(f, mo);
@@ -225,6 +244,143 @@ extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t
     if (rc) return rc;
     *d_out = dst;
     *out_bytes = ob;
+    if (n_reads) *n_reads = m;
+    if (n_dup) *n_dup = nd;
+    return OGE_OK;
+}
+
+// The same chain on a BAM file in HOST memory with the PCIe transfers overlapped (the
+// reference's reader / writer threads overlap I/O with the modules, util/bgzf_input_stream.cpp:180-206,
+// util/bgzf_output_stream.cpp:252-285): the file goes up in G chunks on a copy stream while the host
+// indexes its framing (oge_bgzf_index_host_mt) and the blocks of every chunk already up are inflated;
+// after the sort, the output is deflated in block-aligned segments into two device buffers whose copies
+// down to h_out run while the next segment is compressed.  The output bytes equal oge_mergesort_bgzf_dev's
+// (segments of whole payloads: the same blocks).  h_z / h_out page-locked for full speed.
+static uint64_t env_u64(const char *name, uint64_t dflt) {
+    const char *e = getenv(name);
+    return e && *e ? strtoull(e, nullptr, 10) : dflt;
+}
+
+extern "C" int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_t zbytes, const oge_mergesort_opts *mo, uint8_t *h_out,
+                                       uint64_t out_cap, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if (!mo || !out_bytes || !h_out || (zbytes && !h_z)) return oge_fail(ctx, OGE_ERR_ARG, "null argument");
+    if (mo->level < 0 || mo->level > 9) return oge_fail(ctx, OGE_ERR_ARG, "level must be 0..9");
+    (void)hipSetDevice(ctx->device);
+    Hold hold(ctx);
+    *out_bytes = 0;
+    hipStream_t cs = ctx->side_stream(3);
+    uint8_t *dz = (uint8_t *)ctx->ws("hostpipe_z", zbytes + 64);
+    if (!cs || !dz) return OGE_ERR_HIP;
+    // ---- 1. the file up in G chunks on the copy stream (4 KiB-aligned cuts), an event after each
+    const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(env_u64("OGE_HOSTPIPE_GROUPS", 8), 64));
+    const uint64_t C = ((zbytes + G - 1) / G + 4095) & ~4095ull;
+    std::vector<hipEvent_t> up;
+    struct Evs {
+        std::vector<hipEvent_t> *v;
+        ~Evs() {
+            for (auto e : *v) (void)hipEventDestroy(e);
+        }
+    } evs{&up};
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // dz may still be read by this context's last call
+    for (uint64_t o = 0; o < zbytes; o += C) {
+        hipEvent_t e;
+        OGE_HIP_TRY(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        up.push_back(e);
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(dz + o, h_z + o, std::min(C, zbytes - o), hipMemcpyHostToDevice, cs));
+        OGE_HIP_TRY(ctx, hipEventRecord(e, cs));
+    }
+    // ---- 2. the framing, on the host meanwhile
+    OgeStageTimer *tm = ctx->begin_stage("bgzf_index");
+    std::vector<uint64_t> d0, d1, uo;
+    std::vector<uint32_t> crc;
+    if (!oge_bgzf_index_host_mt(h_z, zbytes, (int)env_u64("OGE_HOSTPIPE_THREADS", 16), d0, d1, uo, crc)) {
+        uint64_t nb = 0;  // the sequential walk, for its error messages
+        int rc = oge_bgzf_index(h_z, zbytes, nullptr, nullptr, nullptr, nullptr, 0, &nb);
+        if (rc != OGE_OK && rc != OGE_ERR_ARG) return oge_fail(ctx, rc, oge_last_error(nullptr));
+        d0.resize(nb), d1.resize(nb), uo.resize(nb + 1), crc.resize(nb);
+        rc = oge_bgzf_index(h_z, zbytes, d0.data(), d1.data(), uo.data(), crc.data(), nb, &nb);
+        if (rc) return oge_fail(ctx, rc, oge_last_error(nullptr));
+    }
+    const uint64_t nb = d0.size(), total = uo[nb];
+    if (!total) return oge_fail(ctx, OGE_ERR_IO, "empty BAM stream (no BAM magic)");
+    uint64_t *dix = (uint64_t *)ctx->ws("pipe_ix", (3 * nb + 2) * 8);
+    uint32_t *dcrc = (uint32_t *)ctx->ws("pipe_ixc", (nb + 1) * 4);
+    if (!dix || !dcrc) return OGE_ERR_HIP;
+    if (nb) {
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(dix, d0.data(), nb * 8, hipMemcpyHostToDevice, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(dix + nb, d1.data(), nb * 8, hipMemcpyHostToDevice, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(dcrc, crc.data(), nb * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(dix + 2 * nb, uo.data(), (nb + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    ctx->end_stage(tm);
+    // ---- 3. inflate: the blocks whose bytes are up, chunk after chunk (the X of the device chain)
+    const uint64_t cap = std::max<uint64_t>(total, oge_bgzf_bound(total) + (1u << 20)) + 64;
+    uint8_t *X = (uint8_t *)ctx->ws("pipe_x", cap);
+    if (!X) return OGE_ERR_HIP;
+    uint64_t b = 0;
+    for (size_t g = 0; g < up.size(); ++g) {
+        const uint64_t end = std::min(zbytes, (g + 1) * C);
+        uint64_t b1 = b;
+        while (b1 < nb && d1[b1] + 8 <= end) ++b1;
+        if (g + 1 == up.size()) b1 = nb;
+        OGE_HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, up[g], 0));
+        if (b1 > b) {
+            const int rc = oge_bgzf_inflate_dev(ctx, dz, zbytes, dix + b, dix + nb + b, dix + 2 * nb + b, dcrc + b, b1 - b, X);
+            if (rc) return rc;
+        }
+        b = b1;
+    }
+    // ---- 4. records, sort (+ markdup)
+    uint64_t *xoff, n;
+    BamFile f;
+    int rc = decode_records(ctx, X, total, &xoff, &n, &f);
+    if (rc) return rc;
+    uint8_t *src, *spare;
+    uint64_t *soff, m, nd;
+    rc = sort_stage(ctx, X, xoff, n, cap, f, mo, &src, &soff, &m, &nd, &spare);
+    if (rc) return rc;
+    (void)spare;
+    // ---- 5. header block(s), then the records deflated segment by segment, each copied down while the
+    //         next one is compressed
+    const std::vector<uint8_t> hb = out_header(f, mo);
+    const std::vector<uint8_t> hz = bgzf_compress_host(hb.data(), hb.size(), mo->level);
+    if (hz.size() + 28 > out_cap) return oge_fail(ctx, OGE_ERR_LIMIT, "output buffer too small");
+    memcpy(h_out, hz.data(), hz.size());
+    uint64_t ends[2] = {0, 0};
+    if (m) {
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&ends[0], soff, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&ends[1], soff + m, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    const uint64_t len = ends[1] - ends[0];
+    const uint64_t SEG = (uint64_t)oge_bgzf::kPay * std::max<uint64_t>(1, env_u64("OGE_HOSTPIPE_SEG_BLOCKS", 32768));
+    const uint64_t bnd = oge_bgzf_bound(std::min(len, SEG));
+    uint8_t *zb[2] = {(uint8_t *)ctx->ws("hostpipe_out0", bnd), (uint8_t *)ctx->ws("hostpipe_out1", bnd)};
+    if (!zb[0] || !zb[1]) return OGE_ERR_HIP;
+    hipEvent_t dn[2];
+    OGE_HIP_TRY(ctx, hipEventCreateWithFlags(&dn[0], hipEventDisableTiming));
+    up.push_back(dn[0]);
+    OGE_HIP_TRY(ctx, hipEventCreateWithFlags(&dn[1], hipEventDisableTiming));
+    up.push_back(dn[1]);
+    uint64_t pos = hz.size();
+    for (uint64_t s0 = 0, k = 0; s0 < len; s0 += SEG, ++k) {
+        const uint64_t sl = std::min(SEG, len - s0);
+        if (k >= 2) OGE_HIP_TRY(ctx, hipEventSynchronize(dn[k & 1]));  // that buffer's copy is done
+        uint64_t got = 0;
+        rc = oge_bgzf_deflate_dev(ctx, src + ends[0] + s0, sl, mo->level, zb[k & 1], bnd, &got);  // returns when written
+        if (rc) return rc;
+        if (pos + got + 28 > out_cap) {
+            (void)hipStreamSynchronize(cs);
+            return oge_fail(ctx, OGE_ERR_LIMIT, "output buffer too small");
+        }
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(h_out + pos, zb[k & 1], got, hipMemcpyDeviceToHost, cs));
+        OGE_HIP_TRY(ctx, hipEventRecord(dn[k & 1], cs));
+        pos += got;
+    }
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(cs));
+    memcpy(h_out + pos, kBgzfEof, 28);
+    *out_bytes = pos + 28;
     if (n_reads) *n_reads = m;
     if (n_dup) *n_dup = nd;
     return OGE_OK;

@@ -226,6 +226,7 @@ def lib() -> C.CDLL:
         "oge_comm_rank": (C.c_int, [vp]),
         "oge_comm_size": (C.c_int, [vp]),
         "oge_comm_transport": (C.c_char_p, [vp]),
+        "oge_mergesort_bgzf_host": (C.c_int, [vp, vp, u64, vp, vp, u64, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]),
         "oge_mergesort_bgzf_dist": (C.c_int, [vp, vp, u64, vp, C.POINTER(vp), C.POINTER(u64), C.POINTER(u64),
                                               C.POINTER(u64)]),
         "oge_sort_markdup_dist": (C.c_int, [vp, vp, vp, u64, i32, C.c_int, vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64),
@@ -524,6 +525,14 @@ class Context:
         check(lib().oge_mergesort_bgzf_dev(self.h, d_z, zbytes, C.byref(opts), C.byref(d), C.byref(ob), C.byref(nr),
                                            C.byref(nd)), self.h)
         return d.value or 0, ob.value, nr.value, nd.value
+
+    def mergesort_bgzf_host(self, h_z: int, zbytes: int, opts: "MergesortOpts", h_out: int, out_cap: int) -> tuple[int, int, int]:
+        """The chain on a BAM file in host memory (page-locked for full speed), PCIe overlapped with the
+        codec -> (out_bytes written to h_out, n_reads, n_dup)."""
+        ob, nr, nd = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(lib().oge_mergesort_bgzf_host(self.h, h_z, zbytes, C.byref(opts), h_out, out_cap, C.byref(ob), C.byref(nr),
+                                            C.byref(nd)), self.h)
+        return ob.value, nr.value, nd.value
 
     def record_offsets_dev(self, d_stream, rec_base: int, end: int, n_ref: int, d_off=None, cap: int = 0) -> int:
         n = C.c_uint64()

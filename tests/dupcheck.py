@@ -19,7 +19,8 @@ alg/mark_duplicates.cpp:
      than one and holding an unpaired end: with a paired end present mark the unpaired ends, else keep
      the first strict max (index order) and mark the rest.  A fragment end is "paired" when
      read2Sequence = mateRefID != -1.
-The checker hashes read names (two 64-bit polynomial hashes + length) instead of comparing them.
+The checker hashes read names (two independent 64-bit hashes + the length, compared as separate keys)
+instead of comparing them.
 """
 from __future__ import annotations
 
@@ -57,13 +58,13 @@ def _rg_libs(header_text: str) -> dict[bytes, str]:
 
 def _hash_bytes(buf, start, length, maxlen, cap):
     """two 64-bit polynomial hashes of buf[start : start + length] (per record; length <= maxlen), int64 wrap"""
-    h1 = torch.zeros_like(start)
+    h1 = torch.full_like(start, 0x6C62272E07BB0142)  # FNV-1a 64 (as int64)
     h2 = torch.full_like(start, 7)
     for k in range(maxlen):
         m = k < length
         b = _u8(buf, torch.where(m, start + k, torch.zeros_like(start)).clamp_(max=cap))
-        h1 = torch.where(m, h1 * 1000003 + b + 1, h1)
-        h2 = torch.where(m, h2 * 0x100000001B3 + (b ^ 0x5A) + 3, h2)
+        h1 = torch.where(m, (h1 ^ b) * 0x100000001B3, h1)
+        h2 = torch.where(m, (h2 + b + 1) * 0x5851F42D4C957F2D, h2)
     return h1, h2
 
 
@@ -114,8 +115,10 @@ def _rg_of(buf, off, end, tag0, cap):
     return found, rs, rl
 
 
-def expected_dups(buf: torch.Tensor, off: torch.Tensor, header_text: str) -> tuple[torch.Tensor, torch.Tensor]:
-    """-> (primary mask, expected 0x400 bit) per record of the sorted stream."""
+def expected_dups(buf: torch.Tensor, off: torch.Tensor, header_text: str, debug: dict | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """-> (primary mask, expected 0x400 bit) per record of the sorted stream.  debug (a dict) receives the
+    pair arrays (read1 / read2 record, chunk keys, score, group id, in chunk order) and per-record
+    coordinate / score / library."""
     dev = off.device
     n = off.numel()
     cap = buf.numel() - 1
@@ -175,16 +178,23 @@ def expected_dups(buf: torch.Tensor, off: torch.Tensor, header_text: str) -> tup
     # ---- D2: pairs.  key RG:name (hash of the RG value and of the name), consecutive occurrences pair up
     ci = torch.nonzero(cand).squeeze(1)
     if ci.numel():
+        # the key RG:name as four sort keys (name hashes and length, RG hash): every one must be equal --
+        # never folded into one word (r05: names differing in their last digit collided when the two name
+        # hashes were XOR-ed together, and the restatement paired ends of different names)
         nh1, nh2 = _hash_bytes(buf, off[ci] + 36, lname[ci] - 1, int(lname.max().item()), cap)
         k_rg = torch.where(found[ci], rh1[ci] ^ (rl[ci] << 40), torch.full_like(ci, -1))
-        k_nm = nh1 ^ (nh2 * 31) ^ (lname[ci] << 56)
-        o = torch.argsort(k_nm, stable=True)  # ci is in index order: stable sorts keep it within a key
+        k_rg2 = torch.where(found[ci], rh2[ci], torch.full_like(ci, -1))
+        k_nm = nh1
+        k_nm2 = nh2 ^ lname[ci]
+        o = torch.argsort(k_nm2, stable=True)  # ci is in index order: stable sorts keep it within a key
+        o = o[torch.argsort(k_nm[o], stable=True)]
+        o = o[torch.argsort(k_rg2[o], stable=True)]
         o = o[torch.argsort(k_rg[o], stable=True)]
         s = ci[o]
-        kn, kr = k_nm[o], k_rg[o]
-        del o, k_nm, k_rg, nh1, nh2
+        kn, kn2, kr, kr2 = k_nm[o], k_nm2[o], k_rg[o], k_rg2[o]
+        del o, k_nm, k_nm2, k_rg, k_rg2, nh1, nh2
         newk = torch.ones_like(s, dtype=torch.bool)
-        newk[1:] = (kn[1:] != kn[:-1]) | (kr[1:] != kr[:-1])
+        newk[1:] = (kn[1:] != kn[:-1]) | (kn2[1:] != kn2[:-1]) | (kr[1:] != kr[:-1]) | (kr2[1:] != kr2[:-1])
         start = torch.cummax(torch.where(newk, torch.arange(s.numel(), device=dev), torch.zeros_like(s)), 0).values
         rank = torch.arange(s.numel(), device=dev) - start
         nxt_same = torch.zeros_like(newk)
@@ -192,7 +202,7 @@ def expected_dups(buf: torch.Tensor, off: torch.Tensor, header_text: str) -> tup
         first = (rank % 2 == 0) & nxt_same  # the first end of a completed pair; its partner is next
         a = s[torch.nonzero(first).squeeze(1)]
         b = s[torch.nonzero(first).squeeze(1) + 1]
-        del s, kn, kr, newk, start, rank, nxt_same, first
+        del s, kn, kn2, kr, kr2, newk, start, rank, nxt_same, first
         # read1 = a unless b's (seq, coord) is smaller
         keep = (ref[b] > ref[a]) | ((ref[b] == ref[a]) & (coord[b] >= coord[a]))
         r1 = torch.where(keep, a, b)
@@ -220,7 +230,11 @@ def expected_dups(buf: torch.Tensor, off: torch.Tensor, header_text: str) -> tup
         lose = p != best[gid]
         dup[r1[lose]] = True
         dup[r2[lose]] = True
+        if debug is not None:
+            debug.update(pr1=r1, pr2=r2, pk1=k1, pk2=k2, psc=psc, pgid=gid)
         del k1, k2, psc, r1, r2, newg, gid, gmax, p, cand_best, best, lose
+    if debug is not None:
+        debug.update(coord=coord, score=score, lib=lib, ends=ends, cand=cand, frag_paired=frag_paired)
     # ---- D4 fragments: every ReadEnds
     fi = torch.nonzero(ends).squeeze(1)
     if fi.numel():

@@ -33,3 +33,21 @@ def test_restated_dups_equal_reference(built, name):
     g = case.meta["sortdedup_v"]
     assert len(idx) == g["n_dup"], (name, len(idx), g["n_dup"])
     assert np.array_equal(idx, case.arrays["sortdedup_v"])
+
+
+@pytest.mark.parametrize("name", ["c1_100k", "c2_20k"])
+def test_restated_mate_join_pairs_equal_names(built, name):
+    """Every pair the restatement forms joins two ends of ONE name (consecutive-digit names: r05 found the
+    XOR of two name hashes colliding on names that differ in their last digit, at 300M)."""
+    case = load_case(name)
+    buf, off, perm = _sorted_stream(case)
+    dbg = {}
+    dupcheck.expected_dups(torch.from_numpy(buf), torch.from_numpy(off[:-1]), case.header, debug=dbg)
+    r1, r2 = dbg["pr1"].numpy(), dbg["pr2"].numpy()
+    assert len(r1) > 1000
+
+    def nm(i):
+        o = int(off[i])
+        return bytes(buf[o + 36:o + 36 + int(buf[o + 12]) - 1])
+
+    assert all(nm(a) == nm(b) for a, b in zip(r1, r2))
