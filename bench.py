@@ -17,8 +17,9 @@ single-candidate parse (DEFLATE_SEARCH below), not zlib's level-6 lazy hash-chai
 Also on the same JSON line:
   kernel_step   -- the sort+dedup device pipeline alone over records already decoded in HBM
                    (oge_sort_markdup_dev), the round-1 headline, with its stage times
-  pcie_inclusive-- one more e2e run with the compressed input uploaded from / the output downloaded
-                   to page-locked host memory inside the timed region (never `value`)
+  pcie_inclusive-- the same chain from a BAM file in page-locked host memory to one in host memory
+                   (oge_mergesort_bgzf_host: upload overlapped with the framing index and inflate, the
+                   download with the deflate), second call timed, the first reported (never `value`)
   roofline      -- the e2e step's dominant kernel: algorithmic bytes per launch / its HIP-event time
                    (events on the context stream), traffic from the committed rocprofv3 PMC summary
   cpu_baseline  -- the REFERENCE itself (oracle/_ref/ref_driver: OpenGE's own ReadSorter +
@@ -51,6 +52,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "Mreads/sec sort+dedup (and realign intervals/sec), 1/2/4/8 MI355X"
+BGZF_EOF = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
 # int32 VALU lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md: SIMD-32, a wave64
 # VALU instruction issues over 2 cycles)
@@ -88,6 +90,40 @@ def log(msg: str) -> None:
 
 
 # ------------------------------------------------------------------------------------------- helpers
+class DevBuf:
+    """Device bytes from the library's own allocator (hipMalloc), not torch's: the chain's workspace later
+    takes over these bytes, and re-acquiring HBM the torch allocator released cost ~1 s per 85 GB on the
+    box (tools/exp_alloc2.py: 0.95 s) against ~1 ms after a hipFree (profiles/r05g_alloc.txt)."""
+
+    def __init__(self, ctx, L, nbytes: int):
+        import ctypes as C
+        self.ctx, self.L = ctx, L
+        p = C.c_void_p()
+        L.check(L.lib().oge_dev_alloc(ctx.h, nbytes, C.byref(p)), ctx.h)
+        self.ptr, self.nbytes = p.value, nbytes
+
+    def put(self, off: int, data: bytes) -> None:
+        b = bytearray(data)
+        import ctypes as C
+        src = (C.c_char * len(b)).from_buffer(b)
+        self.L.check(self.L.lib().oge_memcpy(self.ctx.h, self.ptr + off, C.addressof(src), len(b), 1), self.ctx.h)
+
+    def get(self, off: int, nbytes: int, host_ptr: int | None = None):
+        """nbytes at off -> numpy array (or into host_ptr)"""
+        import numpy as np
+        out = None
+        if host_ptr is None:
+            out = np.empty(nbytes, np.uint8)
+            host_ptr = out.ctypes.data
+        self.L.check(self.L.lib().oge_memcpy(self.ctx.h, host_ptr, self.ptr + off, nbytes, 2), self.ctx.h)
+        return out
+
+    def free(self) -> None:
+        if self.ptr:
+            self.L.check(self.L.lib().oge_dev_free(self.ctx.h, self.ptr), self.ctx.h)
+            self.ptr = 0
+
+
 def bam_header_bytes(header_text: str) -> bytes:
     """BamSerializer::open's header block (util/bam_serializer.h:54-76): magic, text, reference list."""
     refs = []
@@ -350,16 +386,16 @@ def cpu_baseline_reference(sample_reads: int, threads: int) -> dict:
             "seconds": round(dt, 2), "reference_log_tail": marked}
 
 
-def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, "torch.Tensor", int, object]:
+def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, DevBuf, int, object]:
     """Records generated straight into HBM after a `hlen`-byte BAM header prefix (the buffer later
     becomes the input file); the sort+dedup device pipeline alone over the resident records."""
     d_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
     ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), None)
     ctx.sync()
     B = int(d_offs[-1].item())
-    S = torch.empty(hlen + B + 64, dtype=torch.uint8, device=dev)
+    S = DevBuf(ctx, L, hlen + B + 64)
     d_offs += hlen
-    ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), S.data_ptr())
+    ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), S.ptr)
     ctx.sync()
     import ctypes as C
     buf = C.create_string_buffer(1 << 16)
@@ -371,7 +407,7 @@ def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, "torch.Tenso
         d_out = torch.empty(B + 64, dtype=torch.uint8, device=dev)
         d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         d_perm = torch.empty(n, dtype=torch.int32, device=dev)
-        step = lambda: ctx.sort_markdup_dev(S.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(),
+        step = lambda: ctx.sort_markdup_dev(S.ptr, d_offs.data_ptr(), n, opts, d_perm.data_ptr(),
                                             d_out.data_ptr(), d_out_off.data_ptr())
         step()  # first call: workspace growth, code-object load
         torch.cuda.synchronize(dev)
@@ -411,21 +447,25 @@ def zlib6_sample_ratio(S, off: int, nbytes: int, sample: int = 32 << 20) -> dict
     from concurrent.futures import ThreadPoolExecutor
     pay = 65280
     n = max(pay, min(nbytes, sample) // pay * pay)
-    h = S[off:off + n].cpu().numpy().tobytes()
+    h = S.get(off, n).tobytes()
     with ThreadPoolExecutor(16) as ex:
         z = sum(ex.map(lambda i: len(zlib.compress(h[i:i + pay], 6)) - 6 + 26, range(0, len(h), pay)))
     return {"ratio": round(z / len(h), 4), "sample_bytes": len(h),
             "what": "zlib level 6 per 65,280-byte payload + BGZF framing, first bytes of the same record stream"}
 
 
-def build_input(ctx, L, torch, dev, S, total: int, level: int) -> tuple["torch.Tensor", int]:
+def build_input(ctx, L, S: DevBuf, total: int, level: int) -> tuple[DevBuf, int]:
     """The input BAM file in HBM: the library's GPU deflate of [header][records] at `level` plus the
     EOF block, in a buffer of exactly its size (the bound-sized staging buffer is freed)."""
     bound = int(L.lib().oge_bgzf_bound(total))
-    Z = torch.empty(bound + 64, dtype=torch.uint8, device=dev)
-    zb = ctx.bgzf_deflate_dev(S.data_ptr(), total, level, Z.data_ptr(), bound)
+    Z = DevBuf(ctx, L, bound + 64)
+    zb = ctx.bgzf_deflate_dev(S.ptr, total, level, Z.ptr, bound)
     ctx.sync()
-    return Z, zb
+    d_z = DevBuf(ctx, L, zb + 28 + 64)
+    L.check(L.lib().oge_memcpy(ctx.h, d_z.ptr, Z.ptr, zb, 3), ctx.h)
+    d_z.put(zb, BGZF_EOF)
+    Z.free()
+    return d_z, zb + 28
 
 
 def main():
@@ -484,35 +524,29 @@ def main():
         print(json.dumps(kres), flush=True)
         ctx.close()
         return
-    S[:len(hb)].copy_(torch.frombuffer(bytearray(hb), dtype=torch.uint8).to(dev))
+    S.put(0, hb)
     total = len(hb) + B
     seq_bytes = n * ((p.read_len + 1) // 2)
 
     # ---- the input BAM file in HBM (level-6 BGZF, GPU deflate), staging freed
     zref = zlib6_sample_ratio(S, len(hb), B)
-    Z, zb = build_input(ctx, L, torch, dev, S, total, args.level)
-    del S
-    torch.cuda.empty_cache()
-    d_z = torch.empty(zb + 28 + 64, dtype=torch.uint8, device=dev)
-    d_z[:zb].copy_(Z[:zb])
-    d_z[zb:zb + 28].copy_(torch.tensor(list(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")),
-                                       dtype=torch.uint8, device=dev))
-    zbytes = zb + 28
-    del Z
-    torch.cuda.empty_cache()
+    d_z, zbytes = build_input(ctx, L, S, total, args.level)
+    S.free()
     torch.cuda.synchronize(dev)
     log(f"input BAM file in HBM: {zbytes / 1e9:.2f} GB (ratio {zbytes / total:.3f})")
 
     # ---- e2e steps: BAM file in HBM -> mergesort -M chain -> BAM file in HBM
     mopts = L.mergesort_opts(level=args.level, mark_duplicates=1)
-    step = lambda: ctx.mergesort_bgzf_dev(d_z.data_ptr(), zbytes, mopts)
-    warm = []
+    step = lambda: ctx.mergesort_bgzf_dev(d_z.ptr, zbytes, mopts)
+    warm, cold_ws = [], None
     for _ in range(args.warmup):
         torch.cuda.synchronize(dev)
         tw = time.perf_counter()
         step()
         torch.cuda.synchronize(dev)
         warm.append(round((time.perf_counter() - tw) * 1e3, 1))
+        if cold_ws is None:  # the first call on this context: its workspace allocations
+            cold_ws = {"allocations": ctx.counter("ws_allocs"), "ms": round((ctx.counter("ws_alloc_us") or 0) / 1e3, 1)}
         log(f"warmup step {warm[-1]} ms; workspace allocations {ctx.counter('ws_allocs')} taking "
             f"{(ctx.counter('ws_alloc_us') or 0) / 1e3:.1f} ms; stages {stage_ms(ctx, E2E_STAGES)}")
     tot = {}
@@ -540,23 +574,35 @@ def main():
     roof = roofline_entry(s_dom, kinfo[s_dom], t_dom, B)
     others = [roofline_entry(s, kinfo[s], sms[s], B) for s in kinfo if sms.get(s, 0.0) > 0]
 
-    # ---- PCIe-inclusive run (compressed bytes only cross PCIe)
+    # ---- PCIe-inclusive run (compressed bytes only cross PCIe): the file in page-locked host memory,
+    #      oge_mergesort_bgzf_host overlaps its upload with the framing index and inflate, and the output's
+    #      download with the deflate
     pcie = None
     if not args.no_pcie and not args.e2e_only:
         hz = torch.empty(zbytes, dtype=torch.uint8, pin_memory=True)
-        hz.copy_(d_z[:zbytes])
-        ho = torch.empty(max(out_bytes, 1) + (1 << 20), dtype=torch.uint8, pin_memory=True)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        d_z[:zbytes].copy_(hz, non_blocking=True)
-        d_out, ob, _, _ = step()
-        L.check(L.lib().oge_memcpy(ctx.h, ho.data_ptr(), d_out, ob, 2), ctx.h)
-        torch.cuda.synchronize(dev)
-        tp = time.perf_counter() - t1
-        pcie = {"what": "upload of the input BAM file from page-locked host memory + the e2e step + download of "
-                        "the output BAM file, one run", "seconds": round(tp, 3), "mreads_per_s": round(n / tp / 1e6, 1),
-                "bytes_up": zbytes, "bytes_down": ob}
+        d_z.get(0, zbytes, hz.data_ptr())
+        d_z.free()
+        del step
+        ocap = out_bytes + (1 << 20)
+        ho = torch.empty(ocap, dtype=torch.uint8, pin_memory=True)
+        runs = []
+        for _ in range(2):  # the first call grows the upload / segment buffers
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            ob, nr2, nd2 = ctx.mergesort_bgzf_host(hz.data_ptr(), zbytes, mopts, ho.data_ptr(), ocap)
+            runs.append(time.perf_counter() - t1)
+        assert (ob, nr2, nd2) == (out_bytes, nr, nd), (ob, nr2, nd2, out_bytes, nr, nd)
+        tp = runs[-1]
+        pcie = {"what": "oge_mergesort_bgzf_host: the input BAM file in page-locked host memory -> the output BAM "
+                        "file in page-locked host memory; upload overlapped with the host framing index and the "
+                        "inflate, download with the deflate", "seconds": round(tp, 3),
+                "first_call_seconds": round(runs[0], 3), "mreads_per_s": round(n / tp / 1e6, 1),
+                "bytes_up": zbytes, "bytes_down": ob, "stages_ms": stage_ms(ctx, E2E_STAGES)}
+        log(f"pcie-inclusive: {tp:.3f} s (first call {runs[0]:.3f} s); stages {pcie['stages_ms']}")
         del hz, ho
+    else:
+        d_z.free()
+        del step
 
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "Mreads/s", "n_gpus": 1, "steps": K,
@@ -571,9 +617,10 @@ def main():
                    "deflate": {"search": DEFLATE_SEARCH, "gpu_ratio_input_file": round(zbytes / total, 4),
                                "gpu_ratio_output_file": round(out_bytes / total, 4), "zlib6_sample": zref}},
         "roofline": roof, "roofline_stages": others, "stages_ms": sms, "warmup_ms": warm,
+        "cold_ms": warm[0] if warm else None, "cold_over_warm": round(warm[0] / ms_step, 2) if warm else None,
+        "cold_workspace": cold_ws,
         "kernel_step": kres, "pcie_inclusive": pcie,
     }
-    del d_z
     torch.cuda.empty_cache()
     if not args.no_realign and not args.e2e_only:
         log("realign leg")

@@ -139,3 +139,47 @@ def test_pipeline_program_line_and_levels(ctx, tmp_path):
     h = bamutil.read_bam(tmp_path / "p.bam")[0]
     pg = [l for l in h.splitlines() if l.startswith("@PG")]
     assert pg[-1] == "@PG\tID:openge\tCL:openge mergesort -M x\tVN:0.3-dev"  # after the input's own @PG lines
+
+
+def _run_host_pipeline(ctx, src_bytes: bytes, **kw):
+    hz = torch.from_numpy(np.frombuffer(src_bytes, np.uint8).copy()).pin_memory()
+    cap = len(src_bytes) * 2 + (1 << 20)
+    ho = torch.empty(cap, dtype=torch.uint8).pin_memory()
+    o = L.mergesort_opts(**kw)
+    nb, nr, nd = ctx.mergesort_bgzf_host(hz.data_ptr(), len(src_bytes), o, ho.data_ptr(), cap)
+    return ho[:nb].numpy().tobytes(), nr, nd
+
+
+@pytest.mark.parametrize("groups,seg", [("8", "32768"), ("7", "3"), ("1", "1"), ("64", "2")])
+def test_host_pipeline_equals_device_chain(ctx, monkeypatch, tmp_path, groups, seg):
+    """oge_mergesort_bgzf_host (file in host memory, chunked upload, host framing index, segmented
+    deflate with the copies down overlapped) writes the same bytes as the chain on a resident file."""
+    monkeypatch.setenv("OGE_HOSTPIPE_GROUPS", groups)
+    monkeypatch.setenv("OGE_HOSTPIPE_SEG_BLOCKS", seg)
+    p = L.synth_params(60_000, preset="c2", seed=11)
+    recs, offs, hdr = L.synth_host(p)
+    L.write_bam(tmp_path / "in.bam", hdr, recs, offs, len(offs) - 1, level=6)
+    src = (tmp_path / "in.bam").read_bytes()
+    for kw in ({"mark_duplicates": 1}, {}, {"mark_duplicates": 1, "remove_duplicates": 1, "level": 1}):
+        want = _run_pipeline(ctx, src, **kw)
+        got = _run_host_pipeline(ctx, src, **kw)
+        assert got[1:] == want[1:] and got[0] == want[0], kw
+
+
+@pytest.mark.parametrize("name", ["208.yhet.bam", "simple.bam"])
+def test_host_pipeline_reference_inputs(ctx, monkeypatch, name):
+    monkeypatch.setenv("OGE_HOSTPIPE_GROUPS", "5")
+    monkeypatch.setenv("OGE_HOSTPIPE_SEG_BLOCKS", "1")
+    src = (GOLDEN / "inputs" / name).read_bytes()
+    assert _run_host_pipeline(ctx, src, mark_duplicates=1) == _run_pipeline(ctx, src, mark_duplicates=1)
+
+
+def test_host_pipeline_errors(ctx):
+    z = (GOLDEN / "inputs" / "208.truncated.bam").read_bytes()
+    with pytest.raises(L.OgeError, match="truncated"):
+        _run_host_pipeline(ctx, z, mark_duplicates=1)
+    src = (GOLDEN / "inputs" / "208.yhet.bam").read_bytes()
+    hz = np.frombuffer(src, np.uint8).copy()
+    ho = np.empty(64, np.uint8)
+    with pytest.raises(L.OgeError, match="too small"):
+        ctx.mergesort_bgzf_host(hz.ctypes.data, len(src), L.mergesort_opts(), ho.ctypes.data, len(ho))
