@@ -91,9 +91,10 @@ def log(msg: str) -> None:
 
 # ------------------------------------------------------------------------------------------- helpers
 class DevBuf:
-    """Device bytes from the library's own allocator (hipMalloc), not torch's: the chain's workspace later
-    takes over these bytes, and re-acquiring HBM the torch allocator released cost ~1 s per 85 GB on the
-    box (tools/exp_alloc2.py: 0.95 s) against ~1 ms after a hipFree (profiles/r05g_alloc.txt)."""
+    """Device bytes from the library's allocator, or a view of one of the chain's reserved record arenas
+    (oge_mergesort_reserve): the records and the staging file of the setup live in the arenas the chain
+    then uses, so its first call does not re-acquire HBM the setup freed (the driver wipes freed HBM
+    before handing it out again, ~35-45 GB/s: 4.3 s for the two 85.6 GB arenas, profiles/r05i_bench.log)."""
 
     def __init__(self, ctx, L, nbytes: int):
         import ctypes as C
@@ -119,9 +120,18 @@ class DevBuf:
         return out
 
     def free(self) -> None:
-        if self.ptr:
+        if self.ptr and self.owned:
             self.L.check(self.L.lib().oge_dev_free(self.ctx.h, self.ptr), self.ctx.h)
-            self.ptr = 0
+        self.ptr = 0
+
+    owned = True
+
+    @classmethod
+    def view(cls, ctx, L, ptr: int, nbytes: int) -> "DevBuf":
+        """bytes the library owns (one of the chain's reserved arenas): free() only forgets them"""
+        b = cls.__new__(cls)
+        b.ctx, b.L, b.ptr, b.nbytes, b.owned = ctx, L, ptr, nbytes, False
+        return b
 
 
 def bam_header_bytes(header_text: str) -> bytes:
@@ -393,7 +403,8 @@ def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, DevBuf, int,
     ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), None)
     ctx.sync()
     B = int(d_offs[-1].item())
-    S = DevBuf(ctx, L, hlen + B + 64)
+    X, Y, cap = ctx.mergesort_reserve(hlen + B)
+    S = DevBuf.view(ctx, L, Y, cap)  # the chain's sorted-records arena holds the generated records
     d_offs += hlen
     ctx.synth_range_dev(p, 0, n, d_offs.data_ptr(), S.ptr)
     ctx.sync()
@@ -404,11 +415,11 @@ def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, DevBuf, int,
     opts, keep = L.markdup_opts_from_header(hdr_text, p.n_ref)
     res = {"skipped": True}
     if args.kernel_steps > 0:
-        d_out = torch.empty(B + 64, dtype=torch.uint8, device=dev)
+        d_out = DevBuf.view(ctx, L, X, cap)
         d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         d_perm = torch.empty(n, dtype=torch.int32, device=dev)
         step = lambda: ctx.sort_markdup_dev(S.ptr, d_offs.data_ptr(), n, opts, d_perm.data_ptr(),
-                                            d_out.data_ptr(), d_out_off.data_ptr())
+                                            d_out.ptr, d_out_off.data_ptr())
         step()  # first call: workspace growth, code-object load
         torch.cuda.synchronize(dev)
         tot = {s: 0.0 for s in KERNEL_STAGES + SUB_STAGES}
@@ -428,8 +439,10 @@ def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, DevBuf, int,
                "gather_roofline": {"kernel": "k_gather16", "achieved_GBps": round(2 * B / tg / 1e9, 1) if tg else None,
                                    "frac": round(2 * B / tg / 1e9 / HBM_PEAK_GBS, 4) if tg else None,
                                    "algorithmic_bytes": 2 * B}}
-        del d_out, d_out_off, d_perm
+        d_out.free()
+        del d_out_off, d_perm
     del d_offs
+    torch.cuda.empty_cache()
     return res, S, B, hdr_text
 
 
@@ -456,11 +469,15 @@ def zlib6_sample_ratio(S, off: int, nbytes: int, sample: int = 32 << 20) -> dict
 
 def build_input(ctx, L, S: DevBuf, total: int, level: int) -> tuple[DevBuf, int]:
     """The input BAM file in HBM: the library's GPU deflate of [header][records] at `level` plus the
-    EOF block, in a buffer of exactly its size (the bound-sized staging buffer is freed)."""
+    EOF block, in a buffer of exactly its size (the records S and the bound-sized staging buffer are
+    freed)."""
     bound = int(L.lib().oge_bgzf_bound(total))
-    Z = DevBuf(ctx, L, bound + 64)
+    X, _, cap = ctx.mergesort_reserve(total)
+    Z = DevBuf.view(ctx, L, X, cap)  # the chain's other arena stages the compressed file
+    assert cap >= bound + 64
     zb = ctx.bgzf_deflate_dev(S.ptr, total, level, Z.ptr, bound)
     ctx.sync()
+    S.free()
     d_z = DevBuf(ctx, L, zb + 28 + 64)
     L.check(L.lib().oge_memcpy(ctx.h, d_z.ptr, Z.ptr, zb, 3), ctx.h)
     d_z.put(zb, BGZF_EOF)
@@ -531,7 +548,6 @@ def main():
     # ---- the input BAM file in HBM (level-6 BGZF, GPU deflate), staging freed
     zref = zlib6_sample_ratio(S, len(hb), B)
     d_z, zbytes = build_input(ctx, L, S, total, args.level)
-    S.free()
     torch.cuda.synchronize(dev)
     log(f"input BAM file in HBM: {zbytes / 1e9:.2f} GB (ratio {zbytes / total:.3f})")
 

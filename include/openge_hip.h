@@ -144,6 +144,11 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
                          const oge_markdup_opts *opts, uint32_t *d_perm, uint8_t *d_out, uint64_t *d_out_off,
                          uint64_t *n_dup_out);
 
+/* Allocate the mergesort chain's two record arenas for streams of up to `total` decompressed bytes now
+ * (a long-running caller reserves them once; HBM re-acquired inside a call is wiped by the driver first,
+ * ~35-45 GB/s).  *x / *y (cap bytes each) may hold the caller's data between chain calls. */
+int oge_mergesort_reserve(oge_ctx *ctx, uint64_t total, void **x, void **y, uint64_t *cap);
+
 /* ---- the whole mergesort chain on a BAM file resident in HBM -------------------------- */
 /* FileReader -> ReadSorter -> [MarkDuplicates] -> FileWriter as MergeSortCommand::runCommand wires
  * it (commands/command_mergesort.cpp:68-117), every stage on the device: BGZF framing index,

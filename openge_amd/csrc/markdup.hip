@@ -251,15 +251,20 @@ __global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ 
                                                     const RecMeta *__restrict__ meta, KeyLayout L, uint64_t *__restrict__ hi,
                                                     uint64_t *__restrict__ lo, uint2 *__restrict__ idx, uint32_t *__restrict__ val,
                                                     uint64_t *__restrict__ hk, const uint64_t *__restrict__ skeys,
-                                                    int64_t *__restrict__ pax, unsigned long long *__restrict__ dev) {
+                                                    int64_t *__restrict__ pax, unsigned long long *__restrict__ dev,
+                                                    unsigned int *__restrict__ win_bad) {
     uint32_t p = blockIdx.x * kT + threadIdx.x;
     bool has = false;
     int64_t ax = 0, cx = 0;
     if (p < np) {
     uint32_t a = (uint32_t)(pairs[p] >> 32), b = (uint32_t)pairs[p];  // a seen first (smaller record index)
+    // win_bad: pairs from the windowed join (b without kSortPair) whose names differ are counted
+    const bool from_sort = win_bad && (b & 0x80000000u);
+    if (win_bad) b &= 0x7fffffffu;
     if (a > b) { uint32_t t = a; a = b; b = t; }
     const RecMeta A = meta[a], B = meta[b];
     const uint64_t bad = same_pair_key(recs, A, B, L.split_k) ? 0ull : (1ull << 63);
+    if (bad && win_bad && !from_sort) atomicAdd(win_bad, 1u);
     const uint64_t ma = A.m, mb = B.m;
     const int32_t sa = A.seq, ca = A.coord, sb_ = B.seq, cb = B.coord;
     const bool reva = (ma & OGE_M_REV) != 0, revb = (mb & OGE_M_REV) != 0;
@@ -744,6 +749,152 @@ __global__ __launch_bounds__(kT) void k_apply_desc(const uint64_t *__restrict__ 
     }
 }
 
+// ---- windowed mate join (records in coordinate order, one GPU) ----
+// Mates of a proper pair sit within ~ insert size / read spacing records of each other in coordinate
+// order, so most of the ReadEndsMap's pairs are found in a window, without the global hash sort:
+//   k_mate_win    tile of kMjT records + kMjW on each side in an LDS table of candidate fingerprints
+//                 (count, first and last window slot): a tile record whose fingerprint occurs exactly
+//                 twice in its window gets the other occurrence as partner
+//   k_mate_agree  i and j = partner[i] agree (partner[j] == i, equal hash bits): a window pair, owned by
+//                 the smaller index; anything else is a leftover, its hash bits into a global set (a
+//                 bitmap filter in front of an open-addressing table)
+//   k_mate_check  a window pair whose hash is in that set gives both ends to the leftovers: its key has
+//                 other occurrences (first-seen / second-seen pairing must see them all)
+// The leftovers take the sort-based join; every hash bit pattern then occurs exactly twice among the
+// window pairs' records (the same provisional pair the sort path forms from a run of two), or its
+// records all went the sort path.  A window pair whose names differ (a 48-bit collision) makes the caller
+// redo the join by sort (k_pair_build counts them).
+constexpr uint32_t kMjT = 1024, kMjW = 512, kMjSlots = 4096;
+static_assert(kMjT + 2 * kMjW <= kMjSlots / 2, "window table at most half full");
+constexpr uint32_t kNone = 0xffffffffu, kSortPair = 0x80000000u;
+
+__device__ __forceinline__ bool is_cand(const uint32_t *__restrict__ cpos, uint64_t i) { return cpos[i + 1] != cpos[i]; }
+__device__ __forceinline__ uint32_t mj_fp(uint64_t h) {
+    const uint32_t x = (uint32_t)h ^ (uint32_t)(h >> 32) * 0x9E3779B1u;
+    return x ? x : 1u;
+}
+
+__global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ cpos, const uint64_t *__restrict__ cval, uint64_t n,
+                                                   uint32_t ib, uint32_t *__restrict__ partner) {
+    __shared__ uint32_t key[kMjSlots], lo[kMjSlots], hi[kMjSlots], cnt[kMjSlots];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t s = t; s < kMjSlots; s += kMjT) key[s] = 0, lo[s] = kNone, hi[s] = 0, cnt[s] = 0;
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * kMjT, w0 = t0 - (int64_t)kMjW;
+    for (uint32_t w = t; w < kMjT + 2 * kMjW; w += kMjT) {
+        const int64_t i = w0 + (int64_t)w;
+        if (i < 0 || (uint64_t)i >= n || !is_cand(cpos, (uint64_t)i)) continue;
+        const uint32_t f = mj_fp(cval[i] >> ib);
+        uint32_t s = (f * 2654435761u) >> 20;  // 12 bits: kMjSlots
+        for (;;) {
+            const uint32_t o = atomicCAS(&key[s], 0u, f);
+            if (o == 0u || o == f) break;
+            s = (s + 1) & (kMjSlots - 1);
+        }
+        atomicAdd(&cnt[s], 1u);
+        atomicMin(&lo[s], w);
+        atomicMax(&hi[s], w);
+    }
+    __syncthreads();
+    const uint64_t i = (uint64_t)t0 + t;
+    if (i >= n) return;
+    uint32_t r = kNone;
+    if (is_cand(cpos, i)) {
+        const uint32_t f = mj_fp(cval[i] >> ib), w = t + kMjW;
+        uint32_t s = (f * 2654435761u) >> 20;
+        while (key[s] != f) s = (s + 1) & (kMjSlots - 1);
+        if (cnt[s] == 2) r = (uint32_t)(w0 + (int64_t)(lo[s] == w ? hi[s] : lo[s]));
+    }
+    partner[i] = r;
+}
+
+__device__ __forceinline__ uint32_t mj_slot(uint64_t key, uint32_t mask) { return (uint32_t)(mix64(key) & mask); }
+__device__ __forceinline__ uint32_t mj_bit(uint64_t key, uint32_t bmask) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & bmask; }
+constexpr int kMjProbes = 64;
+
+// leftovers (and their keys into the conflict set: a bitmap filter in front of an open-addressing table)
+__global__ __launch_bounds__(kT) void k_mate_agree(const uint32_t *__restrict__ cpos, const uint64_t *__restrict__ cval, uint64_t n,
+                                                   uint32_t ib, const uint32_t *__restrict__ partner, uint32_t *__restrict__ mate,
+                                                   uint32_t *__restrict__ lflag, unsigned long long *__restrict__ tab, uint32_t mask,
+                                                   uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf) {
+    const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (i > n) return;
+    if (i == n) { lflag[n] = 0; return; }
+    uint32_t m = kNone, lf = 0;
+    if (is_cand(cpos, i)) {
+        const uint32_t j = partner[i];
+        const uint64_t h = cval[i] >> ib;
+        if (j != kNone && partner[j] == (uint32_t)i && (cval[j] >> ib) == h) {
+            if (i < j) m = j;
+        } else {
+            lf = 1;
+            const unsigned long long key = h + 1;
+            const uint32_t b = mj_bit(key, bmask);
+            atomicOr(&bits[b >> 5], 1u << (b & 31));
+            uint32_t s = mj_slot(key, mask);
+            int p = 0;
+            for (; p < kMjProbes; ++p) {
+                const unsigned long long o = atomicCAS(&tab[s], 0ull, key);
+                if (o == 0ull || o == key) break;
+                s = (s + 1) & mask;
+            }
+            if (p == kMjProbes) atomicOr(ovf, 1u);
+        }
+    }
+    mate[i] = m;
+    lflag[i] = lf;
+}
+
+// also writes pflag[i] (a pair is owned by i) for every record
+__global__ __launch_bounds__(kT) void k_mate_check(const uint64_t *__restrict__ cval, uint64_t n, uint32_t ib,
+                                                   const unsigned long long *__restrict__ tab, uint32_t mask,
+                                                   const uint32_t *__restrict__ bits, uint32_t bmask, uint32_t *__restrict__ mate,
+                                                   uint32_t *__restrict__ lflag, uint32_t *__restrict__ pflag) {
+    const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (i > n) return;
+    if (i == n) { pflag[n] = 0; return; }
+    const uint32_t m = mate[i];
+    uint32_t own = 0;
+    if (m != kNone) {
+        own = 1;
+        const unsigned long long key = (cval[i] >> ib) + 1;
+        const uint32_t b = mj_bit(key, bmask);
+        uint32_t s = mj_slot(key, mask);
+        bool hit = ((bits[b >> 5] >> (b & 31)) & 1u) != 0;  // a probe run longer than the insert bound: only after an overflow
+        for (int p = 0; hit && p < kMjProbes; ++p) {
+            const unsigned long long o = tab[s];
+            if (o == key) break;
+            if (o == 0ull) { hit = false; break; }
+            s = (s + 1) & mask;
+        }
+        if (hit) {
+            mate[i] = kNone;
+            lflag[i] = 1;
+            lflag[m] = 1;
+            own = 0;
+        }
+    }
+    pflag[i] = own;
+}
+
+// the sort path's pairs of leftovers (a << 32 | b, a < b) -> mate[a] = b | kSortPair, pflag[a] = 1
+__global__ __launch_bounds__(kT) void k_mate_scatter(const uint64_t *__restrict__ pairs, uint32_t np, uint32_t *__restrict__ mate,
+                                                     uint32_t *__restrict__ pflag) {
+    const uint32_t p = blockIdx.x * kT + threadIdx.x;
+    if (p >= np) return;
+    uint32_t a = (uint32_t)(pairs[p] >> 32), b = (uint32_t)pairs[p];
+    if (a > b) { const uint32_t x = a; a = b; b = x; }
+    mate[a] = b | kSortPair;
+    pflag[a] = 1;
+}
+
+// pairs in first-record order from the scanned owner flags
+__global__ __launch_bounds__(kT) void k_mate_compact(const uint32_t *__restrict__ pos, const uint32_t *__restrict__ mate, uint64_t n,
+                                                     uint64_t *__restrict__ pairs) {
+    const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
+    if (i < n && pos[i + 1] != pos[i]) pairs[pos[i]] = (i << 32) | mate[i];
+}
+
 uint32_t bits_for(uint64_t v) {  // bits to hold values 0..v
     uint32_t b = 0;
     while (b < 64 && (v >> b)) ++b;
@@ -880,16 +1031,12 @@ int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *
     return OGE_OK;
 }
 
-int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t *recs, const RecMeta *meta, uint64_t n,
-                      const OgeMdFrags &f, OgeMdPairs *P) {
-    KeyLayout L;
-    int rc = md_layout(ctx, opts, &L);
-    if (rc) return rc;
-    *P = OgeMdPairs{};
+// The sort-based ReadEndsMap pairing (mark_duplicates.cpp:210-245) of the candidates flagged by cpos
+// (exclusive scan of the flags, nc of them) -> pairs a << 32 | b (a first seen), *np of them, in
+// candidate-hash order, in ws "md_pairs"; "md_pairs2" is the spare of the same size.
+static int join_sorted(oge_ctx *ctx, const CandKey &ckl, const uint8_t *recs, const RecMeta *meta, uint64_t n, const uint32_t *cpos,
+                       const uint64_t *cval, uint32_t nc, uint64_t **pairs_out, uint64_t **spare_out, uint32_t *np_out) {
     unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
-    if (!cnt) return OGE_ERR_HIP;
-    const CandKey ckl = md_candkey(opts, n);
-    const uint32_t nc = f.nc;
     const uint64_t nc1 = (uint64_t)nc + 1;
     uint64_t *ck = (uint64_t *)ctx->scratch("md_ck", nc1 * 8);
     uint64_t *ck2 = (uint64_t *)ctx->scratch("md_ck2", nc1 * 8);
@@ -899,14 +1046,13 @@ int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t 
     uint64_t *pairs = (uint64_t *)ctx->scratch("md_pairs", (nc1 / 2 + 1) * 8);
     uint64_t *pairs2 = (uint64_t *)ctx->scratch("md_pairs2", (nc1 / 2 + 1) * 8);
     uint32_t *slow = (uint32_t *)ctx->scratch("md_slow", nc1 * 4);
-    if (!ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !slow) return OGE_ERR_HIP;
+    if (!cnt || !ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !slow) return OGE_ERR_HIP;
     if (n) {
-        hipLaunchKernelGGL(k_cand_pack, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)f.cpos,
-                           (const uint64_t *)f.cval, n, ck);
+        hipLaunchKernelGGL(k_cand_pack, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, cpos, cval, n, ck);
         OGE_LAUNCH_CHECK(ctx);
     }
     uint64_t *sk;
-    rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, ((1ull << ckl.hb) - 1) << ckl.ib, &sk, nullptr);
+    int rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, ((1ull << ckl.hb) - 1) << ckl.ib, &sk, nullptr);
     if (rc) return rc;
     OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + 2, 0, 4, ctx->stream));
     hipLaunchKernelGGL(k_pair_runs, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)sk, (uint64_t)nc, ckl,
@@ -930,10 +1076,16 @@ int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t 
     hipLaunchKernelGGL(k_pair_compact_scan, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)pflag,
                        (const uint64_t *)sparse, (uint64_t)nc, pairs);
     OGE_LAUNCH_CHECK(ctx);
-    // order the pairs by first-mate position: k_pair_build then reads both summaries from nearby rows
-    uint64_t *spairs = pairs;
-    rc = oge_radix_sort_pairs(ctx, pairs, nullptr, pairs2, nullptr, np, bits_mask_hi32(n), &spairs, nullptr);
-    if (rc) return rc;
+    *pairs_out = pairs;
+    *spare_out = pairs2;
+    *np_out = np;
+    return OGE_OK;
+}
+
+// The pair ReadEnds of np pairs in first-record order (k_pair_build).  win_bad (optional): counts the
+// windowed join's pairs whose names differ.
+static int pair_build(oge_ctx *ctx, const KeyLayout &L, const uint8_t *recs, const RecMeta *meta, const OgeMdFrags &f,
+                      const uint64_t *spairs, uint32_t np, OgeMdPairs *P, unsigned int *win_bad) {
     P->np = np;
     if (!np) return OGE_OK;
     P->hi = (uint64_t *)ctx->scratch("md_hi", (uint64_t)np * 8);
@@ -946,11 +1098,118 @@ int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t 
         P->pax = (int64_t *)ctx->scratch("md_pax", (uint64_t)np * 8);
         P->dev = f.dev + 2 * kDevSlots;
         if (!P->pax) return OGE_ERR_HIP;
+        // the pair half of the deviation slots: a redone join starts them again
+        OGE_HIP_TRY(ctx, hipMemsetAsync(P->dev, 0, 2 * kDevSlots * sizeof(unsigned long long), ctx->stream));
     }
-    hipLaunchKernelGGL(k_pair_build, dim3(oge_ceil_div(np, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)spairs, np, recs,
-                       meta, L, P->hi, P->lo, P->idx, P->val, P->hk, f.skeys, P->pax, P->dev);
+    hipLaunchKernelGGL(k_pair_build, dim3(oge_ceil_div(np, kT)), dim3(kT), 0, ctx->stream, spairs, np, recs, meta, L, P->hi, P->lo,
+                       P->idx, P->val, P->hk, f.skeys, P->pax, P->dev, win_bad);
     OGE_LAUNCH_CHECK(ctx);
     return OGE_OK;
+}
+
+static bool mate_win_enabled() {
+    const char *e = getenv("OGE_MD_MATEWIN");  // "0": the sort-based join only (A/B, tests); read per call
+    return !(e && e[0] == '0');
+}
+
+// The windowed join (see k_mate_win) for records in coordinate order; *done = false when it cannot
+// decide (the conflict set overflowed, or a window pair's names differ): the caller runs the sort path.
+static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, const uint8_t *recs, const RecMeta *meta, uint64_t n,
+                       const OgeMdFrags &f, OgeMdPairs *P, bool *done) {
+    *done = false;
+    unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
+    uint32_t *partner = (uint32_t *)ctx->scratch("md_mpart", (n + 1) * 4);
+    uint32_t *mate = (uint32_t *)ctx->scratch("md_mate", (n + 1) * 4);
+    uint32_t *lflag = (uint32_t *)ctx->scratch("md_lflag", (n + 1) * 4);
+    uint32_t *oflag = (uint32_t *)ctx->scratch("md_oflag", (n + 1) * 4);
+    uint64_t *wpairs = (uint64_t *)ctx->scratch("md_wpairs", (n / 2 + 1) * 8);
+    if (!cnt || !partner || !mate || !lflag || !oflag || !wpairs) return OGE_ERR_HIP;
+    // the conflict set: a table of >= n/16 slots behind a bitmap of >= n/2 bits (a probe run past kMjProbes
+    // means too many leftovers for the window path: the sort path decides)
+    uint32_t slots = 1024, nbits = 1u << 15;
+    while (slots < n / 16 && slots < (1u << 30)) slots <<= 1;
+    while (nbits < n / 2 && nbits < (1u << 31)) nbits <<= 1;
+    unsigned long long *tab = (unsigned long long *)ctx->scratch("md_mconf", (uint64_t)slots * 8);
+    uint32_t *bits = (uint32_t *)ctx->scratch("md_mbits", nbits / 8);
+    if (!tab || !bits) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 16, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemsetAsync(tab, 0, (uint64_t)slots * 8, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemsetAsync(bits, 0, nbits / 8, ctx->stream));
+    hipLaunchKernelGGL(k_mate_win, dim3(oge_ceil_div(n, kMjT)), dim3(kMjT), 0, ctx->stream, (const uint32_t *)f.cpos,
+                       (const uint64_t *)f.cval, n, ckl.ib, partner);
+    OGE_LAUNCH_CHECK(ctx);
+    hipLaunchKernelGGL(k_mate_agree, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)f.cpos,
+                       (const uint64_t *)f.cval, n, ckl.ib, (const uint32_t *)partner, mate, lflag, tab, slots - 1, bits, nbits - 1,
+                       cnt + 1);
+    OGE_LAUNCH_CHECK(ctx);
+    hipLaunchKernelGGL(k_mate_check, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)f.cval, n, ckl.ib,
+                       (const unsigned long long *)tab, slots - 1, (const uint32_t *)bits, nbits - 1, mate, lflag, oflag);
+    OGE_LAUNCH_CHECK(ctx);
+    // the leftovers through the sort-based join, their pairs into mate[] / the owner flags
+    int rc = oge_exclusive_scan_u32(ctx, lflag, lflag, n + 1);
+    if (rc) return rc;
+    uint32_t left = 0, ovf = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&left, lflag + n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&ovf, cnt + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->counters["md_mate_left"] = left;
+    if (ovf) {
+        ctx->counters["md_mate_ovf"] = 1;
+        return OGE_OK;
+    }
+    if (left) {
+        uint64_t *lp, *spare;
+        uint32_t lnp = 0;
+        if ((rc = join_sorted(ctx, ckl, recs, meta, n, lflag, f.cval, left, &lp, &spare, &lnp))) return rc;
+        if (lnp) {
+            hipLaunchKernelGGL(k_mate_scatter, dim3(oge_ceil_div(lnp, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)lp, lnp, mate, oflag);
+            OGE_LAUNCH_CHECK(ctx);
+        }
+    }
+    // all pairs in first-record order
+    if ((rc = oge_exclusive_scan_u32(ctx, oflag, oflag, n + 1))) return rc;
+    uint32_t np = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&np, oflag + n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    hipLaunchKernelGGL(k_mate_compact, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)oflag, (const uint32_t *)mate,
+                       n, wpairs);
+    OGE_LAUNCH_CHECK(ctx);
+    OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + 2, 0, 4, ctx->stream));
+    if ((rc = pair_build(ctx, L, recs, meta, f, wpairs, np, P, cnt + 2))) return rc;
+    uint32_t bad = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&bad, cnt + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->counters["md_mate_pairs"] = np;
+    if (bad) {
+        ctx->counters["md_mate_redo"] = bad;
+        *P = OgeMdPairs{};
+        return OGE_OK;
+    }
+    *done = true;
+    return OGE_OK;
+}
+
+int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t *recs, const RecMeta *meta, uint64_t n,
+                      const OgeMdFrags &f, OgeMdPairs *P) {
+    KeyLayout L;
+    int rc = md_layout(ctx, opts, &L);
+    if (rc) return rc;
+    *P = OgeMdPairs{};
+    const CandKey ckl = md_candkey(opts, n);
+    // the windowed join: records in coordinate order (skeys) on one GPU, the default key hash, one chain
+    if (f.skeys && n && n < (1ull << 31) && opts->split_chains <= 1 && opts->debug_hash_bits <= 0 && mate_win_enabled()) {
+        bool done = false;
+        if ((rc = join_window(ctx, L, ckl, recs, meta, n, f, P, &done))) return rc;
+        if (done) return OGE_OK;
+    }
+    uint64_t *pairs, *pairs2;
+    uint32_t np = 0;
+    if ((rc = join_sorted(ctx, ckl, recs, meta, n, f.cpos, f.cval, f.nc, &pairs, &pairs2, &np))) return rc;
+    // order the pairs by first-mate position: k_pair_build then reads both summaries from nearby rows
+    uint64_t *spairs = pairs;
+    rc = oge_radix_sort_pairs(ctx, pairs, nullptr, pairs2, nullptr, np, bits_mask_hi32(n), &spairs, nullptr);
+    if (rc) return rc;
+    return pair_build(ctx, L, recs, meta, f, spairs, np, P, nullptr);
 }
 
 static int pair_groups_sorted(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t *hk, uint32_t *val, uint32_t m,

@@ -218,6 +218,23 @@ static int sort_stage(oge_ctx *ctx, uint8_t *X, uint64_t *xoff, uint64_t n, uint
     return OGE_OK;
 }
 
+// The chain's two record arenas ("pipe_x", "pipe_y": decompressed stream / output file, sorted records)
+// sized for streams of up to `total` decompressed bytes, allocated now: a service that reserves them once
+// at start-up never re-acquires tens of GB of HBM inside a call (HBM this process or another freed is
+// wiped by the driver before it is handed out again: ~35-45 GB/s, profiles/r05g_alloc.txt).  The arenas
+// are free between calls; *x / *y / *cap let the caller stage data in them meanwhile.
+extern "C" int oge_mergesort_reserve(oge_ctx *ctx, uint64_t total, void **x, void **y, uint64_t *cap_out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    (void)hipSetDevice(ctx->device);
+    const uint64_t cap = std::max<uint64_t>(total, oge_bgzf_bound(total) + (1u << 20)) + 64;
+    void *a = ctx->ws("pipe_x", cap), *b = ctx->ws("pipe_y", cap);
+    if (!a || !b) return OGE_ERR_HIP;
+    if (x) *x = a;
+    if (y) *y = b;
+    if (cap_out) *cap_out = cap;
+    return OGE_OK;
+}
+
 extern "C" int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const oge_mergesort_opts *mo,
                                       const uint8_t **d_out, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup) {
     if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
@@ -269,6 +286,15 @@ extern "C" int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_
     (void)hipSetDevice(ctx->device);
     Hold hold(ctx);
     *out_bytes = 0;
+    // OGE_HOSTPIPE_TRACE: host timestamps of the steps on stderr (where the PCIe-inclusive time goes)
+    const bool trace = getenv("OGE_HOSTPIPE_TRACE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what, uint64_t k = 0) {
+        if (trace)
+            fprintf(stderr, "[hostpipe] %8.1f ms %s %llu\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), what,
+                    (unsigned long long)k);
+    };
     hipStream_t cs = ctx->side_stream(3);
     uint8_t *dz = (uint8_t *)ctx->ws("hostpipe_z", zbytes + 64);
     if (!cs || !dz) return OGE_ERR_HIP;
@@ -290,6 +316,7 @@ extern "C" int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_
         OGE_HIP_TRY(ctx, hipMemcpyAsync(dz + o, h_z + o, std::min(C, zbytes - o), hipMemcpyHostToDevice, cs));
         OGE_HIP_TRY(ctx, hipEventRecord(e, cs));
     }
+    mark("upload queued");
     // ---- 2. the framing, on the host meanwhile
     OgeStageTimer *tm = ctx->begin_stage("bgzf_index");
     std::vector<uint64_t> d0, d1, uo;
@@ -314,6 +341,7 @@ extern "C" int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_
     }
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dix + 2 * nb, uo.data(), (nb + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
     ctx->end_stage(tm);
+    mark("host index done");
     // ---- 3. inflate: the blocks whose bytes are up, chunk after chunk (the X of the device chain)
     const uint64_t cap = std::max<uint64_t>(total, oge_bgzf_bound(total) + (1u << 20)) + 64;
     uint8_t *X = (uint8_t *)ctx->ws("pipe_x", cap);
@@ -331,16 +359,19 @@ extern "C" int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_
         }
         b = b1;
     }
+    mark("inflate queued");
     // ---- 4. records, sort (+ markdup)
     uint64_t *xoff, n;
     BamFile f;
     int rc = decode_records(ctx, X, total, &xoff, &n, &f);
     if (rc) return rc;
+    mark("records walked");
     uint8_t *src, *spare;
     uint64_t *soff, m, nd;
     rc = sort_stage(ctx, X, xoff, n, cap, f, mo, &src, &soff, &m, &nd, &spare);
     if (rc) return rc;
     (void)spare;
+    mark("sorted");
     // ---- 5. header block(s), then the records deflated segment by segment, each copied down while the
     //         next one is compressed
     const std::vector<uint8_t> hb = out_header(f, mo);
@@ -356,7 +387,9 @@ extern "C" int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_
     const uint64_t len = ends[1] - ends[0];
     const uint64_t SEG = (uint64_t)oge_bgzf::kPay * std::max<uint64_t>(1, env_u64("OGE_HOSTPIPE_SEG_BLOCKS", 32768));
     const uint64_t bnd = oge_bgzf_bound(std::min(len, SEG));
-    uint8_t *zb[2] = {(uint8_t *)ctx->ws("hostpipe_out0", bnd), (uint8_t *)ctx->ws("hostpipe_out1", bnd)};
+    // each segment is compressed at the same offset mod 256 as its place in h_out: a copy whose source
+    // and destination are co-aligned runs at the link's rate (45 GB/s otherwise, profiles/r05k_bench.log)
+    uint8_t *zb[2] = {(uint8_t *)ctx->ws("hostpipe_out0", bnd + 256), (uint8_t *)ctx->ws("hostpipe_out1", bnd + 256)};
     if (!zb[0] || !zb[1]) return OGE_ERR_HIP;
     hipEvent_t dn[2];
     OGE_HIP_TRY(ctx, hipEventCreateWithFlags(&dn[0], hipEventDisableTiming));
@@ -368,17 +401,20 @@ extern "C" int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_
         const uint64_t sl = std::min(SEG, len - s0);
         if (k >= 2) OGE_HIP_TRY(ctx, hipEventSynchronize(dn[k & 1]));  // that buffer's copy is done
         uint64_t got = 0;
-        rc = oge_bgzf_deflate_dev(ctx, src + ends[0] + s0, sl, mo->level, zb[k & 1], bnd, &got);  // returns when written
+        const uint64_t sh = ((uintptr_t)(h_out + pos)) & 255;
+        rc = oge_bgzf_deflate_dev(ctx, src + ends[0] + s0, sl, mo->level, zb[k & 1] + sh, bnd, &got);  // returns when written
         if (rc) return rc;
+        mark("segment deflated", k);
         if (pos + got + 28 > out_cap) {
             (void)hipStreamSynchronize(cs);
             return oge_fail(ctx, OGE_ERR_LIMIT, "output buffer too small");
         }
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(h_out + pos, zb[k & 1], got, hipMemcpyDeviceToHost, cs));
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(h_out + pos, zb[k & 1] + sh, got, hipMemcpyDeviceToHost, cs));
         OGE_HIP_TRY(ctx, hipEventRecord(dn[k & 1], cs));
         pos += got;
     }
     OGE_HIP_TRY(ctx, hipStreamSynchronize(cs));
+    mark("downloaded", pos);
     memcpy(h_out + pos, kBgzfEof, 28);
     *out_bytes = pos + 28;
     if (n_reads) *n_reads = m;

@@ -187,6 +187,7 @@ def lib() -> C.CDLL:
         "oge_last_error": (C.c_char_p, [vp]),
         "oge_ctx_timing": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_double)]),
         "oge_ctx_counter": (C.c_int, [vp, C.c_char_p, C.POINTER(u64)]),
+        "oge_mergesort_reserve": (C.c_int, [vp, u64, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64)]),
         "oge_version": (C.c_char_p, []),
         "oge_sort_coord": (C.c_int, [vp, vp, u64, vp, u64, i32, vp]),
         "oge_sort_coord_dev": (C.c_int, [vp, vp, vp, u64, i32, vp]),
@@ -525,6 +526,13 @@ class Context:
         check(lib().oge_mergesort_bgzf_dev(self.h, d_z, zbytes, C.byref(opts), C.byref(d), C.byref(ob), C.byref(nr),
                                            C.byref(nd)), self.h)
         return d.value or 0, ob.value, nr.value, nd.value
+
+    def mergesort_reserve(self, total: int) -> tuple[int, int, int]:
+        """Allocate the chain's two record arenas for streams of up to `total` decompressed bytes ->
+        (x, y, cap): device pointers the caller may stage data in between chain calls."""
+        x, y, cap = C.c_void_p(), C.c_void_p(), C.c_uint64()
+        check(lib().oge_mergesort_reserve(self.h, total, C.byref(x), C.byref(y), C.byref(cap)), self.h)
+        return x.value, y.value, cap.value
 
     def mergesort_bgzf_host(self, h_z: int, zbytes: int, opts: "MergesortOpts", h_out: int, out_cap: int) -> tuple[int, int, int]:
         """The chain on a BAM file in host memory (page-locked for full speed), PCIe overlapped with the

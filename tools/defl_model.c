@@ -171,7 +171,7 @@ static uint64_t payload_bits(const uint8_t *in, int n, const Cfg *c) {
             }
         }
     }
-    const int gpuchain = getenv("GPUCHAIN") != NULL;
+    const int gpuchain = getenv("GPUCHAIN") != NULL, firstv = getenv("FIRSTV") != NULL;
     for (int r = 0; c->K > 0 && r < n; r += c->R) {
         int e = r + c->R < n ? r + c->R : n;
         if (gpuchain)
@@ -192,6 +192,7 @@ static uint64_t payload_bits(const uint8_t *in, int n, const Cfg *c) {
                 if (p - (j - 1) > 32768) break;
                 uint32_t wj = rd32(in + j - 1);
                 if ((c->hb == 3 ? (wj & 0xffffff) : wj) == key) cand[p][k++] = j - 1;
+                else if (ex == 0 && firstv) break;  // GPU: a position is a candidate when its first link verifies
             }
             ncand[p] = k;
         }
