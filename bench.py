@@ -611,7 +611,7 @@ def main():
         tp = runs[-1]
         pcie = {"what": "oge_mergesort_bgzf_host: the input BAM file in page-locked host memory -> the output BAM "
                         "file in page-locked host memory; upload overlapped with the host framing index and the "
-                        "inflate, download with the deflate", "seconds": round(tp, 3),
+                        "inflate, download of each deflated segment with the next one's compression", "seconds": round(tp, 3),
                 "first_call_seconds": round(runs[0], 3), "mreads_per_s": round(n / tp / 1e6, 1),
                 "bytes_up": zbytes, "bytes_down": ob, "stages_ms": stage_ms(ctx, E2E_STAGES)}
         log(f"pcie-inclusive: {tp:.3f} s (first call {runs[0]:.3f} s); stages {pcie['stages_ms']}")

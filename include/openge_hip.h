@@ -172,8 +172,10 @@ int oge_mergesort_bgzf_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, co
  * writer threads of BgzfInputStream / BgzfOutputStream, util/bgzf_input_stream.cpp:180-206,
  * util/bgzf_output_stream.cpp:252-285): h_z goes up in chunks on a copy stream while the host indexes its
  * framing and the chunks already up are inflated; after the sort the output is deflated in block-aligned
- * segments whose copies down into h_out (out_cap bytes) run while the next segment is compressed.  The
- * output bytes equal oge_mergesort_bgzf_dev's.  h_z and h_out should be page-locked (oge_host_alloc). */
+ * segments whose copies down into h_out (out_cap bytes) run on a high-priority stream while the next
+ * segment is compressed (OGE_HOSTPIPE_DIRECT=1 with a page-locked h_out of header + oge_bgzf_bound + 28
+ * bytes: the deflate writes straight into h_out instead).  The output bytes equal
+ * oge_mergesort_bgzf_dev's.  h_z and h_out should be page-locked (oge_host_alloc). */
 int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_t zbytes, const oge_mergesort_opts *o, uint8_t *h_out,
                             uint64_t out_cap, uint64_t *out_bytes, uint64_t *n_reads, uint64_t *n_dup);
 

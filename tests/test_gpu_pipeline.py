@@ -150,12 +150,15 @@ def _run_host_pipeline(ctx, src_bytes: bytes, **kw):
     return ho[:nb].numpy().tobytes(), nr, nd
 
 
-@pytest.mark.parametrize("groups,seg", [("8", "32768"), ("7", "3"), ("1", "1"), ("64", "2")])
-def test_host_pipeline_equals_device_chain(ctx, monkeypatch, tmp_path, groups, seg):
-    """oge_mergesort_bgzf_host (file in host memory, chunked upload, host framing index, segmented
-    deflate with the copies down overlapped) writes the same bytes as the chain on a resident file."""
+@pytest.mark.parametrize("groups,seg,direct", [("8", "32768", "1"), ("8", "32768", "0"), ("7", "3", "0"), ("1", "1", "0"),
+                                               ("64", "2", "1")])
+def test_host_pipeline_equals_device_chain(ctx, monkeypatch, tmp_path, groups, seg, direct):
+    """oge_mergesort_bgzf_host (file in host memory, chunked upload, host framing index; the deflate
+    straight into the page-locked output, or segments copied down while the next is compressed) writes the
+    same bytes as the chain on a resident file."""
     monkeypatch.setenv("OGE_HOSTPIPE_GROUPS", groups)
     monkeypatch.setenv("OGE_HOSTPIPE_SEG_BLOCKS", seg)
+    monkeypatch.setenv("OGE_HOSTPIPE_DIRECT", direct)
     p = L.synth_params(60_000, preset="c2", seed=11)
     recs, offs, hdr = L.synth_host(p)
     L.write_bam(tmp_path / "in.bam", hdr, recs, offs, len(offs) - 1, level=6)
