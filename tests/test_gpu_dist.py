@@ -366,3 +366,67 @@ def test_rccl_transport_world1_bgzf_chain(ctx, tmp_path):
         c1.close()
     assert (tr, td) == (nr, nd)
     assert gzip.decompress(got.tobytes()) == gzip.decompress(want.tobytes())
+
+
+def test_rccl_transport_world1_shard_chain(ctx, tmp_path):
+    """bench.py --gpus N's call since r05 (oge_mergesort_bgzf_shard: ONE file, ranks decode their byte
+    ranges) over a one-rank RCCL communicator: the framing and record joins (ncclAllGather), the tail
+    fetch (grouped ncclSend / ncclRecv) and the sort + dedup step equal the one-GPU chain."""
+    import gzip
+    p = L.synth_params(20000, preset="c2", seed=47)
+    recs, offs, hdr = L.synth_host(p)
+    n = len(offs) - 1
+    src = tmp_path / "all.bam"
+    L.write_bam(src, hdr, recs, offs, n, level=6)
+    z = src.read_bytes()
+    opts = L.mergesort_opts(level=6, mark_duplicates=1)
+    dz = torch.from_numpy(np.frombuffer(z + b"\0" * 8, np.uint8).copy()).cuda()
+    d, nb, nr, nd = ctx.mergesort_bgzf_dev(dz.data_ptr(), len(z), opts)
+    want = np.empty(nb, np.uint8)
+    L.check(L.lib().oge_memcpy(ctx.h, want.ctypes.data, d, nb, 2), ctx.h)
+    c1 = L.Context(0)
+    comm = L.comm_init_rank(c1, 1, 0, L.comm_unique_id(), mode="rccl")
+    try:
+        assert comm.transport == "rccl"
+        t = torch.from_numpy(np.frombuffer(z + b"\0" * 8, np.uint8).copy()).cuda()
+        torch.cuda.synchronize()
+        d2, ob, tr, td = comm.mergesort_bgzf_shard(t.data_ptr(), len(z), len(z), opts)
+        got = np.empty(ob, np.uint8)
+        L.check(L.lib().oge_memcpy(c1.h, got.ctypes.data, d2, ob, 2), c1.h)
+    finally:
+        comm.close()
+        c1.close()
+    assert (tr, td) == (nr, nd)
+    assert gzip.decompress(got.tobytes()) == gzip.decompress(want.tobytes())
+
+
+def test_rccl_transport_world1_blocking_records(ctx, monkeypatch):
+    """The blocking record exchange (OGE_DIST_RECORDS=blocking) over a one-rank RCCL communicator: the
+    records themselves go through grouped ncclSend / ncclRecv (to the rank itself: the side-stream mode
+    moves only peers' parts through the transport), non-zero bytes, and the output equals one GPU's."""
+    monkeypatch.setenv("OGE_DIST_RECORDS", "blocking")
+    p = L.synth_params(20000, preset="c2", seed=53)
+    recs, offs, hdr = L.synth_host(p)
+    n = len(offs) - 1
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    c1 = L.Context(0)
+    comm = L.comm_init_rank(c1, 1, 0, L.comm_unique_id(), mode="rccl")
+    try:
+        (srecs, soffs), = _shards(recs, offs, [0, n])
+        d_recs = torch.from_numpy(srecs).cuda()
+        d_offs = torch.from_numpy(soffs).cuda()
+        torch.cuda.synchronize()
+        d, do, no, nd = comm.sort_markdup_dist(d_recs.data_ptr(), d_offs.data_ptr(), n, p.n_ref, opts, True)
+        oo = np.empty(no + 1, np.uint64)
+        L.check(L.lib().oge_memcpy(c1.h, oo.ctypes.data, do, 8 * (no + 1), 2), c1.h)
+        got = np.empty(int(oo[no] - oo[0]), np.uint8)
+        L.check(L.lib().oge_memcpy(c1.h, got.ctypes.data, d + int(oo[0]), got.size, 2), c1.h)
+        ex = {e["tag"]: e for e in comm.exchange_stats()}
+    finally:
+        comm.close()
+        c1.close()
+    want, wd = _single(ctx, recs, offs, n, p.n_ref, opts)
+    assert got.tobytes() == want and nd == wd
+    rec = ex["records"]
+    assert rec["calls"] >= 1 and rec["mode"] == "blocking" and rec["bytes_self"] > 0
+    print("records exchange over RCCL at world 1:", rec)
