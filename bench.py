@@ -704,28 +704,33 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
     ctx.synth_range_dev(p, 0, n_all, d_offs.data_ptr(), None)
     ctx.sync()
     B = int(d_offs[-1].item())
-    S = torch.empty(len(hb) + B + 64, dtype=torch.uint8, device=dev)
-    ctx.synth_range_dev(p, 0, n_all, d_offs.data_ptr(), S.data_ptr() + len(hb))
-    S[:len(hb)].copy_(torch.frombuffer(bytearray(hb), dtype=torch.uint8).to(dev))
+    # the whole file on every rank (library allocations, not the chain's arenas: a rank's chain holds 1/N of
+    # the records), then only this rank's byte range kept
+    total = len(hb) + B
+    S = DevBuf(ctx, L, total + 64)
+    ctx.synth_range_dev(p, 0, n_all, d_offs.data_ptr(), S.ptr + len(hb))
+    S.put(0, hb)
     del d_offs
-    Z, zb = build_input(ctx, L, torch, dev, S, len(hb) + B, args.level)
-    del S
-    Z[zb:zb + 28].copy_(torch.tensor(list(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")),
-                                     dtype=torch.uint8, device=dev))
+    torch.cuda.empty_cache()
+    bound = int(L.lib().oge_bgzf_bound(total))
+    Z = DevBuf(ctx, L, bound + 64)
+    zb = ctx.bgzf_deflate_dev(S.ptr, total, args.level, Z.ptr, bound)
+    ctx.sync()
+    S.free()
+    Z.put(zb, BGZF_EOF)
     zfile = zb + 28
     a, own, end = L.shard_ranges(zfile, world)[rank]
-    d_z = torch.empty(end - a + 64, dtype=torch.uint8, device=dev)
-    d_z[:end - a].copy_(Z[a:end])
+    d_zb = DevBuf(ctx, L, end - a + 64)
+    L.check(L.lib().oge_memcpy(ctx.h, d_zb.ptr, Z.ptr + a, end - a, 3), ctx.h)
+    Z.free()
     zbytes = end - a
-    del Z
-    torch.cuda.empty_cache()
     torch.cuda.synchronize(dev)
     obj = [L.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     comm = L.comm_init_rank(ctx, world, rank, obj[0])
     log(f"rank {rank}: file bytes [{a}, {a + own}) of {zfile} ({zbytes} held), transport {comm.transport}")
     mopts = L.mergesort_opts(level=args.level, mark_duplicates=1)
-    step = lambda: comm.mergesort_bgzf_shard(d_z.data_ptr(), zbytes, own, mopts)
+    step = lambda: comm.mergesort_bgzf_shard(d_zb.ptr, zbytes, own, mopts)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -757,7 +762,7 @@ def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):
         L.check(L.lib().oge_memcpy(ctx.h, hs.data_ptr(), d_last, ob, 2), ctx.h)
         Path(args.dump_dir, f"slice_{rank}.bam").write_bytes(hs[:ob].numpy().tobytes())
     comm.close()
-    del d_z
+    d_zb.free()
     torch.cuda.empty_cache()
     realign_multi = None
     if not args.no_realign:
