@@ -256,7 +256,7 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1, cpu_thread
         if world == 1:
             cli = realign_cli_leg(fa, iv, bam, td)
         t0c = time.perf_counter()
-        w_out, w_oo, _ = run()  # first call in this process (the cross-call scratch is built here)
+        w_out, w_oo, first_st = run()  # first call in this process (the cross-call scratch is built here)
         first_call_s = time.perf_counter() - t0c
         if dump_dir:  # this rank's realigned records (tests concatenate the ranks' parts)
             Path(dump_dir, f"realign_{rank}.bin").write_bytes(np.asarray(w_out[:int(w_oo[-1])]).tobytes())
@@ -295,7 +295,7 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1, cpu_thread
             "seconds": round(dt, 3), "host_threads": 16, "stats": st,
             "timed_region": "the realigner on records already decoded in host memory, second call in the process "
                             "(first_call_seconds: the first; cli: the whole command, file to file, fresh process)",
-            "first_call_seconds": round(first_call_s, 3), "cli": cli,
+            "first_call_seconds": round(first_call_s, 3), "first_call_stats": first_st, "cli": cli,
             "roofline": {"kernel": "k_planes + k_scan_bp (findBestOffset over all consensus x altRead pairs, "
                                    "bit-parallel)",
                          "bound": "valu", "achieved": round(cmp_t, 2) if cmp_t else None,
