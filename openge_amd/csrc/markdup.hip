@@ -768,13 +768,13 @@ constexpr uint32_t kMjT = 1024, kMjW = 512, kMjSlots = 4096;
 static_assert(kMjT + 2 * kMjW <= kMjSlots / 2, "window table at most half full");
 constexpr uint32_t kNone = 0xffffffffu, kSortPair = 0x80000000u;
 
-__device__ __forceinline__ bool is_cand(const uint32_t *__restrict__ cpos, uint64_t i) { return cpos[i + 1] != cpos[i]; }
+__device__ __forceinline__ bool is_cand(const uint32_t *__restrict__ cflag, uint64_t i) { return cflag[i] != 0; }
 __device__ __forceinline__ uint32_t mj_fp(uint64_t h) {
     const uint32_t x = (uint32_t)h ^ (uint32_t)(h >> 32) * 0x9E3779B1u;
     return x ? x : 1u;
 }
 
-__global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ cpos, const uint64_t *__restrict__ cval, uint64_t n,
+__global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ cflag, const uint64_t *__restrict__ cval, uint64_t n,
                                                    uint32_t ib, uint32_t *__restrict__ partner) {
     __shared__ uint32_t key[kMjSlots], lo[kMjSlots], hi[kMjSlots], cnt[kMjSlots];
     const uint32_t t = threadIdx.x;
@@ -783,7 +783,7 @@ __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ 
     const int64_t t0 = (int64_t)blockIdx.x * kMjT, w0 = t0 - (int64_t)kMjW;
     for (uint32_t w = t; w < kMjT + 2 * kMjW; w += kMjT) {
         const int64_t i = w0 + (int64_t)w;
-        if (i < 0 || (uint64_t)i >= n || !is_cand(cpos, (uint64_t)i)) continue;
+        if (i < 0 || (uint64_t)i >= n || !is_cand(cflag, (uint64_t)i)) continue;
         const uint32_t f = mj_fp(cval[i] >> ib);
         uint32_t s = (f * 2654435761u) >> 20;  // 12 bits: kMjSlots
         for (;;) {
@@ -799,7 +799,7 @@ __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ 
     const uint64_t i = (uint64_t)t0 + t;
     if (i >= n) return;
     uint32_t r = kNone;
-    if (is_cand(cpos, i)) {
+    if (is_cand(cflag, i)) {
         const uint32_t f = mj_fp(cval[i] >> ib), w = t + kMjW;
         uint32_t s = (f * 2654435761u) >> 20;
         while (key[s] != f) s = (s + 1) & (kMjSlots - 1);
@@ -813,7 +813,7 @@ __device__ __forceinline__ uint32_t mj_bit(uint64_t key, uint32_t bmask) { retur
 constexpr int kMjProbes = 64;
 
 // leftovers (and their keys into the conflict set: a bitmap filter in front of an open-addressing table)
-__global__ __launch_bounds__(kT) void k_mate_agree(const uint32_t *__restrict__ cpos, const uint64_t *__restrict__ cval, uint64_t n,
+__global__ __launch_bounds__(kT) void k_mate_agree(const uint32_t *__restrict__ cflag, const uint64_t *__restrict__ cval, uint64_t n,
                                                    uint32_t ib, const uint32_t *__restrict__ partner, uint32_t *__restrict__ mate,
                                                    uint32_t *__restrict__ lflag, unsigned long long *__restrict__ tab, uint32_t mask,
                                                    uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf) {
@@ -821,7 +821,7 @@ __global__ __launch_bounds__(kT) void k_mate_agree(const uint32_t *__restrict__ 
     if (i > n) return;
     if (i == n) { lflag[n] = 0; return; }
     uint32_t m = kNone, lf = 0;
-    if (is_cand(cpos, i)) {
+    if (is_cand(cflag, i)) {
         const uint32_t j = partner[i];
         const uint64_t h = cval[i] >> ib;
         if (j != kNone && partner[j] == (uint32_t)i && (cval[j] >> ib) == h) {
@@ -994,6 +994,15 @@ static CandKey md_candkey(const oge_markdup_opts *opts, uint64_t n) {
     return ckl;
 }
 
+static bool mate_win_enabled() {
+    const char *e = getenv("OGE_MD_MATEWIN");  // "0": the sort-based join only (A/B, tests); read per call
+    return !(e && e[0] == '0');
+}
+// the windowed mate join applies: records in coordinate order (skeys) on one GPU, the default key hash, one chain
+static bool mate_window_ok(const oge_markdup_opts *opts, uint64_t n, const uint64_t *skeys) {
+    return skeys && n && n < (1ull << 31) && opts->split_chains <= 1 && opts->debug_hash_bits <= 0 && mate_win_enabled();
+}
+
 int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
                      OgeMdFrags *f, const uint64_t *skeys) {
     KeyLayout L;
@@ -1020,10 +1029,13 @@ int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *
     hipLaunchKernelGGL(k_cand_frag, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, L, ckl, f->cpos, f->fk,
                        f->fv, f->cval, f->desc0, cnt + 3, skeys, f->dev);
     OGE_LAUNCH_CHECK(ctx);
-    rc = oge_exclusive_scan_u32(ctx, f->cpos, f->cpos, n + 1);
-    if (rc) return rc;
     uint32_t nc = 0, ovf = 0;
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&nc, f->cpos + n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    f->cpos_scanned = !mate_window_ok(opts, n, skeys);  // the windowed join reads the flags as they are
+    if (f->cpos_scanned) {
+        rc = oge_exclusive_scan_u32(ctx, f->cpos, f->cpos, n + 1);
+        if (rc) return rc;
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&nc, f->cpos + n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&ovf, cnt + 3, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     f->nc = nc;
@@ -1107,11 +1119,6 @@ static int pair_build(oge_ctx *ctx, const KeyLayout &L, const uint8_t *recs, con
     return OGE_OK;
 }
 
-static bool mate_win_enabled() {
-    const char *e = getenv("OGE_MD_MATEWIN");  // "0": the sort-based join only (A/B, tests); read per call
-    return !(e && e[0] == '0');
-}
-
 // The windowed join (see k_mate_win) for records in coordinate order; *done = false when it cannot
 // decide (the conflict set overflowed, or a window pair's names differ): the caller runs the sort path.
 static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, const uint8_t *recs, const RecMeta *meta, uint64_t n,
@@ -1124,11 +1131,12 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
     uint32_t *oflag = (uint32_t *)ctx->scratch("md_oflag", (n + 1) * 4);
     uint64_t *wpairs = (uint64_t *)ctx->scratch("md_wpairs", (n / 2 + 1) * 8);
     if (!cnt || !partner || !mate || !lflag || !oflag || !wpairs) return OGE_ERR_HIP;
-    // the conflict set: a table of >= n/16 slots behind a bitmap of >= n/2 bits (a probe run past kMjProbes
-    // means too many leftovers for the window path: the sort path decides)
+    // the conflict set: a table of >= n/16 slots behind a bitmap of >= n/2 bits, at most 4 MiB so it stays in
+    // an XCD's L2 for k_mate_check's random reads (a probe run past kMjProbes means too many leftovers for the
+    // window path: the sort path decides)
     uint32_t slots = 1024, nbits = 1u << 15;
     while (slots < n / 16 && slots < (1u << 30)) slots <<= 1;
-    while (nbits < n / 2 && nbits < (1u << 31)) nbits <<= 1;
+    while (nbits < n / 2 && nbits < (1u << 25)) nbits <<= 1;
     unsigned long long *tab = (unsigned long long *)ctx->scratch("md_mconf", (uint64_t)slots * 8);
     uint32_t *bits = (uint32_t *)ctx->scratch("md_mbits", nbits / 8);
     if (!tab || !bits) return OGE_ERR_HIP;
@@ -1196,15 +1204,19 @@ int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t 
     if (rc) return rc;
     *P = OgeMdPairs{};
     const CandKey ckl = md_candkey(opts, n);
-    // the windowed join: records in coordinate order (skeys) on one GPU, the default key hash, one chain
-    if (f.skeys && n && n < (1ull << 31) && opts->split_chains <= 1 && opts->debug_hash_bits <= 0 && mate_win_enabled()) {
+    uint32_t nc = f.nc;
+    if (!f.cpos_scanned) {  // oge_md_cand_frag left the candidate flags for the windowed join
         bool done = false;
         if ((rc = join_window(ctx, L, ckl, recs, meta, n, f, P, &done))) return rc;
         if (done) return OGE_OK;
+        // the sort path after all: the flags' exclusive scan (the window path left them untouched)
+        if ((rc = oge_exclusive_scan_u32(ctx, f.cpos, f.cpos, n + 1))) return rc;
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&nc, f.cpos + n, 4, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
     uint64_t *pairs, *pairs2;
     uint32_t np = 0;
-    if ((rc = join_sorted(ctx, ckl, recs, meta, n, f.cpos, f.cval, f.nc, &pairs, &pairs2, &np))) return rc;
+    if ((rc = join_sorted(ctx, ckl, recs, meta, n, f.cpos, f.cval, nc, &pairs, &pairs2, &np))) return rc;
     // order the pairs by first-mate position: k_pair_build then reads both summaries from nearby rows
     uint64_t *spairs = pairs;
     rc = oge_radix_sort_pairs(ctx, pairs, nullptr, pairs2, nullptr, np, bits_mask_hi32(n), &spairs, nullptr);

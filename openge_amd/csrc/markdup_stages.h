@@ -21,7 +21,9 @@ struct OgeMdFrags {
     uint32_t *fv = nullptr;     // n record indices
     uint64_t *cval = nullptr;   // n candidate keys (hash bits << ib | index)
     uint64_t *desc0 = nullptr;  // n gather descriptors (optional)
-    uint32_t nc = 0;            // candidates
+    uint32_t nc = 0;            // candidates (when cpos_scanned)
+    bool cpos_scanned = true;   // false: cpos holds the 0/1 flags (the windowed mate join needs no scan;
+                                // oge_md_join_build scans them if it falls back to the sort path)
     bool desc_ovf = false;      // a record offset does not fit the descriptor
     const uint64_t *skeys = nullptr;  // sorted coordinate keys (windowed fragment groups), optional
     unsigned long long *dev = nullptr;  // per-block maxima of the fragment (then pair) coordinates' deviation from the anchors
