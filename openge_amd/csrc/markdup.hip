@@ -754,10 +754,11 @@ __global__ __launch_bounds__(kT) void k_apply_desc(const uint64_t *__restrict__ 
 // order, so most of the ReadEndsMap's pairs are found in a window, without the global hash sort:
 //   k_mate_win    tile of kMjT records + kMjW on each side in an LDS table of candidate fingerprints
 //                 (count, first and last window slot): a tile record whose fingerprint occurs exactly
-//                 twice in its window gets the other occurrence as partner
-//   k_mate_agree  i and j = partner[i] agree (partner[j] == i, equal hash bits): a window pair, owned by
-//                 the smaller index; anything else is a leftover, its hash bits into a global set (a
-//                 bitmap filter in front of an open-addressing table)
+//                 twice in its window gets the other occurrence as partner; a partner in the same tile
+//                 decides at once (window pair owned by the smaller index, or both leftovers)
+//   k_mate_agree  a partner in another tile: i and j = partner[i] agree (partner[j] == i, equal hash bits)
+//                 or i is a leftover.  Every leftover's hash bits go into a global set (a bitmap filter in
+//                 front of an open-addressing table)
 //   k_mate_check  a window pair whose hash is in that set gives both ends to the leftovers: its key has
 //                 other occurrences (first-seen / second-seen pairing must see them all)
 // The leftovers take the sort-based join; every hash bit pattern then occurs exactly twice among the
@@ -774,17 +775,46 @@ __device__ __forceinline__ uint32_t mj_fp(uint64_t h) {
     return x ? x : 1u;
 }
 
+__device__ __forceinline__ uint32_t mj_slot(uint64_t key, uint32_t mask) { return (uint32_t)(mix64(key) & mask); }
+__device__ __forceinline__ uint32_t mj_bit(uint64_t key, uint32_t bmask) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & bmask; }
+constexpr int kMjProbes = 64;
+constexpr uint32_t kPending = 2;  // lflag: the partner lies in another tile, k_mate_agree decides
+
+// a leftover's hash bits into the conflict set (bitmap filter + open-addressing table)
+__device__ __forceinline__ void mj_conflict(uint64_t h, unsigned long long *__restrict__ tab, uint32_t mask,
+                                            uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf) {
+    const unsigned long long key = h + 1;
+    const uint32_t b = mj_bit(key, bmask);
+    atomicOr(&bits[b >> 5], 1u << (b & 31));
+    uint32_t s = mj_slot(key, mask);
+    for (int p = 0; p < kMjProbes; ++p) {
+        const unsigned long long o = atomicCAS(&tab[s], 0ull, key);
+        if (o == 0ull || o == key) return;
+        s = (s + 1) & mask;
+    }
+    atomicOr(ovf, 1u);
+}
+
+// Per tile: the window's fingerprint table, then every tile record's decision.  A partner inside the tile
+// saw the same table (agreement is given; the full hash bits are compared from the staged window): a window
+// pair (mate[] of the smaller index) or two leftovers.  A partner in another tile: partner[i], kPending.
 __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ cflag, const uint64_t *__restrict__ cval, uint64_t n,
-                                                   uint32_t ib, uint32_t *__restrict__ partner) {
+                                                   uint32_t ib, uint32_t *__restrict__ partner, uint32_t *__restrict__ mate,
+                                                   uint32_t *__restrict__ lflag, unsigned long long *__restrict__ tab, uint32_t mask,
+                                                   uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf) {
     __shared__ uint32_t key[kMjSlots], lo[kMjSlots], hi[kMjSlots], cnt[kMjSlots];
+    __shared__ uint64_t hv[kMjT + 2 * kMjW];  // the window's hash bits (0: not a candidate)
     const uint32_t t = threadIdx.x;
     for (uint32_t s = t; s < kMjSlots; s += kMjT) key[s] = 0, lo[s] = kNone, hi[s] = 0, cnt[s] = 0;
     __syncthreads();
     const int64_t t0 = (int64_t)blockIdx.x * kMjT, w0 = t0 - (int64_t)kMjW;
     for (uint32_t w = t; w < kMjT + 2 * kMjW; w += kMjT) {
         const int64_t i = w0 + (int64_t)w;
+        hv[w] = 0;
         if (i < 0 || (uint64_t)i >= n || !is_cand(cflag, (uint64_t)i)) continue;
-        const uint32_t f = mj_fp(cval[i] >> ib);
+        const uint64_t h = cval[i] >> ib;
+        hv[w] = h + 1;
+        const uint32_t f = mj_fp(h);
         uint32_t s = (f * 2654435761u) >> 20;  // 12 bits: kMjSlots
         for (;;) {
             const uint32_t o = atomicCAS(&key[s], 0u, f);
@@ -798,51 +828,56 @@ __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ 
     __syncthreads();
     const uint64_t i = (uint64_t)t0 + t;
     if (i >= n) return;
-    uint32_t r = kNone;
-    if (is_cand(cflag, i)) {
-        const uint32_t f = mj_fp(cval[i] >> ib), w = t + kMjW;
+    const uint32_t w = t + kMjW;
+    uint32_t r = kNone, m = kNone, lf = 0;
+    if (hv[w]) {
+        const uint64_t h = hv[w] - 1;
+        const uint32_t f = mj_fp(h);
         uint32_t s = (f * 2654435761u) >> 20;
         while (key[s] != f) s = (s + 1) & (kMjSlots - 1);
-        if (cnt[s] == 2) r = (uint32_t)(w0 + (int64_t)(lo[s] == w ? hi[s] : lo[s]));
+        if (cnt[s] == 2) {
+            const uint32_t pw = lo[s] == w ? hi[s] : lo[s];
+            r = (uint32_t)(w0 + (int64_t)pw);
+            if (pw >= kMjW && pw < kMjW + kMjT) {  // the partner is a record of this tile
+                if (hv[pw] == hv[w]) {
+                    if ((uint64_t)r > i) m = r;
+                } else {
+                    lf = 1;  // a fingerprint collision: two different keys
+                }
+            } else {
+                lf = kPending;
+            }
+        } else {
+            lf = 1;
+        }
+        if (lf == 1) {
+            r = kNone;
+            mj_conflict(h, tab, mask, bits, bmask, ovf);
+        }
     }
     partner[i] = r;
+    mate[i] = m;
+    lflag[i] = lf;
+    if (i + 1 == n) lflag[n] = 0;
 }
 
-__device__ __forceinline__ uint32_t mj_slot(uint64_t key, uint32_t mask) { return (uint32_t)(mix64(key) & mask); }
-__device__ __forceinline__ uint32_t mj_bit(uint64_t key, uint32_t bmask) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & bmask; }
-constexpr int kMjProbes = 64;
-
-// leftovers (and their keys into the conflict set: a bitmap filter in front of an open-addressing table)
-__global__ __launch_bounds__(kT) void k_mate_agree(const uint32_t *__restrict__ cflag, const uint64_t *__restrict__ cval, uint64_t n,
-                                                   uint32_t ib, const uint32_t *__restrict__ partner, uint32_t *__restrict__ mate,
+// the pending records (a partner in another tile): i and j = partner[i] agree (partner[j] == i, equal hash
+// bits) -- a window pair owned by the smaller index -- or i is a leftover
+__global__ __launch_bounds__(kT) void k_mate_agree(const uint64_t *__restrict__ cval, uint64_t n, uint32_t ib,
+                                                   const uint32_t *__restrict__ partner, uint32_t *__restrict__ mate,
                                                    uint32_t *__restrict__ lflag, unsigned long long *__restrict__ tab, uint32_t mask,
                                                    uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf) {
     const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i > n) return;
-    if (i == n) { lflag[n] = 0; return; }
-    uint32_t m = kNone, lf = 0;
-    if (is_cand(cflag, i)) {
-        const uint32_t j = partner[i];
-        const uint64_t h = cval[i] >> ib;
-        if (j != kNone && partner[j] == (uint32_t)i && (cval[j] >> ib) == h) {
-            if (i < j) m = j;
-        } else {
-            lf = 1;
-            const unsigned long long key = h + 1;
-            const uint32_t b = mj_bit(key, bmask);
-            atomicOr(&bits[b >> 5], 1u << (b & 31));
-            uint32_t s = mj_slot(key, mask);
-            int p = 0;
-            for (; p < kMjProbes; ++p) {
-                const unsigned long long o = atomicCAS(&tab[s], 0ull, key);
-                if (o == 0ull || o == key) break;
-                s = (s + 1) & mask;
-            }
-            if (p == kMjProbes) atomicOr(ovf, 1u);
-        }
+    if (i >= n || lflag[i] != kPending) return;
+    const uint32_t j = partner[i];
+    const uint64_t h = cval[i] >> ib;
+    if (partner[j] == (uint32_t)i && (cval[j] >> ib) == h) {
+        if (i < j) mate[i] = j;
+        lflag[i] = 0;
+    } else {
+        lflag[i] = 1;
+        mj_conflict(h, tab, mask, bits, bmask, ovf);
     }
-    mate[i] = m;
-    lflag[i] = lf;
 }
 
 // also writes pflag[i] (a pair is owned by i) for every record
@@ -1144,11 +1179,10 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
     OGE_HIP_TRY(ctx, hipMemsetAsync(tab, 0, (uint64_t)slots * 8, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(bits, 0, nbits / 8, ctx->stream));
     hipLaunchKernelGGL(k_mate_win, dim3(oge_ceil_div(n, kMjT)), dim3(kMjT), 0, ctx->stream, (const uint32_t *)f.cpos,
-                       (const uint64_t *)f.cval, n, ckl.ib, partner);
+                       (const uint64_t *)f.cval, n, ckl.ib, partner, mate, lflag, tab, slots - 1, bits, nbits - 1, cnt + 1);
     OGE_LAUNCH_CHECK(ctx);
-    hipLaunchKernelGGL(k_mate_agree, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)f.cpos,
-                       (const uint64_t *)f.cval, n, ckl.ib, (const uint32_t *)partner, mate, lflag, tab, slots - 1, bits, nbits - 1,
-                       cnt + 1);
+    hipLaunchKernelGGL(k_mate_agree, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)f.cval, n, ckl.ib,
+                       (const uint32_t *)partner, mate, lflag, tab, slots - 1, bits, nbits - 1, cnt + 1);
     OGE_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(k_mate_check, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)f.cval, n, ckl.ib,
                        (const unsigned long long *)tab, slots - 1, (const uint32_t *)bits, nbits - 1, mate, lflag, oflag);
