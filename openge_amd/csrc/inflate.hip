@@ -56,7 +56,9 @@ __device__ bool chain_at(const uint8_t *d, uint64_t s, uint64_t n, bool at_end, 
     return k == 16 || (at_end && q == n && k > 0);
 }
 
-// chunk c covers [p + c*CH, min(lim, p + (c+1)*CH)) (bytes readable up to n); guess its first record start
+// chunk c covers [p + c*CH, min(lim, p + (c+1)*CH)) (bytes readable up to n); guess its first record start.
+// A thread per chunk: the 16-record chain is the cost, and a wave runs 64 of them side by side (r05: a
+// wave per chunk, its lanes testing 64 positions at once, measured 6.4 vs 5.7 ms at 300M reads)
 __global__ void k_rec_guess(const uint8_t *__restrict__ d, uint64_t p, uint64_t lim, uint64_t n, bool at_end, int32_t n_ref,
                             uint64_t CH, uint64_t C, uint64_t *__restrict__ start) {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -89,32 +91,69 @@ __global__ void __launch_bounds__(256) k_rec_guess_first(const uint8_t *__restri
     if (threadIdx.x == 0) *out = best;
 }
 
-// walk chunk c from start[c] to the first record start at or past the chunk end; with out != NULL
-// also write the (absolute) offsets from pos[c], never at or past out[cap] (a stream that changed since
-// the counts in pos were made may hold more records: the caller then detects it and walks again)
-__global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t lim, uint64_t n, uint64_t CH, uint64_t C,
-                           const uint64_t *__restrict__ start, uint64_t *__restrict__ stop, uint64_t *__restrict__ count,
-                           const uint64_t *__restrict__ pos, uint64_t *__restrict__ out, uint64_t cap) {
-    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    const uint64_t end = min(lim, p + (c + 1) * CH);
-    uint64_t q = start[c], k = 0;
-    if (q == kNone) {
-        stop[c] = kNone;
-        count[c] = 0;
-        return;
-    }
-    const uint64_t o0 = out ? pos[c] : 0;
+// the block_size chain from q while it starts before end: k records, *q the first start at or past end
+// (or the invalid record's); with out != NULL the offsets from out[o0], never at or past out[cap]
+__device__ __forceinline__ uint64_t walk_chunk(const uint8_t *__restrict__ d, uint64_t &q, uint64_t end, uint64_t n,
+                                               uint64_t *__restrict__ out, uint64_t o0, uint64_t cap, uint16_t *__restrict__ rel,
+                                               uint64_t cut, uint32_t SC) {
+    uint64_t k = 0, acc = 0;  // rel: four slots per 8-byte store (SC is a multiple of 4)
     while (q < end) {
         if (q + 4 > n) break;
         const uint32_t bs = rd32u(d + q);
         if (bs < 32 || bs > 10000 || q + 4 + bs > n) break;
         if (out && o0 + k < cap) out[o0 + k] = q;
+        if (rel && k < SC) {
+            acc |= (q - cut) << (16 * (k & 3));
+            if ((k & 3) == 3) *(uint64_t *)(rel + (k & ~3ull)) = acc, acc = 0;
+        }
         ++k;
         q += 4 + bs;
     }
+    if (rel && (k & 3) && k < SC) *(uint64_t *)(rel + (k & ~3ull)) = acc;
+    return k;
+}
+
+// walk chunk c from start[c] to the first record start at or past the chunk end; with out != NULL
+// also write the (absolute) offsets from pos[c], never at or past out[cap] (a stream that changed since
+// the counts in pos were made may hold more records: the caller then detects it and walks again); with
+// rel != NULL the first SC record starts relative to the chunk's first byte (< 64 KiB: u16) go to
+// rel[c * SC ...] for k_rec_fill
+__global__ void k_rec_walk(const uint8_t *__restrict__ d, uint64_t p, uint64_t lim, uint64_t n, uint64_t CH, uint64_t C,
+                           const uint64_t *__restrict__ start, uint64_t *__restrict__ stop, uint64_t *__restrict__ count,
+                           const uint64_t *__restrict__ pos, uint64_t *__restrict__ out, uint64_t cap, uint16_t *__restrict__ rel,
+                           uint32_t SC) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const uint64_t cut = p + c * CH, end = min(lim, cut + CH);
+    uint64_t q = start[c];
+    if (q == kNone) {
+        stop[c] = kNone;
+        count[c] = 0;
+        return;
+    }
+    const uint64_t k = walk_chunk(d, q, end, n, out, out ? pos[c] : 0, cap, rel ? rel + c * SC : nullptr, cut, SC);
     stop[c] = q < end ? kNone - 1 : q;  // kNone - 1: invalid record inside the chunk
     count[c] = k;
+}
+
+// the offsets from the converged count walk's slots: one wave per chunk, 64 offsets per store; a chunk
+// with more records than slots (under 128 bytes a record on average) is walked again by its lane 0
+__global__ void __launch_bounds__(256) k_rec_fill(const uint8_t *__restrict__ d, uint64_t p, uint64_t lim, uint64_t n, uint64_t CH,
+                                                  uint64_t C, const uint64_t *__restrict__ start, const uint64_t *__restrict__ count,
+                                                  const uint64_t *__restrict__ pos, const uint16_t *__restrict__ rel, uint32_t SC,
+                                                  uint64_t *__restrict__ out, uint64_t cap) {
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (c >= C) return;
+    const uint64_t k_n = count[c], o0 = pos[c], cut = p + c * CH;
+    if (k_n <= SC) {
+        const uint16_t *r = rel + c * SC;
+        for (uint64_t k = lane; k < k_n; k += 64)
+            if (o0 + k < cap) out[o0 + k] = cut + r[k];
+    } else if (lane == 0) {
+        uint64_t q = start[c];
+        (void)walk_chunk(d, q, min(lim, cut + CH), n, out, o0, cap, nullptr, cut, 0);
+    }
 }
 
 // chunk c + 1 starts where chunk c's walk stopped; *st bit 0: a start moved, bit 1: a stop that is
@@ -659,7 +698,8 @@ int oge_record_guess(oge_ctx *ctx, const uint8_t *d, uint64_t lim, uint64_t bufe
 }
 
 int oge_record_walk(oge_ctx *ctx, const uint8_t *d_stream, uint64_t rec_base, uint64_t limit, uint64_t end, bool at_end,
-                    int32_t n_ref, uint64_t *d_off, uint64_t cap, uint64_t *n_out, uint64_t *exit) {
+                    int32_t n_ref, uint64_t *d_off, uint64_t cap, uint64_t *n_out, uint64_t *exit, bool keep, void *rel_buf,
+                    uint64_t rel_cap) {
     if (!n_out || rec_base > limit || limit > end || (end > rec_base && !d_stream)) return oge_fail(ctx, OGE_ERR_ARG, "bad argument");
     hipSetDevice(ctx->device);
     *n_out = 0;
@@ -676,11 +716,13 @@ int oge_record_walk(oge_ctx *ctx, const uint8_t *d_stream, uint64_t rec_base, ui
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         return OGE_OK;
     }
-    const uint32_t TB = 128, G = oge_ceil_div(C, TB);
+    const uint32_t TB = 128, G = oge_ceil_div(C, TB), G4 = oge_ceil_div(C, 4);
+    uint16_t *rel = nullptr;
+    uint32_t SC = 0;
     // one walk + join pass: *st bit 0 = a start moved, bit 1 = an invalid or unjoined stop
     auto walk_join = [&](uint64_t *pos_arg, uint64_t *out, unsigned int *h) -> int {
         OGE_HIP_TRY(ctx, hipMemsetAsync(st, 0, 4, ctx->stream));
-        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, limit, end, CH, C, start, stop, count, pos_arg, out, cap);
+        k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, limit, end, CH, C, start, stop, count, pos_arg, out, cap, rel, SC);
         OGE_LAUNCH_CHECK(ctx);
         k_rec_join<<<G, TB, 0, ctx->stream>>>(stop, start, C, limit, st);
         OGE_LAUNCH_CHECK(ctx);
@@ -701,30 +743,51 @@ int oge_record_walk(oge_ctx *ctx, const uint8_t *d_stream, uint64_t rec_base, ui
     auto &RW = ctx->recwalk;
     if (d_off && RW.stream == d_stream && RW.base == rec_base && RW.limit == limit && RW.end == end && RW.n_ref == n_ref &&
         RW.C == C) {
-        // the count-only call on this stream converged just before: fill from its chunk starts and
-        // offsets (still in the workspace), then check the walk joined and counted the same
-        const uint64_t n = RW.n;
+        const uint64_t n = RW.n, x = RW.x;
         RW.stream = nullptr;
         if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
-        unsigned int h = 0;
-        uint64_t n2 = 0, x = 0;
-        int rc = walk_join(pos, d_off, &h);
-        if (rc) return rc;
-        if (!h && !(rc = scan_counts(pos2, &n2, &x)) && n2 == n) {
+        if (RW.rel && keep) {
+            // a trusted caller's count and fill calls (keep: the stream is unchanged between them): expand the
+            // count walk's slots
+            k_rec_fill<<<G4, 256, 0, ctx->stream>>>(d_stream, rec_base, limit, end, CH, C, start, count, pos, RW.rel, RW.sc, d_off, cap);
+            OGE_LAUNCH_CHECK(ctx);
             OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &x, 8, hipMemcpyHostToDevice, ctx->stream));
             OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
             *n_out = n;
             *exit = x;
             return OGE_OK;
         }
+        // the count-only call on this stream converged just before: fill from its chunk starts and
+        // offsets (still in the workspace), then check the walk joined and counted the same
+        unsigned int h = 0;
+        uint64_t n2 = 0, x2 = 0;
+        int rc = walk_join(pos, d_off, &h);
+        if (rc) return rc;
+        if (!h && !(rc = scan_counts(pos2, &n2, &x2)) && n2 == n) {
+            OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &x2, 8, hipMemcpyHostToDevice, ctx->stream));
+            OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            *n_out = n;
+            *exit = x2;
+            return OGE_OK;
+        }
         if (rc) return rc;
         // the stream changed between the calls: the full walk below
     }
     RW.stream = nullptr;
+    if (keep && !d_off) {
+        // record slots for the fill call, a multiple of 4 (OGE_RECWALK_SLOTS: a test forces the overflow walk
+        // with few)
+        const char *e = getenv("OGE_RECWALK_SLOTS");
+        SC = e ? (uint32_t)std::min<unsigned long>((std::max<unsigned long>(strtoul(e, nullptr, 10), 1ul) + 3) & ~3ul, 2048ul) : 512u;
+        const uint64_t need = C * SC * 2;
+        rel = rel_buf && rel_cap >= need ? (uint16_t *)rel_buf : (uint16_t *)ctx->ws("rec_rel", need);
+        if (!rel) return OGE_ERR_HIP;
+    }
     k_rec_guess<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, limit, end, at_end, n_ref, CH, C, start);
     OGE_LAUNCH_CHECK(ctx);
     // walk, then every chunk starts where its predecessor's walk stopped (k_rec_join), until no start
-    // moves: the chain from chunk 0 then equals the sequential walk
+    // moves: the chain from chunk 0 then equals the sequential walk (and the slots of the last walk,
+    // whose starts all held, are its records)
     unsigned int h = 0;
     for (int it = 0;; ++it) {
         int rc = walk_join(nullptr, nullptr, &h);
@@ -739,11 +802,13 @@ int oge_record_walk(oge_ctx *ctx, const uint8_t *d_stream, uint64_t rec_base, ui
     *n_out = n;
     *exit = x;
     if (!d_off) {
-        RW.stream = d_stream, RW.base = rec_base, RW.limit = limit, RW.end = end, RW.n_ref = n_ref, RW.n = n, RW.C = C;
+        RW.stream = d_stream, RW.base = rec_base, RW.limit = limit, RW.end = end, RW.n_ref = n_ref, RW.n = n, RW.C = C, RW.x = x;
+        RW.rel = rel, RW.sc = SC;
         return OGE_OK;
     }
     if (cap < n + 1) return oge_fail(ctx, OGE_ERR_ARG, "offset capacity too small (need n + 1)");
-    k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, limit, end, CH, C, start, stop, count, pos, d_off, cap);
+    rel = nullptr;
+    k_rec_walk<<<G, TB, 0, ctx->stream>>>(d_stream, rec_base, limit, end, CH, C, start, stop, count, pos, d_off, cap, nullptr, 0);
     OGE_LAUNCH_CHECK(ctx);
     OGE_HIP_TRY(ctx, hipMemcpyAsync(d_off + n, &x, 8, hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -42,13 +42,16 @@ struct oge_ctx {
     }
     void *alloc(size_t bytes);
     void release(void *p);
-    // the last count-only oge_bam_record_offsets_dev call: its converged chunk starts and offsets stay
-    // in the "rec_walk" workspace, so the offsets call that follows (same stream and range) goes
-    // straight to the fill walk, which is checked to join and count the same
+    // the last count-only record walk: its converged chunk starts and offsets stay in the "rec_walk"
+    // workspace, so the offsets call that follows (same stream and range) goes straight to the fill: from
+    // the count walk's record slots (rel, a trusted internal caller's `keep`), else a second walk that is
+    // checked to join and count the same
     struct RecWalk {
         const void *stream = nullptr;
-        uint64_t base = 0, limit = 0, end = 0, n = 0, C = 0;
+        uint64_t base = 0, limit = 0, end = 0, n = 0, C = 0, x = 0;
         int32_t n_ref = 0;
+        const uint16_t *rel = nullptr;
+        uint32_t sc = 0;
     } recwalk;
     std::map<std::string, uint64_t> counters;  // per call: work counts a stage reports (oge_ctx_counter)
     bool last_scan_generic = false;  // realign scan fell back to the byte-wise kernel
@@ -124,8 +127,12 @@ int oge_bgzf_index_range_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, u
 // [start, limit) of d (bytes readable up to bufend, so the last record may end past limit); at_end says
 // bufend is the end of the stream (a guess chain may stop there).  *exit = the end of the last record
 // (= the first record start at or past limit); d_off (cap >= n + 1) gets the offsets and d_off[n] = *exit.
+// keep (a count call of an internal caller that fills next, on the same unchanged stream): the walk also
+// stores each chunk's record positions (in rel_buf when it holds rel_cap >= the slots' bytes, else
+// workspace "rec_rel"), and the fill call expands them instead of walking the stream again.
 int oge_record_walk(oge_ctx *ctx, const uint8_t *d, uint64_t start, uint64_t limit, uint64_t bufend, bool at_end, int32_t n_ref,
-                    uint64_t *d_off, uint64_t cap, uint64_t *n_out, uint64_t *exit);
+                    uint64_t *d_off, uint64_t cap, uint64_t *n_out, uint64_t *exit, bool keep = false, void *rel_buf = nullptr,
+                    uint64_t rel_cap = 0);
 // The first plausible record start in [0, lim) of d (bufend readable) as k_rec_guess judges it, or ~0.
 int oge_record_guess(oge_ctx *ctx, const uint8_t *d, uint64_t lim, uint64_t bufend, bool at_end, int32_t n_ref, uint64_t *out);
 // the framing walk of a host buffer with T threads (inflate.hip); false: use oge_bgzf_index

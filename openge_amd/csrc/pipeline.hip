@@ -11,7 +11,7 @@
 //
 //   index    oge_bgzf_index_ws  (device framing walk)
 //   inflate  oge_bgzf_inflate_dev into X, CRC-32 checked
-//   records  oge_bam_record_offsets_dev (block_size walk)
+//   records  oge_record_walk (block_size walk; the fill expands the count walk's record slots)
 //   sort     oge_sort_markdup_dev (or sort + gather without -M) X -> Y, bins recomputed
 //   [-R]     oge_drop_flagged_dev Y -> X
 //   write    header block (host) + oge_bgzf_deflate_dev + EOF block into the free buffer
@@ -143,12 +143,17 @@ static int decode_records(oge_ctx *ctx, uint8_t *X, uint64_t total, uint64_t **x
 
     // ---- record boundaries
     tm = ctx->begin_stage("rec_walk");
-    uint64_t n = 0;
-    rc = oge_bam_record_offsets_dev(ctx, X, rec_base, total, n_ref, nullptr, 0, &n);
+    // the count walk keeps each chunk's record positions for the fill (in the sorted-records arena when it
+    // is already there: sort_stage writes it only later)
+    uint64_t n = 0, x = 0;
+    const auto y = ctx->bufs.find("pipe_y");
+    void *rel = y != ctx->bufs.end() ? y->second.p : nullptr;
+    const uint64_t rel_cap = rel ? y->second.cap : 0;
+    rc = oge_record_walk(ctx, X, rec_base, total, total, true, n_ref, nullptr, 0, &n, &x, true, rel, rel_cap);
     if (rc) return rc;
     uint64_t *xoff = (uint64_t *)ctx->ws("pipe_xoff", (n + 1) * 8);
     if (!xoff) return OGE_ERR_HIP;
-    rc = oge_bam_record_offsets_dev(ctx, X, rec_base, total, n_ref, xoff, n + 1, &n);
+    rc = oge_record_walk(ctx, X, rec_base, total, total, true, n_ref, xoff, n + 1, &n, &x, true);
     if (rc) return rc;
     ctx->end_stage(tm);
     *xoff_o = xoff;

@@ -384,10 +384,10 @@ int oge_decode_shard(oge_comm *comm, const uint8_t *d_z, uint64_t zbytes, uint64
         if (!rc && hipMemcpyAsync(xoff, &z, 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) rc = OGE_ERR_HIP;
         if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = OGE_ERR_HIP;
     } else {
-        rc = oge_record_walk(ctx, X, s_rec - B, T, T + L, at_end, n_ref, nullptr, 0, &n, &xe);
+        rc = oge_record_walk(ctx, X, s_rec - B, T, T + L, at_end, n_ref, nullptr, 0, &n, &xe, true);
         if (!rc) {
             xoff = (uint64_t *)ctx->ws("pipe_xoff", (n + 1) * 8);
-            rc = xoff ? oge_record_walk(ctx, X, s_rec - B, T, T + L, at_end, n_ref, xoff, n + 1, &n, &xe) : OGE_ERR_HIP;
+            rc = xoff ? oge_record_walk(ctx, X, s_rec - B, T, T + L, at_end, n_ref, xoff, n + 1, &n, &xe, true) : OGE_ERR_HIP;
         }
     }
     ctx->end_stage(tm);

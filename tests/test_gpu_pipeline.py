@@ -141,6 +141,25 @@ def test_pipeline_program_line_and_levels(ctx, tmp_path):
     assert pg[-1] == "@PG\tID:openge\tCL:openge mergesort -M x\tVN:0.3-dev"  # after the input's own @PG lines
 
 
+@pytest.mark.parametrize("slots", ["1", "8", "300"])
+def test_record_walk_slots(ctx, monkeypatch, tmp_path, slots):
+    """The record walk's fill expands the count walk's per-chunk record slots; a chunk with more records
+    than slots (OGE_RECWALK_SLOTS forces it) is walked again.  Same output either way, with the slots in
+    their own workspace (a fresh context: the sorted-records arena is not there yet) and in that arena."""
+    p = L.synth_params(60_000, preset="mix", seed=17)
+    recs, offs, hdr = L.synth_host(p)
+    L.write_bam(tmp_path / "in.bam", hdr, recs, offs, len(offs) - 1, level=1)
+    src = (tmp_path / "in.bam").read_bytes()
+    want = _run_pipeline(ctx, src, mark_duplicates=1)
+    monkeypatch.setenv("OGE_RECWALK_SLOTS", slots)
+    fresh = L.Context(0)
+    try:
+        assert _run_pipeline(fresh, src, mark_duplicates=1) == want
+        assert _run_pipeline(fresh, src, mark_duplicates=1) == want
+    finally:
+        fresh.close()
+
+
 def _run_host_pipeline(ctx, src_bytes: bytes, **kw):
     hz = torch.from_numpy(np.frombuffer(src_bytes, np.uint8).copy()).pin_memory()
     cap = len(src_bytes) * 2 + (1 << 20)
