@@ -61,6 +61,7 @@ KERNEL_STAGES = ["input_pass", "sort_radix", "sort_ties", "meta_gather", "md_mat
                  "md_apply", "gather_offsets", "gather_records"]
 SUB_STAGES = ["md_pair_win", "md_frag_win", "md_pair_ovf", "md_frag_ovf"]  # nested in md_pairs / md_frags: which group path ran
 E2E_STAGES = ["bgzf_index", "bgzf_inflate", "rec_walk"] + KERNEL_STAGES + ["bgzf_deflate"]
+INFL_PHASES = ["infl_huff", "infl_lz"]  # nested in bgzf_inflate: its two kernels' own times
 
 
 def parse():
@@ -183,6 +184,9 @@ def pmc_traffic(kernel: str, rec_bytes: int) -> dict | None:
 def stage_kernels(B: int, zin: int, zout: int, n: int, seq_bytes: int) -> dict:
     return {
         "bgzf_inflate": ("k_infl", "BGZF inflate: compressed bytes read + payload bytes written", zin + B, "valu"),
+        "infl_huff": ("k_infl_huff", "inflate phase 1, Huffman decode: compressed bytes read + every payload byte written "
+                      "(literal or copy descriptor)", zin + B, "valu"),
+        "infl_lz": ("k_infl_lz", "inflate phase 2, copies + CRC: payload bytes read + written", 2 * B, "valu"),
         "bgzf_deflate": ("k_defl", "BGZF deflate (greedy single-candidate, -c 6): payload read + compressed bytes written", B + zout, "valu"),
         "gather_records": ("k_gather16", "permutation gather + BAM re-encode: 2*B (SURVEY §8d sort bytes)", 2 * B, "hbm"),
         "input_pass": ("k_input_pass", "record parse: B - packed bases (SURVEY §8d dedup bytes) + 2N",
@@ -571,7 +575,7 @@ def main():
     out_bytes = nr = nd = 0
     for _ in range(args.steps):
         d_out, out_bytes, nr, nd = step()
-        for s, v in stage_ms(ctx, E2E_STAGES).items():
+        for s, v in stage_ms(ctx, E2E_STAGES + INFL_PHASES).items():
             tot[s] = tot.get(s, 0.0) + v
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
@@ -586,7 +590,7 @@ def main():
 
     # roofline: the dominant kernel of the e2e step (bound per stage; VALU fraction for the codec)
     kinfo = stage_kernels(B, zbytes, out_bytes, n, seq_bytes)
-    t_dom, s_dom = max((sms.get(s, 0.0), s) for s in kinfo)
+    t_dom, s_dom = max((sms.get(s, 0.0), s) for s in kinfo if s not in INFL_PHASES)
     roof = roofline_entry(s_dom, kinfo[s_dom], t_dom, B)
     others = [roofline_entry(s, kinfo[s], sms[s], B) for s in kinfo if sms.get(s, 0.0) > 0]
 

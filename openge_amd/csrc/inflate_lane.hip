@@ -1132,11 +1132,16 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         const Set &u = B[k % S];
         OGE_HIP_TRY(ctx, hipMemsetAsync(u.next, 0, 8, u.st));
         OGE_HIP_TRY(ctx, hipMemsetAsync(u.bitmap, 0, nb * 2048 * 8, u.st));  // phase 1 stores only words with bits
+        // each phase's own time (stages "infl_huff" / "infl_lz", summed over the chunks) on the one stream
+        OgeStageTimer *t1 = S == 1 ? ctx->begin_stage("infl_huff") : nullptr;
         k_infl_huff<<<g1, 64, 0, u.st>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, u.bitmap, u.xtab, u.scr, err, u.next);
         OGE_LAUNCH_CHECK(ctx);
+        ctx->end_stage(t1);
+        OgeStageTimer *t2 = S == 1 ? ctx->begin_stage("infl_lz") : nullptr;
         k_infl_lz<<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)ncu), kT2, 0, u.st>>>(out, uoff, crc, u.bitmap, u.xtab, b0, nb,
                                                                                    zpow, err);
         OGE_LAUNCH_CHECK(ctx);
+        ctx->end_stage(t2);
     }
     if (S > 1) {  // the context stream waits for every chunk
         for (int j = 0; j < S; ++j) {

@@ -29,14 +29,16 @@ def per_kernel(path, totals=None, scale=1024.0):
 # the stage ran in the profiled command): one entry per stage with its bytes per run, listed first so
 # bench.py's pmc_traffic finds the stage before any single kernel of it
 def stage_entries(ft, wt, spec, vt=None):
+    import re
     out = {}
     for item in filter(None, spec.split(",")):
         pre, runs = item.split("=")
-        f = sum(v for k, v in ft.items() if pre + "_" in k) / float(runs)
-        w = sum(v for k, v in wt.items() if pre + "_" in k) / float(runs)
+        m = re.compile(re.escape(pre) + r"[_(<]").search  # k_infl: k_infl_*; k_infl_huff: that kernel alone
+        f = sum(v for k, v in ft.items() if m(k)) / float(runs)
+        w = sum(v for k, v in wt.items() if m(k)) / float(runs)
         e = {"fetch_size_bytes": f, "write_size_bytes": w, "hbm_bytes": 2 * f + w}
         if vt:
-            e["valu_insts"] = sum(v for k, v in vt.items() if pre + "_" in k) / float(runs)
+            e["valu_insts"] = sum(v for k, v in vt.items() if m(k)) / float(runs)
         out[f"{pre} (stage: all {pre}_* launches of one run)"] = e
     return out
 
