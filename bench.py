@@ -159,12 +159,22 @@ def stage_ms(ctx, names) -> dict:
     return out
 
 
+def pmc_files() -> list:
+    """profiles/r<round><tag>_pmc.json oldest first: round, then tag by length and letters (r05z < r05aa)."""
+    import re
+
+    def key(f):
+        m = re.match(r"r(\d+)([a-z]*)", f.name)
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, f.name)
+    return sorted((f for f in (ROOT / "profiles").glob("r*_pmc.json") if "realign" not in f.name), key=key)
+
+
 def pmc_traffic(kernel: str, rec_bytes: int) -> dict | None:
     """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/r*_pmc.json,
     written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes,
     FETCH_SIZE doubled per MI355X_MICROARCH.md).  Scaled by record bytes when the profiled workload
     differed."""
-    files = sorted(f for f in (ROOT / "profiles").glob("r*_pmc.json") if "realign" not in f.name)
+    files = pmc_files()
     for fn in reversed(files):
         try:
             d = json.loads(fn.read_text())
@@ -197,7 +207,7 @@ def stage_kernels(B: int, zin: int, zout: int, n: int, seq_bytes: int) -> dict:
 def pmc_valu(kernel: str, rec_bytes: int) -> dict | None:
     """VALU lane-instructions per launch of a stage's kernels (SQ_INSTS_VALU x 64) from the newest
     committed PMC summary that has them, scaled by record bytes like pmc_traffic."""
-    files = sorted(f for f in (ROOT / "profiles").glob("r*_pmc.json") if "realign" not in f.name)
+    files = pmc_files()
     for fn in reversed(files):
         try:
             d = json.loads(fn.read_text())

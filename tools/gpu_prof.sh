@@ -1,6 +1,7 @@
 #!/bin/bash
 # the round's profiles without the bench line: rocprofv3 kernel stats of a short bench, then FETCH_SIZE /
-# WRITE_SIZE / SQ_INSTS_VALU passes over one e2e step (input build + step: k_defl runs twice, k_infl once)
+# WRITE_SIZE / SQ_INSTS_VALU passes over one e2e step (input build + step: k_defl runs twice, k_infl once);
+# summarise with STAGES="k_defl=2,k_infl=1,k_infl_huff=1,k_infl_lz=1" python tools/pmc_summary.py gpurun_out/TAG profiles/TAG
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:-prof}
