@@ -98,6 +98,10 @@ int oge_gather_records_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *
 int oge_radix_sort_pairs_dev(oge_ctx *ctx, uint64_t *d_keys, uint32_t *d_vals, uint64_t *d_ktmp, uint32_t *d_vtmp,
                              uint64_t n, uint64_t bit_mask, int *in_tmp_out);
 
+/* Device primitive behind every compaction and offset table, exposed for tests: exclusive prefix sum
+ * of n unsigned elements of elem_bytes (4 or 8) bytes, d_out may equal d_in.  Synchronous. */
+int oge_exclusive_scan_dev(oge_ctx *ctx, const void *d_in, void *d_out, uint64_t n, int elem_bytes);
+
 /* ---- duplicate marking (MarkDuplicates) ------------------------------------------- */
 typedef struct oge_markdup_opts {
     int32_t n_ref;

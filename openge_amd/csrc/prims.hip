@@ -93,9 +93,111 @@ __global__ __launch_bounds__(kThreads) void k_scan_add(T *__restrict__ out, uint
     }
 }
 
+// Reduce-then-scan over 16-byte chunks (r05; in and out 16-byte aligned): a block owns 1024 chunks
+// (16 KiB: 4096 u32 / 2048 u64), lane l of wave w the chunks w*256 + j*64 + l (j < 4), so every load and
+// store instruction of a wave covers 1 KiB contiguously.  k_scanv_reduce reads the tile and writes its sum;
+// k_scanv_down reads it again, scans it in registers (a wave scan over the lanes per j, then the waves) and
+// writes it with the tile's offset: 3n element moves and full 16-byte lanes, against 4n for k_scan_tiles +
+// k_scan_add with each thread's 8 elements in 8 narrow loads (300M u32: 1.55 ms).  A chunk that ends past n
+// is read and written element by element.
+constexpr int kVJ = 4;                      // chunks per lane
+constexpr int kVTile = kThreads * kVJ;      // chunks per block
+
+template <class T>
+__device__ __forceinline__ void load_chunk(const T *__restrict__ in, uint64_t c, uint64_t n, T (&v)[16 / sizeof(T)]) {
+    constexpr int E = 16 / sizeof(T);
+    const uint64_t e0 = c * E;
+    if (e0 + E <= n) {
+        const uint4 q = *(const uint4 *)(in + e0);
+        __builtin_memcpy(v, &q, 16);
+    } else {
+#pragma unroll
+        for (int k = 0; k < E; ++k) v[k] = e0 + k < n ? in[e0 + k] : (T)0;
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(kThreads) void k_scanv_reduce(const T *__restrict__ in, uint64_t n, T *__restrict__ sums) {
+    constexpr int E = 16 / sizeof(T);
+    const uint64_t c0 = (uint64_t)blockIdx.x * kVTile + (threadIdx.x >> 6) * 256 + lane_id();
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < kVJ; ++j) {
+        T v[E];
+        load_chunk(in, c0 + 64 * j, n, v);
+#pragma unroll
+        for (int k = 0; k < E; ++k) s += v[k];
+    }
+    T total;
+    (void)block_excl_scan(s, &total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+template <class T>
+__global__ __launch_bounds__(kThreads) void k_scanv_down(const T *in, T *out, uint64_t n, const T *__restrict__ sums) {
+    constexpr int E = 16 / sizeof(T);
+    __shared__ T wt[kWaves];
+    const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+    const uint64_t c0 = (uint64_t)blockIdx.x * kVTile + w * 256 + lane;
+    T v[kVJ][E], ex[kVJ];
+#pragma unroll
+    for (int j = 0; j < kVJ; ++j) load_chunk(in, c0 + 64 * j, n, v[j]);  // all loads before any store: out may be in
+    T run = 0;  // the wave's running total over its stripes j
+#pragma unroll
+    for (int j = 0; j < kVJ; ++j) {
+        T cs = 0;
+#pragma unroll
+        for (int k = 0; k < E; ++k) cs += v[j][k];
+        const T inc = wave_incl_scan(cs);
+        ex[j] = run + inc - cs;
+        run += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) wt[w] = run;
+    __syncthreads();
+    T off = sums ? sums[blockIdx.x] : (T)0;
+    for (uint32_t i = 0; i < w; ++i) off += wt[i];
+#pragma unroll
+    for (int j = 0; j < kVJ; ++j) {
+        const uint64_t e0 = (c0 + 64 * j) * E;
+        T o[E];
+        T x = off + ex[j];
+#pragma unroll
+        for (int k = 0; k < E; ++k) o[k] = x, x += v[j][k];
+        if (e0 + E <= n) {
+            uint4 q;
+            __builtin_memcpy(&q, o, 16);
+            *(uint4 *)(out + e0) = q;
+        } else {
+#pragma unroll
+            for (int k = 0; k < E; ++k)
+                if (e0 + k < n) out[e0 + k] = o[k];
+        }
+    }
+}
+
 template <class T>
 int scan_impl(oge_ctx *ctx, const T *in, T *out, uint64_t n, int level) {
     if (n == 0) return OGE_OK;
+    if (!(((uintptr_t)in | (uintptr_t)out) & 15)) {
+        constexpr uint64_t per = (uint64_t)kVTile * (16 / sizeof(T));
+        const uint32_t nb = oge_ceil_div(n, per);
+        if (nb == 1) {
+            hipLaunchKernelGGL(k_scanv_down<T>, dim3(1), dim3(kThreads), 0, ctx->stream, in, out, n, (const T *)nullptr);
+            OGE_LAUNCH_CHECK(ctx);
+            return OGE_OK;
+        }
+        char name[32];
+        snprintf(name, sizeof(name), "scan_sums_%d_%zu", level, sizeof(T));
+        T *sums = (T *)ctx->ws(name, (size_t)nb * sizeof(T));
+        if (!sums) return OGE_ERR_HIP;
+        hipLaunchKernelGGL(k_scanv_reduce<T>, dim3(nb), dim3(kThreads), 0, ctx->stream, in, n, sums);
+        OGE_LAUNCH_CHECK(ctx);
+        int rc = scan_impl<T>(ctx, sums, sums, nb, level + 1);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_scanv_down<T>, dim3(nb), dim3(kThreads), 0, ctx->stream, in, out, n, (const T *)sums);
+        OGE_LAUNCH_CHECK(ctx);
+        return OGE_OK;
+    }
     uint32_t nb = oge_ceil_div(n, kScanTile);
     if (nb == 1) {
         hipLaunchKernelGGL(k_scan_tiles<T>, dim3(1), dim3(kThreads), 0, ctx->stream, in, out, n, (T *)nullptr);
@@ -309,6 +411,18 @@ std::vector<Digit> plan_digits(uint64_t mask, uint32_t maxw) {
 }
 
 }  // namespace
+
+extern "C" int oge_exclusive_scan_dev(oge_ctx *ctx, const void *d_in, void *d_out, uint64_t n, int elem_bytes) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
+    if ((elem_bytes != 4 && elem_bytes != 8) || (n && (!d_in || !d_out)) || ((uintptr_t)d_in | (uintptr_t)d_out) % elem_bytes)
+        return oge_fail(ctx, OGE_ERR_ARG, "oge_exclusive_scan_dev: bad arguments");
+    hipSetDevice(ctx->device);
+    const int rc = elem_bytes == 4 ? scan_impl<uint32_t>(ctx, (const uint32_t *)d_in, (uint32_t *)d_out, n, 0)
+                                   : scan_impl<uint64_t>(ctx, (const uint64_t *)d_in, (uint64_t *)d_out, n, 0);
+    if (rc) return rc;
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return OGE_OK;
+}
 
 int oge_exclusive_scan_u32(oge_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n) {
     return scan_impl<uint32_t>(ctx, in, out, n, 0);

@@ -193,6 +193,7 @@ def lib() -> C.CDLL:
         "oge_sort_coord_dev": (C.c_int, [vp, vp, vp, u64, i32, vp]),
         "oge_gather_records_dev": (C.c_int, [vp, vp, vp, vp, u64, vp, vp]),
         "oge_radix_sort_pairs_dev": (C.c_int, [vp, vp, vp, vp, vp, u64, u64, C.POINTER(C.c_int)]),
+        "oge_exclusive_scan_dev": (C.c_int, [vp, vp, vp, u64, C.c_int]),
         "oge_markdup": (C.c_int, [vp, vp, u64, vp, u64, vp, vp, C.POINTER(u64)]),
         "oge_markdup_dev": (C.c_int, [vp, vp, vp, u64, vp, vp, C.c_int, C.POINTER(u64)]),
         "oge_sort_markdup_dev": (C.c_int, [vp, vp, vp, u64, vp, vp, vp, vp, C.POINTER(u64)]),
@@ -484,6 +485,10 @@ class Context:
         t = C.c_int()
         check(lib().oge_radix_sort_pairs_dev(self.h, d_keys, d_vals, d_ktmp, d_vtmp, n, bit_mask, C.byref(t)), self.h)
         return bool(t.value)
+
+    def exclusive_scan_dev(self, d_in, d_out, n: int, elem_bytes: int) -> None:
+        """oge_exclusive_scan_dev: exclusive prefix sum of n u32 (elem_bytes 4) or u64 (8) device elements."""
+        check(lib().oge_exclusive_scan_dev(self.h, d_in, d_out, n, elem_bytes), self.h)
 
     def bgzf_deflate(self, data: bytes | np.ndarray, level: int = 6) -> bytes:
         """BGZF-compress host bytes on the device (no EOF marker)."""

@@ -1,5 +1,5 @@
-"""GPU: the device radix sort every pipeline sort runs on (onesweep, decoupled look-back), against
-numpy's stable sort on the masked key bits."""
+"""GPU: the device radix sort every pipeline sort runs on (reduce-then-scan passes), against numpy's
+stable sort on the masked key bits; the exclusive scan behind every compaction and offset table."""
 import numpy as np
 import pytest
 
@@ -54,3 +54,37 @@ def test_radix_sort_all_equal(ctx):
     vals = np.arange(n, dtype=np.uint32)
     ko, vo = _sort(ctx, keys, vals, 0xFFFF)
     assert np.array_equal(vo, vals) and np.array_equal(ko, keys)
+
+
+@pytest.mark.parametrize("elem", [4, 8])
+@pytest.mark.parametrize("n", [0, 1, 3, 4, 5, 4095, 4096, 4097, 2048 * 3 + 1, 1 << 20, 300_007, 12_345_678])
+@pytest.mark.parametrize("shift", [0, 1])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_exclusive_scan(ctx, elem, n, shift, inplace):
+    """Aligned buffers take the 16-byte-chunk reduce-then-scan (ragged tails element by element),
+    misaligned ones (shift = one element) the narrow kernels; both against numpy, wrapping like the
+    unsigned device arithmetic."""
+    import torch
+    if n > (1 << 20) and (shift or inplace):
+        pytest.skip("large case: aligned out-of-place only")
+    dt = np.uint32 if elem == 4 else np.uint64
+    rng = np.random.default_rng(n + elem)
+    hi = 1 << 20 if elem == 4 else 1 << 40
+    a = rng.integers(0, hi, size=n, dtype=np.uint64).astype(dt)
+    want = np.zeros(n, dtype=dt)
+    if n:
+        want[1:] = np.cumsum(a[:-1], dtype=dt)
+    tdt = torch.int32 if elem == 4 else torch.int64
+    dev = torch.device("cuda", 0)
+    buf = torch.zeros(n + shift + 8, dtype=tdt, device=dev)
+    buf[shift:shift + n] = torch.from_numpy(a.view(np.int32 if elem == 4 else np.int64)).to(dev)
+    out = buf if inplace else torch.full((n + shift + 8,), -1, dtype=tdt, device=dev)
+    base = buf.data_ptr() + shift * elem
+    ctx.exclusive_scan_dev(base, out.data_ptr() + shift * elem, n, elem)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(dt)
+    assert np.array_equal(got[shift:shift + n], want)
+    if not inplace:  # nothing written outside [0, n)
+        assert (got[shift + n:] == dt(-1 & (0xFFFFFFFF if elem == 4 else 0xFFFFFFFFFFFFFFFF))).all()
+        if shift:
+            assert got[0] == dt(0xFFFFFFFF if elem == 4 else 0xFFFFFFFFFFFFFFFF)
