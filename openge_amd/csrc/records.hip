@@ -60,11 +60,27 @@ __device__ __forceinline__ uint32_t qsum4(uint32_t w, uint32_t acc) {
     return __builtin_amdgcn_sad_u8(w & ((ge >> 7) * 0xffu), 0u, acc);
 }
 
-// FNV-1a (64-bit) over the pair key, finished with the MurmurHash3 fmix64 avalanche so every bit
-// of the 48 kept is usable as a radix digit (the mate join sorts by as many bits as fit)
-__device__ __forceinline__ uint64_t h_step(uint64_t h, uint32_t c) { return (h ^ c) * 0x100000001b3ull; }
+// The pair-key hash (split chain, RG string, read name) folded 4 bytes at a time -- each segment's length,
+// then its little-endian words, the tail zero-padded; a 64-bit multiply per word -- and finished with the
+// MurmurHash3 fmix64 avalanche so every bit of the 48 kept is usable as a radix digit (the mate join sorts
+// by as many bits as fit).  Any function of the key bytes serves: the mate join and the pair groups
+// confirm the exact key (test_gpu_parity forces collisions).  r05: words instead of a byte-wise FNV-1a
+// chain, whose one dependent LDS byte read per step sat on the parse's critical path.
+__device__ __forceinline__ uint64_t h_word(uint64_t h, uint32_t w) { return (h ^ w) * 0x9e3779b97f4a7c15ull; }
 __device__ __forceinline__ uint64_t h_fmix(uint64_t h) {
     h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; return h ^ (h >> 33);
+}
+template <class Rd>
+__device__ __forceinline__ uint64_t h_bytes(const Rd &rd, uint64_t h, uint64_t p, uint32_t len) {
+    h = h_word(h, len);
+    uint32_t y = 0;
+    for (; y + 4 <= len; y += 4) h = h_word(h, rd.u32(p + y));
+    if (y < len) {
+        uint32_t w = 0;
+        for (uint32_t k = 0; y + k < len; ++k) w |= rd.u8(p + y + k) << (8 * k);
+        h = h_word(h, w);
+    }
+    return h;
 }
 
 // Record at absolute index r of reader `rd`; i = record index, src = its offset in the arena.
@@ -186,18 +202,14 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
         if (paired_mm) {
             m |= OGE_M_CAND;
             uint64_t h = 0xcbf29ce484222325ull;
-            if (a.rg.split_k > 1) h = h_step(h, 0x100u + (uint32_t)(ref % a.rg.split_k));  // the chain
-            for (uint32_t y = 0; y < rgl; ++y) h = h_step(h, rd.u8(rgv + y));
-            h = h_step(h, ':');
-            const uint32_t nl = lname ? lname - 1u : 0u;
-            for (uint32_t y = 0; y < nl; ++y) h = h_step(h, rd.u8(r + OGE_OFF_NAME + y));
-            h = h_fmix(h);
-            M.hash = (uint32_t)h;
-            M.hash_hi = (uint16_t)(h >> 32);
-            // name slot: l_read_name bytes (with the NUL) when they fit, zero-padded
+            if (a.rg.split_k > 1) h = h_word(h, 0x100u + (uint32_t)(ref % a.rg.split_k));  // the chain
+            h = h_bytes(rd, h, rgv, rgl);
+            // name slot: l_read_name bytes (with the NUL) when they fit, zero-padded; its words also feed the
+            // hash (equal keys have equal lengths, so both take the same branch)
             if (lname <= OGE_NAME_SLOT) {
                 m |= OGE_M_NAMEFIT;
                 uint32_t *ns = (uint32_t *)M.name;
+                h = h_word(h, lname);
 #pragma unroll
                 for (uint32_t q = 0; q < OGE_NAME_SLOT / 4; ++q) {
                     uint32_t v = 0;
@@ -208,7 +220,15 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
                     }
                     ns[q] = v;
                 }
+#pragma unroll
+                for (uint32_t q = 0; q < OGE_NAME_SLOT / 4; ++q)
+                    if (4 * q < lname) h = h_word(h, ns[q]);
+            } else {
+                h = h_bytes(rd, h, r + OGE_OFF_NAME, lname - 1u);
             }
+            h = h_fmix(h);
+            M.hash = (uint32_t)h;
+            M.hash_hi = (uint16_t)(h >> 32);
         }
     }
     M.m = m;
