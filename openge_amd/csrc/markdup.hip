@@ -965,14 +965,20 @@ int oge_markdup_prepare(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, 
         offs[g + 1] = offs[g] + (uint32_t)L + 1;
         p += L + 1;
     }
+    std::vector<uint8_t> w16((size_t)opts->n_rg * 16, 0);  // idw: ids of <= 15 bytes, zero-padded
+    for (int32_t g = 0; g < opts->n_rg; ++g)
+        if (offs[g + 1] - offs[g] - 1 <= 15) memcpy(&w16[(size_t)g * 16], opts->rg_ids + offs[g], offs[g + 1] - offs[g] - 1);
     uint8_t *ids = (uint8_t *)ctx->ws("md_rgids", offs.back() + 16);
+    uint4 *idw = (uint4 *)ctx->ws("md_rgidw", w16.size() + 16);
     uint32_t *doff = (uint32_t *)ctx->ws("md_rgoff", offs.size() * 4);
     int16_t *lib = (int16_t *)ctx->ws("md_rglib", (size_t)(opts->n_rg + 1) * 2);
-    if (!*meta || !ids || !doff || !lib) return OGE_ERR_HIP;
+    if (!*meta || !ids || !idw || !doff || !lib) return OGE_ERR_HIP;
     if (offs.back()) OGE_HIP_TRY(ctx, hipMemcpyAsync(ids, opts->rg_ids, offs.back(), hipMemcpyHostToDevice, ctx->stream));
+    if (!w16.empty()) OGE_HIP_TRY(ctx, hipMemcpyAsync(idw, w16.data(), w16.size(), hipMemcpyHostToDevice, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(doff, offs.data(), offs.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     if (opts->n_rg) OGE_HIP_TRY(ctx, hipMemcpyAsync(lib, opts->rg_lib, (size_t)opts->n_rg * 2, hipMemcpyHostToDevice, ctx->stream));
     rg->ids = ids;
+    rg->idw = idw;
     rg->off = doff;
     rg->lib = lib;
     rg->n_rg = opts->n_rg;

@@ -31,9 +31,11 @@ constexpr int32_t OGE_RGI_NONE = -2, OGE_RGI_UNLISTED = -1;
 constexpr int32_t OGE_MAX_RG = 32767;  // read groups addressable by RecMeta.rgi
 __host__ __device__ inline uint64_t oge_meta_hash48(const RecMeta &M) { return ((uint64_t)M.hash_hi << 32) | M.hash; }
 
-// Read-group table on the device: ids back to back, off[g]..off[g+1]-1 is "ID\0" of group g.
+// Read-group table on the device: ids back to back, off[g]..off[g+1]-1 is "ID\0" of group g; idw[g]
+// the same id zero-padded to 16 bytes when it has at most 15 (a word compare in the input pass).
 struct OgeRgTable {
     const uint8_t *ids;
+    const uint4 *idw;
     const uint32_t *off;
     const int16_t *lib;
     int32_t n_rg;

@@ -152,8 +152,22 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
             const uint32_t t0 = w & 0xff, t1 = (w >> 8) & 0xff, type = (w >> 16) & 0xff;
             p += 3;
             if (t0 == 'R' && t1 == 'G') {
+                // the value's NUL: four bytes per read (the first zero byte of a word by the borrow trick)
                 uint64_t s = p;
-                while (s < tend && rd.u8(s)) ++s;
+                for (;;) {
+                    if (s + 4 <= tend) {
+                        const uint32_t v = rd.u32(s);
+                        const uint32_t z = (v - 0x01010101u) & ~v & 0x80808080u;
+                        if (z) {
+                            s += (uint32_t)__builtin_ctz(z) >> 3;
+                            break;
+                        }
+                        s += 4;
+                    } else {
+                        while (s < tend && rd.u8(s)) ++s;
+                        break;
+                    }
+                }
                 rgv = p;
                 rgl = (uint32_t)(s - p);
                 has = true;
@@ -183,6 +197,22 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
             }
             if (!ok || p >= tend || rd.u8(p) == 0) break;
         }
+        // an RG value of <= 15 bytes as four zero-padded words (compared with the table's idw and hashed)
+        uint32_t rv[4] = {0u, 0u, 0u, 0u};
+        if (rgl <= 15) {
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                if (4 * q >= rgl) continue;
+                uint32_t v = 0;
+                if (rgv + 4 * q + 4 <= tend) {
+                    v = rd.u32(rgv + 4 * q);
+                } else {
+                    for (uint32_t k = 0; 4 * q + k < rgl; ++k) v |= rd.u8(rgv + 4 * q + k) << (8 * k);
+                }
+                const uint32_t rem = rgl - 4 * q;
+                rv[q] = rem < 4 ? v & ((1u << (8 * rem)) - 1u) : v;
+            }
+        }
         int16_t lib = a.rg.unknown_lib;
         M.rgi = OGE_RGI_NONE;
         if (has && rgl) {
@@ -191,7 +221,12 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
                 const uint32_t o = a.rg.off[g], Lg = a.rg.off[g + 1] - o - 1;
                 if (Lg != rgl) continue;
                 bool eq = true;
-                for (uint32_t y = 0; y < Lg && eq; ++y) eq = a.rg.ids[o + y] == rd.u8(rgv + y);
+                if (Lg <= 15) {
+                    const uint4 w = a.rg.idw[g];
+                    eq = w.x == rv[0] && w.y == rv[1] && w.z == rv[2] && w.w == rv[3];
+                } else {
+                    for (uint32_t y = 0; y < Lg && eq; ++y) eq = a.rg.ids[o + y] == rd.u8(rgv + y);
+                }
                 if (eq) { lib = a.rg.lib[g]; M.rgi = (int16_t)g; break; }
             }
         }
@@ -203,7 +238,14 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
             m |= OGE_M_CAND;
             uint64_t h = 0xcbf29ce484222325ull;
             if (a.rg.split_k > 1) h = h_word(h, 0x100u + (uint32_t)(ref % a.rg.split_k));  // the chain
-            h = h_bytes(rd, h, rgv, rgl);
+            if (rgl <= 15) {  // the words read for the lookup (equal keys: equal lengths, the same branch)
+                h = h_word(h, rgl);
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q)
+                    if (4 * q < rgl) h = h_word(h, rv[q]);
+            } else {
+                h = h_bytes(rd, h, rgv, rgl);
+            }
             // name slot: l_read_name bytes (with the NUL) when they fit, zero-padded; its words also feed the
             // hash (equal keys have equal lengths, so both take the same branch)
             if (lname <= OGE_NAME_SLOT) {

@@ -214,3 +214,42 @@ def test_fused_windowed_groups_overflow_path(ctx, monkeypatch, cap):
     assert nd_w == ond
     prim = odup != 2
     assert np.array_equal((fl_w[prim] & 0x400) != 0, odup[prim] == 1)
+
+
+@pytest.mark.parametrize("width", [1, 4, 15, 16, 23])
+def test_markdup_read_group_widths(ctx, width):
+    """Read-group ids of every width around the input pass's word compare (<= 15 bytes: the padded
+    16-byte table; longer: byte by byte), two of them sharing a prefix, plus an id missing from the header:
+    libraries (RG -> LB) and pair keys (RG + name) must give the oracle's dup flags."""
+    from bamutil import rec_bytes, pack_records
+    p = L.synth_params(3000, preset="mix", seed=41)
+    recs, offs, hdr = L.synth_host(p)
+    n = 2 * 3000
+    ids = {k: (f"g{k}" + "x" * width)[:width] if width > 1 else chr(ord("a") + k) for k in range(1, p.n_rg + 1)}
+    if width > 2:
+        ids[2] = ids[1][:-1] + "Y"  # same length, same prefix as group 1
+    lines = []
+    for line in hdr.splitlines():
+        if line.startswith("@RG"):
+            f = line.split("\t")
+            k = int(f[1][len("ID:rg"):])
+            f[1] = "ID:" + ids[k]
+            line = "\t".join(f)
+        lines.append(line)
+    hdr2 = "\n".join(lines) + "\n"
+    out = []
+    for i in range(n):
+        b = bytearray(rec_bytes(recs, offs[i]))
+        assert bytes(b[-7:-4]) == b"RGZ"
+        k = b[-2] - ord("0")
+        v = ids[k] if i % 97 else "unlisted" + "z" * (width % 5)
+        b = b[:-4] + v.encode() + b"\0"
+        b[0:4] = (len(b) - 4).to_bytes(4, "little")
+        out.append(bytes(b))
+    r2, o2 = pack_records(out)
+    perm = oracle.sort_perm(r2, o2, n)
+    srecs, soffs = pack_records([rec_bytes(r2, o2[i]) for i in perm])
+    opts, keep = L.markdup_opts_from_header(hdr2, p.n_ref)
+    dup, nd = ctx.markdup(srecs, soffs, n, opts)
+    odup, ond = oracle.markdup(srecs, soffs, n, hdr2)
+    assert nd == ond and np.array_equal(dup, odup)
