@@ -1009,6 +1009,7 @@ static int realign_ranks(ChainContext &cc, ReadBatch &b, const std::string &ht, 
 }
 
 int LocalRealignment::runInternal(ChainContext &cc, ReadBatch &b) {
+    const auto t0 = std::chrono::steady_clock::now();
     if (cc.to_host(b)) return -1;
     cc.free_device(b);
     const std::string ht = b.header.to_string();
@@ -1017,19 +1018,59 @@ int LocalRealignment::runInternal(ChainContext &cc, ReadBatch &b) {
     oge_realign_opts_init(&o);
     o.threads = cc.threads;
     oge_realign_result *r = nullptr;
+    const auto t1 = std::chrono::steady_clock::now();
     if (oge_localrealign(cc.ctx, ht.data(), ht.size(), b.recs.data(), b.offs.data(), b.n, reference_.c_str(),
                          intervals_.c_str(), &o, &r))
         return cc.fail("LocalRealignment");
+    const auto t2 = std::chrono::steady_clock::now();
     uint64_t bytes = 0;
     const uint8_t *rp = oge_realign_result_records(r, &bytes);
     const uint64_t *op = oge_realign_result_offsets(r);
     const uint64_t n = oge_realign_result_count(r);
-    b.recs.assign(rp, rp + bytes);
-    b.recs.resize(bytes + 16, 0);
-    b.offs.assign(op, op + n + 1);
+    // The result goes straight up to the device when it fits (the writer deflates it there; a host module
+    // downloads it again): a host copy of the 1.1 GB C5 result cost 0.52 s of fresh-page faults, the upload
+    // ~0.06 s.  The offsets are rebased to the uploaded range.
+    uint64_t fr = 0, tot = 0;
+    const uint64_t base = n ? op[0] : 0, len = n ? op[n] - base : 0;
+    void *dr = nullptr, *dof = nullptr;
+    bool up = n && !bgzf_host_codec_forced() && !oge_mem_info(cc.ctx, &fr, &tot) &&
+              2 * len + (n + 1) * 16 + (256ull << 20) < fr;
+    if (up) {
+        std::vector<uint64_t> ro(op, op + n + 1);
+        for (auto &x : ro) x -= base;
+        up = !oge_dev_alloc(cc.ctx, len + 64, &dr) && !oge_dev_alloc(cc.ctx, (n + 1) * 8, &dof) &&
+             !oge_memcpy(cc.ctx, dr, rp + base, len, 1) && !oge_memcpy(cc.ctx, dof, ro.data(), (n + 1) * 8, 1);
+        if (up) {
+            b.recs.clear();
+            b.recs.shrink_to_fit();
+            b.offs.clear();
+            b.offs.shrink_to_fit();
+            b.d_recs = (uint8_t *)dr;
+            b.d_offs = (uint64_t *)dof;
+            b.d_bytes = len;
+            b.dev_valid = true;
+            b.host_valid = false;
+        } else {
+            if (dr) oge_dev_free(cc.ctx, dr);
+            if (dof) oge_dev_free(cc.ctx, dof);
+        }
+    }
+    if (!up) {
+        b.recs.assign(rp, rp + bytes);
+        b.recs.resize(bytes + 16, 0);
+        b.offs.assign(op, op + n + 1);
+    }
     b.n = n;
+    const auto t3 = std::chrono::steady_clock::now();
     if (verbose) fprintf(stderr, "[openge] LocalRealignment: %s\n", oge_realign_result_stats(r));
     oge_realign_result_free(r);
+    if (verbose) {
+        auto sec = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point z) {
+            return std::chrono::duration<double>(z - a).count();
+        };
+        fprintf(stderr, "[openge] LocalRealignment: records to host %.3f s, realign %.3f s, result %s %.3f s, release %.3f s\n",
+                sec(t0, t1), sec(t1, t2), up ? "to the device" : "host copy", sec(t2, t3), sec(t3, std::chrono::steady_clock::now()));
+    }
     return 0;
 }
 
@@ -1111,14 +1152,22 @@ int FileWriter::write_device(ChainContext &cc, ReadBatch &b, BgzfWriter &w, doub
     }
     *t_dev += sec(t, clk());
     const uint64_t len = ends[1] - ends[0];
-    const uint64_t kSeg = 65280ull * 32768;  // 2.14 GB of records per segment
+    // segments of 1024-32768 payloads (67 MB - 2.14 GB of records), about an eighth of the stream: the
+    // page-locked download buffers are sized by the segment and pinning / unpinning them costs ~0.25 s per
+    // GB (a 1.1 GB realign output: 0.5 s in 2.1 GB segments, 0.04 s in 67 MB ones), while a large file keeps
+    // full-size deflate calls.  OGE_WRITE_SEG_BLOCKS fixes the payloads per segment (tests).
+    const char *se = getenv("OGE_WRITE_SEG_BLOCKS");
+    const uint64_t want = se ? std::max(1ul, strtoul(se, nullptr, 10)) : std::min<uint64_t>(32768, std::max<uint64_t>(1024, len / 8 / 65280 + 1));
+    const uint64_t kSeg = 65280ull * want;
     const uint64_t seg = std::min(len, kSeg);
     const uint64_t cap = oge_bgzf_bound(seg);
+    t = clk();
     if (len && (oge_dev_alloc(cc.ctx, cap, &dz) || oge_host_alloc(cc.ctx, cap, &hz[0]) ||
                 (len > seg && oge_host_alloc(cc.ctx, cap, &hz[1])))) {
         release();
         return cc.fail("FileWriter: buffers");
     }
+    if (getenv("OGE_WRITE_TRACE")) fprintf(stderr, "[openge] FileWriter: buffers %.3f s\n", sec(t, clk()));
     w.write_compressed(nullptr, 0);  // flush the header as blocks of its own
     int k = 0;
     for (uint64_t s0 = 0; s0 < len; s0 += seg, k ^= 1) {
@@ -1146,7 +1195,9 @@ int FileWriter::write_device(ChainContext &cc, ReadBatch &b, BgzfWriter &w, doub
     t = clk();
     if (wr.joinable()) wr.join();
     *t_wait += sec(t, clk());
+    t = clk();
     release();
+    if (getenv("OGE_WRITE_TRACE")) fprintf(stderr, "[openge] FileWriter: release %.3f s\n", sec(t, clk()));
     return 0;
 }
 
@@ -1271,8 +1322,25 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
     };
     const auto t0 = clk();
     const bool sliced = !b.slices.empty(), produced = (bool)b.produce;
-    const bool on_device = sliced || produced || (b.dev_valid && !b.host_valid && !bgzf_host_codec_forced());
+    bool on_device = sliced || produced || (b.dev_valid && !b.host_valid && !bgzf_host_codec_forced());
     double t_dev = 0, t_d2h = 0, t_wait = 0;
+    // Host records (the realigner's output) whose bytes sit back to back: up to the device and out through
+    // the GPU deflate -- on the C5 set 1.1 GB of records take 0.78 s with 16 libdeflate threads
+    // (profiles/r05ap_realign_cli.txt), the upload and the device path a fraction of that.  A device that
+    // cannot hold them leaves the host writer in charge.
+    if (!on_device && b.host_valid && !b.dev_valid && b.n && !bgzf_host_codec_forced()) {
+        bool contiguous = b.offs.size() == b.n + 1 && b.offs[b.n] + 16 <= b.recs.size();
+        for (uint64_t k = 0; contiguous && k < b.n; ++k)
+            contiguous = b.offs[k + 1] == b.offs[k] + 4 + oge_rd_u32(b.recs.data() + b.offs[k]);
+        uint64_t fr = 0, tot = 0;
+        const uint64_t bytes = contiguous ? b.offs[b.n] : 0;
+        if (contiguous && !oge_mem_info(cc.ctx, &fr, &tot) && bytes + oge_bgzf_bound(std::min<uint64_t>(bytes, 65280ull * 32768)) +
+                                                                      (b.n + 1) * 8 + (256ull << 20) < fr) {
+            if (cc.to_device(b)) return -1;
+            on_device = true;
+            b.host_valid = false;  // write_device reads the device copy
+        }
+    }
     if (!on_device && cc.to_host(b)) return -1;
     const auto t1 = clk();
     if (!on_device) fix_bins(b, cc.threads);
@@ -1325,7 +1393,7 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
         return -1;
     }
     if (verbose_ && on_device)
-        fprintf(stderr, "[openge] FileWriter: device bins + BGZF %.3f s (gpu, 2.1 GB segments), device->host %.3f s, waiting on the disk %.3f s, "
+        fprintf(stderr, "[openge] FileWriter: device bins + BGZF %.3f s (gpu, segmented), device->host %.3f s, waiting on the disk %.3f s, "
                 "total %.3f s\n", t_dev, t_d2h, t_wait, sec(t2, clk()));
     else if (verbose_)
         fprintf(stderr, "[openge] FileWriter: device->host %.3f s, bins %.3f s, BGZF %.3f s (%s)\n", sec(t0, t1), sec(t1, t2),
