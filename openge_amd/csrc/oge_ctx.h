@@ -99,6 +99,9 @@ static inline uint32_t oge_ceil_div(uint64_t a, uint64_t b) { return (uint32_t)(
 // In-place-or-not exclusive scans. `out` may alias `in`.
 int oge_exclusive_scan_u32(oge_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n);
 int oge_exclusive_scan_u64(oge_ctx *ctx, const uint64_t *in, uint64_t *out, uint64_t n);
+// out[0..n] = the exclusive scan of the record sizes in sorted keys' payload bits (key >> 50), out[n] = their
+// total, in one reduce-then-scan (keys and out 16-byte aligned; returns 1 without work otherwise)
+int oge_offsets_from_keys(oge_ctx *ctx, const uint64_t *keys, uint64_t n, uint64_t *out);
 // Stable LSD radix sort of (key, value) pairs on key bits selected by `bit_mask` (only bits set
 // in the mask are sorted; set bits are grouped into digit passes of <= 8 contiguous bits).
 // Buffers: keys/vals hold the input; ktmp/vtmp scratch of the same size.  On return *kout/*vout

@@ -103,28 +103,34 @@ __global__ __launch_bounds__(kThreads) void k_scan_add(T *__restrict__ out, uint
 constexpr int kVJ = 4;                      // chunks per lane
 constexpr int kVTile = kThreads * kVJ;      // chunks per block
 
-template <class T>
-__device__ __forceinline__ void load_chunk(const T *__restrict__ in, uint64_t c, uint64_t n, T (&v)[16 / sizeof(T)]) {
+// SH: the element is in[i] >> SH (SH = 50: a sort key's record-size payload, sort.hip); elements at or past
+// n_in read as 0
+template <class T, int SH = 0>
+__device__ __forceinline__ void load_chunk(const T *__restrict__ in, uint64_t c, uint64_t n_in, T (&v)[16 / sizeof(T)]) {
     constexpr int E = 16 / sizeof(T);
     const uint64_t e0 = c * E;
-    if (e0 + E <= n) {
+    if (e0 + E <= n_in) {
         const uint4 q = *(const uint4 *)(in + e0);
         __builtin_memcpy(v, &q, 16);
     } else {
 #pragma unroll
-        for (int k = 0; k < E; ++k) v[k] = e0 + k < n ? in[e0 + k] : (T)0;
+        for (int k = 0; k < E; ++k) v[k] = e0 + k < n_in ? in[e0 + k] : (T)0;
+    }
+    if (SH) {
+#pragma unroll
+        for (int k = 0; k < E; ++k) v[k] >>= SH;
     }
 }
 
-template <class T>
-__global__ __launch_bounds__(kThreads) void k_scanv_reduce(const T *__restrict__ in, uint64_t n, T *__restrict__ sums) {
+template <class T, int SH = 0>
+__global__ __launch_bounds__(kThreads) void k_scanv_reduce(const T *__restrict__ in, uint64_t n_in, T *__restrict__ sums) {
     constexpr int E = 16 / sizeof(T);
     const uint64_t c0 = (uint64_t)blockIdx.x * kVTile + (threadIdx.x >> 6) * 256 + lane_id();
     T s = 0;
 #pragma unroll
     for (int j = 0; j < kVJ; ++j) {
         T v[E];
-        load_chunk(in, c0 + 64 * j, n, v);
+        load_chunk<T, SH>(in, c0 + 64 * j, n_in, v);
 #pragma unroll
         for (int k = 0; k < E; ++k) s += v[k];
     }
@@ -133,15 +139,15 @@ __global__ __launch_bounds__(kThreads) void k_scanv_reduce(const T *__restrict__
     if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
-template <class T>
-__global__ __launch_bounds__(kThreads) void k_scanv_down(const T *in, T *out, uint64_t n, const T *__restrict__ sums) {
+template <class T, int SH = 0>
+__global__ __launch_bounds__(kThreads) void k_scanv_down(const T *in, T *out, uint64_t n, uint64_t n_in, const T *__restrict__ sums) {
     constexpr int E = 16 / sizeof(T);
     __shared__ T wt[kWaves];
     const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
     const uint64_t c0 = (uint64_t)blockIdx.x * kVTile + w * 256 + lane;
     T v[kVJ][E], ex[kVJ];
 #pragma unroll
-    for (int j = 0; j < kVJ; ++j) load_chunk(in, c0 + 64 * j, n, v[j]);  // all loads before any store: out may be in
+    for (int j = 0; j < kVJ; ++j) load_chunk<T, SH>(in, c0 + 64 * j, n_in, v[j]);  // all loads before any store: out may be in
     T run = 0;  // the wave's running total over its stripes j
 #pragma unroll
     for (int j = 0; j < kVJ; ++j) {
@@ -175,29 +181,13 @@ __global__ __launch_bounds__(kThreads) void k_scanv_down(const T *in, T *out, ui
     }
 }
 
+template <class T, int SH = 0>
+int scanv_impl(oge_ctx *ctx, const T *in, T *out, uint64_t n, uint64_t n_in, int level);
+
 template <class T>
 int scan_impl(oge_ctx *ctx, const T *in, T *out, uint64_t n, int level) {
     if (n == 0) return OGE_OK;
-    if (!(((uintptr_t)in | (uintptr_t)out) & 15)) {
-        constexpr uint64_t per = (uint64_t)kVTile * (16 / sizeof(T));
-        const uint32_t nb = oge_ceil_div(n, per);
-        if (nb == 1) {
-            hipLaunchKernelGGL(k_scanv_down<T>, dim3(1), dim3(kThreads), 0, ctx->stream, in, out, n, (const T *)nullptr);
-            OGE_LAUNCH_CHECK(ctx);
-            return OGE_OK;
-        }
-        char name[32];
-        snprintf(name, sizeof(name), "scan_sums_%d_%zu", level, sizeof(T));
-        T *sums = (T *)ctx->ws(name, (size_t)nb * sizeof(T));
-        if (!sums) return OGE_ERR_HIP;
-        hipLaunchKernelGGL(k_scanv_reduce<T>, dim3(nb), dim3(kThreads), 0, ctx->stream, in, n, sums);
-        OGE_LAUNCH_CHECK(ctx);
-        int rc = scan_impl<T>(ctx, sums, sums, nb, level + 1);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_scanv_down<T>, dim3(nb), dim3(kThreads), 0, ctx->stream, in, out, n, (const T *)sums);
-        OGE_LAUNCH_CHECK(ctx);
-        return OGE_OK;
-    }
+    if (!(((uintptr_t)in | (uintptr_t)out) & 15)) return scanv_impl<T>(ctx, in, out, n, n, level);
     uint32_t nb = oge_ceil_div(n, kScanTile);
     if (nb == 1) {
         hipLaunchKernelGGL(k_scan_tiles<T>, dim3(1), dim3(kThreads), 0, ctx->stream, in, out, n, (T *)nullptr);
@@ -213,6 +203,28 @@ int scan_impl(oge_ctx *ctx, const T *in, T *out, uint64_t n, int level) {
     int rc = scan_impl<T>(ctx, sums, sums, nb, level + 1);
     if (rc) return rc;
     hipLaunchKernelGGL(k_scan_add<T>, dim3(nb), dim3(kThreads), 0, ctx->stream, out, n, (const T *)sums);
+    OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}
+
+template <class T, int SH>
+int scanv_impl(oge_ctx *ctx, const T *in, T *out, uint64_t n, uint64_t n_in, int level) {
+    constexpr uint64_t per = (uint64_t)kVTile * (16 / sizeof(T));
+    const uint32_t nb = oge_ceil_div(n, per);
+    if (nb == 1) {
+        hipLaunchKernelGGL((k_scanv_down<T, SH>), dim3(1), dim3(kThreads), 0, ctx->stream, in, out, n, n_in, (const T *)nullptr);
+        OGE_LAUNCH_CHECK(ctx);
+        return OGE_OK;
+    }
+    char name[32];
+    snprintf(name, sizeof(name), "scan_sums_%d_%zu", level, sizeof(T));
+    T *sums = (T *)ctx->ws(name, (size_t)nb * sizeof(T));
+    if (!sums) return OGE_ERR_HIP;
+    hipLaunchKernelGGL((k_scanv_reduce<T, SH>), dim3(nb), dim3(kThreads), 0, ctx->stream, in, n_in, sums);
+    OGE_LAUNCH_CHECK(ctx);
+    int rc = scan_impl<T>(ctx, sums, sums, nb, level + 1);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_scanv_down<T, SH>), dim3(nb), dim3(kThreads), 0, ctx->stream, in, out, n, n_in, (const T *)sums);
     OGE_LAUNCH_CHECK(ctx);
     return OGE_OK;
 }
@@ -429,6 +441,10 @@ int oge_exclusive_scan_u32(oge_ctx *ctx, const uint32_t *in, uint32_t *out, uint
 }
 int oge_exclusive_scan_u64(oge_ctx *ctx, const uint64_t *in, uint64_t *out, uint64_t n) {
     return scan_impl<uint64_t>(ctx, in, out, n, 0);
+}
+int oge_offsets_from_keys(oge_ctx *ctx, const uint64_t *keys, uint64_t n, uint64_t *out) {
+    if (((uintptr_t)keys | (uintptr_t)out) & 15) return 1;  // the caller takes the two-kernel path
+    return scanv_impl<uint64_t, 50>(ctx, keys, out, n + 1, n, 0);
 }
 
 int oge_reduce_or_and_u64(oge_ctx *ctx, const uint64_t *in, uint64_t n, uint64_t mask, uint64_t *or_out, uint64_t *and_out) {

@@ -371,15 +371,20 @@ int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d
                           const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
                           const RecMeta *smeta, const uint8_t *d_dup, const uint64_t *desc) {
     OgeStageTimer *t = ctx->begin_stage("gather_offsets");
-    if (sorted_keys)
-        hipLaunchKernelGGL(k_sizes_from_keys, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, sorted_keys, n,
-                           d_out_off);
-    else
-        hipLaunchKernelGGL(k_sizes_from_perm, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off,
-                           d_perm, n, d_out_off);
-    OGE_LAUNCH_CHECK(ctx);
-    int rc = oge_exclusive_scan_u64(ctx, d_out_off, d_out_off, n + 1);
-    if (rc) return rc;
+    // the sizes straight from the sorted keys' payload inside the scan (r05: a sizes kernel first, 0.8 ms)
+    int rc = sorted_keys ? oge_offsets_from_keys(ctx, sorted_keys, n, d_out_off) : 1;
+    if (rc < 0) return rc;
+    if (rc) {
+        if (sorted_keys)
+            hipLaunchKernelGGL(k_sizes_from_keys, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, sorted_keys, n,
+                               d_out_off);
+        else
+            hipLaunchKernelGGL(k_sizes_from_perm, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off,
+                               d_perm, n, d_out_off);
+        OGE_LAUNCH_CHECK(ctx);
+        rc = oge_exclusive_scan_u64(ctx, d_out_off, d_out_off, n + 1);
+        if (rc) return rc;
+    }
     ctx->end_stage(t);
     if (!n) return OGE_OK;
     t = ctx->begin_stage("gather_records");

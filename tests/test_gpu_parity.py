@@ -253,3 +253,29 @@ def test_markdup_read_group_widths(ctx, width):
     dup, nd = ctx.markdup(srecs, soffs, n, opts)
     odup, ond = oracle.markdup(srecs, soffs, n, hdr2)
     assert nd == ond and np.array_equal(dup, odup)
+
+
+def test_sort_markdup_output_offsets_alignment(ctx):
+    """The output offsets come from one fused scan over the sorted keys when d_out_off is 16-byte aligned and
+    from the sizes kernel + scan otherwise: the same offsets and records either way."""
+    import torch
+    p = L.synth_params(3000, preset="mix", seed=29)
+    recs, offs, hdr = L.synth_host(p)
+    n = 6000
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    d_recs = torch.from_numpy(recs).cuda()
+    d_offs = torch.from_numpy(offs.view(np.int64)).cuda()
+    outs = []
+    for shift in (0, 1):
+        d_perm = torch.empty(n, dtype=torch.int32, device="cuda")
+        d_out = torch.zeros(recs.size, dtype=torch.uint8, device="cuda")
+        buf = torch.full((n + 2 + shift,), -1, dtype=torch.int64, device="cuda")
+        d_oo = buf[shift:shift + n + 1]
+        assert (d_oo.data_ptr() % 16 == 0) == (shift == 0)
+        nd = ctx.sort_markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_perm.data_ptr(), d_out.data_ptr(),
+                                  d_oo.data_ptr())
+        ctx.sync()
+        outs.append((nd, d_oo.cpu().numpy().copy(), d_out.cpu().numpy()))
+    assert outs[0][0] == outs[1][0]
+    assert np.array_equal(outs[0][1], outs[1][1]) and outs[0][1][0] == 0 and outs[0][1][-1] == int(offs[-1])
+    assert np.array_equal(outs[0][2], outs[1][2])
