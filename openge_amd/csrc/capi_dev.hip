@@ -426,7 +426,7 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
     if (oge_sort_buffers(ctx, n, &keys, &vals)) return OGE_ERR_HIP;
     unsigned int *counts = oge_sort_counts(ctx);
     if (!counts) return OGE_ERR_HIP;
-    OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 16, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 32, ctx->stream));
     OgeStageTimer *t = ctx->begin_stage("input_pass");
     OgePassArgs a = {};
     a.recs = d_recs;
@@ -438,6 +438,7 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
     a.vals = vals;
     a.n_ref = opts->n_ref;
     a.bad = counts + 2;
+    a.keyred = (unsigned long long *)(counts + 4);
     rc = oge_input_pass(ctx, a);
     if (rc) return rc;
     ctx->end_stage(t);

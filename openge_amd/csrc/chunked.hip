@@ -274,7 +274,7 @@ extern "C" int oge_sort_markdup_chunked(oge_ctx *ctx, uint8_t *h_recs, const uin
             uint32_t *svals;
             unsigned int *counts = oge_sort_counts(ctx);
             if (oge_sort_buffers(ctx, R.n, &skeys, &svals) || !counts) return OGE_ERR_HIP;
-            OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 16, ctx->stream));
+            OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 32, ctx->stream));
             OgePassArgs a = {};
             a.recs = A;
             a.off = d_off;
@@ -285,6 +285,7 @@ extern "C" int oge_sort_markdup_chunked(oge_ctx *ctx, uint8_t *h_recs, const uin
             a.vals = svals;
             a.n_ref = n_ref;
             a.bad = counts + 2;
+            a.keyred = (unsigned long long *)(counts + 4);
             if ((rc = oge_input_pass(ctx, a))) return rc;
             uint64_t *k;
             uint32_t *v;

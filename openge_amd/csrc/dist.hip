@@ -681,7 +681,7 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
     if (!rc && (oge_sort_buffers(ctx, R, &skeys, &svals) || !counts)) rc = OGE_ERR_HIP;
     meta = (RecMeta *)ctx->ws("md_meta", (R + 1) * sizeof(RecMeta));
     if (!rc && !meta) rc = OGE_ERR_HIP;
-    if (!rc) rc = hipMemsetAsync(counts, 0, 16, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
+    if (!rc) rc = hipMemsetAsync(counts, 0, 32, ctx->stream) == hipSuccess ? 0 : dist_hip_fail(ctx, __LINE__);
     // the ReadEnds / key pass over records [r0, r1) of rbuf
     auto pass = [&](uint64_t r0, uint64_t r1) {
         if (rc || r1 <= r0) return;
@@ -696,6 +696,7 @@ static int dist_dedup(Dist &D, uint8_t *rbuf, const uint64_t *roff, uint64_t R, 
         a.vals = sorted ? svals + r0 : nullptr;
         a.n_ref = n_ref;
         a.bad = counts + 2;
+        a.keyred = (unsigned long long *)(counts + 4);
         rc = oge_input_pass(ctx, a);
     };
     if (xr) {

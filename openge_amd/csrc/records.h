@@ -58,6 +58,9 @@ struct OgePassArgs {
     uint64_t ibase;          // index of the pass's first record in a larger array (a pass over a sub-range)
     int32_t n_ref;
     unsigned int *bad;       // bit 0: refID/pos out of range, bit 1: block_size out of [32, 10000]
+    // KEYS: when set, keyred[0] |= every key's sort bits, keyred[1] |= their complement (the sort's varying
+    // bits without a reduction pass of its own) and bad[1] = 1 says they were written
+    unsigned long long *keyred;
     // gather pass: output record k = input record perm[k] (or meta[k].src when smeta is given)
     const uint32_t *perm;
     const RecMeta *smeta;    // summaries in OUTPUT order (bin, flags, src offset), optional

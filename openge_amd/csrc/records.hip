@@ -85,7 +85,8 @@ __device__ __forceinline__ uint64_t h_bytes(const Rd &rd, uint64_t h, uint64_t p
 
 // Record at absolute index r of reader `rd`; i = record index, src = its offset in the arena.
 template <bool META, bool KEYS, class Rd>
-__device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i, uint64_t src, const OgePassArgs &a) {
+__device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i, uint64_t src, const OgePassArgs &a, uint64_t &kor,
+                                            uint64_t &knot) {
     const uint32_t bs = rd.u32(r);
     const int32_t ref = (int32_t)rd.u32(r + OGE_OFF_REFID);
     const int32_t pos = (int32_t)rd.u32(r + OGE_OFF_POS);
@@ -103,6 +104,8 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
         }
         if (bs < 32 || bs > 10000) atomicOr(a.bad, 2u);
         a.keys[i] = k | ((uint64_t)(bs + 4) << 50);
+        kor |= k;
+        knot |= ~k & OGE_SORT_KEY_MASK;
         a.vals[i] = (uint32_t)(a.ibase + i);
     }
     if (!META) return;
@@ -306,6 +309,7 @@ __global__ __launch_bounds__(NT) void k_input_pass(OgePassArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * kTileRecs;
     uint64_t r0 = (uint64_t)blockIdx.x * kTileRecs;
     uint64_t wb0 = 0, wb1 = 0, my_off = 0;
+    uint64_t kor = 0, knot = 0;  // this thread's keys' OR and OR of complements (a.keyred)
     if (r0 < a.n) {
         if (threadIdx.x == 0) window(r0, wb0, wb1);
         if (r0 + threadIdx.x < a.n) my_off = a.off[r0 + threadIdx.x];
@@ -337,10 +341,19 @@ __global__ __launch_bounds__(NT) void k_input_pass(OgePassArgs a) {
         const uint64_t i = r0 + threadIdx.x;
         if (i < r1) {
             const uint32_t bs = (o >= b0 && o + 4 <= b1) ? LdsRd{lds}.u32(o - b0) : 0u;
-            if (bs && o + 4 + bs <= b1) parse_input<META, KEYS>(LdsRd{lds}, o - b0, i, o, a);
-            else parse_input<META, KEYS>(GlbRd{a.recs}, o, i, o, a);
+            if (bs && o + 4 + bs <= b1) parse_input<META, KEYS>(LdsRd{lds}, o - b0, i, o, a, kor, knot);
+            else parse_input<META, KEYS>(GlbRd{a.recs}, o, i, o, a, kor, knot);
         }
         __syncthreads();
+    }
+    if (KEYS && a.keyred) {  // a wave's OR, then one atomic per wave and word
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) kor |= __shfl_xor(kor, d, 64), knot |= __shfl_xor(knot, d, 64);
+        if ((threadIdx.x & 63) == 0) {
+            if (kor) atomicOr(&a.keyred[0], (unsigned long long)kor);
+            if (knot) atomicOr(&a.keyred[1], (unsigned long long)knot);
+            if (blockIdx.x == 0 && threadIdx.x == 0) a.bad[1] = 1u;
+        }
     }
 }
 

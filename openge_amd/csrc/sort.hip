@@ -286,7 +286,7 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     if (!ktmp || !vtmp || !counts) return OGE_ERR_HIP;
     if (!keys_ready) {
         OgeStageTimer *t = ctx->begin_stage("sort_keypack");
-        OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 16, ctx->stream));
+        OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 32, ctx->stream));
         if (n) {
             hipLaunchKernelGGL(k_keypack, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off, n, n_ref, keys,
                                vals, counts + 2);
@@ -294,12 +294,21 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
         }
         ctx->end_stage(t);
     }
-    uint64_t o = 0, a = 0;
-    int rc = oge_reduce_or_and_u64(ctx, keys, n, kSortKeyMask, &o, &a);
-    if (rc) return rc;
-    unsigned int bad = 0;
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&bad, counts + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
+    // the varying key bits: from the input pass when it reduced them (keys_ready, counts[3] set), else a
+    // reduction pass over the keys
+    unsigned int c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(c, counts, 32, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const unsigned int bad = c[2];
+    uint64_t o = 0, a = 0;
+    int rc = 0;
+    if (keys_ready && c[3] == 1) {
+        o = (uint64_t)c[4] | ((uint64_t)c[5] << 32);
+        a = ~((uint64_t)c[6] | ((uint64_t)c[7] << 32));  // AND = complement of the complements' OR
+    } else {
+        rc = oge_reduce_or_and_u64(ctx, keys, n, kSortKeyMask, &o, &a);
+        if (rc) return rc;
+    }
     if (bad & 1) return oge_fail(ctx, OGE_ERR_ARG, "sort: record with refID outside [-1, n_ref) or pos < -1");
     if (bad & 2) return oge_fail(ctx, OGE_ERR_ARG, "sort: record block_size outside [32, 10000] (util/bam_deserializer.h:160)");
     OgeStageTimer *t = ctx->begin_stage("sort_radix");
@@ -363,7 +372,8 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     return OGE_OK;
 }
 
-unsigned int *oge_sort_counts(oge_ctx *ctx) { return (unsigned int *)ctx->ws("sort_counts", 16); }
+// [1] long tie runs, [2] bad-record bits, [3] keyred written, [4..8) the input pass's key OR / complement OR
+unsigned int *oge_sort_counts(oge_ctx *ctx) { return (unsigned int *)ctx->ws("sort_counts", 32); }
 
 // Output offsets (from the size payload of the sorted keys, or from the records) and the gather.
 // smeta (output-order summaries) and dup are optional (see OgePassArgs).
