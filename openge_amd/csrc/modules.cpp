@@ -27,6 +27,12 @@ int ChainContext::fail(const std::string &where) {
     return -1;
 }
 
+// OGE_WRITE_DEVICE=1: host batches are deflated on the GPU (FileWriter, LocalRealignment's result)
+static bool write_device_forced() {
+    const char *e = getenv("OGE_WRITE_DEVICE");
+    return e && !strcmp(e, "1");
+}
+
 int ChainContext::to_device(ReadBatch &b) {
     if (b.dev_valid) return 0;
     const uint64_t bytes = b.offs[b.n];
@@ -1027,13 +1033,14 @@ int LocalRealignment::runInternal(ChainContext &cc, ReadBatch &b) {
     const uint8_t *rp = oge_realign_result_records(r, &bytes);
     const uint64_t *op = oge_realign_result_offsets(r);
     const uint64_t n = oge_realign_result_count(r);
-    // The result goes straight up to the device when it fits (the writer deflates it there; a host module
-    // downloads it again): a host copy of the 1.1 GB C5 result cost 0.52 s of fresh-page faults, the upload
-    // ~0.06 s.  The offsets are rebased to the uploaded range.
+    // OGE_WRITE_DEVICE=1: the result goes straight up to the device when it fits and the writer deflates it
+    // there (a host module downloads it again).  Otherwise (default) the host batch takes it in a threaded
+    // copy into huge pages -- one thread copying into fresh 4 KiB pages took 0.52 s for the 1.1 GB C5 result
+    // -- and the writer compresses it with the host codec (zlib-class level 6, as the reference writes).
     uint64_t fr = 0, tot = 0;
     const uint64_t base = n ? op[0] : 0, len = n ? op[n] - base : 0;
     void *dr = nullptr, *dof = nullptr;
-    bool up = n && !bgzf_host_codec_forced() && !oge_mem_info(cc.ctx, &fr, &tot) &&
+    bool up = n && write_device_forced() && !bgzf_host_codec_forced() && !oge_mem_info(cc.ctx, &fr, &tot) &&
               2 * len + (n + 1) * 16 + (256ull << 20) < fr;
     if (up) {
         std::vector<uint64_t> ro(op, op + n + 1);
@@ -1056,8 +1063,21 @@ int LocalRealignment::runInternal(ChainContext &cc, ReadBatch &b) {
         }
     }
     if (!up) {
-        b.recs.assign(rp, rp + bytes);
-        b.recs.resize(bytes + 16, 0);
+        bytevec fresh;
+        fresh.reserve(bytes + 16);
+        want_huge_pages(fresh.data(), bytes + 16);
+        fresh.resize(bytes + 16);  // uninitialised: the copy below writes every byte but the slack
+        memset(fresh.data() + bytes, 0, 16);
+        const int T = std::max(1, std::min(16, cc.threads));
+        const uint64_t per = (bytes + T - 1) / T;
+        std::vector<std::thread> ts;
+        for (int k = 0; k < T; ++k)
+            ts.emplace_back([&, k]() {
+                const uint64_t a = std::min(bytes, (uint64_t)k * per), z = std::min(bytes, a + per);
+                if (z > a) memcpy(fresh.data() + a, rp + a, z - a);
+            });
+        for (auto &th : ts) th.join();
+        b.recs = std::move(fresh);
         b.offs.assign(op, op + n + 1);
     }
     b.n = n;
@@ -1324,11 +1344,12 @@ int FileWriter::runInternal(ChainContext &cc, ReadBatch &b) {
     const bool sliced = !b.slices.empty(), produced = (bool)b.produce;
     bool on_device = sliced || produced || (b.dev_valid && !b.host_valid && !bgzf_host_codec_forced());
     double t_dev = 0, t_d2h = 0, t_wait = 0;
-    // Host records (the realigner's output) whose bytes sit back to back: up to the device and out through
-    // the GPU deflate -- on the C5 set 1.1 GB of records take 0.78 s with 16 libdeflate threads
-    // (profiles/r05ap_realign_cli.txt), the upload and the device path a fraction of that.  A device that
-    // cannot hold them leaves the host writer in charge.
-    if (!on_device && b.host_valid && !b.dev_valid && b.n && !bgzf_host_codec_forced()) {
+    // OGE_WRITE_DEVICE=1: host records (the realigner's output) whose bytes sit back to back go up to the
+    // device and out through the GPU deflate -- on the C5 set 1.1 GB of records take 0.78 s with 16
+    // libdeflate threads (profiles/r05ap_realign_cli.txt), the upload and the device path a fraction of that,
+    // for an 11 % larger file (the GPU deflate's greedy search).  Off by default: the host codec writes
+    // zlib-class level 6 like the reference.  A device that cannot hold them leaves the host writer in charge.
+    if (!on_device && b.host_valid && !b.dev_valid && b.n && write_device_forced() && !bgzf_host_codec_forced()) {
         bool contiguous = b.offs.size() == b.n + 1 && b.offs[b.n] + 16 <= b.recs.size();
         for (uint64_t k = 0; contiguous && k < b.n; ++k)
             contiguous = b.offs[k + 1] == b.offs[k] + 4 + oge_rd_u32(b.recs.data() + b.offs[k]);

@@ -3,6 +3,7 @@ the REFERENCE's own outputs (tests/golden; made by oracle/_ref from the referenc
 read like the reference's CTest smoke tests (openge/test/CMakeLists.txt:32,44-45) with the outputs
 pinned byte for byte (decompressed records + header text; compressed bytes are not part of parity)."""
 import hashlib
+import os
 import subprocess
 
 import numpy as np
@@ -19,7 +20,7 @@ OPENGE = str(L.PKG / "openge")
 
 
 def run(*args):
-    r = subprocess.run([OPENGE, *map(str, args)], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([OPENGE, *map(str, args)], capture_output=True, text=True, timeout=300, env=dict(os.environ))
     assert r.returncode == 0, r.stderr
     return r
 
@@ -115,10 +116,15 @@ def test_cli_program_record(tmp_path):
     assert ids == ["ID:openge", "ID:openge-2"]
 
 
+@pytest.mark.parametrize("device_write", ["0", "1"])
 @pytest.mark.parametrize("name", ["rl_small", "rl_edge"])
-def test_cli_localrealign_matches_reference(name, tmp_path):
+def test_cli_localrealign_matches_reference(name, device_write, tmp_path, monkeypatch):
+    """Default: the realigned records are written by the host codec; OGE_WRITE_DEVICE=1: they go up to the
+    device and out through the GPU deflate.  The same records either way."""
     meta, arrays, h, recs, offs, fa, iv = load_rl_case(name, tmp_path)
-    run("localrealign", "--nopg", "-R", fa, "-L", iv, tmp_path / "reads.bam", "-o", tmp_path / "rl.bam")
+    monkeypatch.setenv("OGE_WRITE_DEVICE", device_write)
+    r = run("localrealign", "-v", "--nopg", "-R", fa, "-L", iv, tmp_path / "reads.bam", "-o", tmp_path / "rl.bam")
+    assert ("(gpu, segmented)" in r.stderr) == (device_write == "1"), r.stderr
     oh, _, orecs, ooffs = bamutil.read_bam(tmp_path / "rl.bam")
     assert oh == meta["output_header"]
     check_output(meta, arrays, orecs, np.append(ooffs, np.uint64(len(orecs))))
