@@ -128,6 +128,23 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
     M.hash = 0;
     uint64_t m = ((uint64_t)oge_reg2bin(pos, pos + rl) << 48) | ((uint64_t)(flag >> 8) << 40);
     if (!(flag & OGE_F_SECONDARY)) m |= OGE_M_PRIMARY;
+    // name slot, every record: l_read_name bytes (with the NUL) when they fit, zero-padded -- the sort's
+    // tie order compares these instead of the records' bytes (r05: only mate-join candidates had it, and
+    // ties between any other records read their names byte by byte from global memory)
+    if (lname <= OGE_NAME_SLOT) {
+        m |= OGE_M_NAMEFIT;
+        uint32_t *ns = (uint32_t *)M.name;
+#pragma unroll
+        for (uint32_t q = 0; q < OGE_NAME_SLOT / 4; ++q) {
+            uint32_t v = 0;
+            if (4 * q < lname) {
+                v = rd.u32(r + OGE_OFF_NAME + 4 * q);
+                const uint32_t rem = lname - 4 * q;
+                if (rem < 4) v &= (1u << (8 * rem)) - 1u;
+            }
+            ns[q] = v;
+        }
+    }
     if (!((flag & OGE_F_UNMAP) || ref == -1 || (flag & OGE_F_SECONDARY))) {
         m |= OGE_M_FRAG;
         const bool rev = (flag & OGE_F_REVERSE) != 0;
@@ -249,22 +266,11 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
             } else {
                 h = h_bytes(rd, h, rgv, rgl);
             }
-            // name slot: l_read_name bytes (with the NUL) when they fit, zero-padded; its words also feed the
-            // hash (equal keys have equal lengths, so both take the same branch)
+            // the name slot's words (filled above when the name fits) also feed the hash (equal keys have
+            // equal lengths, so both take the same branch)
             if (lname <= OGE_NAME_SLOT) {
-                m |= OGE_M_NAMEFIT;
-                uint32_t *ns = (uint32_t *)M.name;
+                const uint32_t *ns = (const uint32_t *)M.name;
                 h = h_word(h, lname);
-#pragma unroll
-                for (uint32_t q = 0; q < OGE_NAME_SLOT / 4; ++q) {
-                    uint32_t v = 0;
-                    if (4 * q < lname) {
-                        v = rd.u32(r + OGE_OFF_NAME + 4 * q);
-                        const uint32_t rem = lname - 4 * q;
-                        if (rem < 4) v &= (1u << (8 * rem)) - 1u;
-                    }
-                    ns[q] = v;
-                }
 #pragma unroll
                 for (uint32_t q = 0; q < OGE_NAME_SLOT / 4; ++q)
                     if (4 * q < lname) h = h_word(h, ns[q]);

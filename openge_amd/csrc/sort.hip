@@ -139,6 +139,20 @@ __global__ __launch_bounds__(kT) void k_ties_meta(const uint8_t *__restrict__ re
         uint64_t *k = keys + p;
         uint32_t *v = vals + p;
         RecMeta *M = smeta + p;
+        if (len == 2) {
+            // pairs (92 % of the runs on C2): both rows loaded together, one compare, written back only when
+            // they swap.  r05: the insertion sort's row moves were chains of dependent global round trips
+            // (the small-run sort was 4.9 of the stage's 7.8 ms at 300M reads).
+            const RecMeta A = M[0], B = M[1];
+            const uint32_t va = v[0], vb = v[1];
+            if (tie_less_meta(recs, B, A, vb, va)) {
+                const uint64_t ka = k[0], kb = k[1];
+                M[0] = B, M[1] = A;
+                v[0] = vb, v[1] = va;
+                k[0] = kb, k[1] = ka;
+            }
+            continue;
+        }
         for (uint32_t i = 1; i < len; ++i) {
             const RecMeta mi = M[i];
             const uint32_t vi = v[i];
