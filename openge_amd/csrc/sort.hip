@@ -100,27 +100,38 @@ __device__ __forceinline__ bool tie_less_meta(const uint8_t *__restrict__ recs, 
 // in LDS and then sorts them with every lane busy -- one run per lane, rows of a run contiguous.
 // Runs longer than 32 are appended to `large` (rare) for k_tie_large.  Keys, input indices and
 // rows move together.
-constexpr uint32_t kTieTile = 4096;
+constexpr uint32_t kTieTile = 2048;
+constexpr uint32_t kTieHalo = 34;  // keys staged past the tile: a run starting in it is seen up to 33 long
 __global__ __launch_bounds__(kT) void k_ties_meta(const uint8_t *__restrict__ recs, uint64_t *__restrict__ keys,
                                                    uint32_t *__restrict__ vals, RecMeta *__restrict__ smeta, uint64_t n,
                                                    int32_t n_ref, uint2 *__restrict__ large, unsigned int *__restrict__ nlarge) {
+    // the tile's masked keys with one before and kTieHalo after, staged by coalesced loads (r05: every
+    // position read its neighbours and the run's tail from global memory, ~2 ms of the stage at 300M);
+    // ~0 marks positions outside [0, n) (a masked key is below 2^50)
+    __shared__ uint64_t sk[kTieTile + 1 + kTieHalo];
     __shared__ uint32_t hp[kTieTile / 2];
     __shared__ uint8_t hl[kTieTile / 2];
     __shared__ unsigned int nh;
     if (threadIdx.x == 0) nh = 0;
-    __syncthreads();
     const uint64_t tile0 = (uint64_t)blockIdx.x * kTieTile;
+    for (uint32_t i = threadIdx.x; i < kTieTile + 1 + kTieHalo; i += kT) {
+        const uint64_t q = tile0 + i;  // position q - 1
+        sk[i] = (q >= 1 && q - 1 < n) ? (keys[q - 1] & kSortKeyMask) : ~0ull;
+    }
+    __syncthreads();
+    const uint64_t unm = (uint64_t)(uint32_t)n_ref << 33;  // the unmapped run keeps input order
     for (uint32_t j = 0; j < kTieTile / kT; ++j) {
-        const uint64_t p = tile0 + j * kT + threadIdx.x;
+        const uint32_t li = j * kT + threadIdx.x;  // position tile0 + li at sk[li + 1]
+        const uint64_t p = tile0 + li;
         uint32_t len = 0;
         if (p + 1 < n) {
-            const uint64_t k0 = keys[p] & kSortKeyMask;
-            if ((p == 0 || (keys[p - 1] & kSortKeyMask) != k0) && (keys[p + 1] & kSortKeyMask) == k0 &&
-                (k0 >> 33) != (uint64_t)(uint32_t)n_ref) {
-                uint64_t e = p + 2;
-                while (e < n && e - p <= 32 && (keys[e] & kSortKeyMask) == k0) ++e;
-                if (e - p > 32) { while (e < n && (keys[e] & kSortKeyMask) == k0) ++e; }
-                len = (uint32_t)(e - p);
+            const uint64_t k0 = sk[li + 1];
+            if (sk[li] != k0 && sk[li + 2] == k0 && (k0 >> 33) != (unm >> 33)) {
+                uint32_t e = li + 3;  // sk index of position p + 2
+                while (e < kTieTile + 1 + kTieHalo && e - (li + 1) <= 32 && sk[e] == k0) ++e;
+                uint64_t ee = tile0 + e - 1;  // the first position past the run seen so far
+                if (ee - p > 32) { while (ee < n && (keys[ee] & kSortKeyMask) == k0) ++ee; }
+                len = (uint32_t)(ee - p);
             }
         }
         const bool is_large = len > 32;
