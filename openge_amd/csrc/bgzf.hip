@@ -127,9 +127,15 @@ __device__ __forceinline__ uint64_t bits_below(uint32_t q) { return q >= 64 ? ~0
 // staging from HBM with the CU otherwise idle).
 constexpr uint32_t kPre = kPay / 4 / kTP + 1;  // prefetched words per thread (16 for a full payload)
 
+// depth > 1 (levels 8-9): at a candidate the parse also walks the chain of earlier positions with the same
+// 4-byte prefix that the candidate array holds implicitly (cand[c] of a candidate c is c's own verified
+// predecessor, so the chain never leaves the prefix; it ends at the sub-block's start) and takes the longest
+// match of up to `depth` of them; with lazy, a match shorter than 32 bytes gives way to a literal when the
+// next position's best match is longer (zlib's lazy evaluation).  depth 1 without lazy: the greedy parse.
 __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0, uint64_t nb,
                                                    uint64_t *__restrict__ lmask, uint8_t *__restrict__ nmatch,
-                                                   uint32_t *__restrict__ mlist, uint32_t *__restrict__ freq_out) {
+                                                   uint32_t *__restrict__ mlist, uint32_t *__restrict__ freq_out, int depth,
+                                                   int lazy) {
     // 163,600 B of LDS: the payload, two hash tables, the sub-block's candidates (the symbol counts live
     // in the table not in use while a sub-block is parsed; the candidate masks are read back from cand)
     __shared__ __align__(16) uint32_t in[kPay / 4 + 4];
@@ -280,13 +286,8 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
                 cm &= bits_below(sl);
             }
             uint32_t *mp = mlist + (pi * kMaxM) * kNSeg + (uint64_t)sub * kT + t;
-            for (uint32_t p = 0; p < sl;) {
-                const uint64_t m = cm & ~bits_below(p);
-                const uint32_t q = m ? (uint32_t)__builtin_ctzll(m) : sl;
-                lit |= bits_below(q) & ~bits_below(p);  // literals [p, q)
-                if (q >= sl) break;
-                const uint32_t j = cand[s0 + q - base] - 1, pq = s0 + q;
-                const uint32_t maxL = min(258u, sl - q);
+            // match length of candidate j at payload position pq (their first 4 bytes are equal), <= maxL
+            auto ext = [&](uint32_t pq, uint32_t j, uint32_t maxL) {
                 uint32_t L = min(4u, maxL);
                 while (L < maxL) {  // 8 bytes per step
                     const uint32_t x0 = ld32(in, pq + L) ^ ld32(in, j + L);
@@ -301,7 +302,41 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
                     }
                     L += 8;
                 }
-                L = min(L, maxL);
+                return min(L, maxL);
+            };
+            // the best match at segment offset q (a candidate position): its candidate, then (depth > 1) the
+            // chain of earlier same-prefix positions through cand; *jo = the source of the longest (the
+            // nearest of equal lengths)
+            auto best = [&](uint32_t q, uint32_t *jo) {
+                const uint32_t pq = s0 + q, maxL = min(258u, sl - q);
+                uint32_t j = cand[pq - base] - 1, L = ext(pq, j, maxL), bj = j;
+                for (int d = 1; d < depth && L < maxL; ++d) {
+                    if (j < base) break;
+                    const uint32_t nx = cand[j - base];
+                    if (!nx || pq - (nx - 1) > 32768) break;
+                    j = nx - 1;
+                    const uint32_t Lj = ext(pq, j, maxL);
+                    if (Lj > L) L = Lj, bj = j;
+                }
+                *jo = bj;
+                return L;
+            };
+            for (uint32_t p = 0; p < sl;) {
+                const uint64_t m = cm & ~bits_below(p);
+                const uint32_t q = m ? (uint32_t)__builtin_ctzll(m) : sl;
+                lit |= bits_below(q) & ~bits_below(p);  // literals [p, q)
+                if (q >= sl) break;
+                const uint32_t pq = s0 + q;
+                uint32_t j;
+                const uint32_t L = best(q, &j);
+                if (lazy && L >= 3 && L < 32 && q + 1 < sl && ((cm >> (q + 1)) & 1)) {
+                    uint32_t j1;
+                    if (best(q + 1, &j1) > L) {  // a literal here, the longer match from the next position
+                        lit |= 1ull << q;
+                        p = q + 1;
+                        continue;
+                    }
+                }
                 if (L >= 3) {
                     const uint32_t d = pq - j;
                     uint32_t sym, nb, ev, dsym, dnb, dev;
@@ -1150,6 +1185,8 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
     if (!out_bytes || (n && (!d_src || !d_dst))) return oge_fail(ctx, OGE_ERR_ARG, "null buffer");
     if (level < 0 || level > 9) return oge_fail(ctx, OGE_ERR_ARG, "level must be 0..9");
+    // levels 1-7: the greedy one-candidate parse; 8 / 9: same-prefix chains 8 / 32 deep and lazy matching
+    const int depth = level >= 9 ? 32 : level == 8 ? 8 : 1, lazy = level >= 8 ? 1 : 0;
     if (dst_cap < oge_bgzf_bound(n)) return oge_fail(ctx, OGE_ERR_ARG, "dst_cap < oge_bgzf_bound(n)");
     hipSetDevice(ctx->device);
     ctx->reset_timing();
@@ -1222,7 +1259,7 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
         Bufs &u = B[k % S];
         k_defl_parse<<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)ncu), kTP, 0, u.st>>>(d_src, n, b0, nb, u.lmask, u.nmatch,
-                                                                                      u.mlist, u.freq);
+                                                                                      u.mlist, u.freq, depth, lazy);
         OGE_LAUNCH_CHECK(ctx);
         k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs, n, b0, level, u.sizes);
         OGE_LAUNCH_CHECK(ctx);

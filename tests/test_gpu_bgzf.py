@@ -64,11 +64,27 @@ CASES = {
 }
 
 
+@pytest.mark.parametrize("level", [6, 8, 9])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_deflate_roundtrip(ctx, name):
+def test_deflate_roundtrip(ctx, name, level):
     data = CASES[name]
-    z = ctx.bgzf_deflate(data, 6)
+    z = ctx.bgzf_deflate(data, level)
     check_roundtrip(data, z)
+
+
+def test_deflate_chain_levels(ctx):
+    """Levels 8 / 9 walk same-prefix chains with lazy matching: valid BGZF, deterministic, and no larger
+    than level 6 on BAM records (zlib-6 printed beside them)."""
+    data = _bam_bytes(40_000, seed=9)
+    sizes = {}
+    for level in (6, 8, 9):
+        z = ctx.bgzf_deflate(data, level)
+        assert z == ctx.bgzf_deflate(data, level)
+        check_roundtrip(data, z)
+        sizes[level] = len(z)
+    ref = sum(len(zlib.compress(data[i:i + PAY], 6)) for i in range(0, len(data), PAY))
+    print(f"\nBAM payload {len(data)} B: level 6 {sizes[6]}, 8 {sizes[8]}, 9 {sizes[9]}; zlib-6 {ref}")
+    assert sizes[8] <= sizes[6] and sizes[9] <= sizes[6]
 
 
 def test_deflate_empty(ctx):

@@ -9,7 +9,9 @@ import torch
 from openge_amd import lib as L
 if len(sys.argv) > 1:
     L.LIB_PATH = Path(sys.argv[1])
+import os
 reads = 20_000_000
+level = int(os.environ.get("DIAG_LEVEL", 6))
 dev = torch.device("cuda", 0)
 ctx = L.Context(0)
 p = L.synth_params(reads // 2, preset="c2", seed=1234)
@@ -23,7 +25,13 @@ cap = int(L.lib().oge_bgzf_bound(B))
 d_z = torch.empty(cap, dtype=torch.uint8, device=dev)
 ms = []
 for _ in range(4):
-    zb = ctx.bgzf_deflate_dev(d_recs.data_ptr(), B, 6, d_z.data_ptr(), cap)
+    zb = ctx.bgzf_deflate_dev(d_recs.data_ptr(), B, level, d_z.data_ptr(), cap)
     ms.append(round(ctx.timing("bgzf_deflate"), 2))
 sha = hashlib.sha256(d_z[:zb].cpu().numpy().tobytes()).hexdigest()[:16]
-print(sys.argv[1:] or ["default"], "deflate ms", ms[1:], "bytes", zb, "ratio", round(zb / B, 4), "sha", sha, flush=True)
+print(sys.argv[1:] or ["default"], "level", level, "deflate ms", ms[1:], "bytes", zb, "ratio", round(zb / B, 4), "sha", sha, flush=True)
+if os.environ.get("DIAG_ZLIB"):  # zlib level 6 per 65,280-byte payload over the first 32 MiB, for comparison
+    import zlib
+    h = d_recs[: 65280 * 514].cpu().numpy().tobytes()
+    g = bytes(d_z[: 0].cpu().numpy())
+    zs = sum(len(zlib.compress(h[i:i + 65280], 6)) - 6 + 26 for i in range(0, len(h), 65280))
+    print("zlib-6 sample ratio", round(zs / len(h), 4), flush=True)
