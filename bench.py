@@ -481,20 +481,27 @@ def zlib6_sample_ratio(S, off: int, nbytes: int, sample: int = 32 << 20) -> dict
             "what": "zlib level 6 per 65,280-byte payload + BGZF framing, first bytes of the same record stream"}
 
 
-def build_input(ctx, L, S: DevBuf, total: int, level: int) -> tuple[DevBuf, int]:
+def build_input(ctx, L, S: DevBuf, total: int, level: int, chain_probe: dict | None = None) -> tuple[DevBuf, int]:
     """The input BAM file in HBM: the library's GPU deflate of [header][records] at `level` plus the
     EOF block, in a buffer of exactly its size (the records S and the bound-sized staging buffer are
-    freed)."""
+    freed).  chain_probe (a dict): first one level-9 deflate of the same bytes (same-prefix chains + lazy
+    matching, bgzf.hip) -- its stage time and size go into the dict."""
     bound = int(L.lib().oge_bgzf_bound(total))
     X, _, cap = ctx.mergesort_reserve(total)
     Z = DevBuf.view(ctx, L, X, cap)  # the chain's other arena stages the compressed file
     assert cap >= bound + 64
     zb = ctx.bgzf_deflate_dev(S.ptr, total, level, Z.ptr, bound)
     ctx.sync()
-    S.free()
     d_z = DevBuf(ctx, L, zb + 28 + 64)
     L.check(L.lib().oge_memcpy(ctx.h, d_z.ptr, Z.ptr, zb, 3), ctx.h)
     d_z.put(zb, BGZF_EOF)
+    if chain_probe is not None:  # after the level-`level` run, so its workspace is in place
+        z9 = ctx.bgzf_deflate_dev(S.ptr, total, 9, Z.ptr, bound)
+        chain_probe.update({"level": 9, "ms": round(ctx.timing("bgzf_deflate"), 1), "bytes": z9,
+                            "ratio": round(z9 / total, 4),
+                            "search": "levels 8-9: at every candidate the chain of earlier same-prefix positions "
+                                      "(8 / 32 deep) and zlib-style lazy matching; levels 1-7 the greedy search"})
+    S.free()
     Z.free()
     return d_z, zb + 28
 
@@ -561,7 +568,8 @@ def main():
 
     # ---- the input BAM file in HBM (level-6 BGZF, GPU deflate), staging freed
     zref = zlib6_sample_ratio(S, len(hb), B)
-    d_z, zbytes = build_input(ctx, L, S, total, args.level)
+    chain_probe = {}
+    d_z, zbytes = build_input(ctx, L, S, total, args.level, chain_probe)
     torch.cuda.synchronize(dev)
     log(f"input BAM file in HBM: {zbytes / 1e9:.2f} GB (ratio {zbytes / total:.3f})")
 
@@ -645,7 +653,8 @@ def main():
                    "reads_total": n, "record_bytes": B, "input_file_bytes": zbytes, "output_file_bytes": out_bytes,
                    "duplicates_flagged": nd, "parallelism": "1 GPU",
                    "deflate": {"search": DEFLATE_SEARCH, "gpu_ratio_input_file": round(zbytes / total, 4),
-                               "gpu_ratio_output_file": round(out_bytes / total, 4), "zlib6_sample": zref}},
+                               "gpu_ratio_output_file": round(out_bytes / total, 4), "zlib6_sample": zref,
+                               "level9_same_records": chain_probe}},
         "roofline": roof, "roofline_stages": others, "stages_ms": sms, "warmup_ms": warm,
         "cold_ms": warm[0] if warm else None, "cold_over_warm": round(warm[0] / ms_step, 2) if warm else None,
         "cold_workspace": cold_ws,
