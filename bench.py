@@ -463,7 +463,8 @@ def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, DevBuf, int,
 DEFLATE_SEARCH = ("GPU deflate (bgzf.hip): greedy parse, ONE hash candidate per position (4-byte prefix, 4096 "
                   "buckets, filled in rounds of 1024 positions), matches cut at 64-byte segment edges, no lazy "
                   "matching; one dynamic-Huffman block per 65,280-byte payload (length-limited to 15 bits). "
-                  "The level number selects stored (0) or this mode (1-9): it is not zlib's level-6 search")
+                  "Level 0 is stored, 1-7 this mode (it is not zlib's level-6 search), 8-9 add same-prefix chains "
+                  "and lazy matching (level9_same_records)")
 
 
 def zlib6_sample_ratio(S, off: int, nbytes: int, sample: int = 32 << 20) -> dict:
