@@ -383,7 +383,8 @@ uint64_t oge_bgzf_bound(uint64_t n);
 /* Compress n bytes at d_src into consecutive BGZF blocks (65,280-byte payloads; dynamic-Huffman
  * deflate, or stored blocks for level 0 / incompressible payloads) written back to back at d_dst.
  * No EOF marker is appended.  dst_cap must be >= oge_bgzf_bound(n); *out_bytes = stream size.
- * Deterministic: the same input gives the same bytes. */
+ * Levels 1-7: greedy one-candidate parse; 8-9: same-prefix match chains (8 / 32 deep) with lazy
+ * matching, ~1 % smaller output at 1.7-3x the time.  Deterministic: the same input gives the same bytes. */
 int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t n, int level, uint8_t *d_dst,
                          uint64_t dst_cap, uint64_t *out_bytes);
 /* Host-buffer form (uploads, compresses, downloads); dst_cap >= the compressed size. */
