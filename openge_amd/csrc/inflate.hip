@@ -648,6 +648,7 @@ extern "C" int oge_bgzf_inflate_dev(oge_ctx *ctx, const uint8_t *d_z, uint64_t z
     OGE_HIP_TRY(ctx, hipMemcpyAsync(got, err, 8, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (got[0]) {
+        ctx->infl_clean_ptr = nullptr;  // a failed block may have left bits phase 2 did not clear
         char msg[160];
         snprintf(msg, sizeof msg, "BGZF block %u failed to inflate (%s; error bits 0x%x)", got[1],
                  (got[0] >> E_CRC) & 1 ? "CRC mismatch" : "corrupt deflate data", got[0]);

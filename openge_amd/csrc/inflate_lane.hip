@@ -777,7 +777,7 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
 constexpr uint32_t kT2 = 1024;
 
 __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, const uint64_t *__restrict__ uoff,
-                                                 const uint32_t *__restrict__ crc, const uint64_t *__restrict__ bitmap,
+                                                 const uint32_t *__restrict__ crc, uint64_t *__restrict__ bitmap,
                                                  const uint8_t *__restrict__ xtab, uint64_t b0, uint64_t nb,
                                                  const uint32_t *__restrict__ zpow, uint32_t *__restrict__ err) {
     __shared__ __align__(16) uint16_t refs[kSlot + 16];  // later the block's bytes (img)
@@ -810,7 +810,11 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         const uint32_t osz = (uint32_t)(uoff[b + 1] - uoff[b]);
         const uint8_t *O = out + uoff[b];
         hv = u64x2{0, 0};
-        if (t < ((osz + 63) >> 6)) hv = *(const OGE_G u64x2 *)((const OGE_G uint64_t *)(bitmap + i * 2048) + 2 * t);
+        if (t < ((osz + 63) >> 6)) {
+            OGE_G u64x2 *bp = (OGE_G u64x2 *)((OGE_G uint64_t *)(bitmap + i * 2048) + 2 * t);
+            hv = *bp;
+            *bp = u64x2{0, 0};  // cleared behind the read: the next chunk's phase 1 needs no memset (r05)
+        }
         xv = u32x4{0, 0, 0, 0};
         if (t < kXTab / 16) xv = *(const OGE_G u32x4 *)(xtab + i * kXTab + 16 * t);
         const OGE_G uint32_t *W = (const OGE_G uint32_t *)((uintptr_t)(O + q0) & ~(uintptr_t)3);
@@ -1131,7 +1135,18 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nb + 63) / 64, wgs);
         const Set &u = B[k % S];
         OGE_HIP_TRY(ctx, hipMemsetAsync(u.next, 0, 8, u.st));
-        OGE_HIP_TRY(ctx, hipMemsetAsync(u.bitmap, 0, nb * 2048 * 8, u.st));  // phase 1 stores only words with bits
+        // phase 1 stores only words with bits, so the bitmaps must start clear: phase 2 clears every word it
+        // read, which leaves the buffer clear for the next chunk and the next call (ctx->infl_clean: the
+        // buffer and how many of its bytes are known clear; a failed launch forgets it).  Fresh or grown
+        // buffers, and the two-stream layout, are cleared here (a 21 GB memset per 300M-read step before).
+        const uint64_t bbytes = nb * 2048 * 8;
+        const bool clean = S == 1 && ctx->infl_clean_ptr == u.bitmap && ctx->infl_clean_bytes >= bbytes;
+        if (!clean) OGE_HIP_TRY(ctx, hipMemsetAsync(u.bitmap, 0, bbytes, u.st));
+        if (S == 1) {
+            const uint64_t known = clean ? ctx->infl_clean_bytes : bbytes;
+            ctx->infl_clean_ptr = nullptr, ctx->infl_clean_bytes = 0;  // until phase 2 is launched
+            ctx->infl_clean_next = known;
+        }
         // each phase's own time (stages "infl_huff" / "infl_lz", summed over the chunks) on the one stream
         OgeStageTimer *t1 = S == 1 ? ctx->begin_stage("infl_huff") : nullptr;
         k_infl_huff<<<g1, 64, 0, u.st>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, u.bitmap, u.xtab, u.scr, err, u.next);
@@ -1142,6 +1157,7 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
                                                                                    zpow, err);
         OGE_LAUNCH_CHECK(ctx);
         ctx->end_stage(t2);
+        if (S == 1) ctx->infl_clean_ptr = u.bitmap, ctx->infl_clean_bytes = ctx->infl_clean_next;
     }
     if (S > 1) {  // the context stream waits for every chunk
         for (int j = 0; j < S; ++j) {

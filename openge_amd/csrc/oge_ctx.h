@@ -53,6 +53,9 @@ struct oge_ctx {
         const uint16_t *rel = nullptr;
         uint32_t sc = 0;
     } recwalk;
+    // the inflate's phase-1 bitmap buffer and how many of its bytes are known clear (inflate_lane.hip)
+    const void *infl_clean_ptr = nullptr;
+    uint64_t infl_clean_bytes = 0, infl_clean_next = 0;
     std::map<std::string, uint64_t> counters;  // per call: work counts a stage reports (oge_ctx_counter)
     bool last_scan_generic = false;  // realign scan fell back to the byte-wise kernel
     double scan_t[3] = {0, 0, 0};    // realign scan host timings: validate, upload, device + download
