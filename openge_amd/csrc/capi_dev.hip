@@ -178,6 +178,13 @@ int oge_ctx_set_stream(oge_ctx *ctx, void *stream) {
     if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "null ctx");
     hipSetDevice(ctx->device);
     if (stream) {
+        // the old stream's work ends before the new stream's starts: the inflate's bitmap carry-over
+        // (phase 2 clears what phase 1 of the next call relies on) and the record walk's cached starts
+        // are only valid in stream order, so both are also forgotten
+        (void)hipStreamSynchronize(ctx->stream);
+        ctx->infl_clean_ptr = nullptr;
+        ctx->infl_clean_bytes = ctx->infl_clean_next = 0;
+        ctx->recwalk = oge_ctx::RecWalk{};
         if (ctx->own_stream) hipStreamDestroy(ctx->stream);
         ctx->stream = (hipStream_t)stream;
         ctx->own_stream = false;

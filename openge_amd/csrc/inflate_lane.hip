@@ -277,6 +277,11 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
 #if OGE_EXP == 2  // timing experiment: cycles spent taking the prefetched chunk (its wait) vs the decode loop
     uint64_t x_wait = 0, x_loop = 0, x_steps = 0;
 #endif
+#if OGE_EXP == 3  // timing experiment: a wave's cycles in the table builds / block taking / decode loop, and
+                  // how many of its decode iterations run each state's path (some lane in that state)
+    uint64_t y_bld = 0, y_nxt = 0, y_loop = 0, y_clc = 0, y_oc = 0;
+    uint32_t y_it = 0, y_cl = 0, y_hdr = 0, y_sto = 0, y_sym = 0, y_nbcl = 0, y_nbld = 0, y_blk = 0;
+#endif
     auto refill = [&]() {
         if (cnt <= 32) {
             buf |= (uint64_t)q.x << cnt;
@@ -435,6 +440,11 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
             ferr = 0;
         }
         // ---- table builds, the whole wave for one lane at a time
+#if OGE_EXP == 3
+        const uint64_t y0 = __builtin_readcyclecounter();
+        y_nbcl += (uint32_t)__popcll(__ballot(st == ST_BCL));
+        y_nbld += (uint32_t)__popcll(__ballot(st == ST_BLD));
+#endif
         uint64_t need = __ballot(st == ST_BCL || st == ST_BLD);
         if (need) __threadfence_block();  // lanes' code-length stores before the wave reads them
         while (need) {
@@ -529,6 +539,10 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
         // ---- next block for lanes that finished theirs: taken from the launch's queue (one atomic per
         // wave), so a lane never idles while blocks are left -- the launch ends when the queue drains,
         // not when the slowest of a fixed block-per-lane assignment does
+#if OGE_EXP == 3
+        const uint64_t y1 = __builtin_readcyclecounter();
+        y_bld += y1 - y0;
+#endif
         const uint64_t want = __ballot(st == ST_NEXT);
         if (want) {
             const uint32_t leader = (uint32_t)__builtin_ctzll(want);
@@ -559,7 +573,18 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 st = ST_HDR;
             }
         }
+#if OGE_EXP == 3
+        y_blk += (uint32_t)__popcll(__ballot(st == ST_HDR));
+        y_nxt += __builtin_readcyclecounter() - y1;
+#endif
         if (__ballot(st != ST_DONE) == 0) {
+#if OGE_EXP == 3
+            if (lane == 0 && blockIdx.x < 16)
+                printf("infl-exp3 wave %u: cycles build %llu next %llu loop %llu | iters %u: with CL %u HDR %u STORED %u SYM %u | "
+                       "blocks %u builds cl %u tab %u | cycles in iters with CL %llu without %llu\n",
+                       blockIdx.x, (unsigned long long)y_bld, (unsigned long long)y_nxt, (unsigned long long)y_loop, y_it, y_cl,
+                       y_hdr, y_sto, y_sym, y_blk, y_nbcl, y_nbld, (unsigned long long)y_clc, (unsigned long long)y_oc);
+#endif
 #if OGE_EXP == 2
             uint64_t w = x_wait;
 #pragma unroll
@@ -576,7 +601,19 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
         const uint64_t l0 = __builtin_readcyclecounter();
         x_steps += kInner;
 #endif
+#if OGE_EXP == 3
+        const uint64_t y2 = __builtin_readcyclecounter();
+#endif
         for (int it = 0; it < kInner; ++it) {
+#if OGE_EXP == 3
+            ++y_it;
+            const uint64_t yi = __builtin_readcyclecounter();
+            const bool ycl = __ballot(st == ST_CL) != 0;
+            y_cl += ycl;
+            y_hdr += __ballot(st == ST_HDR) != 0;
+            y_sto += __ballot(st == ST_STORED) != 0;
+            y_sym += __ballot(st == ST_SYM) != 0;
+#endif
             if (st == ST_SYM) {
                 // an iteration: up to LB direct literals, one symbol of any kind, up to LB direct literals.
                 // A wave runs the union of its lanes' paths, so a lane should make as much progress per
@@ -758,9 +795,19 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                     else st = ST_HDR;
                 }
             }
+#if OGE_EXP == 3
+            {
+                const uint64_t yc = __builtin_readcyclecounter() - yi;
+                if (ycl) y_clc += yc;
+                else y_oc += yc;
+            }
+#endif
         }
 #if OGE_EXP == 2
         x_loop += __builtin_readcyclecounter() - l0;
+#endif
+#if OGE_EXP == 3
+        y_loop += __builtin_readcyclecounter() - y2;
 #endif
     }
 }

@@ -313,6 +313,19 @@ extern "C" int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_
             for (auto e : *v) (void)hipEventDestroy(e);
         }
     } evs{&up};
+    // Every exit, error paths included, waits for the copy stream (uploads reading h_z, downloads writing
+    // h_out) and the context stream (the direct mode's emitter writes h_out): a caller may free or reuse
+    // its page-locked buffers as soon as this returns.  Declared after `evs`, so it runs first.
+    struct Drain {
+        hipStream_t a, b;
+        ~Drain() {
+            (void)hipStreamSynchronize(a);
+            (void)hipStreamSynchronize(b);
+        }
+    } drain{cs, ctx->stream};
+    // test hook: OGE_HOSTPIPE_FAIL_SEG=k makes segment k (k >= 1) fail after the earlier segments' copies
+    // were queued (tests/test_gpu_pipeline.py::test_host_pipeline_failed_segment_drains)
+    const uint64_t fail_seg = env_u64("OGE_HOSTPIPE_FAIL_SEG", 0);
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // dz may still be read by this context's last call
     for (uint64_t o = 0; o < zbytes; o += C) {
         hipEvent_t e;
@@ -431,13 +444,11 @@ extern "C" int oge_mergesort_bgzf_host(oge_ctx *ctx, const uint8_t *h_z, uint64_
         mark("segment buffer free", k);
         uint64_t got = 0;
         const uint64_t sh = ((uintptr_t)(h_out + pos)) & 255;
+        if (fail_seg && k == fail_seg) return oge_fail(ctx, OGE_ERR_HIP, "injected segment failure (OGE_HOSTPIPE_FAIL_SEG)");
         rc = oge_bgzf_deflate_dev(ctx, src + ends[0] + s0, sl, mo->level, zb[k & 1] + sh, bnd, &got);  // returns when written
         if (rc) return rc;
         mark("segment deflated", k);
-        if (pos + got + 28 > out_cap) {
-            (void)hipStreamSynchronize(cs);
-            return oge_fail(ctx, OGE_ERR_LIMIT, "output buffer too small");
-        }
+        if (pos + got + 28 > out_cap) return oge_fail(ctx, OGE_ERR_LIMIT, "output buffer too small");
         OGE_HIP_TRY(ctx, hipMemcpyAsync(h_out + pos, zb[k & 1] + sh, got, hipMemcpyDeviceToHost, cs));
         OGE_HIP_TRY(ctx, hipEventRecord(dn[k & 1], cs));
         pos += got;

@@ -156,6 +156,23 @@ def test_inflate_rejects_corruption(ctx):
         ctx.bgzf_inflate(bytes(z[:-40]))  # truncated
 
 
+
+def test_inflate_carry_over_on_one_context(ctx):
+    """One context, calls in sequence: a corrupt stream (phase 1 fails some blocks, so phase 2 may not clear
+    every bitmap word it would), then a valid stream, then a smaller one, then a larger one -- each checked
+    byte for byte.  The phase-1 bitmap buffer is carried from call to call as known-clear."""
+    from openge_amd import lib as L
+    big = DATA["bam"] + DATA["text"] + DATA["random"]
+    z = bytearray(bgzf(big, 6))
+    for k in range(200, 240):  # the first block's body: a deflate error, not only a CRC one
+        z[k] ^= 0x5A
+    with pytest.raises(L.OgeError):
+        ctx.bgzf_inflate(bytes(z))
+    for data in (big, DATA["acgt"], DATA["bam"][:70_001], big + DATA["zeros"]):
+        assert ctx.bgzf_inflate(bgzf(data, 6)) == data
+    assert ctx.bgzf_inflate(bgzf(DATA["text"], 6, zlib.Z_FIXED)) == DATA["text"]
+
+
 def _stream(n_pairs, seed):
     """A decompressed BAM stream (header + records) and its record offsets, from the host writer."""
     from openge_amd import lib as L

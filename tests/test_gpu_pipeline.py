@@ -205,3 +205,30 @@ def test_host_pipeline_errors(ctx):
     ho = np.empty(64, np.uint8)
     with pytest.raises(L.OgeError, match="too small"):
         ctx.mergesort_bgzf_host(hz.ctypes.data, len(src), L.mergesort_opts(), ho.ctypes.data, len(ho))
+
+
+def test_host_pipeline_failed_segment_drains(ctx, monkeypatch, tmp_path):
+    """A segment that fails after earlier segments' device-to-host copies were queued: the call returns its
+    error only once those copies (and the uploads) are done, so the page-locked buffers can be reused or
+    freed at once; the next call on the same buffers and context writes the right bytes."""
+    monkeypatch.setenv("OGE_HOSTPIPE_GROUPS", "7")
+    monkeypatch.setenv("OGE_HOSTPIPE_SEG_BLOCKS", "2")
+    p = L.synth_params(30_000, preset="c2", seed=5)
+    recs, offs, hdr = L.synth_host(p)
+    L.write_bam(tmp_path / "in.bam", hdr, recs, offs, len(offs) - 1, level=6)
+    src = (tmp_path / "in.bam").read_bytes()
+    want = _run_pipeline(ctx, src, mark_duplicates=1)
+    hz = torch.from_numpy(np.frombuffer(src, np.uint8).copy()).pin_memory()
+    cap = len(src) * 2 + (1 << 20)
+    ho = torch.zeros(cap, dtype=torch.uint8).pin_memory()
+    o = L.mergesort_opts(mark_duplicates=1)
+    monkeypatch.setenv("OGE_HOSTPIPE_FAIL_SEG", "3")
+    with pytest.raises(L.OgeError, match="injected segment failure"):
+        ctx.mergesort_bgzf_host(hz.data_ptr(), len(src), o, ho.data_ptr(), cap)
+    before = ho.clone()  # whatever the queued copies wrote is complete now: nothing may change any more
+    torch.cuda.synchronize()
+    assert torch.equal(before, ho)
+    ho.fill_(0)
+    monkeypatch.delenv("OGE_HOSTPIPE_FAIL_SEG")
+    nb, nr, nd = ctx.mergesort_bgzf_host(hz.data_ptr(), len(src), o, ho.data_ptr(), cap)
+    assert (ho[:nb].numpy().tobytes(), nr, nd) == want

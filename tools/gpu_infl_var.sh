@@ -5,8 +5,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${1:-infl_var}
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 200 python -u tools/diag_infl.py > $OUT/default.txt 2>&1 || { tail -20 $OUT/default.txt; exit 1; }
-cat $OUT/default.txt
+[ -n "$NODEFAULT" ] || { timeout -k 10 200 python -u tools/diag_infl.py > $OUT/default.txt 2>&1 || { tail -20 $OUT/default.txt; exit 1; }; }
+[ -n "$NODEFAULT" ] || cat $OUT/default.txt
 for v in ${VARS-openge_amd/_var/lib_*.so}; do
   n=$(basename $v .so)
   timeout -k 10 200 python -u tools/diag_infl.py $v > $OUT/$n.txt 2>&1 || { tail -20 $OUT/$n.txt; exit 1; }
