@@ -104,7 +104,7 @@ __constant__ uint8_t kClOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 
 // so building one lane's table never touches another lane's column
 __device__ __forceinline__ uint32_t cl_at(uint32_t i, uint32_t l) { return ((i >> 1) * 64 + l) * 2 + (i & 1); }
 
-enum { ST_HDR = 0, ST_CL = 1, ST_SYM = 2, ST_STORED = 3, ST_BCL = 4, ST_BLD = 5, ST_NEXT = 6, ST_DONE = 7 };
+enum { ST_HDR = 0, ST_CL = 1, ST_SYM = 2, ST_STORED = 3, ST_BCL = 4, ST_BLD = 5, ST_NEXT = 6, ST_DONE = 7, ST_LOAD = 8 };
 
 // the slow-path parameters of one lane, in VGPRs (u16 pairs)
 struct Slow {
@@ -136,6 +136,15 @@ __device__ __forceinline__ uint32_t pick(const uint32_t (&a)[N], uint32_t i) {  
 }
 __device__ __forceinline__ uint32_t u16of(const uint32_t (&a)[6], uint32_t i) {
     return (pick(a, i >> 1) >> ((i & 1) * 16)) & 0xffff;
+}
+// Slow's fields by flat index (the pre-pass record's order): ll[4] l15 pk[9] dl[6] di[6]
+template <int I>
+__device__ __forceinline__ void tset(Slow &T, uint32_t v) {
+    if constexpr (I < 4) T.ll[I] = v;
+    else if constexpr (I == 4) T.l15 = v;
+    else if constexpr (I < 14) T.pk[I - 5] = v;
+    else if constexpr (I < 20) T.dl[I - 14] = v;
+    else T.di[I - 20] = v;
 }
 
 // ---------------------------------------------------------------------------- wave-cooperative builds
@@ -228,6 +237,297 @@ __device__ bool wbuild(P1Lds &S, uint32_t j, OGE_G uint8_t *list, OGE_G uint8_t 
     return true;
 }
 
+// ---------------------------------------------------------------------------- header pre-pass
+// k_infl_prep (r06): the FIRST deflate header of every BGZF block starts at a known byte
+// (d0), so it is parsed -- block type, code-length code, the code lengths -- and its two tables built by one
+// lane per block in a kernel of their own, before phase 1.  Phase 1 then copies a block's ready tables
+// into its lane's LDS column (one wave-wide load per lane) instead of running the header, the code-length
+// decode (a few hundred decode-loop iterations per block) and two wave-wide builds inside its decode loop.
+// Measured before (profiles/r06a/r06b, OGE_EXP=3, 100M reads): the builds were 2.3 % and the iterations
+// carrying a code-length lane 4.2 % of a phase-1 wave's cycles -- the lanes of a wave stay in lockstep
+// (equal-size BGZF payloads), so those phases mostly coincide.
+// Output per block (kPrep bytes, the layout phase 1's copy reads with one 8-byte load per lane): lt image
+// (64 u16) | dt (16 B) | ll (32 B) | dl (32 B) | the Slow parameters (26 u32); the long-literal translation
+// list into the block's xtab slot 0; pmeta[bi] = prepared (bit 31) | deferred long literals (29) | BFINAL
+// (28) | bits from d0 to the first symbol (< 2^24).  Anything unusual -- a stored or invalid first block,
+// an over-subscribed code, more than 256 long literal/length codes, a header past the block's end -- leaves
+// pmeta = 0 and phase 1 parses that block itself, as before (same results, same error codes).
+constexpr uint32_t kPrep = 336;
+constexpr uint32_t P_SLOW = 208;  // byte offset of the Slow parameters: ll[4] l15 pk[9] dl[6] di[6]
+
+template <int N>
+__device__ __forceinline__ void sadd(uint32_t (&a)[N], uint32_t i, uint32_t v) {  // a[i] += v, a in VGPRs
+    sfor<N>([&](auto k) { a[k()] += i == (uint32_t)k() ? v : 0u; });
+}
+
+__global__ void __launch_bounds__(64) k_infl_prep(const uint8_t *__restrict__ z, uint64_t zbytes, const uint64_t *__restrict__ d0a,
+                                                  const uint64_t *__restrict__ d1a, uint64_t b0, uint64_t nb,
+                                                  uint8_t *__restrict__ prep, uint32_t *__restrict__ pmeta,
+                                                  uint8_t *__restrict__ xtab) {
+    // per-lane LDS columns ([entry][lane]: a wave's accesses at one entry index hit 64 banks)
+    __shared__ uint16_t img[64][64];          // the code-length code's table (bytes, cl_at), then the lt image
+    __shared__ uint32_t lens8[40][64];        // code lengths, eight per word: symbol s in nibble s & 7 of word s >> 3
+    __shared__ uint8_t sm[16 + 32 + 30][64];  // dt | ll | dl images
+    // per length (LDS atomics): count | literal count << 16, then rank (bits 0-8) | the length's code /
+    // list base (9-31)
+    __shared__ uint32_t cnt[16][64];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t bi = (uint64_t)blockIdx.x * 64 + lane;
+    if (bi >= nb) return;  // no wave-wide operation below
+    const uint64_t b = b0 + bi;
+    pmeta[bi] = 0;
+    const uint64_t a0 = d0a[b], a1 = d1a[b];
+    if (a1 <= a0 || a1 > zbytes) return;
+    auto len_of = [&](uint32_t s) { return (lens8[s >> 3][lane] >> (4 * (s & 7))) & 15; };
+    // bit reader over the block's bytes: 64-bit buffer fed from 16-byte chunks loaded two ahead (a header
+    // is ~100-300 bytes: a global round trip per refill was most of this kernel's time)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uintptr_t zend = (uintptr_t)z + zbytes, zlast = (zend - 1) & ~(uintptr_t)15;
+    auto load16 = [&](uintptr_t a) { return *(const OGE_G u32x4 *)(a < zend ? a : zlast); };
+    const uintptr_t al16 = ((uintptr_t)z + a0) & ~(uintptr_t)15;
+    u32x4 q = load16(al16), p1 = load16(al16 + 16), p2 = load16(al16 + 32);
+    uintptr_t cp = al16 + 48;
+    uint32_t qn = 4;
+    for (uint32_t k = 0; k < (uint32_t)((a0 & 15) >> 2); ++k) q.x = q.y, q.y = q.z, q.z = q.w, --qn;
+    uint64_t buf = 0;
+    uint32_t cn = 0, used = 0;  // used: bits consumed from d0
+    auto refill = [&]() {
+        while (cn <= 32) {
+            buf |= (uint64_t)q.x << cn;
+            cn += 32;
+            q.x = q.y, q.y = q.z, q.z = q.w;
+            if (--qn == 0) {
+                q = p1, p1 = p2, qn = 4;
+                p2 = load16(cp);
+                cp += 16;
+            }
+        }
+    };
+    auto get = [&](uint32_t k) {
+        const uint32_t v = (uint32_t)buf & ((1u << k) - 1);
+        buf >>= k;
+        cn -= k;
+        used += k;
+        return v;
+    };
+    refill();
+    {
+        const uint32_t sk = (uint32_t)(a0 & 3) * 8;
+        buf >>= sk;
+        cn -= sk;
+    }
+    refill();
+    const uint32_t h = get(3), type = h >> 1;
+    uint32_t hl, hd;
+    if (type == 1) {
+        hl = 288, hd = 30;
+        for (uint32_t w = 0; w < 40; ++w)
+            lens8[w][lane] = w < 18 ? 0x88888888u : w < 32 ? 0x99999999u : w < 35 ? 0x77777777u : w < 36 ? 0x88888888u : 0x55555555u;
+    } else if (type == 2) {
+        hl = get(5) + 257;
+        hd = get(5) + 1;
+        const uint32_t hclen = get(4) + 4;
+        if (hl > 286 || hd > 30) return;
+        uint64_t c = 0;
+        for (uint32_t i = 0; i < hclen; ++i) {
+            refill();
+            c |= (uint64_t)get(3) << (3 * kClOrd[i]);
+        }
+        // the code-length code: counts, Kraft, canonical codes in symbol order, 7-bit direct table
+        uint32_t cl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t s = 0; s < 19; ++s) sadd(cl, (uint32_t)(c >> (3 * s)) & 7, 1);
+        int left = 1;
+        bool ok = true;
+        uint32_t nx[8];
+        uint32_t code = 0;
+        nx[0] = 0;
+        sfor<7>([&](auto k) {
+            constexpr int L = decltype(k)::value + 1;
+            left = 2 * left - (int)cl[L];
+            ok = ok && left >= 0;
+            code = (code + (L > 1 ? cl[L - 1] : 0u)) << 1;
+            nx[L] = code;
+        });
+        if (!ok) return;
+        uint8_t *clt = (uint8_t *)&img[0][0];
+        for (uint32_t i = 0; i < 64; ++i) img[i][lane] = 0;
+        for (uint32_t s = 0; s < 19; ++s) {
+            const uint32_t L = (uint32_t)(c >> (3 * s)) & 7;
+            if (!L) continue;
+            const uint32_t cd = pick(nx, L);
+            sadd(nx, L, 1);
+            const uint32_t rev = __builtin_bitreverse32(cd) >> (32 - L);
+            for (uint32_t k = 0; k < (1u << (7 - L)); ++k) clt[cl_at(rev | (k << L), lane)] = (uint8_t)(s | (L << 5));
+        }
+        // the code lengths (RFC 1951 3.2.7), OR-ed into cleared words (zero runs write nothing)
+        for (uint32_t w = 0; w < 40; ++w) lens8[w][lane] = 0;
+        const uint32_t total = hl + hd;
+        uint32_t ci = 0, prev = 0;
+        while (ci < total) {
+            refill();
+            const uint32_t e = clt[cl_at((uint32_t)buf & 127, lane)];
+            if (!e) return;
+            get(e >> 5);
+            const uint32_t s = e & 31;
+            uint32_t rep = 1, val = s;
+            if (s == 16) {
+                if (ci == 0) return;
+                rep = 3 + get(2), val = prev;
+            } else if (s == 17) {
+                rep = 3 + get(3), val = 0;
+            } else if (s == 18) {
+                rep = 11 + get(7), val = 0;
+            }
+            if (ci + rep > total) return;
+            if (val)
+                for (uint32_t k = 0; k < rep; ++k) {
+                    const uint32_t t = ci + k, s2 = t < hl ? t : t - hl + 288;  // distance lengths at 288.. (the fixed layout)
+                    atomicOr(&lens8[s2 >> 3][lane], val << (4 * (s2 & 7)));
+                }
+            prev = val;
+            ci += rep;
+        }
+        if (!len_of(256)) return;  // no end-of-block code
+    } else {
+        return;  // stored (or invalid) first block: phase 1 handles it
+    }
+    if ((uint64_t)a0 * 8 + used > (uint64_t)a1 * 8 || used >= (1u << 24)) return;
+
+    // ---- literal/length table (TL-bit direct, long codes by canonical limits): what wbuild<5, TL, true> makes
+    uint32_t Slow[26];
+    {
+        for (uint32_t i = 0; i < 16; ++i) cnt[i][lane] = 0;
+        for (uint32_t w = 0; w < (hl + 7) / 8; ++w) {
+            const uint32_t x = lens8[w][lane];
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) {
+                const uint32_t s = 8 * w + i, L = (x >> (4 * i)) & 15;
+                if (s < hl && L) atomicAdd(&cnt[L][lane], s < 256 ? 0x10001u : 1u);  // literal symbols counted high
+            }
+        }
+        uint32_t c[16], lo[16];
+        sfor<16>([&](auto k) {
+            constexpr int L = decltype(k)::value;
+            const uint32_t v = L ? cnt[L][lane] : 0u;
+            c[L] = v & 0xffff;
+            lo[L] = v >> 16;
+        });
+        uint32_t kraft = 0, nlong = 0;
+        sfor<15>([&](auto k) {
+            constexpr int L = decltype(k)::value + 1;
+            kraft += c[L] << (15 - L);
+            if (L > TL) nlong += c[L];
+        });
+        if (kraft > 32768u || nlong > 256) return;
+        uint32_t fst[16], ofl[16], litb[16];
+        sfor<16>([&](auto k) {
+            constexpr int L = decltype(k)::value;
+            uint32_t f = 0, o = 0, lbb = 0;
+            sfor<L>([&](auto m) {
+                constexpr int l = decltype(m)::value;
+                if (l >= 1) {
+                    f += c[l] << (L - l);
+                    if (l > TL) o += c[l], lbb += lo[l];
+                }
+            });
+            fst[L] = f, ofl[L] = o, litb[L] = lbb;
+            // per length: the first code (direct codes) or the list base and the length-code base + 320 (long
+            // codes) above a cleared rank
+            cnt[L][lane] = (L <= TL ? f : o | ((o - lbb - lo[L] + 320) << 9)) << 9;
+        });
+        sfor<4>([&](auto k) {
+            constexpr int L0 = 7 + 2 * decltype(k)::value, L1 = L0 + 1;
+            Slow[decltype(k)::value] = min((fst[L0] + c[L0]) << (15 - L0), 65535u) | (min((fst[L1] + c[L1]) << (15 - L1), 65535u) << 16);
+        });
+        Slow[4] = min(fst[15] + c[15], 65535u);
+        sfor<9>([&](auto k) {
+            constexpr int L = 7 + decltype(k)::value;
+            Slow[5 + decltype(k)::value] = ((ofl[L] - fst[L]) & 0xffff) | ((ofl[L] + lo[L]) << 16) | ((ofl[L] - litb[L]) << 25);
+        });
+        for (uint32_t i = 0; i < 64; ++i) img[i][lane] = 0x100;
+        for (uint32_t i = 16; i < 78; ++i) sm[i][lane] = 0;  // entries no valid code reaches: deterministic bytes
+        OGE_G uint8_t *xl = (OGE_G uint8_t *)(xtab + bi * kXTab);  // table slot 0's translation list
+        for (uint32_t w = 0; w < (hl + 7) / 8; ++w) {
+            const uint32_t x = lens8[w][lane];
+            for (uint32_t i = 0; i < 8; ++i) {
+                const uint32_t s = 8 * w + i, L = (x >> (4 * i)) & 15;
+                if (s >= hl || !L) continue;
+                const uint32_t r = atomicAdd(&cnt[L][lane], 1u), rank = r & 511, inf = r >> 9;
+                if (L <= (uint32_t)TL) {
+                    const uint32_t rev = __builtin_bitreverse32(inf + rank) >> (32 - L);
+                    for (uint32_t k = 0; k < (1u << (TL - L)); ++k) img[rev | (k << L)][lane] = (uint16_t)(s | (L << 9));
+                } else {
+                    xl[(inf & 511) + rank] = (uint8_t)s;
+                    if (s >= 256) sm[16 + min((inf >> 9) + rank - 320, 31u)][lane] = (uint8_t)(s - 256);
+                }
+            }
+        }
+    }
+    // ---- distance table (TD-bit direct): what wbuild<1, TD, false> makes
+    {
+        for (uint32_t i = 0; i < 16; ++i) cnt[i][lane] = 0;
+        for (uint32_t w = 36; w < 36 + (hd + 7) / 8; ++w) {
+            const uint32_t x = lens8[w][lane];
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) {
+                const uint32_t s = 8 * (w - 36) + i, L = (x >> (4 * i)) & 15;
+                if (s < hd && L) atomicAdd(&cnt[L][lane], 1u);
+            }
+        }
+        uint32_t c[16];
+        sfor<16>([&](auto k) {
+            constexpr int L = decltype(k)::value;
+            c[L] = L ? cnt[L][lane] : 0u;
+        });
+        uint32_t kraft = 0;
+        sfor<15>([&](auto k) {
+            constexpr int L = decltype(k)::value + 1;
+            kraft += c[L] << (15 - L);
+        });
+        if (kraft > 32768u) return;
+        uint32_t lim[16], pk[16];
+        sfor<16>([&](auto k) {
+            constexpr int L = decltype(k)::value;
+            uint32_t f = 0, o = 0;
+            sfor<L>([&](auto m) {
+                constexpr int l = decltype(m)::value;
+                if (l >= 1) {
+                    f += c[l] << (L - l);
+                    if (l > TD) o += c[l];
+                }
+            });
+            lim[L] = L ? min((f + c[L]) << (15 - L), 65535u) : 0u;
+            pk[L] = ((o - f) & 0xffff) | (o << 16) | (o << 25);
+            cnt[L][lane] = (L <= TD ? f : o) << 9;
+        });
+        sfor<6>([&](auto k) {
+            constexpr int K = decltype(k)::value;
+            Slow[14 + K] = lim[5 + 2 * K] | (K < 5 ? lim[(6 + 2 * K) & 15] << 16 : 0u);
+            Slow[20 + K] = (pk[5 + 2 * K] & 0xffff) | (K < 5 ? pk[(6 + 2 * K) & 15] << 16 : 0u);
+        });
+        for (uint32_t i = 0; i < 16; ++i) sm[i][lane] = 0;
+        for (uint32_t s = 0; s < hd; ++s) {
+            const uint32_t L = len_of(288 + s);
+            if (!L) continue;
+            const uint32_t r = atomicAdd(&cnt[L][lane], 1u), rank = r & 511, inf = r >> 9;
+            if (L <= (uint32_t)TD) {
+                const uint32_t rev = __builtin_bitreverse32(inf + rank) >> (32 - L);
+                for (uint32_t k = 0; k < (1u << (TD - L)); ++k) sm[rev | (k << L)][lane] = (uint8_t)(s | (L << 5));
+            } else {
+                sm[48 + min(inf + rank, 29u)][lane] = (uint8_t)s;
+            }
+        }
+    }
+    // ---- the record: lt | dt ll dl | Slow
+    OGE_G uint32_t *R = (OGE_G uint32_t *)(prep + bi * kPrep);
+    for (uint32_t i = 0; i < 32; ++i) R[i] = (uint32_t)img[2 * i][lane] | ((uint32_t)img[2 * i + 1][lane] << 16);
+    for (uint32_t i = 0; i < 20; ++i)
+        R[32 + i] = (uint32_t)sm[4 * i][lane] | ((uint32_t)sm[4 * i + 1][lane] << 8) | (4 * i + 2 < 78 ? (uint32_t)sm[4 * i + 2][lane] << 16 : 0u) |
+                    (4 * i + 3 < 78 ? (uint32_t)sm[4 * i + 3][lane] << 24 : 0u);
+    sfor<26>([&](auto k) { R[P_SLOW / 4 + decltype(k)::value] = Slow[decltype(k)::value]; });
+    pmeta[bi] = 0x80000000u | 0x20000000u | ((h & 1) << 28) | used;
+}
+
 // ---------------------------------------------------------------------------- phase 1
 // An iteration (ST_SYM) decodes up to LB literals from the direct table, then one symbol of any kind (a
 // long-code literal, end of block, or a match with its length and distance codes), then up to LB direct
@@ -249,7 +549,8 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                                                       const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
                                                       uint8_t *__restrict__ out, uint64_t *__restrict__ bitmap,
                                                       uint8_t *__restrict__ xtab, uint8_t *__restrict__ scratch,
-                                                      uint32_t *__restrict__ err, unsigned long long *__restrict__ next) {
+                                                      uint32_t *__restrict__ err, unsigned long long *__restrict__ next,
+                                                      const uint8_t *__restrict__ prep, const uint32_t *__restrict__ pmeta) {
     static_assert(LB + 1 < 8, "a batch and the pending literal: fewer bytes than the 8-byte register (put_n shifts < 64)");
     static_assert(sizeof(P1Lds) <= 13312, "12 waves per CU");
     __shared__ P1Lds S;
@@ -565,18 +866,67 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 bi = (uint32_t)(b - b0);
                 bm = lm = 0;
                 bw = 0;
+                // the pre-pass's verdict: prepared (tables ready, the first symbol's bit offset) or not
+                const uint32_t pm = pmeta ? pmeta[bi] : 0u;
                 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-                *(OGE_G u32x4 *)(xtab + (uint64_t)bi * kXTab + kXStart) = u32x4{0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+                *(OGE_G u32x4 *)(xtab + (uint64_t)bi * kXTab + kXStart) =
+                    u32x4{(pm >> 29) & 1 ? 0u : 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
                 tabs = 0;
-                seek((uintptr_t)z + d0a[b]);
+                const uint32_t u = pm & 0xffffff;
+                seek((uintptr_t)z + d0a[b] + (u >> 3));
+                skip(u & 7);
                 under = 0;
-                st = ST_HDR;
+                flg = (pm >> 28) & 1;
+                st = (pm >> 31) ? ST_LOAD : ST_HDR;
             }
         }
 #if OGE_EXP == 3
         y_blk += (uint32_t)__popcll(__ballot(st == ST_HDR));
         y_nxt += __builtin_readcyclecounter() - y1;
 #endif
+        // ---- prepared first tables (k_infl_prep): lane j's record copied into its LDS column and Slow
+        // registers by the whole wave, one 8-byte load per lane; the next lane's record is loaded while
+        // this one is written
+        if (uint64_t ld = __ballot(st == ST_LOAD)) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            auto rec = [&](uint32_t j) {
+                const uint32_t bj = __builtin_amdgcn_readlane(bi, j);
+                const OGE_G u32x2 *R = (const OGE_G u32x2 *)(prep + (uint64_t)bj * kPrep);
+                return lane < kPrep / 8 ? R[lane] : u32x2{0u, 0u};
+            };
+            uint32_t j = (uint32_t)__builtin_ctzll(ld);
+            ld &= ld - 1;
+            u32x2 v = rec(j);
+            for (;;) {
+                const uint32_t jn = ld ? (uint32_t)__builtin_ctzll(ld) : j;
+                u32x2 vn = {0u, 0u};
+                if (ld) vn = rec(jn);
+                if (lane < 16) {
+                    S.lt[4 * lane][j] = (uint16_t)v.x, S.lt[4 * lane + 1][j] = (uint16_t)(v.x >> 16);
+                    S.lt[4 * lane + 2][j] = (uint16_t)v.y, S.lt[4 * lane + 3][j] = (uint16_t)(v.y >> 16);
+                } else if (lane < 26) {  // dt | ll | dl rows (contiguous in P1Lds): 8 per lane
+                    const uint32_t r0 = 8 * (lane - 16);
+                    uint8_t *row = &S.dt[0][0] + r0 * 64 + j;
+#pragma unroll
+                    for (uint32_t i = 0; i < 8; ++i)
+                        if (r0 + i < 16 + 32 + 30) row[i * 64] = (uint8_t)((i < 4 ? v.x : v.y) >> (8 * (i & 3)));
+                }
+                sfor<13>([&](auto k) {
+                    constexpr int K = decltype(k)::value;
+                    const uint32_t a = __builtin_amdgcn_readlane(v.x, P_SLOW / 8 + K), c = __builtin_amdgcn_readlane(v.y, P_SLOW / 8 + K);
+                    if (lane == j) {
+                        tset<2 * K>(T, a);
+                        tset<2 * K + 1>(T, c);
+                    }
+                });
+                if (lane == j) tabs = 3, st = ST_SYM;  // table 0, long literals deferred
+                if (!ld) break;
+                ld &= ld - 1;
+                j = jn;
+                v = vn;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
         if (__ballot(st != ST_DONE) == 0) {
 #if OGE_EXP == 3
             if (lane == 0 && blockIdx.x < 16)
@@ -1149,16 +1499,23 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     const uint64_t wgs = std::min<uint64_t>((chunk + 63) / 64, lanes / 64);
     struct Set {
         uint64_t *bitmap;
-        uint8_t *xtab, *scr;
+        uint8_t *xtab, *scr, *prep;
+        uint32_t *pmeta;
         unsigned long long *next;
         hipStream_t st;
     } B[S];
+    // OGE_INFL_PREP=0: no header pre-pass (phase 1 parses every header itself; the A/B switch)
+    const char *pe = getenv("OGE_INFL_PREP");
+    const bool use_prep = !(pe && *pe == '0');
     for (int k = 0; k < S; ++k) {
         const std::string x = std::to_string(k);
         B[k].bitmap = (uint64_t *)ctx->ws(("infl_bitmap" + x).c_str(), chunk * 2048 * 8);
         B[k].xtab = (uint8_t *)ctx->ws(("infl_xtab" + x).c_str(), chunk * kXTab);
         B[k].scr = (uint8_t *)ctx->ws(("infl_scratch" + x).c_str(), wgs * 64 * kScr);
         B[k].next = (unsigned long long *)ctx->ws(("infl_next" + x).c_str(), 8);
+        B[k].prep = use_prep ? (uint8_t *)ctx->ws(("infl_prep" + x).c_str(), chunk * kPrep) : nullptr;
+        B[k].pmeta = use_prep ? (uint32_t *)ctx->ws(("infl_pmeta" + x).c_str(), chunk * 4) : nullptr;
+        if (use_prep && (!B[k].prep || !B[k].pmeta)) return OGE_ERR_HIP;
         B[k].st = S == 1 ? ctx->stream : ctx->side_stream(k);
         if (!B[k].bitmap || !B[k].xtab || !B[k].scr || !B[k].next || !B[k].st) return OGE_ERR_HIP;
     }
@@ -1195,8 +1552,15 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
             ctx->infl_clean_next = known;
         }
         // each phase's own time (stages "infl_huff" / "infl_lz", summed over the chunks) on the one stream
+        if (use_prep) {
+            OgeStageTimer *t0 = S == 1 ? ctx->begin_stage("infl_prep") : nullptr;
+            k_infl_prep<<<(uint32_t)((nb + 63) / 64), 64, 0, u.st>>>(d_z, zbytes, d0, d1, b0, nb, u.prep, u.pmeta, u.xtab);
+            OGE_LAUNCH_CHECK(ctx);
+            ctx->end_stage(t0);
+        }
         OgeStageTimer *t1 = S == 1 ? ctx->begin_stage("infl_huff") : nullptr;
-        k_infl_huff<<<g1, 64, 0, u.st>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, u.bitmap, u.xtab, u.scr, err, u.next);
+        k_infl_huff<<<g1, 64, 0, u.st>>>(d_z, zbytes, d0, d1, uoff, b0, nb, out, u.bitmap, u.xtab, u.scr, err, u.next, u.prep,
+                                         u.pmeta);
         OGE_LAUNCH_CHECK(ctx);
         ctx->end_stage(t1);
         OgeStageTimer *t2 = S == 1 ? ctx->begin_stage("infl_lz") : nullptr;

@@ -157,6 +157,28 @@ def test_inflate_rejects_corruption(ctx):
 
 
 
+@pytest.mark.parametrize("prep", ["0", "1"])
+def test_inflate_header_prepass_on_and_off(ctx, monkeypatch, prep):
+    """The header pre-pass (k_infl_prep: first deflate header of every BGZF block parsed and its tables
+    built before phase 1) and phase 1's own in-loop header path (OGE_INFL_PREP=0, and whatever the pre-pass
+    declines: stored first blocks, > 256 long codes, corrupt headers) give the same bytes and errors."""
+    from openge_amd import lib as L
+    monkeypatch.setenv("OGE_INFL_PREP", prep)
+    for name in ("bam", "random", "text", "one"):
+        for level in (0, 1, 6, 9):
+            assert ctx.bgzf_inflate(bgzf(DATA[name], level)) == DATA[name]
+        assert ctx.bgzf_inflate(bgzf(DATA[name], 6, zlib.Z_FIXED)) == DATA[name]
+    z = bytearray(bgzf(DATA["bam"], 6))
+    z[18] ^= 0x06  # the first block's BTYPE bits: dynamic -> fixed (decodes garbage: an error)
+    with pytest.raises(L.OgeError):
+        ctx.bgzf_inflate(bytes(z))
+    z = bytearray(bgzf(DATA["bam"], 6))
+    for k in range(21, 40):  # inside the first header's code-length data
+        z[k] ^= 0xA5
+    with pytest.raises(L.OgeError):
+        ctx.bgzf_inflate(bytes(z))
+
+
 def test_inflate_carry_over_on_one_context(ctx):
     """One context, calls in sequence: a corrupt stream (phase 1 fails some blocks, so phase 2 may not clear
     every bitmap word it would), then a valid stream, then a smaller one, then a larger one -- each checked

@@ -31,10 +31,28 @@ L.check(L.lib().oge_bgzf_index(zh.ctypes.data, zb, i0, i0 + 8 * k, i0 + 16 * k, 
 d_idx = torch.from_numpy(idx.view(np.int64)).to(dev); d_crc = torch.from_numpy(crc.view(np.int32)).to(dev)
 d_back = torch.zeros(B + 64, dtype=torch.uint8, device=dev)
 torch.cuda.synchronize()
+ab = os.environ.get("DIAG_AB")  # NAME: alternate NAME=0 / NAME=1 call by call in this process (A/B on one box)
+if ab:
+    res = {"0": [], "1": []}
+    stg = {"0": [], "1": []}
+    for it in range(12):
+        v = "01"[it % 2]
+        os.environ[ab] = v
+        p0 = d_idx.data_ptr()
+        rc = L.lib().oge_bgzf_inflate_dev(ctx.h, d_z.data_ptr(), zb, p0, p0 + 8 * k, p0 + 16 * k, d_crc.data_ptr(), k, d_back.data_ptr())
+        if it >= 2:
+            res[v].append(round(ctx.timing("bgzf_inflate"), 2))
+            stg[v].append({x: round(ctx.timing(x), 2) for x in ("infl_prep", "infl_huff", "infl_lz")})
+    same = bool(torch.equal(d_back[:B], d_recs[:B]))
+    for v in "01":
+        print(f"{ab}={v} reads {reads} blocks {k} inflate ms {res[v]} median {sorted(res[v])[len(res[v]) // 2]} stages {stg[v][-1]}", flush=True)
+    print("rc", rc, "same", same, flush=True)
+    sys.exit(0)
 ms = []
 for _ in range(4):
     p0 = d_idx.data_ptr()
     rc = L.lib().oge_bgzf_inflate_dev(ctx.h, d_z.data_ptr(), zb, p0, p0 + 8 * k, p0 + 16 * k, d_crc.data_ptr(), k, d_back.data_ptr())
     ms.append(round(ctx.timing("bgzf_inflate"), 2))
+    st = {k: round(ctx.timing(k), 2) for k in ("infl_prep", "infl_huff", "infl_lz")}
 same = bool(torch.equal(d_back[:B], d_recs[:B]))
-print(sys.argv[1:] or ["default"], "reads", reads, "blocks", k, "inflate ms", ms[1:], "rc", rc, "same", same, flush=True)
+print(sys.argv[1:] or ["default"], "reads", reads, "blocks", k, "inflate ms", ms[1:], "rc", rc, "same", same, "stages", st, flush=True)
