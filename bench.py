@@ -59,9 +59,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measur
 VALU_INT32_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 KERNEL_STAGES = ["input_pass", "sort_radix", "sort_ties", "meta_gather", "md_matejoin", "md_pairs", "md_frags",
                  "md_apply", "gather_offsets", "gather_records"]
+DEDUP_STAGES = ["md_readends", "md_matejoin", "md_pairs", "md_frags", "md_apply"]
 SUB_STAGES = ["md_pair_win", "md_frag_win", "md_pair_ovf", "md_frag_ovf"]  # nested in md_pairs / md_frags: which group path ran
 E2E_STAGES = ["bgzf_index", "bgzf_inflate", "rec_walk"] + KERNEL_STAGES + ["bgzf_deflate"]
-INFL_PHASES = ["infl_huff", "infl_lz"]  # nested in bgzf_inflate: its two kernels' own times
+INFL_PHASES = ["infl_prep", "infl_huff", "infl_lz"]  # nested in bgzf_inflate: its two kernels' own times
 
 
 def parse():
@@ -269,8 +270,15 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1, cpu_thread
         cli = None
         if world == 1:
             cli = realign_cli_leg(fa, iv, bam, td)
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            dist.barrier()
+        # the headline: the FIRST call in this process -- the realigner's cross-call
+        # scratch (worker pool, record objects, event list, FASTA buffers) is built inside it, as in a fresh
+        # `openge localrealign`; the second call (warm scratch) is reported beside it
         t0c = time.perf_counter()
-        w_out, w_oo, first_st = run()  # first call in this process (the cross-call scratch is built here)
+        w_out, w_oo, first_st = run()
         first_call_s = time.perf_counter() - t0c
         if dump_dir:  # this rank's realigned records (tests concatenate the ranks' parts)
             Path(dump_dir, f"realign_{rank}.bin").write_bytes(np.asarray(w_out[:int(w_oo[-1])]).tobytes())
@@ -278,21 +286,20 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1, cpu_thread
         if world == 1 and cpu_threads:  # the reference's own realigner on the same files, this box's host
             ref_cpu = cpu_baseline_realign(fa, iv, bam, n_intervals, cpu_threads, td)
         if world > 1:
-            import torch
-            import torch.distributed as dist
             dist.barrier()
         t0 = time.perf_counter()
         out, oo, st = run()
         dt = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([dt], dtype=torch.float64)
+            t = torch.tensor([dt, first_call_s], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
+            dt, first_call_s = float(t[0].item()), float(t[1].item())
             if rank != 0:
                 return None
-            return {"metric": "realign intervals/sec", "value": round(n_intervals / dt, 1), "unit": "intervals/s",
+            return {"metric": "realign intervals/sec", "value": round(n_intervals / first_call_s, 1), "unit": "intervals/s",
                     "workload": f"C5: {n_intervals} indel intervals, 24 contigs, {b.n} reads (seed 1234)",
-                    "seconds": round(dt, 3), "n_gpus": world, "scaling": "strong",
+                    "seconds": round(first_call_s, 3), "warm_seconds": round(dt, 3),
+                    "warm_value": round(n_intervals / dt, 1), "n_gpus": world, "scaling": "strong",
                     "parallelism": f"{world} ranks, contig-range shards, no exchange", "host_threads_per_rank": 16,
                     "rank0_reads": hi - lo, "rank0_stats": st}
     # VALU lane-ops per launch from the committed PMC pass (SQ_INSTS_VALU x 64; the instruction count
@@ -304,12 +311,13 @@ def realign_leg(ctx, n_intervals: int, rank: int = 0, world: int = 1, cpu_thread
     # frac: SURVEY §8(d)'s algorithmic ops (#offsets x read length compare-accumulates per consensus x
     # altRead pair) per second over the int32 VALU peak; the bit-parallel kernel's own lane-ops (PMC) as a
     # secondary figure
-    return {"metric": "realign intervals/sec", "value": round(n_intervals / dt, 1), "unit": "intervals/s",
+    return {"metric": "realign intervals/sec", "value": round(n_intervals / first_call_s, 1), "unit": "intervals/s",
             "workload": f"C5: {n_intervals} indel intervals, 24 contigs, {b.n} reads (seed 1234)",
-            "seconds": round(dt, 3), "host_threads": 16, "stats": st,
-            "timed_region": "the realigner on records already decoded in host memory, second call in the process "
-                            "(first_call_seconds: the first; cli: the whole command, file to file, fresh process)",
-            "first_call_seconds": round(first_call_s, 3), "first_call_stats": first_st, "cli": cli,
+            "seconds": round(first_call_s, 3), "host_threads": 16, "stats": first_st,
+            "timed_region": "the realigner on records already decoded in host memory, FIRST call in the process "
+                            "(its scratch built inside the timed region); warm_*: the second call; cli: the whole "
+                            "command, file to file, fresh process",
+            "warm_seconds": round(dt, 3), "warm_value": round(n_intervals / dt, 1), "warm_stats": st, "cli": cli,
             "roofline": {"kernel": "k_planes + k_scan_bp (findBestOffset over all consensus x altRead pairs, "
                                    "bit-parallel)",
                          "bound": "valu", "achieved": round(cmp_t, 2) if cmp_t else None,
@@ -453,6 +461,37 @@ def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, DevBuf, int,
                "gather_roofline": {"kernel": "k_gather16", "achieved_GBps": round(2 * B / tg / 1e9, 1) if tg else None,
                                    "frac": round(2 * B / tg / 1e9 / HBM_PEAK_GBS, 4) if tg else None,
                                    "algorithmic_bytes": 2 * B}}
+        # configs[2]: `openge dedup` on the sorted records -- oge_markdup_dev in place (record index = position in
+        # the file, 0x400 set / cleared in the records themselves) over the records the steps above sorted
+        # (their 0x400 bits are recomputed, not read).  The in-place path verifies the anchors never decrease
+        # and then takes the windowed mate join and groups (markdup.hip oge_markdup_run).
+        # (a context of its own, closed after the leg: without the fused chain's arena loan its workspaces are
+        # ~17 GB that would otherwise stay allocated and shrink the e2e inflate's chunks)
+        dctx = L.Context(torch.cuda.current_device(), stream=ctx.stream)
+        d_dup = torch.empty(n + 1, dtype=torch.uint8, device=dev)
+        md = lambda: dctx.markdup_dev(d_out.ptr, d_out_off.data_ptr(), n, opts, d_dup.data_ptr(), apply=True)
+        md()
+        torch.cuda.synchronize(dev)
+        tot2 = {s: 0.0 for s in DEDUP_STAGES + SUB_STAGES}
+        t0 = time.perf_counter()
+        for _ in range(args.kernel_steps):
+            nd2 = md()
+            for s, v in stage_ms(dctx, DEDUP_STAGES + SUB_STAGES).items():
+                tot2[s] += v
+        torch.cuda.synchronize(dev)
+        dt2 = (time.perf_counter() - t0) / args.kernel_steps
+        sms2 = {s: round(v / K, 3) for s, v in tot2.items()}
+        # dedup's algorithmic bytes = B - sum ceil(l_seq / 2) + 2 N (every record read once
+        # except its packed bases, plus the flag write-back)
+        dbytes = B - n * ((p.read_len + 1) // 2) + 2 * n
+        res["dedup_inplace"] = {
+            "what": "configs[2]: openge dedup's device path, oge_markdup_dev in place over the sorted records in HBM",
+            "ms_per_step": round(dt2 * 1e3, 2), "mreads_per_s": round(n / dt2 / 1e6, 1), "steps": K,
+            "duplicates_flagged": nd2, "equals_fused_chain": nd2 == nd,
+            "windowed_paths": bool(dctx.counter("md_inplace_window")), "stages_ms": sms2,
+            "algorithmic_bytes": dbytes, "hbm_frac_step": round(dbytes / dt2 / 1e9 / HBM_PEAK_GBS, 4)}
+        dctx.close()
+        del d_dup
         d_out.free()
         del d_out_off, d_perm
     del d_offs

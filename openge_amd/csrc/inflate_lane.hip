@@ -1490,7 +1490,7 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     const uint64_t lanes = (uint64_t)ncu * 4 * kWps * 64;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
-    constexpr uint64_t kPerBlk = 2048 * 8 + kXTab;  // bitmaps + translation lists
+    constexpr uint64_t kPerBlk = 2048 * 8 + kXTab + kPrep + 4;  // bitmaps + translation lists + prepared tables
     constexpr int S = kStreams;
     const uint64_t budget =
         std::max<uint64_t>(lanes, std::min<uint64_t>(kChunkLanes * lanes, (uint64_t)(fr / 4) / (S * kPerBlk)));

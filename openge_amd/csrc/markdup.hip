@@ -1532,13 +1532,41 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     return OGE_OK;
 }
 
-// Standalone duplicate marking of records in stream order (record index = position).
+namespace {
+// bad[2] |= 1 when some record's anchor (refID', pos + 1) is smaller than its predecessor's
+__global__ __launch_bounds__(kT) void k_anchors_sorted(const uint64_t *__restrict__ keys, uint64_t n, unsigned int *__restrict__ bad) {
+    bool down = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x + 1; i < n; i += (uint64_t)gridDim.x * kT)
+        down |= anchor_of_key(keys[i]) < anchor_of_key(keys[i - 1]);
+    if (__ballot(down) && (threadIdx.x & 63) == __builtin_ctzll(__ballot(down))) atomicOr(bad + 2, 1u);
+}
+}  // namespace
+
+// Standalone duplicate marking of records in stream order (record index = position): `openge dedup`
+// (commands/command_dedup.cpp:48-69 -> MarkDuplicates over the file's records as they come).
+// r06: the input pass also writes each record's coordinate key, and when the keys'
+// anchors (refID', pos + 1) never decrease -- a coordinate-sorted file, which is what `openge dedup` is
+// run on -- the keys go to the windowed mate join and groups exactly as in the fused chain (whose exactness
+// needs only that the record index order has non-decreasing anchors, not the sort itself).  Anything else
+// (unsorted input, refIDs outside the dictionary, OGE_MD_INPLACE_WINDOW=0) keeps the sort-based paths.
 int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
                     uint8_t *d_dup, int apply, uint64_t *n_dup_out) {
     RecMeta *meta;
     OgeRgTable rg;
     int rc = oge_markdup_prepare(ctx, opts, n, "md_meta", &meta, &rg);
     if (rc) return rc;
+    const char *we = getenv("OGE_MD_INPLACE_WINDOW");
+    const bool try_win = n > 1 && n < (1ull << 31) && !(we && we[0] == '0');
+    uint64_t *keys = nullptr;
+    uint32_t *vals = nullptr;
+    unsigned int *bad = nullptr;
+    if (try_win) {
+        keys = (uint64_t *)ctx->scratch("mdi_keys", (n + 1) * 8);
+        vals = (uint32_t *)ctx->scratch("mdi_vals", (n + 1) * 4);
+        bad = (unsigned int *)ctx->ws("mdi_bad", 16);
+        if (!keys || !vals || !bad) return OGE_ERR_HIP;
+        OGE_HIP_TRY(ctx, hipMemsetAsync(bad, 0, 16, ctx->stream));
+    }
     OgeStageTimer *t = ctx->begin_stage("md_readends");
     OgePassArgs a = {};
     a.recs = d_recs;
@@ -1546,10 +1574,26 @@ int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64
     a.n = n;
     a.meta = meta;
     a.rg = rg;
+    a.keys = keys;
+    a.vals = vals;
+    a.n_ref = opts->n_ref;
+    a.bad = bad;
     rc = oge_input_pass(ctx, a);
     if (rc) return rc;
+    const uint64_t *skeys = nullptr;
+    if (try_win) {
+        hipLaunchKernelGGL(k_anchors_sorted, dim3((uint32_t)std::min<uint64_t>(oge_ceil_div(n, kT), 4096)), dim3(kT), 0, ctx->stream,
+                           (const uint64_t *)keys, n, bad);
+        OGE_LAUNCH_CHECK(ctx);
+        unsigned int hb[3] = {0, 0, 0};
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(hb, bad, 12, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        const bool sorted = !(hb[0] & 1) && !hb[2];
+        ctx->counters["md_inplace_window"] = sorted;
+        if (sorted) skeys = keys;
+    }
     ctx->end_stage(t);
-    return oge_markdup_finish(ctx, d_recs, d_off, n, opts, meta, d_dup, apply, n_dup_out, nullptr, nullptr, nullptr);
+    return oge_markdup_finish(ctx, d_recs, d_off, n, opts, meta, d_dup, apply, n_dup_out, nullptr, nullptr, skeys);
 }
 
 namespace {

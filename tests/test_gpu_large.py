@@ -199,7 +199,20 @@ def test_300m_read_properties():
         assert bool(primary.all())
         bad = int((want != got).sum().item())
         assert bad == 0, f"{bad} of {n} records carry a 0x400 bit the restated MarkDuplicates does not give"
-        del d_out, d_out_off, d_perm, off, got, want, primary
+        del got
+        # configs[2]: `openge dedup`'s in-place device path on the sorted 300M records --
+        # it verifies the anchors never decrease and takes the windowed mate join and groups -- must give every
+        # record the same bit (their 0x400 bits are recomputed, not read)
+        d_dup = torch.empty(n + 1, dtype=torch.uint8, device="cuda")
+        nd2 = ctx.markdup_dev(d_out.data_ptr(), d_out_off.data_ptr(), n, opts, d_dup.data_ptr(), apply=True)
+        ctx.sync()
+        assert ctx.counter("md_inplace_window") == 1
+        assert nd2 == nd
+        del d_dup
+        got2 = ((d_out[off + 19] >> 2) & 1).bool()
+        bad2 = int((want != got2).sum().item())
+        assert bad2 == 0, f"in-place dedup: {bad2} of {n} records differ from the restated MarkDuplicates"
+        del d_out, d_out_off, d_perm, off, got2, want, primary
     finally:
         ctx.close()
         # the next test's library allocations need the HBM torch's caching allocator holds for these tensors

@@ -74,3 +74,65 @@ def test_window_join_c2_counts(ctx, monkeypatch):
     n = len(offs) - 1
     # inter-contig pairs (1%) and pairs with an unmapped mate are the leftovers; most pairs are windowed
     assert c["md_mate_left"] < 0.05 * n and c["md_mate_pairs"] > 0.4 * n
+
+
+def _offsets(buf: np.ndarray, n: int) -> np.ndarray:
+    """record start offsets (n + 1) of a packed record stream, by its block_size fields"""
+    offs = np.empty(n + 1, dtype=np.uint64)
+    o, b = 0, buf.tobytes()
+    for i in range(n):
+        offs[i] = o
+        o += 4 + int.from_bytes(b[o:o + 4], "little")
+    offs[n] = o
+    return offs
+
+
+def _inplace(ctx, recs, offs, n, opts):
+    """oge_markdup_dev in place (`openge dedup`: record index = input position) -> (nd, dup bytes, records
+    after apply, whether the windowed paths ran)."""
+    d_recs = torch.from_numpy(recs.copy()).cuda()
+    d_offs = torch.from_numpy(offs[:n + 1].astype(np.int64)).cuda()
+    d_dup = torch.empty(n + 1, dtype=torch.uint8, device="cuda")
+    nd = ctx.markdup_dev(d_recs.data_ptr(), d_offs.data_ptr(), n, opts, d_dup.data_ptr(), apply=True)
+    ctx.sync()
+    return nd, d_dup[:n].cpu().numpy(), d_recs.cpu().numpy().tobytes(), ctx.counter("md_inplace_window")
+
+
+@pytest.mark.parametrize("preset,pairs,kw", [("c2", 300_000, {}), ("mix", 40_000, {}),
+                                             ("c2", 200_000, {"ins_max": 3000, "n_ref": 1, "ref_len": [2_000_000]})])
+def test_inplace_dedup_window_on_sorted_input(ctx, monkeypatch, preset, pairs, kw):
+    """`openge dedup` on a coordinate-sorted file: the in-place path verifies the input's
+    anchors never decrease and then takes the windowed mate join and groups -- the same marks and records as
+    its sort-based paths (OGE_MD_INPLACE_WINDOW=0), as the fused chain's marks, and as the oracle."""
+    p = L.synth_params(pairs, preset=preset, seed=2468, **kw)
+    recs, offs, hdr = L.synth_host(p, threads=8)
+    n = len(offs) - 1
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    nd_f, sorted_bytes, _ = _fused(ctx, recs, offs, n, opts)  # sorted records, 0x400 already applied
+    srecs = np.frombuffer(sorted_bytes, np.uint8).copy()
+    soffs = _offsets(srecs, n)
+    nd1, dup1, out1, win = _inplace(ctx, srecs, soffs, n, opts)
+    assert win == 1
+    monkeypatch.setenv("OGE_MD_INPLACE_WINDOW", "0")
+    nd0, dup0, out0, win0 = _inplace(ctx, srecs, soffs, n, opts)
+    monkeypatch.delenv("OGE_MD_INPLACE_WINDOW")
+    assert not win0
+    assert nd1 == nd0 == nd_f and np.array_equal(dup1, dup0) and out1 == out0
+    assert out1 == sorted_bytes  # apply on the fused output reproduces its own 0x400 bits
+    odup, ond = oracle.markdup(srecs, soffs[:-1], n, hdr)
+    sure = odup != 2
+    assert np.array_equal(dup1[sure].astype(bool), odup[sure].astype(bool)) and nd1 == ond
+
+
+def test_inplace_dedup_unsorted_input_keeps_sort_paths(ctx):
+    """Input order (not coordinate-sorted): the anchor check fails, the sort-based paths run, and the marks
+    equal the oracle's."""
+    p = L.synth_params(30_000, preset="mix", seed=99)
+    recs, offs, hdr = L.synth_host(p)
+    n = len(offs) - 1
+    opts, keep = L.markdup_opts_from_header(hdr, p.n_ref)
+    nd, dup, _, win = _inplace(ctx, recs, offs, n, opts)
+    assert win == 0
+    odup, ond = oracle.markdup(recs, offs[:-1], n, hdr)
+    sure = odup != 2
+    assert np.array_equal(dup[sure].astype(bool), odup[sure].astype(bool)) and nd == ond
