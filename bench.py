@@ -735,15 +735,18 @@ def exchange_summary(per_rank: list) -> dict:
     for r in per_rank:
         for x in r["exchanges"]:
             t = tags.setdefault(x["tag"], {"calls": x["calls"], "bytes_between_ranks": 0, "bytes_kept": 0, "max_ms": 0.0,
-                                           "mode": x.get("mode", "blocking")})
+                                           "max_device_ms": 0.0, "mode": x.get("mode", "blocking")})
             t["bytes_between_ranks"] += x["bytes_sent"]
             t["bytes_kept"] += x["bytes_self"]
             t["max_ms"] = round(max(t["max_ms"], x["ms"]), 3)
+            t["max_device_ms"] = round(max(t["max_device_ms"], x.get("device_ms", 0.0)), 3)
     return {"by_tag": tags, "per_rank": [r["exchanges"] for r in per_rank],
             "what": "last timed step; bytes_between_ranks = sum over ranks of bytes sent to other ranks; "
                     "ms = host wall time of the tag's collectives on a rank (peers' skew included); mode side_stream = "
                     "the peers' parts moved on a side stream while the rank's own records went through the input "
-                    "pass (RCCL: ms is the time to queue them)"}
+                    "pass (RCCL: ms is the time to queue them); device_ms (RCCL only) = the collectives' own time on their "
+                    "stream from HIP events around them (RCCL calls are stream-ordered and not waited for), peers' skew "
+                    "included"}
 
 
 def multi_gpu(args, ctx, L, torch, dist, dev, p, n_all, world, rank):

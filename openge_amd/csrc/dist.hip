@@ -59,7 +59,8 @@ struct OgeTransport {
     int rank = 0, size = 1;
     virtual ~OgeTransport() {}
     virtual const char *name() const = 0;
-    // device buffers, stream-ordered on ctx->stream and complete on return
+    // device buffers, stream-ordered on ctx->stream: complete on return (host-driven transports) or queued on
+    // it (RCCL, r06) -- callers consume the results on ctx->stream or after synchronizing it
     virtual int alltoallv(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
                           const uint64_t *rbytes, const uint64_t *roff) = 0;
     virtual int allgather_host(oge_ctx *ctx, const void *in, void *out, size_t bytes) = 0;
@@ -84,6 +85,7 @@ struct OgeXchg {
     std::string tag;
     uint64_t sent = 0, recv = 0, self = 0, calls = 0;
     double ms = 0;
+    double dev_ms = 0;  // RCCL: the collectives' own time on their stream (HIP events; waiting for peers included)
     // "blocking": ms covers the data movement; "side_stream": the peers' parts moved on a side stream beside
     // the caller's own work (host transport: ms covers the staged copies, which ran beside it; RCCL: ms is
     // the time to queue them)
@@ -94,6 +96,55 @@ struct oge_comm {
     oge_ctx *ctx = nullptr;
     std::unique_ptr<OgeTransport> tr;
     std::vector<OgeXchg> stats;  // since the last oge_sort_markdup_dist / oge_mergesort_bgzf_dist call
+    // RCCL collectives are stream-ordered and not waited for (r06): their time per tag comes
+    // from event pairs around them, read when the stats are (stats index, start, stop)
+    struct Ev {
+        size_t i;
+        hipEvent_t a, b;
+    };
+    mutable std::vector<Ev> pend;
+    ~oge_comm() { drop_events(); }
+    bool rccl() const { return tr && strcmp(tr->name(), "rccl") == 0; }
+    void drop_events() const {
+        for (auto &e : pend) (void)hipEventDestroy(e.a), (void)hipEventDestroy(e.b);
+        pend.clear();
+    }
+    void settle_events() const {  // the pending pairs' times into their stats (waits for the collectives)
+        for (auto &e : pend) {
+            float t = 0;
+            if (hipEventSynchronize(e.b) == hipSuccess && hipEventElapsedTime(&t, e.a, e.b) == hipSuccess && e.i < stats.size())
+                const_cast<OgeXchg &>(stats[e.i]).dev_ms += t;
+        }
+        drop_events();
+    }
+    void clear_stats() {
+        drop_events();
+        stats.clear();
+    }
+    // an event pair around a collective queued on `st` (RCCL only; null otherwise)
+    struct Bracket {
+        const oge_comm *c;
+        hipStream_t st;
+        hipEvent_t a = nullptr, b = nullptr;
+        Bracket(const oge_comm *c_, hipStream_t s) : c(c_), st(s) {
+            if (!c->rccl()) return;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess || hipEventRecord(a, st) != hipSuccess) {
+                if (a) (void)hipEventDestroy(a);
+                if (b) (void)hipEventDestroy(b);
+                a = b = nullptr;
+            }
+        }
+        void done(size_t i) {
+            if (!a) return;
+            if (hipEventRecord(b, st) == hipSuccess) c->pend.push_back({i, a, b});
+            else (void)hipEventDestroy(a), (void)hipEventDestroy(b);
+            a = b = nullptr;
+        }
+        ~Bracket() {
+            if (a) (void)hipEventDestroy(a), (void)hipEventDestroy(b);
+        }
+    };
+    size_t stat_index(const OgeXchg &x) const { return (size_t)(&x - stats.data()); }
     OgeXchg &stat(const char *tag) {
         for (auto &x : stats)
             if (x.tag == tag) return x;
@@ -105,8 +156,10 @@ struct oge_comm {
     int alltoallv(const char *tag, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
                   const uint64_t *rbytes, const uint64_t *roff) {
         const auto t0 = std::chrono::steady_clock::now();
+        Bracket br(this, ctx->stream);
         const int rc = tr->alltoallv(ctx, send, sbytes, soff, recv, rbytes, roff);
         OgeXchg &x = stat(tag);
+        br.done(stat_index(x));
         x.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         x.calls++;
         for (int p = 0; p < tr->size; ++p) {
@@ -125,8 +178,10 @@ struct oge_comm {
         std::vector<uint64_t> sb(sbytes, sbytes + tr->size), rb(rbytes, rbytes + tr->size);
         sb[tr->rank] = rb[tr->rank] = 0;
         const auto t0 = std::chrono::steady_clock::now();
+        Bracket br(this, st);
         const int rc = tr->alltoallv_peers(ctx, send, sb.data(), soff, recv, rb.data(), roff, st);
         OgeXchg &x = stat(tag);
+        br.done(stat_index(x));
         x.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         x.calls++;
         x.mode = tr->overlaps() ? "side_stream" : "blocking";
@@ -147,8 +202,10 @@ struct oge_comm {
     }
     int reduce_scatter_max_u8(const char *tag, const uint8_t *in, uint8_t *out, size_t chunk) {
         const auto t0 = std::chrono::steady_clock::now();
+        Bracket br(this, ctx->stream);
         const int rc = tr->reduce_scatter_max_u8(ctx, in, out, chunk);
         OgeXchg &x = stat(tag);
+        br.done(stat_index(x));
         x.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         x.calls++;
         x.sent += chunk * (tr->size - 1);
@@ -276,7 +333,8 @@ struct RcclTransport : OgeTransport {
             if (rbytes[p]) OGE_NCCL_TRY(ctx, ncclRecv((uint8_t *)recv + roff[p], rbytes[p], ncclUint8, p, comm, ctx->stream));
         }
         OGE_NCCL_TRY(ctx, ncclGroupEnd());
-        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        // stream-ordered, not waited for (r06): every consumer of `recv` is queued on ctx->stream after it, and
+        // anything the host reads goes through a copy + synchronize on that stream
         return OGE_OK;
     }
     int alltoallv_peers(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv,
@@ -302,8 +360,7 @@ struct RcclTransport : OgeTransport {
     }
     int reduce_scatter_max_u8(oge_ctx *ctx, const uint8_t *in, uint8_t *out, size_t chunk) override {
         if (chunk) OGE_NCCL_TRY(ctx, ncclReduceScatter(in, out, chunk, ncclUint8, ncclMax, comm, ctx->stream));
-        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        return OGE_OK;
+        return OGE_OK;  // stream-ordered (see alltoallv)
     }
 };
 
@@ -991,7 +1048,7 @@ int oge_comm_alltoallv_dev(oge_comm *comm, const char *tag, const void *send, co
     return comm->alltoallv(tag, send, sbytes, soff, recv, rbytes, roff);
 }
 
-void oge_comm_reset_stats(oge_comm *comm) { comm->stats.clear(); }
+void oge_comm_reset_stats(oge_comm *comm) { comm->clear_stats(); }
 
 // ---------------------------------------------------------------------------------------------- ABI
 extern "C" {
@@ -1148,15 +1205,16 @@ const char *oge_comm_transport(const oge_comm *c) { return c ? c->tr->name() : "
 
 int64_t oge_comm_stats_json(const oge_comm *c, char *buf, uint64_t cap) {
     if (!c) return -1;
+    c->settle_events();
     std::string j = "[";
-    char tmp[384];
+    char tmp[448];
     for (size_t i = 0; i < c->stats.size(); ++i) {
         const OgeXchg &x = c->stats[i];
         snprintf(tmp, sizeof tmp,
                  "%s{\"tag\":\"%s\",\"calls\":%llu,\"bytes_sent\":%llu,\"bytes_recv\":%llu,\"bytes_self\":%llu,\"ms\":%.3f,"
-                 "\"mode\":\"%s\"}",
+                 "\"device_ms\":%.3f,\"mode\":\"%s\"}",
                  i ? "," : "", x.tag.c_str(), (unsigned long long)x.calls, (unsigned long long)x.sent, (unsigned long long)x.recv,
-                 (unsigned long long)x.self, x.ms, x.mode);
+                 (unsigned long long)x.self, x.ms, x.dev_ms, x.mode);
         j += tmp;
     }
     j += "]";
@@ -1172,7 +1230,7 @@ int oge_sort_markdup_dist(oge_comm *comm, const uint8_t *d_recs, const uint64_t 
     oge_ctx *ctx = comm->ctx;
     (void)hipSetDevice(ctx->device);
     ctx->reset_timing();
-    if (!ctx->timing_hold) comm->stats.clear();  // a composite entry point (pipeline.hip) keeps its earlier exchanges
+    if (!ctx->timing_hold) comm->clear_stats();  // a composite entry point (pipeline.hip) keeps its earlier exchanges
     if (opts && opts->n_ref != n_ref) return oge_fail(ctx, OGE_ERR_ARG, "oge_sort_markdup_dist: opts->n_ref differs from n_ref");
     return dist_run(comm, d_recs, d_off, n, n_ref, sort, opts, d_out, d_out_off, n_out, n_dup_total);
 }

@@ -429,4 +429,6 @@ def test_rccl_transport_world1_blocking_records(ctx, monkeypatch):
     assert got.tobytes() == want and nd == wd
     rec = ex["records"]
     assert rec["calls"] >= 1 and rec["mode"] == "blocking" and rec["bytes_self"] > 0
+    # r06: RCCL collectives are stream-ordered and not waited for; their time comes from HIP events around them
+    assert rec["device_ms"] > 0 and ex["dup_marks"]["device_ms"] > 0
     print("records exchange over RCCL at world 1:", rec)
