@@ -93,10 +93,16 @@ public:
     // sharing one IPC namespace) -- its heartbeat has not moved for OGE_COMM_STALE_S seconds.  The wall-clock
     // limit (OGE_COMM_TIMEOUT, default 1800 s) is only the backstop for a live peer that never arrives, so
     // a slow rank (a larger input, a GPU under contention) does not break the communicator.
-    static double stale_beat_s() {  // OGE_COMM_STALE_S (default 20)
+    // Trade-off: the heartbeat thread of a LIVE peer that is frozen or starved of CPU (SIGSTOP, a
+    // frozen cgroup, a checkpoint) stops moving too, and once it has been still for the stale limit the
+    // communicator breaks for good, exactly as if the peer had died.  So the limit is a large fraction of the
+    // timeout rather than a fixed few seconds: by default a quarter of OGE_COMM_TIMEOUT, at least 60 s (450 s
+    // with the default timeout; a heartbeat moves every 100 ms), and OGE_COMM_STALE_S overrides it.  Only
+    // peers in another pid namespace are judged this way; a peer in this one is judged by its pid alone.
+    static double stale_beat_s() {
         const char *e = getenv("OGE_COMM_STALE_S");
-        const double t = e && *e ? atof(e) : 20.0;
-        return t > 0 ? t : 20.0;
+        const double t = e && *e ? atof(e) : 0.0;
+        return t > 0 ? t : std::max(60.0, timeout_s() / 4);
     }
     static uint64_t pid_namespace() {
         struct stat st;

@@ -558,8 +558,14 @@ int FileReader::runInternal(ChainContext &cc, ReadBatch &b) {
     if (files_.empty()) files_.push_back("stdin");
     std::vector<uint64_t> file_end;  // record count after each file
     const char *rd = getenv("OGE_READER");
-    if (cc.gpus > 1 && files_.size() == 1 && files_[0] != "stdin" && files_[0] != "-" && sink_takes_shards() &&
-        !(rd && (std::string(rd) == "host" || std::string(rd) == "whole"))) {
+    // the byte-range sharded reader by default only over the host-staged transport, where every multi-rank
+    // test ran; over RCCL (an 8-GPU node) it is opt-in (OGE_READER=sharded) until a G > 1 RCCL run of it has
+    // been recorded: its rank joins and tail fetch are collectives that a fall-back cannot undo
+    const bool want_shards = cc.gpus > 1 && files_.size() == 1 && files_[0] != "stdin" && files_[0] != "-" && sink_takes_shards() &&
+                             !(rd && (std::string(rd) == "host" || std::string(rd) == "whole"));
+    if (want_shards && cc.init_ranks()) return -1;  // the ranks (and so the transport) are needed here anyway
+    const bool rccl = !cc.comms.empty() && cc.comms[0] && std::string(oge_comm_transport(cc.comms[0])) == "rccl";
+    if (want_shards && (!rccl || (rd && std::string(rd) == "sharded"))) {
         const int r = read_sharded(cc, b, files_[0]);
         if (r <= 0) return r;  // 1: the host reader reports why the file cannot be read
     }
