@@ -22,7 +22,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 ARCH = "gfx950"
 
-HIP_SRCS = ["prims.hip", "sort.hip", "records.hip", "markdup.hip", "capi_dev.hip", "realign.hip", "bgzf.hip", "inflate.hip", "inflate_lane.hip", "filter.hip", "sort_name.hip", "pipeline.hip", "dist.hip", "shard.hip", "chunked.hip"]
+HIP_SRCS = ["prims.hip", "sort.hip", "records.hip", "markdup.hip", "capi_dev.hip", "realign.hip", "realign_prep.hip", "bgzf.hip", "inflate.hip", "inflate_lane.hip", "filter.hip", "sort_name.hip", "pipeline.hip", "dist.hip", "shard.hip", "chunked.hip"]
 HOST_SRCS = ["bamio.cpp", "host_capi.cpp", "realign.cpp", "realign_synth.cpp"]
 CLI_SRCS = ["openge_cli.cpp", "modules.cpp"]
 

@@ -1332,6 +1332,8 @@ struct Scratch {
     ScanBatch B;
     std::vector<int32_t> bidx, bscore;
     std::vector<RRead *> order;
+    DevPrepBatch DB;  // phase B on the device: its input and results
+    DevPrepOut DO;
     Fasta fa;
     ~Scratch() {
         for (uint64_t i = 0; i < rlive; ++i) rmem[i].~RRead();
@@ -1381,10 +1383,22 @@ struct Busy {
 
 int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, const uint64_t *offs, uint64_t n,
                 const std::string &fasta_path, const std::string &intervals_path, const RealignParams &P, const ScanFn &scan,
-                ByteBuf &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err) {
+                ByteBuf &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err, const DevPrep *dev) {
     double t0 = now_s();
     ScratchLease lease(P.threads);
     Scratch &S = *lease.s;
+    // phase B on the device: the record arena goes up now, beside the FASTA load, decode and binning
+    uint64_t span_lo = 0;
+    if (dev && n) {
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (uint64_t i = 0; i < n; ++i) lo = std::min(lo, offs[i]), hi = std::max(hi, offs[i]);
+        hi += 4 + rd32(recs + hi);
+        span_lo = lo;
+        if (dev->stage(recs, lo, hi)) {
+            err = "device consensus generation: staging the records failed";
+            return -1;
+        }
+    }
     Pool &pool = *S.pool;
     st.more.emplace_back("t_pool", now_s() - t0);
     Fasta &fa = S.fa;
@@ -1545,21 +1559,14 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     work.clear();
     for (auto &e : ev)
         if (e.t == EV_CLEAN && !e.id->toClean.empty()) work.push_back(e.id);
+    const size_t nw = work.size();
     std::atomic<bool> ferr(false);
     std::string fmsg;
-    Busy bprep(pool.size());
-    pool.run(work.size(), [&](size_t w) {  // (dynamic: intervals differ in size)
-        const double tb = now_s();
-        struct Acc {
-            Busy &b;
-            size_t w;
-            double t;
-            ~Acc() { b.add(w, now_s() - t); }
-        } acc{bprep, w, tb};
+    // B.1 every interval's reference window: ReadBin::getReference (:277-293): pad 30, clamp, upper-case
+    pool.run(nw, [&](size_t w) {
         IntervalData &d = *work[w];
         const std::string &contig = ref_names[d.binLoc.contig];
         const std::string *seq = fa.get(contig);
-        // ReadBin::getReference (:277-293): pad 30, clamp, upper-case
         int padLeft = std::max(d.binLoc.start - 30, 0);
         int padRight = seq ? std::min(d.binLoc.stop + 30, (int)seq->size() - 1) : -1;
         if (!seq || padRight < padLeft) {
@@ -1571,7 +1578,111 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         d.reference = seq->substr((size_t)padLeft, (size_t)(padRight - padLeft + 1));
         for (auto &c : d.reference) c = (char)toupper((unsigned char)c);
         d.leftmost = padLeft;
+    });
+    if (ferr) {
+        err = fmsg;
+        return -4;
+    }
+    // B.2 on the device (realign_prep.hip): every toClean read's left-alignment, sums and consensus, each
+    // interval's consensus set, and the offset scan of its pairs; intervals it hands back run on the host
+    std::vector<uint8_t> on_host(nw, 1);
+    DevPrepBatch &DB = S.DB;
+    DevPrepOut &DO = S.DO;
+    DO.best_index.clear(), DO.best_score.clear(), DO.pairs = 0;
+    uint64_t n_dev_iv = 0;
+    if (dev && nw) {
+        const double tb0 = now_s();
+        DB.ref_off.resize(nw + 1);
+        DB.rd_off.resize(nw + 1);
+        DB.ref_off[0] = DB.rd_off[0] = 0;
+        for (size_t w = 0; w < nw; ++w) {
+            DB.ref_off[w + 1] = DB.ref_off[w] + work[w]->reference.size();
+            DB.rd_off[w + 1] = DB.rd_off[w] + work[w]->toClean.size();
+        }
+        DB.ref.resize(DB.ref_off[nw]);
+        DB.rec.resize(DB.rd_off[nw]);
+        DB.start.resize(DB.rd_off[nw]);
+        pool.run_static(nw, [&](size_t w) {
+            const IntervalData &d = *work[w];
+            memcpy(DB.ref.data() + DB.ref_off[w], d.reference.data(), d.reference.size());
+            uint64_t k = DB.rd_off[w];
+            for (RRead *r : d.toClean) {
+                DB.rec[k] = offs[r->idx] - span_lo;
+                DB.start[k] = r->pos - d.leftmost;
+                ++k;
+            }
+        });
+        const double tb1 = now_s();
+        if (dev->run(DB, DO)) {
+            err = "device consensus generation failed";
+            return -1;
+        }
+        for (size_t w = 0; w < nw; ++w) on_host[w] = DO.iv_host[w], n_dev_iv += !on_host[w];
+        st.more.emplace_back("t_prep_batch", tb1 - tb0);
+        st.more.emplace_back("t_prep_device", now_s() - tb1);
+        st.more.emplace_back("t_prep_device_kernels", DO.t_device);
+    }
+    st.more.emplace_back("prep_device_intervals", (double)n_dev_iv);
+    st.more.emplace_back("prep_host_intervals", (double)(nw - n_dev_iv));
+    const double tb2 = now_s();
+    std::vector<uint64_t> wops(nw, 0);
+    Busy bprep(pool.size());
+    pool.run(nw, [&](size_t w) {  // (dynamic: intervals differ in size)
+        const double tb = now_s();
+        struct Acc {
+            Busy &b;
+            size_t w;
+            double t;
+            ~Acc() { b.add(w, now_s() - t); }
+        } acc{bprep, w, tb};
+        IntervalData &d = *work[w];
         const std::string &ref = d.reference;
+        if (!on_host[w]) {
+            // the device's results: the altReads (their bases and qualities decoded here: phase D reads them),
+            // their cigars and sums, and the consensuses it kept, rebuilt from their creating reads
+            const DevPrepRead *o = DO.reads.data() + DB.rd_off[w];
+            const size_t nt = d.toClean.size();
+            size_t abytes = 0;
+            for (size_t k = 0; k < nt; ++k)
+                if (o[k].flags & DP_ALT) abytes += 2 * (size_t)o[k].ul;
+            d.arena.resize(abytes);
+            char *ap = d.arena.data();
+            d.totalRaw = DO.iv_total_raw[w];
+            for (size_t k = 0; k < nt; ++k) {
+                if (!(o[k].flags & DP_ALT)) continue;
+                RRead *r = d.toClean[k];
+                AlignedRead a(r, ap);
+                ap += 2 * a.bases.size();
+                if (o[k].flags & DP_NEWCIG) {
+                    a.newCigar.resize(o[k].n_ops);
+                    for (uint32_t i = 0; i < o[k].n_ops; ++i) a.newCigar[i] = CigOp{kCigChars[o[k].ops[i] & 15], o[k].ops[i] >> 4};
+                }
+                a.misRef = o[k].raw;
+                a.aligner = o[k].aligner;
+                if (o[k].flags & DP_KEPT) {
+                    Consensus c;
+                    if (!create_consensus(r->pos - d.leftmost, a.cigar(), ref, a.bases, c)) {
+                        std::lock_guard<std::mutex> g(emu);
+                        ferr = true;
+                        fmsg = "device consensus generation: a kept consensus the host does not reproduce";
+                        return;
+                    }
+                    d.cons.push_back(std::move(c));
+                }
+                d.alt.push_back(std::move(a));
+            }
+            if (!d.cons.empty()) {
+                d.pairBase = DO.iv_pair_base[w];
+                uint64_t ops = 0;  // findBestOffset's algorithmic compares (#offsets x read length per pair)
+                for (auto &c : d.cons)
+                    for (auto &a : d.alt) {
+                        const int orig = a.read->pos - d.leftmost, ms = (int)c.str.size() - (int)a.cigar_length();
+                        ops += (uint64_t)std::max(std::max(orig, ms) + 1, 0) * a.bases.size();
+                    }
+                wops[w] = ops;
+            }
+            return;
+        }
         size_t abytes = 0;
         for (RRead *r : d.toClean)
             if (!r->cigar.empty()) abytes += 2 * unclipped_len(*r);
@@ -1612,21 +1723,23 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     });
     if (ferr) {
         err = fmsg;
-        return -4;
+        return -1;
     }
     double t2 = now_s();
     st.t_prepare = t2 - t1;
+    st.more.emplace_back("t_prep_finish", t2 - tb2);
     bprep.report(st, "t_prepare");
 
     // ---------------------------------------------------------------- C: offset scan (GPU)
-    // batch layout: per-interval extents, prefix sums, then a parallel fill
+    // the device intervals' pairs were scanned by dev->run (scores first in bidx / bscore); the host
+    // intervals' batch: per-interval extents, prefix sums, then a parallel fill
     ScanBatch &B = S.B;  // (resized below; every byte written)
-    const size_t nw = work.size();
+    const uint64_t ndev = DO.pairs;
     std::vector<uint64_t> xc(nw + 1, 0), xcb(nw + 1, 0), xr(nw + 1, 0), xrb(nw + 1, 0), xp(nw + 1, 0);
     for (size_t w = 0; w < nw; ++w) {
         const IntervalData &d = *work[w];
         uint64_t cb = 0, rb = 0;
-        const bool on = !d.cons.empty();
+        const bool on = !d.cons.empty() && on_host[w];
         if (on) {
             for (auto &c : d.cons) cb += c.str.size();
             for (auto &a : d.alt) rb += a.bases.size();
@@ -1645,11 +1758,10 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     B.pairs.resize(xp[nw]);
     B.cons_off[0] = 0;
     B.read_off[0] = 0;
-    std::vector<uint64_t> wops(nw, 0);
     pool.run_static(nw, [&](size_t w) {
         IntervalData &d = *work[w];
-        if (d.cons.empty()) return;
-        d.pairBase = xp[w];
+        if (d.cons.empty() || !on_host[w]) return;
+        d.pairBase = ndev + xp[w];
         uint64_t cb = xcb[w], ci0 = xc[w];
         for (size_t c = 0; c < d.cons.size(); ++c) {
             memcpy(B.cons.data() + cb, d.cons[c].str.data(), d.cons[c].str.size());
@@ -1681,15 +1793,20 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         wops[w] = ops;
     });
     for (uint64_t o : wops) st.scan_ops += o;
-    st.scan_pairs = B.pairs.size();
+    st.scan_pairs = ndev + B.pairs.size();
     st.t_scan_build = now_s() - t2;
     std::vector<int32_t> &bidx = S.bidx, &bscore = S.bscore;
+    bidx.assign(DO.best_index.begin(), DO.best_index.end());
+    bscore.assign(DO.best_score.begin(), DO.best_score.end());
     if (!B.pairs.empty()) {
-        int rc = scan(B, bidx, bscore);
+        std::vector<int32_t> hi, hs;
+        int rc = scan(B, hi, hs);
         if (rc) {
             err = "offset scan failed";
             return rc;
         }
+        bidx.insert(bidx.end(), hi.begin(), hi.end());
+        bscore.insert(bscore.end(), hs.begin(), hs.end());
     }
     double t3 = now_s();
     st.t_scan = t3 - t2;

@@ -182,6 +182,52 @@ struct ScanBatch {
 // Fills best_index / best_score (one per pair).  Returns 0 on success.
 typedef std::function<int(const ScanBatch &, std::vector<int32_t> &best_index, std::vector<int32_t> &best_score)> ScanFn;
 
+// ---- consensus generation (phase B) + offset scan (phase C) on the device (r06) ----
+// determineReadsThatNeedCleaning (:918-999) per toClean read -- unclipped bases, leftAlignIndel of the
+// two-block reads (util/gatk/AlignmentUtils.cpp:632-677), mismatchQualitySumIgnoreCigar, getMismatchCount,
+// createAlternateConsensus (:1022-1088) -- and the per-interval consensus set (distinct strings in
+// creation order), then the findBestOffset batch, all on the GPU (realign_prep.hip).  The host hands over
+// each interval's reference window and its toClean reads (record offsets into the arena it staged) and
+// gets back what phase D needs.
+struct DevPrepBatch {
+    uvector<uint8_t> ref;       // reference windows back to back (ReadBin::getReference: padded, upper-cased)
+    uvector<uint64_t> ref_off;  // n_iv + 1
+    uvector<uint64_t> rd_off;   // n_iv + 1: interval w's reads are rec[rd_off[w] .. rd_off[w + 1])
+    uvector<uint64_t> rec;      // toClean reads in interval order: byte offset of the record in the staged arena
+    uvector<int32_t> start;     // read pos - the interval's leftmost (startOnRef)
+};
+// per toClean read (32 bytes): flags, the left-aligned cigar when the read has one, the sums
+enum : uint8_t { DP_SKIP = 1, DP_ALT = 2, DP_CAND = 4, DP_NEWCIG = 8, DP_KEPT = 16, DP_HOST = 32, DP_DUP = 64 };
+struct DevPrepRead {
+    uint8_t flags;     // DP_*: SKIP = empty cigar (refRead), ALT = mismatch sum > 0 (an altRead), CAND = its
+                       // consensus is valid, NEWCIG = newCigar set (ops below), KEPT = its consensus is the first
+                       // of its string in the interval, HOST = the device could not handle it (its interval runs
+                       // on the host), DUP = FLAG 0x400
+    uint8_t n_ops;
+    uint16_t ul;       // unclipped length (bases of the M / I operations)
+    int32_t raw;       // mismatchQualitySumIgnoreCigar at the original start
+    int32_t aligner;   // getMismatchCount's mismatch-quality sum (AlignmentUtils.cpp:58-108)
+    uint32_t cig_len;  // getCigarLength of its current cigar (findBestOffset's maxStart)
+    uint32_t ops[4];   // newCigar: length << 4 | BAM op code
+};
+static_assert(sizeof(DevPrepRead) == 32, "DevPrepRead layout");
+struct DevPrepOut {
+    std::vector<DevPrepRead> reads;       // one per DevPrepBatch read
+    std::vector<uint8_t> iv_host;         // per interval: 1 = run phase B / C of this interval on the host
+    std::vector<int64_t> iv_total_raw;    // per interval: sum of raw over non-duplicate altReads
+    std::vector<uint64_t> iv_pair_base;   // per interval: its first pair in best_index / best_score
+    std::vector<int32_t> best_index, best_score;
+    uint64_t pairs = 0, ops = 0;          // scan pairs, algorithmic compare-accumulates
+    bool generic = false;                 // the byte-wise scan kernel ran
+    double t_upload = 0, t_device = 0, t_download = 0;
+};
+struct DevPrep {
+    // Start copying the record arena [lo, hi) of `recs` to the device (may return before it is done; run
+    // waits for it).  Offsets in DevPrepBatch::rec are relative to lo.
+    std::function<int(const uint8_t *recs, uint64_t lo, uint64_t hi)> stage;
+    std::function<int(const DevPrepBatch &, DevPrepOut &)> run;
+};
+
 struct RealignParams {
     double lod_threshold = 5.0;          // LOD_THRESHOLD (local_realignment.cpp:1435)
     double mismatch_threshold = 0.15;    // MISMATCH_THRESHOLD (:1438)
@@ -231,8 +277,10 @@ private:
 // (sequence dictionary), `fasta` = path of the reference FASTA, `intervals` = path of the target
 // interval list ("chr:start-stop", 1-based).  Output records (encoded, in emission order) are
 // written to `out`, their offsets (n + 1) to `out_off`.
+// dev (optional): phases B and C on the device for every interval it can handle (the others, and all of
+// them without dev, on host threads with `scan`) -- the same results either way.
 int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, const uint64_t *offs, uint64_t n,
                 const std::string &fasta, const std::string &intervals, const RealignParams &P, const ScanFn &scan,
-                ByteBuf &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err);
+                ByteBuf &out, std::vector<uint64_t> &out_off, RealignStats &st, std::string &err, const DevPrep *dev = nullptr);
 
 }  // namespace oge

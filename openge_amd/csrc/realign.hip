@@ -24,11 +24,13 @@
 #include "oge_ctx.h"
 #include "bamio.h"
 #include "realign.h"
+#include "realign_dev.h"
 
 #include <chrono>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -333,8 +335,91 @@ __global__ __launch_bounds__(kT) void k_scan_bp(const int4 *__restrict__ pairs, 
 
 }  // namespace
 
-// Device scan over a host batch: upload, one launch per job class, download.  Jobs are maximal runs
-// of pairs with the same consensus.
+// The scan over a batch already in device memory: planes, then k_scan_bp -- or, when the batch holds codes
+// the 2-bit planes do not carry (lower-case bases, '*'), the byte-wise kernel, whose per-consensus jobs are
+// cut on the host from the offsets and pairs (copied down for it when they only live on the device).
+static int scan_core(oge_ctx *ctx, const RsDevBatch &b, const uint64_t *h_cons_off, const uint64_t *h_read_off, const int32_t *h_pairs,
+                     int32_t *di, int32_t *ds, bool *generic_out) {
+    hipStream_t s = ctx->stream;
+    CPlane *dcp = (CPlane *)ctx->ws("rs_cplanes", (b.cons_words + 1) * sizeof(CPlane));
+    RPlane *drp = (RPlane *)ctx->ws("rs_rplanes", (b.read_words + 1) * sizeof(RPlane));
+    uint32_t *drf = (uint32_t *)ctx->ws("rs_rflags", ((uint64_t)b.n_reads + 1) * 4);
+    uint32_t *dgen = (uint32_t *)ctx->ws("rs_generic", 4);
+    if (!dcp || !drp || !drf || !dgen) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(dgen, 0, 4, s));
+    uint32_t generic = 0;
+    OgeStageTimer *t = ctx->begin_stage("realign_scan");
+    const uint64_t items = (uint64_t)b.n_cons + b.n_reads;
+    hipLaunchKernelGGL(k_planes, dim3((uint32_t)((items + 3) / 4)), dim3(kT), 0, s, b.cons, b.cons_off, b.n_cons, b.cwo, b.bases, b.quals,
+                       b.read_off, b.n_reads, b.rwo, dcp, drp, drf, dgen);
+    OGE_LAUNCH_CHECK(ctx);
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&generic, dgen, 4, hipMemcpyDeviceToHost, s));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(s));
+    if (!generic) {
+        hipLaunchKernelGGL(k_scan_bp, dim3((uint32_t)((b.n_pairs + 3) / 4)), dim3(kT), 0, s, b.pairs, b.n_pairs, b.cons_off, b.cwo, dcp,
+                           b.read_off, b.rwo, drp, drf, b.cons, b.bases, b.quals, di, ds);
+        OGE_LAUNCH_CHECK(ctx);
+    } else {
+        // lower-case bases or '*' present: byte-wise kernel, one workgroup per run of same-consensus pairs
+        std::vector<uint64_t> co, ro;
+        std::vector<int32_t> pr;
+        if (!h_cons_off) {
+            co.resize((uint64_t)b.n_cons + 1), ro.resize((uint64_t)b.n_reads + 1), pr.resize(4 * b.n_pairs);
+            OGE_HIP_TRY(ctx, hipMemcpyAsync(co.data(), b.cons_off, co.size() * 8, hipMemcpyDeviceToHost, s));
+            OGE_HIP_TRY(ctx, hipMemcpyAsync(ro.data(), b.read_off, ro.size() * 8, hipMemcpyDeviceToHost, s));
+            OGE_HIP_TRY(ctx, hipMemcpyAsync(pr.data(), b.pairs, pr.size() * 4, hipMemcpyDeviceToHost, s));
+            OGE_HIP_TRY(ctx, hipStreamSynchronize(s));
+            h_cons_off = co.data(), h_read_off = ro.data(), h_pairs = pr.data();
+        }
+        std::vector<ScanJob> small, big;
+        for (uint64_t i = 0; i < b.n_pairs;) {
+            const uint32_t c = (uint32_t)h_pairs[4 * i];
+            uint64_t j = i;
+            bool isbig = h_cons_off[c + 1] - h_cons_off[c] > kConsCap;
+            for (; j < b.n_pairs && (uint32_t)h_pairs[4 * j] == c; ++j) {
+                const uint32_t rd = (uint32_t)h_pairs[4 * j + 1];
+                if (h_read_off[rd + 1] - h_read_off[rd] > kReadCap) isbig = true;
+            }
+            (isbig ? big : small).push_back({c, (uint32_t)i, (uint32_t)(j - i), 0});
+            i = j;
+        }
+        ScanJob *dj = (ScanJob *)ctx->ws("rs_jobs", (small.size() + big.size() + 1) * sizeof(ScanJob));
+        if (!dj) return OGE_ERR_HIP;
+        std::vector<ScanJob> all(small);
+        all.insert(all.end(), big.begin(), big.end());
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(dj, all.data(), all.size() * sizeof(ScanJob), hipMemcpyHostToDevice, s));
+        if (!small.empty()) {
+            hipLaunchKernelGGL(k_realign_scan<false>, dim3((uint32_t)small.size()), dim3(kT), 0, s, b.cons, b.cons_off, b.bases, b.quals,
+                               b.read_off, b.pairs, dj, di, ds);
+            OGE_LAUNCH_CHECK(ctx);
+        }
+        if (!big.empty()) {
+            hipLaunchKernelGGL(k_realign_scan<true>, dim3((uint32_t)big.size()), dim3(kT), 0, s, b.cons, b.cons_off, b.bases, b.quals,
+                               b.read_off, b.pairs, dj + small.size(), di, ds);
+            OGE_LAUNCH_CHECK(ctx);
+        }
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(s));  // `all` must outlive the upload
+    }
+    ctx->end_stage(t);
+    ctx->last_scan_generic = generic != 0;
+    if (generic_out) *generic_out = generic != 0;
+    return OGE_OK;
+}
+
+int realign_scan_devbatch(oge_ctx *ctx, const RsDevBatch &b, int32_t *best_index, int32_t *best_score, bool *generic) {
+    if (!b.n_pairs) return OGE_OK;
+    int32_t *di = (int32_t *)ctx->ws("rs_idx", b.n_pairs * 4);
+    int32_t *ds = (int32_t *)ctx->ws("rs_score", b.n_pairs * 4);
+    if (!di || !ds) return OGE_ERR_HIP;
+    int rc = scan_core(ctx, b, nullptr, nullptr, nullptr, di, ds, generic);
+    if (rc) return rc;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(best_index, di, b.n_pairs * 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(best_score, ds, b.n_pairs * 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return OGE_OK;
+}
+
+// Device scan over a host batch: validate, upload, scan_core, download.
 static int realign_scan_host(oge_ctx *ctx, const uint8_t *cons, uint64_t cons_bytes, const uint64_t *cons_off, uint32_t n_cons,
                              const uint8_t *bases, const uint8_t *quals, uint64_t read_bytes, const uint64_t *read_off,
                              uint32_t n_reads, const int32_t *pairs, uint64_t n_pairs, int32_t *best_index, int32_t *best_score) {
@@ -369,12 +454,7 @@ static int realign_scan_host(oge_ctx *ctx, const uint8_t *cons, uint64_t cons_by
     int32_t *ds = (int32_t *)ctx->ws("rs_score", n_pairs * 4);
     uint64_t *dcwo = (uint64_t *)ctx->ws("rs_cwo", (n_cons + 1) * 8);
     uint64_t *drwo = (uint64_t *)ctx->ws("rs_rwo", (n_reads + 1) * 8);
-    CPlane *dcp = (CPlane *)ctx->ws("rs_cplanes", (cwo[n_cons] + 1) * sizeof(CPlane));
-    RPlane *drp = (RPlane *)ctx->ws("rs_rplanes", (rwo[n_reads] + 1) * sizeof(RPlane));
-    uint32_t *drf = (uint32_t *)ctx->ws("rs_rflags", ((uint64_t)n_reads + 1) * 4);
-    uint32_t *dgen = (uint32_t *)ctx->ws("rs_generic", 4);
-    if (!dc || !dco || !db || !dq || !dro || !dp || !di || !ds || !dcwo || !drwo || !dcp || !drp || !drf || !dgen)
-        return OGE_ERR_HIP;
+    if (!dc || !dco || !db || !dq || !dro || !dp || !di || !ds || !dcwo || !drwo) return OGE_ERR_HIP;
     hipStream_t s = ctx->stream;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dc, cons, cons_bytes, hipMemcpyHostToDevice, s));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dco, cons_off, (n_cons + 1) * 8, hipMemcpyHostToDevice, s));
@@ -384,54 +464,11 @@ static int realign_scan_host(oge_ctx *ctx, const uint8_t *cons, uint64_t cons_by
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dp, pairs, n_pairs * 16, hipMemcpyHostToDevice, s));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(dcwo, cwo.data(), (n_cons + 1) * 8, hipMemcpyHostToDevice, s));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(drwo, rwo.data(), (n_reads + 1) * 8, hipMemcpyHostToDevice, s));
-    OGE_HIP_TRY(ctx, hipMemsetAsync(dgen, 0, 4, s));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(s));
     const double h2 = clk();
-    uint32_t generic = 0;
-    OgeStageTimer *t = ctx->begin_stage("realign_scan");
-    const uint64_t items = (uint64_t)n_cons + n_reads;
-    hipLaunchKernelGGL(k_planes, dim3((uint32_t)((items + 3) / 4)), dim3(kT), 0, s, dc, dco, n_cons, dcwo, db, dq, dro, n_reads,
-                       drwo, dcp, drp, drf, dgen);
-    OGE_LAUNCH_CHECK(ctx);
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&generic, dgen, 4, hipMemcpyDeviceToHost, s));
-    OGE_HIP_TRY(ctx, hipStreamSynchronize(s));
-    if (!generic) {
-        hipLaunchKernelGGL(k_scan_bp, dim3((uint32_t)((n_pairs + 3) / 4)), dim3(kT), 0, s, dp, n_pairs, dco, dcwo, dcp, dro, drwo,
-                           drp, drf, dc, db, dq, di, ds);
-        OGE_LAUNCH_CHECK(ctx);
-    } else {
-        // lower-case bases or '*' present: byte-wise kernel, one workgroup per run of same-consensus pairs
-        std::vector<ScanJob> small, big;
-        for (uint64_t i = 0; i < n_pairs;) {
-            const uint32_t c = (uint32_t)pairs[4 * i];
-            uint64_t j = i;
-            bool isbig = cons_off[c + 1] - cons_off[c] > kConsCap;
-            for (; j < n_pairs && (uint32_t)pairs[4 * j] == c; ++j) {
-                const uint32_t rd = (uint32_t)pairs[4 * j + 1];
-                if (read_off[rd + 1] - read_off[rd] > kReadCap) isbig = true;
-            }
-            (isbig ? big : small).push_back({c, (uint32_t)i, (uint32_t)(j - i), 0});
-            i = j;
-        }
-        ScanJob *dj = (ScanJob *)ctx->ws("rs_jobs", (small.size() + big.size() + 1) * sizeof(ScanJob));
-        if (!dj) return OGE_ERR_HIP;
-        std::vector<ScanJob> all(small);
-        all.insert(all.end(), big.begin(), big.end());
-        OGE_HIP_TRY(ctx, hipMemcpyAsync(dj, all.data(), all.size() * sizeof(ScanJob), hipMemcpyHostToDevice, s));
-        if (!small.empty()) {
-            hipLaunchKernelGGL(k_realign_scan<false>, dim3((uint32_t)small.size()), dim3(kT), 0, s, dc, dco, db, dq, dro, dp, dj, di,
-                               ds);
-            OGE_LAUNCH_CHECK(ctx);
-        }
-        if (!big.empty()) {
-            hipLaunchKernelGGL(k_realign_scan<true>, dim3((uint32_t)big.size()), dim3(kT), 0, s, dc, dco, db, dq, dro, dp,
-                               dj + small.size(), di, ds);
-            OGE_LAUNCH_CHECK(ctx);
-        }
-        OGE_HIP_TRY(ctx, hipStreamSynchronize(s));  // `all` must outlive the upload
-    }
-    ctx->end_stage(t);
-    ctx->last_scan_generic = generic != 0;
+    const RsDevBatch b{dc, dco, n_cons, dcwo, cwo[n_cons], db, dq, dro, n_reads, drwo, rwo[n_reads], dp, n_pairs};
+    int rc = scan_core(ctx, b, cons_off, read_off, pairs, di, ds, nullptr);
+    if (rc) return rc;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(best_index, di, n_pairs * 4, hipMemcpyDeviceToHost, s));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(best_score, ds, n_pairs * 4, hipMemcpyDeviceToHost, s));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(s));
@@ -509,12 +546,50 @@ int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len,
         if (!scan_rc) oge_ctx_timing(ctx, "realign_scan", &scan_kernel_ms);
         return scan_rc;
     };
+    // phase B on the device (realign_prep.hip; OGE_REALIGN_DEVICE_PREP=0: the host threads): the record arena is
+    // copied by a helper thread while the host loads the FASTA, decodes and bins
+    struct Stager {
+        oge_ctx *ctx;
+        std::thread th;
+        uint8_t *d = nullptr;
+        hipError_t e = hipSuccess;
+        ~Stager() {
+            if (th.joinable()) th.join();
+        }
+    } stg{ctx};
+    int prep_rc = 0;
+    oge::DevPrep dp;
+    dp.stage = [&](const uint8_t *rp, uint64_t lo, uint64_t hi) -> int {
+        stg.d = (uint8_t *)ctx->ws("rp_recs", hi - lo + 64);
+        if (!stg.d) return prep_rc = OGE_ERR_HIP;
+        const int dev = ctx->device;
+        stg.th = std::thread([&stg, rp, lo, hi, dev]() {
+            (void)hipSetDevice(dev);
+            stg.e = hipMemcpy(stg.d, rp + lo, hi - lo, hipMemcpyHostToDevice);
+        });
+        return 0;
+    };
+    dp.run = [&](const oge::DevPrepBatch &B, oge::DevPrepOut &O) -> int {
+        if (stg.th.joinable()) stg.th.join();
+        if (stg.e != hipSuccess) return prep_rc = oge_fail(ctx, OGE_ERR_HIP, (std::string("realign: record upload: ") + hipGetErrorString(stg.e)).c_str());
+        return prep_rc = oge_realign_prep_run(ctx, stg.d, B, O);
+    };
+    const char *pe = getenv("OGE_REALIGN_DEVICE_PREP");
+    const bool use_dev = !(pe && pe[0] == '0');
     std::unique_ptr<oge_realign_result> r(new oge_realign_result());
     oge::RealignStats st;
     const auto tr0 = std::chrono::steady_clock::now();
-    int rc = oge::realign_run(names, recs, rec_off, n, fasta_path, intervals_path, P, scan, r->recs, r->offs, st, err);
+    int rc = oge::realign_run(names, recs, rec_off, n, fasta_path, intervals_path, P, scan, r->recs, r->offs, st, err,
+                              use_dev ? &dp : nullptr);
     st.t_run = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
-    if (rc) return scan_rc ? scan_rc : oge_fail(ctx, rc, ("oge_localrealign: " + err).c_str());
+    if (stg.th.joinable()) stg.th.join();
+    if (rc) return scan_rc ? scan_rc : prep_rc ? prep_rc : oge_fail(ctx, rc, ("oge_localrealign: " + err).c_str());
+    double prep_ms = 0;
+    oge_ctx_timing(ctx, "realign_scan", &scan_kernel_ms);
+    if (scan_kernel_ms < 0) scan_kernel_ms = 0;
+    oge_ctx_timing(ctx, "realign_prep", &prep_ms);
+    st.more.emplace_back("prep_kernel_ms", prep_ms > 0 ? prep_ms : 0.0);
+    st.more.emplace_back("device_prep", use_dev ? 1.0 : 0.0);
     char buf[2048];
     snprintf(buf, sizeof buf,
              "{\"intervals\": %llu, \"intervals_cleaned\": %llu, \"reads_realigned\": %llu, \"scan_pairs\": %llu, "

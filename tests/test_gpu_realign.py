@@ -92,3 +92,46 @@ def test_gpu_contig_sharded_realign_equals_reference(ctx, tmp_path, world):
     whole = b"".join(parts)
     d = R.digest(np.frombuffer(whole + b"\0" * 16, np.uint8), _offsets_of(whole))
     assert d["stream_sha256"] == meta["stream_sha256"]
+
+
+def _realign_both(ctx, monkeypatch, h, recs, offs, fa, iv):
+    monkeypatch.setenv("OGE_REALIGN_DEVICE_PREP", "0")
+    out0, oo0, st0 = ctx.localrealign(h, recs, offs, len(offs) - 1, fa, iv)
+    monkeypatch.setenv("OGE_REALIGN_DEVICE_PREP", "1")
+    out1, oo1, st1 = ctx.localrealign(h, recs, offs, len(offs) - 1, fa, iv)
+    monkeypatch.delenv("OGE_REALIGN_DEVICE_PREP")
+    assert st0["device_prep"] == 0 and st1["device_prep"] == 1
+    b0, b1 = bytes(out0[:int(oo0[-1])]), bytes(out1[:int(oo1[-1])])
+    assert b0 == b1 and list(oo0) == list(oo1)
+    for k in ("scan_pairs", "scan_ops", "intervals_cleaned", "reads_realigned"):
+        assert st0[k] == st1[k], k
+    return st1
+
+
+@pytest.mark.parametrize("name", RL_CASES)
+def test_gpu_device_consensus_generation_equals_host(ctx, tmp_path, monkeypatch, name):
+    """Phase B on the device (realign_prep.hip: left-alignment, mismatch sums, consensus set, batch) and on
+    the host threads (realign.cpp) give the same records, the same scan pairs and compare counts -- on the
+    reference's own rl_* cases (the default path is pinned to them by test_gpu_localrealign_matches_reference)."""
+    meta, arrays, h, recs, offs, fa, iv = load_rl_case(name, tmp_path)
+    st = _realign_both(ctx, monkeypatch, h, recs, offs, fa, iv)
+    assert st["prep_device_intervals"] > 0
+
+
+@pytest.mark.parametrize("seed,knobs", [
+    (11, {}),
+    (12, {"clip_ppm": 300000, "n_ppm": 20000, "lower_ppm": 50000}),
+    (13, {"gapped_ppm": 200000, "alt_indel_ppm": 300000, "noindel_ppm": 200000}),
+    (14, {"qual_min": 0, "qual_max": 93, "dup_ppm": 200000, "mapq0_ppm": 100000, "clip_ppm": 100000}),
+])
+def test_gpu_device_consensus_generation_stress(ctx, tmp_path, monkeypatch, seed, knobs):
+    """Synthetic C5-shaped sets with soft clips, N and lower-case bases, gapped (N) reads, competing indels,
+    a wide quality range, duplicates: device and host phase B give the same output (qualities >= 95, whose
+    weights are negative, are in the rl_qual golden)."""
+    from openge_amd import lib as L
+    p = L.realign_synth_params(n_intervals=1500, seed=seed, **knobs)
+    fa, iv, bam = L.synth_realign(p, tmp_path, level=1)
+    b = L.Bam(bam)
+    offs = np.append(b.offs, np.uint64(b.recs.size))
+    st = _realign_both(ctx, monkeypatch, b.header_text, b.recs, offs, fa, iv)
+    assert st["prep_device_intervals"] > 0 and st["scan_pairs"] > 0
