@@ -105,9 +105,19 @@ __device__ __forceinline__ char alt_at(const Alt &a, int64_t k, const char *ref,
     }
     return ref[k];
 }
+// a == b as strings.  Both are the same reference with one indel of the same kind spliced in (left_align
+// compares moves of one indel), so with equal lengths L they agree outside the span the two indels cover:
+// below min(R) + min(L, 0) both are the reference prefix, from max(R) + max(L, 0) on (insertion) or max(R)
+// on (deletion) both are the same shifted reference suffix -- only that span is compared (a memcmp of the
+// whole window in the reference).
 __device__ bool alt_equal(const Alt &a, const Alt &b, const char *ref, const Read &rd) {
     if (a.sz != b.sz) return false;
-    for (int64_t k = 0; k < a.sz; ++k)
+    int64_t k0 = 0, k1 = a.sz;
+    if (a.del == b.del && a.L == b.L) {
+        k0 = max(min(a.R, b.R) + min(a.L, (int64_t)0), (int64_t)0);
+        k1 = min(max(a.R, b.R) + (a.del ? 0 : max(a.L, (int64_t)0)), a.sz);
+    }
+    for (int64_t k = k0; k < k1; ++k)
         if (alt_at(a, k, ref, rd) != alt_at(b, k, ref, rd)) return false;
     return true;
 }
@@ -597,6 +607,20 @@ struct BatchArgs {
     int4 *pairs;
 };
 
+__device__ __forceinline__ uint64_t wave_incl_u64(uint64_t v, uint32_t lane) {  // inclusive prefix sum over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = ((uint64_t)__shfl_up((unsigned)(v >> 32), d, 64) << 32) | (uint64_t)__shfl_up((unsigned)v, d, 64);
+        if (lane >= (uint32_t)d) v += o;
+    }
+    return v;
+}
+
+// A chunk of 64 reads at a time: each lane loads its own read's summary, record header and cigar and takes
+// its offsets from the wave's prefix sums; then the chunk's kept consensuses and altReads are copied one after
+// the other by the whole wave (consecutive bytes per lane), each read's pointers, offsets and cigar handed to
+// the wave by shuffles.  (r06: one read at a time with every lane loading the same summary and header --
+// dependent round trips per read -- took 3.4 ms of C5; a lane copying its own read's bytes, 9 ms.)
 __global__ __launch_bounds__(64) void k_r2_batch(BatchArgs A) {
     __shared__ uint32_t clen_s[kCandCap];
     const uint32_t w = blockIdx.x, lane = threadIdx.x;
@@ -605,32 +629,81 @@ __global__ __launch_bounds__(64) void k_r2_batch(BatchArgs A) {
     const uint64_t n_alt = A.ac[w + 1] - A.ac[w], n_kept = A.kc[w + 1] - A.kc[w];
     uint64_t ci = A.kc[w], cb = A.kb[w], cw = A.kw[w];
     uint64_t ri = A.ac[w], rb = A.ab[w], rw = A.aw[w];
-    uint32_t c = 0;
-    for (uint64_t r = a; r < b; ++r) {
-        const uint8_t f = A.R.out[r].flags;
-        if (f & oge::DP_KEPT) {
-            const uint64_t len = A.cand_len[r];
-            const uint8_t *src = A.cand + A.cand_off[r];
-            for (uint64_t k = lane; k < len; k += 64) A.cons[cb + k] = src[k];
-            if (lane == 0) A.cons_off[ci] = cb, A.cwo[ci] = cw, clen_s[c] = (uint32_t)len;
-            ci++, c++, cb += len, cw += (len + 63) / 64 + 1;
+    uint64_t c0 = 0;
+    auto bc64 = [](uint64_t v, int src) {
+        return ((uint64_t)__shfl((unsigned)(v >> 32), src, 64) << 32) | (uint64_t)__shfl((unsigned)v, src, 64);
+    };
+    for (uint64_t r0 = a; r0 < b; r0 += 64) {
+        const uint64_t r = r0 + lane;
+        uint8_t f = 0;
+        uint32_t ul = 0;
+        uint64_t len = 0;
+        if (r < b) {
+            f = A.R.out[r].flags;
+            if (f & oge::DP_ALT) ul = A.R.out[r].ul;
+            if (f & oge::DP_KEPT) len = A.cand_len[r];
         }
-        if (f & oge::DP_ALT) {
-            const uint32_t ul = A.R.out[r].ul;
-            const uint8_t *R = A.R.recs + A.R.rec[r];
+        const bool kept = f & oge::DP_KEPT, alt = f & oge::DP_ALT;
+        const uint64_t kw1 = kept ? (len + 63) / 64 + 1 : 0, aw1 = alt ? (ul + 63) / 64 : 0;
+        const uint64_t ik = wave_incl_u64(kept, lane), il = wave_incl_u64(len, lane), iw = wave_incl_u64(kw1, lane);
+        const uint64_t ia = wave_incl_u64(alt, lane), iu = wave_incl_u64(ul, lane), iaw = wave_incl_u64(aw1, lane);
+        // this lane's read: offsets, and for an altRead its header and cigar (packed len << 4 | code)
+        uint64_t src_c = 0, dst_c = cb + il - len, dst_r = rb + iu - ul, seq4 = 0, qual = 0;
+        uint32_t ops[kMaxIn], nops = 0;
+        int64_t lseq = 0;
+        if (kept) {
+            src_c = (uint64_t)(uintptr_t)(A.cand + A.cand_off[r]);
+            A.cons_off[ci + ik - 1] = dst_c;
+            A.cwo[ci + ik - 1] = cw + iw - kw1;
+            clen_s[c0 + ik - 1] = (uint32_t)len;
+        }
+        if (alt) {
             Cig orig;
             Read rd;
             uint32_t flag;
             bool fits;
-            load_read(R, orig, rd, &flag, &fits);
-            for (uint64_t k = lane; k < ul; k += 64) {
-                const int64_t p = unclipped_pos(orig, (int64_t)k, rd.lseq);
-                A.bases[rb + k] = (uint8_t)rd.base(p);
-                A.quals[rb + k] = rd.qual[p];
-            }
-            if (lane == 0) A.read_off[ri] = rb, A.rwo[ri] = rw;
-            ri++, rb += ul, rw += (ul + 63) / 64;
+            load_read(A.R.recs + A.R.rec[r], orig, rd, &flag, &fits);
+            seq4 = (uint64_t)(uintptr_t)rd.seq4, qual = (uint64_t)(uintptr_t)rd.qual, lseq = rd.lseq;
+            nops = (uint32_t)orig.n;
+#pragma unroll
+            for (int j = 0; j < kMaxIn; ++j) ops[j] = j < orig.n ? (orig.len[j] << 4) | orig.code[j] : 0u;
+            A.read_off[ri + ia - 1] = dst_r;
+            A.rwo[ri + ia - 1] = rw + iaw - aw1;
         }
+        // the copies, read by read, by the whole wave
+        uint64_t mk = __ballot(kept);
+        while (mk) {
+            const int src = __builtin_ctzll(mk);
+            mk &= mk - 1;
+            const uint8_t *from = (const uint8_t *)(uintptr_t)bc64(src_c, src);
+            const uint64_t to = bc64(dst_c, src), n = bc64(len, src);
+            for (uint64_t k = lane; k < n; k += 64) A.cons[to + k] = from[k];
+        }
+        uint64_t ma = __ballot(alt);
+        while (ma) {
+            const int src = __builtin_ctzll(ma);
+            ma &= ma - 1;
+            Cig orig;
+            orig.n = (int)__shfl(nops, src, 64);
+#pragma unroll
+            for (int j = 0; j < kMaxIn; ++j) {
+                const uint32_t o = __shfl(ops[j], src, 64);
+                orig.len[j] = o >> 4, orig.code[j] = (uint8_t)(o & 15);
+            }
+            Read rd;
+            rd.seq4 = (const uint8_t *)(uintptr_t)bc64(seq4, src);
+            rd.qual = (const uint8_t *)(uintptr_t)bc64(qual, src);
+            rd.lseq = (int64_t)bc64((uint64_t)lseq, src);
+            const uint64_t to = bc64(dst_r, src), n = __shfl(ul, src, 64);
+            for (uint64_t k = lane; k < n; k += 64) {
+                const int64_t p = unclipped_pos(orig, (int64_t)k, rd.lseq);
+                A.bases[to + k] = (uint8_t)rd.base(p);
+                A.quals[to + k] = rd.qual[p];
+            }
+        }
+        auto last = [](uint64_t v) { return (uint64_t)__shfl((unsigned long long)v, 63, 64); };
+        ci += last(ik), cb += last(il), cw += last(iw), c0 += last(ik);
+        ri += last(ia), rb += last(iu), rw += last(iaw);
     }
     __syncthreads();
     const uint64_t np = n_kept * n_alt;
