@@ -327,6 +327,16 @@ typedef struct oge_realign_result oge_realign_result;
 int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len, const uint8_t *recs,
                      const uint64_t *rec_off, uint64_t n, const char *fasta_path, const char *intervals_path,
                      const oge_realign_opts *opts, oge_realign_result **out);
+/* The same over n_ctx devices (realign sharded by interval ranges).  The work intervals are cut
+ * into n_ctx contiguous ranges balanced by the reads to clean -- cuts fall inside contigs as well, a
+ * single-contig input included -- and device g generates the consensuses of range g and scans their pairs
+ * (realign_prep.hip, realign.hip); binning, decisions and the mate-fixing writer run once on the host over
+ * the whole input, so the output equals oge_localrealign's for any input and no writer state crosses a cut.
+ * Per-device counts are in the result's stats (prep_rank<g>_intervals / _reads / _pairs).  Errors and
+ * messages go to ctxs[0]. */
+int oge_localrealign_multi(oge_ctx *const *ctxs, int n_ctx, const char *header_text, uint64_t header_len, const uint8_t *recs,
+                           const uint64_t *rec_off, uint64_t n, const char *fasta_path, const char *intervals_path,
+                           const oge_realign_opts *opts, oge_realign_result **out);
 uint64_t oge_realign_result_count(const oge_realign_result *r);
 const uint8_t *oge_realign_result_records(const oge_realign_result *r, uint64_t *bytes_out);
 const uint64_t *oge_realign_result_offsets(const oge_realign_result *r);   /* count + 1 entries */

@@ -939,81 +939,36 @@ int MarkDuplicates::runInternal(ChainContext &cc, ReadBatch &b) {
 }
 
 // ----------------------------------------------------------------------------------- LocalRealignment
-// --gpus G: realignment shards by contig -- a read bin, the interval walk and the mate
-// fixer's state never span contigs (alg/local_realignment.cpp:263-275,455-553,
-// gatk/ConstrainedMateFixingManager.cpp:312-330) -- so rank g realigns a contiguous range of whole
-// contigs of the coordinate-sorted input (ranges balanced by record count) and the outputs concatenate.
+// --gpus G: one realignment over the whole input whose per-interval device work (consensus
+// generation, the offset scan) is spread over the G ranks' devices by interval ranges balanced by reads
+// (oge_localrealign_multi) -- cuts fall inside contigs too, so a single-contig input shards; the binning,
+// the decisions and the mate-fixing writer run once, on all host threads, so the output is the one-GPU
+// output.  (Until r05 each rank realigned a range of whole contigs on its own, and a mate-fixer backlog at a
+// shard boundary aborted the run.)
 static int realign_ranks(ChainContext &cc, ReadBatch &b, const std::string &ht, const std::string &ref, const std::string &iv,
                          bool verbose) {
     if (cc.init_ranks()) return -1;
     const int G = cc.gpus;
-    const uint64_t n = b.n;
-    std::vector<int64_t> rid(n);
-    for (uint64_t i = 0; i < n; ++i) {
-        const int32_t r = oge_rd_i32(b.recs.data() + b.offs[i] + OGE_OFF_REFID);
-        rid[i] = r < 0 ? INT64_MAX : r;
-        if (i && rid[i] < rid[i - 1]) {
-            fprintf(stderr, "openge: localrealign --gpus needs coordinate-sorted input\n");
-            return -1;
-        }
-    }
-    std::vector<uint64_t> cut(G + 1, n);  // cuts at contig boundaries nearest the equal-count targets
-    cut[0] = 0;
-    for (int g = 1; g < G; ++g) {
-        uint64_t c = std::max<uint64_t>(cut[g - 1], n * (uint64_t)g / (uint64_t)G);
-        while (c > cut[g - 1] && c < n && rid[c] == rid[c - 1]) --c;  // back to the contig's first record
-        if (c == cut[g - 1]) {                                          // or forward past it
-            c = n * (uint64_t)g / (uint64_t)G;
-            while (c < n && c > 0 && rid[c] == rid[c - 1]) ++c;
-        }
-        cut[g] = std::max(c, cut[g - 1]);
-    }
-    std::vector<oge_realign_result *> res(G, nullptr);
-    std::vector<std::string> why(G);
-    std::vector<std::thread> ts;
-    for (int g = 0; g < G; ++g)
-        ts.emplace_back([&, g]() {
-            oge_realign_opts o;
-            oge_realign_opts_init(&o);
-            o.threads = std::max(1, cc.threads / G);
-            if (oge_localrealign(cc.rank_ctx[g], ht.data(), ht.size(), b.recs.data(), b.offs.data() + cut[g], cut[g + 1] - cut[g],
-                                 ref.c_str(), iv.c_str(), &o, &res[g]))
-                why[g] = oge_last_error(cc.rank_ctx[g]);
-        });
-    for (auto &t : ts) t.join();
-    int ret = 0;
+    oge_realign_opts o;
+    oge_realign_opts_init(&o);
+    o.threads = cc.threads;
+    oge_realign_result *r = nullptr;
+    if (oge_localrealign_multi(cc.rank_ctx.data(), G, ht.data(), ht.size(), b.recs.data(), b.offs.data(), b.n, ref.c_str(), iv.c_str(),
+                               &o, &r))
+        return cc.fail("LocalRealignment");
+    if (verbose) fprintf(stderr, "[openge] LocalRealignment over %d devices: %s\n", G, oge_realign_result_stats(r));
+    uint64_t bytes = 0;
+    const uint8_t *rp = oge_realign_result_records(r, &bytes);
+    const uint64_t *op = oge_realign_result_offsets(r);
+    const uint64_t m = oge_realign_result_count(r);
     bytevec recs;
-    std::vector<uint64_t> offs(1, 0);
-    for (int g = 0; g < G && !ret; ++g) {
-        if (!res[g]) {
-            fprintf(stderr, "openge: LocalRealignment rank %d: %s\n", g, why[g].c_str());
-            ret = -1;
-            break;
-        }
-        const char *st = oge_realign_result_stats(res[g]);
-        const char *tw = strstr(st, "\"tail_waiting\": ");
-        oge_realign_opts d;
-        oge_realign_opts_init(&d);
-        if (g + 1 < G && tw && strtoull(tw + 16, nullptr, 10) >= (uint64_t)d.max_records_in_memory) {
-            // the mate fixer flushed with maxRecordsInMemory reads waiting: that flush keeps its modified
-            // mate entries across the contig boundary, so the ranks would not concatenate exactly
-            fprintf(stderr, "openge: localrealign --gpus: the mate fixer held >= %d reads at a shard boundary; run on one GPU\n",
-                    d.max_records_in_memory);
-            ret = -1;
-            break;
-        }
-        if (verbose) fprintf(stderr, "[openge] LocalRealignment rank %d: %s\n", g, st);
-        uint64_t bytes = 0;
-        const uint8_t *rp = oge_realign_result_records(res[g], &bytes);
-        const uint64_t *op = oge_realign_result_offsets(res[g]);
-        const uint64_t m = oge_realign_result_count(res[g]), base = recs.size();
-        recs.insert(recs.end(), rp + op[0], rp + op[m]);
-        for (uint64_t k = 1; k <= m; ++k) offs.push_back(base + op[k] - op[0]);
+    std::vector<uint64_t> offs(m + 1, 0);
+    if (m) {
+        recs.assign(rp + op[0], rp + op[m]);
+        for (uint64_t k = 0; k <= m; ++k) offs[k] = op[k] - op[0];
     }
-    for (auto *r : res)
-        if (r) oge_realign_result_free(r);
-    if (ret) return ret;
-    b.n = offs.size() - 1;
+    oge_realign_result_free(r);
+    b.n = m;
     recs.resize(recs.size() + 16, 0);
     b.recs = std::move(recs);
     b.offs = std::move(offs);

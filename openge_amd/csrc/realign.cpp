@@ -1332,8 +1332,8 @@ struct Scratch {
     ScanBatch B;
     std::vector<int32_t> bidx, bscore;
     std::vector<RRead *> order;
-    DevPrepBatch DB;  // phase B on the device: its input and results
-    DevPrepOut DO;
+    std::vector<DevPrepBatch> DB;  // phase B on the devices: their inputs and results
+    std::vector<DevPrepOut> DO;
     Fasta fa;
     ~Scratch() {
         for (uint64_t i = 0; i < rlive; ++i) rmem[i].~RRead();
@@ -1394,10 +1394,11 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         for (uint64_t i = 0; i < n; ++i) lo = std::min(lo, offs[i]), hi = std::max(hi, offs[i]);
         hi += 4 + rd32(recs + hi);
         span_lo = lo;
-        if (dev->stage(recs, lo, hi)) {
-            err = "device consensus generation: staging the records failed";
-            return -1;
-        }
+        for (int g = 0; g < std::max(1, dev->ndev); ++g)
+            if (dev->stage(g, recs, lo, hi)) {
+                err = "device consensus generation: staging the records failed";
+                return -1;
+            }
     }
     Pool &pool = *S.pool;
     st.more.emplace_back("t_pool", now_s() - t0);
@@ -1583,29 +1584,49 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         err = fmsg;
         return -4;
     }
-    // B.2 on the device (realign_prep.hip): every toClean read's left-alignment, sums and consensus, each
-    // interval's consensus set, and the offset scan of its pairs; intervals it hands back run on the host
+    // B.2 on the device(s) (realign_prep.hip): every toClean read's left-alignment, sums and consensus, each
+    // interval's consensus set, and the offset scan of its pairs; intervals a device hands back run on the
+    // host.  With several devices, device g takes the g-th contiguous range of work intervals (balanced by
+    // toClean reads) and the results are stitched in interval order.
     std::vector<uint8_t> on_host(nw, 1);
-    DevPrepBatch &DB = S.DB;
-    DevPrepOut &DO = S.DO;
-    DO.best_index.clear(), DO.best_score.clear(), DO.pairs = 0;
-    uint64_t n_dev_iv = 0;
+    std::vector<const DevPrepRead *> iv_reads(nw, nullptr);  // interval w's first read result
+    std::vector<int64_t> iv_traw(nw, 0);
+    std::vector<uint64_t> iv_pbase(nw, 0);
+    std::vector<int32_t> dev_bi, dev_bs;
+    uint64_t n_dev_iv = 0, ndev_pairs = 0;
+    const int G = dev ? std::max(1, dev->ndev) : 0;
     if (dev && nw) {
         const double tb0 = now_s();
-        DB.ref_off.resize(nw + 1);
-        DB.rd_off.resize(nw + 1);
-        DB.ref_off[0] = DB.rd_off[0] = 0;
-        for (size_t w = 0; w < nw; ++w) {
-            DB.ref_off[w + 1] = DB.ref_off[w] + work[w]->reference.size();
-            DB.rd_off[w + 1] = DB.rd_off[w] + work[w]->toClean.size();
+        S.DB.resize((size_t)G);
+        S.DO.resize((size_t)G);
+        std::vector<uint64_t> pre(nw + 1, 0);
+        for (size_t w = 0; w < nw; ++w) pre[w + 1] = pre[w] + work[w]->toClean.size();
+        std::vector<size_t> cut((size_t)G + 1, nw);
+        cut[0] = 0;
+        for (int g = 1; g < G; ++g)
+            cut[(size_t)g] = (size_t)(std::lower_bound(pre.begin(), pre.end(), pre[nw] * (uint64_t)g / (uint64_t)G) - pre.begin());
+        for (int g = 1; g <= G; ++g) cut[(size_t)g] = std::max(std::min(cut[(size_t)g], nw), cut[(size_t)g - 1]);
+        for (int g = 0; g < G; ++g) {
+            DevPrepBatch &DB = S.DB[(size_t)g];
+            const size_t w0 = cut[(size_t)g], w1 = cut[(size_t)g + 1], m = w1 - w0;
+            DB.ref_off.resize(m + 1);
+            DB.rd_off.resize(m + 1);
+            DB.ref_off[0] = DB.rd_off[0] = 0;
+            for (size_t k = 0; k < m; ++k) {
+                DB.ref_off[k + 1] = DB.ref_off[k] + work[w0 + k]->reference.size();
+                DB.rd_off[k + 1] = DB.rd_off[k] + work[w0 + k]->toClean.size();
+            }
+            DB.ref.resize(DB.ref_off[m]);
+            DB.rec.resize(DB.rd_off[m]);
+            DB.start.resize(DB.rd_off[m]);
         }
-        DB.ref.resize(DB.ref_off[nw]);
-        DB.rec.resize(DB.rd_off[nw]);
-        DB.start.resize(DB.rd_off[nw]);
         pool.run_static(nw, [&](size_t w) {
+            const int g = (int)(std::upper_bound(cut.begin(), cut.end(), w) - cut.begin()) - 1;
+            DevPrepBatch &DB = S.DB[(size_t)g];
+            const size_t k0 = w - cut[(size_t)g];
             const IntervalData &d = *work[w];
-            memcpy(DB.ref.data() + DB.ref_off[w], d.reference.data(), d.reference.size());
-            uint64_t k = DB.rd_off[w];
+            memcpy(DB.ref.data() + DB.ref_off[k0], d.reference.data(), d.reference.size());
+            uint64_t k = DB.rd_off[k0];
             for (RRead *r : d.toClean) {
                 DB.rec[k] = offs[r->idx] - span_lo;
                 DB.start[k] = r->pos - d.leftmost;
@@ -1613,15 +1634,48 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
             }
         });
         const double tb1 = now_s();
-        if (dev->run(DB, DO)) {
-            err = "device consensus generation failed";
-            return -1;
+        std::vector<int> rcs((size_t)G, 0);
+        if (G == 1) {
+            rcs[0] = dev->run(0, S.DB[0], S.DO[0]);
+        } else {
+            std::vector<std::thread> ts;
+            for (int g = 0; g < G; ++g) ts.emplace_back([&, g]() { rcs[(size_t)g] = dev->run(g, S.DB[(size_t)g], S.DO[(size_t)g]); });
+            for (auto &t : ts) t.join();
         }
-        for (size_t w = 0; w < nw; ++w) on_host[w] = DO.iv_host[w], n_dev_iv += !on_host[w];
+        for (int g = 0; g < G; ++g)
+            if (rcs[(size_t)g]) {
+                err = "device consensus generation failed (device " + std::to_string(g) + ")";
+                return -1;
+            }
+        for (int g = 0; g < G; ++g) {
+            const DevPrepOut &O = S.DO[(size_t)g];
+            const DevPrepBatch &DB = S.DB[(size_t)g];
+            uint64_t niv = 0;
+            for (size_t w = cut[(size_t)g]; w < cut[(size_t)g + 1]; ++w) {
+                const size_t k = w - cut[(size_t)g];
+                on_host[w] = O.iv_host[k];
+                n_dev_iv += !on_host[w], niv += !on_host[w];
+                iv_reads[w] = O.reads.data() + DB.rd_off[k];
+                iv_traw[w] = O.iv_total_raw[k];
+                iv_pbase[w] = ndev_pairs + O.iv_pair_base[k];
+            }
+            dev_bi.insert(dev_bi.end(), O.best_index.begin(), O.best_index.end());
+            dev_bs.insert(dev_bs.end(), O.best_score.begin(), O.best_score.end());
+            ndev_pairs += O.pairs;
+            if (G > 1) {
+                const std::string pfx = "prep_rank" + std::to_string(g) + "_";
+                st.more.emplace_back(pfx + "intervals", (double)niv);
+                st.more.emplace_back(pfx + "reads", (double)DB.rec.size());
+                st.more.emplace_back(pfx + "pairs", (double)O.pairs);
+            }
+        }
         st.more.emplace_back("t_prep_batch", tb1 - tb0);
         st.more.emplace_back("t_prep_device", now_s() - tb1);
-        st.more.emplace_back("t_prep_device_kernels", DO.t_device);
+        double tk = 0;
+        for (auto &O : S.DO) tk = std::max(tk, O.t_device);
+        st.more.emplace_back("t_prep_device_kernels", tk);
     }
+    st.more.emplace_back("prep_devices", (double)G);
     st.more.emplace_back("prep_device_intervals", (double)n_dev_iv);
     st.more.emplace_back("prep_host_intervals", (double)(nw - n_dev_iv));
     const double tb2 = now_s();
@@ -1640,14 +1694,14 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         if (!on_host[w]) {
             // the device's results: the altReads (their bases and qualities decoded here: phase D reads them),
             // their cigars and sums, and the consensuses it kept, rebuilt from their creating reads
-            const DevPrepRead *o = DO.reads.data() + DB.rd_off[w];
+            const DevPrepRead *o = iv_reads[w];
             const size_t nt = d.toClean.size();
             size_t abytes = 0;
             for (size_t k = 0; k < nt; ++k)
                 if (o[k].flags & DP_ALT) abytes += 2 * (size_t)o[k].ul;
             d.arena.resize(abytes);
             char *ap = d.arena.data();
-            d.totalRaw = DO.iv_total_raw[w];
+            d.totalRaw = iv_traw[w];
             for (size_t k = 0; k < nt; ++k) {
                 if (!(o[k].flags & DP_ALT)) continue;
                 RRead *r = d.toClean[k];
@@ -1672,7 +1726,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
                 d.alt.push_back(std::move(a));
             }
             if (!d.cons.empty()) {
-                d.pairBase = DO.iv_pair_base[w];
+                d.pairBase = iv_pbase[w];
                 uint64_t ops = 0;  // findBestOffset's algorithmic compares (#offsets x read length per pair)
                 for (auto &c : d.cons)
                     for (auto &a : d.alt) {
@@ -1734,7 +1788,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     // the device intervals' pairs were scanned by dev->run (scores first in bidx / bscore); the host
     // intervals' batch: per-interval extents, prefix sums, then a parallel fill
     ScanBatch &B = S.B;  // (resized below; every byte written)
-    const uint64_t ndev = DO.pairs;
+    const uint64_t ndev = ndev_pairs;
     std::vector<uint64_t> xc(nw + 1, 0), xcb(nw + 1, 0), xr(nw + 1, 0), xrb(nw + 1, 0), xp(nw + 1, 0);
     for (size_t w = 0; w < nw; ++w) {
         const IntervalData &d = *work[w];
@@ -1796,8 +1850,8 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     st.scan_pairs = ndev + B.pairs.size();
     st.t_scan_build = now_s() - t2;
     std::vector<int32_t> &bidx = S.bidx, &bscore = S.bscore;
-    bidx.assign(DO.best_index.begin(), DO.best_index.end());
-    bscore.assign(DO.best_score.begin(), DO.best_score.end());
+    bidx.swap(dev_bi);
+    bscore.swap(dev_bs);
     if (!B.pairs.empty()) {
         std::vector<int32_t> hi, hs;
         int rc = scan(B, hi, hs);

@@ -222,10 +222,15 @@ struct DevPrepOut {
     double t_upload = 0, t_device = 0, t_download = 0;
 };
 struct DevPrep {
-    // Start copying the record arena [lo, hi) of `recs` to the device (may return before it is done; run
+    // ndev devices (realign sharded by interval ranges): the work intervals are cut into ndev
+    // contiguous ranges balanced by toClean reads, and device g runs phase B + C of range g; the host phases
+    // (binning, decisions, the mate-fixing writer) run once over the whole input, so the result is the
+    // one-device result for any input -- a single contig included -- with no writer state to hand across a cut.
+    int ndev = 1;
+    // Start copying the record arena [lo, hi) of `recs` to device g (may return before it is done; run
     // waits for it).  Offsets in DevPrepBatch::rec are relative to lo.
-    std::function<int(const uint8_t *recs, uint64_t lo, uint64_t hi)> stage;
-    std::function<int(const DevPrepBatch &, DevPrepOut &)> run;
+    std::function<int(int g, const uint8_t *recs, uint64_t lo, uint64_t hi)> stage;
+    std::function<int(int g, const DevPrepBatch &, DevPrepOut &)> run;  // called concurrently for the devices
 };
 
 struct RealignParams {

@@ -508,13 +508,16 @@ void oge_realign_opts_init(oge_realign_opts *o) {
     o->threads = 0;
 }
 
-int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len, const uint8_t *recs, const uint64_t *rec_off,
-                     uint64_t n, const char *fasta_path, const char *intervals_path, const oge_realign_opts *opts,
-                     oge_realign_result **out) {
-    if (!ctx || !header_text || (!recs && n) || (!rec_off && n) || !fasta_path || !intervals_path || !out)
+static int localrealign_on(oge_ctx *const *ctxs, int G, const char *header_text, uint64_t header_len, const uint8_t *recs,
+                           const uint64_t *rec_off, uint64_t n, const char *fasta_path, const char *intervals_path,
+                           const oge_realign_opts *opts, oge_realign_result **out) {
+    oge_ctx *ctx = ctxs[0];
+    if (!header_text || (!recs && n) || (!rec_off && n) || !fasta_path || !intervals_path || !out)
         return oge_fail(ctx, OGE_ERR_ARG, "oge_localrealign: null argument");
+    for (int g = 0; g < G; ++g)
+        if (!ctxs[g]) return oge_fail(ctx, OGE_ERR_ARG, "oge_localrealign: null context");
     hipSetDevice(ctx->device);
-    ctx->reset_timing();
+    for (int g = 0; g < G; ++g) ctxs[g]->reset_timing();
     oge::BamHeaderModel h;
     std::string err;
     if (!h.parse(std::string(header_text, header_len), err)) return oge_fail(ctx, OGE_ERR_ARG, ("oge_localrealign: " + err).c_str());
@@ -546,33 +549,42 @@ int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len,
         if (!scan_rc) oge_ctx_timing(ctx, "realign_scan", &scan_kernel_ms);
         return scan_rc;
     };
-    // phase B on the device (realign_prep.hip; OGE_REALIGN_DEVICE_PREP=0: the host threads): the record arena is
-    // copied by a helper thread while the host loads the FASTA, decodes and bins
+    // phase B on the device(s) (realign_prep.hip; OGE_REALIGN_DEVICE_PREP=0: the host threads): the record
+    // arena is copied to every device by a helper thread while the host loads the FASTA, decodes and bins
     struct Stager {
-        oge_ctx *ctx;
         std::thread th;
         uint8_t *d = nullptr;
         hipError_t e = hipSuccess;
         ~Stager() {
             if (th.joinable()) th.join();
         }
-    } stg{ctx};
-    int prep_rc = 0;
+    };
+    std::vector<Stager> stg((size_t)G);
+    std::vector<int> prep_rcs((size_t)G, 0);
     oge::DevPrep dp;
-    dp.stage = [&](const uint8_t *rp, uint64_t lo, uint64_t hi) -> int {
-        stg.d = (uint8_t *)ctx->ws("rp_recs", hi - lo + 64);
-        if (!stg.d) return prep_rc = OGE_ERR_HIP;
-        const int dev = ctx->device;
-        stg.th = std::thread([&stg, rp, lo, hi, dev]() {
+    dp.ndev = G;
+    dp.stage = [&](int g, const uint8_t *rp, uint64_t lo, uint64_t hi) -> int {
+        oge_ctx *c = ctxs[g];
+        Stager &sg = stg[(size_t)g];
+        (void)hipSetDevice(c->device);
+        sg.d = (uint8_t *)c->ws("rp_recs", hi - lo + 64);
+        if (!sg.d) return prep_rcs[(size_t)g] = OGE_ERR_HIP;
+        const int dev = c->device;
+        sg.th = std::thread([&sg, rp, lo, hi, dev]() {
             (void)hipSetDevice(dev);
-            stg.e = hipMemcpy(stg.d, rp + lo, hi - lo, hipMemcpyHostToDevice);
+            sg.e = hipMemcpy(sg.d, rp + lo, hi - lo, hipMemcpyHostToDevice);
         });
+        (void)hipSetDevice(ctx->device);
         return 0;
     };
-    dp.run = [&](const oge::DevPrepBatch &B, oge::DevPrepOut &O) -> int {
-        if (stg.th.joinable()) stg.th.join();
-        if (stg.e != hipSuccess) return prep_rc = oge_fail(ctx, OGE_ERR_HIP, (std::string("realign: record upload: ") + hipGetErrorString(stg.e)).c_str());
-        return prep_rc = oge_realign_prep_run(ctx, stg.d, B, O);
+    dp.run = [&](int g, const oge::DevPrepBatch &B, oge::DevPrepOut &O) -> int {
+        oge_ctx *c = ctxs[g];
+        Stager &sg = stg[(size_t)g];
+        if (sg.th.joinable()) sg.th.join();
+        (void)hipSetDevice(c->device);
+        int &rc = prep_rcs[(size_t)g];
+        if (sg.e != hipSuccess) return rc = oge_fail(c, OGE_ERR_HIP, (std::string("realign: record upload: ") + hipGetErrorString(sg.e)).c_str());
+        return rc = oge_realign_prep_run(c, sg.d, B, O);
     };
     const char *pe = getenv("OGE_REALIGN_DEVICE_PREP");
     const bool use_dev = !(pe && pe[0] == '0');
@@ -582,12 +594,27 @@ int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len,
     int rc = oge::realign_run(names, recs, rec_off, n, fasta_path, intervals_path, P, scan, r->recs, r->offs, st, err,
                               use_dev ? &dp : nullptr);
     st.t_run = std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
-    if (stg.th.joinable()) stg.th.join();
-    if (rc) return scan_rc ? scan_rc : prep_rc ? prep_rc : oge_fail(ctx, rc, ("oge_localrealign: " + err).c_str());
+    for (auto &sg : stg)
+        if (sg.th.joinable()) sg.th.join();
+    (void)hipSetDevice(ctx->device);
+    if (rc) {
+        if (scan_rc) return scan_rc;
+        for (int g = 0; g < G; ++g)
+            if (prep_rcs[(size_t)g]) {
+                if (g) oge_fail(ctx, prep_rcs[(size_t)g], oge_last_error(ctxs[g]));
+                return prep_rcs[(size_t)g];
+            }
+        return oge_fail(ctx, rc, ("oge_localrealign: " + err).c_str());
+    }
     double prep_ms = 0;
-    oge_ctx_timing(ctx, "realign_scan", &scan_kernel_ms);
-    if (scan_kernel_ms < 0) scan_kernel_ms = 0;
-    oge_ctx_timing(ctx, "realign_prep", &prep_ms);
+    scan_kernel_ms = 0;
+    for (int g = 0; g < G; ++g) {  // summed over the devices
+        double a = 0, b = 0;
+        oge_ctx_timing(ctxs[g], "realign_scan", &a);
+        oge_ctx_timing(ctxs[g], "realign_prep", &b);
+        scan_kernel_ms += a > 0 ? a : 0.0;
+        prep_ms += b > 0 ? b : 0.0;
+    }
     st.more.emplace_back("prep_kernel_ms", prep_ms > 0 ? prep_ms : 0.0);
     st.more.emplace_back("device_prep", use_dev ? 1.0 : 0.0);
     char buf[2048];
@@ -612,6 +639,20 @@ int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len,
     }
     *out = r.release();
     return OGE_OK;
+}
+
+int oge_localrealign(oge_ctx *ctx, const char *header_text, uint64_t header_len, const uint8_t *recs, const uint64_t *rec_off,
+                     uint64_t n, const char *fasta_path, const char *intervals_path, const oge_realign_opts *opts,
+                     oge_realign_result **out) {
+    if (!ctx) return oge_fail(nullptr, OGE_ERR_ARG, "oge_localrealign: null context");
+    return localrealign_on(&ctx, 1, header_text, header_len, recs, rec_off, n, fasta_path, intervals_path, opts, out);
+}
+
+int oge_localrealign_multi(oge_ctx *const *ctxs, int n_ctx, const char *header_text, uint64_t header_len, const uint8_t *recs,
+                           const uint64_t *rec_off, uint64_t n, const char *fasta_path, const char *intervals_path,
+                           const oge_realign_opts *opts, oge_realign_result **out) {
+    if (!ctxs || n_ctx < 1 || !ctxs[0]) return oge_fail(nullptr, OGE_ERR_ARG, "oge_localrealign_multi: no contexts");
+    return localrealign_on(ctxs, n_ctx, header_text, header_len, recs, rec_off, n, fasta_path, intervals_path, opts, out);
 }
 
 uint64_t oge_realign_result_count(const oge_realign_result *r) { return r && !r->offs.empty() ? r->offs.size() - 1 : 0; }

@@ -247,6 +247,8 @@ def lib() -> C.CDLL:
         "oge_host_free": (C.c_int, [vp, vp]),
         "oge_realign_opts_init": (None, [vp]),
         "oge_localrealign": (C.c_int, [vp, C.c_char_p, u64, vp, vp, u64, C.c_char_p, C.c_char_p, vp, C.POINTER(vp)]),
+        "oge_localrealign_multi": (C.c_int, [vp, C.c_int, C.c_char_p, u64, vp, vp, u64, C.c_char_p, C.c_char_p, vp,
+                                             C.POINTER(vp)]),
         "oge_realign_result_count": (u64, [vp]),
         "oge_realign_result_records": (vp, [vp, C.POINTER(u64)]),
         "oge_realign_result_offsets": (vp, [vp]),
@@ -598,15 +600,23 @@ class Context:
         return bi[:n], bs[:n]
 
     def localrealign(self, header_text: str, recs: np.ndarray, offs: np.ndarray, n: int, fasta: str, intervals: str,
-                     opts: RealignOpts | None = None) -> tuple[np.ndarray, np.ndarray, dict]:
+                     opts: RealignOpts | None = None, more: "list[Context] | None" = None) -> tuple[np.ndarray, np.ndarray, dict]:
         """LocalRealignment over coordinate-sorted records -> (out recs, out offsets[n+1], stats).
-        The arrays are read-only-by-convention views of the library's result buffer (no copy)."""
+        The arrays are read-only-by-convention views of the library's result buffer (no copy).  more: further
+        contexts -- the device work is then spread over [self] + more by interval ranges
+        (oge_localrealign_multi)."""
         import json
         L = lib()
         hb = header_text.encode()
         res = C.c_void_p()
-        check(L.oge_localrealign(self.h, hb, len(hb), _ptr(recs), _ptr(offs), n, fasta.encode(), intervals.encode(),
-                                 C.byref(opts) if opts is not None else None, C.byref(res)), self.h)
+        if more:
+            hs = (C.c_void_p * (1 + len(more)))(self.h.value, *[c.h.value for c in more])
+            check(L.oge_localrealign_multi(hs, len(hs), hb, len(hb), _ptr(recs), _ptr(offs), n, fasta.encode(),
+                                           intervals.encode(), C.byref(opts) if opts is not None else None, C.byref(res)),
+                  self.h)
+        else:
+            check(L.oge_localrealign(self.h, hb, len(hb), _ptr(recs), _ptr(offs), n, fasta.encode(), intervals.encode(),
+                                     C.byref(opts) if opts is not None else None, C.byref(res)), self.h)
         holder = _RealignResult(res)  # frees the result when the last view goes away
         cnt = int(L.oge_realign_result_count(res))
         nb = C.c_uint64()

@@ -210,14 +210,27 @@ def test_cli_gpus_matches_reference(case, tmp_path, G):
     assert len(offs) == case.n - case.meta["sortdedup_v"]["n_dup"]
 
 
-@pytest.mark.parametrize("name", ["rl_small", "rl_edge"])
-def test_cli_localrealign_gpus_matches_reference(name, tmp_path):
-    """localrealign --gpus 2: contig-range shards (whole contigs per rank), concatenated."""
+@pytest.mark.parametrize("G", [2, 4, 8])
+@pytest.mark.parametrize("name", ["rl_short", "rl_small", "rl_c5_2k"])
+def test_cli_localrealign_gpus_matches_reference(name, G, tmp_path):
+    """localrealign --gpus G: the device work sharded over G ranks by interval
+    ranges (oge_localrealign_multi) -- rl_short is ONE contig, so the cuts fall inside it -- equals the
+    reference's output; every rank gets a share of the intervals, within 10 % of the mean on the C5-shaped
+    set (ranges balanced by reads)."""
+    import json
     meta, arrays, h, recs, offs, fa, iv = load_rl_case(name, tmp_path)
-    run("localrealign", "--nopg", "--gpus", 2, "-R", fa, "-L", iv, tmp_path / "reads.bam", "-o", tmp_path / "rl.bam")
+    r = run("localrealign", "-v", "--nopg", "--gpus", G, "-R", fa, "-L", iv, tmp_path / "reads.bam", "-o", tmp_path / "rl.bam")
     oh, _, orecs, ooffs = bamutil.read_bam(tmp_path / "rl.bam")
     assert oh == meta["output_header"]
     check_output(meta, arrays, orecs, np.append(ooffs, np.uint64(len(orecs))))
+    line = [l for l in r.stderr.splitlines() if f"LocalRealignment over {G} devices" in l]
+    assert line, r.stderr
+    st = json.loads(line[0].split(": ", 1)[1])
+    iv_per = [st[f"prep_rank{g}_intervals"] for g in range(G)]
+    assert sum(iv_per) == st["prep_device_intervals"] and st["prep_host_intervals"] == 0 and min(iv_per) > 0
+    if name == "rl_c5_2k":
+        mean = sum(iv_per) / G
+        assert max(iv_per) <= 1.1 * mean and min(iv_per) >= 0.9 * mean, iv_per
 
 
 def test_cli_chunked_matches_reference(case, tmp_path):

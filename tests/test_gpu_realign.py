@@ -135,3 +135,20 @@ def test_gpu_device_consensus_generation_stress(ctx, tmp_path, monkeypatch, seed
     offs = np.append(b.offs, np.uint64(b.recs.size))
     st = _realign_both(ctx, monkeypatch, b.header_text, b.recs, offs, fa, iv)
     assert st["prep_device_intervals"] > 0 and st["scan_pairs"] > 0
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+@pytest.mark.parametrize("name", ["rl_short", "rl_c5_2k"])
+def test_gpu_realign_interval_sharded_over_contexts(ctx, tmp_path, name, G):
+    """oge_localrealign_multi: phase B + C over G contexts (one device here; G devices on a node) by interval
+    ranges -- inside the one contig of rl_short -- equals the reference's output."""
+    from openge_amd import lib as L
+    meta, arrays, h, recs, offs, fa, iv = load_rl_case(name, tmp_path)
+    more = [L.Context(0) for _ in range(G - 1)]
+    try:
+        out, oo, st = ctx.localrealign(h, recs, offs, len(offs) - 1, fa, iv, more=more)
+        check_output(meta, arrays, out, oo)
+        assert st["prep_devices"] == G and all(st[f"prep_rank{g}_intervals"] > 0 for g in range(G))
+    finally:
+        for c in more:
+            c.close()
