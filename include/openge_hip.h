@@ -220,16 +220,21 @@ int oge_comm_unique_id(uint8_t *id_out, uint64_t bytes);
  * process sees >= nranks devices, else compares the ranks' PCI bus ids in the shared segment
  * (OGE_COMM_DIR, default /dev/shm or /tmp; OGE_COMM_STAGE_MB per-rank staging, default 32). */
 int oge_comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, oge_comm **out);
-/* The same with the transport chosen by the caller (mode "auto" | "rccl" | "host"; NULL = OGE_COMM).
- * In auto mode with fewer visible devices than ranks, the shared-segment meeting is tried only when
- * the launcher says every rank is on this node (LOCAL_WORLD_SIZE / OMPI_COMM_WORLD_LOCAL_SIZE /
- * MPI_LOCALNRANKS == nranks); otherwise RCCL, the only transport that reaches other hosts.  The CLI,
- * whose ranks are threads of one process, passes "host" when they share a device. */
+/* The same with the transport chosen by the caller (mode "auto" | "rccl" | "host" | "node"; NULL =
+ * OGE_COMM).  In auto mode with fewer visible devices than ranks, the shared-segment meeting is tried
+ * only when the launcher says every rank is on this node (LOCAL_WORLD_SIZE / OMPI_COMM_WORLD_LOCAL_SIZE /
+ * MPI_LOCALNRANKS == nranks); otherwise RCCL, the only transport that reaches other hosts.  "node" =
+ * OGE_COMM's choice with every rank known to be on this node.  The CLI, whose ranks are threads of one
+ * process, passes "host" when they share a device, else "node".  RCCL ranks on one node exchange their
+ * small host-side values (statuses, counts, splitter samples) through a shared segment instead of a
+ * device round trip (OGE_COMM_HOSTX=0: the device round trip). */
 int oge_comm_init_rank_mode(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, const char *mode, oge_comm **out);
 /* Per-exchange record of the communicator's last oge_sort_markdup_dist / oge_mergesort_bgzf_dist /
  * oge_mergesort_bgzf_shard / oge_bgzf_decode_shard call:
- * a JSON array of {tag, calls, bytes_sent, bytes_recv, bytes_self, ms} (bytes to / from other ranks and
- * kept on this rank; host wall time of the collectives, waiting for peers included).  Returns the JSON
+ * a JSON array of {tag, calls, bytes_sent, bytes_recv, bytes_self, ms, device_ms, mode} (bytes to / from
+ * other ranks and kept on this rank; host wall time of the collectives, waiting for peers included; RCCL's
+ * time on its stream; mode: blocking | side_stream for device exchanges, host_memory | device_round_trip
+ * for the host-side allgathers).  Returns the JSON
  * length; writes it (NUL-terminated) when cap > length. */
 int64_t oge_comm_stats_json(const oge_comm *comm, char *buf, uint64_t cap);
 /* One process, n contexts in one call (test harness): RCCL when the contexts' devices are distinct,

@@ -76,6 +76,8 @@ struct OgeTransport {
     }
     // whether alltoallv_peers really runs beside the context stream (the default above does not)
     virtual bool overlaps() const { return false; }
+    // how allgather_host moves its bytes (the `mode` of its tags in the exchange stats)
+    virtual const char *gather_mode() const { return "host_memory"; }
 };
 
 // One exchange site of a step: bytes this rank sent to / received from other ranks (and kept), and the
@@ -193,6 +195,7 @@ struct oge_comm {
         const auto t0 = std::chrono::steady_clock::now();
         const int rc = tr->allgather_host(ctx, in, out, bytes);
         OgeXchg &x = stat(tag);
+        x.mode = tr->gather_mode();
         x.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         x.calls++;
         x.sent += bytes * (tr->size - 1);
@@ -321,9 +324,17 @@ struct ShmTransport : OgeTransport {
 
 struct RcclTransport : OgeTransport {
     ncclComm_t comm = nullptr;
+    // The small host-side exchanges (statuses, per-destination counts, splitter samples) go through host
+    // memory when every rank is on this node (r06): the node's shared segment for ranks
+    // in separate processes, the in-process hub for oge_comm_init's ranks.  Otherwise (ranks on several
+    // hosts) a device round trip through ncclAllGather.
+    std::unique_ptr<oge_dist::ShmSeg> hx_seg;
+    std::shared_ptr<oge_dist::Hub> hx_hub;
     ~RcclTransport() override {
+        hx_seg.reset();
         if (comm) ncclCommDestroy(comm);
     }
+    const char *gather_mode() const override { return hx_seg || hx_hub ? "host_memory" : "device_round_trip"; }
     const char *name() const override { return "rccl"; }
     int alltoallv(oge_ctx *ctx, const void *send, const uint64_t *sbytes, const uint64_t *soff, void *recv, const uint64_t *rbytes,
                   const uint64_t *roff) override {
@@ -350,6 +361,16 @@ struct RcclTransport : OgeTransport {
     }
     bool overlaps() const override { return true; }
     int allgather_host(oge_ctx *ctx, const void *in, void *out, size_t bytes) override {
+        if (hx_hub) {
+            HipOps ops{ctx};
+            oge_dist::LocalColl<HipOps> c{*hx_hub, rank, ops};
+            return c.allgather_host(in, out, bytes);
+        }
+        if (hx_seg) {
+            StageOps ops{ctx};
+            oge_dist::ShmColl<StageOps> c{*hx_seg, ops};
+            return c.allgather_host(in, out, bytes) ? oge_fail(ctx, OGE_ERR_HIP, "rccl transport: host allgather timed out") : OGE_OK;
+        }
         uint8_t *d = (uint8_t *)ctx->ws("comm_allgather", bytes * size);
         if (!d) return OGE_ERR_HIP;
         OGE_HIP_TRY(ctx, hipMemcpyAsync(d + bytes * rank, in, bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -1083,27 +1104,36 @@ static int launcher_local_ranks() {
     return 0;
 }
 
+// OGE_COMM_HOSTX=0: RCCL's host exchanges take the device round trip even on one node
+static bool hostx_enabled() {
+    const char *e = getenv("OGE_COMM_HOSTX");
+    return !(e && *e == '0');
+}
+
 // Transport of one rank.  mode: "rccl", "host" or "auto" (nullptr / "": OGE_COMM, default auto).  RCCL
 // between distinct GPUs, the host-staged transport (dist_shm.h) when ranks share one.  auto: a process
 // that sees at least `nranks` devices takes RCCL at once (bench.py / the CLI give rank r device r %
 // count).  With fewer visible devices than ranks, the shared-segment meeting (which compares the ranks'
 // PCI bus ids: all distinct -> RCCL, else host) is only tried when every rank is known to be on this
 // node -- the launcher's local rank count equals nranks (torchrun's LOCAL_WORLD_SIZE, ...), or the caller
-// runs every rank itself (the CLI's threads pass "host"); otherwise (a multi-node job, 2 x 8 GPUs with a
-// device-isolating launcher) RCCL, which is the only transport that reaches other hosts.
+// runs every rank itself (the CLI's threads pass "host" when ranks share devices, else "node" = auto on one
+// node); otherwise (a multi-node job, 2 x 8 GPUs with a device-isolating launcher) RCCL, which is the only
+// transport that reaches other hosts.  RCCL ranks known to be on one node also meet in a small shared
+// segment for their host exchanges (RcclTransport::hx_seg; OGE_COMM_HOSTX=0 turns that off).
 static int comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id, const char *want, oge_comm **out) {
     if (!ctx || !id || !out || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
         return oge_fail(ctx, OGE_ERR_ARG, "oge_comm_init_rank: bad arguments");
     (void)hipSetDevice(ctx->device);
-    const char *e = want && *want ? want : getenv("OGE_COMM");
+    const bool node = want && !strcmp(want, "node");  // the caller runs every rank on this node (the CLI's threads)
+    const char *e = want && *want && !node ? want : getenv("OGE_COMM");
     std::string mode = e && *e ? e : "auto";
     if (mode == "local") mode = "host";  // oge_comm_init's in-process name for "ranks share a GPU"
+    const bool one_node = node || launcher_local_ranks() == nranks;
     if (mode != "auto" && mode != "rccl" && mode != "host")
         return oge_fail(ctx, OGE_ERR_ARG, "OGE_COMM must be auto, rccl or host");
     int ndev = 0;
     (void)hipGetDeviceCount(&ndev);
-    std::unique_ptr<oge_dist::ShmSeg> seg;
-    const bool one_node = launcher_local_ranks() == nranks;
+    std::unique_ptr<oge_dist::ShmSeg> seg, hx;
     if (mode == "host" || (mode == "auto" && ndev < nranks && one_node)) {
         char bus[64] = {0};
         (void)hipDeviceGetPCIBusId(bus, sizeof bus - 1, ctx->device);
@@ -1120,7 +1150,8 @@ static int comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id,
         bool shared = false;
         for (int a = 0; a < nranks; ++a)
             for (int b = a + 1; b < nranks; ++b) shared = shared || !strcmp(seg->post(a).bus, seg->post(b).bus);
-        if (mode == "auto" && !shared) seg.reset();  // distinct GPUs: RCCL after all
+        if (mode == "auto" && !shared) hx = std::move(seg);  // distinct GPUs: RCCL after all (the segment stays for
+                                                             // the host exchanges)
     }
     oge_comm *c = new oge_comm();
     c->ctx = ctx;
@@ -1144,6 +1175,30 @@ static int comm_init_rank(oge_ctx *ctx, int nranks, int rank, const uint8_t *id,
         }
         t->rank = rank;
         t->size = nranks;
+        if (one_node && hostx_enabled()) {
+            // the host exchanges' segment (RcclTransport::hx_seg): met right after ncclCommInitRank, which every
+            // rank has passed, so the meeting takes milliseconds (bounded at 60 s); then one allreduce makes
+            // every rank take the same route
+            if (!hx) {
+                char bus[64] = {0};
+                (void)hipDeviceGetPCIBusId(bus, sizeof bus - 1, ctx->device);
+                uint64_t h = 1469598103934665603ull;
+                for (size_t i = 0; i < sizeof(ncclUniqueId) + kIdNonce; ++i) h = (h ^ id[i]) * 1099511628211ull;
+                char name[64];
+                snprintf(name, sizeof name, "oge_hx_%016llx", (unsigned long long)h);
+                std::string err;
+                hx.reset(oge_dist::ShmSeg::open(name, nranks, rank, 1ull << 20, bus, &err, 60.0));
+            }
+            int have = hx ? 1 : 0;
+            int *d = (int *)ctx->ws("comm_hx_agree", sizeof(int));
+            if (!d || hipMemcpyAsync(d, &have, sizeof have, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+                ncclAllReduce(d, d, 1, ncclInt32, ncclMin, t->comm, ctx->stream) != ncclSuccess ||
+                hipMemcpyAsync(&have, d, sizeof have, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                hipStreamSynchronize(ctx->stream) != hipSuccess)
+                have = 0;
+            if (!have) hx.reset();
+            t->hx_seg = std::move(hx);
+        }
         c->tr = std::move(t);
     }
     *out = c;
@@ -1185,11 +1240,14 @@ int oge_comm_init(oge_ctx **ctxs, int n, oge_comm **out) {
     for (int g = 0; g < n; ++g) devs[g] = ctxs[g]->device;
     ncclResult_t r = ncclCommInitAll(cs.data(), n, devs.data());
     if (r != ncclSuccess) return oge_fail(nullptr, OGE_ERR_HIP, (std::string("ncclCommInitAll: ") + ncclGetErrorString(r)).c_str());
+    // the ranks are threads of this process: their host exchanges meet at one hub (RcclTransport::hx_hub)
+    std::shared_ptr<oge_dist::Hub> hx_hub = hostx_enabled() ? std::make_shared<oge_dist::Hub>(n) : nullptr;
     for (int g = 0; g < n; ++g) {
         auto t = std::make_unique<RcclTransport>();
         t->comm = cs[g];
         t->rank = g;
         t->size = n;
+        t->hx_hub = hx_hub;
         out[g] = new oge_comm();
         out[g]->ctx = ctxs[g];
         out[g]->tr = std::move(t);

@@ -115,8 +115,10 @@ public:
     }
 
     // Every rank calls open with the same name; returns after all G ranks have joined (or nullptr on a
-    // failure / timeout, with *err set).  The file is unlinked once everyone has it mapped.
-    static ShmSeg *open(const std::string &name, int G, int rank, uint64_t W, const char *bus, std::string *err) {
+    // failure / timeout, with *err set).  The file is unlinked once everyone has it mapped.  meet_s > 0 bounds
+    // the wait for the others (else OGE_COMM_TIMEOUT).
+    static ShmSeg *open(const std::string &name, int G, int rank, uint64_t W, const char *bus, std::string *err,
+                        double meet_s = 0) {
         if (G < 1 || G > kShmMaxRanks || rank < 0 || rank >= G) {
             *err = "host transport: bad rank / size";
             return nullptr;
@@ -169,7 +171,7 @@ public:
         for (uint64_t it = 0; s->ctl_->joined.load(std::memory_order_acquire) < (uint32_t)G; ++it) {
             // a rank that joined last and exited at once is not a failure of the meeting (the next
             // barrier sees it): re-check the count after a failed wait
-            if (s->waited_too_long(t0, it) && s->ctl_->joined.load(std::memory_order_acquire) < (uint32_t)G) {
+            if (s->waited_too_long(t0, it, meet_s) && s->ctl_->joined.load(std::memory_order_acquire) < (uint32_t)G) {
                 if (rank == 0) unlink(path.c_str());
                 *err = "host transport: not every rank joined " + path + " in time";
                 delete s;
@@ -208,7 +210,7 @@ public:
     }
 
 private:
-    bool waited_too_long(std::chrono::steady_clock::time_point t0, uint64_t it) {
+    bool waited_too_long(std::chrono::steady_clock::time_point t0, uint64_t it, double limit_s = 0) {
         if (it < 4096) {
             sched_yield();
             return false;
@@ -216,7 +218,7 @@ private:
         std::this_thread::sleep_for(std::chrono::microseconds(50));
         if ((it & 1023) != 0) return false;
         if (peer_gone()) return true;
-        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s();
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > (limit_s > 0 ? limit_s : timeout_s());
     }
     bool peer_gone() {  // a rank that posted its pid and whose process has exited
         const auto now = std::chrono::steady_clock::now();

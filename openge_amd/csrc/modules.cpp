@@ -96,7 +96,7 @@ int ChainContext::init_ranks() {
             ts.emplace_back([&, g]() {
                 // every rank is a thread of this process: the shared-segment meeting is node-local by
                 // construction, so ranks sharing a device take the host transport
-                rcs[g] = oge_comm_init_rank_mode(rank_ctx[g], gpus, g, id.data(), gpus > ndev ? "host" : nullptr, &comms[g]);
+                rcs[g] = oge_comm_init_rank_mode(rank_ctx[g], gpus, g, id.data(), gpus > ndev ? "host" : "node", &comms[g]);
                 if (rcs[g]) why[g] = oge_last_error(rank_ctx[g]);
             });
         for (auto &t : ts) t.join();

@@ -31,6 +31,12 @@
 
 namespace oge {
 
+// The first call in a process touches every page of its per-read arrays for the first time (the scratch
+// keeps them for later calls): those are hvectors (uvector.h: 2 MiB pages, no serial zero fill on a
+// resize -- the workers that fill them touch their pages first).
+template <class T>
+using BigVec = hvector<T>;
+
 // =====================================================================================  threads
 // Persistent workers (kept across calls with the run's Scratch).  run_static maps index i to worker
 // i % size(); run hands indices out one at a time (prepare and decide: intervals differ in size; r03
@@ -369,7 +375,13 @@ static void tag_edit_i32(std::string &t, const char *tag, int32_t v) {
 // the raw bytes (case preserved).
 struct Fasta {
     std::unordered_map<std::string, std::string> seq;
-    std::string data;  // the file (kept, like the sequences' storage, for the next load: see Scratch)
+    BigVec<char> data;  // the file (kept, like the sequences' storage, for the next load: see Scratch; no zero
+                        // fill on a resize, the workers' preads touch its pages first)
+    size_t find_nl(size_t from) const {
+        if (from >= data.size()) return std::string::npos;
+        const void *q = memchr(data.data() + from, '\n', data.size() - from);
+        return q ? (size_t)((const char *)q - data.data()) : std::string::npos;
+    }
     // Whole file in one read; contigs (">" lines) located serially, their bodies de-lined in
     // parallel.  Line handling as FastaReader: name up to the first blank, CR before LF dropped.
     bool load(const std::string &path, std::string &err, Pool &pool) {
@@ -406,7 +418,7 @@ struct Fasta {
         }
         char buf[1 << 16];
         size_t k;
-        while ((k = fread(buf, 1, sizeof buf, f)) > 0) data.append(buf, k);  // non-seekable input
+        while ((k = fread(buf, 1, sizeof buf, f)) > 0) data.insert(data.end(), buf, buf + k);  // non-seekable input
         fclose(f);
         std::vector<size_t> hs;
         const char *b = data.data(), *e = b + data.size();
@@ -418,11 +430,11 @@ struct Fasta {
         std::vector<size_t> les(hs.size());
         for (size_t c = 0; c < hs.size(); ++c) {
             const size_t h = hs[c], stop = c + 1 < hs.size() ? hs[c + 1] : data.size();
-            size_t le = data.find('\n', h);
+            size_t le = find_nl(h);
             if (le == std::string::npos || le > stop) le = stop;
             size_t ne = h + 1;
             while (ne < le && data[ne] != ' ' && data[ne] != '\t' && data[ne] != '\r') ++ne;
-            names[c].assign(data, h + 1, ne - h - 1);
+            names[c].assign(data.data() + h + 1, ne - h - 1);
             les[c] = le;
         }
         std::unordered_map<std::string, size_t> last;
@@ -439,11 +451,11 @@ struct Fasta {
             out.reserve(stop > le ? stop - le : 0);
             size_t p = le + 1;
             while (p < stop) {
-                size_t q = data.find('\n', p);
+                size_t q = find_nl(p);
                 if (q == std::string::npos || q > stop) q = stop;
                 size_t qe = q;
                 if (qe > p && data[qe - 1] == '\r') --qe;
-                out.append(data, p, qe - p);
+                out.append(data.data() + p, qe - p);
                 p = q + 1;
             }
         });
@@ -1118,7 +1130,7 @@ private:
 class MateFixer {
 public:
     // `counter` = reads added before this one's first (EMIT_FREQUENCY counts the whole stream)
-    MateFixer(const RealignParams &P, std::vector<RRead *> &out, uint64_t counter = 0) : P_(P), out_(out), counter_(counter) {}
+    MateFixer(const RealignParams &P, BigVec<RRead *> &out, uint64_t counter = 0) : P_(P), out_(out), counter_(counter) {}
     size_t waiting() const { return waiting_.size(); }
 
     // canMoveReads (:245-251)
@@ -1255,7 +1267,7 @@ private:
     }
 
     const RealignParams &P_;
-    std::vector<RRead *> &out_;
+    BigVec<RRead *> &out_;
     uint64_t counter_ = 0;
     WaitQueue waiting_;
     MateTable mates_;
@@ -1324,14 +1336,14 @@ struct Scratch {
     std::unique_ptr<Pool> pool;
     RRead *rmem = nullptr;  // the decoded records: [0, rlive) constructed and kept across calls (the decode
     uint64_t rcap = 0, rlive = 0;  // overwrites every field; cigar / owned-tag storage is reused)
-    std::vector<int32_t> lstop;
-    std::vector<uint8_t> dnc;
+    BigVec<int32_t> lstop;
+    BigVec<uint8_t> dnc;
     std::vector<std::unique_ptr<IntervalData>> ids;
-    std::vector<Event> ev;
+    BigVec<Event> ev;
     std::vector<IntervalData *> work;
     ScanBatch B;
-    std::vector<int32_t> bidx, bscore;
-    std::vector<RRead *> order;
+    hvector<int32_t> bidx, bscore;
+    BigVec<RRead *> order;
     std::vector<DevPrepBatch> DB;  // phase B on the devices: their inputs and results
     std::vector<DevPrepOut> DO;
     Fasta fa;
@@ -1424,7 +1436,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         S.rlive = 0;
         std::free(S.rmem);
         S.rcap = 0;
-        S.rmem = (RRead *)std::malloc(std::max<uint64_t>(n, 1) * sizeof(RRead));
+        S.rmem = (RRead *)big_alloc(std::max<uint64_t>(n, 1) * sizeof(RRead));
         if (!S.rmem) {
             err = "out of host memory for the decoded records";
             return -1;
@@ -1445,8 +1457,8 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     std::mutex emu;
     std::string derr;
     // decode, plus what binning asks of every read (its GenomeLoc stop, doNotTryToClean)
-    std::vector<int32_t> &lstop = S.lstop;  // (every entry written by the decode below)
-    std::vector<uint8_t> &dnc = S.dnc;
+    BigVec<int32_t> &lstop = S.lstop;  // (every entry written by the decode below)
+    BigVec<uint8_t> &dnc = S.dnc;
     lstop.resize(n);
     dnc.resize(n);
     pool.run_chunks(n, dchunk, [&](size_t b, size_t end) {
@@ -1480,8 +1492,9 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     // ---------------------------------------------------------------- A: map_func (:455-553)
     std::vector<std::unique_ptr<IntervalData>> &ids = S.ids;  // objects reused across calls
     size_t nids = 0;
-    std::vector<Event> &ev = S.ev;
+    BigVec<Event> &ev = S.ev;
     ev.clear();
+    ev.reserve(n + 2 * ivs.size() + 16);  // a read is one event at most, an interval two (no regrowth copies)
     auto new_id = [&](int interval) {
         if (nids == ids.size()) ids.emplace_back(new IntervalData());
         IntervalData *d = ids[nids++].get();
@@ -1592,7 +1605,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     std::vector<const DevPrepRead *> iv_reads(nw, nullptr);  // interval w's first read result
     std::vector<int64_t> iv_traw(nw, 0);
     std::vector<uint64_t> iv_pbase(nw, 0);
-    std::vector<int32_t> dev_bi, dev_bs;
+    hvector<int32_t> dev_bi, dev_bs;
     uint64_t n_dev_iv = 0, ndev_pairs = 0;
     const int G = dev ? std::max(1, dev->ndev) : 0;
     if (dev && nw) {
@@ -1659,8 +1672,13 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
                 iv_traw[w] = O.iv_total_raw[k];
                 iv_pbase[w] = ndev_pairs + O.iv_pair_base[k];
             }
-            dev_bi.insert(dev_bi.end(), O.best_index.begin(), O.best_index.end());
-            dev_bs.insert(dev_bs.end(), O.best_score.begin(), O.best_score.end());
+            if (G == 1) {  // the one device's results taken as they are (their buffers come back next call)
+                dev_bi.swap(S.DO[0].best_index);
+                dev_bs.swap(S.DO[0].best_score);
+            } else {
+                dev_bi.insert(dev_bi.end(), O.best_index.begin(), O.best_index.end());
+                dev_bs.insert(dev_bs.end(), O.best_score.begin(), O.best_score.end());
+            }
             ndev_pairs += O.pairs;
             if (G > 1) {
                 const std::string pfx = "prep_rank" + std::to_string(g) + "_";
@@ -1849,9 +1867,13 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     for (uint64_t o : wops) st.scan_ops += o;
     st.scan_pairs = ndev + B.pairs.size();
     st.t_scan_build = now_s() - t2;
-    std::vector<int32_t> &bidx = S.bidx, &bscore = S.bscore;
+    hvector<int32_t> &bidx = S.bidx, &bscore = S.bscore;
     bidx.swap(dev_bi);
     bscore.swap(dev_bs);
+    if (G == 1 && nw && !S.DO.empty()) {  // the previous call's buffers back to the device's result slot (capacity kept)
+        S.DO[0].best_index.swap(dev_bi);
+        S.DO[0].best_score.swap(dev_bs);
+    }
     if (!B.pairs.empty()) {
         std::vector<int32_t> hi, hs;
         int rc = scan(B, hi, hs);
@@ -1944,7 +1966,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     // each on its own writer whose EMIT_FREQUENCY counter starts where the stream's would be -- with
     // one exception: a flush that also finds >= maxRecordsInMemory reads waiting keeps the modified
     // mate entries.  A segment ending that way sends the whole phase to the sequential path.
-    auto emit_events = [&](size_t e0, size_t e1, uint64_t add0, std::vector<RRead *> &ord, uint64_t &cl, uint64_t &rr) {
+    auto emit_events = [&](size_t e0, size_t e1, uint64_t add0, BigVec<RRead *> &ord, uint64_t &cl, uint64_t &rr) {
         MateFixer mf(P, ord, add0);
         for (size_t k = e0; k < e1; ++k) {
             const Event &e = ev[k];
@@ -1977,7 +1999,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     struct Seg {
         size_t e0, e1;
         uint64_t add0;
-        std::vector<RRead *> ord;
+        BigVec<RRead *> ord;
         uint64_t cl = 0, rr = 0;
         size_t left = 0;
     };
@@ -2067,7 +2089,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
             });
         }
     }
-    std::vector<RRead *> &order = S.order;
+    BigVec<RRead *> &order = S.order;
     order.clear();
     if (sequential) {
         order.reserve(n);
@@ -2084,7 +2106,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
         order.resize(at.back());
         pool.run(segs.size(), [&](size_t k) {
             std::copy(segs[k].ord.begin(), segs[k].ord.end(), order.begin() + (ptrdiff_t)at[k]);
-            std::vector<RRead *>().swap(segs[k].ord);
+            BigVec<RRead *>().swap(segs[k].ord);
         });
         st.more.emplace_back("t_mate_concat", now_s() - tc);
     }
@@ -2129,7 +2151,7 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     // call); the records and the large containers stay with the scratch (see Scratch)
     pool.run(nids, [&](size_t k) { ids[k]->reset(-1); });
     const double t6 = now_s();
-    for (auto &g : segs) std::vector<RRead *>().swap(g.ord);
+    for (auto &g : segs) BigVec<RRead *>().swap(g.ord);
     st.t_release = now_s() - t5;
     st.more.emplace_back("t_release_intervals", t6 - t5);
     st.more.emplace_back("t_release_reads", now_s() - t6);

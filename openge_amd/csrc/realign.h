@@ -190,11 +190,11 @@ typedef std::function<int(const ScanBatch &, std::vector<int32_t> &best_index, s
 // each interval's reference window and its toClean reads (record offsets into the arena it staged) and
 // gets back what phase D needs.
 struct DevPrepBatch {
-    uvector<uint8_t> ref;       // reference windows back to back (ReadBin::getReference: padded, upper-cased)
-    uvector<uint64_t> ref_off;  // n_iv + 1
-    uvector<uint64_t> rd_off;   // n_iv + 1: interval w's reads are rec[rd_off[w] .. rd_off[w + 1])
-    uvector<uint64_t> rec;      // toClean reads in interval order: byte offset of the record in the staged arena
-    uvector<int32_t> start;     // read pos - the interval's leftmost (startOnRef)
+    hvector<uint8_t> ref;       // reference windows back to back (ReadBin::getReference: padded, upper-cased)
+    hvector<uint64_t> ref_off;  // n_iv + 1
+    hvector<uint64_t> rd_off;   // n_iv + 1: interval w's reads are rec[rd_off[w] .. rd_off[w + 1])
+    hvector<uint64_t> rec;      // toClean reads in interval order: byte offset of the record in the staged arena
+    hvector<int32_t> start;     // read pos - the interval's leftmost (startOnRef)
 };
 // per toClean read (32 bytes): flags, the left-aligned cigar when the read has one, the sums
 enum : uint8_t { DP_SKIP = 1, DP_ALT = 2, DP_CAND = 4, DP_NEWCIG = 8, DP_KEPT = 16, DP_HOST = 32, DP_DUP = 64 };
@@ -212,11 +212,11 @@ struct DevPrepRead {
 };
 static_assert(sizeof(DevPrepRead) == 32, "DevPrepRead layout");
 struct DevPrepOut {
-    std::vector<DevPrepRead> reads;       // one per DevPrepBatch read
+    hvector<DevPrepRead> reads;           // one per DevPrepBatch read
     std::vector<uint8_t> iv_host;         // per interval: 1 = run phase B / C of this interval on the host
     std::vector<int64_t> iv_total_raw;    // per interval: sum of raw over non-duplicate altReads
     std::vector<uint64_t> iv_pair_base;   // per interval: its first pair in best_index / best_score
-    std::vector<int32_t> best_index, best_score;
+    hvector<int32_t> best_index, best_score;
     uint64_t pairs = 0, ops = 0;          // scan pairs, algorithmic compare-accumulates
     bool generic = false;                 // the byte-wise scan kernel ran
     double t_upload = 0, t_device = 0, t_download = 0;

@@ -726,7 +726,7 @@ int oge_realign_prep_run(oge_ctx *ctx, const uint8_t *d_recs, const oge::DevPrep
     const double t0 = clk();
     const uint32_t nw = (uint32_t)(B.rd_off.size() - 1);
     const uint64_t nr = B.rec.size();
-    O.reads.assign(nr, oge::DevPrepRead{});
+    O.reads.resize(nr);  // (every entry copied back from the device below)
     O.iv_host.assign(nw, 0);
     O.iv_total_raw.assign(nw, 0);
     O.iv_pair_base.assign(nw, 0);
@@ -815,8 +815,8 @@ int oge_realign_prep_run(oge_ctx *ctx, const uint8_t *d_recs, const oge::DevPrep
     ctx->end_stage(tm);
     const double t1 = clk();
     // the offset scan over the batch in place
-    O.best_index.assign(n_pairs, 0);
-    O.best_score.assign(n_pairs, 0);
+    O.best_index.resize(n_pairs);  // (written by the scan)
+    O.best_score.resize(n_pairs);
     RsDevBatch S{dc, dco, (uint32_t)n_cons, dcwo, cons_words, db, dq, dro, (uint32_t)n_reads, drwo, read_words, dp, n_pairs};
     if (n_pairs) {
         if ((rc = realign_scan_devbatch(ctx, S, O.best_index.data(), O.best_score.data(), &O.generic))) return rc;

@@ -299,13 +299,21 @@ def test_dist_uniform_key_pile(ctx, frac, G):
         assert sorted(counts)[-1] == n and sum(1 for c in counts if c) == 1
 
 
-@pytest.mark.parametrize("sort", [True, False])
-def test_rccl_transport_world1(ctx, sort):
+@pytest.mark.parametrize("sort,hostx", [(True, False), (False, False), (True, True), (False, True)])
+def test_rccl_transport_world1(ctx, sort, hostx, monkeypatch, tmp_path):
     """RcclTransport's three methods on the one-GPU box: a one-rank communicator forced onto RCCL
     (oge_comm_init_rank_mode "rccl": ncclCommInitRank with one rank) runs the whole distributed step --
-    all-to-all-v as grouped ncclSend / ncclRecv to itself, ncclAllGather for the plans and samples,
-    ncclReduceScatter(max) for the marks -- and must equal the one-GPU output (sort + dedup, and the
-    in-place dedup mode).  More ranks need more GPUs (RCCL refuses two ranks on one device)."""
+    all-to-all-v as grouped ncclSend / ncclRecv to itself, the plans and samples gathered, ncclReduceScatter
+    (max) for the marks -- and must equal the one-GPU output (sort + dedup, and the in-place dedup mode).
+    hostx: the launcher says every rank is on this node (LOCAL_WORLD_SIZE), so the statuses, plans and
+    samples go through the node's shared segment ("host_memory"); else through ncclAllGather and a device
+    round trip.  More ranks need more GPUs (RCCL refuses two ranks on one device)."""
+    monkeypatch.setenv("OGE_COMM_DIR", str(tmp_path))
+    for v in ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS", "SLURM_NTASKS_PER_NODE",
+              "SLURM_STEP_TASKS_PER_NODE"):
+        monkeypatch.delenv(v, raising=False)
+    if hostx:
+        monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
     p = L.synth_params(20000, preset="c2", seed=31)
     recs, offs, hdr = L.synth_host(p)
     n = len(offs) - 1
@@ -326,6 +334,8 @@ def test_rccl_transport_world1(ctx, sort):
         L.check(L.lib().oge_memcpy(c1.h, got.ctypes.data, d + int(oo[0]), got.size, 2), c1.h)
         ex = {e["tag"]: e for e in comm.exchange_stats()}
         assert ex and all(e["calls"] >= 1 for e in ex.values())
+        assert ex["status"]["mode"] == ("host_memory" if hostx else "device_round_trip")
+        assert ex["plans"]["mode"] == ex["status"]["mode"]
     finally:
         comm.close()
         c1.close()
