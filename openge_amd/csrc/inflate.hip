@@ -331,6 +331,127 @@ __global__ void k_nonzero_u32(const uint32_t *__restrict__ a, uint64_t n, uint32
     if (i < n) f[i] = a[i] != 0;
     else if (i == n) f[i] = 0;
 }
+
+// ---- segment walk (r06): the framing chain followed from known starts instead of a scan of every byte.
+// [s, own) is cut into segments of kSegBytes (more than the largest block, 64 KiB, so every segment but a
+// short last one holds a block start).  Segment 0 starts at s; segment k > 0 guesses its first block start
+// -- the first position of its first kSegScan bytes where three headers chain (or a chain reaches the end of
+// the buffer) -- and one thread per segment walks BSIZE links while the block starts lie in the segment.  A
+// segment is right when its start is where its predecessor's walk left off; a wrong guess (a false chain
+// inside deflate data) is walked again from there, so the result is the sequential walk from s.  Reads:
+// the headers plus ~half a block per segment for the guesses, not the whole file.
+constexpr uint64_t kSegBytes = 1ull << 20;
+constexpr uint64_t kSegScan = 256ull << 10;
+constexpr uint64_t kSegNone = ~0ull, kSegBad = ~0ull - 1;
+
+__device__ bool chain3(const uint8_t *__restrict__ z, uint64_t zbytes, uint64_t p) {
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t bs = bgzf_head(z, zbytes, p);
+        if (!bs) return false;
+        p += bs;
+        if (p == zbytes) return true;
+    }
+    return true;
+}
+
+// one wave per segment k >= 1: start[k] = the guess (kSegNone: none within kSegScan); 64 lanes test 16
+// positions each per 1 KiB step, the lowest valid position wins
+__global__ void __launch_bounds__(256) k_seg_guess(const uint8_t *__restrict__ z, uint64_t zbytes, uint64_t s, uint64_t own,
+                                                   uint64_t nseg, uint64_t *__restrict__ start) {
+    const uint64_t k = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    if (k >= nseg) return;
+    if (k == 0) {
+        if (lane == 0) start[0] = s;
+        return;
+    }
+    const uint64_t a = s + k * kSegBytes, lim = min(min(a + kSegScan, own), zbytes);
+    uint64_t found = kSegNone;
+    for (uint64_t c = a; c < lim && found == kSegNone; c += 64 * 16) {
+        uint64_t mine = kSegNone;
+        const uint64_t p0 = c + 16ull * lane;
+        // the lane's 16 positions + 3 bytes of look-ahead in registers; only the gzip/deflate/FEXTRA
+        // signature 1f 8b 08 04 goes on to the header chain's loads
+        uint32_t v[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            uint32_t x = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint64_t pb = p0 + 4 * q + b;
+                if (pb < zbytes) x |= (uint32_t)z[pb] << (8 * b);
+            }
+            v[q] = x;
+        }
+        for (uint32_t j = 0; j < 16 && mine == kSegNone; ++j) {
+            const uint64_t p = p0 + j;
+            if (p >= lim) break;
+            const uint32_t sig = (j & 3) ? __builtin_amdgcn_alignbyte(v[(j >> 2) + 1], v[j >> 2], j & 3) : v[j >> 2];
+            if (sig == 0x04088b1fu && chain3(z, zbytes, p)) mine = p;
+        }
+        // the lowest lane with a hit
+        const uint64_t m = __ballot(mine != kSegNone);
+        if (m) found = __shfl(mine, __ffsll((long long)m) - 1, 64);
+    }
+    if (lane == 0) start[k] = found;
+}
+
+// one thread per segment: walk from start[k] while block starts lie below the segment's end b (the last
+// segment: below own); ex[k] = where the walk left off (kSegBad: an invalid header on the way), cnt[k] =
+// blocks.  EMIT: the starts and sizes go to cpos / cbs from base[k].  only: walk only the segments whose
+// flag is set (the re-walks), prev_ex: their start is the predecessor's exit.
+template <bool EMIT>
+__global__ void __launch_bounds__(256) k_seg_walk(const uint8_t *__restrict__ z, uint64_t zbytes, uint64_t s, uint64_t own,
+                                                  uint64_t nseg, const uint64_t *__restrict__ start, uint64_t *__restrict__ ex,
+                                                  uint32_t *__restrict__ cnt, const uint32_t *__restrict__ base,
+                                                  uint64_t *__restrict__ cpos, uint32_t *__restrict__ cbs) {
+    const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= nseg) return;
+    const uint64_t b = k + 1 == nseg ? own : s + (k + 1) * kSegBytes;
+    uint64_t p = start[k];
+    uint32_t c = 0;
+    uint64_t o = EMIT ? base[k] : 0;
+    if (p == kSegNone) {
+        if (!EMIT) ex[k] = kSegNone, cnt[k] = 0;
+        return;
+    }
+    while (p < b) {
+        const uint32_t bs = bgzf_head(z, zbytes, p);
+        if (!bs) {
+            p = kSegBad;
+            break;
+        }
+        if (EMIT) cpos[o] = p, cbs[o] = bs, ++o;
+        ++c;
+        p += bs;
+    }
+    if (!EMIT) ex[k] = p, cnt[k] = c;
+}
+
+// segments whose start is not their predecessor's exit take that exit as their start (ex_prev: the exits of
+// the last walk); *chg counts them
+__global__ void k_seg_join(uint64_t nseg, const uint64_t *__restrict__ ex, uint64_t *__restrict__ start, unsigned int *__restrict__ chg) {
+    const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k == 0 || k >= nseg) return;
+    const uint64_t want = ex[k - 1];
+    if (start[k] != want) {
+        start[k] = want;
+        atomicAdd(chg, 1u);
+    }
+}
+
+// the first header candidate of [0, lim) (the kIndexFirst guess): atomicMin over positions
+__global__ void __launch_bounds__(256) k_first_cand(const uint8_t *__restrict__ z, uint64_t zbytes, uint64_t lim,
+                                                    unsigned long long *__restrict__ first) {
+    const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    for (uint32_t j = 0; j < 16; ++j) {
+        const uint64_t p = p0 + j;
+        if (p >= lim) return;
+        if (z[p] == 31 && bgzf_head(z, zbytes, p)) {
+            atomicMin(first, (unsigned long long)p);
+            return;
+        }
+    }
+}
 }  // namespace
 
 // ------------------------------------------------------------------------------------ host side
@@ -481,24 +602,21 @@ __global__ void k_bgzf_unstash(const uint32_t *__restrict__ cnt, const uint32_t 
     for (uint32_t j = 0; j < c; ++j) cpos[o + j] = stash_pos[b * kStash + j], cbs[o + j] = stash_bs[b * kStash + j];
 }
 
-int oge_bgzf_index_range_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t s, uint64_t own, OgeBgzfIndex *ix,
-                            uint64_t *s_used, uint64_t *xend) {
-    hipSetDevice(ctx->device);
-    ix->nblk = 0;
-    ix->total = 0;
-    if (own > zbytes || (s != kIndexFirst && s >= own)) return 2;
-    if ((uintptr_t)d_z & 3) return 1;
+// candidates by a scan of every byte position of [0, own) (the r02-r05 path; now the fallback of the
+// segment walk): 0 with *cpos / *cbs / *m set (the chain check follows), 1 = no candidate at s, 2 = none in
+// the range
+static int scan_candidates(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t *s_io, uint64_t own, uint32_t *bad,
+                           uint64_t **cpos_o, uint32_t **cbs_o, uint64_t *m_o) {
+    uint64_t s = *s_io;
     const uint64_t per_blk = 256ull * kIdxPos;
     const uint64_t G = (own + per_blk - 1) / per_blk;
     if (!G) return 2;
     if (G > 0xffffffffull) return 1;
     uint32_t *cnt = (uint32_t *)ctx->ws("bix_cnt", (G + 1) * 4);
     uint32_t *base = (uint32_t *)ctx->ws("bix_base", (G + 1) * 4);
-    uint32_t *bad = (uint32_t *)ctx->ws("bix_bad", 32);
     uint64_t *stash_pos = (uint64_t *)ctx->ws("bix_stash_pos", G * kStash * 8);
     uint32_t *stash_bs = (uint32_t *)ctx->ws("bix_stash_bs", G * kStash * 4);
-    if (!cnt || !base || !bad || !stash_pos || !stash_bs) return OGE_ERR_HIP;
-    OGE_HIP_TRY(ctx, hipMemsetAsync(bad, 0, 32, ctx->stream));
+    if (!cnt || !base || !stash_pos || !stash_bs) return OGE_ERR_HIP;
     k_bgzf_cand<false><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, own, cnt, nullptr, nullptr, nullptr, stash_pos, stash_bs,
                                                               bad + 1);
     OGE_LAUNCH_CHECK(ctx);
@@ -513,9 +631,7 @@ int oge_bgzf_index_range_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, u
     if (!m) return s == kIndexFirst ? 2 : 1;
     uint64_t *cpos = (uint64_t *)ctx->ws("bix_cpos", m * 8);
     uint32_t *cbs = (uint32_t *)ctx->ws("bix_cbs", m * 4);
-    uint32_t *isz = (uint32_t *)ctx->ws("bix_isz", (m + 1) * 4);
-    uint32_t *slot = (uint32_t *)ctx->ws("bix_slot", (m + 1) * 4);
-    if (!cpos || !cbs || !isz || !slot) return OGE_ERR_HIP;
+    if (!cpos || !cbs) return OGE_ERR_HIP;
     if (stash_ovf)  // a block with more than kStash candidates: the second scan places them
         k_bgzf_cand<true><<<(uint32_t)G, 256, 0, ctx->stream>>>(d_z, zbytes, own, cnt, base, cpos, cbs);
     else
@@ -525,6 +641,91 @@ int oge_bgzf_index_range_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, u
         OGE_HIP_TRY(ctx, hipMemcpyAsync(&s, cpos, 8, hipMemcpyDeviceToHost, ctx->stream));
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
+    *s_io = s, *cpos_o = cpos, *cbs_o = cbs, *m_o = m;
+    return OGE_OK;
+}
+
+// the block chain from s by the segment walk (see k_seg_walk): 0 with the exact chain's starts and sizes in
+// *cpos / *cbs (*m blocks), 1 = an invalid header on the chain (the host walk reports it), 3 = undecided
+// (no candidate near the start of a kIndexFirst range, or wrong guesses that keep moving): the scan decides
+static int seg_candidates(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t *s_io, uint64_t own, uint64_t **cpos_o,
+                          uint32_t **cbs_o, uint64_t *m_o) {
+    uint64_t s = *s_io;
+    unsigned long long *w = (unsigned long long *)ctx->ws("bix_seg_w", 16);
+    if (!w) return OGE_ERR_HIP;
+    unsigned int *chg = (unsigned int *)(w + 1);
+    if (s == kIndexFirst) {
+        const uint64_t lim = std::min<uint64_t>(own, kSegScan);
+        unsigned long long first = ~0ull;
+        OGE_HIP_TRY(ctx, hipMemsetAsync(w, 0xff, 8, ctx->stream));
+        if (lim) k_first_cand<<<(uint32_t)oge_ceil_div(oge_ceil_div(lim, 16), 256), 256, 0, ctx->stream>>>(d_z, zbytes, lim, w);
+        OGE_LAUNCH_CHECK(ctx);
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&first, w, 8, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (first == ~0ull) return 3;
+        s = first;
+    }
+    if (s >= own) return 3;
+    const uint64_t nseg = (own - s + kSegBytes - 1) / kSegBytes;
+    if (nseg > 0xffffffffull) return 3;
+    uint64_t *start = (uint64_t *)ctx->ws("bix_seg_start", (nseg + 1) * 8);
+    uint64_t *ex = (uint64_t *)ctx->ws("bix_seg_ex", (nseg + 1) * 8);
+    uint32_t *cnt = (uint32_t *)ctx->ws("bix_seg_cnt", (nseg + 1) * 4);
+    uint32_t *base = (uint32_t *)ctx->ws("bix_seg_base", (nseg + 1) * 4);
+    if (!start || !ex || !cnt || !base) return OGE_ERR_HIP;
+    k_seg_guess<<<(uint32_t)oge_ceil_div(nseg * 64, 256), 256, 0, ctx->stream>>>(d_z, zbytes, s, own, nseg, start);
+    OGE_LAUNCH_CHECK(ctx);
+    const uint32_t gw = (uint32_t)oge_ceil_div(nseg, 256);
+    for (int it = 0;; ++it) {
+        k_seg_walk<false><<<gw, 256, 0, ctx->stream>>>(d_z, zbytes, s, own, nseg, start, ex, cnt, nullptr, nullptr, nullptr);
+        OGE_LAUNCH_CHECK(ctx);
+        OGE_HIP_TRY(ctx, hipMemsetAsync(chg, 0, 4, ctx->stream));
+        k_seg_join<<<gw, 256, 0, ctx->stream>>>(nseg, ex, start, chg);
+        OGE_LAUNCH_CHECK(ctx);
+        unsigned int hc = 0;
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(&hc, chg, 4, hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (!hc) break;
+        if (it == 32) return 3;
+    }
+    uint64_t xl = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&xl, ex + nseg - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + nseg, 0, 4, ctx->stream));
+    int rc = oge_exclusive_scan_u32(ctx, cnt, base, nseg + 1);
+    if (rc) return rc;
+    uint32_t m32 = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&m32, base + nseg, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (xl == kSegBad || xl == kSegNone || xl < own || !m32) return 1;  // every bad or missing exit reaches the last
+    uint64_t *cpos = (uint64_t *)ctx->ws("bix_cpos", (uint64_t)m32 * 8);
+    uint32_t *cbs = (uint32_t *)ctx->ws("bix_cbs", (uint64_t)m32 * 4);
+    if (!cpos || !cbs) return OGE_ERR_HIP;
+    k_seg_walk<true><<<gw, 256, 0, ctx->stream>>>(d_z, zbytes, s, own, nseg, start, ex, cnt, base, cpos, cbs);
+    OGE_LAUNCH_CHECK(ctx);
+    *s_io = s, *cpos_o = cpos, *cbs_o = cbs, *m_o = m32;
+    return OGE_OK;
+}
+
+int oge_bgzf_index_range_ws(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, uint64_t s, uint64_t own, OgeBgzfIndex *ix,
+                            uint64_t *s_used, uint64_t *xend) {
+    hipSetDevice(ctx->device);
+    ix->nblk = 0;
+    ix->total = 0;
+    if (own > zbytes || (s != kIndexFirst && s >= own)) return 2;
+    if ((uintptr_t)d_z & 3) return 1;
+    uint32_t *bad = (uint32_t *)ctx->ws("bix_bad", 32);
+    if (!bad) return OGE_ERR_HIP;
+    OGE_HIP_TRY(ctx, hipMemsetAsync(bad, 0, 32, ctx->stream));
+    uint64_t *cpos = nullptr, m = 0;
+    uint32_t *cbs = nullptr;
+    // the segment walk (r06), the byte scan when it cannot decide (or with OGE_BGZF_INDEX=scan)
+    const char *mode = getenv("OGE_BGZF_INDEX");
+    int rc = mode && !strcmp(mode, "scan") ? 3 : seg_candidates(ctx, d_z, zbytes, &s, own, &cpos, &cbs, &m);
+    if (rc == 3) rc = scan_candidates(ctx, d_z, zbytes, &s, own, bad, &cpos, &cbs, &m);
+    if (rc) return rc;
+    uint32_t *isz = (uint32_t *)ctx->ws("bix_isz", (m + 1) * 4);
+    uint32_t *slot = (uint32_t *)ctx->ws("bix_slot", (m + 1) * 4);
+    if (!isz || !slot) return OGE_ERR_HIP;
     if (s_used) *s_used = s;
     unsigned long long *dx = (unsigned long long *)(bad + 4);
     k_bgzf_chain<<<oge_ceil_div(m, 256), 256, 0, ctx->stream>>>(d_z, zbytes, s, own, cpos, cbs, m, bad, isz, dx);

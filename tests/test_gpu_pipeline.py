@@ -74,8 +74,37 @@ def _streams():
         yield name, (GOLDEN / "inputs" / name).read_bytes()
 
 
-@pytest.mark.parametrize("name,z", list(_streams()), ids=lambda x: x if isinstance(x, str) else "")
-def test_device_bgzf_index_equals_host_walk(ctx, name, z):
+def _planted_chains():
+    """A level-0 stream of several MiB with a false three-header chain planted inside a stored payload just
+    past every 1 MiB segment boundary of the device index's segment walk: each segment's guess is the false
+    chain, whose walk breaks, and the join re-walks the segment from its predecessor's exit."""
+    p = L.synth_params(10_000, preset="c2", seed=9)
+    recs, offs, hdr = L.synth_host(p)
+    z = bytearray(bamutil.bgzf_blocks(recs[:int(offs[-1])].tobytes(), 0))
+    n, hix, _ = _host_index(bytes(z))
+    starts = sorted(int(x) - 18 for x in hix[:n])  # d0 = start + 12 + xlen (6): the block starts
+    fake = b"".join(struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, ord("B"), ord("C"), 2, 39) + b"\0" * 22
+                    for _ in range(3))
+    planted = 0
+    for k in range(1, len(z) >> 20):
+        q = (k << 20) + 64
+        nxt = min(x for x in starts if x >= (k << 20))
+        prv = max(x for x in starts if x < (k << 20))
+        if prv + 18 + 5 <= q and q + len(fake) + 8 < nxt:
+            z[q:q + len(fake)] = fake
+            planted += 1
+    assert planted >= 3 and len(z) > 4 << 20
+    return bytes(z)
+
+
+@pytest.mark.parametrize("mode", ["segments", "scan"])
+@pytest.mark.parametrize("name,z", list(_streams()) + [("planted_chains", _planted_chains())],
+                         ids=lambda x: x if isinstance(x, str) else "")
+def test_device_bgzf_index_equals_host_walk(ctx, name, z, mode, monkeypatch):
+    """The segment walk (r06 default) and the byte scan it falls back to (OGE_BGZF_INDEX=scan) both equal the
+    host walk; the scan hands planted false headers to the host walk, the segment walk walks past them."""
+    if mode == "scan":
+        monkeypatch.setenv("OGE_BGZF_INDEX", "scan")
     n, hix, hcrc = _host_index(z)
     m, dix, dcrc = _dev_index(ctx, z)
     assert m == n
