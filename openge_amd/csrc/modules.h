@@ -20,6 +20,10 @@ namespace oge {
 
 struct ChainContext;
 
+// Start reading the chain's input file into host memory on helper threads (the CLI calls this before it
+// brings up HIP); FileReader takes the bytes when it streams that file to the device.
+void prefetch_input(const std::string &path);
+
 // Records of one chain, resident in host memory, HBM, or both.
 struct ReadBatch {
     BamHeaderModel header;

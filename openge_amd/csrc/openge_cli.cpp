@@ -156,6 +156,8 @@ int main(int argc, const char **argv) {
     }
     timeval t0;
     gettimeofday(&t0, nullptr);
+    // one input file on one GPU: its bytes come off the disk / page cache while HIP initialises
+    if (p.inputs.size() == 1 && p.inputs[0] != "stdin" && cc.gpus == 1) prefetch_input(p.inputs[0]);
     if (oge_ctx_create(cc.device, &cc.ctx)) {
         fprintf(stderr, "openge: %s\n", oge_last_error(nullptr));
         return -1;

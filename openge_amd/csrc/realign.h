@@ -262,19 +262,33 @@ struct ByteBuf {
     ByteBuf() = default;
     ByteBuf(const ByteBuf &) = delete;
     ByteBuf &operator=(const ByteBuf &) = delete;
-    ~ByteBuf() { std::free(p_); }
+    // n bytes (uninitialised) + 16 zeroed bytes of slack past them
     bool alloc(size_t n) {
-        std::free(p_);
-        p_ = (uint8_t *)std::malloc(n ? n : 1);
-        n_ = p_ ? n : 0;
-        return p_ != nullptr;
+        v_ = bytevec();
+        n_ = 0;
+        try {
+            v_.reserve(n + 16);
+            v_.resize(n + 16);
+        } catch (const std::bad_alloc &) {
+            v_ = bytevec();
+            return false;
+        }
+        memset(v_.data() + n, 0, 16);
+        n_ = n;
+        return true;
     }
-    uint8_t *data() { return p_; }
-    const uint8_t *data() const { return p_; }
+    uint8_t *data() { return v_.data(); }
+    const uint8_t *data() const { return v_.data(); }
     size_t size() const { return n_; }
+    // hands the storage over (size() + 16 bytes: the slack included, what a ReadBatch holds), no copy
+    void take(bytevec &dst) {
+        dst = std::move(v_);
+        v_ = bytevec();
+        n_ = 0;
+    }
 
 private:
-    uint8_t *p_ = nullptr;
+    bytevec v_;
     size_t n_ = 0;
 };
 

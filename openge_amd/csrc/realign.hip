@@ -665,3 +665,12 @@ const char *oge_realign_result_stats(const oge_realign_result *r) { return r ? r
 void oge_realign_result_free(oge_realign_result *r) { delete r; }
 
 }  // extern "C"
+
+// (C++, the library's own modules) the result's records and offsets moved out without a copy: recs gets
+// the records + 16 bytes of zeroed slack (ReadBatch's layout), offs the n + 1 offsets (offs[0] = 0)
+void oge_realign_result_take(oge_realign_result *r, oge::bytevec &recs, std::vector<uint64_t> &offs) {
+    r->recs.take(recs);
+    offs = std::move(r->offs);
+    r->offs = std::vector<uint64_t>();
+}
+
