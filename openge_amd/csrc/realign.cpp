@@ -87,6 +87,22 @@ public:
     void run_chunks(size_t n, size_t chunk, F f) {  // f(begin, end) over [0, n) in chunks
         run((n + chunk - 1) / chunk, [&](size_t c) { f(c * chunk, std::min(n, (c + 1) * chunk)); });
     }
+    // f(0..n) handed out in increasing order to the workers while the calling thread runs lead() beside them
+    // (and then helps with what is left); one thread: f over all, then lead
+    template <class F, class G>
+    void run_lead(size_t n, F f, G lead) {
+        if (n_ == 1) {
+            for (size_t i = 0; i < n; ++i) f(i);
+            lead();
+            return;
+        }
+        std::atomic<size_t> next(0);
+        exec([&](int t) {
+            tl_worker = t;
+            if (t == 0) lead();
+            for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+        });
+    }
 
 private:
     void exec(const std::function<void(int)> &job) {
@@ -1456,13 +1472,19 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     std::atomic<bool> bad(false);
     std::mutex emu;
     std::string derr;
-    // decode, plus what binning asks of every read (its GenomeLoc stop, doNotTryToClean)
+    // decode, plus what binning asks of every read (its GenomeLoc stop, doNotTryToClean), on the workers in
+    // 4096-read chunks; the calling thread bins the reads in order beside them, waiting for each chunk (r06:
+    // the binning walk was a serial 0.05 s after the decode)
     BigVec<int32_t> &lstop = S.lstop;  // (every entry written by the decode below)
     BigVec<uint8_t> &dnc = S.dnc;
     lstop.resize(n);
     dnc.resize(n);
-    pool.run_chunks(n, dchunk, [&](size_t b, size_t end) {
+    const uint64_t ndch = (n + dchunk - 1) / dchunk;
+    std::unique_ptr<std::atomic<uint8_t>[]> cdone(new std::atomic<uint8_t>[ndch ? ndch : 1]);
+    for (uint64_t c = 0; c < ndch; ++c) cdone[c].store(0, std::memory_order_relaxed);
+    auto decode_chunk = [&](size_t c) {
         std::string e;
+        const size_t b = c * dchunk, end = std::min<size_t>(n, b + dchunk);
         for (size_t i = b; i < end; ++i) {
             if (!rread_decode(recs + offs[i], reads[i], e)) {
                 std::lock_guard<std::mutex> g(emu);
@@ -1474,21 +1496,9 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
             lstop[i] = read_loc(reads[i]).stop;
             dnc[i] = do_not_clean(reads[i], P);
         }
-    });
-    if (bad) {
-        err = derr;
-        return -1;
-    }
-    for (uint64_t i = 0; i < n; ++i) {
-        if (reads[i].ref < -1 || reads[i].ref >= (int)ref_names.size()) {
-            err = "record refID outside the sequence dictionary";
-            return -1;
-        }
-    }
+        cdone[c].store(1, std::memory_order_release);
+    };
 
-    const double td = now_s();
-    st.t_fasta = tf - t0;
-    st.t_decode = td - tf;
     // ---------------------------------------------------------------- A: map_func (:455-553)
     std::vector<std::unique_ptr<IntervalData>> &ids = S.ids;  // objects reused across calls
     size_t nids = 0;
@@ -1516,52 +1526,76 @@ int realign_run(const std::vector<std::string> &ref_names, const uint8_t *recs, 
     // map_func; `continue` re-dispatches the read after the loading bin changed (the reference's
     // recursive calls).  Once the intervals are exhausted every read passes straight through (a bin
     // of its own in the reference, which emits it unchanged).
-    for (uint64_t i = 0; i < n; ++i) {
-        RRead *r = &reads[i];
-        for (;;) {
-            if (loading->interval < 0) {
-                ev.push_back({EV_READ, r, loading});
-                break;
+    bool badref = false;
+    auto bin_all = [&]() {
+        for (uint64_t i = 0; i < n; ++i) {
+            if (i % dchunk == 0) {
+                const uint64_t c = i / dchunk;
+                while (!cdone[c].load(std::memory_order_acquire)) std::this_thread::yield();
+                if (bad.load(std::memory_order_relaxed)) return;  // a record that does not decode: reported below
             }
-            if (r->ref == -1) {
-                ev.push_back({EV_CLEAN, nullptr, loading});
-                it = ivs.size();
-                loading = new_id(-1);
-                saw = false;
-                continue;
+            RRead *r = &reads[i];
+            if (r->ref < -1 || r->ref >= (int)ref_names.size()) {
+                badref = true;
+                return;
             }
-            GLoc loc;
-            loc.contig = r->ref;
-            loc.start = r->pos;
-            loc.stop = lstop[i];
-            GLoc rl = loc;
-            if (rl.stop == 0) rl.stop = rl.start;
-            const GLoc &cur = ivs[loading->interval];
-            if (rl.is_before(cur)) {
-                if (!saw) ev.push_back({EV_READ, r, loading});
-                else loading->notToClean.push_back(r);
-            } else if (rl.overlaps(cur)) {
-                saw = true;
-                if (dnc[i]) loading->notToClean.push_back(r);
-                else bin_add(loading, r, loc);
-                if ((int)(loading->toClean.size() + loading->notToClean.size()) >= P.max_reads) {
-                    ev.push_back({EV_LIST, nullptr, loading});
-                    ++it;
+            for (;;) {
+                if (loading->interval < 0) {
+                    ev.push_back({EV_READ, r, loading});
+                    break;
+                }
+                if (r->ref == -1) {
+                    ev.push_back({EV_CLEAN, nullptr, loading});
+                    it = ivs.size();
+                    loading = new_id(-1);
+                    saw = false;
+                    continue;
+                }
+                GLoc loc;
+                loc.contig = r->ref;
+                loc.start = r->pos;
+                loc.stop = lstop[i];
+                GLoc rl = loc;
+                if (rl.stop == 0) rl.stop = rl.start;
+                const GLoc &cur = ivs[loading->interval];
+                if (rl.is_before(cur)) {
+                    if (!saw) ev.push_back({EV_READ, r, loading});
+                    else loading->notToClean.push_back(r);
+                } else if (rl.overlaps(cur)) {
+                    saw = true;
+                    if (dnc[i]) loading->notToClean.push_back(r);
+                    else bin_add(loading, r, loc);
+                    if ((int)(loading->toClean.size() + loading->notToClean.size()) >= P.max_reads) {
+                        ev.push_back({EV_LIST, nullptr, loading});
+                        ++it;
+                        loading = new_id(it < ivs.size() ? (int)it : -1);
+                        saw = false;
+                    }
+                } else {
+                    ev.push_back({EV_CLEAN, nullptr, loading});
+                    do {
+                        ++it;
+                    } while (it < ivs.size() && ivs[it].is_before(rl));
                     loading = new_id(it < ivs.size() ? (int)it : -1);
                     saw = false;
+                    continue;
                 }
-            } else {
-                ev.push_back({EV_CLEAN, nullptr, loading});
-                do {
-                    ++it;
-                } while (it < ivs.size() && ivs[it].is_before(rl));
-                loading = new_id(it < ivs.size() ? (int)it : -1);
-                saw = false;
-                continue;
+                break;
             }
-            break;
         }
+    };
+    pool.run_lead(ndch, decode_chunk, bin_all);
+    if (bad) {  // (a decode error first, as when the whole input was decoded before the binning)
+        err = derr;
+        return -1;
     }
+    if (badref) {
+        err = "record refID outside the sequence dictionary";
+        return -1;
+    }
+    const double td = now_s();
+    st.t_fasta = tf - t0;
+    st.t_decode = td - tf;  // decode and binning, side by side
     // onTraversalDone (:577-607)
     if (!loading->toClean.empty()) ev.push_back({EV_CLEAN, nullptr, loading});
     else if (!loading->notToClean.empty()) ev.push_back({EV_LIST, nullptr, loading});
