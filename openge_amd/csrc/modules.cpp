@@ -232,13 +232,16 @@ struct Prefetch {
     bool ok = false;
 };
 Prefetch *g_prefetch = nullptr;
+bool g_prefetch_used = false;  // (the reader's -v line says so)
 }  // namespace
 
 void prefetch_input(const std::string &path) {
     const char *e = getenv("OGE_PREFETCH");
     if ((e && *e == '0') || g_prefetch) return;
     struct stat st;
-    if (stat(path.c_str(), &st) || !S_ISREG(st.st_mode) || st.st_size < (64ll << 20) || st.st_size > (8ll << 30)) return;
+    const char *mn = getenv("OGE_PREFETCH_MIN");  // smallest file prefetched (bytes; tests lower it)
+    const long long pmin = mn && *mn ? atoll(mn) : (64ll << 20);
+    if (stat(path.c_str(), &st) || !S_ISREG(st.st_mode) || st.st_size < pmin || st.st_size < 1 || st.st_size > (8ll << 30)) return;
     auto *P = new Prefetch();
     P->path = path;
     P->size = (uint64_t)st.st_size;
@@ -314,6 +317,7 @@ static int stream_to_device(ChainContext &cc, const std::string &path, void **dz
     {
         bytevec pre;
         if (take_prefetch(path, Z, pre)) {  // read while HIP came up: one copy from the helper's buffer
+            g_prefetch_used = true;
             const bool ok = !oge_dev_alloc(cc.ctx, Z + 16, &dz) && !oge_memcpy(cc.ctx, dz, pre.data(), Z, 1);
             std::thread([](bytevec v) { v = bytevec(); }, std::move(pre)).detach();  // unmapped beside what follows
             close(fd);
@@ -500,7 +504,8 @@ int FileReader::read_device(ChainContext &cc, ReadBatch &b, const std::string &p
         fprintf(stderr,
                 "[openge] FileReader (device%s): file %.3f s, upload %.3f s, inflate %.3f s (kernels %.3f s, release of the "
                 "compressed copies %.3f s), records %.3f s\n",
-                streamed ? ", streamed + device index" : "", sec(t0, t1), sec(t1, t2), sec(t2, t3), t_kern / 1e3, sec(t2b, t3),
+                streamed ? (g_prefetch_used ? ", prefetched + device index" : ", streamed + device index") : "", sec(t0, t1),
+                sec(t1, t2), sec(t2, t3), t_kern / 1e3, sec(t2b, t3),
                 sec(t3, clk()));
     return 0;
 }

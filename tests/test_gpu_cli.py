@@ -259,17 +259,21 @@ def test_cli_chunked_matches_reference(case, tmp_path):
     assert len(offs) == case.n - case.meta["sortdedup_v"]["n_dup"]
 
 
-def test_cli_streamed_reader_matches_reference(case, tmp_path):
+@pytest.mark.parametrize("prefetch", [False, True])
+def test_cli_streamed_reader_matches_reference(case, tmp_path, prefetch):
     """Files are streamed into HBM through page-locked buffers and indexed on the device
     (OGE_STREAM_MIN lowers the size threshold and the chunk to 64 KiB, so the golden inputs take that
-    path in many chunks): the reference's mergesort -M outputs."""
+    path in many chunks): the reference's mergesort -M outputs.  prefetch: the CLI reads the file on
+    helper threads while HIP comes up and the reader copies those bytes up (OGE_PREFETCH_MIN lowers its
+    64 MiB threshold)."""
     import os
     src = case_input(case, tmp_path)
     env = dict(os.environ, OGE_STREAM_MIN="1")
+    env.update({"OGE_PREFETCH_MIN": "1"} if prefetch else {"OGE_PREFETCH": "0"})
     r = subprocess.run([OPENGE, "mergesort", "-M", "--nopg", "-v", str(src), "-o", str(tmp_path / "o.bam")],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
-    assert "streamed + device index" in r.stderr
+    assert ("prefetched + device index" if prefetch else "streamed + device index") in r.stderr
     h, m, t = digests(tmp_path / "o.bam")
     g = case.meta["sortdedup_v"]
     assert h == g["header"] and m == g["mapped_sha256"] and t == g["tail_multiset_sha256"]
