@@ -388,7 +388,8 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
 // handed out longest-first to the least frequent symbols.
 struct HuffScratch {
     uint16_t sorted[kLit];
-    uint32_t w[2 * kLit];      // node weights, later the node depths; first the sort keys (512)
+    uint32_t w[2 * kLit];      // the leaves' weights (+ 2 sentinels), later the node depths
+    uint32_t nw[kLit + 2];     // the internal nodes' weights, in creation order (+ sentinels)
     uint16_t parent[2 * kLit]; // parent node, later the pointer-jumping ancestor
     uint32_t cnt[16];
     uint32_t m;
@@ -398,94 +399,128 @@ static_assert(2 * kLit >= 512, "the sort keys live in HuffScratch::w");
 // One wave, everything but the two-queue merge lane-parallel (r03: the r02 version ran the depth walk,
 // the depth counts and the length hand-out as serial lane-0 loops over LDS, one LDS round trip per step;
 // the same lengths, so the same compressed bytes).
-__device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, HuffScratch &hs) {
-    const int lane = threadIdx.x;
-    // the used symbols ranked by (frequency, symbol): keys f << 9 | symbol (f <= 65281), unused slots
-    // 0xffffffff, bitonic-sorted in LDS by the wave (literal/length alphabet: 512 slots, 45 stages; r03
-    // counted, for every symbol, the keys below it -- n^2 / 64 LDS reads per lane)
-    uint32_t m = 0;
-    uint32_t *key = hs.w;
-    const uint32_t S = n <= 32 ? 32u : n <= 64 ? 64u : n <= 128 ? 128u : n <= 256 ? 256u : 512u;  // sorted slots
-    for (int i0 = 0; i0 < (int)S; i0 += 64) {  // every lane takes part in every ballot: m is wave-uniform
-        const int i = i0 + lane;
-        const uint32_t fi = i < n ? f[i] : 0;
-        if (i < n) len[i] = 0;
-        if (i < (int)S) key[i] = fi ? (fi << 9) | (uint32_t)i : 0xffffffffu;
-        m += __popcll(__ballot(fi != 0));
-    }
-    __syncthreads();
-    for (uint32_t k = 2; k <= S; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+// Bitonic sort of S <= 512 keys held 8 per lane (key index = 8 lane + e), ascending: stages whose partner
+// lies in the same lane compare registers, the others exchange through a lane shuffle -- no LDS, no barriers
+// (r06; the r03-r05 network ran its 45 stages on LDS with a barrier each)
+template <int S>
+__device__ __forceinline__ void sort8(uint32_t (&key)[8], uint32_t lane) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {  // S / 2 compare-exchange pairs, up to four per lane
-                const uint32_t p = (uint32_t)lane + 64 * q;
-                if (p >= S / 2) break;
-                const uint32_t a = ((p & ~(j - 1)) << 1) | (p & (j - 1)), b = a | j;
-                const uint32_t x = key[a], y = key[b];
-                const bool up = (a & k) == 0;
-                if ((x > y) == up) key[a] = y, key[b] = x;
+    for (uint32_t k = 2; k <= (uint32_t)S; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 8) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const uint32_t idx = 8 * lane + (uint32_t)e;
+                    const uint32_t y = (uint32_t)__shfl_xor((int)key[e], (int)(j >> 3), 64);
+                    const bool up = (idx & k) == 0, lower = (idx & j) == 0;
+                    const uint32_t mn = min(key[e], y), mx = max(key[e], y);
+                    key[e] = (up == lower) ? mn : mx;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if ((uint32_t)e & j) continue;
+                    const int e2 = e | (int)j;
+                    const uint32_t idx = 8 * lane + (uint32_t)e;
+                    const bool up = (idx & k) == 0;
+                    const uint32_t x = key[e], y = key[e2];
+                    if ((x > y) == up) key[e] = y, key[e2] = x;
+                }
             }
-            __syncthreads();
         }
     }
-    for (uint32_t r = lane; r < m; r += 64) hs.sorted[r] = (uint16_t)(key[r] & 511);
+}
+
+#if OGE_EXP == 3
+__device__ uint64_t g_hl_clk[8];  // timing experiment: huff_lengths' phase clocks of block 0, literal alphabet
+#define HLCLK(k) do { if (n == kLit && blockIdx.x == 0 && threadIdx.x == 0) g_hl_clk[k] = __builtin_readcyclecounter(); } while (0)
+#else
+#define HLCLK(k) do { } while (0)
+#endif
+__device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, HuffScratch &hs) {
+    const int lane = threadIdx.x;
+    HLCLK(0);
+    // the used symbols ranked by (frequency, symbol): keys f << 9 | symbol (f <= 65281), unused slots
+    // 0xffffffff, sorted in registers by the wave (8 keys per lane, 512 slots at most)
+    uint32_t m = 0;
+    const uint32_t S = n <= 32 ? 32u : n <= 64 ? 64u : n <= 128 ? 128u : n <= 256 ? 256u : 512u;  // sorted slots
+    uint32_t key[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int i = 8 * lane + e;
+        const uint32_t fi = i < n ? f[i] : 0;
+        if (i < n) len[i] = 0;
+        key[e] = fi ? (fi << 9) | (uint32_t)i : 0xffffffffu;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m += __popcll(__ballot(key[e] != 0xffffffffu));  // every lane in every ballot
+    HLCLK(1);
+    switch (S) {
+    case 32: sort8<32>(key, lane); break;
+    case 64: sort8<64>(key, lane); break;
+    case 128: sort8<128>(key, lane); break;
+    case 256: sort8<256>(key, lane); break;
+    default: sort8<512>(key, lane); break;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const uint32_t r = 8 * lane + (uint32_t)e;
+        if (r < m) hs.sorted[r] = (uint16_t)(key[e] & 511), hs.w[r] = key[e] >> 9;  // rank r's symbol and weight
+    }
     __syncthreads();
+    HLCLK(2);
     if (m == 0) return;
     if (m == 1) {
         if (lane == 0) len[hs.sorted[0]] = 1;
         __syncthreads();
         return;
     }
-    for (uint32_t k = lane; k < m; k += 64) hs.w[k] = f[hs.sorted[k]];
-    __syncthreads();
     const uint32_t root = 2 * m - 2;
-    if (lane == 0) {  // two-queue merge (lane 0).  A step's two picks can only take the next two entries
-        // of either queue, so those four are read together at the start of the step (one LDS round trip per
-        // step instead of one per pick; entries not yet created are never taken: nodes are made in order)
-        uint32_t i = 0, j = m, nx = m;
+    // two-queue merge (lane 0) over the leaves w[0, m) and the nodes nw[] in creation order (tree index m + k).
+    // r06: queues closed by +inf sentinels -- an exhausted leaf queue and a node not made yet read as +inf --
+    // so a pick is one compare and two selects (the same picks as the guarded r05 merge: ties take the leaf);
+    // the merge runs on the scalar unit, which the CU's 16 waves share, so its instruction count is its time
+    if (lane < 2) hs.w[m + lane] = 0xffffffffu;
+    for (uint32_t k = lane; k <= m; k += 64) hs.nw[k] = 0xffffffffu;
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t i = 0, j = 0;
         for (uint32_t c = 0; c + 1 < m; ++c) {
-            // unconditional reads (both pairs in one LDS round trip); an entry past its queue's end is read
-            // but never picked
-            const uint32_t l0 = hs.w[i], l1 = hs.w[i + 1], n0 = hs.w[j], n1 = hs.w[j + 1];
-            uint32_t a, b, wa, wb;
-            if (i < m && (j >= nx || l0 <= n0)) {  // first pick
-                a = i, wa = l0;
-                const bool leaf = i + 1 < m && (j >= nx || l1 <= n0);  // second pick
-                b = leaf ? i + 1 : j, wb = leaf ? l1 : n0;
-                i += leaf ? 2 : 1;
-                j += leaf ? 0 : 1;
-            } else {
-                a = j, wa = n0;
-                const bool leaf = i < m && (j + 1 >= nx || l0 <= n1);
-                b = leaf ? i : j + 1, wb = leaf ? l0 : n1;
-                i += leaf ? 1 : 0;
-                j += leaf ? 1 : 2;
-            }
-            const uint32_t sw = wa + wb;
-            hs.w[nx] = sw;
-            hs.parent[a] = (uint16_t)nx;
-            hs.parent[b] = (uint16_t)nx;
-            ++nx;
+            const uint32_t l0 = hs.w[i], l1 = hs.w[i + 1], n0 = hs.nw[j], n1 = hs.nw[j + 1];
+            const bool p1 = l0 <= n0;  // first pick: the leaf unless the node is lighter
+            const uint32_t a = p1 ? i : m + j, wa = p1 ? l0 : n0;
+            const uint32_t lh = p1 ? l1 : l0, nh = p1 ? n0 : n1;  // the queue heads after it
+            const bool p2 = lh <= nh;
+            const uint32_t b = p2 ? (p1 ? i + 1 : i) : m + (p1 ? j : j + 1), wb = p2 ? lh : nh;
+            i += (uint32_t)p1 + (uint32_t)p2;
+            j += 2u - (uint32_t)p1 - (uint32_t)p2;
+            hs.nw[c] = wa + wb;
+            hs.parent[a] = (uint16_t)(m + c);
+            hs.parent[b] = (uint16_t)(m + c);
         }
         hs.parent[root] = (uint16_t)root;
     }
     __syncthreads();
+    HLCLK(3);
     // depths by pointer jumping over the parent tree: d[x] = edges to the root (<= 10 doublings)
     for (uint32_t x = lane; x <= root; x += 64) hs.w[x] = x == root ? 0u : 1u;
     __syncthreads();
     for (int round = 0; round < 10; ++round) {
         uint32_t nd[9], na[9];
+        bool open = false;  // some ancestor is not the root yet
 #pragma unroll
         for (int q = 0; q < 9; ++q) {
             const uint32_t x = lane + 64 * q;
             nd[q] = 0, na[q] = 0;
             if (x <= root) {
                 const uint32_t a = hs.parent[x];
+                open |= a != root;
                 nd[q] = hs.w[x] + (a != root ? hs.w[a] : 0u);
                 na[q] = hs.parent[a];
             }
         }
-        __syncthreads();
+        if (!__syncthreads_or(open)) break;  // every depth final (r06: typical trees need 4-5 of the 10 rounds)
 #pragma unroll
         for (int q = 0; q < 9; ++q) {
             const uint32_t x = lane + 64 * q;
@@ -493,6 +528,7 @@ __device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, Huff
         }
         __syncthreads();
     }
+    HLCLK(4);
     // leaves per clamped depth (ballots), Kraft repair (lane 0, <= 15 entries), lengths handed out
     // longest-first to the least frequent symbols: rank k gets the b whose range holds k
     if (lane < 16) hs.cnt[lane] = 0;
@@ -536,6 +572,14 @@ __device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, Huff
         len[hs.sorted[k]] = (uint8_t)b;
     }
     __syncthreads();
+    HLCLK(5);
+#if OGE_EXP == 3
+    if (n == kLit && blockIdx.x == 0 && threadIdx.x == 0)
+        printf("huff_lengths lit: keys %llu sort %llu merge %llu depths %llu counts+lengths %llu (m %u)\n",
+               (unsigned long long)(g_hl_clk[1] - g_hl_clk[0]), (unsigned long long)(g_hl_clk[2] - g_hl_clk[1]),
+               (unsigned long long)(g_hl_clk[3] - g_hl_clk[2]), (unsigned long long)(g_hl_clk[4] - g_hl_clk[3]),
+               (unsigned long long)(g_hl_clk[5] - g_hl_clk[4]), m);
+#endif
 }
 
 // canonical codes, bit-reversed for LSB-first emission: out[i] = rcode | len << 16
@@ -605,19 +649,19 @@ __global__ void __launch_bounds__(64) k_defl_huff(const uint32_t *__restrict__ f
 #define XCLK()
 #endif
     XCLK();
-    for (int i = lane; i < kFreq; i += 64) f[i] = freq_in[(uint64_t)blockIdx.x * kFreq + i];
+    uint32_t nzl = 0, nzd = 0;  // used literal/length and distance codes (ballots: r05 counted on lane 0)
+    for (int i = lane, r = 0; r < (kFreq + 63) / 64; i += 64, ++r) {
+        const uint32_t v = i < kFreq ? freq_in[(uint64_t)blockIdx.x * kFreq + i] + (i == 256) : 0u;  // + end of block
+        if (i < kFreq) f[i] = v;
+        nzl += (uint32_t)__popcll(__ballot(i < kLit && v != 0));
+        nzd += (uint32_t)__popcll(__ballot(i >= kLit && i < kFreq && v != 0));
+    }
     __syncthreads();
-    if (lane == 0) {
-        f[256] = 1;  // end of block
-        // at least two used codes per tree (a one-code tree would be incomplete)
-        uint32_t nz = 0;
-        for (int i = 0; i < kLit; ++i) nz += f[i] != 0;
-        for (int i = 0; nz < 2 && i < kLit; ++i)
-            if (!f[i]) f[i] = 1, ++nz;
-        nz = 0;
-        for (int i = 0; i < kDist; ++i) nz += f[kLit + i] != 0;
-        for (int i = 0; nz < 2 && i < kDist; ++i)
-            if (!f[kLit + i]) f[kLit + i] = 1, ++nz;
+    if (lane == 0 && (nzl < 2 || nzd < 2)) {  // at least two used codes per tree (a one-code tree would be incomplete)
+        for (int i = 0; nzl < 2 && i < kLit; ++i)
+            if (!f[i]) f[i] = 1, ++nzl;
+        for (int i = 0; nzd < 2 && i < kDist; ++i)
+            if (!f[kLit + i]) f[kLit + i] = 1, ++nzd;
     }
     __syncthreads();
     XCLK();
