@@ -390,6 +390,7 @@ struct HuffScratch {
     uint16_t sorted[kLit];
     uint32_t w[2 * kLit];      // the leaves' weights (+ 2 sentinels), later the node depths
     uint32_t nw[kLit + 2];     // the internal nodes' weights, in creation order (+ sentinels)
+    uint64_t pick[(kLit + 31) / 32];  // the merge's picks, 2 bits per node: leaf first, leaf second
     uint16_t parent[2 * kLit]; // parent node, later the pointer-jumping ancestor
     uint32_t cnt[16];
     uint32_t m;
@@ -484,22 +485,50 @@ __device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, Huff
     if (lane < 2) hs.w[m + lane] = 0xffffffffu;
     for (uint32_t k = lane; k <= m; k += 64) hs.nw[k] = 0xffffffffu;
     __syncthreads();
-    if (lane == 0) {
+    if (lane == 0) {  // weights and picks only: the parents follow from the picks below, lane-parallel
         uint32_t i = 0, j = 0;
+        uint64_t bits = 0;
         for (uint32_t c = 0; c + 1 < m; ++c) {
             const uint32_t l0 = hs.w[i], l1 = hs.w[i + 1], n0 = hs.nw[j], n1 = hs.nw[j + 1];
             const bool p1 = l0 <= n0;  // first pick: the leaf unless the node is lighter
-            const uint32_t a = p1 ? i : m + j, wa = p1 ? l0 : n0;
+            const uint32_t wa = p1 ? l0 : n0;
             const uint32_t lh = p1 ? l1 : l0, nh = p1 ? n0 : n1;  // the queue heads after it
             const bool p2 = lh <= nh;
-            const uint32_t b = p2 ? (p1 ? i + 1 : i) : m + (p1 ? j : j + 1), wb = p2 ? lh : nh;
+            const uint32_t wb = p2 ? lh : nh;
             i += (uint32_t)p1 + (uint32_t)p2;
             j += 2u - (uint32_t)p1 - (uint32_t)p2;
             hs.nw[c] = wa + wb;
-            hs.parent[a] = (uint16_t)(m + c);
-            hs.parent[b] = (uint16_t)(m + c);
+            bits |= (uint64_t)((uint32_t)p1 | (uint32_t)p2 << 1) << (2 * (c & 31));
+            if ((c & 31) == 31) hs.pick[c >> 5] = bits, bits = 0;
         }
-        hs.parent[root] = (uint16_t)root;
+        if ((m - 1) & 31) hs.pick[(m - 2) >> 5] = bits;
+    }
+    __syncthreads();
+    // node c's children from the picks: the leaves taken before step c are a prefix sum of the picks (i_c),
+    // the nodes 2c - i_c; a leaf pick takes the next leaf, a node pick the next node
+    {
+        uint32_t carry = 0;  // leaves taken by the steps of the chunks before
+        for (uint32_t c0 = 0; c0 + 1 < m; c0 += 64) {
+            const uint32_t c = c0 + lane;
+            const bool live = c + 1 < m;
+            const uint32_t pb = live ? (uint32_t)(hs.pick[c >> 5] >> (2 * (c & 31))) & 3u : 0u;
+            const uint32_t p1 = pb & 1u, p2 = pb >> 1, nl = p1 + p2;
+            uint32_t inc = nl;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o, 64);
+                if (lane >= (uint32_t)o) inc += y;
+            }
+            const uint32_t ic = carry + inc - nl, jc = 2 * c - ic;  // queue heads at step c
+            carry += __shfl(inc, 63, 64);
+            if (live) {
+                const uint32_t a = p1 ? ic : m + jc;
+                const uint32_t b = p2 ? (p1 ? ic + 1 : ic) : m + (p1 ? jc : jc + 1);
+                hs.parent[a] = (uint16_t)(m + c);
+                hs.parent[b] = (uint16_t)(m + c);
+            }
+        }
+        if (lane == 0) hs.parent[root] = (uint16_t)root;
     }
     __syncthreads();
     HLCLK(3);
