@@ -558,47 +558,54 @@ __device__ void huff_lengths(const uint32_t *f, int n, int M, uint8_t *len, Huff
         __syncthreads();
     }
     HLCLK(4);
-    // leaves per clamped depth (ballots), Kraft repair (lane 0, <= 15 entries), lengths handed out
-    // longest-first to the least frequent symbols: rank k gets the b whose range holds k
+    // leaves per clamped depth (LDS atomics), Kraft repair (lane 0, <= 15 entries, only when the clamp made the
+    // code incomplete), lengths handed out longest-first to the least frequent symbols: rank k gets the b whose
+    // range holds k (r06: per-depth ballots and per-rank walks over the counts before)
     if (lane < 16) hs.cnt[lane] = 0;
     __syncthreads();
-    for (uint32_t k0 = 0; k0 < m; k0 += 64) {
-        const uint32_t k = k0 + lane;
-        const uint32_t dk = k < m ? min(hs.w[k], (uint32_t)M) : 0u;
-        for (int b = 1; b <= M; ++b) {
-            const uint32_t c = (uint32_t)__popcll(__ballot(k < m && dk == (uint32_t)b));
-            if (lane == 0 && c) hs.cnt[b] += c;
+    for (uint32_t k = lane; k < m; k += 64) atomicAdd(&hs.cnt[min(hs.w[k], (uint32_t)M)], 1u);
+    __syncthreads();
+    {
+        const uint32_t c = lane >= 1 && lane <= M ? hs.cnt[lane] : 0u;
+        uint32_t K = c << ((M - lane) & 31);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) K += __shfl_xor(K, o, 64);
+        if (lane == 0 && K != (1u << M)) {
+            const uint32_t one = 1u << M;
+            while (K > one) {  // over-subscribed after clamping: lengthen the longest code < M
+                int b = M - 1;
+                while (hs.cnt[b] == 0) --b;
+                hs.cnt[b]--;
+                hs.cnt[b + 1]++;
+                K -= 1u << (M - b - 1);
+            }
+            while (K < one) {  // under-subscribed: shorten the longest code that still fits
+                int b = M;
+                while (hs.cnt[b] == 0 || K + (1u << (M - b)) > one) --b;
+                hs.cnt[b]--;
+                hs.cnt[b - 1]++;
+                K += 1u << (M - b);
+            }
         }
     }
     __syncthreads();
-    if (lane == 0) {
-        const uint32_t one = 1u << M;
-        uint32_t K = 0;
-        for (int b = 1; b <= M; ++b) K += hs.cnt[b] << (M - b);
-        while (K > one) {  // over-subscribed after clamping: lengthen the longest code < M
-            int b = M - 1;
-            while (hs.cnt[b] == 0) --b;
-            hs.cnt[b]--;
-            hs.cnt[b + 1]++;
-            K -= 1u << (M - b - 1);
+    {
+        // suf[b] = codes of length >= b; rank k gets the number of b in 1..M with suf[b] > k
+        uint32_t suf = lane >= 1 && lane <= M ? hs.cnt[lane] : 0u;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t y = __shfl_down(suf, o, 64);
+            if (lane + o < 16) suf += y;
         }
-        while (K < one) {  // under-subscribed: shorten the longest code that still fits
-            int b = M;
-            while (hs.cnt[b] == 0 || K + (1u << (M - b)) > one) --b;
-            hs.cnt[b]--;
-            hs.cnt[b - 1]++;
-            K += 1u << (M - b);
+        uint32_t sb[15];
+#pragma unroll
+        for (int b = 0; b < 15; ++b) sb[b] = (uint32_t)__shfl((int)suf, b + 1, 64);
+        for (uint32_t k = lane; k < m; k += 64) {
+            uint32_t b = 0;
+#pragma unroll
+            for (int q = 0; q < 15; ++q) b += (q < M && k < sb[q]) ? 1u : 0u;
+            len[hs.sorted[k]] = (uint8_t)b;
         }
-    }
-    __syncthreads();
-    for (uint32_t k = lane; k < m; k += 64) {
-        uint32_t acc = 0, b = M;
-        for (int bb = M; bb >= 1; --bb) {  // ranks [acc, acc + cnt[bb]) get length bb
-            const uint32_t c = hs.cnt[bb];
-            if (k >= acc && k < acc + c) b = bb;
-            acc += c;
-        }
-        len[hs.sorted[k]] = (uint8_t)b;
     }
     __syncthreads();
     HLCLK(5);
