@@ -58,7 +58,6 @@ struct DeflTab {
 };
 
 
-__device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashBits); }
 
 // length 3..258 -> symbol 257..285, extra bits, extra value
 __device__ __forceinline__ void len_code(uint32_t L, uint32_t &sym, uint32_t &nb, uint32_t &ev) {
@@ -94,8 +93,9 @@ __device__ __forceinline__ void dist_code(uint32_t D, uint32_t &sym, uint32_t &n
 // positions (two per payload):
 //   candidates  rounds of R * 512 consecutive positions: position p looks up the 4096-bucket hash of its
 //               4-byte prefix (the table as the earlier rounds left it: deterministic), keeps the
-//               candidate only if the 4 bytes match within 32 KiB, then the round's positions enter the
-//               table (atomicMax: the latest position wins).  A wave's 64 lanes hold 64 consecutive
+//               candidate only if its 15-bit tag matches within 32 KiB (r06; the 4 bytes themselves are
+//               compared where the parse visits it), then the round's positions enter the table
+//               (atomicMax: the latest position wins).  A wave's 64 lanes hold 64 consecutive
 //               positions = one 64-byte segment, so one ballot gives the segment's candidate mask.
 //   parse       each thread greedily parses its own segment: literal runs are skipped with the mask
 //               (ctz to the next candidate: no per-literal work in the serial chain); at a candidate the
@@ -132,6 +132,7 @@ constexpr uint32_t kPre = kPay / 4 / kTP + 1;  // prefetched words per thread (1
 // predecessor, so the chain never leaves the prefix; it ends at the sub-block's start) and takes the longest
 // match of up to `depth` of them; with lazy, a match shorter than 32 bytes gives way to a literal when the
 // next position's best match is longer (zlib's lazy evaluation).  depth 1 without lazy: the greedy parse.
+template <bool CHAIN>  // depth > 1 (levels 8-9): exact candidates for the chain walks
 __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ src, uint64_t n, uint64_t blk0, uint64_t nb,
                                                    uint64_t *__restrict__ lmask, uint8_t *__restrict__ nmatch,
                                                    uint32_t *__restrict__ mlist, uint32_t *__restrict__ freq_out, int depth,
@@ -241,9 +242,17 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
                 uint32_t h = 0, c = 0;
                 if (p + 4 <= len) {
                     const uint32_t w = ld32(in, p);
-                    h = hash4(w);
-                    const uint32_t j1 = A[h];
-                    if (j1 && p - (j1 - 1) <= 32768 && ld32(in, j1 - 1) == w) c = j1;
+                    // bucket = the top 12 bits of the multiplicative hash.  Levels 1-7 (r06): entries are
+                    // position + 1 << 15 | tag, the tag the hash's next 15 bits, so a bucket entry of another
+                    // prefix is rejected in registers instead of by reading the candidate's bytes inside this
+                    // chain of dependent LDS reads (20M reads: 27.15 -> 26.32 ms, the same bytes); the rare tag
+                    // collisions are caught where the parse visits a candidate.  The chained levels keep
+                    // entries of position + 1 and verify the 4 bytes here: every cand entry they walk is exact.
+                    const uint32_t x = w * 2654435761u, tg = CHAIN ? 0u : (x >> 5) & 0x7fffu;
+                    h = x >> (32 - kHashBits);
+                    const uint32_t e = A[h], j1 = CHAIN ? e : e >> 15;
+                    if (j1 && p - (j1 - 1) <= 32768 && (CHAIN ? ld32(in, j1 - 1) == w : (e & 0x7fffu) == tg)) c = j1;
+                    h |= tg << 16;
                 }
                 hh[k] = h;
                 cc[k] = c;
@@ -254,9 +263,10 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
                 if (p < end) cand[p - base] = (uint16_t)cc[k];
                 if (vp[k]) atomicMax(&B[hp[k]], vp[k]);
                 const bool ins = p + 4 <= len && p < end;
-                if (ins) atomicMax(&B[hh[k]], p + 1);
-                hp[k] = hh[k];
-                vp[k] = ins ? p + 1 : 0u;
+                const uint32_t iv = CHAIN ? p + 1 : ((p + 1) << 15) | (hh[k] >> 16), hb = hh[k] & 0xffffu;
+                if (ins) atomicMax(&B[hb], iv);
+                hp[k] = hb;
+                vp[k] = ins ? iv : 0u;
             }
             __syncthreads();
         }
@@ -309,8 +319,13 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
             // nearest of equal lengths)
             auto best = [&](uint32_t q, uint32_t *jo) {
                 const uint32_t pq = s0 + q, maxL = min(258u, sl - q);
-                uint32_t j = cand[pq - base] - 1, L = ext(pq, j, maxL), bj = j;
-                for (int d = 1; d < depth && L < maxL; ++d) {
+                uint32_t j = cand[pq - base] - 1;
+                if (!CHAIN && ld32(in, pq) != ld32(in, j)) {  // a tag collision: no candidate (a literal)
+                    *jo = j;
+                    return 0u;
+                }
+                uint32_t L = ext(pq, j, maxL), bj = j;
+                for (int d = 1; CHAIN && d < depth && L < maxL; ++d) {
                     if (j < base) break;
                     const uint32_t nx = cand[j - base];
                     if (!nx || pq - (nx - 1) > 32768) break;
@@ -329,7 +344,7 @@ __global__ void __launch_bounds__(kTP) k_defl_parse(const uint8_t *__restrict__ 
                 const uint32_t pq = s0 + q;
                 uint32_t j;
                 const uint32_t L = best(q, &j);
-                if (lazy && L >= 3 && L < 32 && q + 1 < sl && ((cm >> (q + 1)) & 1)) {
+                if (CHAIN && lazy && L >= 3 && L < 32 && q + 1 < sl && ((cm >> (q + 1)) & 1)) {
                     uint32_t j1;
                     if (best(q + 1, &j1) > L) {  // a literal here, the longer match from the next position
                         lit |= 1ull << q;
@@ -1338,8 +1353,12 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     for (uint64_t b0 = 0; b0 < nblk; b0 += chunk, ++k) {
         const uint32_t nb = (uint32_t)std::min(chunk, nblk - b0);
         Bufs &u = B[k % S];
-        k_defl_parse<<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)ncu), kTP, 0, u.st>>>(d_src, n, b0, nb, u.lmask, u.nmatch,
-                                                                                      u.mlist, u.freq, depth, lazy);
+        if (depth > 1)
+            k_defl_parse<true><<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)ncu), kTP, 0, u.st>>>(d_src, n, b0, nb, u.lmask, u.nmatch,
+                                                                                            u.mlist, u.freq, depth, lazy);
+        else
+            k_defl_parse<false><<<(uint32_t)std::min<uint64_t>(nb, (uint64_t)ncu), kTP, 0, u.st>>>(d_src, n, b0, nb, u.lmask, u.nmatch,
+                                                                                             u.mlist, u.freq, 1, 0);
         OGE_LAUNCH_CHECK(ctx);
         k_defl_huff<<<nb, 64, 0, u.st>>>(u.freq, u.tabs, n, b0, level, u.sizes);
         OGE_LAUNCH_CHECK(ctx);
