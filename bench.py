@@ -458,6 +458,7 @@ def kernel_leg(ctx, L, torch, dev, p, n, hlen, args) -> tuple[dict, DevBuf, int,
         res = {"what": "oge_sort_markdup_dev over records already decoded in HBM (no codec)",
                "ms_per_step": round(dt * 1e3, 2), "mreads_per_s": round(n / dt / 1e6, 1), "steps": K,
                "duplicates_flagged": nd, "stages_ms": sms,
+               "mate_join": {k: ctx.counter("md_mate_" + k) for k in ("pairs", "left", "ovf", "redo")},
                "gather_roofline": {"kernel": "k_gather16", "achieved_GBps": round(2 * B / tg / 1e9, 1) if tg else None,
                                    "frac": round(2 * B / tg / 1e9 / HBM_PEAK_GBS, 4) if tg else None,
                                    "algorithmic_bytes": 2 * B}}

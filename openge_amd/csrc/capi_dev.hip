@@ -5,6 +5,7 @@
 #include "bam_layout.h"
 #include "synth.h"
 #include "records.h"
+#include "markdup_stages.h"
 
 #include <cstdio>
 #include <cstring>
@@ -22,6 +23,9 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
                        const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out, uint64_t *d_desc, bool *desc_ok,
                        const uint64_t *skeys);
 int oge_meta_gather(oge_ctx *ctx, const RecMeta *in, const uint32_t *perm, uint64_t n, RecMeta *out);
+int oge_sort_keys_dev_hook(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+                           bool keys_ready, uint64_t **kout, uint32_t **vout, const RecMeta *meta_in, RecMeta *meta_out,
+                           const OgeSortGatherHook *hook);
 int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
                     uint8_t *d_dup, int apply, uint64_t *n_dup_out);
 
@@ -454,14 +458,28 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
     RecMeta *meta = (RecMeta *)ctx->ws("md_meta", (n + 1) * sizeof(RecMeta));
     uint8_t *dd = (uint8_t *)ctx->ws("sm_dup", n + 1);
     if (!meta || !dd) return OGE_ERR_HIP;
-    rc = oge_sort_keys_dev(ctx, d_recs, d_off, n, opts->n_ref, true, &k, &v, meta_in, meta);
+    // the summaries are gathered after the tie sort, in final order, by the same pass that derives the
+    // mate-join / fragment / descriptor words from them (oge_md_cand_frag_gather: one pass over the rows)
+    struct Cf {
+        const oge_markdup_opts *opts;
+        const RecMeta *in;
+        RecMeta *out;
+        uint64_t n;
+        OgeMdFrags F;
+    } cf{opts, meta_in, meta, n, {}};
+    OgeSortGatherHook hook{[](void *u, oge_ctx *c, const uint32_t *perm, const uint64_t *skeys) {
+                               Cf *x = (Cf *)u;
+                               return oge_md_cand_frag_gather(c, x->opts, x->in, perm, x->n, x->out, true, skeys, &x->F);
+                           },
+                           &cf};
+    rc = oge_sort_keys_dev_hook(ctx, d_recs, d_off, n, opts->n_ref, true, &k, &v, meta_in, meta, &hook);
     if (rc) return rc;
     if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_perm, v, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
     uint64_t nd = 0;
     uint64_t *desc = (uint64_t *)ctx->ws("sm_desc", (n + 1) * 8);
     if (!desc) return OGE_ERR_HIP;
     bool desc_ok = false;
-    rc = oge_markdup_finish(ctx, (uint8_t *)d_recs, d_off, n, opts, meta, dd, 0, &nd, desc, &desc_ok, k);
+    rc = oge_markdup_finish_pre(ctx, (uint8_t *)d_recs, d_off, n, opts, meta, dd, 0, &nd, desc, &desc_ok, k, n ? &cf.F : nullptr);
     if (rc) return rc;
     if (n_dup_out) *n_dup_out = nd;
     ctx->end_loan();  // the gather below writes d_out

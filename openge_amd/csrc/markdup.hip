@@ -402,6 +402,28 @@ __device__ __forceinline__ uint64_t frag_key(const RecMeta &R, KeyLayout L) {
 //              by k_apply_desc once the dup bits are known; a src past 39 bits sets *ovf.
 // skeys (optional): the records' sorted coordinate keys; then the fragment coordinates' deviation
 // from the anchors is reduced into dev[0..1] for the windowed fragment groups.
+// the products of record i from its summary (only the first 32 bytes of R are read: m, src, seq, coord, hash)
+__device__ __forceinline__ void cand_frag_one(const RecMeta &R, uint64_t i, KeyLayout L, CandKey ck, uint32_t *__restrict__ f,
+                                              uint64_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                                              uint64_t *__restrict__ cval, uint64_t *__restrict__ desc0,
+                                              unsigned int *__restrict__ ovf, const uint64_t *__restrict__ skeys, bool &has,
+                                              int64_t &ax, int64_t &cx) {
+    f[i] = (R.m & OGE_M_CAND) ? 1u : 0u;
+    keys[i] = frag_key(R, L);
+    vals[i] = (uint32_t)i;
+    cval[i] = ((oge_meta_hash48(R) >> (48 - ck.hb)) << ck.ib) | i;
+    if (desc0) {
+        if (R.src >> 39) atomicOr(ovf, 1u);
+        desc0[i] = (R.src & ((1ull << 39) - 1)) | ((R.m & OGE_M_PRIMARY) ? (1ull << 39) : 0ull) |
+                   ((R.m >> 48) << 40) | (((R.m >> 40) & 0xff) << 56);
+    }
+    if (skeys && (R.m & OGE_M_FRAG)) {
+        has = true;
+        ax = anchor_of_key(skeys[i]);
+        cx = win_x((uint32_t)R.seq, (int64_t)R.coord + 1);
+    }
+}
+
 __global__ __launch_bounds__(kT) void k_cand_frag(const RecMeta *__restrict__ meta, uint64_t n, KeyLayout L, CandKey ck,
                                                    uint32_t *__restrict__ f, uint64_t *__restrict__ keys,
                                                    uint32_t *__restrict__ vals, uint64_t *__restrict__ cval,
@@ -412,22 +434,50 @@ __global__ __launch_bounds__(kT) void k_cand_frag(const RecMeta *__restrict__ me
     int64_t ax = 0, cx = 0;
     if (i < n) {
         const RecMeta R = meta[i];
-        f[i] = (R.m & OGE_M_CAND) ? 1u : 0u;
-        keys[i] = frag_key(R, L);
-        vals[i] = (uint32_t)i;
-        cval[i] = ((oge_meta_hash48(R) >> (48 - ck.hb)) << ck.ib) | i;
-        if (desc0) {
-            if (R.src >> 39) atomicOr(ovf, 1u);
-            desc0[i] = (R.src & ((1ull << 39) - 1)) | ((R.m & OGE_M_PRIMARY) ? (1ull << 39) : 0ull) |
-                       ((R.m >> 48) << 40) | (((R.m >> 40) & 0xff) << 56);
-        }
-        if (skeys && (R.m & OGE_M_FRAG)) {
-            has = true;
-            ax = anchor_of_key(skeys[i]);
-            cx = win_x((uint32_t)R.seq, (int64_t)R.coord + 1);
-        }
+        cand_frag_one(R, i, L, ck, f, keys, vals, cval, desc0, ovf, skeys, has, ax, cx);
     } else if (i == n) {
         f[i] = 0;
+    }
+    if (skeys) win_dev_update(has, ax, cx, dev);
+}
+
+// k_cand_frag fused into the summary gather (r06, the one-GPU sort + dedup pipeline): out[i] = in[perm[i]]
+// with four lanes per 64-byte row (as k_meta_gather), and the first lane of each four, given the second
+// lane's 16 bytes by a shuffle, writes k_cand_frag's products for output record i -- the sorted rows are not
+// streamed a second time.  perm is the FINAL order (the tie sort ran on perm first: k_ties_meta<false>).
+__global__ __launch_bounds__(kT) void k_meta_gather_cf(const RecMeta *__restrict__ in, const uint32_t *__restrict__ perm,
+                                                        uint64_t n, RecMeta *__restrict__ out, KeyLayout L, CandKey ck,
+                                                        uint32_t *__restrict__ f, uint64_t *__restrict__ keys,
+                                                        uint32_t *__restrict__ vals, uint64_t *__restrict__ cval,
+                                                        uint64_t *__restrict__ desc0, unsigned int *__restrict__ ovf,
+                                                        const uint64_t *__restrict__ skeys, unsigned long long *__restrict__ dev) {
+    static_assert(sizeof(RecMeta) == 64 && offsetof(RecMeta, seq) == 16 && offsetof(RecMeta, hash) == 28,
+                  "m, src in the first 16 bytes; seq, coord, rgi, hash_hi, hash in the next 16");
+    const uint64_t g = (uint64_t)blockIdx.x * kT + threadIdx.x, i = g >> 2;
+    const uint32_t part = (uint32_t)g & 3, lane = threadIdx.x & 63;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (i < n) {
+        v = ((const uint4 *)(in + perm[i]))[part];
+        ((uint4 *)(out + i))[part] = v;
+    }
+    const uint32_t b0 = __shfl(v.x, (int)lane + 1, 64), b1 = __shfl(v.y, (int)lane + 1, 64);
+    const uint32_t b2 = __shfl(v.z, (int)lane + 1, 64), b3 = __shfl(v.w, (int)lane + 1, 64);
+    bool has = false;
+    int64_t ax = 0, cx = 0;
+    if (part == 0) {
+        if (i < n) {
+            RecMeta R;
+            R.m = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            R.src = (uint64_t)v.z | ((uint64_t)v.w << 32);
+            R.seq = (int32_t)b0;
+            R.coord = (int32_t)b1;
+            R.rgi = (int16_t)(b2 & 0xffff);
+            R.hash_hi = (uint16_t)(b2 >> 16);
+            R.hash = b3;
+            cand_frag_one(R, i, L, ck, f, keys, vals, cval, desc0, ovf, skeys, has, ax, cx);
+        } else if (i == n) {
+            f[n] = 0;
+        }
     }
     if (skeys) win_dev_update(has, ax, cx, dev);
 }
@@ -780,6 +830,32 @@ __device__ __forceinline__ uint32_t mj_bit(uint64_t key, uint32_t bmask) { retur
 constexpr int kMjProbes = 64;
 constexpr uint32_t kPending = 2;  // lflag: the partner lies in another tile, k_mate_agree decides
 
+// Leftovers (records the sort-based join pairs) appended to lk as their candidate keys (hash bits << ib |
+// index).  One counter would serialise the appends at its L2 channel (~88 atomics/us: at 300M reads ~2M wave
+// appends took 20 ms), so the list is striped: record r goes to stripe (r >> 10) % kMjStripes, each stripe
+// with its own counter (128 bytes apart) and a region of lcap slots -- every record is appended at most once
+// and a stripe's records number at most lcap, so no region overflows.  k_left_pack then concatenates them.
+constexpr uint32_t kMjStripes = 64, kMjCntStride = 32;
+__device__ __forceinline__ uint32_t mj_stripe(uint64_t r) { return (uint32_t)(r >> 10) & (kMjStripes - 1); }
+// the lanes of a wave hold 64 consecutive records of one 1024-record tile: one stripe, one atomic per wave
+__device__ __forceinline__ void mj_left(bool pred, uint64_t key, uint64_t rec, uint64_t *__restrict__ lk,
+                                        unsigned int *__restrict__ lcnt, uint32_t lcap) {
+    const uint64_t m = __ballot(pred);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)(__ffsll((long long)m) - 1);
+    const uint32_t st = mj_stripe(rec);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(lcnt + st * kMjCntStride, (unsigned int)__popcll(m));
+    base = __shfl(base, (int)leader, 64) + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    if (pred) lk[(uint64_t)st * lcap + base] = key;
+}
+// one record of any tile (the partner end of a conflicting window pair: rare)
+__device__ __forceinline__ void mj_left1(uint64_t key, uint64_t rec, uint64_t *__restrict__ lk, unsigned int *__restrict__ lcnt,
+                                         uint32_t lcap) {
+    const uint32_t st = mj_stripe(rec);
+    lk[(uint64_t)st * lcap + atomicAdd(lcnt + st * kMjCntStride, 1u)] = key;
+}
+
 // a leftover's hash bits into the conflict set (bitmap filter + open-addressing table)
 __device__ __forceinline__ void mj_conflict(uint64_t h, unsigned long long *__restrict__ tab, uint32_t mask,
                                             uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf) {
@@ -801,7 +877,8 @@ __device__ __forceinline__ void mj_conflict(uint64_t h, unsigned long long *__re
 __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ cflag, const uint64_t *__restrict__ cval, uint64_t n,
                                                    uint32_t ib, uint32_t *__restrict__ partner, uint32_t *__restrict__ mate,
                                                    uint32_t *__restrict__ lflag, unsigned long long *__restrict__ tab, uint32_t mask,
-                                                   uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf) {
+                                                   uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf,
+                                                   uint64_t *__restrict__ lk, unsigned int *__restrict__ lcnt, uint32_t lcap) {
     __shared__ uint32_t key[kMjSlots], lo[kMjSlots], hi[kMjSlots], cnt[kMjSlots];
     __shared__ uint64_t hv[kMjT + 2 * kMjW];  // the window's hash bits (0: not a candidate)
     const uint32_t t = threadIdx.x;
@@ -830,8 +907,9 @@ __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ 
     if (i >= n) return;
     const uint32_t w = t + kMjW;
     uint32_t r = kNone, m = kNone, lf = 0;
+    uint64_t h = 0;
     if (hv[w]) {
-        const uint64_t h = hv[w] - 1;
+        h = hv[w] - 1;
         const uint32_t f = mj_fp(h);
         uint32_t s = (f * 2654435761u) >> 20;
         while (key[s] != f) s = (s + 1) & (kMjSlots - 1);
@@ -855,6 +933,7 @@ __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ 
             mj_conflict(h, tab, mask, bits, bmask, ovf);
         }
     }
+    mj_left(lf == 1, (h << ib) | i, i, lk, lcnt, lcap);
     partner[i] = r;
     mate[i] = m;
     lflag[i] = lf;
@@ -866,68 +945,100 @@ __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ 
 __global__ __launch_bounds__(kT) void k_mate_agree(const uint64_t *__restrict__ cval, uint64_t n, uint32_t ib,
                                                    const uint32_t *__restrict__ partner, uint32_t *__restrict__ mate,
                                                    uint32_t *__restrict__ lflag, unsigned long long *__restrict__ tab, uint32_t mask,
-                                                   uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf) {
+                                                   uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf,
+                                                   uint64_t *__restrict__ lk, unsigned int *__restrict__ lcnt, uint32_t lcap) {
     const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
     if (i >= n || lflag[i] != kPending) return;
     const uint32_t j = partner[i];
-    const uint64_t h = cval[i] >> ib;
-    if (partner[j] == (uint32_t)i && (cval[j] >> ib) == h) {
+    const uint64_t ci = cval[i], h = ci >> ib;
+    const bool agree = partner[j] == (uint32_t)i && (cval[j] >> ib) == h;
+    if (agree) {
         if (i < j) mate[i] = j;
         lflag[i] = 0;
     } else {
         lflag[i] = 1;
         mj_conflict(h, tab, mask, bits, bmask, ovf);
     }
+    mj_left(!agree, ci, i, lk, lcnt, lcap);
 }
 
-// also writes pflag[i] (a pair is owned by i) for every record
+// also counts the pairs each 256-record block owns (bcnt[blockIdx]: mate[i] != kNone afterwards; k_mate_scatter
+// adds the sort path's) for k_mate_compact (r06: per-record owner flags and their full scan before)
 __global__ __launch_bounds__(kT) void k_mate_check(const uint64_t *__restrict__ cval, uint64_t n, uint32_t ib,
                                                    const unsigned long long *__restrict__ tab, uint32_t mask,
                                                    const uint32_t *__restrict__ bits, uint32_t bmask, uint32_t *__restrict__ mate,
-                                                   uint32_t *__restrict__ lflag, uint32_t *__restrict__ pflag) {
+                                                   uint32_t *__restrict__ bcnt, uint64_t *__restrict__ lk,
+                                                   unsigned int *__restrict__ lcnt, uint32_t lcap) {
+    __shared__ uint32_t ws[kT / 64];
     const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i > n) return;
-    if (i == n) { pflag[n] = 0; return; }
-    const uint32_t m = mate[i];
+    const uint32_t m = i < n ? mate[i] : kNone;
     uint32_t own = 0;
+    bool hit = false;
+    uint64_t h = 0;
     if (m != kNone) {
         own = 1;
-        const unsigned long long key = (cval[i] >> ib) + 1;
+        h = cval[i] >> ib;
+        const unsigned long long key = h + 1;
         const uint32_t b = mj_bit(key, bmask);
         uint32_t s = mj_slot(key, mask);
-        bool hit = ((bits[b >> 5] >> (b & 31)) & 1u) != 0;  // a probe run longer than the insert bound: only after an overflow
+        hit = ((bits[b >> 5] >> (b & 31)) & 1u) != 0;  // a probe run longer than the insert bound: only after an overflow
         for (int p = 0; hit && p < kMjProbes; ++p) {
             const unsigned long long o = tab[s];
             if (o == key) break;
             if (o == 0ull) { hit = false; break; }
             s = (s + 1) & mask;
         }
-        if (hit) {
+        if (hit) {  // both ends to the leftovers (a window pair's ends have equal hash bits)
             mate[i] = kNone;
-            lflag[i] = 1;
-            lflag[m] = 1;
             own = 0;
         }
     }
-    pflag[i] = own;
+    mj_left(hit, (h << ib) | i, i, lk, lcnt, lcap);
+    if (hit) mj_left1((h << ib) | m, m, lk, lcnt, lcap);
+    const uint32_t wsum = oge_wave_sum(own);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = wsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int q = 0; q < kT / 64; ++q) t += ws[q];
+        bcnt[blockIdx.x] = t;
+    }
 }
 
-// the sort path's pairs of leftovers (a << 32 | b, a < b) -> mate[a] = b | kSortPair, pflag[a] = 1
+// the sort path's pairs of leftovers (a << 32 | b, a < b) -> mate[a] = b | kSortPair, counted in a's block
 __global__ __launch_bounds__(kT) void k_mate_scatter(const uint64_t *__restrict__ pairs, uint32_t np, uint32_t *__restrict__ mate,
-                                                     uint32_t *__restrict__ pflag) {
+                                                     uint32_t *__restrict__ bcnt) {
     const uint32_t p = blockIdx.x * kT + threadIdx.x;
     if (p >= np) return;
     uint32_t a = (uint32_t)(pairs[p] >> 32), b = (uint32_t)pairs[p];
     if (a > b) { const uint32_t x = a; a = b; b = x; }
     mate[a] = b | kSortPair;
-    pflag[a] = 1;
+    atomicAdd(&bcnt[a / kT], 1u);
 }
 
-// pairs in first-record order from the scanned owner flags
-__global__ __launch_bounds__(kT) void k_mate_compact(const uint32_t *__restrict__ pos, const uint32_t *__restrict__ mate, uint64_t n,
+// pairs in first-record order: block b's owners (mate[i] != kNone) from boff[b] (the scanned block counts) in
+// record order -- ranks by ballot inside each wave, wave offsets through LDS
+__global__ __launch_bounds__(kT) void k_mate_compact(const uint32_t *__restrict__ boff, const uint32_t *__restrict__ mate, uint64_t n,
                                                      uint64_t *__restrict__ pairs) {
+    __shared__ uint32_t ws[kT / 64];
     const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i < n && pos[i + 1] != pos[i]) pairs[pos[i]] = (i << 32) | mate[i];
+    const uint32_t m = i < n ? mate[i] : kNone, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool own = m != kNone;
+    const uint64_t b = __ballot(own);
+    if (lane == 0) ws[w] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t r = boff[blockIdx.x] + (uint32_t)__popcll(b & ((1ull << lane) - 1));
+    for (uint32_t q = 0; q < w; ++q) r += ws[q];
+    if (own) pairs[r] = (i << 32) | m;
+}
+
+// the stripes of lk concatenated into out (stripe s from the sum of the counts before it): blockIdx.y = stripe
+__global__ __launch_bounds__(kT) void k_left_pack(const uint64_t *__restrict__ lk, const unsigned int *__restrict__ lcnt, uint32_t lcap,
+                                                  uint64_t *__restrict__ out) {
+    const uint32_t st = blockIdx.y, c = lcnt[st * kMjCntStride];
+    uint32_t off = 0;
+    for (uint32_t q = 0; q < st; ++q) off += lcnt[q * kMjCntStride];
+    for (uint32_t j = blockIdx.x * kT + threadIdx.x; j < c; j += gridDim.x * kT) out[off + j] = lk[(uint64_t)st * lcap + j];
 }
 
 uint32_t bits_for(uint64_t v) {  // bits to hold values 0..v
@@ -1044,8 +1155,9 @@ static bool mate_window_ok(const oge_markdup_opts *opts, uint64_t n, const uint6
     return skeys && n && n < (1ull << 31) && opts->split_chains <= 1 && opts->debug_hash_bits <= 0 && mate_win_enabled();
 }
 
-int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
-                     OgeMdFrags *f, const uint64_t *skeys) {
+// gin / perm (the fused gather): meta[i] = gin[perm[i]] is written here too, by k_meta_gather_cf
+static int cand_frag_launch(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
+                            OgeMdFrags *f, const uint64_t *skeys, const RecMeta *gin, const uint32_t *perm) {
     KeyLayout L;
     int rc = md_layout(ctx, opts, &L);
     if (rc) return rc;
@@ -1067,9 +1179,23 @@ int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *
         if (!f->dev) return OGE_ERR_HIP;
         OGE_HIP_TRY(ctx, hipMemsetAsync(f->dev, 0, 4 * kDevSlots * sizeof(unsigned long long), ctx->stream));
     }
-    hipLaunchKernelGGL(k_cand_frag, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, L, ckl, f->cpos, f->fk,
-                       f->fv, f->cval, f->desc0, cnt + 3, skeys, f->dev);
+    if (perm)
+        hipLaunchKernelGGL(k_meta_gather_cf, dim3(oge_ceil_div(4 * (n + 1), kT)), dim3(kT), 0, ctx->stream, gin, perm, n,
+                           (RecMeta *)meta, L, ckl, f->cpos, f->fk, f->fv, f->cval, f->desc0, cnt + 3, skeys, f->dev);
+    else
+        hipLaunchKernelGGL(k_cand_frag, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, meta, n, L, ckl, f->cpos, f->fk,
+                           f->fv, f->cval, f->desc0, cnt + 3, skeys, f->dev);
     OGE_LAUNCH_CHECK(ctx);
+    f->fused = perm != nullptr;
+    return OGE_OK;
+}
+
+// after the launch: the candidate scan (unless the windowed join takes the flags) and the overflow word
+static int cand_frag_post(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, OgeMdFrags *f) {
+    unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
+    if (!cnt) return OGE_ERR_HIP;
+    const uint64_t *skeys = f->skeys;
+    int rc;
     uint32_t nc = 0, ovf = 0;
     f->cpos_scanned = !mate_window_ok(opts, n, skeys);  // the windowed join reads the flags as they are
     if (f->cpos_scanned) {
@@ -1084,14 +1210,29 @@ int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *
     return OGE_OK;
 }
 
+int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
+                     OgeMdFrags *f, const uint64_t *skeys) {
+    int rc = cand_frag_launch(ctx, opts, meta, n, want_desc, f, skeys, nullptr, nullptr);
+    return rc ? rc : cand_frag_post(ctx, opts, n, f);
+}
+
+int oge_md_cand_frag_gather(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *in, const uint32_t *perm, uint64_t n,
+                            RecMeta *out, bool want_desc, const uint64_t *skeys, OgeMdFrags *f) {
+    return cand_frag_launch(ctx, opts, out, n, want_desc, f, skeys, in, perm);
+}
+
 // The sort-based ReadEndsMap pairing (mark_duplicates.cpp:210-245) of the candidates flagged by cpos
 // (exclusive scan of the flags, nc of them) -> pairs a << 32 | b (a first seen), *np of them, in
 // candidate-hash order, in ws "md_pairs"; "md_pairs2" is the spare of the same size.
+// packed (optional): the nc candidate keys already in an array of at least nc + 1 (in any order; cpos unused):
+// sorted on hash AND index bits, which puts each hash run in record order as the stable hash-only sort does
+// for keys packed in record order.
 static int join_sorted(oge_ctx *ctx, const CandKey &ckl, const uint8_t *recs, const RecMeta *meta, uint64_t n, const uint32_t *cpos,
-                       const uint64_t *cval, uint32_t nc, uint64_t **pairs_out, uint64_t **spare_out, uint32_t *np_out) {
+                       const uint64_t *cval, uint32_t nc, uint64_t **pairs_out, uint64_t **spare_out, uint32_t *np_out,
+                       uint64_t *packed = nullptr) {
     unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
     const uint64_t nc1 = (uint64_t)nc + 1;
-    uint64_t *ck = (uint64_t *)ctx->scratch("md_ck", nc1 * 8);
+    uint64_t *ck = packed ? packed : (uint64_t *)ctx->scratch("md_ck", nc1 * 8);
     uint64_t *ck2 = (uint64_t *)ctx->scratch("md_ck2", nc1 * 8);
     uint8_t *used = (uint8_t *)ctx->scratch("md_used", nc1);
     uint32_t *pflag = (uint32_t *)ctx->scratch("md_pflag", nc1 * 4);
@@ -1100,12 +1241,13 @@ static int join_sorted(oge_ctx *ctx, const CandKey &ckl, const uint8_t *recs, co
     uint64_t *pairs2 = (uint64_t *)ctx->scratch("md_pairs2", (nc1 / 2 + 1) * 8);
     uint32_t *slow = (uint32_t *)ctx->scratch("md_slow", nc1 * 4);
     if (!cnt || !ck || !ck2 || !used || !pflag || !sparse || !pairs || !pairs2 || !slow) return OGE_ERR_HIP;
-    if (n) {
+    if (n && !packed) {
         hipLaunchKernelGGL(k_cand_pack, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, cpos, cval, n, ck);
         OGE_LAUNCH_CHECK(ctx);
     }
     uint64_t *sk;
-    int rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, ((1ull << ckl.hb) - 1) << ckl.ib, &sk, nullptr);
+    const uint64_t smask = ((1ull << ckl.hb) - 1) << ckl.ib | (packed ? ckl.idx_mask() : 0ull);
+    int rc = oge_radix_sort_pairs(ctx, ck, nullptr, ck2, nullptr, nc, smask, &sk, nullptr);
     if (rc) return rc;
     OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + 2, 0, 4, ctx->stream));
     hipLaunchKernelGGL(k_pair_runs, dim3(oge_ceil_div(nc1, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)sk, (uint64_t)nc, ckl,
@@ -1166,12 +1308,19 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
                        const OgeMdFrags &f, OgeMdPairs *P, bool *done) {
     *done = false;
     unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
+    unsigned int *lcnt = (unsigned int *)ctx->ws("md_lcnt", kMjStripes * kMjCntStride * 4);
+    const uint32_t nb = (uint32_t)oge_ceil_div(n, kT);
     uint32_t *partner = (uint32_t *)ctx->scratch("md_mpart", (n + 1) * 4);
     uint32_t *mate = (uint32_t *)ctx->scratch("md_mate", (n + 1) * 4);
     uint32_t *lflag = (uint32_t *)ctx->scratch("md_lflag", (n + 1) * 4);
-    uint32_t *oflag = (uint32_t *)ctx->scratch("md_oflag", (n + 1) * 4);
+    uint32_t *bcnt = (uint32_t *)ctx->scratch("md_bcnt", ((uint64_t)nb + 1) * 4);
     uint64_t *wpairs = (uint64_t *)ctx->scratch("md_wpairs", (n / 2 + 1) * 8);
-    if (!cnt || !partner || !mate || !lflag || !oflag || !wpairs) return OGE_ERR_HIP;
+    // the leftovers' candidate keys, appended by the three kernels below into kMjStripes regions of lcap
+    // slots (the records of a stripe's 1024-record tiles: see mj_left), then packed (r06: flags, a scan over all
+    // records and a packing pass before)
+    const uint32_t lcap = (uint32_t)(oge_ceil_div(oge_ceil_div(n, 1024), kMjStripes) * 1024ull);
+    uint64_t *lk = (uint64_t *)ctx->scratch("md_lk", (uint64_t)kMjStripes * lcap * 8);
+    if (!cnt || !lcnt || !partner || !mate || !lflag || !bcnt || !wpairs || !lk) return OGE_ERR_HIP;
     // the conflict set: a table of >= n/16 slots behind a bitmap of >= n/2 bits, at most 4 MiB so it stays in
     // an XCD's L2 for k_mate_check's random reads (a probe run past kMjProbes means too many leftovers for the
     // window path: the sort path decides)
@@ -1182,46 +1331,54 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
     uint32_t *bits = (uint32_t *)ctx->scratch("md_mbits", nbits / 8);
     if (!tab || !bits) return OGE_ERR_HIP;
     OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 16, ctx->stream));
+    OGE_HIP_TRY(ctx, hipMemsetAsync(lcnt, 0, kMjStripes * kMjCntStride * 4, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(tab, 0, (uint64_t)slots * 8, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(bits, 0, nbits / 8, ctx->stream));
     hipLaunchKernelGGL(k_mate_win, dim3(oge_ceil_div(n, kMjT)), dim3(kMjT), 0, ctx->stream, (const uint32_t *)f.cpos,
-                       (const uint64_t *)f.cval, n, ckl.ib, partner, mate, lflag, tab, slots - 1, bits, nbits - 1, cnt + 1);
+                       (const uint64_t *)f.cval, n, ckl.ib, partner, mate, lflag, tab, slots - 1, bits, nbits - 1, cnt + 1, lk, lcnt,
+                       lcap);
     OGE_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(k_mate_agree, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)f.cval, n, ckl.ib,
-                       (const uint32_t *)partner, mate, lflag, tab, slots - 1, bits, nbits - 1, cnt + 1);
+                       (const uint32_t *)partner, mate, lflag, tab, slots - 1, bits, nbits - 1, cnt + 1, lk, lcnt, lcap);
     OGE_LAUNCH_CHECK(ctx);
-    hipLaunchKernelGGL(k_mate_check, dim3(oge_ceil_div(n + 1, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)f.cval, n, ckl.ib,
-                       (const unsigned long long *)tab, slots - 1, (const uint32_t *)bits, nbits - 1, mate, lflag, oflag);
+    hipLaunchKernelGGL(k_mate_check, dim3(nb), dim3(kT), 0, ctx->stream, (const uint64_t *)f.cval, n, ckl.ib,
+                       (const unsigned long long *)tab, slots - 1, (const uint32_t *)bits, nbits - 1, mate, bcnt, lk, lcnt, lcap);
     OGE_LAUNCH_CHECK(ctx);
-    // the leftovers through the sort-based join, their pairs into mate[] / the owner flags
-    int rc = oge_exclusive_scan_u32(ctx, lflag, lflag, n + 1);
-    if (rc) return rc;
-    uint32_t left = 0, ovf = 0;
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&left, lflag + n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    uint32_t lc[kMjStripes * kMjCntStride], ovf = 0;
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(lc, lcnt, sizeof(lc), hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&ovf, cnt + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t left = 0;
+    uint32_t lmax = 0;
+    for (uint32_t q = 0; q < kMjStripes; ++q) left += lc[q * kMjCntStride], lmax = std::max(lmax, lc[q * kMjCntStride]);
     ctx->counters["md_mate_left"] = left;
-    if (ovf) {
+    if (ovf || lmax > lcap) {
         ctx->counters["md_mate_ovf"] = 1;
         return OGE_OK;
     }
-    if (left) {
+    int rc;
+    if (left) {  // the leftovers through the sort-based join, their pairs into mate[] / the block counts
+        uint64_t *lkc = (uint64_t *)ctx->scratch("md_ck", (left + 1) * 8);
+        if (!lkc) return OGE_ERR_HIP;
+        hipLaunchKernelGGL(k_left_pack, dim3(std::max<uint32_t>(1, oge_ceil_div(lmax, 4 * kT)), kMjStripes), dim3(kT), 0, ctx->stream,
+                           (const uint64_t *)lk, (const unsigned int *)lcnt, lcap, lkc);
+        OGE_LAUNCH_CHECK(ctx);
         uint64_t *lp, *spare;
         uint32_t lnp = 0;
-        if ((rc = join_sorted(ctx, ckl, recs, meta, n, lflag, f.cval, left, &lp, &spare, &lnp))) return rc;
+        if ((rc = join_sorted(ctx, ckl, recs, meta, n, nullptr, f.cval, (uint32_t)left, &lp, &spare, &lnp, lkc))) return rc;
         if (lnp) {
-            hipLaunchKernelGGL(k_mate_scatter, dim3(oge_ceil_div(lnp, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)lp, lnp, mate, oflag);
+            hipLaunchKernelGGL(k_mate_scatter, dim3(oge_ceil_div(lnp, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)lp, lnp, mate, bcnt);
             OGE_LAUNCH_CHECK(ctx);
         }
     }
-    // all pairs in first-record order
-    if ((rc = oge_exclusive_scan_u32(ctx, oflag, oflag, n + 1))) return rc;
+    // all pairs in first-record order: the blocks' counts scanned, each block's owners written from its offset
+    OGE_HIP_TRY(ctx, hipMemsetAsync(bcnt + nb, 0, 4, ctx->stream));
+    if ((rc = oge_exclusive_scan_u32(ctx, bcnt, bcnt, (uint64_t)nb + 1))) return rc;
     uint32_t np = 0;
-    OGE_HIP_TRY(ctx, hipMemcpyAsync(&np, oflag + n, 4, hipMemcpyDeviceToHost, ctx->stream));
-    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    hipLaunchKernelGGL(k_mate_compact, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint32_t *)oflag, (const uint32_t *)mate,
-                       n, wpairs);
+    OGE_HIP_TRY(ctx, hipMemcpyAsync(&np, bcnt + nb, 4, hipMemcpyDeviceToHost, ctx->stream));
+    hipLaunchKernelGGL(k_mate_compact, dim3(nb), dim3(kT), 0, ctx->stream, (const uint32_t *)bcnt, (const uint32_t *)mate, n, wpairs);
     OGE_LAUNCH_CHECK(ctx);
+    OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + 2, 0, 4, ctx->stream));
     if ((rc = pair_build(ctx, L, recs, meta, f, wpairs, np, P, cnt + 2))) return rc;
     uint32_t bad = 0;
@@ -1468,9 +1625,18 @@ int oge_md_apply_inplace(oge_ctx *ctx, uint8_t *recs, const uint64_t *off, uint6
 // (record index = i); its bytes are at recs + meta[i].src (only read to confirm pair keys).
 // dup[i] receives 1/0/2 (see oge_markdup); with apply, FLAG 0x400 is rewritten in place at
 // recs + off[i].
+int oge_markdup_finish_pre(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
+                           const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out, uint64_t *d_desc, bool *desc_ok,
+                           const uint64_t *skeys, const OgeMdFrags *pre);
 int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n,
                        const oge_markdup_opts *opts, const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out,
                        uint64_t *d_desc, bool *desc_ok, const uint64_t *skeys) {
+    return oge_markdup_finish_pre(ctx, d_recs, d_off, n, opts, meta, d_dup, apply, n_dup_out, d_desc, desc_ok, skeys, nullptr);
+}
+// pre: the products of oge_md_cand_frag_gather (the fused gather already wrote them for these n records)
+int oge_markdup_finish_pre(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
+                           const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out, uint64_t *d_desc, bool *desc_ok,
+                           const uint64_t *skeys, const OgeMdFrags *pre) {
     if (desc_ok) *desc_ok = false;
     KeyLayout L;
     int rc = md_layout(ctx, opts, &L);
@@ -1485,7 +1651,14 @@ int oge_markdup_finish(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uin
     // ---- mate join ----
     OgeStageTimer *t = ctx->begin_stage("md_matejoin");
     OgeMdFrags F;
-    rc = oge_md_cand_frag(ctx, opts, meta, n, d_desc != nullptr, &F, skeys);
+    if (pre) {  // the fused gather's products: only the scan / overflow read-back is left
+        if (!pre->fused || pre->skeys != skeys || (d_desc && !pre->desc0))
+            return oge_fail(ctx, OGE_ERR_ARG, "markdup: precomputed summaries do not match this call");
+        F = *pre;
+        rc = cand_frag_post(ctx, opts, n, &F);
+    } else {
+        rc = oge_md_cand_frag(ctx, opts, meta, n, d_desc != nullptr, &F, skeys);
+    }
     if (rc) return rc;
     const bool use_desc = d_desc && !F.desc_ovf;
     OgeMdPairs P;

@@ -27,6 +27,7 @@ struct OgeMdFrags {
     bool desc_ovf = false;      // a record offset does not fit the descriptor
     const uint64_t *skeys = nullptr;  // sorted coordinate keys (windowed fragment groups), optional
     unsigned long long *dev = nullptr;  // per-block maxima of the fragment (then pair) coordinates' deviation from the anchors
+    bool fused = false;         // written by oge_md_cand_frag_gather (the scan / read-back not done yet)
 };
 
 struct OgeMdPairs {  // pair ReadEnds, np entries (see k_pair_build for the packing of hi / lo)
@@ -42,6 +43,13 @@ struct OgeMdPairs {  // pair ReadEnds, np entries (see k_pair_build for the pack
 // windowed group stages (oge_md_*_groups_win)
 int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
                      OgeMdFrags *f, const uint64_t *skeys = nullptr);
+// The same products written by the summary gather itself (out[i] = in[perm[i]], perm the final sorted order);
+// oge_markdup_finish_pre(..., f) then runs the rest.  Launch only: f is finished by oge_markdup_finish_pre.
+int oge_md_cand_frag_gather(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *in, const uint32_t *perm, uint64_t n,
+                            RecMeta *out, bool want_desc, const uint64_t *skeys, OgeMdFrags *f);
+int oge_markdup_finish_pre(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
+                           const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out, uint64_t *d_desc, bool *desc_ok,
+                           const uint64_t *skeys, const OgeMdFrags *pre);
 // recs: the bytes RecMeta.src points into (only read for names that do not fit the summary)
 int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t *recs, const RecMeta *meta, uint64_t n,
                       const OgeMdFrags &f, OgeMdPairs *p);

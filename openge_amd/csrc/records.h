@@ -72,6 +72,12 @@ struct OgePassArgs {
 };
 
 struct oge_ctx;
+// oge_sort_keys_dev_hook: called after the tie sort with the final permutation (perm[k] = input index of
+// output record k) and the sorted keys; it gathers the summaries itself (and whatever it derives from them)
+struct OgeSortGatherHook {
+    int (*fn)(void *user, oge_ctx *ctx, const uint32_t *perm, const uint64_t *skeys);
+    void *user;
+};
 int oge_input_pass(oge_ctx *ctx, const OgePassArgs &a);
 int oge_gather_pass(oge_ctx *ctx, const OgePassArgs &a);
 // Output offsets (from the sorted keys' size payload, or from the records) + the record gather.

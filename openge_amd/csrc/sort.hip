@@ -102,9 +102,14 @@ __device__ __forceinline__ bool tie_less_meta(const uint8_t *__restrict__ recs, 
 // rows move together.
 constexpr uint32_t kTieTile = 2048;
 constexpr uint32_t kTieHalo = 34;  // keys staged past the tile: a run starting in it is seen up to 33 long
+// ROWS = false (r06, the gather-fused pipeline): the summaries are not in output order yet; a run's rows are
+// read through its input indices (meta_in[vals[p]]) and only keys and indices move -- the rows are gathered
+// once, in final order, after the tie sort.
+template <bool ROWS>
 __global__ __launch_bounds__(kT) void k_ties_meta(const uint8_t *__restrict__ recs, uint64_t *__restrict__ keys,
                                                    uint32_t *__restrict__ vals, RecMeta *__restrict__ smeta, uint64_t n,
-                                                   int32_t n_ref, uint2 *__restrict__ large, unsigned int *__restrict__ nlarge) {
+                                                   int32_t n_ref, uint2 *__restrict__ large, unsigned int *__restrict__ nlarge,
+                                                   const RecMeta *__restrict__ meta_in) {
     // the tile's masked keys with one before and kTieHalo after, staged by coalesced loads (r05: every
     // position read its neighbours and the run's tail from global memory, ~2 ms of the stage at 300M);
     // ~0 marks positions outside [0, n) (a masked key is below 2^50)
@@ -149,33 +154,33 @@ __global__ __launch_bounds__(kT) void k_ties_meta(const uint8_t *__restrict__ re
         const uint32_t len = hl[h];
         uint64_t *k = keys + p;
         uint32_t *v = vals + p;
-        RecMeta *M = smeta + p;
+        RecMeta *M = ROWS ? smeta + p : nullptr;
         if (len == 2) {
             // pairs (92 % of the runs on C2): both rows loaded together, one compare, written back only when
             // they swap.  r05: the insertion sort's row moves were chains of dependent global round trips
             // (the small-run sort was 4.9 of the stage's 7.8 ms at 300M reads).
-            const RecMeta A = M[0], B = M[1];
             const uint32_t va = v[0], vb = v[1];
+            const RecMeta A = ROWS ? M[0] : meta_in[va], B = ROWS ? M[1] : meta_in[vb];
             if (tie_less_meta(recs, B, A, vb, va)) {
                 const uint64_t ka = k[0], kb = k[1];
-                M[0] = B, M[1] = A;
+                if (ROWS) M[0] = B, M[1] = A;
                 v[0] = vb, v[1] = va;
                 k[0] = kb, k[1] = ka;
             }
             continue;
         }
         for (uint32_t i = 1; i < len; ++i) {
-            const RecMeta mi = M[i];
             const uint32_t vi = v[i];
+            const RecMeta mi = ROWS ? M[i] : meta_in[vi];
             const uint64_t ki = k[i];
             int jj = (int)i - 1;
-            while (jj >= 0 && tie_less_meta(recs, mi, M[jj], vi, v[jj])) {
-                M[jj + 1] = M[jj];
+            while (jj >= 0 && tie_less_meta(recs, mi, ROWS ? M[jj] : meta_in[v[jj]], vi, v[jj])) {
+                if (ROWS) M[jj + 1] = M[jj];
                 v[jj + 1] = v[jj];
                 k[jj + 1] = k[jj];
                 --jj;
             }
-            M[jj + 1] = mi;
+            if (ROWS) M[jj + 1] = mi;
             v[jj + 1] = vi;
             k[jj + 1] = ki;
         }
@@ -298,8 +303,20 @@ int oge_meta_gather(oge_ctx *ctx, const RecMeta *in, const uint32_t *perm, uint6
 
 // With meta_in/meta_out, meta_out receives the summaries in output order, and the small tie runs
 // are ordered on them (k_ties_meta) instead of on the record bytes.
+// With a gather hook (the fused sort + dedup pipeline): the summaries are gathered by hook->fn AFTER the
+// tie sort, in final order, instead of by oge_meta_gather before it (see k_ties_meta<false>); meta_out is
+// then not written here.
+int oge_sort_keys_dev_hook(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+                           bool keys_ready, uint64_t **kout, uint32_t **vout, const RecMeta *meta_in, RecMeta *meta_out,
+                           const OgeSortGatherHook *hook);
 int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
                       bool keys_ready, uint64_t **kout, uint32_t **vout, const RecMeta *meta_in, RecMeta *meta_out) {
+    return oge_sort_keys_dev_hook(ctx, d_recs, d_off, n, n_ref, keys_ready, kout, vout, meta_in, meta_out, nullptr);
+}
+int oge_sort_keys_dev_hook(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, uint64_t n, int32_t n_ref,
+                           bool keys_ready, uint64_t **kout, uint32_t **vout, const RecMeta *meta_in, RecMeta *meta_out,
+                           const OgeSortGatherHook *hook) {
+    if (hook && !meta_in) return oge_fail(ctx, OGE_ERR_ARG, "sort: a gather hook needs the input summaries");
     if (n_ref < 0 || n_ref >= (1 << 17)) return oge_fail(ctx, OGE_ERR_LIMIT, "sort: n_ref outside [0, 131072)");
     if (n > 0xFFFFFFFEull) return oge_fail(ctx, OGE_ERR_LIMIT, "sort: more than 2^32-2 records");
     uint64_t *keys;
@@ -347,7 +364,7 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     uint2 *large = (uint2 *)ctx->scratch("sort_large", (n / 33 + 1) * sizeof(uint2));
     if (!large) return OGE_ERR_HIP;
     OGE_HIP_TRY(ctx, hipMemsetAsync(counts, 0, 8, ctx->stream));
-    if (meta_out) {
+    if (meta_out && !hook) {
         t = ctx->begin_stage("meta_gather");
         rc = oge_meta_gather(ctx, meta_in, *vout, n, meta_out);
         if (rc) return rc;
@@ -355,9 +372,12 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
     }
     t = ctx->begin_stage("sort_ties");
     if (n > 1) {
-        if (meta_out)
-            hipLaunchKernelGGL(k_ties_meta, dim3(oge_ceil_div(n, kTieTile)), dim3(kT), 0, ctx->stream, d_recs, *kout, *vout,
-                               meta_out, n, n_ref, large, counts + 1);
+        if (hook)
+            hipLaunchKernelGGL(k_ties_meta<false>, dim3(oge_ceil_div(n, kTieTile)), dim3(kT), 0, ctx->stream, d_recs, *kout,
+                               *vout, (RecMeta *)nullptr, n, n_ref, large, counts + 1, meta_in);
+        else if (meta_out)
+            hipLaunchKernelGGL(k_ties_meta<true>, dim3(oge_ceil_div(n, kTieTile)), dim3(kT), 0, ctx->stream, d_recs, *kout,
+                               *vout, meta_out, n, n_ref, large, counts + 1, (const RecMeta *)nullptr);
         else
             hipLaunchKernelGGL(k_ties, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout, n,
                                n_ref, large, counts + 1, true);
@@ -386,7 +406,7 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
         hipLaunchKernelGGL(k_tie_large, dim3(nlarge), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout,
                            (const uint2 *)large, (const uint64_t *)dso, sk, sv);
         OGE_LAUNCH_CHECK(ctx);
-        if (meta_out) {
+        if (meta_out && !hook) {
             hipLaunchKernelGGL(k_meta_refill, dim3(nlarge), dim3(kT), 0, ctx->stream, meta_in, (const uint32_t *)*vout,
                                (const uint2 *)large, meta_out);
             OGE_LAUNCH_CHECK(ctx);
@@ -394,6 +414,11 @@ int oge_sort_keys_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off
         OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
     ctx->end_stage(t);
+    if (hook) {
+        t = ctx->begin_stage("meta_gather");
+        if ((rc = hook->fn(hook->user, ctx, *vout, *kout))) return rc;
+        ctx->end_stage(t);
+    }
     return OGE_OK;
 }
 
