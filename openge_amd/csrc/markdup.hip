@@ -285,9 +285,11 @@ __global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ 
                         (uint64_t)((uint32_t)r2c ^ 0x80000000u);
     hi[p] = ((uint64_t)score << 48) | kh;
     lo[p] = kl;
-    hk[p] = mix64(mix64(kh) ^ kl);
+    if (hk) {  // (the windowed join leaves them to the fallback paths that sort by them: pairs_hk)
+        hk[p] = mix64(mix64(kh) ^ kl);
+        val[p] = p;
+    }
     idx[p] = make_uint2(i1, i2);
-    val[p] = p;
     if (skeys) {
         ax = anchor_of_key(skeys[a]);
         cx = win_x((uint32_t)r1s, (int64_t)r1c + 1);
@@ -828,7 +830,8 @@ __device__ __forceinline__ uint32_t mj_fp(uint64_t h) {
 __device__ __forceinline__ uint32_t mj_slot(uint64_t key, uint32_t mask) { return (uint32_t)(mix64(key) & mask); }
 __device__ __forceinline__ uint32_t mj_bit(uint64_t key, uint32_t bmask) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & bmask; }
 constexpr int kMjProbes = 64;
-constexpr uint32_t kPending = 2;  // lflag: the partner lies in another tile, k_mate_agree decides
+constexpr uint32_t kPending = 2;  // k_mate_win's decision: the partner lies in another tile, k_mate_agree decides
+constexpr uint32_t kPendBit = 0x80000000u;  // partner[i] of a pending record (record indices < 2^31)
 
 // Leftovers (records the sort-based join pairs) appended to lk as their candidate keys (hash bits << ib |
 // index).  One counter would serialise the appends at its L2 channel (~88 atomics/us: at 300M reads ~2M wave
@@ -873,10 +876,10 @@ __device__ __forceinline__ void mj_conflict(uint64_t h, unsigned long long *__re
 
 // Per tile: the window's fingerprint table, then every tile record's decision.  A partner inside the tile
 // saw the same table (agreement is given; the full hash bits are compared from the staged window): a window
-// pair (mate[] of the smaller index) or two leftovers.  A partner in another tile: partner[i], kPending.
+// pair (mate[] of the smaller index) or two leftovers.  A partner in another tile: partner[i] | kPendBit.
 __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ cflag, const uint64_t *__restrict__ cval, uint64_t n,
                                                    uint32_t ib, uint32_t *__restrict__ partner, uint32_t *__restrict__ mate,
-                                                   uint32_t *__restrict__ lflag, unsigned long long *__restrict__ tab, uint32_t mask,
+                                                   unsigned long long *__restrict__ tab, uint32_t mask,
                                                    uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf,
                                                    uint64_t *__restrict__ lk, unsigned int *__restrict__ lcnt, uint32_t lcap) {
     __shared__ uint32_t key[kMjSlots], lo[kMjSlots], hi[kMjSlots], cnt[kMjSlots];
@@ -934,29 +937,27 @@ __global__ __launch_bounds__(kMjT) void k_mate_win(const uint32_t *__restrict__ 
         }
     }
     mj_left(lf == 1, (h << ib) | i, i, lk, lcnt, lcap);
-    partner[i] = r;
+    partner[i] = lf == kPending ? r | kPendBit : r;  // (kNone: no partner)
     mate[i] = m;
-    lflag[i] = lf;
-    if (i + 1 == n) lflag[n] = 0;
 }
 
 // the pending records (a partner in another tile): i and j = partner[i] agree (partner[j] == i, equal hash
 // bits) -- a window pair owned by the smaller index -- or i is a leftover
 __global__ __launch_bounds__(kT) void k_mate_agree(const uint64_t *__restrict__ cval, uint64_t n, uint32_t ib,
                                                    const uint32_t *__restrict__ partner, uint32_t *__restrict__ mate,
-                                                   uint32_t *__restrict__ lflag, unsigned long long *__restrict__ tab, uint32_t mask,
+                                                   unsigned long long *__restrict__ tab, uint32_t mask,
                                                    uint32_t *__restrict__ bits, uint32_t bmask, unsigned int *__restrict__ ovf,
                                                    uint64_t *__restrict__ lk, unsigned int *__restrict__ lcnt, uint32_t lcap) {
     const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
-    if (i >= n || lflag[i] != kPending) return;
-    const uint32_t j = partner[i];
+    if (i >= n) return;
+    const uint32_t pi = partner[i];
+    if (pi == kNone || !(pi & kPendBit)) return;
+    const uint32_t j = pi & ~kPendBit;
     const uint64_t ci = cval[i], h = ci >> ib;
-    const bool agree = partner[j] == (uint32_t)i && (cval[j] >> ib) == h;
+    const bool agree = partner[j] == ((uint32_t)i | kPendBit) && (cval[j] >> ib) == h;
     if (agree) {
         if (i < j) mate[i] = j;
-        lflag[i] = 0;
     } else {
-        lflag[i] = 1;
         mj_conflict(h, tab, mask, bits, bmask, ovf);
     }
     mj_left(!agree, ci, i, lk, lcnt, lcap);
@@ -972,12 +973,13 @@ __global__ __launch_bounds__(kT) void k_mate_check(const uint64_t *__restrict__ 
     __shared__ uint32_t ws[kT / 64];
     const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
     const uint32_t m = i < n ? mate[i] : kNone;
+    const uint64_t cv = i < n ? cval[i] : 0;  // loaded beside mate[i], not after it (the bitmap read waits on both)
     uint32_t own = 0;
     bool hit = false;
     uint64_t h = 0;
     if (m != kNone) {
         own = 1;
-        h = cval[i] >> ib;
+        h = cv >> ib;
         const unsigned long long key = h + 1;
         const uint32_t b = mj_bit(key, bmask);
         uint32_t s = mj_slot(key, mask);
@@ -1279,16 +1281,21 @@ static int join_sorted(oge_ctx *ctx, const CandKey &ckl, const uint8_t *recs, co
 
 // The pair ReadEnds of np pairs in first-record order (k_pair_build).  win_bad (optional): counts the
 // windowed join's pairs whose names differ.
+// lazy_hk (the windowed join, whose pair groups are windowed too): hk / val are not written here, only by
+// pairs_hk when a fallback path sorts by them.
 static int pair_build(oge_ctx *ctx, const KeyLayout &L, const uint8_t *recs, const RecMeta *meta, const OgeMdFrags &f,
-                      const uint64_t *spairs, uint32_t np, OgeMdPairs *P, unsigned int *win_bad) {
+                      const uint64_t *spairs, uint32_t np, OgeMdPairs *P, unsigned int *win_bad, bool lazy_hk = false) {
     P->np = np;
     if (!np) return OGE_OK;
     P->hi = (uint64_t *)ctx->scratch("md_hi", (uint64_t)np * 8);
     P->lo = (uint64_t *)ctx->scratch("md_lo", (uint64_t)np * 8);
-    P->hk = (uint64_t *)ctx->scratch("md_hi2", (uint64_t)np * 8);
     P->idx = (uint2 *)ctx->scratch("md_pidx", (uint64_t)np * sizeof(uint2));
-    P->val = (uint32_t *)ctx->scratch("md_pv", (uint64_t)np * 4);
-    if (!P->hi || !P->lo || !P->hk || !P->idx || !P->val) return OGE_ERR_HIP;
+    if (!lazy_hk) {
+        P->hk = (uint64_t *)ctx->scratch("md_hi2", (uint64_t)np * 8);
+        P->val = (uint32_t *)ctx->scratch("md_pv", (uint64_t)np * 4);
+        if (!P->hk || !P->val) return OGE_ERR_HIP;
+    }
+    if (!P->hi || !P->lo || !P->idx) return OGE_ERR_HIP;
     if (f.skeys) {
         P->pax = (int64_t *)ctx->scratch("md_pax", (uint64_t)np * 8);
         P->dev = f.dev + 2 * kDevSlots;
@@ -1312,7 +1319,6 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
     const uint32_t nb = (uint32_t)oge_ceil_div(n, kT);
     uint32_t *partner = (uint32_t *)ctx->scratch("md_mpart", (n + 1) * 4);
     uint32_t *mate = (uint32_t *)ctx->scratch("md_mate", (n + 1) * 4);
-    uint32_t *lflag = (uint32_t *)ctx->scratch("md_lflag", (n + 1) * 4);
     uint32_t *bcnt = (uint32_t *)ctx->scratch("md_bcnt", ((uint64_t)nb + 1) * 4);
     uint64_t *wpairs = (uint64_t *)ctx->scratch("md_wpairs", (n / 2 + 1) * 8);
     // the leftovers' candidate keys, appended by the three kernels below into kMjStripes regions of lcap
@@ -1320,7 +1326,7 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
     // records and a packing pass before)
     const uint32_t lcap = (uint32_t)(oge_ceil_div(oge_ceil_div(n, 1024), kMjStripes) * 1024ull);
     uint64_t *lk = (uint64_t *)ctx->scratch("md_lk", (uint64_t)kMjStripes * lcap * 8);
-    if (!cnt || !lcnt || !partner || !mate || !lflag || !bcnt || !wpairs || !lk) return OGE_ERR_HIP;
+    if (!cnt || !lcnt || !partner || !mate || !bcnt || !wpairs || !lk) return OGE_ERR_HIP;
     // the conflict set: a table of >= n/16 slots behind a bitmap of >= n/2 bits, at most 4 MiB so it stays in
     // an XCD's L2 for k_mate_check's random reads (a probe run past kMjProbes means too many leftovers for the
     // window path: the sort path decides)
@@ -1335,11 +1341,11 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
     OGE_HIP_TRY(ctx, hipMemsetAsync(tab, 0, (uint64_t)slots * 8, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(bits, 0, nbits / 8, ctx->stream));
     hipLaunchKernelGGL(k_mate_win, dim3(oge_ceil_div(n, kMjT)), dim3(kMjT), 0, ctx->stream, (const uint32_t *)f.cpos,
-                       (const uint64_t *)f.cval, n, ckl.ib, partner, mate, lflag, tab, slots - 1, bits, nbits - 1, cnt + 1, lk, lcnt,
+                       (const uint64_t *)f.cval, n, ckl.ib, partner, mate, tab, slots - 1, bits, nbits - 1, cnt + 1, lk, lcnt,
                        lcap);
     OGE_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(k_mate_agree, dim3(oge_ceil_div(n, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)f.cval, n, ckl.ib,
-                       (const uint32_t *)partner, mate, lflag, tab, slots - 1, bits, nbits - 1, cnt + 1, lk, lcnt, lcap);
+                       (const uint32_t *)partner, mate, tab, slots - 1, bits, nbits - 1, cnt + 1, lk, lcnt, lcap);
     OGE_LAUNCH_CHECK(ctx);
     hipLaunchKernelGGL(k_mate_check, dim3(nb), dim3(kT), 0, ctx->stream, (const uint64_t *)f.cval, n, ckl.ib,
                        (const unsigned long long *)tab, slots - 1, (const uint32_t *)bits, nbits - 1, mate, bcnt, lk, lcnt, lcap);
@@ -1380,7 +1386,7 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
     OGE_LAUNCH_CHECK(ctx);
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + 2, 0, 4, ctx->stream));
-    if ((rc = pair_build(ctx, L, recs, meta, f, wpairs, np, P, cnt + 2))) return rc;
+    if ((rc = pair_build(ctx, L, recs, meta, f, wpairs, np, P, cnt + 2, true))) return rc;
     uint32_t bad = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&bad, cnt + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -1421,9 +1427,23 @@ int oge_md_join_build(oge_ctx *ctx, const oge_markdup_opts *opts, const uint8_t 
     return pair_build(ctx, L, recs, meta, f, spairs, np, P, nullptr);
 }
 
+// hk / val of pairs built without them (pair_build's lazy_hk), for the paths that sort by them
+static int pairs_hk(oge_ctx *ctx, OgeMdPairs &P) {
+    if (P.hk || !P.np) return OGE_OK;
+    P.hk = (uint64_t *)ctx->scratch("md_hi2", (uint64_t)P.np * 8);
+    P.val = (uint32_t *)ctx->scratch("md_pv", (uint64_t)P.np * 4);
+    if (!P.hk || !P.val) return OGE_ERR_HIP;
+    hipLaunchKernelGGL(k_pair_rehash, dim3(oge_ceil_div(P.np, kT)), dim3(kT), 0, ctx->stream, (const uint64_t *)P.hi,
+                       (const uint64_t *)P.lo, P.np, P.hk, P.val);
+    OGE_LAUNCH_CHECK(ctx);
+    return OGE_OK;
+}
+
 static int pair_groups_sorted(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t *hk, uint32_t *val, uint32_t m,
                               const OgeMdPairs &P, uint8_t *dup);
-int oge_md_pair_groups(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &P, uint8_t *dup) {
+int oge_md_pair_groups(oge_ctx *ctx, const oge_markdup_opts *opts, const OgeMdPairs &P0, uint8_t *dup) {
+    OgeMdPairs P = P0;
+    if (int rc = pairs_hk(ctx, P)) return rc;
     return pair_groups_sorted(ctx, opts, P.hk, P.val, P.np, P, dup);
 }
 
@@ -1564,12 +1584,14 @@ int oge_md_pair_groups_win(oge_ctx *ctx, const oge_markdup_opts *opts, const Oge
     ctx->end_stage(t);
     if (W.novf) {  // the overflowing tiles' pairs through the sort-based stage
         t = ctx->begin_stage("md_pair_ovf");
+        OgeMdPairs Q = P;
+        if ((rc = pairs_hk(ctx, Q))) return rc;
         uint64_t *ok = (uint64_t *)ctx->scratch("md_ohk", W.ovf_items * 8 + 8);
         uint32_t *ov = (uint32_t *)ctx->scratch("md_opv", W.ovf_items * 4 + 4);
         unsigned int *cnt = (unsigned int *)ctx->ws("md_ocnt", 4);
         if (!ok || !ov || !cnt) return OGE_ERR_HIP;
         OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 4, ctx->stream));
-        hipLaunchKernelGGL(k_win_collect<true>, dim3(W.novf), dim3(kT), 0, ctx->stream, (const uint64_t *)P.hk,
+        hipLaunchKernelGGL(k_win_collect<true>, dim3(W.novf), dim3(kT), 0, ctx->stream, (const uint64_t *)Q.hk,
                            (const uint32_t *)nullptr, (const uint64_t *)P.hi, (const uint64_t *)P.lo,
                            (const uint64_t *)nullptr, (const int64_t *)P.pax, (uint64_t)P.np, L, (const uint2 *)W.bounds,
                            (const uint32_t *)W.ovl, ok, ov, cnt);
