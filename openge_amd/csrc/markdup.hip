@@ -23,6 +23,7 @@
 #include "records.h"
 #include "rec_parse.h"
 #include "markdup_stages.h"
+#include "md_keys.h"
 
 #include <algorithm>
 #include <cstring>
@@ -32,19 +33,6 @@ namespace {
 
 constexpr int kT = 256;
 enum { RE_F = 1, RE_R = 2, RE_FF = 3, RE_RR = 4, RE_FR = 5, RE_RF = 6 };
-
-// --- compaction of pair candidates (order-preserving) ---
-// candidate key = top hb bits of the 48-bit pair-key hash << ib | record index (ib = bits for an
-// index, hb = min(48, 64 - ib)): the hash takes every key bit the index leaves free, so collision
-// runs (which fall to the exact slow path of k_pair_runs) stay rare at full-GPU sizes.  Only the hash
-// bits are radix-sorted; the stable LSD sort keeps record order inside a hash run (the
-// ReadEndsMap's first/second-seen).
-struct CandKey {
-    uint32_t ib, hb;
-    int32_t split_k;
-    __host__ __device__ uint64_t idx_mask() const { return (1ull << ib) - 1; }
-    __host__ __device__ uint64_t hash_of(uint64_t k) const { return k >> ib; }
-};
 
 __device__ bool pair_key_of(const uint8_t *r, const uint8_t **rg, uint32_t *rgl, uint32_t *nl) {
     const uint32_t bs = oge_ldu32(r);
@@ -173,11 +161,6 @@ __global__ __launch_bounds__(kT) void k_pair_compact_scan(const uint32_t *__rest
     if (p < nc && pos[p + 1] != pos[p]) pairs[pos[p]] = sparse[p];
 }
 
-struct KeyLayout {
-    uint32_t sb, lb;  // bits for refID and library id
-    int32_t split_k;
-};
-
 __device__ __forceinline__ int orient_byte(bool r1neg, bool r2neg) {
     return r1neg ? (r2neg ? RE_RR : RE_RF) : (r2neg ? RE_FR : RE_FF);
 }
@@ -191,16 +174,6 @@ __device__ __forceinline__ uint64_t mix64(uint64_t h) {
     h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; return h ^ (h >> 33);
 }
 
-// ---- windowed grouping support (records in ByPosition order, one GPU) ----
-// A record's 5' coordinate (its fragment / pair group coordinate) lies within a few read lengths of
-// its sort position, so in sorted order every group's members sit inside a short window.  Positions
-// are compared as X(ref, v) = ref * 2^34 + v + 2^32 (v = pos + 1 or 5' coordinate + 1, |v| < 2^32).
-__device__ __forceinline__ int64_t win_x(uint32_t ref, int64_t v) { return ((int64_t)ref << 34) + v + (1ll << 32); }
-// the anchor of a sorted record: (refID', pos + 1) of its coordinate sort key (records.hip)
-__device__ __forceinline__ int64_t anchor_of_key(uint64_t k) {
-    return win_x((uint32_t)(k >> 33) & 0x1ffffu, (int64_t)((k >> 1) & 0xffffffffu));
-}
-constexpr int64_t kDevBias = 1ll << 40;  // deviations are kept as D + 2^40 (0 = none seen)
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -378,23 +351,6 @@ __global__ __launch_bounds__(kT) void k_pair_groups_h(const uint64_t *__restrict
     }
 }
 
-// fragment key: bit 63 paired, bits [47,63) score, bit 46 "not a fragment",
-// lib << (sb+33) | refID << 33 | biased coord << 1 | reverse
-__device__ __forceinline__ uint64_t frag_key(const RecMeta &R, KeyLayout L) {
-    const uint64_t m = R.m;
-    uint64_t k;
-    if (!(m & OGE_M_FRAG)) {
-        k = 1ull << 46;
-    } else {
-        const uint64_t lib = (m >> 16) & 0xFFFF;
-        k = (lib << (L.sb + 33)) | ((uint64_t)(uint32_t)R.seq << 33) | ((uint64_t)((uint32_t)R.coord ^ 0x80000000u) << 1) |
-            ((m & OGE_M_REV) ? 1ull : 0ull);
-        k |= ((m & 0xFFFF) << 47) | ((m & OGE_M_PAIRED) ? (1ull << 63) : 0ull);
-    }
-    return k;
-}
-
-
 // One pass over the summaries for the two per-record products that need nothing else: the
 // mate-join candidate flag and the fragment key, so the 64-byte rows
 // are streamed once instead of twice.
@@ -404,28 +360,6 @@ __device__ __forceinline__ uint64_t frag_key(const RecMeta &R, KeyLayout L) {
 //              by k_apply_desc once the dup bits are known; a src past 39 bits sets *ovf.
 // skeys (optional): the records' sorted coordinate keys; then the fragment coordinates' deviation
 // from the anchors is reduced into dev[0..1] for the windowed fragment groups.
-// the products of record i from its summary (only the first 32 bytes of R are read: m, src, seq, coord, hash)
-__device__ __forceinline__ void cand_frag_one(const RecMeta &R, uint64_t i, KeyLayout L, CandKey ck, uint32_t *__restrict__ f,
-                                              uint64_t *__restrict__ keys, uint32_t *__restrict__ vals,
-                                              uint64_t *__restrict__ cval, uint64_t *__restrict__ desc0,
-                                              unsigned int *__restrict__ ovf, const uint64_t *__restrict__ skeys, bool &has,
-                                              int64_t &ax, int64_t &cx) {
-    f[i] = (R.m & OGE_M_CAND) ? 1u : 0u;
-    keys[i] = frag_key(R, L);
-    vals[i] = (uint32_t)i;
-    cval[i] = ((oge_meta_hash48(R) >> (48 - ck.hb)) << ck.ib) | i;
-    if (desc0) {
-        if (R.src >> 39) atomicOr(ovf, 1u);
-        desc0[i] = (R.src & ((1ull << 39) - 1)) | ((R.m & OGE_M_PRIMARY) ? (1ull << 39) : 0ull) |
-                   ((R.m >> 48) << 40) | (((R.m >> 40) & 0xff) << 56);
-    }
-    if (skeys && (R.m & OGE_M_FRAG)) {
-        has = true;
-        ax = anchor_of_key(skeys[i]);
-        cx = win_x((uint32_t)R.seq, (int64_t)R.coord + 1);
-    }
-}
-
 __global__ __launch_bounds__(kT) void k_cand_frag(const RecMeta *__restrict__ meta, uint64_t n, KeyLayout L, CandKey ck,
                                                    uint32_t *__restrict__ f, uint64_t *__restrict__ keys,
                                                    uint32_t *__restrict__ vals, uint64_t *__restrict__ cval,
@@ -1158,10 +1092,10 @@ static bool mate_window_ok(const oge_markdup_opts *opts, uint64_t n, const uint6
 }
 
 // gin / perm (the fused gather): meta[i] = gin[perm[i]] is written here too, by k_meta_gather_cf
-static int cand_frag_launch(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
-                            OgeMdFrags *f, const uint64_t *skeys, const RecMeta *gin, const uint32_t *perm) {
-    KeyLayout L;
-    int rc = md_layout(ctx, opts, &L);
+// the products' buffers (and, with want_dev, the zeroed deviation slots); *L / *ck the layouts they use
+static int cand_frag_alloc(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, bool want_desc, bool want_dev, OgeMdFrags *f,
+                           KeyLayout *L, CandKey *ck) {
+    int rc = md_layout(ctx, opts, L);
     if (rc) return rc;
     *f = OgeMdFrags{};
     unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
@@ -1173,14 +1107,24 @@ static int cand_frag_launch(oge_ctx *ctx, const oge_markdup_opts *opts, const Re
     f->cval = (uint64_t *)ctx->scratch("md_cval", (n + 1) * 8);
     f->desc0 = want_desc ? (uint64_t *)ctx->scratch("md_desc0", (n + 1) * 8) : nullptr;
     if (!f->cpos || !f->fk || !f->fv || !f->cval || (want_desc && !f->desc0)) return OGE_ERR_HIP;
-    const CandKey ckl = md_candkey(opts, n);
-    if (skeys) {
-        f->skeys = skeys;
+    *ck = md_candkey(opts, n);
+    if (want_dev) {
         // per-block deviation maxima: kDevSlots word pairs for the fragments, as many for the pairs
         f->dev = (unsigned long long *)ctx->ws("md_devslots", 4 * kDevSlots * sizeof(unsigned long long));
         if (!f->dev) return OGE_ERR_HIP;
         OGE_HIP_TRY(ctx, hipMemsetAsync(f->dev, 0, 4 * kDevSlots * sizeof(unsigned long long), ctx->stream));
     }
+    return OGE_OK;
+}
+
+static int cand_frag_launch(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
+                            OgeMdFrags *f, const uint64_t *skeys, const RecMeta *gin, const uint32_t *perm) {
+    KeyLayout L;
+    CandKey ckl;
+    int rc = cand_frag_alloc(ctx, opts, n, want_desc, skeys != nullptr, f, &L, &ckl);
+    if (rc) return rc;
+    unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
+    f->skeys = skeys;
     if (perm)
         hipLaunchKernelGGL(k_meta_gather_cf, dim3(oge_ceil_div(4 * (n + 1), kT)), dim3(kT), 0, ctx->stream, gin, perm, n,
                            (RecMeta *)meta, L, ckl, f->cpos, f->fk, f->fv, f->cval, f->desc0, cnt + 3, skeys, f->dev);
@@ -1773,6 +1717,18 @@ int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64
     a.vals = vals;
     a.n_ref = opts->n_ref;
     a.bad = bad;
+    // with the keys (try_win) the input pass also writes k_cand_frag's words from the summaries it builds
+    // (r06): the rows are not streamed a second time
+    OgeMdFrags F;
+    if (try_win) {
+        KeyLayout L;
+        CandKey ck;
+        if ((rc = cand_frag_alloc(ctx, opts, n, false, true, &F, &L, &ck))) return rc;
+        OGE_HIP_TRY(ctx, hipMemsetAsync(F.cpos + n, 0, 4, ctx->stream));
+        a.cf_f = F.cpos, a.cf_fk = F.fk, a.cf_fv = F.fv, a.cf_cval = F.cval, a.cf_dev = F.dev;
+        a.cf_sb = L.sb, a.cf_lb = L.lb, a.cf_split = L.split_k, a.cf_ib = ck.ib, a.cf_hb = ck.hb;
+        F.fused = true;
+    }
     rc = oge_input_pass(ctx, a);
     if (rc) return rc;
     const uint64_t *skeys = nullptr;
@@ -1786,9 +1742,12 @@ int oge_markdup_run(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64
         const bool sorted = !(hb[0] & 1) && !hb[2];
         ctx->counters["md_inplace_window"] = sorted;
         if (sorted) skeys = keys;
+        F.skeys = skeys;  // unsorted: the words stand, the deviation slots go unused (no windowed stage)
+        if (!sorted) F.dev = nullptr;
     }
     ctx->end_stage(t);
-    return oge_markdup_finish(ctx, d_recs, d_off, n, opts, meta, d_dup, apply, n_dup_out, nullptr, nullptr, skeys);
+    return oge_markdup_finish_pre(ctx, d_recs, d_off, n, opts, meta, d_dup, apply, n_dup_out, nullptr, nullptr, skeys,
+                                  try_win ? &F : nullptr);
 }
 
 namespace {

@@ -69,6 +69,15 @@ struct OgePassArgs {
                              // final FLAG high byte << 56 (written by k_apply)
     uint8_t *out;
     const uint64_t *out_off; // n+1 output offsets
+    // input pass of the in-place dedup (oge_markdup_run, META + KEYS): each record's mate-join / fragment key
+    // words from the summary just built (md_keys.h cand_frag_one) and the fragments' deviation maxima into
+    // cf_dev's slots; cf_f == NULL: not written
+    uint32_t *cf_f;
+    uint64_t *cf_fk, *cf_cval;
+    uint32_t *cf_fv;
+    unsigned long long *cf_dev;
+    uint32_t cf_sb, cf_lb, cf_ib, cf_hb;
+    int32_t cf_split;
 };
 
 struct oge_ctx;

@@ -27,6 +27,7 @@
 #include "bam_layout.h"
 #include "dev_util.h"
 #include "records.h"
+#include "md_keys.h"
 
 namespace {
 
@@ -86,7 +87,8 @@ __device__ __forceinline__ uint64_t h_bytes(const Rd &rd, uint64_t h, uint64_t p
 // Record at absolute index r of reader `rd`; i = record index, src = its offset in the arena.
 template <bool META, bool KEYS, class Rd>
 __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i, uint64_t src, const OgePassArgs &a, uint64_t &kor,
-                                            uint64_t &knot) {
+                                            uint64_t &knot, uint64_t &dv0, uint64_t &dv1) {
+    uint64_t kk = 0;  // the coordinate key (KEYS)
     const uint32_t bs = rd.u32(r);
     const int32_t ref = (int32_t)rd.u32(r + OGE_OFF_REFID);
     const int32_t pos = (int32_t)rd.u32(r + OGE_OFF_POS);
@@ -104,6 +106,7 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
         }
         if (bs < 32 || bs > 10000) atomicOr(a.bad, 2u);
         a.keys[i] = k | ((uint64_t)(bs + 4) << 50);
+        kk = k;
         kor |= k;
         knot |= ~k & OGE_SORT_KEY_MASK;
         a.vals[i] = (uint32_t)(a.ibase + i);
@@ -284,6 +287,18 @@ __device__ __forceinline__ void parse_input(const Rd &rd, uint64_t r, uint64_t i
     }
     M.m = m;
     a.meta[i] = M;
+    if (KEYS && a.cf_f) {  // the in-place dedup's key words (k_cand_frag's, without the descriptors)
+        bool has = false;
+        int64_t ax = 0, cx = 0;
+        cand_frag_one(M, i, KeyLayout{a.cf_sb, a.cf_lb, a.cf_split}, CandKey{a.cf_ib, a.cf_hb, a.cf_split}, a.cf_f, a.cf_fk,
+                      a.cf_fv, a.cf_cval, nullptr, nullptr, nullptr, has, ax, cx);
+        if (m & OGE_M_FRAG) {
+            ax = anchor_of_key(kk);
+            cx = win_x((uint32_t)M.seq, (int64_t)M.coord + 1);
+            dv0 = max(dv0, (uint64_t)(ax - cx + kDevBias));
+            dv1 = max(dv1, (uint64_t)(cx - ax + kDevBias));
+        }
+    }
 }
 
 // NT records per tile and NT threads per block; the tile window is NT x 304 bytes of LDS (76 KB at
@@ -316,6 +331,7 @@ __global__ __launch_bounds__(NT) void k_input_pass(OgePassArgs a) {
     uint64_t r0 = (uint64_t)blockIdx.x * kTileRecs;
     uint64_t wb0 = 0, wb1 = 0, my_off = 0;
     uint64_t kor = 0, knot = 0;  // this thread's keys' OR and OR of complements (a.keyred)
+    uint64_t dv0 = 0, dv1 = 0;   // this thread's fragment deviation maxima (a.cf_dev)
     if (r0 < a.n) {
         if (threadIdx.x == 0) window(r0, wb0, wb1);
         if (r0 + threadIdx.x < a.n) my_off = a.off[r0 + threadIdx.x];
@@ -347,11 +363,12 @@ __global__ __launch_bounds__(NT) void k_input_pass(OgePassArgs a) {
         const uint64_t i = r0 + threadIdx.x;
         if (i < r1) {
             const uint32_t bs = (o >= b0 && o + 4 <= b1) ? LdsRd{lds}.u32(o - b0) : 0u;
-            if (bs && o + 4 + bs <= b1) parse_input<META, KEYS>(LdsRd{lds}, o - b0, i, o, a, kor, knot);
-            else parse_input<META, KEYS>(GlbRd{a.recs}, o, i, o, a, kor, knot);
+            if (bs && o + 4 + bs <= b1) parse_input<META, KEYS>(LdsRd{lds}, o - b0, i, o, a, kor, knot, dv0, dv1);
+            else parse_input<META, KEYS>(GlbRd{a.recs}, o, i, o, a, kor, knot, dv0, dv1);
         }
         __syncthreads();
     }
+    if (META && KEYS && a.cf_dev) md_dev_slots(dv0, dv1, a.cf_dev);
     if (KEYS && a.keyred) {  // a wave's OR, then one atomic per wave and word
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) kor |= __shfl_xor(kor, d, 64), knot |= __shfl_xor(knot, d, 64);
