@@ -220,17 +220,14 @@ __global__ __launch_bounds__(kDevSlots) void k_dev_fold(const unsigned long long
 
 // skeys (optional, records in sorted order): pax[p] = anchor of the pair's first record a (pairs
 // arrive sorted by a) and the deviation of read1's 5' coordinate from it into dev[0..1].
-__global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ pairs, uint32_t np, const uint8_t *__restrict__ recs,
-                                                    const RecMeta *__restrict__ meta, KeyLayout L, uint64_t *__restrict__ hi,
-                                                    uint64_t *__restrict__ lo, uint2 *__restrict__ idx, uint32_t *__restrict__ val,
-                                                    uint64_t *__restrict__ hk, const uint64_t *__restrict__ skeys,
-                                                    int64_t *__restrict__ pax, unsigned long long *__restrict__ dev,
-                                                    unsigned int *__restrict__ win_bad) {
-    uint32_t p = blockIdx.x * kT + threadIdx.x;
-    bool has = false;
-    int64_t ax = 0, cx = 0;
-    if (p < np) {
-    uint32_t a = (uint32_t)(pairs[p] >> 32), b = (uint32_t)pairs[p];  // a seen first (smaller record index)
+// The pair ReadEnds of pair (a, b) at slot p (a seen first: the smaller record index; with win_bad, b may
+// carry kSortPair).  *has / *ax / *cx: the deviation sample for win_dev_update.
+__device__ __forceinline__ void pair_entry(uint32_t p, uint32_t a, uint32_t b, const uint8_t *__restrict__ recs,
+                                           const RecMeta *__restrict__ meta, KeyLayout L, uint64_t *__restrict__ hi,
+                                           uint64_t *__restrict__ lo, uint2 *__restrict__ idx, uint32_t *__restrict__ val,
+                                           uint64_t *__restrict__ hk, const uint64_t *__restrict__ skeys,
+                                           int64_t *__restrict__ pax, unsigned int *__restrict__ win_bad, bool &has,
+                                           int64_t &ax, int64_t &cx) {
     // win_bad: pairs from the windowed join (b without kSortPair) whose names differ are counted
     const bool from_sort = win_bad && (b & 0x80000000u);
     if (win_bad) b &= 0x7fffffffu;
@@ -269,6 +266,20 @@ __global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ 
         pax[p] = ax;
         has = !bad;
     }
+}
+
+__global__ __launch_bounds__(kT) void k_pair_build(const uint64_t *__restrict__ pairs, uint32_t np, const uint8_t *__restrict__ recs,
+                                                    const RecMeta *__restrict__ meta, KeyLayout L, uint64_t *__restrict__ hi,
+                                                    uint64_t *__restrict__ lo, uint2 *__restrict__ idx, uint32_t *__restrict__ val,
+                                                    uint64_t *__restrict__ hk, const uint64_t *__restrict__ skeys,
+                                                    int64_t *__restrict__ pax, unsigned long long *__restrict__ dev,
+                                                    unsigned int *__restrict__ win_bad) {
+    const uint32_t p = blockIdx.x * kT + threadIdx.x;
+    bool has = false;
+    int64_t ax = 0, cx = 0;
+    if (p < np) {
+        const uint64_t pr = pairs[p];
+        pair_entry(p, (uint32_t)(pr >> 32), (uint32_t)pr, recs, meta, L, hi, lo, idx, val, hk, skeys, pax, win_bad, has, ax, cx);
     }
     if (skeys) win_dev_update(has, ax, cx, dev);
 }
@@ -952,10 +963,14 @@ __global__ __launch_bounds__(kT) void k_mate_scatter(const uint64_t *__restrict_
     atomicAdd(&bcnt[a / kT], 1u);
 }
 
-// pairs in first-record order: block b's owners (mate[i] != kNone) from boff[b] (the scanned block counts) in
-// record order -- ranks by ballot inside each wave, wave offsets through LDS
+// pairs in first-record order: block b's owners (mate[i] != kNone) take slots boff[b], ... in record order
+// (ranks by ballot inside each wave, wave offsets through LDS), and each owner builds its pair's ReadEnds
+// there at once (r06: the pairs were first written out as words, then read back by k_pair_build)
 __global__ __launch_bounds__(kT) void k_mate_compact(const uint32_t *__restrict__ boff, const uint32_t *__restrict__ mate, uint64_t n,
-                                                     uint64_t *__restrict__ pairs) {
+                                                     const uint8_t *__restrict__ recs, const RecMeta *__restrict__ meta, KeyLayout L,
+                                                     uint64_t *__restrict__ hi, uint64_t *__restrict__ lo, uint2 *__restrict__ idx,
+                                                     const uint64_t *__restrict__ skeys, int64_t *__restrict__ pax,
+                                                     unsigned long long *__restrict__ dev, unsigned int *__restrict__ win_bad) {
     __shared__ uint32_t ws[kT / 64];
     const uint64_t i = (uint64_t)blockIdx.x * kT + threadIdx.x;
     const uint32_t m = i < n ? mate[i] : kNone, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -965,7 +980,10 @@ __global__ __launch_bounds__(kT) void k_mate_compact(const uint32_t *__restrict_
     __syncthreads();
     uint32_t r = boff[blockIdx.x] + (uint32_t)__popcll(b & ((1ull << lane) - 1));
     for (uint32_t q = 0; q < w; ++q) r += ws[q];
-    if (own) pairs[r] = (i << 32) | m;
+    bool has = false;
+    int64_t ax = 0, cx = 0;
+    if (own) pair_entry(r, (uint32_t)i, m, recs, meta, L, hi, lo, idx, nullptr, nullptr, skeys, pax, win_bad, has, ax, cx);
+    if (skeys) win_dev_update(has, ax, cx, dev);
 }
 
 // the stripes of lk concatenated into out (stripe s from the sum of the counts before it): blockIdx.y = stripe
@@ -1247,6 +1265,7 @@ static int pair_build(oge_ctx *ctx, const KeyLayout &L, const uint8_t *recs, con
         // the pair half of the deviation slots: a redone join starts them again
         OGE_HIP_TRY(ctx, hipMemsetAsync(P->dev, 0, 2 * kDevSlots * sizeof(unsigned long long), ctx->stream));
     }
+    if (!spairs) return OGE_OK;  // (the windowed join builds them in k_mate_compact)
     hipLaunchKernelGGL(k_pair_build, dim3(oge_ceil_div(np, kT)), dim3(kT), 0, ctx->stream, spairs, np, recs, meta, L, P->hi, P->lo,
                        P->idx, P->val, P->hk, f.skeys, P->pax, P->dev, win_bad);
     OGE_LAUNCH_CHECK(ctx);
@@ -1264,13 +1283,12 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
     uint32_t *partner = (uint32_t *)ctx->scratch("md_mpart", (n + 1) * 4);
     uint32_t *mate = (uint32_t *)ctx->scratch("md_mate", (n + 1) * 4);
     uint32_t *bcnt = (uint32_t *)ctx->scratch("md_bcnt", ((uint64_t)nb + 1) * 4);
-    uint64_t *wpairs = (uint64_t *)ctx->scratch("md_wpairs", (n / 2 + 1) * 8);
     // the leftovers' candidate keys, appended by the three kernels below into kMjStripes regions of lcap
     // slots (the records of a stripe's 1024-record tiles: see mj_left), then packed (r06: flags, a scan over all
     // records and a packing pass before)
     const uint32_t lcap = (uint32_t)(oge_ceil_div(oge_ceil_div(n, 1024), kMjStripes) * 1024ull);
     uint64_t *lk = (uint64_t *)ctx->scratch("md_lk", (uint64_t)kMjStripes * lcap * 8);
-    if (!cnt || !lcnt || !partner || !mate || !bcnt || !wpairs || !lk) return OGE_ERR_HIP;
+    if (!cnt || !lcnt || !partner || !mate || !bcnt || !lk) return OGE_ERR_HIP;
     // the conflict set: a table of >= n/16 slots behind a bitmap of >= n/2 bits, at most 4 MiB so it stays in
     // an XCD's L2 for k_mate_check's random reads (a probe run past kMjProbes means too many leftovers for the
     // window path: the sort path decides)
@@ -1326,11 +1344,14 @@ static int join_window(oge_ctx *ctx, const KeyLayout &L, const CandKey &ckl, con
     if ((rc = oge_exclusive_scan_u32(ctx, bcnt, bcnt, (uint64_t)nb + 1))) return rc;
     uint32_t np = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&np, bcnt + nb, 4, hipMemcpyDeviceToHost, ctx->stream));
-    hipLaunchKernelGGL(k_mate_compact, dim3(nb), dim3(kT), 0, ctx->stream, (const uint32_t *)bcnt, (const uint32_t *)mate, n, wpairs);
-    OGE_LAUNCH_CHECK(ctx);
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(cnt + 2, 0, 4, ctx->stream));
-    if ((rc = pair_build(ctx, L, recs, meta, f, wpairs, np, P, cnt + 2, true))) return rc;
+    if ((rc = pair_build(ctx, L, recs, meta, f, nullptr, np, P, cnt + 2, true))) return rc;  // buffers only
+    if (np) {
+        hipLaunchKernelGGL(k_mate_compact, dim3(nb), dim3(kT), 0, ctx->stream, (const uint32_t *)bcnt, (const uint32_t *)mate, n,
+                           recs, meta, L, P->hi, P->lo, P->idx, f.skeys, P->pax, P->dev, cnt + 2);
+        OGE_LAUNCH_CHECK(ctx);
+    }
     uint32_t bad = 0;
     OGE_HIP_TRY(ctx, hipMemcpyAsync(&bad, cnt + 2, 4, hipMemcpyDeviceToHost, ctx->stream));
     OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
