@@ -460,30 +460,50 @@ int oge_sort_markdup_dev(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_
     if (!meta || !dd) return OGE_ERR_HIP;
     // the summaries are gathered after the tie sort, in final order, by the same pass that derives the
     // mate-join / fragment / descriptor words from them (oge_md_cand_frag_gather: one pass over the rows)
+    // the descriptors in a workspace, not in scratch: scratch lives in the lent output buffer, which the gather
+    // overwrites while it reads them (the deferred apply)
+    uint64_t *desc = (uint64_t *)ctx->ws("sm_desc", (n + 1) * 8);
+    if (!desc) return OGE_ERR_HIP;
     struct Cf {
         const oge_markdup_opts *opts;
         const RecMeta *in;
         RecMeta *out;
         uint64_t n;
+        uint64_t *desc0;
         OgeMdFrags F;
-    } cf{opts, meta_in, meta, n, {}};
+    } cf{opts, meta_in, meta, n, desc, {}};
     OgeSortGatherHook hook{[](void *u, oge_ctx *c, const uint32_t *perm, const uint64_t *skeys) {
                                Cf *x = (Cf *)u;
-                               return oge_md_cand_frag_gather(c, x->opts, x->in, perm, x->n, x->out, true, skeys, &x->F);
+                               return oge_md_cand_frag_gather(c, x->opts, x->in, perm, x->n, x->out, true, skeys, &x->F, x->desc0);
                            },
                            &cf};
     rc = oge_sort_keys_dev_hook(ctx, d_recs, d_off, n, opts->n_ref, true, &k, &v, meta_in, meta, &hook);
     if (rc) return rc;
     if (n) OGE_HIP_TRY(ctx, hipMemcpyAsync(d_perm, v, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
     uint64_t nd = 0;
-    uint64_t *desc = (uint64_t *)ctx->ws("sm_desc", (n + 1) * 8);
-    if (!desc) return OGE_ERR_HIP;
     bool desc_ok = false;
+    cf.F.defer_apply = true;  // the gather finishes the descriptors and counts the duplicates (MODE 3)
     rc = oge_markdup_finish_pre(ctx, (uint8_t *)d_recs, d_off, n, opts, meta, dd, 0, &nd, desc, &desc_ok, k, n ? &cf.F : nullptr);
     if (rc) return rc;
-    if (n_dup_out) *n_dup_out = nd;
+    const bool deferred = n && nd == ~0ull;
+    unsigned int *nds = deferred ? (unsigned int *)ctx->ws("sm_ndup", 64 * 32 * 4) : nullptr;
+    if (deferred) {
+        if (!nds) return OGE_ERR_HIP;
+        OGE_HIP_TRY(ctx, hipMemsetAsync(nds, 0, 64 * 32 * 4, ctx->stream));
+    }
     ctx->end_loan();  // the gather below writes d_out
-    return oge_gather_with_sizes(ctx, d_recs, d_off, v, k, n, d_out, d_out_off, meta, dd, desc_ok ? desc : nullptr);
+    rc = oge_gather_with_sizes(ctx, d_recs, d_off, v, k, n, d_out, d_out_off, meta, dd,
+                               deferred ? cf.F.desc0 : desc_ok ? desc : nullptr, nds);
+    if (rc) return rc;
+    if (deferred) {
+        uint32_t h[64 * 32];
+        OGE_HIP_TRY(ctx, hipMemcpyAsync(h, nds, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+        OGE_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        nd = 0;
+        for (int q = 0; q < 64; ++q) nd += h[q * 32];
+    }
+    if (n_dup_out) *n_dup_out = nd;
+    return OGE_OK;
 }
 
 }  // extern "C"

@@ -1112,7 +1112,7 @@ static bool mate_window_ok(const oge_markdup_opts *opts, uint64_t n, const uint6
 // gin / perm (the fused gather): meta[i] = gin[perm[i]] is written here too, by k_meta_gather_cf
 // the products' buffers (and, with want_dev, the zeroed deviation slots); *L / *ck the layouts they use
 static int cand_frag_alloc(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t n, bool want_desc, bool want_dev, OgeMdFrags *f,
-                           KeyLayout *L, CandKey *ck) {
+                           KeyLayout *L, CandKey *ck, uint64_t *desc0_buf = nullptr) {
     int rc = md_layout(ctx, opts, L);
     if (rc) return rc;
     *f = OgeMdFrags{};
@@ -1123,7 +1123,7 @@ static int cand_frag_alloc(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t 
     f->fk = (uint64_t *)ctx->scratch("md_fk", (n + 1) * 8);
     f->fv = (uint32_t *)ctx->scratch("md_fv", (n + 1) * 4);
     f->cval = (uint64_t *)ctx->scratch("md_cval", (n + 1) * 8);
-    f->desc0 = want_desc ? (uint64_t *)ctx->scratch("md_desc0", (n + 1) * 8) : nullptr;
+    f->desc0 = !want_desc ? nullptr : desc0_buf ? desc0_buf : (uint64_t *)ctx->scratch("md_desc0", (n + 1) * 8);
     if (!f->cpos || !f->fk || !f->fv || !f->cval || (want_desc && !f->desc0)) return OGE_ERR_HIP;
     *ck = md_candkey(opts, n);
     if (want_dev) {
@@ -1136,10 +1136,11 @@ static int cand_frag_alloc(oge_ctx *ctx, const oge_markdup_opts *opts, uint64_t 
 }
 
 static int cand_frag_launch(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *meta, uint64_t n, bool want_desc,
-                            OgeMdFrags *f, const uint64_t *skeys, const RecMeta *gin, const uint32_t *perm) {
+                            OgeMdFrags *f, const uint64_t *skeys, const RecMeta *gin, const uint32_t *perm,
+                            uint64_t *desc0_buf = nullptr) {
     KeyLayout L;
     CandKey ckl;
-    int rc = cand_frag_alloc(ctx, opts, n, want_desc, skeys != nullptr, f, &L, &ckl);
+    int rc = cand_frag_alloc(ctx, opts, n, want_desc, skeys != nullptr, f, &L, &ckl, desc0_buf);
     if (rc) return rc;
     unsigned int *cnt = (unsigned int *)ctx->ws("md_counts", 16);
     f->skeys = skeys;
@@ -1181,8 +1182,8 @@ int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *
 }
 
 int oge_md_cand_frag_gather(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *in, const uint32_t *perm, uint64_t n,
-                            RecMeta *out, bool want_desc, const uint64_t *skeys, OgeMdFrags *f) {
-    return cand_frag_launch(ctx, opts, out, n, want_desc, f, skeys, in, perm);
+                            RecMeta *out, bool want_desc, const uint64_t *skeys, OgeMdFrags *f, uint64_t *desc0_buf) {
+    return cand_frag_launch(ctx, opts, out, n, want_desc, f, skeys, in, perm, desc0_buf);
 }
 
 // The sort-based ReadEndsMap pairing (mark_duplicates.cpp:210-245) of the candidates flagged by cpos
@@ -1669,6 +1670,12 @@ int oge_markdup_finish_pre(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off,
     ctx->end_stage(t);
 
     // ---- apply ----
+    if (pre && pre->defer_apply && use_desc && !apply && !opts->compat_nonverbose_index) {
+        // the record gather finishes the descriptors (desc0 + dup) and counts the duplicates itself
+        if (desc_ok) *desc_ok = true;
+        *n_dup_out = ~0ull;
+        return OGE_OK;
+    }
     t = ctx->begin_stage("md_apply");
     OGE_HIP_TRY(ctx, hipMemsetAsync(cnt, 0, 16, ctx->stream));
     OGE_HIP_TRY(ctx, hipMemsetAsync(ndup, 0, 8, ctx->stream));

@@ -28,6 +28,9 @@ struct OgeMdFrags {
     const uint64_t *skeys = nullptr;  // sorted coordinate keys (windowed fragment groups), optional
     unsigned long long *dev = nullptr;  // per-block maxima of the fragment (then pair) coordinates' deviation from the anchors
     bool fused = false;         // written by oge_md_cand_frag_gather (the scan / read-back not done yet)
+    bool defer_apply = false;   // (oge_markdup_finish_pre's pre, set by the caller) descriptors wanted: leave
+                                // the apply to the record gather (desc0 + dup, MODE 3); *n_dup_out is then
+                                // the gather's to count
 };
 
 struct OgeMdPairs {  // pair ReadEnds, np entries (see k_pair_build for the packing of hi / lo)
@@ -45,8 +48,10 @@ int oge_md_cand_frag(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *
                      OgeMdFrags *f, const uint64_t *skeys = nullptr);
 // The same products written by the summary gather itself (out[i] = in[perm[i]], perm the final sorted order);
 // oge_markdup_finish_pre(..., f) then runs the rest.  Launch only: f is finished by oge_markdup_finish_pre.
+// desc0_buf (optional): where the descriptors go (default: context scratch, which a caller lending its output
+// buffer as scratch must not read once the output is written -- the deferred apply reads them in the gather)
 int oge_md_cand_frag_gather(oge_ctx *ctx, const oge_markdup_opts *opts, const RecMeta *in, const uint32_t *perm, uint64_t n,
-                            RecMeta *out, bool want_desc, const uint64_t *skeys, OgeMdFrags *f);
+                            RecMeta *out, bool want_desc, const uint64_t *skeys, OgeMdFrags *f, uint64_t *desc0_buf = nullptr);
 int oge_markdup_finish_pre(oge_ctx *ctx, uint8_t *d_recs, const uint64_t *d_off, uint64_t n, const oge_markdup_opts *opts,
                            const RecMeta *meta, uint8_t *d_dup, int apply, uint64_t *n_dup_out, uint64_t *d_desc, bool *desc_ok,
                            const uint64_t *skeys, const OgeMdFrags *pre);

@@ -66,7 +66,9 @@ struct OgePassArgs {
     const RecMeta *smeta;    // summaries in OUTPUT order (bin, flags, src offset), optional
     const uint8_t *dup;      // output order: 1 sets 0x400, 0 clears it (primary records only)
     const uint64_t *desc;    // output order, replaces smeta + dup when given: src (40 bits) | bin << 40 |
-                             // final FLAG high byte << 56 (written by k_apply)
+                             // final FLAG high byte << 56 (written by k_apply); with ndup: k_cand_frag's desc0
+                             // (primary bit 39, FLAG byte before the dup bit), finished here with dup[]
+    unsigned int *ndup;      // with desc0 + dup: primaries flagged, counted into 64 counters 32 words apart
     uint8_t *out;
     const uint64_t *out_off; // n+1 output offsets
     // input pass of the in-place dedup (oge_markdup_run, META + KEYS): each record's mate-join / fragment key
@@ -92,4 +94,5 @@ int oge_gather_pass(oge_ctx *ctx, const OgePassArgs &a);
 // Output offsets (from the sorted keys' size payload, or from the records) + the record gather.
 int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
                           const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
-                          const RecMeta *smeta, const uint8_t *d_dup, const uint64_t *desc = nullptr);
+                          const RecMeta *smeta, const uint8_t *d_dup, const uint64_t *desc = nullptr,
+                          unsigned int *ndup = nullptr);

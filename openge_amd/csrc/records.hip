@@ -448,9 +448,11 @@ __device__ __forceinline__ GChunk gchunk_plan(const uint32_t *sdw, uint32_t cnt,
 }
 
 // MODE 0: source = off[perm[k]], bin/flags parsed from the record; 1: from the output-order summaries
-// (smeta) and dup[]; 2: from the 8-byte descriptors (desc).
+// (smeta) and dup[]; 2: from the 8-byte descriptors (desc); 3: from k_cand_frag's descriptors and dup[]
+// (r06: the dedup's apply pass folded in here), the primaries flagged counted into a.ndup.
 template <int MODE>
 __global__ __launch_bounds__(kT) void k_gather16(OgePassArgs a) {
+    uint32_t nd = 0;  // MODE 3: flagged primaries of this lane's records
     __shared__ uint32_t sd[kT / 64][65];   // per wave: output start of record j relative to the batch
     __shared__ uint64_t ss[kT / 64][64];   // source offset of record j
     __shared__ uint32_t sbf[kT / 64][64];  // bin | FLAG-high-byte << 16 to write
@@ -473,6 +475,17 @@ __global__ __launch_bounds__(kT) void k_gather16(OgePassArgs a) {
                 bin = (uint32_t)(D >> 40) & 0xffff;
                 fhi = (uint32_t)(D >> 56);
                 primary = false;  // 0x400 already applied in the descriptor
+            } else if (MODE == 3) {
+                const uint64_t D = a.desc[rec];
+                s = D & ((1ull << 39) - 1);
+                bin = (uint32_t)(D >> 40) & 0xffff;
+                fhi = (uint32_t)(D >> 56);
+                primary = false;  // applied here, not below
+                if ((D >> 39) & 1) {
+                    const bool d = a.dup[rec] == 1;
+                    fhi = d ? (fhi | 0x04u) : (fhi & ~0x04u);
+                    nd += d;
+                }
             } else if (MODE == 1) {
                 const RecMeta M = a.smeta[rec];
                 s = M.src;
@@ -532,6 +545,10 @@ __global__ __launch_bounds__(kT) void k_gather16(OgePassArgs a) {
         }
         __builtin_amdgcn_wave_barrier();
     }
+    if (MODE == 3) {  // a wave's count, one atomic per wave on one of 64 counters
+        const uint32_t ws = oge_wave_sum(nd);
+        if ((threadIdx.x & 63) == 0 && ws) atomicAdd(a.ndup + (blockIdx.x & 63) * 32, ws);
+    }
 }
 
 }  // namespace
@@ -560,7 +577,9 @@ int oge_gather_pass(oge_ctx *ctx, const OgePassArgs &a) {
     if (!a.n) return OGE_OK;
     constexpr uint64_t cap = 131072;  // blocks in flight enough to cover the gather's latency (48 -> 41 ms, r01)
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(oge_ceil_div(a.n, 64 * (kT / 64)), cap);
-    if (a.desc)
+    if (a.desc && a.ndup)
+        hipLaunchKernelGGL(k_gather16<3>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
+    else if (a.desc)
         hipLaunchKernelGGL(k_gather16<2>, dim3(blocks), dim3(kT), 0, ctx->stream, a);
     else if (a.smeta)
         hipLaunchKernelGGL(k_gather16<1>, dim3(blocks), dim3(kT), 0, ctx->stream, a);

@@ -429,7 +429,7 @@ unsigned int *oge_sort_counts(oge_ctx *ctx) { return (unsigned int *)ctx->ws("so
 // smeta (output-order summaries) and dup are optional (see OgePassArgs).
 int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d_off, const uint32_t *d_perm,
                           const uint64_t *sorted_keys, uint64_t n, uint8_t *d_out, uint64_t *d_out_off,
-                          const RecMeta *smeta, const uint8_t *d_dup, const uint64_t *desc) {
+                          const RecMeta *smeta, const uint8_t *d_dup, const uint64_t *desc, unsigned int *ndup) {
     OgeStageTimer *t = ctx->begin_stage("gather_offsets");
     // the sizes straight from the sorted keys' payload inside the scan (r05: a sizes kernel first, 0.8 ms)
     int rc = sorted_keys ? oge_offsets_from_keys(ctx, sorted_keys, n, d_out_off) : 1;
@@ -456,8 +456,9 @@ int oge_gather_with_sizes(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *d
     a.out = d_out;
     a.out_off = d_out_off;
     a.smeta = desc ? nullptr : smeta;
-    a.dup = desc ? nullptr : d_dup;
+    a.dup = desc && !ndup ? nullptr : d_dup;
     a.desc = desc;
+    a.ndup = desc ? ndup : nullptr;
     rc = oge_gather_pass(ctx, a);
     if (rc) return rc;
     ctx->end_stage(t);
