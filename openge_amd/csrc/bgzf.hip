@@ -936,15 +936,16 @@ struct LdsBits {  // LSB-first bit writer into LDS words; its first and last wor
     uint32_t *base;
     uint64_t acc;
     uint32_t nacc, wpos;
-    bool first;
-    __device__ __forceinline__ void init(uint32_t *b, uint32_t bit) { base = b, acc = 0, nacc = bit & 31, wpos = bit >> 5, first = true; }
+    __device__ __forceinline__ void init(uint32_t *b, uint32_t bit) { base = b, acc = 0, nacc = bit & 31, wpos = bit >> 5; }
     __device__ __forceinline__ void put(uint32_t v, uint32_t nb) {  // nb <= 32, nacc < 32 on entry
         acc |= (uint64_t)v << nacc;
         nacc += nb;
         if (nacc >= 32) {
             const uint32_t w = (uint32_t)acc;
-            if (first) atomicOr(base + wpos, w), first = false;
-            else base[wpos] = w;
+            // every word by LDS OR: the image is zeroed, so an OR into an interior word is its store, and the
+            // first word (shared with the previous segment) needs no flag and no branch of its own (r06: the
+            // first-word flag's nested branch at every store, 20M deflate 25.65 -> 25.21 ms, same bytes)
+            atomicOr(base + wpos, w);
             ++wpos;
             acc >>= 32;
             nacc -= 32;
