@@ -10,7 +10,6 @@ oge_mergesort_bgzf_dev output of the same reads.  Replaces SplitByChromosome / S
 import gzip
 import json
 import os
-import socket
 import subprocess
 import sys
 from pathlib import Path
@@ -36,12 +35,6 @@ def _header_bytes(stream: bytes) -> int:
         (ln,) = struct.unpack_from("<i", stream, q)
         q += 4 + ln + 4
     return q
-
-
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 @pytest.fixture(scope="module")
@@ -91,8 +84,10 @@ def test_bench_multiprocess_bootstrap_matches_reference(world, realign, records,
                OMP_NUM_THREADS="2")
     if records == "blocking":
         env["OGE_DIST_RECORDS"] = "blocking"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+    # --standalone: the launcher binds its rendezvous port itself (port 0), so no other process can take it
+    # between a probe and the bind (a probed free port was taken once on a shared box: EADDRINUSE)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1", "--nnodes=1",
+           f"--nproc-per-node={world}",
            str(ROOT / "bench.py"), "--gpus", str(world), "--pairs", "20000", "--seed", "99", "--steps", "1",
            "--warmup", "1", "--dump-dir", str(tmp_path)]
     cmd += ["--realign-intervals", str(RL_INTERVALS)] if realign else ["--no-realign"]
