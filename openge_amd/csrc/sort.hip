@@ -273,6 +273,106 @@ __global__ __launch_bounds__(kT) void k_tie_large(const uint8_t *__restrict__ re
     }
 }
 
+// One workgroup per long run, with the summaries (r06): when every member's name fits its 32-byte slot and
+// the run has at most kLongMax members, the (name slot, flag) rows are staged in LDS once and a bitonic sort
+// of member positions runs on them -- each compare reads LDS only.  k_tie_large compares through the record
+// bytes, a chain of dependent global loads per compare (1.2 ms at 300M C2 reads for ~50 runs of ~1,000
+// members at position 0 of the contigs).  Other runs take the k_tie_large path in the same workgroup.
+constexpr uint32_t kLongMax = 2048;
+__global__ __launch_bounds__(kT) void k_tie_large_meta(const uint8_t *__restrict__ recs, const uint64_t *__restrict__ off,
+                                                        uint64_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                                                        const uint2 *__restrict__ segs, const uint64_t *__restrict__ scratch_off,
+                                                        uint64_t *__restrict__ sk, uint32_t *__restrict__ sv,
+                                                        const RecMeta *__restrict__ meta_in) {
+    __shared__ uint32_t nm[kLongMax][OGE_NAME_SLOT / 4];  // name slots, bytes in compare order (bswapped words)
+    __shared__ uint64_t kk[kLongMax];
+    __shared__ uint32_t vv[kLongMax];
+    __shared__ uint16_t fl[kLongMax];
+    __shared__ uint16_t pm[kLongMax];
+    const uint2 sg = segs[blockIdx.x];
+    bool fit = sg.y <= kLongMax;
+    if (fit) {
+        for (uint32_t i = threadIdx.x; i < sg.y; i += kT) {
+            const uint32_t v = vals[sg.x + i];
+            const RecMeta &M = meta_in[v];
+            fit = fit && (M.m & OGE_M_NAMEFIT);
+            const uint32_t *w = (const uint32_t *)M.name;
+#pragma unroll
+            for (uint32_t q = 0; q < OGE_NAME_SLOT / 4; ++q) nm[i][q] = __builtin_bswap32(w[q]);
+            fl[i] = oge_rd_u16(recs + M.src + OGE_OFF_FLAG);
+            kk[i] = keys[sg.x + i];
+            vv[i] = v;
+            pm[i] = (uint16_t)i;
+        }
+    }
+    if (!__syncthreads_and(fit)) {  // uniform: the record-byte path
+        uint32_t P = 1;
+        while (P < sg.y) P <<= 1;
+        uint64_t *K = sk + scratch_off[blockIdx.x];
+        uint32_t *V = sv + scratch_off[blockIdx.x];
+        for (uint32_t i = threadIdx.x; i < P; i += kT) {
+            if (i < sg.y) { K[i] = keys[sg.x + i]; V[i] = vals[sg.x + i]; }
+            else { K[i] = 0; V[i] = 0xFFFFFFFFu; }
+        }
+        __syncthreads();
+        for (uint32_t k2 = 2; k2 <= P; k2 <<= 1) {
+            for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = threadIdx.x; i < P; i += kT) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const bool up = (i & k2) == 0;
+                        const uint32_t vi = V[i], vl = V[l];
+                        if (up ? tie_less(recs, off, vl, vi) : tie_less(recs, off, vi, vl)) {
+                            V[i] = vl; V[l] = vi;
+                            const uint64_t t = K[i]; K[i] = K[l]; K[l] = t;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t i = threadIdx.x; i < sg.y; i += kT) {
+            keys[sg.x + i] = K[i];
+            vals[sg.x + i] = V[i];
+        }
+        return;
+    }
+    uint32_t P = 1;
+    while (P < sg.y) P <<= 1;
+    for (uint32_t i = sg.y + threadIdx.x; i < P; i += kT) pm[i] = (uint16_t)i;  // pads: after every member
+    __syncthreads();
+    const uint32_t n = sg.y;
+    auto less = [&](uint32_t a, uint32_t b) {  // member a before member b (tie_less_meta's order)
+        if (a >= n) return false;
+        if (b >= n) return true;
+#pragma unroll
+        for (uint32_t q = 0; q < OGE_NAME_SLOT / 4; ++q) {
+            const uint32_t x = nm[a][q], y = nm[b][q];
+            if (x != y) return x < y;
+        }
+        if (fl[a] != fl[b]) return fl[a] < fl[b];
+        return vv[a] < vv[b];
+    };
+    for (uint32_t k2 = 2; k2 <= P; k2 <<= 1) {
+        for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += kT) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & k2) == 0;
+                    const uint32_t a = pm[i], b = pm[l];
+                    if (up ? less(b, a) : less(a, b)) pm[i] = (uint16_t)b, pm[l] = (uint16_t)a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += kT) {
+        const uint32_t s = pm[i];
+        keys[sg.x + i] = kk[s];
+        vals[sg.x + i] = vv[s];
+    }
+}
+
 __global__ __launch_bounds__(kT) void k_sizes_from_keys(const uint64_t *__restrict__ keys, uint64_t n,
                                                          uint64_t *__restrict__ sizes) {
     uint64_t p = (uint64_t)blockIdx.x * kT + threadIdx.x;
@@ -403,8 +503,12 @@ int oge_sort_keys_dev_hook(oge_ctx *ctx, const uint8_t *d_recs, const uint64_t *
         uint32_t *sv = (uint32_t *)ctx->scratch("sort_large_v", tot * 4);
         if (!dso || !sk || !sv) return OGE_ERR_HIP;
         OGE_HIP_TRY(ctx, hipMemcpyAsync(dso, so.data(), nlarge * 8, hipMemcpyHostToDevice, ctx->stream));
-        hipLaunchKernelGGL(k_tie_large, dim3(nlarge), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout,
-                           (const uint2 *)large, (const uint64_t *)dso, sk, sv);
+        if (meta_in)
+            hipLaunchKernelGGL(k_tie_large_meta, dim3(nlarge), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout,
+                               (const uint2 *)large, (const uint64_t *)dso, sk, sv, meta_in);
+        else
+            hipLaunchKernelGGL(k_tie_large, dim3(nlarge), dim3(kT), 0, ctx->stream, d_recs, d_off, *kout, *vout,
+                               (const uint2 *)large, (const uint64_t *)dso, sk, sv);
         OGE_LAUNCH_CHECK(ctx);
         if (meta_out && !hook) {
             hipLaunchKernelGGL(k_meta_refill, dim3(nlarge), dim3(kT), 0, ctx->stream, meta_in, (const uint32_t *)*vout,

@@ -151,6 +151,40 @@ def test_sort_markdup_forced_hash_collisions(ctx, bits):
             assert bool(f & 0x400) == bool(odup[k]), k
 
 
+@pytest.mark.parametrize("long_name", [False, True])
+def test_long_tie_runs(ctx, long_name):
+    """Equal-coordinate runs longer than 32 (k_tie_large_meta: LDS rows up to 2,048 members; the record-byte
+    path past that, or when a member's name overflows the 32-byte slot): names sharing prefixes, exact
+    name ties broken by flag and then by input index.  Sort-only and fused sort + dedup orders equal the
+    oracle's, and so do the fused pipeline's FLAG bits."""
+    import torch
+    from bamutil import make_record, pack_records, rec_bytes
+    rng = np.random.default_rng(11)
+    recs = []
+    for pos, cnt in [(100, 33), (200, 40), (300, 257), (400, 1000), (500, 2048), (600, 2049), (700, 3000)]:
+        for j in range(cnt):
+            nm = f"q{int(rng.integers(0, cnt // 3 + 1)):05d}" if j % 5 else f"q{int(rng.integers(0, 40))}"
+            if long_name and pos == 400 and j == 7:
+                nm = "L" * 40
+            flag = int(rng.choice([0, 0x1 | 0x40 | 0x8, 0x1 | 0x80 | 0x8, 0x100]))
+            recs.append(make_record(nm, flag, 0, pos, "20M", "A" * 20))
+    for j in range(500):  # ragged background
+        recs.append(make_record(f"b{j}", 0x10 if j & 1 else 0, 0, int(rng.integers(0, 1000)), "20M", "C" * 20))
+    order = rng.permutation(len(recs))
+    rr, oo = pack_records([recs[i] for i in order])
+    n = len(recs)
+    hdr = "@HD\tVN:1.0\tSO:unsorted\n@SQ\tSN:c0\tLN:10000\n"
+    operm = oracle.sort_perm(rr, oo, n)
+    assert np.array_equal(ctx.sort_coord(rr, oo, n, 1), operm)
+    opts, keep = L.markdup_opts_from_header(hdr, 1)
+    nd, fl, perm, _ = _fused_dup_flags(ctx, rr, oo, n, opts)
+    assert np.array_equal(perm, operm)
+    srecs, soffs = pack_records([rec_bytes(rr, oo[i]) for i in operm])
+    odup, ond = oracle.markdup(srecs, soffs, n, hdr)
+    assert nd == ond
+    assert np.array_equal(fl, _expected_flags(srecs, soffs, n, odup))
+
+
 def _fused_dup_flags(ctx, recs, offs, n, opts):
     import torch
     d_recs = torch.from_numpy(recs).cuda()
