@@ -1179,6 +1179,9 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
 // 8-position chunks c = 1024 k + t (k < 8) for the refs / image passes (a wave's 64 lanes touch 64
 // consecutive chunks: conflict-free LDS).
 constexpr uint32_t kT2 = 1024;
+#ifndef OGE_LZ_HOPS
+#define OGE_LZ_HOPS 3  // refs hops per pointer-jumping round (step 4); >= 2
+#endif
 
 __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, const uint64_t *__restrict__ uoff,
                                                  const uint32_t *__restrict__ crc, uint64_t *__restrict__ bitmap,
@@ -1357,26 +1360,35 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
                 continue;
             }
             const uint32_t r8[8] = {v.x & 0xffff, v.x >> 16, v.y & 0xffff, v.y >> 16, v.z & 0xffff, v.z >> 16, v.w & 0xffff, v.w >> 16};
-            uint32_t rr[8];
+            uint32_t r1[8], rr[8];
 #pragma unroll
-            for (uint32_t i = 0; i < 8; ++i) rr[i] = refs[r8[i]];  // all issued before any is used
+            for (uint32_t i = 0; i < 8; ++i) r1[i] = refs[r8[i]];  // all issued before any is used
             // a second hop in the same round (r06): every value any thread reads or writes is an ancestor of
             // its position on the copy chain, so reading refs while other chunks are rewritten is race-free;
             // a round advances 3x instead of 2x (more when a source was already rewritten this round).
             // 100M reads: k_infl_lz 72.2 -> 70.4 ms; a third hop 71.7 (profiles/r06cq, r06cr)
 #pragma unroll
-            for (uint32_t i = 0; i < 8; ++i) rr[i] = refs[rr[i]];
-            bool ch = false;
+            for (uint32_t i = 0; i < 8; ++i) rr[i] = refs[r1[i]];
+            // with the root test below, a third hop pays (67.8 -> 66.7 ms; without the test it did not)
 #pragma unroll
-            for (uint32_t i = 0; i < 8; ++i) ch |= rr[i] != r8[i];
+            for (int h = 2; h < OGE_LZ_HOPS; ++h) {
+#pragma unroll
+                for (uint32_t i = 0; i < 8; ++i) r1[i] = rr[i], rr[i] = refs[rr[i]];
+            }
+            bool ch = false, fin = true;
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) ch |= rr[i] != r8[i], fin &= rr[i] == r1[i];
             if (ch) {  // positions past the end point at themselves: never changed
                 uint4 o;
                 o.x = rr[0] | (rr[1] << 16), o.y = rr[2] | (rr[3] << 16), o.z = rr[4] | (rr[5] << 16), o.w = rr[6] | (rr[7] << 16);
                 *(uint4 *)(refs + q) = o;
-                changed = 1;
-            } else {
-                act &= ~(1u << k);
             }
+            // refs[r1] == r1 names a root (a non-root's ref is always below it), so a chunk whose last hops
+            // all returned the previous hop's value now holds roots only: it leaves `act` at once and does not
+            // keep the workgroup in the loop for a round that would only confirm it (100M reads: k_infl_lz
+            // 70.3 -> 67.8 ms, profiles/r06cu)
+            if (!ch || fin) act &= ~(1u << k);
+            else changed = 1;
         }
 #if OGE_EXP == 7
         zr = round + 1;
