@@ -1298,31 +1298,30 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
             const uint32_t x = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
             const uint32_t p = q0 + jb, len = (x & 0xff) + 3, dist = ((x >> 8) & 0x7fff) + 1;
             const uint32_t e = min(p + len, osz);  // phase 1 checked it; a failed block must not write past the array
-            // refs over [p, e): single entries up to the next 8-aligned position, then 8 entries per 16-byte
-            // store, then the tail
-            uint32_t q = p;
-            const uint32_t a8 = min((p + 7) & ~7u, e);
-            if (dist >= len) {  // refs[q] = q - dist: the source lies before the copy
-                for (; q < a8; ++q) refs[q] = (uint16_t)(q - dist);
-                for (; q + 8 <= e; q += 8) {
-                    const uint32_t r = q - dist;
-                    uint4 v;
-                    v.x = (r & 0xffff) | (((r + 1) & 0xffff) << 16), v.y = ((r + 2) & 0xffff) | (((r + 3) & 0xffff) << 16);
-                    v.z = ((r + 4) & 0xffff) | (((r + 5) & 0xffff) << 16), v.w = ((r + 6) & 0xffff) | (((r + 7) & 0xffff) << 16);
-                    *(uint4 *)(refs + q) = v;
+            // refs over [p, e) in stores as wide as the alignment allows: 1 / 2 / 4 entries up to the next
+            // 8-aligned position, 8 per 16-byte store, then 4 / 2 / 1 (at most 3 + 3 narrow stores per copy,
+            // was up to 7 + 7 single entries: a wave waits for its lane with the most; 100M reads: k_infl_lz 66.4 -> 64.9 ms,
+            // profiles/r06cy).  An overlapping copy (dist < len) repeats its first dist bytes: refs[p + j] =
+            // p - dist + j mod dist, always before p (r03 chained q -> q - dist inside the copy: len / dist levels
+            // of pointer jumping for a run)
+            const uint32_t r0 = p - dist;
+            uint32_t k = 0;
+            auto fill = [&](auto &&nx) {
+                uint32_t q = p;
+                if ((q & 1) && q < e) refs[q++] = (uint16_t)nx();
+                if ((q & 2) && q + 2 <= e) {
+                    uint32_t a = nx();
+                    a |= nx() << 16;
+                    *(uint32_t *)(refs + q) = a;
+                    q += 2;
                 }
-                for (; q < e; ++q) refs[q] = (uint16_t)(q - dist);
-            } else {  // an overlapping copy repeats its first dist bytes: refs[p + j] = p - dist + j mod dist,
-                      // always before p (r03 chained q -> q - dist inside the copy: len / dist levels of
-                      // pointer jumping for a run)
-                const uint32_t r0 = p - dist;
-                uint32_t k = 0;
-                auto nx = [&]() {
-                    const uint32_t r = r0 + k;
-                    k = k + 1 == dist ? 0u : k + 1;
-                    return r & 0xffff;
-                };
-                for (; q < a8; ++q) refs[q] = (uint16_t)nx();
+                if ((q & 4) && q + 4 <= e) {
+                    uint2 v;
+                    v.x = nx(), v.x |= nx() << 16;
+                    v.y = nx(), v.y |= nx() << 16;
+                    *(uint2 *)(refs + q) = v;
+                    q += 4;
+                }
                 for (; q + 8 <= e; q += 8) {
                     uint4 v;
                     v.x = nx(), v.x |= nx() << 16;
@@ -1331,7 +1330,29 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
                     v.w = nx(), v.w |= nx() << 16;
                     *(uint4 *)(refs + q) = v;
                 }
-                for (; q < e; ++q) refs[q] = (uint16_t)nx();
+                if (q + 4 <= e) {
+                    uint2 v;
+                    v.x = nx(), v.x |= nx() << 16;
+                    v.y = nx(), v.y |= nx() << 16;
+                    *(uint2 *)(refs + q) = v;
+                    q += 4;
+                }
+                if (q + 2 <= e) {
+                    uint32_t a = nx();
+                    a |= nx() << 16;
+                    *(uint32_t *)(refs + q) = a;
+                    q += 2;
+                }
+                if (q < e) refs[q] = (uint16_t)nx();
+            };
+            if (dist >= len) {  // refs[q] = q - dist: the source lies before the copy
+                fill([&]() { return (r0 + k++) & 0xffffu; });
+            } else {
+                fill([&]() {
+                    const uint32_t r = r0 + k;
+                    k = k + 1 == dist ? 0u : k + 1;
+                    return r & 0xffffu;
+                });
             }
         }
     }
