@@ -48,6 +48,9 @@ void *oge_ctx::alloc(size_t bytes) {
         if (hipMallocAsync(&p, bytes, stream) != hipSuccess) return nullptr;
         return p;
     }
+    // experiment (OGE_ALLOC_CONTIG=1): physically contiguous buffers, i.e. the largest page fragments
+    static const bool contig = getenv("OGE_ALLOC_CONTIG") && atoi(getenv("OGE_ALLOC_CONTIG")) == 1;
+    if (contig && hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess) return p;
     return hipMalloc(&p, bytes) == hipSuccess ? p : nullptr;
 }
 

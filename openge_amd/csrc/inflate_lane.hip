@@ -544,6 +544,10 @@ __global__ void __launch_bounds__(64) k_infl_prep(const uint8_t *__restrict__ z,
 // when it holds a whole 8-byte chunk of the output; the block's first and last chunk (shared with the
 // neighbouring blocks) are stored byte by byte.  Bitmap words (holes, deferred literals) per 64
 // positions, zeroed before the launch, stored when a lane leaves a word that has bits.
+// a block's hole / deferred-literal bitmap pairs (1024 x 16 B) at this stride in u64 words (r06: a skew of
+// 64 or 512 B per block measured equal, profiles/r06dd)
+constexpr uint64_t kBmStride = 2048;
+
 __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restrict__ z, uint64_t zbytes,
                                                       const uint64_t *__restrict__ d0a, const uint64_t *__restrict__ d1a,
                                                       const uint64_t *__restrict__ uoff, uint64_t b0, uint64_t nb,
@@ -706,7 +710,7 @@ __global__ void __launch_bounds__(64, kWps) k_infl_huff(const uint8_t *__restric
                 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
                 u64x2 v;
                 v.x = bm, v.y = lm;
-                *(OGE_G u64x2 *)(bitmap + (uint64_t)bi * 2048 + 2 * bw) = v;
+                *(OGE_G u64x2 *)(bitmap + (uint64_t)bi * kBmStride + 2 * bw) = v;
             }
             bm = lm = 0;
             bw = w;
@@ -1218,7 +1222,7 @@ __global__ void __launch_bounds__(kT2) k_infl_lz(uint8_t *__restrict__ out, cons
         const uint8_t *O = out + uoff[b];
         hv = u64x2{0, 0};
         if (t < ((osz + 63) >> 6)) {
-            OGE_G u64x2 *bp = (OGE_G u64x2 *)((OGE_G uint64_t *)(bitmap + i * 2048) + 2 * t);
+            OGE_G u64x2 *bp = (OGE_G u64x2 *)((OGE_G uint64_t *)(bitmap + i * kBmStride) + 2 * t);
             hv = *bp;
             *bp = u64x2{0, 0};  // cleared behind the read: the next chunk's phase 1 needs no memset (r05)
         }
@@ -1536,7 +1540,7 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     const uint64_t lanes = (uint64_t)ncu * 4 * kWps * 64;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
-    constexpr uint64_t kPerBlk = 2048 * 8 + kXTab + kPrep + 4;  // bitmaps + translation lists + prepared tables
+    constexpr uint64_t kPerBlk = kBmStride * 8 + kXTab + kPrep + 4;  // bitmaps + translation lists + prepared tables
     constexpr int S = kStreams;
     const uint64_t budget =
         std::max<uint64_t>(lanes, std::min<uint64_t>(kChunkLanes * lanes, (uint64_t)(fr / 4) / (S * kPerBlk)));
@@ -1555,7 +1559,7 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
     const bool use_prep = !(pe && *pe == '0');
     for (int k = 0; k < S; ++k) {
         const std::string x = std::to_string(k);
-        B[k].bitmap = (uint64_t *)ctx->ws(("infl_bitmap" + x).c_str(), chunk * 2048 * 8);
+        B[k].bitmap = (uint64_t *)ctx->ws(("infl_bitmap" + x).c_str(), chunk * kBmStride * 8);
         B[k].xtab = (uint8_t *)ctx->ws(("infl_xtab" + x).c_str(), chunk * kXTab);
         B[k].scr = (uint8_t *)ctx->ws(("infl_scratch" + x).c_str(), wgs * 64 * kScr);
         B[k].next = (unsigned long long *)ctx->ws(("infl_next" + x).c_str(), 8);
@@ -1589,7 +1593,7 @@ int oge_inflate_lanes(oge_ctx *ctx, const uint8_t *d_z, uint64_t zbytes, const u
         // read, which leaves the buffer clear for the next chunk and the next call (ctx->infl_clean: the
         // buffer and how many of its bytes are known clear; a failed launch forgets it).  Fresh or grown
         // buffers, and the two-stream layout, are cleared here (a 21 GB memset per 300M-read step before).
-        const uint64_t bbytes = nb * 2048 * 8;
+        const uint64_t bbytes = nb * kBmStride * 8;
         const bool clean = S == 1 && ctx->infl_clean_ptr == u.bitmap && ctx->infl_clean_bytes >= bbytes;
         if (!clean) OGE_HIP_TRY(ctx, hipMemsetAsync(u.bitmap, 0, bbytes, u.st));
         if (S == 1) {
