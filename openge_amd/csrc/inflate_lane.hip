@@ -27,8 +27,9 @@
 //   descriptor (L-3, D-1 in 23 bits) and sets the hole's start bit in the block's bitmap.
 // Phase 2 (k_infl_lz, persistent 1024-thread workgroups, one block at a time, the next block's bytes loaded
 //   under this block's CRC): deferred literals translated; refs[p] = p for
-//   every position, then refs[p + j] = p - D + j for every hole; pointer jumping (refs[q] = refs[refs[q]])
-//   in LDS until every position points at a literal; the block's bytes are then staged in LDS, every
+//   every position, then refs[p + j] = p - D + j for every hole; pointer jumping (three hops per round,
+//   refs[q] = refs[refs[refs[refs[q]]]], chunks retired by a root test) in LDS until every position points
+//   at a literal; the block's bytes are then staged in LDS, every
 //   byte gathered from its root, CRC-32 checked and written out.
 #include <hip/hip_runtime.h>
 
