@@ -9,7 +9,7 @@
 //
 // Layout: the input is cut into 65,280-byte payloads (htslib's framing, as the host writer uses).
 // Each payload becomes one BGZF block holding one final deflate block with dynamic Huffman codes
-// (or a stored block when that is smaller).  Per chunk of 4096 payloads:
+// (or a stored block when that is smaller).  Per chunk of 16384 payloads:
 //
 //   k_defl_parse   one 512-thread workgroup per payload, the payload in LDS: hash-table match candidates
 //                  in rounds, a greedy parse of every 64-byte segment by its thread (literal runs
@@ -1236,16 +1236,16 @@ __global__ void __launch_bounds__(kT, 4) k_defl_emit(const uint8_t *__restrict__
     }
 }
 
-// exclusive scan of n <= 8192 block sizes, one 1024-thread workgroup, 8 consecutive entries per thread
-// (the per-chunk offsets; runs on the chunk's own stream)
-constexpr uint32_t kMaxChunk = 8192;
+// exclusive scan of n <= kMaxChunk block sizes, one 1024-thread workgroup, kPer consecutive entries per
+// thread (the per-chunk offsets; runs on the chunk's own stream)
+constexpr uint32_t kMaxChunk = 16384, kPer = kMaxChunk / 1024;
 __global__ void __launch_bounds__(1024) k_scan_chunk(const uint32_t *__restrict__ in, uint32_t n, uint32_t *__restrict__ out) {
     __shared__ uint32_t ws[16];
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    uint32_t a[8], v = 0;
+    uint32_t a[kPer], v = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        a[i] = 8 * t + i < n ? in[8 * t + i] : 0;
+    for (uint32_t i = 0; i < kPer; ++i) {
+        a[i] = kPer * t + i < n ? in[kPer * t + i] : 0;
         v += a[i];
     }
     uint32_t x = v;
@@ -1267,8 +1267,8 @@ __global__ void __launch_bounds__(1024) k_scan_chunk(const uint32_t *__restrict_
     __syncthreads();
     uint32_t excl = ws[w] + x - v;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        if (8 * t + i < n) out[8 * t + i] = excl;
+    for (uint32_t i = 0; i < kPer; ++i) {
+        if (kPer * t + i < n) out[kPer * t + i] = excl;
         excl += a[i];
     }
 }
@@ -1309,9 +1309,15 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     if (!n) return OGE_OK;
     const uint64_t nblk = (n + kPay - 1) / kPay;
     const int ncu = ctx->cu_count();  // persistent parse workgroups: one per CU of this context's device
-    // payloads per chunk: one launch of each kernel (4096 measured best in r02: 2048 / 4096 / 8192,
-    // profiles/r02_ab/codec_k*.json)
-    const uint64_t chunk = std::min<uint64_t>(nblk, 4096);
+    // payloads per chunk: one launch of each kernel.  r02 measured 4096 best (2048 / 4096 / 8192,
+    // profiles/r02_ab/codec_k*.json); on the r06 kernels larger chunks win (fewer persistent-parse tails):
+    // 100M reads 126.7 / 124.0 / 122.4 ms for 4096 / 8192 / 16384, 40M reads (11 chunks) 50.5 / 48.8 ms for
+    // 4096 / 16384, the same bytes (profiles/r06dg-di).  Buffers: ~97 KB per payload and stream set.
+#ifndef OGE_DEFL_CHUNK  // experiment builds: another chunk
+#define OGE_DEFL_CHUNK kMaxChunk
+#endif
+    static_assert(OGE_DEFL_CHUNK <= kMaxChunk, "k_scan_chunk bound");
+    const uint64_t chunk = std::min<uint64_t>(nblk, OGE_DEFL_CHUNK);
     // Chunks go round-robin over S streams: one chunk's Huffman and emit kernels run on the CUs beside
     // another chunk's parse workgroups (150 KiB of LDS, one per CU); only the offset advance, which
     // gives each chunk its base in the output stream, is ordered chunk after chunk (events).

@@ -10,7 +10,7 @@ from openge_amd import lib as L
 if len(sys.argv) > 1:
     L.LIB_PATH = Path(sys.argv[1])
 import os
-reads = 20_000_000
+reads = int(os.environ.get("DIAG_READS", 20_000_000))
 level = int(os.environ.get("DIAG_LEVEL", 6))
 dev = torch.device("cuda", 0)
 ctx = L.Context(0)
