@@ -1313,17 +1313,31 @@ extern "C" int oge_bgzf_deflate_dev(oge_ctx *ctx, const uint8_t *d_src, uint64_t
     // profiles/r02_ab/codec_k*.json); on the r06 kernels larger chunks win (fewer persistent-parse tails):
     // 100M reads 126.7 / 124.0 / 122.4 ms for 4096 / 8192 / 16384, 40M reads (11 chunks) 50.5 / 48.8 ms for
     // 4096 / 16384, the same bytes (profiles/r06dg-di).  Buffers: ~97 KB per payload and stream set.
-#ifndef OGE_DEFL_CHUNK  // experiment builds: another chunk
-#define OGE_DEFL_CHUNK kMaxChunk
-#endif
-    static_assert(OGE_DEFL_CHUNK <= kMaxChunk, "k_scan_chunk bound");
-    const uint64_t chunk = std::min<uint64_t>(nblk, OGE_DEFL_CHUNK);
-    // Chunks go round-robin over S streams: one chunk's Huffman and emit kernels run on the CUs beside
-    // another chunk's parse workgroups (150 KiB of LDS, one per CU); only the offset advance, which
-    // gives each chunk its base in the output stream, is ordered chunk after chunk (events).
+    // The chunk halves (down to 4096) until the S buffer sets fit in a quarter of the device memory that is free
+    // or already held by them (a caller that keeps most of HBM, like the 300M chain test, gets 4096).
 #ifndef OGE_DEFL_STREAMS
 #define OGE_DEFL_STREAMS 3
 #endif
+#ifndef OGE_DEFL_CHUNK  // experiment builds: another largest chunk
+#define OGE_DEFL_CHUNK kMaxChunk
+#endif
+    static_assert(OGE_DEFL_CHUNK <= kMaxChunk, "k_scan_chunk bound");
+    constexpr uint64_t kPerPay = (uint64_t)kNSeg * 8 + kNSeg + (uint64_t)kMaxM * kNSeg * 4 + kFreq * 4 + sizeof(DeflTab) + 8;
+    const int S0 = nblk > 4096 ? OGE_DEFL_STREAMS : 1;
+    uint64_t chunk = std::min<uint64_t>(nblk, OGE_DEFL_CHUNK);
+    if (chunk > 4096) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
+        uint64_t held = 0;
+        for (int s = 0; s < 3; ++s) {
+            const auto it = ctx->bufs.find("defl_mlist" + std::to_string(s));
+            if (it != ctx->bufs.end()) held += it->second.cap / ((uint64_t)kMaxM * kNSeg * 4) * kPerPay;
+        }
+        while (chunk > 4096 && (uint64_t)S0 * chunk * kPerPay > (fr + held) / 4) chunk = std::max<uint64_t>(4096, chunk / 2);
+    }
+    // Chunks go round-robin over S streams: one chunk's Huffman and emit kernels run on the CUs beside
+    // another chunk's parse workgroups (150 KiB of LDS, one per CU); only the offset advance, which
+    // gives each chunk its base in the output stream, is ordered chunk after chunk (events).
     // B[] below holds three buffer sets; 300M chain: 2 streams 423.6 ms, 3 streams 417.4 ms (r04)
     static_assert(OGE_DEFL_STREAMS >= 1 && OGE_DEFL_STREAMS <= 3, "deflate: 1-3 streams");
     const int S = nblk > chunk ? OGE_DEFL_STREAMS : 1;
