@@ -224,7 +224,7 @@ def test_300m_read_properties():
 def _byte_checksum(buf: torch.Tensor, base: int, acc: list) -> None:
     """Fold bytes buf (uint8, device) at absolute stream positions base.. into acc = [s1, s2]:
     s_k = sum of byte_i * w_k(i) mod 2^64 with two different position weights (int64 wraps)."""
-    step = 1 << 28
+    step = 1 << 26  # 512 MiB int64 temporaries: the context still holds its workspaces (deflate: up to 4.8 GB)
     for o in range(0, buf.numel(), step):
         b = buf[o:o + step].to(torch.int64)
         i = torch.arange(base + o, base + o + b.numel(), dtype=torch.int64, device=buf.device)
